@@ -1,0 +1,356 @@
+"""CPU oracle for the Code-NeRF ray-marching hot path.
+
+TEST INFRASTRUCTURE ONLY.  This module is a CPU (PyTorch fp32) restatement of
+the reference algorithm (akashsharma02/code-nerf, mounted read-only at
+/root/reference in the build container).  Only ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import
+it, and only as the *checker* (or as the timed CPU baseline).  The product path
+(``code-nerf_amd/codenerf``) never imports it and has no CPU fallback.
+
+Pinning: ``tests/golden/make_golden.py`` imports the real reference (with three
+harness-side shims: ``torch.cuda.Device`` alias, stub ``imageio`` and
+``torch.utils.tensorboard`` modules) and writes fixtures under
+``tests/golden/``.  ``tests/test_oracle_golden.py`` checks that every function
+here reproduces those fixtures (bit for bit: the op sequence is the reference's,
+on the same aten CPU kernels).
+
+Every function cites the reference ``file:line`` it restates.  The op order is
+kept where it changes fp32 rounding (e.g. ``ro + rd * z``, ``cumsum``), because
+the fixtures pin bits, not just values.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+Tensor = torch.Tensor
+
+# ---------------------------------------------------------------------------
+# Rays                                       view_synthesis/nerf/ray_sampler.py
+# ---------------------------------------------------------------------------
+
+
+def ray_directions(height: int, width: int, intrinsics: Tensor) -> Tensor:
+    """Camera-frame pixel directions, (H, W, 3).
+
+    ray_sampler.py:31-51: ``indexing='xy'`` meshgrid, no +0.5 pixel centre
+    (quirk Q3); dir = ((w - cx)/f, -(h - cy)/f, -1).
+    """
+    f = intrinsics[..., 0, 0]
+    cx = intrinsics[..., 0, 2]
+    cy = intrinsics[..., 1, 2]
+    cols = torch.arange(width, dtype=intrinsics.dtype)
+    rows = torch.arange(height, dtype=intrinsics.dtype)
+    ii, jj = torch.meshgrid(cols, rows, indexing="xy")
+    return torch.stack([(ii - cx) / f, -(jj - cy) / f, -torch.ones_like(ii)], dim=-1)
+
+
+def ray_bundle(directions: Tensor, c2w: Tensor) -> Tuple[Tensor, Tensor]:
+    """Rotate the bundle by c2w (B,4,4) -> ro, rd (B,H,W,3).
+
+    ray_sampler.py:95-99 (einsum 'hwij,bji->bhwj'; ro is an expand of t).
+    """
+    rd = torch.einsum("hwij, bji->bhwj", directions[..., None], c2w[..., :3, :3]).contiguous()
+    ro = c2w[..., :3, -1][:, None, None, :].expand(rd.shape)
+    return ro, rd
+
+
+def gather_rays(ro: Tensor, rd: Tensor, select_inds) -> Tuple[Tensor, Tensor]:
+    """Gather the selected pixels of each image; ray_sampler.py:66-82.
+
+    ``select_inds`` is the (B, S) int array drawn on the host by
+    ``np.random.permutation`` (ray_sampler.py:71-75).
+    """
+    b = ro.shape[0]
+    ro_f, rd_f = ro.flatten(1, 2), rd.flatten(1, 2)
+    o = torch.cat([ro_f[i, select_inds[i], :] for i in range(b)], dim=0)
+    d = torch.cat([rd_f[i, select_inds[i], :] for i in range(b)], dim=0)
+    return o, d
+
+
+# ---------------------------------------------------------------------------
+# Points                                    view_synthesis/nerf/point_sampler.py
+# ---------------------------------------------------------------------------
+
+
+def depth_bins(num_coarse: int, near: float, far: float, spacing_mode: str) -> Dict[str, Tensor]:
+    """z / lower / upper of the stratified sampler; point_sampler.py:33-47.
+
+    Quirk Q2: the branch named "lindisp" is linear in depth; every other mode
+    (the configs use "lindepth") is linear in disparity.
+    """
+    t = torch.linspace(0.0, 1.0, num_coarse, dtype=torch.float32)
+    if spacing_mode == "lindisp":
+        z = near * (1.0 - t) + far * t
+    else:
+        z = 1.0 / (1.0 / near * (1.0 - t) + 1.0 / far * t)
+    mids = 0.5 * (z[..., 1:] + z[..., :-1])
+    return {
+        "z": z,
+        "upper": torch.cat((mids, z[..., -1:]), dim=-1),
+        "lower": torch.cat((z[..., :1], mids), dim=-1),
+    }
+
+
+def sample_uniform(ro: Tensor, rd: Tensor, bins: Dict[str, Tensor],
+                   t_rand: Optional[Tensor] = None) -> Tuple[Tensor, Tensor]:
+    """Stratified depths and points; point_sampler.py:49-71.
+
+    ``t_rand`` (R, Nc) replaces ``torch.rand_like`` (:64) when perturbing.
+    """
+    n = ro.shape[-2]
+    nc = bins["z"].shape[-1]
+    if t_rand is not None:
+        upper = bins["upper"].expand(n, nc)
+        lower = bins["lower"].expand(n, nc)
+        z = lower + (upper - lower) * t_rand
+    else:
+        z = bins["z"].expand(n, nc)
+    pts = ro[..., None, :] + rd[..., None, :] * z[..., :, None]
+    return pts, z
+
+
+def sample_pdf(ro: Tensor, rd: Tensor, weights: Tensor, z: Tensor, num_fine: int,
+               u: Optional[Tensor] = None, return_inds: bool = False):
+    """Inverse-CDF fine sampling + sorted merge; point_sampler.py:73-120.
+
+    ``weights`` is the coarse ``weights[..., 1:-1]`` (Nc-2 wide, :84).  ``u``
+    (R, Nf) replaces ``torch.rand`` (:93); without it u = linspace(0, 1, Nf).
+    """
+    assert z.shape[-1] - 2 == weights.shape[-1], "weights must be Nc-2 wide"
+    mids = 0.5 * (z[..., 1:] + z[..., :-1])
+    w = weights + 1e-5
+    pdf = w / torch.sum(w, dim=-1, keepdim=True)
+    cdf = torch.cumsum(pdf, dim=-1)
+    cdf = torch.cat([torch.zeros_like(cdf[..., :1]), cdf], dim=-1)
+    if u is None:
+        u = torch.linspace(0.0, 1.0, steps=num_fine, dtype=weights.dtype)
+        u = u.expand(list(cdf.shape[:-1]) + [num_fine])
+    u = u.contiguous()
+    cdf = cdf.contiguous()
+    inds = torch.searchsorted(cdf, u, right=True)
+    below = torch.max(torch.zeros_like(inds - 1), inds - 1)
+    above = torch.min((cdf.shape[-1] - 1) * torch.ones_like(inds), inds)
+    idx = torch.stack((below, above), dim=-1)
+    shape = (idx.shape[0], idx.shape[1], cdf.shape[-1])
+    cdf_g = torch.gather(cdf.unsqueeze(1).expand(shape), 2, idx)
+    bins_g = torch.gather(mids.unsqueeze(1).expand(shape), 2, idx)
+    denom = cdf_g[..., 1] - cdf_g[..., 0]
+    denom = torch.where(denom < 1e-5, torch.ones_like(denom), denom)
+    t = (u - cdf_g[..., 0]) / denom
+    samples = (bins_g[..., 0] + t * (bins_g[..., 1] - bins_g[..., 0])).detach()
+    z_all, _ = torch.sort(torch.cat((z, samples), dim=-1), dim=-1)
+    pts = ro[..., None, :] + rd[..., None, :] * z_all[..., :, None]
+    if return_inds:
+        return pts, z_all, inds, cdf
+    return pts, z_all
+
+
+# ---------------------------------------------------------------------------
+# Positional encoding                       view_synthesis/nerf/position_embed.py
+# ---------------------------------------------------------------------------
+
+
+def frequency_bands(num_freq: int, log_sampling: bool) -> Tensor:
+    """position_embed.py:17-33."""
+    if log_sampling:
+        return 2.0 ** torch.linspace(0.0, num_freq - 1, num_freq, dtype=torch.float32)
+    return torch.linspace(2.0 ** 0.0, 2.0 ** (num_freq - 1), num_freq, dtype=torch.float32)
+
+
+def posenc(x: Tensor, freqs: Tensor, include_input: bool) -> Tensor:
+    """[x, sin(f0 x), cos(f0 x), sin(f1 x), ...]; position_embed.py:35-53."""
+    parts = [x] if include_input else []
+    for f in freqs:
+        parts.append(torch.sin(x * f))
+        parts.append(torch.cos(x * f))
+    return parts[0] if len(parts) == 1 else torch.cat(parts, dim=-1)
+
+
+# ---------------------------------------------------------------------------
+# Code-conditioned MLP                      view_synthesis/models/model.py
+# ---------------------------------------------------------------------------
+
+
+def _linear(p: Dict[str, Tensor], name: str, x: Tensor) -> Tensor:
+    return torch.nn.functional.linear(x, p[name + ".weight"], p[name + ".bias"])
+
+
+def codenerf_mlp(p: Dict[str, Tensor], z_s: Tensor, z_t: Tensor, x: Tensor, dim_xyz: int) -> Tensor:
+    """CodeNeRFModel.forward, model.py:160-194 -> (M, 4) = [rgb_raw(3), sigma_raw]."""
+    relu = torch.nn.functional.relu
+    xyz, view = x[..., :dim_xyz], x[..., dim_xyz:]
+    zs1 = relu(_linear(p, "shape_code_layer1", z_s))
+    zs2 = relu(_linear(p, "shape_code_layer2", z_s))
+    zt1 = relu(_linear(p, "texture_code_layer1", z_t))
+    h = relu(_linear(p, "layer_xyz1", xyz))
+    h = relu(_linear(p, "layer_xyz2", torch.cat((h, zs1), dim=-1)))
+    o = _linear(p, "fc_out", torch.cat((h, zs2), dim=-1))
+    sigma, feat = o[..., :1], o[..., 1:]
+    v = relu(_linear(p, "layer_dir1", torch.cat((feat, view), dim=-1)))
+    v = relu(_linear(p, "layer_dir2", v))
+    rgb = _linear(p, "fc_rgb", torch.cat((v, zt1), dim=-1))
+    return torch.cat((rgb, sigma), dim=-1)
+
+
+class EmbedCfg:
+    """The four embedder knobs of cfg.nerf.embedder (nerf/__init__.py:57-69)."""
+
+    def __init__(self, num_xyz=10, num_dir=4, include_xyz=True, include_dir=True,
+                 log_xyz=True, log_dir=True):
+        self.fx = frequency_bands(num_xyz, log_xyz)
+        self.fd = frequency_bands(num_dir, log_dir)
+        self.inc_x = include_xyz
+        self.inc_d = include_dir
+        self.dim_xyz = (3 if include_xyz else 0) + 6 * num_xyz
+
+
+def forward_pass(p: Dict[str, Tensor], emb: EmbedCfg, rd: Tensor, pts: Tensor,
+                 z_s: Tensor, z_t: Tensor) -> Tensor:
+    """nerf/__init__.py:94-134 -> (R, S, 4).
+
+    Quirk Q1: ``viewdirs.repeat([1, S, 1])`` tiles the whole (R, 3) ray list, so
+    flattened sample row k = r*S + s gets the view direction of ray k mod R
+    while its point and codes come from ray k div S.
+    """
+    r, s = pts.shape[0], pts.shape[1]
+    zs = z_s[:, None, :].expand(-1, s, -1).reshape(-1, z_s.shape[-1])
+    zt = z_t[:, None, :].expand(-1, s, -1).reshape(-1, z_t.shape[-1])
+    enc = posenc(pts.reshape(-1, pts.shape[-1]), emb.fx, emb.inc_x)
+    vd = rd / rd.norm(p=2, dim=-1).unsqueeze(-1)
+    vd = vd.repeat([1, s, 1])
+    vd = vd.reshape(-1, vd.shape[-1])
+    enc = torch.cat((enc, posenc(vd, emb.fd, emb.inc_d)), dim=-1)
+    out = codenerf_mlp(p, zs, zt, enc, emb.dim_xyz)
+    return out.reshape([r, s, out.shape[-1]])
+
+
+# ---------------------------------------------------------------------------
+# Volume integration                        view_synthesis/nerf/volumetric_render.py
+# ---------------------------------------------------------------------------
+
+
+def volume_render(raw: Tensor, z: Tensor, rd: Tensor):
+    """volumetric_render.py:36-66 -> (rgb, disp, acc, weights, depth).
+
+    Q12: sigma = softplus(raw3 - 1) with torch's threshold 20; rgb =
+    sigmoid*1.002 - 0.001.  Q13: last delta 1e10*|rd|; transmittance is
+    exp(-exclusive cumsum).
+    """
+    d = z[..., 1:] - z[..., :-1]
+    d = torch.cat((d, torch.full_like(d[..., :1], 1e10)), dim=-1)
+    delta = d * rd[..., None, :].norm(p=2, dim=-1)
+    sigma = torch.nn.functional.softplus(raw[..., 3] - 1)
+    sd = sigma * delta
+    rgb = torch.sigmoid(raw[..., :3]) * (1 + 2 * 0.001) - 0.001
+    trans = torch.exp(-torch.cat([torch.zeros_like(sd[..., :1]), torch.cumsum(sd[..., :-1], axis=-1)], dim=-1))
+    alpha = 1.0 - torch.exp(-sd)
+    w = alpha * trans
+    rgb_map = (w[..., None] * rgb).sum(dim=-2)
+    depth = (w * z).sum(dim=-1)
+    acc = w.sum(dim=-1)
+    disp = 1.0 / torch.max(1e-10 * torch.ones_like(depth), depth / acc)
+    return rgb_map, disp, acc, w, depth
+
+
+# ---------------------------------------------------------------------------
+# Orchestration                             view_synthesis/nerf/__init__.py
+# ---------------------------------------------------------------------------
+
+
+class Sampling:
+    """The point-sampler knobs (nerf/__init__.py:31-38)."""
+
+    def __init__(self, num_coarse, num_fine, near, far, spacing_mode="lindepth"):
+        self.nc, self.nf = num_coarse, num_fine
+        self.bins = depth_bins(num_coarse, near, far, spacing_mode)
+
+
+def predict_radiance_and_render(ro, rd, smp: Sampling, emb: EmbedCfg, p_coarse, p_fine,
+                                z_s, z_t, t_rand=None, u=None, coarse_only=False):
+    """nerf/__init__.py:74-91, also returning the maps the reference drops.
+
+    Returns a dict: rgb_coarse, depth_coarse, acc_coarse, weights_coarse, and
+    (unless ``coarse_only``) rgb_fine, depth_fine, acc_fine, z_fine.
+    """
+    pts, z = sample_uniform(ro, rd, smp.bins, t_rand)
+    raw = forward_pass(p_coarse, emb, rd, pts, z_s, z_t)
+    rgb_c, disp_c, acc_c, w_c, depth_c = volume_render(raw, z, rd)
+    out = {"rgb_coarse": rgb_c, "depth_coarse": depth_c, "acc_coarse": acc_c,
+           "weights_coarse": w_c, "disp_coarse": disp_c}
+    if coarse_only:
+        return out
+    pts_f, z_f = sample_pdf(ro, rd, w_c[..., 1:-1], z, smp.nf, u)
+    raw_f = forward_pass(p_fine, emb, rd, pts_f, z_s, z_t)
+    rgb_f, disp_f, acc_f, _, depth_f = volume_render(raw_f, z_f, rd)
+    out.update({"rgb_fine": rgb_f, "depth_fine": depth_f, "acc_fine": acc_f, "z_fine": z_f,
+                "disp_fine": disp_f})
+    return out
+
+
+def get_minibatches(x: Tensor, chunksize: int) -> List[Tensor]:
+    """utils/util.py:230-235."""
+    return [x[i: i + chunksize] for i in range(0, x.shape[0], chunksize)]
+
+
+def split_sizes(num_rays: int, n: int) -> Tuple[List[int], List[int]]:
+    """Per-rank ray counts and pads; nerf/__init__.py:179-187 (quirk Q5)."""
+    per = torch.full([n], (num_rays / n), dtype=int)
+    padding = num_rays - torch.sum(per)
+    per[-1] = num_rays - torch.sum(per[:-1])
+    pad = torch.zeros([n], dtype=int)
+    if padding > 0:
+        pad[:-1] = padding
+    return per.tolist(), pad.tolist()
+
+
+def render_image(ro, rd, z_s, z_t, smp, emb, p_coarse, p_fine, chunksize, n_ranks=1,
+                 coarse_only=False, t_rand=None, u=None, key="rgb_fine"):
+    """Single-process emulation of parallel_image_render (nerf/__init__.py:137-226).
+
+    Rank r renders its Q5 slice chunked by ``chunksize`` (so Q1 applies per
+    chunk); rank 0's gather is the concatenation of the slices.  ``t_rand``
+    and ``u`` are full-image (N, Nc) / (N, Nf) uniforms indexed by ray.
+    Returns the full-image dict of concatenated outputs.
+    """
+    n = ro.shape[0]
+    per, _ = split_sizes(n, n_ranks)
+    outs: Dict[str, List[Tensor]] = {}
+    start = 0
+    for r in range(n_ranks):
+        stop = start + per[r]
+        for c0 in range(start, stop, chunksize):
+            c1 = min(c0 + chunksize, stop)
+            tr = None if t_rand is None else t_rand[c0:c1]
+            uu = None if u is None else u[c0:c1]
+            o = predict_radiance_and_render(ro[c0:c1], rd[c0:c1], smp, emb, p_coarse, p_fine,
+                                            z_s[c0:c1], z_t[c0:c1], tr, uu, coarse_only)
+            for k, v in o.items():
+                outs.setdefault(k, []).append(v)
+        start = stop
+    return {k: torch.cat(v, dim=0) for k, v in outs.items()}
+
+
+# ---------------------------------------------------------------------------
+# Eval / train helpers                       eval.py, utils/util.py
+# ---------------------------------------------------------------------------
+
+
+def pose_spherical(theta: Tensor, phi: Tensor, rho: Tensor) -> Tensor:
+    """Differentiable camera-on-sphere pose; eval.py:22-38."""
+    c2w = torch.eye(n=4, device=theta.device)
+    st, ct, sp, cp = torch.sin(theta), torch.cos(theta), torch.sin(phi), torch.cos(phi)
+    c2w[0, 0], c2w[1, 0] = -sp, cp
+    c2w[0, 1], c2w[1, 1], c2w[2, 1] = -st * cp, -st * sp, ct
+    c2w[0, 2], c2w[1, 2], c2w[2, 2] = ct * cp, ct * sp, st
+    c2w[0, 3], c2w[1, 3], c2w[2, 3] = rho * ct * cp, rho * ct * sp, rho * st
+    return c2w
+
+
+def mse2psnr(mse: float) -> float:
+    """utils/util.py:216-227."""
+    if mse == 0:
+        mse = 1e-5
+    return -10.0 * math.log10(mse)

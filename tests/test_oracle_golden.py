@@ -1,0 +1,168 @@
+"""The CPU oracle reproduces the reference's own outputs (fixtures from tests/golden/make_golden.py).
+
+Bit-exact (max |d| == 0) wherever the oracle runs the reference's op sequence on
+the same aten CPU kernels; this is what pins the oracle.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle import codenerf_oracle as O
+from codenerf import synthetic
+
+
+def load(name):
+    return {k: torch.from_numpy(v) for k, v in np.load(os.path.join(GOLDEN, name)).items()}
+
+
+def same(a, b, tol=0.0):
+    a, b = torch.as_tensor(a), torch.as_tensor(b)
+    assert a.shape == b.shape, (a.shape, b.shape)
+    d = (a.double() - b.double()).abs().max().item() if a.numel() else 0.0
+    assert d <= tol, d
+
+
+def test_rays():
+    g = load("rays_small.npz")
+    d = O.ray_directions(12, 16, g["intrinsics"])
+    same(d, g["directions"])
+    ro, rd = O.ray_bundle(d, g["poses"])
+    same(ro, g["ro"])
+    same(rd, g["rd"])
+    o, r = O.gather_rays(ro, rd, g["select_inds"].numpy())
+    same(o, g["ro_sel"])
+    same(r, g["rd_sel"])
+
+
+@pytest.mark.parametrize("tag", ["nc8_nf8_lindepth_d", "nc8_nf8_lindepth_p", "nc8_nf8_lindisp_d", "nc8_nf8_lindisp_p",
+                                 "nc32_nf128_lindepth_d", "nc32_nf128_lindepth_p", "nc64_nf64_lindepth_d",
+                                 "nc64_nf64_lindepth_p"])
+def test_points(tag):
+    g = load("points_small.npz")
+    nc, nf = [int(x[2:]) for x in tag.split("_")[:2]]
+    mode = tag.split("_")[2]
+    bins = O.depth_bins(nc, 0.8, 1.8, mode)
+    same(bins["z"], g[tag + "_zbins"])
+    same(bins["lower"], g[tag + "_lower"])
+    same(bins["upper"], g[tag + "_upper"])
+    pts, z = O.sample_uniform(g["ro"], g["rd"], bins, g.get(tag + "_t_rand"))
+    same(z, g[tag + "_z"])
+    same(pts, g[tag + "_pts"])
+    pf, zf = O.sample_pdf(g["ro"], g["rd"], g[tag + "_w"], z, nf, g.get(tag + "_u"))
+    same(zf, g[tag + "_zf"])
+    if tag + "_ptsf" in g:
+        same(pf, g[tag + "_ptsf"])
+
+
+def test_posenc():
+    g = load("posenc.npz")
+    for L, log, inc in [(10, True, True), (4, True, True), (6, False, True), (3, True, False)]:
+        k = f"L{L}_{int(log)}_{int(inc)}"
+        f = O.frequency_bands(L, log)
+        same(f, g[k + "_freqs"])
+        same(O.posenc(g["x"], f, inc), g[k])
+
+
+def test_mlp():
+    g = load("mlp.npz")
+    p = synthetic.codenerf_params(0)
+    same(O.codenerf_mlp(p, g["z_s"], g["z_t"], g["x"], 63), g["raw"])
+
+
+def test_volume_render():
+    g = load("volrender.npz")
+    rgb, disp, acc, w, depth = O.volume_render(g["raw"], g["z"], g["rd"])
+    for a, k in zip([rgb, disp, acc, w, depth], ["rgb", "disp", "acc", "weights", "depth"]):
+        same(a, g[k])
+
+
+@pytest.mark.parametrize("nc,nf", [(8, 8), (32, 128)])
+@pytest.mark.parametrize("n_ranks", [1, 2, 3])
+def test_render_small(nc, nf, n_ranks):
+    g = load("render_small.npz")
+    d = O.ray_directions(12, 16, g["intrinsics"])
+    ro, rd = O.ray_bundle(d, g["pose"])
+    ro, rd = ro.reshape(-1, 3), rd.reshape(-1, 3)
+    n = ro.shape[0]
+    if n_ranks > 1:
+        per, _ = O.split_sizes(n, n_ranks)
+        assert per == g[f"nc{nc}_n{n_ranks}_split"].tolist()
+    smp = O.Sampling(nc, nf, 0.8, 1.8)
+    emb = O.EmbedCfg()
+    with torch.no_grad():
+        out = O.render_image(ro, rd, g["z_s"].expand(n, -1), g["z_t"].expand(n, -1), smp, emb,
+                             synthetic.codenerf_params(0), synthetic.codenerf_params(1), 50, n_ranks)
+    same(out["rgb_fine"], g[f"nc{nc}_n{n_ranks}_rgb"])
+
+
+def test_render_small_perturbed():
+    g = load("render_small.npz")
+    d = O.ray_directions(12, 16, g["intrinsics"])
+    ro, rd = O.ray_bundle(d, g["pose"])
+    ro, rd = ro.reshape(-1, 3), rd.reshape(-1, 3)
+    n = ro.shape[0]
+    with torch.no_grad():
+        out = O.render_image(ro, rd, g["z_s"].expand(n, -1), g["z_t"].expand(n, -1), O.Sampling(8, 8, 0.8, 1.8),
+                             O.EmbedCfg(), synthetic.codenerf_params(0), synthetic.codenerf_params(1), 50,
+                             t_rand=g["p_t_rand"], u=g["p_u"])
+    same(out["rgb_coarse"], g["p_rgb_coarse"])
+    same(out["rgb_fine"], g["p_rgb_fine"])
+
+
+def test_render_full_coarse():
+    """C2 at full size (128x128, 64 coarse samples, 4096-ray chunks)."""
+    g = load("render_full.npz")
+    d = O.ray_directions(128, 128, g["intrinsics"])
+    ro, rd = O.ray_bundle(d, g["pose"])
+    ro, rd = ro.reshape(-1, 3), rd.reshape(-1, 3)
+    n = ro.shape[0]
+    with torch.no_grad():
+        out = O.render_image(ro, rd, g["z_s"].expand(n, -1), g["z_t"].expand(n, -1), O.Sampling(64, 64, 0.8, 1.8),
+                             O.EmbedCfg(), synthetic.codenerf_params(0), synthetic.codenerf_params(1), 4096,
+                             coarse_only=True)
+    same(out["rgb_coarse"], g["rgb_c"])
+    same(out["depth_coarse"], g["depth_c"])
+    same(out["acc_coarse"], g["acc_c"])
+
+
+def test_eval_step_gradients():
+    """eval.py:145-167 autograd (codes + spherical pose) through the oracle."""
+    g = load("eval_grad.npz")
+    theta = g["theta"].clone().requires_grad_(True)
+    phi = g["phi"].clone().requires_grad_(True)
+    rho = g["rho"].clone().requires_grad_(True)
+    zs = g["z_s"].clone().requires_grad_(True)
+    zt = g["z_t"].clone().requires_grad_(True)
+    pc, pf = synthetic.codenerf_params(0), synthetic.codenerf_params(1)
+    for p in list(pc.values()) + list(pf.values()):
+        p.requires_grad_(True)
+    c2w = O.pose_spherical(theta, phi, rho)[None]
+    d = O.ray_directions(12, 16, load("render_small.npz")["intrinsics"])
+    ro, rd = O.ray_bundle(d, c2w)
+    ro, rd = O.gather_rays(ro, rd, g["select_inds"].numpy())
+    n = ro.shape[0]
+    tp = g["target"][None][..., g["select_inds"].numpy(), :].squeeze()
+    zse, zte = zs.expand(n, -1), zt.expand(n, -1)
+    out = O.predict_radiance_and_render(ro, rd, O.Sampling(8, 8, 0.8, 1.8), O.EmbedCfg(), pc, pf, zse, zte)
+    lc = torch.nn.functional.mse_loss(out["rgb_coarse"][..., :3], tp[..., :3])
+    lf = torch.nn.functional.mse_loss(out["rgb_fine"][..., :3], tp[..., :3])
+    loss = lc + lf + 1e-5 * (torch.norm(zse, p=2) + torch.norm(zte, p=2))
+    loss.backward()
+    same(out["rgb_coarse"].detach(), g["rgb_coarse"])
+    same(out["rgb_fine"].detach(), g["rgb_fine"])
+    same(loss.detach(), g["loss"])
+    for t, k in [(theta, "theta"), (phi, "phi"), (rho, "rho"), (zs, "z_s"), (zt, "z_t")]:
+        same(t.grad, g["g_" + k], 1e-9)
+    same(pf["fc_rgb.weight"].grad, g["g_fine_fc_rgb_w"], 1e-9)
+    same(pc["fc_out.bias"].grad, g["g_coarse_fc_out_b"], 1e-9)
+
+
+def test_split_sizes():
+    """Q5: truncating split, last rank takes the remainder."""
+    assert O.split_sizes(1024, 3)[0] == [341, 341, 342]
+    assert O.split_sizes(16384, 8)[0] == [2048] * 8
+    per, pad = O.split_sizes(100, 7)
+    assert per == [14] * 6 + [16] and pad == [2] * 6 + [0]
