@@ -1,0 +1,227 @@
+"""Benchmark: rendered rays/s on SRN-cars 128x128 at 64 samples/ray (BASELINE.json metric, config C2).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline] [--hierarchical]
+
+One step renders N full 128x128 images (16384 rays each, 64 coarse samples per
+ray, srn-cars-code near 0.8 / far 1.8, lindepth, 4096-ray chunks) through the
+gfx950 path: ray bundle -> per-object code terms -> depths -> fused
+encode+MLP field kernel (fp32 MFMA) -> compositing.  With N ranks every image
+is split over the ranks exactly like the reference's parallel_image_render
+(nerf/__init__.py:179-218) and the rendered pixels are all-gathered to rank 0
+over RCCL; per-rank work is fixed (16384 rays), so scaling is weak.
+
+Inputs are synthetic (no dataset/checkpoint offline): hash-initialised
+CodeNeRFModel weights of the reference architecture, one latent code pair,
+spherical poses.  Everything is resident in HBM before timing.
+
+JSON line fields beyond the driver contract: ``roofline`` (the field kernel,
+timed by HIP events on its stream inside the timed steps), ``cpu_baseline``
+(the CPU oracle -- the reference's op sequence in torch fp32 -- on this host,
+rank 0, one full image), ``psnr_vs_ref`` (our image vs that CPU render).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "code-nerf_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+H = W = 128
+FOCAL = 131.25
+NC, NF = 64, 64
+NEAR, FAR = 0.8, 1.8
+CHUNK = 4096
+FLOP_PER_SAMPLE = 572_416          # hoisted CodeNeRF MLP per sample-evaluation
+PEAK_FP32_MFMA_TFLOPS = 157.3      # MI355X dense fp32 matrix peak (MI355X_MICROARCH.md)
+
+
+def pose(theta, phi, rho):
+    """eval.py:22-38 pose_spherical (host, float32)."""
+    import math
+    st, ct, sp, cp = math.sin(theta), math.cos(theta), math.sin(phi), math.cos(phi)
+    m = torch.eye(4)
+    m[0, 0], m[1, 0] = -sp, cp
+    m[0, 1], m[1, 1], m[2, 1] = -st * cp, -st * sp, ct
+    m[0, 2], m[1, 2], m[2, 2] = ct * cp, ct * sp, st
+    m[0, 3], m[1, 3], m[2, 3] = rho * ct * cp, rho * ct * sp, rho * st
+    return m
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--hierarchical", action="store_true", help="also time the 64+64 (C3) render")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    n = max(world, 1)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    import codenerf
+    from codenerf import synthetic
+    from codenerf.models import CodeNeRFModel
+    from codenerf.nerf import PointSampler, PositionalEmbedder, RaySampler, gather_rows, render_rays
+    from codenerf.utils import split_sizes
+    codenerf.load_library()
+
+    k = synthetic.srn_intrinsics(H, FOCAL)
+    rs = RaySampler(H, W, k, sample_size=4096, device=dev, datatype=torch.float32)
+    ps = PointSampler(NC, NF, NEAR, FAR, "lindepth", False, torch.float32, dev)
+    emb = (PositionalEmbedder(10, True, True, torch.float32, dev), PositionalEmbedder(4, True, True, torch.float32, dev))
+    models = []
+    for seed in (0, 1):
+        m = CodeNeRFModel(256, 1, 256, 256, 10, 4)
+        m.load_state_dict(synthetic.codenerf_params(seed))
+        models.append(m.to(dev).eval())
+    zs = synthetic.latent_codes(5, 1).to(dev)
+    zt = synthetic.latent_codes(6, 1).to(dev)
+    poses = torch.stack([pose(0.5 + 0.3 * i, 0.3, 1.3) for i in range(n)]).to(dev)
+    n_img_rays = H * W
+    per, _ = split_sizes(n_img_rays, n)
+    start = sum(per[:rank])
+    chunk = min(CHUNK, per[rank])
+    rays_per_rank = per[rank] * n
+    for mm in models:
+        mm.packed()                              # weights packed once (frozen, as in eval)
+
+    timing = {"field_ms": 0.0, "field_launches": 0}
+
+    def step(record: bool, coarse_only: bool = True):
+        with torch.no_grad():
+            ro, rd = rs.get_bundle(poses)                    # (n, H, W, 3)
+            ro = ro.reshape(n, -1, 3)[:, start:start + per[rank]].reshape(-1, 3)
+            rd = rd.reshape(n, -1, 3)[:, start:start + per[rank]].reshape(-1, 3)
+            r = ro.shape[0]
+            hook = {} if record else None
+            out = render_rays(ro, rd, zs.expand(r, -1), zt.expand(r, -1), ps, emb, models[0], models[1],
+                              chunk_rows=chunk, coarse_only=coarse_only, events=hook)
+            rgb = out["rgb_coarse" if coarse_only else "rgb_fine"]
+            if world > 1:
+                rgb = gather_rows(rgb, [per[rank] * n] * n, rank)
+                if rgb is not None and len(set(per)) == 1:        # (rank, image, row) -> (image, rank, row)
+                    rgb = rgb.view(n, n, per[0], 3).transpose(0, 1).reshape(n * n_img_rays, 3)
+            if record:
+                timing["pending"] = timing.get("pending", []) + hook["field"]
+            return rgb
+
+    def timed(k_steps, w_steps, coarse_only=True):
+        for _ in range(w_steps):
+            step(False, coarse_only)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        timing["pending"] = []
+        t0 = time.perf_counter()
+        for _ in range(k_steps):
+            img = step(True, coarse_only)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([dt], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        ms = [a.elapsed_time(b) for a, b in timing["pending"]]
+        return dt, ms, img
+
+    dt, field_ms, img = timed(args.steps, args.warmup, coarse_only=True)
+    total_rays = n_img_rays * n * args.steps
+    value = total_rays / dt
+    field_avg_ms = sum(field_ms) / max(1, len(field_ms))
+    samples_per_launch = rays_per_rank * NC
+    flop_per_launch = samples_per_launch * FLOP_PER_SAMPLE
+    achieved_tf = flop_per_launch / (field_avg_ms * 1e-3) / 1e12
+
+    extra = {}
+    if args.hierarchical:
+        dth, _, _ = timed(max(1, args.steps // 2), 1, coarse_only=False)
+        extra["hierarchical_64_64_rays_per_s"] = n_img_rays * n * max(1, args.steps // 2) / dth
+
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "field_kernel_traffic.json")
+    if os.path.exists(tpath):
+        with open(tpath) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+
+    result = {
+        "metric": "rendered rays/sec (128x128, 64 samples/ray)",
+        "value": value,
+        "unit": "rays/s",
+        "n_gpus": n,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (hash-initialised CodeNeRFModel weights, one latent code pair, spherical poses)",
+        "config": {"workload": "C2: srn-cars-code 128x128 image per rank-step, 64 coarse samples/ray, "
+                               "chunk 4096, lindepth near 0.8 far 1.8, fused HIP render",
+                   "images_per_step": n, "rays_per_image": n_img_rays, "samples_per_ray": NC,
+                   "parallelism": f"ray-sharded x{n} + RCCL all-gather" if n > 1 else "single GPU"},
+        "roofline": {"kernel": "field_kernel<kFromRayZ> (fused posenc + CodeNeRF MLP, fp32 MFMA)",
+                     "bound": "mfma", "achieved": achieved_tf, "peak": PEAK_FP32_MFMA_TFLOPS,
+                     "unit": "TFLOP/s", "frac": achieved_tf / PEAK_FP32_MFMA_TFLOPS, "traffic": traffic,
+                     "avg_launch_ms": field_avg_ms, "flop_per_launch": flop_per_launch},
+    }
+    result.update(extra)
+
+    if rank == 0 and not args.no_cpu_baseline:
+        result["cpu_baseline"], result["psnr_vs_ref"] = cpu_baseline(img, k, poses, n)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(img, k, poses, n):
+    """The CPU oracle (reference op sequence, torch fp32) on this host: one full C2 image."""
+    from oracle import codenerf_oracle as O
+    from codenerf import synthetic
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    d = O.ray_directions(H, W, k)
+    ro, rd = O.ray_bundle(d, poses[:1].cpu())
+    ro, rd = ro.reshape(-1, 3), rd.reshape(-1, 3)
+    nr = ro.shape[0]
+    zs, zt = synthetic.latent_codes(5, 1).expand(nr, -1), synthetic.latent_codes(6, 1).expand(nr, -1)
+    pc, pf = synthetic.codenerf_params(0), synthetic.codenerf_params(1)
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        out = O.render_image(ro, rd, zs, zt, O.Sampling(NC, NF, NEAR, FAR), O.EmbedCfg(), pc, pf, CHUNK,
+                             coarse_only=True)
+    dt = time.perf_counter() - t0
+    ref = out["rgb_coarse"]
+    mine = img[:nr].float().cpu() if img is not None else None
+    psnr = None
+    if mine is not None and mine.shape == ref.shape:
+        mse = float(((mine - ref) ** 2).mean())
+        psnr = O.mse2psnr(mse)
+    return ({"value": nr / dt, "unit": "rays/s", "cores": threads, "kind": "port",
+             "sample": f"one full 128x128 image (16384 rays x 64 coarse samples, chunk 4096), {dt:.1f} s"}, psnr)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,95 @@
+"""ctypes binding of libcodenerf_hip.so (the C ABI in include/codenerf.h).
+
+The library is loaded lazily on first use and AFTER ``import torch``, so its
+``libamdhip64.so.7`` dependency resolves to the HIP runtime torch already
+loaded (one runtime, one set of streams).  There is no CPU fallback: if the
+library is missing or no GPU is visible, every op raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("CODENERF_LIB", os.path.join(_HERE, "lib", "libcodenerf_hip.so"))
+
+CN_OK, CN_EINVAL, CN_EUNSUPPORTED = 0, -1, -2
+CN_NUM_PARAMS = 18
+CN_CODE_BIAS_STRIDE = 520
+
+_p = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_f = ctypes.c_float
+_i = ctypes.c_int
+_fp = ctypes.POINTER(ctypes.c_float)
+
+# name -> (restype, argtypes); mirrors include/codenerf.h one to one.
+SIGNATURES = {
+    "cn_version": (ctypes.c_char_p, []),
+    "cn_error_string": (ctypes.c_char_p, [_i]),
+    "cn_ray_directions": (_i, [_i64, _i64, _f, _f, _f, _p, _p]),
+    "cn_ray_bundle": (_i, [_p, _i64, _p, _i64, _p, _p, _p]),
+    "cn_gather_rays": (_i, [_p, _p, _i64, _i64, _p, _i64, _p, _p, _p]),
+    "cn_sample_uniform": (_i, [_p, _p, _i64, _p, _p, _p, _i64, _p, _p, _p, _p]),
+    "cn_ray_points": (_i, [_p, _p, _p, _i64, _i64, _p, _p]),
+    "cn_sample_pdf": (_i, [_p, _p, _p, _i64, _p, _i64, _i64, _i64, _p, _p, _p, _p]),
+    "cn_posenc": (_i, [_p, _i64, _i64, _fp, _i64, _i, _p, _p]),
+    "cn_volume_render": (_i, [_p, _p, _p, _i64, _i64, _p, _p, _p, _p, _p, _p]),
+    "cn_mlp_packed_floats": (_i64, []),
+    "cn_mlp_pack": (_i, [ctypes.POINTER(_p), _p, _p]),
+    "cn_code_bias": (_i, [ctypes.POINTER(_p), _p, _p, _i64, _p, _p]),
+    "cn_mlp_forward": (_i, [_p, _p, _p, _i64, _p, _i64, _p, _p]),
+    "cn_radiance_field": (_i, [_p, _p, _p, _i64, _p, _p, _p, _p, _i64, _i64, _i64, _fp, _fp, _p, _p]),
+}
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+class CodeNerfError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load (once) and type the library; raises if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise CodeNerfError(
+            f"libcodenerf_hip.so not found at {path}; build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)")
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != CN_OK:
+        msg = load().cn_error_string(rc).decode()
+        raise CodeNerfError(f"{what} failed: {msg} (code {rc})")
+
+
+def ptr(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_of(t: torch.Tensor):
+    """The current HIP stream of t's device, as the C ABI's cn_stream_t."""
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def host_floats(values) -> "ctypes.Array":
+    vals = [float(v) for v in values]
+    return (ctypes.c_float * max(1, len(vals)))(*vals)
+
+
+def pointer_array(tensors):
+    arr = (ctypes.c_void_p * len(tensors))(*[t.data_ptr() for t in tensors])
+    return ctypes.cast(arr, ctypes.POINTER(ctypes.c_void_p)), arr

@@ -1,0 +1,131 @@
+"""CodeNeRFModel / ShapeTextureEmbedding with the reference's parameter contract.
+
+view_synthesis/models/model.py:87-194.  The nn.Linear submodules keep the
+reference's names and shapes (state_dicts load unchanged, including
+checkpoints written by train.py:129-138), but ``forward`` runs the fused gfx950
+field kernel (cn_mlp_forward) instead of nine addmm/cat/relu chains.
+
+Only the configuration every runnable reference config instantiates is
+implemented on the GPU: hidden 256, shape/texture codes 256, 10 xyz and 4 dir
+frequencies with the inputs included.  Other shapes construct (so checkpoints
+can be inspected) but raise on forward.
+"""
+from __future__ import annotations
+
+from typing import List, Tuple
+
+import torch
+
+from .. import ops
+
+PARAM_ORDER = ("layer_xyz1", "layer_xyz2", "fc_out", "shape_code_layer1", "shape_code_layer2",
+               "texture_code_layer1", "layer_dir1", "layer_dir2", "fc_rgb")
+
+
+class CodeNeRFModel(torch.nn.Module):
+    """model.py:123-194."""
+
+    def __init__(self, hidden_size=128, num_embeddings=1, shape_code_size=128, texture_code_size=128,
+                 num_encoding_fn_xyz=6, num_encoding_fn_dir=4, include_input_xyz=True, include_input_dir=True):
+        super().__init__()
+        self.hidden_size = hidden_size
+        self.shape_code_size = shape_code_size
+        self.texture_code_size = texture_code_size
+        self.dim_xyz = (3 if include_input_xyz else 0) + 6 * num_encoding_fn_xyz
+        self.dim_dir = (3 if include_input_dir else 0) + 6 * num_encoding_fn_dir
+        h, c = hidden_size, shape_code_size
+        self.layer_xyz1 = torch.nn.Linear(self.dim_xyz, h)
+        self.layer_xyz2 = torch.nn.Linear(h + c, h)
+        self.fc_out = torch.nn.Linear(h + c, c + 1)
+        self.shape_code_layer1 = torch.nn.Linear(c, c)
+        self.shape_code_layer2 = torch.nn.Linear(c, c)
+        self.texture_code_layer1 = torch.nn.Linear(c, c)
+        self.layer_dir1 = torch.nn.Linear(self.dim_dir + c, h)
+        self.layer_dir2 = torch.nn.Linear(h, h)
+        self.fc_rgb = torch.nn.Linear(h + texture_code_size, 3)
+        self._packed = None
+        self._packed_key = None
+
+    # --- kernel plumbing -------------------------------------------------
+    def supported(self) -> bool:
+        return (self.hidden_size == 256 and self.shape_code_size == 256 and self.texture_code_size == 256
+                and self.dim_xyz == 63 and self.dim_dir == 27)
+
+    def _require_supported(self):
+        if not self.supported():
+            raise NotImplementedError(
+                "the gfx950 field kernel implements CodeNeRFModel(hidden 256, codes 256, L_xyz 10, L_dir 4, "
+                f"inputs included); got hidden {self.hidden_size}, codes {self.shape_code_size}/"
+                f"{self.texture_code_size}, dims {self.dim_xyz}/{self.dim_dir}")
+
+    def param_list(self) -> List[torch.Tensor]:
+        out = []
+        for name in PARAM_ORDER:
+            lin = getattr(self, name)
+            out += [lin.weight, lin.bias]
+        return out
+
+    def packed(self) -> torch.Tensor:
+        """MFMA-fragment layout of the weights, repacked whenever a parameter changed."""
+        self._require_supported()
+        params = self.param_list()
+        key = tuple((p.data_ptr(), p._version) for p in params)
+        if self._packed is None or self._packed_key != key:
+            self._packed = ops.mlp_pack(params)
+            self._packed_key = key
+        return self._packed
+
+    def code_bias(self, z_s: torch.Tensor, z_t: torch.Tensor) -> torch.Tensor:
+        return ops.code_bias(self.param_list(), z_s, z_t)
+
+    # --- reference API ---------------------------------------------------
+    def forward(self, z_s: torch.Tensor, z_t: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+        """model.py:160-194: per-row codes (M, 256) x2 and encoded rows (M, 90) -> (M, 4)."""
+        self._require_supported()
+        if torch.is_grad_enabled() and any(t.requires_grad for t in [z_s, z_t, x] + self.param_list()):
+            from ..autograd import mlp_forward_autograd
+            return mlp_forward_autograd(self, z_s, z_t, x)
+        codes_s, codes_t, index = _dedupe_codes(z_s, z_t)
+        cb = ops.code_bias(self.param_list(), codes_s, codes_t)
+        return ops.mlp_forward(self.packed(), cb, x, index)
+
+
+def _dedupe_codes(z_s: torch.Tensor, z_t: torch.Tensor):
+    """Rows of an ``expand``-ed code tensor share storage: fold them to one code row."""
+    if z_s.dim() == 2 and z_s.stride(0) == 0 and z_t.stride(0) == 0:
+        return z_s[:1], z_t[:1], None
+    return z_s, z_t, None
+
+
+class ShapeTextureEmbedding(torch.nn.Module):
+    """model.py:87-120: per-object shape / texture code tables."""
+
+    def __init__(self, num_embeddings, shape_code_size=128, texture_code_size=128):
+        super().__init__()
+        self.num_embeddings = num_embeddings
+        self.shape_code_size = shape_code_size
+        self.texture_code_size = texture_code_size
+        self.shape_embedding = torch.nn.Embedding(num_embeddings, shape_code_size)
+        self.texture_embedding = torch.nn.Embedding(num_embeddings, texture_code_size)
+
+    def forward(self, object_ids: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        return self.shape_embedding(object_ids), self.texture_embedding(object_ids)
+
+    def get_all_embeddings(self, device) -> Tuple[torch.Tensor, torch.Tensor]:
+        idx = torch.arange(0, self.num_embeddings, dtype=torch.int64, device=device)
+        return self.shape_embedding(idx), self.texture_embedding(idx)
+
+    def get_params_tensor(self) -> Tuple[torch.Tensor, torch.Tensor]:
+        shape, texture = None, None
+        for name, p in self.named_parameters():
+            if "shape" in name:
+                shape = p.data.reshape(-1)
+            if "texture" in name:
+                texture = p.data.reshape(-1)
+        return shape, texture
+
+
+def get_params_tensor(model, is_distributed):
+    """model.py:79-84."""
+    m = model.module if is_distributed else model
+    return m.get_params_tensor()

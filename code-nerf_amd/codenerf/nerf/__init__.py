@@ -1,0 +1,215 @@
+"""Render orchestration on the gfx950 kernels (view_synthesis/nerf/__init__.py).
+
+Same entry points, argument meaning and return values as the reference:
+prepare_samplers (:15), prepare_embedders (:42), predict_radiance_and_render
+(:74), forward_pass (:94), parallel_image_render (:137).  Underneath, a whole
+ray list (a rank's full slice, not one 4096-ray chunk at a time) goes through
+one launch per stage -- depth sampling, the fused encode+MLP field kernel,
+compositing, inverse-CDF resampling -- with the reference's per-chunk
+semantics (quirk Q1) reproduced inside the field kernel's index math from
+``chunk_rows``.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Tuple, Union
+
+import torch
+import torch.distributed as dist
+
+from .. import ops
+from ..utils import get_minibatches, split_sizes  # noqa: F401
+from .point_sampler import PointSampler
+from .position_embed import PositionalEmbedder
+from .ray_sampler import RaySampler
+from .volumetric_render import volume_render
+
+__all__ = ["RaySampler", "PointSampler", "PositionalEmbedder", "volume_render", "prepare_samplers",
+           "prepare_embedders", "predict_radiance_and_render", "forward_pass", "parallel_image_render",
+           "render_rays"]
+
+
+def prepare_samplers(cfg, height: int, width: int, intrinsics, datatype, device) -> Tuple[RaySampler, PointSampler]:
+    """nerf/__init__.py:15-39."""
+    ray_sampler = RaySampler(height, width, intrinsics, sample_size=cfg.nerf.ray_sampler.num_random_rays,
+                             device=device, datatype=datatype)
+    ps = cfg.nerf.point_sampler
+    point_sampler = PointSampler(ps.num_coarse, ps.num_fine, ps.near_limit, ps.far_limit,
+                                 spacing_mode=ps.spacing_mode, perturb=ps.perturb, dtype=datatype, device=device)
+    return ray_sampler, point_sampler
+
+
+def prepare_embedders(cfg, datatype, device) -> Tuple[PositionalEmbedder, Optional[PositionalEmbedder]]:
+    """nerf/__init__.py:42-71."""
+    e = cfg.nerf.embedder
+    exyz = PositionalEmbedder(e.num_encoding_fn_xyz, e.log_sampling_xyz, e.include_input_xyz, datatype, device)
+    edir = None
+    if e.use_viewdirs:
+        edir = PositionalEmbedder(e.num_encoding_fn_dir, e.log_sampling_dir, e.include_input_dir, datatype, device)
+    return exyz, edir
+
+
+def _unwrap(model):
+    return model.module if hasattr(model, "module") else model
+
+
+def _check_embedders(embedders):
+    exyz, edir = embedders
+    if edir is None:
+        raise NotImplementedError("CodeNeRFModel consumes view directions; use_viewdirs=False has no runnable "
+                                  "reference path (layer_dir1 expects dim_dir inputs)")
+    if not (exyz.num_freq == 10 and exyz.include_input and edir.num_freq == 4 and edir.include_input):
+        raise NotImplementedError("the field kernel implements L_xyz=10 / L_dir=4 with inputs included")
+    return exyz.freqs, edir.freqs
+
+
+def _codes(z_s: torch.Tensor, z_t: torch.Tensor):
+    """One code row when the per-ray codes are an expand() of one row (eval / render), else per ray."""
+    if z_s.stride(0) == 0 and z_t.stride(0) == 0:
+        return z_s[:1], z_t[:1]
+    return z_s, z_t
+
+
+def _field(model, embedders, rd, z_s, z_t, chunk_rows, pts=None, ro=None, z=None):
+    fx, fd = _check_embedders(embedders)
+    m = _unwrap(model)
+    needs_grad = torch.is_grad_enabled() and (
+        any(t is not None and t.requires_grad for t in (rd, z_s, z_t, pts, ro)) or
+        any(p.requires_grad for p in m.param_list()))
+    if needs_grad:
+        from ..autograd import radiance_field_autograd
+        return radiance_field_autograd(m, rd, z_s, z_t, chunk_rows, fx, fd, pts=pts, ro=ro, z=z)
+    cs, ct = _codes(z_s, z_t)
+    cb = m.code_bias(cs, ct)
+    n_samples = pts.shape[1] if pts is not None else z.shape[1]
+    return ops.radiance_field(m.packed(), cb, rd, n_samples, chunk_rows, fx, fd, pts=pts, ro=ro, z=z)
+
+
+def forward_pass(model, embedders, rd: torch.Tensor, pts: torch.Tensor,
+                 object_embedding: Tuple[torch.Tensor, torch.Tensor]) -> torch.Tensor:
+    """nerf/__init__.py:94-134: embed + MLP for one chunk -> (R, S, 4).
+
+    Q1: sample row k = r*S + s takes the view direction of ray k mod R, R = this call's ray count.
+    """
+    if rd is None:
+        _check_embedders((embedders[0], None))
+    z_s, z_t = object_embedding
+    return _field(model, embedders, rd, z_s, z_t, chunk_rows=pts.shape[0], pts=pts)
+
+
+def render_rays(ro: torch.Tensor, rd: torch.Tensor, z_s: torch.Tensor, z_t: torch.Tensor,
+                point_sampler: PointSampler, embedders, coarse_model, fine_model=None, chunk_rows: Optional[int] = None,
+                t_rand: Optional[torch.Tensor] = None, u: Optional[torch.Tensor] = None,
+                coarse_only: bool = False, events: Optional[dict] = None) -> Dict[str, torch.Tensor]:
+    """predict_radiance_and_render over a whole ray list, chunk semantics kept via ``chunk_rows``.
+
+    Returns rgb/depth/acc for the coarse pass (+ weights) and, unless
+    ``coarse_only``, the fine pass.  Equal to running the reference's
+    predict_radiance_and_render on every ``chunk_rows`` slice and concatenating.
+    ``events`` (bench instrumentation): a dict that receives (start, end)
+    torch.cuda.Event pairs around each field-kernel launch under key "field".
+    """
+    def timed_field(*a, **kw):
+        if events is None:
+            return _field(*a, **kw)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        r = _field(*a, **kw)
+        e1.record()
+        events.setdefault("field", []).append((e0, e1))
+        return r
+
+    n = ro.shape[0]
+    chunk_rows = n if chunk_rows is None else chunk_rows
+    ps = point_sampler
+    if ps.perturb and t_rand is None:
+        t_rand = torch.rand(n, ps.num_samples_coarse, dtype=torch.float32, device=ro.device)
+    _, z_c = ops.sample_uniform(ro.detach(), rd.detach(), ps.z_vals, ps.lower, ps.upper,
+                                t_rand if ps.perturb else None, want_pts=False)
+    grad = torch.is_grad_enabled() and (ro.requires_grad or rd.requires_grad)
+    if grad:
+        from ..autograd import sample_points_autograd
+        raw_c = _field(coarse_model, embedders, rd, z_s, z_t, chunk_rows, pts=sample_points_autograd(ro, rd, z_c))
+    else:
+        raw_c = timed_field(coarse_model, embedders, rd, z_s, z_t, chunk_rows, ro=ro, z=z_c)
+    rgb_c, disp_c, acc_c, w_c, depth_c = volume_render(raw_c, z_c, rd)
+    out = {"rgb_coarse": rgb_c, "disp_coarse": disp_c, "acc_coarse": acc_c, "weights_coarse": w_c,
+           "depth_coarse": depth_c, "z_coarse": z_c}
+    if coarse_only:
+        return out
+    if ps.perturb and u is None:
+        u = torch.rand(n, ps.num_samples_fine, dtype=torch.float32, device=ro.device)
+    _, z_f = ops.sample_pdf(ro.detach(), rd.detach(), w_c.detach()[..., 1:-1], z_c, ps.num_samples_fine,
+                            u if ps.perturb else None, want_pts=False)
+    if grad:
+        from ..autograd import sample_points_autograd
+        raw_f = _field(fine_model, embedders, rd, z_s, z_t, chunk_rows, pts=sample_points_autograd(ro, rd, z_f))
+    else:
+        raw_f = timed_field(fine_model, embedders, rd, z_s, z_t, chunk_rows, ro=ro, z=z_f)
+    rgb_f, disp_f, acc_f, _, depth_f = volume_render(raw_f, z_f, rd)
+    out.update({"rgb_fine": rgb_f, "disp_fine": disp_f, "acc_fine": acc_f, "depth_fine": depth_f, "z_fine": z_f})
+    return out
+
+
+def predict_radiance_and_render(rays: Tuple[torch.Tensor, torch.Tensor], point_sampler: PointSampler,
+                                embedders, coarse_model, fine_model,
+                                latent_embedding: Tuple[torch.Tensor, torch.Tensor]) -> Tuple[torch.Tensor, torch.Tensor]:
+    """nerf/__init__.py:74-91 -> (rgb_coarse, rgb_fine)."""
+    ro, rd = rays
+    z_s, z_t = latent_embedding
+    out = render_rays(ro, rd, z_s, z_t, point_sampler, embedders, coarse_model, fine_model)
+    return out["rgb_coarse"], out["rgb_fine"]
+
+
+def parallel_image_render(cfg, pose: torch.Tensor, object_embedding, models, samplers, embedders, device,
+                          key: str = "rgb_fine", coarse_only: bool = False) -> Optional[torch.Tensor]:
+    """nerf/__init__.py:137-226: shard the image's rays over ranks, render, gather on rank 0.
+
+    The split is the reference's (Q5: truncating, the last rank takes the
+    remainder); each rank renders its contiguous slice in ONE pass with the
+    reference's chunking (``cfg.nerf.validation.chunksize``) kept as Q1
+    semantics; one all-gather (RCCL over xGMI on MI355X) of the padded
+    per-rank rows.  Rank 0 returns (H*W, 3); the others return None.
+    """
+    rank = 0
+    is_distributed = bool(getattr(cfg, "is_distributed", False))
+    n_gpus = int(getattr(cfg, "gpus", 1))
+    if is_distributed:
+        rank = dist.get_rank()
+    for _, model in models.items():
+        model.eval()
+    with torch.no_grad():
+        ray_sampler, point_sampler = samplers
+        ro, rd = ray_sampler.get_bundle(tform_cam2world=pose)
+        ro, rd = ro.reshape(-1, 3), rd.reshape(-1, 3)
+        num_rays = ro.shape[0]
+        per, pad = split_sizes(num_rays, n_gpus)
+        start = sum(per[:rank])
+        sl = slice(start, start + per[rank])
+        z_s, z_t = object_embedding
+        z_s = z_s.to(device).expand(num_rays, -1)[sl]
+        z_t = z_t.to(device).expand(num_rays, -1)[sl]
+        out = render_rays(ro[sl].to(device), rd[sl].to(device), z_s, z_t, point_sampler, embedders,
+                          models["nerf_coarse"], models.get("nerf_fine"), cfg.nerf.validation.chunksize,
+                          coarse_only=coarse_only)
+        rgb = out[key]
+        if not is_distributed:
+            return rgb
+        return gather_rows(rgb, per, rank)
+
+
+def gather_rows(rows: torch.Tensor, per: List[int], rank: int) -> Optional[torch.Tensor]:
+    """Pad every rank's rows to the largest share, all-gather, trim on rank 0 (nerf/__init__.py:212-224)."""
+    world = len(per)
+    width = max(per)
+    padded = torch.zeros((width,) + tuple(rows.shape[1:]), dtype=rows.dtype, device=rows.device)
+    padded[: rows.shape[0]] = rows
+    if dist.get_backend() == "nccl":
+        allrows = torch.empty((world * width,) + tuple(rows.shape[1:]), dtype=rows.dtype, device=rows.device)
+        dist.all_gather_into_tensor(allrows, padded)
+        parts = list(allrows.split(width))
+    else:
+        parts = [torch.zeros_like(padded) for _ in range(world)]
+        dist.all_gather(parts, padded)
+    if rank != 0:
+        return None
+    return torch.cat([p[: per[i]] for i, p in enumerate(parts)], dim=0)

@@ -1,0 +1,49 @@
+// Shared helpers for the gfx950 kernels of libcodenerf_hip.so.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "codenerf.h"
+
+#define CN_CHECK_ARG(cond)          \
+  do {                              \
+    if (!(cond)) return CN_EINVAL;  \
+  } while (0)
+
+namespace cn {
+
+constexpr int kWave = 64;
+
+inline hipStream_t as_stream(cn_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Launch status: hipGetLastError after a launch (sticky errors surface too).
+inline int launch_status() {
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? CN_OK : static_cast<int>(e);
+}
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Grid for a grid-stride elementwise kernel: at most 256 CUs x 8 blocks.
+inline unsigned elementwise_grid(int64_t n, int block) {
+  int64_t g = ceil_div(n, block);
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  return static_cast<unsigned>(g);
+}
+
+// Exact fp32 a*b then +c with two roundings (never contracted into an FMA):
+// matches torch's separate mul and add kernels bit for bit.
+__device__ __forceinline__ float mul_add_rn(float a, float b, float c) {
+  return __fadd_rn(__fmul_rn(a, b), c);
+}
+
+// torch.nn.functional.softplus(x) with beta 1, threshold 20 (volumetric_render.py:32).
+__device__ __forceinline__ float softplus20(float x) {
+  return x > 20.0f ? x : log1pf(expf(x));
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+}  // namespace cn

@@ -1,0 +1,562 @@
+// Code-conditioned MLP: CodeNeRFModel (view_synthesis/models/model.py:123-194)
+// fused with the positional encoding and Q1 view-direction mapping of
+// forward_pass (view_synthesis/nerf/__init__.py:94-134).
+//
+// Per sample the reference evaluates 9 Linear layers over concatenated inputs.
+// Three of them (the code layers, model.py:174-177) and the code halves of
+// layer_xyz2 / fc_out / fc_rgb depend only on the object's codes, so they are
+// folded once per code row into bias vectors (cn_code_bias).  The remaining
+// per-sample work -- 63->256, 256->256, 256->257, (256+27)->256, 256->256,
+// 256->3 -- is 286,208 MAC = 572,416 FLOP per sample and runs on fp32 MFMA
+// (v_mfma_f32_32x32x2_f32, exact f32 products, ~157 TFLOP/s peak on gfx950).
+//
+// Kernel shape: 256-thread workgroup = 4 waves, one wave per SIMD (the layer's
+// 256-wide input and output tiles take ~300 VGPRs), 32 samples per wave, 128
+// per workgroup.  Activations never leave registers: each layer's accumulator
+// is the next layer's B operand (mlp_layout.h).  Weights (1.25 MiB packed,
+// resident in every XCD's L2) stream through a double-buffered LDS ring in
+// chunks of 16 k-steps; each chunk is 128-144 MFMAs per wave (8-9 K cycles),
+// its successor is loaded into registers while it runs and written to LDS
+// behind it.
+#include "cn_common.h"
+#include "mlp_layout.h"
+
+namespace cn {
+namespace mlp {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+struct Params {
+  const float* p[CN_NUM_PARAMS];
+};
+
+enum ParamIdx {
+  kWXyz1 = 0, kBXyz1, kWXyz2, kBXyz2, kWOut, kBOut, kWSc1, kBSc1, kWSc2, kBSc2, kWTc1, kBTc1,
+  kWDir1, kBDir1, kWDir2, kBDir2, kWRgb, kBRgb
+};
+
+// ---------------------------------------------------------------- packing
+
+__global__ void pack_kernel(Params P, float* __restrict__ packed) {
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < kPackedFloats;
+       idx += gridDim.x * blockDim.x) {
+    float v = 0.0f;
+    if (idx >= kBiasXyz1) {
+      const int j = idx - kBiasXyz1;
+      v = j < 256 ? P.p[kBXyz1][j] : (j < 512 ? P.p[kBDir1][j - 256] : P.p[kBDir2][j - 512]);
+    } else {
+      constexpr int offs[kNumLayers + 1] = {layer_offset(0), layer_offset(1), layer_offset(2),
+                                            layer_offset(3), layer_offset(4), layer_offset(5),
+                                            layer_offset(6)};
+      int l = 0;
+      while (l + 1 < kNumLayers && idx >= offs[l + 1]) ++l;
+      int rem = idx - offs[l];
+      const int nbp = kBlocksPad[l];
+      const int ob = rem % nbp;
+      rem /= nbp;
+      const int lane = rem % 64, t = rem / 64;
+      const int i = lane & 31, h = lane >> 5;
+      int row = -1, col = -1, in_dim = 0;
+      const float* W = nullptr;
+      switch (l) {
+        case kXyz1: W = P.p[kWXyz1]; in_dim = kDimXyz; row = 32 * ob + i; col = k_from_enc(t, h, 15); break;
+        case kXyz2: W = P.p[kWXyz2]; in_dim = kHidden + kCode; row = 32 * ob + i; col = k_from_acc(t, h); break;
+        case kOut:
+          W = P.p[kWOut]; in_dim = kHidden + kCode; col = k_from_acc(t, h);
+          row = ob < 8 ? 1 + 32 * ob + i : ((ob == 8 && i == 0) ? 0 : -1);
+          break;
+        case kDir1:
+          W = P.p[kWDir1]; in_dim = kCode + kDimDir; row = 32 * ob + i;
+          if (t < 128) {
+            col = k_from_acc(t, h);
+          } else {
+            const int e = k_from_enc(t - 128, h, 6);
+            col = e < 0 ? -1 : kCode + e;
+          }
+          break;
+        case kDir2: W = P.p[kWDir2]; in_dim = kHidden; row = 32 * ob + i; col = k_from_acc(t, h); break;
+        default: W = P.p[kWRgb]; in_dim = kHidden + kCode; row = (ob == 0 && i < 3) ? i : -1; col = k_from_acc(t, h); break;
+      }
+      if (row >= 0 && col >= 0) v = W[row * in_dim + col];
+    }
+    packed[idx] = v;
+  }
+}
+
+// ---------------------------------------------------------------- code bias
+// One workgroup per code row: the three code layers (model.py:174-177), then
+// the code halves of layer_xyz2 / fc_out / fc_rgb plus their biases.
+
+__global__ __launch_bounds__(256) void code_bias_kernel(Params P, const float* __restrict__ z_s,
+                                                        const float* __restrict__ z_t,
+                                                        float* __restrict__ out) {
+  __shared__ float zs[kCode], zt[kCode], s1[kCode], s2[kCode], t1[kCode];
+  const int c = blockIdx.x, j = threadIdx.x;
+  zs[j] = z_s[(int64_t)c * kCode + j];
+  zt[j] = z_t[(int64_t)c * kCode + j];
+  __syncthreads();
+  {
+    const float* w1 = P.p[kWSc1] + j * kCode;
+    const float* w2 = P.p[kWSc2] + j * kCode;
+    const float* w3 = P.p[kWTc1] + j * kCode;
+    float a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    for (int k = 0; k < kCode; ++k) {
+      a1 = fmaf(w1[k], zs[k], a1);
+      a2 = fmaf(w2[k], zs[k], a2);
+      a3 = fmaf(w3[k], zt[k], a3);
+    }
+    s1[j] = fmaxf(a1 + P.p[kBSc1][j], 0.f);
+    s2[j] = fmaxf(a2 + P.p[kBSc2][j], 0.f);
+    t1[j] = fmaxf(a3 + P.p[kBTc1][j], 0.f);
+  }
+  __syncthreads();
+  float* o = out + (int64_t)c * kCbStride;
+  {
+    const float* wx = P.p[kWXyz2] + j * (kHidden + kCode) + kHidden;
+    const float* wo = P.p[kWOut] + (1 + j) * (kHidden + kCode) + kHidden;
+    float ax = 0.f, ao = 0.f;
+    for (int k = 0; k < kCode; ++k) {
+      ax = fmaf(wx[k], s1[k], ax);
+      ao = fmaf(wo[k], s2[k], ao);
+    }
+    o[kCbXyz2 + j] = ax + P.p[kBXyz2][j];
+    o[kCbFeat + j] = ao + P.p[kBOut][1 + j];
+  }
+  if (j < 4) {
+    float a = 0.f, b = 0.f;
+    if (j == 0) {
+      const float* w = P.p[kWOut] + kHidden;  // fc_out row 0 (sigma)
+      for (int k = 0; k < kCode; ++k) a = fmaf(w[k], s2[k], a);
+      b = P.p[kBOut][0];
+    } else {
+      const float* w = P.p[kWRgb] + (j - 1) * (kHidden + kCode) + kHidden;
+      for (int k = 0; k < kCode; ++k) a = fmaf(w[k], t1[k], a);
+      b = P.p[kBRgb][j - 1];
+    }
+    o[kCbSigma + j] = a + b;
+  }
+  if (j >= 4 && j < 8) o[kCbRgb + j - 1] = 0.f;  // pad 516..519
+}
+
+// ---------------------------------------------------------------- field kernel
+
+enum InputMode { kFromPts = 0, kFromRayZ = 1, kFromEncoded = 2 };
+
+struct FieldArgs {
+  const float* packed;
+  const float* code_bias;
+  const int64_t* code_index;
+  int64_t n_codes;
+  const float* pts;  // kFromPts: (n_rays*S, 3)
+  const float* ro;   // kFromRayZ
+  const float* rd;   // view directions (kFromPts / kFromRayZ)
+  const float* z;    // kFromRayZ: (n_rays*S)
+  const float* x;    // kFromEncoded: (m, 90)
+  int64_t n_rays, n_samples, chunk_rows, m;
+  float fx[10];
+  float fd[4];
+  float* raw;
+};
+
+constexpr int kWaves = 4;
+constexpr int kThreads = 64 * kWaves;
+constexpr int kTile = 32 * kWaves;          // samples per workgroup
+constexpr int kChunkSteps = 16;
+constexpr int kMaxChunkFloats = kChunkSteps * 64 * 12;  // fc_out chunks (nbp 12)
+
+struct Chunk {
+  int layer, t0, steps;
+};
+
+// The weight stream: every layer in 16-k-step chunks (layer_dir1 ends with
+// its 14-step view-direction chunk).
+constexpr int kNumChunks = 2 + 8 + 8 + 9 + 8 + 8;
+__host__ __device__ constexpr Chunk chunk_at(int c) {
+  return c < 2 ? Chunk{kXyz1, 16 * c, 16}
+       : c < 10 ? Chunk{kXyz2, 16 * (c - 2), 16}
+       : c < 18 ? Chunk{kOut, 16 * (c - 10), 16}
+       : c < 27 ? Chunk{kDir1, 16 * (c - 18), c == 26 ? 14 : 16}
+       : c < 35 ? Chunk{kDir2, 16 * (c - 27), 16}
+                : Chunk{kRgb, 16 * (c - 35), 16};
+}
+__host__ __device__ constexpr int chunk_floats(int c) {
+  return chunk_at(c).steps * 64 * kBlocksPad[chunk_at(c).layer];
+}
+__host__ __device__ constexpr int chunk_src(int c) {
+  return layer_offset(chunk_at(c).layer) + chunk_at(c).t0 * 64 * kBlocksPad[chunk_at(c).layer];
+}
+// float4 loads per thread to stage a chunk
+__host__ __device__ constexpr int chunk_loads(int c) { return (chunk_floats(c) / 4 + kThreads - 1) / kThreads; }
+constexpr int kMaxLoads = (kMaxChunkFloats / 4) / kThreads;  // 12
+
+struct State {
+  floatx16 act[8];   // layer input (B operands), 256 features x 32 samples
+  floatx16 acc[9];   // layer output accumulators
+  floatx16 denc;     // view-direction encoding (14 k-steps of layer_dir1)
+  float4 stage[kMaxLoads];
+  float sigma;
+  int lane, h;
+  int64_t cb_row;    // code-bias row (floats offset)
+  float vd[3];       // unit view direction of this sample's Q1 ray
+};
+
+template <int C>
+__device__ __forceinline__ void load_chunk(State& s, const float* __restrict__ packed) {
+  constexpr int n4 = chunk_floats(C) / 4;
+  const float4* src = reinterpret_cast<const float4*>(packed + chunk_src(C));
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < chunk_loads(C); ++i) {
+    const int q = i * kThreads + tid;
+    if (n4 % kThreads == 0 || q < n4) s.stage[i] = src[q];
+  }
+}
+
+template <int C>
+__device__ __forceinline__ void store_chunk(State& s, float* lds) {
+  constexpr int n4 = chunk_floats(C) / 4;
+  float4* dst = reinterpret_cast<float4*>(lds);
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < chunk_loads(C); ++i) {
+    const int q = i * kThreads + tid;
+    if (n4 % kThreads == 0 || q < n4) dst[q] = s.stage[i];
+  }
+}
+
+// Bias-initialised accumulators for layer L (acc = b, then acc += W x).
+template <int L>
+__device__ __forceinline__ void init_acc(State& s, const FieldArgs& a) {
+  const float* cb = a.code_bias + s.cb_row;
+  const float* base = L == kXyz1 ? a.packed + kBiasXyz1
+                    : L == kXyz2 ? cb + kCbXyz2
+                    : L == kOut ? cb + kCbFeat
+                    : L == kDir1 ? a.packed + kBiasDir1
+                    : L == kDir2 ? a.packed + kBiasDir2
+                                 : cb + kCbRgb;
+  if constexpr (L == kRgb) {
+    // block 0 rows 0..2 (lane half 0, registers 0..2)
+    s.acc[0] = floatx16{0};
+    if (s.h == 0) {
+      s.acc[0][0] = base[0];
+      s.acc[0][1] = base[1];
+      s.acc[0][2] = base[2];
+    }
+  } else {
+#pragma unroll
+    for (int ob = 0; ob < 8; ++ob) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 b = *reinterpret_cast<const float4*>(base + 32 * ob + 8 * q + 4 * s.h);
+        s.acc[ob][4 * q + 0] = b.x;
+        s.acc[ob][4 * q + 1] = b.y;
+        s.acc[ob][4 * q + 2] = b.z;
+        s.acc[ob][4 * q + 3] = b.w;
+      }
+    }
+    if constexpr (L == kOut) {
+      s.acc[8] = floatx16{0};
+      if (s.h == 0) s.acc[8][0] = cb[kCbSigma];
+    }
+  }
+}
+
+// B operand of k-step t (global within layer L).
+template <int L, int T>
+__device__ __forceinline__ float b_operand(const State& s) {
+  if constexpr (L == kXyz1) {
+    return s.act[T >> 4][T & 15];
+  } else if constexpr (L == kDir1 && T >= 128) {
+    return s.denc[T - 128];
+  } else {
+    return s.act[T >> 4][T & 15];
+  }
+}
+
+template <int C, int T>
+__device__ __forceinline__ void mfma_step(State& s, const float* lds) {
+  constexpr Chunk ch = chunk_at(C);
+  constexpr int L = ch.layer;
+  constexpr int nbp = kBlocksPad[L];
+  constexpr int nb = kBlocks[L];
+  const float* ap = lds + (T * 64 + s.lane) * nbp;
+  float a[nbp];
+  if constexpr (nbp % 4 == 0) {
+#pragma unroll
+    for (int j = 0; j < nbp / 4; ++j) {
+      const float4 v = *reinterpret_cast<const float4*>(ap + 4 * j);
+      a[4 * j] = v.x; a[4 * j + 1] = v.y; a[4 * j + 2] = v.z; a[4 * j + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < nbp; ++j) a[j] = ap[j];
+  }
+  const float b = b_operand<L, ch.t0 + T>(s);
+#pragma unroll
+  for (int ob = 0; ob < nb; ++ob) s.acc[ob] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[ob], b, s.acc[ob], 0, 0, 0);
+}
+
+template <int C, int T>
+__device__ __forceinline__ void mfma_steps(State& s, const float* lds) {
+  if constexpr (T < chunk_at(C).steps) {
+    mfma_step<C, T>(s, lds);
+    mfma_steps<C, T + 1>(s, lds);
+  }
+}
+
+// sincos pair q of lane half h: x[d] * f[k] for p = 2q + h.
+template <int Q, int NF>
+__device__ __forceinline__ void enc_pair(const float* x, const float* f, int h, float& sn, float& cs) {
+  constexpr int p0 = 2 * Q, p1 = 2 * Q + 1;
+  const float a0 = __fmul_rn(x[p0 % 3], f[p0 / 3]);
+  const float a1 = (p1 / 3 < NF) ? __fmul_rn(x[p1 % 3], f[p1 / 3]) : 0.0f;
+  sincosf(h ? a1 : a0, &sn, &cs);
+}
+
+__device__ __forceinline__ void encode_xyz(State& s, const float x[3], const float* fx) {
+#pragma unroll
+  for (int q = 0; q < 15; ++q) {
+    float sn, cs;
+    switch (q) {  // compile-time pair index after unrolling
+#define CN_PAIR(Q) case Q: enc_pair<Q, 10>(x, fx, s.h, sn, cs); break;
+      CN_PAIR(0) CN_PAIR(1) CN_PAIR(2) CN_PAIR(3) CN_PAIR(4) CN_PAIR(5) CN_PAIR(6) CN_PAIR(7)
+      CN_PAIR(8) CN_PAIR(9) CN_PAIR(10) CN_PAIR(11) CN_PAIR(12) CN_PAIR(13) CN_PAIR(14)
+#undef CN_PAIR
+    }
+    s.act[q >> 4][q & 15] = sn;
+    s.act[(q + 15) >> 4][(q + 15) & 15] = cs;
+  }
+  s.act[1][14] = s.h ? x[2] : x[0];
+  s.act[1][15] = s.h ? 0.0f : x[1];
+}
+
+__device__ __forceinline__ void encode_dir(State& s, const float* fd) {
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    float sn, cs;
+    switch (q) {
+#define CN_PAIR(Q) case Q: enc_pair<Q, 4>(s.vd, fd, s.h, sn, cs); break;
+      CN_PAIR(0) CN_PAIR(1) CN_PAIR(2) CN_PAIR(3) CN_PAIR(4) CN_PAIR(5)
+#undef CN_PAIR
+    }
+    s.denc[q] = sn;
+    s.denc[6 + q] = cs;
+  }
+  s.denc[12] = s.h ? s.vd[2] : s.vd[0];
+  s.denc[13] = s.h ? 0.0f : s.vd[1];
+}
+
+// Pre-encoded rows (CodeNeRFModel.forward on x): gather this half's features.
+template <int T>
+__device__ __forceinline__ void gather_enc_xyz(State& s, const float* xr) {
+  if constexpr (T < 32) {
+    constexpr int e0 = k_from_enc(T, 0, 15), e1 = k_from_enc(T, 1, 15);
+    const float v0 = e0 >= 0 ? xr[e0 < 0 ? 0 : e0] : 0.0f;
+    const float v1 = e1 >= 0 ? xr[e1 < 0 ? 0 : e1] : 0.0f;
+    s.act[T >> 4][T & 15] = s.h ? v1 : v0;
+    gather_enc_xyz<T + 1>(s, xr);
+  }
+}
+template <int T>
+__device__ __forceinline__ void gather_enc_dir(State& s, const float* xr) {
+  if constexpr (T < 14) {
+    constexpr int e0 = k_from_enc(T, 0, 6), e1 = k_from_enc(T, 1, 6);
+    const float v0 = e0 >= 0 ? xr[kDimXyz + (e0 < 0 ? 0 : e0)] : 0.0f;
+    const float v1 = e1 >= 0 ? xr[kDimXyz + (e1 < 0 ? 0 : e1)] : 0.0f;
+    s.denc[T] = s.h ? v1 : v0;
+    gather_enc_dir<T + 1>(s, xr);
+  }
+}
+
+template <int L>
+__device__ __forceinline__ void finish_layer(State& s) {
+  if constexpr (L == kOut) {
+#pragma unroll
+    for (int ob = 0; ob < 8; ++ob) s.act[ob] = s.acc[ob];  // feat: no activation
+    s.sigma = s.acc[8][0];
+  } else if constexpr (L != kRgb) {
+#pragma unroll
+    for (int ob = 0; ob < 8; ++ob)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s.act[ob][r] = fmaxf(s.acc[ob][r], 0.0f);
+  }
+}
+
+template <int MODE, int C>
+__device__ __forceinline__ void run_chunks(State& s, const FieldArgs& a, float* lds0, float* lds1) {
+  if constexpr (C < kNumChunks) {
+    constexpr Chunk ch = chunk_at(C);
+    float* cur = (C & 1) ? lds1 : lds0;
+    float* nxt = (C & 1) ? lds0 : lds1;
+    if constexpr (ch.t0 == 0) init_acc<ch.layer>(s, a);
+    if constexpr (C + 1 < kNumChunks) load_chunk<C + 1>(s, a.packed);
+    if constexpr (ch.layer == kDir1 && ch.t0 == 0 && MODE != kFromEncoded) encode_dir(s, a.fd);
+    mfma_steps<C, 0>(s, cur);
+    constexpr bool last_of_layer = (C + 1 == kNumChunks) || chunk_at(C + 1).layer != ch.layer;
+    if constexpr (last_of_layer) finish_layer<ch.layer>(s);
+    if constexpr (C + 1 < kNumChunks) {
+      store_chunk<C + 1>(s, nxt);
+      __syncthreads();
+    }
+    run_chunks<MODE, C + 1>(s, a, lds0, lds1);
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kThreads, 1) void field_kernel(FieldArgs a) {
+  __shared__ __attribute__((aligned(16))) float lds[2][kMaxChunkFloats];
+  State s;
+  s.lane = threadIdx.x & 63;
+  s.h = s.lane >> 5;
+  const int wave = threadIdx.x >> 6;
+  const int64_t row = (int64_t)blockIdx.x * kTile + wave * 32 + (s.lane & 31);
+  const bool valid = row < a.m;
+  const int64_t rc = valid ? row : a.m - 1;
+
+  // ---- per-sample inputs
+  int64_t code_of;
+  if constexpr (MODE == kFromEncoded) {
+    const float* xr = a.x + rc * (kDimXyz + kDimDir);
+    gather_enc_xyz<0>(s, xr);
+    gather_enc_dir<0>(s, xr);
+    code_of = rc;
+  } else {
+    const int64_t S = a.n_samples;
+    const int64_t ray = rc / S, smp = rc - ray * S;
+    float x[3];
+    if constexpr (MODE == kFromPts) {
+      x[0] = a.pts[3 * rc]; x[1] = a.pts[3 * rc + 1]; x[2] = a.pts[3 * rc + 2];
+    } else {
+      const float zv = a.z[rc];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) x[j] = mul_add_rn(a.rd[3 * ray + j], zv, a.ro[3 * ray + j]);
+    }
+    // Q1 (nerf/__init__.py:127-128): within a chunk of Rc rays, sample row
+    // k = r*S + s takes the view direction of ray k mod Rc.
+    const int64_t base = (ray / a.chunk_rows) * a.chunk_rows;
+    const int64_t rcnt = min(a.chunk_rows, a.n_rays - base);
+    const int64_t dray = base + ((ray - base) * S + smp) % rcnt;
+    const float d0 = a.rd[3 * dray], d1 = a.rd[3 * dray + 1], d2 = a.rd[3 * dray + 2];
+    const float nrm = __fsqrt_rn(__fadd_rn(__fadd_rn(__fmul_rn(d0, d0), __fmul_rn(d1, d1)), __fmul_rn(d2, d2)));
+    s.vd[0] = __fdiv_rn(d0, nrm);
+    s.vd[1] = __fdiv_rn(d1, nrm);
+    s.vd[2] = __fdiv_rn(d2, nrm);
+    encode_xyz(s, x, a.fx);
+    code_of = ray;
+  }
+  const int64_t crow = a.code_index ? a.code_index[code_of] : (a.n_codes == 1 ? 0 : code_of);
+  s.cb_row = crow * kCbStride;
+
+  // ---- weight stream prologue: chunk 0 into buffer 0
+  load_chunk<0>(s, a.packed);
+  store_chunk<0>(s, lds[0]);
+  __syncthreads();
+  run_chunks<MODE, 0>(s, a, lds[0], lds[1]);
+
+  // ---- raw = [rgb(3), sigma]: block 0 rows 0..2 of fc_rgb live in lane half 0
+  if (valid && s.h == 0) {
+    float4 o;
+    o.x = s.acc[0][0];
+    o.y = s.acc[0][1];
+    o.z = s.acc[0][2];
+    o.w = s.sigma;
+    reinterpret_cast<float4*>(a.raw)[row] = o;
+  }
+}
+
+}  // namespace mlp
+}  // namespace cn
+
+using namespace cn::mlp;
+
+namespace {
+
+int make_params(const float* const* params, Params* P) {
+  if (!params) return CN_EINVAL;
+  for (int i = 0; i < CN_NUM_PARAMS; ++i) {
+    if (!params[i]) return CN_EINVAL;
+    P->p[i] = params[i];
+  }
+  return CN_OK;
+}
+
+int launch_field(int mode, FieldArgs& a, hipStream_t st) {
+  const unsigned grid = static_cast<unsigned>(cn::ceil_div(a.m, kTile));
+  switch (mode) {
+    case kFromPts: hipLaunchKernelGGL(field_kernel<kFromPts>, dim3(grid), dim3(kThreads), 0, st, a); break;
+    case kFromRayZ: hipLaunchKernelGGL(field_kernel<kFromRayZ>, dim3(grid), dim3(kThreads), 0, st, a); break;
+    default: hipLaunchKernelGGL(field_kernel<kFromEncoded>, dim3(grid), dim3(kThreads), 0, st, a); break;
+  }
+  return cn::launch_status();
+}
+
+}  // namespace
+
+static_assert(kPackedFloats == 327424, "packed layout changed: update docs");
+static_assert(kCbStride == CN_CODE_BIAS_STRIDE, "code-bias stride mismatch");
+
+extern "C" int64_t cn_mlp_packed_floats(void) { return kPackedFloats; }
+
+extern "C" int cn_mlp_pack(const float* const* params, float* packed, cn_stream_t stream) {
+  Params P;
+  if (make_params(params, &P) != CN_OK || !packed) return CN_EINVAL;
+  hipLaunchKernelGGL(pack_kernel, dim3(cn::elementwise_grid(kPackedFloats, 256)), dim3(256), 0,
+                     cn::as_stream(stream), P, packed);
+  return cn::launch_status();
+}
+
+extern "C" int cn_code_bias(const float* const* params, const float* z_s, const float* z_t,
+                            int64_t n_codes, float* code_bias, cn_stream_t stream) {
+  Params P;
+  if (make_params(params, &P) != CN_OK) return CN_EINVAL;
+  CN_CHECK_ARG(z_s && z_t && code_bias && n_codes > 0 && n_codes <= (1ll << 31) - 1);
+  hipLaunchKernelGGL(code_bias_kernel, dim3(static_cast<unsigned>(n_codes)), dim3(256), 0,
+                     cn::as_stream(stream), P, z_s, z_t, code_bias);
+  return cn::launch_status();
+}
+
+extern "C" int cn_mlp_forward(const float* packed, const float* code_bias,
+                              const int64_t* code_index, int64_t n_codes, const float* x,
+                              int64_t m, float* raw, cn_stream_t stream) {
+  CN_CHECK_ARG(packed && code_bias && x && raw && m > 0 && n_codes > 0);
+  CN_CHECK_ARG(code_index || n_codes == 1 || n_codes == m);
+  CN_CHECK_ARG(cn::ceil_div(m, kTile) <= 0x7fffffff);
+  FieldArgs a = {};
+  a.packed = packed;
+  a.code_bias = code_bias;
+  a.code_index = code_index;
+  a.n_codes = n_codes;
+  a.x = x;
+  a.m = m;
+  a.raw = raw;
+  return launch_field(kFromEncoded, a, cn::as_stream(stream));
+}
+
+extern "C" int cn_radiance_field(const float* packed, const float* code_bias,
+                                 const int64_t* code_index, int64_t n_codes, const float* pts,
+                                 const float* ro, const float* rd, const float* z, int64_t n_rays,
+                                 int64_t n_samples, int64_t chunk_rows, const float* freqs_xyz,
+                                 const float* freqs_dir, float* raw, cn_stream_t stream) {
+  CN_CHECK_ARG(packed && code_bias && rd && raw && freqs_xyz && freqs_dir);
+  CN_CHECK_ARG(n_rays > 0 && n_samples > 0 && chunk_rows > 0 && n_codes > 0);
+  CN_CHECK_ARG(pts || (ro && z));
+  CN_CHECK_ARG(code_index || n_codes == 1 || n_codes == n_rays);
+  FieldArgs a = {};
+  a.packed = packed;
+  a.code_bias = code_bias;
+  a.code_index = code_index;
+  a.n_codes = n_codes;
+  a.pts = pts;
+  a.ro = ro;
+  a.rd = rd;
+  a.z = z;
+  a.n_rays = n_rays;
+  a.n_samples = n_samples;
+  a.chunk_rows = chunk_rows;
+  a.m = n_rays * n_samples;
+  CN_CHECK_ARG(cn::ceil_div(a.m, kTile) <= 0x7fffffff);
+  for (int i = 0; i < 10; ++i) a.fx[i] = freqs_xyz[i];
+  for (int i = 0; i < 4; ++i) a.fd[i] = freqs_dir[i];
+  a.raw = raw;
+  return launch_field(pts ? kFromPts : kFromRayZ, a, cn::as_stream(stream));
+}

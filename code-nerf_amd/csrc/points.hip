@@ -1,0 +1,207 @@
+// Point sampling: PointSampler (view_synthesis/nerf/point_sampler.py).
+//
+// sample_uniform is a pure stream (12 B ray + 4 B bin in, 16 B per sample out).
+// sample_pdf gives one wavefront to one ray: the ray's cdf, bins and merged
+// depth list live in LDS, searchsorted is a binary search there, and the
+// final sort is a rank sort (every value counts the values that precede it),
+// which handles unsorted perturbed fine samples and ties without a network.
+#include "cn_common.h"
+
+namespace {
+
+// point_sampler.py:60-70.  z = lower + (upper - lower) * t (perturb) or z_bins;
+// pts = ro + rd * z, each op rounded separately as torch does.
+__global__ void sample_uniform_kernel(const float* __restrict__ ro, const float* __restrict__ rd,
+                                      int64_t n_rays, const float* __restrict__ zb,
+                                      const float* __restrict__ lower,
+                                      const float* __restrict__ upper, int64_t nc,
+                                      const float* __restrict__ t_rand, float* __restrict__ z_out,
+                                      float* __restrict__ pts_out) {
+  const int64_t n = n_rays * nc;
+  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = q / nc, i = q % nc;
+    float z;
+    if (t_rand) {
+      z = __fadd_rn(lower[i], __fmul_rn(__fsub_rn(upper[i], lower[i]), t_rand[q]));
+    } else {
+      z = zb[i];
+    }
+    z_out[q] = z;
+    if (pts_out) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) pts_out[3 * q + j] = cn::mul_add_rn(rd[3 * r + j], z, ro[3 * r + j]);
+    }
+  }
+}
+
+// pts = ro[..., None, :] + rd[..., None, :] * z[..., :, None] (point_sampler.py:70, :118).
+__global__ void ray_points_kernel(const float* __restrict__ ro, const float* __restrict__ rd,
+                                  const float* __restrict__ z, int64_t n_rays, int64_t s,
+                                  float* __restrict__ pts) {
+  const int64_t n = n_rays * s * 3;
+  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = q / 3, j = q - 3 * e, r = e / s;
+    pts[q] = cn::mul_add_rn(rd[3 * r + j], z[e], ro[3 * r + j]);
+  }
+}
+
+constexpr int kPdfWaves = 4;       // rays per 256-thread block
+constexpr int kPdfMaxN = 512;      // nc + nf
+
+// torch.linspace(0, 1, n) on the CPU (RangeFactoriesKernel: symmetric halves).
+__device__ __forceinline__ float linspace01(int i, int n) {
+  if (n == 1) return 0.0f;
+  const float step = __fdiv_rn(1.0f, static_cast<float>(n - 1));
+  if (i < n / 2) return __fmul_rn(step, static_cast<float>(i));
+  return __fsub_rn(1.0f, __fmul_rn(step, static_cast<float>(n - 1 - i)));
+}
+
+// torch.sum over a contiguous fp32 row on the CPU (aten SumKernel.cpp): rows
+// shorter than 8 use the scalar 4-way ILP row_sum; longer rows accumulate
+// 8-wide vectors in 4 ILP partials, fold them, add the scalar tail first and
+// then the 8 lanes in order.  Exact for n < 512 (no cascade level is taken).
+__device__ float torch_cpu_row_sum(const float* x, int n) {
+  if (n < 8) {
+    float p[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    const int s = n / 4;
+    for (int i = 0; i < s; ++i)
+      for (int k = 0; k < 4; ++k) p[k] = __fadd_rn(p[k], x[4 * i + k]);
+    for (int i = 4 * s; i < n; ++i) p[0] = __fadd_rn(p[0], x[i]);
+    return __fadd_rn(__fadd_rn(__fadd_rn(p[0], p[1]), p[2]), p[3]);
+  }
+  const int nv = n / 8, s = nv / 4;
+  float fin = 0.0f;
+  for (int k = 8 * nv; k < n; ++k) fin = __fadd_rn(fin, x[k]);
+  for (int k = 0; k < 8; ++k) {
+    float a[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    for (int i = 0; i < s; ++i)
+      for (int j = 0; j < 4; ++j) a[j] = __fadd_rn(a[j], x[(4 * i + j) * 8 + k]);
+    float p = a[0];
+    for (int i = 4 * s; i < nv; ++i) p = __fadd_rn(p, x[8 * i + k]);
+    p = __fadd_rn(__fadd_rn(__fadd_rn(p, a[1]), a[2]), a[3]);
+    fin = __fadd_rn(fin, p);
+  }
+  return fin;
+}
+
+// point_sampler.py:84-118, one wave per ray.
+__global__ __launch_bounds__(256) void sample_pdf_kernel(
+    const float* __restrict__ ro, const float* __restrict__ rd, const float* __restrict__ weights,
+    int64_t w_stride, const float* __restrict__ z, int64_t n_rays, int nc, int nf,
+    const float* __restrict__ u_in, float* __restrict__ z_out, float* __restrict__ pts_out) {
+  __shared__ float s_cdf[kPdfWaves][256];
+  __shared__ float s_mid[kPdfWaves][256];
+  __shared__ float s_val[kPdfWaves][kPdfMaxN];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int64_t r_raw = blockIdx.x * (int64_t)kPdfWaves + wv;
+  const bool valid = r_raw < n_rays;       // wave-uniform; every wave reaches each barrier
+  const int64_t r = valid ? r_raw : n_rays - 1;
+  float* cdf = s_cdf[wv];
+  float* mid = s_mid[wv];
+  float* val = s_val[wv];
+  const float* zr = z + r * nc;
+  const float* wr = weights + r * w_stride;
+  const int nw = nc - 2;      // pdf entries
+  const int ncdf = nc - 1;    // cdf / bins entries
+  const int n = nc + nf;
+
+  // bins = 0.5 * (z[1:] + z[:-1]) (:85); coarse depths into the merge list
+  for (int j = lane; j < ncdf; j += 64) mid[j] = __fmul_rn(0.5f, __fadd_rn(zr[j + 1], zr[j]));
+  for (int j = lane; j < nc; j += 64) val[j] = zr[j];
+
+  // w = weights + 1e-5 (:86), staged in cdf[1..nw]
+  for (int j = lane; j < nw; j += 64) cdf[j + 1] = __fadd_rn(wr[j], 1e-5f);
+  __syncthreads();
+  if (lane == 0) {
+    // pdf = w / sum(w) (:87) with torch's CPU summation order, then
+    // cdf = [0, cumsum(pdf)] (:88-89): torch's CPU cumsum accumulates in double
+    // and rounds every prefix.  A few hundred scalar ops per ray.
+    const float total = torch_cpu_row_sum(cdf + 1, nw);
+    double acc = 0.0;
+    cdf[0] = 0.0f;
+    for (int j = 1; j <= nw; ++j) {
+      acc += static_cast<double>(__fdiv_rn(cdf[j], total));
+      cdf[j] = static_cast<float>(acc);
+    }
+  }
+  __syncthreads();
+
+  // invert the cdf (:92-113)
+  for (int i = lane; i < nf; i += 64) {
+    const float u = u_in ? u_in[r * nf + i] : linspace01(i, nf);
+    int lo = 0, hi = ncdf;  // searchsorted(right=True): first j with cdf[j] > u
+    while (lo < hi) {
+      const int m = (lo + hi) >> 1;
+      if (cdf[m] <= u) lo = m + 1; else hi = m;
+    }
+    const int below = lo - 1 > 0 ? lo - 1 : 0;
+    const int above = lo < ncdf - 1 ? lo : ncdf - 1;
+    const float c0 = cdf[below], c1 = cdf[above];
+    float denom = __fsub_rn(c1, c0);
+    if (denom < 1e-5f) denom = 1.0f;
+    const float t = __fdiv_rn(__fsub_rn(u, c0), denom);
+    const float b0 = mid[below], b1 = mid[above];
+    val[nc + i] = __fadd_rn(b0, __fmul_rn(t, __fsub_rn(b1, b0)));
+  }
+  __syncthreads();
+  if (!valid) return;
+
+  // sort(cat(z, samples)) (:116): stable rank of every value
+  for (int i = lane; i < n; i += 64) {
+    const float v = val[i];
+    int pos = 0;
+    for (int k = 0; k < n; ++k) {
+      const float w = val[k];
+      pos += (w < v) || (w == v && k < i);
+    }
+    float* zo = z_out + r * n;
+    zo[pos] = v;
+    if (pts_out) {
+      float* po = pts_out + (r * n + pos) * 3;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) po[j] = cn::mul_add_rn(rd[3 * r + j], v, ro[3 * r + j]);
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int cn_sample_uniform(const float* ro, const float* rd, int64_t n_rays,
+                                 const float* z_bins, const float* lower, const float* upper,
+                                 int64_t nc, const float* t_rand, float* z_out, float* pts_out,
+                                 cn_stream_t stream) {
+  CN_CHECK_ARG(n_rays > 0 && nc > 0 && z_out);
+  CN_CHECK_ARG(t_rand ? (lower && upper) : (z_bins != nullptr));
+  CN_CHECK_ARG(!pts_out || (ro && rd));
+  const int64_t n = n_rays * nc;
+  hipLaunchKernelGGL(sample_uniform_kernel, dim3(cn::elementwise_grid(n, 256)), dim3(256), 0,
+                     cn::as_stream(stream), ro, rd, n_rays, z_bins, lower, upper, nc, t_rand,
+                     z_out, pts_out);
+  return cn::launch_status();
+}
+
+extern "C" int cn_sample_pdf(const float* ro, const float* rd, const float* weights,
+                             int64_t w_stride, const float* z, int64_t n_rays, int64_t nc,
+                             int64_t nf, const float* u, float* z_out, float* pts_out,
+                             cn_stream_t stream) {
+  CN_CHECK_ARG(n_rays > 0 && nc >= 3 && nc <= 256 && nf > 0 && nc + nf <= kPdfMaxN);
+  CN_CHECK_ARG(weights && z && z_out && w_stride >= nc - 2);
+  CN_CHECK_ARG(!pts_out || (ro && rd));
+  const unsigned grid = static_cast<unsigned>(cn::ceil_div(n_rays, kPdfWaves));
+  hipLaunchKernelGGL(sample_pdf_kernel, dim3(grid), dim3(64 * kPdfWaves), 0,
+                     cn::as_stream(stream), ro, rd, weights, w_stride, z, n_rays,
+                     static_cast<int>(nc), static_cast<int>(nf), u, z_out, pts_out);
+  return cn::launch_status();
+}
+
+extern "C" int cn_ray_points(const float* ro, const float* rd, const float* z, int64_t n_rays,
+                             int64_t n_samples, float* pts, cn_stream_t stream) {
+  CN_CHECK_ARG(ro && rd && z && pts && n_rays > 0 && n_samples > 0);
+  const int64_t n = n_rays * n_samples * 3;
+  hipLaunchKernelGGL(ray_points_kernel, dim3(cn::elementwise_grid(n, 256)), dim3(256), 0,
+                     cn::as_stream(stream), ro, rd, z, n_rays, n_samples, pts);
+  return cn::launch_status();
+}

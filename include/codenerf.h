@@ -1,0 +1,151 @@
+/*
+ * codenerf.h — C ABI of libcodenerf_hip.so, the MI355X (gfx950) Code-NeRF renderer.
+ *
+ * Drop-in boundary for the ray-marching hot path of akashsharma02/code-nerf.
+ * The reference is pure Python (PyTorch 1.8) with no FFI; each entry point
+ * below replaces one of its tensor-in/tensor-out functions (cited file:line,
+ * relative to the reference root).  The Python mirror (code-nerf_amd/codenerf)
+ * binds these with ctypes; INTEGRATION.md shows the binding.
+ *
+ * Conventions (all entry points):
+ *   - Pointers are DEVICE pointers to contiguous row-major fp32 (int64 for
+ *     indices) unless marked "host".  The caller owns every buffer; nothing
+ *     is allocated, freed or retained across calls.
+ *   - Work is enqueued on `stream` (a hipStream_t; NULL = legacy default
+ *     stream) and is asynchronous; no entry point synchronises the device,
+ *     so all of them can be captured into a hipGraph.
+ *   - Return value: 0 on success; a negative CN_E* for an argument error
+ *     (nothing launched); a positive hipError_t from the launch.
+ *   - Reentrant; one process per GPU (mirrors mp.spawn in train.py/eval.py).
+ */
+#ifndef CODENERF_H_
+#define CODENERF_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* cn_stream_t; /* hipStream_t */
+
+#define CN_OK 0
+#define CN_EINVAL (-1)       /* bad size / null pointer / out-of-range argument */
+#define CN_EUNSUPPORTED (-2) /* configuration outside what the kernels implement */
+
+/* Architecture the fused MLP kernels implement (CodeNeRFModel, model.py:123-158,
+ * as every runnable config instantiates it: hidden_size 256, code sizes 256,
+ * num_encoding_fn_xyz 10, num_encoding_fn_dir 4, include_input_* True). */
+#define CN_HIDDEN 256
+#define CN_CODE 256
+#define CN_DIM_XYZ 63
+#define CN_DIM_DIR 27
+#define CN_NUM_PARAMS 18        /* weight/bias tensors of CodeNeRFModel, state_dict order */
+#define CN_CODE_BIAS_STRIDE 520 /* floats per code row: c_xyz2[256] c_out[257] c_rgb[3] pad[4] */
+
+const char* cn_version(void);
+const char* cn_error_string(int code);
+
+/* --- Rays: view_synthesis/nerf/ray_sampler.py -------------------------- */
+
+/* RaySampler.__init__ directions, ray_sampler.py:35-51 (Q3: no +0.5).
+ * dirs: (height, width, 3). */
+int cn_ray_directions(int64_t height, int64_t width, float focal, float cx, float cy,
+                      float* dirs, cn_stream_t stream);
+
+/* RaySampler.get_bundle, ray_sampler.py:84-99: rd = R * d, ro = t.
+ * dirs: (hw, 3); c2w: (batch, 4, 4); ro, rd: (batch, hw, 3). */
+int cn_ray_bundle(const float* dirs, int64_t hw, const float* c2w, int64_t batch,
+                  float* ro, float* rd, cn_stream_t stream);
+
+/* RaySampler.sample gather, ray_sampler.py:77-80 (indices from the host RNG).
+ * ro, rd: (batch, hw, 3); select_inds: (batch, sample_size) int64;
+ * ro_out, rd_out: (batch*sample_size, 3). */
+int cn_gather_rays(const float* ro, const float* rd, int64_t batch, int64_t hw,
+                   const int64_t* select_inds, int64_t sample_size, float* ro_out,
+                   float* rd_out, cn_stream_t stream);
+
+/* --- Points: view_synthesis/nerf/point_sampler.py ---------------------- */
+
+/* PointSampler.sample_uniform, point_sampler.py:49-71.
+ * z_bins/lower/upper: (nc) from PointSampler.__init__ (:33-47);
+ * t_rand: (n_rays, nc) or NULL (no perturbation);
+ * z_out: (n_rays, nc); pts_out: (n_rays, nc, 3) or NULL. */
+int cn_sample_uniform(const float* ro, const float* rd, int64_t n_rays, const float* z_bins,
+                      const float* lower, const float* upper, int64_t nc, const float* t_rand,
+                      float* z_out, float* pts_out, cn_stream_t stream);
+
+/* pts = ro + rd * z for per-ray depth lists (point_sampler.py:70 and :118).
+ * ro, rd: (n_rays, 3); z: (n_rays, n_samples); pts: (n_rays, n_samples, 3). */
+int cn_ray_points(const float* ro, const float* rd, const float* z, int64_t n_rays,
+                  int64_t n_samples, float* pts, cn_stream_t stream);
+
+/* PointSampler.sample_pdf, point_sampler.py:73-120.
+ * weights: row r at weights + r*w_stride, nc-2 values (the coarse weights[..., 1:-1]);
+ * z: (n_rays, nc) sorted; u: (n_rays, nf) or NULL (u = linspace(0, 1, nf));
+ * z_out: (n_rays, nc+nf) sorted; pts_out: (n_rays, nc+nf, 3) or NULL.  nc <= 256, nf <= 256. */
+int cn_sample_pdf(const float* ro, const float* rd, const float* weights, int64_t w_stride,
+                  const float* z, int64_t n_rays, int64_t nc, int64_t nf, const float* u,
+                  float* z_out, float* pts_out, cn_stream_t stream);
+
+/* --- Encoding: view_synthesis/nerf/position_embed.py ------------------- */
+
+/* PositionalEmbedder.embed, position_embed.py:35-53.
+ * x: (m, d); freqs: HOST array of num_freq floats (frequency_bands, :17-33);
+ * out: (m, d*(include_input + 2*num_freq)).  num_freq <= 32. */
+int cn_posenc(const float* x, int64_t m, int64_t d, const float* freqs, int64_t num_freq,
+              int include_input, float* out, cn_stream_t stream);
+
+/* --- Volume integration: view_synthesis/nerf/volumetric_render.py ------ */
+
+/* volume_render, volumetric_render.py:36-66.
+ * raw: (n_rays, n_samples, 4); z: (n_rays, n_samples); rd: (n_rays, 3);
+ * rgb: (n_rays, 3); disp, acc, depth: (n_rays); weights: (n_rays, n_samples) or NULL. */
+int cn_volume_render(const float* raw, const float* z, const float* rd, int64_t n_rays,
+                     int64_t n_samples, float* rgb, float* disp, float* acc, float* weights,
+                     float* depth, cn_stream_t stream);
+
+/* --- Code-conditioned MLP: view_synthesis/models/model.py -------------- */
+
+/* Floats needed for one packed model (cn_mlp_pack output). */
+int64_t cn_mlp_packed_floats(void);
+
+/* Pack a CodeNeRFModel state_dict (model.py:145-156) into the MFMA fragment
+ * layout the field kernel streams.  params: HOST array of CN_NUM_PARAMS device
+ * pointers in state_dict order (layer_xyz1.weight, layer_xyz1.bias, layer_xyz2.*,
+ * fc_out.*, shape_code_layer1.*, shape_code_layer2.*, texture_code_layer1.*,
+ * layer_dir1.*, layer_dir2.*, fc_rgb.*). */
+int cn_mlp_pack(const float* const* params, float* packed, cn_stream_t stream);
+
+/* The per-object terms of CodeNeRFModel.forward that the reference recomputes
+ * for every sample (model.py:174-177 and the code halves of :180-192), once
+ * per code row: out row i = [W_xyz2[:,256:] zs1 + b_xyz2 | W_out[:,256:] zs2 + b_out |
+ * W_rgb[:,256:] zt1 + b_rgb | 0 0 0 0] with zs1/zs2/zt1 the relu'd code layers.
+ * z_s, z_t: (n_codes, 256); code_bias: (n_codes, CN_CODE_BIAS_STRIDE). */
+int cn_code_bias(const float* const* params, const float* z_s, const float* z_t,
+                 int64_t n_codes, float* code_bias, cn_stream_t stream);
+
+/* CodeNeRFModel.forward(z_s, z_t, x), model.py:160-194, for pre-encoded rows.
+ * x: (m, 90) = [xyz 63 | dir 27]; code row of row i = code_index ? code_index[i]
+ * : (n_codes == 1 ? 0 : i); raw: (m, 4) = [rgb_raw(3), sigma_raw]. */
+int cn_mlp_forward(const float* packed, const float* code_bias, const int64_t* code_index,
+                   int64_t n_codes, const float* x, int64_t m, float* raw, cn_stream_t stream);
+
+/* forward_pass, nerf/__init__.py:94-134: embed + MLP for a ray chunk list.
+ * Points come from pts (n_rays, n_samples, 3) if non-NULL, else pts = ro + rd*z
+ * with z: (n_rays, n_samples).  rays are cut into consecutive chunks of
+ * chunk_rows (util.get_minibatches) and Q1 applies per chunk: sample row
+ * k = r*S + s of a chunk of Rc rays takes the view direction of ray k mod Rc.
+ * freqs_xyz (10) / freqs_dir (4): HOST arrays.  code row of ray r as in
+ * cn_mlp_forward (with r for i).  raw: (n_rays, n_samples, 4). */
+int cn_radiance_field(const float* packed, const float* code_bias, const int64_t* code_index,
+                      int64_t n_codes, const float* pts, const float* ro, const float* rd,
+                      const float* z, int64_t n_rays, int64_t n_samples, int64_t chunk_rows,
+                      const float* freqs_xyz, const float* freqs_dir, float* raw,
+                      cn_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CODENERF_H_ */

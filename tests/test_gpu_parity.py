@@ -1,0 +1,304 @@
+"""HIP path vs the reference (golden fixtures) and the CPU oracle, through the C ABI.
+
+Tolerances (north_star: rendered RGB/depth within 1e-4 absolute on fp32; ray /
+pixel integer indexing bit-exact):
+  * ray directions / bundle / gather, uniform depths, ray points: bit-exact or
+    1 ulp-level (1e-6) where the reference's einsum/bmm order differs;
+  * positional encoding: 2e-6 (accurate sinf/cosf vs torch CPU, both <= 2 ulp);
+  * raw MLP output: 1e-4 absolute (fp32 MFMA, reassociated sums);
+  * rendered rgb / depth / acc: 1e-4 absolute.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+TOL_RENDER = 1e-4
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import codenerf
+    codenerf.load_library()
+    return torch.device("cuda", 0)
+
+
+def load(name, device):
+    return {k: torch.from_numpy(v).to(device) for k, v in np.load(os.path.join(GOLDEN, name)).items()}
+
+
+def maxdiff(a, b):
+    a, b = torch.as_tensor(a).double().cpu(), torch.as_tensor(b).double().cpu()
+    assert a.shape == b.shape, (a.shape, b.shape)
+    return (a - b).abs().max().item() if a.numel() else 0.0
+
+
+def models(dev, seeds=(0, 1)):
+    from codenerf import synthetic
+    from codenerf.models import CodeNeRFModel
+    out = []
+    for s in seeds:
+        m = CodeNeRFModel(hidden_size=256, shape_code_size=256, texture_code_size=256, num_encoding_fn_xyz=10,
+                          num_encoding_fn_dir=4)
+        m.load_state_dict(synthetic.codenerf_params(s))
+        out.append(m.to(dev).eval())
+    return out
+
+
+def embedders(dev):
+    from codenerf.nerf import PositionalEmbedder
+    return PositionalEmbedder(10, True, True, torch.float32, dev), PositionalEmbedder(4, True, True, torch.float32, dev)
+
+
+# ---------------------------------------------------------------- rays
+
+
+def test_rays_bit_exact(dev):
+    from codenerf.nerf import RaySampler
+    g = load("rays_small.npz", dev)
+    rs = RaySampler(12, 16, g["intrinsics"].cpu(), sample_size=40, device=dev, datatype=torch.float32)
+    assert maxdiff(rs.directions, g["directions"]) == 0.0
+    ro, rd = rs.get_bundle(g["poses"])
+    assert maxdiff(ro, g["ro"]) == 0.0
+    assert maxdiff(rd, g["rd"]) <= 1e-6
+    np.random.seed(7)
+    o, d, sel = rs.sample(g["poses"])
+    assert np.array_equal(sel, g["select_inds"].cpu().numpy())       # host RNG: bit-exact indices
+    assert maxdiff(o, g["ro_sel"]) == 0.0
+    assert maxdiff(d, g["rd_sel"]) <= 1e-6
+
+
+# ---------------------------------------------------------------- points
+
+TAGS = ["nc8_nf8_lindepth_d", "nc8_nf8_lindepth_p", "nc8_nf8_lindisp_d", "nc8_nf8_lindisp_p",
+        "nc32_nf128_lindepth_d", "nc32_nf128_lindepth_p", "nc64_nf64_lindepth_d", "nc64_nf64_lindepth_p"]
+
+
+@pytest.mark.parametrize("tag", TAGS)
+def test_points(dev, tag):
+    from codenerf.nerf import PointSampler
+    g = load("points_small.npz", dev)
+    nc, nf = [int(x[2:]) for x in tag.split("_")[:2]]
+    mode, pert = tag.split("_")[2], tag.endswith("_p")
+    ps = PointSampler(nc, nf, 0.8, 1.8, spacing_mode=mode, perturb=pert, dtype=torch.float32, device=dev)
+    assert maxdiff(ps.z_vals, g[tag + "_zbins"]) == 0.0
+    pts, z = ps.sample_uniform(g["ro"], g["rd"], t_rand=g.get(tag + "_t_rand"))
+    assert maxdiff(z, g[tag + "_z"]) == 0.0
+    assert maxdiff(pts, g[tag + "_pts"]) == 0.0
+    pf, zf = ps.sample_pdf(g["ro"], g["rd"], g[tag + "_w"], z, u=g.get(tag + "_u"))
+    assert maxdiff(zf, g[tag + "_zf"]) <= 1e-6
+    assert bool((zf[:, 1:] >= zf[:, :-1]).all())
+    if tag + "_ptsf" in g:
+        assert maxdiff(pf, g[tag + "_ptsf"]) <= 2e-6
+
+
+def test_sample_pdf_strided_weights_and_indices(dev):
+    """weights[..., 1:-1] view (nerf/__init__.py:87) and searchsorted indices vs the oracle."""
+    from oracle import codenerf_oracle as O
+    from codenerf import ops
+    torch.manual_seed(3)
+    n, nc, nf = 777, 64, 64
+    ro, rd = torch.randn(n, 3), torch.randn(n, 3)
+    w = torch.rand(n, nc) ** 4
+    z = O.depth_bins(nc, 0.8, 1.8, "lindepth")["z"].expand(n, nc).contiguous()
+    u = torch.rand(n, nf)
+    _, zf_ref = O.sample_pdf(ro, rd, w[..., 1:-1], z, nf, u)
+    wd = w.to(dev)
+    _, zf = ops.sample_pdf(ro.to(dev), rd.to(dev), wd[..., 1:-1], z.to(dev), nf, u.to(dev), want_pts=False)
+    assert maxdiff(zf, zf_ref) == 0.0   # same sum order, double cumsum, same searchsorted -> same bits
+
+
+# ---------------------------------------------------------------- encoding
+
+
+def test_posenc(dev):
+    from codenerf.nerf import PositionalEmbedder
+    g = load("posenc.npz", dev)
+    for L, log, inc in [(10, True, True), (4, True, True), (6, False, True), (3, True, False)]:
+        k = f"L{L}_{int(log)}_{int(inc)}"
+        e = PositionalEmbedder(L, log, inc, torch.float32, dev)
+        assert maxdiff(e.frequency_bands, g[k + "_freqs"]) == 0.0
+        assert maxdiff(e.embed(g["x"]), g[k]) <= 2e-6
+
+
+# ---------------------------------------------------------------- compositing
+
+
+def test_volume_render(dev):
+    from codenerf.nerf import volume_render
+    g = load("volrender.npz", dev)
+    rgb, disp, acc, w, depth = volume_render(g["raw"], g["z"], g["rd"])
+    for a, k, tol in [(rgb, "rgb", 1e-6), (acc, "acc", 1e-6), (w, "weights", 1e-6), (depth, "depth", 2e-6),
+                      (disp, "disp", 1e-5)]:
+        ref = g[k]
+        fin = torch.isfinite(ref)
+        assert bool((torch.isfinite(a) == fin).all()), k
+        assert maxdiff(a[fin], ref[fin]) <= tol, k
+
+
+@pytest.mark.parametrize("s", [1, 7, 64, 65, 192, 300])
+def test_volume_render_sizes(dev, s):
+    from oracle import codenerf_oracle as O
+    from codenerf import ops
+    torch.manual_seed(s)
+    n = 129
+    raw = torch.randn(n, s, 4) * 2
+    z = torch.sort(1 + torch.rand(n, s), -1).values
+    rd = torch.randn(n, 3)
+    ref = O.volume_render(raw, z, rd)
+    got = ops.volume_render(raw.to(dev), z.to(dev), rd.to(dev))
+    for a, b in zip(got, ref):
+        fin = torch.isfinite(b)
+        assert maxdiff(a.cpu()[fin], b[fin]) <= 5e-6
+
+
+# ---------------------------------------------------------------- MLP
+
+
+def test_mlp_forward_golden(dev):
+    g = load("mlp.npz", dev)
+    m, = models(dev, (0,))
+    with torch.no_grad():
+        raw = m(g["z_s"], g["z_t"], g["x"])
+    assert maxdiff(raw, g["raw"]) <= 1e-4
+
+
+@pytest.mark.parametrize("m_rows", [1, 127, 128, 1000])
+def test_mlp_forward_rows(dev, m_rows):
+    from oracle import codenerf_oracle as O
+    from codenerf import synthetic
+    mdl, = models(dev, (0,))
+    torch.manual_seed(m_rows)
+    x = torch.randn(m_rows, 90)
+    zs, zt = synthetic.latent_codes(1, 1).expand(m_rows, -1), synthetic.latent_codes(2, 1).expand(m_rows, -1)
+    ref = O.codenerf_mlp(synthetic.codenerf_params(0), zs, zt, x, 63)
+    with torch.no_grad():
+        got = mdl(zs.to(dev), zt.to(dev), x.to(dev))
+    assert maxdiff(got, ref) <= 1e-4
+
+
+@pytest.mark.parametrize("r,s", [(50, 8), (37, 64), (300, 3)])
+def test_forward_pass_q1(dev, r, s):
+    """forward_pass with R not dividing anything: Q1 view-dir tiling (row k -> ray k mod R)."""
+    from oracle import codenerf_oracle as O
+    from codenerf import synthetic
+    from codenerf.nerf import forward_pass
+    torch.manual_seed(r * s)
+    rd = torch.randn(r, 3)
+    pts = torch.randn(r, s, 3)
+    zs, zt = synthetic.latent_codes(3, r), synthetic.latent_codes(4, r)     # per-ray codes
+    ref = O.forward_pass(synthetic.codenerf_params(0), O.EmbedCfg(), rd, pts, zs, zt)
+    mdl, = models(dev, (0,))
+    with torch.no_grad():
+        got = forward_pass(mdl, embedders(dev), rd.to(dev), pts.to(dev), (zs.to(dev), zt.to(dev)))
+    assert maxdiff(got, ref) <= 1e-4
+
+
+# ---------------------------------------------------------------- rendering
+
+
+def _image_rays(dev, g, h, w):
+    from codenerf.nerf import RaySampler
+    rs = RaySampler(h, w, g["intrinsics"].cpu(), sample_size=min(4096, h * w), device=dev, datatype=torch.float32)
+    ro, rd = rs.get_bundle(g["pose"])
+    return rs, ro.reshape(-1, 3), rd.reshape(-1, 3)
+
+
+@pytest.mark.parametrize("nc,nf", [(8, 8), (32, 128)])
+@pytest.mark.parametrize("n_ranks", [1, 2, 3])
+def test_render_small_golden(dev, nc, nf, n_ranks):
+    """parallel_image_render of the reference, rank slices rendered one by one (chunk 50, Q1 + Q5)."""
+    from codenerf.nerf import PointSampler, render_rays
+    from codenerf.utils import split_sizes
+    g = load("render_small.npz", dev)
+    _, ro, rd = _image_rays(dev, g, 12, 16)
+    ps = PointSampler(nc, nf, 0.8, 1.8, "lindepth", False, torch.float32, dev)
+    mc, mf = models(dev)
+    n = ro.shape[0]
+    per, _ = split_sizes(n, n_ranks)
+    outs, start = [], 0
+    with torch.no_grad():
+        for r in range(n_ranks):
+            sl = slice(start, start + per[r])
+            start += per[r]
+            o = render_rays(ro[sl], rd[sl], g["z_s"].expand(n, -1)[sl], g["z_t"].expand(n, -1)[sl], ps, embedders(dev),
+                            mc, mf, chunk_rows=50)
+            outs.append(o["rgb_fine"])
+    assert maxdiff(torch.cat(outs), g[f"nc{nc}_n{n_ranks}_rgb"]) <= TOL_RENDER
+
+
+def test_render_small_perturbed_golden(dev):
+    from codenerf.nerf import PointSampler, render_rays
+    g = load("render_small.npz", dev)
+    _, ro, rd = _image_rays(dev, g, 12, 16)
+    ps = PointSampler(8, 8, 0.8, 1.8, "lindepth", True, torch.float32, dev)
+    mc, mf = models(dev)
+    n = ro.shape[0]
+    with torch.no_grad():
+        o = render_rays(ro, rd, g["z_s"].expand(n, -1), g["z_t"].expand(n, -1), ps, embedders(dev), mc, mf,
+                        chunk_rows=50, t_rand=g["p_t_rand"], u=g["p_u"])
+    assert maxdiff(o["rgb_coarse"], g["p_rgb_coarse"]) <= TOL_RENDER
+    assert maxdiff(o["rgb_fine"], g["p_rgb_fine"]) <= TOL_RENDER
+
+
+def test_render_full_golden(dev):
+    """C2 (128x128, 64 coarse) and C3 (64+64) at full size against the reference."""
+    from codenerf.nerf import PointSampler, render_rays
+    g = load("render_full.npz", dev)
+    _, ro, rd = _image_rays(dev, g, 128, 128)
+    ps = PointSampler(64, 64, 0.8, 1.8, "lindepth", False, torch.float32, dev)
+    mc, mf = models(dev)
+    n = ro.shape[0]
+    with torch.no_grad():
+        o = render_rays(ro, rd, g["z_s"].expand(n, -1), g["z_t"].expand(n, -1), ps, embedders(dev), mc, mf,
+                        chunk_rows=4096)
+    d = {k: maxdiff(o[a], g[k]) for a, k in [("rgb_coarse", "rgb_c"), ("depth_coarse", "depth_c"),
+                                             ("acc_coarse", "acc_c"), ("rgb_fine", "rgb_f"),
+                                             ("depth_fine", "depth_f"), ("acc_fine", "acc_f")]}
+    print("max |d| vs reference:", d)
+    assert max(d.values()) <= TOL_RENDER, d
+    # size-independent properties at full size
+    assert bool((o["acc_fine"] <= 1.0 + 1e-6).all())
+    assert bool((o["z_fine"][:, 1:] >= o["z_fine"][:, :-1]).all())
+    with torch.no_grad():
+        o2 = render_rays(ro, rd, g["z_s"].expand(n, -1), g["z_t"].expand(n, -1), ps, embedders(dev), mc, mf,
+                         chunk_rows=4096)
+    assert torch.equal(o["rgb_fine"], o2["rgb_fine"])       # deterministic
+
+
+def test_chunking_is_semantics_not_tiling(dev):
+    """Q1: chunk_rows changes results exactly as the reference's chunking does (vs oracle)."""
+    from oracle import codenerf_oracle as O
+    from codenerf import synthetic
+    from codenerf.nerf import PointSampler, render_rays
+    g = load("render_small.npz", dev)
+    _, ro, rd = _image_rays(dev, g, 12, 16)
+    n = ro.shape[0]
+    zs, zt = g["z_s"].expand(n, -1), g["z_t"].expand(n, -1)
+    ps = PointSampler(8, 8, 0.8, 1.8, "lindepth", False, torch.float32, dev)
+    mc, mf = models(dev)
+    for chunk in (64, 100, 192):
+        with torch.no_grad():
+            o = render_rays(ro, rd, zs, zt, ps, embedders(dev), mc, mf, chunk_rows=chunk)
+            ref = O.render_image(ro.cpu(), rd.cpu(), zs.cpu(), zt.cpu(), O.Sampling(8, 8, 0.8, 1.8), O.EmbedCfg(),
+                                 synthetic.codenerf_params(0), synthetic.codenerf_params(1), chunk)
+        assert maxdiff(o["rgb_fine"], ref["rgb_fine"]) <= TOL_RENDER
+
+
+def test_errors_are_loud(dev):
+    from codenerf import ops
+    from codenerf._lib import CodeNerfError
+    with pytest.raises(ValueError):
+        ops.posenc(torch.zeros(4, 3), [1.0], True)              # CPU tensor: no fallback
+    with pytest.raises(AssertionError):
+        ops.volume_render(torch.zeros(4, 5, 4, device=dev), torch.zeros(4, 6, device=dev), torch.zeros(4, 3, device=dev))
+    with pytest.raises(CodeNerfError):
+        ops.sample_pdf(torch.zeros(2, 3, device=dev), torch.zeros(2, 3, device=dev), torch.zeros(2, 300, device=dev),
+                       torch.zeros(2, 302, device=dev), 8)       # nc > 256 rejected by the C ABI
