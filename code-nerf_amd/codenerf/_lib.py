@@ -35,7 +35,7 @@ SIGNATURES = {
     "cn_gather_rays": (_i, [_p, _p, _i64, _i64, _p, _i64, _p, _p, _p]),
     "cn_sample_uniform": (_i, [_p, _p, _i64, _p, _p, _p, _i64, _p, _p, _p, _p]),
     "cn_ray_points": (_i, [_p, _p, _p, _i64, _i64, _p, _p]),
-    "cn_sample_pdf": (_i, [_p, _p, _p, _i64, _p, _i64, _i64, _i64, _p, _p, _p, _p]),
+    "cn_sample_pdf": (_i, [_p, _p, _p, _i64, _p, _i64, _i64, _i64, _p, _i64, _p, _p, _p]),
     "cn_posenc": (_i, [_p, _i64, _i64, _fp, _i64, _i, _p, _p]),
     "cn_volume_render": (_i, [_p, _p, _p, _i64, _i64, _p, _p, _p, _p, _p, _p]),
     "cn_mlp_packed_floats": (_i64, []),

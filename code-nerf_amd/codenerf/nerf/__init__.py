@@ -139,7 +139,7 @@ def render_rays(ro: torch.Tensor, rd: torch.Tensor, z_s: torch.Tensor, z_t: torc
     if ps.perturb and u is None:
         u = torch.rand(n, ps.num_samples_fine, dtype=torch.float32, device=ro.device)
     _, z_f = ops.sample_pdf(ro.detach(), rd.detach(), w_c.detach()[..., 1:-1], z_c, ps.num_samples_fine,
-                            u if ps.perturb else None, want_pts=False)
+                            u if ps.perturb else ps.u_lin, want_pts=False)
     if grad:
         from ..autograd import sample_points_autograd
         raw_f = _field(fine_model, embedders, rd, z_s, z_t, chunk_rows, pts=sample_points_autograd(ro, rd, z_f))

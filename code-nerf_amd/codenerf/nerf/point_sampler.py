@@ -38,6 +38,9 @@ class PointSampler(object):
         self.mids = mids.to(self.device)
         self.upper = torch.cat((mids, z[-1:])).to(self.device)
         self.lower = torch.cat((z[:1], mids)).to(self.device)
+        # u of the unperturbed inverse-CDF pass (point_sampler.py:95), built by torch
+        # on the host once: the same bits as the reference's linspace
+        self.u_lin = torch.linspace(0.0, 1.0, steps=num_samples_fine, dtype=torch.float32).to(self.device)
 
     def sample_uniform(self, ro: torch.Tensor, rd: torch.Tensor, t_rand: Optional[torch.Tensor] = None,
                        want_pts: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -57,6 +60,6 @@ class PointSampler(object):
         if self.perturb and u is None:
             u = torch.rand(weights.shape[0], self.num_samples_fine, dtype=torch.float32, device=weights.device)
         _, z = ops.sample_pdf(ro.detach(), rd.detach(), weights.detach(), z_vals.detach(), self.num_samples_fine,
-                              u if self.perturb else None, want_pts=False)
+                              u if self.perturb else self.u_lin, want_pts=False)
         from ..autograd import sample_points_autograd
         return (sample_points_autograd(ro, rd, z) if want_pts else None), z

@@ -104,7 +104,8 @@ def sample_pdf(ro: Tensor, rd: Tensor, weights: Tensor, z: Tensor, num_fine: int
                u: Optional[Tensor] = None, want_pts: bool = True):
     """PointSampler.sample_pdf (point_sampler.py:73-120) -> pts (R,Nc+Nf,3) | None, z (R,Nc+Nf).
 
-    ``weights`` may be the strided view ``w[..., 1:-1]`` of a contiguous (R, Nc) tensor.
+    ``weights`` may be the strided view ``w[..., 1:-1]`` of a contiguous (R, Nc) tensor;
+    ``u`` is (R, Nf) per-ray draws or one (Nf,) row shared by every ray.
     """
     lib = _lib_ready()
     ro, rd, z = _cuda(ro, "ro"), _cuda(rd, "rd"), _cuda(z, "z_vals")
@@ -113,12 +114,14 @@ def sample_pdf(ro: Tensor, rd: Tensor, weights: Tensor, z: Tensor, num_fine: int
     if weights.device.type != "cuda" or weights.dtype != torch.float32 or weights.stride(-1) != 1:
         weights = _cuda(weights, "weights")
     w_stride = weights.stride(0)
+    u_stride = 0
     if u is not None:
         u = _cuda(u, "u")
-        assert u.shape == (n, num_fine), "u must be (num_rays, num_fine)"
+        assert u.shape in ((n, num_fine), (num_fine,)), "u must be (num_rays, num_fine) or (num_fine,)"
+        u_stride = num_fine if u.dim() == 2 else 0
     zo = torch.empty(n, nc + num_fine, device=z.device, dtype=torch.float32)
     pts = torch.empty(n, nc + num_fine, 3, device=z.device, dtype=torch.float32) if want_pts else None
-    check(lib.cn_sample_pdf(ptr(ro), ptr(rd), ptr(weights), w_stride, ptr(z), n, nc, num_fine, ptr(u), ptr(zo),
+    check(lib.cn_sample_pdf(ptr(ro), ptr(rd), ptr(weights), w_stride, ptr(z), n, nc, num_fine, ptr(u), u_stride, ptr(zo),
                             ptr(pts), stream_of(zo)), "cn_sample_pdf")
     return pts, zo
 
@@ -156,6 +159,8 @@ def volume_render(raw: Tensor, z: Tensor, rd: Tensor, want_weights: bool = True)
     w = torch.empty(n, s, device=dev, dtype=torch.float32) if want_weights else None
     check(lib.cn_volume_render(ptr(raw), ptr(z), ptr(rd), n, s, ptr(rgb), ptr(disp), ptr(acc), ptr(w), ptr(depth),
                                stream_of(raw)), "cn_volume_render")
+    if w is not None and s == 1:
+        w = w[:, :0]          # the reference's S == 1 weights are (R, 0) (see volume.hip)
     return rgb, disp, acc, w, depth
 
 

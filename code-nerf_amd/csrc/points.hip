@@ -90,7 +90,8 @@ __device__ float torch_cpu_row_sum(const float* x, int n) {
 __global__ __launch_bounds__(256) void sample_pdf_kernel(
     const float* __restrict__ ro, const float* __restrict__ rd, const float* __restrict__ weights,
     int64_t w_stride, const float* __restrict__ z, int64_t n_rays, int nc, int nf,
-    const float* __restrict__ u_in, float* __restrict__ z_out, float* __restrict__ pts_out) {
+    const float* __restrict__ u_in, int64_t u_stride, float* __restrict__ z_out,
+    float* __restrict__ pts_out) {
   __shared__ float s_cdf[kPdfWaves][256];
   __shared__ float s_mid[kPdfWaves][256];
   __shared__ float s_val[kPdfWaves][kPdfMaxN];
@@ -131,7 +132,7 @@ __global__ __launch_bounds__(256) void sample_pdf_kernel(
 
   // invert the cdf (:92-113)
   for (int i = lane; i < nf; i += 64) {
-    const float u = u_in ? u_in[r * nf + i] : linspace01(i, nf);
+    const float u = u_in ? u_in[r * u_stride + i] : linspace01(i, nf);
     int lo = 0, hi = ncdf;  // searchsorted(right=True): first j with cdf[j] > u
     while (lo < hi) {
       const int m = (lo + hi) >> 1;
@@ -185,15 +186,16 @@ extern "C" int cn_sample_uniform(const float* ro, const float* rd, int64_t n_ray
 
 extern "C" int cn_sample_pdf(const float* ro, const float* rd, const float* weights,
                              int64_t w_stride, const float* z, int64_t n_rays, int64_t nc,
-                             int64_t nf, const float* u, float* z_out, float* pts_out,
-                             cn_stream_t stream) {
+                             int64_t nf, const float* u, int64_t u_stride, float* z_out,
+                             float* pts_out, cn_stream_t stream) {
   CN_CHECK_ARG(n_rays > 0 && nc >= 3 && nc <= 256 && nf > 0 && nc + nf <= kPdfMaxN);
   CN_CHECK_ARG(weights && z && z_out && w_stride >= nc - 2);
   CN_CHECK_ARG(!pts_out || (ro && rd));
+  CN_CHECK_ARG(!u || u_stride == 0 || u_stride >= nf);
   const unsigned grid = static_cast<unsigned>(cn::ceil_div(n_rays, kPdfWaves));
   hipLaunchKernelGGL(sample_pdf_kernel, dim3(grid), dim3(64 * kPdfWaves), 0,
                      cn::as_stream(stream), ro, rd, weights, w_stride, z, n_rays,
-                     static_cast<int>(nc), static_cast<int>(nf), u, z_out, pts_out);
+                     static_cast<int>(nc), static_cast<int>(nf), u, u_stride, z_out, pts_out);
   return cn::launch_status();
 }
 

@@ -32,15 +32,19 @@ __device__ __forceinline__ float wave_sum(float v) {
 
 __global__ __launch_bounds__(256) void volume_render_kernel(
     const float* __restrict__ raw, const float* __restrict__ z, const float* __restrict__ rd,
-    int64_t n_rays, int S, float* __restrict__ rgb, float* __restrict__ disp,
+    int64_t n_rays, int S_in, float* __restrict__ rgb, float* __restrict__ disp,
     float* __restrict__ acc, float* __restrict__ weights, float* __restrict__ depth) {
   const int lane = threadIdx.x & 63;
   const int64_t r = blockIdx.x * (int64_t)kRaysPerBlock + (threadIdx.x >> 6);
   if (r >= n_rays) return;
-  const int run = (S + 63) / 64;
+  // S == 1: the reference's dists = cat(z[1:] - z[:-1], full_like(that[..., :1], 1e10))
+  // is EMPTY (both pieces are 0 wide), so no sample contributes (rgb = acc = depth = 0,
+  // disp = NaN, weights (R, 0)).  Reproduced by treating the ray as sample-free.
+  const int S = S_in == 1 ? 0 : S_in;
+  const int run = (S_in + 63) / 64;
   const int j0 = lane * run;
-  const float* zr = z + r * S;
-  const float4* rr = reinterpret_cast<const float4*>(raw) + r * S;
+  const float* zr = z + r * S_in;
+  const float4* rr = reinterpret_cast<const float4*>(raw) + r * S_in;
   const float d0 = rd[3 * r], d1 = rd[3 * r + 1], d2 = rd[3 * r + 2];
   const float nrm = __fsqrt_rn(__fadd_rn(__fadd_rn(__fmul_rn(d0, d0), __fmul_rn(d1, d1)), __fmul_rn(d2, d2)));
 
@@ -81,7 +85,7 @@ __global__ __launch_bounds__(256) void volume_render_kernel(
       cb += w * c2;
       dep += w * zz[i];
       ac += w;
-      if (weights) weights[r * S + j] = w;
+      if (weights) weights[r * S_in + j] = w;
       if (j + 1 < S) prefix += static_cast<double>(sd[i]);
     }
   }
@@ -96,7 +100,9 @@ __global__ __launch_bounds__(256) void volume_render_kernel(
     rgb[3 * r + 2] = cb;
     depth[r] = dep;
     acc[r] = ac;
-    disp[r] = 1.0f / fmaxf(1e-10f, dep / ac);  // (:63); NaN when acc == 0, as in torch
+    // (:63) torch.max propagates NaN: disp is NaN when acc == 0
+    const float q = dep / ac;
+    disp[r] = (q != q) ? q : 1.0f / fmaxf(1e-10f, q);
   }
 }
 

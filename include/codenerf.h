@@ -82,11 +82,13 @@ int cn_ray_points(const float* ro, const float* rd, const float* z, int64_t n_ra
 
 /* PointSampler.sample_pdf, point_sampler.py:73-120.
  * weights: row r at weights + r*w_stride, nc-2 values (the coarse weights[..., 1:-1]);
- * z: (n_rays, nc) sorted; u: (n_rays, nf) or NULL (u = linspace(0, 1, nf));
+ * z: (n_rays, nc) sorted; u: row r at u + r*u_stride, nf values (u_stride 0 = one
+ * row for every ray, e.g. the host's torch.linspace(0, 1, nf)), or NULL for an
+ * in-kernel linspace;
  * z_out: (n_rays, nc+nf) sorted; pts_out: (n_rays, nc+nf, 3) or NULL.  nc <= 256, nf <= 256. */
 int cn_sample_pdf(const float* ro, const float* rd, const float* weights, int64_t w_stride,
                   const float* z, int64_t n_rays, int64_t nc, int64_t nf, const float* u,
-                  float* z_out, float* pts_out, cn_stream_t stream);
+                  int64_t u_stride, float* z_out, float* pts_out, cn_stream_t stream);
 
 /* --- Encoding: view_synthesis/nerf/position_embed.py ------------------- */
 

@@ -54,7 +54,7 @@ def test_argument_errors_need_no_gpu(lib_path):
     from codenerf import _lib
     lib = _lib.load(lib_path)
     assert lib.cn_volume_render(None, None, None, 1, 1, None, None, None, None, None, None) == _lib.CN_EINVAL
-    assert lib.cn_sample_pdf(None, None, None, 0, None, 1, 300, 8, None, None, None, None) == _lib.CN_EINVAL
+    assert lib.cn_sample_pdf(None, None, None, 0, None, 1, 300, 8, None, 0, None, None, None) == _lib.CN_EINVAL
     assert lib.cn_radiance_field(None, None, None, 1, None, None, None, None, 1, 1, 1, None, None, None, None) \
         == _lib.CN_EINVAL
 
