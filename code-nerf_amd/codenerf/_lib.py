@@ -18,6 +18,8 @@ LIB_PATH = os.environ.get("CODENERF_LIB", os.path.join(_HERE, "lib", "libcodener
 
 CN_OK, CN_EINVAL, CN_EUNSUPPORTED = 0, -1, -2
 CN_NUM_PARAMS = 18
+CN_FMT_F32, CN_FMT_BF16X3 = 0, 1
+FORMATS = {"f32": CN_FMT_F32, "bf16x3": CN_FMT_BF16X3}
 CN_CODE_BIAS_STRIDE = 520
 
 _p = ctypes.c_void_p
@@ -38,11 +40,11 @@ SIGNATURES = {
     "cn_sample_pdf": (_i, [_p, _p, _p, _i64, _p, _i64, _i64, _i64, _p, _i64, _p, _p, _p]),
     "cn_posenc": (_i, [_p, _i64, _i64, _fp, _i64, _i, _p, _p]),
     "cn_volume_render": (_i, [_p, _p, _p, _i64, _i64, _p, _p, _p, _p, _p, _p]),
-    "cn_mlp_packed_floats": (_i64, []),
-    "cn_mlp_pack": (_i, [ctypes.POINTER(_p), _p, _p]),
+    "cn_mlp_packed_floats": (_i64, [_i]),
+    "cn_mlp_pack": (_i, [ctypes.POINTER(_p), _i, _p, _p]),
     "cn_code_bias": (_i, [ctypes.POINTER(_p), _p, _p, _i64, _p, _p]),
-    "cn_mlp_forward": (_i, [_p, _p, _p, _i64, _p, _i64, _p, _p]),
-    "cn_radiance_field": (_i, [_p, _p, _p, _i64, _p, _p, _p, _p, _i64, _i64, _i64, _fp, _fp, _p, _p]),
+    "cn_mlp_forward": (_i, [_p, _i, _p, _p, _i64, _p, _i64, _p, _p]),
+    "cn_radiance_field": (_i, [_p, _i, _p, _p, _i64, _p, _p, _p, _p, _i64, _i64, _i64, _fp, _fp, _p, _p]),
 }
 
 _lib: Optional[ctypes.CDLL] = None

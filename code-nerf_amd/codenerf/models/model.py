@@ -12,6 +12,7 @@ can be inspected) but raise on forward.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Tuple
 
 import torch
@@ -43,6 +44,9 @@ class CodeNeRFModel(torch.nn.Module):
         self.layer_dir1 = torch.nn.Linear(self.dim_dir + c, h)
         self.layer_dir2 = torch.nn.Linear(h, h)
         self.fc_rgb = torch.nn.Linear(h + texture_code_size, 3)
+        # field-kernel arithmetic: "bf16x3" (3-product bf16 split, fp32 accumulate) or
+        # "f32" (exact-product fp32 MFMA); both are held to the same parity tests
+        self.precision = os.environ.get("CODENERF_PRECISION", "bf16x3")
         self._packed = None
         self._packed_key = None
 
@@ -69,9 +73,9 @@ class CodeNeRFModel(torch.nn.Module):
         """MFMA-fragment layout of the weights, repacked whenever a parameter changed."""
         self._require_supported()
         params = self.param_list()
-        key = tuple((p.data_ptr(), p._version) for p in params)
+        key = (self.precision,) + tuple((p.data_ptr(), p._version) for p in params)
         if self._packed is None or self._packed_key != key:
-            self._packed = ops.mlp_pack(params)
+            self._packed = ops.mlp_pack(params, self.precision)
             self._packed_key = key
         return self._packed
 
@@ -87,7 +91,7 @@ class CodeNeRFModel(torch.nn.Module):
             return mlp_forward_autograd(self, z_s, z_t, x)
         codes_s, codes_t, index = _dedupe_codes(z_s, z_t)
         cb = ops.code_bias(self.param_list(), codes_s, codes_t)
-        return ops.mlp_forward(self.packed(), cb, x, index)
+        return ops.mlp_forward(self.packed(), cb, x, index, precision=self.precision)
 
 
 def _dedupe_codes(z_s: torch.Tensor, z_t: torch.Tensor):

@@ -167,18 +167,28 @@ def volume_render(raw: Tensor, z: Tensor, rd: Tensor, want_weights: bool = True)
 # ------------------------------------------------------------------ MLP
 
 
-def mlp_packed_floats() -> int:
-    return int(_lib_ready().cn_mlp_packed_floats())
+def _fmt(precision: str) -> int:
+    if precision not in _lib.FORMATS:
+        raise ValueError(f"precision must be one of {sorted(_lib.FORMATS)}, got {precision!r}")
+    return _lib.FORMATS[precision]
 
 
-def mlp_pack(params: Sequence[Tensor]) -> Tensor:
-    """Pack a CodeNeRFModel state_dict (model.py:145-156, state_dict order) for the field kernel."""
+def mlp_packed_floats(precision: str = "f32") -> int:
+    return int(_lib_ready().cn_mlp_packed_floats(_fmt(precision)))
+
+
+def mlp_pack(params: Sequence[Tensor], precision: str = "f32") -> Tensor:
+    """Pack a CodeNeRFModel state_dict (model.py:145-156, state_dict order) for the field kernel.
+
+    precision "f32": fp32 fragments for v_mfma_f32_32x32x2_f32; "bf16x3": bf16 hi/lo
+    fragments for the 3-product split on v_mfma_f32_32x32x16_bf16 (include/codenerf.h).
+    """
     lib = _lib_ready()
     assert len(params) == _lib.CN_NUM_PARAMS, "expected the 18 CodeNeRFModel weight/bias tensors"
     params = [_cuda(p.detach(), f"param{i}") for i, p in enumerate(params)]
-    out = torch.empty(mlp_packed_floats(), device=params[0].device, dtype=torch.float32)
+    out = torch.empty(mlp_packed_floats(precision), device=params[0].device, dtype=torch.float32)
     arr, keep = _lib.pointer_array(params)
-    check(lib.cn_mlp_pack(arr, ptr(out), stream_of(out)), "cn_mlp_pack")
+    check(lib.cn_mlp_pack(arr, _fmt(precision), ptr(out), stream_of(out)), "cn_mlp_pack")
     del keep
     return out
 
@@ -196,7 +206,8 @@ def code_bias(params: Sequence[Tensor], z_s: Tensor, z_t: Tensor) -> Tensor:
     return out
 
 
-def mlp_forward(packed: Tensor, cb: Tensor, x: Tensor, code_index: Optional[Tensor] = None) -> Tensor:
+def mlp_forward(packed: Tensor, cb: Tensor, x: Tensor, code_index: Optional[Tensor] = None,
+                precision: str = "f32") -> Tensor:
     """CodeNeRFModel.forward on pre-encoded rows (model.py:160-194): (M, 90) -> (M, 4)."""
     lib = _lib_ready()
     x = _cuda(x, "x")
@@ -208,7 +219,8 @@ def mlp_forward(packed: Tensor, cb: Tensor, x: Tensor, code_index: Optional[Tens
     else:
         assert n_codes in (1, m), "codes must be one row or one row per sample"
     raw = torch.empty(m, 4, device=x.device, dtype=torch.float32)
-    check(lib.cn_mlp_forward(ptr(packed), ptr(cb), ptr(code_index), n_codes, ptr(x), m, ptr(raw), stream_of(x)),
+    check(lib.cn_mlp_forward(ptr(packed), _fmt(precision), ptr(cb), ptr(code_index), n_codes, ptr(x), m, ptr(raw),
+                             stream_of(x)),
           "cn_mlp_forward")
     return raw
 
@@ -216,7 +228,7 @@ def mlp_forward(packed: Tensor, cb: Tensor, x: Tensor, code_index: Optional[Tens
 def radiance_field(packed: Tensor, cb: Tensor, rd: Tensor, n_samples: int, chunk_rows: int,
                    freqs_xyz: Sequence[float], freqs_dir: Sequence[float], pts: Optional[Tensor] = None,
                    ro: Optional[Tensor] = None, z: Optional[Tensor] = None,
-                   code_index: Optional[Tensor] = None) -> Tensor:
+                   code_index: Optional[Tensor] = None, precision: str = "f32") -> Tensor:
     """forward_pass (nerf/__init__.py:94-134) fused with the MLP -> raw (R, S, 4)."""
     lib = _lib_ready()
     rd = _cuda(rd, "rd")
@@ -234,7 +246,7 @@ def radiance_field(packed: Tensor, cb: Tensor, rd: Tensor, n_samples: int, chunk
         assert n_codes in (1, n), "codes must be one row or one row per ray"
     assert len(freqs_xyz) == 10 and len(freqs_dir) == 4, "the field kernel implements L_xyz=10, L_dir=4"
     raw = torch.empty(n, n_samples, 4, device=rd.device, dtype=torch.float32)
-    check(lib.cn_radiance_field(ptr(packed), ptr(cb), ptr(code_index), n_codes, ptr(pts), ptr(ro), ptr(rd), ptr(z),
+    check(lib.cn_radiance_field(ptr(packed), _fmt(precision), ptr(cb), ptr(code_index), n_codes, ptr(pts), ptr(ro), ptr(rd), ptr(z),
                                 n, n_samples, chunk_rows, _lib.host_floats(freqs_xyz), _lib.host_floats(freqs_dir),
                                 ptr(raw), stream_of(rd)), "cn_radiance_field")
     return raw

@@ -18,22 +18,10 @@
 // chunks of 16 k-steps; each chunk is 128-144 MFMAs per wave (8-9 K cycles),
 // its successor is loaded into registers while it runs and written to LDS
 // behind it.
-#include "cn_common.h"
-#include "mlp_layout.h"
+#include "mlp_common.h"
 
 namespace cn {
 namespace mlp {
-
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-
-struct Params {
-  const float* p[CN_NUM_PARAMS];
-};
-
-enum ParamIdx {
-  kWXyz1 = 0, kBXyz1, kWXyz2, kBXyz2, kWOut, kBOut, kWSc1, kBSc1, kWSc2, kBSc2, kWTc1, kBTc1,
-  kWDir1, kBDir1, kWDir2, kBDir2, kWRgb, kBRgb
-};
 
 // ---------------------------------------------------------------- packing
 
@@ -139,24 +127,6 @@ __global__ __launch_bounds__(256) void code_bias_kernel(Params P, const float* _
 }
 
 // ---------------------------------------------------------------- field kernel
-
-enum InputMode { kFromPts = 0, kFromRayZ = 1, kFromEncoded = 2 };
-
-struct FieldArgs {
-  const float* packed;
-  const float* code_bias;
-  const int64_t* code_index;
-  int64_t n_codes;
-  const float* pts;  // kFromPts: (n_rays*S, 3)
-  const float* ro;   // kFromRayZ
-  const float* rd;   // view directions (kFromPts / kFromRayZ)
-  const float* z;    // kFromRayZ: (n_rays*S)
-  const float* x;    // kFromEncoded: (m, 90)
-  int64_t n_rays, n_samples, chunk_rows, m;
-  float fx[10];
-  float fd[4];
-  float* raw;
-};
 
 constexpr int kWaves = 4;
 constexpr int kThreads = 64 * kWaves;
@@ -304,68 +274,10 @@ __device__ __forceinline__ void mfma_steps(State& s, const float* lds) {
   }
 }
 
-// sincos pair q of lane half h: x[d] * f[k] for p = 2q + h.
-template <int Q, int NF>
-__device__ __forceinline__ void enc_pair(const float* x, const float* f, int h, float& sn, float& cs) {
-  constexpr int p0 = 2 * Q, p1 = 2 * Q + 1;
-  const float a0 = __fmul_rn(x[p0 % 3], f[p0 / 3]);
-  const float a1 = (p1 / 3 < NF) ? __fmul_rn(x[p1 % 3], f[p1 / 3]) : 0.0f;
-  sincosf(h ? a1 : a0, &sn, &cs);
-}
-
-__device__ __forceinline__ void encode_xyz(State& s, const float x[3], const float* fx) {
+template <int N>
+__device__ __forceinline__ void put_act(State& s, const float* v) {
 #pragma unroll
-  for (int q = 0; q < 15; ++q) {
-    float sn, cs;
-    switch (q) {  // compile-time pair index after unrolling
-#define CN_PAIR(Q) case Q: enc_pair<Q, 10>(x, fx, s.h, sn, cs); break;
-      CN_PAIR(0) CN_PAIR(1) CN_PAIR(2) CN_PAIR(3) CN_PAIR(4) CN_PAIR(5) CN_PAIR(6) CN_PAIR(7)
-      CN_PAIR(8) CN_PAIR(9) CN_PAIR(10) CN_PAIR(11) CN_PAIR(12) CN_PAIR(13) CN_PAIR(14)
-#undef CN_PAIR
-    }
-    s.act[q >> 4][q & 15] = sn;
-    s.act[(q + 15) >> 4][(q + 15) & 15] = cs;
-  }
-  s.act[1][14] = s.h ? x[2] : x[0];
-  s.act[1][15] = s.h ? 0.0f : x[1];
-}
-
-__device__ __forceinline__ void encode_dir(State& s, const float* fd) {
-#pragma unroll
-  for (int q = 0; q < 6; ++q) {
-    float sn, cs;
-    switch (q) {
-#define CN_PAIR(Q) case Q: enc_pair<Q, 4>(s.vd, fd, s.h, sn, cs); break;
-      CN_PAIR(0) CN_PAIR(1) CN_PAIR(2) CN_PAIR(3) CN_PAIR(4) CN_PAIR(5)
-#undef CN_PAIR
-    }
-    s.denc[q] = sn;
-    s.denc[6 + q] = cs;
-  }
-  s.denc[12] = s.h ? s.vd[2] : s.vd[0];
-  s.denc[13] = s.h ? 0.0f : s.vd[1];
-}
-
-// Pre-encoded rows (CodeNeRFModel.forward on x): gather this half's features.
-template <int T>
-__device__ __forceinline__ void gather_enc_xyz(State& s, const float* xr) {
-  if constexpr (T < 32) {
-    constexpr int e0 = k_from_enc(T, 0, 15), e1 = k_from_enc(T, 1, 15);
-    const float v0 = e0 >= 0 ? xr[e0 < 0 ? 0 : e0] : 0.0f;
-    const float v1 = e1 >= 0 ? xr[e1 < 0 ? 0 : e1] : 0.0f;
-    s.act[T >> 4][T & 15] = s.h ? v1 : v0;
-    gather_enc_xyz<T + 1>(s, xr);
-  }
-}
-template <int T>
-__device__ __forceinline__ void gather_enc_dir(State& s, const float* xr) {
-  if constexpr (T < 14) {
-    constexpr int e0 = k_from_enc(T, 0, 6), e1 = k_from_enc(T, 1, 6);
-    const float v0 = e0 >= 0 ? xr[kDimXyz + (e0 < 0 ? 0 : e0)] : 0.0f;
-    const float v1 = e1 >= 0 ? xr[kDimXyz + (e1 < 0 ? 0 : e1)] : 0.0f;
-    s.denc[T] = s.h ? v1 : v0;
-    gather_enc_dir<T + 1>(s, xr);
-  }
+  for (int t = 0; t < N; ++t) s.act[t >> 4][t & 15] = v[t];
 }
 
 template <int L>
@@ -390,7 +302,12 @@ __device__ __forceinline__ void run_chunks(State& s, const FieldArgs& a, float* 
     float* nxt = (C & 1) ? lds0 : lds1;
     if constexpr (ch.t0 == 0) init_acc<ch.layer>(s, a);
     if constexpr (C + 1 < kNumChunks) load_chunk<C + 1>(s, a.packed);
-    if constexpr (ch.layer == kDir1 && ch.t0 == 0 && MODE != kFromEncoded) encode_dir(s, a.fd);
+    if constexpr (ch.layer == kDir1 && ch.t0 == 0 && MODE != kFromEncoded) {
+      float v[14];
+      encode_pairs<6, 4>(s.vd, a.fd, s.h, v);
+#pragma unroll
+      for (int t = 0; t < 14; ++t) s.denc[t] = v[t];
+    }
     mfma_steps<C, 0>(s, cur);
     constexpr bool last_of_layer = (C + 1 == kNumChunks) || chunk_at(C + 1).layer != ch.layer;
     if constexpr (last_of_layer) finish_layer<ch.layer>(s);
@@ -414,38 +331,22 @@ __global__ __launch_bounds__(kThreads, 1) void field_kernel(FieldArgs a) {
   const int64_t rc = valid ? row : a.m - 1;
 
   // ---- per-sample inputs
-  int64_t code_of;
+  const SampleIn in = decode_sample<MODE>(a, rc);
+  float enc[32];
   if constexpr (MODE == kFromEncoded) {
     const float* xr = a.x + rc * (kDimXyz + kDimDir);
-    gather_enc_xyz<0>(s, xr);
-    gather_enc_dir<0>(s, xr);
-    code_of = rc;
-  } else {
-    const int64_t S = a.n_samples;
-    const int64_t ray = rc / S, smp = rc - ray * S;
-    float x[3];
-    if constexpr (MODE == kFromPts) {
-      x[0] = a.pts[3 * rc]; x[1] = a.pts[3 * rc + 1]; x[2] = a.pts[3 * rc + 2];
-    } else {
-      const float zv = a.z[rc];
+    gather_pairs<15>(xr, 0, s.h, enc);
+    float d[14];
+    gather_pairs<6>(xr, kDimXyz, s.h, d);
 #pragma unroll
-      for (int j = 0; j < 3; ++j) x[j] = mul_add_rn(a.rd[3 * ray + j], zv, a.ro[3 * ray + j]);
-    }
-    // Q1 (nerf/__init__.py:127-128): within a chunk of Rc rays, sample row
-    // k = r*S + s takes the view direction of ray k mod Rc.
-    const int64_t base = (ray / a.chunk_rows) * a.chunk_rows;
-    const int64_t rcnt = min(a.chunk_rows, a.n_rays - base);
-    const int64_t dray = base + ((ray - base) * S + smp) % rcnt;
-    const float d0 = a.rd[3 * dray], d1 = a.rd[3 * dray + 1], d2 = a.rd[3 * dray + 2];
-    const float nrm = __fsqrt_rn(__fadd_rn(__fadd_rn(__fmul_rn(d0, d0), __fmul_rn(d1, d1)), __fmul_rn(d2, d2)));
-    s.vd[0] = __fdiv_rn(d0, nrm);
-    s.vd[1] = __fdiv_rn(d1, nrm);
-    s.vd[2] = __fdiv_rn(d2, nrm);
-    encode_xyz(s, x, a.fx);
-    code_of = ray;
+    for (int t = 0; t < 14; ++t) s.denc[t] = d[t];
+  } else {
+    encode_pairs<15, 10>(in.x, a.fx, s.h, enc);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) s.vd[j] = in.vd[j];
   }
-  const int64_t crow = a.code_index ? a.code_index[code_of] : (a.n_codes == 1 ? 0 : code_of);
-  s.cb_row = crow * kCbStride;
+  put_act<32>(s, enc);
+  s.cb_row = code_row(a, in.code_of) * kCbStride;
 
   // ---- weight stream prologue: chunk 0 into buffer 0
   load_chunk<0>(s, a.packed);
@@ -480,7 +381,8 @@ int make_params(const float* const* params, Params* P) {
   return CN_OK;
 }
 
-int launch_field(int mode, FieldArgs& a, hipStream_t st) {
+int launch_field(int fmt, int mode, FieldArgs& a, hipStream_t st) {
+  if (fmt == CN_FMT_BF16X3) return launch_field_x3(mode, a, st);
   const unsigned grid = static_cast<unsigned>(cn::ceil_div(a.m, kTile));
   switch (mode) {
     case kFromPts: hipLaunchKernelGGL(field_kernel<kFromPts>, dim3(grid), dim3(kThreads), 0, st, a); break;
@@ -490,16 +392,22 @@ int launch_field(int mode, FieldArgs& a, hipStream_t st) {
   return cn::launch_status();
 }
 
+bool valid_fmt(int fmt) { return fmt == CN_FMT_F32 || fmt == CN_FMT_BF16X3; }
+
 }  // namespace
 
 static_assert(kPackedFloats == 327424, "packed layout changed: update docs");
 static_assert(kCbStride == CN_CODE_BIAS_STRIDE, "code-bias stride mismatch");
 
-extern "C" int64_t cn_mlp_packed_floats(void) { return kPackedFloats; }
+extern "C" int64_t cn_mlp_packed_floats(int fmt) {
+  if (!valid_fmt(fmt)) return -1;
+  return fmt == CN_FMT_BF16X3 ? packed_floats_x3() : kPackedFloats;
+}
 
-extern "C" int cn_mlp_pack(const float* const* params, float* packed, cn_stream_t stream) {
+extern "C" int cn_mlp_pack(const float* const* params, int fmt, float* packed, cn_stream_t stream) {
   Params P;
-  if (make_params(params, &P) != CN_OK || !packed) return CN_EINVAL;
+  if (make_params(params, &P) != CN_OK || !packed || !valid_fmt(fmt)) return CN_EINVAL;
+  if (fmt == CN_FMT_BF16X3) return launch_pack_x3(P, packed, cn::as_stream(stream));
   hipLaunchKernelGGL(pack_kernel, dim3(cn::elementwise_grid(kPackedFloats, 256)), dim3(256), 0,
                      cn::as_stream(stream), P, packed);
   return cn::launch_status();
@@ -515,10 +423,10 @@ extern "C" int cn_code_bias(const float* const* params, const float* z_s, const 
   return cn::launch_status();
 }
 
-extern "C" int cn_mlp_forward(const float* packed, const float* code_bias,
+extern "C" int cn_mlp_forward(const float* packed, int fmt, const float* code_bias,
                               const int64_t* code_index, int64_t n_codes, const float* x,
                               int64_t m, float* raw, cn_stream_t stream) {
-  CN_CHECK_ARG(packed && code_bias && x && raw && m > 0 && n_codes > 0);
+  CN_CHECK_ARG(packed && code_bias && x && raw && m > 0 && n_codes > 0 && valid_fmt(fmt));
   CN_CHECK_ARG(code_index || n_codes == 1 || n_codes == m);
   CN_CHECK_ARG(cn::ceil_div(m, kTile) <= 0x7fffffff);
   FieldArgs a = {};
@@ -529,15 +437,15 @@ extern "C" int cn_mlp_forward(const float* packed, const float* code_bias,
   a.x = x;
   a.m = m;
   a.raw = raw;
-  return launch_field(kFromEncoded, a, cn::as_stream(stream));
+  return launch_field(fmt, kFromEncoded, a, cn::as_stream(stream));
 }
 
-extern "C" int cn_radiance_field(const float* packed, const float* code_bias,
+extern "C" int cn_radiance_field(const float* packed, int fmt, const float* code_bias,
                                  const int64_t* code_index, int64_t n_codes, const float* pts,
                                  const float* ro, const float* rd, const float* z, int64_t n_rays,
                                  int64_t n_samples, int64_t chunk_rows, const float* freqs_xyz,
                                  const float* freqs_dir, float* raw, cn_stream_t stream) {
-  CN_CHECK_ARG(packed && code_bias && rd && raw && freqs_xyz && freqs_dir);
+  CN_CHECK_ARG(packed && code_bias && rd && raw && freqs_xyz && freqs_dir && valid_fmt(fmt));
   CN_CHECK_ARG(n_rays > 0 && n_samples > 0 && chunk_rows > 0 && n_codes > 0);
   CN_CHECK_ARG(pts || (ro && z));
   CN_CHECK_ARG(code_index || n_codes == 1 || n_codes == n_rays);
@@ -558,5 +466,5 @@ extern "C" int cn_radiance_field(const float* packed, const float* code_bias,
   for (int i = 0; i < 10; ++i) a.fx[i] = freqs_xyz[i];
   for (int i = 0; i < 4; ++i) a.fd[i] = freqs_dir[i];
   a.raw = raw;
-  return launch_field(pts ? kFromPts : kFromRayZ, a, cn::as_stream(stream));
+  return launch_field(fmt, pts ? kFromPts : kFromRayZ, a, cn::as_stream(stream));
 }

@@ -1,0 +1,125 @@
+// Pieces shared by the fp32 and 3xbf16 field kernels: launch arguments, the
+// per-sample input decode (points, Q1 view direction, code row) and the
+// positional-encoding feature values each lane half owns.
+#pragma once
+
+#include "cn_common.h"
+#include "mlp_layout.h"
+
+namespace cn {
+namespace mlp {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+struct Params {
+  const float* p[CN_NUM_PARAMS];
+};
+
+enum ParamIdx {
+  kWXyz1 = 0, kBXyz1, kWXyz2, kBXyz2, kWOut, kBOut, kWSc1, kBSc1, kWSc2, kBSc2, kWTc1, kBTc1,
+  kWDir1, kBDir1, kWDir2, kBDir2, kWRgb, kBRgb
+};
+
+enum InputMode { kFromPts = 0, kFromRayZ = 1, kFromEncoded = 2 };
+
+struct FieldArgs {
+  const float* packed;
+  const float* code_bias;
+  const int64_t* code_index;
+  int64_t n_codes;
+  const float* pts;  // kFromPts: (n_rays*S, 3)
+  const float* ro;   // kFromRayZ
+  const float* rd;   // view directions (kFromPts / kFromRayZ)
+  const float* z;    // kFromRayZ: (n_rays*S)
+  const float* x;    // kFromEncoded: (m, 90)
+  int64_t n_rays, n_samples, chunk_rows, m;
+  float fx[10];
+  float fd[4];
+  float* raw;
+};
+
+// One sample's inputs: point, unit Q1 view direction, code row.
+struct SampleIn {
+  float x[3];
+  float vd[3];
+  int64_t code_of;  // ray (or row) whose code applies
+};
+
+template <int MODE>
+__device__ __forceinline__ SampleIn decode_sample(const FieldArgs& a, int64_t rc) {
+  SampleIn in;
+  if constexpr (MODE == kFromEncoded) {
+    in.code_of = rc;
+  } else {
+    const int64_t S = a.n_samples;
+    const int64_t ray = rc / S, smp = rc - ray * S;
+    if constexpr (MODE == kFromPts) {
+      in.x[0] = a.pts[3 * rc]; in.x[1] = a.pts[3 * rc + 1]; in.x[2] = a.pts[3 * rc + 2];
+    } else {
+      const float zv = a.z[rc];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) in.x[j] = mul_add_rn(a.rd[3 * ray + j], zv, a.ro[3 * ray + j]);
+    }
+    // Q1 (nerf/__init__.py:127-128): within a chunk of Rc rays, sample row
+    // k = r*S + s takes the view direction of ray k mod Rc.
+    const int64_t base = (ray / a.chunk_rows) * a.chunk_rows;
+    const int64_t rcnt = min(a.chunk_rows, a.n_rays - base);
+    const int64_t dray = base + ((ray - base) * S + smp) % rcnt;
+    const float d0 = a.rd[3 * dray], d1 = a.rd[3 * dray + 1], d2 = a.rd[3 * dray + 2];
+    const float nrm = __fsqrt_rn(__fadd_rn(__fadd_rn(__fmul_rn(d0, d0), __fmul_rn(d1, d1)), __fmul_rn(d2, d2)));
+    in.vd[0] = __fdiv_rn(d0, nrm);
+    in.vd[1] = __fdiv_rn(d1, nrm);
+    in.vd[2] = __fdiv_rn(d2, nrm);
+    in.code_of = ray;
+  }
+  return in;
+}
+
+__device__ __forceinline__ int64_t code_row(const FieldArgs& a, int64_t code_of) {
+  return a.code_index ? a.code_index[code_of] : (a.n_codes == 1 ? 0 : code_of);
+}
+
+// sincos of pair q of lane half h: x[d] * f[k] for p = 2q + h, k = p / 3, d = p % 3.
+template <int Q, int NF>
+__device__ __forceinline__ void enc_pair(const float* x, const float* f, int h, float& sn, float& cs) {
+  constexpr int p0 = 2 * Q, p1 = 2 * Q + 1;
+  const float a0 = __fmul_rn(x[p0 % 3], f[p0 / 3]);
+  const float a1 = (p1 / 3 < NF) ? __fmul_rn(x[p1 % 3], f[p1 / 3]) : 0.0f;
+  sincosf(h ? a1 : a0, &sn, &cs);
+}
+
+// The 2P+2 encoding values lane half h feeds, in k_from_enc order (mlp_layout.h):
+// sines of its P pairs, cosines, then raw inputs (x0, x1 | x2, 0).
+template <int P, int NF, int Q = 0>
+__device__ __forceinline__ void encode_pairs(const float* x, const float* f, int h, float* out) {
+  if constexpr (Q < P) {
+    float sn, cs;
+    enc_pair<Q, NF>(x, f, h, sn, cs);
+    out[Q] = sn;
+    out[P + Q] = cs;
+    encode_pairs<P, NF, Q + 1>(x, f, h, out);
+  } else {
+    out[2 * P] = h ? x[2] : x[0];
+    out[2 * P + 1] = h ? 0.0f : x[1];
+  }
+}
+
+// 3xbf16 variant (mlp_x3.hip).
+int64_t packed_floats_x3();
+int launch_pack_x3(const Params& P, float* packed, hipStream_t st);
+int launch_field_x3(int mode, FieldArgs& a, hipStream_t st);
+
+// Pre-encoded rows: the same 2P+2 values gathered from x (base = column offset).
+template <int P, int T = 0>
+__device__ __forceinline__ void gather_pairs(const float* xr, int base, int h, float* out) {
+  if constexpr (T < 2 * P + 2) {
+    constexpr int e0 = k_from_enc(T, 0, P), e1 = k_from_enc(T, 1, P);
+    const float v0 = e0 >= 0 ? xr[base + (e0 < 0 ? 0 : e0)] : 0.0f;
+    const float v1 = e1 >= 0 ? xr[base + (e1 < 0 ? 0 : e1)] : 0.0f;
+    out[T] = h ? v1 : v0;
+    gather_pairs<P, T + 1>(xr, base, h, out);
+  }
+}
+
+}  // namespace mlp
+}  // namespace cn

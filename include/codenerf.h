@@ -41,7 +41,15 @@ typedef void* cn_stream_t; /* hipStream_t */
 #define CN_DIM_XYZ 63
 #define CN_DIM_DIR 27
 #define CN_NUM_PARAMS 18        /* weight/bias tensors of CodeNeRFModel, state_dict order */
-#define CN_CODE_BIAS_STRIDE 520 /* floats per code row: c_xyz2[256] c_out[257] c_rgb[3] pad[4] */
+#define CN_CODE_BIAS_STRIDE 520 /* floats per code row: c_xyz2[256] c_feat[256] c_sigma c_rgb[3] pad[4] */
+
+/* Packed-weight formats of the field kernel (cn_mlp_pack):
+ *   CN_FMT_F32    fp32 fragments, v_mfma_f32_32x32x2_f32 (exact f32 products);
+ *   CN_FMT_BF16X3 bf16 hi/lo fragments, Wh.Xh + Wh.Xl + Wl.Xh on
+ *                 v_mfma_f32_32x32x16_bf16 with fp32 accumulation (~2^-17 relative
+ *                 per product; 5.3x the fp32 MFMA rate). */
+#define CN_FMT_F32 0
+#define CN_FMT_BF16X3 1
 
 const char* cn_version(void);
 const char* cn_error_string(int code);
@@ -109,15 +117,15 @@ int cn_volume_render(const float* raw, const float* z, const float* rd, int64_t 
 
 /* --- Code-conditioned MLP: view_synthesis/models/model.py -------------- */
 
-/* Floats needed for one packed model (cn_mlp_pack output). */
-int64_t cn_mlp_packed_floats(void);
+/* Floats needed for one packed model of format fmt (cn_mlp_pack output); -1 for a bad fmt. */
+int64_t cn_mlp_packed_floats(int fmt);
 
 /* Pack a CodeNeRFModel state_dict (model.py:145-156) into the MFMA fragment
  * layout the field kernel streams.  params: HOST array of CN_NUM_PARAMS device
  * pointers in state_dict order (layer_xyz1.weight, layer_xyz1.bias, layer_xyz2.*,
  * fc_out.*, shape_code_layer1.*, shape_code_layer2.*, texture_code_layer1.*,
  * layer_dir1.*, layer_dir2.*, fc_rgb.*). */
-int cn_mlp_pack(const float* const* params, float* packed, cn_stream_t stream);
+int cn_mlp_pack(const float* const* params, int fmt, float* packed, cn_stream_t stream);
 
 /* The per-object terms of CodeNeRFModel.forward that the reference recomputes
  * for every sample (model.py:174-177 and the code halves of :180-192), once
@@ -130,7 +138,7 @@ int cn_code_bias(const float* const* params, const float* z_s, const float* z_t,
 /* CodeNeRFModel.forward(z_s, z_t, x), model.py:160-194, for pre-encoded rows.
  * x: (m, 90) = [xyz 63 | dir 27]; code row of row i = code_index ? code_index[i]
  * : (n_codes == 1 ? 0 : i); raw: (m, 4) = [rgb_raw(3), sigma_raw]. */
-int cn_mlp_forward(const float* packed, const float* code_bias, const int64_t* code_index,
+int cn_mlp_forward(const float* packed, int fmt, const float* code_bias, const int64_t* code_index,
                    int64_t n_codes, const float* x, int64_t m, float* raw, cn_stream_t stream);
 
 /* forward_pass, nerf/__init__.py:94-134: embed + MLP for a ray chunk list.
@@ -140,7 +148,7 @@ int cn_mlp_forward(const float* packed, const float* code_bias, const int64_t* c
  * k = r*S + s of a chunk of Rc rays takes the view direction of ray k mod Rc.
  * freqs_xyz (10) / freqs_dir (4): HOST arrays.  code row of ray r as in
  * cn_mlp_forward (with r for i).  raw: (n_rays, n_samples, 4). */
-int cn_radiance_field(const float* packed, const float* code_bias, const int64_t* code_index,
+int cn_radiance_field(const float* packed, int fmt, const float* code_bias, const int64_t* code_index,
                       int64_t n_codes, const float* pts, const float* ro, const float* rd,
                       const float* z, int64_t n_rays, int64_t n_samples, int64_t chunk_rows,
                       const float* freqs_xyz, const float* freqs_dir, float* raw,

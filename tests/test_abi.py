@@ -45,7 +45,7 @@ def test_ctypes_table_matches_header(lib_path):
     assert sorted(_lib.SIGNATURES) == declared_symbols()
     lib = _lib.load(lib_path)
     assert lib.cn_version().decode().startswith("libcodenerf_hip")
-    assert lib.cn_mlp_packed_floats() == 327424
+    assert lib.cn_mlp_packed_floats(0) == 327424 and lib.cn_mlp_packed_floats(1) == 303872
     assert lib.cn_error_string(-1).decode().startswith("invalid argument")
 
 
@@ -55,7 +55,7 @@ def test_argument_errors_need_no_gpu(lib_path):
     lib = _lib.load(lib_path)
     assert lib.cn_volume_render(None, None, None, 1, 1, None, None, None, None, None, None) == _lib.CN_EINVAL
     assert lib.cn_sample_pdf(None, None, None, 0, None, 1, 300, 8, None, 0, None, None, None) == _lib.CN_EINVAL
-    assert lib.cn_radiance_field(None, None, None, 1, None, None, None, None, 1, 1, 1, None, None, None, None) \
+    assert lib.cn_radiance_field(None, 0, None, None, 1, None, None, None, None, 1, 1, 1, None, None, None, None) \
         == _lib.CN_EINVAL
 
 

@@ -40,7 +40,13 @@ def maxdiff(a, b):
     return (a - b).abs().max().item() if a.numel() else 0.0
 
 
-def models(dev, seeds=(0, 1)):
+@pytest.fixture(params=["f32", "bf16x3"])
+def precision(request):
+    """Both field-kernel formats are held to the same tolerances."""
+    return request.param
+
+
+def models(dev, seeds=(0, 1), precision="f32"):
     from codenerf import synthetic
     from codenerf.models import CodeNeRFModel
     out = []
@@ -48,6 +54,7 @@ def models(dev, seeds=(0, 1)):
         m = CodeNeRFModel(hidden_size=256, shape_code_size=256, texture_code_size=256, num_encoding_fn_xyz=10,
                           num_encoding_fn_dir=4)
         m.load_state_dict(synthetic.codenerf_params(s))
+        m.precision = precision
         out.append(m.to(dev).eval())
     return out
 
@@ -169,19 +176,19 @@ def test_volume_render_sizes(dev, s):
 # ---------------------------------------------------------------- MLP
 
 
-def test_mlp_forward_golden(dev):
+def test_mlp_forward_golden(dev, precision):
     g = load("mlp.npz", dev)
-    m, = models(dev, (0,))
+    m, = models(dev, (0,), precision)
     with torch.no_grad():
         raw = m(g["z_s"], g["z_t"], g["x"])
     assert maxdiff(raw, g["raw"]) <= 1e-4
 
 
 @pytest.mark.parametrize("m_rows", [1, 127, 128, 1000])
-def test_mlp_forward_rows(dev, m_rows):
+def test_mlp_forward_rows(dev, precision, m_rows):
     from oracle import codenerf_oracle as O
     from codenerf import synthetic
-    mdl, = models(dev, (0,))
+    mdl, = models(dev, (0,), precision)
     torch.manual_seed(m_rows)
     x = torch.randn(m_rows, 90)
     zs, zt = synthetic.latent_codes(1, 1).expand(m_rows, -1), synthetic.latent_codes(2, 1).expand(m_rows, -1)
@@ -192,7 +199,7 @@ def test_mlp_forward_rows(dev, m_rows):
 
 
 @pytest.mark.parametrize("r,s", [(50, 8), (37, 64), (300, 3)])
-def test_forward_pass_q1(dev, r, s):
+def test_forward_pass_q1(dev, precision, r, s):
     """forward_pass with R not dividing anything: Q1 view-dir tiling (row k -> ray k mod R)."""
     from oracle import codenerf_oracle as O
     from codenerf import synthetic
@@ -202,7 +209,7 @@ def test_forward_pass_q1(dev, r, s):
     pts = torch.randn(r, s, 3)
     zs, zt = synthetic.latent_codes(3, r), synthetic.latent_codes(4, r)     # per-ray codes
     ref = O.forward_pass(synthetic.codenerf_params(0), O.EmbedCfg(), rd, pts, zs, zt)
-    mdl, = models(dev, (0,))
+    mdl, = models(dev, (0,), precision)
     with torch.no_grad():
         got = forward_pass(mdl, embedders(dev), rd.to(dev), pts.to(dev), (zs.to(dev), zt.to(dev)))
     assert maxdiff(got, ref) <= 1e-4
@@ -220,14 +227,14 @@ def _image_rays(dev, g, h, w):
 
 @pytest.mark.parametrize("nc,nf", [(8, 8), (32, 128)])
 @pytest.mark.parametrize("n_ranks", [1, 2, 3])
-def test_render_small_golden(dev, nc, nf, n_ranks):
+def test_render_small_golden(dev, precision, nc, nf, n_ranks):
     """parallel_image_render of the reference, rank slices rendered one by one (chunk 50, Q1 + Q5)."""
     from codenerf.nerf import PointSampler, render_rays
     from codenerf.utils import split_sizes
     g = load("render_small.npz", dev)
     _, ro, rd = _image_rays(dev, g, 12, 16)
     ps = PointSampler(nc, nf, 0.8, 1.8, "lindepth", False, torch.float32, dev)
-    mc, mf = models(dev)
+    mc, mf = models(dev, precision=precision)
     n = ro.shape[0]
     per, _ = split_sizes(n, n_ranks)
     outs, start = [], 0
@@ -241,12 +248,12 @@ def test_render_small_golden(dev, nc, nf, n_ranks):
     assert maxdiff(torch.cat(outs), g[f"nc{nc}_n{n_ranks}_rgb"]) <= TOL_RENDER
 
 
-def test_render_small_perturbed_golden(dev):
+def test_render_small_perturbed_golden(dev, precision):
     from codenerf.nerf import PointSampler, render_rays
     g = load("render_small.npz", dev)
     _, ro, rd = _image_rays(dev, g, 12, 16)
     ps = PointSampler(8, 8, 0.8, 1.8, "lindepth", True, torch.float32, dev)
-    mc, mf = models(dev)
+    mc, mf = models(dev, precision=precision)
     n = ro.shape[0]
     with torch.no_grad():
         o = render_rays(ro, rd, g["z_s"].expand(n, -1), g["z_t"].expand(n, -1), ps, embedders(dev), mc, mf,
@@ -255,13 +262,13 @@ def test_render_small_perturbed_golden(dev):
     assert maxdiff(o["rgb_fine"], g["p_rgb_fine"]) <= TOL_RENDER
 
 
-def test_render_full_golden(dev):
+def test_render_full_golden(dev, precision):
     """C2 (128x128, 64 coarse) and C3 (64+64) at full size against the reference."""
     from codenerf.nerf import PointSampler, render_rays
     g = load("render_full.npz", dev)
     _, ro, rd = _image_rays(dev, g, 128, 128)
     ps = PointSampler(64, 64, 0.8, 1.8, "lindepth", False, torch.float32, dev)
-    mc, mf = models(dev)
+    mc, mf = models(dev, precision=precision)
     n = ro.shape[0]
     with torch.no_grad():
         o = render_rays(ro, rd, g["z_s"].expand(n, -1), g["z_t"].expand(n, -1), ps, embedders(dev), mc, mf,
@@ -280,7 +287,7 @@ def test_render_full_golden(dev):
     assert torch.equal(o["rgb_fine"], o2["rgb_fine"])       # deterministic
 
 
-def test_chunking_is_semantics_not_tiling(dev):
+def test_chunking_is_semantics_not_tiling(dev, precision):
     """Q1: chunk_rows changes results exactly as the reference's chunking does (vs oracle)."""
     from oracle import codenerf_oracle as O
     from codenerf import synthetic
@@ -290,7 +297,7 @@ def test_chunking_is_semantics_not_tiling(dev):
     n = ro.shape[0]
     zs, zt = g["z_s"].expand(n, -1), g["z_t"].expand(n, -1)
     ps = PointSampler(8, 8, 0.8, 1.8, "lindepth", False, torch.float32, dev)
-    mc, mf = models(dev)
+    mc, mf = models(dev, precision=precision)
     for chunk in (64, 100, 192):
         with torch.no_grad():
             o = render_rays(ro, rd, zs, zt, ps, embedders(dev), mc, mf, chunk_rows=chunk)
