@@ -94,40 +94,53 @@ __global__ void pack_x3_kernel(Params P, float* __restrict__ packed) {
 }
 
 // ---------------------------------------------------------------- kernel
+//
+// Weight stream: 44 chunks of <= 2 k-steps (<= 36 KiB) through a 4-slot LDS
+// ring filled by LDS-DMA (global_load_lds, 1 KiB per wave-instruction, no
+// VGPR staging).  Chunk c+3 is issued when chunk c starts, so three chunks
+// (~4.6 K MFMA cycles) are in flight; one raw s_barrier per chunk, preceded by
+// a counted `s_waitcnt vmcnt(N)` that retires only this wave's DMA for chunk c.
+// No ordinary global load is live inside the stream (hipcc would wait
+// vmcnt(0) for it, draining the ring): per-layer biases are read with scalar
+// loads (see init_acc).
 
 constexpr int kWaves = 4;
 constexpr int kThreads = 64 * kWaves;
 constexpr int kTile = 32 * kWaves;
-constexpr int kChunkSteps = 4;
-constexpr int kMaxChunkQuads = kChunkSteps * 64 * 9 * 2;   // fc_out chunk: 72 KiB
+constexpr int kChunkSteps = 2;
+constexpr int kSlotQuads = kChunkSteps * 64 * 9 * 2;   // 36 KiB: an fc_out chunk
+constexpr int kSlots = 4;
+constexpr int kAhead = kSlots - 1;                      // chunks in flight
+constexpr int kLdsFloats = kSlots * kSlotQuads * 4;    // 144 KiB ring
 
 struct Chunk {
   int layer, s0, steps;
 };
-constexpr int kNumChunks = 1 + 4 + 4 + 5 + 4 + 4;
+// chunk c -> (layer, first k-step, k-steps); layer_dir1 ends with its 2 view-direction k-steps
+constexpr int kChunksPerLayer[kNumLayers] = {2, 8, 8, 9, 8, 8};
+constexpr int kNumChunks = 2 + 8 + 8 + 9 + 8 + 8;
 __host__ __device__ constexpr Chunk chunk_at(int c) {
-  return c < 1 ? Chunk{kXyz1, 0, 4}
-       : c < 5 ? Chunk{kXyz2, 4 * (c - 1), 4}
-       : c < 9 ? Chunk{kOut, 4 * (c - 5), 4}
-       : c < 14 ? Chunk{kDir1, 4 * (c - 9), c == 13 ? 2 : 4}
-       : c < 18 ? Chunk{kDir2, 4 * (c - 14), 4}
-                : Chunk{kRgb, 4 * (c - 18), 4};
+  int l = 0;
+  while (c >= kChunksPerLayer[l]) c -= kChunksPerLayer[l++];
+  return Chunk{l, 2 * c, 2};
 }
 __host__ __device__ constexpr int chunk_quads(int c) { return chunk_at(c).steps * 64 * kNb[chunk_at(c).layer] * 2; }
 __host__ __device__ constexpr int chunk_src(int c) {
   return layer_off(chunk_at(c).layer) + chunk_at(c).s0 * 64 * kNb[chunk_at(c).layer] * 2;
 }
-__host__ __device__ constexpr int chunk_loads(int c) { return (chunk_quads(c) + kThreads - 1) / kThreads; }
-constexpr int kMaxLoads = (kMaxChunkQuads / kThreads + 1) / 2;  // 9 (half a chunk)
+// wave-instructions (1 KiB = 64 quads each) per chunk and per wave
+__host__ __device__ constexpr int chunk_dma(int c) { return chunk_quads(c) / 64; }
+__host__ __device__ constexpr int wave_dma(int c, int w) {
+  return c >= kNumChunks ? 0 : (chunk_dma(c) - w + kWaves - 1) / kWaves;
+}
 
 struct State {
   bf16x8 bh[16], bl[16];  // B operands (hi / lo) of the current layer's 16 k-steps
   bf16x8 dh[2], dl[2];    // view-direction encoding k-steps of layer_dir1
   floatx16 acc[9];
-  float4 stage[kMaxLoads];
   float sigma;
-  int lane, h;
-  int64_t cb_row;
+  int lane, h, wave;
+  int crow;               // this lane's code-bias row
   float vd[3];
 };
 
@@ -140,104 +153,180 @@ __device__ __forceinline__ void split8(const float* v, bf16x8& hi, bf16x8& lo) {
   }
 }
 
-// The next chunk is staged through registers in two halves (one per half of
-// the current chunk's k-steps) to keep the staging to 9 float4 per thread.
-constexpr int kParts = 2;
-template <int C, int PART>
-__device__ __forceinline__ void load_chunk(State& s, const float* __restrict__ packed) {
-  constexpr int n = chunk_quads(C);
-  constexpr int nl = chunk_loads(C);
-  constexpr int i0 = PART * ((nl + kParts - 1) / kParts);
-  constexpr int i1 = (PART + 1) * ((nl + kParts - 1) / kParts) < nl ? (PART + 1) * ((nl + kParts - 1) / kParts) : nl;
-  const float4* src = reinterpret_cast<const float4*>(packed) + chunk_src(C);
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
+
+// Issue this wave's share of chunk C's DMA into ring slot C % kSlots.
+template <int C>
+__device__ __forceinline__ void issue_chunk(const State& s, const float* __restrict__ packed, float* lds) {
+  if constexpr (C < kNumChunks) {
+    constexpr int n = chunk_dma(C);
+    const float4* src = reinterpret_cast<const float4*>(packed) + chunk_src(C);
+    float4* slot = reinterpret_cast<float4*>(lds) + (C % kSlots) * kSlotQuads;
 #pragma unroll
-  for (int i = i0; i < i1; ++i) {
-    const int q = i * kThreads + threadIdx.x;
-    if (n % kThreads == 0 || q < n) s.stage[i - i0] = src[q];
+    for (int i = 0; i < (n + kWaves - 1) / kWaves; ++i) {
+      const int ins = i * kWaves + s.wave;  // wave-uniform
+      if (n % kWaves == 0 || ins < n) {
+        __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src + ins * 64 + s.lane), (lds_ptr_t)(slot + ins * 64), 16, 0, 0);
+      }
+    }
   }
 }
 
-template <int C, int PART>
-__device__ __forceinline__ void store_chunk(State& s, float4* lds) {
-  constexpr int n = chunk_quads(C);
-  constexpr int nl = chunk_loads(C);
-  constexpr int i0 = PART * ((nl + kParts - 1) / kParts);
-  constexpr int i1 = (PART + 1) * ((nl + kParts - 1) / kParts) < nl ? (PART + 1) * ((nl + kParts - 1) / kParts) : nl;
-#pragma unroll
-  for (int i = i0; i < i1; ++i) {
-    const int q = i * kThreads + threadIdx.x;
-    if (n % kThreads == 0 || q < n) lds[q] = s.stage[i - i0];
+// Wait until this wave's DMA for chunk C has landed (later chunks stay in flight).
+// One asm statement: the counted wait, this wave's LDS reads retired, the barrier.
+// Nothing (no LDS read of chunk C) can be scheduled across it.
+template <int C, int W>
+__device__ __forceinline__ void wait_chunk_w() {
+  constexpr int pending = wave_dma(C + 1, W) + wave_dma(C + 2, W);
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(pending) : "memory");
+}
+template <int C>
+__device__ __forceinline__ void wait_chunk(int wave) {
+  // the per-wave DMA count differs only when a chunk's instruction count is not a
+  // multiple of 4; branch on the (wave-uniform) wave index with constant counts
+  switch (wave) {
+    case 0: wait_chunk_w<C, 0>(); break;
+    case 1: wait_chunk_w<C, 1>(); break;
+    case 2: wait_chunk_w<C, 2>(); break;
+    default: wait_chunk_w<C, 3>(); break;
   }
 }
 
+typedef const __attribute__((address_space(4))) float* const_fptr;
+
+// acc[ob][r] = bias[acc_row(ob, r, h)] (or keep acc where !take), from a
+// wave-uniform bias vector read with scalar loads.
 template <int L>
-__device__ __forceinline__ void init_acc(State& s, const FieldArgs& a) {
-  const float* cb = a.code_bias + s.cb_row;
-  const float* base = L == kXyz1 ? a.packed + kBiasXyz1
-                    : L == kXyz2 ? cb + kCbXyz2
-                    : L == kOut ? cb + kCbFeat
-                    : L == kDir1 ? a.packed + kBiasDir1
-                    : L == kDir2 ? a.packed + kBiasDir2
-                                 : cb + kCbRgb;
+__device__ __forceinline__ void bias_from_row(State& s, const float* ub, bool take) {
+  const_fptr cp = (const_fptr)ub;
   if constexpr (L == kRgb) {
-    s.acc[0] = floatx16{0};
-    if (s.h == 0) {
-      s.acc[0][0] = base[0];
-      s.acc[0][1] = base[1];
-      s.acc[0][2] = base[2];
+    const float b0 = cp[0], b1 = cp[1], b2 = cp[2];
+    if (take && s.h == 0) {
+      s.acc[0][0] = b0;
+      s.acc[0][1] = b1;
+      s.acc[0][2] = b2;
     }
   } else {
 #pragma unroll
     for (int ob = 0; ob < 8; ++ob) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float4 b = *reinterpret_cast<const float4*>(base + 32 * ob + 8 * q + 4 * s.h);
-        s.acc[ob][4 * q + 0] = b.x;
-        s.acc[ob][4 * q + 1] = b.y;
-        s.acc[ob][4 * q + 2] = b.z;
-        s.acc[ob][4 * q + 3] = b.w;
+      for (int r = 0; r < 16; ++r) {
+        const float v0 = cp[acc_row(ob, r, 0)], v1 = cp[acc_row(ob, r, 1)];
+        const float v = s.h ? v1 : v0;
+        s.acc[ob][r] = take ? v : s.acc[ob][r];
       }
     }
     if constexpr (L == kOut) {
-      s.acc[8] = floatx16{0};
-      if (s.h == 0) s.acc[8][0] = cb[kCbSigma];
+      const float sg = cp[kCbSigma - kCbFeat];
+      if (take && s.h == 0) s.acc[8][0] = sg;
+    }
+  }
+}
+
+// Bias-initialised accumulators (acc = b, then acc += W x).  Every bias read is
+// a scalar load (s_load through the constant cache: lgkmcnt, so the DMA ring's
+// vmcnt accounting is untouched).  Per-code biases loop over the distinct code
+// rows of the wave (one pass when all 32 samples share an object).
+template <int L>
+__device__ __forceinline__ void init_acc(State& s, const FieldArgs& a) {
+  constexpr int cb_off = L == kXyz2 ? kCbXyz2 : L == kOut ? kCbFeat : L == kRgb ? kCbRgb : 0;
+  constexpr bool from_code = (L == kXyz2 || L == kOut || L == kRgb);
+  constexpr int const_off = L == kXyz1 ? kBiasXyz1 : L == kDir1 ? kBiasDir1 : kBiasDir2;
+#pragma unroll
+  for (int ob = 0; ob < (L == kOut ? 9 : (L == kRgb ? 1 : 8)); ++ob) s.acc[ob] = floatx16{0};
+  if constexpr (!from_code) {
+    bias_from_row<L>(s, a.packed + const_off, true);
+  } else {
+    unsigned long long todo = ~0ull;
+    while (todo) {
+      const int first = __builtin_ctzll(todo);
+      const int row = __builtin_amdgcn_readfirstlane(__shfl(s.crow, first));
+      const bool mine = (s.crow == row);
+      bias_from_row<L>(s, a.code_bias + (int64_t)row * kCbStride + cb_off, mine);
+      todo &= ~__ballot(mine);
     }
   }
 }
 
 template <int C, int T>
-__device__ __forceinline__ void mfma_step(State& s, const float4* lds) {
+__device__ __forceinline__ bf16x8 b_hi(const State& s) {
   constexpr Chunk ch = chunk_at(C);
-  constexpr int L = ch.layer;
-  constexpr int nb = kNb[L];
-  constexpr int ks = ch.s0 + T;  // k-step within the layer
-  const bf16x8 bh = (L == kDir1 && ks >= 16) ? s.dh[ks - 16] : s.bh[ks < 16 ? ks : 0];
-  const bf16x8 bl = (L == kDir1 && ks >= 16) ? s.dl[ks - 16] : s.bl[ks < 16 ? ks : 0];
-  const float4* ap = lds + (T * 64 + s.lane) * nb * 2;
+  constexpr int ks = ch.s0 + T;
+  return (ch.layer == kDir1 && ks >= 16) ? s.dh[ks >= 16 ? ks - 16 : 0] : s.bh[ks < 16 ? ks : 0];
+}
+template <int C, int T>
+__device__ __forceinline__ bf16x8 b_lo(const State& s) {
+  constexpr Chunk ch = chunk_at(C);
+  constexpr int ks = ch.s0 + T;
+  return (ch.layer == kDir1 && ks >= 16) ? s.dl[ks >= 16 ? ks - 16 : 0] : s.bl[ks < 16 ? ks : 0];
+}
+
+// A chunk's MFMAs in units of (k-step, group of <= 3 output blocks): the A
+// fragments (hi + lo, 8 VGPRs per block) of unit u+1 are read from LDS while
+// unit u's 3 x |group| MFMAs run -- two 24-VGPR buffers in flight.
+constexpr int kGroup = 3;
+template <int C>
+__host__ __device__ constexpr int groups() { return (kNb[chunk_at(C).layer] + kGroup - 1) / kGroup; }
+template <int C>
+__host__ __device__ constexpr int units() { return chunk_at(C).steps * groups<C>(); }
+
+template <int C, int U>
+__device__ __forceinline__ void load_unit(const State& s, const float* lds, bf16x8* ah, bf16x8* al) {
+  if constexpr (U < units<C>()) {
+    constexpr int nb = kNb[chunk_at(C).layer];
+    constexpr int T = U / groups<C>(), g = U % groups<C>();
+    const float4* ap = reinterpret_cast<const float4*>(lds) + (C % kSlots) * kSlotQuads + (T * 64 + s.lane) * nb * 2;
 #pragma unroll
-  for (int ob = 0; ob < nb; ++ob) {
-    const float4 qh = ap[2 * ob], ql = ap[2 * ob + 1];
-    const bf16x8 ah = __builtin_bit_cast(bf16x8, qh);
-    const bf16x8 al = __builtin_bit_cast(bf16x8, ql);
-    s.acc[ob] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, s.acc[ob], 0, 0, 0);
-    s.acc[ob] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, s.acc[ob], 0, 0, 0);
-    s.acc[ob] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, s.acc[ob], 0, 0, 0);
+    for (int i = 0; i < kGroup; ++i) {
+      constexpr int dummy = 0;
+      (void)dummy;
+      if (g * kGroup + i < nb) {
+        ah[i] = __builtin_bit_cast(bf16x8, ap[2 * (g * kGroup + i)]);
+        al[i] = __builtin_bit_cast(bf16x8, ap[2 * (g * kGroup + i) + 1]);
+      }
+    }
   }
 }
 
-template <int C, int T, int T1>
-__device__ __forceinline__ void mfma_steps(State& s, const float4* lds) {
-  if constexpr (T < T1) {
-    mfma_step<C, T>(s, lds);
-    mfma_steps<C, T + 1, T1>(s, lds);
+template <int C, int U>
+__device__ __forceinline__ void mfma_unit(State& s, const bf16x8* ah, const bf16x8* al) {
+  constexpr int nb = kNb[chunk_at(C).layer];
+  constexpr int T = U / groups<C>(), g = U % groups<C>();
+  const bf16x8 bh = b_hi<C, T>(s), bl = b_lo<C, T>(s);
+#pragma unroll
+  for (int i = 0; i < kGroup; ++i) {
+    if (g * kGroup + i < nb) {
+      floatx16& acc = s.acc[g * kGroup + i];
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh, acc, 0, 0, 0);
+    }
   }
+}
+
+template <int C, int U>
+__device__ __forceinline__ void chunk_units(State& s, const float* lds, bf16x8* ah_cur, bf16x8* al_cur,
+                                            bf16x8* ah_nxt, bf16x8* al_nxt) {
+  if constexpr (U < units<C>()) {
+    load_unit<C, U + 1>(s, lds, ah_nxt, al_nxt);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_unit<C, U>(s, ah_cur, al_cur);
+    __builtin_amdgcn_sched_barrier(0);
+    chunk_units<C, U + 1>(s, lds, ah_nxt, al_nxt, ah_cur, al_cur);
+  }
+}
+
+template <int C>
+__device__ __forceinline__ void chunk_mfma(State& s, const float* lds) {
+  bf16x8 ah0[kGroup], al0[kGroup], ah1[kGroup], al1[kGroup];
+  load_unit<C, 0>(s, lds, ah0, al0);
+  chunk_units<C, 0>(s, lds, ah0, al0, ah1, al1);
 }
 
 template <int L>
 __device__ __forceinline__ void finish_layer(State& s) {
-  if constexpr (L == kRgb) {
-    return;
-  } else {
+  if constexpr (L != kRgb) {
     if constexpr (L == kOut) s.sigma = s.acc[8][0];
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
@@ -256,20 +345,15 @@ __device__ __forceinline__ void finish_layer(State& s) {
 }
 
 template <int MODE, int C>
-__device__ __forceinline__ void run_chunks(State& s, const FieldArgs& a, float4* lds0, float4* lds1) {
+__device__ __forceinline__ void run_chunks(State& s, const FieldArgs& a, float* lds) {
   if constexpr (C < kNumChunks) {
     constexpr Chunk ch = chunk_at(C);
-    float4* cur = (C & 1) ? lds1 : lds0;
-    float4* nxt = (C & 1) ? lds0 : lds1;
+    // chunk C landed for every wave, and every wave is done with chunk C-1
+    wait_chunk<C>(s.wave);
+    __builtin_amdgcn_sched_barrier(0);
+    issue_chunk<C + kAhead>(s, a.packed, lds);   // into the slot chunk C-1 used
     if constexpr (ch.s0 == 0) init_acc<ch.layer>(s, a);
-    if constexpr (C + 1 < kNumChunks) load_chunk<C + 1, 0>(s, a.packed);
-    constexpr int half = (ch.steps + 1) / 2;
-    mfma_steps<C, 0, half>(s, cur);
-    if constexpr (C + 1 < kNumChunks) {
-      store_chunk<C + 1, 0>(s, nxt);
-      load_chunk<C + 1, 1>(s, a.packed);
-    }
-    mfma_steps<C, half, ch.steps>(s, cur);
+    chunk_mfma<C>(s, lds);
     constexpr bool last_of_layer = (C + 1 == kNumChunks) || chunk_at(C + 1).layer != ch.layer;
     if constexpr (last_of_layer) finish_layer<ch.layer>(s);
     // view-direction encoding for layer_dir1, made while the fc_out accumulators are dead
@@ -281,25 +365,22 @@ __device__ __forceinline__ void run_chunks(State& s, const FieldArgs& a, float4*
       split8(v, s.dh[0], s.dl[0]);
       split8(v + 8, s.dh[1], s.dl[1]);
     }
-    if constexpr (C + 1 < kNumChunks) {
-      store_chunk<C + 1, 1>(s, nxt);
-      __syncthreads();
-    }
-    run_chunks<MODE, C + 1>(s, a, lds0, lds1);
+    run_chunks<MODE, C + 1>(s, a, lds);
   }
 }
 
 template <int MODE>
 __global__ __launch_bounds__(kThreads, 1) void field_x3_kernel(FieldArgs a) {
-  __shared__ float4 lds[2][kMaxChunkQuads];
+  __shared__ __attribute__((aligned(16))) float lds[kLdsFloats];  // the ONE LDS object
   State s;
   s.lane = threadIdx.x & 63;
   s.h = s.lane >> 5;
-  const int wave = threadIdx.x >> 6;
-  const int64_t row = (int64_t)blockIdx.x * kTile + wave * 32 + (s.lane & 31);
+  s.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t row = (int64_t)blockIdx.x * kTile + s.wave * 32 + (s.lane & 31);
   const bool valid = row < a.m;
   const int64_t rc = valid ? row : a.m - 1;
 
+  // ---- per-sample inputs (ordinary loads, all before the DMA stream starts)
   const SampleIn in = decode_sample<MODE>(a, rc);
   float enc[32];
   if constexpr (MODE == kFromEncoded) {
@@ -318,14 +399,15 @@ __global__ __launch_bounds__(kThreads, 1) void field_x3_kernel(FieldArgs a) {
   }
 #pragma unroll
   for (int k = 0; k < 4; ++k) split8(enc + 8 * k, s.bh[k], s.bl[k]);
-  s.cb_row = code_row(a, in.code_of) * kCbStride;
+  s.crow = static_cast<int>(code_row(a, in.code_of));
 
-  load_chunk<0, 0>(s, a.packed);
-  store_chunk<0, 0>(s, lds[0]);
-  load_chunk<0, 1>(s, a.packed);
-  store_chunk<0, 1>(s, lds[0]);
-  __syncthreads();
-  run_chunks<MODE, 0>(s, a, lds[0], lds[1]);
+  // ---- weight stream: every input load has landed (an s_waitcnt the compiler
+  // sees, so it tracks nothing stale into the DMA stream); prime the ring
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  issue_chunk<0>(s, a.packed, lds);
+  issue_chunk<1>(s, a.packed, lds);
+  issue_chunk<2>(s, a.packed, lds);
+  run_chunks<MODE, 0>(s, a, lds);
 
   if (valid && s.h == 0) {
     float4 o;
