@@ -11,8 +11,23 @@
 // 8s..8s+7 become k-step s (16 features) of the next layer's B operand after a
 // hi/lo split (element j of lane half h = feature 16s + 8(j>>2) + 4h + (j&3) of
 // the block, cdna_hip_programming.md section 3), so activations never leave
-// registers.  Weight fragments (32 B per lane per output block per k-step: hi
-// then lo) stream through a 2 x 72 KiB LDS ring in 22 chunks of <= 4 k-steps.
+// registers.
+//
+// Weight stream.  Every chunk has ONE format -- 2 k-steps x 9 block slots x
+// {hi, lo} x 64 lanes quads = 36 KiB, fragment-major so a wave's ds_read_b128 of
+// one fragment is 1 KiB contiguous (bank-conflict free) -- and the chunks lie in stream order in the
+// packed buffer, so chunk c is just `packed + c * 36 KiB`.  A 4-slot LDS ring is
+// filled by LDS-DMA (global_load_lds, 1 KiB per wave-instruction, 9 per wave per
+// chunk); chunk c+3 is issued when chunk c starts, and a constant
+// `s_waitcnt vmcnt(18)` + s_barrier retires chunk c (two dummy chunks at the end
+// keep the count constant).  No ordinary global load is live in the stream
+// (biases are scalar loads), so the counted waits are exact.
+//
+// Code size.  The four 256-input layers (layer_xyz2, fc_out, layer_dir1's feature
+// part, layer_dir2) run through ONE runtime loop whose body is a single unrolled
+// 16-k-step layer: fully unrolling all six layers (~140 KiB of code) made the
+// kernel instruction-fetch bound (ablation: removing every MFMA saved only 4 %).
+// fc_out's 9th output block (sigma) is a uniform branch.
 #include "mlp_common.h"
 
 namespace cn {
@@ -21,14 +36,16 @@ namespace x3 {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-constexpr int kSteps[kNumLayers] = {4, 16, 16, 18, 16, 16};   // 16-wide k-steps
-constexpr int kNb[kNumLayers] = {8, 8, 9, 8, 8, 1};
-
-// Layout in 16-byte quads: layer l, k-step s, lane L, block ob, {hi, lo}.
-__host__ __device__ constexpr int layer_quads(int l) { return kSteps[l] * 64 * kNb[l] * 2; }
-__host__ __device__ constexpr int layer_off(int l) { return l == 0 ? 0 : layer_off(l - 1) + layer_quads(l - 1); }
-constexpr int kQuads = layer_off(kNumLayers);
-constexpr int kBiasXyz1 = kQuads * 4;   // floats
+constexpr int kSlotBlocks = 9;
+constexpr int kQuadsPerStep = 64 * kSlotBlocks * 2;      // one k-step of a chunk
+constexpr int kChunkQuads = 2 * kQuadsPerStep;            // 2304 quads = 36 KiB
+constexpr int kDmaPerWave = kChunkQuads / 64 / 4;        // 9
+// stream: L0 2 | L1 8 | L2 8 | L3 8 + 1 (view dir) | L4 8 | L5 1 | 2 dummies
+constexpr int kChunkL1 = 2, kChunkL2 = 10, kChunkL3 = 18, kChunkDir = 26, kChunkL4 = 27, kChunkRgb = 35;
+constexpr int kRealChunks = 36;
+constexpr int kStreamChunks = kRealChunks + 2;
+constexpr int kQuads = kStreamChunks * kChunkQuads;
+constexpr int kBiasXyz1 = kQuads * 4;  // floats
 constexpr int kBiasDir1 = kBiasXyz1 + 256;
 constexpr int kBiasDir2 = kBiasDir1 + 256;
 constexpr int kPackedFloats = kBiasDir2 + 256;
@@ -50,6 +67,21 @@ __device__ __forceinline__ unsigned short bf16_bits(float x) {
   return __builtin_bit_cast(unsigned short, b);
 }
 
+// (chunk, step-in-chunk T, slot j) -> (layer, k-step, output block); -1 layer = zeros
+__device__ void chunk_map(int c, int T, int j, int& l, int& ks, int& ob) {
+  l = -1;
+  ks = 0;
+  ob = j;
+  if (c < kChunkL1) { l = kXyz1; ks = 2 * c + T; }
+  else if (c < kChunkL2) { l = kXyz2; ks = 2 * (c - kChunkL1) + T; }
+  else if (c < kChunkL3) { l = kOut; ks = 2 * (c - kChunkL2) + T; }
+  else if (c < kChunkDir) { l = kDir1; ks = 2 * (c - kChunkL3) + T; }
+  else if (c == kChunkDir) { l = kDir1; ks = 16 + T; }
+  else if (c < kChunkRgb) { l = kDir2; ks = 2 * (c - kChunkL4) + T; }
+  else if (c == kChunkRgb) { l = kRgb; ks = 9 * T + j; ob = 0; if (ks >= 16) l = -1; }
+  if (l >= 0 && l != kOut && ob >= 8) l = -1;
+}
+
 __global__ void pack_x3_kernel(Params P, float* __restrict__ packed) {
   unsigned short* q16 = reinterpret_cast<unsigned short*>(packed);
   const int n_elems = kQuads * 8;  // bf16 elements
@@ -61,32 +93,32 @@ __global__ void pack_x3_kernel(Params P, float* __restrict__ packed) {
           j < 256 ? P.p[kBXyz1][j] : (j < 512 ? P.p[kBDir1][j - 256] : P.p[kBDir2][j - 512]);
       continue;
     }
-    const int quad = idx >> 3, j = idx & 7;
-    constexpr int offs[kNumLayers + 1] = {layer_off(0), layer_off(1), layer_off(2), layer_off(3),
-                                          layer_off(4), layer_off(5), layer_off(6)};
-    int l = 0;
-    while (l + 1 < kNumLayers && quad >= offs[l + 1]) ++l;
-    int rem = quad - offs[l];
-    const int part = rem & 1;  // 0 hi, 1 lo
-    rem >>= 1;
-    const int nb = kNb[l];
-    const int ob = rem % nb;
-    rem /= nb;
-    const int lane = rem % 64, s = rem / 64;
-    const int i = lane & 31, h = lane >> 5;
-    const int col = in_col(l, s, h, j);
-    int row = -1, in_dim = 0;
-    const float* W = nullptr;
-    switch (l) {
-      case kXyz1: W = P.p[kWXyz1]; in_dim = kDimXyz; row = 32 * ob + i; break;
-      case kXyz2: W = P.p[kWXyz2]; in_dim = kHidden + kCode; row = 32 * ob + i; break;
-      case kOut: W = P.p[kWOut]; in_dim = kHidden + kCode;
-        row = ob < 8 ? 1 + 32 * ob + i : ((ob == 8 && i == 0) ? 0 : -1); break;
-      case kDir1: W = P.p[kWDir1]; in_dim = kCode + kDimDir; row = 32 * ob + i; break;
-      case kDir2: W = P.p[kWDir2]; in_dim = kHidden; row = 32 * ob + i; break;
-      default: W = P.p[kWRgb]; in_dim = kHidden + kCode; row = (ob == 0 && i < 3) ? i : -1; break;
+    const int quad = idx >> 3, e = idx & 7;
+    const int c = quad / kChunkQuads;
+    int r = quad % kChunkQuads;
+    const int T = r / kQuadsPerStep;
+    r %= kQuadsPerStep;
+    const int frag = r / 64, lane = r % 64;  // fragment-major: 1 KiB per (slot, hi|lo)
+    const int slot = frag >> 1, part = frag & 1;
+    int l, ks, ob;
+    chunk_map(c, T, slot, l, ks, ob);
+    float w = 0.0f;
+    if (l >= 0) {
+      const int i = lane & 31, h = lane >> 5;
+      const int col = in_col(l, ks, h, e);
+      int row = -1, in_dim = 0;
+      const float* W = nullptr;
+      switch (l) {
+        case kXyz1: W = P.p[kWXyz1]; in_dim = kDimXyz; row = 32 * ob + i; break;
+        case kXyz2: W = P.p[kWXyz2]; in_dim = kHidden + kCode; row = 32 * ob + i; break;
+        case kOut: W = P.p[kWOut]; in_dim = kHidden + kCode;
+          row = ob < 8 ? 1 + 32 * ob + i : (i == 0 ? 0 : -1); break;
+        case kDir1: W = P.p[kWDir1]; in_dim = kCode + kDimDir; row = 32 * ob + i; break;
+        case kDir2: W = P.p[kWDir2]; in_dim = kHidden; row = 32 * ob + i; break;
+        default: W = P.p[kWRgb]; in_dim = kHidden + kCode; row = i < 3 ? i : -1; break;
+      }
+      if (row >= 0 && col >= 0) w = W[row * in_dim + col];
     }
-    const float w = (row >= 0 && col >= 0) ? W[row * in_dim + col] : 0.0f;
     const __bf16 hi = static_cast<__bf16>(w);
     const float lo = w - static_cast<float>(hi);
     q16[idx] = part == 0 ? bf16_bits(w) : bf16_bits(lo);
@@ -94,45 +126,12 @@ __global__ void pack_x3_kernel(Params P, float* __restrict__ packed) {
 }
 
 // ---------------------------------------------------------------- kernel
-//
-// Weight stream: 44 chunks of <= 2 k-steps (<= 36 KiB) through a 4-slot LDS
-// ring filled by LDS-DMA (global_load_lds, 1 KiB per wave-instruction, no
-// VGPR staging).  Chunk c+3 is issued when chunk c starts, so three chunks
-// (~4.6 K MFMA cycles) are in flight; one raw s_barrier per chunk, preceded by
-// a counted `s_waitcnt vmcnt(N)` that retires only this wave's DMA for chunk c.
-// No ordinary global load is live inside the stream (hipcc would wait
-// vmcnt(0) for it, draining the ring): per-layer biases are read with scalar
-// loads (see init_acc).
 
 constexpr int kWaves = 4;
 constexpr int kThreads = 64 * kWaves;
 constexpr int kTile = 32 * kWaves;
-constexpr int kChunkSteps = 2;
-constexpr int kSlotQuads = kChunkSteps * 64 * 9 * 2;   // 36 KiB: an fc_out chunk
 constexpr int kSlots = 4;
-constexpr int kAhead = kSlots - 1;                      // chunks in flight
-constexpr int kLdsFloats = kSlots * kSlotQuads * 4;    // 144 KiB ring
-
-struct Chunk {
-  int layer, s0, steps;
-};
-// chunk c -> (layer, first k-step, k-steps); layer_dir1 ends with its 2 view-direction k-steps
-constexpr int kChunksPerLayer[kNumLayers] = {2, 8, 8, 9, 8, 8};
-constexpr int kNumChunks = 2 + 8 + 8 + 9 + 8 + 8;
-__host__ __device__ constexpr Chunk chunk_at(int c) {
-  int l = 0;
-  while (c >= kChunksPerLayer[l]) c -= kChunksPerLayer[l++];
-  return Chunk{l, 2 * c, 2};
-}
-__host__ __device__ constexpr int chunk_quads(int c) { return chunk_at(c).steps * 64 * kNb[chunk_at(c).layer] * 2; }
-__host__ __device__ constexpr int chunk_src(int c) {
-  return layer_off(chunk_at(c).layer) + chunk_at(c).s0 * 64 * kNb[chunk_at(c).layer] * 2;
-}
-// wave-instructions (1 KiB = 64 quads each) per chunk and per wave
-__host__ __device__ constexpr int chunk_dma(int c) { return chunk_quads(c) / 64; }
-__host__ __device__ constexpr int wave_dma(int c, int w) {
-  return c >= kNumChunks ? 0 : (chunk_dma(c) - w + kWaves - 1) / kWaves;
-}
+constexpr int kLdsQuads = kSlots * kChunkQuads;  // 144 KiB ring
 
 struct State {
   bf16x8 bh[16], bl[16];  // B operands (hi / lo) of the current layer's 16 k-steps
@@ -155,223 +154,174 @@ __device__ __forceinline__ void split8(const float* v, bf16x8& hi, bf16x8& lo) {
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
-
-// Issue this wave's share of chunk C's DMA into ring slot C % kSlots.
-template <int C>
-__device__ __forceinline__ void issue_chunk(const State& s, const float* __restrict__ packed, float* lds) {
-  if constexpr (C < kNumChunks) {
-    constexpr int n = chunk_dma(C);
-    const float4* src = reinterpret_cast<const float4*>(packed) + chunk_src(C);
-    float4* slot = reinterpret_cast<float4*>(lds) + (C % kSlots) * kSlotQuads;
-#pragma unroll
-    for (int i = 0; i < (n + kWaves - 1) / kWaves; ++i) {
-      const int ins = i * kWaves + s.wave;  // wave-uniform
-      if (n % kWaves == 0 || ins < n) {
-        __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src + ins * 64 + s.lane), (lds_ptr_t)(slot + ins * 64), 16, 0, 0);
-      }
-    }
-  }
-}
-
-// Wait until this wave's DMA for chunk C has landed (later chunks stay in flight).
-// One asm statement: the counted wait, this wave's LDS reads retired, the barrier.
-// Nothing (no LDS read of chunk C) can be scheduled across it.
-template <int C, int W>
-__device__ __forceinline__ void wait_chunk_w() {
-  constexpr int pending = wave_dma(C + 1, W) + wave_dma(C + 2, W);
-  asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(pending) : "memory");
-}
-template <int C>
-__device__ __forceinline__ void wait_chunk(int wave) {
-  // the per-wave DMA count differs only when a chunk's instruction count is not a
-  // multiple of 4; branch on the (wave-uniform) wave index with constant counts
-  switch (wave) {
-    case 0: wait_chunk_w<C, 0>(); break;
-    case 1: wait_chunk_w<C, 1>(); break;
-    case 2: wait_chunk_w<C, 2>(); break;
-    default: wait_chunk_w<C, 3>(); break;
-  }
-}
-
 typedef const __attribute__((address_space(4))) float* const_fptr;
 
-// acc[ob][r] = bias[acc_row(ob, r, h)] (or keep acc where !take), from a
-// wave-uniform bias vector read with scalar loads.
-template <int L>
-__device__ __forceinline__ void bias_from_row(State& s, const float* ub, bool take) {
+// Issue this wave's 9 DMA instructions of chunk c into ring slot c % 4.
+__device__ __forceinline__ void issue_chunk(const State& s, const float* __restrict__ packed, float4* lds, int c) {
+  const float4* src = reinterpret_cast<const float4*>(packed) + c * kChunkQuads + s.wave * 64 + s.lane;
+  float4* slot = lds + (c & (kSlots - 1)) * kChunkQuads + s.wave * 64;
+#pragma unroll
+  for (int i = 0; i < kDmaPerWave; ++i) {
+#ifndef CN_ABLATE_NO_DMA
+    __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src + i * 256), (lds_ptr_t)(slot + i * 256), 16, 0, 0);
+#endif
+  }
+}
+
+// Chunk c landed for every wave and every wave is done with chunk c-1 (its slot
+// is refilled next): one asm statement, so no LDS read can be scheduled across it.
+__device__ __forceinline__ void chunk_barrier() {
+#ifdef CN_ABLATE_NO_DMA
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#else
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(2 * kDmaPerWave) : "memory");
+#endif
+}
+
+// acc[ob][r] = bias[acc_row(ob, r, h)] where `take`, from a wave-uniform bias
+// vector read with scalar loads (lgkmcnt: the ring's vmcnt count is untouched).
+__device__ __forceinline__ void bias_blocks(State& s, const float* ub, bool take) {
   const_fptr cp = (const_fptr)ub;
-  if constexpr (L == kRgb) {
-    const float b0 = cp[0], b1 = cp[1], b2 = cp[2];
-    if (take && s.h == 0) {
-      s.acc[0][0] = b0;
-      s.acc[0][1] = b1;
-      s.acc[0][2] = b2;
+#pragma unroll
+  for (int ob = 0; ob < 8; ++ob) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float v0 = cp[acc_row(ob, r, 0)], v1 = cp[acc_row(ob, r, 1)];
+      const float v = s.h ? v1 : v0;
+      s.acc[ob][r] = take ? v : s.acc[ob][r];
     }
-  } else {
+  }
+}
+
+// Bias-initialised accumulators for layer `layer` (runtime, wave-uniform).
+// Per-code biases loop over the distinct code rows of the wave (one pass when
+// all 32 samples share an object).
+__device__ __forceinline__ void init_acc(State& s, const FieldArgs& a, int layer) {
 #pragma unroll
-    for (int ob = 0; ob < 8; ++ob) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float v0 = cp[acc_row(ob, r, 0)], v1 = cp[acc_row(ob, r, 1)];
-        const float v = s.h ? v1 : v0;
-        s.acc[ob][r] = take ? v : s.acc[ob][r];
+  for (int ob = 0; ob < 9; ++ob) s.acc[ob] = floatx16{0};
+#ifdef CN_ABLATE_NO_BIAS
+  return;
+#endif
+  const bool per_code = (layer == kXyz2 || layer == kOut || layer == kRgb);
+  const int off = !per_code ? (layer == kXyz1 ? kBiasXyz1 : (layer == kDir1 ? kBiasDir1 : kBiasDir2))
+                            : (layer == kXyz2 ? kCbXyz2 : (layer == kOut ? kCbFeat : kCbRgb));
+  unsigned long long todo = ~0ull;
+  while (todo) {
+    const float* base;
+    bool mine = true;
+    if (!per_code) {
+      base = a.packed + off;
+    } else {
+      const int row = __builtin_amdgcn_readfirstlane(__shfl(s.crow, __builtin_ctzll(todo)));
+      mine = (s.crow == row);
+      base = a.code_bias + (int64_t)row * kCbStride + off;
+    }
+    if (layer == kRgb) {
+      const_fptr cp = (const_fptr)base;
+      const float b0 = cp[0], b1 = cp[1], b2 = cp[2];
+      if (mine && s.h == 0) {
+        s.acc[0][0] = b0;
+        s.acc[0][1] = b1;
+        s.acc[0][2] = b2;
+      }
+    } else {
+      bias_blocks(s, base, mine);
+      if (layer == kOut) {
+        const float sg = ((const_fptr)(base + (kCbSigma - kCbFeat)))[0];
+        if (mine && s.h == 0) s.acc[8][0] = sg;
       }
     }
-    if constexpr (L == kOut) {
-      const float sg = cp[kCbSigma - kCbFeat];
-      if (take && s.h == 0) s.acc[8][0] = sg;
-    }
+    todo &= ~__ballot(mine);
   }
 }
 
-// Bias-initialised accumulators (acc = b, then acc += W x).  Every bias read is
-// a scalar load (s_load through the constant cache: lgkmcnt, so the DMA ring's
-// vmcnt accounting is untouched).  Per-code biases loop over the distinct code
-// rows of the wave (one pass when all 32 samples share an object).
-template <int L>
-__device__ __forceinline__ void init_acc(State& s, const FieldArgs& a) {
-  constexpr int cb_off = L == kXyz2 ? kCbXyz2 : L == kOut ? kCbFeat : L == kRgb ? kCbRgb : 0;
-  constexpr bool from_code = (L == kXyz2 || L == kOut || L == kRgb);
-  constexpr int const_off = L == kXyz1 ? kBiasXyz1 : L == kDir1 ? kBiasDir1 : kBiasDir2;
+// A fragments of slot blocks [J0, J0+3) of k-step T of the chunk in `slot`.
+template <int T, int J0>
+__device__ __forceinline__ void load_a(const State& s, const float4* slot, bf16x8* ah, bf16x8* al) {
+  const float4* ap = slot + T * kQuadsPerStep + s.lane;
 #pragma unroll
-  for (int ob = 0; ob < (L == kOut ? 9 : (L == kRgb ? 1 : 8)); ++ob) s.acc[ob] = floatx16{0};
-  if constexpr (!from_code) {
-    bias_from_row<L>(s, a.packed + const_off, true);
-  } else {
-    unsigned long long todo = ~0ull;
-    while (todo) {
-      const int first = __builtin_ctzll(todo);
-      const int row = __builtin_amdgcn_readfirstlane(__shfl(s.crow, first));
-      const bool mine = (s.crow == row);
-      bias_from_row<L>(s, a.code_bias + (int64_t)row * kCbStride + cb_off, mine);
-      todo &= ~__ballot(mine);
-    }
+  for (int i = 0; i < 3; ++i) {
+    ah[i] = __builtin_bit_cast(bf16x8, ap[(2 * (J0 + i)) * 64]);
+    al[i] = __builtin_bit_cast(bf16x8, ap[(2 * (J0 + i) + 1) * 64]);
   }
 }
 
-template <int C, int T>
-__device__ __forceinline__ bf16x8 b_hi(const State& s) {
-  constexpr Chunk ch = chunk_at(C);
-  constexpr int ks = ch.s0 + T;
-  return (ch.layer == kDir1 && ks >= 16) ? s.dh[ks >= 16 ? ks - 16 : 0] : s.bh[ks < 16 ? ks : 0];
-}
-template <int C, int T>
-__device__ __forceinline__ bf16x8 b_lo(const State& s) {
-  constexpr Chunk ch = chunk_at(C);
-  constexpr int ks = ch.s0 + T;
-  return (ch.layer == kDir1 && ks >= 16) ? s.dl[ks >= 16 ? ks - 16 : 0] : s.bl[ks < 16 ? ks : 0];
+__device__ __forceinline__ void mfma3(floatx16& acc, bf16x8 ah, bf16x8 al, bf16x8 bh, bf16x8 bl) {
+#ifdef CN_ABLATE_NO_MFMA
+  asm volatile("" ::"v"(ah), "v"(al), "v"(bh), "v"(bl));
+#else
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
+#endif
 }
 
-// A chunk's MFMAs in units of (k-step, group of <= 3 output blocks): the A
-// fragments (hi + lo, 8 VGPRs per block) of unit u+1 are read from LDS while
-// unit u's 3 x |group| MFMAs run -- two 24-VGPR buffers in flight.
-constexpr int kGroup = 3;
-template <int C>
-__host__ __device__ constexpr int groups() { return (kNb[chunk_at(C).layer] + kGroup - 1) / kGroup; }
-template <int C>
-__host__ __device__ constexpr int units() { return chunk_at(C).steps * groups<C>(); }
-
-template <int C, int U>
-__device__ __forceinline__ void load_unit(const State& s, const float* lds, bf16x8* ah, bf16x8* al) {
-  if constexpr (U < units<C>()) {
-    constexpr int nb = kNb[chunk_at(C).layer];
-    constexpr int T = U / groups<C>(), g = U % groups<C>();
-    const float4* ap = reinterpret_cast<const float4*>(lds) + (C % kSlots) * kSlotQuads + (T * 64 + s.lane) * nb * 2;
+// One 2-k-step chunk against 8 (+ block 8 when with9) output blocks.  The A
+// fragments of the next group of 3 blocks are read while the current group's
+// MFMAs run (two 24-VGPR buffers).
+__device__ __forceinline__ void chunk_mfma(State& s, const float4* slot, bf16x8 bh0, bf16x8 bl0, bf16x8 bh1,
+                                           bf16x8 bl1, bool with9) {
+  bf16x8 ah[3], al[3], nh[3], nl[3];
+  load_a<0, 0>(s, slot, ah, al);
+  load_a<0, 3>(s, slot, nh, nl);
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int i = 0; i < kGroup; ++i) {
-      constexpr int dummy = 0;
-      (void)dummy;
-      if (g * kGroup + i < nb) {
-        ah[i] = __builtin_bit_cast(bf16x8, ap[2 * (g * kGroup + i)]);
-        al[i] = __builtin_bit_cast(bf16x8, ap[2 * (g * kGroup + i) + 1]);
-      }
+  for (int i = 0; i < 3; ++i) mfma3(s.acc[i], ah[i], al[i], bh0, bl0);
+  __builtin_amdgcn_sched_barrier(0);
+  load_a<0, 6>(s, slot, ah, al);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) mfma3(s.acc[3 + i], nh[i], nl[i], bh0, bl0);
+  __builtin_amdgcn_sched_barrier(0);
+  load_a<1, 0>(s, slot, nh, nl);
+  __builtin_amdgcn_sched_barrier(0);
+  mfma3(s.acc[6], ah[0], al[0], bh0, bl0);
+  mfma3(s.acc[7], ah[1], al[1], bh0, bl0);
+  if (with9) mfma3(s.acc[8], ah[2], al[2], bh0, bl0);
+  __builtin_amdgcn_sched_barrier(0);
+  load_a<1, 3>(s, slot, ah, al);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) mfma3(s.acc[i], nh[i], nl[i], bh1, bl1);
+  __builtin_amdgcn_sched_barrier(0);
+  load_a<1, 6>(s, slot, nh, nl);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) mfma3(s.acc[3 + i], ah[i], al[i], bh1, bl1);
+  __builtin_amdgcn_sched_barrier(0);
+  mfma3(s.acc[6], nh[0], nl[0], bh1, bl1);
+  mfma3(s.acc[7], nh[1], nl[1], bh1, bl1);
+  if (with9) mfma3(s.acc[8], nh[2], nl[2], bh1, bl1);
+}
+
+// Barrier, refill, MFMAs of chunk c with B operands of k-steps (k0, k0+1).
+__device__ __forceinline__ void run_chunk(State& s, const FieldArgs& a, float4* lds, int& c, bf16x8 bh0,
+                                          bf16x8 bl0, bf16x8 bh1, bf16x8 bl1, bool with9) {
+  chunk_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  if (c + 3 < kStreamChunks) issue_chunk(s, a.packed, lds, c + 3);
+  chunk_mfma(s, lds + (c & (kSlots - 1)) * kChunkQuads, bh0, bl0, bh1, bl1, with9);
+  ++c;
+}
+
+// acc -> next layer's B operands: relu (not for fc_out's feat), hi/lo split.
+__device__ __forceinline__ void finish_layer(State& s, bool relu) {
+  const float lo = relu ? 0.0f : -__builtin_inff();
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+#pragma unroll
+    for (int sp = 0; sp < 2; ++sp) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = fmaxf(s.acc[b][8 * sp + j], lo);
+      split8(v, s.bh[2 * b + sp], s.bl[2 * b + sp]);
     }
-  }
-}
-
-template <int C, int U>
-__device__ __forceinline__ void mfma_unit(State& s, const bf16x8* ah, const bf16x8* al) {
-  constexpr int nb = kNb[chunk_at(C).layer];
-  constexpr int T = U / groups<C>(), g = U % groups<C>();
-  const bf16x8 bh = b_hi<C, T>(s), bl = b_lo<C, T>(s);
-#pragma unroll
-  for (int i = 0; i < kGroup; ++i) {
-    if (g * kGroup + i < nb) {
-      floatx16& acc = s.acc[g * kGroup + i];
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh, acc, 0, 0, 0);
-    }
-  }
-}
-
-template <int C, int U>
-__device__ __forceinline__ void chunk_units(State& s, const float* lds, bf16x8* ah_cur, bf16x8* al_cur,
-                                            bf16x8* ah_nxt, bf16x8* al_nxt) {
-  if constexpr (U < units<C>()) {
-    load_unit<C, U + 1>(s, lds, ah_nxt, al_nxt);
-    __builtin_amdgcn_sched_barrier(0);
-    mfma_unit<C, U>(s, ah_cur, al_cur);
-    __builtin_amdgcn_sched_barrier(0);
-    chunk_units<C, U + 1>(s, lds, ah_nxt, al_nxt, ah_cur, al_cur);
-  }
-}
-
-template <int C>
-__device__ __forceinline__ void chunk_mfma(State& s, const float* lds) {
-  bf16x8 ah0[kGroup], al0[kGroup], ah1[kGroup], al1[kGroup];
-  load_unit<C, 0>(s, lds, ah0, al0);
-  chunk_units<C, 0>(s, lds, ah0, al0, ah1, al1);
-}
-
-template <int L>
-__device__ __forceinline__ void finish_layer(State& s) {
-  if constexpr (L != kRgb) {
-    if constexpr (L == kOut) s.sigma = s.acc[8][0];
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
-#pragma unroll
-      for (int sp = 0; sp < 2; ++sp) {
-        float v[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float x = s.acc[b][8 * sp + j];
-          v[j] = (L == kOut) ? x : fmaxf(x, 0.0f);  // feat = fc_out[1:] has no activation
-        }
-        split8(v, s.bh[2 * b + sp], s.bl[2 * b + sp]);
-      }
-    }
-  }
-}
-
-template <int MODE, int C>
-__device__ __forceinline__ void run_chunks(State& s, const FieldArgs& a, float* lds) {
-  if constexpr (C < kNumChunks) {
-    constexpr Chunk ch = chunk_at(C);
-    // chunk C landed for every wave, and every wave is done with chunk C-1
-    wait_chunk<C>(s.wave);
-    __builtin_amdgcn_sched_barrier(0);
-    issue_chunk<C + kAhead>(s, a.packed, lds);   // into the slot chunk C-1 used
-    if constexpr (ch.s0 == 0) init_acc<ch.layer>(s, a);
-    chunk_mfma<C>(s, lds);
-    constexpr bool last_of_layer = (C + 1 == kNumChunks) || chunk_at(C + 1).layer != ch.layer;
-    if constexpr (last_of_layer) finish_layer<ch.layer>(s);
-    // view-direction encoding for layer_dir1, made while the fc_out accumulators are dead
-    if constexpr (last_of_layer && ch.layer == kOut && MODE != kFromEncoded) {
-      float v[16];
-      encode_pairs<6, 4>(s.vd, a.fd, s.h, v);
-      v[14] = 0.0f;
-      v[15] = 0.0f;
-      split8(v, s.dh[0], s.dl[0]);
-      split8(v + 8, s.dh[1], s.dl[1]);
-    }
-    run_chunks<MODE, C + 1>(s, a, lds);
   }
 }
 
 template <int MODE>
 __global__ __launch_bounds__(kThreads, 1) void field_x3_kernel(FieldArgs a) {
-  __shared__ __attribute__((aligned(16))) float lds[kLdsFloats];  // the ONE LDS object
+  __shared__ __attribute__((aligned(16))) float4 lds[kLdsQuads];  // the ONE LDS object
   State s;
   s.lane = threadIdx.x & 63;
   s.h = s.lane >> 5;
@@ -401,13 +351,55 @@ __global__ __launch_bounds__(kThreads, 1) void field_x3_kernel(FieldArgs a) {
   for (int k = 0; k < 4; ++k) split8(enc + 8 * k, s.bh[k], s.bl[k]);
   s.crow = static_cast<int>(code_row(a, in.code_of));
 
-  // ---- weight stream: every input load has landed (an s_waitcnt the compiler
-  // sees, so it tracks nothing stale into the DMA stream); prime the ring
+  // every input load has landed (an s_waitcnt the compiler sees, so nothing stale
+  // is tracked into the DMA stream); prime the ring with chunks 0..2
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-  issue_chunk<0>(s, a.packed, lds);
-  issue_chunk<1>(s, a.packed, lds);
-  issue_chunk<2>(s, a.packed, lds);
-  run_chunks<MODE, 0>(s, a, lds);
+  issue_chunk(s, a.packed, lds, 0);
+  issue_chunk(s, a.packed, lds, 1);
+  issue_chunk(s, a.packed, lds, 2);
+  int c = 0;
+
+  // ---- layer_xyz1 (63 -> 256): 4 k-steps of encoding
+  init_acc(s, a, kXyz1);
+  run_chunk(s, a, lds, c, s.bh[0], s.bl[0], s.bh[1], s.bl[1], false);
+  run_chunk(s, a, lds, c, s.bh[2], s.bl[2], s.bh[3], s.bl[3], false);
+  finish_layer(s, true);
+
+  // ---- layer_xyz2, fc_out, layer_dir1 (feature part), layer_dir2: one loop body
+  for (int layer = kXyz2; layer <= kDir2; ++layer) {
+    init_acc(s, a, layer);
+    const bool with9 = (layer == kOut);
+#pragma unroll
+    for (int k = 0; k < 16; k += 2) run_chunk(s, a, lds, c, s.bh[k], s.bl[k], s.bh[k + 1], s.bl[k + 1], with9);
+    if (layer == kDir1) run_chunk(s, a, lds, c, s.dh[0], s.dl[0], s.dh[1], s.dl[1], false);
+    if (layer == kOut) {
+      s.sigma = s.acc[8][0];
+      if constexpr (MODE != kFromEncoded) {
+        // view-direction encoding for layer_dir1 (fc_out's accumulators are dead)
+        float v[16];
+        encode_pairs<6, 4>(s.vd, a.fd, s.h, v);
+        v[14] = 0.0f;
+        v[15] = 0.0f;
+        split8(v, s.dh[0], s.dl[0]);
+        split8(v + 8, s.dh[1], s.dl[1]);
+      }
+    }
+    finish_layer(s, layer != kOut);  // fc_out's feat has no activation
+  }
+
+  // ---- fc_rgb (256 -> 3): one chunk holding its 16 k-steps of block 0
+  init_acc(s, a, kRgb);
+  chunk_barrier();
+  {
+    const float4* slot = lds + (c & (kSlots - 1)) * kChunkQuads;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const float4* ap = slot + (k / 9) * kQuadsPerStep + (2 * (k % 9)) * 64 + s.lane;
+      mfma3(s.acc[0], __builtin_bit_cast(bf16x8, ap[0]), __builtin_bit_cast(bf16x8, ap[64]), s.bh[k], s.bl[k]);
+    }
+  }
+  // drain the dummy chunks' DMA before the workgroup's LDS is released
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
   if (valid && s.h == 0) {
     float4 o;
@@ -418,6 +410,9 @@ __global__ __launch_bounds__(kThreads, 1) void field_x3_kernel(FieldArgs a) {
     reinterpret_cast<float4*>(a.raw)[row] = o;
   }
 }
+
+static_assert(kChunkRgb + 1 == kRealChunks, "chunk schedule");
+static_assert(kDmaPerWave * 64 * 4 == kChunkQuads, "chunk = 36 DMA wave-instructions");
 
 }  // namespace x3
 
