@@ -45,6 +45,20 @@ SIGNATURES = {
     "cn_code_bias": (_i, [ctypes.POINTER(_p), _p, _p, _i64, _p, _p]),
     "cn_mlp_forward": (_i, [_p, _i, _p, _p, _i64, _p, _i64, _p, _p]),
     "cn_radiance_field": (_i, [_p, _i, _p, _p, _i64, _p, _p, _p, _p, _i64, _i64, _i64, _fp, _fp, _p, _p]),
+    "cn_radiance_field_train": (_i, [_p, _p, _p, _i64, _p, _p, _p, _p, _i64, _i64, _i64, _fp, _fp, _p, _p, _p]),
+    "cn_mlp_forward_train": (_i, [_p, _p, _p, _i64, _p, _i64, _p, _p, _p]),
+    "cn_encode_inputs": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _fp, _fp, _p, _p]),
+    "cn_field_backward_workspace_floats": (_i64, [_i64]),
+    "cn_field_backward": (_i, [ctypes.POINTER(_p), _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p, _i64, _fp, _fp,
+                               _p, ctypes.POINTER(_p), _p, _p, _p, _p, _p]),
+    "cn_code_bias_backward": (_i, [ctypes.POINTER(_p), _p, _p, _i64, _p, _p, _p, ctypes.POINTER(_p), _p]),
+    "cn_volume_render_backward": (_i, [_p, _p, _p, _i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p]),
+    "cn_ray_bundle_backward": (_i, [_p, _i64, _i64, _p, _p, _p, _p]),
+    "cn_gather_rays_backward": (_i, [_p, _p, _i64, _i64, _p, _i64, _p, _p, _p]),
+    "cn_posenc_backward": (_i, [_p, _i64, _i64, _fp, _i64, _i, _p, _p, _p]),
+    "cn_ray_points_backward": (_i, [_p, _p, _i64, _i64, _p, _p, _p]),
+    "cn_gemm_nn":(_i, [_p, _i64, _p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _p]),
+    "cn_gemm_tn": (_i, [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _p]),
 }
 
 _lib: Optional[ctypes.CDLL] = None

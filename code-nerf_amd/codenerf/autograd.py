@@ -1,7 +1,16 @@
 """torch.autograd.Function wrappers of the HIP ops.
 
-Each wrapper runs the HIP forward; when no input requires grad it returns the
-plain op result and records nothing.
+The gradients ``loss.backward()`` takes through the reference's eval step
+(test-time optimisation of pose + codes, view_synthesis/eval.py) and training
+step: get_bundle -> sample gather -> point sampling (depths detached,
+point_sampler.py:115) -> forward_pass / CodeNeRFModel.forward -> volume_render.
+Every forward and backward runs on the gfx950 kernels through the C ABI;
+torch only allocates buffers and routes gradients.
+
+When no input requires grad each wrapper returns the plain op result and
+records nothing.  The differentiable field always runs the fp32 kernel
+(``cn_radiance_field_train``), which also stores the activations the backward
+reads; the bf16x3 format is an inference-only choice.
 """
 from __future__ import annotations
 
@@ -16,44 +25,239 @@ def _needs_grad(*ts) -> bool:
     return torch.is_grad_enabled() and any(isinstance(t, torch.Tensor) and t.requires_grad for t in ts)
 
 
-def _no_backward(name):
-    raise NotImplementedError(f"backward of {name} on the gfx950 path is not built yet")
+def _d(t):
+    return None if t is None else t.detach()
+
+
+# ------------------------------------------------------------------ rays
+
+
+class RayBundle(torch.autograd.Function):
+    """get_bundle (ray_sampler.py:84-99) -> ro, rd; gradient w.r.t. tform_cam2world."""
+
+    @staticmethod
+    def forward(ctx, dirs, c2w):
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(dirs)
+        ctx.batch = c2w.shape[0]
+        return ops.ray_bundle(dirs, c2w)
+
+    @staticmethod
+    def backward(ctx, g_ro, g_rd):
+        if not ctx.needs_input_grad[1] or (g_ro is None and g_rd is None):
+            return None, None
+        (dirs,) = ctx.saved_tensors
+        return None, ops.ray_bundle_backward(dirs, ctx.batch, _c(g_ro), _c(g_rd))
+
+
+class GatherRays(torch.autograd.Function):
+    """RaySampler.sample gather (ray_sampler.py:77-80); scatter-add backward."""
+
+    @staticmethod
+    def forward(ctx, ro, rd, sel):
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(sel)
+        ctx.shape = ro.shape
+        return ops.gather_rays(ro, rd, sel)
+
+    @staticmethod
+    def backward(ctx, g_o, g_d):
+        if g_o is None and g_d is None:
+            return None, None, None
+        (sel,) = ctx.saved_tensors
+        b = sel.shape[0]
+        hw = ctx.shape.numel() // (3 * b)
+        d_ro, d_rd = ops.gather_rays_backward(_c(g_o), _c(g_d), b, hw, sel)
+        return d_ro.view(ctx.shape), d_rd.view(ctx.shape), None
+
+
+class SamplePoints(torch.autograd.Function):
+    """pts = ro + rd * z with z detached (point_sampler.py:70, :115-118)."""
+
+    @staticmethod
+    def forward(ctx, ro, rd, z):
+        ctx.save_for_backward(z)
+        return ops.ray_points(ro, rd, z)
+
+    @staticmethod
+    def backward(ctx, g):
+        (z,) = ctx.saved_tensors
+        d_ro, d_rd = ops.ray_points_backward(g.contiguous(), z, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+        return d_ro, d_rd, None
+
+
+class Posenc(torch.autograd.Function):
+    """PositionalEmbedder.embed (position_embed.py:35-53)."""
+
+    @staticmethod
+    def forward(ctx, x, freqs, include_input):
+        ctx.save_for_backward(x)
+        ctx.freqs, ctx.include_input = list(freqs), bool(include_input)
+        return ops.posenc(x, freqs, include_input)
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        return ops.posenc_backward(x, ctx.freqs, ctx.include_input, g.contiguous()), None, None
+
+
+class VolumeRender(torch.autograd.Function):
+    """volume_render (volumetric_render.py:36-66) -> rgb, disp, acc, weights, depth."""
+
+    @staticmethod
+    def forward(ctx, raw, z, rd):
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(raw, z, rd)
+        return ops.volume_render(raw, z, rd)
+
+    @staticmethod
+    def backward(ctx, g_rgb, g_disp, g_acc, g_w, g_depth):
+        if all(g is None for g in (g_rgb, g_disp, g_acc, g_w, g_depth)):
+            return None, None, None
+        raw, z, rd = ctx.saved_tensors
+        d_raw, d_rd = ops.volume_render_backward(raw, z, rd, _c(g_rgb), _c(g_disp), _c(g_acc), _c(g_w), _c(g_depth),
+                                                 want_rd=ctx.needs_input_grad[2])
+        return d_raw, None, d_rd
+
+
+def _c(t):
+    return None if t is None else t.contiguous()
+
+
+# ------------------------------------------------------------------ field
+
+
+class _FieldMeta:
+    """Non-tensor arguments of the field Functions."""
+
+    def __init__(self, n_samples, chunk_rows, fx, fd, code_index=None):
+        self.n_samples, self.chunk_rows = n_samples, chunk_rows
+        self.fx, self.fd = list(fx) if fx is not None else None, list(fd) if fd is not None else None
+        self.code_index = code_index
+
+
+def _param_grad_buffers(params, needs):
+    if not any(needs):
+        return None
+    return [torch.zeros_like(p) for p in params]
+
+
+class RadianceField(torch.autograd.Function):
+    """forward_pass (nerf/__init__.py:94-134) + CodeNeRFModel.forward (model.py:160-194), fused.
+
+    Inputs: rd (R,3), pts (R,S,3) or (ro (R,3), z (R,S)), code rows z_s/z_t (n_codes, 256),
+    then the 18 parameters in state_dict order.  Output raw (R, S, 4).
+    """
+
+    @staticmethod
+    def forward(ctx, meta, rd, pts, ro, z, z_s, z_t, *params):
+        params = [p.detach() for p in params]
+        cb = ops.code_bias(params, z_s, z_t)
+        packed = ops.mlp_pack(params, "f32")
+        raw, saved = ops.radiance_field_train(packed, cb, rd, meta.n_samples, meta.chunk_rows, meta.fx, meta.fd,
+                                              pts=pts, ro=ro, z=z, code_index=meta.code_index)
+        ctx.x_enc = ops.encode_inputs(rd, meta.n_samples, meta.chunk_rows, meta.fx, meta.fd, pts=pts, ro=ro, z=z)
+        ctx.meta, ctx.acts = meta, saved
+        ctx.save_for_backward(rd, pts, ro, z, z_s, z_t, *params)
+        return raw
+
+    @staticmethod
+    def backward(ctx, g_raw):
+        rd, pts, ro, z, z_s, z_t, *params = ctx.saved_tensors
+        needs = ctx.needs_input_grad
+        meta = ctx.meta
+        pg = _param_grad_buffers(params, needs[7:])
+        want_z = needs[5] or needs[6]
+        r = ops.field_backward(params, ctx.acts, ctx.x_enc, g_raw.contiguous(), rd.shape[0], meta.n_samples,
+                               meta.chunk_rows, z_s.shape[0], meta.fx, meta.fd, rd=rd, pts=pts, ro=ro, z=z,
+                               code_index=meta.code_index, param_grads=pg, want_code=want_z or pg is not None,
+                               want_pts=needs[2], want_ro=needs[3], want_rd=needs[1])
+        dz_s = dz_t = None
+        if r["g_code"] is not None:
+            dz_s, dz_t = ops.code_bias_backward(params, z_s, z_t, r["g_code"], pg, want_z=want_z)
+        ctx.acts = ctx.x_enc = None
+        grads = pg if pg is not None else [None] * len(params)
+        return (None, r["d_rd"], r["d_pts"], r["d_ro"], None, dz_s, dz_t, *grads)
+
+
+class MLPForward(torch.autograd.Function):
+    """CodeNeRFModel.forward(z_s, z_t, x) on encoded rows (model.py:160-194)."""
+
+    @staticmethod
+    def forward(ctx, x, z_s, z_t, *params):
+        params = [p.detach() for p in params]
+        cb = ops.code_bias(params, z_s, z_t)
+        packed = ops.mlp_pack(params, "f32")
+        raw, saved = ops.mlp_forward_train(packed, cb, x)
+        ctx.acts = saved
+        ctx.save_for_backward(x, z_s, z_t, *params)
+        return raw
+
+    @staticmethod
+    def backward(ctx, g_raw):
+        x, z_s, z_t, *params = ctx.saved_tensors
+        needs = ctx.needs_input_grad
+        pg = _param_grad_buffers(params, needs[3:])
+        want_z = needs[1] or needs[2]
+        m = x.shape[0]
+        r = ops.field_backward(params, ctx.acts, x, g_raw.contiguous(), m, 1, m, z_s.shape[0], param_grads=pg,
+                               want_code=want_z or pg is not None, want_x=needs[0])
+        dz_s = dz_t = None
+        if r["g_code"] is not None:
+            dz_s, dz_t = ops.code_bias_backward(params, z_s, z_t, r["g_code"], pg, want_z=want_z)
+        ctx.acts = None
+        grads = pg if pg is not None else [None] * len(params)
+        return (r.get("d_x"), dz_s, dz_t, *grads)
+
+
+# ------------------------------------------------------------------ entry points used by the package
 
 
 def ray_bundle_autograd(dirs, c2w):
     if not _needs_grad(c2w):
         return ops.ray_bundle(dirs, c2w.detach())
-    _no_backward("ray_bundle")
+    return RayBundle.apply(dirs.detach(), c2w)
 
 
 def gather_rays_autograd(ro, rd, sel):
     if not _needs_grad(ro, rd):
         return ops.gather_rays(ro.detach(), rd.detach(), sel)
-    _no_backward("gather_rays")
+    return GatherRays.apply(ro, rd, sel)
 
 
 def sample_points_autograd(ro, rd, z):
     """pts = ro + rd * z for sorted depths z (detached, point_sampler.py:70,115-118)."""
     if not _needs_grad(ro, rd):
         return ops.ray_points(ro.detach(), rd.detach(), z.detach())
-    _no_backward("sample points")
+    return SamplePoints.apply(ro, rd, z.detach())
 
 
 def posenc_autograd(x, freqs: Sequence[float], include_input: bool):
     if not _needs_grad(x):
         return ops.posenc(x.detach(), freqs, include_input)
-    _no_backward("posenc")
+    return Posenc.apply(x, list(freqs), include_input)
 
 
 def volume_render_autograd(raw, z, rd):
     if not _needs_grad(raw, rd):
         return ops.volume_render(raw.detach(), z.detach(), rd.detach())
-    _no_backward("volume_render")
+    return VolumeRender.apply(raw, z.detach(), rd)
+
+
+def _code_rows(z_s, z_t):
+    """One code row when the per-row codes are an expand() of one row, else one per row."""
+    if z_s.dim() == 2 and z_s.stride(0) == 0 and z_t.stride(0) == 0:
+        return z_s[:1], z_t[:1]
+    return z_s, z_t
 
 
 def mlp_forward_autograd(model, z_s, z_t, x):
-    _no_backward("CodeNeRFModel.forward")
+    cs, ct = _code_rows(z_s, z_t)
+    return MLPForward.apply(x, cs, ct, *model.param_list())
 
 
 def radiance_field_autograd(model, rd, z_s, z_t, chunk_rows, fx, fd, pts=None, ro=None, z=None):
-    _no_backward("forward_pass")
+    cs, ct = _code_rows(z_s, z_t)
+    n_samples = pts.shape[1] if pts is not None else z.shape[1]
+    meta = _FieldMeta(n_samples, chunk_rows, fx, fd)
+    return RadianceField.apply(meta, rd, pts, ro, _d(z), cs, ct, *model.param_list())

@@ -126,12 +126,9 @@ def render_rays(ro: torch.Tensor, rd: torch.Tensor, z_s: torch.Tensor, z_t: torc
         t_rand = torch.rand(n, ps.num_samples_coarse, dtype=torch.float32, device=ro.device)
     _, z_c = ops.sample_uniform(ro.detach(), rd.detach(), ps.z_vals, ps.lower, ps.upper,
                                 t_rand if ps.perturb else None, want_pts=False)
-    grad = torch.is_grad_enabled() and (ro.requires_grad or rd.requires_grad)
-    if grad:
-        from ..autograd import sample_points_autograd
-        raw_c = _field(coarse_model, embedders, rd, z_s, z_t, chunk_rows, pts=sample_points_autograd(ro, rd, z_c))
-    else:
-        raw_c = timed_field(coarse_model, embedders, rd, z_s, z_t, chunk_rows, ro=ro, z=z_c)
+    # pts = ro + rd z is formed inside the field kernel (z detached, point_sampler.py:115); with
+    # gradients on, the field's backward returns d ro / d rd through both the points and the view dirs
+    raw_c = timed_field(coarse_model, embedders, rd, z_s, z_t, chunk_rows, ro=ro, z=z_c)
     rgb_c, disp_c, acc_c, w_c, depth_c = volume_render(raw_c, z_c, rd)
     out = {"rgb_coarse": rgb_c, "disp_coarse": disp_c, "acc_coarse": acc_c, "weights_coarse": w_c,
            "depth_coarse": depth_c, "z_coarse": z_c}
@@ -141,11 +138,7 @@ def render_rays(ro: torch.Tensor, rd: torch.Tensor, z_s: torch.Tensor, z_t: torc
         u = torch.rand(n, ps.num_samples_fine, dtype=torch.float32, device=ro.device)
     _, z_f = ops.sample_pdf(ro.detach(), rd.detach(), w_c.detach()[..., 1:-1], z_c, ps.num_samples_fine,
                             u if ps.perturb else ps.u_lin, want_pts=False)
-    if grad:
-        from ..autograd import sample_points_autograd
-        raw_f = _field(fine_model, embedders, rd, z_s, z_t, chunk_rows, pts=sample_points_autograd(ro, rd, z_f))
-    else:
-        raw_f = timed_field(fine_model, embedders, rd, z_s, z_t, chunk_rows, ro=ro, z=z_f)
+    raw_f = timed_field(fine_model, embedders, rd, z_s, z_t, chunk_rows, ro=ro, z=z_f)
     rgb_f, disp_f, acc_f, _, depth_f = volume_render(raw_f, z_f, rd)
     out.update({"rgb_fine": rgb_f, "disp_fine": disp_f, "acc_fine": acc_f, "depth_fine": depth_f, "z_fine": z_f})
     return out

@@ -250,3 +250,226 @@ def radiance_field(packed: Tensor, cb: Tensor, rd: Tensor, n_samples: int, chunk
                                 n, n_samples, chunk_rows, _lib.host_floats(freqs_xyz), _lib.host_floats(freqs_dir),
                                 ptr(raw), stream_of(rd)), "cn_radiance_field")
     return raw
+
+
+# ------------------------------------------------------------------ backward (A14)
+
+
+def _opt(t: Optional[Tensor], name: str) -> Optional[Tensor]:
+    return None if t is None else _cuda(t, name)
+
+
+def volume_render_backward(raw: Tensor, z: Tensor, rd: Tensor, g_rgb=None, g_disp=None, g_acc=None,
+                           g_weights=None, g_depth=None, want_rd: bool = True) -> Tuple[Tensor, Optional[Tensor]]:
+    """Gradient of volume_render (volumetric_render.py:36-66) -> d_raw (R,S,4), d_rd (R,3) or None."""
+    lib = _lib_ready()
+    raw, z, rd = _cuda(raw, "radiance_field"), _cuda(z, "depth_values"), _cuda(rd, "ray_directions")
+    n, s = z.shape
+    assert raw.shape == (n, s, 4) and rd.shape == (n, 3)
+    g_rgb, g_disp, g_acc, g_depth = (_opt(g_rgb, "g_rgb"), _opt(g_disp, "g_disp"), _opt(g_acc, "g_acc"),
+                                     _opt(g_depth, "g_depth"))
+    if g_weights is not None and g_weights.shape[-1] != s:   # S == 1: the reference's weights are (R, 0)
+        g_weights = None
+    g_weights = _opt(g_weights, "g_weights")
+    d_raw = torch.empty_like(raw)
+    d_rd = torch.empty_like(rd) if want_rd else None
+    check(lib.cn_volume_render_backward(ptr(raw), ptr(z), ptr(rd), n, s, ptr(g_rgb), ptr(g_disp), ptr(g_acc),
+                                        ptr(g_weights), ptr(g_depth), ptr(d_raw), ptr(d_rd), stream_of(raw)),
+          "cn_volume_render_backward")
+    return d_raw, d_rd
+
+
+def ray_bundle_backward(dirs: Tensor, batch: int, g_ro: Optional[Tensor], g_rd: Optional[Tensor]) -> Tensor:
+    """Gradient of get_bundle (ray_sampler.py:95-98) w.r.t. tform_cam2world -> (B, 4, 4)."""
+    lib = _lib_ready()
+    dirs = _cuda(dirs, "directions")
+    hw = dirs.numel() // 3
+    g_ro, g_rd = _opt(g_ro, "g_ro"), _opt(g_rd, "g_rd")
+    d = torch.zeros(batch, 4, 4, device=dirs.device, dtype=torch.float32)
+    if g_ro is None and g_rd is None:
+        return d
+    check(lib.cn_ray_bundle_backward(ptr(dirs), hw, batch, ptr(g_ro), ptr(g_rd), ptr(d), stream_of(d)),
+          "cn_ray_bundle_backward")
+    return d
+
+
+def gather_rays_backward(g_ro: Optional[Tensor], g_rd: Optional[Tensor], batch: int, hw: int,
+                         select_inds: Tensor) -> Tuple[Tensor, Tensor]:
+    """Gradient of the sample gather (ray_sampler.py:77-80) -> d ro, d rd (B, HW, 3)."""
+    lib = _lib_ready()
+    sel = _cuda(select_inds, "select_inds", torch.int64)
+    g_ro, g_rd = _opt(g_ro, "g_ro"), _opt(g_rd, "g_rd")
+    d_ro = torch.zeros(batch, hw, 3, device=sel.device, dtype=torch.float32)
+    d_rd = torch.zeros_like(d_ro)
+    check(lib.cn_gather_rays_backward(ptr(g_ro), ptr(g_rd), batch, hw, ptr(sel), sel.shape[1], ptr(d_ro), ptr(d_rd),
+                                      stream_of(sel)), "cn_gather_rays_backward")
+    return d_ro, d_rd
+
+
+def radiance_field_train(packed: Tensor, cb: Tensor, rd: Tensor, n_samples: int, chunk_rows: int,
+                         freqs_xyz: Sequence[float], freqs_dir: Sequence[float], pts: Optional[Tensor] = None,
+                         ro: Optional[Tensor] = None, z: Optional[Tensor] = None,
+                         code_index: Optional[Tensor] = None) -> Tuple[Tensor, Tensor]:
+    """fp32 radiance_field that also keeps the activations -> raw (R,S,4), saved (5, R*S, 256)."""
+    lib = _lib_ready()
+    rd = _cuda(rd, "rd")
+    n = rd.shape[0]
+    if pts is not None:
+        pts = _cuda(pts, "pts")
+        assert pts.shape == (n, n_samples, 3)
+    else:
+        ro, z = _cuda(ro, "ro"), _cuda(z, "z")
+        assert z.shape == (n, n_samples)
+    if code_index is not None:
+        code_index = _cuda(code_index, "code_index", torch.int64)
+    raw = torch.empty(n, n_samples, 4, device=rd.device, dtype=torch.float32)
+    saved = torch.empty(5, n * n_samples, 256, device=rd.device, dtype=torch.float32)
+    check(lib.cn_radiance_field_train(ptr(packed), ptr(cb), ptr(code_index), cb.shape[0], ptr(pts), ptr(ro), ptr(rd),
+                                      ptr(z), n, n_samples, chunk_rows, _lib.host_floats(freqs_xyz),
+                                      _lib.host_floats(freqs_dir), ptr(raw), ptr(saved), stream_of(rd)),
+          "cn_radiance_field_train")
+    return raw, saved
+
+
+def mlp_forward_train(packed: Tensor, cb: Tensor, x: Tensor, code_index: Optional[Tensor] = None
+                      ) -> Tuple[Tensor, Tensor]:
+    """fp32 mlp_forward that also keeps the activations -> raw (M,4), saved (5, M, 256)."""
+    lib = _lib_ready()
+    x = _cuda(x, "x")
+    assert x.dim() == 2 and x.shape[1] == 90
+    m = x.shape[0]
+    if code_index is not None:
+        code_index = _cuda(code_index, "code_index", torch.int64)
+    raw = torch.empty(m, 4, device=x.device, dtype=torch.float32)
+    saved = torch.empty(5, m, 256, device=x.device, dtype=torch.float32)
+    check(lib.cn_mlp_forward_train(ptr(packed), ptr(cb), ptr(code_index), cb.shape[0], ptr(x), m, ptr(raw),
+                                   ptr(saved), stream_of(x)), "cn_mlp_forward_train")
+    return raw, saved
+
+
+def encode_inputs(rd: Tensor, n_samples: int, chunk_rows: int, freqs_xyz: Sequence[float],
+                  freqs_dir: Sequence[float], pts: Optional[Tensor] = None, ro: Optional[Tensor] = None,
+                  z: Optional[Tensor] = None) -> Tensor:
+    """forward_pass's MLP input rows (nerf/__init__.py:116-132) -> (R*S, 90)."""
+    lib = _lib_ready()
+    rd = _cuda(rd, "rd")
+    n = rd.shape[0]
+    pts, ro, z = _opt(pts, "pts"), _opt(ro, "ro"), _opt(z, "z")
+    x = torch.empty(n * n_samples, 90, device=rd.device, dtype=torch.float32)
+    check(lib.cn_encode_inputs(ptr(pts), ptr(ro), ptr(rd), ptr(z), n, n_samples, chunk_rows,
+                               _lib.host_floats(freqs_xyz), _lib.host_floats(freqs_dir), ptr(x), stream_of(rd)),
+          "cn_encode_inputs")
+    return x
+
+
+def field_backward(params: Sequence[Tensor], saved: Tensor, x_enc: Tensor, d_raw: Tensor, n_rays: int,
+                   n_samples: int, chunk_rows: int, n_codes: int, freqs_xyz=None, freqs_dir=None,
+                   rd: Optional[Tensor] = None, pts: Optional[Tensor] = None, ro: Optional[Tensor] = None,
+                   z: Optional[Tensor] = None, code_index: Optional[Tensor] = None,
+                   param_grads: Optional[Sequence[Tensor]] = None, want_code: bool = False,
+                   want_pts: bool = False, want_ro: bool = False, want_rd: bool = False, want_x: bool = False):
+    """Backward of forward_pass + CodeNeRFModel.forward -> dict of d_pts / d_ro / d_rd / g_code / d_x.
+
+    ``param_grads``: 18 zero-or-running fp32 buffers the parameter gradients accumulate into.
+    """
+    lib = _lib_ready()
+    m = n_rays * n_samples
+    params = [_cuda(p.detach(), f"param{i}") for i, p in enumerate(params)]
+    d_raw = _cuda(d_raw, "d_raw")
+    assert d_raw.numel() == 4 * m and saved.shape == (5, m, 256) and x_enc.shape == (m, 90)
+    dev = d_raw.device
+    rd, pts, ro, z = _opt(rd, "rd"), _opt(pts, "pts"), _opt(ro, "ro"), _opt(z, "z")
+    if code_index is not None:
+        code_index = _cuda(code_index, "code_index", torch.int64)
+    ws = torch.empty(int(lib.cn_field_backward_workspace_floats(m)), device=dev, dtype=torch.float32)
+    out = {}
+    g_code = torch.zeros(n_codes, _lib.CN_CODE_BIAS_STRIDE, device=dev, dtype=torch.float32) if want_code else None
+    d_pts = torch.empty(n_rays, n_samples, 3, device=dev, dtype=torch.float32) if want_pts else None
+    d_ro = torch.zeros(n_rays, 3, device=dev, dtype=torch.float32) if want_ro else None
+    d_rd = torch.zeros(n_rays, 3, device=dev, dtype=torch.float32) if want_rd else None
+    arr, keep = _lib.pointer_array(params)
+    garr, gkeep = (None, None)
+    if param_grads is not None:
+        assert len(param_grads) == _lib.CN_NUM_PARAMS and all(g.is_contiguous() for g in param_grads)
+        garr, gkeep = _lib.pointer_array(list(param_grads))
+    fx = _lib.host_floats(freqs_xyz) if freqs_xyz is not None else None
+    fd = _lib.host_floats(freqs_dir) if freqs_dir is not None else None
+    check(lib.cn_field_backward(arr, ptr(saved), ptr(x_enc), ptr(d_raw), ptr(pts), ptr(ro), ptr(rd), ptr(z), n_rays,
+                                n_samples, chunk_rows, ptr(code_index), n_codes, fx, fd, ptr(ws), garr, ptr(g_code),
+                                ptr(d_pts), ptr(d_ro), ptr(d_rd), stream_of(d_raw)), "cn_field_backward")
+    del keep, gkeep
+    out.update(g_code=g_code, d_pts=d_pts, d_ro=d_ro, d_rd=d_rd)
+    if want_x:
+        off = 2 * 257 * m
+        out["d_x"] = ws[off: off + 90 * m].view(m, 90)
+    return out
+
+
+def code_bias_backward(params: Sequence[Tensor], z_s: Tensor, z_t: Tensor, g_code: Tensor,
+                       param_grads: Optional[Sequence[Tensor]] = None, want_z: bool = True):
+    """Backward of code_bias (model.py:174-177 + the code halves) -> dz_s, dz_t (n_codes, 256) or None."""
+    lib = _lib_ready()
+    params = [_cuda(p.detach(), f"param{i}") for i, p in enumerate(params)]
+    z_s, z_t, g_code = _cuda(z_s.detach(), "z_s"), _cuda(z_t.detach(), "z_t"), _cuda(g_code, "g_code")
+    n = z_s.shape[0]
+    dz_s = torch.empty_like(z_s) if want_z else None
+    dz_t = torch.empty_like(z_t) if want_z else None
+    arr, keep = _lib.pointer_array(params)
+    garr, gkeep = (None, None)
+    if param_grads is not None:
+        garr, gkeep = _lib.pointer_array(list(param_grads))
+    check(lib.cn_code_bias_backward(arr, ptr(z_s), ptr(z_t), n, ptr(g_code), ptr(dz_s), ptr(dz_t), garr,
+                                    stream_of(g_code)), "cn_code_bias_backward")
+    del keep, gkeep
+    return dz_s, dz_t
+
+
+def gemm_nn(a: Tensor, b: Tensor, mask: Optional[Tensor] = None) -> Tensor:
+    """C = A B (masked where mask <= 0) on the fp32 MFMA tile kernel."""
+    lib = _lib_ready()
+    a, b = _cuda(a, "A"), _cuda(b, "B")
+    (m, k), (k2, n) = a.shape, b.shape
+    assert k == k2
+    mask = _opt(mask, "mask")
+    c = torch.empty(m, n, device=a.device, dtype=torch.float32)
+    check(lib.cn_gemm_nn(ptr(a), k, ptr(b), n, ptr(c), n, ptr(mask), n, m, n, k, stream_of(a)), "cn_gemm_nn")
+    return c
+
+
+def gemm_tn(a: Tensor, b: Tensor, c: Optional[Tensor] = None) -> Tensor:
+    """C += A^T B on the fp32 MFMA tile kernel (C zero-initialised when not given)."""
+    lib = _lib_ready()
+    a, b = _cuda(a, "A"), _cuda(b, "B")
+    (m, n), (m2, k) = a.shape, b.shape
+    assert m == m2
+    if c is None:
+        c = torch.zeros(n, k, device=a.device, dtype=torch.float32)
+    check(lib.cn_gemm_tn(ptr(a), n, ptr(b), k, ptr(c), k, m, n, k, stream_of(a)), "cn_gemm_tn")
+    return c
+
+
+def posenc_backward(x: Tensor, freqs: Sequence[float], include_input: bool, g_enc: Tensor) -> Tensor:
+    """Gradient of PositionalEmbedder.embed (position_embed.py:35-53) w.r.t. its input."""
+    lib = _lib_ready()
+    x, g_enc = _cuda(x, "x"), _cuda(g_enc, "g_enc")
+    d = x.shape[-1]
+    m = x.numel() // d
+    assert g_enc.numel() == m * d * (int(include_input) + 2 * len(freqs))
+    dx = torch.empty_like(x)
+    check(lib.cn_posenc_backward(ptr(x), m, d, _lib.host_floats(freqs), len(freqs), int(include_input), ptr(g_enc),
+                                 ptr(dx), stream_of(x)), "cn_posenc_backward")
+    return dx
+
+
+def ray_points_backward(g_pts: Tensor, z: Tensor, want_ro: bool = True, want_rd: bool = True):
+    """Gradient of pts = ro + rd z (point_sampler.py:70, :118; z detached) -> d_ro, d_rd (R, 3)."""
+    lib = _lib_ready()
+    g_pts, z = _cuda(g_pts, "g_pts"), _cuda(z, "z")
+    n, s = z.shape
+    assert g_pts.shape == (n, s, 3)
+    d_ro = torch.zeros(n, 3, device=z.device, dtype=torch.float32) if want_ro else None
+    d_rd = torch.zeros(n, 3, device=z.device, dtype=torch.float32) if want_rd else None
+    if want_ro or want_rd:
+        check(lib.cn_ray_points_backward(ptr(g_pts), ptr(z), n, s, ptr(d_ro), ptr(d_rd), stream_of(z)),
+              "cn_ray_points_backward")
+    return d_ro, d_rd

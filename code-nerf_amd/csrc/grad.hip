@@ -1,0 +1,522 @@
+// Backward pass of the field: the gradients torch's
+// autograd takes through forward_pass / CodeNeRFModel.forward
+// (view_synthesis/nerf/__init__.py:94-134, models/model.py:160-194).
+//
+// Building blocks, all fp32 (exact-product MFMA, v_mfma_f32_32x32x2_f32):
+//   gemm_nn  C[m][n]  = (A[m][:] . B[:][n]) * (mask[m][n] > 0)     dX = dPre . W  (+ ReLU mask)
+//   gemm_tn  C[n][k] += sum_m A[m][n] B[m][k]   (split-M, atomics)   dW = dPre^T . X
+//   col_sum  out[j]  += sum_m A[m][j]                                 db
+//   seg_sum  out[code(m)][j] += A[m][j]                               per-object code-term gradients
+// and the element-wise pieces: posenc backward, the Q1 view-direction scatter,
+// pts = ro + rd z backward, and the code-layer backward.
+#include "cn_common.h"
+#include "mlp_common.h"
+
+namespace cn {
+namespace grad {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+// ---------------------------------------------------------------- GEMMs
+constexpr int kBM = 64, kBN = 64, kBK = 32;
+
+// 64x64 tile per 256-thread block; wave (wr, wc) owns a 32x32 quadrant.
+__global__ __launch_bounds__(256) void gemm_nn_kernel(const float* __restrict__ A, int64_t lda,
+                                                      const float* __restrict__ B, int64_t ldb,
+                                                      float* __restrict__ C, int64_t ldc,
+                                                      const float* __restrict__ mask, int64_t ldm,
+                                                      int64_t M, int N, int K) {
+  __shared__ float As[kBM][kBK + 1];
+  __shared__ float Bs[kBK][kBN];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int64_t m0 = (int64_t)blockIdx.x * kBM;
+  const int n0 = blockIdx.y * kBN;
+  floatx16 acc = {0};
+  for (int k0 = 0; k0 < K; k0 += kBK) {
+#pragma unroll
+    for (int i = 0; i < (kBM * kBK) / 256; ++i) {
+      const int e = i * 256 + tid, r = e / kBK, c = e % kBK;
+      const int64_t m = m0 + r;
+      As[r][c] = (m < M && k0 + c < K) ? A[m * lda + k0 + c] : 0.0f;
+    }
+#pragma unroll
+    for (int i = 0; i < (kBK * kBN) / 256; ++i) {
+      const int e = i * 256 + tid, r = e / kBN, c = e % kBN;
+      Bs[r][c] = (k0 + r < K && n0 + c < N) ? B[(int64_t)(k0 + r) * ldb + n0 + c] : 0.0f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < kBK; kk += 2) {
+      const float a = As[32 * wr + (lane & 31)][kk + (lane >> 5)];
+      const float b = Bs[kk + (lane >> 5)][32 * wc + (lane & 31)];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  const int col = n0 + 32 * wc + (lane & 31);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int64_t m = m0 + 32 * wr + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    if (m < M && col < N) {
+      float v = acc[r];
+      if (mask && !(mask[m * ldm + col] > 0.0f)) v = 0.0f;  // ReLU'(x) = [x > 0], torch's threshold_backward
+      C[m * ldc + col] = v;
+    }
+  }
+}
+
+constexpr int kSliceM = 2048;  // rows reduced per block before the atomic flush
+
+__global__ __launch_bounds__(256) void gemm_tn_kernel(const float* __restrict__ A, int64_t lda,
+                                                      const float* __restrict__ B, int64_t ldb,
+                                                      float* __restrict__ C, int64_t ldc, int64_t M,
+                                                      int N, int K) {
+  __shared__ float As[kBK][kBN];   // [m][n]
+  __shared__ float Bs[kBK][kBN];   // [m][k]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int n0 = blockIdx.x * kBN, k0 = blockIdx.y * kBN;
+  const int64_t mb = (int64_t)blockIdx.z * kSliceM;
+  const int64_t me = min(M, mb + kSliceM);
+  floatx16 acc = {0};
+  for (int64_t m0 = mb; m0 < me; m0 += kBK) {
+#pragma unroll
+    for (int i = 0; i < (kBK * kBN) / 256; ++i) {
+      const int e = i * 256 + tid, r = e / kBN, c = e % kBN;
+      const int64_t m = m0 + r;
+      As[r][c] = (m < me && n0 + c < N) ? A[m * lda + n0 + c] : 0.0f;
+      Bs[r][c] = (m < me && k0 + c < K) ? B[m * ldb + k0 + c] : 0.0f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < kBK; kk += 2) {
+      const float a = As[kk + (lane >> 5)][32 * wr + (lane & 31)];
+      const float b = Bs[kk + (lane >> 5)][32 * wc + (lane & 31)];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  const int col = k0 + 32 * wc + (lane & 31);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = n0 + 32 * wr + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    if (row < N && col < K) atomicAdd(&C[(int64_t)row * ldc + col], acc[r]);
+  }
+}
+
+// out[code(m)][j * ostride] += A[m][j] for j < N; code(m) = code_index ? code_index[m / S]
+// : (n_codes == 1 ? 0 : m / S).  Each thread owns a column and walks a row slice,
+// flushing when the code changes (rows of one ray are contiguous).
+__global__ __launch_bounds__(256) void seg_sum_kernel(const float* __restrict__ A, int64_t lda, int64_t M,
+                                                      int N, int64_t S, const int64_t* __restrict__ code_index,
+                                                      int64_t n_codes, float* __restrict__ out,
+                                                      int64_t out_ld) {
+  const int64_t mb = (int64_t)blockIdx.x * kSliceM, me = min(M, mb + kSliceM);
+  for (int j = threadIdx.x; j < N; j += blockDim.x) {
+    float sum = 0.0f;
+    int64_t cur = -1;
+    for (int64_t m = mb; m < me; ++m) {
+      const int64_t ray = m / S;
+      const int64_t code = code_index ? code_index[ray] : (n_codes == 1 ? 0 : ray);
+      if (code != cur) {
+        if (cur >= 0) atomicAdd(&out[cur * out_ld + j], sum);
+        cur = code;
+        sum = 0.0f;
+      }
+      sum += A[m * lda + j];
+    }
+    if (cur >= 0) atomicAdd(&out[cur * out_ld + j], sum);
+  }
+}
+
+// ---------------------------------------------------------------- element-wise pieces
+
+// PositionalEmbedder.embed backward: d x[m][d] from d enc[m][(inc + 2k + {0,1}) * D + d].
+struct Freqs {
+  float f[32];
+};
+
+__host__ inline Freqs make_freqs(const float* host, int n) {
+  Freqs r = {};
+  for (int i = 0; i < n; ++i) r.f[i] = host[i];
+  return r;
+}
+
+__global__ void posenc_backward_kernel(const float* __restrict__ x, int64_t ldx, const float* __restrict__ denc,
+                                       int64_t ldenc, int64_t M, int D, Freqs fr, int nf, int inc,
+                                       float* __restrict__ dx, int64_t lddx) {
+  const int64_t n = M * D;
+  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n; q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = q / D;
+    const int d = static_cast<int>(q - m * D);
+    const float v = x[m * ldx + d];
+    const float* g = denc + m * ldenc;
+    float acc = inc ? g[d] : 0.0f;
+    for (int k = 0; k < nf; ++k) {
+      const float f_k = fr.f[k];
+      float sn, cs;
+      sincosf(__fmul_rn(v, f_k), &sn, &cs);
+      acc += f_k * (g[(inc + 2 * k) * D + d] * cs - g[(inc + 2 * k + 1) * D + d] * sn);
+    }
+    dx[m * lddx + d] = acc;
+  }
+}
+
+// forward_pass's view directions (nerf/__init__.py:125-128): vd = rd[dray] / |rd[dray]| with the Q1
+// ray map; d rd[dray] += (g - vd (vd . g)) / |rd[dray]|.
+__global__ void viewdir_backward_kernel(const float* __restrict__ rd, const float* __restrict__ dvd, int64_t lddvd,
+                                        int64_t n_rays, int64_t S, int64_t chunk_rows, float* __restrict__ d_rd) {
+  const int64_t M = n_rays * S;
+  for (int64_t m = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; m < M; m += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t ray = m / S, smp = m - ray * S;
+    const int64_t base = (ray / chunk_rows) * chunk_rows;
+    const int64_t rcnt = min(chunk_rows, n_rays - base);
+    const int64_t dray = base + ((ray - base) * S + smp) % rcnt;
+    const float d0 = rd[3 * dray], d1 = rd[3 * dray + 1], d2 = rd[3 * dray + 2];
+    const float nrm = sqrtf(d0 * d0 + d1 * d1 + d2 * d2);
+    const float v0 = d0 / nrm, v1 = d1 / nrm, v2 = d2 / nrm;
+    const float g0 = dvd[m * lddvd], g1 = dvd[m * lddvd + 1], g2 = dvd[m * lddvd + 2];
+    const float dot = v0 * g0 + v1 * g1 + v2 * g2;
+    atomicAdd(&d_rd[3 * dray], (g0 - v0 * dot) / nrm);
+    atomicAdd(&d_rd[3 * dray + 1], (g1 - v1 * dot) / nrm);
+    atomicAdd(&d_rd[3 * dray + 2], (g2 - v2 * dot) / nrm);
+  }
+}
+
+// pts = ro + rd * z (point_sampler.py:70, :118): d ro[r] += sum_s d pts, d rd[r] += sum_s d pts * z.
+__global__ void ray_points_backward_kernel(const float* __restrict__ dpts, int64_t ldp, const float* __restrict__ z,
+                                           int64_t n_rays, int64_t S, float* __restrict__ d_ro,
+                                           float* __restrict__ d_rd) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n_rays; r += (int64_t)gridDim.x * blockDim.x) {
+    float o0 = 0.f, o1 = 0.f, o2 = 0.f, e0 = 0.f, e1 = 0.f, e2 = 0.f;
+    for (int64_t s = 0; s < S; ++s) {
+      const int64_t m = r * S + s;
+      const float zz = z[m];
+      const float g0 = dpts[m * ldp], g1 = dpts[m * ldp + 1], g2 = dpts[m * ldp + 2];
+      o0 += g0; o1 += g1; o2 += g2;
+      e0 += g0 * zz; e1 += g1 * zz; e2 += g2 * zz;
+    }
+    if (d_ro) {
+      d_ro[3 * r] += o0; d_ro[3 * r + 1] += o1; d_ro[3 * r + 2] += o2;
+    }
+    if (d_rd) {
+      d_rd[3 * r] += e0; d_rd[3 * r + 1] += e1; d_rd[3 * r + 2] += e2;
+    }
+  }
+}
+
+// Q1 view-direction + point encoding of forward_pass, row-major (M, 90) = [xyz 63 | dir 27]
+// (the input the reference hands CodeNeRFModel.forward, nerf/__init__.py:116-132).
+__global__ void encode_inputs_kernel(mlp::FieldArgs a, float* __restrict__ out) {
+  const int64_t M = a.m;
+  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < M * 90; q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = q / 90;
+    const int c = static_cast<int>(q - m * 90);
+    const mlp::SampleIn in = a.pts ? mlp::decode_sample<mlp::kFromPts>(a, m) : mlp::decode_sample<mlp::kFromRayZ>(a, m);
+    const bool dir = c >= 63;
+    const int cc = dir ? c - 63 : c;
+    const float* v = dir ? in.vd : in.x;
+    float o;
+    if (cc < 3) {
+      o = v[cc];
+    } else {
+      const int b = (cc - 3) / 3, comp = (cc - 3) % 3;
+      const float arg = __fmul_rn(v[comp], dir ? a.fd[b >> 1] : a.fx[b >> 1]);
+      o = (b & 1) ? cosf(arg) : sinf(arg);
+    }
+    out[q] = o;
+  }
+}
+
+// dst[m][0:ncols] = src[m][0:ncols] (strided), e.g. d raw[:, 3] -> fc_out's sigma row.
+__global__ void copy_cols_kernel(const float* __restrict__ src, int64_t lds_, float* __restrict__ dst, int64_t ldd,
+                                 int64_t M, int ncols) {
+  const int64_t n = M * ncols;
+  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n; q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = q / ncols;
+    const int c = static_cast<int>(q - m * ncols);
+    dst[m * ldd + c] = src[m * lds_ + c];
+  }
+}
+
+// ---------------------------------------------------------------- code layers (model.py:174-177)
+// Per code row: recompute zs1 / zs2 / zt1, pull the summed code-term gradients g
+// (520-wide, cn_code_bias layout) back through the code halves of layer_xyz2 /
+// fc_out / fc_rgb and the three code layers.  dW / db accumulate with atomics.
+__global__ __launch_bounds__(256) void code_backward_kernel(mlp::Params P, const float* __restrict__ z_s,
+                                                            const float* __restrict__ z_t, const float* __restrict__ g,
+                                                            float* __restrict__ dz_s, float* __restrict__ dz_t,
+                                                            mlp::Params G) {
+  using namespace mlp;
+  __shared__ float zs[256], zt[256], s1[256], s2[256], t1[256], ds1[256], ds2[256], dt1[256], go[257];
+  const int c = blockIdx.x, j = threadIdx.x;
+  const float* gr = g + (int64_t)c * kCbStride;
+  zs[j] = z_s[(int64_t)c * 256 + j];
+  zt[j] = z_t[(int64_t)c * 256 + j];
+  go[1 + j] = gr[kCbFeat + j];
+  if (j == 0) go[0] = gr[kCbSigma];
+  __syncthreads();
+  {
+    float a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    for (int k = 0; k < 256; ++k) {
+      a1 = fmaf(P.p[kWSc1][j * 256 + k], zs[k], a1);
+      a2 = fmaf(P.p[kWSc2][j * 256 + k], zs[k], a2);
+      a3 = fmaf(P.p[kWTc1][j * 256 + k], zt[k], a3);
+    }
+    s1[j] = fmaxf(a1 + P.p[kBSc1][j], 0.f);
+    s2[j] = fmaxf(a2 + P.p[kBSc2][j], 0.f);
+    t1[j] = fmaxf(a3 + P.p[kBTc1][j], 0.f);
+  }
+  __syncthreads();
+  // d zs1 = W_xyz2[:, 256:]^T g_x2, d zs2 = W_out[:, 256:]^T g_o, d zt1 = W_rgb[:, 256:]^T g_rgb (masked)
+  {
+    float a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    for (int n = 0; n < 256; ++n) a1 = fmaf(P.p[kWXyz2][n * 512 + 256 + j], gr[kCbXyz2 + n], a1);
+    for (int n = 0; n < 257; ++n) a2 = fmaf(P.p[kWOut][n * 512 + 256 + j], go[n], a2);
+    for (int n = 0; n < 3; ++n) a3 = fmaf(P.p[kWRgb][n * 512 + 256 + j], gr[kCbRgb + n], a3);
+    ds1[j] = s1[j] > 0.f ? a1 : 0.f;
+    ds2[j] = s2[j] > 0.f ? a2 : 0.f;
+    dt1[j] = t1[j] > 0.f ? a3 : 0.f;
+  }
+  __syncthreads();
+  {
+    float a = 0.f, b = 0.f;
+    for (int n = 0; n < 256; ++n) {
+      a = fmaf(P.p[kWSc1][n * 256 + j], ds1[n], a);
+      a = fmaf(P.p[kWSc2][n * 256 + j], ds2[n], a);
+      b = fmaf(P.p[kWTc1][n * 256 + j], dt1[n], b);
+    }
+    if (dz_s) dz_s[(int64_t)c * 256 + j] = a;
+    if (dz_t) dz_t[(int64_t)c * 256 + j] = b;
+  }
+  if (!G.p[kWSc1]) return;
+  // weight gradients of the code layers and the code halves (row j of each)
+  for (int k = 0; k < 256; ++k) {
+    atomicAdd(&const_cast<float*>(G.p[kWSc1])[j * 256 + k], ds1[j] * zs[k]);
+    atomicAdd(&const_cast<float*>(G.p[kWSc2])[j * 256 + k], ds2[j] * zs[k]);
+    atomicAdd(&const_cast<float*>(G.p[kWTc1])[j * 256 + k], dt1[j] * zt[k]);
+    atomicAdd(&const_cast<float*>(G.p[kWXyz2])[j * 512 + 256 + k], gr[kCbXyz2 + j] * s1[k]);
+    atomicAdd(&const_cast<float*>(G.p[kWOut])[(1 + j) * 512 + 256 + k], go[1 + j] * s2[k]);
+  }
+  atomicAdd(&const_cast<float*>(G.p[kBSc1])[j], ds1[j]);
+  atomicAdd(&const_cast<float*>(G.p[kBSc2])[j], ds2[j]);
+  atomicAdd(&const_cast<float*>(G.p[kBTc1])[j], dt1[j]);
+  atomicAdd(&const_cast<float*>(G.p[kWOut])[256 + j], go[0] * s2[j]);              // fc_out row 0 (sigma)
+  if (j < 3)
+    for (int k = 0; k < 256; ++k)
+      atomicAdd(&const_cast<float*>(G.p[kWRgb])[j * 512 + 256 + k], gr[kCbRgb + j] * t1[k]);
+}
+
+}  // namespace grad
+}  // namespace cn
+
+// ================================================================ C ABI
+using namespace cn;
+
+namespace {
+
+int gemm_nn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, const float* mask,
+            int64_t ldm, int64_t M, int N, int K, hipStream_t st) {
+  dim3 grid(static_cast<unsigned>(ceil_div(M, grad::kBM)), static_cast<unsigned>(ceil_div(N, grad::kBN)));
+  hipLaunchKernelGGL(grad::gemm_nn_kernel, grid, dim3(256), 0, st, A, lda, B, ldb, C, ldc, mask, ldm, M, N, K);
+  return launch_status();
+}
+
+int gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M, int N, int K,
+            hipStream_t st) {
+  dim3 grid(static_cast<unsigned>(ceil_div(N, grad::kBN)), static_cast<unsigned>(ceil_div(K, grad::kBN)),
+            static_cast<unsigned>(ceil_div(M, grad::kSliceM)));
+  hipLaunchKernelGGL(grad::gemm_tn_kernel, grid, dim3(256), 0, st, A, lda, B, ldb, C, ldc, M, N, K);
+  return launch_status();
+}
+
+int seg_sum(const float* A, int64_t lda, int64_t M, int N, int64_t S, const int64_t* code_index, int64_t n_codes,
+            float* out, int64_t out_ld, hipStream_t st) {
+  hipLaunchKernelGGL(grad::seg_sum_kernel, dim3(static_cast<unsigned>(ceil_div(M, grad::kSliceM))), dim3(256), 0, st,
+                     A, lda, M, N, S, code_index, n_codes, out, out_ld);
+  return launch_status();
+}
+
+#define CN_TRY(x)              \
+  do {                         \
+    const int rc_ = (x);       \
+    if (rc_ != CN_OK) return rc_; \
+  } while (0)
+
+}  // namespace
+
+extern "C" int cn_gemm_nn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
+                          const float* mask, int64_t ldm, int64_t M, int64_t N, int64_t K, cn_stream_t stream) {
+  CN_CHECK_ARG(A && B && C && M > 0 && N > 0 && K > 0 && N <= 65536 && K <= 65536);
+  CN_CHECK_ARG(lda >= K && ldb >= N && ldc >= N && (!mask || ldm >= N));
+  return gemm_nn(A, lda, B, ldb, C, ldc, mask, ldm, M, (int)N, (int)K, as_stream(stream));
+}
+
+extern "C" int cn_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M,
+                          int64_t N, int64_t K, cn_stream_t stream) {
+  CN_CHECK_ARG(A && B && C && M > 0 && N > 0 && K > 0 && N <= 65536 && K <= 65536);
+  CN_CHECK_ARG(lda >= N && ldb >= K && ldc >= K);
+  return gemm_tn(A, lda, B, ldb, C, ldc, M, (int)N, (int)K, as_stream(stream));
+}
+
+extern "C" int cn_encode_inputs(const float* pts, const float* ro, const float* rd, const float* z, int64_t n_rays,
+                                int64_t n_samples, int64_t chunk_rows, const float* freqs_xyz, const float* freqs_dir,
+                                float* x, cn_stream_t stream) {
+  CN_CHECK_ARG(rd && x && freqs_xyz && freqs_dir && (pts || (ro && z)));
+  CN_CHECK_ARG(n_rays > 0 && n_samples > 0 && chunk_rows > 0);
+  mlp::FieldArgs a = {};
+  a.pts = pts;
+  a.ro = ro;
+  a.rd = rd;
+  a.z = z;
+  a.n_rays = n_rays;
+  a.n_samples = n_samples;
+  a.chunk_rows = chunk_rows;
+  a.m = n_rays * n_samples;
+  for (int i = 0; i < 10; ++i) a.fx[i] = freqs_xyz[i];
+  for (int i = 0; i < 4; ++i) a.fd[i] = freqs_dir[i];
+  hipLaunchKernelGGL(grad::encode_inputs_kernel, dim3(elementwise_grid(a.m * 90, 256)), dim3(256), 0,
+                     as_stream(stream), a, x);
+  return launch_status();
+}
+
+// Field backward: see include/codenerf.h.
+extern "C" int cn_field_backward(const float* const* params, const float* saved, const float* x_enc,
+                                 const float* d_raw, const float* pts, const float* ro, const float* rd,
+                                 const float* z, int64_t n_rays, int64_t n_samples, int64_t chunk_rows,
+                                 const int64_t* code_index, int64_t n_codes, const float* freqs_xyz,
+                                 const float* freqs_dir, float* workspace, float* const* grads, float* g_code,
+                                 float* d_pts, float* d_ro, float* d_rd, cn_stream_t stream) {
+  using namespace mlp;
+  CN_CHECK_ARG(params && saved && x_enc && d_raw && workspace);
+  CN_CHECK_ARG(n_rays > 0 && n_samples > 0 && chunk_rows > 0 && n_codes > 0);
+  if (d_pts || d_ro || d_rd) CN_CHECK_ARG(rd && freqs_xyz && freqs_dir && (pts || (ro && z)));
+  CN_CHECK_ARG(!d_pts || pts);
+  CN_CHECK_ARG(!d_ro || (ro && z && !pts));
+  for (int i = 0; i < CN_NUM_PARAMS; ++i) CN_CHECK_ARG(params[i]);
+  hipStream_t st = as_stream(stream);
+  const int64_t M = n_rays * n_samples;
+  const float* h1 = saved;
+  const float* h2 = saved + M * 256;
+  const float* feat = saved + 2 * M * 256;
+  const float* v1 = saved + 3 * M * 256;
+  const float* v2 = saved + 4 * M * 256;
+  float* dpa = workspace;              // (M, 257)
+  float* dpb = workspace + M * 257;    // (M, 257)
+  float* denc = workspace + 2 * M * 257;  // (M, 90)
+  float* dxp = workspace + 2 * M * 257 + M * 90;  // (M, 6): d pts | d viewdir
+  const bool wg = grads && grads[0];
+  auto G = [&](int i) { return grads ? grads[i] : nullptr; };
+
+  // fc_rgb: rgb = W_rgb [v2 | zt1] + b
+  CN_TRY(gemm_nn(d_raw, 4, params[kWRgb], 512, dpa, 257, v2, 256, M, 256, 3, st));  // d pre(layer_dir2)
+  if (wg) {
+    CN_TRY(gemm_tn(d_raw, 4, v2, 256, G(kWRgb), 512, M, 3, 256, st));
+    CN_TRY(seg_sum(d_raw, 4, M, 3, M, nullptr, 1, G(kBRgb), 1, st));
+  }
+  if (g_code) CN_TRY(seg_sum(d_raw, 4, M, 3, n_samples, code_index, n_codes, g_code + kCbRgb, kCbStride, st));
+  // layer_dir2: v2 = relu(W v1 + b)
+  CN_TRY(gemm_nn(dpa, 257, params[kWDir2], 256, dpb, 257, v1, 256, M, 256, 256, st));  // d pre(layer_dir1)
+  if (wg) {
+    CN_TRY(gemm_tn(dpa, 257, v1, 256, G(kWDir2), 256, M, 256, 256, st));
+    CN_TRY(seg_sum(dpa, 257, M, 256, M, nullptr, 1, G(kBDir2), 1, st));
+  }
+  // layer_dir1: v1 = relu(W [feat | dir] + b) -> d feat into dpa[:, 1:], d dir into denc[:, 63:]
+  CN_TRY(gemm_nn(dpb, 257, params[kWDir1], 283, dpa + 1, 257, nullptr, 0, M, 256, 256, st));
+  CN_TRY(gemm_nn(dpb, 257, params[kWDir1] + 256, 283, denc + 63, 90, nullptr, 0, M, 27, 256, st));
+  if (wg) {
+    CN_TRY(gemm_tn(dpb, 257, feat, 256, G(kWDir1), 283, M, 256, 256, st));
+    CN_TRY(gemm_tn(dpb, 257, x_enc + 63, 90, G(kWDir1) + 256, 283, M, 256, 27, st));
+    CN_TRY(seg_sum(dpb, 257, M, 256, M, nullptr, 1, G(kBDir1), 1, st));
+  }
+  // fc_out: [sigma | feat] = W [h2 | zs2] + b (no activation)
+  hipLaunchKernelGGL(grad::copy_cols_kernel, dim3(elementwise_grid(M, 256)), dim3(256), 0, st, d_raw + 3, 4, dpa, 257, M, 1);
+  CN_TRY(launch_status());
+  CN_TRY(gemm_nn(dpa, 257, params[kWOut], 512, dpb, 257, h2, 256, M, 256, 257, st));  // d pre(layer_xyz2)
+  if (wg) {
+    CN_TRY(gemm_tn(dpa, 257, h2, 256, G(kWOut), 512, M, 257, 256, st));
+    CN_TRY(seg_sum(dpa, 257, M, 257, M, nullptr, 1, G(kBOut), 1, st));
+  }
+  if (g_code) {
+    CN_TRY(seg_sum(dpa, 257, M, 1, n_samples, code_index, n_codes, g_code + kCbSigma, kCbStride, st));
+    CN_TRY(seg_sum(dpa + 1, 257, M, 256, n_samples, code_index, n_codes, g_code + kCbFeat, kCbStride, st));
+  }
+  // layer_xyz2: h2 = relu(W [h1 | zs1] + b)
+  CN_TRY(gemm_nn(dpb, 257, params[kWXyz2], 512, dpa, 257, h1, 256, M, 256, 256, st));  // d pre(layer_xyz1)
+  if (wg) {
+    CN_TRY(gemm_tn(dpb, 257, h1, 256, G(kWXyz2), 512, M, 256, 256, st));
+    CN_TRY(seg_sum(dpb, 257, M, 256, M, nullptr, 1, G(kBXyz2), 1, st));
+  }
+  if (g_code) CN_TRY(seg_sum(dpb, 257, M, 256, n_samples, code_index, n_codes, g_code + kCbXyz2, kCbStride, st));
+  // layer_xyz1: h1 = relu(W xyz63 + b)
+  CN_TRY(gemm_nn(dpa, 257, params[kWXyz1], 63, denc, 90, nullptr, 0, M, 63, 256, st));
+  if (wg) {
+    CN_TRY(gemm_tn(dpa, 257, x_enc, 90, G(kWXyz1), 63, M, 256, 63, st));
+    CN_TRY(seg_sum(dpa, 257, M, 256, M, nullptr, 1, G(kBXyz1), 1, st));
+  }
+  // encodings -> points / view directions
+  if (d_pts || d_ro || d_rd) {
+    hipLaunchKernelGGL(grad::posenc_backward_kernel, dim3(elementwise_grid(M * 3, 256)), dim3(256), 0, st, x_enc, 90,
+                       denc, 90, M, 3, grad::make_freqs(freqs_xyz, 10), 10, 1, dxp, 6);
+    CN_TRY(launch_status());
+    hipLaunchKernelGGL(grad::posenc_backward_kernel, dim3(elementwise_grid(M * 3, 256)), dim3(256), 0, st, x_enc + 63,
+                       90, denc + 63, 90, M, 3, grad::make_freqs(freqs_dir, 4), 4, 1, dxp + 3, 6);
+    CN_TRY(launch_status());
+    if (d_rd) {
+      hipLaunchKernelGGL(grad::viewdir_backward_kernel, dim3(elementwise_grid(M, 256)), dim3(256), 0, st, rd, dxp + 3, 6,
+                         n_rays, n_samples, chunk_rows, d_rd);
+      CN_TRY(launch_status());
+    }
+    if (pts) {
+      if (d_pts) {
+        hipLaunchKernelGGL(grad::copy_cols_kernel, dim3(elementwise_grid(M * 3, 256)), dim3(256), 0, st, dxp, 6, d_pts, 3,
+                           M, 3);
+        CN_TRY(launch_status());
+      }
+    } else if (d_ro || d_rd) {
+      hipLaunchKernelGGL(grad::ray_points_backward_kernel, dim3(elementwise_grid(n_rays, 256)), dim3(256), 0, st, dxp, 6, z,
+                         n_rays, n_samples, d_ro, d_rd);
+      CN_TRY(launch_status());
+    }
+  }
+  return CN_OK;
+}
+
+extern "C" int64_t cn_field_backward_workspace_floats(int64_t m) { return m * (2 * 257 + 90 + 6); }
+
+extern "C" int cn_code_bias_backward(const float* const* params, const float* z_s, const float* z_t, int64_t n_codes,
+                                     const float* g_code, float* dz_s, float* dz_t, float* const* grads,
+                                     cn_stream_t stream) {
+  using namespace mlp;
+  CN_CHECK_ARG(params && z_s && z_t && g_code && n_codes > 0 && n_codes < (1ll << 31));
+  Params P, G = {};
+  for (int i = 0; i < CN_NUM_PARAMS; ++i) {
+    CN_CHECK_ARG(params[i]);
+    P.p[i] = params[i];
+    G.p[i] = grads ? grads[i] : nullptr;
+  }
+  hipLaunchKernelGGL(grad::code_backward_kernel, dim3(static_cast<unsigned>(n_codes)), dim3(256), 0, as_stream(stream), P,
+                     z_s, z_t, g_code, dz_s, dz_t, G);
+  return launch_status();
+}
+
+extern "C" int cn_posenc_backward(const float* x, int64_t m, int64_t d, const float* freqs, int64_t num_freq,
+                                  int include_input, const float* g_enc, float* dx, cn_stream_t stream) {
+  CN_CHECK_ARG(x && g_enc && dx && m > 0 && d > 0 && num_freq >= 0 && num_freq <= 32 && (num_freq == 0 || freqs));
+  const int inc = include_input ? 1 : 0;
+  const int64_t ld = d * (inc + 2 * num_freq);
+  CN_CHECK_ARG(ld > 0);
+  hipLaunchKernelGGL(grad::posenc_backward_kernel, dim3(elementwise_grid(m * d, 256)), dim3(256), 0, as_stream(stream),
+                     x, d, g_enc, ld, m, static_cast<int>(d), grad::make_freqs(freqs, static_cast<int>(num_freq)),
+                     static_cast<int>(num_freq), inc, dx, d);
+  return launch_status();
+}
+
+extern "C" int cn_ray_points_backward(const float* g_pts, const float* z, int64_t n_rays, int64_t n_samples,
+                                      float* d_ro, float* d_rd, cn_stream_t stream) {
+  CN_CHECK_ARG(g_pts && z && n_rays > 0 && n_samples > 0 && (d_ro || d_rd));
+  hipLaunchKernelGGL(grad::ray_points_backward_kernel, dim3(elementwise_grid(n_rays, 256)), dim3(256), 0,
+                     as_stream(stream), g_pts, 3, z, n_rays, n_samples, d_ro, d_rd);
+  return launch_status();
+}

@@ -160,6 +160,8 @@ __host__ __device__ constexpr int chunk_loads(int c) { return (chunk_floats(c) /
 constexpr int kMaxLoads = (kMaxChunkFloats / 4) / kThreads;  // 12
 
 struct State {
+  float* save_row;   // this sample's row of plane 0 of FieldArgs::save (or null)
+  int64_t plane;     // floats between save planes
   floatx16 act[8];   // layer input (B operands), 256 features x 32 samples
   floatx16 acc[9];   // layer output accumulators
   floatx16 denc;     // view-direction encoding (14 k-steps of layer_dir1)
@@ -280,6 +282,22 @@ __device__ __forceinline__ void put_act(State& s, const float* v) {
   for (int t = 0; t < N; ++t) s.act[t >> 4][t & 15] = v[t];
 }
 
+// Training mode: the layer's post-activation outputs, row-major (m, 256) per layer.
+template <int L>
+__device__ __forceinline__ void save_layer(const State& s) {
+  if constexpr (L != kRgb) {
+    if (s.save_row) {
+      float* dst = s.save_row + L * s.plane;
+#pragma unroll
+      for (int ob = 0; ob < 8; ++ob)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          *reinterpret_cast<float4*>(dst + 32 * ob + 8 * q + 4 * s.h) =
+              make_float4(s.act[ob][4 * q], s.act[ob][4 * q + 1], s.act[ob][4 * q + 2], s.act[ob][4 * q + 3]);
+    }
+  }
+}
+
 template <int L>
 __device__ __forceinline__ void finish_layer(State& s) {
   if constexpr (L == kOut) {
@@ -310,7 +328,10 @@ __device__ __forceinline__ void run_chunks(State& s, const FieldArgs& a, float* 
     }
     mfma_steps<C, 0>(s, cur);
     constexpr bool last_of_layer = (C + 1 == kNumChunks) || chunk_at(C + 1).layer != ch.layer;
-    if constexpr (last_of_layer) finish_layer<ch.layer>(s);
+    if constexpr (last_of_layer) {
+      finish_layer<ch.layer>(s);
+      save_layer<ch.layer>(s);
+    }
     if constexpr (C + 1 < kNumChunks) {
       store_chunk<C + 1>(s, nxt);
       __syncthreads();
@@ -329,6 +350,8 @@ __global__ __launch_bounds__(kThreads, 1) void field_kernel(FieldArgs a) {
   const int64_t row = (int64_t)blockIdx.x * kTile + wave * 32 + (s.lane & 31);
   const bool valid = row < a.m;
   const int64_t rc = valid ? row : a.m - 1;
+  s.save_row = (a.save && valid) ? a.save + row * 256 : nullptr;
+  s.plane = a.m * 256;
 
   // ---- per-sample inputs
   const SampleIn in = decode_sample<MODE>(a, rc);
@@ -467,4 +490,52 @@ extern "C" int cn_radiance_field(const float* packed, int fmt, const float* code
   for (int i = 0; i < 4; ++i) a.fd[i] = freqs_dir[i];
   a.raw = raw;
   return launch_field(fmt, pts ? kFromPts : kFromRayZ, a, cn::as_stream(stream));
+}
+
+extern "C" int cn_radiance_field_train(const float* packed, const float* code_bias, const int64_t* code_index,
+                                       int64_t n_codes, const float* pts, const float* ro, const float* rd,
+                                       const float* z, int64_t n_rays, int64_t n_samples, int64_t chunk_rows,
+                                       const float* freqs_xyz, const float* freqs_dir, float* raw, float* save,
+                                       cn_stream_t stream) {
+  CN_CHECK_ARG(packed && code_bias && rd && raw && save && freqs_xyz && freqs_dir);
+  CN_CHECK_ARG(n_rays > 0 && n_samples > 0 && chunk_rows > 0 && n_codes > 0);
+  CN_CHECK_ARG(pts || (ro && z));
+  CN_CHECK_ARG(code_index || n_codes == 1 || n_codes == n_rays);
+  FieldArgs a = {};
+  a.packed = packed;
+  a.code_bias = code_bias;
+  a.code_index = code_index;
+  a.n_codes = n_codes;
+  a.pts = pts;
+  a.ro = ro;
+  a.rd = rd;
+  a.z = z;
+  a.n_rays = n_rays;
+  a.n_samples = n_samples;
+  a.chunk_rows = chunk_rows;
+  a.m = n_rays * n_samples;
+  CN_CHECK_ARG(cn::ceil_div(a.m, kTile) <= 0x7fffffff);
+  for (int i = 0; i < 10; ++i) a.fx[i] = freqs_xyz[i];
+  for (int i = 0; i < 4; ++i) a.fd[i] = freqs_dir[i];
+  a.raw = raw;
+  a.save = save;
+  return launch_field(CN_FMT_F32, pts ? kFromPts : kFromRayZ, a, cn::as_stream(stream));
+}
+
+extern "C" int cn_mlp_forward_train(const float* packed, const float* code_bias, const int64_t* code_index,
+                                    int64_t n_codes, const float* x, int64_t m, float* raw, float* save,
+                                    cn_stream_t stream) {
+  CN_CHECK_ARG(packed && code_bias && x && raw && save && m > 0 && n_codes > 0);
+  CN_CHECK_ARG(code_index || n_codes == 1 || n_codes == m);
+  CN_CHECK_ARG(cn::ceil_div(m, kTile) <= 0x7fffffff);
+  FieldArgs a = {};
+  a.packed = packed;
+  a.code_bias = code_bias;
+  a.code_index = code_index;
+  a.n_codes = n_codes;
+  a.x = x;
+  a.m = m;
+  a.raw = raw;
+  a.save = save;
+  return launch_field(CN_FMT_F32, kFromEncoded, a, cn::as_stream(stream));
 }

@@ -36,6 +36,7 @@ struct FieldArgs {
   float fx[10];
   float fd[4];
   float* raw;
+  float* save;  // fp32 kernel only: (5, m, 256) post-activation h1, h2, feat, v1, v2 for the backward
 };
 
 // One sample's inputs: point, unit Q1 view direction, code row.

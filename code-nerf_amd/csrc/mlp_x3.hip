@@ -140,6 +140,7 @@ struct State {
   float sigma;
   int lane, h, wave;
   int crow;               // this lane's code-bias row
+  bool uniform_code;      // all 32 samples of the wave use one code row
   float vd[3];
 };
 
@@ -178,61 +179,103 @@ __device__ __forceinline__ void chunk_barrier() {
 #endif
 }
 
-// acc[ob][r] = bias[acc_row(ob, r, h)] where `take`, from a wave-uniform bias
-// vector read with scalar loads (lgkmcnt: the ring's vmcnt count is untouched).
-__device__ __forceinline__ void bias_blocks(State& s, const float* ub, bool take) {
-  const_fptr cp = (const_fptr)ub;
-#pragma unroll
-  for (int ob = 0; ob < 8; ++ob) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float v0 = cp[acc_row(ob, r, 0)], v1 = cp[acc_row(ob, r, 1)];
-      const float v = s.h ? v1 : v0;
-      s.acc[ob][r] = take ? v : s.acc[ob][r];
-    }
-  }
+// Biases.  acc starts as b (1 x 32 rows) via ONE MFMA per output block: A holds
+// {bf16(b_i), bf16(b_i - hi)} at k = 0, 1 (lane half 0), B holds ones at k = 0, 1
+// for every sample, so D = hi + lo in fp32.  The bias vectors sit in LDS after the
+// ring (constants + each wave's code row, staged before the DMA stream) and are
+// read by inline-asm ds_reads: hipcc cannot prove them disjoint from the in-flight
+// DMA and would otherwise wait vmcnt(0), draining the ring.  A wave whose samples
+// use several code rows takes per-lane vector loads instead (slow path, rare:
+// S < 32 with per-ray codes).
+constexpr int kBiasLds = 768 + kWaves * kCbStride;
+
+__device__ __forceinline__ unsigned lds_addr(const float* p) {
+  return static_cast<unsigned>(reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) void*)p));
 }
 
-// Bias-initialised accumulators for layer `layer` (runtime, wave-uniform).
-// Per-code biases loop over the distinct code rows of the wave (one pass when
-// all 32 samples share an object).
-__device__ __forceinline__ void init_acc(State& s, const FieldArgs& a, int layer) {
+// 8 floats at p + 32*ob (ob = 0..7), one LDS round trip, invisible to hipcc's waitcnt pass.
+__device__ __forceinline__ void lds_read8_stride32(const float* p, float* v) {
+  asm volatile(
+      "ds_read_b32 %0, %8\n\tds_read_b32 %1, %8 offset:128\n\tds_read_b32 %2, %8 offset:256\n\t"
+      "ds_read_b32 %3, %8 offset:384\n\tds_read_b32 %4, %8 offset:512\n\tds_read_b32 %5, %8 offset:640\n\t"
+      "ds_read_b32 %6, %8 offset:768\n\tds_read_b32 %7, %8 offset:896\n\ts_waitcnt lgkmcnt(0)"
+      : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7])
+      : "v"(lds_addr(p))
+      : "memory");
+}
+
+__device__ __forceinline__ float lds_read1(const float* p) {
+  float v;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(v) : "v"(lds_addr(p)) : "memory");
+  return v;
+}
+
+__device__ __forceinline__ void bias_mfma(floatx16& acc, float v, bf16x8 one) {
+  bf16x8 f = {};
+  const __bf16 hi = static_cast<__bf16>(v);
+  f[0] = hi;
+  f[1] = static_cast<__bf16>(v - static_cast<float>(hi));
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f, one, floatx16{0}, 0, 0, 0);
+}
+
+__device__ __forceinline__ void init_acc(State& s, const FieldArgs& a, const float* blds, int layer) {
+#ifdef CN_ABLATE_NO_BIAS
 #pragma unroll
   for (int ob = 0; ob < 9; ++ob) s.acc[ob] = floatx16{0};
-#ifdef CN_ABLATE_NO_BIAS
   return;
 #endif
   const bool per_code = (layer == kXyz2 || layer == kOut || layer == kRgb);
-  const int off = !per_code ? (layer == kXyz1 ? kBiasXyz1 : (layer == kDir1 ? kBiasDir1 : kBiasDir2))
-                            : (layer == kXyz2 ? kCbXyz2 : (layer == kOut ? kCbFeat : kCbRgb));
-  unsigned long long todo = ~0ull;
-  while (todo) {
-    const float* base;
-    bool mine = true;
-    if (!per_code) {
-      base = a.packed + off;
-    } else {
-      const int row = __builtin_amdgcn_readfirstlane(__shfl(s.crow, __builtin_ctzll(todo)));
-      mine = (s.crow == row);
-      base = a.code_bias + (int64_t)row * kCbStride + off;
+  const int i = s.lane & 31;
+  if (!per_code || s.uniform_code) {
+    bf16x8 one = {};
+    if (s.h == 0) {
+      one[0] = static_cast<__bf16>(1.0f);
+      one[1] = static_cast<__bf16>(1.0f);
     }
+    const float* src = per_code ? blds + 768 + s.wave * kCbStride
+                                : blds + (layer == kXyz1 ? 0 : (layer == kDir1 ? 256 : 512));
     if (layer == kRgb) {
-      const_fptr cp = (const_fptr)base;
-      const float b0 = cp[0], b1 = cp[1], b2 = cp[2];
-      if (mine && s.h == 0) {
-        s.acc[0][0] = b0;
-        s.acc[0][1] = b1;
-        s.acc[0][2] = b2;
-      }
-    } else {
-      bias_blocks(s, base, mine);
-      if (layer == kOut) {
-        const float sg = ((const_fptr)(base + (kCbSigma - kCbFeat)))[0];
-        if (mine && s.h == 0) s.acc[8][0] = sg;
+      const float v = lds_read1(src + kCbRgb + (i < 3 ? i : 0));
+      bias_mfma(s.acc[0], (s.h == 0 && i < 3) ? v : 0.0f, one);
+      return;
+    }
+    const int off = per_code ? (layer == kXyz2 ? kCbXyz2 : kCbFeat) : 0;
+    float v[8];
+    lds_read8_stride32(src + off + i, v);
+#pragma unroll
+    for (int ob = 0; ob < 8; ++ob) bias_mfma(s.acc[ob], s.h == 0 ? v[ob] : 0.0f, one);
+    if (layer == kOut) {
+      const float sg = lds_read1(src + kCbSigma);
+      bias_mfma(s.acc[8], (s.h == 0 && i == 0) ? sg : 0.0f, one);
+    }
+    return;
+  }
+  // slow path: per-lane code rows
+  const float* base = a.code_bias + (int64_t)s.crow * kCbStride;
+#pragma unroll
+  for (int ob = 0; ob < 9; ++ob) s.acc[ob] = floatx16{0};
+  if (layer == kRgb) {
+    if (s.h == 0) {
+      s.acc[0][0] = base[kCbRgb];
+      s.acc[0][1] = base[kCbRgb + 1];
+      s.acc[0][2] = base[kCbRgb + 2];
+    }
+  } else {
+    const float* b = base + (layer == kXyz2 ? kCbXyz2 : kCbFeat);
+#pragma unroll
+    for (int ob = 0; ob < 8; ++ob) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 v = *reinterpret_cast<const float4*>(b + 32 * ob + 8 * q + 4 * s.h);
+        s.acc[ob][4 * q + 0] = v.x;
+        s.acc[ob][4 * q + 1] = v.y;
+        s.acc[ob][4 * q + 2] = v.z;
+        s.acc[ob][4 * q + 3] = v.w;
       }
     }
-    todo &= ~__ballot(mine);
+    if (layer == kOut && s.h == 0) s.acc[8][0] = base[kCbSigma];
   }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): nothing pending leaks past the branch
 }
 
 // A fragments of slot blocks [J0, J0+3) of k-step T of the chunk in `slot`.
@@ -313,7 +356,10 @@ __device__ __forceinline__ void finish_layer(State& s, bool relu) {
     for (int sp = 0; sp < 2; ++sp) {
       float v[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = fmaxf(s.acc[b][8 * sp + j], lo);
+      for (int j = 0; j < 8; ++j) {
+        const float x = s.acc[b][8 * sp + j];
+        asm("v_max_f32 %0, %1, %2" : "=v"(v[j]) : "v"(x), "v"(lo));
+      }
       split8(v, s.bh[2 * b + sp], s.bl[2 * b + sp]);
     }
   }
@@ -321,7 +367,10 @@ __device__ __forceinline__ void finish_layer(State& s, bool relu) {
 
 template <int MODE>
 __global__ __launch_bounds__(kThreads, 1) void field_x3_kernel(FieldArgs a) {
-  __shared__ __attribute__((aligned(16))) float4 lds[kLdsQuads];  // the ONE LDS object
+  // ONE LDS object (a second one makes hipcc wait vmcnt(0) before every ring read):
+  // the DMA ring, then the bias vectors
+  __shared__ __attribute__((aligned(16))) float4 lds[kLdsQuads + kBiasLds / 4];
+  float* blds = reinterpret_cast<float*>(lds + kLdsQuads);
   State s;
   s.lane = threadIdx.x & 63;
   s.h = s.lane >> 5;
@@ -350,6 +399,16 @@ __global__ __launch_bounds__(kThreads, 1) void field_x3_kernel(FieldArgs a) {
 #pragma unroll
   for (int k = 0; k < 4; ++k) split8(enc + 8 * k, s.bh[k], s.bl[k]);
   s.crow = static_cast<int>(code_row(a, in.code_of));
+  const int crow0 = __builtin_amdgcn_readfirstlane(s.crow);
+  // wave-uniform by construction; readfirstlane makes it an SGPR so the bias
+  // fast/slow choice is a scalar branch (a VGPR bool would run both paths masked)
+  s.uniform_code = __builtin_amdgcn_readfirstlane(__ballot(s.crow != crow0) == 0 ? 1 : 0) != 0;
+  for (int j = threadIdx.x; j < 768; j += kThreads) blds[j] = a.packed[kBiasXyz1 + j];
+  if (s.uniform_code) {
+    const float* src = a.code_bias + (int64_t)crow0 * kCbStride;
+    for (int j = s.lane; j < kCbStride; j += 64) blds[768 + s.wave * kCbStride + j] = src[j];
+  }
+  __syncthreads();
 
   // every input load has landed (an s_waitcnt the compiler sees, so nothing stale
   // is tracked into the DMA stream); prime the ring with chunks 0..2
@@ -360,14 +419,14 @@ __global__ __launch_bounds__(kThreads, 1) void field_x3_kernel(FieldArgs a) {
   int c = 0;
 
   // ---- layer_xyz1 (63 -> 256): 4 k-steps of encoding
-  init_acc(s, a, kXyz1);
+  init_acc(s, a, blds, kXyz1);
   run_chunk(s, a, lds, c, s.bh[0], s.bl[0], s.bh[1], s.bl[1], false);
   run_chunk(s, a, lds, c, s.bh[2], s.bl[2], s.bh[3], s.bl[3], false);
   finish_layer(s, true);
 
   // ---- layer_xyz2, fc_out, layer_dir1 (feature part), layer_dir2: one loop body
   for (int layer = kXyz2; layer <= kDir2; ++layer) {
-    init_acc(s, a, layer);
+    init_acc(s, a, blds, layer);
     const bool with9 = (layer == kOut);
 #pragma unroll
     for (int k = 0; k < 16; k += 2) run_chunk(s, a, lds, c, s.bh[k], s.bl[k], s.bh[k + 1], s.bl[k + 1], with9);
@@ -388,7 +447,7 @@ __global__ __launch_bounds__(kThreads, 1) void field_x3_kernel(FieldArgs a) {
   }
 
   // ---- fc_rgb (256 -> 3): one chunk holding its 16 k-steps of block 0
-  init_acc(s, a, kRgb);
+  init_acc(s, a, blds, kRgb);
   chunk_barrier();
   {
     const float4* slot = lds + (c & (kSlots - 1)) * kChunkQuads;

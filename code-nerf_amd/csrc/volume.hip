@@ -119,3 +119,150 @@ extern "C" int cn_volume_render(const float* raw, const float* z, const float* r
                      disp, acc, weights, depth);
   return cn::launch_status();
 }
+
+// ---------------------------------------------------------------- backward
+// Gradient of volume_render (volumetric_render.py:36-66) w.r.t. raw and rd.
+// With sd_i = sigma_i delta_i, T_i = exp(-sum_{j<i} sd_j), w_i = (1 - e^{-sd_i}) T_i:
+//   G_i = g_w_i + g_rgb . c_i + g_depth z_i + g_acc          (dL/dw_i)
+//   dL/dsd_i = G_i T_i e^{-sd_i} - sum_{j>i} G_j w_j          (reverse wave scan)
+//   d raw_i[0:3] = w_i g_rgb 1.002 s(1-s);  d raw_i[3] = dL/dsd_i delta_i softplus'(raw_i[3]-1)
+//   d rd = (sum_i dL/dsd_i sigma_i dist_i) rd/|rd|
+// g_disp folds into g_depth / g_acc through disp = 1/max(1e-10, depth/acc).
+// z is never differentiated (the reference detaches its samples).
+namespace {
+
+__device__ __forceinline__ float wave_sum_f(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+__device__ __forceinline__ float wave_exclusive_suffix(float v, int lane) {
+  float incl = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const float o = __shfl_down(incl, off);
+    if (lane + off < 64) incl += o;
+  }
+  return incl - v;
+}
+
+__global__ __launch_bounds__(256) void volume_render_backward_kernel(
+    const float* __restrict__ raw, const float* __restrict__ z, const float* __restrict__ rd,
+    int64_t n_rays, int S_in, const float* __restrict__ g_rgb, const float* __restrict__ g_disp,
+    const float* __restrict__ g_acc, const float* __restrict__ g_w, const float* __restrict__ g_depth,
+    float* __restrict__ d_raw, float* __restrict__ d_rd) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = blockIdx.x * (int64_t)kRaysPerBlock + (threadIdx.x >> 6);
+  if (r >= n_rays) return;
+  const int S = S_in == 1 ? 0 : S_in;  // see the forward: S == 1 has no contributing sample
+  const int run = (S_in + 63) / 64;
+  const int j0 = lane * run;
+  const float* zr = z + r * S_in;
+  const float4* rr = reinterpret_cast<const float4*>(raw) + r * S_in;
+  float4* dr = reinterpret_cast<float4*>(d_raw) + r * S_in;
+  const float d0 = rd[3 * r], d1 = rd[3 * r + 1], d2 = rd[3 * r + 2];
+  const float nrm = __fsqrt_rn(__fadd_rn(__fadd_rn(__fmul_rn(d0, d0), __fmul_rn(d1, d1)), __fmul_rn(d2, d2)));
+
+  float sd[kMaxRun], zz[kMaxRun], dist[kMaxRun], sig[kMaxRun], w[kMaxRun], tr[kMaxRun];
+  float4 rv[kMaxRun];
+  double run_sum = 0.0;
+#pragma unroll
+  for (int i = 0; i < kMaxRun; ++i) {
+    const int j = j0 + i;
+    sd[i] = 0.0f;
+    if (i < run && j < S) {
+      zz[i] = zr[j];
+      rv[i] = rr[j];
+      dist[i] = (j + 1 < S) ? __fsub_rn(zr[j + 1], zz[i]) : 1e10f;
+      sig[i] = cn::softplus20(__fsub_rn(rv[i].w, 1.0f));
+      sd[i] = __fmul_rn(sig[i], __fmul_rn(dist[i], nrm));
+      if (j + 1 < S) run_sum += static_cast<double>(sd[i]);
+    }
+  }
+  double prefix = wave_exclusive_scan(run_sum, lane);
+  float dep = 0.f, ac = 0.f;
+#pragma unroll
+  for (int i = 0; i < kMaxRun; ++i) {
+    const int j = j0 + i;
+    w[i] = 0.0f;
+    tr[i] = 0.0f;
+    if (i < run && j < S) {
+      tr[i] = expf(-static_cast<float>(prefix));
+      w[i] = __fmul_rn(__fsub_rn(1.0f, expf(-sd[i])), tr[i]);
+      dep += w[i] * zz[i];
+      ac += w[i];
+      if (j + 1 < S) prefix += static_cast<double>(sd[i]);
+    }
+  }
+  dep = wave_sum_f(dep);
+  ac = wave_sum_f(ac);
+  const float gr0 = g_rgb ? g_rgb[3 * r] : 0.f, gr1 = g_rgb ? g_rgb[3 * r + 1] : 0.f;
+  const float gr2 = g_rgb ? g_rgb[3 * r + 2] : 0.f;
+  float gdep = g_depth ? g_depth[r] : 0.f, gacc = g_acc ? g_acc[r] : 0.f;
+  if (g_disp) {
+    const float q = dep / ac;
+    if (q > 1e-10f) {  // d(1/q)/dq = -1/q^2; below the clamp torch routes the gradient to the constant
+      const float gq = -g_disp[r] / (q * q);
+      gdep += gq / ac;
+      gacc += gq * (-dep / (ac * ac));
+    }
+  }
+  // G_i and the per-sample colour gradients
+  float G[kMaxRun], gw_run = 0.f;
+#pragma unroll
+  for (int i = 0; i < kMaxRun; ++i) {
+    const int j = j0 + i;
+    G[i] = 0.0f;
+    if (i < run && j < S) {
+      const float s0 = cn::sigmoidf_(rv[i].x), s1 = cn::sigmoidf_(rv[i].y), s2 = cn::sigmoidf_(rv[i].z);
+      const float c0 = s0 * 1.002f - 0.001f, c1 = s1 * 1.002f - 0.001f, c2 = s2 * 1.002f - 0.001f;
+      G[i] = gr0 * c0 + gr1 * c1 + gr2 * c2 + gdep * zz[i] + gacc + (g_w ? g_w[r * S_in + j] : 0.f);
+      rv[i].x = w[i] * gr0 * 1.002f * s0 * (1.0f - s0);  // reuse rv for d_raw[0:3]
+      rv[i].y = w[i] * gr1 * 1.002f * s1 * (1.0f - s1);
+      rv[i].z = w[i] * gr2 * 1.002f * s2 * (1.0f - s2);
+      gw_run += G[i] * w[i];
+    }
+  }
+  float suffix = wave_exclusive_suffix(gw_run, lane);  // sum of G_j w_j over later lanes' runs
+  float gnorm = 0.f;
+#pragma unroll
+  for (int i = kMaxRun - 1; i >= 0; --i) {
+    const int j = j0 + i;
+    if (i < run && j < S) {
+      const float dsd = G[i] * tr[i] * expf(-sd[i]) - suffix;
+      suffix += G[i] * w[i];
+      const float x = rv[i].w - 1.0f;
+      const float dsp = x > 20.0f ? 1.0f : cn::sigmoidf_(x);
+      float4 o = rv[i];
+      o.w = dsd * (dist[i] * nrm) * dsp;
+      dr[j] = o;
+      gnorm += dsd * sig[i] * dist[i];
+    } else if (i < run && j < S_in) {
+      dr[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  gnorm = wave_sum_f(gnorm);
+  if (lane == 0 && d_rd) {
+    const float inv = nrm > 0.f ? gnorm / nrm : 0.f;
+    d_rd[3 * r] = inv * d0;
+    d_rd[3 * r + 1] = inv * d1;
+    d_rd[3 * r + 2] = inv * d2;
+  }
+}
+
+}  // namespace
+
+extern "C" int cn_volume_render_backward(const float* raw, const float* z, const float* rd,
+                                         int64_t n_rays, int64_t n_samples, const float* g_rgb,
+                                         const float* g_disp, const float* g_acc,
+                                         const float* g_weights, const float* g_depth,
+                                         float* d_raw, float* d_rd, cn_stream_t stream) {
+  CN_CHECK_ARG(raw && z && rd && d_raw);
+  CN_CHECK_ARG(n_rays > 0 && n_samples > 0 && n_samples <= 64 * kMaxRun);
+  const unsigned grid = static_cast<unsigned>(cn::ceil_div(n_rays, kRaysPerBlock));
+  hipLaunchKernelGGL(volume_render_backward_kernel, dim3(grid), dim3(64 * kRaysPerBlock), 0,
+                     cn::as_stream(stream), raw, z, rd, n_rays, static_cast<int>(n_samples), g_rgb,
+                     g_disp, g_acc, g_weights, g_depth, d_raw, d_rd);
+  return cn::launch_status();
+}

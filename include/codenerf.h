@@ -154,6 +154,101 @@ int cn_radiance_field(const float* packed, int fmt, const float* code_bias, cons
                       const float* freqs_xyz, const float* freqs_dir, float* raw,
                       cn_stream_t stream);
 
+/* --- Backward (autograd through the eval / train step) ------------------
+ * The gradients loss.backward() takes through the path in the reference's
+ * test-time optimisation (view_synthesis/eval.py) and training step:
+ * pose -> get_bundle -> sample -> sample_uniform / sample_pdf (depths
+ * detached, point_sampler.py:115) -> forward_pass -> CodeNeRFModel.forward
+ * -> volume_render.  All fp32. */
+
+/* cn_radiance_field in fp32 that also stores the post-activation hidden rows
+ * the backward needs: save = (5, M, 256) planes h1, h2, feat, v1, v2 with
+ * M = n_rays * n_samples (layer_xyz1, layer_xyz2, fc_out[1:], layer_dir1,
+ * layer_dir2 of model.py:179-191).  packed must be an fp32 (CN_FMT_F32) pack. */
+int cn_radiance_field_train(const float* packed, const float* code_bias, const int64_t* code_index,
+                            int64_t n_codes, const float* pts, const float* ro, const float* rd,
+                            const float* z, int64_t n_rays, int64_t n_samples, int64_t chunk_rows,
+                            const float* freqs_xyz, const float* freqs_dir, float* raw, float* save,
+                            cn_stream_t stream);
+
+/* cn_mlp_forward in fp32 that also stores the (5, m, 256) activations (as above). */
+int cn_mlp_forward_train(const float* packed, const float* code_bias, const int64_t* code_index,
+                         int64_t n_codes, const float* x, int64_t m, float* raw, float* save,
+                         cn_stream_t stream);
+
+/* The (M, 90) rows forward_pass hands CodeNeRFModel.forward (nerf/__init__.py:116-132):
+ * [posenc(pts) 63 | posenc(Q1 view dir) 27].  pts, or ro + z. */
+int cn_encode_inputs(const float* pts, const float* ro, const float* rd, const float* z, int64_t n_rays,
+                     int64_t n_samples, int64_t chunk_rows, const float* freqs_xyz, const float* freqs_dir,
+                     float* x, cn_stream_t stream);
+
+/* Floats of scratch cn_field_backward needs for M sample rows. */
+int64_t cn_field_backward_workspace_floats(int64_t m);
+
+/* Backward of forward_pass + CodeNeRFModel.forward (model.py:160-194) from
+ * d_raw (M, 4).  saved / x_enc from cn_radiance_field_train / cn_encode_inputs.
+ * grads: 18 pointers (model.py parameter order, same as params) ACCUMULATED
+ * into (+=), or NULL for no parameter gradients; the code-layer parameters
+ * (shape/texture_code_layer*) and the code halves of layer_xyz2 / fc_out /
+ * fc_rgb get their gradients from cn_code_bias_backward instead.
+ * g_code: (n_codes, CN_CODE_BIAS_STRIDE) accumulated gradient of the
+ * per-object code terms (cn_code_bias layout), or NULL.
+ * d_pts (M, 3) is written when the inputs were pts; d_ro / d_rd (n_rays, 3) are
+ * ACCUMULATED into (view-direction and, for ro + z inputs, point gradients).
+ * With d_pts, d_ro and d_rd all NULL, pts / ro / rd / z / freqs may be NULL too
+ * (rows from cn_mlp_forward_train: n_rays = M, n_samples = 1).  On return
+ * workspace[2*257*M, 2*257*M + 90*M) holds dL/dx_enc (M, 90). */
+int cn_field_backward(const float* const* params, const float* saved, const float* x_enc,
+                      const float* d_raw, const float* pts, const float* ro, const float* rd,
+                      const float* z, int64_t n_rays, int64_t n_samples, int64_t chunk_rows,
+                      const int64_t* code_index, int64_t n_codes, const float* freqs_xyz,
+                      const float* freqs_dir, float* workspace, float* const* grads, float* g_code,
+                      float* d_pts, float* d_ro, float* d_rd, cn_stream_t stream);
+
+/* Backward of cn_code_bias (the code layers, model.py:174-177, and the code
+ * halves of layer_xyz2 / fc_out / fc_rgb) from g_code.  dz_s / dz_t (n_codes, 256)
+ * are written (either may be NULL); grads as in cn_field_backward (accumulated). */
+int cn_code_bias_backward(const float* const* params, const float* z_s, const float* z_t, int64_t n_codes,
+                          const float* g_code, float* dz_s, float* dz_t, float* const* grads,
+                          cn_stream_t stream);
+
+/* Backward of volume_render (volumetric_render.py:36-66) w.r.t. raw and rd
+ * (z is detached in the reference).  Any of g_rgb (R,3), g_disp, g_acc, g_depth
+ * (R), g_weights (R,S) may be NULL (zero).  d_raw (R,S,4) and d_rd (R,3, may be
+ * NULL) are written. */
+int cn_volume_render_backward(const float* raw, const float* z, const float* rd, int64_t n_rays,
+                              int64_t n_samples, const float* g_rgb, const float* g_disp,
+                              const float* g_acc, const float* g_weights, const float* g_depth,
+                              float* d_raw, float* d_rd, cn_stream_t stream);
+
+/* Backward of get_bundle (ray_sampler.py:95-98): d_c2w (batch, 4, 4) rows 0..2
+ * ACCUMULATED from g_ro / g_rd (batch*hw, 3), either may be NULL (not both). */
+int cn_ray_bundle_backward(const float* dirs, int64_t hw, int64_t batch, const float* g_ro,
+                           const float* g_rd, float* d_c2w, cn_stream_t stream);
+
+/* Backward of the sample gather (ray_sampler.py:77-80): scatter-add g_ro / g_rd
+ * (batch*sample_size, 3) into d_ro / d_rd (batch*hw, 3). */
+int cn_gather_rays_backward(const float* g_ro, const float* g_rd, int64_t batch, int64_t hw,
+                            const int64_t* select_inds, int64_t sample_size, float* d_ro, float* d_rd,
+                            cn_stream_t stream);
+
+/* Backward of cn_posenc (position_embed.py:35-53): dx (m, d) from g_enc (m, d*(inc + 2*num_freq)). */
+int cn_posenc_backward(const float* x, int64_t m, int64_t d, const float* freqs, int64_t num_freq,
+                       int include_input, const float* g_enc, float* dx, cn_stream_t stream);
+
+/* Backward of cn_ray_points (z detached, point_sampler.py:115): d_ro += sum_s g_pts,
+ * d_rd += sum_s g_pts * z; either output may be NULL (not both). */
+int cn_ray_points_backward(const float* g_pts, const float* z, int64_t n_rays, int64_t n_samples,
+                           float* d_ro, float* d_rd, cn_stream_t stream);
+
+/* fp32 MFMA GEMMs the backward is built from (row-major, leading dims in floats):
+ *   cn_gemm_nn: C[M][N] = A[M][K] B[K][N], zeroed where mask[m][n] <= 0 (mask may be NULL);
+ *   cn_gemm_tn: C[N][K] += sum_m A[M][N] B[M][K] (accumulates). */
+int cn_gemm_nn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
+               const float* mask, int64_t ldm, int64_t M, int64_t N, int64_t K, cn_stream_t stream);
+int cn_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M,
+               int64_t N, int64_t K, cn_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

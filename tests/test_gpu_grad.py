@@ -1,0 +1,319 @@
+"""Backward pass on the HIP kernels vs torch autograd of the oracle.
+
+Every gradient here is computed by the gfx950 backward kernels through the C
+ABI (codenerf.autograd) and compared with ``torch.autograd`` run over the CPU
+oracle (oracle/codenerf_oracle.py, pinned to the reference by
+tests/golden/*.npz) on the same inputs, and against the reference's own eval
+step gradients (tests/golden/eval_grad.npz).
+
+Tolerance: gradients are sums over many samples taken in a different order
+(MFMA tiles, atomics), so they are compared relative to the tensor's largest
+magnitude: max|g - g_ref| <= GRAD_RTOL * max|g_ref| (+1e-7 absolute).
+Forward outputs keep the render tolerance (1e-4 absolute).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+GRAD_RTOL = 2e-4
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import codenerf
+    codenerf.load_library()
+    return torch.device("cuda", 0)
+
+
+def O():
+    import oracle.codenerf_oracle as o
+    return o
+
+
+def close(g, ref, rtol=GRAD_RTOL, what=""):
+    g, ref = torch.as_tensor(g).double().cpu(), torch.as_tensor(ref).double().cpu()
+    assert g.shape == ref.shape, (what, g.shape, ref.shape)
+    scale = ref.abs().max().item() if ref.numel() else 0.0
+    err = (g - ref).abs().max().item() if ref.numel() else 0.0
+    assert err <= rtol * scale + 1e-7, f"{what}: max err {err:.3e} vs scale {scale:.3e}"
+
+
+def model(dev, seed):
+    from codenerf import synthetic
+    from codenerf.models import CodeNeRFModel
+    m = CodeNeRFModel(hidden_size=256, shape_code_size=256, texture_code_size=256, num_encoding_fn_xyz=10,
+                      num_encoding_fn_dir=4)
+    m.load_state_dict(synthetic.codenerf_params(seed))
+    return m.to(dev)
+
+
+def oracle_params(m):
+    return {k: v.detach().cpu().clone().requires_grad_(True) for k, v in m.state_dict().items()}
+
+
+def embedders(dev):
+    from codenerf.nerf import PositionalEmbedder
+    return PositionalEmbedder(10, True, True, torch.float32, dev), PositionalEmbedder(4, True, True, torch.float32, dev)
+
+
+# ---------------------------------------------------------------- GEMM building blocks
+
+
+@pytest.mark.parametrize("m,n,k", [(1000, 257, 283), (64, 3, 256), (4097, 256, 27)])
+def test_gemm_nn_masked(dev, m, n, k):
+    from codenerf import ops
+    g = torch.Generator().manual_seed(m + n + k)
+    a, b = torch.randn(m, k, generator=g), torch.randn(k, n, generator=g)
+    mask = torch.randn(m, n, generator=g)
+    c = ops.gemm_nn(a.to(dev), b.to(dev), mask.to(dev))
+    ref = (a.double() @ b.double()) * (mask > 0)
+    close(c, ref, 1e-5, "gemm_nn")
+
+
+@pytest.mark.parametrize("m,n,k", [(5000, 257, 256), (33, 3, 256), (4096, 256, 63)])
+def test_gemm_tn_accumulates(dev, m, n, k):
+    from codenerf import ops
+    g = torch.Generator().manual_seed(m * 3 + n + k)
+    a, b = torch.randn(m, n, generator=g), torch.randn(m, k, generator=g)
+    c0 = torch.randn(n, k, generator=g)
+    c = ops.gemm_tn(a.to(dev), b.to(dev), c0.to(dev).clone())
+    close(c, c0.double() + a.double().t() @ b.double(), 1e-5, "gemm_tn")
+
+
+# ---------------------------------------------------------------- element-wise stages
+
+
+@pytest.mark.parametrize("s", [2, 7, 24, 64, 129])
+def test_volume_render_backward(dev, s):
+    from codenerf.nerf import volume_render
+    o = O()
+    r = 53
+    g = torch.Generator().manual_seed(s)
+    raw = torch.randn(r, s, 4, generator=g) * 2.0
+    raw[..., 3] += 2.0
+    raw[0, :, 3] = 30.0            # softplus threshold branch
+    z = torch.sort(0.8 + torch.rand(r, s, generator=g), dim=-1).values
+    rd = torch.randn(r, 3, generator=g)
+    wr, wd, wa, wdep = (torch.randn(r, 3, generator=g), torch.randn(r, generator=g), torch.randn(r, generator=g),
+                        torch.randn(r, generator=g))
+    ww = torch.randn(r, s, generator=g)
+
+    def loss(outs):
+        rgb, disp, acc, w, depth = outs
+        dd = wd.to(disp.device)
+        return ((rgb * wr.to(rgb.device)).sum() + 1e-2 * (disp * dd).sum() + (acc * wa.to(acc.device)).sum()
+                + (w * ww.to(w.device)).sum() + (depth * wdep.to(depth.device)).sum())
+
+    raw_c, rd_c = raw.clone().requires_grad_(True), rd.clone().requires_grad_(True)
+    loss(o.volume_render(raw_c, z, rd_c)).backward()
+    raw_g, rd_g = raw.to(dev).requires_grad_(True), rd.to(dev).requires_grad_(True)
+    outs = volume_render(raw_g, z.to(dev), rd_g)
+    loss(outs).backward()
+    close(raw_g.grad, raw_c.grad, what="d raw")
+    close(rd_g.grad, rd_c.grad, what="d rd")
+
+
+def test_posenc_backward(dev):
+    from codenerf.nerf import PositionalEmbedder
+    o = O()
+    x = torch.randn(777, 3) * 1.5
+    gout = torch.randn(777, 63)
+    xc = x.clone().requires_grad_(True)
+    (o.posenc(xc, o.frequency_bands(10, True), True) * gout).sum().backward()
+    xg = x.to(dev).requires_grad_(True)
+    emb = PositionalEmbedder(10, True, True, torch.float32, dev)
+    (emb.embed(xg) * gout.to(dev)).sum().backward()
+    close(xg.grad, xc.grad, 1e-5, "posenc")
+
+
+def test_ray_bundle_gather_points_backward(dev):
+    """get_bundle -> sample gather -> pts = ro + rd z: d c2w (ray_sampler.py:77-99, point_sampler.py:70)."""
+    from codenerf.nerf import RaySampler
+    o = O()
+    from codenerf import synthetic
+    K = synthetic.srn_intrinsics(24, focal=30.0)
+    h = w = 24
+    rs = RaySampler(h, w, K, sample_size=100, device=dev, datatype=torch.float32)
+    c2w = o.pose_spherical(torch.tensor([0.5]), torch.tensor([0.3]), torch.tensor([1.3]))[None]
+    gz = torch.Generator().manual_seed(3)
+    z = torch.sort(0.8 + torch.rand(100, 9, generator=gz), dim=-1).values
+    gp = torch.randn(100, 9, 3, generator=gz)
+    np.random.seed(11)
+    c_g = c2w.to(dev).requires_grad_(True)
+    ro, rd, sel = rs.sample(c_g)
+    from codenerf.nerf import PointSampler  # noqa: F401
+    from codenerf.autograd import sample_points_autograd
+    pts = sample_points_autograd(ro, rd, z.to(dev))
+    ((pts * gp.to(dev)).sum() + (rd * 0.5).sum()).backward()
+    c_c = c2w.clone().requires_grad_(True)
+    dirs = o.ray_directions(h, w, K)
+    ro_c, rd_c = o.ray_bundle(dirs, c_c)
+    ro_c, rd_c = o.gather_rays(ro_c, rd_c, sel)
+    pts_c = ro_c[:, None, :] + rd_c[:, None, :] * z[..., None]
+    ((pts_c * gp).sum() + (rd_c * 0.5).sum()).backward()
+    close(c_g.grad, c_c.grad, 1e-5, "d c2w")
+
+
+# ---------------------------------------------------------------- field (forward_pass + CodeNeRFModel)
+
+
+def _oracle_field(o, p, rd, pts, zs, zt, chunk):
+    emb = o.EmbedCfg()
+    outs = []
+    for c0 in range(0, rd.shape[0], chunk):
+        sl = slice(c0, min(c0 + chunk, rd.shape[0]))
+        outs.append(o.forward_pass(p, emb, rd[sl], pts[sl], zs[sl], zt[sl]))
+    return torch.cat(outs)
+
+
+@pytest.mark.parametrize("mode,r,s,chunk,per_ray_codes", [
+    ("rayz", 37, 16, 13, False),
+    ("pts", 37, 16, 37, False),
+    ("rayz", 20, 9, 20, True),
+    ("rayz", 300, 64, 128, False),
+])
+def test_field_backward(dev, mode, r, s, chunk, per_ray_codes):
+    from codenerf import nerf, synthetic
+    o = O()
+    m = model(dev, 0)
+    p = oracle_params(m)
+    g = torch.Generator().manual_seed(r * s)
+    ro = torch.randn(r, 3, generator=g) * 0.3 + torch.tensor([0.0, 0.0, 1.3])
+    rd = torch.randn(r, 3, generator=g)
+    z = torch.sort(0.8 + torch.rand(r, s, generator=g), dim=-1).values
+    if per_ray_codes:
+        zs, zt = torch.randn(r, 256, generator=g) * 0.3, torch.randn(r, 256, generator=g) * 0.3
+    else:
+        zs, zt = synthetic.latent_codes(5, 1), synthetic.latent_codes(6, 1)
+    gout = torch.randn(r, s, 4, generator=g)
+
+    # oracle
+    ro_c, rd_c = ro.clone().requires_grad_(True), rd.clone().requires_grad_(True)
+    zs_c, zt_c = zs.clone().requires_grad_(True), zt.clone().requires_grad_(True)
+    pts_c = ro_c[:, None, :] + rd_c[:, None, :] * z[..., None]
+    zse = zs_c if per_ray_codes else zs_c.expand(r, -1)
+    zte = zt_c if per_ray_codes else zt_c.expand(r, -1)
+    raw_c = _oracle_field(o, p, rd_c, pts_c, zse, zte, chunk)
+    (raw_c * gout).sum().backward()
+
+    # HIP
+    ro_g, rd_g = ro.to(dev).requires_grad_(True), rd.to(dev).requires_grad_(True)
+    zs_g, zt_g = zs.to(dev).requires_grad_(True), zt.to(dev).requires_grad_(True)
+    zsg = zs_g if per_ray_codes else zs_g.expand(r, -1)
+    ztg = zt_g if per_ray_codes else zt_g.expand(r, -1)
+    emb = embedders(dev)
+    if mode == "pts":
+        from codenerf.autograd import sample_points_autograd
+        raw_g = nerf._field(m, emb, rd_g, zsg, ztg, chunk, pts=sample_points_autograd(ro_g, rd_g, z.to(dev)))
+    else:
+        raw_g = nerf._field(m, emb, rd_g, zsg, ztg, chunk, ro=ro_g, z=z.to(dev))
+    (raw_g * gout.to(dev)).sum().backward()
+
+    assert (raw_g.detach().cpu() - raw_c.detach()).abs().max().item() <= 1e-4
+    close(ro_g.grad, ro_c.grad, what="d ro")
+    close(rd_g.grad, rd_c.grad, what="d rd")
+    close(zs_g.grad, zs_c.grad, what="d z_s")
+    close(zt_g.grad, zt_c.grad, what="d z_t")
+    for (name, prm) in m.named_parameters():
+        close(prm.grad, p[name].grad, what=name)
+
+
+@pytest.mark.parametrize("m_rows,dedupe", [(1000, True), (257, False)])
+def test_model_forward_backward(dev, m_rows, dedupe):
+    """CodeNeRFModel(z_s, z_t, x) with grads on x, codes and weights (model.py:160-194)."""
+    o = O()
+    m = model(dev, 1)
+    p = oracle_params(m)
+    g = torch.Generator().manual_seed(m_rows)
+    x = torch.randn(m_rows, 90, generator=g)
+    if dedupe:
+        zs, zt = torch.randn(1, 256, generator=g) * 0.3, torch.randn(1, 256, generator=g) * 0.3
+    else:
+        zs, zt = torch.randn(m_rows, 256, generator=g) * 0.3, torch.randn(m_rows, 256, generator=g) * 0.3
+    gout = torch.randn(m_rows, 4, generator=g)
+    xc, zsc, ztc = [t.clone().requires_grad_(True) for t in (x, zs, zt)]
+    e = (lambda t: t.expand(m_rows, -1)) if dedupe else (lambda t: t)
+    (o.codenerf_mlp(p, e(zsc), e(ztc), xc, 63) * gout).sum().backward()
+    xg, zsg, ztg = [t.to(dev).requires_grad_(True) for t in (x, zs, zt)]
+    raw = m(e(zsg), e(ztg), xg)
+    (raw * gout.to(dev)).sum().backward()
+    close(xg.grad, xc.grad, what="d x")
+    close(zsg.grad, zsc.grad, what="d z_s")
+    close(ztg.grad, ztc.grad, what="d z_t")
+    for (name, prm) in m.named_parameters():
+        close(prm.grad, p[name].grad, what=name)
+
+
+# ---------------------------------------------------------------- the reference's eval step (C5)
+
+
+def test_eval_step_gradients_golden(dev):
+    """eval.py:145-160 through the whole path, vs the reference's own autograd (eval_grad.npz)."""
+    from codenerf import synthetic
+    from codenerf.evaluate import pose_spherical
+    from codenerf.nerf import PointSampler, RaySampler, predict_radiance_and_render
+    gd = {k: torch.from_numpy(v) for k, v in np.load(os.path.join(GOLDEN, "eval_grad.npz")).items()}
+    K = torch.from_numpy(np.load(os.path.join(GOLDEN, "rays_small.npz"))["intrinsics"])
+    models = {"nerf_coarse": model(dev, 0), "nerf_fine": model(dev, 1)}
+    for mm in models.values():
+        mm.train()
+    emb = embedders(dev)
+    ps = PointSampler(8, 8, 0.8, 1.8, spacing_mode="lindepth", perturb=False, dtype=torch.float32, device=dev)
+    rs = RaySampler(12, 16, K, sample_size=64, device=dev, datatype=torch.float32)
+    theta, phi, rho = [gd[k].to(dev).requires_grad_(True) for k in ("theta", "phi", "rho")]
+    zs, zt = gd["z_s"].to(dev).requires_grad_(True), gd["z_t"].to(dev).requires_grad_(True)
+    target = gd["target"].to(dev)
+    np.random.seed(9)
+    c2w = pose_spherical(theta, phi, rho)[None, :]
+    ro, rd, sel = rs.sample(tform_cam2world=c2w)
+    assert np.array_equal(sel, gd["select_inds"].numpy())
+    tp = target[None][..., torch.as_tensor(sel, device=dev), :].squeeze()
+    zse, zte = zs.expand(ro.shape[0], -1), zt.expand(ro.shape[0], -1)
+    rgb_c, rgb_f = predict_radiance_and_render((ro, rd), ps, emb, models["nerf_coarse"], models["nerf_fine"],
+                                               (zse, zte))
+    assert (rgb_c.detach().cpu() - gd["rgb_coarse"]).abs().max().item() <= 1e-4
+    assert (rgb_f.detach().cpu() - gd["rgb_fine"]).abs().max().item() <= 1e-4
+    lc = torch.nn.functional.mse_loss(rgb_c[..., :3], tp[..., :3])
+    lf = torch.nn.functional.mse_loss(rgb_f[..., :3], tp[..., :3])
+    loss = lc + lf + 1e-5 * (torch.norm(zse, p=2) + torch.norm(zte, p=2))
+    loss.backward()
+    assert abs(loss.item() - gd["loss"].item()) <= 1e-5
+    for name, t in [("theta", theta), ("phi", phi), ("rho", rho)]:
+        ref = gd["g_" + name]
+        assert (t.grad.cpu() - ref).abs().max().item() <= 1e-3 * max(1.0, ref.abs().max().item()), name
+    close(zs.grad, gd["g_z_s"], 1e-3, "g_z_s")
+    close(zt.grad, gd["g_z_t"], 1e-3, "g_z_t")
+    close(models["nerf_fine"].fc_rgb.weight.grad, gd["g_fine_fc_rgb_w"], 1e-3, "fine fc_rgb.weight")
+    close(models["nerf_coarse"].fc_out.bias.grad, gd["g_coarse_fc_out_b"], 1e-3, "coarse fc_out.bias")
+    for key, mm in models.items():
+        for n, prm in mm.named_parameters():
+            ref = gd[f"gnorm_{key}.{n}"].item()
+            assert abs(prm.grad.norm().item() - ref) <= 1e-3 * ref + 1e-8, (key, n)
+
+
+def test_test_time_optimize_runs(dev):
+    """A few iterations of the eval loop run end to end on the HIP path and move codes and pose."""
+    from codenerf.evaluate import test_time_optimize
+    from codenerf.nerf import PointSampler, RaySampler
+    K = torch.from_numpy(np.load(os.path.join(GOLDEN, "rays_small.npz"))["intrinsics"])
+    models = {"nerf_coarse": model(dev, 0), "nerf_fine": model(dev, 1)}
+    emb = embedders(dev)
+    ps = PointSampler(8, 8, 0.8, 1.8, spacing_mode="lindepth", perturb=False, dtype=torch.float32, device=dev)
+    rs = RaySampler(12, 16, K, sample_size=64, device=dev, datatype=torch.float32)
+    target = torch.rand(12 * 16, 4, generator=torch.Generator().manual_seed(1)).to(dev)
+    codes = (torch.randn(4, 256) * 0.3, torch.randn(4, 256) * 0.3)
+    np.random.seed(0)
+    zs, zt, (theta, phi, rho), hist = test_time_optimize(target, (rs, ps), emb, models, codes, iterations=6,
+                                                         val_lr=5e-2)
+    assert len(hist) == 6 and np.isfinite([h["total_loss"] for h in hist]).all()
+    assert not torch.allclose(zs.detach().cpu(), codes[0].mean(0, keepdim=True))
+    assert abs(theta.item() - 1.57) > 1e-4 and abs(rho.item() - 1.30) > 1e-4
+    assert all(p.requires_grad for mm in models.values() for p in mm.parameters())
