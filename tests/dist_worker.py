@@ -1,0 +1,75 @@
+"""Worker for tests/test_distributed_cpu.py: one gloo rank of parallel_image_render.
+
+Runs the package's real parallel_image_render (Q5 split, per-rank slice,
+code expand, padded all-gather, trim on rank 0 -- nerf/__init__.py:137-226)
+on CPU.  Only the per-slice renderer underneath is swapped for the oracle's
+chunked predict_radiance_and_render (test infrastructure; no GPU here), so the
+test pins the sharding and the collective, not the kernels.
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+for p in (ROOT, os.path.join(ROOT, "code-nerf_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+class _Cfg(dict):
+    def __getattr__(self, k):
+        return self[k]
+
+
+class _Params(dict):
+    def eval(self):
+        return self
+
+
+def run(rank, world, port, nc, nf, out_path):
+    import codenerf.nerf as N
+    from codenerf import synthetic
+    import oracle.codenerf_oracle as O
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        g = np.load(os.path.join(HERE, "golden", "render_small.npz"))
+        K, pose = torch.from_numpy(g["intrinsics"]), torch.from_numpy(g["pose"])
+        zs, zt = torch.from_numpy(g["z_s"]), torch.from_numpy(g["z_t"])
+        smp, emb = O.Sampling(nc, nf, 0.8, 1.8), O.EmbedCfg()
+        models = {"nerf_coarse": _Params(synthetic.codenerf_params(0)),
+                  "nerf_fine": _Params(synthetic.codenerf_params(1))}
+        seen = {}
+
+        class Rays:
+            def get_bundle(self, tform_cam2world):
+                return O.ray_bundle(O.ray_directions(12, 16, K), tform_cam2world)
+
+        def oracle_render_rays(ro, rd, z_s, z_t, point_sampler, embedders, coarse, fine, chunk_rows=None,
+                               coarse_only=False, **_):
+            seen["rows"] = ro.shape[0]
+            outs = {}
+            for c0 in range(0, ro.shape[0], chunk_rows):
+                sl = slice(c0, min(c0 + chunk_rows, ro.shape[0]))
+                o = O.predict_radiance_and_render(ro[sl], rd[sl], smp, emb, coarse, fine, z_s[sl], z_t[sl],
+                                                  coarse_only=coarse_only)
+                for k, v in o.items():
+                    outs.setdefault(k, []).append(v)
+            return {k: torch.cat(v) for k, v in outs.items()}
+
+        N.render_rays = oracle_render_rays
+        cfg = _Cfg(is_distributed=True, gpus=world, nerf=_Cfg(validation=_Cfg(chunksize=50)))
+        rgb = N.parallel_image_render(cfg, pose, [zs, zt], models, (Rays(), None), (None, None), "cpu")
+        rows = torch.tensor([seen["rows"]])
+        all_rows = [torch.zeros_like(rows) for _ in range(world)]
+        dist.all_gather(all_rows, rows)
+        if rank == 0:
+            np.savez(out_path, rgb=rgb.numpy(), rows=torch.cat(all_rows).numpy())
+        else:
+            assert rgb is None
+    finally:
+        dist.destroy_process_group()
