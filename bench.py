@@ -5,7 +5,11 @@
 One step renders N full 128x128 images (16384 rays each, 64 coarse samples per
 ray, srn-cars-code near 0.8 / far 1.8, lindepth, 4096-ray chunks) through the
 gfx950 path: ray bundle -> per-object code terms -> depths -> fused
-encode+MLP field kernel (fp32 MFMA) -> compositing.  With N ranks every image
+encode+MLP field kernel -> compositing.  The field kernel runs the
+3xbf16 split (Wh.Xh + Wh.Xl + Wl.Xh on bf16 MFMA, fp32 accumulation; fp32-level
+accuracy, parity-tested at the same 1e-4 as the fp32 kernel) by default;
+``--precision f32`` selects the exact-product fp32 MFMA kernel, which is also
+timed beside it and reported under ``f32_kernel``.  With N ranks every image
 is split over the ranks exactly like the reference's parallel_image_render
 (nerf/__init__.py:179-218) and the rendered pixels are all-gathered to rank 0
 over RCCL; per-rank work is fixed (16384 rays), so scaling is weak.
@@ -42,6 +46,10 @@ NEAR, FAR = 0.8, 1.8
 CHUNK = 4096
 FLOP_PER_SAMPLE = 572_416          # hoisted CodeNeRF MLP per sample-evaluation
 PEAK_FP32_MFMA_TFLOPS = 157.3      # MI355X dense fp32 matrix peak (MI355X_MICROARCH.md)
+PEAK_BF16_MFMA_TFLOPS = 2516.6     # MI355X dense bf16 matrix peak (guide: ~2.5 PF dense)
+KERNELS = {"f32": ("field_kernel<kFromRayZ> (fused posenc + CodeNeRF MLP, fp32 MFMA)", 1, PEAK_FP32_MFMA_TFLOPS),
+           "bf16x3": ("field_x3_kernel<kFromRayZ> (fused posenc + CodeNeRF MLP, 3xbf16 MFMA)", 3,
+                      PEAK_BF16_MFMA_TFLOPS)}
 
 
 def pose(theta, phi, rho):
@@ -63,6 +71,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--hierarchical", action="store_true", help="also time the 64+64 (C3) render")
+    ap.add_argument("--precision", default="bf16x3", choices=sorted(KERNELS))
+    ap.add_argument("--no-f32-compare", action="store_true", help="skip the fp32-kernel side measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -90,6 +100,7 @@ def main():
     for seed in (0, 1):
         m = CodeNeRFModel(256, 1, 256, 256, 10, 4)
         m.load_state_dict(synthetic.codenerf_params(seed))
+        m.precision = args.precision
         models.append(m.to(dev).eval())
     zs = synthetic.latent_codes(5, 1).to(dev)
     zt = synthetic.latent_codes(6, 1).to(dev)
@@ -151,9 +162,23 @@ def main():
     field_avg_ms = sum(field_ms) / max(1, len(field_ms))
     samples_per_launch = rays_per_rank * NC
     flop_per_launch = samples_per_launch * FLOP_PER_SAMPLE
-    achieved_tf = flop_per_launch / (field_avg_ms * 1e-3) / 1e12
+    algo_tf = flop_per_launch / (field_avg_ms * 1e-3) / 1e12       # fp32-equivalent algorithmic rate
+    kname, passes, peak = KERNELS[args.precision]
+    achieved_tf = passes * algo_tf                                  # MFMA flops the hardware executes
 
     extra = {}
+    if args.precision != "f32" and not args.no_f32_compare:
+        for mm in models:
+            mm.precision = "f32"
+            mm.packed()
+        dtf, fms, _ = timed(max(1, args.steps // 2), 1, coarse_only=True)
+        f_ms = sum(fms) / max(1, len(fms))
+        extra["f32_kernel"] = {"value": n_img_rays * n * max(1, args.steps // 2) / dtf, "unit": "rays/s",
+                               "field_avg_ms": f_ms,
+                               "achieved_tflops": flop_per_launch / (f_ms * 1e-3) / 1e12,
+                               "peak": PEAK_FP32_MFMA_TFLOPS}
+        for mm in models:
+            mm.precision = args.precision
     if args.hierarchical:
         dth, _, _ = timed(max(1, args.steps // 2), 1, coarse_only=False)
         extra["hierarchical_64_64_rays_per_s"] = n_img_rays * n * max(1, args.steps // 2) / dth
@@ -162,7 +187,8 @@ def main():
     tpath = os.path.join(ROOT, "profiles", "field_kernel_traffic.json")
     if os.path.exists(tpath):
         with open(tpath) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
+            tj = json.load(f)
+            traffic = tj.get(args.precision, {}).get("hbm_bytes_per_launch")
 
     result = {
         "metric": "rendered rays/sec (128x128, 64 samples/ray)",
@@ -175,16 +201,16 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "bf16x3" if args.precision == "bf16x3" else "f32",
         "data": "synthetic (hash-initialised CodeNeRFModel weights, one latent code pair, spherical poses)",
         "config": {"workload": "C2: srn-cars-code 128x128 image per rank-step, 64 coarse samples/ray, "
                                "chunk 4096, lindepth near 0.8 far 1.8, fused HIP render",
                    "images_per_step": n, "rays_per_image": n_img_rays, "samples_per_ray": NC,
                    "parallelism": f"ray-sharded x{n} + RCCL all-gather" if n > 1 else "single GPU"},
-        "roofline": {"kernel": "field_kernel<kFromRayZ> (fused posenc + CodeNeRF MLP, fp32 MFMA)",
-                     "bound": "mfma", "achieved": achieved_tf, "peak": PEAK_FP32_MFMA_TFLOPS,
-                     "unit": "TFLOP/s", "frac": achieved_tf / PEAK_FP32_MFMA_TFLOPS, "traffic": traffic,
-                     "avg_launch_ms": field_avg_ms, "flop_per_launch": flop_per_launch},
+        "roofline": {"kernel": kname, "bound": "mfma", "achieved": achieved_tf, "peak": peak,
+                     "unit": "TFLOP/s", "frac": achieved_tf / peak, "traffic": traffic,
+                     "avg_launch_ms": field_avg_ms, "flop_per_launch": flop_per_launch,
+                     "mfma_passes": passes, "fp32_equiv_tflops": algo_tf},
     }
     result.update(extra)
 
