@@ -72,58 +72,64 @@ __global__ void pack_kernel(Params P, float* __restrict__ packed) {
 }
 
 // ---------------------------------------------------------------- code bias
-// One workgroup per code row: the three code layers (model.py:174-177), then
-// the code halves of layer_xyz2 / fc_out / fc_rgb plus their biases.
+// One workgroup (16 waves) per code row: the three code layers (model.py:174-177),
+// then the code halves of layer_xyz2 / fc_out / fc_rgb plus their biases.  Each
+// output is one wave-wide dot product: 64 lanes read a 256-float weight row as
+// one coalesced float4 each, then a butterfly sum.
 
-__global__ __launch_bounds__(256) void code_bias_kernel(Params P, const float* __restrict__ z_s,
-                                                        const float* __restrict__ z_t,
-                                                        float* __restrict__ out) {
-  __shared__ float zs[kCode], zt[kCode], s1[kCode], s2[kCode], t1[kCode];
-  const int c = blockIdx.x, j = threadIdx.x;
-  zs[j] = z_s[(int64_t)c * kCode + j];
-  zt[j] = z_t[(int64_t)c * kCode + j];
+constexpr int kCbThreads = 1024;
+
+__device__ __forceinline__ float wave_dot256(const float* __restrict__ w, const float* v, int lane) {
+  const float4 a = reinterpret_cast<const float4*>(w)[lane];
+  const float4 b = reinterpret_cast<const float4*>(v)[lane];
+  float s = fmaf(a.x, b.x, fmaf(a.y, b.y, fmaf(a.z, b.z, a.w * b.w)));
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  return s;
+}
+
+__global__ __launch_bounds__(kCbThreads) void code_bias_kernel(Params P, const float* __restrict__ z_s,
+                                                               const float* __restrict__ z_t,
+                                                               float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) float zs[kCode], zt[kCode], s1[kCode], s2[kCode], t1[kCode];
+  const int c = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  constexpr int kW = kCbThreads / 64;
+  if (t < kCode) {
+    zs[t] = z_s[(int64_t)c * kCode + t];
+    zt[t] = z_t[(int64_t)c * kCode + t];
+  }
   __syncthreads();
-  {
-    const float* w1 = P.p[kWSc1] + j * kCode;
-    const float* w2 = P.p[kWSc2] + j * kCode;
-    const float* w3 = P.p[kWTc1] + j * kCode;
-    float a1 = 0.f, a2 = 0.f, a3 = 0.f;
-    for (int k = 0; k < kCode; ++k) {
-      a1 = fmaf(w1[k], zs[k], a1);
-      a2 = fmaf(w2[k], zs[k], a2);
-      a3 = fmaf(w3[k], zt[k], a3);
+  for (int r = wave; r < 3 * kCode; r += kW) {
+    const int l = r / kCode, j = r % kCode;
+    const float* w = P.p[l == 0 ? kWSc1 : (l == 1 ? kWSc2 : kWTc1)] + j * kCode;
+    const float a = wave_dot256(w, l == 2 ? zt : zs, lane);
+    if (lane == 0) {
+      const float v = fmaxf(a + P.p[l == 0 ? kBSc1 : (l == 1 ? kBSc2 : kBTc1)][j], 0.f);
+      (l == 0 ? s1 : (l == 1 ? s2 : t1))[j] = v;
     }
-    s1[j] = fmaxf(a1 + P.p[kBSc1][j], 0.f);
-    s2[j] = fmaxf(a2 + P.p[kBSc2][j], 0.f);
-    t1[j] = fmaxf(a3 + P.p[kBTc1][j], 0.f);
   }
   __syncthreads();
   float* o = out + (int64_t)c * kCbStride;
-  {
-    const float* wx = P.p[kWXyz2] + j * (kHidden + kCode) + kHidden;
-    const float* wo = P.p[kWOut] + (1 + j) * (kHidden + kCode) + kHidden;
-    float ax = 0.f, ao = 0.f;
-    for (int k = 0; k < kCode; ++k) {
-      ax = fmaf(wx[k], s1[k], ax);
-      ao = fmaf(wo[k], s2[k], ao);
-    }
-    o[kCbXyz2 + j] = ax + P.p[kBXyz2][j];
-    o[kCbFeat + j] = ao + P.p[kBOut][1 + j];
-  }
-  if (j < 4) {
-    float a = 0.f, b = 0.f;
-    if (j == 0) {
-      const float* w = P.p[kWOut] + kHidden;  // fc_out row 0 (sigma)
-      for (int k = 0; k < kCode; ++k) a = fmaf(w[k], s2[k], a);
-      b = P.p[kBOut][0];
+  // rows: 0..255 layer_xyz2, 256..512 fc_out (row 0 = sigma), 513..515 fc_rgb
+  for (int r = wave; r < 2 * kCode + 4; r += kW) {
+    const float* w;
+    const float* v;
+    float b;
+    int dst;
+    if (r < kCode) {
+      w = P.p[kWXyz2] + r * (kHidden + kCode) + kHidden; v = s1; b = P.p[kBXyz2][r]; dst = kCbXyz2 + r;
+    } else if (r < 2 * kCode + 1) {
+      const int i = r - kCode;  // fc_out row i
+      w = P.p[kWOut] + i * (kHidden + kCode) + kHidden; v = s2; b = P.p[kBOut][i];
+      dst = i == 0 ? kCbSigma : kCbFeat + i - 1;
     } else {
-      const float* w = P.p[kWRgb] + (j - 1) * (kHidden + kCode) + kHidden;
-      for (int k = 0; k < kCode; ++k) a = fmaf(w[k], t1[k], a);
-      b = P.p[kBRgb][j - 1];
+      const int i = r - 2 * kCode - 1;
+      w = P.p[kWRgb] + i * (kHidden + kCode) + kHidden; v = t1; b = P.p[kBRgb][i]; dst = kCbRgb + i;
     }
-    o[kCbSigma + j] = a + b;
+    const float a = wave_dot256(w, v, lane);
+    if (lane == 0) o[dst] = a + b;
   }
-  if (j >= 4 && j < 8) o[kCbRgb + j - 1] = 0.f;  // pad 516..519
+  if (t >= 4 && t < 8) o[kCbRgb + t - 1] = 0.f;  // pad 516..519
 }
 
 // ---------------------------------------------------------------- field kernel
@@ -441,7 +447,7 @@ extern "C" int cn_code_bias(const float* const* params, const float* z_s, const 
   Params P;
   if (make_params(params, &P) != CN_OK) return CN_EINVAL;
   CN_CHECK_ARG(z_s && z_t && code_bias && n_codes > 0 && n_codes <= (1ll << 31) - 1);
-  hipLaunchKernelGGL(code_bias_kernel, dim3(static_cast<unsigned>(n_codes)), dim3(256), 0,
+  hipLaunchKernelGGL(code_bias_kernel, dim3(static_cast<unsigned>(n_codes)), dim3(kCbThreads), 0,
                      cn::as_stream(stream), P, z_s, z_t, code_bias);
   return cn::launch_status();
 }

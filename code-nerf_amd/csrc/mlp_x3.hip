@@ -2,32 +2,36 @@
 // with every fp32 GEMM x.W computed as  Wh.Xh + Wh.Xl + Wl.Xh  on
 // v_mfma_f32_32x32x16_bf16 (fp32 accumulate), where Wh = bf16(W),
 // Wl = bf16(W - Wh) (packed once) and Xh/Xl the same split of the activations
-// (done in registers at each layer's epilogue).  The dropped Wl.Xl term and the
-// lo rounding leave ~2^-17 relative error per product -- far inside the 1e-4
-// rendered-RGB tolerance -- at 3/16 of the fp32-MFMA cost: 1,776 MFMAs x 32
-// cycles per 32-sample wave tile instead of 4,720 x 64.
+// (done in registers).  The dropped Wl.Xl term and the lo rounding leave ~2^-17
+// relative error per product -- far inside the 1e-4 rendered-RGB tolerance --
+// at 3/16 of the fp32-MFMA cost.
 //
-// Register dataflow as in mlp.hip: a 32x32 fp32 accumulator block's registers
-// 8s..8s+7 become k-step s (16 features) of the next layer's B operand after a
-// hi/lo split (element j of lane half h = feature 16s + 8(j>>2) + 4h + (j&3) of
-// the block, cdna_hip_programming.md section 3), so activations never leave
-// registers.
+// Register dataflow.  A 32x32 fp32 accumulator block's registers 0..7 / 8..15
+// are the next layer's B operand for k-steps 2b / 2b+1 (element j of lane half h
+// = feature 32b + (j&3) + 8(j>>2) + 4h of the block, mlp_layout.h), so
+// activations never leave registers.  Each wave keeps one "slot" of 16 VGPRs
+// per accumulator block.  At the end of a layer the accumulators are copied
+// raw (fp32) into the slots, interleaved with the layer's last MFMAs; the next
+// layer converts slot b+1 (activation + hi/lo bf16 split, ~10 VALU per pair)
+// while its MFMAs on slot b run, so the epilogue hides in the MFMA issue gaps
+// instead of standing between layers (one wave per SIMD: nothing else would
+// cover it).
 //
-// Weight stream.  Every chunk has ONE format -- 2 k-steps x 9 block slots x
-// {hi, lo} x 64 lanes quads = 36 KiB, fragment-major so a wave's ds_read_b128 of
-// one fragment is 1 KiB contiguous (bank-conflict free) -- and the chunks lie in stream order in the
-// packed buffer, so chunk c is just `packed + c * 36 KiB`.  A 4-slot LDS ring is
-// filled by LDS-DMA (global_load_lds, 1 KiB per wave-instruction, 9 per wave per
-// chunk); chunk c+3 is issued when chunk c starts, and a constant
-// `s_waitcnt vmcnt(18)` + s_barrier retires chunk c (two dummy chunks at the end
-// keep the count constant).  No ordinary global load is live in the stream
-// (biases are scalar loads), so the counted waits are exact.
+// sigma (fc_out row 0) is an fp32 dot product over layer_xyz2's outputs taken
+// during that same conversion (2 FMAs per pair), so every weight chunk has the
+// same 8-block shape.
 //
-// Code size.  The four 256-input layers (layer_xyz2, fc_out, layer_dir1's feature
-// part, layer_dir2) run through ONE runtime loop whose body is a single unrolled
-// 16-k-step layer: fully unrolling all six layers (~140 KiB of code) made the
-// kernel instruction-fetch bound (ablation: removing every MFMA saved only 4 %).
-// fc_out's 9th output block (sigma) is a uniform branch.
+// Weight stream.  Chunk = 2 k-steps x 8 blocks x {hi, lo} x 64 lanes quads =
+// 32 KiB, fragment-major so a wave's ds_read_b128 of one fragment is 1 KiB
+// contiguous (bank-conflict free); chunk c lies at packed + c * 32 KiB.  A 4-slot
+// LDS ring is filled by LDS-DMA (global_load_lds, 1 KiB per wave-instruction, 8 per
+// wave per chunk); chunk c+3 is issued when chunk c starts and a counted
+// `s_waitcnt vmcnt` + s_barrier retires chunk c.  No ordinary global load is live
+// in the stream, so the counted waits are exact.
+//
+// Code size.  The four 256-input layers run through ONE runtime loop whose body
+// is a single unrolled 16-k-step layer (a fully unrolled kernel is
+// instruction-fetch bound).
 #include "mlp_common.h"
 
 namespace cn {
@@ -35,20 +39,22 @@ namespace mlp {
 namespace x3 {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kSlotBlocks = 9;
-constexpr int kQuadsPerStep = 64 * kSlotBlocks * 2;      // one k-step of a chunk
-constexpr int kChunkQuads = 2 * kQuadsPerStep;            // 2304 quads = 36 KiB
-constexpr int kDmaPerWave = kChunkQuads / 64 / 4;        // 9
-// stream: L0 2 | L1 8 | L2 8 | L3 8 + 1 (view dir) | L4 8 | L5 1 | 2 dummies
-constexpr int kChunkL1 = 2, kChunkL2 = 10, kChunkL3 = 18, kChunkDir = 26, kChunkL4 = 27, kChunkRgb = 35;
-constexpr int kRealChunks = 36;
-constexpr int kStreamChunks = kRealChunks + 2;
-constexpr int kQuads = kStreamChunks * kChunkQuads;
+constexpr int kBlk = 8;                              // 32-row output blocks per k-step
+constexpr int kQuadsPerStep = 64 * kBlk * 2;         // one k-step of a chunk (16 KiB)
+constexpr int kChunkQuads = 2 * kQuadsPerStep;       // 2048 quads = 32 KiB
+constexpr int kDmaPerWave = kChunkQuads / 64 / 4;    // 8
+// stream: xyz1 2 | xyz2 8 | fc_out 8 | layer_dir1 view-dir k-steps 1 | layer_dir1 8 | layer_dir2 8 | fc_rgb 1
+constexpr int kChunkL1 = 2, kChunkL2 = 10, kChunkDir = 18, kChunkL3 = 19, kChunkL4 = 27, kChunkRgb = 35;
+constexpr int kChunks = 36;
+constexpr int kQuads = kChunks * kChunkQuads;
 constexpr int kBiasXyz1 = kQuads * 4;  // floats
-constexpr int kBiasDir1 = kBiasXyz1 + 256;
-constexpr int kBiasDir2 = kBiasDir1 + 256;
-constexpr int kPackedFloats = kBiasDir2 + 256;
+constexpr int kSigmaOff = 768;         // after b_xyz1, b_dir1, b_dir2: fc_out row 0 over h2, [h][b][reg]
+constexpr int kConsts = 1024;
+constexpr int kPackedFloats = kBiasXyz1 + kConsts;
 
 // Input feature of lane half h, element j, k-step s of layer l (-1 = zero pad).
 __host__ __device__ constexpr int in_col(int l, int s, int h, int j) {
@@ -67,30 +73,34 @@ __device__ __forceinline__ unsigned short bf16_bits(float x) {
   return __builtin_bit_cast(unsigned short, b);
 }
 
-// (chunk, step-in-chunk T, slot j) -> (layer, k-step, output block); -1 layer = zeros
+// (chunk, step-in-chunk T, slot j) -> (layer, k-step, output block)
 __device__ void chunk_map(int c, int T, int j, int& l, int& ks, int& ob) {
-  l = -1;
-  ks = 0;
   ob = j;
   if (c < kChunkL1) { l = kXyz1; ks = 2 * c + T; }
   else if (c < kChunkL2) { l = kXyz2; ks = 2 * (c - kChunkL1) + T; }
-  else if (c < kChunkL3) { l = kOut; ks = 2 * (c - kChunkL2) + T; }
-  else if (c < kChunkDir) { l = kDir1; ks = 2 * (c - kChunkL3) + T; }
+  else if (c < kChunkDir) { l = kOut; ks = 2 * (c - kChunkL2) + T; }
   else if (c == kChunkDir) { l = kDir1; ks = 16 + T; }
+  else if (c < kChunkL4) { l = kDir1; ks = 2 * (c - kChunkL3) + T; }
   else if (c < kChunkRgb) { l = kDir2; ks = 2 * (c - kChunkL4) + T; }
-  else if (c == kChunkRgb) { l = kRgb; ks = 9 * T + j; ob = 0; if (ks >= 16) l = -1; }
-  if (l >= 0 && l != kOut && ob >= 8) l = -1;
+  else { l = kRgb; ks = 8 * T + j; ob = 0; }
 }
 
 __global__ void pack_x3_kernel(Params P, float* __restrict__ packed) {
   unsigned short* q16 = reinterpret_cast<unsigned short*>(packed);
   const int n_elems = kQuads * 8;  // bf16 elements
-  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n_elems + 768;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n_elems + kConsts;
        idx += gridDim.x * blockDim.x) {
     if (idx >= n_elems) {
       const int j = idx - n_elems;
-      packed[kBiasXyz1 + j] =
-          j < 256 ? P.p[kBXyz1][j] : (j < 512 ? P.p[kBDir1][j - 256] : P.p[kBDir2][j - 512]);
+      float v;
+      if (j < 256) v = P.p[kBXyz1][j];
+      else if (j < 512) v = P.p[kBDir1][j - 256];
+      else if (j < 768) v = P.p[kBDir2][j - 512];
+      else {
+        const int t = j - kSigmaOff, h = t >> 7, b = (t >> 4) & 7, r = t & 15;
+        v = P.p[kWOut][acc_row(b, r, h)];  // fc_out row 0 at input feature acc_row(b, r, h) of h2
+      }
+      packed[kBiasXyz1 + j] = v;
       continue;
     }
     const int quad = idx >> 3, e = idx & 7;
@@ -98,27 +108,23 @@ __global__ void pack_x3_kernel(Params P, float* __restrict__ packed) {
     int r = quad % kChunkQuads;
     const int T = r / kQuadsPerStep;
     r %= kQuadsPerStep;
-    const int frag = r / 64, lane = r % 64;  // fragment-major: 1 KiB per (slot, hi|lo)
+    const int frag = r / 64, lane = r % 64;  // fragment-major: 1 KiB per (block, hi|lo)
     const int slot = frag >> 1, part = frag & 1;
     int l, ks, ob;
     chunk_map(c, T, slot, l, ks, ob);
-    float w = 0.0f;
-    if (l >= 0) {
-      const int i = lane & 31, h = lane >> 5;
-      const int col = in_col(l, ks, h, e);
-      int row = -1, in_dim = 0;
-      const float* W = nullptr;
-      switch (l) {
-        case kXyz1: W = P.p[kWXyz1]; in_dim = kDimXyz; row = 32 * ob + i; break;
-        case kXyz2: W = P.p[kWXyz2]; in_dim = kHidden + kCode; row = 32 * ob + i; break;
-        case kOut: W = P.p[kWOut]; in_dim = kHidden + kCode;
-          row = ob < 8 ? 1 + 32 * ob + i : (i == 0 ? 0 : -1); break;
-        case kDir1: W = P.p[kWDir1]; in_dim = kCode + kDimDir; row = 32 * ob + i; break;
-        case kDir2: W = P.p[kWDir2]; in_dim = kHidden; row = 32 * ob + i; break;
-        default: W = P.p[kWRgb]; in_dim = kHidden + kCode; row = i < 3 ? i : -1; break;
-      }
-      if (row >= 0 && col >= 0) w = W[row * in_dim + col];
+    const int i = lane & 31, h = lane >> 5;
+    const int col = in_col(l, ks, h, e);
+    int row = -1, in_dim = 0;
+    const float* W = nullptr;
+    switch (l) {
+      case kXyz1: W = P.p[kWXyz1]; in_dim = kDimXyz; row = 32 * ob + i; break;
+      case kXyz2: W = P.p[kWXyz2]; in_dim = kHidden + kCode; row = 32 * ob + i; break;
+      case kOut: W = P.p[kWOut]; in_dim = kHidden + kCode; row = 1 + 32 * ob + i; break;
+      case kDir1: W = P.p[kWDir1]; in_dim = kCode + kDimDir; row = 32 * ob + i; break;
+      case kDir2: W = P.p[kWDir2]; in_dim = kHidden; row = 32 * ob + i; break;
+      default: W = P.p[kWRgb]; in_dim = kHidden + kCode; row = i < 3 ? i : -1; break;
     }
+    const float w = (row >= 0 && col >= 0) ? W[row * in_dim + col] : 0.0f;
     const __bf16 hi = static_cast<__bf16>(w);
     const float lo = w - static_cast<float>(hi);
     q16[idx] = part == 0 ? bf16_bits(w) : bf16_bits(lo);
@@ -130,70 +136,107 @@ __global__ void pack_x3_kernel(Params P, float* __restrict__ packed) {
 constexpr int kWaves = 4;
 constexpr int kThreads = 64 * kWaves;
 constexpr int kTile = 32 * kWaves;
-constexpr int kSlots = 4;
-constexpr int kLdsQuads = kSlots * kChunkQuads;  // 144 KiB ring
+constexpr int kRing = 4;
+constexpr int kLdsQuads = kRing * kChunkQuads;  // 128 KiB ring
+// after the ring: the constant vectors (1024), then each wave's code row
+constexpr int kBiasLds = kConsts + kWaves * kCbStride;
 
 struct State {
-  bf16x8 bh[16], bl[16];  // B operands (hi / lo) of the current layer's 16 k-steps
+  float sl[8][16];        // per accumulator block: raw fp32 copy, then {hi, lo} bf16 of k-steps 2b, 2b+1
   bf16x8 dh[2], dl[2];    // view-direction encoding k-steps of layer_dir1
-  floatx16 acc[9];
-  float sigma;
+  floatx16 acc[8];
+  float sigma, sig;       // fc_out row 0; running partial of this lane half
   int lane, h, wave;
   int crow;               // this lane's code-bias row
   bool uniform_code;      // all 32 samples of the wave use one code row
-  float vd[3];
 };
-
-__device__ __forceinline__ void split8(const float* v, bf16x8& hi, bf16x8& lo) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const __bf16 b = static_cast<__bf16>(v[j]);
-    hi[j] = b;
-    lo[j] = static_cast<__bf16>(v[j] - static_cast<float>(b));
-  }
-}
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
-typedef const __attribute__((address_space(4))) float* const_fptr;
 
-// Issue this wave's 9 DMA instructions of chunk c into ring slot c % 4.
+__device__ __forceinline__ bf16x8 dw8(const float* f) {
+  const u32x4 u = {__float_as_uint(f[0]), __float_as_uint(f[1]), __float_as_uint(f[2]), __float_as_uint(f[3])};
+  return __builtin_bit_cast(bf16x8, u);
+}
+
+template <int J>
+__device__ __forceinline__ bf16x8 Bh(const State& s, int t) { return dw8(s.sl[J] + 8 * t); }
+template <int J>
+__device__ __forceinline__ bf16x8 Bl(const State& s, int t) { return dw8(s.sl[J] + 8 * t + 4); }
+#define CN_SLOT_B(J) Bh<J>(s, 0), Bl<J>(s, 0), Bh<J>(s, 1), Bl<J>(s, 1)
+
+__device__ __forceinline__ float vmax(float x, float lo) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(lo));
+  return r;
+}
+
+// Values 2K, 2K+1 of a raw block -> activation, hi/lo bf16 into `out` (k-step
+// K/4, dword K%4); sig += w . v (the sigma dot product, kept only in fc_out).
+template <int K>
+__device__ __forceinline__ void conv_piece(const float* raw, float* out, float lo_clamp, const float* w, float& sig) {
+  f32x2 v;
+  v.x = vmax(raw[2 * K], lo_clamp);
+  v.y = vmax(raw[2 * K + 1], lo_clamp);
+  if (w) {
+    sig = fmaf(w[2 * K], v.x, sig);
+    sig = fmaf(w[2 * K + 1], v.y, sig);
+  }
+  const bf16x2 hb = __builtin_convertvector(v, bf16x2);
+  const unsigned hu = __builtin_bit_cast(unsigned, hb);
+  f32x2 back;
+  back.x = __uint_as_float(hu << 16);
+  back.y = __uint_as_float(hu & 0xffff0000u);
+  const bf16x2 lb = __builtin_convertvector(v - back, bf16x2);
+  unsigned hi_w = hu, lo_w = __builtin_bit_cast(unsigned, lb);
+  // pin the piece here: without it LLVM sinks the arithmetic to the B operand's
+  // first use (the next chunk), out of the MFMA gaps it is meant to fill
+  asm volatile("" : "+v"(hi_w), "+v"(lo_w), "+v"(sig));
+  constexpr int t = K / 4, d = K % 4;
+  out[8 * t + d] = __uint_as_float(hi_w);
+  out[8 * t + 4 + d] = __uint_as_float(lo_w);
+}
+
+template <int K = 0>
+__device__ __forceinline__ void conv_all(const float* raw, float* out, float lo, const float* w, float& sig) {
+  if constexpr (K < 8) {
+    conv_piece<K>(raw, out, lo, w, sig);
+    conv_all<K + 1>(raw, out, lo, w, sig);
+  }
+}
+
+// Issue this wave's 8 DMA instructions of chunk c into ring slot c % 4.
 __device__ __forceinline__ void issue_chunk(const State& s, const float* __restrict__ packed, float4* lds, int c) {
-  const float4* src = reinterpret_cast<const float4*>(packed) + c * kChunkQuads + s.wave * 64 + s.lane;
-  float4* slot = lds + (c & (kSlots - 1)) * kChunkQuads + s.wave * 64;
+  const float4* src = reinterpret_cast<const float4*>(packed) + (c * kChunkQuads + s.wave * 64);
+  float4* slot = lds + (c & (kRing - 1)) * kChunkQuads + s.wave * 64;
 #pragma unroll
   for (int i = 0; i < kDmaPerWave; ++i) {
 #ifndef CN_ABLATE_NO_DMA
-    __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src + i * 256), (lds_ptr_t)(slot + i * 256), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src + i * 256 + s.lane), (lds_ptr_t)(slot + i * 256), 16, 0, 0);
 #endif
   }
 }
 
 // Chunk c landed for every wave and every wave is done with chunk c-1 (its slot
-// is refilled next): one asm statement, so no LDS read can be scheduled across it.
+// is refilled next).  OUT = this wave's DMA instructions issued after chunk c.
+// One asm statement, so no LDS read can be scheduled across it.
+template <int OUT>
 __device__ __forceinline__ void chunk_barrier() {
 #ifdef CN_ABLATE_NO_DMA
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #else
-  asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(2 * kDmaPerWave) : "memory");
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(OUT) : "memory");
 #endif
 }
 
-// Biases.  acc starts as b (1 x 32 rows) via ONE MFMA per output block: A holds
-// {bf16(b_i), bf16(b_i - hi)} at k = 0, 1 (lane half 0), B holds ones at k = 0, 1
-// for every sample, so D = hi + lo in fp32.  The bias vectors sit in LDS after the
-// ring (constants + each wave's code row, staged before the DMA stream) and are
-// read by inline-asm ds_reads: hipcc cannot prove them disjoint from the in-flight
-// DMA and would otherwise wait vmcnt(0), draining the ring.  A wave whose samples
-// use several code rows takes per-lane vector loads instead (slow path, rare:
-// S < 32 with per-ray codes).
-constexpr int kBiasLds = 768 + kWaves * kCbStride;
-
-__device__ __forceinline__ unsigned lds_addr(const float* p) {
+// Small LDS reads outside the ring (biases, sigma weights).  Inline asm: hipcc
+// cannot prove them disjoint from the in-flight DMA and would otherwise wait
+// vmcnt(0), draining the ring.
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
   return static_cast<unsigned>(reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) void*)p));
 }
 
-// 8 floats at p + 32*ob (ob = 0..7), one LDS round trip, invisible to hipcc's waitcnt pass.
+// 8 floats at p + 32*ob (ob = 0..7), one LDS round trip.
 __device__ __forceinline__ void lds_read8_stride32(const float* p, float* v) {
   asm volatile(
       "ds_read_b32 %0, %8\n\tds_read_b32 %1, %8 offset:128\n\tds_read_b32 %2, %8 offset:256\n\t"
@@ -204,57 +247,89 @@ __device__ __forceinline__ void lds_read8_stride32(const float* p, float* v) {
       : "memory");
 }
 
+// 16 consecutive floats (64 B aligned), one LDS round trip.
+__device__ __forceinline__ void lds_read16(const float* p, float* v) {
+  u32x4 a, b, c, d;
+  asm volatile(
+      "ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:16\n\tds_read_b128 %2, %4 offset:32\n\t"
+      "ds_read_b128 %3, %4 offset:48\n\ts_waitcnt lgkmcnt(0)"
+      : "=&v"(a), "=&v"(b), "=&v"(c), "=&v"(d)
+      : "v"(lds_addr(p))
+      : "memory");
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[i] = __uint_as_float(a[i]);
+    v[4 + i] = __uint_as_float(b[i]);
+    v[8 + i] = __uint_as_float(c[i]);
+    v[12 + i] = __uint_as_float(d[i]);
+  }
+}
+
+// The same without a wait: the values are first used after the next chunk
+// barrier, whose lgkmcnt(0) covers them (volatile asm keeps the order).
+__device__ __forceinline__ void lds_read16_async(const float* p, float* v) {
+  u32x4 a, b, c, d;
+  asm volatile(
+      "ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:16\n\tds_read_b128 %2, %4 offset:32\n\t"
+      "ds_read_b128 %3, %4 offset:48"
+      : "=&v"(a), "=&v"(b), "=&v"(c), "=&v"(d)
+      : "v"(lds_addr(p))
+      : "memory");
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[i] = __uint_as_float(a[i]);
+    v[4 + i] = __uint_as_float(b[i]);
+    v[8 + i] = __uint_as_float(c[i]);
+    v[12 + i] = __uint_as_float(d[i]);
+  }
+}
+
 __device__ __forceinline__ float lds_read1(const float* p) {
   float v;
   asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(v) : "v"(lds_addr(p)) : "memory");
   return v;
 }
 
-__device__ __forceinline__ void bias_mfma(floatx16& acc, float v, bf16x8 one) {
+// Biases.  acc starts as b via ONE MFMA per output block: A holds {bf16(b_i),
+// bf16(b_i - hi)} at k = 0, 1 (lane half 0), B holds ones at k = 0, 1, so D = hi
+// + lo in fp32.
+__device__ __forceinline__ floatx16 bias_mfma(float v, bf16x8 one) {
   bf16x8 f = {};
   const __bf16 hi = static_cast<__bf16>(v);
   f[0] = hi;
   f[1] = static_cast<__bf16>(v - static_cast<float>(hi));
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f, one, floatx16{0}, 0, 0, 0);
+#ifdef CN_ABLATE_NO_MFMA
+  floatx16 r = {};
+  r[0] = v;
+  asm volatile("" ::"v"(f), "v"(one));
+  return r;
+#else
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(f, one, floatx16{0}, 0, 0, 0);
+#endif
 }
 
-__device__ __forceinline__ void init_acc(State& s, const FieldArgs& a, const float* blds, int layer) {
-#ifdef CN_ABLATE_NO_BIAS
-#pragma unroll
-  for (int ob = 0; ob < 9; ++ob) s.acc[ob] = floatx16{0};
-  return;
-#endif
-  const bool per_code = (layer == kXyz2 || layer == kOut || layer == kRgb);
-  const int i = s.lane & 31;
-  if (!per_code || s.uniform_code) {
-    bf16x8 one = {};
-    if (s.h == 0) {
-      one[0] = static_cast<__bf16>(1.0f);
-      one[1] = static_cast<__bf16>(1.0f);
-    }
-    const float* src = per_code ? blds + 768 + s.wave * kCbStride
-                                : blds + (layer == kXyz1 ? 0 : (layer == kDir1 ? 256 : 512));
-    if (layer == kRgb) {
-      const float v = lds_read1(src + kCbRgb + (i < 3 ? i : 0));
-      bias_mfma(s.acc[0], (s.h == 0 && i < 3) ? v : 0.0f, one);
-      return;
-    }
-    const int off = per_code ? (layer == kXyz2 ? kCbXyz2 : kCbFeat) : 0;
-    float v[8];
-    lds_read8_stride32(src + off + i, v);
-#pragma unroll
-    for (int ob = 0; ob < 8; ++ob) bias_mfma(s.acc[ob], s.h == 0 ? v[ob] : 0.0f, one);
-    if (layer == kOut) {
-      const float sg = lds_read1(src + kCbSigma);
-      bias_mfma(s.acc[8], (s.h == 0 && i == 0) ? sg : 0.0f, one);
-    }
-    return;
+__device__ __forceinline__ bf16x8 ones_b(int h) {
+  bf16x8 one = {};
+  if (h == 0) {
+    one[0] = static_cast<__bf16>(1.0f);
+    one[1] = static_cast<__bf16>(1.0f);
   }
-  // slow path: per-lane code rows
+  return one;
+}
+
+// Bias vector of `layer` for this lane's 8 blocks (lane half 0 carries it).
+__device__ __forceinline__ void bias_values(const State& s, const float* blds, int layer, float* v) {
+  const bool per_code = (layer == kXyz2 || layer == kOut);
+  const float* src = per_code ? blds + kConsts + s.wave * kCbStride + (layer == kXyz2 ? kCbXyz2 : kCbFeat)
+                              : blds + (layer == kXyz1 ? 0 : (layer == kDir1 ? 256 : 512));
+  lds_read8_stride32(src + (s.lane & 31), v);
+}
+
+// Slow path (a wave whose samples use several code rows): per-lane loads.
+__device__ __forceinline__ void init_acc_per_lane(State& s, const FieldArgs& a, int layer) {
   const float* base = a.code_bias + (int64_t)s.crow * kCbStride;
-#pragma unroll
-  for (int ob = 0; ob < 9; ++ob) s.acc[ob] = floatx16{0};
   if (layer == kRgb) {
+    s.acc[0] = floatx16{0};
     if (s.h == 0) {
       s.acc[0][0] = base[kCbRgb];
       s.acc[0][1] = base[kCbRgb + 1];
@@ -273,20 +348,8 @@ __device__ __forceinline__ void init_acc(State& s, const FieldArgs& a, const flo
         s.acc[ob][4 * q + 3] = v.w;
       }
     }
-    if (layer == kOut && s.h == 0) s.acc[8][0] = base[kCbSigma];
   }
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): nothing pending leaks past the branch
-}
-
-// A fragments of slot blocks [J0, J0+3) of k-step T of the chunk in `slot`.
-template <int T, int J0>
-__device__ __forceinline__ void load_a(const State& s, const float4* slot, bf16x8* ah, bf16x8* al) {
-  const float4* ap = slot + T * kQuadsPerStep + s.lane;
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    ah[i] = __builtin_bit_cast(bf16x8, ap[(2 * (J0 + i)) * 64]);
-    al[i] = __builtin_bit_cast(bf16x8, ap[(2 * (J0 + i) + 1) * 64]);
-  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): nothing pending leaks out
 }
 
 __device__ __forceinline__ void mfma3(floatx16& acc, bf16x8 ah, bf16x8 al, bf16x8 bh, bf16x8 bl) {
@@ -299,166 +362,315 @@ __device__ __forceinline__ void mfma3(floatx16& acc, bf16x8 ah, bf16x8 al, bf16x
 #endif
 }
 
-// One 2-k-step chunk against 8 (+ block 8 when with9) output blocks.  The A
-// fragments of the next group of 3 blocks are read while the current group's
-// MFMAs run (two 24-VGPR buffers).
-__device__ __forceinline__ void chunk_mfma(State& s, const float4* slot, bf16x8 bh0, bf16x8 bl0, bf16x8 bh1,
-                                           bf16x8 bl1, bool with9) {
-  bf16x8 ah[3], al[3], nh[3], nl[3];
-  load_a<0, 0>(s, slot, ah, al);
-  load_a<0, 3>(s, slot, nh, nl);
-  __builtin_amdgcn_sched_barrier(0);
+// A fragments {hi, lo} of blocks (2P, 2P+1) of k-step T of the chunk in `slot`.
+template <int T, int P>
+__device__ __forceinline__ void load_a(const State& s, const float4* slot, bf16x8* a) {
+  const float4* ap = slot + T * kQuadsPerStep + s.lane;
 #pragma unroll
-  for (int i = 0; i < 3; ++i) mfma3(s.acc[i], ah[i], al[i], bh0, bl0);
-  __builtin_amdgcn_sched_barrier(0);
-  load_a<0, 6>(s, slot, ah, al);
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int i = 0; i < 3; ++i) mfma3(s.acc[3 + i], nh[i], nl[i], bh0, bl0);
-  __builtin_amdgcn_sched_barrier(0);
-  load_a<1, 0>(s, slot, nh, nl);
-  __builtin_amdgcn_sched_barrier(0);
-  mfma3(s.acc[6], ah[0], al[0], bh0, bl0);
-  mfma3(s.acc[7], ah[1], al[1], bh0, bl0);
-  if (with9) mfma3(s.acc[8], ah[2], al[2], bh0, bl0);
-  __builtin_amdgcn_sched_barrier(0);
-  load_a<1, 3>(s, slot, ah, al);
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int i = 0; i < 3; ++i) mfma3(s.acc[i], nh[i], nl[i], bh1, bl1);
-  __builtin_amdgcn_sched_barrier(0);
-  load_a<1, 6>(s, slot, nh, nl);
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int i = 0; i < 3; ++i) mfma3(s.acc[3 + i], ah[i], al[i], bh1, bl1);
-  __builtin_amdgcn_sched_barrier(0);
-  mfma3(s.acc[6], nh[0], nl[0], bh1, bl1);
-  mfma3(s.acc[7], nh[1], nl[1], bh1, bl1);
-  if (with9) mfma3(s.acc[8], nh[2], nl[2], bh1, bl1);
+  for (int i = 0; i < 2; ++i) {
+    a[2 * i] = __builtin_bit_cast(bf16x8, ap[(2 * (2 * P + i)) * 64]);
+    a[2 * i + 1] = __builtin_bit_cast(bf16x8, ap[(2 * (2 * P + i) + 1) * 64]);
+  }
 }
 
-// Barrier, refill, MFMAs of chunk c with B operands of k-steps (k0, k0+1).
-__device__ __forceinline__ void run_chunk(State& s, const FieldArgs& a, float4* lds, int& c, bf16x8 bh0,
-                                          bf16x8 bl0, bf16x8 bh1, bf16x8 bl1, bool with9) {
-  chunk_barrier();
+// Scheduling pattern of one group: 6 MFMAs, each followed by up to N VALU; the
+// next group's 4 A reads go out with the first two MFMAs.
+template <int N>
+__device__ __forceinline__ void group_pattern() {
+#pragma unroll
+  for (int m = 0; m < 6; ++m) {
+    if (m < 2) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    if constexpr (N > 0) __builtin_amdgcn_sched_group_barrier(0x002, N, 0);
+  }
+}
+
+struct NoFill {
+  template <int G>
+  __device__ __forceinline__ void step() {}
+};
+
+// Convert slot J (raw block of the previous layer) into packed B operands, one
+// pair of values per group; sigma partial alongside.
+template <int J>
+struct ConvFill {
+  State& s;
+  float lo;
+  float w[16];  // sigma weights of this slot
+  float out[16];
+  template <int G>
+  __device__ __forceinline__ void step() {
+    conv_piece<G>(s.sl[J], out, lo, w, s.sig);
+    if constexpr (G == 7) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s.sl[J][i] = out[i];
+    }
+  }
+};
+
+__device__ __forceinline__ void copy_acc(State& s, int b) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    float x = s.acc[b][i];
+    asm volatile("" : "+v"(x));  // materialise the copy here (see conv_piece)
+    s.sl[b][i] = x;
+  }
+}
+
+// Last chunk of a layer: once block pair P's final MFMAs (T = 1, group 4 + P) are
+// issued, copy the pair's accumulators into their slots during the next group.
+struct CopyFill {
+  State& s;
+  template <int G>
+  __device__ __forceinline__ void step() {
+    if constexpr (G >= 5) {
+      copy_acc(s, 2 * (G - 5));
+      copy_acc(s, 2 * (G - 5) + 1);
+    }
+  }
+};
+
+// One 2-k-step chunk against the 8 output blocks: 8 groups (T, block pair) of 6
+// MFMAs; the A fragments of group g+1 are read during group g; fill.step<g>() is
+// VALU work (independent of the chunk) placed in group g's MFMA issue gaps.
+template <int NV, typename Fill>
+__device__ __forceinline__ void chunk_mfma(State& s, const float4* slot, bf16x8 bh0, bf16x8 bl0, bf16x8 bh1,
+                                           bf16x8 bl1, Fill& fill) {
+  bf16x8 a0[4], a1[4];
+  load_a<0, 0>(s, slot, a0);
   __builtin_amdgcn_sched_barrier(0);
-  if (c + 3 < kStreamChunks) issue_chunk(s, a.packed, lds, c + 3);
-  chunk_mfma(s, lds + (c & (kSlots - 1)) * kChunkQuads, bh0, bl0, bh1, bl1, with9);
+#define CN_GROUP(G, CUR, NXT)                                                     \
+  {                                                                              \
+    constexpr int T = (G) / 4, P = (G) % 4;                                      \
+    if constexpr ((G) < 7) load_a<((G) + 1) / 4, ((G) + 1) % 4>(s, slot, NXT);  \
+    const bf16x8 bh = T ? bh1 : bh0, bl = T ? bl1 : bl0;                         \
+    mfma3(s.acc[2 * P], CUR[0], CUR[1], bh, bl);                                 \
+    mfma3(s.acc[2 * P + 1], CUR[2], CUR[3], bh, bl);                             \
+    fill.template step<G>();                                                     \
+    group_pattern<NV>();                                                         \
+    __builtin_amdgcn_sched_barrier(0);                                           \
+  }
+  CN_GROUP(0, a0, a1)
+  CN_GROUP(1, a1, a0)
+  CN_GROUP(2, a0, a1)
+  CN_GROUP(3, a1, a0)
+  CN_GROUP(4, a0, a1)
+  CN_GROUP(5, a1, a0)
+  CN_GROUP(6, a0, a1)
+  CN_GROUP(7, a1, a0)
+#undef CN_GROUP
+}
+
+// Barrier, refill, MFMAs of chunk c.
+template <int NV, typename Fill>
+__device__ __forceinline__ void run_chunk(State& s, const FieldArgs& a, float4* lds, int& c, bf16x8 bh0, bf16x8 bl0,
+                                          bf16x8 bh1, bf16x8 bl1, Fill& fill) {
+  if (c + 2 < kChunks) chunk_barrier<2 * kDmaPerWave>();
+  else if (c + 1 < kChunks) chunk_barrier<kDmaPerWave>();
+  else chunk_barrier<0>();
+  __builtin_amdgcn_sched_barrier(0);
+  if (c + 3 < kChunks) issue_chunk(s, a.packed, lds, c + 3);
+  chunk_mfma<NV>(s, lds + (c & (kRing - 1)) * kChunkQuads, bh0, bl0, bh1, bl1, fill);
   ++c;
 }
 
-// acc -> next layer's B operands: relu (not for fc_out's feat), hi/lo split.
-__device__ __forceinline__ void finish_layer(State& s, bool relu) {
-  const float lo = relu ? 0.0f : -__builtin_inff();
-#pragma unroll
-  for (int b = 0; b < 8; ++b) {
-#pragma unroll
-    for (int sp = 0; sp < 2; ++sp) {
-      float v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float x = s.acc[b][8 * sp + j];
-        asm("v_max_f32 %0, %1, %2" : "=v"(v[j]) : "v"(x), "v"(lo));
-      }
-      split8(v, s.bh[2 * b + sp], s.bl[2 * b + sp]);
-    }
+// Chunk J of a 256-input layer: B from slot J, converting slot J+1 meanwhile
+// (the last chunk copies the accumulators out instead).
+template <int J>
+__device__ __forceinline__ void layer_chunk(State& s, const FieldArgs& a, float4* lds, int& c, const float* blds,
+                                            float lo) {
+  if constexpr (J < 7) {
+    ConvFill<J + 1> f{s, lo, {}, {}};
+    lds_read16_async(blds + kSigmaOff + (s.h * 8 + J + 1) * 16, f.w);
+    run_chunk<2>(s, a, lds, c, CN_SLOT_B(J), f);
+  } else {
+    CopyFill f{s};
+    run_chunk<6>(s, a, lds, c, CN_SLOT_B(J), f);
+    copy_acc(s, 6);
+    copy_acc(s, 7);
   }
+}
+
+// Bias-initialise the accumulators of `layer` while converting slot 0.
+__device__ __forceinline__ void begin_layer(State& s, const FieldArgs& a, const float* blds, int layer, float lo) {
+  float w[16];
+  lds_read16(blds + kSigmaOff + (s.h * 8) * 16, w);
+  float out[16];
+  if (s.uniform_code || !(layer == kXyz2 || layer == kOut)) {
+    float v[8];
+    bias_values(s, blds, layer, v);
+    const bf16x8 one = ones_b(s.h);
+#define CN_BIAS(B)                                   \
+  s.acc[B] = bias_mfma(s.h == 0 ? v[B] : 0.0f, one); \
+  conv_piece<B>(s.sl[0], out, lo, w, s.sig);
+    CN_BIAS(0) CN_BIAS(1) CN_BIAS(2) CN_BIAS(3) CN_BIAS(4) CN_BIAS(5) CN_BIAS(6) CN_BIAS(7)
+#undef CN_BIAS
+  } else {
+    init_acc_per_lane(s, a, layer);
+    conv_all(s.sl[0], out, lo, w, s.sig);
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) s.sl[0][i] = out[i];
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 template <int MODE>
 __global__ __launch_bounds__(kThreads, 1) void field_x3_kernel(FieldArgs a) {
   // ONE LDS object (a second one makes hipcc wait vmcnt(0) before every ring read):
-  // the DMA ring, then the bias vectors
+  // the DMA ring, then the constant vectors and code rows
   __shared__ __attribute__((aligned(16))) float4 lds[kLdsQuads + kBiasLds / 4];
   float* blds = reinterpret_cast<float*>(lds + kLdsQuads);
   State s;
   s.lane = threadIdx.x & 63;
   s.h = s.lane >> 5;
   s.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  s.sig = 0.0f;
+  s.sigma = 0.0f;
   const int64_t row = (int64_t)blockIdx.x * kTile + s.wave * 32 + (s.lane & 31);
   const bool valid = row < a.m;
   const int64_t rc = valid ? row : a.m - 1;
 
-  // ---- per-sample inputs (ordinary loads, all before the DMA stream starts)
+  // ---- per-sample inputs, constant vectors, code rows (ordinary loads); then prime the ring
   const SampleIn in = decode_sample<MODE>(a, rc);
-  float enc[32];
-  if constexpr (MODE == kFromEncoded) {
-    const float* xr = a.x + rc * (kDimXyz + kDimDir);
-    gather_pairs<15>(xr, 0, s.h, enc);
-    float d[16];
-    gather_pairs<6>(xr, kDimXyz, s.h, d);
-    d[14] = 0.0f;
-    d[15] = 0.0f;
-    split8(d, s.dh[0], s.dl[0]);
-    split8(d + 8, s.dh[1], s.dl[1]);
-  } else {
-    encode_pairs<15, 10>(in.x, a.fx, s.h, enc);
-#pragma unroll
-    for (int j = 0; j < 3; ++j) s.vd[j] = in.vd[j];
-  }
-#pragma unroll
-  for (int k = 0; k < 4; ++k) split8(enc + 8 * k, s.bh[k], s.bl[k]);
   s.crow = static_cast<int>(code_row(a, in.code_of));
   const int crow0 = __builtin_amdgcn_readfirstlane(s.crow);
   // wave-uniform by construction; readfirstlane makes it an SGPR so the bias
   // fast/slow choice is a scalar branch (a VGPR bool would run both paths masked)
   s.uniform_code = __builtin_amdgcn_readfirstlane(__ballot(s.crow != crow0) == 0 ? 1 : 0) != 0;
-  for (int j = threadIdx.x; j < 768; j += kThreads) blds[j] = a.packed[kBiasXyz1 + j];
-  if (s.uniform_code) {
+  float cst[kConsts / kThreads];
+#pragma unroll
+  for (int k = 0; k < kConsts / kThreads; ++k) cst[k] = a.packed[kBiasXyz1 + k * kThreads + threadIdx.x];
+  float cbr[9];
+  {
     const float* src = a.code_bias + (int64_t)crow0 * kCbStride;
-    for (int j = s.lane; j < kCbStride; j += 64) blds[768 + s.wave * kCbStride + j] = src[j];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const int j = s.lane + 64 * k;
+      cbr[k] = (s.uniform_code && j < kCbStride) ? src[j] : 0.0f;
+    }
   }
-  __syncthreads();
-
-  // every input load has landed (an s_waitcnt the compiler sees, so nothing stale
-  // is tracked into the DMA stream); prime the ring with chunks 0..2
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  float enc[32];
+  float dv[16];
+  if constexpr (MODE == kFromEncoded) {
+    const float* xr = a.x + rc * (kDimXyz + kDimDir);
+    gather_pairs<15>(xr, 0, s.h, enc);
+    gather_pairs<6>(xr, kDimXyz, s.h, dv);
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): every ordinary load has landed
   issue_chunk(s, a.packed, lds, 0);
   issue_chunk(s, a.packed, lds, 1);
   issue_chunk(s, a.packed, lds, 2);
   int c = 0;
 
-  // ---- layer_xyz1 (63 -> 256): 4 k-steps of encoding
-  init_acc(s, a, blds, kXyz1);
-  run_chunk(s, a, lds, c, s.bh[0], s.bl[0], s.bh[1], s.bl[1], false);
-  run_chunk(s, a, lds, c, s.bh[2], s.bl[2], s.bh[3], s.bl[3], false);
-  finish_layer(s, true);
-
-  // ---- layer_xyz2, fc_out, layer_dir1 (feature part), layer_dir2: one loop body
-  for (int layer = kXyz2; layer <= kDir2; ++layer) {
-    init_acc(s, a, blds, layer);
-    const bool with9 = (layer == kOut);
-#pragma unroll
-    for (int k = 0; k < 16; k += 2) run_chunk(s, a, lds, c, s.bh[k], s.bl[k], s.bh[k + 1], s.bl[k + 1], with9);
-    if (layer == kDir1) run_chunk(s, a, lds, c, s.dh[0], s.dl[0], s.dh[1], s.dl[1], false);
-    if (layer == kOut) {
-      s.sigma = s.acc[8][0];
-      if constexpr (MODE != kFromEncoded) {
-        // view-direction encoding for layer_dir1 (fc_out's accumulators are dead)
-        float v[16];
-        encode_pairs<6, 4>(s.vd, a.fd, s.h, v);
-        v[14] = 0.0f;
-        v[15] = 0.0f;
-        split8(v, s.dh[0], s.dl[0]);
-        split8(v + 8, s.dh[1], s.dl[1]);
-      }
-    }
-    finish_layer(s, layer != kOut);  // fc_out's feat has no activation
+  // ---- encodings (VALU, under the ring's first fills)
+  if constexpr (MODE != kFromEncoded) {
+    encode_pairs<15, 10>(in.x, a.fx, s.h, enc);
+    encode_pairs<6, 4>(in.vd, a.fd, s.h, dv);
   }
+  dv[14] = 0.0f;
+  dv[15] = 0.0f;
+  {
+    float sg = 0.0f;
+    const float lo = -__builtin_inff();
+    conv_all(dv, s.sl[0], lo, nullptr, sg);
+    conv_all(enc, s.sl[6], lo, nullptr, sg);
+    conv_all(enc + 16, s.sl[7], lo, nullptr, sg);
+  }
+  s.dh[0] = Bh<0>(s, 0);
+  s.dl[0] = Bl<0>(s, 0);
+  s.dh[1] = Bh<0>(s, 1);
+  s.dl[1] = Bl<0>(s, 1);
+#pragma unroll
+  for (int k = 0; k < kConsts / kThreads; ++k) blds[k * kThreads + threadIdx.x] = cst[k];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const int j = s.lane + 64 * k;
+    if (j < kCbStride) blds[kConsts + s.wave * kCbStride + j] = cbr[k];
+  }
+  __syncthreads();
+
+  // ---- layer_xyz1 (63 -> 256): 4 k-steps of encoding in slots 6, 7
+  {
+    float v[8];
+    bias_values(s, blds, kXyz1, v);
+    const bf16x8 one = ones_b(s.h);
+#pragma unroll
+    for (int ob = 0; ob < 8; ++ob) s.acc[ob] = bias_mfma(s.h == 0 ? v[ob] : 0.0f, one);
+    NoFill nf;
+    run_chunk<0>(s, a, lds, c, CN_SLOT_B(6), nf);
+    CopyFill cf{s};
+    run_chunk<6>(s, a, lds, c, CN_SLOT_B(7), cf);
+    copy_acc(s, 6);
+    copy_acc(s, 7);
+  }
+
+  // ---- layer_xyz2, fc_out, layer_dir1, layer_dir2: one loop body
+  for (int layer = kXyz2; layer <= kDir2; ++layer) {
+    // activation of the layer that produced the slots: none after fc_out (feat)
+    const float lo = layer == kDir1 ? -__builtin_inff() : 0.0f;
+    s.sig = 0.0f;
+    begin_layer(s, a, blds, layer, lo);
+    if (layer == kDir1) {
+      NoFill nf;
+      run_chunk<0>(s, a, lds, c, s.dh[0], s.dl[0], s.dh[1], s.dl[1], nf);
+    }
+    layer_chunk<0>(s, a, lds, c, blds, lo);
+    layer_chunk<1>(s, a, lds, c, blds, lo);
+    layer_chunk<2>(s, a, lds, c, blds, lo);
+    layer_chunk<3>(s, a, lds, c, blds, lo);
+    layer_chunk<4>(s, a, lds, c, blds, lo);
+    layer_chunk<5>(s, a, lds, c, blds, lo);
+    layer_chunk<6>(s, a, lds, c, blds, lo);
+    layer_chunk<7>(s, a, lds, c, blds, lo);
+    // fc_out's pass converted layer_xyz2's outputs: its partials are sigma's h2 term
+    if (layer == kOut) s.sigma = s.sig + __shfl_xor(s.sig, 32);
+  }
+  // sigma's code / bias term (cn_code_bias: b_out[0] + W_out[0, 256:] zs2)
+  if (s.uniform_code) s.sigma += lds_read1(blds + kConsts + s.wave * kCbStride + kCbSigma);
+  else s.sigma += a.code_bias[(int64_t)s.crow * kCbStride + kCbSigma];
 
   // ---- fc_rgb (256 -> 3): one chunk holding its 16 k-steps of block 0
-  init_acc(s, a, blds, kRgb);
-  chunk_barrier();
   {
-    const float4* slot = lds + (c & (kSlots - 1)) * kChunkQuads;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const float4* ap = slot + (k / 9) * kQuadsPerStep + (2 * (k % 9)) * 64 + s.lane;
-      mfma3(s.acc[0], __builtin_bit_cast(bf16x8, ap[0]), __builtin_bit_cast(bf16x8, ap[64]), s.bh[k], s.bl[k]);
+    if (s.uniform_code) {
+      const int i = s.lane & 31;
+      const float v = lds_read1(blds + kConsts + s.wave * kCbStride + kCbRgb + (i < 3 ? i : 0));
+      s.acc[0] = bias_mfma((s.h == 0 && i < 3) ? v : 0.0f, ones_b(s.h));
+    } else {
+      init_acc_per_lane(s, a, kRgb);
     }
+    {
+      float out[16];
+      conv_all(s.sl[0], out, 0.0f, nullptr, s.sig);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s.sl[0][i] = out[i];
+    }
+    chunk_barrier<0>();
+    const float4* slot = lds + (c & (kRing - 1)) * kChunkQuads + s.lane;
+#define CN_RGB(B)                                                                                      \
+  {                                                                                                    \
+    const float4* ap = slot + ((B) / 4) * kQuadsPerStep + (2 * ((2 * (B)) % 8)) * 64;                  \
+    mfma3(s.acc[0], __builtin_bit_cast(bf16x8, ap[0]), __builtin_bit_cast(bf16x8, ap[64]), Bh<B>(s, 0), \
+          Bl<B>(s, 0));                                                                                \
+    mfma3(s.acc[0], __builtin_bit_cast(bf16x8, ap[128]), __builtin_bit_cast(bf16x8, ap[192]),           \
+          Bh<B>(s, 1), Bl<B>(s, 1));                                                                   \
   }
-  // drain the dummy chunks' DMA before the workgroup's LDS is released
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#define CN_RGB_CONV(B)                                  \
+  {                                                     \
+    float out[16];                                      \
+    conv_all(s.sl[B], out, 0.0f, nullptr, s.sig);       \
+    _Pragma("unroll") for (int i = 0; i < 16; ++i) s.sl[B][i] = out[i]; \
+  }
+    CN_RGB(0) CN_RGB_CONV(1)
+    CN_RGB(1) CN_RGB_CONV(2)
+    CN_RGB(2) CN_RGB_CONV(3)
+    CN_RGB(3) CN_RGB_CONV(4)
+    CN_RGB(4) CN_RGB_CONV(5)
+    CN_RGB(5) CN_RGB_CONV(6)
+    CN_RGB(6) CN_RGB_CONV(7)
+    CN_RGB(7)
+#undef CN_RGB
+#undef CN_RGB_CONV
+  }
 
   if (valid && s.h == 0) {
     float4 o;
@@ -470,15 +682,15 @@ __global__ __launch_bounds__(kThreads, 1) void field_x3_kernel(FieldArgs a) {
   }
 }
 
-static_assert(kChunkRgb + 1 == kRealChunks, "chunk schedule");
-static_assert(kDmaPerWave * 64 * 4 == kChunkQuads, "chunk = 36 DMA wave-instructions");
+static_assert(kChunkRgb + 1 == kChunks, "chunk schedule");
+static_assert(kDmaPerWave * 64 * 4 == kChunkQuads, "chunk = 32 DMA wave-instructions");
 
 }  // namespace x3
 
 int64_t packed_floats_x3() { return x3::kPackedFloats; }
 
 int launch_pack_x3(const Params& P, float* packed, hipStream_t st) {
-  const int64_t n = (int64_t)x3::kQuads * 8 + 768;
+  const int64_t n = (int64_t)x3::kQuads * 8 + x3::kConsts;
   hipLaunchKernelGGL(x3::pack_x3_kernel, dim3(cn::elementwise_grid(n, 256)), dim3(256), 0, st, P, packed);
   return cn::launch_status();
 }
