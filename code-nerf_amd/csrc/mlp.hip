@@ -72,12 +72,19 @@ __global__ void pack_kernel(Params P, float* __restrict__ packed) {
 }
 
 // ---------------------------------------------------------------- code bias
-// One workgroup (16 waves) per code row: the three code layers (model.py:174-177),
-// then the code halves of layer_xyz2 / fc_out / fc_rgb plus their biases.  Each
-// output is one wave-wide dot product: 64 lanes read a 256-float weight row as
-// one coalesced float4 each, then a butterfly sum.
+// Per code row: the three code layers (model.py:174-177), then the code halves
+// of layer_xyz2 / fc_out / fc_rgb plus their biases.  Each code row is spread
+// over kCbSlices workgroups so the 1.5 MiB of weight rows are read by many CUs
+// at once (one CU per code was latency bound, ~85 us): slice q < 8 forms
+// xyz2 rows 32q..32q+31, slices 8..15 fc_out rows (slice 15 also row 256),
+// slice 16 the three fc_rgb rows.  Each slice first forms the one code-layer
+// vector it consumes (s1, s2 or t1; 256 dots, L2-resident weights after the
+// first slice touches them).  Every output is one wave-wide dot product: 64
+// lanes read a 256-float weight row as one coalesced float4 each, then a
+// butterfly sum.
 
-constexpr int kCbThreads = 1024;
+constexpr int kCbThreads = 512;
+constexpr int kCbSlices = 17;
 
 __device__ __forceinline__ float wave_dot256(const float* __restrict__ w, const float* v, int lane) {
   const float4 a = reinterpret_cast<const float4*>(w)[lane];
@@ -91,45 +98,47 @@ __device__ __forceinline__ float wave_dot256(const float* __restrict__ w, const 
 __global__ __launch_bounds__(kCbThreads) void code_bias_kernel(Params P, const float* __restrict__ z_s,
                                                                const float* __restrict__ z_t,
                                                                float* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) float zs[kCode], zt[kCode], s1[kCode], s2[kCode], t1[kCode];
-  const int c = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  __shared__ __attribute__((aligned(16))) float z[kCode], hv[kCode];
+  const int64_t c = blockIdx.x / kCbSlices;
+  const int q = blockIdx.x % kCbSlices, t = threadIdx.x, lane = t & 63, wave = t >> 6;
   constexpr int kW = kCbThreads / 64;
-  if (t < kCode) {
-    zs[t] = z_s[(int64_t)c * kCode + t];
-    zt[t] = z_t[(int64_t)c * kCode + t];
-  }
+  const int l = q < 8 ? 0 : (q < 16 ? 1 : 2);  // 0: s1 -> xyz2, 1: s2 -> fc_out, 2: t1 -> fc_rgb
+  if (t < kCode) z[t] = (l == 2 ? z_t : z_s)[c * kCode + t];
   __syncthreads();
-  for (int r = wave; r < 3 * kCode; r += kW) {
-    const int l = r / kCode, j = r % kCode;
-    const float* w = P.p[l == 0 ? kWSc1 : (l == 1 ? kWSc2 : kWTc1)] + j * kCode;
-    const float a = wave_dot256(w, l == 2 ? zt : zs, lane);
-    if (lane == 0) {
-      const float v = fmaxf(a + P.p[l == 0 ? kBSc1 : (l == 1 ? kBSc2 : kBTc1)][j], 0.f);
-      (l == 0 ? s1 : (l == 1 ? s2 : t1))[j] = v;
+  {
+    const float* W = P.p[l == 0 ? kWSc1 : (l == 1 ? kWSc2 : kWTc1)];
+    const float* B = P.p[l == 0 ? kBSc1 : (l == 1 ? kBSc2 : kBTc1)];
+#pragma unroll 8
+    for (int i = 0; i < kCode / kW; ++i) {
+      const int j = wave + i * kW;
+      const float a = wave_dot256(W + j * kCode, z, lane);
+      if (lane == 0) hv[j] = fmaxf(a + B[j], 0.f);
     }
   }
   __syncthreads();
-  float* o = out + (int64_t)c * kCbStride;
-  // rows: 0..255 layer_xyz2, 256..512 fc_out (row 0 = sigma), 513..515 fc_rgb
-  for (int r = wave; r < 2 * kCode + 4; r += kW) {
+  float* o = out + c * kCbStride;
+  int r0, nr;
+  if (l == 0) { r0 = 32 * q; nr = 32; }
+  else if (l == 1) { r0 = 32 * (q - 8); nr = q == 15 ? 33 : 32; }
+  else { r0 = 0; nr = 3; }
+  for (int r = r0 + wave; r < r0 + nr; r += kW) {
     const float* w;
-    const float* v;
     float b;
     int dst;
-    if (r < kCode) {
-      w = P.p[kWXyz2] + r * (kHidden + kCode) + kHidden; v = s1; b = P.p[kBXyz2][r]; dst = kCbXyz2 + r;
-    } else if (r < 2 * kCode + 1) {
-      const int i = r - kCode;  // fc_out row i
-      w = P.p[kWOut] + i * (kHidden + kCode) + kHidden; v = s2; b = P.p[kBOut][i];
+    if (l == 0) {
+      w = P.p[kWXyz2] + r * (kHidden + kCode) + kHidden; b = P.p[kBXyz2][r]; dst = kCbXyz2 + r;
+    } else if (l == 1) {
+      // slice rows 0..255 map to fc_out rows 1..256 (feat); row 256 -> fc_out row 0 (sigma)
+      const int i = r == kCode ? 0 : r + 1;
+      w = P.p[kWOut] + i * (kHidden + kCode) + kHidden; b = P.p[kBOut][i];
       dst = i == 0 ? kCbSigma : kCbFeat + i - 1;
     } else {
-      const int i = r - 2 * kCode - 1;
-      w = P.p[kWRgb] + i * (kHidden + kCode) + kHidden; v = t1; b = P.p[kBRgb][i]; dst = kCbRgb + i;
+      w = P.p[kWRgb] + r * (kHidden + kCode) + kHidden; b = P.p[kBRgb][r]; dst = kCbRgb + r;
     }
-    const float a = wave_dot256(w, v, lane);
+    const float a = wave_dot256(w, hv, lane);
     if (lane == 0) o[dst] = a + b;
   }
-  if (t >= 4 && t < 8) o[kCbRgb + t - 1] = 0.f;  // pad 516..519
+  if (l == 2 && t >= 3 && t < kCbStride - kCbRgb) o[kCbRgb + t] = 0.f;  // pad 516..519
 }
 
 // ---------------------------------------------------------------- field kernel
@@ -446,8 +455,8 @@ extern "C" int cn_code_bias(const float* const* params, const float* z_s, const 
                             int64_t n_codes, float* code_bias, cn_stream_t stream) {
   Params P;
   if (make_params(params, &P) != CN_OK) return CN_EINVAL;
-  CN_CHECK_ARG(z_s && z_t && code_bias && n_codes > 0 && n_codes <= (1ll << 31) - 1);
-  hipLaunchKernelGGL(code_bias_kernel, dim3(static_cast<unsigned>(n_codes)), dim3(kCbThreads), 0,
+  CN_CHECK_ARG(z_s && z_t && code_bias && n_codes > 0 && n_codes * kCbSlices <= (1ll << 31) - 1);
+  hipLaunchKernelGGL(code_bias_kernel, dim3(static_cast<unsigned>(n_codes * kCbSlices)), dim3(kCbThreads), 0,
                      cn::as_stream(stream), P, z_s, z_t, code_bias);
   return cn::launch_status();
 }

@@ -24,14 +24,26 @@
 // Weight stream.  Chunk = 2 k-steps x 8 blocks x {hi, lo} x 64 lanes quads =
 // 32 KiB, fragment-major so a wave's ds_read_b128 of one fragment is 1 KiB
 // contiguous (bank-conflict free); chunk c lies at packed + c * 32 KiB.  A 4-slot
-// LDS ring is filled by LDS-DMA (global_load_lds, 1 KiB per wave-instruction, 8 per
-// wave per chunk); chunk c+3 is issued when chunk c starts and a counted
-// `s_waitcnt vmcnt` + s_barrier retires chunk c.  No ordinary global load is live
-// in the stream, so the counted waits are exact.
+// LDS ring is filled by LDS-DMA (buffer_load_dwordx4 ... lds, 1 KiB per
+// wave-instruction, 8 per wave per chunk, offsets in SGPRs).  Each chunk is
+// split by ONE barrier M_c after its 4th MFMA group (of 8): M_c = chunk c+1
+// landed for every wave (counted `s_waitcnt vmcnt(8)`) and every wave is done
+// with chunk c-1.  Groups 0-3 of chunk c issue pieces 4-7 of chunk c+2, groups
+// 4-7 pieces 0-3 of chunk c+3 (slot of chunk c-1), one piece per group so the
+// DMA issue cost hides in MFMA gaps, and group 7 already reads chunk c+1's
+// first A fragments -- the MFMA pipe never waits for a chunk boundary.  No
+// ordinary global load is live in the stream, so the counted waits are exact.
+//
+// Persistent tiles.  The grid is one workgroup per CU; each loops over
+// 128-sample tiles.  The stream is cyclic (36 chunks, a multiple of the 4 ring
+// slots): the last three chunks of a tile prefetch the first three of the
+// next, so the ring never drains or re-primes between tiles.
 //
 // Code size.  The four 256-input layers run through ONE runtime loop whose body
 // is a single unrolled 16-k-step layer (a fully unrolled kernel is
 // instruction-fetch bound).
+#include <algorithm>
+
 #include "mlp_common.h"
 
 namespace cn {
@@ -149,10 +161,12 @@ struct State {
   int lane, h, wave;
   int crow;               // this lane's code-bias row
   bool uniform_code;      // all 32 samples of the wave use one code row
+  bf16x8 pre[4];          // next chunk's group-0 A fragments, read by the chunk before it
+  __amdgpu_buffer_rsrc_t wsrc;  // the packed stream as a buffer resource
+  unsigned voff;          // this lane's byte offset inside a 1 KiB-per-wave piece row
 };
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
-typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
 
 __device__ __forceinline__ bf16x8 dw8(const float* f) {
   const u32x4 u = {__float_as_uint(f[0]), __float_as_uint(f[1]), __float_as_uint(f[2]), __float_as_uint(f[3])};
@@ -205,29 +219,52 @@ __device__ __forceinline__ void conv_all(const float* raw, float* out, float lo,
   }
 }
 
-// Issue this wave's 8 DMA instructions of chunk c into ring slot c % 4.
-__device__ __forceinline__ void issue_chunk(const State& s, const float* __restrict__ packed, float4* lds, int c) {
-  const float4* src = reinterpret_cast<const float4*>(packed) + (c * kChunkQuads + s.wave * 64);
-  float4* slot = lds + (c & (kRing - 1)) * kChunkQuads + s.wave * 64;
-#pragma unroll
-  for (int i = 0; i < kDmaPerWave; ++i) {
+// One LDS-DMA piece: 1 KiB per wave (16 B per lane) of chunk `cn`, piece `i`
+// (piece i of chunk cn covers quads [i*256, i*256+256) of the chunk; this wave
+// moves quads i*256 + wave*64 + lane).
+__device__ __forceinline__ void dma_piece(const State& s, float4* lds, int cn, int i) {
 #ifndef CN_ABLATE_NO_DMA
-    __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src + i * 256 + s.lane), (lds_ptr_t)(slot + i * 256), 16, 0, 0);
+  const unsigned soff = __builtin_amdgcn_readfirstlane((unsigned)(cn * kChunkQuads + i * 256) * 16u);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(s.wsrc, (lds_ptr_t)(lds + (cn & (kRing - 1)) * kChunkQuads + i * 256 + s.wave * 64),
+                                           16, s.voff, soff, 0, 0);
 #endif
-  }
 }
 
-// Chunk c landed for every wave and every wave is done with chunk c-1 (its slot
-// is refilled next).  OUT = this wave's DMA instructions issued after chunk c.
-// One asm statement, so no LDS read can be scheduled across it.
+// The pieces running chunk c issues: groups 0-3 pieces 4-7 of chunk c+2, groups
+// 4-7 pieces 0-3 of chunk c+3, wrapping into the next tile's first chunks
+// (kChunks is a multiple of kRing, so the ring slot is unchanged by the wrap).
+struct Dma {
+  const State& s;
+  float4* lds;
+  int ca, cb;  // c+2, c+3 mod kChunks
+  template <int G>
+  __device__ __forceinline__ void piece() const {
+    if constexpr (G < 4) dma_piece(s, lds, ca, 4 + G);
+    else dma_piece(s, lds, cb, G - 4);
+  }
+};
+
+__device__ __forceinline__ Dma dma_for(const State& s, float4* lds, int c) {
+  const int ca = c + 2 < kChunks ? c + 2 : c + 2 - kChunks;
+  const int cb = c + 3 < kChunks ? c + 3 : c + 3 - kChunks;
+  return Dma{s, lds, ca, cb};
+}
+
+// M_c: chunk c+1 landed for every wave (all but this wave's OUT youngest DMA
+// pieces retired), every wave is past chunk c-1, and every LDS read of this
+// wave (incl. the asynchronous sigma-weight reads) has returned.  One asm
+// statement, so no LDS read can be scheduled across it.
 template <int OUT>
 __device__ __forceinline__ void chunk_barrier() {
-#ifdef CN_ABLATE_NO_DMA
+#if defined(CN_ABLATE_NO_BARRIER)
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" ::"n"(OUT) : "memory");
+#elif defined(CN_ABLATE_NO_DMA)
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #else
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(OUT) : "memory");
 #endif
 }
+constexpr int kMidOut = 8;  // chunk c+2's pieces are younger than chunk c+1's at M_c
 
 // Small LDS reads outside the ring (biases, sigma weights).  Inline asm: hipcc
 // cannot prove them disjoint from the in-flight DMA and would otherwise wait
@@ -374,12 +411,14 @@ __device__ __forceinline__ void load_a(const State& s, const float4* slot, bf16x
 }
 
 // Scheduling pattern of one group: 6 MFMAs, each followed by up to N VALU; the
-// next group's 4 A reads go out with the first two MFMAs.
-template <int N>
+// next group's 4 A reads go out with the first two MFMAs, the group's DMA piece
+// with the third.
+template <int N, bool READS = true>
 __device__ __forceinline__ void group_pattern() {
 #pragma unroll
   for (int m = 0; m < 6; ++m) {
-    if (m < 2) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    if (READS && m < 2) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    if (m == 2) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
     if constexpr (N > 0) __builtin_amdgcn_sched_group_barrier(0x002, N, 0);
   }
@@ -400,7 +439,22 @@ struct ConvFill {
   float out[16];
   template <int G>
   __device__ __forceinline__ void step() {
-    conv_piece<G>(s.sl[J], out, lo, w, s.sig);
+#ifndef CN_ABLATE_NO_FILL
+    // w (read asynchronously at the chunk start) is usable only after M_c, so the
+    // sigma products of pieces 0-3 are taken in steps 4-7 from the raw values
+    if constexpr (G < 4) {
+      conv_piece<G>(s.sl[J], out, lo, nullptr, s.sig);
+    } else {
+      conv_piece<G>(s.sl[J], out, lo, w, s.sig);
+      constexpr int K = G - 4;
+      const float v0 = vmax(s.sl[J][2 * K], lo), v1 = vmax(s.sl[J][2 * K + 1], lo);
+      s.sig = fmaf(w[2 * K], v0, s.sig);
+      s.sig = fmaf(w[2 * K + 1], v1, s.sig);
+    }
+#else
+    out[2 * G] = s.sl[J][2 * G];
+    out[2 * G + 1] = s.sl[J][2 * G + 1];
+#endif
     if constexpr (G == 7) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) s.sl[J][i] = out[i];
@@ -431,24 +485,38 @@ struct CopyFill {
 };
 
 // One 2-k-step chunk against the 8 output blocks: 8 groups (T, block pair) of 6
-// MFMAs; the A fragments of group g+1 are read during group g; fill.step<g>() is
-// VALU work (independent of the chunk) placed in group g's MFMA issue gaps.
-template <int NV, typename Fill>
-__device__ __forceinline__ void chunk_mfma(State& s, const float4* slot, bf16x8 bh0, bf16x8 bl0, bf16x8 bh1,
+// MFMAs; the A fragments of group g+1 are read during group g (group 7 reads
+// the next chunk's group 0 into s.pre when PREF); fill.step<g>() is VALU work
+// (independent of the chunk) placed in group g's MFMA issue gaps; group g also
+// issues one DMA piece; M_c sits between groups 3 and 4.  SELF: group 0's
+// fragments are read here (first chunk of a tile) instead of arriving in s.pre.
+template <int NV, bool SELF, bool PREF, typename Fill>
+__device__ __forceinline__ void chunk_mfma(State& s, float4* lds, int c, bf16x8 bh0, bf16x8 bl0, bf16x8 bh1,
                                            bf16x8 bl1, Fill& fill) {
+  const float4* slot = lds + (c & (kRing - 1)) * kChunkQuads;
+  const float4* nslot = lds + ((c + 1) & (kRing - 1)) * kChunkQuads;
+  const Dma dma = dma_for(s, lds, c);
   bf16x8 a0[4], a1[4];
-  load_a<0, 0>(s, slot, a0);
+  if constexpr (SELF) {
+    load_a<0, 0>(s, slot, a0);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a0[i] = s.pre[i];
+  }
   __builtin_amdgcn_sched_barrier(0);
 #define CN_GROUP(G, CUR, NXT)                                                     \
   {                                                                              \
     constexpr int T = (G) / 4, P = (G) % 4;                                      \
     if constexpr ((G) < 7) load_a<((G) + 1) / 4, ((G) + 1) % 4>(s, slot, NXT);  \
+    else if constexpr (PREF) load_a<0, 0>(s, nslot, s.pre);                      \
     const bf16x8 bh = T ? bh1 : bh0, bl = T ? bl1 : bl0;                         \
     mfma3(s.acc[2 * P], CUR[0], CUR[1], bh, bl);                                 \
     mfma3(s.acc[2 * P + 1], CUR[2], CUR[3], bh, bl);                             \
+    dma.template piece<G>();                                                     \
     fill.template step<G>();                                                     \
-    group_pattern<NV>();                                                         \
+    group_pattern<NV, ((G) < 7 || PREF)>();                                      \
     __builtin_amdgcn_sched_barrier(0);                                           \
+    if constexpr ((G) == 3) chunk_barrier<kMidOut>();                            \
   }
   CN_GROUP(0, a0, a1)
   CN_GROUP(1, a1, a0)
@@ -461,16 +529,11 @@ __device__ __forceinline__ void chunk_mfma(State& s, const float4* slot, bf16x8 
 #undef CN_GROUP
 }
 
-// Barrier, refill, MFMAs of chunk c.
-template <int NV, typename Fill>
+// Chunk c's MFMAs (with its DMA pieces and M_c inside).
+template <int NV, bool SELF = false, typename Fill>
 __device__ __forceinline__ void run_chunk(State& s, const FieldArgs& a, float4* lds, int& c, bf16x8 bh0, bf16x8 bl0,
                                           bf16x8 bh1, bf16x8 bl1, Fill& fill) {
-  if (c + 2 < kChunks) chunk_barrier<2 * kDmaPerWave>();
-  else if (c + 1 < kChunks) chunk_barrier<kDmaPerWave>();
-  else chunk_barrier<0>();
-  __builtin_amdgcn_sched_barrier(0);
-  if (c + 3 < kChunks) issue_chunk(s, a.packed, lds, c + 3);
-  chunk_mfma<NV>(s, lds + (c & (kRing - 1)) * kChunkQuads, bh0, bl0, bh1, bl1, fill);
+  chunk_mfma<NV, SELF, true>(s, lds, c, bh0, bl0, bh1, bl1, fill);
   ++c;
 }
 
@@ -514,32 +577,24 @@ __device__ __forceinline__ void begin_layer(State& s, const FieldArgs& a, const 
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// One 128-sample tile: inputs, encodings, the six layers (chunks 0..35 of the
+// stream, which also prefetch chunks 0..2 for the next tile), the raw store.
 template <int MODE>
-__global__ __launch_bounds__(kThreads, 1) void field_x3_kernel(FieldArgs a) {
-  // ONE LDS object (a second one makes hipcc wait vmcnt(0) before every ring read):
-  // the DMA ring, then the constant vectors and code rows
-  __shared__ __attribute__((aligned(16))) float4 lds[kLdsQuads + kBiasLds / 4];
-  float* blds = reinterpret_cast<float*>(lds + kLdsQuads);
-  State s;
-  s.lane = threadIdx.x & 63;
-  s.h = s.lane >> 5;
-  s.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+__device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4* lds, float* blds, int64_t tile) {
   s.sig = 0.0f;
   s.sigma = 0.0f;
-  const int64_t row = (int64_t)blockIdx.x * kTile + s.wave * 32 + (s.lane & 31);
+  const int64_t row = tile * kTile + s.wave * 32 + (s.lane & 31);
   const bool valid = row < a.m;
   const int64_t rc = valid ? row : a.m - 1;
 
-  // ---- per-sample inputs, constant vectors, code rows (ordinary loads); then prime the ring
+  // ---- per-sample inputs and this wave's code row (ordinary loads; the DMA in
+  // flight -- chunks 0..2 of this tile -- retires with them)
   const SampleIn in = decode_sample<MODE>(a, rc);
   s.crow = static_cast<int>(code_row(a, in.code_of));
   const int crow0 = __builtin_amdgcn_readfirstlane(s.crow);
   // wave-uniform by construction; readfirstlane makes it an SGPR so the bias
   // fast/slow choice is a scalar branch (a VGPR bool would run both paths masked)
   s.uniform_code = __builtin_amdgcn_readfirstlane(__ballot(s.crow != crow0) == 0 ? 1 : 0) != 0;
-  float cst[kConsts / kThreads];
-#pragma unroll
-  for (int k = 0; k < kConsts / kThreads; ++k) cst[k] = a.packed[kBiasXyz1 + k * kThreads + threadIdx.x];
   float cbr[9];
   {
     const float* src = a.code_bias + (int64_t)crow0 * kCbStride;
@@ -557,15 +612,17 @@ __global__ __launch_bounds__(kThreads, 1) void field_x3_kernel(FieldArgs a) {
     gather_pairs<6>(xr, kDimXyz, s.h, dv);
   }
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): every ordinary load has landed
-  issue_chunk(s, a.packed, lds, 0);
-  issue_chunk(s, a.packed, lds, 1);
-  issue_chunk(s, a.packed, lds, 2);
   int c = 0;
 
-  // ---- encodings (VALU, under the ring's first fills)
+  // ---- encodings (VALU)
   if constexpr (MODE != kFromEncoded) {
+#ifndef CN_ABLATE_NO_ENC
     encode_pairs<15, 10>(in.x, a.fx, s.h, enc);
     encode_pairs<6, 4>(in.vd, a.fd, s.h, dv);
+#else
+    for (int i = 0; i < 32; ++i) enc[i] = in.x[i % 3] * (float)(i + 1);
+    for (int i = 0; i < 16; ++i) dv[i] = in.vd[i % 3] * (float)(i + 1);
+#endif
   }
   dv[14] = 0.0f;
   dv[15] = 0.0f;
@@ -580,14 +637,12 @@ __global__ __launch_bounds__(kThreads, 1) void field_x3_kernel(FieldArgs a) {
   s.dl[0] = Bl<0>(s, 0);
   s.dh[1] = Bh<0>(s, 1);
   s.dl[1] = Bl<0>(s, 1);
-#pragma unroll
-  for (int k = 0; k < kConsts / kThreads; ++k) blds[k * kThreads + threadIdx.x] = cst[k];
+  // this wave's code row: read back only by this wave (LDS is in order per wave)
 #pragma unroll
   for (int k = 0; k < 9; ++k) {
     const int j = s.lane + 64 * k;
     if (j < kCbStride) blds[kConsts + s.wave * kCbStride + j] = cbr[k];
   }
-  __syncthreads();
 
   // ---- layer_xyz1 (63 -> 256): 4 k-steps of encoding in slots 6, 7
   {
@@ -597,7 +652,7 @@ __global__ __launch_bounds__(kThreads, 1) void field_x3_kernel(FieldArgs a) {
 #pragma unroll
     for (int ob = 0; ob < 8; ++ob) s.acc[ob] = bias_mfma(s.h == 0 ? v[ob] : 0.0f, one);
     NoFill nf;
-    run_chunk<0>(s, a, lds, c, CN_SLOT_B(6), nf);
+    run_chunk<0, true>(s, a, lds, c, CN_SLOT_B(6), nf);
     CopyFill cf{s};
     run_chunk<6>(s, a, lds, c, CN_SLOT_B(7), cf);
     copy_acc(s, 6);
@@ -629,7 +684,8 @@ __global__ __launch_bounds__(kThreads, 1) void field_x3_kernel(FieldArgs a) {
   if (s.uniform_code) s.sigma += lds_read1(blds + kConsts + s.wave * kCbStride + kCbSigma);
   else s.sigma += a.code_bias[(int64_t)s.crow * kCbStride + kCbSigma];
 
-  // ---- fc_rgb (256 -> 3): one chunk holding its 16 k-steps of block 0
+  // ---- fc_rgb (256 -> 3): one chunk holding its 16 k-steps of block 0; it
+  // prefetches chunk 2 of the next tile like any other chunk
   {
     if (s.uniform_code) {
       const int i = s.lane & 31;
@@ -644,15 +700,20 @@ __global__ __launch_bounds__(kThreads, 1) void field_x3_kernel(FieldArgs a) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) s.sl[0][i] = out[i];
     }
-    chunk_barrier<0>();
+    const Dma dma = dma_for(s, lds, c);
     const float4* slot = lds + (c & (kRing - 1)) * kChunkQuads + s.lane;
+    // group 0's fragments arrived in s.pre (frags 0-3 of k-step 0 = CN_RGB(0)'s)
 #define CN_RGB(B)                                                                                      \
   {                                                                                                    \
     const float4* ap = slot + ((B) / 4) * kQuadsPerStep + (2 * ((2 * (B)) % 8)) * 64;                  \
-    mfma3(s.acc[0], __builtin_bit_cast(bf16x8, ap[0]), __builtin_bit_cast(bf16x8, ap[64]), Bh<B>(s, 0), \
-          Bl<B>(s, 0));                                                                                \
-    mfma3(s.acc[0], __builtin_bit_cast(bf16x8, ap[128]), __builtin_bit_cast(bf16x8, ap[192]),           \
-          Bh<B>(s, 1), Bl<B>(s, 1));                                                                   \
+    const bf16x8 f0 = (B) == 0 ? s.pre[0] : __builtin_bit_cast(bf16x8, ap[0]);                         \
+    const bf16x8 f1 = (B) == 0 ? s.pre[1] : __builtin_bit_cast(bf16x8, ap[64]);                        \
+    const bf16x8 f2 = (B) == 0 ? s.pre[2] : __builtin_bit_cast(bf16x8, ap[128]);                       \
+    const bf16x8 f3 = (B) == 0 ? s.pre[3] : __builtin_bit_cast(bf16x8, ap[192]);                       \
+    mfma3(s.acc[0], f0, f1, Bh<B>(s, 0), Bl<B>(s, 0));                                                 \
+    dma.template piece<B>();                                                                           \
+    mfma3(s.acc[0], f2, f3, Bh<B>(s, 1), Bl<B>(s, 1));                                                 \
+    if constexpr ((B) == 3) chunk_barrier<kMidOut>();                                                  \
   }
 #define CN_RGB_CONV(B)                                  \
   {                                                     \
@@ -682,8 +743,42 @@ __global__ __launch_bounds__(kThreads, 1) void field_x3_kernel(FieldArgs a) {
   }
 }
 
+template <int MODE>
+__global__ __launch_bounds__(kThreads, 1) void field_x3_kernel(FieldArgs a) {
+  // ONE LDS object (a second one makes hipcc wait vmcnt(0) before every ring read):
+  // the DMA ring, then the constant vectors and code rows
+  __shared__ __attribute__((aligned(16))) float4 lds[kLdsQuads + kBiasLds / 4];
+  float* blds = reinterpret_cast<float*>(lds + kLdsQuads);
+  State s;
+  s.lane = threadIdx.x & 63;
+  s.h = s.lane >> 5;
+  s.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  s.wsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.packed), 0, kPackedFloats * 4, 0x00020000);
+  s.voff = static_cast<unsigned>(s.wave * 64 + s.lane) * 16u;
+
+  // constant vectors (biases, sigma weights) once per workgroup, then prime the ring
+#pragma unroll
+  for (int k = 0; k < kConsts / kThreads; ++k) blds[k * kThreads + threadIdx.x] = a.packed[kBiasXyz1 + k * kThreads + threadIdx.x];
+  __syncthreads();
+  // prime: chunks 0 and 1 and pieces 0-3 of chunk 2 (chunk 0's groups 0-3 issue the rest)
+#pragma unroll
+  for (int i = 0; i < kDmaPerWave; ++i) dma_piece(s, lds, 0, i);
+#pragma unroll
+  for (int i = 0; i < kDmaPerWave; ++i) dma_piece(s, lds, 1, i);
+#pragma unroll
+  for (int i = 0; i < kDmaPerWave / 2; ++i) dma_piece(s, lds, 2, i);
+
+  const int64_t n_tiles = (a.m + kTile - 1) / kTile;
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) field_tile<MODE>(s, a, lds, blds, tile);
+  // the last tile prefetched chunks 0..2 of a tile that does not exist: they
+  // must land before the workgroup's LDS is released
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+}
+
 static_assert(kChunkRgb + 1 == kChunks, "chunk schedule");
 static_assert(kDmaPerWave * 64 * 4 == kChunkQuads, "chunk = 32 DMA wave-instructions");
+static_assert(kDmaPerWave == 8, "one DMA piece per MFMA group (8 groups per chunk)");
+static_assert(kChunks % kRing == 0, "cyclic stream: chunk c + 36 reuses chunk c's ring slot");
 
 }  // namespace x3
 
@@ -695,8 +790,21 @@ int launch_pack_x3(const Params& P, float* packed, hipStream_t st) {
   return cn::launch_status();
 }
 
+// Workgroups of the persistent grid: one per CU (the kernel holds a CU's LDS and
+// every SIMD's registers), never more than there are tiles.
+static int64_t cu_count() {
+  static int n[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (n[dev] == 0) {
+    int v = 0;
+    n[dev] = (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ? v : 256;
+  }
+  return n[dev];
+}
+
 int launch_field_x3(int mode, FieldArgs& a, hipStream_t st) {
-  const unsigned grid = static_cast<unsigned>(cn::ceil_div(a.m, x3::kTile));
+  const unsigned grid = static_cast<unsigned>(std::min<int64_t>(cn::ceil_div(a.m, x3::kTile), cu_count()));
   switch (mode) {
     case kFromPts: hipLaunchKernelGGL(x3::field_x3_kernel<kFromPts>, dim3(grid), dim3(x3::kThreads), 0, st, a); break;
     case kFromRayZ: hipLaunchKernelGGL(x3::field_x3_kernel<kFromRayZ>, dim3(grid), dim3(x3::kThreads), 0, st, a); break;

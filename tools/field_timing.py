@@ -17,6 +17,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--precision", default="bf16x3")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--rays", type=int, nargs="+", default=[16384], help="ray counts (x64 samples) to time")
     ap.add_argument("--tag", default=os.path.basename(os.environ.get("CODENERF_LIB", "default")))
     args = ap.parse_args()
     from codenerf import ops, synthetic
@@ -26,7 +27,13 @@ def main():
     m.load_state_dict(synthetic.codenerf_params(0))
     m = m.to(dev)
     m.precision = args.precision
-    n, s = 16384, 64
+    for n in args.rays:
+        run(args, m, n, dev)
+
+
+def run(args, m, n, dev):
+    from codenerf import ops, synthetic
+    s = 64
     g = torch.Generator(device="cpu").manual_seed(0)
     ro = (torch.rand(n, 3, generator=g) * 0.2).to(dev)
     rd = torch.randn(n, 3, generator=g).to(dev)
@@ -46,7 +53,7 @@ def main():
     torch.cuda.synchronize()
     ms = sorted(a.elapsed_time(b) for a, b in ev)
     flop = n * s * 572416
-    print(json.dumps({"tag": args.tag, "precision": args.precision, "median_ms": ms[len(ms) // 2], "min_ms": ms[0],
+    print(json.dumps({"tag": args.tag, "rays": n, "precision": args.precision, "median_ms": ms[len(ms) // 2], "min_ms": ms[0],
                       "tflops": flop / (ms[len(ms) // 2] * 1e-3) / 1e12, "raw_checksum": float(raw.double().sum())}))
 
 
