@@ -73,6 +73,8 @@ def main():
     ap.add_argument("--hierarchical", action="store_true", help="also time the 64+64 (C3) render")
     ap.add_argument("--precision", default="bf16x3", choices=sorted(KERNELS))
     ap.add_argument("--no-f32-compare", action="store_true", help="skip the fp32-kernel side measurement")
+    ap.add_argument("--eval-iters", type=int, default=10,
+                    help="C5: time this many test-time-optimisation iterations (0 = skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -183,6 +185,9 @@ def main():
         dth, _, _ = timed(max(1, args.steps // 2), 1, coarse_only=False)
         extra["hierarchical_64_64_rays_per_s"] = n_img_rays * n * max(1, args.steps // 2) / dth
 
+    if args.eval_iters > 0:
+        extra["eval_c5"] = eval_bench(dev, rs, emb, models, args.eval_iters)
+
     traffic = None
     tpath = os.path.join(ROOT, "profiles", "field_kernel_traffic.json")
     if os.path.exists(tpath):
@@ -220,6 +225,50 @@ def main():
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def eval_bench(dev, rs, emb, models, iters):
+    """C5 (srn-cars-code-3080-val.yml): one eval.py:141-165 iteration = 2048 random rays, 64+64
+    perturbed samples, forward + backward through the HIP kernels into (codes, theta, phi, rho),
+    AdamW step.  Weights frozen (their grads are never read by the reference's optimiser)."""
+    import numpy as np
+    from codenerf.evaluate import eval_step_loss
+    from codenerf.nerf import PointSampler
+    ps = PointSampler(NC, NF, NEAR, FAR, "lindepth", True, torch.float32, dev)
+    rs.sample_size = 2048
+    target = torch.rand(H * W, 4, generator=torch.Generator().manual_seed(3)).to(dev)
+    mods = {"nerf_coarse": models[0], "nerf_fine": models[1]}
+    saved = [(m, m.precision) for m in models]
+    for m in models:
+        m.requires_grad_(False)
+    zs = (torch.randn(1, 256, generator=torch.Generator().manual_seed(4)) * 0.3).to(dev).requires_grad_(True)
+    zt = (torch.randn(1, 256, generator=torch.Generator().manual_seed(5)) * 0.3).to(dev).requires_grad_(True)
+    th = torch.tensor([1.57], device=dev).requires_grad_(True)
+    ph = torch.tensor([0.0], device=dev).requires_grad_(True)
+    rh = torch.tensor([1.3], device=dev).requires_grad_(True)
+    opt = torch.optim.AdamW([{"params": [zs, zt]}, {"params": [th, ph]}, {"params": [rh]}], lr=1e-2)
+    np.random.seed(0)
+
+    def it():
+        loss, _ = eval_step_loss(th, ph, rh, zs, zt, target, (rs, ps), emb, mods, 1e-5)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+
+    for _ in range(2):
+        it()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        it()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / iters
+    for m, prec in saved:
+        m.requires_grad_(True)
+        m.precision = prec
+    return {"ms_per_iter": dt * 1e3, "rays_per_s": 2048 / dt, "rays_per_iter": 2048, "samples": "64+64 perturbed",
+            "note": "forward+backward through the fp32 training field kernel; host-side numpy ray permutation "
+                    "and the per-iteration .item() logging of eval.py included"}
 
 
 def cpu_baseline(img, k, poses, n):

@@ -18,54 +18,84 @@ namespace grad {
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 // ---------------------------------------------------------------- GEMMs
-constexpr int kBM = 64, kBN = 64, kBK = 32;
 
-// 64x64 tile per 256-thread block; wave (wr, wc) owns a 32x32 quadrant.
+// gemm_nn: 256 x 64 output tile per 256-thread block, 64 x 64 per wave (2 x 2
+// v_mfma_f32_32x32x2_f32 tiles, 64 accumulators).  k runs in tiles of 16; inside
+// a tile lane half h owns k = h*8 .. h*8+7, so MFMA step kk pairs k = kk and
+// 8 + kk -- any pairing of k between the A and B operands gives the same sum,
+// and this one makes each lane's A values 8 consecutive floats of its row (read
+// straight from global memory, no LDS) and its B values 8 consecutive floats
+// of B^T.  B^T (64 columns x K) is staged in LDS once per block.
+constexpr int kNT = 64, kMT = 256, kKT = 16;
+constexpr int kMaxK = 288;  // B^T tile in LDS: 64 x 288 floats = 72 KiB
+
 __global__ __launch_bounds__(256) void gemm_nn_kernel(const float* __restrict__ A, int64_t lda,
                                                       const float* __restrict__ B, int64_t ldb,
                                                       float* __restrict__ C, int64_t ldc,
                                                       const float* __restrict__ mask, int64_t ldm,
                                                       int64_t M, int N, int K) {
-  __shared__ float As[kBM][kBK + 1];
-  __shared__ float Bs[kBK][kBN];
+  __shared__ __attribute__((aligned(16))) float Bt[kNT][kMaxK + 4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
-  const int64_t m0 = (int64_t)blockIdx.x * kBM;
-  const int n0 = blockIdx.y * kBN;
-  floatx16 acc = {0};
-  for (int k0 = 0; k0 < K; k0 += kBK) {
-#pragma unroll
-    for (int i = 0; i < (kBM * kBK) / 256; ++i) {
-      const int e = i * 256 + tid, r = e / kBK, c = e % kBK;
-      const int64_t m = m0 + r;
-      As[r][c] = (m < M && k0 + c < K) ? A[m * lda + k0 + c] : 0.0f;
-    }
-#pragma unroll
-    for (int i = 0; i < (kBK * kBN) / 256; ++i) {
-      const int e = i * 256 + tid, r = e / kBN, c = e % kBN;
-      Bs[r][c] = (k0 + r < K && n0 + c < N) ? B[(int64_t)(k0 + r) * ldb + n0 + c] : 0.0f;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int kk = 0; kk < kBK; kk += 2) {
-      const float a = As[32 * wr + (lane & 31)][kk + (lane >> 5)];
-      const float b = Bs[kk + (lane >> 5)][32 * wc + (lane & 31)];
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
-    }
-    __syncthreads();
+  const int i = lane & 31, h = lane >> 5;
+  const int n0 = blockIdx.y * kNT;
+  const int kp = (K + kKT - 1) / kKT * kKT;
+  // B^T: Bt[n][k] = B[k][n0 + n] (zero outside K x N)
+  for (int e = tid; e < kNT * kp; e += 256) {
+    const int k = e / kNT, n = e % kNT;
+    Bt[n][k] = (k < K && n0 + n < N) ? B[(int64_t)k * ldb + n0 + n] : 0.0f;
   }
-  const int col = n0 + 32 * wc + (lane & 31);
+  __syncthreads();
+  const int64_t m0 = (int64_t)blockIdx.x * kMT + wave * 64;
+  int64_t rows[2];
+  bool rv[2];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int64_t m = m0 + 32 * wr + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-    if (m < M && col < N) {
-      float v = acc[r];
-      if (mask && !(mask[m * ldm + col] > 0.0f)) v = 0.0f;  // ReLU'(x) = [x > 0], torch's threshold_backward
-      C[m * ldc + col] = v;
-    }
+  for (int t = 0; t < 2; ++t) {
+    rows[t] = m0 + 32 * t + i;
+    rv[t] = rows[t] < M;
+    if (!rv[t]) rows[t] = M - 1;
   }
+  floatx16 acc[2][2] = {};
+  for (int k0 = 0; k0 < kp; k0 += kKT) {
+    float a[2][8], b[2][8];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const float* ar = A + rows[t] * lda + k0 + h * 8;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) a[t][q] = (k0 + h * 8 + q < K) ? ar[q] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const float4* bp = reinterpret_cast<const float4*>(&Bt[32 * u + i][k0 + h * 8]);
+      const float4 x = bp[0], y = bp[1];
+      b[u][0] = x.x; b[u][1] = x.y; b[u][2] = x.z; b[u][3] = x.w;
+      b[u][4] = y.x; b[u][5] = y.y; b[u][6] = y.z; b[u][7] = y.w;
+    }
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[t][kk], b[u][kk], acc[t][u], 0, 0, 0);
+  }
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int col = n0 + 32 * u + i;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t m = m0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (m < M && col < N) {
+          float v = acc[t][u][r];
+          if (mask && !(mask[m * ldm + col] > 0.0f)) v = 0.0f;  // ReLU'(x) = [x > 0], torch's threshold_backward
+          C[m * ldc + col] = v;
+        }
+      }
+    }
 }
 
+constexpr int kBN = 64, kBK = 32;  // gemm_tn tiles
 constexpr int kSliceM = 2048;  // rows reduced per block before the atomic flush
 
 __global__ __launch_bounds__(256) void gemm_tn_kernel(const float* __restrict__ A, int64_t lda,
@@ -105,29 +135,72 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(const float* __restrict__ 
   }
 }
 
-// out[code(m)][j * ostride] += A[m][j] for j < N; code(m) = code_index ? code_index[m / S]
-// : (n_codes == 1 ? 0 : m / S).  Each thread owns a column and walks a row slice,
-// flushing when the code changes (rows of one ray are contiguous).
+// out[code(m)][j] += A[m][j] for j < N; code(m) = code_index ? code_index[m / S]
+// : (n_codes == 1 ? 0 : m / S).  Block = 4 waves over kSegRows consecutive rows
+// and 64 columns: lane j of a wave owns column c0 + j (each row read is one
+// coalesced 256-B segment), walks its quarter of the rows and flushes when the
+// code changes (rows of one ray are contiguous, so the code is wave-uniform).
+// Runs of one code are reduced across the 4 waves in LDS first, so the common
+// single-code case costs one atomic per column per block.
+constexpr int kSegRows = 1024;
+
+__device__ __forceinline__ int64_t seg_code(int64_t m, int64_t S, const int64_t* code_index, int64_t n_codes) {
+  const int64_t ray = m / S;
+  return code_index ? code_index[ray] : (n_codes == 1 ? 0 : ray);
+}
+
 __global__ __launch_bounds__(256) void seg_sum_kernel(const float* __restrict__ A, int64_t lda, int64_t M,
                                                       int N, int64_t S, const int64_t* __restrict__ code_index,
                                                       int64_t n_codes, float* __restrict__ out,
                                                       int64_t out_ld) {
-  const int64_t mb = (int64_t)blockIdx.x * kSliceM, me = min(M, mb + kSliceM);
-  for (int j = threadIdx.x; j < N; j += blockDim.x) {
-    float sum = 0.0f;
-    int64_t cur = -1;
-    for (int64_t m = mb; m < me; ++m) {
-      const int64_t ray = m / S;
-      const int64_t code = code_index ? code_index[ray] : (n_codes == 1 ? 0 : ray);
-      if (code != cur) {
-        if (cur >= 0) atomicAdd(&out[cur * out_ld + j], sum);
-        cur = code;
-        sum = 0.0f;
-      }
-      sum += A[m * lda + j];
-    }
-    if (cur >= 0) atomicAdd(&out[cur * out_ld + j], sum);
+  __shared__ float part[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.y * 64 + lane;
+  const int64_t mb = (int64_t)blockIdx.x * kSegRows, me = min(M, mb + kSegRows);
+  // one code over the whole block: fast path with a cross-wave LDS reduction
+  const int64_t code0 = seg_code(mb, S, code_index, n_codes);
+  int diff = 0;
+  if (code_index) {
+    for (int64_t r = mb / S + threadIdx.x; r <= (me - 1) / S; r += blockDim.x) diff |= code_index[r] != code0;
+  } else {
+    diff = n_codes != 1 && (mb / S) != ((me - 1) / S);
   }
+  const bool one = !__syncthreads_or(diff);
+  constexpr int kQ = kSegRows / 4;
+  const int64_t qb = mb + (int64_t)wave * kQ, qe = min(me, qb + kQ);
+  if (one) {
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    if (c < N) {
+      int64_t m = qb;
+      for (; m + 4 <= qe; m += 4) {
+        s0 += A[m * lda + c];
+        s1 += A[(m + 1) * lda + c];
+        s2 += A[(m + 2) * lda + c];
+        s3 += A[(m + 3) * lda + c];
+      }
+      for (; m < qe; ++m) s0 += A[m * lda + c];
+    }
+    part[wave][lane] = (s0 + s1) + (s2 + s3);
+    __syncthreads();
+    if (wave == 0 && c < N) {
+      const float t = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+      atomicAdd(&out[code0 * out_ld + c], t);
+    }
+    return;
+  }
+  if (c >= N || qb >= qe) return;
+  float sum = 0.0f;
+  int64_t cur = seg_code(qb, S, code_index, n_codes);
+  for (int64_t m = qb; m < qe; ++m) {
+    const int64_t code = seg_code(m, S, code_index, n_codes);
+    if (code != cur) {
+      atomicAdd(&out[cur * out_ld + c], sum);
+      cur = code;
+      sum = 0.0f;
+    }
+    sum += A[m * lda + c];
+  }
+  atomicAdd(&out[cur * out_ld + c], sum);
 }
 
 // ---------------------------------------------------------------- element-wise pieces
@@ -318,7 +391,8 @@ namespace {
 
 int gemm_nn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, const float* mask,
             int64_t ldm, int64_t M, int N, int K, hipStream_t st) {
-  dim3 grid(static_cast<unsigned>(ceil_div(M, grad::kBM)), static_cast<unsigned>(ceil_div(N, grad::kBN)));
+  if (K > grad::kMaxK) return CN_EINVAL;
+  dim3 grid(static_cast<unsigned>(ceil_div(M, grad::kMT)), static_cast<unsigned>(ceil_div(N, grad::kNT)));
   hipLaunchKernelGGL(grad::gemm_nn_kernel, grid, dim3(256), 0, st, A, lda, B, ldb, C, ldc, mask, ldm, M, N, K);
   return launch_status();
 }
@@ -333,7 +407,8 @@ int gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, 
 
 int seg_sum(const float* A, int64_t lda, int64_t M, int N, int64_t S, const int64_t* code_index, int64_t n_codes,
             float* out, int64_t out_ld, hipStream_t st) {
-  hipLaunchKernelGGL(grad::seg_sum_kernel, dim3(static_cast<unsigned>(ceil_div(M, grad::kSliceM))), dim3(256), 0, st,
+  dim3 grid(static_cast<unsigned>(ceil_div(M, grad::kSegRows)), static_cast<unsigned>(ceil_div(N, 64)));
+  hipLaunchKernelGGL(grad::seg_sum_kernel, grid, dim3(256), 0, st,
                      A, lda, M, N, S, code_index, n_codes, out, out_ld);
   return launch_status();
 }
@@ -348,7 +423,7 @@ int seg_sum(const float* A, int64_t lda, int64_t M, int N, int64_t S, const int6
 
 extern "C" int cn_gemm_nn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
                           const float* mask, int64_t ldm, int64_t M, int64_t N, int64_t K, cn_stream_t stream) {
-  CN_CHECK_ARG(A && B && C && M > 0 && N > 0 && K > 0 && N <= 65536 && K <= 65536);
+  CN_CHECK_ARG(A && B && C && M > 0 && N > 0 && K > 0 && N <= 65536 && K <= 288);
   CN_CHECK_ARG(lda >= K && ldb >= N && ldc >= N && (!mask || ldm >= N));
   return gemm_nn(A, lda, B, ldb, C, ldc, mask, ldm, M, (int)N, (int)K, as_stream(stream));
 }

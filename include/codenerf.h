@@ -242,7 +242,7 @@ int cn_ray_points_backward(const float* g_pts, const float* z, int64_t n_rays, i
                            float* d_ro, float* d_rd, cn_stream_t stream);
 
 /* fp32 MFMA GEMMs the backward is built from (row-major, leading dims in floats):
- *   cn_gemm_nn: C[M][N] = A[M][K] B[K][N], zeroed where mask[m][n] <= 0 (mask may be NULL);
+ *   cn_gemm_nn: C[M][N] = A[M][K] B[K][N], zeroed where mask[m][n] <= 0 (mask may be NULL); K <= 288;
  *   cn_gemm_tn: C[N][K] += sum_m A[M][N] B[M][K] (accumulates). */
 int cn_gemm_nn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
                const float* mask, int64_t ldm, int64_t M, int64_t N, int64_t K, cn_stream_t stream);

@@ -67,7 +67,7 @@ def embedders(dev):
 # ---------------------------------------------------------------- GEMM building blocks
 
 
-@pytest.mark.parametrize("m,n,k", [(1000, 257, 283), (64, 3, 256), (4097, 256, 27)])
+@pytest.mark.parametrize("m,n,k", [(1000, 257, 283), (64, 3, 256), (4097, 256, 27), (20001, 256, 256), (300, 63, 3)])
 def test_gemm_nn_masked(dev, m, n, k):
     from codenerf import ops
     g = torch.Generator().manual_seed(m + n + k)
