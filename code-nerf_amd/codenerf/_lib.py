@@ -18,8 +18,8 @@ LIB_PATH = os.environ.get("CODENERF_LIB", os.path.join(_HERE, "lib", "libcodener
 
 CN_OK, CN_EINVAL, CN_EUNSUPPORTED = 0, -1, -2
 CN_NUM_PARAMS = 18
-CN_FMT_F32, CN_FMT_BF16X3 = 0, 1
-FORMATS = {"f32": CN_FMT_F32, "bf16x3": CN_FMT_BF16X3}
+CN_FMT_F32, CN_FMT_BF16X3, CN_FMT_BF16X3_T = 0, 1, 2
+FORMATS = {"f32": CN_FMT_F32, "bf16x3": CN_FMT_BF16X3, "bf16x3_t": CN_FMT_BF16X3_T}
 CN_CODE_BIAS_STRIDE = 520
 
 _p = ctypes.c_void_p
@@ -51,6 +51,10 @@ SIGNATURES = {
     "cn_field_backward_workspace_floats": (_i64, [_i64]),
     "cn_field_backward": (_i, [ctypes.POINTER(_p), _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p, _i64, _fp, _fp,
                                _p, ctypes.POINTER(_p), _p, _p, _p, _p, _p]),
+    "cn_field_mask_words": (_i64, [_i64]),
+    "cn_radiance_field_masks": (_i, [_p, _p, _p, _i64, _p, _p, _p, _p, _i64, _i64, _i64, _fp, _fp, _p, _p, _p]),
+    "cn_field_backward_x3": (_i, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p, _i64, _fp, _fp, _p, _p, _p, _p,
+                                  _p]),
     "cn_code_bias_backward": (_i, [ctypes.POINTER(_p), _p, _p, _i64, _p, _p, _p, ctypes.POINTER(_p), _p]),
     "cn_volume_render_backward": (_i, [_p, _p, _p, _i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p]),
     "cn_ray_bundle_backward": (_i, [_p, _i64, _i64, _p, _p, _p, _p]),

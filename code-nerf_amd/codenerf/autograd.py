@@ -8,9 +8,10 @@ Every forward and backward runs on the gfx950 kernels through the C ABI;
 torch only allocates buffers and routes gradients.
 
 When no input requires grad each wrapper returns the plain op result and
-records nothing.  The differentiable field always runs the fp32 kernel
-(``cn_radiance_field_train``), which also stores the activations the backward
-reads; the bf16x3 format is an inference-only choice.
+records nothing.  The differentiable field runs, for frozen weights and a
+bf16x3 model (the eval step), the 3xbf16 kernel with ReLU masks and the fused
+backward kernel; otherwise the fp32 kernel (``cn_radiance_field_train``) that
+stores the activations the layer-wise backward reads.
 """
 from __future__ import annotations
 
@@ -130,8 +131,9 @@ def _c(t):
 class _FieldMeta:
     """Non-tensor arguments of the field Functions."""
 
-    def __init__(self, n_samples, chunk_rows, fx, fd, code_index=None):
+    def __init__(self, n_samples, chunk_rows, fx, fd, code_index=None, precision="f32"):
         self.n_samples, self.chunk_rows = n_samples, chunk_rows
+        self.precision = precision
         self.fx, self.fd = list(fx) if fx is not None else None, list(fd) if fd is not None else None
         self.code_index = code_index
 
@@ -147,12 +149,29 @@ class RadianceField(torch.autograd.Function):
 
     Inputs: rd (R,3), pts (R,S,3) or (ro (R,3), z (R,S)), code rows z_s/z_t (n_codes, 256),
     then the 18 parameters in state_dict order.  Output raw (R, S, 4).
+
+    With frozen weights (the eval step) and a bf16x3 model the forward is the
+    3xbf16 field kernel writing ReLU masks and the backward ONE fused kernel
+    (cn_field_backward_x3); otherwise the fp32 training kernel keeps the
+    activations for the layer-wise backward (weight gradients).
     """
 
     @staticmethod
     def forward(ctx, meta, rd, pts, ro, z, z_s, z_t, *params):
         params = [p.detach() for p in params]
         cb = ops.code_bias(params, z_s, z_t)
+        n_rays = rd.shape[0]
+        fused = (meta.precision == "bf16x3" and not any(ctx.needs_input_grad[7:])
+                 and ops.fused_backward_supported(z_s.shape[0], meta.n_samples, meta.code_index))
+        ctx.fused = fused
+        if fused:
+            raw, masks = ops.radiance_field_masks(ops.mlp_pack(params, "bf16x3"), cb, rd, meta.n_samples,
+                                                  meta.chunk_rows, meta.fx, meta.fd, pts=pts, ro=ro, z=z,
+                                                  code_index=meta.code_index)
+            ctx.masks = masks
+            ctx.meta = meta
+            ctx.save_for_backward(rd, pts, ro, z, z_s, z_t, *params)
+            return raw
         packed = ops.mlp_pack(params, "f32")
         raw, saved = ops.radiance_field_train(packed, cb, rd, meta.n_samples, meta.chunk_rows, meta.fx, meta.fd,
                                               pts=pts, ro=ro, z=z, code_index=meta.code_index)
@@ -166,6 +185,17 @@ class RadianceField(torch.autograd.Function):
         rd, pts, ro, z, z_s, z_t, *params = ctx.saved_tensors
         needs = ctx.needs_input_grad
         meta = ctx.meta
+        if ctx.fused:
+            want_z = needs[5] or needs[6]
+            r = ops.field_backward_x3(ops.mlp_pack(params, "bf16x3_t"), ctx.masks, g_raw.contiguous(), rd.shape[0],
+                                      meta.n_samples, meta.chunk_rows, z_s.shape[0], meta.fx, meta.fd, rd=rd,
+                                      pts=pts, ro=ro, z=z, code_index=meta.code_index, want_pts=needs[2],
+                                      want_ro=needs[3], want_rd=needs[1])
+            dz_s = dz_t = None
+            if want_z:
+                dz_s, dz_t = ops.code_bias_backward(params, z_s, z_t, r["g_code"], None, want_z=True)
+            ctx.masks = None
+            return (None, r["d_rd"], r["d_pts"], r["d_ro"], None, dz_s, dz_t, *([None] * len(params)))
         pg = _param_grad_buffers(params, needs[7:])
         want_z = needs[5] or needs[6]
         r = ops.field_backward(params, ctx.acts, ctx.x_enc, g_raw.contiguous(), rd.shape[0], meta.n_samples,
@@ -259,5 +289,5 @@ def mlp_forward_autograd(model, z_s, z_t, x):
 def radiance_field_autograd(model, rd, z_s, z_t, chunk_rows, fx, fd, pts=None, ro=None, z=None):
     cs, ct = _code_rows(z_s, z_t)
     n_samples = pts.shape[1] if pts is not None else z.shape[1]
-    meta = _FieldMeta(n_samples, chunk_rows, fx, fd)
+    meta = _FieldMeta(n_samples, chunk_rows, fx, fd, precision=getattr(model, "precision", "f32"))
     return RadianceField.apply(meta, rd, pts, ro, _d(z), cs, ct, *model.param_list())

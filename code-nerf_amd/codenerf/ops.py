@@ -181,7 +181,8 @@ def mlp_pack(params: Sequence[Tensor], precision: str = "f32") -> Tensor:
     """Pack a CodeNeRFModel state_dict (model.py:145-156, state_dict order) for the field kernel.
 
     precision "f32": fp32 fragments for v_mfma_f32_32x32x2_f32; "bf16x3": bf16 hi/lo
-    fragments for the 3-product split on v_mfma_f32_32x32x16_bf16 (include/codenerf.h).
+    fragments for the 3-product split on v_mfma_f32_32x32x16_bf16 (include/codenerf.h);
+    "bf16x3_t": the transposed 3xbf16 pack of the fused backward.
     """
     lib = _lib_ready()
     assert len(params) == _lib.CN_NUM_PARAMS, "expected the 18 CodeNeRFModel weight/bias tensors"
@@ -473,3 +474,62 @@ def ray_points_backward(g_pts: Tensor, z: Tensor, want_ro: bool = True, want_rd:
         check(lib.cn_ray_points_backward(ptr(g_pts), ptr(z), n, s, ptr(d_ro), ptr(d_rd), stream_of(z)),
               "cn_ray_points_backward")
     return d_ro, d_rd
+
+
+# ------------------------------------------------------------------ fused 3xbf16 backward (eval step)
+
+
+def radiance_field_masks(packed: Tensor, cb: Tensor, rd: Tensor, n_samples: int, chunk_rows: int,
+                         freqs_xyz: Sequence[float], freqs_dir: Sequence[float], pts: Optional[Tensor] = None,
+                         ro: Optional[Tensor] = None, z: Optional[Tensor] = None,
+                         code_index: Optional[Tensor] = None) -> Tuple[Tensor, Tensor]:
+    """3xbf16 radiance_field that also writes the ReLU masks -> raw (R,S,4), masks (uint32 words as int32)."""
+    lib = _lib_ready()
+    rd = _cuda(rd, "rd")
+    n = rd.shape[0]
+    if pts is not None:
+        pts = _cuda(pts, "pts")
+        assert pts.shape == (n, n_samples, 3)
+    else:
+        ro, z = _cuda(ro, "ro"), _cuda(z, "z")
+        assert z.shape == (n, n_samples)
+    if code_index is not None:
+        code_index = _cuda(code_index, "code_index", torch.int64)
+    m = n * n_samples
+    raw = torch.empty(n, n_samples, 4, device=rd.device, dtype=torch.float32)
+    masks = torch.empty(int(lib.cn_field_mask_words(m)), device=rd.device, dtype=torch.int32)
+    check(lib.cn_radiance_field_masks(ptr(packed), ptr(cb), ptr(code_index), cb.shape[0], ptr(pts), ptr(ro), ptr(rd),
+                                      ptr(z), n, n_samples, chunk_rows, _lib.host_floats(freqs_xyz),
+                                      _lib.host_floats(freqs_dir), ptr(raw), ptr(masks), stream_of(rd)),
+          "cn_radiance_field_masks")
+    return raw, masks
+
+
+def fused_backward_supported(n_codes: int, n_samples: int, code_index: Optional[Tensor] = None) -> bool:
+    """cn_field_backward_x3 needs one code row per 32 consecutive samples."""
+    return n_codes == 1 or n_samples % 32 == 0
+
+
+def field_backward_x3(packed_t: Tensor, masks: Tensor, d_raw: Tensor, n_rays: int, n_samples: int,
+                      chunk_rows: int, n_codes: int, freqs_xyz: Sequence[float], freqs_dir: Sequence[float],
+                      rd: Tensor, pts: Optional[Tensor] = None, ro: Optional[Tensor] = None,
+                      z: Optional[Tensor] = None, code_index: Optional[Tensor] = None, want_pts: bool = False,
+                      want_ro: bool = False, want_rd: bool = False):
+    """Fused backward of forward_pass + CodeNeRFModel.forward (frozen weights) -> g_code / d_pts / d_ro / d_rd."""
+    lib = _lib_ready()
+    m = n_rays * n_samples
+    d_raw = _cuda(d_raw, "d_raw")
+    assert d_raw.numel() == 4 * m
+    dev = d_raw.device
+    rd, pts, ro, z = _opt(rd, "rd"), _opt(pts, "pts"), _opt(ro, "ro"), _opt(z, "z")
+    if code_index is not None:
+        code_index = _cuda(code_index, "code_index", torch.int64)
+    g_code = torch.zeros(n_codes, _lib.CN_CODE_BIAS_STRIDE, device=dev, dtype=torch.float32)
+    d_pts = torch.empty(n_rays, n_samples, 3, device=dev, dtype=torch.float32) if want_pts else None
+    d_ro = torch.zeros(n_rays, 3, device=dev, dtype=torch.float32) if want_ro else None
+    d_rd = torch.zeros(n_rays, 3, device=dev, dtype=torch.float32) if want_rd else None
+    check(lib.cn_field_backward_x3(ptr(packed_t), ptr(masks), ptr(d_raw), ptr(pts), ptr(ro), ptr(rd), ptr(z),
+                                   n_rays, n_samples, chunk_rows, ptr(code_index), n_codes,
+                                   _lib.host_floats(freqs_xyz), _lib.host_floats(freqs_dir), ptr(g_code),
+                                   ptr(d_pts), ptr(d_ro), ptr(d_rd), stream_of(d_raw)), "cn_field_backward_x3")
+    return {"g_code": g_code, "d_pts": d_pts, "d_ro": d_ro, "d_rd": d_rd}

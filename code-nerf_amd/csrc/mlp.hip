@@ -431,6 +431,7 @@ int launch_field(int fmt, int mode, FieldArgs& a, hipStream_t st) {
 }
 
 bool valid_fmt(int fmt) { return fmt == CN_FMT_F32 || fmt == CN_FMT_BF16X3; }
+bool valid_pack_fmt(int fmt) { return valid_fmt(fmt) || fmt == CN_FMT_BF16X3_T; }
 
 }  // namespace
 
@@ -438,14 +439,15 @@ static_assert(kPackedFloats == 327424, "packed layout changed: update docs");
 static_assert(kCbStride == CN_CODE_BIAS_STRIDE, "code-bias stride mismatch");
 
 extern "C" int64_t cn_mlp_packed_floats(int fmt) {
-  if (!valid_fmt(fmt)) return -1;
-  return fmt == CN_FMT_BF16X3 ? packed_floats_x3() : kPackedFloats;
+  if (!valid_pack_fmt(fmt)) return -1;
+  return fmt == CN_FMT_F32 ? kPackedFloats : packed_floats_x3();
 }
 
 extern "C" int cn_mlp_pack(const float* const* params, int fmt, float* packed, cn_stream_t stream) {
   Params P;
-  if (make_params(params, &P) != CN_OK || !packed || !valid_fmt(fmt)) return CN_EINVAL;
+  if (make_params(params, &P) != CN_OK || !packed || !valid_pack_fmt(fmt)) return CN_EINVAL;
   if (fmt == CN_FMT_BF16X3) return launch_pack_x3(P, packed, cn::as_stream(stream));
+  if (fmt == CN_FMT_BF16X3_T) return launch_pack_x3t(P, packed, cn::as_stream(stream));
   hipLaunchKernelGGL(pack_kernel, dim3(cn::elementwise_grid(kPackedFloats, 256)), dim3(256), 0,
                      cn::as_stream(stream), P, packed);
   return cn::launch_status();
@@ -553,4 +555,74 @@ extern "C" int cn_mlp_forward_train(const float* packed, const float* code_bias,
   a.raw = raw;
   a.save = save;
   return launch_field(CN_FMT_F32, kFromEncoded, a, cn::as_stream(stream));
+}
+
+extern "C" int64_t cn_field_mask_words(int64_t m) { return m > 0 ? mask_words_x3(m) : -1; }
+
+extern "C" int cn_radiance_field_masks(const float* packed, const float* code_bias, const int64_t* code_index,
+                                       int64_t n_codes, const float* pts, const float* ro, const float* rd,
+                                       const float* z, int64_t n_rays, int64_t n_samples, int64_t chunk_rows,
+                                       const float* freqs_xyz, const float* freqs_dir, float* raw, uint32_t* masks,
+                                       cn_stream_t stream) {
+  CN_CHECK_ARG(packed && code_bias && rd && raw && masks && freqs_xyz && freqs_dir);
+  CN_CHECK_ARG(n_rays > 0 && n_samples > 0 && chunk_rows > 0 && n_codes > 0);
+  CN_CHECK_ARG(pts || (ro && z));
+  CN_CHECK_ARG(code_index || n_codes == 1 || n_codes == n_rays);
+  FieldArgs a = {};
+  a.packed = packed;
+  a.code_bias = code_bias;
+  a.code_index = code_index;
+  a.n_codes = n_codes;
+  a.pts = pts;
+  a.ro = ro;
+  a.rd = rd;
+  a.z = z;
+  a.n_rays = n_rays;
+  a.n_samples = n_samples;
+  a.chunk_rows = chunk_rows;
+  a.m = n_rays * n_samples;
+  CN_CHECK_ARG(cn::ceil_div(a.m, kTile) <= 0x7fffffff);
+  for (int i = 0; i < 10; ++i) a.fx[i] = freqs_xyz[i];
+  for (int i = 0; i < 4; ++i) a.fd[i] = freqs_dir[i];
+  a.raw = raw;
+  a.masks = masks;
+  return launch_field_x3(pts ? kFromPts : kFromRayZ, a, cn::as_stream(stream));
+}
+
+extern "C" int cn_field_backward_x3(const float* packed_t, const uint32_t* masks, const float* d_raw,
+                                    const float* pts, const float* ro, const float* rd, const float* z,
+                                    int64_t n_rays, int64_t n_samples, int64_t chunk_rows,
+                                    const int64_t* code_index, int64_t n_codes, const float* freqs_xyz,
+                                    const float* freqs_dir, float* g_code, float* d_pts, float* d_ro, float* d_rd,
+                                    cn_stream_t stream) {
+  CN_CHECK_ARG(packed_t && masks && d_raw && rd && g_code && freqs_xyz && freqs_dir);
+  CN_CHECK_ARG(n_rays > 0 && n_samples > 0 && chunk_rows > 0 && n_codes > 0);
+  CN_CHECK_ARG(pts || (ro && z));
+  CN_CHECK_ARG(!d_pts || pts);
+  CN_CHECK_ARG(!d_ro || (ro && z && !pts));
+  CN_CHECK_ARG(code_index || n_codes == 1 || n_codes == n_rays);
+  // one code row per 32-sample wave: a single code, or every wave inside one ray
+  if (!(n_codes == 1 || n_samples % 32 == 0)) return CN_EUNSUPPORTED;
+  FieldArgs a = {};
+  a.packed = packed_t;
+  a.code_index = code_index;
+  a.n_codes = n_codes;
+  a.pts = pts;
+  a.ro = ro;
+  a.rd = rd;
+  a.z = z;
+  a.n_rays = n_rays;
+  a.n_samples = n_samples;
+  a.chunk_rows = chunk_rows;
+  a.m = n_rays * n_samples;
+  CN_CHECK_ARG(cn::ceil_div(a.m, kTile) <= 0x7fffffff);
+  for (int i = 0; i < 10; ++i) a.fx[i] = freqs_xyz[i];
+  for (int i = 0; i < 4; ++i) a.fd[i] = freqs_dir[i];
+  a.masks = const_cast<uint32_t*>(masks);
+  a.d_raw = d_raw;
+  a.g_code = g_code;
+  a.d_pts = d_pts;
+  a.d_ro = d_ro;
+  a.d_rd = d_rd;
+  return launch_field_x3_bwd(pts ? kFromPts : kFromRayZ, a, cn::as_stream(stream));
 }

@@ -37,6 +37,13 @@ struct FieldArgs {
   float fd[4];
   float* raw;
   float* save;  // fp32 kernel only: (5, m, 256) post-activation h1, h2, feat, v1, v2 for the backward
+  // 3xbf16 training forward / fused backward (mlp_x3.hip)
+  unsigned* masks;       // ReLU masks, kMaskWordsPerTile per 128-sample tile
+  const float* d_raw;    // backward: dL/draw (m, 4)
+  float* g_code;         // backward: (n_codes, kCbStride) accumulated
+  float* d_pts;          // backward: (m, 3) written (kFromPts)
+  float* d_ro;           // backward: (n_rays, 3) accumulated (kFromRayZ)
+  float* d_rd;           // backward: (n_rays, 3) accumulated
 };
 
 // One sample's inputs: point, unit Q1 view direction, code row.
@@ -105,10 +112,14 @@ __device__ __forceinline__ void encode_pairs(const float* x, const float* f, int
   }
 }
 
-// 3xbf16 variant (mlp_x3.hip).
+// 3xbf16 variant (mlp_x3.hip): forward (optionally writing ReLU masks) and the
+// fused backward over the transposed pack.
 int64_t packed_floats_x3();
 int launch_pack_x3(const Params& P, float* packed, hipStream_t st);
+int launch_pack_x3t(const Params& P, float* packed, hipStream_t st);
 int launch_field_x3(int mode, FieldArgs& a, hipStream_t st);
+int64_t mask_words_x3(int64_t m);
+int launch_field_x3_bwd(int mode, FieldArgs& a, hipStream_t st);
 
 // Pre-encoded rows: the same 2P+2 values gathered from x (base = column offset).
 template <int P, int T = 0>

@@ -162,6 +162,7 @@ struct State {
   int crow;               // this lane's code-bias row
   bool uniform_code;      // all 32 samples of the wave use one code row
   bf16x8 pre[4];          // next chunk's group-0 A fragments, read by the chunk before it
+  unsigned mw[4];         // training forward: ReLU mask words being built for the current layer
   __amdgpu_buffer_rsrc_t wsrc;  // the packed stream as a buffer resource
   unsigned voff;          // this lane's byte offset inside a 1 KiB-per-wave piece row
 };
@@ -187,14 +188,21 @@ __device__ __forceinline__ float vmax(float x, float lo) {
 
 // Values 2K, 2K+1 of a raw block -> activation, hi/lo bf16 into `out` (k-step
 // K/4, dword K%4); sig += w . v (the sigma dot product, kept only in fc_out).
+// mb (training forward): bits 2K, 2K+1 of the slot's 16-bit ReLU mask |= [v > 0]
+// (v is post-activation, so >= +0: the mask bit is min(bits(v), 1)).
 template <int K>
-__device__ __forceinline__ void conv_piece(const float* raw, float* out, float lo_clamp, const float* w, float& sig) {
+__device__ __forceinline__ void conv_piece(const float* raw, float* out, float lo_clamp, const float* w, float& sig,
+                                           unsigned* mb = nullptr) {
   f32x2 v;
   v.x = vmax(raw[2 * K], lo_clamp);
   v.y = vmax(raw[2 * K + 1], lo_clamp);
   if (w) {
     sig = fmaf(w[2 * K], v.x, sig);
     sig = fmaf(w[2 * K + 1], v.y, sig);
+  }
+  if (mb) {
+    *mb |= min(__float_as_uint(v.x), 1u) << (2 * K);
+    *mb |= min(__float_as_uint(v.y), 1u) << (2 * K + 1);
   }
   const bf16x2 hb = __builtin_convertvector(v, bf16x2);
   const unsigned hu = __builtin_bit_cast(unsigned, hb);
@@ -212,11 +220,18 @@ __device__ __forceinline__ void conv_piece(const float* raw, float* out, float l
 }
 
 template <int K = 0>
-__device__ __forceinline__ void conv_all(const float* raw, float* out, float lo, const float* w, float& sig) {
+__device__ __forceinline__ void conv_all(const float* raw, float* out, float lo, const float* w, float& sig,
+                                         unsigned* mb = nullptr) {
   if constexpr (K < 8) {
-    conv_piece<K>(raw, out, lo, w, sig);
-    conv_all<K + 1>(raw, out, lo, w, sig);
+    conv_piece<K>(raw, out, lo, w, sig, mb);
+    conv_all<K + 1>(raw, out, lo, w, sig, mb);
   }
+}
+
+// The 16 mask bits of slot J go to bits 16 (J & 1) .. of word J >> 1.
+template <int J>
+__device__ __forceinline__ void put_mask(unsigned* mw, unsigned mb) {
+  mw[J >> 1] |= mb << (16 * (J & 1));
 }
 
 // One LDS-DMA piece: 1 KiB per wave (16 B per lane) of chunk `cn`, piece `i`
@@ -263,6 +278,7 @@ __device__ __forceinline__ void chunk_barrier() {
 #else
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(OUT) : "memory");
 #endif
+  __builtin_amdgcn_sched_barrier(0);  // nothing (ring reads included) is scheduled above the wait
 }
 constexpr int kMidOut = 8;  // chunk c+2's pieces are younger than chunk c+1's at M_c
 
@@ -431,21 +447,22 @@ struct NoFill {
 
 // Convert slot J (raw block of the previous layer) into packed B operands, one
 // pair of values per group; sigma partial alongside.
-template <int J>
+template <int J, bool MASKS = false>
 struct ConvFill {
   State& s;
   float lo;
   float w[16];  // sigma weights of this slot
   float out[16];
+  unsigned mb;
   template <int G>
   __device__ __forceinline__ void step() {
 #ifndef CN_ABLATE_NO_FILL
     // w (read asynchronously at the chunk start) is usable only after M_c, so the
     // sigma products of pieces 0-3 are taken in steps 4-7 from the raw values
     if constexpr (G < 4) {
-      conv_piece<G>(s.sl[J], out, lo, nullptr, s.sig);
+      conv_piece<G>(s.sl[J], out, lo, nullptr, s.sig, MASKS ? &mb : nullptr);
     } else {
-      conv_piece<G>(s.sl[J], out, lo, w, s.sig);
+      conv_piece<G>(s.sl[J], out, lo, w, s.sig, MASKS ? &mb : nullptr);
       constexpr int K = G - 4;
       const float v0 = vmax(s.sl[J][2 * K], lo), v1 = vmax(s.sl[J][2 * K + 1], lo);
       s.sig = fmaf(w[2 * K], v0, s.sig);
@@ -458,6 +475,7 @@ struct ConvFill {
     if constexpr (G == 7) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) s.sl[J][i] = out[i];
+      if constexpr (MASKS) put_mask<J>(s.mw, mb);
     }
   }
 };
@@ -539,11 +557,11 @@ __device__ __forceinline__ void run_chunk(State& s, const FieldArgs& a, float4* 
 
 // Chunk J of a 256-input layer: B from slot J, converting slot J+1 meanwhile
 // (the last chunk copies the accumulators out instead).
-template <int J>
+template <int J, bool MASKS = false>
 __device__ __forceinline__ void layer_chunk(State& s, const FieldArgs& a, float4* lds, int& c, const float* blds,
                                             float lo) {
   if constexpr (J < 7) {
-    ConvFill<J + 1> f{s, lo, {}, {}};
+    ConvFill<J + 1, MASKS> f{s, lo, {}, {}, 0u};
     lds_read16_async(blds + kSigmaOff + (s.h * 8 + J + 1) * 16, f.w);
     run_chunk<2>(s, a, lds, c, CN_SLOT_B(J), f);
   } else {
@@ -555,32 +573,53 @@ __device__ __forceinline__ void layer_chunk(State& s, const FieldArgs& a, float4
 }
 
 // Bias-initialise the accumulators of `layer` while converting slot 0.
+template <bool MASKS = false>
 __device__ __forceinline__ void begin_layer(State& s, const FieldArgs& a, const float* blds, int layer, float lo) {
   float w[16];
   lds_read16(blds + kSigmaOff + (s.h * 8) * 16, w);
   float out[16];
+  unsigned mb = 0;
+  unsigned* mbp = MASKS ? &mb : nullptr;
   if (s.uniform_code || !(layer == kXyz2 || layer == kOut)) {
     float v[8];
     bias_values(s, blds, layer, v);
     const bf16x8 one = ones_b(s.h);
 #define CN_BIAS(B)                                   \
   s.acc[B] = bias_mfma(s.h == 0 ? v[B] : 0.0f, one); \
-  conv_piece<B>(s.sl[0], out, lo, w, s.sig);
+  conv_piece<B>(s.sl[0], out, lo, w, s.sig, mbp);
     CN_BIAS(0) CN_BIAS(1) CN_BIAS(2) CN_BIAS(3) CN_BIAS(4) CN_BIAS(5) CN_BIAS(6) CN_BIAS(7)
 #undef CN_BIAS
   } else {
     init_acc_per_lane(s, a, layer);
-    conv_all(s.sl[0], out, lo, w, s.sig);
+    conv_all(s.sl[0], out, lo, w, s.sig, mbp);
   }
 #pragma unroll
   for (int i = 0; i < 16; ++i) s.sl[0][i] = out[i];
+  if constexpr (MASKS) put_mask<0>(s.mw, mb);
   __builtin_amdgcn_sched_barrier(0);
+}
+
+// Training forward: the 4 mask words of one converted layer (tile, wave, slot l
+// of kMaskLayers) as one 16-B store per lane.
+constexpr int kMaskLayers = 5;  // h1, h2, feat (unused), v1, v2
+constexpr int kMaskWordsPerTile = kWaves * kMaskLayers * 64 * 4;
+__device__ __forceinline__ void store_masks(State& s, const FieldArgs& a, int64_t tile, int l) {
+  uint4 v;
+  v.x = s.mw[0];
+  v.y = s.mw[1];
+  v.z = s.mw[2];
+  v.w = s.mw[3];
+  reinterpret_cast<uint4*>(a.masks)[((tile * kWaves + s.wave) * kMaskLayers + l) * 64 + s.lane] = v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) s.mw[i] = 0u;
 }
 
 // One 128-sample tile: inputs, encodings, the six layers (chunks 0..35 of the
 // stream, which also prefetch chunks 0..2 for the next tile), the raw store.
-template <int MODE>
+template <int MODE, bool MASKS>
 __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4* lds, float* blds, int64_t tile) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) s.mw[i] = 0u;
   s.sig = 0.0f;
   s.sigma = 0.0f;
   const int64_t row = tile * kTile + s.wave * 32 + (s.lane & 31);
@@ -664,19 +703,21 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
     // activation of the layer that produced the slots: none after fc_out (feat)
     const float lo = layer == kDir1 ? -__builtin_inff() : 0.0f;
     s.sig = 0.0f;
-    begin_layer(s, a, blds, layer, lo);
+    begin_layer<MASKS>(s, a, blds, layer, lo);
     if (layer == kDir1) {
       NoFill nf;
       run_chunk<0>(s, a, lds, c, s.dh[0], s.dl[0], s.dh[1], s.dl[1], nf);
     }
-    layer_chunk<0>(s, a, lds, c, blds, lo);
-    layer_chunk<1>(s, a, lds, c, blds, lo);
-    layer_chunk<2>(s, a, lds, c, blds, lo);
-    layer_chunk<3>(s, a, lds, c, blds, lo);
-    layer_chunk<4>(s, a, lds, c, blds, lo);
-    layer_chunk<5>(s, a, lds, c, blds, lo);
-    layer_chunk<6>(s, a, lds, c, blds, lo);
-    layer_chunk<7>(s, a, lds, c, blds, lo);
+    layer_chunk<0, MASKS>(s, a, lds, c, blds, lo);
+    layer_chunk<1, MASKS>(s, a, lds, c, blds, lo);
+    layer_chunk<2, MASKS>(s, a, lds, c, blds, lo);
+    layer_chunk<3, MASKS>(s, a, lds, c, blds, lo);
+    layer_chunk<4, MASKS>(s, a, lds, c, blds, lo);
+    layer_chunk<5, MASKS>(s, a, lds, c, blds, lo);
+    layer_chunk<6, MASKS>(s, a, lds, c, blds, lo);
+    layer_chunk<7, MASKS>(s, a, lds, c, blds, lo);
+    // the conversions of this pass were the previous layer's outputs: h1, h2, feat, v1
+    if constexpr (MASKS) store_masks(s, a, tile, layer - kXyz2);
     // fc_out's pass converted layer_xyz2's outputs: its partials are sigma's h2 term
     if (layer == kOut) s.sigma = s.sig + __shfl_xor(s.sig, 32);
   }
@@ -696,9 +737,11 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
     }
     {
       float out[16];
-      conv_all(s.sl[0], out, 0.0f, nullptr, s.sig);
+      unsigned mb = 0;
+      conv_all(s.sl[0], out, 0.0f, nullptr, s.sig, MASKS ? &mb : nullptr);
 #pragma unroll
       for (int i = 0; i < 16; ++i) s.sl[0][i] = out[i];
+      if constexpr (MASKS) put_mask<0>(s.mw, mb);
     }
     const Dma dma = dma_for(s, lds, c);
     const float4* slot = lds + (c & (kRing - 1)) * kChunkQuads + s.lane;
@@ -715,11 +758,13 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
     mfma3(s.acc[0], f2, f3, Bh<B>(s, 1), Bl<B>(s, 1));                                                 \
     if constexpr ((B) == 3) chunk_barrier<kMidOut>();                                                  \
   }
-#define CN_RGB_CONV(B)                                  \
-  {                                                     \
-    float out[16];                                      \
-    conv_all(s.sl[B], out, 0.0f, nullptr, s.sig);       \
-    _Pragma("unroll") for (int i = 0; i < 16; ++i) s.sl[B][i] = out[i]; \
+#define CN_RGB_CONV(B)                                                     \
+  {                                                                        \
+    float out[16];                                                         \
+    unsigned mb = 0;                                                       \
+    conv_all(s.sl[B], out, 0.0f, nullptr, s.sig, MASKS ? &mb : nullptr);   \
+    _Pragma("unroll") for (int i = 0; i < 16; ++i) s.sl[B][i] = out[i];    \
+    if constexpr (MASKS) put_mask<B>(s.mw, mb);                            \
   }
     CN_RGB(0) CN_RGB_CONV(1)
     CN_RGB(1) CN_RGB_CONV(2)
@@ -733,6 +778,7 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
 #undef CN_RGB_CONV
   }
 
+  if constexpr (MASKS) store_masks(s, a, tile, 4);  // v2
   if (valid && s.h == 0) {
     float4 o;
     o.x = s.acc[0][0];
@@ -743,7 +789,7 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
   }
 }
 
-template <int MODE>
+template <int MODE, bool MASKS>
 __global__ __launch_bounds__(kThreads, 1) void field_x3_kernel(FieldArgs a) {
   // ONE LDS object (a second one makes hipcc wait vmcnt(0) before every ring read):
   // the DMA ring, then the constant vectors and code rows
@@ -769,7 +815,7 @@ __global__ __launch_bounds__(kThreads, 1) void field_x3_kernel(FieldArgs a) {
   for (int i = 0; i < kDmaPerWave / 2; ++i) dma_piece(s, lds, 2, i);
 
   const int64_t n_tiles = (a.m + kTile - 1) / kTile;
-  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) field_tile<MODE>(s, a, lds, blds, tile);
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) field_tile<MODE, MASKS>(s, a, lds, blds, tile);
   // the last tile prefetched chunks 0..2 of a tile that does not exist: they
   // must land before the workgroup's LDS is released
   __builtin_amdgcn_s_waitcnt(0x0F70);
@@ -779,6 +825,535 @@ static_assert(kChunkRgb + 1 == kChunks, "chunk schedule");
 static_assert(kDmaPerWave * 64 * 4 == kChunkQuads, "chunk = 32 DMA wave-instructions");
 static_assert(kDmaPerWave == 8, "one DMA piece per MFMA group (8 groups per chunk)");
 static_assert(kChunks % kRing == 0, "cyclic stream: chunk c + 36 reuses chunk c's ring slot");
+
+
+// ================================================================ fused backward
+// The eval-step backward (frozen weights) of forward_pass + CodeNeRFModel.forward
+// (nerf/__init__.py:94-134, model.py:160-194): from d raw (m, 4) to the per-code
+// sums g_code and the ray gradients, in one persistent launch on the forward's
+// machinery.  dX = dPre . W is computed as D = W^T . dPre^T: A = W^T streamed
+// through the same ring (a transposed pack, again 36 chunks), B = dPre in the
+// slots.  The ReLU masks come from the training forward (field_x3_kernel<.., true>:
+// 128 bits per lane per layer).  Chunk schedule:
+//   0      fc_rgb^T      d v2   = Wr^T d_rgb                          (k-step 0 real)
+//   1-8    layer_dir2^T  d v1   = Wd2^T (m_v2 . d v2)
+//   9-16   layer_dir1^T  d feat = Wd1[:, :256]^T (m_v1 . d v1)
+//   17     layer_dir1^T  d dir  = Wd1[:, 256:]^T (m_v1 . d v1)        (1 block x 16 k-steps)
+//   18-25  fc_out^T      d h2   = Wo[1:, :256]^T d feat + Wo[0, :256] d sigma (rank-1 init MFMA)
+//   26-33  layer_xyz2^T  d h1   = Wx2[:, :256]^T (m_h2 . d h2)
+//   34-35  layer_xyz1^T  d enc  = Wx1^T (m_h1 . d h1)                  (2 blocks x 16 k-steps)
+// The output rows of the two encoding layers are ordered like the forward's
+// encoding k-steps (k_from_enc), so each lane half back-propagates through the
+// sin/cos pairs it owns with one sincosf per pair, as in the forward.
+// g_code = sum over a code's samples of [m_h2 . d h2 | d feat | d sigma | d rgb]
+// (cn_code_bias layout): 8-lane DPP sums + LDS float atomics into one row per
+// wave, flushed to global atomics when the wave's code row changes.
+
+constexpr int kTChunkD1 = 9, kTChunkDir = 17, kTChunkOut = 18, kTChunkX2 = 26, kTChunkX1 = 34;
+constexpr int kTSigmaCol = 0, kTZeros = 256;  // transposed-pack constants: fc_out row 0 over h2, zeros
+// LDS after the ring: constants, one g_code row per wave, a shared dummy target
+// for the lanes of a reduction that hold no sum (lane offset + largest column).
+constexpr int kGaccOff = kConsts;
+constexpr int kDummyOff = kGaccOff + kWaves * kCbStride;
+constexpr int kBwdLdsFloats = kDummyOff + 64 + kCbStride;
+
+// Accumulator coordinates of A row rho of a block: register and lane half.
+__host__ __device__ constexpr int reg_of_row(int rho) { return (rho & 3) + 4 * (rho >> 3); }
+__host__ __device__ constexpr int half_of_row(int rho) { return (rho >> 2) & 1; }
+
+__global__ void pack_x3t_kernel(Params P, float* __restrict__ packed) {
+  unsigned short* q16 = reinterpret_cast<unsigned short*>(packed);
+  const int n_elems = kQuads * 8;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n_elems + kConsts; idx += gridDim.x * blockDim.x) {
+    if (idx >= n_elems) {
+      const int j = idx - n_elems;
+      packed[kBiasXyz1 + j] = j < 256 ? P.p[kWOut][j] : 0.0f;  // fc_out row 0, h2 half
+      continue;
+    }
+    const int quad = idx >> 3, e = idx & 7;
+    const int c = quad / kChunkQuads;
+    int r = quad % kChunkQuads;
+    const int T = r / kQuadsPerStep;
+    r %= kQuadsPerStep;
+    const int frag = r / 64, lane = r % 64;
+    const int slot = frag >> 1, part = frag & 1;
+    const int i = lane & 31, h = lane >> 5;
+    float w = 0.0f;
+    if (c == 0) {  // fc_rgb^T: k = rgb channel e (lane half 0, k-step 0)
+      if (T == 0 && h == 0 && e < 3) w = P.p[kWRgb][e * (kHidden + kCode) + 32 * slot + i];
+    } else if (c < kTChunkDir) {
+      const bool d2 = c < kTChunkD1;
+      const int ks = 2 * (c - (d2 ? 1 : kTChunkD1)) + T;
+      const int kf = acc_row(ks >> 1, 8 * (ks & 1) + e, h);
+      w = d2 ? P.p[kWDir2][kf * kHidden + 32 * slot + i] : P.p[kWDir1][kf * (kCode + kDimDir) + 32 * slot + i];
+    } else if (c == kTChunkDir) {
+      const int ks = 8 * T + slot;
+      const int kf = acc_row(ks >> 1, 8 * (ks & 1) + e, h);
+      const int t = reg_of_row(i);
+      const int col = t < 14 ? k_from_enc(t, half_of_row(i), 6) : -1;
+      if (col >= 0) w = P.p[kWDir1][kf * (kCode + kDimDir) + kCode + col];
+    } else if (c < kTChunkX1) {
+      const bool out = c < kTChunkX2;
+      const int ks = 2 * (c - (out ? kTChunkOut : kTChunkX2)) + T;
+      const int kf = acc_row(ks >> 1, 8 * (ks & 1) + e, h);
+      w = out ? P.p[kWOut][(1 + kf) * (kHidden + kCode) + 32 * slot + i]
+              : P.p[kWXyz2][kf * (kHidden + kCode) + 32 * slot + i];
+    } else {  // layer_xyz1^T: 2 blocks x 16 k-steps over 2 chunks
+      const int q = c - kTChunkX1;
+      const int ks = 8 * q + 4 * T + (slot >> 1), ob = slot & 1;
+      const int kf = acc_row(ks >> 1, 8 * (ks & 1) + e, h);
+      const int col = k_from_enc(16 * ob + reg_of_row(i), half_of_row(i), 15);
+      if (col >= 0) w = P.p[kWXyz1][kf * kDimXyz + col];
+    }
+    const __bf16 hi = static_cast<__bf16>(w);
+    const float lo = w - static_cast<float>(hi);
+    q16[idx] = part == 0 ? bf16_bits(w) : bf16_bits(lo);
+  }
+}
+
+// ---- backward pieces
+
+// Masked value: raw if bit `bit` of word m is set, else +0.
+__device__ __forceinline__ float masked(float raw, unsigned m, int bit) {
+  return __uint_as_float(__float_as_uint(raw) &
+                         static_cast<unsigned>(__builtin_amdgcn_sbfe(static_cast<int>(m), bit, 1)));
+}
+
+// Values 2K, 2K+1 of raw slot (mask word m, bits from `off`) -> hi/lo bf16 into
+// `out` (conv_piece's layout); the masked values are returned for reductions.
+template <int K>
+__device__ __forceinline__ void convm_piece(const float* raw, float* out, unsigned m, int off, float& vx, float& vy) {
+  f32x2 v;
+  v.x = masked(raw[2 * K], m, off + 2 * K);
+  v.y = masked(raw[2 * K + 1], m, off + 2 * K + 1);
+  vx = v.x;
+  vy = v.y;
+  const bf16x2 hb = __builtin_convertvector(v, bf16x2);
+  const unsigned hu = __builtin_bit_cast(unsigned, hb);
+  f32x2 back;
+  back.x = __uint_as_float(hu << 16);
+  back.y = __uint_as_float(hu & 0xffff0000u);
+  const bf16x2 lb = __builtin_convertvector(v - back, bf16x2);
+  unsigned hi_w = hu, lo_w = __builtin_bit_cast(unsigned, lb);
+  asm volatile("" : "+v"(hi_w), "+v"(lo_w));
+  constexpr int t = K / 4, d = K % 4;
+  out[8 * t + d] = __uint_as_float(hi_w);
+  out[8 * t + 4 + d] = __uint_as_float(lo_w);
+}
+
+// Sum over each group of 8 lanes; lanes with (lane & 7) == 7 hold the sums.
+__device__ __forceinline__ float sum8(float x) {
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xF, 0xF, true));   // quad_perm 1,0,3,2
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4E, 0xF, 0xF, true));   // quad_perm 2,3,0,1
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x114, 0xF, 0xF, true));  // row_shr:4
+  return x;
+}
+
+// LDS float atomic at byte address base + IMM (no return).
+template <int IMM>
+__device__ __forceinline__ void ds_add(unsigned base, float v) {
+  asm volatile("ds_add_f32 %0, %1 offset:%2" ::"v"(base), "v"(v), "i"(IMM));
+}
+
+// Row R of block J (lane half h) is feature acc_row(J, R, h); its g_code column
+// sits at gbase + 4 * acc_row(J, R, 0) bytes (gbase carries the 4h and the
+// layer's column offset; lanes that hold no sum point at the dummy row).
+template <int J, int R>
+__device__ __forceinline__ void red_add(unsigned gbase, float v) {
+  ds_add<4 * acc_row(J, R, 0)>(gbase, sum8(v));
+}
+
+// Convert slot J of a backward pass (mask words mw; RED: also sum into g_code).
+template <int J, bool RED>
+struct ConvMaskFill {
+  State& s;
+  const unsigned* mw;
+  unsigned gbase;
+  float out[16];
+  template <int G>
+  __device__ __forceinline__ void step() {
+    float vx, vy;
+    convm_piece<G>(s.sl[J], out, mw[J >> 1], 16 * (J & 1), vx, vy);
+    if constexpr (RED) {
+      red_add<J, 2 * G>(gbase, vx);
+      red_add<J, 2 * G + 1>(gbase, vy);
+    }
+    if constexpr (G == 7) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s.sl[J][i] = out[i];
+    }
+  }
+};
+
+template <int J, bool RED>
+__device__ __forceinline__ void conv_slot(State& s, const unsigned* mw, unsigned gbase) {
+  ConvMaskFill<J, RED> f{s, mw, gbase, {}};
+  f.template step<0>();
+  f.template step<1>();
+  f.template step<2>();
+  f.template step<3>();
+  f.template step<4>();
+  f.template step<5>();
+  f.template step<6>();
+  f.template step<7>();
+}
+
+// Init MFMA of a backward pass: acc[b] = A_b . [ds_h, ds_l, ds_h] with A_b row i =
+// [wh, wh, wl] of blds[off + 32 b + i] -- fc_out^T's rank-1 sigma term, or zeros.
+template <int NB>
+__device__ __forceinline__ void bwd_init(State& s, const float* blds, int off, bf16x8 sig_b) {
+  float v[8];
+  lds_read8_stride32(blds + off + (s.lane & 31), v);
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    bf16x8 f = {};
+    if (s.h == 0) {
+      const __bf16 hi = static_cast<__bf16>(v[b]);
+      f[0] = hi;
+      f[1] = hi;
+      f[2] = static_cast<__bf16>(v[b] - static_cast<float>(hi));
+    }
+#ifdef CN_ABLATE_NO_MFMA
+    s.acc[b] = floatx16{};
+    asm volatile("" ::"v"(f), "v"(sig_b));
+#else
+    s.acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f, sig_b, floatx16{0}, 0, 0, 0);
+#endif
+  }
+}
+
+// One backward pass over 8-block chunks: init, slot 0, chunks 0..6 converting
+// slot J+1, chunk 7 copying the accumulators out (COPY) or leaving them
+// (layer_dir1^T, whose d-dir chunk still reads the slots).
+template <bool RED, bool COPY = true>
+__device__ __forceinline__ void bwd_pass(State& s, const FieldArgs& a, float4* lds, int& c, const float* blds,
+                                         int init_off, bf16x8 sig_b, const unsigned* mw, unsigned gbase) {
+  bwd_init<8>(s, blds, init_off, sig_b);
+  conv_slot<0, RED>(s, mw, gbase);
+  __builtin_amdgcn_sched_barrier(0);
+#define CN_BWD_CHUNK(J)                                              \
+  {                                                                  \
+    ConvMaskFill<(J) + 1, RED> f{s, mw, gbase, {}};                  \
+    run_chunk<RED ? 4 : 2>(s, a, lds, c, CN_SLOT_B(J), f);           \
+  }
+  CN_BWD_CHUNK(0)
+  CN_BWD_CHUNK(1)
+  CN_BWD_CHUNK(2)
+  CN_BWD_CHUNK(3)
+  CN_BWD_CHUNK(4)
+  CN_BWD_CHUNK(5)
+  CN_BWD_CHUNK(6)
+#undef CN_BWD_CHUNK
+  if constexpr (COPY) {
+    CopyFill f{s};
+    run_chunk<6>(s, a, lds, c, CN_SLOT_B(7), f);
+    copy_acc(s, 6);
+    copy_acc(s, 7);
+  } else {
+    NoFill f;
+    run_chunk<0>(s, a, lds, c, CN_SLOT_B(7), f);
+  }
+}
+
+// layer_dir1^T's d-dir chunk (1 block x 16 k-steps into acc2; step B reads slot B);
+// d feat (acc[0..7], final) is copied into the slots one step behind the reads.
+__device__ __forceinline__ void bwd_dir_chunk(State& s, float4* lds, int& c, floatx16& acc2) {
+  const Dma dma = dma_for(s, lds, c);
+  const float4* slot = lds + (c & (kRing - 1)) * kChunkQuads + s.lane;
+  const float4* nslot = lds + ((c + 1) & (kRing - 1)) * kChunkQuads;
+  acc2 = floatx16{0};
+#define CN_DIR(B)                                                                                    \
+  {                                                                                                  \
+    const float4* ap = slot + ((B) / 4) * kQuadsPerStep + (2 * ((2 * (B)) % 8)) * 64;                \
+    const bf16x8 f0 = (B) == 0 ? s.pre[0] : __builtin_bit_cast(bf16x8, ap[0]);                       \
+    const bf16x8 f1 = (B) == 0 ? s.pre[1] : __builtin_bit_cast(bf16x8, ap[64]);                      \
+    const bf16x8 f2 = (B) == 0 ? s.pre[2] : __builtin_bit_cast(bf16x8, ap[128]);                     \
+    const bf16x8 f3 = (B) == 0 ? s.pre[3] : __builtin_bit_cast(bf16x8, ap[192]);                     \
+    mfma3(acc2, f0, f1, Bh<B>(s, 0), Bl<B>(s, 0));                                                   \
+    dma.template piece<B>();                                                                         \
+    mfma3(acc2, f2, f3, Bh<B>(s, 1), Bl<B>(s, 1));                                                   \
+    if constexpr ((B) > 0) copy_acc(s, (B) - 1);                                                     \
+    if constexpr ((B) == 3) chunk_barrier<kMidOut>();                                                \
+    if constexpr ((B) == 7) load_a<0, 0>(s, nslot, s.pre);                                           \
+  }
+  CN_DIR(0) CN_DIR(1) CN_DIR(2) CN_DIR(3) CN_DIR(4) CN_DIR(5) CN_DIR(6) CN_DIR(7)
+#undef CN_DIR
+  copy_acc(s, 7);
+  ++c;
+}
+
+// layer_xyz1^T chunk Q (k-steps 8Q..8Q+7, blocks 0 and 1): step B reads slot
+// 4Q + B/2 and converts the next slot (4 pieces per step) with mask mw.
+template <int Q>
+__device__ __forceinline__ void bwd_xyz1_chunk(State& s, float4* lds, int& c, const unsigned* mw) {
+  const Dma dma = dma_for(s, lds, c);
+  const float4* slot = lds + (c & (kRing - 1)) * kChunkQuads + s.lane;
+  const float4* nslot = lds + ((c + 1) & (kRing - 1)) * kChunkQuads;
+  constexpr int kNext = 4 * Q + 1;  // first slot this chunk converts
+  float out[4][16];
+#define CN_X1(B)                                                                                        \
+  {                                                                                                     \
+    constexpr int SB = 4 * Q + (B) / 2, TT = (B) & 1;                                                   \
+    const float4* ap = slot + ((B) / 4) * kQuadsPerStep + (4 * ((B) % 4)) * 64;                         \
+    const bf16x8 f0 = (B) == 0 ? s.pre[0] : __builtin_bit_cast(bf16x8, ap[0]);                          \
+    const bf16x8 f1 = (B) == 0 ? s.pre[1] : __builtin_bit_cast(bf16x8, ap[64]);                         \
+    const bf16x8 f2 = (B) == 0 ? s.pre[2] : __builtin_bit_cast(bf16x8, ap[128]);                        \
+    const bf16x8 f3 = (B) == 0 ? s.pre[3] : __builtin_bit_cast(bf16x8, ap[192]);                        \
+    mfma3(s.acc[0], f0, f1, Bh<SB>(s, TT), Bl<SB>(s, TT));                                              \
+    dma.template piece<B>();                                                                            \
+    mfma3(s.acc[1], f2, f3, Bh<SB>(s, TT), Bl<SB>(s, TT));                                              \
+    if constexpr (SB + 1 < 8) {                                                                         \
+      constexpr int NS = SB + 1, P0 = 4 * TT;                                                           \
+      float vx, vy;                                                                                     \
+      convm_piece<P0>(s.sl[NS], out[NS - kNext], mw[NS >> 1], 16 * (NS & 1), vx, vy);                   \
+      convm_piece<P0 + 1>(s.sl[NS], out[NS - kNext], mw[NS >> 1], 16 * (NS & 1), vx, vy);               \
+      convm_piece<P0 + 2>(s.sl[NS], out[NS - kNext], mw[NS >> 1], 16 * (NS & 1), vx, vy);               \
+      convm_piece<P0 + 3>(s.sl[NS], out[NS - kNext], mw[NS >> 1], 16 * (NS & 1), vx, vy);               \
+      if constexpr (TT == 1) {                                                                          \
+        _Pragma("unroll") for (int i = 0; i < 16; ++i) s.sl[NS][i] = out[NS - kNext][i];                \
+      }                                                                                                 \
+    }                                                                                                   \
+    if constexpr ((B) == 3) chunk_barrier<kMidOut>();                                                   \
+    if constexpr ((B) == 7 && Q == 0) load_a<0, 0>(s, nslot, s.pre);                                    \
+  }
+  CN_X1(0) CN_X1(1) CN_X1(2) CN_X1(3) CN_X1(4) CN_X1(5) CN_X1(6) CN_X1(7)
+#undef CN_X1
+  ++c;
+}
+
+// d input of one lane half from the encoding gradients g it holds (k_from_enc
+// order: sines of its pairs, cosines, raw inputs): the forward's pairs, one
+// sincosf each.
+template <int P, int NF, int Q = 0>
+__device__ __forceinline__ void posenc_bwd(const float* x, const float* f, int h, const float* g, float* dx) {
+  if constexpr (Q < P) {
+    constexpr int p0 = 2 * Q, p1 = 2 * Q + 1;
+    constexpr int d0 = p0 % 3, d1 = p1 % 3, k0 = p0 / 3, k1 = p1 / 3;
+    const bool live = k1 < NF || h == 0;
+    const float fk = h ? f[k1 < NF ? k1 : 0] : f[k0];
+    const float arg = __fmul_rn(h ? x[d1] : x[d0], fk);
+    float sn, cs;
+    sincosf(arg, &sn, &cs);
+    const float v = live ? fk * (g[Q] * cs - g[P + Q] * sn) : 0.0f;
+    dx[d0] += h ? 0.0f : v;
+    dx[d1] += h ? v : 0.0f;
+    posenc_bwd<P, NF, Q + 1>(x, f, h, g, dx);
+  } else {
+    // raw inputs: slot 2P = x0 (h 0) / x2 (h 1), slot 2P+1 = x1 (h 0)
+    dx[0] += h ? 0.0f : g[2 * P];
+    dx[2] += h ? g[2 * P] : 0.0f;
+    dx[1] += h ? 0.0f : g[2 * P + 1];
+  }
+}
+
+// Flush this wave's g_code row (LDS) into g_code[code] and zero it.
+__device__ __forceinline__ void flush_gcode(const State& s, const FieldArgs& a, float* blds, int code) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  float* row = blds + kGaccOff + s.wave * kCbStride;
+#pragma unroll
+  for (int k = 0; k < (kCbStride + 63) / 64; ++k) {
+    const int j = s.lane + 64 * k;
+    if (j < kCbStride) {
+      float v;
+      asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_addr(row + j)) : "memory");
+      if (v != 0.0f) atomicAdd(a.g_code + (int64_t)code * kCbStride + j, v);
+      asm volatile("ds_write_b32 %0, %1" ::"v"(lds_addr(row + j)), "v"(0.0f) : "memory");
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+template <int MODE>
+__device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* lds, float* blds, int64_t tile,
+                                         int& cur_code) {
+  const int64_t row = tile * kTile + s.wave * 32 + (s.lane & 31);
+  const bool valid = row < a.m;
+  const int64_t rc = valid ? row : a.m - 1;
+
+  // ---- inputs: sample, d raw, masks (h1, h2, v1, v2), code row (wave-uniform: host-checked)
+  const SampleIn in = decode_sample<MODE>(a, rc);
+  const int crow0 = __builtin_amdgcn_readfirstlane(static_cast<int>(code_row(a, in.code_of)));
+  float4 dr = reinterpret_cast<const float4*>(a.d_raw)[rc];
+  const float zv = MODE == kFromRayZ ? a.z[rc] : 0.0f;
+  unsigned mk[4][4];
+#pragma unroll
+  for (int l = 0; l < 4; ++l) {
+    const int ml = l < 2 ? l : l + 1;  // skip the feat slot
+    const uint4 v =
+        reinterpret_cast<const uint4*>(a.masks)[((tile * kWaves + s.wave) * kMaskLayers + ml) * 64 + s.lane];
+    mk[l][0] = v.x;
+    mk[l][1] = v.y;
+    mk[l][2] = v.z;
+    mk[l][3] = v.w;
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  if (!valid) dr = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (crow0 != cur_code) {
+    if (cur_code >= 0) flush_gcode(s, a, blds, cur_code);
+    cur_code = crow0;
+  }
+  int c = 0;
+  const unsigned dummy = lds_addr(blds + kDummyOff) + 4u * s.lane;
+  const unsigned gl = lds_addr(blds + kGaccOff + s.wave * kCbStride) + 16u * s.h;  // + 4h floats
+  const unsigned gbase = (s.lane & 7) == 7 ? gl : dummy;
+  const unsigned gbase0 = ((s.lane & 7) == 7 && s.h == 0) ? gl : dummy;
+
+  // g_code sigma / rgb: this wave's samples (lane half 1 repeats them)
+  ds_add<4 * kCbSigma>(gbase0, sum8(dr.w));
+  ds_add<4 * kCbRgb>(gbase0, sum8(dr.x));
+  ds_add<4 * (kCbRgb + 1)>(gbase0, sum8(dr.y));
+  ds_add<4 * (kCbRgb + 2)>(gbase0, sum8(dr.z));
+  // B operands: d rgb at k-step 0 (lane half 0, k = channel) and the sigma init [dh, dl, dh]
+  bf16x8 rh = {}, rl = {}, sig_b = {};
+  if (s.h == 0) {
+    const float d3[3] = {dr.x, dr.y, dr.z};
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+      const __bf16 hi = static_cast<__bf16>(d3[e]);
+      rh[e] = hi;
+      rl[e] = static_cast<__bf16>(d3[e] - static_cast<float>(hi));
+    }
+    const __bf16 sh = static_cast<__bf16>(dr.w);
+    sig_b[0] = sh;
+    sig_b[1] = static_cast<__bf16>(dr.w - static_cast<float>(sh));
+    sig_b[2] = sh;
+  }
+  const bf16x8 z8 = {};
+
+  // ---- fc_rgb^T (chunk 0)
+  {
+    bwd_init<8>(s, blds, kTZeros, sig_b);
+    CopyFill f{s};
+    chunk_mfma<6, true, true>(s, lds, c, rh, rl, z8, z8, f);
+    ++c;
+    copy_acc(s, 6);
+    copy_acc(s, 7);
+  }
+  // ---- layer_dir2^T (m_v2), layer_dir1^T (m_v1) + its d-dir chunk
+  floatx16 acc2;
+  bwd_pass<false, true>(s, a, lds, c, blds, kTZeros, sig_b, mk[3], gbase);
+  bwd_pass<false, false>(s, a, lds, c, blds, kTZeros, sig_b, mk[2], gbase);
+  bwd_dir_chunk(s, lds, c, acc2);
+  // ---- fc_out^T (d feat unmasked, sigma rank-1 init), layer_xyz2^T (m_h2): g_code sums
+  const unsigned ones[4] = {~0u, ~0u, ~0u, ~0u};
+  for (int l = 0; l < 2; ++l) {
+    const unsigned* mw = l == 0 ? ones : mk[1];
+    const unsigned gb = gbase + 4u * (l == 0 ? kCbFeat : kCbXyz2);
+    bwd_pass<true, true>(s, a, lds, c, blds, l == 0 ? kTSigmaCol : kTZeros, sig_b, mw, gb);
+  }
+  // ---- layer_xyz1^T (m_h1) into acc[0..1]
+  bwd_init<2>(s, blds, kTZeros, sig_b);
+  {
+    float vx, vy, out[16];
+    convm_piece<0>(s.sl[0], out, mk[0][0], 0, vx, vy);
+    convm_piece<1>(s.sl[0], out, mk[0][0], 0, vx, vy);
+    convm_piece<2>(s.sl[0], out, mk[0][0], 0, vx, vy);
+    convm_piece<3>(s.sl[0], out, mk[0][0], 0, vx, vy);
+    convm_piece<4>(s.sl[0], out, mk[0][0], 0, vx, vy);
+    convm_piece<5>(s.sl[0], out, mk[0][0], 0, vx, vy);
+    convm_piece<6>(s.sl[0], out, mk[0][0], 0, vx, vy);
+    convm_piece<7>(s.sl[0], out, mk[0][0], 0, vx, vy);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s.sl[0][i] = out[i];
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  bwd_xyz1_chunk<0>(s, lds, c, mk[0]);
+  bwd_xyz1_chunk<1>(s, lds, c, mk[0]);
+
+  // ---- encodings -> d pts, d view dir (each lane half its own pairs), then the rays
+  float dx[3] = {0.f, 0.f, 0.f}, dv[3] = {0.f, 0.f, 0.f};
+  {
+    float g[32];
+#pragma unroll
+    for (int t = 0; t < 32; ++t) g[t] = s.acc[t >> 4][t & 15];
+    posenc_bwd<15, 10>(in.x, a.fx, s.h, g, dx);
+    float gd[14];
+#pragma unroll
+    for (int t = 0; t < 14; ++t) gd[t] = acc2[t];
+    posenc_bwd<6, 4>(in.vd, a.fd, s.h, gd, dv);
+  }
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    dx[d] += __shfl_xor(dx[d], 32);
+    dv[d] += __shfl_xor(dv[d], 32);
+  }
+  const int64_t S = a.n_samples;
+  if constexpr (MODE == kFromRayZ) {
+    // pts = ro + rd z (z detached): d ro += d pts, d rd += d pts z.  With S % 32 == 0 the
+    // wave's 32 samples are one ray: sum over the lane half first, one atomic per value.
+    float gro[3], grd[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      gro[d] = valid ? dx[d] : 0.0f;
+      grd[d] = valid ? dx[d] * zv : 0.0f;
+    }
+    const bool one_ray = S % 32 == 0;
+    if (one_ray) {
+#pragma unroll
+      for (int off = 16; off >= 1; off >>= 1)
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+          gro[d] += __shfl_xor(gro[d], off);
+          grd[d] += __shfl_xor(grd[d], off);
+        }
+    }
+    if (valid && s.h == 0 && (!one_ray || (s.lane & 31) == 0)) {
+      const int64_t ray = rc / S;
+      if (a.d_ro)
+        for (int d = 0; d < 3; ++d) atomicAdd(a.d_ro + 3 * ray + d, gro[d]);
+      if (a.d_rd)
+        for (int d = 0; d < 3; ++d) atomicAdd(a.d_rd + 3 * ray + d, grd[d]);
+    }
+  }
+  if (valid && s.h == 0) {
+    const int64_t ray = rc / S, smp = rc - ray * S;
+    if constexpr (MODE != kFromRayZ) {
+      if (a.d_pts)
+        for (int d = 0; d < 3; ++d) a.d_pts[3 * rc + d] = dx[d];
+    }
+    if (a.d_rd) {
+      // Q1 view direction vd = rd[dray] / |rd[dray]|: d rd[dray] += (g - vd (vd . g)) / |rd[dray]|
+      const int64_t base = (ray / a.chunk_rows) * a.chunk_rows;
+      const int64_t rcnt = min(a.chunk_rows, a.n_rays - base);
+      const int64_t dray = base + ((ray - base) * S + smp) % rcnt;
+      const float d0 = a.rd[3 * dray], d1 = a.rd[3 * dray + 1], d2 = a.rd[3 * dray + 2];
+      const float nrm = sqrtf(d0 * d0 + d1 * d1 + d2 * d2);
+      const float dot = in.vd[0] * dv[0] + in.vd[1] * dv[1] + in.vd[2] * dv[2];
+      for (int d = 0; d < 3; ++d) atomicAdd(a.d_rd + 3 * dray + d, (dv[d] - in.vd[d] * dot) / nrm);
+    }
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kThreads, 1) void field_x3_bwd_kernel(FieldArgs a) {
+  __shared__ __attribute__((aligned(16))) float4 lds[kLdsQuads + kBwdLdsFloats / 4];
+  float* blds = reinterpret_cast<float*>(lds + kLdsQuads);
+  State s;
+  s.lane = threadIdx.x & 63;
+  s.h = s.lane >> 5;
+  s.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  s.wsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.packed), 0, kPackedFloats * 4, 0x00020000);
+  s.voff = static_cast<unsigned>(s.wave * 64 + s.lane) * 16u;
+#pragma unroll
+  for (int k = 0; k < kConsts / kThreads; ++k)
+    blds[k * kThreads + threadIdx.x] = a.packed[kBiasXyz1 + k * kThreads + threadIdx.x];
+  for (int j = threadIdx.x; j < kBwdLdsFloats - kGaccOff; j += kThreads) blds[kGaccOff + j] = 0.0f;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kDmaPerWave; ++i) dma_piece(s, lds, 0, i);
+#pragma unroll
+  for (int i = 0; i < kDmaPerWave; ++i) dma_piece(s, lds, 1, i);
+#pragma unroll
+  for (int i = 0; i < kDmaPerWave / 2; ++i) dma_piece(s, lds, 2, i);
+  int cur_code = -1;
+  const int64_t n_tiles = (a.m + kTile - 1) / kTile;
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) bwd_tile<MODE>(s, a, lds, blds, tile, cur_code);
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  if (cur_code >= 0) flush_gcode(s, a, blds, cur_code);
+}
+
+static_assert(kTChunkX1 + 2 == kChunks, "backward chunk schedule");
+static_assert(kBwdLdsFloats * 4 + kLdsQuads * 16 <= 160 * 1024, "LDS budget");
 
 }  // namespace x3
 
@@ -803,12 +1378,38 @@ static int64_t cu_count() {
   return n[dev];
 }
 
-int launch_field_x3(int mode, FieldArgs& a, hipStream_t st) {
+int launch_pack_x3t(const Params& P, float* packed, hipStream_t st) {
+  const int64_t n = (int64_t)x3::kQuads * 8 + x3::kConsts;
+  hipLaunchKernelGGL(x3::pack_x3t_kernel, dim3(cn::elementwise_grid(n, 256)), dim3(256), 0, st, P, packed);
+  return cn::launch_status();
+}
+
+int64_t mask_words_x3(int64_t m) { return cn::ceil_div(m, x3::kTile) * x3::kMaskWordsPerTile; }
+
+int launch_field_x3_bwd(int mode, FieldArgs& a, hipStream_t st) {
   const unsigned grid = static_cast<unsigned>(std::min<int64_t>(cn::ceil_div(a.m, x3::kTile), cu_count()));
   switch (mode) {
-    case kFromPts: hipLaunchKernelGGL(x3::field_x3_kernel<kFromPts>, dim3(grid), dim3(x3::kThreads), 0, st, a); break;
-    case kFromRayZ: hipLaunchKernelGGL(x3::field_x3_kernel<kFromRayZ>, dim3(grid), dim3(x3::kThreads), 0, st, a); break;
-    default: hipLaunchKernelGGL(x3::field_x3_kernel<kFromEncoded>, dim3(grid), dim3(x3::kThreads), 0, st, a); break;
+    case kFromPts: hipLaunchKernelGGL(x3::field_x3_bwd_kernel<kFromPts>, dim3(grid), dim3(x3::kThreads), 0, st, a); break;
+    case kFromRayZ: hipLaunchKernelGGL(x3::field_x3_bwd_kernel<kFromRayZ>, dim3(grid), dim3(x3::kThreads), 0, st, a); break;
+    default: return CN_EUNSUPPORTED;
+  }
+  return cn::launch_status();
+}
+
+int launch_field_x3(int mode, FieldArgs& a, hipStream_t st) {
+  const unsigned grid = static_cast<unsigned>(std::min<int64_t>(cn::ceil_div(a.m, x3::kTile), cu_count()));
+  if (a.masks) {
+    switch (mode) {
+      case kFromPts: hipLaunchKernelGGL((x3::field_x3_kernel<kFromPts, true>), dim3(grid), dim3(x3::kThreads), 0, st, a); break;
+      case kFromRayZ: hipLaunchKernelGGL((x3::field_x3_kernel<kFromRayZ, true>), dim3(grid), dim3(x3::kThreads), 0, st, a); break;
+      default: return CN_EUNSUPPORTED;
+    }
+    return cn::launch_status();
+  }
+  switch (mode) {
+    case kFromPts: hipLaunchKernelGGL((x3::field_x3_kernel<kFromPts, false>), dim3(grid), dim3(x3::kThreads), 0, st, a); break;
+    case kFromRayZ: hipLaunchKernelGGL((x3::field_x3_kernel<kFromRayZ, false>), dim3(grid), dim3(x3::kThreads), 0, st, a); break;
+    default: hipLaunchKernelGGL((x3::field_x3_kernel<kFromEncoded, false>), dim3(grid), dim3(x3::kThreads), 0, st, a); break;
   }
   return cn::launch_status();
 }

@@ -50,6 +50,9 @@ typedef void* cn_stream_t; /* hipStream_t */
  *                 per product; 5.3x the fp32 MFMA rate). */
 #define CN_FMT_F32 0
 #define CN_FMT_BF16X3 1
+/*   CN_FMT_BF16X3_T  the transposed 3xbf16 pack the fused backward streams
+ *                    (cn_field_backward_x3); not a forward format. */
+#define CN_FMT_BF16X3_T 2
 
 const char* cn_version(void);
 const char* cn_error_string(int code);
@@ -204,6 +207,30 @@ int cn_field_backward(const float* const* params, const float* saved, const floa
                       const int64_t* code_index, int64_t n_codes, const float* freqs_xyz,
                       const float* freqs_dir, float* workspace, float* const* grads, float* g_code,
                       float* d_pts, float* d_ro, float* d_rd, cn_stream_t stream);
+
+/* --- Fused 3xbf16 backward (eval-step gradients, frozen weights) ---------
+ * The gradients eval.py's loss.backward() takes into the codes and the pose
+ * (eval.py:141-160; the reference's weight gradients are never read there).
+ * Forward: cn_radiance_field_masks = cn_radiance_field on a CN_FMT_BF16X3 pack
+ * that also writes the ReLU masks of layer_xyz1 / layer_xyz2 / layer_dir1 /
+ * layer_dir2 (cn_field_mask_words(M) uint32 words).  Backward: one launch from
+ * d_raw (M, 4) through the whole field on a CN_FMT_BF16X3_T pack of the same
+ * weights: g_code (n_codes, CN_CODE_BIAS_STRIDE) ACCUMULATED as in
+ * cn_field_backward (feed cn_code_bias_backward for dz_s / dz_t), d_pts (M, 3)
+ * written for pts inputs, d_ro / d_rd (n_rays, 3) ACCUMULATED.  Needs one code
+ * row per 32 consecutive samples (n_codes == 1, or n_samples % 32 == 0), else
+ * CN_EUNSUPPORTED (use cn_field_backward). */
+int64_t cn_field_mask_words(int64_t m);
+int cn_radiance_field_masks(const float* packed, const float* code_bias, const int64_t* code_index,
+                            int64_t n_codes, const float* pts, const float* ro, const float* rd,
+                            const float* z, int64_t n_rays, int64_t n_samples, int64_t chunk_rows,
+                            const float* freqs_xyz, const float* freqs_dir, float* raw, uint32_t* masks,
+                            cn_stream_t stream);
+int cn_field_backward_x3(const float* packed_t, const uint32_t* masks, const float* d_raw, const float* pts,
+                         const float* ro, const float* rd, const float* z, int64_t n_rays, int64_t n_samples,
+                         int64_t chunk_rows, const int64_t* code_index, int64_t n_codes,
+                         const float* freqs_xyz, const float* freqs_dir, float* g_code, float* d_pts,
+                         float* d_ro, float* d_rd, cn_stream_t stream);
 
 /* Backward of cn_code_bias (the code layers, model.py:174-177, and the code
  * halves of layer_xyz2 / fc_out / fc_rgb) from g_code.  dz_s / dz_t (n_codes, 256)

@@ -178,19 +178,28 @@ def _linear(p: Dict[str, Tensor], name: str, x: Tensor) -> Tensor:
     return torch.nn.functional.linear(x, p[name + ".weight"], p[name + ".bias"])
 
 
-def codenerf_mlp(p: Dict[str, Tensor], z_s: Tensor, z_t: Tensor, x: Tensor, dim_xyz: int) -> Tensor:
-    """CodeNeRFModel.forward, model.py:160-194 -> (M, 4) = [rgb_raw(3), sigma_raw]."""
+def codenerf_mlp(p: Dict[str, Tensor], z_s: Tensor, z_t: Tensor, x: Tensor, dim_xyz: int,
+                 relu_masks: Optional[Dict[str, Tensor]] = None) -> Tensor:
+    """CodeNeRFModel.forward, model.py:160-194 -> (M, 4) = [rgb_raw(3), sigma_raw].
+
+    ``relu_masks`` (test aid, default off): {"h1", "h2", "v1", "v2"} -> (M, 256) 0/1
+    masks used in place of the four per-sample ReLUs' own decisions (pre * mask), so
+    a backward can be checked against the ReLU kinks a kernel's forward recorded.
+    """
     relu = torch.nn.functional.relu
+
+    def act(name, pre):
+        return relu(pre) if relu_masks is None else pre * relu_masks[name]
     xyz, view = x[..., :dim_xyz], x[..., dim_xyz:]
     zs1 = relu(_linear(p, "shape_code_layer1", z_s))
     zs2 = relu(_linear(p, "shape_code_layer2", z_s))
     zt1 = relu(_linear(p, "texture_code_layer1", z_t))
-    h = relu(_linear(p, "layer_xyz1", xyz))
-    h = relu(_linear(p, "layer_xyz2", torch.cat((h, zs1), dim=-1)))
+    h = act("h1", _linear(p, "layer_xyz1", xyz))
+    h = act("h2", _linear(p, "layer_xyz2", torch.cat((h, zs1), dim=-1)))
     o = _linear(p, "fc_out", torch.cat((h, zs2), dim=-1))
     sigma, feat = o[..., :1], o[..., 1:]
-    v = relu(_linear(p, "layer_dir1", torch.cat((feat, view), dim=-1)))
-    v = relu(_linear(p, "layer_dir2", v))
+    v = act("v1", _linear(p, "layer_dir1", torch.cat((feat, view), dim=-1)))
+    v = act("v2", _linear(p, "layer_dir2", v))
     rgb = _linear(p, "fc_rgb", torch.cat((v, zt1), dim=-1))
     return torch.cat((rgb, sigma), dim=-1)
 
@@ -208,8 +217,8 @@ class EmbedCfg:
 
 
 def forward_pass(p: Dict[str, Tensor], emb: EmbedCfg, rd: Tensor, pts: Tensor,
-                 z_s: Tensor, z_t: Tensor) -> Tensor:
-    """nerf/__init__.py:94-134 -> (R, S, 4).
+                 z_s: Tensor, z_t: Tensor, relu_masks: Optional[Dict[str, Tensor]] = None) -> Tensor:
+    """nerf/__init__.py:94-134 -> (R, S, 4).  ``relu_masks``: see codenerf_mlp (rows r*S + s).
 
     Quirk Q1: ``viewdirs.repeat([1, S, 1])`` tiles the whole (R, 3) ray list, so
     flattened sample row k = r*S + s gets the view direction of ray k mod R
@@ -223,7 +232,7 @@ def forward_pass(p: Dict[str, Tensor], emb: EmbedCfg, rd: Tensor, pts: Tensor,
     vd = vd.repeat([1, s, 1])
     vd = vd.reshape(-1, vd.shape[-1])
     enc = torch.cat((enc, posenc(vd, emb.fd, emb.inc_d)), dim=-1)
-    out = codenerf_mlp(p, zs, zt, enc, emb.dim_xyz)
+    out = codenerf_mlp(p, zs, zt, enc, emb.dim_xyz, relu_masks)
     return out.reshape([r, s, out.shape[-1]])
 
 

@@ -165,13 +165,37 @@ def test_ray_bundle_gather_points_backward(dev):
 # ---------------------------------------------------------------- field (forward_pass + CodeNeRFModel)
 
 
-def _oracle_field(o, p, rd, pts, zs, zt, chunk):
+def _oracle_field(o, p, rd, pts, zs, zt, chunk, masks=None):
     emb = o.EmbedCfg()
+    s = pts.shape[1]
     outs = []
     for c0 in range(0, rd.shape[0], chunk):
-        sl = slice(c0, min(c0 + chunk, rd.shape[0]))
-        outs.append(o.forward_pass(p, emb, rd[sl], pts[sl], zs[sl], zt[sl]))
+        c1 = min(c0 + chunk, rd.shape[0])
+        mk = None if masks is None else {k: v[c0 * s:c1 * s] for k, v in masks.items()}
+        outs.append(o.forward_pass(p, emb, rd[c0:c1], pts[c0:c1], zs[c0:c1], zt[c0:c1], mk))
     return torch.cat(outs)
+
+
+def decode_relu_masks(words: torch.Tensor, m_rows: int):
+    """cn_radiance_field_masks' ReLU decisions -> {"h1", "h2", "v1", "v2"}: (m_rows, 256) 0/1 floats.
+
+    Layout (csrc/mlp_x3.hip store_masks / put_mask / conv_piece): per 128-sample tile, wave w,
+    layer slot l (h1, h2, feat, v1, v2) and lane L, 4 words; bit b of word q is sample
+    tile*128 + 32w + (L & 31), feature 32(2q + (b >> 4)) + (i & 3) + 8(i >> 2) + 4(L >> 5), i = b & 15.
+    """
+    w = words.detach().cpu().to(torch.int64) & 0xFFFFFFFF
+    tiles = w.numel() // (4 * 5 * 64 * 4)
+    bits = ((w.view(tiles, 4, 5, 64, 4, 1) >> torch.arange(32)) & 1).float()
+    lane = torch.arange(64).view(64, 1, 1)
+    q = torch.arange(4).view(1, 4, 1)
+    b = torch.arange(32).view(1, 1, 32)
+    i = b & 15
+    feat = 32 * (2 * q + (b >> 4)) + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5)
+    row = (lane & 31).expand(64, 4, 32)
+    out = torch.zeros(tiles, 4, 5, 32, 256)
+    out[:, :, :, row, feat] = bits
+    out = out.permute(0, 1, 3, 2, 4).reshape(tiles * 128, 5, 256)[:m_rows]
+    return {k: out[:, l].contiguous() for k, l in (("h1", 0), ("h2", 1), ("v1", 3), ("v2", 4))}
 
 
 @pytest.mark.parametrize("mode,r,s,chunk,per_ray_codes", [
@@ -224,6 +248,79 @@ def test_field_backward(dev, mode, r, s, chunk, per_ray_codes):
     close(zt_g.grad, zt_c.grad, what="d z_t")
     for (name, prm) in m.named_parameters():
         close(prm.grad, p[name].grad, what=name)
+
+
+@pytest.mark.parametrize("mode,r,s,chunk,per_ray_codes,fused", [
+    ("rayz", 37, 16, 13, False, True),
+    ("pts", 37, 16, 37, False, True),
+    ("rayz", 20, 32, 20, True, True),
+    ("rayz", 300, 64, 128, False, True),
+    ("rayz", 64, 128, 64, False, True),
+    ("rayz", 20, 9, 20, True, False),   # codes change inside a 32-sample wave: layer-wise fp32 path
+])
+def test_field_backward_eval_fused(dev, monkeypatch, mode, r, s, chunk, per_ray_codes, fused):
+    """Frozen bf16x3 model (the eval step): the 3xbf16 forward with ReLU masks and ONE fused backward
+    launch (cn_field_backward_x3) give the oracle's d ro / d rd / d z_s / d z_t.
+
+    The oracle takes the ReLU decisions the kernel's forward recorded (decode_relu_masks): a
+    pre-activation within the 3xbf16 error of 0 can fall on the other side of the kink in an
+    independent fp32 forward, which moves that sample's gradient by a whole weight column -- a
+    property of the kink, not an error of the backward."""
+    from codenerf import nerf, ops, synthetic
+    calls = {"fused": 0, "masks": None}
+    real_bwd, real_fwd = ops.field_backward_x3, ops.radiance_field_masks
+
+    def spy_bwd(*a, **k):
+        calls["fused"] += 1
+        return real_bwd(*a, **k)
+
+    def spy_fwd(*a, **k):
+        raw, masks = real_fwd(*a, **k)
+        calls["masks"] = masks
+        return raw, masks
+    monkeypatch.setattr(ops, "field_backward_x3", spy_bwd)
+    monkeypatch.setattr(ops, "radiance_field_masks", spy_fwd)
+    o = O()
+    m = model(dev, 0)
+    p = oracle_params(m)
+    m.precision = "bf16x3"
+    m.requires_grad_(False)
+    g = torch.Generator().manual_seed(r * s + 7)
+    ro = torch.randn(r, 3, generator=g) * 0.3 + torch.tensor([0.0, 0.0, 1.3])
+    rd = torch.randn(r, 3, generator=g)
+    z = torch.sort(0.8 + torch.rand(r, s, generator=g), dim=-1).values
+    if per_ray_codes:
+        zs, zt = torch.randn(r, 256, generator=g) * 0.3, torch.randn(r, 256, generator=g) * 0.3
+    else:
+        zs, zt = synthetic.latent_codes(5, 1), synthetic.latent_codes(6, 1)
+    gout = torch.randn(r, s, 4, generator=g)
+
+    ro_g, rd_g = ro.to(dev).requires_grad_(True), rd.to(dev).requires_grad_(True)
+    zs_g, zt_g = zs.to(dev).requires_grad_(True), zt.to(dev).requires_grad_(True)
+    zsg = zs_g if per_ray_codes else zs_g.expand(r, -1)
+    ztg = zt_g if per_ray_codes else zt_g.expand(r, -1)
+    emb = embedders(dev)
+    if mode == "pts":
+        from codenerf.autograd import sample_points_autograd
+        raw_g = nerf._field(m, emb, rd_g, zsg, ztg, chunk, pts=sample_points_autograd(ro_g, rd_g, z.to(dev)))
+    else:
+        raw_g = nerf._field(m, emb, rd_g, zsg, ztg, chunk, ro=ro_g, z=z.to(dev))
+    (raw_g * gout.to(dev)).sum().backward()
+    assert calls["fused"] == (1 if fused else 0)
+    masks = decode_relu_masks(calls["masks"], r * s) if fused else None
+
+    ro_c, rd_c = ro.clone().requires_grad_(True), rd.clone().requires_grad_(True)
+    zs_c, zt_c = zs.clone().requires_grad_(True), zt.clone().requires_grad_(True)
+    pts_c = ro_c[:, None, :] + rd_c[:, None, :] * z[..., None]
+    zse = zs_c if per_ray_codes else zs_c.expand(r, -1)
+    zte = zt_c if per_ray_codes else zt_c.expand(r, -1)
+    raw_c = _oracle_field(o, {k: v.detach() for k, v in p.items()}, rd_c, pts_c, zse, zte, chunk, masks)
+    (raw_c * gout).sum().backward()
+    assert (raw_g.detach().cpu() - raw_c.detach()).abs().max().item() <= 1e-4
+    close(ro_g.grad, ro_c.grad, what="d ro")
+    close(rd_g.grad, rd_c.grad, what="d rd")
+    close(zs_g.grad, zs_c.grad, what="d z_s")
+    close(zt_g.grad, zt_c.grad, what="d z_t")
 
 
 @pytest.mark.parametrize("m_rows,dedupe", [(1000, True), (257, False)])
