@@ -278,7 +278,9 @@ __device__ __forceinline__ void chunk_barrier() {
 #else
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(OUT) : "memory");
 #endif
+#ifndef CN_ABLATE_NO_MC_FENCE
   __builtin_amdgcn_sched_barrier(0);  // nothing (ring reads included) is scheduled above the wait
+#endif
 }
 constexpr int kMidOut = 8;  // chunk c+2's pieces are younger than chunk c+1's at M_c
 

@@ -10,4 +10,4 @@ rc=$?; echo "pytest rc=$rc"; tail -3 $O/pytest_gpu.log; [ $rc -ne 0 ] && exit $r
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline ${BENCH_ARGS} > $O/bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -1 $O/bench.log | cut -c1-2500; [ $rc -ne 0 ] && exit $rc
-python $R/tools/kstats.py $O/prof/run_kernel_stats.csv | head -25
+python $R/tools/kstats.py $O/prof/run_kernel_stats.csv > $O/kstats.txt; head -25 $O/kstats.txt
