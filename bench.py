@@ -75,6 +75,8 @@ def main():
     ap.add_argument("--no-f32-compare", action="store_true", help="skip the fp32-kernel side measurement")
     ap.add_argument("--eval-iters", type=int, default=10,
                     help="C5: time this many test-time-optimisation iterations (0 = skip)")
+    ap.add_argument("--train-iters", type=int, default=3,
+                    help="C3 training: time this many train.py iterations (4 x 4096 rays each; 0 = skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -187,6 +189,8 @@ def main():
 
     if args.eval_iters > 0:
         extra["eval_c5"] = eval_bench(dev, rs, emb, models, args.eval_iters)
+    if args.train_iters > 0:
+        extra["train_c3"] = train_bench(dev, k, args.train_iters, world)
 
     traffic = None
     tpath = os.path.join(ROOT, "profiles", "field_kernel_traffic.json")
@@ -267,8 +271,77 @@ def eval_bench(dev, rs, emb, models, iters):
         m.requires_grad_(True)
         m.precision = prec
     return {"ms_per_iter": dt * 1e3, "rays_per_s": 2048 / dt, "rays_per_iter": 2048, "samples": "64+64 perturbed",
-            "note": "forward+backward through the fp32 training field kernel; host-side numpy ray permutation "
-                    "and the per-iteration .item() logging of eval.py included"}
+            "note": "forward with ReLU masks + one fused backward launch per field (3xbf16, frozen weights); "
+                    "host-side numpy ray permutation and eval.py's per-iteration psnr read-back included"}
+
+
+def train_bench(dev, k, iters, world):
+    """C3 training (srn-cars-code.yml; train.py:64-114): one iteration = 4 images x 4096 random rays,
+    chunk 4096 -> 4 optimiser steps, each 64+64 perturbed samples per ray with per-object codes from a
+    2458-object table, fwd + bwd into both MLPs and both code tables, flat AdamW (one launch), LambdaLR,
+    and with N ranks one RCCL all-reduce of the flat gradient per step (DDP's average)."""
+    import numpy as np
+    from types import SimpleNamespace as NS
+    from codenerf import nerf as N, train as T
+    n_objects, batch = 2458, 4
+    cfg = NS(is_distributed=world > 1,
+             models=NS(embedding=NS(shape_code_size=256, texture_code_size=256), nerf_coarse=NS(hidden_size=256),
+                       nerf_fine=NS(hidden_size=256)),
+             nerf=NS(embedder=NS(num_encoding_fn_xyz=10, include_input_xyz=True, log_sampling_xyz=True,
+                                 num_encoding_fn_dir=4, include_input_dir=True, log_sampling_dir=True,
+                                 use_viewdirs=True),
+                     ray_sampler=NS(num_random_rays=4096),
+                     point_sampler=NS(num_coarse=NC, num_fine=NF, near_limit=NEAR, far_limit=FAR,
+                                      spacing_mode="lindepth", perturb=True),
+                     train=NS(chunksize=4096)),
+             optimizer=NS(type="AdamW", lr=1e-4, embedding_lr=1e-3, scheduler_gamma=0.1,
+                          scheduler_step_size=5000000),
+             experiment=NS(regularizer_lambda=1e-5))
+    rank = dist.get_rank() if world > 1 else 0
+    torch.manual_seed(rank + 1)                   # train.py:29-31: each rank draws its own rays
+    np.random.seed(rank + 1)
+    models = T.prepare_models(cfg, n_objects, dev)
+    opt, sched = T.prepare_optimizer(cfg, models)
+    samplers = N.prepare_samplers(cfg, H, W, k, torch.float32, dev)
+    embedders = N.prepare_embedders(cfg, torch.float32, dev)
+    g = torch.Generator().manual_seed(7 + rank)
+    data = {"color": torch.rand(batch, H, W, 4, generator=g).to(dev),
+            "pose": torch.stack([pose(0.4 + 0.5 * i, 0.3, 1.3) for i in range(batch)]).to(dev),
+            "object_id": torch.randint(0, n_objects, (batch,), generator=g).to(dev)}
+    T.train_iteration(cfg, data, models, opt, sched, samplers, embedders)        # warm-up
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        logs = T.train_iteration(cfg, data, models, opt, sched, samplers, embedders)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    # the optimiser launch alone (HIP events on its stream), gradients from the last step
+    n_params = sum(p.numel() for m in models.values() for p in m.parameters())
+    evs = []
+    for _ in range(10):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        opt.step()
+        e1.record()
+        evs.append((e0, e1))
+    torch.cuda.synchronize()
+    adamw_ms = sorted(a.elapsed_time(b) for a, b in evs)[len(evs) // 2]
+    rays = batch * 4096 * iters * world
+    return {"ms_per_iter": dt / iters * 1e3, "rays_per_s": rays / dt, "rays_per_iter_per_rank": batch * 4096,
+            "optimizer_steps_per_iter": batch, "samples": "64+64 perturbed", "objects": n_objects,
+            "params": n_params, "loss": float(logs[-1]["total_loss"]),
+            "adamw": {"median_ms": adamw_ms, "bytes": 28 * n_params,
+                      "gbps": 28 * n_params / (adamw_ms * 1e-3) / 1e9},
+            "note": "fp32 training field kernel (activations kept), layer-wise fp32 MFMA backward, "
+                    "flat AdamW; train.py's per-chunk psnr read-back included"}
 
 
 def cpu_baseline(img, k, poses, n):

@@ -63,6 +63,9 @@ SIGNATURES = {
     "cn_ray_points_backward": (_i, [_p, _p, _i64, _i64, _p, _p, _p]),
     "cn_gemm_nn":(_i, [_p, _i64, _p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _p]),
     "cn_gemm_tn": (_i, [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _p]),
+    "cn_adamw_step": (_i, [_p, _p, _p, _p, _i64, ctypes.POINTER(_i64), ctypes.POINTER(_i64),
+                           ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i64),
+                           ctypes.c_double, ctypes.c_double, ctypes.c_double, _p]),
 }
 
 _lib: Optional[ctypes.CDLL] = None

@@ -286,8 +286,9 @@ def mlp_forward_autograd(model, z_s, z_t, x):
     return MLPForward.apply(x, cs, ct, *model.param_list())
 
 
-def radiance_field_autograd(model, rd, z_s, z_t, chunk_rows, fx, fd, pts=None, ro=None, z=None):
-    cs, ct = _code_rows(z_s, z_t)
+def radiance_field_autograd(model, rd, z_s, z_t, chunk_rows, fx, fd, pts=None, ro=None, z=None, code_index=None):
+    cs, ct = (z_s, z_t) if code_index is not None else _code_rows(z_s, z_t)
     n_samples = pts.shape[1] if pts is not None else z.shape[1]
-    meta = _FieldMeta(n_samples, chunk_rows, fx, fd, precision=getattr(model, "precision", "f32"))
+    meta = _FieldMeta(n_samples, chunk_rows, fx, fd, code_index=code_index,
+                      precision=getattr(model, "precision", "f32"))
     return RadianceField.apply(meta, rd, pts, ro, _d(z), cs, ct, *model.param_list())

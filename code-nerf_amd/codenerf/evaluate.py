@@ -47,7 +47,8 @@ def eval_step_loss(theta, phi, rho, shape_code, texture_code, target_pixels, sam
     lf = torch.nn.functional.mse_loss(rgb_f[..., :3], tp[..., :3])
     reg = regularizer_lambda * (torch.norm(z_s, p=2) + torch.norm(z_t, p=2))
     loss = lc + lf + reg
-    return loss, {"nerf_loss_coarse": lc.item(), "nerf_loss_fine": lf.item(), "embedding_loss": reg.item(),
+    # eval.py:159 reads the fine loss back every iteration (psnr); the other terms are read only when logged
+    return loss, {"nerf_loss_coarse": lc.detach(), "nerf_loss_fine": lf.detach(), "embedding_loss": reg.detach(),
                   "psnr": mse2psnr(lf.item())}
 
 
@@ -90,12 +91,13 @@ def test_time_optimize(target_pixels: torch.Tensor, samplers, embedders, models,
             opt.zero_grad()
             loss.backward()
             opt.step()
-            logs["total_loss"] = loss.item()
+            logs["total_loss"] = loss.detach()
             history.append(logs)
             if log_every and (it % log_every == 0 or it == iterations - 1):
-                print(f"[val-optim {it}] " + " ".join(f"{k}={v:.5f}" for k, v in logs.items()))
+                print(f"[val-optim {it}] " + " ".join(f"{k}={float(v):.5f}" for k, v in logs.items()))
     finally:
         for k, flags in saved.items():
             for p, f in zip(models[k].parameters(), flags):
                 p.requires_grad_(f)
+    history = [{k: float(v) for k, v in h.items()} for h in history]
     return shape_code, texture_code, (theta, phi, rho), history

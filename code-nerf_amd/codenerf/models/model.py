@@ -101,6 +101,15 @@ def _dedupe_codes(z_s: torch.Tensor, z_t: torch.Tensor):
     return z_s, z_t, None
 
 
+class CodeRows:
+    """The distinct code rows behind per-ray codes: z_s = shape_rows[index], z_t = texture_rows[index]."""
+
+    __slots__ = ("shape_rows", "texture_rows", "index")
+
+    def __init__(self, shape_rows: torch.Tensor, texture_rows: torch.Tensor, index: torch.Tensor):
+        self.shape_rows, self.texture_rows, self.index = shape_rows, texture_rows, index
+
+
 class ShapeTextureEmbedding(torch.nn.Module):
     """model.py:87-120: per-object shape / texture code tables."""
 
@@ -113,7 +122,19 @@ class ShapeTextureEmbedding(torch.nn.Module):
         self.texture_embedding = torch.nn.Embedding(num_embeddings, texture_code_size)
 
     def forward(self, object_ids: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
-        return self.shape_embedding(object_ids), self.texture_embedding(object_ids)
+        """model.py:102-105.  On the device the distinct ids are looked up once and the per-ray
+        rows gathered from them; both returned tensors carry that factorisation
+        (``_cn_code_rows``), so the field kernels run the per-object code layers once per
+        object (one per 4096-ray chunk in train.py) instead of once per ray."""
+        if object_ids.device.type != "cuda" or object_ids.dim() != 1:
+            return self.shape_embedding(object_ids), self.texture_embedding(object_ids)
+        uniq, index = torch.unique(object_ids, return_inverse=True)
+        rows_s, rows_t = self.shape_embedding(uniq), self.texture_embedding(uniq)
+        z_s, z_t = rows_s[index], rows_t[index]
+        tag = CodeRows(rows_s, rows_t, index)
+        z_s._cn_code_rows = tag
+        z_t._cn_code_rows = tag
+        return z_s, z_t
 
     def get_all_embeddings(self, device) -> Tuple[torch.Tensor, torch.Tensor]:
         idx = torch.arange(0, self.num_embeddings, dtype=torch.int64, device=device)
@@ -130,6 +151,6 @@ class ShapeTextureEmbedding(torch.nn.Module):
 
 
 def get_params_tensor(model, is_distributed):
-    """model.py:79-84."""
-    m = model.module if is_distributed else model
+    """model.py:79-84 (the build's modules are never DDP-wrapped: see codenerf.train)."""
+    m = getattr(model, "module", model)
     return m.get_params_tensor()

@@ -63,26 +63,32 @@ def _check_embedders(embedders):
 
 
 def _codes(z_s: torch.Tensor, z_t: torch.Tensor):
-    """One code row when the per-ray codes are an expand() of one row (eval / render), else per ray."""
+    """Code rows for the field kernels -> (z_s rows, z_t rows, per-ray code index or None):
+    the distinct rows when the codes came from ShapeTextureEmbedding (train), one row when
+    they are an expand() of one row (eval / render), else one row per ray."""
+    tag = getattr(z_s, "_cn_code_rows", None)
+    if tag is not None and getattr(z_t, "_cn_code_rows", None) is tag and tag.index.shape[0] == z_s.shape[0]:
+        return tag.shape_rows, tag.texture_rows, (None if tag.shape_rows.shape[0] == 1 else tag.index)
     if z_s.stride(0) == 0 and z_t.stride(0) == 0:
-        return z_s[:1], z_t[:1]
-    return z_s, z_t
+        return z_s[:1], z_t[:1], None
+    return z_s, z_t, None
 
 
 def _field(model, embedders, rd, z_s, z_t, chunk_rows, pts=None, ro=None, z=None):
     fx, fd = _check_embedders(embedders)
     m = _unwrap(model)
+    cs, ct, code_index = _codes(z_s, z_t)
     needs_grad = torch.is_grad_enabled() and (
-        any(t is not None and t.requires_grad for t in (rd, z_s, z_t, pts, ro)) or
+        any(t is not None and t.requires_grad for t in (rd, cs, ct, pts, ro)) or
         any(p.requires_grad for p in m.param_list()))
     if needs_grad:
         from ..autograd import radiance_field_autograd
-        return radiance_field_autograd(m, rd, z_s, z_t, chunk_rows, fx, fd, pts=pts, ro=ro, z=z)
-    cs, ct = _codes(z_s, z_t)
+        return radiance_field_autograd(m, rd, cs, ct, chunk_rows, fx, fd, pts=pts, ro=ro, z=z,
+                                       code_index=code_index)
     cb = m.code_bias(cs, ct)
     n_samples = pts.shape[1] if pts is not None else z.shape[1]
     return ops.radiance_field(m.packed(), cb, rd, n_samples, chunk_rows, fx, fd, pts=pts, ro=ro, z=z,
-                              precision=m.precision)
+                              code_index=code_index, precision=m.precision)
 
 
 def forward_pass(model, embedders, rd: torch.Tensor, pts: torch.Tensor,

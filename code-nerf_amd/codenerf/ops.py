@@ -8,6 +8,7 @@ PyTorch compute.
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Optional, Sequence, Tuple
 
 import torch
@@ -533,3 +534,32 @@ def field_backward_x3(packed_t: Tensor, masks: Tensor, d_raw: Tensor, n_rays: in
                                    _lib.host_floats(freqs_xyz), _lib.host_floats(freqs_dir), ptr(g_code),
                                    ptr(d_pts), ptr(d_ro), ptr(d_rd), stream_of(d_raw)), "cn_field_backward_x3")
     return {"g_code": g_code, "d_pts": d_pts, "d_ro": d_ro, "d_rd": d_rd}
+
+
+# ------------------------------------------------------------------ training step: optimiser
+
+
+def adamw_step(param: Tensor, grad: Tensor, exp_avg: Tensor, exp_avg_sq: Tensor, segments,
+               beta1: float, beta2: float, eps: float) -> None:
+    """torch.optim.AdamW.step (train.py:113) on flat fp32 buffers, in place (cn_adamw_step).
+
+    ``segments``: [(begin, end, lr, weight_decay, step)] float ranges (multiples of 4).
+    """
+    lib = _lib_ready()
+    bufs = [_cuda(t, name) for t, name in ((param, "param"), (grad, "grad"), (exp_avg, "exp_avg"),
+                                          (exp_avg_sq, "exp_avg_sq"))]
+    n = param.numel()
+    assert all(b.data_ptr() == t.data_ptr() and b.numel() == n for b, t in zip(bufs, (param, grad, exp_avg, exp_avg_sq))), \
+        "flat optimiser buffers must be contiguous and of one size"
+    assert segments and all(b % 4 == 0 and e % 4 == 0 and 0 <= b < e <= n for b, e, *_ in segments)
+    k = len(segments)
+
+    def arr(ct, vals):
+        return (ct * k)(*vals)
+    check(lib.cn_adamw_step(ptr(param), ptr(grad), ptr(exp_avg), ptr(exp_avg_sq), k,
+                            arr(ctypes.c_int64, [int(s[0]) for s in segments]),
+                            arr(ctypes.c_int64, [int(s[1]) for s in segments]),
+                            arr(ctypes.c_double, [float(s[2]) for s in segments]),
+                            arr(ctypes.c_double, [float(s[3]) for s in segments]),
+                            arr(ctypes.c_int64, [int(s[4]) for s in segments]),
+                            float(beta1), float(beta2), float(eps), stream_of(param)), "cn_adamw_step")

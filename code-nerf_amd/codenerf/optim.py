@@ -1,0 +1,230 @@
+"""The training step's optimiser on the gfx950 kernels.
+
+``AdamW`` is a drop-in for ``torch.optim.AdamW`` as the reference builds and drives
+it (utils/util.py:159-170: param groups nerf_coarse, nerf_fine and the embedding
+tables at ``embedding_lr`` under a LambdaLR; train.py:111-114: zero_grad, backward,
+step, scheduler.step): the same constructor, ``param_groups``, per-parameter state
+(``step``, ``exp_avg``, ``exp_avg_sq``) and state_dict format, so checkpoints move
+between the two.
+
+MI355X layout: every parameter of every group lives in ONE flat fp32 HBM buffer
+(each tensor 256-B aligned) with matching flat buffers for the gradient and both
+moments; the parameters (and the moments in ``state``) are views into them.
+``step()`` is then one kernel launch (cn_adamw_step) for both MLPs and both code
+tables, HBM-bound at 28 B per parameter, instead of torch's per-tensor kernel
+chain; the data-parallel gradient average the reference gets from DDP
+(util.py:139-142) is ONE collective over the flat gradient (``allreduce_grads``:
+RCCL over xGMI with the nccl backend, gloo on CPU), and DDP's construction-time
+parameter broadcast is one broadcast of the flat parameter buffer
+(``broadcast_params``).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from . import ops
+
+ALIGN = 64  # floats: every tensor starts on a 256-B boundary
+
+
+def _round_up(n: int) -> int:
+    return (n + ALIGN - 1) // ALIGN * ALIGN
+
+
+class AdamW(torch.optim.Optimizer):
+    """torch.optim.AdamW (decoupled weight decay; amsgrad / maximize off) on flat buffers."""
+
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 1e-2, amsgrad: bool = False, *, maximize: bool = False,
+                 foreach=None, capturable: bool = False, differentiable: bool = False, fused=None):
+        if not 0.0 <= lr:
+            raise ValueError(f"Invalid learning rate: {lr}")
+        if not 0.0 <= eps:
+            raise ValueError(f"Invalid epsilon value: {eps}")
+        if not 0.0 <= betas[0] < 1.0:
+            raise ValueError(f"Invalid beta parameter at index 0: {betas[0]}")
+        if not 0.0 <= betas[1] < 1.0:
+            raise ValueError(f"Invalid beta parameter at index 1: {betas[1]}")
+        if not 0.0 <= weight_decay:
+            raise ValueError(f"Invalid weight_decay value: {weight_decay}")
+        if amsgrad or maximize or capturable or differentiable:
+            raise NotImplementedError("codenerf.optim.AdamW implements amsgrad=False, maximize=False "
+                                      "(the reference's AdamW)")
+        defaults = dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay, amsgrad=False,
+                        maximize=False, foreach=foreach, capturable=False, differentiable=False, fused=fused,
+                        decoupled_weight_decay=True)
+        self._flat: Optional[Dict[str, torch.Tensor]] = None
+        super().__init__(params, defaults)
+        self._build()
+
+    # ---- flat buffers -------------------------------------------------
+    def add_param_group(self, param_group) -> None:
+        super().add_param_group(param_group)
+        if self._flat is not None:
+            self._build()
+
+    def _build(self) -> None:
+        params = [p for g in self.param_groups for p in g["params"]]
+        dev = params[0].device
+        for p in params:
+            if p.dtype != torch.float32 or p.device != dev:
+                raise TypeError("codenerf.optim.AdamW needs fp32 parameters on one device")
+        offs, starts, o = {}, [0], 0
+        for g in self.param_groups:
+            for p in g["params"]:
+                offs[p] = o
+                o += _round_up(p.numel())
+            starts.append(o)
+        n = max(o, ALIGN)
+        flat = {k: torch.zeros(n, device=dev, dtype=torch.float32)
+                for k in ("param", "grad", "exp_avg", "exp_avg_sq")}
+        with torch.no_grad():
+            for p, off in offs.items():
+                k = p.numel()
+                flat["param"][off:off + k].copy_(p.detach().reshape(-1))
+                grad = p.grad
+                p.data = flat["param"][off:off + k].view_as(p)
+                if grad is not None:
+                    flat["grad"][off:off + k].copy_(grad.reshape(-1))
+                    p.grad = flat["grad"][off:off + k].view_as(p)
+        self._flat, self._offs, self._starts = flat, offs, starts
+        self._adopt_state()
+
+    def _view(self, key: str, p: torch.Tensor) -> torch.Tensor:
+        off = self._offs[p]
+        return self._flat[key][off:off + p.numel()].view_as(p)
+
+    def _adopt_state(self) -> None:
+        """Point every parameter's moments at the flat buffers (after a build or a load)."""
+        with torch.no_grad():
+            for p in self._offs:
+                st = self.state.get(p)
+                if not st:
+                    continue
+                for key in ("exp_avg", "exp_avg_sq"):
+                    view = self._view(key, p)
+                    t = st.get(key)
+                    if t is not None and t.data_ptr() != view.data_ptr():
+                        view.copy_(t.reshape(p.shape))
+                    st[key] = view
+                step = st.get("step", 0.0)
+                st["step"] = step if torch.is_tensor(step) else torch.tensor(float(step), dtype=torch.float32)
+
+    def flat_buffers(self) -> Dict[str, torch.Tensor]:
+        """The flat fp32 buffers: param, grad, exp_avg, exp_avg_sq (group g spans
+        ``group_starts[g]:group_starts[g + 1]``)."""
+        return self._flat
+
+    @property
+    def group_starts(self) -> List[int]:
+        return list(self._starts)
+
+    def _sync_grads(self) -> List[torch.Tensor]:
+        """Move every gradient into the flat buffer (autograd may have installed a new
+        tensor) and point ``.grad`` at it; returns the parameters without a gradient."""
+        missing = []
+        with torch.no_grad():
+            for p in self._offs:
+                if p.grad is None:
+                    missing.append(p)
+                    continue
+                view = self._view("grad", p)
+                if p.grad.data_ptr() != view.data_ptr():
+                    view.copy_(p.grad)
+                    p.grad = view
+        return missing
+
+    # ---- reference API ------------------------------------------------
+    def zero_grad(self, set_to_none: bool = True) -> None:
+        """train.py:111.  ``set_to_none`` (torch's default) drops the gradients as torch does;
+        otherwise the flat gradient is cleared in one memset and stays attached."""
+        if set_to_none:
+            for p in self._offs:
+                p.grad = None
+        else:
+            self._flat["grad"].zero_()
+            for p in self._offs:
+                p.grad = self._view("grad", p)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        """One AdamW update of every parameter that has a gradient: ONE cn_adamw_step launch.
+        Parameters without a gradient keep their values and state, as in torch."""
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        self._sync_grads()
+        g0 = self.param_groups[0]
+        betas, eps = tuple(g0["betas"]), float(g0["eps"])
+        for g in self.param_groups:
+            if g.get("amsgrad") or g.get("maximize"):
+                raise NotImplementedError("codenerf.optim.AdamW: amsgrad / maximize")
+            if tuple(g["betas"]) != betas or float(g["eps"]) != eps:
+                raise NotImplementedError("codenerf.optim.AdamW: betas and eps must be shared by all groups")
+        segments = []
+        for g in self.param_groups:
+            lr, wd = float(g["lr"]), float(g["weight_decay"])
+            for p in g["params"]:
+                if p.grad is None:
+                    continue
+                st = self.state[p]
+                if len(st) == 0:
+                    st["step"] = torch.tensor(0.0, dtype=torch.float32)
+                    st["exp_avg"] = self._view("exp_avg", p)
+                    st["exp_avg_sq"] = self._view("exp_avg_sq", p)
+                st["step"] += 1
+                t = int(st["step"].item())
+                off = self._offs[p]
+                end = off + _round_up(p.numel())
+                if segments and segments[-1][1] == off and segments[-1][2:] == [lr, wd, t]:
+                    segments[-1][1] = end
+                else:
+                    segments.append([off, end, lr, wd, t])
+        if not segments:
+            return loss
+        f = self._flat
+        ops.adamw_step(f["param"], f["grad"], f["exp_avg"], f["exp_avg_sq"], segments, betas[0], betas[1], eps)
+        # the kernel wrote through raw pointers: tell autograd and the packed-weight caches
+        torch.autograd.graph.increment_version(list(self._offs))
+        return loss
+
+    def state_dict(self):
+        """torch.optim.AdamW's format; the moments are copied out of the flat buffers."""
+        sd = super().state_dict()
+        sd["state"] = {k: {n: (t.clone() if torch.is_tensor(t) else t) for n, t in v.items()}
+                       for k, v in sd["state"].items()}
+        return sd
+
+    def load_state_dict(self, state_dict) -> None:
+        super().load_state_dict(state_dict)
+        self._adopt_state()
+
+    # ---- data parallel ------------------------------------------------
+    def allreduce_grads(self, group=None) -> None:
+        """Average the gradients over the process group (the reference's DDP, util.py:139-142):
+        ONE all-reduce of the flat gradient buffer.  A missing gradient counts as zero."""
+        if not (dist.is_available() and dist.is_initialized()):
+            return
+        world = dist.get_world_size(group)
+        if world == 1:
+            return
+        for p in self._sync_grads():
+            view = self._view("grad", p)
+            view.zero_()
+            p.grad = view
+        grad = self._flat["grad"]
+        if dist.get_backend(group) == dist.Backend.NCCL:
+            dist.all_reduce(grad, op=dist.ReduceOp.AVG, group=group)
+        else:
+            dist.all_reduce(grad, op=dist.ReduceOp.SUM, group=group)
+            grad.div_(world)
+
+    def broadcast_params(self, src: int = 0, group=None) -> None:
+        """Start every replica from rank ``src``'s parameters (DDP's construction-time
+        broadcast): one broadcast of the flat parameter buffer."""
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+            dist.broadcast(self._flat["param"], src=src, group=group)

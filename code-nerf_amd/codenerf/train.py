@@ -1,0 +1,130 @@
+"""The training step of train.py on the gfx950 kernels.
+
+``prepare_models`` / ``prepare_optimizer`` mirror utils/util.py:93-144 and :147-172;
+``train_iteration`` is train.py:64-114 for one loaded batch (ray sampling and the
+target-pixel gather :76-80, chunking :82-90, then per chunk ``train_minibatch``:
+embedding lookup, hierarchical render, losses, backward, optimiser and scheduler
+steps, :92-114).
+
+By design:
+* the three modules are not wrapped in DDP.  The gradient average DDP performs is
+  ONE all-reduce of the optimiser's flat gradient buffer
+  (``codenerf.optim.AdamW.allreduce_grads``) between ``loss.backward()`` and
+  ``optimizer.step()``; DDP's construction-time broadcast is one broadcast of the
+  flat parameter buffer (``prepare_optimizer``);
+* ``cfg.optimizer.type == "AdamW"`` (every CodeNeRF config) selects the flat
+  one-launch AdamW; any other type is built from ``torch.optim`` as the reference
+  builds it (its update then runs in torch);
+* the embedding lookup folds each chunk's distinct objects
+  (``ShapeTextureEmbedding``), so the code layers run once per object.
+The loss terms keep the reference's definitions, including the regulariser on
+``.data`` (train.py:106-107 through model.py:113-120: a constant, no gradient).
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+from typing import Dict, List
+
+import torch
+import torch.distributed as dist
+
+from . import nerf
+from .models import CodeNeRFModel, ShapeTextureEmbedding, get_params_tensor
+from .optim import AdamW
+from .utils import get_minibatches, mse2psnr
+
+
+def prepare_models(cfg, num_objects: int, device) -> "OrderedDict[str, torch.nn.Module]":
+    """utils/util.py:93-144 without the DDP wrappers (see the module docstring)."""
+    emb_cfg, e = cfg.models.embedding, cfg.nerf.embedder
+    models = OrderedDict()
+    models["embedding"] = ShapeTextureEmbedding(num_embeddings=num_objects, shape_code_size=emb_cfg.shape_code_size,
+                                                texture_code_size=emb_cfg.texture_code_size).to(device)
+    for key in ("nerf_coarse", "nerf_fine"):
+        models[key] = CodeNeRFModel(hidden_size=getattr(cfg.models, key).hidden_size, num_embeddings=num_objects,
+                                    shape_code_size=emb_cfg.shape_code_size,
+                                    texture_code_size=emb_cfg.texture_code_size,
+                                    num_encoding_fn_xyz=e.num_encoding_fn_xyz, include_input_xyz=e.include_input_xyz,
+                                    num_encoding_fn_dir=e.num_encoding_fn_dir,
+                                    include_input_dir=e.include_input_dir).to(device)
+    return models
+
+
+def prepare_optimizer(cfg, models):
+    """utils/util.py:147-172: one optimiser over nerf_coarse, nerf_fine and the embedding
+    (at ``embedding_lr``) and LambdaLR(gamma ** (epoch / step_size))."""
+    groups = [{"params": list(models["nerf_coarse"].parameters())},
+              {"params": list(models["nerf_fine"].parameters())},
+              {"params": list(models["embedding"].parameters()), "lr": cfg.optimizer.embedding_lr}]
+    if cfg.optimizer.type == "AdamW":
+        optimizer = AdamW(groups, lr=cfg.optimizer.lr)
+        if getattr(cfg, "is_distributed", False):
+            optimizer.broadcast_params(0)
+    else:
+        optimizer = getattr(torch.optim, cfg.optimizer.type)(groups, lr=cfg.optimizer.lr)
+    gamma, step_size = cfg.optimizer.scheduler_gamma, cfg.optimizer.scheduler_step_size
+    scheduler = torch.optim.lr_scheduler.LambdaLR(optimizer, lr_lambda=lambda epoch: gamma ** (epoch / step_size))
+    return optimizer, scheduler
+
+
+def _average_gradients(optimizer, models) -> None:
+    if hasattr(optimizer, "allreduce_grads"):
+        optimizer.allreduce_grads()
+        return
+    # a torch optimiser: one coalesced all-reduce of every gradient
+    grads = [p.grad for m in models.values() for p in m.parameters() if p.grad is not None]
+    flat = torch.cat([g.reshape(-1) for g in grads])
+    dist.all_reduce(flat)
+    flat.div_(dist.get_world_size())
+    o = 0
+    for g in grads:
+        g.copy_(flat[o:o + g.numel()].view_as(g))
+        o += g.numel()
+
+
+def train_minibatch(models, optimizer, scheduler, point_sampler, embedders, ro, rd, object_ids, target_pixels,
+                    regularizer_lambda: float, is_distributed: bool = False) -> Dict[str, object]:
+    """train.py:92-114 for one chunk -> the losses train.py logs (tensors) and its psnr (float,
+    read back every chunk as train.py:105 does)."""
+    target_object_embedding = models["embedding"](object_ids)
+    rgb_coarse, rgb_fine = nerf.predict_radiance_and_render((ro, rd), point_sampler, embedders, models["nerf_coarse"],
+                                                            models["nerf_fine"], target_object_embedding)
+    loss_coarse = torch.nn.functional.mse_loss(rgb_coarse[..., :3], target_pixels[..., :3])
+    loss_fine = torch.nn.functional.mse_loss(rgb_fine[..., :3], target_pixels[..., :3])
+    psnr = mse2psnr(loss_fine.item())
+    shape_params, texture_params = get_params_tensor(models["embedding"], is_distributed)
+    regularization = regularizer_lambda * (torch.norm(shape_params, p=2) + torch.norm(texture_params, p=2))
+    loss = loss_coarse + loss_fine + regularization
+    optimizer.zero_grad()
+    loss.backward()
+    if is_distributed:
+        _average_gradients(optimizer, models)
+    optimizer.step()
+    scheduler.step()
+    return {"nerf_loss_coarse": loss_coarse.detach(), "nerf_loss_fine": loss_fine.detach(),
+            "embedding_loss": regularization.detach(), "total_loss": loss.detach(), "psnr": psnr}
+
+
+def train_iteration(cfg, train_data: Dict[str, torch.Tensor], models, optimizer, scheduler, samplers,
+                    embedders) -> List[Dict[str, object]]:
+    """train.py:64-114 for one loaded batch (``color`` (B,H,W,C), ``pose`` (B,4,4), ``object_id``
+    (B,) on the device) -> the per-chunk logs."""
+    ray_sampler, point_sampler = samplers
+    is_distributed = bool(getattr(cfg, "is_distributed", False))
+    for m in models.values():
+        m.train()
+    ro_batch, rd_batch, select_inds = ray_sampler.sample(tform_cam2world=train_data["pose"])
+    n_rays = ray_sampler.sample_size
+    color = train_data["color"].flatten(1, 2)
+    sel = torch.as_tensor(select_inds, device=color.device)
+    target = torch.cat([color[k, sel[k], :] for k in range(color.shape[0])], dim=0)
+    object_ids = train_data["object_id"][:, None].expand(-1, n_rays).reshape(-1)
+    chunk = cfg.nerf.train.chunksize
+    assert chunk <= n_rays * color.shape[0], \
+        "Chunksize needs to atleast be less than to the number of rays sampled from a single image"
+    logs = []
+    for ro, rd, ids, tp in zip(get_minibatches(ro_batch, chunk), get_minibatches(rd_batch, chunk),
+                               get_minibatches(object_ids, chunk), get_minibatches(target, chunk)):
+        logs.append(train_minibatch(models, optimizer, scheduler, point_sampler, embedders, ro, rd, ids, tp,
+                                    cfg.experiment.regularizer_lambda, is_distributed))
+    return logs

@@ -268,6 +268,22 @@ int cn_posenc_backward(const float* x, int64_t m, int64_t d, const float* freqs,
 int cn_ray_points_backward(const float* g_pts, const float* z, int64_t n_rays, int64_t n_samples,
                            float* d_ro, float* d_rd, cn_stream_t stream);
 
+/* --- Training step: the optimiser (train.py:111-114, utils/util.py:147-172) ---
+ * torch.optim.AdamW.step (decoupled weight decay; amsgrad / maximize off) over ONE
+ * flat fp32 buffer holding every trained parameter, with its gradient and both
+ * moments in three more buffers of the same layout (all 16-B aligned).  The update
+ * runs over n_segments ranges [seg_begin[k], seg_end[k]) (HOST int64 arrays, float
+ * offsets, multiples of 4, ascending, disjoint); segment k has its own lr[k],
+ * weight_decay[k] (HOST double arrays) and step[k] (HOST int64, the step number
+ * after this update, >= 1) -- normally one segment per param group; elements in no
+ * segment are not touched.  Per element, in torch's _single_tensor_adam order with
+ * each op rounded to fp32:
+ *   p = p (1 - lr wd); m = lerp(m, g, 1 - beta1); v = v beta2 + ((1 - beta2) g) g;
+ *   p = p + (-lr / (1 - beta1^step)) m / (sqrt(v) / sqrt(1 - beta2^step) + eps). */
+int cn_adamw_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n_segments,
+                  const int64_t* seg_begin, const int64_t* seg_end, const double* lr, const double* weight_decay,
+                  const int64_t* step, double beta1, double beta2, double eps, cn_stream_t stream);
+
 /* fp32 MFMA GEMMs the backward is built from (row-major, leading dims in floats):
  *   cn_gemm_nn: C[M][N] = A[M][K] B[K][N], zeroed where mask[m][n] <= 0 (mask may be NULL); K <= 288;
  *   cn_gemm_tn: C[N][K] += sum_m A[M][N] B[M][K] (accumulates). */

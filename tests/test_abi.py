@@ -57,6 +57,10 @@ def test_argument_errors_need_no_gpu(lib_path):
     assert lib.cn_sample_pdf(None, None, None, 0, None, 1, 300, 8, None, 0, None, None, None) == _lib.CN_EINVAL
     assert lib.cn_radiance_field(None, 0, None, None, 1, None, None, None, None, 1, 1, 1, None, None, None, None) \
         == _lib.CN_EINVAL
+    import ctypes
+    one = (ctypes.c_int64 * 1)(0)
+    assert lib.cn_adamw_step(None, None, None, None, 1, one, one, None, None, one, 0.9, 0.999, 1e-8, None) \
+        == _lib.CN_EINVAL
 
 
 def test_ops_refuse_cpu_tensors():

@@ -1,0 +1,180 @@
+"""Training step on the HIP kernels.
+
+* codenerf.optim.AdamW -- one cn_adamw_step launch over flat buffers -- against
+  torch.optim.AdamW on the CPU, the optimiser the reference instantiates
+  (utils/util.py:159-164), over several steps under LambdaLR with per-group learning
+  rates, including a step where one parameter has no gradient (skipped, as in torch).
+  ADAM_RTOL is relative to each tensor's largest magnitude: the same fp32 op sequence,
+  but torch's CPU kernels may contract a mul+add into an FMA in their scalar tails.
+* one train.py:92-114 chunk step (embedding lookup -> 16+16 render -> losses ->
+  backward -> AdamW -> LambdaLR) against torch autograd over the oracle on the same
+  parameters: the loss within 1e-5 and every parameter / code-table gradient within
+  GRAD_RTOL, for chunks holding one object and several (the per-object code index).
+* a whole train_iteration (ray sampling, target gather, chunk loop) runs and steps.
+"""
+import types
+
+import numpy as np
+import pytest
+import torch
+
+from test_gpu_grad import GRAD_RTOL, O, close, dev, embedders, model, oracle_params  # noqa: F401
+
+pytestmark = pytest.mark.gpu
+
+ADAM_RTOL = 1e-6
+NS = types.SimpleNamespace
+
+
+def test_adamw_matches_torch(dev):
+    from codenerf.optim import AdamW
+    g = torch.Generator().manual_seed(0)
+    shapes = [[(256, 63), (256,), (3, 512), (3,)], [(257, 512), (257,)], [(40, 256), (40, 256)]]
+    lrs = [1e-4, 2e-4, 1e-3]
+    cpu = [[torch.nn.Parameter(torch.randn(*s, generator=g) * 0.1) for s in grp] for grp in shapes]
+    gpu = [[torch.nn.Parameter(p.detach().clone().to(dev)) for p in grp] for grp in cpu]
+    ref = torch.optim.AdamW([{"params": grp, "lr": lr} for grp, lr in zip(cpu, lrs)], lr=1e-4, foreach=False)
+    opt = AdamW([{"params": grp, "lr": lr} for grp, lr in zip(gpu, lrs)], lr=1e-4)
+    lam = lambda e: 0.1 ** (e / 3)  # noqa: E731
+    s_ref = torch.optim.lr_scheduler.LambdaLR(ref, lam)
+    s_opt = torch.optim.lr_scheduler.LambdaLR(opt, lam)
+    pc = [p for grp in cpu for p in grp]
+    pg = [p for grp in gpu for p in grp]
+    for it in range(6):
+        for a, b in zip(pc, pg):
+            scale = 10.0 ** float(torch.randint(-6, 1, (1,), generator=g))
+            gr = torch.randn(a.shape, generator=g) * scale
+            a.grad, b.grad = gr.clone(), gr.to(dev)
+        if it == 3:
+            pc[1].grad = None
+            pg[1].grad = None
+        ref.step()
+        opt.step()
+        s_ref.step()
+        s_opt.step()
+        ref.zero_grad()
+        opt.zero_grad()
+    for a, b in zip(pc, pg):
+        close(b.detach(), a.detach(), ADAM_RTOL, "param")
+        close(opt.state[b]["exp_avg"], ref.state[a]["exp_avg"], ADAM_RTOL, "exp_avg")
+        close(opt.state[b]["exp_avg_sq"], ref.state[a]["exp_avg_sq"], ADAM_RTOL, "exp_avg_sq")
+        assert float(opt.state[b]["step"]) == float(ref.state[a]["step"])
+    assert float(opt.state[pg[1]]["step"]) == 5.0
+
+
+def test_adamw_state_dict_interop(dev):
+    """Optimiser checkpoints (train.py:130-137) move between this AdamW and torch.optim.AdamW."""
+    from codenerf.optim import AdamW
+    g = torch.Generator().manual_seed(1)
+    ps = [torch.nn.Parameter(torch.randn(64, 32, generator=g).to(dev)) for _ in range(3)]
+    opt = AdamW([{"params": ps[:2]}, {"params": ps[2:], "lr": 1e-3}], lr=1e-4)
+    for _ in range(2):
+        for p in ps:
+            p.grad = torch.randn(p.shape, generator=g).to(dev)
+        opt.step()
+    ref_ps = [torch.nn.Parameter(p.detach().clone()) for p in ps]
+    ref = torch.optim.AdamW([{"params": ref_ps[:2]}, {"params": ref_ps[2:], "lr": 1e-3}], lr=1e-4)
+    ref.load_state_dict(opt.state_dict())
+    for p, q in zip(ps, ref_ps):
+        assert torch.equal(ref.state[q]["exp_avg"], opt.state[p]["exp_avg"])
+        assert float(ref.state[q]["step"]) == 2.0
+    qs = [torch.nn.Parameter(p.detach().clone()) for p in ps]
+    opt2 = AdamW([{"params": qs[:2]}, {"params": qs[2:], "lr": 1e-3}], lr=1e-4)
+    opt2.load_state_dict(ref.state_dict())
+    f = opt2.flat_buffers()
+    for p, q in zip(ps, qs):
+        st = opt2.state[q]
+        assert torch.equal(st["exp_avg_sq"], opt.state[p]["exp_avg_sq"])
+        assert st["exp_avg"].data_ptr() - f["exp_avg"].data_ptr() == q.data_ptr() - f["param"].data_ptr()
+    for p, q in zip(ps, qs):                     # both continue identically
+        gr = torch.randn(p.shape, generator=g).to(dev)
+        p.grad, q.grad = gr.clone(), gr.clone()
+    opt.step()
+    opt2.step()
+    for p, q in zip(ps, qs):
+        assert torch.equal(p.detach(), q.detach())
+
+
+def _train_models(dev, n_obj):
+    from codenerf.models import ShapeTextureEmbedding
+    emb = ShapeTextureEmbedding(n_obj, 256, 256)
+    g = torch.Generator().manual_seed(11)
+    with torch.no_grad():
+        emb.shape_embedding.weight.copy_(torch.randn(n_obj, 256, generator=g) * 0.3)
+        emb.texture_embedding.weight.copy_(torch.randn(n_obj, 256, generator=g) * 0.3)
+    return {"embedding": emb.to(dev), "nerf_coarse": model(dev, 0), "nerf_fine": model(dev, 1)}
+
+
+def _opt_cfg():
+    return NS(optimizer=NS(type="AdamW", lr=1e-4, embedding_lr=1e-3, scheduler_gamma=0.1,
+                           scheduler_step_size=5000000))
+
+
+@pytest.mark.parametrize("chunk,mixed", [(64, False), (128, True)])
+def test_train_minibatch_matches_oracle(dev, chunk, mixed):
+    from codenerf import train as T
+    from codenerf.nerf import PointSampler
+    o = O()
+    n_obj, n, lam = 3, 128, 1e-5
+    models = _train_models(dev, n_obj)
+    g = torch.Generator().manual_seed(chunk)
+    ro = torch.randn(n, 3, generator=g) * 0.1 + torch.tensor([0.0, 0.0, 1.3])
+    rd = torch.randn(n, 3, generator=g) * 0.2 + torch.tensor([0.0, 0.0, -1.0])
+    ids = torch.randint(0, n_obj, (n,), generator=g) if mixed else torch.tensor([0] * 64 + [2] * 64)
+    tgt = torch.rand(n, 4, generator=g)
+    opt, sched = T.prepare_optimizer(_opt_cfg(), models)
+    ps = PointSampler(16, 16, 0.8, 1.8, spacing_mode="lindepth", perturb=False, dtype=torch.float32, device=dev)
+    emb = embedders(dev)
+    smp, ecfg = o.Sampling(16, 16, 0.8, 1.8), o.EmbedCfg()
+    for c0 in range(0, n, chunk):
+        sl = slice(c0, c0 + chunk)
+        # the oracle on the current parameters: the reference's chunk step under torch autograd
+        pc, pf = oracle_params(models["nerf_coarse"]), oracle_params(models["nerf_fine"])
+        ts = models["embedding"].shape_embedding.weight.detach().cpu().clone().requires_grad_(True)
+        tt = models["embedding"].texture_embedding.weight.detach().cpu().clone().requires_grad_(True)
+        out = o.predict_radiance_and_render(ro[sl], rd[sl], smp, ecfg, pc, pf, ts[ids[sl]], tt[ids[sl]])
+        lc = torch.nn.functional.mse_loss(out["rgb_coarse"][..., :3], tgt[sl, :3])
+        lf = torch.nn.functional.mse_loss(out["rgb_fine"][..., :3], tgt[sl, :3])
+        loss = lc + lf + lam * (torch.norm(ts.detach(), p=2) + torch.norm(tt.detach(), p=2))
+        loss.backward()
+        logs = T.train_minibatch(models, opt, sched, ps, emb, ro[sl].to(dev), rd[sl].to(dev), ids[sl].to(dev),
+                                 tgt[sl].to(dev), lam)
+        assert abs(float(logs["total_loss"]) - loss.item()) <= 1e-5
+        for key, ref in (("nerf_coarse", pc), ("nerf_fine", pf)):
+            for name, prm in models[key].named_parameters():
+                close(prm.grad, ref[name].grad, what=f"{key}.{name}")
+        close(models["embedding"].shape_embedding.weight.grad, ts.grad, what="shape table")
+        close(models["embedding"].texture_embedding.weight.grad, tt.grad, what="texture table")
+    assert float(opt.state[models["nerf_fine"].fc_rgb.weight]["step"]) == n // chunk
+    assert sched.last_epoch == n // chunk
+
+
+def test_train_iteration_runs(dev):
+    from codenerf import nerf as N, synthetic, train as T
+    from codenerf.evaluate import pose_spherical
+    cfg = NS(is_distributed=False,
+             models=NS(embedding=NS(shape_code_size=256, texture_code_size=256), nerf_coarse=NS(hidden_size=256),
+                       nerf_fine=NS(hidden_size=256)),
+             nerf=NS(embedder=NS(num_encoding_fn_xyz=10, include_input_xyz=True, log_sampling_xyz=True,
+                                 num_encoding_fn_dir=4, include_input_dir=True, log_sampling_dir=True,
+                                 use_viewdirs=True),
+                     ray_sampler=NS(num_random_rays=96),
+                     point_sampler=NS(num_coarse=16, num_fine=16, near_limit=0.8, far_limit=1.8,
+                                      spacing_mode="lindepth", perturb=True),
+                     train=NS(chunksize=64)),
+             optimizer=_opt_cfg().optimizer, experiment=NS(regularizer_lambda=1e-5))
+    torch.manual_seed(0)
+    np.random.seed(0)
+    models = T.prepare_models(cfg, 5, dev)
+    opt, sched = T.prepare_optimizer(cfg, models)
+    samplers = N.prepare_samplers(cfg, 32, 32, synthetic.srn_intrinsics(32, 35.0), torch.float32, dev)
+    embs = N.prepare_embedders(cfg, torch.float32, dev)
+    poses = torch.stack([pose_spherical(torch.tensor(0.5 + 0.4 * i), torch.tensor(0.3), torch.tensor(1.3))
+                         for i in range(2)])
+    data = {"color": torch.rand(2, 32, 32, 4).to(dev), "pose": poses.to(dev), "object_id": torch.tensor([1, 3]).to(dev)}
+    before = [p.detach().clone() for p in models["nerf_fine"].parameters()]
+    logs = T.train_iteration(cfg, data, models, opt, sched, samplers, embs)
+    assert len(logs) == 3                        # 2 x 96 rays in chunks of 64 (the middle one holds both objects)
+    assert all(np.isfinite(float(lg["total_loss"])) for lg in logs)
+    assert any(not torch.equal(a, b.detach()) for a, b in zip(before, models["nerf_fine"].parameters()))
+    assert sched.last_epoch == 3

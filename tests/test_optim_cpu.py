@@ -1,0 +1,124 @@
+"""Flat-buffer AdamW host logic on the CPU.
+
+The update itself is one HIP kernel (cn_adamw_step; tests/test_gpu_train.py holds it
+against torch.optim.AdamW).  Here: the flat layout (values kept, 256-B aligned views,
+gradients landing in the flat buffer), zero_grad semantics, the refusal to update
+without a GPU, and the data-parallel pieces -- the gradient average and the
+start-of-training parameter broadcast -- over gloo with 2 ranks.
+"""
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+SHAPES = [(256, 63), (256,), (3, 512), (3,), (40, 256)]
+
+
+def _params(seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return [torch.nn.Parameter(torch.randn(*s, generator=g)) for s in SHAPES]
+
+
+def _opt(ps):
+    from codenerf.optim import AdamW
+    return AdamW([{"params": ps[:4]}, {"params": ps[4:], "lr": 1e-3}], lr=1e-4)
+
+
+def test_flat_layout_keeps_values_and_aliases():
+    from codenerf.optim import ALIGN
+    ps = _params()
+    before = [p.detach().clone() for p in ps]
+    opt = _opt(ps)
+    f = opt.flat_buffers()
+    assert set(f) == {"param", "grad", "exp_avg", "exp_avg_sq"}
+    starts = opt.group_starts
+    assert len(starts) == 3 and starts[0] == 0 and starts[-1] <= f["param"].numel()
+    for p, b in zip(ps, before):
+        assert torch.equal(p.detach(), b)
+        assert (p.data_ptr() - f["param"].data_ptr()) // 4 % ALIGN == 0
+    with torch.no_grad():
+        f["param"].add_(1.0)                      # the parameters are views of the buffer
+    assert torch.equal(ps[2].detach(), before[2] + 1.0)
+
+
+def test_gradients_land_in_the_flat_buffer():
+    ps = _params()
+    opt = _opt(ps)
+    opt.zero_grad()
+    assert all(p.grad is None for p in ps)
+    sum((p * p).sum() for p in ps[:3]).backward()     # ps[3], ps[4] get no gradient
+    missing = opt._sync_grads()
+    assert [id(p) for p in missing] == [id(p) for p in ps[3:]]
+    f = opt.flat_buffers()
+    for p in ps[:3]:
+        assert p.grad.data_ptr() - f["grad"].data_ptr() == p.data_ptr() - f["param"].data_ptr()
+        assert torch.equal(p.grad, 2 * p.detach())
+    opt.zero_grad(set_to_none=False)
+    assert all(p.grad is not None and not p.grad.any() for p in ps)
+
+
+def test_step_needs_the_gpu():
+    ps = _params()
+    opt = _opt(ps)
+    for p in ps:
+        p.grad = torch.ones_like(p)
+    with pytest.raises(ValueError, match="no CPU fallback"):
+        opt.step()
+
+
+def test_refuses_unsupported_options():
+    from codenerf.optim import AdamW
+    with pytest.raises(NotImplementedError):
+        AdamW(_params(), amsgrad=True)
+    with pytest.raises(TypeError):
+        AdamW([torch.nn.Parameter(torch.zeros(3, dtype=torch.float64))])
+
+
+def test_state_dict_matches_torch_layout():
+    ps = _params()
+    opt = _opt(ps)
+    ref = torch.optim.AdamW([{"params": _params()[:4]}, {"params": _params()[4:], "lr": 1e-3}], lr=1e-4)
+    a, b = opt.state_dict(), ref.state_dict()
+    assert a["state"] == {} and [g["params"] for g in a["param_groups"]] == [g["params"] for g in b["param_groups"]]
+    assert set(a["param_groups"][0]) == set(b["param_groups"][0])
+
+
+def _dp_worker(rank, world, port, out):
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        ps = _params(seed=rank)                  # replicas start apart (train.py:29-31 seeds by rank)
+        opt = _opt(ps)
+        opt.broadcast_params(0)
+        for p in ps:
+            p.grad = torch.full_like(p, float(rank + 1))
+        if rank == 1:
+            ps[3].grad = None                    # absent on one rank: counts as zero
+        opt.allreduce_grads()
+        np.savez(out.format(rank), params=torch.cat([p.detach().reshape(-1) for p in ps]).numpy(),
+                 grads=torch.cat([p.grad.reshape(-1) for p in ps]).numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_allreduce_and_broadcast_gloo(tmp_path):
+    world = 2
+    out = str(tmp_path / "r{}.npz")
+    mp.start_processes(_dp_worker, args=(world, _free_port(), out), nprocs=world, join=True, start_method="spawn")
+    r0, r1 = np.load(out.format(0)), np.load(out.format(1))
+    ref = torch.cat([p.detach().reshape(-1) for p in _params(seed=0)]).numpy()
+    assert np.array_equal(r0["params"], ref) and np.array_equal(r1["params"], ref)
+    sizes = [int(np.prod(s)) for s in SHAPES]
+    exp = np.concatenate([np.full(n, 1.5, np.float32) for n in sizes])
+    o3 = sum(sizes[:3])
+    exp[o3:o3 + sizes[3]] = 0.5                   # (1 + 0) / 2
+    assert np.array_equal(r0["grads"], exp) and np.array_equal(r1["grads"], exp)
