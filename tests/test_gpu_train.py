@@ -111,9 +111,31 @@ def _opt_cfg():
 
 
 @pytest.mark.parametrize("chunk,mixed", [(64, False), (128, True)])
-def test_train_minibatch_matches_oracle(dev, chunk, mixed):
-    from codenerf import train as T
+def test_train_minibatch_matches_oracle(dev, monkeypatch, chunk, mixed):
+    """The oracle re-uses two discrete decisions of the kernels' forward, as in the fused eval
+    test: the fine depths (sample_pdf's searchsorted can pick the neighbouring bin when the
+    coarse weights differ in the last bit) and the ReLU decisions (read from the saved
+    activations); both are properties of the reference's discontinuities, not kernel error."""
+    from codenerf import ops, train as T
     from codenerf.nerf import PointSampler
+    seen = {"z_fine": None, "saved": []}
+    real_pdf, real_train = ops.sample_pdf, ops.radiance_field_train
+
+    def spy_pdf(*a, **k):
+        r = real_pdf(*a, **k)
+        seen["z_fine"] = r[1].detach().cpu()
+        return r
+
+    def spy_train(*a, **k):
+        raw, saved = real_train(*a, **k)
+        seen["saved"].append(saved)
+        return raw, saved
+    monkeypatch.setattr(ops, "sample_pdf", spy_pdf)
+    monkeypatch.setattr(ops, "radiance_field_train", spy_train)
+
+    def relu_masks(saved):
+        sv = saved.detach().cpu()
+        return {k: (sv[i] > 0).float() for k, i in (("h1", 0), ("h2", 1), ("v1", 3), ("v2", 4))}
     o = O()
     n_obj, n, lam = 3, 128, 1e-5
     models = _train_models(dev, n_obj)
@@ -132,13 +154,20 @@ def test_train_minibatch_matches_oracle(dev, chunk, mixed):
         pc, pf = oracle_params(models["nerf_coarse"]), oracle_params(models["nerf_fine"])
         ts = models["embedding"].shape_embedding.weight.detach().cpu().clone().requires_grad_(True)
         tt = models["embedding"].texture_embedding.weight.detach().cpu().clone().requires_grad_(True)
-        out = o.predict_radiance_and_render(ro[sl], rd[sl], smp, ecfg, pc, pf, ts[ids[sl]], tt[ids[sl]])
-        lc = torch.nn.functional.mse_loss(out["rgb_coarse"][..., :3], tgt[sl, :3])
-        lf = torch.nn.functional.mse_loss(out["rgb_fine"][..., :3], tgt[sl, :3])
-        loss = lc + lf + lam * (torch.norm(ts.detach(), p=2) + torch.norm(tt.detach(), p=2))
-        loss.backward()
+        seen["saved"].clear()
         logs = T.train_minibatch(models, opt, sched, ps, emb, ro[sl].to(dev), rd[sl].to(dev), ids[sl].to(dev),
                                  tgt[sl].to(dev), lam)
+        r, d = ro[sl], rd[sl]
+        zs, zt = ts[ids[sl]], tt[ids[sl]]
+        pts_c, z_c = o.sample_uniform(r, d, smp.bins, None)
+        rgb_c = o.volume_render(o.forward_pass(pc, ecfg, d, pts_c, zs, zt, relu_masks(seen["saved"][0])), z_c, d)[0]
+        z_f = seen["z_fine"]
+        pts_f = r[..., None, :] + d[..., None, :] * z_f[..., :, None]
+        rgb_f = o.volume_render(o.forward_pass(pf, ecfg, d, pts_f, zs, zt, relu_masks(seen["saved"][1])), z_f, d)[0]
+        lc = torch.nn.functional.mse_loss(rgb_c[..., :3], tgt[sl, :3])
+        lf = torch.nn.functional.mse_loss(rgb_f[..., :3], tgt[sl, :3])
+        loss = lc + lf + lam * (torch.norm(ts.detach(), p=2) + torch.norm(tt.detach(), p=2))
+        loss.backward()
         assert abs(float(logs["total_loss"]) - loss.item()) <= 1e-5
         for key, ref in (("nerf_coarse", pc), ("nerf_fine", pf)):
             for name, prm in models[key].named_parameters():
