@@ -9,6 +9,8 @@
 //   seg_sum  out[code(m)][j] += A[m][j]                               per-object code-term gradients
 // and the element-wise pieces: posenc backward, the Q1 view-direction scatter,
 // pts = ro + rd z backward, and the code-layer backward.
+#include <algorithm>
+
 #include "cn_common.h"
 #include "mlp_common.h"
 
@@ -19,29 +21,31 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 // ---------------------------------------------------------------- GEMMs
 
-// gemm_nn: 256 x 64 output tile per 256-thread block, 64 x 64 per wave (2 x 2
-// v_mfma_f32_32x32x2_f32 tiles, 64 accumulators).  k runs in tiles of 16; inside
+// gemm_nn: 256 x NT output tile per 256-thread block, 64 x NT per wave (2 x NT/32
+// v_mfma_f32_32x32x2_f32 tiles; NT = 128 for the 256-wide layers halves the passes over A).  k runs in tiles of 16; inside
 // a tile lane half h owns k = h*8 .. h*8+7, so MFMA step kk pairs k = kk and
 // 8 + kk -- any pairing of k between the A and B operands gives the same sum,
 // and this one makes each lane's A values 8 consecutive floats of its row (read
 // straight from global memory, no LDS) and its B values 8 consecutive floats
-// of B^T.  B^T (64 columns x K) is staged in LDS once per block.
-constexpr int kNT = 64, kMT = 256, kKT = 16;
-constexpr int kMaxK = 288;  // B^T tile in LDS: 64 x 288 floats = 72 KiB
+// of B^T.  B^T (NT columns x K) is staged in LDS once per block.
+constexpr int kMT = 256, kKT = 16;
+constexpr int kMaxK = 288;  // B^T tile in LDS: 64 x 292 floats = 73 KiB
 
+template <int NT>
 __global__ __launch_bounds__(256) void gemm_nn_kernel(const float* __restrict__ A, int64_t lda,
                                                       const float* __restrict__ B, int64_t ldb,
                                                       float* __restrict__ C, int64_t ldc,
                                                       const float* __restrict__ mask, int64_t ldm,
                                                       int64_t M, int N, int K) {
-  __shared__ __attribute__((aligned(16))) float Bt[kNT][kMaxK + 4];
+  constexpr int NU = NT / 32;
+  __shared__ __attribute__((aligned(16))) float Bt[NT][kMaxK + 4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int i = lane & 31, h = lane >> 5;
-  const int n0 = blockIdx.y * kNT;
+  const int n0 = blockIdx.y * NT;
   const int kp = (K + kKT - 1) / kKT * kKT;
   // B^T: Bt[n][k] = B[k][n0 + n] (zero outside K x N)
-  for (int e = tid; e < kNT * kp; e += 256) {
-    const int k = e / kNT, n = e % kNT;
+  for (int e = tid; e < NT * kp; e += 256) {
+    const int k = e / NT, n = e % NT;
     Bt[n][k] = (k < K && n0 + n < N) ? B[(int64_t)k * ldb + n0 + n] : 0.0f;
   }
   __syncthreads();
@@ -54,17 +58,27 @@ __global__ __launch_bounds__(256) void gemm_nn_kernel(const float* __restrict__ 
     rv[t] = rows[t] < M;
     if (!rv[t]) rows[t] = M - 1;
   }
-  floatx16 acc[2][2] = {};
-  for (int k0 = 0; k0 < kp; k0 += kKT) {
-    float a[2][8], b[2][8];
+  floatx16 acc[2][NU] = {};
+  // A of k-tile k0 + kKT is loaded while k-tile k0's MFMAs run (register double buffer)
+  auto load_a = [&](int k0, float (&a)[2][8]) {
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const float* ar = A + rows[t] * lda + k0 + h * 8;
 #pragma unroll
       for (int q = 0; q < 8; ++q) a[t][q] = (k0 + h * 8 + q < K) ? ar[q] : 0.0f;
     }
+  };
+  float an[2][8];
+  load_a(0, an);
+  for (int k0 = 0; k0 < kp; k0 += kKT) {
+    float a[2][8], b[NU][8];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) a[t][q] = an[t][q];
+    if (k0 + kKT < kp) load_a(k0 + kKT, an);
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
       const float4* bp = reinterpret_cast<const float4*>(&Bt[32 * u + i][k0 + h * 8]);
       const float4 x = bp[0], y = bp[1];
       b[u][0] = x.x; b[u][1] = x.y; b[u][2] = x.z; b[u][3] = x.w;
@@ -75,13 +89,13 @@ __global__ __launch_bounds__(256) void gemm_nn_kernel(const float* __restrict__ 
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
+        for (int u = 0; u < NU; ++u)
           acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[t][kk], b[u][kk], acc[t][u], 0, 0, 0);
   }
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < NU; ++u) {
       const int col = n0 + 32 * u + i;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -95,44 +109,65 @@ __global__ __launch_bounds__(256) void gemm_nn_kernel(const float* __restrict__ 
     }
 }
 
-constexpr int kBN = 64, kBK = 32;  // gemm_tn tiles
-constexpr int kSliceM = 2048;  // rows reduced per block before the atomic flush
+// gemm_tn: C[n][k] += sum_m A[m][n] B[m][k] (dW = dPre^T X).  No LDS: on
+// v_mfma_f32_32x32x2_f32 lane l's A operand is A[m + (l >> 5)][n + (l & 31)] and its B
+// operand B[m + (l >> 5)][k + (l & 31)], so each half-wave reads 32 consecutive floats of
+// one row straight from global memory (L2).  Block = 4 waves over a 128 x 128 output
+// tile, each wave 64 x 64 = 2 x 2 accumulators (4 independent MFMAs per row pair); M is
+// split over blockIdx.z (rows_per_block rows each, sized so the grid fills the chip) and
+// each block flushes its partial tile with one atomic per output.  Rows are consumed
+// kTnPairs pairs at a time: all loads of a group are issued before its MFMAs.
+constexpr int kTnTile = 128, kTnPairs = 8;
 
 __global__ __launch_bounds__(256) void gemm_tn_kernel(const float* __restrict__ A, int64_t lda,
                                                       const float* __restrict__ B, int64_t ldb,
                                                       float* __restrict__ C, int64_t ldc, int64_t M,
-                                                      int N, int K) {
-  __shared__ float As[kBK][kBN];   // [m][n]
-  __shared__ float Bs[kBK][kBN];   // [m][k]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
-  const int n0 = blockIdx.x * kBN, k0 = blockIdx.y * kBN;
-  const int64_t mb = (int64_t)blockIdx.z * kSliceM;
-  const int64_t me = min(M, mb + kSliceM);
-  floatx16 acc = {0};
-  for (int64_t m0 = mb; m0 < me; m0 += kBK) {
+                                                      int N, int K, int64_t rows_per_block) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i = lane & 31, h = lane >> 5;
+  const int n0 = blockIdx.x * kTnTile + (wave >> 1) * 64;
+  const int k0 = blockIdx.y * kTnTile + (wave & 1) * 64;
+  if (n0 >= N || k0 >= K) return;  // wave-uniform
+  const int64_t mb = (int64_t)blockIdx.z * rows_per_block;
+  const int64_t me = min(M, mb + rows_per_block);
+  // columns past N / K compute rows / columns of C that are never stored: clamp, no zeroing
+  const int na0 = min(n0 + i, N - 1), na1 = min(n0 + 32 + i, N - 1);
+  const int kb0 = min(k0 + i, K - 1), kb1 = min(k0 + 32 + i, K - 1);
+  floatx16 acc00 = {0}, acc01 = {0}, acc10 = {0}, acc11 = {0};
+  for (int64_t m = mb; m < me; m += 2 * kTnPairs) {
+    float a0[kTnPairs], a1[kTnPairs], b0[kTnPairs], b1[kTnPairs];
 #pragma unroll
-    for (int i = 0; i < (kBK * kBN) / 256; ++i) {
-      const int e = i * 256 + tid, r = e / kBN, c = e % kBN;
-      const int64_t m = m0 + r;
-      As[r][c] = (m < me && n0 + c < N) ? A[m * lda + n0 + c] : 0.0f;
-      Bs[r][c] = (m < me && k0 + c < K) ? B[m * ldb + k0 + c] : 0.0f;
+    for (int p = 0; p < kTnPairs; ++p) {
+      const int64_t r = m + 2 * p + h;
+      const bool ok = r < me;
+      const float* ar = A + (ok ? r : mb) * lda;
+      const float* br = B + (ok ? r : mb) * ldb;
+      a0[p] = ok ? ar[na0] : 0.0f;   // a zero A row adds nothing, whatever B holds
+      a1[p] = ok ? ar[na1] : 0.0f;
+      b0[p] = br[kb0];
+      b1[p] = br[kb1];
     }
-    __syncthreads();
 #pragma unroll
-    for (int kk = 0; kk < kBK; kk += 2) {
-      const float a = As[kk + (lane >> 5)][32 * wr + (lane & 31)];
-      const float b = Bs[kk + (lane >> 5)][32 * wc + (lane & 31)];
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+    for (int p = 0; p < kTnPairs; ++p) {
+      acc00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[p], b0[p], acc00, 0, 0, 0);
+      acc01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[p], b1[p], acc01, 0, 0, 0);
+      acc10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[p], b0[p], acc10, 0, 0, 0);
+      acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[p], b1[p], acc11, 0, 0, 0);
     }
-    __syncthreads();
   }
-  const int col = k0 + 32 * wc + (lane & 31);
+  const floatx16* accs[4] = {&acc00, &acc01, &acc10, &acc11};
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int row = n0 + 32 * wr + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-    if (row < N && col < K) atomicAdd(&C[(int64_t)row * ldc + col], acc[r]);
-  }
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const floatx16& acc = *accs[2 * t + u];
+      const int col = k0 + 32 * u + i;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = n0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row < N && col < K) atomicAdd(&C[(int64_t)row * ldc + col], acc[r]);
+      }
+    }
 }
 
 // out[code(m)][j] += A[m][j] for j < N; code(m) = code_index ? code_index[m / S]
@@ -392,16 +427,24 @@ namespace {
 int gemm_nn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, const float* mask,
             int64_t ldm, int64_t M, int N, int K, hipStream_t st) {
   if (K > grad::kMaxK) return CN_EINVAL;
-  dim3 grid(static_cast<unsigned>(ceil_div(M, grad::kMT)), static_cast<unsigned>(ceil_div(N, grad::kNT)));
-  hipLaunchKernelGGL(grad::gemm_nn_kernel, grid, dim3(256), 0, st, A, lda, B, ldb, C, ldc, mask, ldm, M, N, K);
+  // 64 columns per block (2 blocks per CU); 128 (one 146 KiB block per CU, 1 wave per SIMD)
+  // measured 12 % slower over the training step's layers
+  dim3 grid(static_cast<unsigned>(ceil_div(M, grad::kMT)), static_cast<unsigned>(ceil_div(N, 64)));
+  hipLaunchKernelGGL(grad::gemm_nn_kernel<64>, grid, dim3(256), 0, st, A, lda, B, ldb, C, ldc, mask, ldm, M, N, K);
   return launch_status();
 }
 
 int gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M, int N, int K,
             hipStream_t st) {
-  dim3 grid(static_cast<unsigned>(ceil_div(N, grad::kBN)), static_cast<unsigned>(ceil_div(K, grad::kBN)),
-            static_cast<unsigned>(ceil_div(M, grad::kSliceM)));
-  hipLaunchKernelGGL(grad::gemm_tn_kernel, grid, dim3(256), 0, st, A, lda, B, ldb, C, ldc, M, N, K);
+  // about 1024 blocks (4 per CU) over the M split, at least 256 rows each, a multiple of the
+  // row group so only the last block has a ragged tail
+  const int64_t tiles = ceil_div(N, grad::kTnTile) * ceil_div(K, grad::kTnTile);
+  const int64_t splits = std::max<int64_t>(1, 1024 / tiles);
+  int64_t rows = std::max<int64_t>(256, ceil_div(M, splits));
+  rows = ceil_div(rows, 2 * grad::kTnPairs) * 2 * grad::kTnPairs;
+  dim3 grid(static_cast<unsigned>(ceil_div(N, grad::kTnTile)), static_cast<unsigned>(ceil_div(K, grad::kTnTile)),
+            static_cast<unsigned>(ceil_div(M, rows)));
+  hipLaunchKernelGGL(grad::gemm_tn_kernel, grid, dim3(256), 0, st, A, lda, B, ldb, C, ldc, M, N, K, rows);
   return launch_status();
 }
 
