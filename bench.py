@@ -346,7 +346,7 @@ def train_bench(dev, k, iters, world):
             "params": n_params, "loss": float(logs[-1]["total_loss"]),
             "adamw": {"kernel_ms": adamw_ms, "bytes": 28 * n_params,
                       "gbps": 28 * n_params / (adamw_ms * 1e-3) / 1e9},
-            "note": "fp32 training field kernel (activations kept), layer-wise fp32 MFMA backward, "
+            "note": "fp32 training field kernel (activations kept), layer-wise 3xbf16 MFMA backward GEMMs, "
                     "flat AdamW; train.py's per-chunk psnr read-back included"}
 
 

@@ -51,6 +51,8 @@ SIGNATURES = {
     "cn_field_backward_workspace_floats": (_i64, [_i64]),
     "cn_field_backward": (_i, [ctypes.POINTER(_p), _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p, _i64, _fp, _fp,
                                _p, ctypes.POINTER(_p), _p, _p, _p, _p, _p]),
+    "cn_field_backward_fmt": (_i, [_i, ctypes.POINTER(_p), _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p, _i64,
+                                   _fp, _fp, _p, ctypes.POINTER(_p), _p, _p, _p, _p, _p]),
     "cn_field_mask_words": (_i64, [_i64]),
     "cn_radiance_field_masks": (_i, [_p, _p, _p, _i64, _p, _p, _p, _p, _i64, _i64, _i64, _fp, _fp, _p, _p, _p]),
     "cn_field_backward_x3": (_i, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p, _i64, _fp, _fp, _p, _p, _p, _p,
@@ -63,6 +65,8 @@ SIGNATURES = {
     "cn_ray_points_backward": (_i, [_p, _p, _i64, _i64, _p, _p, _p]),
     "cn_gemm_nn":(_i, [_p, _i64, _p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _p]),
     "cn_gemm_tn": (_i, [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _p]),
+    "cn_gemm_nn_x3": (_i, [_p, _i64, _p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _p]),
+    "cn_gemm_tn_x3": (_i, [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _p]),
     "cn_adamw_step": (_i, [_p, _p, _p, _p, _i64, ctypes.POINTER(_i64), ctypes.POINTER(_i64),
                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i64),
                            ctypes.c_double, ctypes.c_double, ctypes.c_double, _p]),

@@ -201,7 +201,7 @@ class RadianceField(torch.autograd.Function):
         r = ops.field_backward(params, ctx.acts, ctx.x_enc, g_raw.contiguous(), rd.shape[0], meta.n_samples,
                                meta.chunk_rows, z_s.shape[0], meta.fx, meta.fd, rd=rd, pts=pts, ro=ro, z=z,
                                code_index=meta.code_index, param_grads=pg, want_code=want_z or pg is not None,
-                               want_pts=needs[2], want_ro=needs[3], want_rd=needs[1])
+                               want_pts=needs[2], want_ro=needs[3], want_rd=needs[1], precision=meta.precision)
         dz_s = dz_t = None
         if r["g_code"] is not None:
             dz_s, dz_t = ops.code_bias_backward(params, z_s, z_t, r["g_code"], pg, want_z=want_z)

@@ -369,10 +369,12 @@ def field_backward(params: Sequence[Tensor], saved: Tensor, x_enc: Tensor, d_raw
                    rd: Optional[Tensor] = None, pts: Optional[Tensor] = None, ro: Optional[Tensor] = None,
                    z: Optional[Tensor] = None, code_index: Optional[Tensor] = None,
                    param_grads: Optional[Sequence[Tensor]] = None, want_code: bool = False,
-                   want_pts: bool = False, want_ro: bool = False, want_rd: bool = False, want_x: bool = False):
+                   want_pts: bool = False, want_ro: bool = False, want_rd: bool = False, want_x: bool = False,
+                   precision: str = "f32"):
     """Backward of forward_pass + CodeNeRFModel.forward -> dict of d_pts / d_ro / d_rd / g_code / d_x.
 
     ``param_grads``: 18 zero-or-running fp32 buffers the parameter gradients accumulate into.
+    ``precision``: the GEMMs' arithmetic, "f32" (exact products) or "bf16x3" (split bf16 MFMA).
     """
     lib = _lib_ready()
     m = n_rays * n_samples
@@ -396,9 +398,9 @@ def field_backward(params: Sequence[Tensor], saved: Tensor, x_enc: Tensor, d_raw
         garr, gkeep = _lib.pointer_array(list(param_grads))
     fx = _lib.host_floats(freqs_xyz) if freqs_xyz is not None else None
     fd = _lib.host_floats(freqs_dir) if freqs_dir is not None else None
-    check(lib.cn_field_backward(arr, ptr(saved), ptr(x_enc), ptr(d_raw), ptr(pts), ptr(ro), ptr(rd), ptr(z), n_rays,
+    check(lib.cn_field_backward_fmt(_lib.FORMATS[precision], arr, ptr(saved), ptr(x_enc), ptr(d_raw), ptr(pts), ptr(ro), ptr(rd), ptr(z), n_rays,
                                 n_samples, chunk_rows, ptr(code_index), n_codes, fx, fd, ptr(ws), garr, ptr(g_code),
-                                ptr(d_pts), ptr(d_ro), ptr(d_rd), stream_of(d_raw)), "cn_field_backward")
+                                ptr(d_pts), ptr(d_ro), ptr(d_rd), stream_of(d_raw)), "cn_field_backward_fmt")
     del keep, gkeep
     out.update(g_code=g_code, d_pts=d_pts, d_ro=d_ro, d_rd=d_rd)
     if want_x:
@@ -426,27 +428,29 @@ def code_bias_backward(params: Sequence[Tensor], z_s: Tensor, z_t: Tensor, g_cod
     return dz_s, dz_t
 
 
-def gemm_nn(a: Tensor, b: Tensor, mask: Optional[Tensor] = None) -> Tensor:
-    """C = A B (masked where mask <= 0) on the fp32 MFMA tile kernel."""
+def gemm_nn(a: Tensor, b: Tensor, mask: Optional[Tensor] = None, precision: str = "f32") -> Tensor:
+    """C = A B (masked where mask <= 0) on the fp32 (or 3xbf16) MFMA tile kernel."""
     lib = _lib_ready()
     a, b = _cuda(a, "A"), _cuda(b, "B")
     (m, k), (k2, n) = a.shape, b.shape
     assert k == k2
     mask = _opt(mask, "mask")
     c = torch.empty(m, n, device=a.device, dtype=torch.float32)
-    check(lib.cn_gemm_nn(ptr(a), k, ptr(b), n, ptr(c), n, ptr(mask), n, m, n, k, stream_of(a)), "cn_gemm_nn")
+    fn, name = (lib.cn_gemm_nn_x3, "cn_gemm_nn_x3") if precision == "bf16x3" else (lib.cn_gemm_nn, "cn_gemm_nn")
+    check(fn(ptr(a), k, ptr(b), n, ptr(c), n, ptr(mask), n, m, n, k, stream_of(a)), name)
     return c
 
 
-def gemm_tn(a: Tensor, b: Tensor, c: Optional[Tensor] = None) -> Tensor:
-    """C += A^T B on the fp32 MFMA tile kernel (C zero-initialised when not given)."""
+def gemm_tn(a: Tensor, b: Tensor, c: Optional[Tensor] = None, precision: str = "f32") -> Tensor:
+    """C += A^T B on the fp32 (or 3xbf16) MFMA tile kernel (C zero-initialised when not given)."""
     lib = _lib_ready()
     a, b = _cuda(a, "A"), _cuda(b, "B")
     (m, n), (m2, k) = a.shape, b.shape
     assert m == m2
     if c is None:
         c = torch.zeros(n, k, device=a.device, dtype=torch.float32)
-    check(lib.cn_gemm_tn(ptr(a), n, ptr(b), k, ptr(c), k, m, n, k, stream_of(a)), "cn_gemm_tn")
+    fn, name = (lib.cn_gemm_tn_x3, "cn_gemm_tn_x3") if precision == "bf16x3" else (lib.cn_gemm_tn, "cn_gemm_tn")
+    check(fn(ptr(a), n, ptr(b), k, ptr(c), k, m, n, k, stream_of(a)), name)
     return c
 
 

@@ -170,6 +170,199 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(const float* __restrict__ 
     }
 }
 
+// ---------------------------------------------------------------- 3xbf16 GEMMs
+// The same two products on v_mfma_f32_32x32x16_bf16 with each fp32 operand split
+// x = hi + lo (hi = bf16(x), lo = bf16(x - hi)) and Ah.Bh + Ah.Bl + Al.Bh accumulated in
+// fp32 (the dropped Al.Bl and the lo rounding leave ~2^-17 relative error per product,
+// the field kernel's scheme).  On 32x32x16 lane l = 32h + i holds A[row i][k = 8h + j]
+// and B[k = 8h + j][col i], j = 0..7: exactly the 8 consecutive k values the fp32
+// kernels' lanes already load, so one bf16 MFMA triple replaces 8 fp32 MFMAs.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void split_pair(float x, float y, unsigned& hi, unsigned& lo) {
+  const f32x2 v = {x, y};
+  const unsigned hu = __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2));
+  const f32x2 back = {__uint_as_float(hu << 16), __uint_as_float(hu & 0xffff0000u)};
+  hi = hu;
+  lo = __builtin_bit_cast(unsigned, __builtin_convertvector(v - back, bf16x2));
+}
+
+__device__ __forceinline__ void split8(const float* v, u32x4& hi, u32x4& lo) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    unsigned h, l;
+    split_pair(v[2 * q], v[2 * q + 1], h, l);
+    hi[q] = h;
+    lo[q] = l;
+  }
+}
+
+__device__ __forceinline__ floatx16 mfma3(floatx16 acc, u32x4 ah, u32x4 al, u32x4 bh, u32x4 bl) {
+  const bf16x8 a_h = __builtin_bit_cast(bf16x8, ah), a_l = __builtin_bit_cast(bf16x8, al);
+  const bf16x8 b_h = __builtin_bit_cast(bf16x8, bh), b_l = __builtin_bit_cast(bf16x8, bl);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_h, b_h, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_h, b_l, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_l, b_h, acc, 0, 0, 0);
+  return acc;
+}
+
+// XCD-aware block order: workgroups are dispatched to the 8 XCDs round-robin, so
+// block b runs on XCD b % 8.  Renumber so each XCD takes a contiguous range of the
+// logical tile order: the tiles that share input rows (the column blocks of one row
+// tile, the output tiles of one M split) then run back to back on ONE XCD and the
+// shared rows come from its L2 instead of HBM once per tile.
+__device__ __forceinline__ unsigned xcd_order(unsigned b, unsigned total) {
+  if (total % 8 != 0) return b;
+  return (b % 8) * (total / 8) + b / 8;
+}
+
+// gemm_nn_x3: block = 256 rows x NT columns, 4 waves x 64 rows.  B^T is split once per
+// block into fragment-major LDS (k-tile, column block u, hi|lo, lane) so a wave's read of
+// one fragment is 1 KiB contiguous (conflict free).  1D grid, XCD-ordered row tiles.
+template <int NT>
+__global__ __launch_bounds__(256) void gemm_nn_x3_kernel(const float* __restrict__ A, int64_t lda,
+                                                         const float* __restrict__ B, int64_t ldb,
+                                                         float* __restrict__ C, int64_t ldc,
+                                                         const float* __restrict__ mask, int64_t ldm,
+                                                         int64_t M, int N, int K, int n_col_blocks) {
+  constexpr int NU = NT / 32;
+  __shared__ u32x4 Bf[(kMaxK / kKT) * NU * 2 * 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int i = lane & 31, h = lane >> 5;
+  const unsigned v = xcd_order(blockIdx.x, gridDim.x);
+  const int64_t row_tile = v / n_col_blocks;
+  const int n0 = (v % n_col_blocks) * NT;
+  const int nkt = (K + kKT - 1) / kKT;
+  for (int e = tid; e < nkt * NU * 64; e += 256) {
+    const int kt = e / (NU * 64), u = (e / 64) % NU, l = e % 64;
+    const int n = n0 + 32 * u + (l & 31), kb = kt * kKT + 8 * (l >> 5);
+    float bv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bv[j] = (kb + j < K && n < N) ? B[(int64_t)(kb + j) * ldb + n] : 0.0f;
+    u32x4 hi, lo;
+    split8(bv, hi, lo);
+    Bf[((kt * NU + u) * 2) * 64 + l] = hi;
+    Bf[((kt * NU + u) * 2 + 1) * 64 + l] = lo;
+  }
+  __syncthreads();
+  const int64_t m0 = row_tile * kMT + wave * 64;
+  int64_t rows[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    rows[t] = m0 + 32 * t + i;
+    if (rows[t] >= M) rows[t] = M - 1;
+  }
+  floatx16 acc[2][NU] = {};
+  auto load_a = [&](int k0, float (&a)[2][8]) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const float* ar = A + rows[t] * lda + k0 + h * 8;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) a[t][q] = (k0 + h * 8 + q < K) ? ar[q] : 0.0f;
+    }
+  };
+  float an[2][8];
+  load_a(0, an);
+  for (int kt = 0; kt < nkt; ++kt) {
+    u32x4 ah[2], al[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) split8(an[t], ah[t], al[t]);
+    if (kt + 1 < nkt) load_a((kt + 1) * kKT, an);
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const u32x4 bh = Bf[((kt * NU + u) * 2) * 64 + lane];
+      const u32x4 bl = Bf[((kt * NU + u) * 2 + 1) * 64 + lane];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) acc[t][u] = mfma3(acc[t][u], ah[t], al[t], bh, bl);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int col = n0 + 32 * u + i;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t m = m0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (m < M && col < N) {
+          float x = acc[t][u][r];
+          if (mask && !(mask[m * ldm + col] > 0.0f)) x = 0.0f;
+          C[m * ldc + col] = x;
+        }
+      }
+    }
+}
+
+// gemm_tn_x3: C[n][k] += sum_m A[m][n] B[m][k].  Wave = 64 x 64 output (2 x 2
+// accumulators), block = 128 x 128; lane (i, h) reads A[m + 8h + j][n + i] and
+// B[m + 8h + j][k + i] for j = 0..7 (each half-wave row read is 128 contiguous bytes).
+// 1D grid over (M split, output tile), XCD-ordered so the tiles of one split share L2.
+constexpr int kTnRowsX3 = 16, kTnGroupsX3 = 2;
+
+__global__ __launch_bounds__(256) void gemm_tn_x3_kernel(const float* __restrict__ A, int64_t lda,
+                                                         const float* __restrict__ B, int64_t ldb,
+                                                         float* __restrict__ C, int64_t ldc, int64_t M, int N,
+                                                         int K, int64_t rows_per_block, int tiles_n, int tiles) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i = lane & 31, h = lane >> 5;
+  const unsigned v = xcd_order(blockIdx.x, gridDim.x);
+  const int tile = v % tiles;
+  const int64_t split = v / tiles;
+  const int n0 = (tile % tiles_n) * kTnTile + (wave >> 1) * 64;
+  const int k0 = (tile / tiles_n) * kTnTile + (wave & 1) * 64;
+  if (n0 >= N || k0 >= K) return;  // wave-uniform
+  const int64_t mb = split * rows_per_block;
+  const int64_t me = min(M, mb + rows_per_block);
+  const int na0 = min(n0 + i, N - 1), na1 = min(n0 + 32 + i, N - 1);
+  const int kb0 = min(k0 + i, K - 1), kb1 = min(k0 + 32 + i, K - 1);
+  floatx16 acc00 = {0}, acc01 = {0}, acc10 = {0}, acc11 = {0};
+  // kTnGroupsX3 16-row groups per iteration: all their loads are issued before any MFMA
+  for (int64_t m = mb; m < me; m += kTnRowsX3 * kTnGroupsX3) {
+    float a0[kTnGroupsX3][8], a1[kTnGroupsX3][8], b0[kTnGroupsX3][8], b1[kTnGroupsX3][8];
+#pragma unroll
+    for (int g = 0; g < kTnGroupsX3; ++g)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int64_t r = m + kTnRowsX3 * g + 8 * h + j;
+        const bool ok = r < me;
+        const float* ar = A + (ok ? r : mb) * lda;
+        const float* br = B + (ok ? r : mb) * ldb;
+        a0[g][j] = ok ? ar[na0] : 0.0f;  // a zero A row adds nothing, whatever B holds
+        a1[g][j] = ok ? ar[na1] : 0.0f;
+        b0[g][j] = br[kb0];
+        b1[g][j] = br[kb1];
+      }
+#pragma unroll
+    for (int g = 0; g < kTnGroupsX3; ++g) {
+      u32x4 a0h, a0l, a1h, a1l, b0h, b0l, b1h, b1l;
+      split8(a0[g], a0h, a0l);
+      split8(a1[g], a1h, a1l);
+      split8(b0[g], b0h, b0l);
+      split8(b1[g], b1h, b1l);
+      acc00 = mfma3(acc00, a0h, a0l, b0h, b0l);
+      acc01 = mfma3(acc01, a0h, a0l, b1h, b1l);
+      acc10 = mfma3(acc10, a1h, a1l, b0h, b0l);
+      acc11 = mfma3(acc11, a1h, a1l, b1h, b1l);
+    }
+  }
+  const floatx16* accs[4] = {&acc00, &acc01, &acc10, &acc11};
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const floatx16& acc = *accs[2 * t + u];
+      const int col = k0 + 32 * u + i;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = n0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row < N && col < K) atomicAdd(&C[(int64_t)row * ldc + col], acc[r]);
+      }
+    }
+}
+
 // out[code(m)][j] += A[m][j] for j < N; code(m) = code_index ? code_index[m / S]
 // : (n_codes == 1 ? 0 : m / S).  Block = 4 waves over kSegRows consecutive rows
 // and 64 columns: lane j of a wave owns column c0 + j (each row read is one
@@ -425,8 +618,15 @@ using namespace cn;
 namespace {
 
 int gemm_nn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, const float* mask,
-            int64_t ldm, int64_t M, int N, int K, hipStream_t st) {
+            int64_t ldm, int64_t M, int N, int K, hipStream_t st, bool x3 = false) {
   if (K > grad::kMaxK) return CN_EINVAL;
+  if (x3) {
+    const int64_t ncb = ceil_div(N, 64), tiles = ceil_div(M, grad::kMT) * ncb;
+    if (tiles > 0x7fffffff) return CN_EINVAL;
+    hipLaunchKernelGGL(grad::gemm_nn_x3_kernel<64>, dim3(static_cast<unsigned>(tiles)), dim3(256), 0, st, A, lda, B,
+                       ldb, C, ldc, mask, ldm, M, N, K, static_cast<int>(ncb));
+    return launch_status();
+  }
   // 64 columns per block (2 blocks per CU); 128 (one 146 KiB block per CU, 1 wave per SIMD)
   // measured 12 % slower over the training step's layers
   dim3 grid(static_cast<unsigned>(ceil_div(M, grad::kMT)), static_cast<unsigned>(ceil_div(N, 64)));
@@ -435,10 +635,20 @@ int gemm_nn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, 
 }
 
 int gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M, int N, int K,
-            hipStream_t st) {
+            hipStream_t st, bool x3 = false) {
   // about 1024 blocks (4 per CU) over the M split, at least 256 rows each, a multiple of the
   // row group so only the last block has a ragged tail
   const int64_t tiles = ceil_div(N, grad::kTnTile) * ceil_div(K, grad::kTnTile);
+  if (x3) {
+    constexpr int64_t grp = grad::kTnRowsX3 * grad::kTnGroupsX3;
+    const int64_t splits = std::max<int64_t>(1, 1024 / tiles);
+    int64_t rows = std::max<int64_t>(256, ceil_div(M, splits));
+    rows = ceil_div(rows, grp) * grp;
+    const int64_t nb = ceil_div(M, rows) * tiles;
+    hipLaunchKernelGGL(grad::gemm_tn_x3_kernel, dim3(static_cast<unsigned>(nb)), dim3(256), 0, st, A, lda, B, ldb, C,
+                       ldc, M, N, K, rows, static_cast<int>(ceil_div(N, grad::kTnTile)), static_cast<int>(tiles));
+    return launch_status();
+  }
   const int64_t splits = std::max<int64_t>(1, 1024 / tiles);
   int64_t rows = std::max<int64_t>(256, ceil_div(M, splits));
   rows = ceil_div(rows, 2 * grad::kTnPairs) * 2 * grad::kTnPairs;
@@ -478,6 +688,20 @@ extern "C" int cn_gemm_tn(const float* A, int64_t lda, const float* B, int64_t l
   return gemm_tn(A, lda, B, ldb, C, ldc, M, (int)N, (int)K, as_stream(stream));
 }
 
+extern "C" int cn_gemm_nn_x3(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
+                             const float* mask, int64_t ldm, int64_t M, int64_t N, int64_t K, cn_stream_t stream) {
+  CN_CHECK_ARG(A && B && C && M > 0 && N > 0 && K > 0 && N <= 65536 && K <= 288);
+  CN_CHECK_ARG(lda >= K && ldb >= N && ldc >= N && (!mask || ldm >= N));
+  return gemm_nn(A, lda, B, ldb, C, ldc, mask, ldm, M, (int)N, (int)K, as_stream(stream), true);
+}
+
+extern "C" int cn_gemm_tn_x3(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
+                             int64_t M, int64_t N, int64_t K, cn_stream_t stream) {
+  CN_CHECK_ARG(A && B && C && M > 0 && N > 0 && K > 0 && N <= 65536 && K <= 65536);
+  CN_CHECK_ARG(lda >= N && ldb >= K && ldc >= K);
+  return gemm_tn(A, lda, B, ldb, C, ldc, M, (int)N, (int)K, as_stream(stream), true);
+}
+
 extern "C" int cn_encode_inputs(const float* pts, const float* ro, const float* rd, const float* z, int64_t n_rays,
                                 int64_t n_samples, int64_t chunk_rows, const float* freqs_xyz, const float* freqs_dir,
                                 float* x, cn_stream_t stream) {
@@ -506,7 +730,20 @@ extern "C" int cn_field_backward(const float* const* params, const float* saved,
                                  const int64_t* code_index, int64_t n_codes, const float* freqs_xyz,
                                  const float* freqs_dir, float* workspace, float* const* grads, float* g_code,
                                  float* d_pts, float* d_ro, float* d_rd, cn_stream_t stream) {
+  return cn_field_backward_fmt(CN_FMT_F32, params, saved, x_enc, d_raw, pts, ro, rd, z, n_rays, n_samples,
+                               chunk_rows, code_index, n_codes, freqs_xyz, freqs_dir, workspace, grads, g_code,
+                               d_pts, d_ro, d_rd, stream);
+}
+
+extern "C" int cn_field_backward_fmt(int fmt, const float* const* params, const float* saved, const float* x_enc,
+                                     const float* d_raw, const float* pts, const float* ro, const float* rd,
+                                     const float* z, int64_t n_rays, int64_t n_samples, int64_t chunk_rows,
+                                     const int64_t* code_index, int64_t n_codes, const float* freqs_xyz,
+                                     const float* freqs_dir, float* workspace, float* const* grads, float* g_code,
+                                     float* d_pts, float* d_ro, float* d_rd, cn_stream_t stream) {
   using namespace mlp;
+  CN_CHECK_ARG(fmt == CN_FMT_F32 || fmt == CN_FMT_BF16X3);
+  const bool x3 = fmt == CN_FMT_BF16X3;
   CN_CHECK_ARG(params && saved && x_enc && d_raw && workspace);
   CN_CHECK_ARG(n_rays > 0 && n_samples > 0 && chunk_rows > 0 && n_codes > 0);
   if (d_pts || d_ro || d_rd) CN_CHECK_ARG(rd && freqs_xyz && freqs_dir && (pts || (ro && z)));
@@ -528,32 +765,32 @@ extern "C" int cn_field_backward(const float* const* params, const float* saved,
   auto G = [&](int i) { return grads ? grads[i] : nullptr; };
 
   // fc_rgb: rgb = W_rgb [v2 | zt1] + b
-  CN_TRY(gemm_nn(d_raw, 4, params[kWRgb], 512, dpa, 257, v2, 256, M, 256, 3, st));  // d pre(layer_dir2)
+  CN_TRY(gemm_nn(d_raw, 4, params[kWRgb], 512, dpa, 257, v2, 256, M, 256, 3, st, x3));  // d pre(layer_dir2)
   if (wg) {
-    CN_TRY(gemm_tn(d_raw, 4, v2, 256, G(kWRgb), 512, M, 3, 256, st));
+    CN_TRY(gemm_tn(d_raw, 4, v2, 256, G(kWRgb), 512, M, 3, 256, st, x3));
     CN_TRY(seg_sum(d_raw, 4, M, 3, M, nullptr, 1, G(kBRgb), 1, st));
   }
   if (g_code) CN_TRY(seg_sum(d_raw, 4, M, 3, n_samples, code_index, n_codes, g_code + kCbRgb, kCbStride, st));
   // layer_dir2: v2 = relu(W v1 + b)
-  CN_TRY(gemm_nn(dpa, 257, params[kWDir2], 256, dpb, 257, v1, 256, M, 256, 256, st));  // d pre(layer_dir1)
+  CN_TRY(gemm_nn(dpa, 257, params[kWDir2], 256, dpb, 257, v1, 256, M, 256, 256, st, x3));  // d pre(layer_dir1)
   if (wg) {
-    CN_TRY(gemm_tn(dpa, 257, v1, 256, G(kWDir2), 256, M, 256, 256, st));
+    CN_TRY(gemm_tn(dpa, 257, v1, 256, G(kWDir2), 256, M, 256, 256, st, x3));
     CN_TRY(seg_sum(dpa, 257, M, 256, M, nullptr, 1, G(kBDir2), 1, st));
   }
   // layer_dir1: v1 = relu(W [feat | dir] + b) -> d feat into dpa[:, 1:], d dir into denc[:, 63:]
-  CN_TRY(gemm_nn(dpb, 257, params[kWDir1], 283, dpa + 1, 257, nullptr, 0, M, 256, 256, st));
-  CN_TRY(gemm_nn(dpb, 257, params[kWDir1] + 256, 283, denc + 63, 90, nullptr, 0, M, 27, 256, st));
+  CN_TRY(gemm_nn(dpb, 257, params[kWDir1], 283, dpa + 1, 257, nullptr, 0, M, 256, 256, st, x3));
+  CN_TRY(gemm_nn(dpb, 257, params[kWDir1] + 256, 283, denc + 63, 90, nullptr, 0, M, 27, 256, st, x3));
   if (wg) {
-    CN_TRY(gemm_tn(dpb, 257, feat, 256, G(kWDir1), 283, M, 256, 256, st));
-    CN_TRY(gemm_tn(dpb, 257, x_enc + 63, 90, G(kWDir1) + 256, 283, M, 256, 27, st));
+    CN_TRY(gemm_tn(dpb, 257, feat, 256, G(kWDir1), 283, M, 256, 256, st, x3));
+    CN_TRY(gemm_tn(dpb, 257, x_enc + 63, 90, G(kWDir1) + 256, 283, M, 256, 27, st, x3));
     CN_TRY(seg_sum(dpb, 257, M, 256, M, nullptr, 1, G(kBDir1), 1, st));
   }
   // fc_out: [sigma | feat] = W [h2 | zs2] + b (no activation)
   hipLaunchKernelGGL(grad::copy_cols_kernel, dim3(elementwise_grid(M, 256)), dim3(256), 0, st, d_raw + 3, 4, dpa, 257, M, 1);
   CN_TRY(launch_status());
-  CN_TRY(gemm_nn(dpa, 257, params[kWOut], 512, dpb, 257, h2, 256, M, 256, 257, st));  // d pre(layer_xyz2)
+  CN_TRY(gemm_nn(dpa, 257, params[kWOut], 512, dpb, 257, h2, 256, M, 256, 257, st, x3));  // d pre(layer_xyz2)
   if (wg) {
-    CN_TRY(gemm_tn(dpa, 257, h2, 256, G(kWOut), 512, M, 257, 256, st));
+    CN_TRY(gemm_tn(dpa, 257, h2, 256, G(kWOut), 512, M, 257, 256, st, x3));
     CN_TRY(seg_sum(dpa, 257, M, 257, M, nullptr, 1, G(kBOut), 1, st));
   }
   if (g_code) {
@@ -561,16 +798,16 @@ extern "C" int cn_field_backward(const float* const* params, const float* saved,
     CN_TRY(seg_sum(dpa + 1, 257, M, 256, n_samples, code_index, n_codes, g_code + kCbFeat, kCbStride, st));
   }
   // layer_xyz2: h2 = relu(W [h1 | zs1] + b)
-  CN_TRY(gemm_nn(dpb, 257, params[kWXyz2], 512, dpa, 257, h1, 256, M, 256, 256, st));  // d pre(layer_xyz1)
+  CN_TRY(gemm_nn(dpb, 257, params[kWXyz2], 512, dpa, 257, h1, 256, M, 256, 256, st, x3));  // d pre(layer_xyz1)
   if (wg) {
-    CN_TRY(gemm_tn(dpb, 257, h1, 256, G(kWXyz2), 512, M, 256, 256, st));
+    CN_TRY(gemm_tn(dpb, 257, h1, 256, G(kWXyz2), 512, M, 256, 256, st, x3));
     CN_TRY(seg_sum(dpb, 257, M, 256, M, nullptr, 1, G(kBXyz2), 1, st));
   }
   if (g_code) CN_TRY(seg_sum(dpb, 257, M, 256, n_samples, code_index, n_codes, g_code + kCbXyz2, kCbStride, st));
   // layer_xyz1: h1 = relu(W xyz63 + b)
-  CN_TRY(gemm_nn(dpa, 257, params[kWXyz1], 63, denc, 90, nullptr, 0, M, 63, 256, st));
+  CN_TRY(gemm_nn(dpa, 257, params[kWXyz1], 63, denc, 90, nullptr, 0, M, 63, 256, st, x3));
   if (wg) {
-    CN_TRY(gemm_tn(dpa, 257, x_enc, 90, G(kWXyz1), 63, M, 256, 63, st));
+    CN_TRY(gemm_tn(dpa, 257, x_enc, 90, G(kWXyz1), 63, M, 256, 63, st, x3));
     CN_TRY(seg_sum(dpa, 257, M, 256, M, nullptr, 1, G(kBXyz1), 1, st));
   }
   // encodings -> points / view directions

@@ -208,6 +208,17 @@ int cn_field_backward(const float* const* params, const float* saved, const floa
                       const float* freqs_dir, float* workspace, float* const* grads, float* g_code,
                       float* d_pts, float* d_ro, float* d_rd, cn_stream_t stream);
 
+/* cn_field_backward with the GEMMs' arithmetic chosen by fmt: CN_FMT_F32 (exact-product
+ * fp32 MFMA, what cn_field_backward runs) or CN_FMT_BF16X3 (every dX / dW GEMM as
+ * Ah.Bh + Ah.Bl + Al.Bh on bf16 MFMA with fp32 accumulation, ~2^-17 relative error per
+ * product; the training step).  Same arguments, outputs and workspace otherwise. */
+int cn_field_backward_fmt(int fmt, const float* const* params, const float* saved, const float* x_enc,
+                          const float* d_raw, const float* pts, const float* ro, const float* rd,
+                          const float* z, int64_t n_rays, int64_t n_samples, int64_t chunk_rows,
+                          const int64_t* code_index, int64_t n_codes, const float* freqs_xyz,
+                          const float* freqs_dir, float* workspace, float* const* grads, float* g_code,
+                          float* d_pts, float* d_ro, float* d_rd, cn_stream_t stream);
+
 /* --- Fused 3xbf16 backward (eval-step gradients, frozen weights) ---------
  * The gradients eval.py's loss.backward() takes into the codes and the pose
  * (eval.py:141-160; the reference's weight gradients are never read there).
@@ -291,6 +302,12 @@ int cn_gemm_nn(const float* A, int64_t lda, const float* B, int64_t ldb, float* 
                const float* mask, int64_t ldm, int64_t M, int64_t N, int64_t K, cn_stream_t stream);
 int cn_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M,
                int64_t N, int64_t K, cn_stream_t stream);
+/* The same two products as 3xbf16 (split operands on v_mfma_f32_32x32x16_bf16, fp32
+ * accumulation; the GEMMs of cn_field_backward_fmt(CN_FMT_BF16X3)). */
+int cn_gemm_nn_x3(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
+                  const float* mask, int64_t ldm, int64_t M, int64_t N, int64_t K, cn_stream_t stream);
+int cn_gemm_tn_x3(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M,
+                  int64_t N, int64_t K, cn_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -67,25 +67,33 @@ def embedders(dev):
 # ---------------------------------------------------------------- GEMM building blocks
 
 
-@pytest.mark.parametrize("m,n,k", [(1000, 257, 283), (64, 3, 256), (4097, 256, 27), (20001, 256, 256), (300, 63, 3)])
-def test_gemm_nn_masked(dev, m, n, k):
+# 3xbf16 (split operands, Ah.Bh + Ah.Bl + Al.Bh): ~2^-17 relative error per product, so the
+# tolerance relative to the result's largest magnitude is 3e-5 instead of fp32's 1e-5.
+GEMM_TOL = {"f32": 1e-5, "bf16x3": 3e-5}
+
+
+@pytest.mark.parametrize("precision", ["f32", "bf16x3"])
+@pytest.mark.parametrize("m,n,k", [(1000, 257, 283), (64, 3, 256), (4097, 256, 27), (20001, 256, 256), (300, 63, 3),
+                                   (65536, 256, 256)])
+def test_gemm_nn_masked(dev, m, n, k, precision):
     from codenerf import ops
     g = torch.Generator().manual_seed(m + n + k)
     a, b = torch.randn(m, k, generator=g), torch.randn(k, n, generator=g)
     mask = torch.randn(m, n, generator=g)
-    c = ops.gemm_nn(a.to(dev), b.to(dev), mask.to(dev))
+    c = ops.gemm_nn(a.to(dev), b.to(dev), mask.to(dev), precision=precision)
     ref = (a.double() @ b.double()) * (mask > 0)
-    close(c, ref, 1e-5, "gemm_nn")
+    close(c, ref, GEMM_TOL[precision], "gemm_nn " + precision)
 
 
-@pytest.mark.parametrize("m,n,k", [(5000, 257, 256), (33, 3, 256), (4096, 256, 63)])
-def test_gemm_tn_accumulates(dev, m, n, k):
+@pytest.mark.parametrize("precision", ["f32", "bf16x3"])
+@pytest.mark.parametrize("m,n,k", [(5000, 257, 256), (33, 3, 256), (4096, 256, 63), (65536, 256, 256), (70001, 3, 283)])
+def test_gemm_tn_accumulates(dev, m, n, k, precision):
     from codenerf import ops
     g = torch.Generator().manual_seed(m * 3 + n + k)
     a, b = torch.randn(m, n, generator=g), torch.randn(m, k, generator=g)
     c0 = torch.randn(n, k, generator=g)
-    c = ops.gemm_tn(a.to(dev), b.to(dev), c0.to(dev).clone())
-    close(c, c0.double() + a.double().t() @ b.double(), 1e-5, "gemm_tn")
+    c = ops.gemm_tn(a.to(dev), b.to(dev), c0.to(dev).clone(), precision=precision)
+    close(c, c0.double() + a.double().t() @ b.double(), GEMM_TOL[precision], "gemm_tn " + precision)
 
 
 # ---------------------------------------------------------------- element-wise stages
@@ -204,10 +212,14 @@ def decode_relu_masks(words: torch.Tensor, m_rows: int):
     ("rayz", 20, 9, 20, True),
     ("rayz", 300, 64, 128, False),
 ])
-def test_field_backward(dev, mode, r, s, chunk, per_ray_codes):
+@pytest.mark.parametrize("precision", ["f32", "bf16x3"])
+def test_field_backward(dev, mode, r, s, chunk, per_ray_codes, precision):
+    """Training-mode backward (weights need grad): fp32 forward keeping activations, layer-wise
+    GEMM backward in the model's precision (exact fp32 products or 3xbf16)."""
     from codenerf import nerf, synthetic
     o = O()
     m = model(dev, 0)
+    m.precision = precision
     p = oracle_params(m)
     g = torch.Generator().manual_seed(r * s)
     ro = torch.randn(r, 3, generator=g) * 0.3 + torch.tensor([0.0, 0.0, 1.3])
