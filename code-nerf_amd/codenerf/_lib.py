@@ -20,6 +20,7 @@ CN_OK, CN_EINVAL, CN_EUNSUPPORTED = 0, -1, -2
 CN_NUM_PARAMS = 18
 CN_FMT_F32, CN_FMT_BF16X3, CN_FMT_BF16X3_T = 0, 1, 2
 FORMATS = {"f32": CN_FMT_F32, "bf16x3": CN_FMT_BF16X3, "bf16x3_t": CN_FMT_BF16X3_T}
+CN_FIELD_BWD_LDP = 260  # row stride of cn_field_backward's (M, 257) gradient buffers (include/codenerf.h)
 CN_CODE_BIAS_STRIDE = 520
 
 _p = ctypes.c_void_p

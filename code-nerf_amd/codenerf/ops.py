@@ -404,7 +404,7 @@ def field_backward(params: Sequence[Tensor], saved: Tensor, x_enc: Tensor, d_raw
     del keep, gkeep
     out.update(g_code=g_code, d_pts=d_pts, d_ro=d_ro, d_rd=d_rd)
     if want_x:
-        off = 2 * 257 * m
+        off = 2 * _lib.CN_FIELD_BWD_LDP * m
         out["d_x"] = ws[off: off + 90 * m].view(m, 90)
     return out
 

@@ -219,81 +219,142 @@ __device__ __forceinline__ unsigned xcd_order(unsigned b, unsigned total) {
   return (b % 8) * (total / 8) + b / 8;
 }
 
-// gemm_nn_x3: block = 256 rows x NT columns, 4 waves x 64 rows.  B^T is split once per
-// block into fragment-major LDS (k-tile, column block u, hi|lo, lane) so a wave's read of
-// one fragment is 1 KiB contiguous (conflict free).  1D grid, XCD-ordered row tiles.
-template <int NT>
-__global__ __launch_bounds__(256) void gemm_nn_x3_kernel(const float* __restrict__ A, int64_t lda,
+// gemm_nn_x3: block = 8 waves x 32 rows = 256 rows, each wave all 32 NU columns of its
+// column group (NU <= 8 accumulators, so A is read from HBM exactly once for N <= 256).
+// k runs in 32-deep pairs of MFMA k-tiles.  Any permutation of k inside a pair is valid if
+// A and B use the same one, so lane half h takes k = 16h .. 16h + 15 of the pair (k-tile s
+// of the pair: 16h + 8s + j): each lane reads one full 64-byte run of its row per pair
+// (a whole 128-byte line per row across the two halves) instead of scattered 32-byte
+// pieces.  B^T streams through LDS one pair (two 16-deep slabs) at a time, double-buffered
+// and fragment-major (slab, column block u, hi|lo, lane: one fragment read is 1 KiB
+// contiguous).  During pair p each thread loads its B entries and the wave its A run of
+// pair p + 1, runs p's MFMAs, then splits and stores pair p + 1.  One barrier per pair.
+// VEC: lda % 4 == 0 and A 16-byte aligned (four dwordx4 per row per pair).
+constexpr int kNnWaves = 4, kNnRows = 32 * kNnWaves, kNnThreads = 64 * kNnWaves;
+
+template <int NU, bool VEC>
+__global__ __launch_bounds__(kNnThreads, 2) void gemm_nn_x3_kernel(const float* __restrict__ A, int64_t lda,
                                                          const float* __restrict__ B, int64_t ldb,
                                                          float* __restrict__ C, int64_t ldc,
                                                          const float* __restrict__ mask, int64_t ldm,
-                                                         int64_t M, int N, int K, int n_col_blocks) {
-  constexpr int NU = NT / 32;
-  __shared__ u32x4 Bf[(kMaxK / kKT) * NU * 2 * 64];
+                                                         int64_t M, int N, int K) {
+  __shared__ u32x4 Bs[2][2][NU * 2 * 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int i = lane & 31, h = lane >> 5;
-  const unsigned v = xcd_order(blockIdx.x, gridDim.x);
-  const int64_t row_tile = v / n_col_blocks;
-  const int n0 = (v % n_col_blocks) * NT;
-  const int nkt = (K + kKT - 1) / kKT;
-  for (int e = tid; e < nkt * NU * 64; e += 256) {
-    const int kt = e / (NU * 64), u = (e / 64) % NU, l = e % 64;
-    const int n = n0 + 32 * u + (l & 31), kb = kt * kKT + 8 * (l >> 5);
-    float bv[8];
+  const int n0 = blockIdx.y * 256;
+  const int nkp = (K + 31) / 32;
+  const int64_t m0 = (int64_t)blockIdx.x * kNnRows + wave * 32;
+  const int64_t row = min(m0 + i, M - 1);
+  const float* arow = A + row * lda + h * 16;
+  // this thread's B entries of a slab: column blocks u = tid / 64 + kNnWaves e (< NU), lane tid % 64
+  constexpr int kSE = (NU + kNnWaves - 1) / kNnWaves;
+  const int sl = tid & 63;
+  const int sk = 16 * (sl >> 5);
+  auto load_b = [&](int p, float (&bv)[kSE][2][8]) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) bv[j] = (kb + j < K && n < N) ? B[(int64_t)(kb + j) * ldb + n] : 0.0f;
-    u32x4 hi, lo;
-    split8(bv, hi, lo);
-    Bf[((kt * NU + u) * 2) * 64 + l] = hi;
-    Bf[((kt * NU + u) * 2 + 1) * 64 + l] = lo;
-  }
-  __syncthreads();
-  const int64_t m0 = row_tile * kMT + wave * 64;
-  int64_t rows[2];
+    for (int e = 0; e < kSE; ++e) {
+      const int su = (tid >> 6) + kNnWaves * e;
+      const int sn = n0 + 32 * su + (sl & 31);
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    rows[t] = m0 + 32 * t + i;
-    if (rows[t] >= M) rows[t] = M - 1;
-  }
-  floatx16 acc[2][NU] = {};
-  auto load_a = [&](int k0, float (&a)[2][8]) {
+      for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const float* ar = A + rows[t] * lda + k0 + h * 8;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) a[t][q] = (k0 + h * 8 + q < K) ? ar[q] : 0.0f;
+        for (int j = 0; j < 8; ++j) {
+          const int k = 32 * p + sk + 8 * t + j;
+          bv[e][t][j] = (su < NU && k < K && sn < N) ? B[(int64_t)k * ldb + sn] : 0.0f;
+        }
     }
   };
-  float an[2][8];
-  load_a(0, an);
-  for (int kt = 0; kt < nkt; ++kt) {
-    u32x4 ah[2], al[2];
+  auto store_b = [&](int buf, const float (&bv)[kSE][2][8]) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t) split8(an[t], ah[t], al[t]);
-    if (kt + 1 < nkt) load_a((kt + 1) * kKT, an);
+    for (int e = 0; e < kSE; ++e) {
+      const int su = (tid >> 6) + kNnWaves * e;
+      if (su < NU) {
 #pragma unroll
-    for (int u = 0; u < NU; ++u) {
-      const u32x4 bh = Bf[((kt * NU + u) * 2) * 64 + lane];
-      const u32x4 bl = Bf[((kt * NU + u) * 2 + 1) * 64 + lane];
-#pragma unroll
-      for (int t = 0; t < 2; ++t) acc[t][u] = mfma3(acc[t][u], ah[t], al[t], bh, bl);
-    }
-  }
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int u = 0; u < NU; ++u) {
-      const int col = n0 + 32 * u + i;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t m = m0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (m < M && col < N) {
-          float x = acc[t][u][r];
-          if (mask && !(mask[m * ldm + col] > 0.0f)) x = 0.0f;
-          C[m * ldc + col] = x;
+        for (int t = 0; t < 2; ++t) {
+          u32x4 hi, lo;
+          split8(bv[e][t], hi, lo);
+          Bs[buf][t][(su * 2) * 64 + sl] = hi;
+          Bs[buf][t][(su * 2 + 1) * 64 + sl] = lo;
         }
       }
     }
+  };
+  auto load_a = [&](int p, float (&a)[16]) {
+    const int kb = 32 * p + h * 16;
+    if (VEC && kb + 16 <= K) {
+      const float4* ap = reinterpret_cast<const float4*>(arow + 32 * p);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 x = ap[q];
+        a[4 * q] = x.x; a[4 * q + 1] = x.y; a[4 * q + 2] = x.z; a[4 * q + 3] = x.w;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) a[q] = (kb + q < K) ? arow[32 * p + q] : 0.0f;
+    }
+  };
+  floatx16 acc[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) acc[u] = floatx16{0};
+  float an[16], bn[kSE][2][8];
+  load_b(0, bn);
+  load_a(0, an);
+  store_b(0, bn);
+  __syncthreads();
+  for (int p = 0; p < nkp; ++p) {
+    const int buf = p & 1;
+    u32x4 ah[2], al[2];
+    split8(an, ah[0], al[0]);
+    split8(an + 8, ah[1], al[1]);
+    const bool more = p + 1 < nkp;
+    if (more) {
+      load_b(p + 1, bn);
+      load_a(p + 1, an);
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const u32x4 bh = Bs[buf][t][(u * 2) * 64 + lane];
+        const u32x4 bl = Bs[buf][t][(u * 2 + 1) * 64 + lane];
+        acc[u] = mfma3(acc[u], ah[t], al[t], bh, bl);
+      }
+    if (more) store_b(buf ^ 1, bn);
+    __syncthreads();
+  }
+  // Epilogue.  Full tiles (the common case) take the mask in batches of 16 loads with no
+  // per-element branch, so a batch is one memory round trip; ragged tiles are guarded.
+  if (m0 + 32 <= M && n0 + 32 * NU <= N) {
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int col = n0 + 32 * u + i;
+      float mk[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t m = m0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        mk[r] = mask ? mask[m * ldm + col] : 1.0f;
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t m = m0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        C[m * ldc + col] = mk[r] > 0.0f ? acc[u][r] : 0.0f;
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int col = n0 + 32 * u + i;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int64_t m = m0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (m < M && col < N) {
+        float x = acc[u][r];
+        if (mask && !(mask[m * ldm + col] > 0.0f)) x = 0.0f;
+        C[m * ldc + col] = x;
+      }
+    }
+  }
 }
 
 // gemm_tn_x3: C[n][k] += sum_m A[m][n] B[m][k].  Wave = 64 x 64 output (2 x 2
@@ -615,16 +676,33 @@ __global__ __launch_bounds__(256) void code_backward_kernel(mlp::Params P, const
 // ================================================================ C ABI
 using namespace cn;
 
+// Row stride (floats) of the (M, 257) pre-activation gradient buffers of the field backward:
+// padded to a multiple of 4 so every row starts 16-byte aligned (dwordx4 A loads).
+constexpr int64_t kLdP = 260;
+
 namespace {
 
 int gemm_nn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, const float* mask,
             int64_t ldm, int64_t M, int N, int K, hipStream_t st, bool x3 = false) {
   if (K > grad::kMaxK) return CN_EINVAL;
   if (x3) {
-    const int64_t ncb = ceil_div(N, 64), tiles = ceil_div(M, grad::kMT) * ncb;
-    if (tiles > 0x7fffffff) return CN_EINVAL;
-    hipLaunchKernelGGL(grad::gemm_nn_x3_kernel<64>, dim3(static_cast<unsigned>(tiles)), dim3(256), 0, st, A, lda, B,
-                       ldb, C, ldc, mask, ldm, M, N, K, static_cast<int>(ncb));
+    const int nu = static_cast<int>(std::min<int64_t>(8, ceil_div(N, 32)));
+    const bool vec = lda % 4 == 0 && (reinterpret_cast<uintptr_t>(A) & 15) == 0;
+    dim3 grid(static_cast<unsigned>(ceil_div(M, grad::kNnRows)), static_cast<unsigned>(ceil_div(N, 256)));
+#define CN_NN_X3(NU_)                                                                                          \
+  case NU_:                                                                                                     \
+    if (vec)                                                                                                    \
+      hipLaunchKernelGGL((grad::gemm_nn_x3_kernel<NU_, true>), grid, dim3(grad::kNnThreads), 0, st, A, lda, B, ldb, C, ldc,  \
+                         mask, ldm, M, N, K);                                                                   \
+    else                                                                                                        \
+      hipLaunchKernelGGL((grad::gemm_nn_x3_kernel<NU_, false>), grid, dim3(grad::kNnThreads), 0, st, A, lda, B, ldb, C, ldc, \
+                         mask, ldm, M, N, K);                                                                   \
+    break;
+    switch (nu) {
+      CN_NN_X3(1) CN_NN_X3(2) CN_NN_X3(3) CN_NN_X3(4) CN_NN_X3(5) CN_NN_X3(6) CN_NN_X3(7) CN_NN_X3(8)
+      default: return CN_EINVAL;
+    }
+#undef CN_NN_X3
     return launch_status();
   }
   // 64 columns per block (2 blocks per CU); 128 (one 146 KiB block per CU, 1 wave per SIMD)
@@ -757,58 +835,58 @@ extern "C" int cn_field_backward_fmt(int fmt, const float* const* params, const 
   const float* feat = saved + 2 * M * 256;
   const float* v1 = saved + 3 * M * 256;
   const float* v2 = saved + 4 * M * 256;
-  float* dpa = workspace;              // (M, 257)
-  float* dpb = workspace + M * 257;    // (M, 257)
-  float* denc = workspace + 2 * M * 257;  // (M, 90)
-  float* dxp = workspace + 2 * M * 257 + M * 90;  // (M, 6): d pts | d viewdir
+  float* dpa = workspace;              // (M, 257) in rows of kLdP
+  float* dpb = workspace + M * kLdP;    // (M, 257) in rows of kLdP
+  float* denc = workspace + 2 * M * kLdP;  // (M, 90)
+  float* dxp = workspace + 2 * M * kLdP + M * 90;  // (M, 6): d pts | d viewdir
   const bool wg = grads && grads[0];
   auto G = [&](int i) { return grads ? grads[i] : nullptr; };
 
   // fc_rgb: rgb = W_rgb [v2 | zt1] + b
-  CN_TRY(gemm_nn(d_raw, 4, params[kWRgb], 512, dpa, 257, v2, 256, M, 256, 3, st, x3));  // d pre(layer_dir2)
+  CN_TRY(gemm_nn(d_raw, 4, params[kWRgb], 512, dpa, kLdP, v2, 256, M, 256, 3, st, x3));  // d pre(layer_dir2)
   if (wg) {
     CN_TRY(gemm_tn(d_raw, 4, v2, 256, G(kWRgb), 512, M, 3, 256, st, x3));
     CN_TRY(seg_sum(d_raw, 4, M, 3, M, nullptr, 1, G(kBRgb), 1, st));
   }
   if (g_code) CN_TRY(seg_sum(d_raw, 4, M, 3, n_samples, code_index, n_codes, g_code + kCbRgb, kCbStride, st));
   // layer_dir2: v2 = relu(W v1 + b)
-  CN_TRY(gemm_nn(dpa, 257, params[kWDir2], 256, dpb, 257, v1, 256, M, 256, 256, st, x3));  // d pre(layer_dir1)
+  CN_TRY(gemm_nn(dpa, kLdP, params[kWDir2], 256, dpb, kLdP, v1, 256, M, 256, 256, st, x3));  // d pre(layer_dir1)
   if (wg) {
-    CN_TRY(gemm_tn(dpa, 257, v1, 256, G(kWDir2), 256, M, 256, 256, st, x3));
-    CN_TRY(seg_sum(dpa, 257, M, 256, M, nullptr, 1, G(kBDir2), 1, st));
+    CN_TRY(gemm_tn(dpa, kLdP, v1, 256, G(kWDir2), 256, M, 256, 256, st, x3));
+    CN_TRY(seg_sum(dpa, kLdP, M, 256, M, nullptr, 1, G(kBDir2), 1, st));
   }
   // layer_dir1: v1 = relu(W [feat | dir] + b) -> d feat into dpa[:, 1:], d dir into denc[:, 63:]
-  CN_TRY(gemm_nn(dpb, 257, params[kWDir1], 283, dpa + 1, 257, nullptr, 0, M, 256, 256, st, x3));
-  CN_TRY(gemm_nn(dpb, 257, params[kWDir1] + 256, 283, denc + 63, 90, nullptr, 0, M, 27, 256, st, x3));
+  CN_TRY(gemm_nn(dpb, kLdP, params[kWDir1], 283, dpa + 1, kLdP, nullptr, 0, M, 256, 256, st, x3));
+  CN_TRY(gemm_nn(dpb, kLdP, params[kWDir1] + 256, 283, denc + 63, 90, nullptr, 0, M, 27, 256, st, x3));
   if (wg) {
-    CN_TRY(gemm_tn(dpb, 257, feat, 256, G(kWDir1), 283, M, 256, 256, st, x3));
-    CN_TRY(gemm_tn(dpb, 257, x_enc + 63, 90, G(kWDir1) + 256, 283, M, 256, 27, st, x3));
-    CN_TRY(seg_sum(dpb, 257, M, 256, M, nullptr, 1, G(kBDir1), 1, st));
+    CN_TRY(gemm_tn(dpb, kLdP, feat, 256, G(kWDir1), 283, M, 256, 256, st, x3));
+    CN_TRY(gemm_tn(dpb, kLdP, x_enc + 63, 90, G(kWDir1) + 256, 283, M, 256, 27, st, x3));
+    CN_TRY(seg_sum(dpb, kLdP, M, 256, M, nullptr, 1, G(kBDir1), 1, st));
   }
   // fc_out: [sigma | feat] = W [h2 | zs2] + b (no activation)
-  hipLaunchKernelGGL(grad::copy_cols_kernel, dim3(elementwise_grid(M, 256)), dim3(256), 0, st, d_raw + 3, 4, dpa, 257, M, 1);
+  hipLaunchKernelGGL(grad::copy_cols_kernel, dim3(elementwise_grid(M, 256)), dim3(256), 0, st, d_raw + 3, 4, dpa, kLdP, M, 1);
   CN_TRY(launch_status());
-  CN_TRY(gemm_nn(dpa, 257, params[kWOut], 512, dpb, 257, h2, 256, M, 256, 257, st, x3));  // d pre(layer_xyz2)
+  CN_TRY(gemm_nn(dpa, kLdP, params[kWOut], 512, dpb, kLdP, h2, 256, M, 256, 257, st, x3));  // d pre(layer_xyz2)
   if (wg) {
-    CN_TRY(gemm_tn(dpa, 257, h2, 256, G(kWOut), 512, M, 257, 256, st, x3));
-    CN_TRY(seg_sum(dpa, 257, M, 257, M, nullptr, 1, G(kBOut), 1, st));
+    CN_TRY(gemm_tn(dpa, kLdP, h2, 256, G(kWOut), 512, M, 257, 256, st, x3));
+    CN_TRY(seg_sum(dpa, kLdP, M, 257, M, nullptr, 1, G(kBOut), 1, st));
   }
   if (g_code) {
-    CN_TRY(seg_sum(dpa, 257, M, 1, n_samples, code_index, n_codes, g_code + kCbSigma, kCbStride, st));
-    CN_TRY(seg_sum(dpa + 1, 257, M, 256, n_samples, code_index, n_codes, g_code + kCbFeat, kCbStride, st));
+    CN_TRY(seg_sum(dpa, kLdP, M, 1, n_samples, code_index, n_codes, g_code + kCbSigma, kCbStride, st));
+    CN_TRY(seg_sum(dpa + 1, kLdP, M, 256, n_samples, code_index, n_codes, g_code + kCbFeat, kCbStride, st));
   }
   // layer_xyz2: h2 = relu(W [h1 | zs1] + b)
-  CN_TRY(gemm_nn(dpb, 257, params[kWXyz2], 512, dpa, 257, h1, 256, M, 256, 256, st, x3));  // d pre(layer_xyz1)
+  CN_TRY(gemm_nn(dpb, kLdP, params[kWXyz2], 512, dpa, kLdP, h1, 256, M, 256, 256, st, x3));  // d pre(layer_xyz1)
   if (wg) {
-    CN_TRY(gemm_tn(dpb, 257, h1, 256, G(kWXyz2), 512, M, 256, 256, st, x3));
-    CN_TRY(seg_sum(dpb, 257, M, 256, M, nullptr, 1, G(kBXyz2), 1, st));
+    CN_TRY(gemm_tn(dpb, kLdP, h1, 256, G(kWXyz2), 512, M, 256, 256, st, x3));
+    CN_TRY(seg_sum(dpb, kLdP, M, 256, M, nullptr, 1, G(kBXyz2), 1, st));
   }
-  if (g_code) CN_TRY(seg_sum(dpb, 257, M, 256, n_samples, code_index, n_codes, g_code + kCbXyz2, kCbStride, st));
+  if (g_code) CN_TRY(seg_sum(dpb, kLdP, M, 256, n_samples, code_index, n_codes, g_code + kCbXyz2, kCbStride, st));
   // layer_xyz1: h1 = relu(W xyz63 + b)
-  CN_TRY(gemm_nn(dpa, 257, params[kWXyz1], 63, denc, 90, nullptr, 0, M, 63, 256, st, x3));
+  CN_TRY(gemm_nn(dpa, kLdP, params[kWXyz1], 63, denc, 90, nullptr, 0, M, 63, 256, st, x3));
   if (wg) {
-    CN_TRY(gemm_tn(dpa, 257, x_enc, 90, G(kWXyz1), 63, M, 256, 63, st, x3));
-    CN_TRY(seg_sum(dpa, 257, M, 256, M, nullptr, 1, G(kBXyz1), 1, st));
+    CN_TRY(gemm_tn(dpa, kLdP, x_enc, 90, G(kWXyz1), 63, M, 256, 63, st, x3));
+    CN_TRY(seg_sum(dpa, kLdP, M, 256, M, nullptr, 1, G(kBXyz1), 1, st));
   }
   // encodings -> points / view directions
   if (d_pts || d_ro || d_rd) {
@@ -838,7 +916,7 @@ extern "C" int cn_field_backward_fmt(int fmt, const float* const* params, const 
   return CN_OK;
 }
 
-extern "C" int64_t cn_field_backward_workspace_floats(int64_t m) { return m * (2 * 257 + 90 + 6); }
+extern "C" int64_t cn_field_backward_workspace_floats(int64_t m) { return m * (2 * kLdP + 90 + 6); }
 
 extern "C" int cn_code_bias_backward(const float* const* params, const float* z_s, const float* z_t, int64_t n_codes,
                                      const float* g_code, float* dz_s, float* dz_t, float* const* grads,

@@ -200,7 +200,7 @@ int64_t cn_field_backward_workspace_floats(int64_t m);
  * ACCUMULATED into (view-direction and, for ro + z inputs, point gradients).
  * With d_pts, d_ro and d_rd all NULL, pts / ro / rd / z / freqs may be NULL too
  * (rows from cn_mlp_forward_train: n_rays = M, n_samples = 1).  On return
- * workspace[2*257*M, 2*257*M + 90*M) holds dL/dx_enc (M, 90). */
+ * workspace[2*260*M, 2*260*M + 90*M) holds dL/dx_enc (M, 90). */
 int cn_field_backward(const float* const* params, const float* saved, const float* x_enc,
                       const float* d_raw, const float* pts, const float* ro, const float* rd,
                       const float* z, int64_t n_rays, int64_t n_samples, int64_t chunk_rows,
