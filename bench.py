@@ -1,33 +1,34 @@
 """Benchmark: rendered rays/s on SRN-cars 128x128 at 64 samples/ray (BASELINE.json metric, config C2).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline] [--hierarchical]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--images-per-step B] [--no-cpu-baseline]
 
-One step renders N full 128x128 images (16384 rays each, 64 coarse samples per
-ray, srn-cars-code near 0.8 / far 1.8, lindepth, 4096-ray chunks) through the
-gfx950 path: ray bundle -> per-object code terms -> depths -> fused
-encode+MLP field kernel -> compositing.  The field kernel runs the
-3xbf16 split (Wh.Xh + Wh.Xl + Wl.Xh on bf16 MFMA, fp32 accumulation; fp32-level
-accuracy, parity-tested at the same 1e-4 as the fp32 kernel) by default;
-``--precision f32`` selects the exact-product fp32 MFMA kernel, which is also
-timed beside it and reported under ``f32_kernel``.  With N ranks every image
-is split over the ranks exactly like the reference's parallel_image_render
-(nerf/__init__.py:179-218) and the rendered pixels are all-gathered to rank 0
-over RCCL; per-rank work is fixed (16384 rays), so scaling is weak.
+One step renders B novel 128x128 views of one held-out car per rank (default B = 16; 16384 rays
+each, 64 coarse samples per ray, srn-cars-code near 0.8 / far 1.8, lindepth, 4096-ray chunks)
+through the gfx950 path: ray bundle -> per-object code terms -> depths -> fused encode+MLP field
+kernel -> compositing, in the reference's precision (fp32: exact-product fp32 MFMA).  That is the
+headline ``value`` / ``dtype`` / ``roofline``.  Beside it, on the same batch: the opt-in 3xbf16
+field kernel (``bf16x3``, its own roofline against the bf16 MFMA peak), the C3 64+64 hierarchical
+render, the C4 chairs render sharded over the ranks, one C5 eval step and one C3 training
+iteration, and the CPU baseline.
 
-Inputs are synthetic (no dataset/checkpoint offline): hash-initialised
-CodeNeRFModel weights of the reference architecture, one latent code pair,
-spherical poses.  Everything is resident in HBM before timing.
+Ranks: under torch.distributed.run (WORLD_SIZE set) each process is one rank.  Otherwise
+``--gpus N`` > 1 spawns N worker processes itself (as the reference's mp.spawn, train.py:159-179)
+before this process touches the GPU, and refuses to run when fewer than N GPUs are visible.
+With N ranks every view is split over the ranks exactly like parallel_image_render
+(nerf/__init__.py:179-218) and the rendered pixels are all-gathered to rank 0 over RCCL; per-rank
+work is fixed (B views' worth of rays), so C2 scaling is weak.
 
-JSON line fields beyond the driver contract: ``roofline`` (the field kernel,
-timed by HIP events on its stream inside the timed steps), ``cpu_baseline``
-(the CPU oracle -- the reference's op sequence in torch fp32 -- on this host,
-rank 0, one full image), ``psnr_vs_ref`` (our image vs that CPU render).
+Inputs are synthetic (no dataset/checkpoint offline): hash-initialised CodeNeRFModel weights of the
+reference architecture, one latent code pair, spherical poses.  Everything is resident in HBM
+before timing.
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
+import socket
 import sys
 import time
 
@@ -54,7 +55,6 @@ KERNELS = {"f32": ("field_kernel<kFromRayZ> (fused posenc + CodeNeRF MLP, fp32 M
 
 def pose(theta, phi, rho):
     """eval.py:22-38 pose_spherical (host, float32)."""
-    import math
     st, ct, sp, cp = math.sin(theta), math.cos(theta), math.sin(phi), math.cos(phi)
     m = torch.eye(4)
     m[0, 0], m[1, 0] = -sp, cp
@@ -64,29 +64,68 @@ def pose(theta, phi, rho):
     return m
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--images-per-step", type=int, default=16,
+                    help="views of the car rendered per rank per step (16 x 16384 rays: ~90 ms of fp32 work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--hierarchical", action="store_true", help="also time the 64+64 (C3) render")
-    ap.add_argument("--precision", default="bf16x3", choices=sorted(KERNELS))
-    ap.add_argument("--no-f32-compare", action="store_true", help="skip the fp32-kernel side measurement")
+    ap.add_argument("--no-extras", action="store_true", help="headline + bf16x3 only (profiling runs)")
+    ap.add_argument("--precision", default="f32", choices=sorted(KERNELS),
+                    help="headline field-kernel arithmetic (f32 = the reference's precision)")
     ap.add_argument("--eval-iters", type=int, default=10,
                     help="C5: time this many test-time-optimisation iterations (0 = skip)")
     ap.add_argument("--train-iters", type=int, default=3,
                     help="C3 training: time this many train.py iterations (4 x 4096 rays each; 0 = skip)")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
 
+
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _spawned(local_rank: int, argv, n: int, port: int):
+    os.environ.update(RANK=str(local_rank), LOCAL_RANK=str(local_rank), WORLD_SIZE=str(n),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    run(parse_args(argv))
+
+
+def main():
+    args = parse_args()
+    if "WORLD_SIZE" in os.environ:
+        world = int(os.environ["WORLD_SIZE"])
+        if args.gpus not in (1, world):
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+        run(args)
+        return
+    if args.gpus <= 1:
+        run(args)
+        return
+    # spawn one process per GPU before this process touches the GPU (device_count does not
+    # initialise HIP on this image); never re-exec a process that has
+    visible = torch.cuda.device_count()
+    if visible < args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs, found {visible}")
+    import torch.multiprocessing as mp
+    mp.start_processes(_spawned, args=(sys.argv[1:], args.gpus, free_port()), nprocs=args.gpus, join=True,
+                       start_method="spawn")
+
+
+def run(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     n = max(world, 1)
+    rccl_world = 1
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+        rccl_world = dist.get_world_size()
     dev = torch.device("cuda", local)
 
     import codenerf
@@ -95,7 +134,9 @@ def main():
     from codenerf.nerf import PointSampler, PositionalEmbedder, RaySampler, gather_rows, render_rays
     from codenerf.utils import split_sizes
     codenerf.load_library()
+    info = codenerf.build_info()
 
+    B = args.images_per_step
     k = synthetic.srn_intrinsics(H, FOCAL)
     rs = RaySampler(H, W, k, sample_size=4096, device=dev, datatype=torch.float32)
     ps = PointSampler(NC, NF, NEAR, FAR, "lindepth", False, torch.float32, dev)
@@ -104,50 +145,57 @@ def main():
     for seed in (0, 1):
         m = CodeNeRFModel(256, 1, 256, 256, 10, 4)
         m.load_state_dict(synthetic.codenerf_params(seed))
-        m.precision = args.precision
         models.append(m.to(dev).eval())
     zs = synthetic.latent_codes(5, 1).to(dev)
     zt = synthetic.latent_codes(6, 1).to(dev)
-    poses = torch.stack([pose(0.5 + 0.3 * i, 0.3, 1.3) for i in range(n)]).to(dev)
+    # B*n views on a turntable around the car; rank r renders its Q5 slice of every view
+    views = B * n
+    poses = torch.stack([pose(0.5 + 0.7 * math.sin(0.37 * i), 2 * math.pi * i / views, 1.3)
+                         for i in range(views)]).to(dev)
     n_img_rays = H * W
     per, _ = split_sizes(n_img_rays, n)
     start = sum(per[:rank])
     chunk = min(CHUNK, per[rank])
-    rays_per_rank = per[rank] * n
-    for mm in models:
-        mm.packed()                              # weights packed once (frozen, as in eval)
+    rays_per_rank = per[rank] * views
 
-    timing = {"field_ms": 0.0, "field_launches": 0}
+    def set_precision(prec):
+        for mm in models:
+            mm.precision = prec
+            mm.packed()                          # weights packed once per format (frozen, as in eval)
 
-    def step(record: bool, coarse_only: bool = True):
+    timing = {}
+
+    def render_step(record: bool, coarse_only: bool, ps_=ps, poses_=poses, per_=per, start_=start, chunk_=chunk):
         with torch.no_grad():
-            ro, rd = rs.get_bundle(poses)                    # (n, H, W, 3)
-            ro = ro.reshape(n, -1, 3)[:, start:start + per[rank]].reshape(-1, 3)
-            rd = rd.reshape(n, -1, 3)[:, start:start + per[rank]].reshape(-1, 3)
+            nv = poses_.shape[0]
+            ro, rd = rs.get_bundle(poses_)                    # (views, H, W, 3)
+            ro = ro.reshape(nv, -1, 3)[:, start_:start_ + per_[rank]].reshape(-1, 3)
+            rd = rd.reshape(nv, -1, 3)[:, start_:start_ + per_[rank]].reshape(-1, 3)
             r = ro.shape[0]
             hook = {} if record else None
-            out = render_rays(ro, rd, zs.expand(r, -1), zt.expand(r, -1), ps, emb, models[0], models[1],
-                              chunk_rows=chunk, coarse_only=coarse_only, events=hook)
+            out = render_rays(ro, rd, zs.expand(r, -1), zt.expand(r, -1), ps_, emb, models[0], models[1],
+                              chunk_rows=chunk_, coarse_only=coarse_only, events=hook)
             rgb = out["rgb_coarse" if coarse_only else "rgb_fine"]
             if world > 1:
-                rgb = gather_rows(rgb, [per[rank] * n] * n, rank)
-                if rgb is not None and len(set(per)) == 1:        # (rank, image, row) -> (image, rank, row)
-                    rgb = rgb.view(n, n, per[0], 3).transpose(0, 1).reshape(n * n_img_rays, 3)
+                rgb = gather_rows(rgb, [p * nv for p in per_], rank)
+                if rgb is not None and len(set(per_)) == 1:     # (rank, view, row) -> (view, rank, row)
+                    rgb = rgb.view(n, nv, per_[0], 3).transpose(0, 1).reshape(nv * n_img_rays, 3)
             if record:
-                timing["pending"] = timing.get("pending", []) + hook["field"]
+                timing["pending"] += hook["field"]
             return rgb
 
-    def timed(k_steps, w_steps, coarse_only=True):
+    def timed(k_steps, w_steps, fn):
         for _ in range(w_steps):
-            step(False, coarse_only)
+            fn(False)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         timing["pending"] = []
         t0 = time.perf_counter()
+        img = None
         for _ in range(k_steps):
-            img = step(True, coarse_only)
+            img = fn(True)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -160,79 +208,114 @@ def main():
         ms = [a.elapsed_time(b) for a, b in timing["pending"]]
         return dt, ms, img
 
-    dt, field_ms, img = timed(args.steps, args.warmup, coarse_only=True)
-    total_rays = n_img_rays * n * args.steps
-    value = total_rays / dt
-    field_avg_ms = sum(field_ms) / max(1, len(field_ms))
     samples_per_launch = rays_per_rank * NC
     flop_per_launch = samples_per_launch * FLOP_PER_SAMPLE
-    algo_tf = flop_per_launch / (field_avg_ms * 1e-3) / 1e12       # fp32-equivalent algorithmic rate
-    kname, passes, peak = KERNELS[args.precision]
-    achieved_tf = passes * algo_tf                                  # MFMA flops the hardware executes
 
-    extra = {}
-    if args.precision != "f32" and not args.no_f32_compare:
-        for mm in models:
-            mm.precision = "f32"
-            mm.packed()
-        dtf, fms, _ = timed(max(1, args.steps // 2), 1, coarse_only=True)
-        f_ms = sum(fms) / max(1, len(fms))
-        extra["f32_kernel"] = {"value": n_img_rays * n * max(1, args.steps // 2) / dtf, "unit": "rays/s",
-                               "field_avg_ms": f_ms,
-                               "achieved_tflops": flop_per_launch / (f_ms * 1e-3) / 1e12,
-                               "peak": PEAK_FP32_MFMA_TFLOPS}
-        for mm in models:
-            mm.precision = args.precision
-    if args.hierarchical:
-        dth, _, _ = timed(max(1, args.steps // 2), 1, coarse_only=False)
-        extra["hierarchical_64_64_rays_per_s"] = n_img_rays * n * max(1, args.steps // 2) / dth
+    def roofline(prec, field_ms):
+        kname, passes, peak = KERNELS[prec]
+        avg = sum(field_ms) / max(1, len(field_ms))
+        algo_tf = flop_per_launch / (avg * 1e-3) / 1e12       # algorithmic (fp32-equivalent) rate
+        achieved = passes * algo_tf                           # MFMA flops the hardware executes
+        return {"kernel": kname, "bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                "frac": achieved / peak, "traffic": traffic_of(prec, samples_per_launch), "avg_launch_ms": avg,
+                "launches_timed": len(field_ms), "flop_per_launch": flop_per_launch,
+                "samples_per_launch": samples_per_launch, "flop_per_sample": FLOP_PER_SAMPLE,
+                "mfma_passes": passes, "fp32_equiv_tflops": algo_tf,
+                "timing": "HIP events on the launching (current) stream around every field launch of the timed steps"}
 
-    if args.eval_iters > 0:
-        extra["eval_c5"] = eval_bench(dev, rs, emb, models, args.eval_iters)
-    if args.train_iters > 0:
-        extra["train_c3"] = train_bench(dev, k, args.train_iters, world)
-
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", "field_kernel_traffic.json")
-    if os.path.exists(tpath):
-        with open(tpath) as f:
-            tj = json.load(f)
-            traffic = tj.get(args.precision, {}).get("hbm_bytes_per_launch")
-
+    # ---- headline: C2 in the reference's precision
+    set_precision(args.precision)
+    dt, field_ms, img = timed(args.steps, args.warmup, lambda rec: render_step(rec, True))
+    total_rays = n_img_rays * views * args.steps
+    value = total_rays / dt
     result = {
         "metric": "rendered rays/sec (128x128, 64 samples/ray)",
         "value": value,
         "unit": "rays/s",
         "n_gpus": n,
+        "rccl_world_size": rccl_world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3,
+        "timed_s": dt,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16x3" if args.precision == "bf16x3" else "f32",
+        "dtype": "f32" if args.precision == "f32" else args.precision,
         "data": "synthetic (hash-initialised CodeNeRFModel weights, one latent code pair, spherical poses)",
-        "config": {"workload": "C2: srn-cars-code 128x128 image per rank-step, 64 coarse samples/ray, "
+        "config": {"workload": "C2: srn-cars-code, one held-out car, 128x128 views, 64 coarse samples/ray, "
                                "chunk 4096, lindepth near 0.8 far 1.8, fused HIP render",
-                   "images_per_step": n, "rays_per_image": n_img_rays, "samples_per_ray": NC,
+                   "images_per_step": views, "images_per_rank_step": B, "rays_per_image": n_img_rays,
+                   "samples_per_ray": NC,
                    "parallelism": f"ray-sharded x{n} + RCCL all-gather" if n > 1 else "single GPU"},
-        "roofline": {"kernel": kname, "bound": "mfma", "achieved": achieved_tf, "peak": peak,
-                     "unit": "TFLOP/s", "frac": achieved_tf / peak, "traffic": traffic,
-                     "avg_launch_ms": field_avg_ms, "flop_per_launch": flop_per_launch,
-                     "mfma_passes": passes, "fp32_equiv_tflops": algo_tf},
+        "roofline": roofline(args.precision, field_ms),
+        "build": {"cn_version": info["version"], "tree_src": info["tree_src"]},
     }
-    result.update(extra)
+    psnr_img = {args.precision: img}
+
+    # ---- the other field-kernel format on the same batch
+    other = "bf16x3" if args.precision == "f32" else "f32"
+    set_precision(other)
+    dto, fms_o, img_o = timed(args.steps, args.warmup, lambda rec: render_step(rec, True))
+    psnr_img[other] = img_o
+    result[other] = {"value": total_rays / dto, "unit": "rays/s", "ms_per_step": dto / args.steps * 1e3,
+                     "dtype": other, "roofline": roofline(other, fms_o),
+                     "note": ("opt-in 3-product bf16 split (Wh.Xh + Wh.Xl + Wl.Xh, fp32 accumulate): narrower than "
+                              "the reference's fp32; parity-tested at the same tolerances incl. trained-magnitude "
+                              "weights (tests/test_gpu_configs.py)") if other == "bf16x3" else "reference precision"}
+    set_precision(args.precision)
+
+    if not args.no_extras:
+        # ---- C3: 64+64 hierarchical render, same views
+        k3 = max(1, args.steps // 4)
+        dth, f3, _ = timed(k3, 1, lambda rec: render_step(rec, False))
+        result["hierarchical_64_64"] = {"value": n_img_rays * views * k3 / dth, "unit": "rays/s",
+                                        "ms_per_step": dth / k3 * 1e3, "steps": k3, "dtype": args.precision,
+                                        "field_launch_ms_avg": sum(f3) / max(1, len(f3)),
+                                        "samples_per_ray": "64 coarse + 128 fine (64+64 merged)"}
+        # ---- C4: chairs (Nc 32 / Nf 128, near 1.25 far 2.75), B views each sharded over the ranks
+        ps4 = PointSampler(32, 128, 1.25, 2.75, "lindepth", False, torch.float32, dev)
+        poses4 = torch.stack([pose(0.5 + 0.7 * math.sin(0.37 * i), 2 * math.pi * i / B, 2.0)
+                              for i in range(B)]).to(dev)
+        dt4, f4, _ = timed(k3, 1, lambda rec: render_step(rec, False, ps4, poses4, per, start, chunk))
+        result["c4_chairs_sharded"] = {"value": n_img_rays * B * k3 / dt4, "unit": "rays/s", "scaling": "strong",
+                                       "ms_per_step": dt4 / k3 * 1e3, "steps": k3, "views_per_step": B,
+                                       "rays_per_rank_per_view": per[rank], "dtype": args.precision,
+                                       "samples_per_ray": "32 coarse + 160 fine",
+                                       "field_launch_ms_avg": sum(f4) / max(1, len(f4))}
+        if args.eval_iters > 0:
+            result["eval_c5"] = {p: eval_bench(dev, rs, emb, models, args.eval_iters, p) for p in ("f32", "bf16x3")}
+            set_precision(args.precision)
+        if args.train_iters > 0:
+            result["train_c3"] = train_bench(dev, k, args.train_iters, world)
 
     if rank == 0 and not args.no_cpu_baseline:
-        result["cpu_baseline"], result["psnr_vs_ref"] = cpu_baseline(img, k, poses, n)
+        cb, ref_img = cpu_baseline(k, poses[:1])
+        result["cpu_baseline"] = cb
+        from oracle.codenerf_oracle import mse2psnr
+        for prec, im in psnr_img.items():
+            if im is not None:
+                mse = float(((im[:n_img_rays].float().cpu() - ref_img) ** 2).mean())
+                result.setdefault("psnr_vs_ref", {})[prec] = mse2psnr(mse)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def eval_bench(dev, rs, emb, models, iters):
-    """C5 (srn-cars-code-3080-val.yml): one eval.py:141-165 iteration = 2048 random rays, 64+64
+def traffic_of(prec, samples):
+    """HBM bytes per launch from the PMC passes (profiles/field_kernel_traffic.json: FETCH_SIZE and
+    WRITE_SIZE in separate rocprofv3 passes, gfx950-corrected), scaled from per-sample bytes."""
+    tpath = os.path.join(ROOT, "profiles", "field_kernel_traffic.json")
+    if not os.path.exists(tpath):
+        return None
+    with open(tpath) as f:
+        per_sample = json.load(f).get(prec, {}).get("hbm_bytes_per_sample")
+    return None if per_sample is None else per_sample * samples
+
+
+def eval_bench(dev, rs, emb, models, iters, precision):
+    """C5 (srn-cars-code-3080-val.yml): one eval.py:141-167 iteration = 2048 random rays, 64+64
     perturbed samples, forward + backward through the HIP kernels into (codes, theta, phi, rho),
     AdamW step.  Weights frozen (their grads are never read by the reference's optimiser)."""
     import numpy as np
@@ -245,6 +328,7 @@ def eval_bench(dev, rs, emb, models, iters):
     saved = [(m, m.precision) for m in models]
     for m in models:
         m.requires_grad_(False)
+        m.precision = precision
     zs = (torch.randn(1, 256, generator=torch.Generator().manual_seed(4)) * 0.3).to(dev).requires_grad_(True)
     zt = (torch.randn(1, 256, generator=torch.Generator().manual_seed(5)) * 0.3).to(dev).requires_grad_(True)
     th = torch.tensor([1.57], device=dev).requires_grad_(True)
@@ -270,9 +354,11 @@ def eval_bench(dev, rs, emb, models, iters):
     for m, prec in saved:
         m.requires_grad_(True)
         m.precision = prec
+    note = ("3xbf16 forward with ReLU masks + one fused backward launch per field" if precision == "bf16x3" else
+            "fp32 forward keeping activations + layer-wise fp32 MFMA backward")
     return {"ms_per_iter": dt * 1e3, "rays_per_s": 2048 / dt, "rays_per_iter": 2048, "samples": "64+64 perturbed",
-            "note": "forward with ReLU masks + one fused backward launch per field (3xbf16, frozen weights); "
-                    "host-side numpy ray permutation and eval.py's per-iteration psnr read-back included"}
+            "dtype": precision,
+            "note": note + "; host-side numpy ray permutation and eval.py's per-iteration psnr read-back included"}
 
 
 def train_bench(dev, k, iters, world):
@@ -343,38 +429,72 @@ def train_bench(dev, k, iters, world):
     rays = batch * 4096 * iters * world
     return {"ms_per_iter": dt / iters * 1e3, "rays_per_s": rays / dt, "rays_per_iter_per_rank": batch * 4096,
             "optimizer_steps_per_iter": batch, "samples": "64+64 perturbed", "objects": n_objects,
-            "params": n_params, "loss": float(logs[-1]["total_loss"]),
+            "params": n_params, "loss": float(logs[-1]["total_loss"]), "dtype": "f32",
             "adamw": {"kernel_ms": adamw_ms, "bytes": 28 * n_params,
                       "gbps": 28 * n_params / (adamw_ms * 1e-3) / 1e9},
-            "note": "fp32 training field kernel (activations kept), layer-wise 3xbf16 MFMA backward GEMMs, "
+            "note": "fp32 training field kernel (activations kept), layer-wise fp32 MFMA backward GEMMs, "
                     "flat AdamW; train.py's per-chunk psnr read-back included"}
 
 
-def cpu_baseline(img, k, poses, n):
-    """The CPU oracle (reference op sequence, torch fp32) on this host: one full C2 image."""
+def cpu_threads() -> int:
+    """Host threads for the CPU baseline: the process's CPU share (cgroup / affinity), not the
+    machine's count -- on the GPU box os.cpu_count() reports the whole host while the job gets
+    OMP_NUM_THREADS (16) cores."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def cpu_baseline(k, pose1):
+    """The CPU oracle (the reference's op sequence, torch fp32) on this host, median of 3:
+    C2 = 3 full 128x128 images (64 coarse samples), C3 = 3 samples of one 4096-ray chunk at 64+64."""
     from oracle import codenerf_oracle as O
     from codenerf import synthetic
-    threads = min(16, os.cpu_count() or 1)
+    threads = cpu_threads()
     torch.set_num_threads(threads)
     d = O.ray_directions(H, W, k)
-    ro, rd = O.ray_bundle(d, poses[:1].cpu())
+    ro, rd = O.ray_bundle(d, pose1.cpu())
     ro, rd = ro.reshape(-1, 3), rd.reshape(-1, 3)
     nr = ro.shape[0]
     zs, zt = synthetic.latent_codes(5, 1).expand(nr, -1), synthetic.latent_codes(6, 1).expand(nr, -1)
     pc, pf = synthetic.codenerf_params(0), synthetic.codenerf_params(1)
-    t0 = time.perf_counter()
+    c2, ref = [], None
     with torch.no_grad():
-        out = O.render_image(ro, rd, zs, zt, O.Sampling(NC, NF, NEAR, FAR), O.EmbedCfg(), pc, pf, CHUNK,
-                             coarse_only=True)
-    dt = time.perf_counter() - t0
-    ref = out["rgb_coarse"]
-    mine = img[:nr].float().cpu() if img is not None else None
-    psnr = None
-    if mine is not None and mine.shape == ref.shape:
-        mse = float(((mine - ref) ** 2).mean())
-        psnr = O.mse2psnr(mse)
-    return ({"value": nr / dt, "unit": "rays/s", "cores": threads, "kind": "port",
-             "sample": f"one full 128x128 image (16384 rays x 64 coarse samples, chunk 4096), {dt:.1f} s"}, psnr)
+        for _ in range(3):
+            t0 = time.perf_counter()
+            out = O.render_image(ro, rd, zs, zt, O.Sampling(NC, NF, NEAR, FAR), O.EmbedCfg(), pc, pf, CHUNK,
+                                 coarse_only=True)
+            c2.append(time.perf_counter() - t0)
+            ref = out["rgb_coarse"]
+        c3 = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            O.render_image(ro[:CHUNK], rd[:CHUNK], zs[:CHUNK], zt[:CHUNK], O.Sampling(NC, NF, NEAR, FAR), O.EmbedCfg(),
+                           pc, pf, CHUNK)
+            c3.append(time.perf_counter() - t0)
+    m2, m3 = sorted(c2)[1], sorted(c3)[1]
+    return ({"value": nr / m2, "unit": "rays/s", "cores": threads, "kind": "port",
+             "sample": f"C2: median of 3 full 128x128 images (16384 rays x 64 coarse samples, chunk 4096): "
+                       f"{', '.join(f'{t:.2f}' for t in c2)} s",
+             "hierarchical_64_64": {"value": CHUNK / m3, "unit": "rays/s",
+                                    "sample": f"C3: median of 3 renders of one 4096-ray chunk at 64+64: "
+                                              f"{', '.join(f'{t:.2f}' for t in c3)} s"},
+             "host": host_cpu()}, ref)
+
+
+def host_cpu() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 if __name__ == "__main__":

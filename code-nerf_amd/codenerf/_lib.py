@@ -20,7 +20,6 @@ CN_OK, CN_EINVAL, CN_EUNSUPPORTED = 0, -1, -2
 CN_NUM_PARAMS = 18
 CN_FMT_F32, CN_FMT_BF16X3, CN_FMT_BF16X3_T = 0, 1, 2
 FORMATS = {"f32": CN_FMT_F32, "bf16x3": CN_FMT_BF16X3, "bf16x3_t": CN_FMT_BF16X3_T}
-CN_FIELD_BWD_LDP = 260  # row stride of cn_field_backward's (M, 257) gradient buffers (include/codenerf.h)
 CN_CODE_BIAS_STRIDE = 520
 
 _p = ctypes.c_void_p
@@ -50,6 +49,7 @@ SIGNATURES = {
     "cn_mlp_forward_train": (_i, [_p, _p, _p, _i64, _p, _i64, _p, _p, _p]),
     "cn_encode_inputs": (_i, [_p, _p, _p, _p, _i64, _i64, _i64, _fp, _fp, _p, _p]),
     "cn_field_backward_workspace_floats": (_i64, [_i64]),
+    "cn_field_backward_dx_offset": (_i64, [_i64]),
     "cn_field_backward": (_i, [ctypes.POINTER(_p), _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p, _i64, _fp, _fp,
                                _p, ctypes.POINTER(_p), _p, _p, _p, _p, _p]),
     "cn_field_backward_fmt": (_i, [_i, ctypes.POINTER(_p), _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p, _i64,
@@ -94,8 +94,22 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    _check_provenance(lib)
     _lib = lib
     return lib
+
+
+def _check_provenance(lib) -> None:
+    """Refuse a library built from other sources than the tree next to it (codenerf/provenance.py):
+    a stale prebuilt .so would otherwise run silently in place of the checked-out kernels."""
+    from . import provenance
+    if os.environ.get("CODENERF_ALLOW_STALE") == "1" or not os.path.isdir(os.path.join(provenance._PKG, "csrc")):
+        return
+    built = provenance.version_of(lib.cn_version().decode()).get("src")
+    here = provenance.source_hash()
+    if built != here:
+        raise CodeNerfError(f"{LIB_PATH} was built from sources {built}, the tree holds {here}: rebuild it "
+                            "(`make -C code-nerf_amd/csrc`) or set CODENERF_ALLOW_STALE=1")
 
 
 def check(rc: int, what: str) -> None:

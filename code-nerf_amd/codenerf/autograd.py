@@ -131,9 +131,10 @@ def _c(t):
 class _FieldMeta:
     """Non-tensor arguments of the field Functions."""
 
-    def __init__(self, n_samples, chunk_rows, fx, fd, code_index=None, precision="f32"):
+    def __init__(self, n_samples, chunk_rows, fx, fd, code_index=None, precision="f32", train_precision="f32"):
         self.n_samples, self.chunk_rows = n_samples, chunk_rows
         self.precision = precision
+        self.train_precision = train_precision
         self.fx, self.fd = list(fx) if fx is not None else None, list(fd) if fd is not None else None
         self.code_index = code_index
 
@@ -201,7 +202,8 @@ class RadianceField(torch.autograd.Function):
         r = ops.field_backward(params, ctx.acts, ctx.x_enc, g_raw.contiguous(), rd.shape[0], meta.n_samples,
                                meta.chunk_rows, z_s.shape[0], meta.fx, meta.fd, rd=rd, pts=pts, ro=ro, z=z,
                                code_index=meta.code_index, param_grads=pg, want_code=want_z or pg is not None,
-                               want_pts=needs[2], want_ro=needs[3], want_rd=needs[1], precision=meta.precision)
+                               want_pts=needs[2], want_ro=needs[3], want_rd=needs[1],
+                               precision=meta.train_precision)
         dz_s = dz_t = None
         if r["g_code"] is not None:
             dz_s, dz_t = ops.code_bias_backward(params, z_s, z_t, r["g_code"], pg, want_z=want_z)
@@ -214,7 +216,8 @@ class MLPForward(torch.autograd.Function):
     """CodeNeRFModel.forward(z_s, z_t, x) on encoded rows (model.py:160-194)."""
 
     @staticmethod
-    def forward(ctx, x, z_s, z_t, *params):
+    def forward(ctx, train_precision, x, z_s, z_t, *params):
+        ctx.train_precision = train_precision
         params = [p.detach() for p in params]
         cb = ops.code_bias(params, z_s, z_t)
         packed = ops.mlp_pack(params, "f32")
@@ -226,18 +229,18 @@ class MLPForward(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_raw):
         x, z_s, z_t, *params = ctx.saved_tensors
-        needs = ctx.needs_input_grad
+        needs = ctx.needs_input_grad[1:]
         pg = _param_grad_buffers(params, needs[3:])
         want_z = needs[1] or needs[2]
         m = x.shape[0]
         r = ops.field_backward(params, ctx.acts, x, g_raw.contiguous(), m, 1, m, z_s.shape[0], param_grads=pg,
-                               want_code=want_z or pg is not None, want_x=needs[0])
+                               want_code=want_z or pg is not None, want_x=needs[0], precision=ctx.train_precision)
         dz_s = dz_t = None
         if r["g_code"] is not None:
             dz_s, dz_t = ops.code_bias_backward(params, z_s, z_t, r["g_code"], pg, want_z=want_z)
         ctx.acts = None
         grads = pg if pg is not None else [None] * len(params)
-        return (r.get("d_x"), dz_s, dz_t, *grads)
+        return (None, r.get("d_x"), dz_s, dz_t, *grads)
 
 
 # ------------------------------------------------------------------ entry points used by the package
@@ -283,12 +286,13 @@ def _code_rows(z_s, z_t):
 
 def mlp_forward_autograd(model, z_s, z_t, x):
     cs, ct = _code_rows(z_s, z_t)
-    return MLPForward.apply(x, cs, ct, *model.param_list())
+    return MLPForward.apply(getattr(model, "train_precision", "f32"), x, cs, ct, *model.param_list())
 
 
 def radiance_field_autograd(model, rd, z_s, z_t, chunk_rows, fx, fd, pts=None, ro=None, z=None, code_index=None):
     cs, ct = (z_s, z_t) if code_index is not None else _code_rows(z_s, z_t)
     n_samples = pts.shape[1] if pts is not None else z.shape[1]
     meta = _FieldMeta(n_samples, chunk_rows, fx, fd, code_index=code_index,
-                      precision=getattr(model, "precision", "f32"))
+                      precision=getattr(model, "precision", "f32"),
+                      train_precision=getattr(model, "train_precision", "f32"))
     return RadianceField.apply(meta, rd, pts, ro, _d(z), cs, ct, *model.param_list())

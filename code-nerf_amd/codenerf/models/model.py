@@ -44,9 +44,13 @@ class CodeNeRFModel(torch.nn.Module):
         self.layer_dir1 = torch.nn.Linear(self.dim_dir + c, h)
         self.layer_dir2 = torch.nn.Linear(h, h)
         self.fc_rgb = torch.nn.Linear(h + texture_code_size, 3)
-        # field-kernel arithmetic: "bf16x3" (3-product bf16 split, fp32 accumulate) or
-        # "f32" (exact-product fp32 MFMA); both are held to the same parity tests
-        self.precision = os.environ.get("CODENERF_PRECISION", "bf16x3")
+        # field-kernel arithmetic: "f32" (exact-product fp32 MFMA, the reference's precision;
+        # default) or "bf16x3" (opt-in: 3-product bf16 split, fp32 accumulate, ~2^-17 relative
+        # per product; parity-tested at the same tolerances incl. trained-magnitude weights)
+        self.precision = os.environ.get("CODENERF_PRECISION", "f32")
+        # arithmetic of the training backward's weight-gradient / dX GEMMs, independent of the
+        # inference format: the reference trains fully in fp32
+        self.train_precision = os.environ.get("CODENERF_TRAIN_PRECISION", "f32")
         self._packed = None
         self._packed_key = None
 

@@ -404,7 +404,7 @@ def field_backward(params: Sequence[Tensor], saved: Tensor, x_enc: Tensor, d_raw
     del keep, gkeep
     out.update(g_code=g_code, d_pts=d_pts, d_ro=d_ro, d_rd=d_rd)
     if want_x:
-        off = 2 * _lib.CN_FIELD_BWD_LDP * m
+        off = int(lib.cn_field_backward_dx_offset(m))
         out["d_x"] = ws[off: off + 90 * m].view(m, 90)
     return out
 
@@ -431,13 +431,17 @@ def code_bias_backward(params: Sequence[Tensor], z_s: Tensor, z_t: Tensor, g_cod
 def gemm_nn(a: Tensor, b: Tensor, mask: Optional[Tensor] = None, precision: str = "f32") -> Tensor:
     """C = A B (masked where mask <= 0) on the fp32 (or 3xbf16) MFMA tile kernel."""
     lib = _lib_ready()
-    a, b = _cuda(a, "A"), _cuda(b, "B")
+    # A may be a row-strided view (lda > k, unit column stride), as the field backward's
+    # (M, 257)-in-rows-of-260 gradient buffers are
+    if not (a.is_cuda and a.dtype == torch.float32 and a.dim() == 2 and a.stride(1) == 1 and a.stride(0) >= a.shape[1]):
+        a = _cuda(a, "A")
+    b = _cuda(b, "B")
     (m, k), (k2, n) = a.shape, b.shape
     assert k == k2
     mask = _opt(mask, "mask")
     c = torch.empty(m, n, device=a.device, dtype=torch.float32)
     fn, name = (lib.cn_gemm_nn_x3, "cn_gemm_nn_x3") if precision == "bf16x3" else (lib.cn_gemm_nn, "cn_gemm_nn")
-    check(fn(ptr(a), k, ptr(b), n, ptr(c), n, ptr(mask), n, m, n, k, stream_of(a)), name)
+    check(fn(ptr(a), a.stride(0), ptr(b), n, ptr(c), n, ptr(mask), n, m, n, k, stream_of(a)), name)
     return c
 
 

@@ -206,16 +206,28 @@ class AdamW(torch.optim.Optimizer):
     # ---- data parallel ------------------------------------------------
     def allreduce_grads(self, group=None) -> None:
         """Average the gradients over the process group (the reference's DDP, util.py:139-142):
-        ONE all-reduce of the flat gradient buffer.  A missing gradient counts as zero."""
+        ONE all-reduce of the flat gradient buffer (plus one of a per-parameter has-grad flag).
+        A gradient missing on this rank counts as zero; a parameter without a gradient on every
+        rank keeps ``grad = None``."""
         if not (dist.is_available() and dist.is_initialized()):
             return
         world = dist.get_world_size(group)
         if world == 1:
             return
-        for p in self._sync_grads():
-            view = self._view("grad", p)
-            view.zero_()
-            p.grad = view
+        missing = set(self._sync_grads())
+        params = list(self._offs)
+        # which parameters hold a gradient on SOME rank (DDP reduces those; a parameter no rank
+        # touched keeps grad None, so step() skips it exactly as torch's AdamW would)
+        flags = torch.tensor([0 if p in missing else 1 for p in params], dtype=torch.int32,
+                             device=self._flat["grad"].device)
+        dist.all_reduce(flags, op=dist.ReduceOp.SUM, group=group)
+        anywhere = flags.cpu().tolist()
+        for p, cnt in zip(params, anywhere):
+            if p in missing:
+                view = self._view("grad", p)
+                view.zero_()
+                if cnt > 0:
+                    p.grad = view
         grad = self._flat["grad"]
         if dist.get_backend(group) == dist.Backend.NCCL:
             dist.all_reduce(grad, op=dist.ReduceOp.AVG, group=group)

@@ -62,24 +62,48 @@ def prepare_optimizer(cfg, models):
             optimizer.broadcast_params(0)
     else:
         optimizer = getattr(torch.optim, cfg.optimizer.type)(groups, lr=cfg.optimizer.lr)
+        if getattr(cfg, "is_distributed", False):
+            broadcast_parameters(models)
     gamma, step_size = cfg.optimizer.scheduler_gamma, cfg.optimizer.scheduler_step_size
     scheduler = torch.optim.lr_scheduler.LambdaLR(optimizer, lr_lambda=lambda epoch: gamma ** (epoch / step_size))
     return optimizer, scheduler
+
+
+def broadcast_parameters(models, src: int = 0) -> None:
+    """DDP's construction-time broadcast (utils/util.py:139-142) for any optimiser: every replica
+    starts from rank ``src``'s parameters (one coalesced broadcast)."""
+    params = [p for m in models.values() for p in m.parameters()]
+    flat = torch.cat([p.detach().reshape(-1) for p in params])
+    dist.broadcast(flat, src=src)
+    o = 0
+    with torch.no_grad():
+        for p in params:
+            p.copy_(flat[o:o + p.numel()].view_as(p))
+            o += p.numel()
 
 
 def _average_gradients(optimizer, models) -> None:
     if hasattr(optimizer, "allreduce_grads"):
         optimizer.allreduce_grads()
         return
-    # a torch optimiser: one coalesced all-reduce of every gradient
-    grads = [p.grad for m in models.values() for p in m.parameters() if p.grad is not None]
-    flat = torch.cat([g.reshape(-1) for g in grads])
+    # a torch optimiser: one coalesced all-reduce over EVERY parameter (missing gradients as
+    # zeros, so every rank reduces the same size) plus a has-grad flag per parameter
+    params = [p for m in models.values() for p in m.parameters()]
+    dev = params[0].device
+    flat = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in params])
+    flags = torch.tensor([int(p.grad is not None) for p in params], dtype=torch.int32, device=dev)
+    dist.all_reduce(flags)
     dist.all_reduce(flat)
     flat.div_(dist.get_world_size())
     o = 0
-    for g in grads:
-        g.copy_(flat[o:o + g.numel()].view_as(g))
-        o += g.numel()
+    for p, cnt in zip(params, flags.cpu().tolist()):
+        if cnt > 0:
+            g = flat[o:o + p.numel()].view_as(p)
+            if p.grad is None:
+                p.grad = g.clone()
+            else:
+                p.grad.copy_(g)
+        o += p.numel()
 
 
 def train_minibatch(models, optimizer, scheduler, point_sampler, embedders, ro, rd, object_ids, target_pixels,

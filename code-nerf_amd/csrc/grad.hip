@@ -219,7 +219,7 @@ __device__ __forceinline__ unsigned xcd_order(unsigned b, unsigned total) {
   return (b % 8) * (total / 8) + b / 8;
 }
 
-// gemm_nn_x3: block = 8 waves x 32 rows = 256 rows, each wave all 32 NU columns of its
+// gemm_nn_x3: block = kNnWaves (4) waves x 32 rows = 128 rows, each wave all 32 NU columns of its
 // column group (NU <= 8 accumulators, so A is read from HBM exactly once for N <= 256).
 // k runs in 32-deep pairs of MFMA k-tiles.  Any permutation of k inside a pair is valid if
 // A and B use the same one, so lane half h takes k = 16h .. 16h + 15 of the pair (k-tile s
@@ -917,6 +917,9 @@ extern "C" int cn_field_backward_fmt(int fmt, const float* const* params, const 
 }
 
 extern "C" int64_t cn_field_backward_workspace_floats(int64_t m) { return m * (2 * kLdP + 90 + 6); }
+
+// Offset (floats) of the (M, 90) dL/dx block inside that workspace (MLPForward's d x).
+extern "C" int64_t cn_field_backward_dx_offset(int64_t m) { return m > 0 ? 2 * kLdP * m : -1; }
 
 extern "C" int cn_code_bias_backward(const float* const* params, const float* z_s, const float* z_t, int64_t n_codes,
                                      const float* g_code, float* dz_s, float* dz_t, float* const* grads,

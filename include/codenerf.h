@@ -187,6 +187,8 @@ int cn_encode_inputs(const float* pts, const float* ro, const float* rd, const f
 
 /* Floats of scratch cn_field_backward needs for M sample rows. */
 int64_t cn_field_backward_workspace_floats(int64_t m);
+/* Offset (floats) of the (M, 90) dL/dx rows inside that scratch after cn_field_backward. */
+int64_t cn_field_backward_dx_offset(int64_t m);
 
 /* Backward of forward_pass + CodeNeRFModel.forward (model.py:160-194) from
  * d_raw (M, 4).  saved / x_enc from cn_radiance_field_train / cn_encode_inputs.

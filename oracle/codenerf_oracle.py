@@ -179,16 +179,21 @@ def _linear(p: Dict[str, Tensor], name: str, x: Tensor) -> Tensor:
 
 
 def codenerf_mlp(p: Dict[str, Tensor], z_s: Tensor, z_t: Tensor, x: Tensor, dim_xyz: int,
-                 relu_masks: Optional[Dict[str, Tensor]] = None) -> Tensor:
+                 relu_masks: Optional[Dict[str, Tensor]] = None,
+                 pre_out: Optional[Dict[str, Tensor]] = None) -> Tensor:
     """CodeNeRFModel.forward, model.py:160-194 -> (M, 4) = [rgb_raw(3), sigma_raw].
 
     ``relu_masks`` (test aid, default off): {"h1", "h2", "v1", "v2"} -> (M, 256) 0/1
     masks used in place of the four per-sample ReLUs' own decisions (pre * mask), so
     a backward can be checked against the ReLU kinks a kernel's forward recorded.
+    ``pre_out`` (test aid): a dict that receives the four per-sample pre-activations,
+    so a kernel's recorded ReLU decisions can be checked against this oracle's own.
     """
     relu = torch.nn.functional.relu
 
     def act(name, pre):
+        if pre_out is not None:
+            pre_out[name] = pre.detach()
         return relu(pre) if relu_masks is None else pre * relu_masks[name]
     xyz, view = x[..., :dim_xyz], x[..., dim_xyz:]
     zs1 = relu(_linear(p, "shape_code_layer1", z_s))
@@ -217,7 +222,8 @@ class EmbedCfg:
 
 
 def forward_pass(p: Dict[str, Tensor], emb: EmbedCfg, rd: Tensor, pts: Tensor,
-                 z_s: Tensor, z_t: Tensor, relu_masks: Optional[Dict[str, Tensor]] = None) -> Tensor:
+                 z_s: Tensor, z_t: Tensor, relu_masks: Optional[Dict[str, Tensor]] = None,
+                 pre_out: Optional[Dict[str, Tensor]] = None) -> Tensor:
     """nerf/__init__.py:94-134 -> (R, S, 4).  ``relu_masks``: see codenerf_mlp (rows r*S + s).
 
     Quirk Q1: ``viewdirs.repeat([1, S, 1])`` tiles the whole (R, 3) ray list, so
@@ -232,7 +238,7 @@ def forward_pass(p: Dict[str, Tensor], emb: EmbedCfg, rd: Tensor, pts: Tensor,
     vd = vd.repeat([1, s, 1])
     vd = vd.reshape(-1, vd.shape[-1])
     enc = torch.cat((enc, posenc(vd, emb.fd, emb.inc_d)), dim=-1)
-    out = codenerf_mlp(p, zs, zt, enc, emb.dim_xyz, relu_masks)
+    out = codenerf_mlp(p, zs, zt, enc, emb.dim_xyz, relu_masks, pre_out)
     return out.reshape([r, s, out.shape[-1]])
 
 

@@ -83,9 +83,13 @@ def small_intrinsics():
     return k
 
 
-def main():
+def main(only=None):
     nerf, model_mod, util, ev = import_reference()
     torch.set_num_threads(8)
+    if only:
+        for name in only:
+            ROUND2[name](nerf, model_mod, ev)
+        return
     pose = lambda th, ph, rh: ev.pose_spherical(torch.tensor([th]), torch.tensor([ph]), torch.tensor([rh]))  # noqa: E731
 
     # ---------------------------------------------------------------- rays
@@ -265,7 +269,207 @@ def main():
          g_fine_fc_rgb_w=models["nerf_fine"].fc_rgb.weight.grad, g_coarse_fc_out_b=models["nerf_coarse"].fc_out.bias.grad,
          **pw)
     print("split(1024,3) =", util.get_minibatches(torch.arange(10), 4))
+    for fn in ROUND2.values():
+        fn(nerf, model_mod, ev)
+
+
+# ==================================================================== round 2 fixtures
+# Each writes one .npz; ``python make_golden.py trained chairs lego c5`` regenerates a subset.
+
+
+def _pose(ev, th, ph, rh):
+    return ev.pose_spherical(torch.tensor([th]), torch.tensor([ph]), torch.tensor([rh]))
+
+
+def _make_model_p(model_mod, params):
+    m = model_mod.CodeNeRFModel(hidden_size=256, num_embeddings=1, shape_code_size=256, texture_code_size=256,
+                                num_encoding_fn_xyz=10, num_encoding_fn_dir=4, include_input_xyz=True,
+                                include_input_dir=True)
+    m.load_state_dict(params)
+    return m.eval()
+
+
+def _full_render(nerf, ps, emb, models, ro, rd, zs, zt, chunk, keep_coarse=True):
+    """The body of predict_radiance_and_render (nerf/__init__.py:81-89) per chunk, keeping depth/acc."""
+    cols = {k: [] for k in ["rgb_c", "depth_c", "acc_c", "rgb_f", "depth_f", "acc_f"]}
+    with torch.no_grad():
+        for c0 in range(0, ro.shape[0], chunk):
+            o, d = ro[c0:c0 + chunk], rd[c0:c0 + chunk]
+            n = o.shape[0]
+            lat = (zs.expand(n, -1), zt.expand(n, -1))
+            pts, z = ps.sample_uniform(o, d)
+            raw_c = nerf.forward_pass(models["nerf_coarse"], emb, d, pts, lat)
+            rgb_c, _, acc_c, w_c, depth_c = nerf.volume_render(raw_c, z, d)
+            pts2, z2 = ps.sample_pdf(o, d, w_c[..., 1:-1], z)
+            raw_f = nerf.forward_pass(models["nerf_fine"], emb, d, pts2, lat)
+            rgb_f, _, acc_f, _, depth_f = nerf.volume_render(raw_f, z2, d)
+            for k, v in zip(cols, [rgb_c, depth_c, acc_c, rgb_f, depth_f, acc_f]):
+                cols[k].append(v)
+    out = {k: torch.cat(v) for k, v in cols.items()}
+    if not keep_coarse:
+        out = {k: v for k, v in out.items() if k.endswith("_f")}
+    return out
+
+
+def _embedders(nerf):
+    return (nerf.PositionalEmbedder(10, True, True, torch.float32, "cpu"),
+            nerf.PositionalEmbedder(4, True, True, torch.float32, "cpu"))
+
+
+def gen_trained(nerf, model_mod, ev):
+    """Trained-magnitude weights (synthetic.TRAINED_CASES: weights x3/x4, codes ~unit variance,
+    sigma_raw 10-50): the MLP on 1000 random rows and the full 128x128 C2/C3 render."""
+    out = {}
+    g = torch.Generator().manual_seed(21)
+    x = torch.randn(1000, 90, generator=g)
+    x[:, :63] *= 1.5
+    out["x"] = x
+    K = synthetic.srn_intrinsics(128)
+    rs = nerf.RaySampler(128, 128, K, sample_size=4096, device="cpu", datatype=torch.float32)
+    cam = _pose(ev, 0.5, 0.3, 1.3)[None]
+    ro, rd = rs.get_bundle(cam)
+    ro, rd = ro.reshape(-1, 3), rd.reshape(-1, 3)
+    out.update(intrinsics=K, pose=cam)
+    emb = _embedders(nerf)
+    ps = nerf.PointSampler(64, 64, 0.8, 1.8, spacing_mode="lindepth", perturb=False, dtype=torch.float32,
+                           device="cpu")
+    for case in synthetic.TRAINED_CASES:
+        models = {"nerf_coarse": _make_model_p(model_mod, synthetic.trained_params(0, case)),
+                  "nerf_fine": _make_model_p(model_mod, synthetic.trained_params(1, case))}
+        zs, zt = synthetic.trained_codes(5, 1, case), synthetic.trained_codes(6, 1, case)
+        zr_s, zr_t = synthetic.trained_codes(7, 1000, case), synthetic.trained_codes(8, 1000, case)
+        with torch.no_grad():
+            out[case + "_mlp_raw"] = models["nerf_coarse"](zr_s, zr_t, x)
+        r = _full_render(nerf, ps, emb, models, ro, rd, zs, zt, 4096)
+        out.update({f"{case}_{k}": v for k, v in r.items()})
+    save("render_trained.npz", **out)
+
+
+def gen_chairs(nerf, model_mod, ev):
+    """C4 (srn-chairs-code.yml:53-60): 128x128, Nc 32 / Nf 128, near 1.25, far 2.75, validation
+    chunk 4096, rendered by parallel_image_render's per-rank slicing for 1/2/4/8 ranks."""
+    K = synthetic.srn_intrinsics(128)
+    rs = nerf.RaySampler(128, 128, K, sample_size=4096, device="cpu", datatype=torch.float32)
+    cam = _pose(ev, 0.5, 0.3, 2.0)[None]
+    emb = _embedders(nerf)
+    models = {"nerf_coarse": make_model(model_mod, 0), "nerf_fine": make_model(model_mod, 1)}
+    zs, zt = synthetic.latent_codes(5, 1), synthetic.latent_codes(6, 1)
+    ps = nerf.PointSampler(32, 128, 1.25, 2.75, spacing_mode="lindepth", perturb=False, dtype=torch.float32,
+                           device="cpu")
+    out = {"intrinsics": K, "pose": cam, "z_s": zs, "z_t": zt}
+    n_all = 128 * 128
+    for n_ranks in (1, 2, 4, 8):
+        cfg = Cfg(is_distributed=n_ranks > 1, gpus=n_ranks, nerf=Cfg(validation=Cfg(chunksize=4096)))
+        if n_ranks == 1:
+            img = nerf.parallel_image_render(cfg, cam, [zs, zt], models, (rs, ps), emb, "cpu")
+        else:
+            pieces = {}
+            real_rank, real_gather = nerf.dist.get_rank, torch.distributed.all_gather
+            for r in range(n_ranks):
+                nerf.dist.get_rank = lambda r=r: r
+                torch.distributed.all_gather = lambda lst, t, r=r: pieces.__setitem__(r, t.clone())
+                nerf.parallel_image_render(cfg, cam, [zs, zt], models, (rs, ps), emb, "cpu")
+            nerf.dist.get_rank, torch.distributed.all_gather = real_rank, real_gather
+            per = torch.full([n_ranks], (n_all / n_ranks), dtype=int)
+            per[-1] = n_all - torch.sum(per[:-1])
+            img = torch.cat([pieces[r][: per[r]] for r in range(n_ranks)], dim=0)
+            out[f"n{n_ranks}_split"] = per.numpy()
+        out[f"n{n_ranks}_rgb"] = img
+    ro, rd = rs.get_bundle(cam)
+    r = _full_render(nerf, ps, emb, models, ro.reshape(-1, 3), rd.reshape(-1, 3), zs, zt, 4096)
+    out.update(depth_f=r["depth_f"], acc_f=r["acc_f"], rgb_c=r["rgb_c"])
+    save("render_chairs.npz", **out)
+
+
+LEGO_FOCAL = 0.5 * 64 / float(np.tan(0.5 * 0.6911112070083618))   # Blender lego camera_angle_x at 64 px
+
+
+def gen_lego(nerf, model_mod, ev):
+    """C1 plumbing (config/lego.yml:37-46 with BASELINE.json's 64x64 / 32 samples): every leaf
+    component driven with lego's parameters -- near 2, far 6, lindepth, Nc 32, Nf 128, chunk 8192
+    (validation) -- deterministic and perturbed (uniforms recorded)."""
+    K = torch.eye(4, dtype=torch.float32)
+    K[0, 0] = K[1, 1] = LEGO_FOCAL
+    K[0, 2] = K[1, 2] = 32.0
+    rs = nerf.RaySampler(64, 64, K, sample_size=1024, device="cpu", datatype=torch.float32)
+    cam = _pose(ev, 0.6, -0.4, 4.0)[None]
+    ro, rd = rs.get_bundle(cam)
+    ro, rd = ro.reshape(-1, 3), rd.reshape(-1, 3)
+    emb = _embedders(nerf)
+    models = {"nerf_coarse": make_model(model_mod, 2), "nerf_fine": make_model(model_mod, 3)}
+    zs, zt = synthetic.latent_codes(9, 1), synthetic.latent_codes(10, 1)
+    out = {"intrinsics": K, "pose": cam, "directions": rs.directions, "ro": ro, "rd": rd, "z_s": zs, "z_t": zt}
+    for pert in (False, True):
+        tag = "p" if pert else "d"
+        ps = nerf.PointSampler(32, 128, 2.0, 6.0, spacing_mode="lindepth", perturb=pert, dtype=torch.float32,
+                               device="cpu")
+        torch.manual_seed(123)
+        pts, z = ps.sample_uniform(ro, rd)
+        raw = nerf.forward_pass(models["nerf_coarse"], emb, rd, pts, (zs.expand(4096, -1), zt.expand(4096, -1)))
+        rgb_c, disp_c, acc_c, w_c, depth_c = nerf.volume_render(raw, z, rd)
+        pts_f, z_f = ps.sample_pdf(ro, rd, w_c[..., 1:-1], z)
+        raw_f = nerf.forward_pass(models["nerf_fine"], emb, rd, pts_f, (zs.expand(4096, -1), zt.expand(4096, -1)))
+        rgb_f, _, acc_f, _, depth_f = nerf.volume_render(raw_f, z_f, rd)
+        if pert:
+            # the draws are re-made by the tests from the same seed (torch CPU Philox, same image);
+            # their head and sums are stored so a different generator fails loudly
+            torch.manual_seed(123)
+            t_rand, u = torch.rand(4096, 32), torch.rand(4096, 128)
+            out.update(t_rand_head=t_rand[:4], u_head=u[:4], t_rand_sum=t_rand.double().sum(),
+                       u_sum=u.double().sum())
+        # row subsets keep the fixture small; every row was computed over the whole 4096-ray list (Q1)
+        out.update({f"{tag}_z": z[:512], f"{tag}_raw": raw[:64], f"{tag}_rgb_c": rgb_c, f"{tag}_acc_c": acc_c,
+                    f"{tag}_depth_c": depth_c, f"{tag}_w_c": w_c[:512], f"{tag}_z_f": z_f[:512], f"{tag}_rgb_f": rgb_f,
+                    f"{tag}_depth_f": depth_f, f"{tag}_acc_f": acc_f})
+        if not pert:
+            out["enc_xyz"] = emb[0].embed(pts.reshape(-1, 3)[:256])
+            out["d_pts"] = pts[:64]
+    save("lego_c1.npz", **out)
+
+
+def gen_c5(nerf, model_mod, ev):
+    """C5 at size (srn-cars-code-3080-val.yml): one eval.py:141-167 step, 2048 rays over a 128x128
+    view, 64 + 64 perturbed samples (uniforms recorded), whole batch in one predict_radiance_and_render
+    call; gradients into theta, phi, rho and both codes (weights also require grad, as in eval.py)."""
+    K = synthetic.srn_intrinsics(128)
+    rs = nerf.RaySampler(128, 128, K, sample_size=2048, device="cpu", datatype=torch.float32)
+    ps = nerf.PointSampler(64, 64, 0.8, 1.8, spacing_mode="lindepth", perturb=True, dtype=torch.float32,
+                           device="cpu")
+    emb = _embedders(nerf)
+    models = {"nerf_coarse": make_model(model_mod, 0), "nerf_fine": make_model(model_mod, 1)}
+    for mm in models.values():
+        mm.train()
+    g = torch.Generator().manual_seed(31)
+    target = torch.rand(128 * 128, 4, generator=g)
+    theta = torch.tensor([1.2]).requires_grad_(True)
+    phi = torch.tensor([0.4]).requires_grad_(True)
+    rho = torch.tensor([1.35]).requires_grad_(True)
+    zs = synthetic.latent_codes(5, 1).clone().requires_grad_(True)
+    zt = synthetic.latent_codes(6, 1).clone().requires_grad_(True)
+    np.random.seed(17)
+    c2w = ev.pose_spherical(theta, phi, rho)[None, :]
+    ro, rd, sel = rs.sample(tform_cam2world=c2w)
+    tp = target[None][..., sel, :].squeeze()
+    zse, zte = zs.expand(ro.shape[0], -1), zt.expand(ro.shape[0], -1)
+    torch.manual_seed(4242)
+    rgb_c, rgb_f = nerf.predict_radiance_and_render((ro, rd), ps, emb, models["nerf_coarse"], models["nerf_fine"],
+                                                    (zse, zte))
+    torch.manual_seed(4242)
+    t_rand, u = torch.rand(2048, 64), torch.rand(2048, 64)
+    lc = torch.nn.functional.mse_loss(rgb_c[..., :3], tp[..., :3])
+    lf = torch.nn.functional.mse_loss(rgb_f[..., :3], tp[..., :3])
+    loss = lc + lf + 1e-5 * (torch.norm(zse, p=2) + torch.norm(zte, p=2))
+    loss.backward()
+    pw = {f"gnorm_{k}.{n}": p.grad.norm() for k, mm in models.items() for n, p in mm.named_parameters()}
+    save("eval_c5.npz", target=target, select_inds=sel.astype(np.int64), theta=theta, phi=phi, rho=rho,
+         z_s=zs, z_t=zt, t_rand=t_rand, u=u, rgb_coarse=rgb_c, rgb_fine=rgb_f, loss=loss, g_theta=theta.grad,
+         g_phi=phi.grad, g_rho=rho.grad, g_z_s=zs.grad, g_z_t=zt.grad,
+         g_fine_fc_rgb_w=models["nerf_fine"].fc_rgb.weight.grad,
+         g_coarse_layer_xyz1_w=models["nerf_coarse"].layer_xyz1.weight.grad, **pw)
+
+
+ROUND2 = {"trained": gen_trained, "chairs": gen_chairs, "lego": gen_lego, "c5": gen_c5}
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:] or None)

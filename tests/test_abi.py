@@ -68,3 +68,21 @@ def test_ops_refuse_cpu_tensors():
     from codenerf import ops
     with pytest.raises(ValueError):
         ops.posenc(torch.zeros(3, 3), [1.0, 2.0], True)
+
+
+def test_backward_workspace_layout(lib_path):
+    """The d x block sits inside the workspace the library sizes (no hand-kept stride in Python)."""
+    from codenerf import _lib
+    lib = _lib.load(lib_path)
+    for m in (1, 257, 100000):
+        ws, off = lib.cn_field_backward_workspace_floats(m), lib.cn_field_backward_dx_offset(m)
+        assert 0 < off and off + 90 * m <= ws
+    assert lib.cn_field_backward_dx_offset(0) == -1
+
+
+def test_library_built_from_this_tree(lib_path):
+    """cn_version() carries the hash of the sources it was compiled from (codenerf/provenance.py)."""
+    from codenerf import _lib, provenance
+    lib = _lib.load(lib_path)
+    v = provenance.version_of(lib.cn_version().decode())
+    assert v.get("src") == provenance.source_hash(), (v, provenance.source_hash())

@@ -22,6 +22,9 @@ from conftest import GOLDEN
 pytestmark = pytest.mark.gpu
 
 GRAD_RTOL = 2e-4
+# against an oracle that takes its own ReLU / resampling decisions (a kink crossed within the kernel's
+# rounding error moves one sample's contribution by a whole weight column)
+INDEPENDENT_RTOL = 2e-3
 
 
 @pytest.fixture(scope="module")
@@ -83,6 +86,21 @@ def test_gemm_nn_masked(dev, m, n, k, precision):
     c = ops.gemm_nn(a.to(dev), b.to(dev), mask.to(dev), precision=precision)
     ref = (a.double() @ b.double()) * (mask > 0)
     close(c, ref, GEMM_TOL[precision], "gemm_nn " + precision)
+
+
+@pytest.mark.parametrize("precision", ["f32", "bf16x3"])
+@pytest.mark.parametrize("m,k,lda", [(1000, 257, 260), (777, 256, 260), (129, 63, 90)])
+def test_gemm_nn_strided_a(dev, m, k, lda, precision):
+    """Row-strided A (lda > K, the field backward's rows of 260): the dwordx4 VEC path with a
+    ragged K and the scalar tail, masked."""
+    from codenerf import ops
+    g = torch.Generator().manual_seed(m + k)
+    store = torch.randn(m, lda, generator=g)
+    a = store[:, :k]
+    b = torch.randn(k, 256, generator=g)
+    mask = torch.randn(m, 256, generator=g)
+    c = ops.gemm_nn(store.to(dev)[:, :k], b.to(dev), mask.to(dev), precision=precision)
+    close(c, (a.double() @ b.double()) * (mask > 0), GEMM_TOL[precision], f"gemm_nn lda={lda} " + precision)
 
 
 @pytest.mark.parametrize("precision", ["f32", "bf16x3"])
@@ -173,15 +191,43 @@ def test_ray_bundle_gather_points_backward(dev):
 # ---------------------------------------------------------------- field (forward_pass + CodeNeRFModel)
 
 
-def _oracle_field(o, p, rd, pts, zs, zt, chunk, masks=None):
+def _oracle_field(o, p, rd, pts, zs, zt, chunk, masks=None, pre_out=None):
     emb = o.EmbedCfg()
     s = pts.shape[1]
-    outs = []
+    outs, pres = [], []
     for c0 in range(0, rd.shape[0], chunk):
         c1 = min(c0 + chunk, rd.shape[0])
         mk = None if masks is None else {k: v[c0 * s:c1 * s] for k, v in masks.items()}
-        outs.append(o.forward_pass(p, emb, rd[c0:c1], pts[c0:c1], zs[c0:c1], zt[c0:c1], mk))
+        pre = {} if pre_out is not None else None
+        outs.append(o.forward_pass(p, emb, rd[c0:c1], pts[c0:c1], zs[c0:c1], zt[c0:c1], mk, pre))
+        pres.append(pre)
+    if pre_out is not None:
+        for k in pres[0]:
+            pre_out[k] = torch.cat([q[k] for q in pres])
     return torch.cat(outs)
+
+
+# ReLU decisions a kernel recorded may differ from an independent fp32 forward only where the
+# pre-activation is within that kernel's arithmetic error of 0: fp32 MFMA (reassociated sums)
+# ~1e-6 relative, 3xbf16 ~2^-17 per product; MASK_BAND is relative to the layer's max |pre|.
+MASK_BAND = {"f32": 1e-5, "bf16x3": 1e-4}
+
+
+def check_mask_agreement(masks, pre, band_rel, what=""):
+    """Every ReLU decision in ``masks`` ((M, 256) 0/1 per layer) that disagrees with the oracle's own
+    pre-activation ``pre`` must sit inside the error band; returns the number of disagreements."""
+    n_dis = 0
+    for k, m in masks.items():
+        p = pre[k].double()
+        own = p > 0
+        dis = m.bool() != own
+        scale = p.abs().max().item()
+        bad = dis & (p.abs() >= band_rel * scale)
+        assert not bool(bad.any()), (f"{what} layer {k}: {int(bad.sum())} ReLU decisions differ from the oracle "
+                                     f"outside the band (max |pre| there {p.abs()[bad].max().item():.3e}, "
+                                     f"band {band_rel * scale:.3e})")
+        n_dis += int(dis.sum())
+    return n_dis
 
 
 def decode_relu_masks(words: torch.Tensor, m_rows: int):
@@ -220,6 +266,7 @@ def test_field_backward(dev, mode, r, s, chunk, per_ray_codes, precision):
     o = O()
     m = model(dev, 0)
     m.precision = precision
+    m.train_precision = precision
     p = oracle_params(m)
     g = torch.Generator().manual_seed(r * s)
     ro = torch.randn(r, 3, generator=g) * 0.3 + torch.tensor([0.0, 0.0, 1.3])
@@ -274,10 +321,12 @@ def test_field_backward_eval_fused(dev, monkeypatch, mode, r, s, chunk, per_ray_
     """Frozen bf16x3 model (the eval step): the 3xbf16 forward with ReLU masks and ONE fused backward
     launch (cn_field_backward_x3) give the oracle's d ro / d rd / d z_s / d z_t.
 
-    The oracle takes the ReLU decisions the kernel's forward recorded (decode_relu_masks): a
-    pre-activation within the 3xbf16 error of 0 can fall on the other side of the kink in an
-    independent fp32 forward, which moves that sample's gradient by a whole weight column -- a
-    property of the kink, not an error of the backward."""
+    Checked three ways: (1) against the oracle with its own ReLU decisions (INDEPENDENT_RTOL);
+    (2) every ReLU decision the kernel's forward recorded (decode_relu_masks) equals the oracle's
+    own except where |pre-activation| is inside the 3xbf16 error band (check_mask_agreement); (3)
+    with those recorded decisions, the oracle's gradients match at GRAD_RTOL -- a pre-activation
+    within the kernel's error of 0 can fall on the other side of the kink, which moves that
+    sample's gradient by a whole weight column."""
     from codenerf import nerf, ops, synthetic
     calls = {"fused": 0, "masks": None}
     real_bwd, real_fwd = ops.field_backward_x3, ops.radiance_field_masks
@@ -321,18 +370,32 @@ def test_field_backward_eval_fused(dev, monkeypatch, mode, r, s, chunk, per_ray_
     assert calls["fused"] == (1 if fused else 0)
     masks = decode_relu_masks(calls["masks"], r * s) if fused else None
 
-    ro_c, rd_c = ro.clone().requires_grad_(True), rd.clone().requires_grad_(True)
-    zs_c, zt_c = zs.clone().requires_grad_(True), zt.clone().requires_grad_(True)
-    pts_c = ro_c[:, None, :] + rd_c[:, None, :] * z[..., None]
-    zse = zs_c if per_ray_codes else zs_c.expand(r, -1)
-    zte = zt_c if per_ray_codes else zt_c.expand(r, -1)
-    raw_c = _oracle_field(o, {k: v.detach() for k, v in p.items()}, rd_c, pts_c, zse, zte, chunk, masks)
-    (raw_c * gout).sum().backward()
-    assert (raw_g.detach().cpu() - raw_c.detach()).abs().max().item() <= 1e-4
-    close(ro_g.grad, ro_c.grad, what="d ro")
-    close(rd_g.grad, rd_c.grad, what="d rd")
-    close(zs_g.grad, zs_c.grad, what="d z_s")
-    close(zt_g.grad, zt_c.grad, what="d z_t")
+    pd = {k: v.detach() for k, v in p.items()}
+
+    def oracle(mk, pre=None):
+        ro_c, rd_c = ro.clone().requires_grad_(True), rd.clone().requires_grad_(True)
+        zs_c, zt_c = zs.clone().requires_grad_(True), zt.clone().requires_grad_(True)
+        pts_c = ro_c[:, None, :] + rd_c[:, None, :] * z[..., None]
+        zse = zs_c if per_ray_codes else zs_c.expand(r, -1)
+        zte = zt_c if per_ray_codes else zt_c.expand(r, -1)
+        raw_c = _oracle_field(o, pd, rd_c, pts_c, zse, zte, chunk, mk, pre)
+        (raw_c * gout).sum().backward()
+        return raw_c.detach(), ro_c.grad, rd_c.grad, zs_c.grad, zt_c.grad
+
+    # 1. the oracle with its OWN ReLU decisions: independent of anything the kernel recorded
+    pre = {}
+    own = oracle(None, pre)
+    assert (raw_g.detach().cpu() - own[0]).abs().max().item() <= 1e-4
+    for got, ref, what in zip((ro_g.grad, rd_g.grad, zs_g.grad, zt_g.grad), own[1:], ("ro", "rd", "z_s", "z_t")):
+        close(got, ref, INDEPENDENT_RTOL, "d " + what + " (oracle's own ReLU decisions)")
+    if fused:
+        # 2. the kernel's recorded decisions agree with the oracle's except inside the 3xbf16 band ...
+        n_dis = check_mask_agreement(masks, pre, MASK_BAND["bf16x3"], "fused forward")
+        print(f"ReLU decisions differing from the oracle (all in-band): {n_dis}")
+        # 3. ... so with those decisions the gradients must match tightly
+        fed = oracle(masks)
+        for got, ref, what in zip((ro_g.grad, rd_g.grad, zs_g.grad, zt_g.grad), fed[1:], ("ro", "rd", "z_s", "z_t")):
+            close(got, ref, what="d " + what)
 
 
 @pytest.mark.parametrize("m_rows,dedupe", [(1000, True), (257, False)])
@@ -426,3 +489,4 @@ def test_test_time_optimize_runs(dev):
     assert not torch.allclose(zs.detach().cpu(), codes[0].mean(0, keepdim=True))
     assert abs(theta.item() - 1.57) > 1e-4 and abs(rho.item() - 1.30) > 1e-4
     assert all(p.requires_grad for mm in models.values() for p in mm.parameters())
+

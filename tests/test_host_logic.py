@@ -68,3 +68,43 @@ def test_synthetic_weights_are_deterministic():
     assert list(a) == [f"{n}.{p}" for n in ["layer_xyz1", "layer_xyz2", "fc_out", "shape_code_layer1",
                                             "shape_code_layer2", "texture_code_layer1", "layer_dir1", "layer_dir2",
                                             "fc_rgb"] for p in ["weight", "bias"]]
+
+
+from test_gpu_grad import MASK_BAND, check_mask_agreement  # noqa: E402  (helpers only; no GPU needed)
+
+
+def test_mask_checker_catches_a_flipped_bit():
+    """A deliberately flipped ReLU decision at a large pre-activation fails check_mask_agreement
+    (the guard that keeps the recorded-decision comparison from being self-fulfilling)."""
+    g = torch.Generator().manual_seed(5)
+    pre = {k: torch.randn(300, 256, generator=g) for k in ("h1", "h2", "v1", "v2")}
+    masks = {k: (v > 0).float() for k, v in pre.items()}
+    assert check_mask_agreement(masks, pre, MASK_BAND["bf16x3"]) == 0
+    near = dict(masks)
+    i = int(pre["h2"].abs().argmin())           # a kink-adjacent flip is allowed
+    near["h2"] = masks["h2"].clone().view(-1)
+    near["h2"][i] = 1.0 - near["h2"][i]
+    near["h2"] = near["h2"].view(300, 256)
+    if pre["h2"].view(-1)[i].abs() < MASK_BAND["bf16x3"] * pre["h2"].abs().max():
+        assert check_mask_agreement(near, pre, MASK_BAND["bf16x3"]) == 1
+    bad = dict(masks)
+    j = int(pre["v1"].abs().argmax())
+    bad["v1"] = masks["v1"].clone().view(-1)
+    bad["v1"][j] = 1.0 - bad["v1"][j]
+    bad["v1"] = bad["v1"].view(300, 256)
+    with pytest.raises(AssertionError):
+        check_mask_agreement(bad, pre, MASK_BAND["bf16x3"])
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    """bench.py --gpus N with fewer than N visible GPUs fails loudly instead of reporting 1 rank."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="0")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "64", "--steps", "1"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode != 0
+    assert "needs 64 visible GPUs" in (r.stderr + r.stdout)

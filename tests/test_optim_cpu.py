@@ -103,9 +103,27 @@ def _dp_worker(rank, world, port, out):
             p.grad = torch.full_like(p, float(rank + 1))
         if rank == 1:
             ps[3].grad = None                    # absent on one rank: counts as zero
+        ps[1].grad = None                        # absent on every rank: stays None (step skips it)
         opt.allreduce_grads()
+        assert ps[1].grad is None
         np.savez(out.format(rank), params=torch.cat([p.detach().reshape(-1) for p in ps]).numpy(),
-                 grads=torch.cat([p.grad.reshape(-1) for p in ps]).numpy())
+                 grads=torch.cat([(p.grad if p.grad is not None else torch.full_like(p, -7.0)).reshape(-1)
+                                  for p in ps]).numpy())
+        # the torch-optimiser fallback: ranks with DIFFERENT missing gradients issue the same
+        # all-reduce sizes (no hang) and the same flags
+        from types import SimpleNamespace
+        from codenerf import train as T
+        qs = _params(seed=10 + rank)
+        mods = {"m": SimpleNamespace(parameters=lambda: iter(qs))}
+        T.broadcast_parameters(mods)
+        for q in qs:
+            q.grad = torch.full_like(q, float(rank + 1))
+        qs[rank].grad = None                     # rank 0 lacks q0, rank 1 lacks q1
+        qs[4].grad = None                        # nobody has q4
+        T._average_gradients(torch.optim.SGD(qs, lr=0.1), mods)
+        np.savez(out.format(rank) + ".fallback.npz",
+                 params=torch.cat([q.detach().reshape(-1) for q in qs]).numpy(),
+                 g0=qs[0].grad.numpy(), g1=qs[1].grad.numpy(), g2=qs[2].grad.numpy(), none4=qs[4].grad is None)
     finally:
         dist.destroy_process_group()
 
@@ -121,4 +139,10 @@ def test_allreduce_and_broadcast_gloo(tmp_path):
     exp = np.concatenate([np.full(n, 1.5, np.float32) for n in sizes])
     o3 = sum(sizes[:3])
     exp[o3:o3 + sizes[3]] = 0.5                   # (1 + 0) / 2
+    exp[sizes[0]:sizes[0] + sizes[1]] = -7.0      # no rank had it: grad None
     assert np.array_equal(r0["grads"], exp) and np.array_equal(r1["grads"], exp)
+    f0, f1 = np.load(out.format(0) + ".fallback.npz"), np.load(out.format(1) + ".fallback.npz")
+    ref10 = torch.cat([q.detach().reshape(-1) for q in _params(seed=10)]).numpy()
+    assert np.array_equal(f0["params"], ref10) and np.array_equal(f1["params"], ref10)   # broadcast from rank 0
+    for f in (f0, f1):
+        assert np.all(f["g0"] == 1.0) and np.all(f["g1"] == 0.5) and np.all(f["g2"] == 1.5) and bool(f["none4"])

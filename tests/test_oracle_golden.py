@@ -166,3 +166,120 @@ def test_split_sizes():
     assert O.split_sizes(16384, 8)[0] == [2048] * 8
     per, pad = O.split_sizes(100, 7)
     assert per == [14] * 6 + [16] and pad == [2] * 6 + [0]
+
+
+# ---------------------------------------------------------------- round-2 fixtures (make_golden.py gen_*)
+
+
+def _srn_rays(g, size=128):
+    d = O.ray_directions(size, size, g["intrinsics"])
+    ro, rd = O.ray_bundle(d, g["pose"])
+    return ro.reshape(-1, 3), rd.reshape(-1, 3)
+
+
+@pytest.mark.parametrize("case", sorted(synthetic.TRAINED_CASES))
+def test_trained_magnitude(case):
+    """Trained-magnitude weights: the MLP rows and the first 4096-ray chunk of the C3 render."""
+    g = load("render_trained.npz")
+    pc, pf = synthetic.trained_params(0, case), synthetic.trained_params(1, case)
+    with torch.no_grad():
+        raw = O.codenerf_mlp(pc, synthetic.trained_codes(7, 1000, case), synthetic.trained_codes(8, 1000, case),
+                             g["x"], 63)
+    same(raw, g[case + "_mlp_raw"])
+    assert raw[:, 3].median() > 10.0             # sigma_raw in the trained range
+    ro, rd = _srn_rays(g)
+    n = 4096
+    zs, zt = synthetic.trained_codes(5, 1, case).expand(n, -1), synthetic.trained_codes(6, 1, case).expand(n, -1)
+    with torch.no_grad():
+        out = O.predict_radiance_and_render(ro[:n], rd[:n], O.Sampling(64, 64, 0.8, 1.8), O.EmbedCfg(), pc, pf, zs, zt)
+    for a, k in [("rgb_coarse", "rgb_c"), ("depth_coarse", "depth_c"), ("rgb_fine", "rgb_f"), ("depth_fine", "depth_f"),
+                 ("acc_fine", "acc_f")]:
+        same(out[a], g[f"{case}_{k}"][:n])
+
+
+def test_chairs_c4_chunk():
+    """C4 (chairs, Nc 32 / Nf 128, near 1.25 far 2.75): the first chunk of the 1-rank image and the
+    8-rank split (2048-ray slices -> 2048-ray chunks, Q1) of rank 0."""
+    g = load("render_chairs.npz")
+    ro, rd = _srn_rays(g)
+    assert O.split_sizes(16384, 8)[0] == g["n8_split"].tolist()
+    pc, pf = synthetic.codenerf_params(0), synthetic.codenerf_params(1)
+    smp = O.Sampling(32, 128, 1.25, 2.75)
+    for n, key in [(4096, "n1_rgb"), (2048, "n8_rgb")]:
+        zs, zt = g["z_s"].expand(n, -1), g["z_t"].expand(n, -1)
+        with torch.no_grad():
+            out = O.predict_radiance_and_render(ro[:n], rd[:n], smp, O.EmbedCfg(), pc, pf, zs, zt)
+        same(out["rgb_fine"], g[key][:n])
+    same(g["n1_rgb"], g["n2_rgb"])             # 8192-ray slices keep the 4096-ray chunks
+    same(g["n1_rgb"], g["n4_rgb"])
+
+
+def lego_uniforms(g):
+    torch.manual_seed(123)
+    t_rand, u = torch.rand(4096, 32), torch.rand(4096, 128)
+    same(t_rand[:4], g["t_rand_head"])
+    same(u[:4], g["u_head"])
+    assert abs(t_rand.double().sum().item() - g["t_rand_sum"].item()) < 0.05      # stored as fp32
+    assert abs(u.double().sum().item() - g["u_sum"].item()) < 0.05
+    return t_rand, u
+
+
+@pytest.mark.parametrize("tag", ["d", "p"])
+def test_lego_c1(tag):
+    """C1: every leaf with lego's parameters (64x64, Nc 32, Nf 128, near 2, far 6, one 4096-ray chunk)."""
+    g = load("lego_c1.npz")
+    d = O.ray_directions(64, 64, g["intrinsics"])
+    same(d, g["directions"])
+    ro, rd = O.ray_bundle(d, g["pose"])
+    ro, rd = ro.reshape(-1, 3), rd.reshape(-1, 3)
+    same(ro, g["ro"])
+    same(rd, g["rd"])
+    smp = O.Sampling(32, 128, 2.0, 6.0)
+    t_rand, u = lego_uniforms(g) if tag == "p" else (None, None)
+    pc, pf = synthetic.codenerf_params(2), synthetic.codenerf_params(3)
+    zs, zt = g["z_s"].expand(4096, -1), g["z_t"].expand(4096, -1)
+    pts, z = O.sample_uniform(ro, rd, smp.bins, t_rand)
+    same(z[:512], g[tag + "_z"])
+    if tag == "d":
+        same(pts[:64], g["d_pts"])
+        same(O.posenc(pts.reshape(-1, 3)[:256], O.frequency_bands(10, True), True), g["enc_xyz"])
+    with torch.no_grad():
+        raw = O.forward_pass(pc, O.EmbedCfg(), rd, pts, zs, zt)
+        out = O.predict_radiance_and_render(ro, rd, smp, O.EmbedCfg(), pc, pf, zs, zt, t_rand, u)
+    same(raw[:64], g[tag + "_raw"])
+    same(out["weights_coarse"][:512], g[tag + "_w_c"])
+    same(out["z_fine"][:512], g[tag + "_z_f"])
+    for a, k in [("rgb_coarse", "rgb_c"), ("acc_coarse", "acc_c"), ("depth_coarse", "depth_c"), ("rgb_fine", "rgb_f"),
+                 ("depth_fine", "depth_f"), ("acc_fine", "acc_f")]:
+        same(out[a], g[f"{tag}_{k}"])
+
+
+def test_eval_c5_gradients():
+    """C5 at size: one eval step (2048 rays of a 128x128 view, 64 + 64 perturbed) through the oracle's
+    autograd equals the reference's own."""
+    g = load("eval_c5.npz")
+    theta, phi, rho = [g[k].clone().requires_grad_(True) for k in ("theta", "phi", "rho")]
+    zs, zt = g["z_s"].clone().requires_grad_(True), g["z_t"].clone().requires_grad_(True)
+    pc, pf = synthetic.codenerf_params(0), synthetic.codenerf_params(1)
+    for p in list(pc.values()) + list(pf.values()):
+        p.requires_grad_(True)
+    c2w = O.pose_spherical(theta, phi, rho)[None]
+    d = O.ray_directions(128, 128, synthetic.srn_intrinsics(128))
+    ro, rd = O.ray_bundle(d, c2w)
+    sel = g["select_inds"].numpy()
+    ro, rd = O.gather_rays(ro, rd, sel)
+    n = ro.shape[0]
+    tp = g["target"][None][..., sel, :].squeeze()
+    zse, zte = zs.expand(n, -1), zt.expand(n, -1)
+    out = O.predict_radiance_and_render(ro, rd, O.Sampling(64, 64, 0.8, 1.8), O.EmbedCfg(), pc, pf, zse, zte,
+                                        g["t_rand"], g["u"])
+    lc = torch.nn.functional.mse_loss(out["rgb_coarse"][..., :3], tp[..., :3])
+    lf = torch.nn.functional.mse_loss(out["rgb_fine"][..., :3], tp[..., :3])
+    loss = lc + lf + 1e-5 * (torch.norm(zse, p=2) + torch.norm(zte, p=2))
+    loss.backward()
+    same(out["rgb_coarse"].detach(), g["rgb_coarse"])
+    same(out["rgb_fine"].detach(), g["rgb_fine"])
+    same(loss.detach(), g["loss"])
+    for t, k in [(theta, "theta"), (phi, "phi"), (rho, "rho"), (zs, "z_s"), (zt, "z_t")]:
+        same(t.grad, g["g_" + k], 1e-8)
+    same(pf["fc_rgb.weight"].grad, g["g_fine_fc_rgb_w"], 1e-8)
