@@ -144,8 +144,11 @@ def test_lego_c1_leaf_ops(dev, tag):
     assert maxdiff(z[:512], g[tag + "_z"]) == 0.0
     emb = embedders(dev)
     if tag == "d":
-        assert maxdiff(pts[:64], g["d_pts"]) == 0.0
-        assert maxdiff(emb[0].embed(pts.reshape(-1, 3)[:256]), g["enc_xyz"]) <= 2e-6
+        # pts = ro + rd z: bit-exact on the fixture's own rays (cn_ray_points), and within rd's
+        # einsum-order ulp x far on ours
+        assert maxdiff(ps.sample_uniform(g["ro"], g["rd"])[0][:64], g["d_pts"]) == 0.0
+        assert maxdiff(pts[:64], g["d_pts"]) <= 6e-6
+        assert maxdiff(emb[0].embed(g["d_pts"][:8].reshape(-1, 3)), g["enc_xyz"]) <= 2e-6
     mc = model_from(dev, synthetic.codenerf_params(2), "f32")
     mf = model_from(dev, synthetic.codenerf_params(3), "f32")
     zs, zt = g["z_s"].expand(4096, -1), g["z_t"].expand(4096, -1)
@@ -154,8 +157,12 @@ def test_lego_c1_leaf_ops(dev, tag):
         assert maxdiff(raw[:64], g[tag + "_raw"]) <= 1e-4
         w = volume_render(raw, z, rd)[3]
         assert maxdiff(w[:512], g[tag + "_w_c"]) <= 1e-5
-        _, z_f = ps.sample_pdf(ro, rd, w[..., 1:-1], z, u=u)
-        assert maxdiff(z_f[:512], g[tag + "_z_f"]) <= 1e-4
+        # inverse-CDF resampling on the reference's own coarse weights (identical inputs): the
+        # fine depths to 1e-5 (near-empty bins amplify a weight's last bit by 1/pdf, so a
+        # resampling of OUR weights is checked end to end through the rendered maps below)
+        _, z_f = ps.sample_pdf(ro[:512], rd[:512], g[tag + "_w_c"][..., 1:-1], z[:512],
+                               u=None if u is None else u[:512])
+        assert maxdiff(z_f, g[tag + "_z_f"]) <= 1e-5
         o = render_rays(ro, rd, zs, zt, ps, emb, mc, mf, chunk_rows=8192, t_rand=t_rand, u=u)
     for a, k in [("rgb_coarse", "rgb_c"), ("acc_coarse", "acc_c"), ("depth_coarse", "depth_c"), ("rgb_fine", "rgb_f"),
                  ("depth_fine", "depth_f"), ("acc_fine", "acc_f")]:

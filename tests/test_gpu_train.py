@@ -18,8 +18,8 @@ import numpy as np
 import pytest
 import torch
 
-from test_gpu_grad import (GRAD_RTOL, INDEPENDENT_RTOL, MASK_BAND, O, check_mask_agreement, close,  # noqa: F401
-                           dev, embedders, model, oracle_params)
+from test_gpu_grad import (GRAD_RTOL, MASK_BAND, O, check_mask_agreement, close, dev, embedders,  # noqa: F401
+                           explained_by_kinks, model, oracle_params)
 
 pytestmark = pytest.mark.gpu
 
@@ -119,12 +119,13 @@ def test_train_minibatch_matches_oracle(dev, monkeypatch, chunk, mixed):
     band; (3) with those decisions fed to the oracle, every gradient matches at GRAD_RTOL."""
     from codenerf import ops, train as T
     from codenerf.nerf import PointSampler
-    seen = {"z_fine": None, "saved": []}
+    seen = {"z_fine": None, "saved": [], "w_coarse": None}
     real_pdf, real_train = ops.sample_pdf, ops.radiance_field_train
 
     def spy_pdf(*a, **k):
         r = real_pdf(*a, **k)
         seen["z_fine"] = r[1].detach().cpu()
+        seen["w_coarse"] = a[2].detach().cpu().clone()       # the kernel's weights[..., 1:-1]
         return r
 
     def spy_train(*a, **k):
@@ -175,30 +176,44 @@ def test_train_minibatch_matches_oracle(dev, monkeypatch, chunk, mixed):
             lf = torch.nn.functional.mse_loss(rgb_f[..., :3], tgt[sl, :3])
             loss = lc + lf + lam * (torch.norm(ts.detach(), p=2) + torch.norm(tt.detach(), p=2))
             loss.backward()
-            return loss.item(), pc, pf, ts, tt, z_f
+            return loss.item(), pc, pf, ts, tt, z_f, w_c.detach(), z_c
 
-        def compare(res, rtol, tag):
-            loss, pc, pf, ts, tt, _ = res
-            assert abs(float(logs["total_loss"]) - loss) <= 1e-5, tag
-            for key, ref in (("nerf_coarse", pc), ("nerf_fine", pf)):
-                for name, prm in models[key].named_parameters():
-                    close(prm.grad, ref[name].grad, rtol, f"{tag} {key}.{name}")
-            close(models["embedding"].shape_embedding.weight.grad, ts.grad, rtol, f"{tag} shape table")
-            close(models["embedding"].texture_embedding.weight.grad, tt.grad, rtol, f"{tag} texture table")
+        def grads_of(res):
+            _, pc, pf, ts, tt = res[:5]
+            out = {f"{key}.{name}": ref[name].grad for key, ref in (("nerf_coarse", pc), ("nerf_fine", pf))
+                   for name in ref}
+            out.update({"shape table": ts.grad, "texture table": tt.grad})
+            return out
 
-        # 1. fully independent: the oracle's own fine depths and ReLU decisions
+        got = {f"{key}.{name}": prm.grad for key in ("nerf_coarse", "nerf_fine")
+               for name, prm in models[key].named_parameters()}
+        got.update({"shape table": models["embedding"].shape_embedding.weight.grad,
+                    "texture table": models["embedding"].texture_embedding.weight.grad})
+
+        # 1. the oracle on its OWN decisions (fine depths, ReLU kinks): independent of the kernels
         pre_c, pre_f = {}, {}
         own = oracle_step(pre_c=pre_c, pre_f=pre_f)
-        compare(own, INDEPENDENT_RTOL, "independent")
-        # 2. the kernels' discrete decisions equal the oracle's up to their rounding: fine depths
-        #    (continuous in the cdf) within 1e-5, ReLU decisions inside the fp32 band
-        assert (seen["z_fine"] - own[5]).abs().max().item() <= 1e-5
+        assert abs(float(logs["total_loss"]) - own[0]) <= 1e-5
+        # 2. the kernels' discrete decisions are the reference's up to their rounding:
+        #    (a) coarse weights within 1e-5 of the oracle's, (b) sample_pdf of those weights is the
+        #    kernel's z_fine bit for bit, (c) every differing ReLU decision is inside the fp32 band
+        w_own, z_c = own[6], own[7]
+        assert (seen["w_coarse"] - w_own[..., 1:-1]).abs().max().item() <= 1e-5
+        assert torch.equal(o.sample_pdf(r, d, seen["w_coarse"], z_c, 16)[1], seen["z_fine"])
         n_dis = (check_mask_agreement(relu_masks(seen["saved"][0]), pre_c, MASK_BAND["f32"], "coarse")
                  + check_mask_agreement(relu_masks(seen["saved"][1]), pre_f, MASK_BAND["f32"], "fine"))
-        print(f"chunk {c0}: ReLU decisions differing from the oracle (all in-band): {n_dis}")
-        # 3. with those decisions fed back, the gradients match at GRAD_RTOL
-        compare(oracle_step(relu_masks(seen["saved"][0]), relu_masks(seen["saved"][1]), seen["z_fine"]), GRAD_RTOL,
-                "recorded decisions")
+        z_dis = int((seen["z_fine"] != own[5]).sum())
+        print(f"chunk {c0}: differing ReLU decisions (all in-band) {n_dis}, differing fine depths {z_dis}")
+        # 3. with exactly those decisions the oracle matches every gradient at GRAD_RTOL ...
+        fed = oracle_step(relu_masks(seen["saved"][0]), relu_masks(seen["saved"][1]), seen["z_fine"])
+        assert abs(float(logs["total_loss"]) - fed[0]) <= 1e-5
+        g_own, g_fed = grads_of(own), grads_of(fed)
+        for k in got:
+            close(got[k], g_fed[k], GRAD_RTOL, "recorded decisions " + k)
+            # ... so every deviation from the independent oracle is what the in-band kinks move
+            explained_by_kinks(got[k], g_own[k], g_fed[k], k)
+            if n_dis == 0 and z_dis == 0:
+                close(got[k], g_own[k], GRAD_RTOL, "independent " + k)
     assert float(opt.state[models["nerf_fine"].fc_rgb.weight]["step"]) == n // chunk
     assert sched.last_epoch == n // chunk
 
