@@ -48,7 +48,10 @@ CHUNK = 4096
 FLOP_PER_SAMPLE = 572_416          # hoisted CodeNeRF MLP per sample-evaluation
 PEAK_FP32_MFMA_TFLOPS = 157.3      # MI355X dense fp32 matrix peak (MI355X_MICROARCH.md)
 PEAK_BF16_MFMA_TFLOPS = 2516.6     # MI355X dense bf16 matrix peak (guide: ~2.5 PF dense)
-KERNELS = {"f32": ("field_kernel<kFromRayZ> (fused posenc + CodeNeRF MLP, fp32 MFMA)", 1, PEAK_FP32_MFMA_TFLOPS),
+KERNELS = {"f32": ("field_w16_kernel<kFromRayZ> (fused posenc + CodeNeRF MLP, fp32 v_mfma_f32_16x16x4_f32, "
+                    "2 waves/SIMD)", 1, PEAK_FP32_MFMA_TFLOPS),
+           "f32_v1": ("field_kernel<kFromRayZ> (fused posenc + CodeNeRF MLP, fp32 v_mfma_f32_32x32x2_f32, "
+                      "1 wave/SIMD)", 1, PEAK_FP32_MFMA_TFLOPS),
            "bf16x3": ("field_x3_kernel<kFromRayZ> (fused posenc + CodeNeRF MLP, 3xbf16 MFMA)", 3,
                       PEAK_BF16_MFMA_TFLOPS)}
 
@@ -263,6 +266,14 @@ def run(args):
                      "note": ("opt-in 3-product bf16 split (Wh.Xh + Wh.Xl + Wl.Xh, fp32 accumulate): narrower than "
                               "the reference's fp32; parity-tested at the same tolerances incl. trained-magnitude "
                               "weights (tests/test_gpu_configs.py)") if other == "bf16x3" else "reference precision"}
+    if args.precision == "f32":
+        # the previous fp32 kernel (32x32x2, one wave per SIMD; still the training forward)
+        set_precision("f32_v1")
+        dtv, fms_v, img_v = timed(args.steps, args.warmup, lambda rec: render_step(rec, True))
+        psnr_img["f32_v1"] = img_v
+        result["f32_v1"] = {"value": total_rays / dtv, "unit": "rays/s", "ms_per_step": dtv / args.steps * 1e3,
+                            "dtype": "f32", "roofline": roofline("f32_v1", fms_v),
+                            "note": "round-1 fp32 kernel, kept as the training forward (stores activations)"}
     set_precision(args.precision)
 
     if not args.no_extras:

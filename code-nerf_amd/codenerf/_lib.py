@@ -18,8 +18,18 @@ LIB_PATH = os.environ.get("CODENERF_LIB", os.path.join(_HERE, "lib", "libcodener
 
 CN_OK, CN_EINVAL, CN_EUNSUPPORTED = 0, -1, -2
 CN_NUM_PARAMS = 18
-CN_FMT_F32, CN_FMT_BF16X3, CN_FMT_BF16X3_T = 0, 1, 2
-FORMATS = {"f32": CN_FMT_F32, "bf16x3": CN_FMT_BF16X3, "bf16x3_t": CN_FMT_BF16X3_T}
+CN_FMT_F32, CN_FMT_BF16X3, CN_FMT_BF16X3_T, CN_FMT_F32_W16 = 0, 1, 2, 3
+FORMATS = {"f32": CN_FMT_F32, "bf16x3": CN_FMT_BF16X3, "bf16x3_t": CN_FMT_BF16X3_T, "f32_w16": CN_FMT_F32_W16}
+
+
+def kernel_format(precision: str) -> str:
+    """Packed format / field kernel that runs a precision: "f32" -> the 16x16x4 two-waves-per-SIMD
+    fp32 kernel ("f32_w16"; CODENERF_F32_KERNEL=v1 selects the 32x32x2 one), "bf16x3" -> itself."""
+    if precision == "f32":
+        return "f32" if os.environ.get("CODENERF_F32_KERNEL") == "v1" else "f32_w16"
+    if precision == "f32_v1":          # fp32, the 32x32x2 one-wave-per-SIMD kernel (mlp.hip)
+        return "f32"
+    return precision
 CN_CODE_BIAS_STRIDE = 520
 
 _p = ctypes.c_void_p

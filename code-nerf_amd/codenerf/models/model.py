@@ -73,13 +73,19 @@ class CodeNeRFModel(torch.nn.Module):
             out += [lin.weight, lin.bias]
         return out
 
+    def kernel_format(self) -> str:
+        """The packed format (= field kernel) of this model's inference precision."""
+        from .._lib import kernel_format
+        return kernel_format(self.precision)
+
     def packed(self) -> torch.Tensor:
         """MFMA-fragment layout of the weights, repacked whenever a parameter changed."""
         self._require_supported()
         params = self.param_list()
-        key = (self.precision,) + tuple((p.data_ptr(), p._version) for p in params)
+        fmt = self.kernel_format()
+        key = (fmt,) + tuple((p.data_ptr(), p._version) for p in params)
         if self._packed is None or self._packed_key != key:
-            self._packed = ops.mlp_pack(params, self.precision)
+            self._packed = ops.mlp_pack(params, fmt)
             self._packed_key = key
         return self._packed
 
@@ -95,7 +101,7 @@ class CodeNeRFModel(torch.nn.Module):
             return mlp_forward_autograd(self, z_s, z_t, x)
         codes_s, codes_t, index = _dedupe_codes(z_s, z_t)
         cb = ops.code_bias(self.param_list(), codes_s, codes_t)
-        return ops.mlp_forward(self.packed(), cb, x, index, precision=self.precision)
+        return ops.mlp_forward(self.packed(), cb, x, index, precision=self.kernel_format())
 
 
 def _dedupe_codes(z_s: torch.Tensor, z_t: torch.Tensor):

@@ -88,7 +88,7 @@ def _field(model, embedders, rd, z_s, z_t, chunk_rows, pts=None, ro=None, z=None
     cb = m.code_bias(cs, ct)
     n_samples = pts.shape[1] if pts is not None else z.shape[1]
     return ops.radiance_field(m.packed(), cb, rd, n_samples, chunk_rows, fx, fd, pts=pts, ro=ro, z=z,
-                              code_index=code_index, precision=m.precision)
+                              code_index=code_index, precision=m.kernel_format())
 
 
 def forward_pass(model, embedders, rd: torch.Tensor, pts: torch.Tensor,

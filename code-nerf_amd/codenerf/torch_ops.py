@@ -20,7 +20,7 @@ from typing import List, Optional, Tuple
 import torch
 from torch import Tensor
 
-from . import ops
+from . import _lib, ops
 
 _NS = "codenerf"
 
@@ -182,7 +182,8 @@ def _code_rows(z_s, z_t):
 def codenerf_mlp(z_s: Tensor, z_t: Tensor, x: Tensor, params: List[Tensor], precision: str = "f32") -> Tensor:
     """CodeNeRFModel.forward (model.py:160-194) on encoded rows; params in state_dict order."""
     cs, ct = _code_rows(z_s, z_t)
-    return ops.mlp_forward(ops.mlp_pack(params, precision), ops.code_bias(params, cs, ct), x, precision=precision)
+    fmt = _lib.kernel_format(precision)
+    return ops.mlp_forward(ops.mlp_pack(params, fmt), ops.code_bias(params, cs, ct), x, precision=fmt)
 
 
 @codenerf_mlp.register_fake
@@ -245,8 +246,11 @@ class _ParamModel:
     def param_list(self):
         return self._params
 
+    def kernel_format(self):
+        return _lib.kernel_format(self.precision)
+
     def packed(self):
-        return ops.mlp_pack(self._params, self.precision)
+        return ops.mlp_pack(self._params, self.kernel_format())
 
     def code_bias(self, z_s, z_t):
         return ops.code_bias(self._params, z_s, z_t)

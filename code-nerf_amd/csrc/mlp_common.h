@@ -121,6 +121,11 @@ int launch_field_x3(int mode, FieldArgs& a, hipStream_t st);
 int64_t mask_words_x3(int64_t m);
 int launch_field_x3_bwd(int mode, FieldArgs& a, hipStream_t st);
 
+// fp32 16x16x4 two-waves-per-SIMD variant (mlp_f32.hip): inference forward.
+int64_t packed_floats_w16();
+int launch_pack_w16(const Params& P, float* packed, hipStream_t st);
+int launch_field_w16(int mode, FieldArgs& a, hipStream_t st);
+
 // Pre-encoded rows: the same 2P+2 values gathered from x (base = column offset).
 template <int P, int T = 0>
 __device__ __forceinline__ void gather_pairs(const float* xr, int base, int h, float* out) {

@@ -1,0 +1,526 @@
+// fp32 field kernel, v2: the fused posenc + CodeNeRF MLP of mlp.hip (forward_pass,
+// view_synthesis/nerf/__init__.py:94-134 + CodeNeRFModel.forward, models/model.py:160-194)
+// on v_mfma_f32_16x16x4_f32 -- exact fp32 products and fp32 accumulation (an fmaf chain
+// per MFMA), the reference's arithmetic -- at TWO waves per SIMD.
+//
+// Why 16x16x4 and not 32x32x2.  Both run at the fp32 peak (64 FLOP/clk/SIMD), but a
+// 32-sample wave tile needs a 256-wide input AND a 256-wide output held in registers
+// (~300 VGPRs: one wave per SIMD).  A lone wave leaves the matrix pipe idle at every
+// barrier, LDS-read wait and layer epilogue.  A 16-sample tile holds the same two
+// 256-vectors in 64 + 64 registers, so two waves share each SIMD and one's MFMAs cover
+// the other's stalls.  Tile = 8 waves x 16 samples = 128 samples per workgroup.
+//
+// Register dataflow (as in mlp_layout.h, for the 16x16 shape).  D = W x X^T with
+// A = 16 rows of W (lane l: row l & 15, k-step input g = l >> 4), B = the samples'
+// inputs (lane l: sample l & 15, input g), D = 16 output features x 16 samples with
+// feature 4(l >> 4) + r in register r.  So accumulator block ob, register r is the next
+// layer's B operand for k-step 4ob + r: lane group g feeds input feature 16ob + 4g + r.
+// The pack applies that permutation to every W once; activations never leave registers.
+// The positional encodings are spread the same way: lane group g computes the sin/cos
+// of pairs p = 4i + g (7-8 sincosf per lane for xyz, 3 for the view direction).
+//
+// Weight stream.  Chunk = 8 k-steps x 16 output blocks x 64 lanes = 32 KiB, laid out
+// [k-step][block quad q][lane][block 4q..4q+3] so a lane's A values of one k-step are 4
+// ds_read_b128 of a 1 KiB contiguous run (conflict free).  36 chunks per tile
+// (xyz1 2 | xyz2 8 | fc_out 8 | dir1 8 + view-dir 1 | dir2 8 | rgb 1) stream through a
+// 4-slot LDS ring by LDS-DMA (buffer_load_dwordx4 ... lds; 4 wave-instructions per wave
+// per chunk).  One barrier M_c in the middle of chunk c: chunk c+1 has landed (counted
+// vmcnt) and every wave is done with chunk c-1, whose slot then receives chunk c+3.  The
+// first A fragments of chunk c+1 are read during chunk c's last k-step, so the matrix
+// pipe never waits on a chunk boundary.  The stream is cyclic across tiles.
+//
+// sigma (fc_out row 0) is an fp32 dot product over layer_xyz2's outputs taken in the
+// xyz2 epilogue (64 FMAs per lane + a 4-group butterfly); fc_rgb is one 16-row block
+// (rows 0..2 real) over 64 k-steps, accumulated in 4 interleaved chains.
+#include <algorithm>
+
+#include "mlp_common.h"
+
+namespace cn {
+namespace mlp {
+namespace w16 {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+constexpr int kWaves = 8;
+constexpr int kThreads = 64 * kWaves;
+constexpr int kTile = 16 * kWaves;            // samples per workgroup tile
+constexpr int kStepQuads = 16 * 64 / 4;       // one 16-block k-step: 256 float4 (4 KiB)
+constexpr int kChunkSteps = 8;
+constexpr int kChunkQuads = kChunkSteps * kStepQuads;   // 2048 float4 = 32 KiB
+constexpr int kRing = 4;
+constexpr int kPiecesPerWave = kChunkQuads / (64 * kWaves);   // 4 x 1 KiB per wave per chunk
+// the stream: xyz1 2 | xyz2 8 | fc_out 8 | dir1 8 | dir1 view-dir 1 | dir2 8 | rgb 1
+constexpr int kCL2 = 2, kCL3 = 10, kCL4 = 18, kCDir = 26, kCL5 = 27, kCRgb = 35, kChunks = 36;
+constexpr int kStreamFloats = kChunks * kChunkQuads * 4;
+// constants after the stream: b_xyz1 | b_dir1 | b_dir2 | sigma weights (fc_out row 0 over
+// h2, [g][ob][r] = W_out[0][16 ob + 4 g + r])
+constexpr int kCB1 = 0, kCBD1 = 256, kCBD2 = 512, kCSig = 768, kConsts = 1024;
+constexpr int kPackedFloats = kStreamFloats + kConsts;
+// LDS: the ring, the constants, one code-bias row per wave
+constexpr int kLdsQuads = kRing * kChunkQuads + (kConsts + kWaves * kCbStride) / 4;
+
+static_assert(kChunks % kRing == 0, "cyclic stream: chunk c + 36 reuses chunk c's ring slot");
+static_assert(kPiecesPerWave == 4, "4 DMA wave-instructions per chunk per wave");
+static_assert(kLdsQuads * 16 <= 160 * 1024, "LDS budget");
+
+// ---------------------------------------------------------------- feature maps
+
+// Input feature (256-wide previous-layer output) fed at k-step t by lane group g.
+__host__ __device__ constexpr int col_acc(int t, int g) { return 16 * (t >> 2) + 4 * g + (t & 3); }
+
+// xyz encoding column (position_embed.py:44-53: x_d -> d, sin(f_k x_d) -> 3+6k+d,
+// cos(f_k x_d) -> 6+6k+d) fed at k-step t (0..15) by lane group g: sines of pairs
+// p = 4i + g at t = i, cosines at t = 8 + i; groups 2, 3 have 7 pairs and put the raw
+// inputs in the free k-steps 7 / 15 (x0, x1 | x2, pad).
+__host__ __device__ constexpr int col_enc_xyz(int t, int g) {
+  const int i = t & 7, p = 4 * i + g;
+  if (p < 30) return (t < 8 ? 3 : 6) + 6 * (p / 3) + p % 3;
+  return t < 8 ? (g == 2 ? 0 : 2) : (g == 2 ? 1 : -1);
+}
+
+// View-direction encoding column (27 wide) at k-step s (0..6) of the view-dir chunk:
+// sines of pairs p = 4i + g at s = i (i < 3), cosines at s = 3 + i, raw component g at s = 6.
+__host__ __device__ constexpr int col_enc_dir(int s, int g) {
+  if (s < 6) {
+    const int p = 4 * (s % 3) + g;
+    return (s < 3 ? 3 : 6) + 6 * (p / 3) + p % 3;
+  }
+  return (s == 6 && g < 3) ? g : -1;
+}
+
+// ---------------------------------------------------------------- packing
+
+__global__ void pack_w16_kernel(Params P, float* __restrict__ packed) {
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < kPackedFloats; idx += gridDim.x * blockDim.x) {
+    float v = 0.0f;
+    if (idx >= kStreamFloats) {
+      const int j = idx - kStreamFloats;
+      if (j < 256) v = P.p[kBXyz1][j];
+      else if (j < 512) v = P.p[kBDir1][j - 256];
+      else if (j < 768) v = P.p[kBDir2][j - 512];
+      else {
+        const int t = j - kCSig, g = t >> 6, ob = (t >> 2) & 15, r = t & 3;
+        v = P.p[kWOut][16 * ob + 4 * g + r];  // fc_out row 0, input feature 16 ob + 4 g + r of h2
+      }
+    } else {
+      const int c = idx / (kChunkQuads * 4), rem = idx % (kChunkQuads * 4);
+      if (c == kCRgb) {
+        // fc_rgb: 64 k-steps of block 0, [k-step quad][lane][k-step & 3]
+        if (rem < 64 * 64) {
+          const int lane = (rem % 256) / 4, t = 4 * (rem / 256) + rem % 4;
+          const int i = lane & 15, g = lane >> 4;
+          if (i < 3) v = P.p[kWRgb][i * (kHidden + kCode) + col_acc(t, g)];
+        }
+      } else {
+        const int s = rem / (kStepQuads * 4), q = (rem % (kStepQuads * 4)) / 256;
+        const int lane = (rem % 256) / 4, ob = 4 * q + rem % 4;
+        const int i = lane & 15, g = lane >> 4;
+        int row = 16 * ob + i, col = -1, in_dim = 0;
+        const float* W = nullptr;
+        if (c < kCL2) { W = P.p[kWXyz1]; in_dim = kDimXyz; col = col_enc_xyz(8 * c + s, g); }
+        else if (c < kCL3) { W = P.p[kWXyz2]; in_dim = kHidden + kCode; col = col_acc(8 * (c - kCL2) + s, g); }
+        else if (c < kCL4) { W = P.p[kWOut]; in_dim = kHidden + kCode; row += 1; col = col_acc(8 * (c - kCL3) + s, g); }
+        else if (c < kCDir) { W = P.p[kWDir1]; in_dim = kCode + kDimDir; col = col_acc(8 * (c - kCL4) + s, g); }
+        else if (c == kCDir) {
+          W = P.p[kWDir1]; in_dim = kCode + kDimDir;
+          const int e = col_enc_dir(s, g);
+          col = e < 0 ? -1 : kCode + e;
+        } else { W = P.p[kWDir2]; in_dim = kHidden; col = col_acc(8 * (c - kCL5) + s, g); }
+        if (col >= 0) v = W[row * in_dim + col];
+      }
+    }
+    packed[idx] = v;
+  }
+}
+
+// ---------------------------------------------------------------- kernel state
+
+struct State {
+  floatx4 act[16];   // layer input: block ob register r = input feature 16 ob + 4 g + r
+  floatx4 acc[16];   // layer output accumulators
+  floatx4 pre[4];    // the next chunk's first A fragments (read during this chunk's last k-step)
+  float denc[8];     // view-direction encoding, k-steps of the view-dir chunk
+  float sig;         // sigma partial (this lane group's 64 features)
+  int lane, g, wave;
+  int crow;          // this lane's code-bias row
+  bool uniform_code; // all 16 samples of the wave use one code row
+  __amdgpu_buffer_rsrc_t wsrc;
+  unsigned voff;
+};
+
+
+// One LDS-DMA piece: 1 KiB of chunk cn (piece p of 4 for this wave).
+__device__ __forceinline__ void dma_piece(const State& s, float4* lds, int cn, int p) {
+  const int src = cn < kChunks ? cn : cn - kChunks;
+  const unsigned soff = __builtin_amdgcn_readfirstlane((unsigned)(src * kChunkQuads + p * 64 * kWaves) * 16u);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(
+      s.wsrc, (lds_ptr_t)(lds + (cn & (kRing - 1)) * kChunkQuads + p * 64 * kWaves + s.wave * 64), 16, s.voff,
+      soff, 0, 0);
+}
+
+__device__ __forceinline__ void dma_chunk(const State& s, float4* lds, int cn) {
+#pragma unroll
+  for (int p = 0; p < kPiecesPerWave; ++p) dma_piece(s, lds, cn, p);
+}
+
+// M_c: chunk c+1 landed for every wave (all but this wave's 4 youngest DMA pieces --
+// chunk c+2's -- retired), every wave past chunk c-1, this wave's LDS reads returned.
+__device__ __forceinline__ void chunk_barrier() {
+  asm volatile("s_waitcnt vmcnt(4)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// A fragments of k-step T (16 blocks) of the chunk at `slot` (float4 units, lane applied).
+template <int T>
+__device__ __forceinline__ void read_a(const float4* slot, floatx4* a) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) a[q] = *reinterpret_cast<const floatx4*>(slot + T * kStepQuads + q * 64);
+}
+
+__device__ __forceinline__ void mfma_step(State& s, const floatx4* a, float b) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      s.acc[4 * q + j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q][j], b, s.acc[4 * q + j], 0, 0, 0);
+}
+
+// Scheduling of one k-step: the 4 A reads of the next k-step between the first MFMAs.
+__device__ __forceinline__ void step_pattern() {
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+  }
+  __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
+}
+
+// One 16-block chunk of NS k-steps; the B operand of k-step T is getb(T) (compile time).
+// The last k-step reads the next chunk's first fragments into s.pre.
+template <int NS, typename GetB>
+__device__ __forceinline__ void chunk16(State& s, float4* lds, int c, GetB getb) {
+  const float4* slot = lds + (c & (kRing - 1)) * kChunkQuads + s.lane;
+  const float4* nslot = lds + ((c + 1) & (kRing - 1)) * kChunkQuads + s.lane;
+  floatx4 a0[4], a1[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) a0[q] = s.pre[q];
+  __builtin_amdgcn_sched_barrier(0);
+#define CN_STEP(T, CUR, NXT)                                         \
+  if constexpr ((T) < NS) {                                         \
+    if constexpr ((T) + 1 < NS) read_a<(T) + 1>(slot, NXT);         \
+    else read_a<0>(nslot, s.pre);                                   \
+    mfma_step(s, CUR, getb.template at<(T)>());                     \
+    step_pattern();                                                 \
+    __builtin_amdgcn_sched_barrier(0);                              \
+    if constexpr ((T) == 3) {                                       \
+      chunk_barrier();                                              \
+      dma_chunk(s, lds, c + 3);                                     \
+    }                                                               \
+  }
+  CN_STEP(0, a0, a1)
+  CN_STEP(1, a1, a0)
+  CN_STEP(2, a0, a1)
+  CN_STEP(3, a1, a0)
+  CN_STEP(4, a0, a1)
+  CN_STEP(5, a1, a0)
+  CN_STEP(6, a0, a1)
+  CN_STEP(7, a1, a0)
+#undef CN_STEP
+}
+
+// B sources
+template <int K0>
+struct ActB {
+  const State& s;
+  template <int T>
+  __device__ __forceinline__ float at() const {
+    constexpr int t = K0 + T;
+    return s.act[t >> 2][t & 3];
+  }
+};
+template <int K0>
+struct ArrB {
+  const float* v;
+  template <int T>
+  __device__ __forceinline__ float at() const { return v[K0 + T]; }
+};
+
+// A 256-input layer: 8 chunks, B from s.act.
+__device__ __forceinline__ void layer256(State& s, float4* lds, int& c) {
+  chunk16<8>(s, lds, c + 0, ActB<0>{s});
+  chunk16<8>(s, lds, c + 1, ActB<8>{s});
+  chunk16<8>(s, lds, c + 2, ActB<16>{s});
+  chunk16<8>(s, lds, c + 3, ActB<24>{s});
+  chunk16<8>(s, lds, c + 4, ActB<32>{s});
+  chunk16<8>(s, lds, c + 5, ActB<40>{s});
+  chunk16<8>(s, lds, c + 6, ActB<48>{s});
+  chunk16<8>(s, lds, c + 7, ActB<56>{s});
+  c += 8;
+}
+
+// Bias-initialise the 16 accumulators from a 256-vector (row 16 ob + 4 g + r).
+__device__ __forceinline__ void bias_from(State& s, const float* v) {
+#pragma unroll
+  for (int ob = 0; ob < 16; ++ob) s.acc[ob] = *reinterpret_cast<const floatx4*>(v + 16 * ob + 4 * s.g);
+}
+
+// The code-bias vector at `off` of this lane's code row: the wave's LDS copy, or (codes
+// varying inside the wave) a per-lane global read.
+__device__ __forceinline__ void bias_code(State& s, const FieldArgs& a, const float* crow_lds, int off) {
+  if (s.uniform_code) {
+    bias_from(s, crow_lds + off);
+  } else {
+    bias_from(s, a.code_bias + (int64_t)s.crow * kCbStride + off);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): nothing ordinary stays in flight in the stream
+  }
+}
+
+template <int MODE>
+__device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4* lds, float* clds, float* crow_lds,
+                                          int64_t tile, int& c) {
+  const int64_t row = tile * kTile + s.wave * 16 + (s.lane & 15);
+  const bool valid = row < a.m;
+  const int64_t rc = valid ? row : a.m - 1;
+
+  // ---- per-sample inputs, code row (ordinary loads: the in-flight DMA retires with them)
+  const SampleIn in = decode_sample<MODE>(a, rc);
+  s.crow = static_cast<int>(code_row(a, in.code_of));
+  const int crow0 = __builtin_amdgcn_readfirstlane(s.crow);
+  s.uniform_code = __builtin_amdgcn_readfirstlane(__ballot(s.crow != crow0) == 0 ? 1 : 0) != 0;
+  float cbr[9];
+  {
+    const float* src = a.code_bias + (int64_t)crow0 * kCbStride;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const int j = s.lane + 64 * k;
+      cbr[k] = j < kCbStride ? src[j] : 0.0f;
+    }
+  }
+  float enc[16];
+  if constexpr (MODE == kFromEncoded) {
+    const float* xr = a.x + rc * (kDimXyz + kDimDir);
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int col = col_enc_xyz(t, s.g);
+      enc[t] = col >= 0 ? xr[col] : 0.0f;
+    }
+#pragma unroll
+    for (int t = 0; t < 7; ++t) {
+      const int col = col_enc_dir(t, s.g);
+      s.denc[t] = col >= 0 ? xr[kDimXyz + col] : 0.0f;
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const int j = s.lane + 64 * k;
+    if (j < kCbStride) crow_lds[j] = cbr[k];
+  }
+
+  // ---- encodings: lane group g owns pairs p = 4 i + g
+  if constexpr (MODE != kFromEncoded) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int p = 4 * i + s.g;
+      const int pc = p < 30 ? p : 0;
+      const float arg = __fmul_rn(in.x[pc % 3], a.fx[pc / 3]);
+      float sn, cs;
+      sincosf(arg, &sn, &cs);
+      if (i == 7 && p >= 30) {  // groups 2, 3: raw inputs
+        sn = s.g == 2 ? in.x[0] : in.x[2];
+        cs = s.g == 2 ? in.x[1] : 0.0f;
+      }
+      enc[i] = sn;
+      enc[8 + i] = cs;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int p = 4 * i + s.g;
+      const float arg = __fmul_rn(in.vd[p % 3], a.fd[p / 3]);
+      sincosf(arg, &s.denc[i], &s.denc[3 + i]);
+    }
+    s.denc[6] = s.g == 0 ? in.vd[0] : (s.g == 1 ? in.vd[1] : (s.g == 2 ? in.vd[2] : 0.0f));
+  }
+  s.denc[7] = 0.0f;
+
+  // ---- layer_xyz1 (63 -> 256): 2 chunks of encoding k-steps
+  bias_from(s, clds + kCB1);
+  chunk16<8>(s, lds, c + 0, ArrB<0>{enc});
+  chunk16<8>(s, lds, c + 1, ArrB<8>{enc});
+  c += 2;
+
+  // ---- layer_xyz2, fc_out, layer_dir1 (+ view-dir chunk), layer_dir2
+  for (int layer = kXyz2; layer <= kDir2; ++layer) {
+    // activation of the previous layer's outputs: ReLU, none after fc_out (feat)
+    if (layer == kDir1) {
+#pragma unroll
+      for (int ob = 0; ob < 16; ++ob) s.act[ob] = s.acc[ob];
+    } else {
+#pragma unroll
+      for (int ob = 0; ob < 16; ++ob)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s.act[ob][r] = fmaxf(s.acc[ob][r], 0.0f);
+    }
+    if (layer == kOut) {
+      // sigma = fc_out row 0 . [h2, zs2] + b: the h2 part here, the code part from cn_code_bias
+      float sg = 0.0f;
+#pragma unroll
+      for (int ob = 0; ob < 16; ++ob) {
+        const floatx4 w = *reinterpret_cast<const floatx4*>(clds + kCSig + 64 * s.g + 4 * ob);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sg = fmaf(w[r], s.act[ob][r], sg);
+      }
+      s.sig = sg;
+    }
+    if (layer == kXyz2) bias_code(s, a, crow_lds, kCbXyz2);
+    else if (layer == kOut) bias_code(s, a, crow_lds, kCbFeat);
+    else bias_from(s, clds + (layer == kDir1 ? kCBD1 : kCBD2));
+    __builtin_amdgcn_sched_barrier(0);
+    layer256(s, lds, c);
+    if (layer == kDir1) {
+      chunk16<7>(s, lds, c, ArrB<0>{s.denc});
+      c += 1;
+    }
+  }
+
+  // ---- fc_rgb (256 -> 3): one chunk, 64 k-steps of block 0 in 4 chains
+#pragma unroll
+  for (int ob = 0; ob < 16; ++ob)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s.act[ob][r] = fmaxf(s.acc[ob][r], 0.0f);
+  {
+    float b0 = 0.0f, b1 = 0.0f, b2 = 0.0f, bs = 0.0f;
+    if (s.uniform_code) {
+      b0 = crow_lds[kCbRgb];
+      b1 = crow_lds[kCbRgb + 1];
+      b2 = crow_lds[kCbRgb + 2];
+      bs = crow_lds[kCbSigma];
+    } else {
+      const float* cb = a.code_bias + (int64_t)s.crow * kCbStride;
+      b0 = cb[kCbRgb];
+      b1 = cb[kCbRgb + 1];
+      b2 = cb[kCbRgb + 2];
+      bs = cb[kCbSigma];
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+    }
+    // lane group 0 holds output rows 0..3 (registers 0..3) of block 0
+    s.acc[0] = s.g == 0 ? floatx4{b0, b1, b2, 0.0f} : floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+    s.acc[1] = s.acc[2] = s.acc[3] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+    float sg = s.sig;
+    sg += __shfl_xor(sg, 16);
+    sg += __shfl_xor(sg, 32);
+    s.sig = sg + bs;
+  }
+  {
+    const float4* slot = lds + (c & (kRing - 1)) * kChunkQuads + s.lane;
+    const float4* nslot = lds + ((c + 1) & (kRing - 1)) * kChunkQuads + s.lane;
+    floatx4 a0[4], a1[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) a0[q] = s.pre[q];
+    // k-step quads 0..3 arrived in s.pre; quads 4q'..4q'+3 are read one group ahead
+#define CN_RGB(G, CUR, NXT)                                                              \
+  {                                                                                      \
+    if constexpr ((G) < 3) {                                                             \
+      _Pragma("unroll") for (int q = 0; q < 4; ++q) NXT[q] = *reinterpret_cast<const floatx4*>(slot + (4 * ((G) + 1) + q) * 64); \
+    } else {                                                                             \
+      read_a<0>(nslot, s.pre);                                                           \
+    }                                                                                    \
+    _Pragma("unroll") for (int q = 0; q < 4; ++q)                                        \
+    _Pragma("unroll") for (int j = 0; j < 4; ++j) {                                      \
+      s.acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(CUR[q][j], s.act[4 * (G) + q][j], s.acc[j], 0, 0, 0); \
+    }                                                                                    \
+    step_pattern();                                                                      \
+    __builtin_amdgcn_sched_barrier(0);                                                   \
+    if constexpr ((G) == 1) {                                                            \
+      chunk_barrier();                                                                   \
+      dma_chunk(s, lds, c + 3);                                                          \
+    }                                                                                    \
+  }
+    CN_RGB(0, a0, a1)
+    CN_RGB(1, a1, a0)
+    CN_RGB(2, a0, a1)
+    CN_RGB(3, a1, a0)
+#undef CN_RGB
+    c += 1;
+  }
+  if (valid && s.g == 0) {
+    const floatx4 r = (s.acc[0] + s.acc[1]) + (s.acc[2] + s.acc[3]);
+    float4 o;
+    o.x = r[0];
+    o.y = r[1];
+    o.z = r[2];
+    o.w = s.sig;
+    reinterpret_cast<float4*>(a.raw)[row] = o;
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kThreads, 2) void field_w16_kernel(FieldArgs a) {
+  // ONE LDS object (a second one makes hipcc wait vmcnt(0) before ring reads): the DMA
+  // ring, then the constants, then one code-bias row per wave
+  __shared__ __attribute__((aligned(16))) float4 lds[kLdsQuads];
+  float* clds = reinterpret_cast<float*>(lds + kRing * kChunkQuads);
+  State s;
+  s.lane = threadIdx.x & 63;
+  s.g = s.lane >> 4;
+  s.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  s.wsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.packed), 0, kPackedFloats * 4, 0x00020000);
+  s.voff = static_cast<unsigned>(s.wave * 64 + s.lane) * 16u;
+  s.sig = 0.0f;
+  float* crow_lds = clds + kConsts + s.wave * kCbStride;
+
+  for (int k = threadIdx.x; k < kConsts; k += kThreads) clds[k] = a.packed[kStreamFloats + k];
+  // prime the ring with chunks 0..2, wait for chunk 0 everywhere, read its first fragments
+  dma_chunk(s, lds, 0);
+  dma_chunk(s, lds, 1);
+  dma_chunk(s, lds, 2);
+  asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  read_a<0>(lds + s.lane, s.pre);
+
+  const int64_t n_tiles = (a.m + kTile - 1) / kTile;
+  int c = 0;
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    c = 0;
+    field_tile<MODE>(s, a, lds, clds, crow_lds, tile, c);
+  }
+  // the last tile prefetched chunks 0..2 of a tile that does not exist: they must land
+  // before the workgroup's LDS is released
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+}
+
+}  // namespace w16
+
+static int64_t cu_count_w16() {
+  static int n[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (n[dev] == 0) {
+    int v = 0;
+    n[dev] = (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ? v : 256;
+  }
+  return n[dev];
+}
+
+int64_t packed_floats_w16() { return w16::kPackedFloats; }
+
+int launch_pack_w16(const Params& P, float* packed, hipStream_t st) {
+  hipLaunchKernelGGL(w16::pack_w16_kernel, dim3(cn::elementwise_grid(w16::kPackedFloats, 256)), dim3(256), 0, st, P,
+                     packed);
+  return cn::launch_status();
+}
+
+int launch_field_w16(int mode, FieldArgs& a, hipStream_t st) {
+  const unsigned grid = static_cast<unsigned>(std::min<int64_t>(cn::ceil_div(a.m, w16::kTile), cu_count_w16()));
+  switch (mode) {
+    case kFromPts: hipLaunchKernelGGL(w16::field_w16_kernel<kFromPts>, dim3(grid), dim3(w16::kThreads), 0, st, a); break;
+    case kFromRayZ: hipLaunchKernelGGL(w16::field_w16_kernel<kFromRayZ>, dim3(grid), dim3(w16::kThreads), 0, st, a); break;
+    default: hipLaunchKernelGGL(w16::field_w16_kernel<kFromEncoded>, dim3(grid), dim3(w16::kThreads), 0, st, a); break;
+  }
+  return cn::launch_status();
+}
+
+}  // namespace mlp
+}  // namespace cn

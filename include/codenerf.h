@@ -53,6 +53,10 @@ typedef void* cn_stream_t; /* hipStream_t */
 /*   CN_FMT_BF16X3_T  the transposed 3xbf16 pack the fused backward streams
  *                    (cn_field_backward_x3); not a forward format. */
 #define CN_FMT_BF16X3_T 2
+/*   CN_FMT_F32_W16   fp32 fragments for v_mfma_f32_16x16x4_f32 at two waves per SIMD
+ *                    (the inference kernel of precision "f32"; exact f32 products as
+ *                    CN_FMT_F32, whose kernel remains the training forward). */
+#define CN_FMT_F32_W16 3
 
 const char* cn_version(void);
 const char* cn_error_string(int code);

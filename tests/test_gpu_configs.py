@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
 
 TOL_RENDER = 1e-4
 RAW_RTOL = 1e-5
-PRECISIONS = ["f32", "bf16x3"]
+PRECISIONS = ["f32", "f32_v1", "bf16x3"]
 
 
 def model_from(dev, params, precision):

@@ -40,9 +40,11 @@ def maxdiff(a, b):
     return (a - b).abs().max().item() if a.numel() else 0.0
 
 
-@pytest.fixture(params=["f32", "bf16x3"])
+@pytest.fixture(params=["f32", "f32_v1", "bf16x3"])
 def precision(request):
-    """Both field-kernel formats are held to the same tolerances."""
+    """Every field kernel is held to the same tolerances: fp32 on 16x16x4 MFMA (two waves per
+    SIMD, the default), fp32 on 32x32x2 MFMA (one wave per SIMD, also the training forward) and
+    the opt-in 3xbf16 split."""
     return request.param
 
 
