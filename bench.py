@@ -70,7 +70,7 @@ def pose(theta, phi, rho):
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--images-per-step", type=int, default=16,
                     help="views of the car rendered per rank per step (16 x 16384 rays: ~90 ms of fp32 work)")

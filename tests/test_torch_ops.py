@@ -87,8 +87,13 @@ def test_mlp_ops(dev):
     x = torch.randn(300, 90, generator=g).to(dev)
     zs, zt = (torch.randn(1, 256, generator=g) * 0.3).to(dev), (torch.randn(1, 256, generator=g) * 0.3).to(dev)
     raw = torch.ops.codenerf.codenerf_mlp(zs.expand(300, -1), zt.expand(300, -1), x, p, "f32")
-    ref = ops.mlp_forward(ops.mlp_pack(p, "f32"), ops.code_bias(p, zs, zt), x)
-    assert torch.equal(raw, ref)
+    # precision "f32" runs the 16x16x4 two-waves-per-SIMD kernel (format f32_w16); the training
+    # forward (codenerf_mlp_train) is the 32x32x2 kernel: same fp32 products, other summation order
+    cb = ops.code_bias(p, zs, zt)
+    ref_w16 = ops.mlp_forward(ops.mlp_pack(p, "f32_w16"), cb, x, precision="f32_w16")
+    assert torch.equal(raw, ref_w16)
+    ref = ops.mlp_forward(ops.mlp_pack(p, "f32"), cb, x)
+    assert (ref_w16 - ref).abs().max().item() <= 1e-5
     pr = [t.clone().requires_grad_(True) for t in p]
     xg, zsg = x.clone().requires_grad_(True), zs.clone().requires_grad_(True)
     raw_t, _ = torch.ops.codenerf.codenerf_mlp_train(zsg, zt, xg, pr)
