@@ -45,6 +45,11 @@ SIGNATURES = {
     "cn_ray_directions": (_i, [_i64, _i64, _f, _f, _f, _p, _p]),
     "cn_ray_bundle": (_i, [_p, _i64, _p, _i64, _p, _p, _p]),
     "cn_gather_rays": (_i, [_p, _p, _i64, _i64, _p, _i64, _p, _p, _p]),
+    "cn_pose_rays": (_i, [_p, _p, _p, _p, _i64, _p, _i64, _p, _i64, _p, _i64, _p, _p, _p, _p, _p]),
+    "cn_pose_rays_backward": (_i, [_p, _p, _p, _i64, _p, _i64, _p, _i64, _p, _p, _p, _p, _p, _p, _p]),
+    "cn_random_select": (_i, [_i64, _i64, _i64, ctypes.c_uint64, ctypes.c_uint64, _p, _p]),
+    "cn_pose_error": (_i, [_p, _p, _i64, _p, _p, _p]),
+    "cn_srn_unpack": (_i, [_p, _i64, _i64, _i64, _p, _i64, _p, _p, _p]),
     "cn_sample_uniform": (_i, [_p, _p, _i64, _p, _p, _p, _i64, _p, _p, _p, _p]),
     "cn_ray_points": (_i, [_p, _p, _p, _i64, _i64, _p, _p]),
     "cn_sample_pdf": (_i, [_p, _p, _p, _i64, _p, _i64, _i64, _i64, _p, _i64, _p, _p, _p]),
@@ -78,6 +83,8 @@ SIGNATURES = {
     "cn_gemm_tn": (_i, [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _p]),
     "cn_gemm_nn_x3": (_i, [_p, _i64, _p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _p]),
     "cn_gemm_tn_x3": (_i, [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _p]),
+    "cn_render_loss": (_i, [_p, _p, _p, _i64, _i64, _p, _p, _i64, _i64, _f, _p, _p]),
+    "cn_render_loss_backward": (_i, [_p, _p, _p, _i64, _i64, _p, _p, _i64, _i64, _f, _p, _p, _p, _p, _p, _p, _p]),
     "cn_adamw_step": (_i, [_p, _p, _p, _p, _i64, ctypes.POINTER(_i64), ctypes.POINTER(_i64),
                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i64),
                            ctypes.c_double, ctypes.c_double, ctypes.c_double, _p]),

@@ -72,6 +72,44 @@ class GatherRays(torch.autograd.Function):
         return d_ro.view(ctx.shape), d_rd.view(ctx.shape), None
 
 
+class PoseRays(torch.autograd.Function):
+    """pose_spherical (eval.py:22-38) + sample (ray_sampler.py:53-99) + target gather (eval.py:147-148),
+    one launch each way.  The pose is (theta, phi, rho) -- gradients through the analytic d c2w --
+    or a c2w (B, 4, 4) -- gradient d c2w, as get_bundle + gather's autograd."""
+
+    @staticmethod
+    def forward(ctx, dirs, theta, phi, rho, c2w, sel, target):
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(dirs, theta, phi, rho, sel)
+        ctx.angles = theta is not None
+        ctx.shapes = (theta.shape, phi.shape, rho.shape) if ctx.angles else None
+        ctx.batch = theta.numel() if ctx.angles else c2w.shape[0]
+        ro, rd, c2w_out, tgt = ops.pose_rays(dirs, theta, phi, rho, c2w=c2w, select_inds=sel, target=target)
+        ctx.mark_non_differentiable(c2w_out)
+        if tgt is not None:
+            ctx.mark_non_differentiable(tgt)
+        return ro, rd, c2w_out, tgt
+
+    @staticmethod
+    def backward(ctx, g_ro, g_rd, _g_c2w, _g_tgt):
+        none = [None] * 7
+        if g_ro is None and g_rd is None:
+            return tuple(none)
+        dirs, theta, phi, rho, sel = ctx.saved_tensors
+        want_c2w = ctx.needs_input_grad[4]
+        if ctx.angles and not any(ctx.needs_input_grad[1:4]):
+            return tuple(none)
+        if not ctx.angles and not want_c2w:
+            return tuple(none)
+        (dt, dp, dr), d_c2w = ops.pose_rays_backward(dirs, ctx.batch, _c(g_ro), _c(g_rd), theta, phi, rho,
+                                                     select_inds=sel, want_c2w=want_c2w)
+        if ctx.angles:
+            for i, (g, sh) in enumerate(zip((dt, dp, dr), ctx.shapes)):
+                none[1 + i] = g.view(sh) if ctx.needs_input_grad[1 + i] else None
+        none[4] = d_c2w
+        return tuple(none)
+
+
 class SamplePoints(torch.autograd.Function):
     """pts = ro + rd * z with z detached (point_sampler.py:70, :115-118)."""
 
@@ -243,6 +281,42 @@ class MLPForward(torch.autograd.Function):
         return (None, r.get("d_x"), dz_s, dz_t, *grads)
 
 
+# ------------------------------------------------------------------ loss
+
+
+class RenderLoss(torch.autograd.Function):
+    """The step's loss (train.py:103-108, eval.py:157-163) -> total (scalar) and the (6,) stats
+    [coarse, fine, regulariser, total, ||z_s||, ||z_t||] (not differentiable)."""
+
+    @staticmethod
+    def forward(ctx, rgb_c, rgb_f, target, z_s, z_t, expand, lam):
+        ctx.set_materialize_grads(False)
+        stats = ops.render_loss(rgb_c, rgb_f, target, z_s, z_t, expand, lam)
+        ctx.save_for_backward(rgb_c, rgb_f, target, z_s, z_t, stats)
+        ctx.expand, ctx.lam = expand, lam
+        ctx.mark_non_differentiable(stats)
+        return stats[3], stats
+
+    @staticmethod
+    def backward(ctx, g_total, _g_stats):
+        if g_total is None:
+            return (None,) * 7
+        rgb_c, rgb_f, target, z_s, z_t, stats = ctx.saved_tensors
+        want = ctx.needs_input_grad[:2] + ctx.needs_input_grad[3:5]
+        d = ops.render_loss_backward(rgb_c, rgb_f, target, z_s, z_t, ctx.expand, ctx.lam, stats,
+                                     g_total.reshape(1).contiguous(), want)
+        return d[0], d[1], None, d[2], d[3], None, None
+
+
+def render_loss_autograd(rgb_c, rgb_f, target, z_s=None, z_t=None, expand: int = 1, lam: float = 0.0):
+    """-> (total loss, stats (6,)).  The regulariser is differentiated only where z_s / z_t require grad."""
+    tgt = target.detach()
+    if not _needs_grad(rgb_c, rgb_f, z_s, z_t):
+        stats = ops.render_loss(_d(rgb_c), _d(rgb_f), tgt, _d(z_s), _d(z_t), expand, lam)
+        return stats[3], stats
+    return RenderLoss.apply(rgb_c, rgb_f, tgt, z_s, z_t, expand, lam)
+
+
 # ------------------------------------------------------------------ entry points used by the package
 
 
@@ -250,6 +324,14 @@ def ray_bundle_autograd(dirs, c2w):
     if not _needs_grad(c2w):
         return ops.ray_bundle(dirs, c2w.detach())
     return RayBundle.apply(dirs.detach(), c2w)
+
+
+def pose_rays_autograd(dirs, theta=None, phi=None, rho=None, c2w=None, sel=None, target=None):
+    """(theta, phi, rho) or c2w -> ro, rd (B*S, 3), c2w (B, 4, 4), target rows (B*S, C) | None."""
+    tgt = None if target is None else target.detach()
+    if not _needs_grad(theta, phi, rho, c2w):
+        return ops.pose_rays(dirs, _d(theta), _d(phi), _d(rho), c2w=_d(c2w), select_inds=sel, target=tgt)
+    return PoseRays.apply(dirs.detach(), theta, phi, rho, c2w, sel, tgt)
 
 
 def gather_rays_autograd(ro, rd, sel):

@@ -1,24 +1,31 @@
-"""Test-time optimisation of pose + latent codes (eval.py:22-38, :41-205) on the gfx950 kernels.
+"""Test-time optimisation of pose + latent codes and the validation render (eval.py:22-38, :82-205)
+on the gfx950 kernels.
 
-The reference's eval loop renders a random ray batch from the current pose
-estimate, takes the MSE against the target pixels plus a code regulariser,
-and steps an optimiser over (z_s, z_t, theta, phi, rho).  Here every stage of
-that step -- ray bundle, gather, sampling, the fused field, compositing and
-all of their backwards -- runs on the HIP kernels (codenerf.autograd); torch
-supplies the 4x4 pose algebra, the scalar losses and the optimiser.
+The reference's eval loop renders a random ray batch from the current pose estimate, takes
+the MSE against the target pixels plus a code regulariser, and steps an optimiser over
+(z_s, z_t, theta, phi, rho); after the last iteration it renders the whole view from the
+optimised pose with ``parallel_image_render`` and reports its PSNR.  Here one eval
+iteration is: the fused pose path (``RaySampler.sample_spherical``: pose_spherical +
+sample + target gather, one launch; its backward one more), the hierarchical render and its
+backward on the HIP kernels (codenerf.autograd), the fused loss (cn_render_loss, one
+launch each way), the pose metric (cn_pose_error) and, for ``val_type: AdamW``, the flat
+one-launch AdamW (codenerf.optim).  torch only routes the tensors.
 """
 from __future__ import annotations
 
 from typing import Dict, Optional, Tuple
 
 import torch
+import torch.distributed as dist
 
-from . import nerf
+from . import nerf, ops
 from .utils import mse2psnr
 
 
 def pose_spherical(theta: torch.Tensor, phi: torch.Tensor, rho: torch.Tensor) -> torch.Tensor:
-    """eval.py:22-38: camera on a sphere of radius rho looking at the origin -> (4, 4) c2w."""
+    """eval.py:22-38: camera on a sphere of radius rho looking at the origin -> (4, 4) c2w.
+    (Host-side helper with the reference's torch ops; the eval step itself builds the pose inside
+    cn_pose_rays.)"""
     c2w = torch.eye(n=4, device=theta.device)
     st, ct, sp, cp = torch.sin(theta), torch.cos(theta), torch.sin(phi), torch.cos(phi)
     c2w[0, 0], c2w[1, 0] = -sp, cp
@@ -29,40 +36,60 @@ def pose_spherical(theta: torch.Tensor, phi: torch.Tensor, rho: torch.Tensor) ->
 
 
 def eval_step_loss(theta, phi, rho, shape_code, texture_code, target_pixels, samplers, embedders, models,
-                   regularizer_lambda: float) -> Tuple[torch.Tensor, Dict[str, float]]:
-    """One iteration's forward of eval.py:145-160 -> (loss, logs).
+                   regularizer_lambda: float, gt_pose: Optional[torch.Tensor] = None,
+                   t_rand: Optional[torch.Tensor] = None, u: Optional[torch.Tensor] = None
+                   ) -> Tuple[torch.Tensor, Dict[str, object]]:
+    """One iteration's forward of eval.py:145-163 -> (loss, logs).
 
-    ``target_pixels``: (H*W, 4) image of the object; rays are drawn by
-    ``RaySampler.sample`` (host numpy RNG, as the reference).
-    """
+    ``target_pixels``: (H*W, C) image of the object; rays are drawn by the ray sampler's RNG
+    (host numpy as the reference, or rng="device").  ``gt_pose`` (4, 4): the view's pose, for
+    the logged pose error (eval.py:161-162).  ``t_rand`` / ``u``: injected stratified / fine
+    uniforms (parity tests), else drawn on the device.  logs: device tensors (read back only
+    when logged) plus psnr, which eval.py:159 reads back every iteration."""
     ray_sampler, point_sampler = samplers
-    cam_pose = pose_spherical(theta, phi, rho)[None, :]
-    ro, rd, select_inds = ray_sampler.sample(tform_cam2world=cam_pose)
-    sel = torch.as_tensor(select_inds, device=target_pixels.device)
-    tp = target_pixels[None][..., sel, :].squeeze()
-    z_s, z_t = shape_code.expand(ro.shape[0], -1), texture_code.expand(ro.shape[0], -1)
-    rgb_c, rgb_f = nerf.predict_radiance_and_render((ro, rd), point_sampler, embedders, models["nerf_coarse"],
-                                                    models["nerf_fine"], (z_s, z_t))
-    lc = torch.nn.functional.mse_loss(rgb_c[..., :3], tp[..., :3])
-    lf = torch.nn.functional.mse_loss(rgb_f[..., :3], tp[..., :3])
-    reg = regularizer_lambda * (torch.norm(z_s, p=2) + torch.norm(z_t, p=2))
-    loss = lc + lf + reg
-    # eval.py:159 reads the fine loss back every iteration (psnr); the other terms are read only when logged
-    return loss, {"nerf_loss_coarse": lc.detach(), "nerf_loss_fine": lf.detach(), "embedding_loss": reg.detach(),
-                  "psnr": mse2psnr(lf.item())}
+    ro, rd, select_inds, cam_pose, tp = ray_sampler.sample_spherical(theta, phi, rho, target=target_pixels)
+    n = ro.shape[0]
+    z_s, z_t = shape_code.expand(n, -1), texture_code.expand(n, -1)
+    # predict_radiance_and_render (nerf/__init__.py:74-91) over the whole ray batch
+    out = nerf.render_rays(ro, rd, z_s, z_t, point_sampler, embedders, models["nerf_coarse"], models["nerf_fine"],
+                           chunk_rows=n, t_rand=t_rand, u=u)
+    rgb_c, rgb_f = out["rgb_coarse"], out["rgb_fine"]
+    # mse(coarse) + mse(fine) + lambda (||z_s|| + ||z_t||), the codes expanded over the n rays
+    loss, stats = nerf_loss(rgb_c, rgb_f, tp, shape_code, texture_code, n, regularizer_lambda)
+    logs = {"nerf_loss_coarse": stats[0], "nerf_loss_fine": stats[1], "embedding_loss": stats[2],
+            "psnr": mse2psnr(stats[1].item())}
+    if gt_pose is not None:
+        logs["pose_error"] = ops.pose_error(gt_pose.reshape(1, 4, 4), cam_pose)[1][0]
+    logs["cam_pose"] = cam_pose
+    return loss, logs
+
+
+def nerf_loss(rgb_c, rgb_f, target, shape_code, texture_code, expand: int, regularizer_lambda: float):
+    """eval.py:157-163 -> (loss, stats (6,)) through cn_render_loss (one launch each way)."""
+    from .autograd import render_loss_autograd
+    return render_loss_autograd(rgb_c, rgb_f, target, shape_code, texture_code, expand, regularizer_lambda)
+
+
+def _optimizer(kind: str, groups, lr: float):
+    if kind == "AdamW":
+        from .optim import AdamW
+        return AdamW(groups, lr=lr)
+    return getattr(torch.optim, kind)(groups, lr=lr)
 
 
 def test_time_optimize(target_pixels: torch.Tensor, samplers, embedders, models, init_codes,
                        iterations: int, val_lr: float = 1e-2, angle_lr: float = 1e-2, radius_lr: float = 1e-2,
                        regularizer_lambda: float = 1e-5, optimizer: str = "AdamW",
                        init_pose: Tuple[float, float, float] = (1.57, 0.0, 1.30),
-                       freeze_models: bool = True, log_every: Optional[int] = None):
-    """eval.py:121-171: optimise codes + (theta, phi, rho) against one image.
+                       freeze_models: bool = True, log_every: Optional[int] = None,
+                       gt_pose: Optional[torch.Tensor] = None):
+    """eval.py:121-180: optimise codes + (theta, phi, rho) against one image.
 
-    ``freeze_models``: the reference leaves the MLP weights requiring grad, so its
-    backward also forms weight gradients that its optimiser never reads; they
-    do not change the result, and freezing skips those GEMMs.
-    Returns (shape_code, texture_code, (theta, phi, rho), history).
+    ``init_codes``: the embedding tables (z_s, z_t); the start point is their mean (eval.py:121-127).
+    ``freeze_models``: the reference leaves the MLP weights requiring grad, so its backward also
+    forms weight gradients that its optimiser never reads; they do not change the result, and
+    freezing skips those GEMMs.
+    Returns (shape_code, texture_code, (theta, phi, rho), history, cam_pose of the last iteration).
     """
     dev = target_pixels.device
     z_s0, z_t0 = init_codes
@@ -71,33 +98,76 @@ def test_time_optimize(target_pixels: torch.Tensor, samplers, embedders, models,
     theta = torch.tensor([init_pose[0]], device=dev).requires_grad_(True)
     phi = torch.tensor([init_pose[1]], device=dev).requires_grad_(True)
     rho = torch.tensor([init_pose[2]], device=dev).requires_grad_(True)
-    opt = getattr(torch.optim, optimizer)([
+    opt = _optimizer(optimizer, [
         {"params": [shape_code, texture_code]},
         {"params": [theta, phi], "lr": angle_lr},
         {"params": [rho], "lr": radius_lr},
-    ], lr=val_lr)
+    ], val_lr)
     saved = {}
     if freeze_models:
         for k, m in models.items():
             saved[k] = [p.requires_grad for p in m.parameters()]
             m.requires_grad_(False)
-    history = []
+    history, cam_pose = [], None
     try:
         for it in range(iterations):
             for m in models.values():
                 m.train()
             loss, logs = eval_step_loss(theta, phi, rho, shape_code, texture_code, target_pixels, samplers,
-                                        embedders, models, regularizer_lambda)
+                                        embedders, models, regularizer_lambda, gt_pose=gt_pose)
+            cam_pose = logs.pop("cam_pose")
             opt.zero_grad()
             loss.backward()
             opt.step()
             logs["total_loss"] = loss.detach()
             history.append(logs)
-            if log_every and (it % log_every == 0 or it == iterations - 1):
-                print(f"[val-optim {it}] " + " ".join(f"{k}={float(v):.5f}" for k, v in logs.items()))
+            if log_every and ((it != 0 and it % log_every == 0) or it == iterations - 1):
+                print(f"[VALOPT] Iter: {it:>8} " + " ".join(f"{k}: {float(v):>4.4f}" for k, v in logs.items()))
     finally:
         for k, flags in saved.items():
             for p, f in zip(models[k].parameters(), flags):
                 p.requires_grad_(f)
     history = [{k: float(v) for k, v in h.items()} for h in history]
-    return shape_code, texture_code, (theta, phi, rho), history
+    return shape_code, texture_code, (theta, phi, rho), history, cam_pose
+
+
+def validate(cfg, val_data: Dict[str, torch.Tensor], models, samplers, embedders, device,
+             log_every: Optional[int] = None) -> Dict[str, object]:
+    """eval.py:82-205 for one loaded validation view (``color`` (1,H,W,C), ``pose`` (1,4,4)):
+
+    1. rank 0's view is broadcast to every rank (eval.py:111-115);
+    2. test-time optimisation of the codes (from the mean of the trained tables) and the pose
+       (eval.py:121-180);
+    3. the whole view rendered from the optimised pose with ``parallel_image_render`` (sharded
+       over the ranks, one all-gather) and its MSE / PSNR against the target on rank 0
+       (eval.py:182-205).
+    Returns {"history", "rgb" (H*W,3) on rank 0, "loss", "psnr", "pose_error", "codes", "pose"}."""
+    is_distributed = bool(getattr(cfg, "is_distributed", False))
+    color = val_data["color"].to(device, torch.float32)
+    gt_pose = val_data["pose"].to(device, torch.float32)
+    if is_distributed:
+        color, gt_pose = color.contiguous(), gt_pose.contiguous()
+        dist.broadcast(color, 0)
+        dist.broadcast(gt_pose, 0)
+    emb = models["embedding"]
+    emb = getattr(emb, "module", emb)
+    all_s, all_t = emb.get_all_embeddings(device=device)
+    e, o = cfg.experiment, cfg.optimizer
+    zs, zt, (th, ph, rh), history, cam_pose = test_time_optimize(
+        color.reshape(-1, color.shape[-1]), samplers, embedders, models, (all_s.detach(), all_t.detach()),
+        e.val_iterations, val_lr=o.val_lr, angle_lr=getattr(o, "angle_lr", o.val_lr),
+        radius_lr=getattr(o, "radius_lr", o.val_lr), regularizer_lambda=e.regularizer_lambda,
+        optimizer=getattr(o, "val_type", "AdamW"), log_every=log_every, gt_pose=gt_pose)
+    rgb = nerf.parallel_image_render(cfg, cam_pose, [zs.detach(), zt.detach()], models, samplers, embedders,
+                                     device)
+    out = {"history": history, "rgb": rgb, "codes": (zs.detach(), zt.detach()),
+           "pose": (float(th), float(ph), float(rh)), "cam_pose": cam_pose}
+    rank0 = (not is_distributed) or dist.get_rank() == 0
+    if rank0:
+        assert rgb is not None, "Main process must contain rgb"
+        target = color.reshape(-1, color.shape[-1])
+        stats = ops.render_loss(None, rgb, target)
+        out["loss"] = float(stats[1])
+        out["psnr"] = mse2psnr(out["loss"])
+        out["pose_error"] = float(ops.pose_error(gt_pose.reshape(1, 4, 4), cam_pose)[1][0])
+    return out

@@ -1,13 +1,20 @@
 """RaySampler on the gfx950 kernels (view_synthesis/nerf/ray_sampler.py:7-99).
 
-Directions are generated once on the device (cn_ray_directions); get_bundle
-rotates them by the c2w poses (cn_ray_bundle); sample draws the pixel subset
-with the host numpy RNG exactly as the reference does (bit-identical
-``select_inds`` for the same seed) and gathers on the device (cn_gather_rays).
+Directions are generated once on the device (cn_ray_directions).  ``sample`` draws the
+pixel subset with the host numpy RNG exactly as the reference does (bit-identical
+``select_inds`` for the same seed) and then computes ONLY those rays on the device:
+one cn_pose_rays launch does get_bundle + the gather (the reference rotates all H*W
+directions, then gathers).  ``get_bundle`` still returns the whole (B, H, W, 3) bundle.
+
+``sample_spherical`` is the eval step's pose path fused:
+pose_spherical(theta, phi, rho) (eval.py:22-38) -> sample -> the target-pixel gather
+(eval.py:147-148) in one launch, with the analytic gradient into theta, phi, rho in one
+more.  ``rng="device"`` replaces the host permutation by an on-device Philox draw
+(cn_random_select; same distribution, different draws -- throughput mode).
 """
 from __future__ import annotations
 
-from typing import Tuple, Union
+from typing import Optional, Tuple, Union
 
 import numpy as np
 import torch
@@ -18,10 +25,11 @@ from .. import ops
 class RaySampler(object):
 
     def __init__(self, height: int, width: int, intrinsics: Union[torch.Tensor, np.ndarray], sample_size: int,
-                 device, datatype):
+                 device, datatype, rng: str = "numpy", seed: int = 0):
         assert height > 0 and width > 0, "Height and width must be positive integers"
         assert sample_size > 0 and sample_size <= height * width, \
             "Sample size must be a positive number less than height * width"
+        assert rng in ("numpy", "device"), "rng must be 'numpy' (the reference's draws) or 'device' (Philox)"
         self.height, self.width, self.sample_size = height, width, sample_size
         self.device = torch.device(device)
         if isinstance(intrinsics, np.ndarray):
@@ -33,18 +41,56 @@ class RaySampler(object):
         self.cx = float(k[0, 2])
         self.cy = float(k[1, 2])
         self.directions = ops.ray_directions(height, width, self.focal_length, self.cx, self.cy, self.device)
+        self.rng, self.seed, self._draws = rng, seed, 0
 
-    def sample(self, tform_cam2world: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor, np.ndarray]:
-        """ray_sampler.py:53-82 -> ro, rd (B*S, 3), select_inds (B, S) numpy."""
-        batch = tform_cam2world.shape[0]
+    def select_inds(self, batch: int):
+        """ray_sampler.py:41-42: per image np.random.permutation(H*W)[:S] -> (numpy (B,S) | None,
+        device int64 (B,S)).  rng="device": Philox on the device (no host copy, numpy None)."""
         n = self.height * self.width
+        if self.rng == "device":
+            sel = ops.random_select(batch, n, self.sample_size, self.seed, self._draws, self.device)
+            self._draws += 1
+            return None, sel
         pixel_range = np.arange(0, n)
         select_inds = np.asarray([np.random.permutation(pixel_range)[: self.sample_size] for _ in range(batch)])
-        ro, rd = self.get_bundle(tform_cam2world)
         sel = torch.from_numpy(select_inds.astype(np.int64)).to(self.device, non_blocking=True)
-        from ..autograd import gather_rays_autograd
-        o, d = gather_rays_autograd(ro, rd, sel)
-        return o, d, select_inds
+        return select_inds, sel
+
+    def sample(self, tform_cam2world: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor, np.ndarray]:
+        """ray_sampler.py:53-82 -> ro, rd (B*S, 3), select_inds (B, S) (numpy; a device tensor with
+        rng="device")."""
+        from ..autograd import pose_rays_autograd
+        batch = tform_cam2world.shape[0]
+        select_inds, sel = self.select_inds(batch)
+        c2w = tform_cam2world.to(self.device, torch.float32)
+        ro, rd, _, _ = pose_rays_autograd(self.directions, c2w=c2w, sel=sel)
+        return ro, rd, (sel if select_inds is None else select_inds)
+
+    def sample_pixels(self, tform_cam2world: torch.Tensor, color: torch.Tensor):
+        """train.py:76-80 fused: sample(tform_cam2world) and the target pixels
+        ``color.flatten(1, 2)[k, select_inds[k], :]`` concatenated over the images, in one launch.
+        color: (B, H, W, C) -> ro, rd (B*S, 3), select_inds, target rows (B*S, C)."""
+        from ..autograd import pose_rays_autograd
+        batch = tform_cam2world.shape[0]
+        select_inds, sel = self.select_inds(batch)
+        c2w = tform_cam2world.to(self.device, torch.float32)
+        target = color.reshape(batch, self.height * self.width, -1)
+        ro, rd, _, tgt = pose_rays_autograd(self.directions, c2w=c2w, sel=sel, target=target)
+        return ro, rd, (sel if select_inds is None else select_inds), tgt
+
+    def sample_spherical(self, theta: torch.Tensor, phi: torch.Tensor, rho: torch.Tensor,
+                         target: Optional[torch.Tensor] = None):
+        """eval.py:145-148 fused: cam_pose = pose_spherical(theta, phi, rho); ro, rd, select_inds =
+        sample(cam_pose); target_pixels = target[..., select_inds, :].  theta, phi, rho: (B,) each
+        (the reference's (1,) leaves); target: (B, H*W, C) or (H*W, C) for B = 1.
+        -> ro, rd (B*S, 3), select_inds, cam_pose (B, 4, 4) (no grad), target rows (B*S, C) | None."""
+        from ..autograd import pose_rays_autograd
+        batch = theta.numel()
+        select_inds, sel = self.select_inds(batch)
+        if target is not None:
+            target = target.reshape(batch, self.height * self.width, -1)
+        ro, rd, cam, tgt = pose_rays_autograd(self.directions, theta, phi, rho, sel=sel, target=target)
+        return ro, rd, (sel if select_inds is None else select_inds), cam, tgt
 
     def get_bundle(self, tform_cam2world: torch.Tensor):
         """ray_sampler.py:84-99 -> ro, rd (B, H, W, 3)."""

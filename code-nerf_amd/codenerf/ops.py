@@ -71,6 +71,90 @@ def gather_rays(ro: Tensor, rd: Tensor, select_inds: Tensor) -> Tuple[Tensor, Te
     return o, d
 
 
+# ------------------------------------------------------------------ fused pose path
+
+
+def pose_rays(dirs: Tensor, theta: Optional[Tensor] = None, phi: Optional[Tensor] = None,
+              rho: Optional[Tensor] = None, c2w: Optional[Tensor] = None, select_inds: Optional[Tensor] = None,
+              target: Optional[Tensor] = None):
+    """pose_spherical (eval.py:22-38) -> sample (ray_sampler.py:53-99) -> target gather
+    (eval.py:147-148) in one launch.  theta, phi, rho (B,) each, or c2w (B,4,4); select_inds
+    (B,S) int64 or None (whole bundle); target (B,HW,C) or None -> ro, rd (B*S,3), c2w (B,4,4),
+    target rows (B*S,C) | None."""
+    lib = _lib_ready()
+    dirs = _cuda(dirs, "directions")
+    hw = dirs.numel() // 3
+    assert (theta is None) != (c2w is None), "give exactly one of (theta, phi, rho) and c2w"
+    if theta is not None:
+        theta, phi, rho = (_cuda(t, n).reshape(-1) for t, n in ((theta, "theta"), (phi, "phi"), (rho, "rho")))
+        b = theta.numel()
+        assert phi.numel() == b and rho.numel() == b, "theta, phi and rho must have one value per pose"
+    else:
+        c2w = _cuda(c2w, "tform_cam2world")
+        assert c2w.dim() == 3 and c2w.shape[-2:] == (4, 4), "tform_cam2world must be (batch, 4, 4)"
+        b = c2w.shape[0]
+    if select_inds is not None:
+        select_inds = _cuda(select_inds, "select_inds", torch.int64)
+        assert select_inds.dim() == 2 and select_inds.shape[0] == b, "select_inds must be (batch, sample_size)"
+        s = select_inds.shape[1]
+    else:
+        s = hw
+    ch = 0
+    tgt_out = None
+    if target is not None:
+        target = _cuda(target, "target")
+        assert target.shape[0] == b and target.numel() % (b * hw) == 0, "target must be (batch, H*W, C)"
+        ch = target.numel() // (b * hw)
+        tgt_out = torch.empty(b * s, ch, device=dirs.device, dtype=torch.float32)
+    ro = torch.empty(b * s, 3, device=dirs.device, dtype=torch.float32)
+    rd = torch.empty_like(ro)
+    c2w_out = torch.empty(b, 4, 4, device=dirs.device, dtype=torch.float32)
+    check(lib.cn_pose_rays(ptr(theta), ptr(phi), ptr(rho), ptr(c2w), b, ptr(dirs), hw, ptr(select_inds), s,
+                           ptr(target), ch, ptr(c2w_out), ptr(ro), ptr(rd), ptr(tgt_out), stream_of(ro)),
+          "cn_pose_rays")
+    return ro, rd, c2w_out, tgt_out
+
+
+def pose_rays_backward(dirs: Tensor, batch: int, g_ro: Optional[Tensor], g_rd: Optional[Tensor],
+                       theta: Optional[Tensor] = None, phi: Optional[Tensor] = None, rho: Optional[Tensor] = None,
+                       select_inds: Optional[Tensor] = None, want_c2w: bool = False):
+    """Backward of pose_rays -> (d_theta, d_phi, d_rho (B,) each | None, d_c2w (B,4,4) | None)."""
+    lib = _lib_ready()
+    dirs = _cuda(dirs, "directions")
+    hw = dirs.numel() // 3
+    s = hw if select_inds is None else select_inds.shape[1]
+    g_ro, g_rd = _opt(g_ro, "g_ro"), _opt(g_rd, "g_rd")
+    angles = theta is not None
+    d = [torch.empty(batch, device=dirs.device, dtype=torch.float32) if angles else None for _ in range(3)]
+    d_c2w = torch.empty(batch, 4, 4, device=dirs.device, dtype=torch.float32) if want_c2w else None
+    check(lib.cn_pose_rays_backward(ptr(theta), ptr(phi), ptr(rho), batch, ptr(dirs), hw, ptr(select_inds), s,
+                                    ptr(g_ro), ptr(g_rd), ptr(d_c2w), ptr(d[0]), ptr(d[1]), ptr(d[2]),
+                                    stream_of(dirs)), "cn_pose_rays_backward")
+    return (d[0], d[1], d[2]), d_c2w
+
+
+def random_select(batch: int, hw: int, sample_size: int, seed: int, offset: int, device) -> Tensor:
+    """On-device np.random.permutation(hw)[:sample_size] per image (ray_sampler.py:41-42, same
+    distribution; Philox4x32-10) -> (batch, sample_size) int64."""
+    lib = _lib_ready()
+    out = torch.empty(batch, sample_size, device=device, dtype=torch.int64)
+    check(lib.cn_random_select(batch, hw, sample_size, seed & (2 ** 64 - 1), offset & (2 ** 64 - 1), ptr(out),
+                               stream_of(out)), "cn_random_select")
+    return out
+
+
+def pose_error(gt_c2w: Tensor, cam_c2w: Tensor) -> Tuple[Tensor, Tensor]:
+    """eval.py:161-162: (SE3.Log(inverse(gt) @ cam) (B,6), its 2-norm (B,))."""
+    lib = _lib_ready()
+    gt, cam = _cuda(gt_c2w, "gt_pose").reshape(-1, 4, 4), _cuda(cam_c2w, "cam_pose").reshape(-1, 4, 4)
+    assert gt.shape == cam.shape, "poses must both be (batch, 4, 4)"
+    b = gt.shape[0]
+    twist = torch.empty(b, 6, device=gt.device, dtype=torch.float32)
+    err = torch.empty(b, device=gt.device, dtype=torch.float32)
+    check(lib.cn_pose_error(ptr(gt), ptr(cam), b, ptr(twist), ptr(err), stream_of(gt)), "cn_pose_error")
+    return twist, err
+
+
 # ------------------------------------------------------------------ points
 
 
@@ -571,3 +655,59 @@ def adamw_step(param: Tensor, grad: Tensor, exp_avg: Tensor, exp_avg_sq: Tensor,
                             arr(ctypes.c_double, [float(s[3]) for s in segments]),
                             arr(ctypes.c_int64, [int(s[4]) for s in segments]),
                             float(beta1), float(beta2), float(eps), stream_of(param)), "cn_adamw_step")
+
+
+# ------------------------------------------------------------------ the step's loss
+
+
+def render_loss(rgb_coarse: Optional[Tensor], rgb_fine: Optional[Tensor], target: Tensor,
+                z_s: Optional[Tensor] = None, z_t: Optional[Tensor] = None, expand: int = 1,
+                regularizer_lambda: float = 0.0) -> Tensor:
+    """train.py:103-108 / eval.py:157-163 in one launch -> (6,) [loss_coarse, loss_fine, regulariser,
+    total, ||z_s||, ||z_t||]; ``||z||`` over z's elements times ``expand`` (expanded rows)."""
+    lib = _lib_ready()
+    rc, rf = _opt(rgb_coarse, "rgb_coarse"), _opt(rgb_fine, "rgb_fine")
+    target = _cuda(target, "target")
+    n = (rc if rc is not None else rf).shape[0]
+    assert target.shape[0] == n and target.dim() == 2 and target.shape[1] >= 3, "target must be (R, >=3)"
+    zs, zt = _opt(z_s, "z_s"), _opt(z_t, "z_t")
+    n_code = 0 if zs is None else zs.numel()
+    assert zt is None or zt.numel() == n_code, "z_s and z_t must have the same size"
+    out = torch.empty(6, device=target.device, dtype=torch.float32)
+    check(lib.cn_render_loss(ptr(rc), ptr(rf), ptr(target), target.shape[1], n, ptr(zs), ptr(zt), n_code, expand,
+                             regularizer_lambda, ptr(out), stream_of(out)), "cn_render_loss")
+    return out
+
+
+def render_loss_backward(rgb_coarse, rgb_fine, target, z_s, z_t, expand, regularizer_lambda, stats, grad_total,
+                         want=(True, True, True, True)):
+    """Backward of render_loss -> (d_rgb_coarse, d_rgb_fine, d_z_s, d_z_t), None where not wanted."""
+    lib = _lib_ready()
+    rc, rf = _opt(rgb_coarse, "rgb_coarse"), _opt(rgb_fine, "rgb_fine")
+    target = _cuda(target, "target")
+    n = (rc if rc is not None else rf).shape[0]
+    zs, zt = _opt(z_s, "z_s"), _opt(z_t, "z_t")
+    n_code = 0 if zs is None else zs.numel()
+    outs = [torch.empty_like(t) if (w and t is not None) else None for w, t in zip(want, (rc, rf, zs, zt))]
+    check(lib.cn_render_loss_backward(ptr(rc), ptr(rf), ptr(target), target.shape[1], n, ptr(zs), ptr(zt), n_code,
+                                      expand, regularizer_lambda, ptr(stats), ptr(_cuda(grad_total, "grad")),
+                                      *[ptr(o) for o in outs], stream_of(target)), "cn_render_loss_backward")
+    return tuple(outs)
+
+
+# ------------------------------------------------------------------ SRN data resident in HBM
+
+
+def srn_unpack(images: Tensor, view_index: Tensor, want_color: bool = True, want_mask: bool = True):
+    """dataset.py:77-80 for a batch of resident uint8 views (n, h, w, c) -> color (B, h, w, c) float,
+    mask (B, h, w, 1) float (either None when not wanted)."""
+    lib = _lib_ready()
+    images = _cuda(images, "images", torch.uint8)
+    idx = _cuda(view_index, "view_index", torch.int64).reshape(-1)
+    n, h, w, c = images.shape
+    b = idx.numel()
+    color = torch.empty(b, h, w, c, device=images.device, dtype=torch.float32) if want_color else None
+    mask = torch.empty(b, h, w, 1, device=images.device, dtype=torch.float32) if want_mask else None
+    check(lib.cn_srn_unpack(ptr(images), n, h * w, c, ptr(idx), b, ptr(color), ptr(mask), stream_of(images)),
+          "cn_srn_unpack")
+    return color, mask

@@ -31,6 +31,7 @@ import torch.distributed as dist
 from . import nerf
 from .models import CodeNeRFModel, ShapeTextureEmbedding, get_params_tensor
 from .optim import AdamW
+from .autograd import render_loss_autograd
 from .utils import get_minibatches, mse2psnr
 
 
@@ -113,20 +114,21 @@ def train_minibatch(models, optimizer, scheduler, point_sampler, embedders, ro, 
     target_object_embedding = models["embedding"](object_ids)
     rgb_coarse, rgb_fine = nerf.predict_radiance_and_render((ro, rd), point_sampler, embedders, models["nerf_coarse"],
                                                             models["nerf_fine"], target_object_embedding)
-    loss_coarse = torch.nn.functional.mse_loss(rgb_coarse[..., :3], target_pixels[..., :3])
-    loss_fine = torch.nn.functional.mse_loss(rgb_fine[..., :3], target_pixels[..., :3])
-    psnr = mse2psnr(loss_fine.item())
+    # mse coarse + mse fine + lambda (||shape table|| + ||texture table||) on .data (a constant):
+    # one cn_render_loss launch forward, one backward into the two rgb tensors
     shape_params, texture_params = get_params_tensor(models["embedding"], is_distributed)
-    regularization = regularizer_lambda * (torch.norm(shape_params, p=2) + torch.norm(texture_params, p=2))
-    loss = loss_coarse + loss_fine + regularization
+    loss, stats = render_loss_autograd(rgb_coarse, rgb_fine, target_pixels, shape_params, texture_params, 1,
+                                       regularizer_lambda)
+    loss_coarse, loss_fine, regularization = stats[0], stats[1], stats[2]
+    psnr = mse2psnr(loss_fine.item())
     optimizer.zero_grad()
     loss.backward()
     if is_distributed:
         _average_gradients(optimizer, models)
     optimizer.step()
     scheduler.step()
-    return {"nerf_loss_coarse": loss_coarse.detach(), "nerf_loss_fine": loss_fine.detach(),
-            "embedding_loss": regularization.detach(), "total_loss": loss.detach(), "psnr": psnr}
+    return {"nerf_loss_coarse": loss_coarse, "nerf_loss_fine": loss_fine, "embedding_loss": regularization,
+            "total_loss": loss.detach(), "psnr": psnr}
 
 
 def train_iteration(cfg, train_data: Dict[str, torch.Tensor], models, optimizer, scheduler, samplers,
@@ -137,11 +139,10 @@ def train_iteration(cfg, train_data: Dict[str, torch.Tensor], models, optimizer,
     is_distributed = bool(getattr(cfg, "is_distributed", False))
     for m in models.values():
         m.train()
-    ro_batch, rd_batch, select_inds = ray_sampler.sample(tform_cam2world=train_data["pose"])
+    # sample + the per-image target gather (train.py:76-80) in one cn_pose_rays launch
+    ro_batch, rd_batch, select_inds, target = ray_sampler.sample_pixels(train_data["pose"], train_data["color"])
     n_rays = ray_sampler.sample_size
-    color = train_data["color"].flatten(1, 2)
-    sel = torch.as_tensor(select_inds, device=color.device)
-    target = torch.cat([color[k, sel[k], :] for k in range(color.shape[0])], dim=0)
+    color = train_data["color"]
     object_ids = train_data["object_id"][:, None].expand(-1, n_rays).reshape(-1)
     chunk = cfg.nerf.train.chunksize
     assert chunk <= n_rays * color.shape[0], \

@@ -80,6 +80,50 @@ int cn_gather_rays(const float* ro, const float* rd, int64_t batch, int64_t hw,
                    const int64_t* select_inds, int64_t sample_size, float* ro_out,
                    float* rd_out, cn_stream_t stream);
 
+/* --- Fused pose path (eval.py:22-38 pose_spherical + ray_sampler.py:53-99 sample
+ *     + eval.py:147-148 target gather) ------------------- */
+
+/* The pose from theta, phi, rho (batch) each (eval.py:33-37), or given as c2w (batch, 4, 4)
+ * when theta is NULL, then ONLY the selected rays:
+ * select_inds (batch, sample_size) int64 (the sample gather, ray_sampler.py:77-80), or NULL
+ * with sample_size == hw for the whole bundle (get_bundle).  dirs: (hw, 3) from
+ * cn_ray_directions.  ro, rd: (batch*sample_size, 3); c2w_out (batch, 4, 4) or NULL;
+ * target (batch, hw, target_channels) gathered into target_out (batch*sample_size,
+ * target_channels) when both are non-NULL.  Out-of-range indices give NaN rows. */
+int cn_pose_rays(const float* theta, const float* phi, const float* rho, const float* c2w, int64_t batch,
+                 const float* dirs,
+                 int64_t hw, const int64_t* select_inds, int64_t sample_size, const float* target,
+                 int64_t target_channels, float* c2w_out, float* ro, float* rd, float* target_out,
+                 cn_stream_t stream);
+
+/* Backward of cn_pose_rays from g_ro / g_rd (batch*sample_size, 3; either may be NULL, not
+ * both): d_c2w (batch, 4, 4) WRITTEN (rows 0..2; row 3 zero) and/or d_theta, d_phi, d_rho
+ * (batch) WRITTEN (any may be NULL) through the analytic d c2w / d(theta, phi, rho). */
+int cn_pose_rays_backward(const float* theta, const float* phi, const float* rho, int64_t batch,
+                          const float* dirs, int64_t hw, const int64_t* select_inds, int64_t sample_size,
+                          const float* g_ro, const float* g_rd, float* d_c2w, float* d_theta, float* d_phi,
+                          float* d_rho, cn_stream_t stream);
+
+/* Device replacement of ray_sampler.py:41-42's np.random.permutation(hw)[:sample_size]
+ * per image (throughput mode; same distribution, not the same draws): Philox4x32-10 keyed
+ * by seed, counter (pixel, image, offset).  select_inds: (batch, sample_size) int64.
+ * hw <= 16384 (one workgroup sorts an image's keys in LDS), else CN_EUNSUPPORTED. */
+int cn_random_select(int64_t batch, int64_t hw, int64_t sample_size, uint64_t seed, uint64_t offset,
+                     int64_t* select_inds, cn_stream_t stream);
+
+/* The eval pose metric, eval.py:161-162: twist = SE3.Log(inverse(gt) @ cam)
+ * (utils/lieutils.py:709-718) and err = ||twist||_2 per pose.  gt_c2w, cam_c2w: (batch, 4, 4);
+ * twist (batch, 6) = (w, v) and/or err (batch). */
+int cn_pose_error(const float* gt_c2w, const float* cam_c2w, int64_t batch, float* twist, float* err,
+                  cn_stream_t stream);
+
+/* --- SRN data resident in HBM (view_synthesis/datasets/dataset.py:60-94) --
+ * images: (n_views, hw, channels) uint8, the decoded and cropped views; view_index: (batch) int64.
+ * color (batch, hw, channels) = u8 / 255.0 (rounded once to fp32, as numpy's float64 quotient
+ * cast to float32) and/or mask (batch, hw) = 1.0 where every channel != 255, else 0.0. */
+int cn_srn_unpack(const uint8_t* images, int64_t n_views, int64_t hw, int64_t channels,
+                  const int64_t* view_index, int64_t batch, float* color, float* mask, cn_stream_t stream);
+
 /* --- Points: view_synthesis/nerf/point_sampler.py ---------------------- */
 
 /* PointSampler.sample_uniform, point_sampler.py:49-71.
@@ -284,6 +328,24 @@ int cn_posenc_backward(const float* x, int64_t m, int64_t d, const float* freqs,
  * d_rd += sum_s g_pts * z; either output may be NULL (not both). */
 int cn_ray_points_backward(const float* g_pts, const float* z, int64_t n_rays, int64_t n_samples,
                            float* d_ro, float* d_rd, cn_stream_t stream);
+
+/* --- The step's scalar loss (train.py:103-108, eval.py:157-163) ---------------
+ * out[6] = [mse(rgb_coarse, target[:, :3]), mse(rgb_fine, target[:, :3]),
+ *           lambda * (||z_s|| + ||z_t||), their sum, ||z_s||, ||z_t||] (fp32, device), with
+ * ||z|| = sqrt(expand * sum z^2) over n_code values (a code row expanded over `expand` rays,
+ * eval; or whole tables with expand 1, train).  rgb_*: (n_rays, 3), either may be NULL;
+ * target rows of target_stride floats (the first 3 are rgb).  n_code 0: no regulariser. */
+int cn_render_loss(const float* rgb_coarse, const float* rgb_fine, const float* target,
+                   int64_t target_stride, int64_t n_rays, const float* z_s, const float* z_t,
+                   int64_t n_code, int64_t expand, float regularizer_lambda, float* out,
+                   cn_stream_t stream);
+/* Its backward for an upstream gradient *grad_total (device scalar) of the sum, reading
+ * the forward's out as stats: d_rgb_* (n_rays, 3) and d_z_* (n_code) WRITTEN (any NULL). */
+int cn_render_loss_backward(const float* rgb_coarse, const float* rgb_fine, const float* target,
+                            int64_t target_stride, int64_t n_rays, const float* z_s, const float* z_t,
+                            int64_t n_code, int64_t expand, float regularizer_lambda, const float* stats,
+                            const float* grad_total, float* d_rgb_coarse, float* d_rgb_fine, float* d_z_s,
+                            float* d_z_t, cn_stream_t stream);
 
 /* --- Training step: the optimiser (train.py:111-114, utils/util.py:147-172) ---
  * torch.optim.AdamW.step (decoupled weight decay; amsgrad / maximize off) over ONE

@@ -369,3 +369,120 @@ def mse2psnr(mse: float) -> float:
     if mse == 0:
         mse = 1e-5
     return -10.0 * math.log10(mse)
+
+
+def render_loss(rgb_c: Optional[Tensor], rgb_f: Tensor, target: Tensor, z_s: Optional[Tensor] = None,
+                z_t: Optional[Tensor] = None, lam: float = 0.0) -> Tensor:
+    """train.py:103-108 / eval.py:157-163: mse coarse + mse fine + lam (||z_s|| + ||z_t||) (z_* as given,
+    e.g. expanded over the rays)."""
+    lc = torch.nn.functional.mse_loss(rgb_c[..., :3], target[..., :3]) if rgb_c is not None else torch.zeros(())
+    lf = torch.nn.functional.mse_loss(rgb_f[..., :3], target[..., :3])
+    reg = torch.zeros(())
+    if z_s is not None:
+        reg = lam * (torch.norm(z_s, p=2) + torch.norm(z_t, p=2))
+    return lc + lf + reg
+
+
+# ---------------------------------------------------------------------------
+# SE3 pose error                                     utils/lieutils.py, eval.py:161-162
+# ---------------------------------------------------------------------------
+
+
+def _sin_by_t(t: Tensor) -> Tensor:
+    """lieutils.py:58-81 (coeff_A forward, eps 1e-3)."""
+    out = torch.zeros_like(t)
+    s = torch.abs(t) < 1e-3
+    l = s == 0
+    t2 = t[s] ** 2
+    out[s] = 1 - t2 / 6 * (1 - t2 / 20 * (1 - t2 / 42))
+    out[l] = torch.sin(t[l]) / t[l]
+    return out
+
+
+def so3_log(R: Tensor) -> Tensor:
+    """lieutils.py:528-566 for (B,3,3) -> (B,3).  Quirks kept: acos of (tr-1)/2 > 1 is NaN, neither
+    branch applies and w = 0.  The |sin t/t| <= 1e-7 branch raises NameError in the reference
+    ('torh', :553); restated here as that branch intends."""
+    tr = torch.stack([torch.trace(m) for m in R])
+    c = (tr - 1) / 2
+    t = torch.acos(c)
+    sc = _sin_by_t(t)
+    idx0 = torch.abs(sc) <= 1e-7
+    idx1 = torch.abs(sc) > 1e-7
+    sc = sc.view(-1, 1, 1)
+    X = torch.zeros_like(R)
+    if idx1.any():
+        X[idx1] = (R[idx1] - R[idx1].transpose(1, 2)) / (2 * sc[idx1])
+    if idx0.any():
+        t2 = t[idx0] ** 2
+        A = (R[idx0] + torch.eye(3).type_as(R).unsqueeze(0)) * t2.view(-1, 1, 1) / 2
+        s3 = torch.sign(A[:, 0, 2])
+        s3[s3 == 0] = 1
+        s23 = torch.sign(A[:, 1, 2])
+        s23[s23 == 0] = 1
+        w = torch.stack((torch.sqrt(A[:, 0, 0]), torch.sqrt(A[:, 1, 1]) * (s23 * s3), torch.sqrt(A[:, 2, 2]) * s3),
+                        dim=-1)
+        X[idx0] = so3_hat(w)
+    return torch.stack((X[:, 2, 1], X[:, 0, 2], X[:, 1, 0]), dim=1)
+
+
+def so3_hat(x: Tensor) -> Tensor:
+    """lieutils.py:465-480."""
+    x1, x2, x3 = x[:, 0], x[:, 1], x[:, 2]
+    o = torch.zeros_like(x1)
+    return torch.stack((torch.stack((o, -x3, x2), 1), torch.stack((x3, o, -x1), 1), torch.stack((-x2, x1, o), 1)), 1)
+
+
+def se3_log(g: Tensor) -> Tensor:
+    """lieutils.py:709-718 (+ inv_vecs_Xg_ig :568-582): (B,4,4) -> (B,6) = (w, v)."""
+    g = g.reshape(-1, 4, 4)
+    R, p = g[:, 0:3, 0:3], g[:, 0:3, 3]
+    w = so3_log(R)
+    t = w.norm(p=2, dim=1).view(-1, 1, 1)
+    X = so3_hat(w)
+    S = X.bmm(X)
+    s = torch.abs(t) < 1e-3
+    l = s == 0
+    eta = torch.zeros_like(t)
+    t2 = t[s] ** 2
+    eta[s] = ((t2 / 40 + 1) * t2 / 42 + 1) * t2 / 720 + 1 / 12
+    eta[l] = (1 - (t[l] / 2) / torch.tan(t[l] / 2)) / (t[l] ** 2)
+    H = torch.eye(3) - 1 / 2 * X + eta * S
+    v = H.bmm(p.contiguous().view(-1, 3, 1)).view(-1, 3)
+    return torch.cat((w, v), dim=1)
+
+
+def pose_error(gt: Tensor, cam: Tensor) -> Tensor:
+    """eval.py:161-162: ||SE3.Log(inverse(gt) @ cam)||_2 per pose."""
+    g = torch.matmul(torch.inverse(gt.reshape(-1, 4, 4)), cam.reshape(-1, 4, 4))
+    return se3_log(g).norm(p=2, dim=1)
+
+
+# ---------------------------------------------------------------------------
+# SRN on-disk format                          view_synthesis/datasets/dataset.py
+# ---------------------------------------------------------------------------
+
+
+def srn_item(rgb_png: str, pose_txt: str, intrinsics_txt: str, object_index: int) -> Dict[str, object]:
+    """SRNDataset.__getitem__ (dataset.py:60-94): PNG -> /255, mask (all channels != 255), crop
+    size//8 on each side (rows by the width's crop, columns by the height's), pose @ diag(1,-1,-1,1),
+    principal point shifted by the crops.  PNG decoding by Pillow (imageio's PNG backend)."""
+    import numpy as np
+    from PIL import Image
+    with open(intrinsics_txt) as f:
+        lines = f.readlines()
+    focal, cx, cy, _ = map(float, lines[0].split())
+    height, width = map(int, lines[-1].split())
+    rgb = np.asarray(Image.open(rgb_png))
+    mask = (rgb != 255).all(axis=-1)[..., None].astype(np.uint8) * 255
+    rgb = rgb / 255.0
+    mask = mask / 255.0
+    ch, cw = height // 8, width // 8
+    rgb = rgb[cw:width - cw, ch:height - ch, ...]
+    mask = mask[cw:width - cw, ch:height - ch, ...]
+    pose = np.loadtxt(pose_txt).reshape(4, 4) @ np.diag([1, -1, -1, 1])
+    k = np.eye(4)
+    k[0, 0], k[1, 1] = focal, focal
+    k[0, 2], k[1, 2] = cx - cw, cy - ch
+    return {"object_id": object_index, "intrinsic": k.astype(np.float32), "color": rgb.astype(np.float32),
+            "mask": mask.astype(np.float32), "pose": pose.astype(np.float32)}

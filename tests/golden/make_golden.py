@@ -468,7 +468,70 @@ def gen_c5(nerf, model_mod, ev):
          g_coarse_layer_xyz1_w=models["nerf_coarse"].layer_xyz1.weight.grad, **pw)
 
 
-ROUND2 = {"trained": gen_trained, "chairs": gen_chairs, "lego": gen_lego, "c5": gen_c5}
+def gen_se3(nerf, model_mod, ev):
+    """eval.py:161-162's pose error through the reference's own utils.SE3.Log (lieutils.py:709-718)."""
+    import importlib
+    util = importlib.import_module("view_synthesis.utils")
+    g = torch.Generator().manual_seed(23)
+    gts, cams = [], []
+    for k in range(24):
+        th, ph, rh = (torch.rand(3, generator=g) * torch.tensor([3.0, 6.2, 1.0]) + torch.tensor([-1.5, -3.1, 0.8]))
+        gt = ev.pose_spherical(th[None], ph[None], rh[None])
+        d = torch.randn(3, generator=g) * (0.3 if k < 16 else 1e-4)   # small and tiny perturbations
+        cam = ev.pose_spherical((th + d[0])[None], (ph + d[1])[None], (rh + d[2])[None])
+        gts.append(gt)
+        cams.append(cam)
+    gts.append(gts[0])
+    cams.append(gts[0].clone())                       # identical poses: (tr - 1) / 2 rounds to >= 1
+    gt, cam = torch.stack(gts), torch.stack(cams)
+    twist = torch.stack([util.SE3.Log(torch.matmul(torch.inverse(a), b)) for a, b in zip(gt, cam)])
+    err = torch.stack([torch.norm(util.SE3.Log(torch.matmul(torch.inverse(a), b)), p=2) for a, b in zip(gt, cam)])
+    save("se3_pose_error.npz", gt=gt, cam=cam, twist=twist, err=err)
+
+
+def gen_srn(nerf, model_mod, ev):
+    """The reference's SRNDataset (dataset.py:10-94) over the tiny synthetic tree of srn_tree.py.
+    imageio is not installed: the harness maps imageio.imread to Pillow (imageio's PNG backend)."""
+    import importlib
+    import tempfile
+    from PIL import Image
+    sys.path.insert(0, HERE)
+    import srn_tree
+    sys.modules["imageio"].imread = lambda path: np.asarray(Image.open(path))
+    ds_mod = importlib.import_module("view_synthesis.datasets.dataset")
+    out = {}
+    with tempfile.TemporaryDirectory() as tmp:
+        base = srn_tree.write_tree(tmp)
+        for stage in ("train", "val"):
+            ds = ds_mod.SRNDataset(base, stage)
+            out[f"{stage}_num_objects"] = ds.num_objects
+            out[f"{stage}_num_views"] = ds.num_views
+            out[f"{stage}_files"] = np.array([os.path.relpath(str(p), base) for _, p in ds.rgb_all_filenames])
+            for i in range(len(ds)):       # RGB and RGBA files: channel counts differ per item
+                for k, v in ds[i].items():
+                    out[f"{stage}_{i}_{k}"] = np.asarray(v)
+    save("srn_tiny.npz", **out)
+
+
+def gen_loss(nerf, model_mod, ev):
+    """train.py:103-107 / eval.py:157-160 loss terms and their gradients on random inputs."""
+    g = torch.Generator().manual_seed(31)
+    R = 300
+    rgb_c, rgb_f = torch.rand(R, 3, generator=g).requires_grad_(True), torch.rand(R, 3, generator=g).requires_grad_(True)
+    target = torch.rand(R, 4, generator=g)
+    zs, zt = (torch.randn(1, 256, generator=g) * 0.3).requires_grad_(True), (torch.randn(1, 256, generator=g) * 0.3).requires_grad_(True)
+    zse, zte = zs.expand(R, -1), zt.expand(R, -1)
+    lc = torch.nn.functional.mse_loss(rgb_c[..., :3], target[..., :3])
+    lf = torch.nn.functional.mse_loss(rgb_f[..., :3], target[..., :3])
+    reg = 1e-2 * (torch.norm(zse, p=2) + torch.norm(zte, p=2))
+    loss = lc + lf + reg
+    loss.backward()
+    save("loss.npz", rgb_c=rgb_c, rgb_f=rgb_f, target=target, z_s=zs, z_t=zt, lam=np.float32(1e-2), lc=lc, lf=lf,
+         reg=reg, loss=loss, g_rgb_c=rgb_c.grad, g_rgb_f=rgb_f.grad, g_z_s=zs.grad, g_z_t=zt.grad)
+
+
+ROUND2 = {"trained": gen_trained, "chairs": gen_chairs, "lego": gen_lego, "c5": gen_c5, "se3": gen_se3,
+          "srn": gen_srn, "loss": gen_loss}
 
 
 if __name__ == "__main__":

@@ -497,8 +497,9 @@ def test_test_time_optimize_runs(dev):
     target = torch.rand(12 * 16, 4, generator=torch.Generator().manual_seed(1)).to(dev)
     codes = (torch.randn(4, 256) * 0.3, torch.randn(4, 256) * 0.3)
     np.random.seed(0)
-    zs, zt, (theta, phi, rho), hist = test_time_optimize(target, (rs, ps), emb, models, codes, iterations=6,
-                                                         val_lr=5e-2)
+    zs, zt, (theta, phi, rho), hist, cam = test_time_optimize(target, (rs, ps), emb, models, codes, iterations=6,
+                                                              val_lr=5e-2)
+    assert cam.shape == (1, 4, 4)
     assert len(hist) == 6 and np.isfinite([h["total_loss"] for h in hist]).all()
     assert not torch.allclose(zs.detach().cpu(), codes[0].mean(0, keepdim=True))
     assert abs(theta.item() - 1.57) > 1e-4 and abs(rho.item() - 1.30) > 1e-4

@@ -283,3 +283,46 @@ def test_eval_c5_gradients():
     for t, k in [(theta, "theta"), (phi, "phi"), (rho, "rho"), (zs, "z_s"), (zt, "z_t")]:
         same(t.grad, g["g_" + k], 1e-8)
     same(pf["fc_rgb.weight"].grad, g["g_fine_fc_rgb_w"], 1e-8)
+
+
+# ---------------------------------------------------------------- round 2: pose metric, loss, SRN format
+
+
+def test_se3_pose_error():
+    """lieutils.SE3.Log of inverse(gt) @ cam (eval.py:161-162), incl. near-identity poses."""
+    g = load("se3_pose_error.npz")
+    tw = O.se3_log(torch.matmul(torch.inverse(g["gt"]), g["cam"]))
+    same(tw, g["twist"], 1e-6)
+    same(O.pose_error(g["gt"], g["cam"]), g["err"], 1e-6)
+
+
+def test_loss_terms():
+    g = load("loss.npz")
+    rc, rf = g["rgb_c"].clone().requires_grad_(True), g["rgb_f"].clone().requires_grad_(True)
+    zs, zt = g["z_s"].clone().requires_grad_(True), g["z_t"].clone().requires_grad_(True)
+    loss = O.render_loss(rc, rf, g["target"], zs.expand(300, -1), zt.expand(300, -1), float(g["lam"]))
+    loss.backward()
+    same(loss, g["loss"])
+    for t, k in ((rc, "g_rgb_c"), (rf, "g_rgb_f"), (zs, "g_z_s"), (zt, "g_z_t")):
+        same(t.grad, g[k])
+
+
+def test_srn_item_restatement(tmp_path):
+    """dataset.py:60-94 on the tiny synthetic SRN tree: the oracle's restatement reproduces the
+    reference loader's every output (decode, /255, mask, crop, pose flip, principal point)."""
+    import sys
+    sys.path.insert(0, GOLDEN)
+    import srn_tree
+    g = np.load(os.path.join(GOLDEN, "srn_tiny.npz"))
+    base = srn_tree.write_tree(str(tmp_path))
+    for stage in ("train", "val"):
+        files = list(g[f"{stage}_files"])
+        obj_dirs = sorted({f.split("/rgb/")[0] for f in files})
+        for i, f in enumerate(files):
+            obj = f.split("/rgb/")[0]
+            view = os.path.basename(f)[:-4]
+            item = O.srn_item(os.path.join(base, f), os.path.join(base, obj, "pose", view + ".txt"),
+                              os.path.join(base, obj, "intrinsics.txt"), obj_dirs.index(obj))
+            for k in ("color", "mask", "pose", "intrinsic", "object_id"):
+                ref = g[f"{stage}_{i}_{k}"]
+                assert np.array_equal(np.asarray(item[k]), ref), (stage, i, k)
