@@ -365,11 +365,12 @@ def eval_bench(dev, rs, emb, models, iters, precision):
     for m, prec in saved:
         m.requires_grad_(True)
         m.precision = prec
-    note = ("3xbf16 forward with ReLU masks + one fused backward launch per field" if precision == "bf16x3" else
-            "fp32 forward keeping activations + layer-wise fp32 MFMA backward")
+    note = ("3xbf16 forward with ReLU masks + one fused 3xbf16 backward launch per field" if precision == "bf16x3"
+            else "fp32 16x16x4 forward with ReLU masks + one fused fp32 backward launch per field")
     return {"ms_per_iter": dt * 1e3, "rays_per_s": 2048 / dt, "rays_per_iter": 2048, "samples": "64+64 perturbed",
             "dtype": precision,
-            "note": note + "; host-side numpy ray permutation and eval.py's per-iteration psnr read-back included"}
+            "note": note + "; fused pose path + loss; host-side numpy ray permutation and eval.py's per-iteration psnr "
+                           "read-back included"}
 
 
 def train_bench(dev, k, iters, world):

@@ -18,8 +18,9 @@ LIB_PATH = os.environ.get("CODENERF_LIB", os.path.join(_HERE, "lib", "libcodener
 
 CN_OK, CN_EINVAL, CN_EUNSUPPORTED = 0, -1, -2
 CN_NUM_PARAMS = 18
-CN_FMT_F32, CN_FMT_BF16X3, CN_FMT_BF16X3_T, CN_FMT_F32_W16 = 0, 1, 2, 3
-FORMATS = {"f32": CN_FMT_F32, "bf16x3": CN_FMT_BF16X3, "bf16x3_t": CN_FMT_BF16X3_T, "f32_w16": CN_FMT_F32_W16}
+CN_FMT_F32, CN_FMT_BF16X3, CN_FMT_BF16X3_T, CN_FMT_F32_W16, CN_FMT_F32_W16_T = 0, 1, 2, 3, 4
+FORMATS = {"f32": CN_FMT_F32, "bf16x3": CN_FMT_BF16X3, "bf16x3_t": CN_FMT_BF16X3_T, "f32_w16": CN_FMT_F32_W16,
+           "f32_w16_t": CN_FMT_F32_W16_T}
 
 
 def kernel_format(precision: str) -> str:
@@ -71,6 +72,11 @@ SIGNATURES = {
                                    _fp, _fp, _p, ctypes.POINTER(_p), _p, _p, _p, _p, _p]),
     "cn_field_mask_words": (_i64, [_i64]),
     "cn_radiance_field_masks": (_i, [_p, _p, _p, _i64, _p, _p, _p, _p, _i64, _i64, _i64, _fp, _fp, _p, _p, _p]),
+    "cn_field_mask_words_fmt": (_i64, [_i, _i64]),
+    "cn_radiance_field_masks_fmt": (_i, [_i, _p, _p, _p, _i64, _p, _p, _p, _p, _i64, _i64, _i64, _fp, _fp, _p, _p,
+                                         _p]),
+    "cn_field_backward_fused": (_i, [_i, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p, _i64, _fp, _fp, _p, _p,
+                                     _p, _p, _p]),
     "cn_field_backward_x3": (_i, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p, _i64, _fp, _fp, _p, _p, _p, _p,
                                   _p]),
     "cn_code_bias_backward": (_i, [ctypes.POINTER(_p), _p, _p, _i64, _p, _p, _p, ctypes.POINTER(_p), _p]),

@@ -189,10 +189,10 @@ class RadianceField(torch.autograd.Function):
     Inputs: rd (R,3), pts (R,S,3) or (ro (R,3), z (R,S)), code rows z_s/z_t (n_codes, 256),
     then the 18 parameters in state_dict order.  Output raw (R, S, 4).
 
-    With frozen weights (the eval step) and a bf16x3 model the forward is the
-    3xbf16 field kernel writing ReLU masks and the backward ONE fused kernel
-    (cn_field_backward_x3); otherwise the fp32 training kernel keeps the
-    activations for the layer-wise backward (weight gradients).
+    With frozen weights (the eval step) the forward is the field kernel of the model's
+    precision writing ReLU masks and the backward ONE fused kernel (cn_field_backward_fused:
+    fp32 16x16x4 for "f32", 3xbf16 for "bf16x3"); with weight gradients the fp32
+    training kernel keeps the activations for the layer-wise backward.
     """
 
     @staticmethod
@@ -200,13 +200,14 @@ class RadianceField(torch.autograd.Function):
         params = [p.detach() for p in params]
         cb = ops.code_bias(params, z_s, z_t)
         n_rays = rd.shape[0]
-        fused = (meta.precision == "bf16x3" and not any(ctx.needs_input_grad[7:])
-                 and ops.fused_backward_supported(z_s.shape[0], meta.n_samples, meta.code_index))
+        fused = (meta.precision in ("bf16x3", "f32") and not any(ctx.needs_input_grad[7:])
+                 and ops.fused_backward_supported(z_s.shape[0], meta.n_samples, meta.code_index, meta.precision))
         ctx.fused = fused
         if fused:
-            raw, masks = ops.radiance_field_masks(ops.mlp_pack(params, "bf16x3"), cb, rd, meta.n_samples,
+            pack = "bf16x3" if meta.precision == "bf16x3" else "f32_w16"
+            raw, masks = ops.radiance_field_masks(ops.mlp_pack(params, pack), cb, rd, meta.n_samples,
                                                   meta.chunk_rows, meta.fx, meta.fd, pts=pts, ro=ro, z=z,
-                                                  code_index=meta.code_index)
+                                                  code_index=meta.code_index, precision=meta.precision)
             ctx.masks = masks
             ctx.meta = meta
             ctx.save_for_backward(rd, pts, ro, z, z_s, z_t, *params)
@@ -226,10 +227,11 @@ class RadianceField(torch.autograd.Function):
         meta = ctx.meta
         if ctx.fused:
             want_z = needs[5] or needs[6]
-            r = ops.field_backward_x3(ops.mlp_pack(params, "bf16x3_t"), ctx.masks, g_raw.contiguous(), rd.shape[0],
+            pack_t = "bf16x3_t" if meta.precision == "bf16x3" else "f32_w16_t"
+            r = ops.field_backward_x3(ops.mlp_pack(params, pack_t), ctx.masks, g_raw.contiguous(), rd.shape[0],
                                       meta.n_samples, meta.chunk_rows, z_s.shape[0], meta.fx, meta.fd, rd=rd,
                                       pts=pts, ro=ro, z=z, code_index=meta.code_index, want_pts=needs[2],
-                                      want_ro=needs[3], want_rd=needs[1])
+                                      want_ro=needs[3], want_rd=needs[1], precision=meta.precision)
             dz_s = dz_t = None
             if want_z:
                 dz_s, dz_t = ops.code_bias_backward(params, z_s, z_t, r["g_code"], None, want_z=True)

@@ -575,8 +575,11 @@ def ray_points_backward(g_pts: Tensor, z: Tensor, want_ro: bool = True, want_rd:
 def radiance_field_masks(packed: Tensor, cb: Tensor, rd: Tensor, n_samples: int, chunk_rows: int,
                          freqs_xyz: Sequence[float], freqs_dir: Sequence[float], pts: Optional[Tensor] = None,
                          ro: Optional[Tensor] = None, z: Optional[Tensor] = None,
-                         code_index: Optional[Tensor] = None) -> Tuple[Tensor, Tensor]:
-    """3xbf16 radiance_field that also writes the ReLU masks -> raw (R,S,4), masks (uint32 words as int32)."""
+                         code_index: Optional[Tensor] = None, precision: str = "bf16x3") -> Tuple[Tensor, Tensor]:
+    """radiance_field that also writes the ReLU masks of the fused backward -> raw (R,S,4), masks (uint32
+    words as int32).  precision "bf16x3" (packed "bf16x3") or "f32" (packed "f32_w16": the fp32
+    16x16x4 kernel)."""
+    fmt = _lib.CN_FMT_BF16X3 if precision == "bf16x3" else _lib.CN_FMT_F32_W16
     lib = _lib_ready()
     rd = _cuda(rd, "rd")
     n = rd.shape[0]
@@ -590,25 +593,28 @@ def radiance_field_masks(packed: Tensor, cb: Tensor, rd: Tensor, n_samples: int,
         code_index = _cuda(code_index, "code_index", torch.int64)
     m = n * n_samples
     raw = torch.empty(n, n_samples, 4, device=rd.device, dtype=torch.float32)
-    masks = torch.empty(int(lib.cn_field_mask_words(m)), device=rd.device, dtype=torch.int32)
-    check(lib.cn_radiance_field_masks(ptr(packed), ptr(cb), ptr(code_index), cb.shape[0], ptr(pts), ptr(ro), ptr(rd),
-                                      ptr(z), n, n_samples, chunk_rows, _lib.host_floats(freqs_xyz),
-                                      _lib.host_floats(freqs_dir), ptr(raw), ptr(masks), stream_of(rd)),
-          "cn_radiance_field_masks")
+    masks = torch.empty(int(lib.cn_field_mask_words_fmt(fmt, m)), device=rd.device, dtype=torch.int32)
+    check(lib.cn_radiance_field_masks_fmt(fmt, ptr(packed), ptr(cb), ptr(code_index), cb.shape[0], ptr(pts), ptr(ro),
+                                          ptr(rd), ptr(z), n, n_samples, chunk_rows, _lib.host_floats(freqs_xyz),
+                                          _lib.host_floats(freqs_dir), ptr(raw), ptr(masks), stream_of(rd)),
+          "cn_radiance_field_masks_fmt")
     return raw, masks
 
 
-def fused_backward_supported(n_codes: int, n_samples: int, code_index: Optional[Tensor] = None) -> bool:
-    """cn_field_backward_x3 needs one code row per 32 consecutive samples."""
-    return n_codes == 1 or n_samples % 32 == 0
+def fused_backward_supported(n_codes: int, n_samples: int, code_index: Optional[Tensor] = None,
+                             precision: str = "bf16x3") -> bool:
+    """cn_field_backward_fused needs one code row per wave: 32 consecutive samples (bf16x3) or 16 (f32)."""
+    return n_codes == 1 or n_samples % (32 if precision == "bf16x3" else 16) == 0
 
 
 def field_backward_x3(packed_t: Tensor, masks: Tensor, d_raw: Tensor, n_rays: int, n_samples: int,
                       chunk_rows: int, n_codes: int, freqs_xyz: Sequence[float], freqs_dir: Sequence[float],
                       rd: Tensor, pts: Optional[Tensor] = None, ro: Optional[Tensor] = None,
                       z: Optional[Tensor] = None, code_index: Optional[Tensor] = None, want_pts: bool = False,
-                      want_ro: bool = False, want_rd: bool = False):
-    """Fused backward of forward_pass + CodeNeRFModel.forward (frozen weights) -> g_code / d_pts / d_ro / d_rd."""
+                      want_ro: bool = False, want_rd: bool = False, precision: str = "bf16x3"):
+    """Fused backward of forward_pass + CodeNeRFModel.forward (frozen weights) -> g_code / d_pts / d_ro / d_rd.
+    precision "bf16x3" (packed_t "bf16x3_t") or "f32" (packed_t "f32_w16_t", masks of the f32_w16 forward)."""
+    fmt_t = _lib.CN_FMT_BF16X3_T if precision == "bf16x3" else _lib.CN_FMT_F32_W16_T
     lib = _lib_ready()
     m = n_rays * n_samples
     d_raw = _cuda(d_raw, "d_raw")
@@ -621,10 +627,10 @@ def field_backward_x3(packed_t: Tensor, masks: Tensor, d_raw: Tensor, n_rays: in
     d_pts = torch.empty(n_rays, n_samples, 3, device=dev, dtype=torch.float32) if want_pts else None
     d_ro = torch.zeros(n_rays, 3, device=dev, dtype=torch.float32) if want_ro else None
     d_rd = torch.zeros(n_rays, 3, device=dev, dtype=torch.float32) if want_rd else None
-    check(lib.cn_field_backward_x3(ptr(packed_t), ptr(masks), ptr(d_raw), ptr(pts), ptr(ro), ptr(rd), ptr(z),
-                                   n_rays, n_samples, chunk_rows, ptr(code_index), n_codes,
-                                   _lib.host_floats(freqs_xyz), _lib.host_floats(freqs_dir), ptr(g_code),
-                                   ptr(d_pts), ptr(d_ro), ptr(d_rd), stream_of(d_raw)), "cn_field_backward_x3")
+    check(lib.cn_field_backward_fused(fmt_t, ptr(packed_t), ptr(masks), ptr(d_raw), ptr(pts), ptr(ro), ptr(rd),
+                                      ptr(z), n_rays, n_samples, chunk_rows, ptr(code_index), n_codes,
+                                      _lib.host_floats(freqs_xyz), _lib.host_floats(freqs_dir), ptr(g_code),
+                                      ptr(d_pts), ptr(d_ro), ptr(d_rd), stream_of(d_raw)), "cn_field_backward_fused")
     return {"g_code": g_code, "d_pts": d_pts, "d_ro": d_ro, "d_rd": d_rd}
 
 

@@ -432,7 +432,7 @@ int launch_field(int fmt, int mode, FieldArgs& a, hipStream_t st) {
 }
 
 bool valid_fmt(int fmt) { return fmt == CN_FMT_F32 || fmt == CN_FMT_BF16X3 || fmt == CN_FMT_F32_W16; }
-bool valid_pack_fmt(int fmt) { return valid_fmt(fmt) || fmt == CN_FMT_BF16X3_T; }
+bool valid_pack_fmt(int fmt) { return valid_fmt(fmt) || fmt == CN_FMT_BF16X3_T || fmt == CN_FMT_F32_W16_T; }
 
 }  // namespace
 
@@ -441,7 +441,7 @@ static_assert(kCbStride == CN_CODE_BIAS_STRIDE, "code-bias stride mismatch");
 
 extern "C" int64_t cn_mlp_packed_floats(int fmt) {
   if (!valid_pack_fmt(fmt)) return -1;
-  if (fmt == CN_FMT_F32_W16) return packed_floats_w16();
+  if (fmt == CN_FMT_F32_W16 || fmt == CN_FMT_F32_W16_T) return packed_floats_w16();
   return fmt == CN_FMT_F32 ? kPackedFloats : packed_floats_x3();
 }
 
@@ -451,6 +451,7 @@ extern "C" int cn_mlp_pack(const float* const* params, int fmt, float* packed, c
   if (fmt == CN_FMT_BF16X3) return launch_pack_x3(P, packed, cn::as_stream(stream));
   if (fmt == CN_FMT_BF16X3_T) return launch_pack_x3t(P, packed, cn::as_stream(stream));
   if (fmt == CN_FMT_F32_W16) return launch_pack_w16(P, packed, cn::as_stream(stream));
+  if (fmt == CN_FMT_F32_W16_T) return launch_pack_w16t(P, packed, cn::as_stream(stream));
   hipLaunchKernelGGL(pack_kernel, dim3(cn::elementwise_grid(kPackedFloats, 256)), dim3(256), 0,
                      cn::as_stream(stream), P, packed);
   return cn::launch_status();
@@ -562,11 +563,28 @@ extern "C" int cn_mlp_forward_train(const float* packed, const float* code_bias,
 
 extern "C" int64_t cn_field_mask_words(int64_t m) { return m > 0 ? mask_words_x3(m) : -1; }
 
+extern "C" int64_t cn_field_mask_words_fmt(int fmt, int64_t m) {
+  if (m <= 0) return -1;
+  if (fmt == CN_FMT_BF16X3) return mask_words_x3(m);
+  if (fmt == CN_FMT_F32_W16) return mask_words_w16(m);
+  return -1;
+}
+
 extern "C" int cn_radiance_field_masks(const float* packed, const float* code_bias, const int64_t* code_index,
                                        int64_t n_codes, const float* pts, const float* ro, const float* rd,
                                        const float* z, int64_t n_rays, int64_t n_samples, int64_t chunk_rows,
                                        const float* freqs_xyz, const float* freqs_dir, float* raw, uint32_t* masks,
                                        cn_stream_t stream) {
+  return cn_radiance_field_masks_fmt(CN_FMT_BF16X3, packed, code_bias, code_index, n_codes, pts, ro, rd, z, n_rays,
+                                     n_samples, chunk_rows, freqs_xyz, freqs_dir, raw, masks, stream);
+}
+
+extern "C" int cn_radiance_field_masks_fmt(int fmt, const float* packed, const float* code_bias,
+                                           const int64_t* code_index, int64_t n_codes, const float* pts,
+                                           const float* ro, const float* rd, const float* z, int64_t n_rays,
+                                           int64_t n_samples, int64_t chunk_rows, const float* freqs_xyz,
+                                           const float* freqs_dir, float* raw, uint32_t* masks, cn_stream_t stream) {
+  CN_CHECK_ARG(fmt == CN_FMT_BF16X3 || fmt == CN_FMT_F32_W16);
   CN_CHECK_ARG(packed && code_bias && rd && raw && masks && freqs_xyz && freqs_dir);
   CN_CHECK_ARG(n_rays > 0 && n_samples > 0 && chunk_rows > 0 && n_codes > 0);
   CN_CHECK_ARG(pts || (ro && z));
@@ -589,7 +607,8 @@ extern "C" int cn_radiance_field_masks(const float* packed, const float* code_bi
   for (int i = 0; i < 4; ++i) a.fd[i] = freqs_dir[i];
   a.raw = raw;
   a.masks = masks;
-  return launch_field_x3(pts ? kFromPts : kFromRayZ, a, cn::as_stream(stream));
+  return fmt == CN_FMT_BF16X3 ? launch_field_x3(pts ? kFromPts : kFromRayZ, a, cn::as_stream(stream))
+                              : launch_field_w16(pts ? kFromPts : kFromRayZ, a, cn::as_stream(stream));
 }
 
 extern "C" int cn_field_backward_x3(const float* packed_t, const uint32_t* masks, const float* d_raw,
@@ -598,14 +617,32 @@ extern "C" int cn_field_backward_x3(const float* packed_t, const uint32_t* masks
                                     const int64_t* code_index, int64_t n_codes, const float* freqs_xyz,
                                     const float* freqs_dir, float* g_code, float* d_pts, float* d_ro, float* d_rd,
                                     cn_stream_t stream) {
+  return cn_field_backward_fused(CN_FMT_BF16X3_T, packed_t, masks, d_raw, pts, ro, rd, z, n_rays, n_samples,
+                                 chunk_rows, code_index, n_codes, freqs_xyz, freqs_dir, g_code, d_pts, d_ro, d_rd,
+                                 stream);
+}
+
+// Debug hook for tools/debug_w16_bwd.py (not part of the ABI header): when set, the fp32 fused
+// backward dumps its intermediate gradients there ((6, M, 256) floats).
+static float* cn_debug_buffer = nullptr;
+extern "C" void cn_debug_set_buffer(float* p) { cn_debug_buffer = p; }
+
+extern "C" int cn_field_backward_fused(int fmt_t, const float* packed_t, const uint32_t* masks, const float* d_raw,
+                                       const float* pts, const float* ro, const float* rd, const float* z,
+                                       int64_t n_rays, int64_t n_samples, int64_t chunk_rows,
+                                       const int64_t* code_index, int64_t n_codes, const float* freqs_xyz,
+                                       const float* freqs_dir, float* g_code, float* d_pts, float* d_ro,
+                                       float* d_rd, cn_stream_t stream) {
+  CN_CHECK_ARG(fmt_t == CN_FMT_BF16X3_T || fmt_t == CN_FMT_F32_W16_T);
   CN_CHECK_ARG(packed_t && masks && d_raw && rd && g_code && freqs_xyz && freqs_dir);
   CN_CHECK_ARG(n_rays > 0 && n_samples > 0 && chunk_rows > 0 && n_codes > 0);
   CN_CHECK_ARG(pts || (ro && z));
   CN_CHECK_ARG(!d_pts || pts);
   CN_CHECK_ARG(!d_ro || (ro && z && !pts));
   CN_CHECK_ARG(code_index || n_codes == 1 || n_codes == n_rays);
-  // one code row per 32-sample wave: a single code, or every wave inside one ray
-  if (!(n_codes == 1 || n_samples % 32 == 0)) return CN_EUNSUPPORTED;
+  // one code row per wave (32 samples x3, 16 samples w16): a single code, or every wave inside one ray
+  const int wave_samples = fmt_t == CN_FMT_BF16X3_T ? 32 : 16;
+  if (!(n_codes == 1 || n_samples % wave_samples == 0)) return CN_EUNSUPPORTED;
   FieldArgs a = {};
   a.packed = packed_t;
   a.code_index = code_index;
@@ -627,5 +664,7 @@ extern "C" int cn_field_backward_x3(const float* packed_t, const uint32_t* masks
   a.d_pts = d_pts;
   a.d_ro = d_ro;
   a.d_rd = d_rd;
-  return launch_field_x3_bwd(pts ? kFromPts : kFromRayZ, a, cn::as_stream(stream));
+  a.save = cn_debug_buffer;  // tools/debug_w16_bwd.py only (NULL otherwise)
+  return fmt_t == CN_FMT_BF16X3_T ? launch_field_x3_bwd(pts ? kFromPts : kFromRayZ, a, cn::as_stream(stream))
+                                  : launch_field_w16_bwd(pts ? kFromPts : kFromRayZ, a, cn::as_stream(stream));
 }

@@ -124,7 +124,10 @@ int launch_field_x3_bwd(int mode, FieldArgs& a, hipStream_t st);
 // fp32 16x16x4 two-waves-per-SIMD variant (mlp_f32.hip): inference forward.
 int64_t packed_floats_w16();
 int launch_pack_w16(const Params& P, float* packed, hipStream_t st);
-int launch_field_w16(int mode, FieldArgs& a, hipStream_t st);
+int launch_field_w16(int mode, FieldArgs& a, hipStream_t st);  // a.masks: also the ReLU masks
+int64_t mask_words_w16(int64_t m);
+int launch_pack_w16t(const Params& P, float* packed, hipStream_t st);
+int launch_field_w16_bwd(int mode, FieldArgs& a, hipStream_t st);
 
 // Pre-encoded rows: the same 2P+2 values gathered from x (base = column offset).
 template <int P, int T = 0>

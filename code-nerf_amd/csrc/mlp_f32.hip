@@ -141,6 +141,7 @@ struct State {
   floatx4 act[16];   // layer input: block ob register r = input feature 16 ob + 4 g + r
   floatx4 acc[16];   // layer output accumulators
   floatx4 pre[4];    // the next chunk's first A fragments (read during this chunk's last k-step)
+  floatx4 acc2[4];   // backward: the narrow chunks' accumulators (2 blocks x 2 chains)
   float denc[8];     // view-direction encoding, k-steps of the view-dir chunk
   float sig;         // sigma partial (this lane group's 64 features)
   int lane, g, wave;
@@ -277,7 +278,32 @@ __device__ __forceinline__ void bias_code(State& s, const FieldArgs& a, const fl
   }
 }
 
-template <int MODE>
+// ReLU masks for the fused backward: 4 layers (h1, h2, v1, v2) x 64 bits per lane (bit 4 ob + r
+// of feature 16 ob + 4 g + r: pre-activation > 0), one 8-B store per lane per layer.
+constexpr int kMaskLayers = 4;
+constexpr int kMaskWordsPerTile = kWaves * kMaskLayers * 64 * 2;
+
+// act = relu(acc); MASKS: also store the layer's mask bits (slot ml of the tile's mask block).
+template <bool MASKS>
+__device__ __forceinline__ void relu_act(State& s, const FieldArgs& a, int64_t tile, int ml) {
+  unsigned w0 = 0, w1 = 0;
+#pragma unroll
+  for (int ob = 0; ob < 16; ++ob)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float v = s.acc[ob][r];
+      s.act[ob][r] = fmaxf(v, 0.0f);
+      if constexpr (MASKS) {
+        const unsigned bit = v > 0.0f ? 1u : 0u;
+        if (ob < 8) w0 |= bit << (4 * ob + r);
+        else w1 |= bit << (4 * (ob - 8) + r);
+      }
+    }
+  if constexpr (MASKS)
+    reinterpret_cast<uint2*>(a.masks)[((tile * kWaves + s.wave) * kMaskLayers + ml) * 64 + s.lane] = make_uint2(w0, w1);
+}
+
+template <int MODE, bool MASKS>
 __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4* lds, float* clds, float* crow_lds,
                                           int64_t tile, int& c) {
   const int64_t row = tile * kTile + s.wave * 16 + (s.lane & 15);
@@ -358,10 +384,7 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
 #pragma unroll
       for (int ob = 0; ob < 16; ++ob) s.act[ob] = s.acc[ob];
     } else {
-#pragma unroll
-      for (int ob = 0; ob < 16; ++ob)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) s.act[ob][r] = fmaxf(s.acc[ob][r], 0.0f);
+      relu_act<MASKS>(s, a, tile, layer == kXyz2 ? 0 : (layer == kOut ? 1 : 2));
     }
     if (layer == kOut) {
       // sigma = fc_out row 0 . [h2, zs2] + b: the h2 part here, the code part from cn_code_bias
@@ -386,10 +409,7 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
   }
 
   // ---- fc_rgb (256 -> 3): one chunk, 64 k-steps of block 0 in 4 chains
-#pragma unroll
-  for (int ob = 0; ob < 16; ++ob)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) s.act[ob][r] = fmaxf(s.acc[ob][r], 0.0f);
+  relu_act<MASKS>(s, a, tile, 3);
   {
     float b0 = 0.0f, b1 = 0.0f, b2 = 0.0f, bs = 0.0f;
     if (s.uniform_code) {
@@ -456,7 +476,7 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
   }
 }
 
-template <int MODE>
+template <int MODE, bool MASKS>
 __global__ __launch_bounds__(kThreads, 2) void field_w16_kernel(FieldArgs a) {
   // ONE LDS object (a second one makes hipcc wait vmcnt(0) before ring reads): the DMA
   // ring, then the constants, then one code-bias row per wave
@@ -484,11 +504,425 @@ __global__ __launch_bounds__(kThreads, 2) void field_w16_kernel(FieldArgs a) {
   int c = 0;
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
     c = 0;
-    field_tile<MODE>(s, a, lds, clds, crow_lds, tile, c);
+    field_tile<MODE, MASKS>(s, a, lds, clds, crow_lds, tile, c);
   }
   // the last tile prefetched chunks 0..2 of a tile that does not exist: they must land
   // before the workgroup's LDS is released
   __builtin_amdgcn_s_waitcnt(0x0F70);
+}
+
+
+// ================================================================ fused backward
+// The eval-step backward (frozen weights) of forward_pass + CodeNeRFModel.forward
+// (nerf/__init__.py:94-134, model.py:160-194) in fp32 (exact products, the reference's
+// arithmetic): from d raw (m, 4) to the per-code sums g_code and the ray gradients, in one
+// persistent launch on the forward's machinery.  dX = dPre . W is D = W^T . dPre^T: A = W^T
+// streamed through the same ring (the transposed pack CN_FMT_F32_W16_T, again 36 chunks),
+// B = the masked gradients in registers (a layer's D layout is the next layer's B layout, as
+// in the forward).  The ReLU masks come from the forward (field_w16_kernel<.., true>).
+// Chunk schedule:
+//   0      fc_rgb^T      d v2   = Wr[:, :256]^T d rgb                 (k-step 0 real)
+//   1-8    layer_dir2^T  d v1   = Wd2^T (m_v2 . d v2)
+//   9-16   layer_dir1^T  d feat = Wd1[:, :256]^T (m_v1 . d v1)
+//   17     layer_dir1^T  d dir  = Wd1[:, 256:]^T (m_v1 . d v1)        (narrow: 2 blocks x 64 k-steps)
+//   18-25  fc_out^T      d h2   = Wo[1:, :256]^T d feat + Wo[0, :256] d sigma (sigma term by VALU)
+//   26-33  layer_xyz2^T  d h1   = Wx2[:, :256]^T (m_h2 . d h2)
+//   34-35  layer_xyz1^T  d enc  = Wx1^T (m_h1 . d h1)                  (narrow: blocks 0-1, 2-3)
+// A narrow chunk keeps the wide chunk's memory layout [k-step][q][lane][j] with q = (block
+// b = q >> 1, half = q & 1) and k-step 8 T + 4 half + j, so it runs the same 8-step schedule.
+// The narrow outputs are ordered like the forward's encoding k-steps (col_enc_xyz /
+// col_enc_dir), so each lane group back-propagates through the sin/cos pairs it owns.
+// g_code = per code row sum over its samples of [m_h2 . d h2 | d feat | d sigma | d rgb]
+// (cn_code_bias layout): 16-lane DPP sums + LDS float atomics into one row per wave, flushed
+// to global atomics when the wave's code row changes.
+
+constexpr int kTRgb = 0, kTDir2 = 1, kTDir1 = 9, kTDDir = 17, kTOut = 18, kTXyz2 = 26, kTXyz1 = 34;
+constexpr int kTSig = 0;  // transposed-pack constants: fc_out row 0 over h2, [g][ob][r]
+// LDS after the ring: constants, one g_code row per wave
+constexpr int kBGacc = kConsts;
+constexpr int kBwdLdsFloats = kBGacc + kWaves * kCbStride;
+constexpr int kBwdLdsQuads = kRing * kChunkQuads + kBwdLdsFloats / 4;
+static_assert(kBwdLdsQuads * 16 <= 160 * 1024, "LDS budget (backward)");
+static_assert(kTXyz1 + 2 == kChunks, "backward chunk schedule");
+
+__global__ void pack_w16t_kernel(Params P, float* __restrict__ packed) {
+  constexpr int kX2 = kHidden + kCode, kD1 = kCode + kDimDir;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < kPackedFloats; idx += gridDim.x * blockDim.x) {
+    float v = 0.0f;
+    if (idx >= kStreamFloats) {
+      const int t = idx - kStreamFloats;
+      if (t < 256) {
+        const int g = t >> 6, ob = (t >> 2) & 15, r = t & 3;
+        v = P.p[kWOut][16 * ob + 4 * g + r];  // fc_out row 0, h2 feature 16 ob + 4 g + r
+      }
+    } else {
+      const int c = idx / (kChunkQuads * 4), rem = idx % (kChunkQuads * 4);
+      const int st = rem / (kStepQuads * 4), q = (rem % (kStepQuads * 4)) / 256;
+      const int lane = (rem % 256) / 4, j = rem % 4;
+      const int i = lane & 15, g = lane >> 4;
+      if (c == kTDDir || c >= kTXyz1) {
+        const int b = q >> 1, t = 8 * st + 4 * (q & 1) + j;
+        const int kin = col_acc(t, g);
+        if (c == kTDDir) {
+          const int e = col_enc_dir(4 * b + (i & 3), i >> 2);
+          if (e >= 0) v = P.p[kWDir1][kin * kD1 + kCode + e];
+        } else {
+          const int bb = 2 * (c - kTXyz1) + b;
+          const int col = col_enc_xyz(4 * bb + (i & 3), i >> 2);
+          if (col >= 0) v = P.p[kWXyz1][kin * kDimXyz + col];
+        }
+      } else {
+        const int row = 16 * (4 * q + j) + i;  // backward output = forward input feature
+        if (c == kTRgb) {
+          if (st == 0 && g < 3) v = P.p[kWRgb][g * kX2 + row];
+        } else {
+          // W^T[row][kin] = W[roff + kin][row] of the layer this chunk belongs to
+          const float* W;
+          int first, ld, roff = 0;
+          if (c < kTDir1) {
+            W = P.p[kWDir2], first = kTDir2, ld = kHidden;
+          } else if (c < kTDDir) {
+            W = P.p[kWDir1], first = kTDir1, ld = kD1;
+          } else if (c < kTXyz2) {
+            W = P.p[kWOut], first = kTOut, ld = kX2, roff = 1;
+          } else {
+            W = P.p[kWXyz2], first = kTXyz2, ld = kX2;
+          }
+          const int kin = col_acc(8 * (c - first) + st, g);
+          v = W[(roff + kin) * ld + row];
+        }
+      }
+    }
+    packed[idx] = v;
+  }
+}
+
+// Sum over each row of 16 lanes (the 16 samples of one lane group); lane 16 g + 15 holds it.
+__device__ __forceinline__ float sum16(float x) {
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x111, 0xF, 0xF, true));  // row_shr:1
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x112, 0xF, 0xF, true));  // row_shr:2
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x114, 0xF, 0xF, true));  // row_shr:4
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x118, 0xF, 0xF, true));  // row_shr:8
+  return x;
+}
+
+// g_code[col + 16 ob + 4 g + r] += sum over the wave's samples of v[ob][r] (all 64 features of
+// this lane group); row = this wave's g_code row in LDS.
+__device__ __forceinline__ void gcode_add64(const State& s, float* row, int col, const floatx4* v) {
+  const bool holder = (s.lane & 15) == 15;
+  float* base = row + col + 4 * s.g;
+#pragma unroll
+  for (int ob = 0; ob < 16; ++ob)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float t = sum16(v[ob][r]);
+      if (holder) atomicAdd(base + 16 * ob + r, t);
+    }
+}
+
+// act = acc where the mask bit is set, else +0 (torch's relu backward: grad * (pre > 0)).
+__device__ __forceinline__ void mask_act(State& s, uint2 m) {
+#pragma unroll
+  for (int ob = 0; ob < 16; ++ob) {
+    const unsigned w = ob < 8 ? m.x : m.y;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const unsigned keep = static_cast<unsigned>(__builtin_amdgcn_sbfe(static_cast<int>(w), 4 * (ob & 7) + r, 1));
+      s.act[ob][r] = __uint_as_float(__float_as_uint(s.acc[ob][r]) & keep);
+    }
+  }
+}
+
+__device__ __forceinline__ void zero_acc(State& s) {
+#pragma unroll
+  for (int ob = 0; ob < 16; ++ob) s.acc[ob] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+}
+
+// fc_rgb^T: only k-step 0 of chunk c is real; the chunk's barrier and DMA, then its 16 MFMAs.
+__device__ __forceinline__ void chunk_k0(State& s, float4* lds, int c, float b) {
+  const float4* nslot = lds + ((c + 1) & (kRing - 1)) * kChunkQuads + s.lane;
+  floatx4 a0[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) a0[q] = s.pre[q];
+  __builtin_amdgcn_sched_barrier(0);
+  chunk_barrier();
+  dma_chunk(s, lds, c + 3);
+  read_a<0>(nslot, s.pre);
+  mfma_step(s, a0, b);
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// A narrow step: blocks b = q >> 1 of k-steps 8 T + 4 (q & 1) + j, four independent chains.
+template <int T>
+__device__ __forceinline__ void mfma_narrow(State& s, const floatx4* a) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      s.acc2[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q][j], s.act[2 * T + (q & 1)][j], s.acc2[q], 0, 0, 0);
+}
+
+// A narrow chunk (2 blocks x 64 k-steps, B from s.act) into s.acc2, on chunk16's schedule.
+__device__ __forceinline__ void chunk_narrow(State& s, float4* lds, int c) {
+  const float4* slot = lds + (c & (kRing - 1)) * kChunkQuads + s.lane;
+  const float4* nslot = lds + ((c + 1) & (kRing - 1)) * kChunkQuads + s.lane;
+  floatx4 a0[4], a1[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) a0[q] = s.pre[q];
+  __builtin_amdgcn_sched_barrier(0);
+#define CN_NSTEP(T, CUR, NXT)                                        \
+  {                                                                 \
+    if constexpr ((T) + 1 < 8) read_a<(T) + 1>(slot, NXT);          \
+    else read_a<0>(nslot, s.pre);                                   \
+    mfma_narrow<(T)>(s, CUR);                                       \
+    step_pattern();                                                 \
+    __builtin_amdgcn_sched_barrier(0);                              \
+    if constexpr ((T) == 3) {                                       \
+      chunk_barrier();                                              \
+      dma_chunk(s, lds, c + 3);                                     \
+    }                                                               \
+  }
+  CN_NSTEP(0, a0, a1)
+  CN_NSTEP(1, a1, a0)
+  CN_NSTEP(2, a0, a1)
+  CN_NSTEP(3, a1, a0)
+  CN_NSTEP(4, a0, a1)
+  CN_NSTEP(5, a1, a0)
+  CN_NSTEP(6, a0, a1)
+  CN_NSTEP(7, a1, a0)
+#undef CN_NSTEP
+}
+
+// Flush this wave's g_code row (LDS) into g_code[code] and zero it.
+__device__ __forceinline__ void flush_gcode(const State& s, const FieldArgs& a, float* row, int code) {
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS atomics landed
+#pragma unroll
+  for (int k = 0; k < (kCbStride + 63) / 64; ++k) {
+    const int j = s.lane + 64 * k;
+    if (j < kCbStride) {
+      const float v = row[j];
+      if (v != 0.0f) atomicAdd(a.g_code + (int64_t)code * kCbStride + j, v);
+      row[j] = 0.0f;
+    }
+  }
+}
+
+// Debug dump (a.save non-NULL, tools/debug_w16_bwd.py): the accumulators of one backward stage
+// as (M, 256) rows, feature 16 ob + 4 g + r.
+__device__ __forceinline__ void dbg_acc(const State& s, const FieldArgs& a, int stage, int64_t row, bool valid) {
+  if (!a.save || !valid) return;
+  float* d = a.save + ((int64_t)stage * a.m + row) * 256 + 4 * s.g;
+#pragma unroll
+  for (int ob = 0; ob < 16; ++ob)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) d[16 * ob + r] = s.acc[ob][r];
+}
+
+template <int MODE>
+__device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* lds, float* grow, int64_t tile,
+                                        int& cur_code) {
+  const int64_t row = tile * kTile + s.wave * 16 + (s.lane & 15);
+  const bool valid = row < a.m;
+  const int64_t rc = valid ? row : a.m - 1;
+  const float* clds = reinterpret_cast<const float*>(lds + kRing * kChunkQuads);
+
+  // ---- inputs: sample, d raw, masks (h1, h2, v1, v2), code row (wave-uniform: host-checked)
+  const SampleIn in = decode_sample<MODE>(a, rc);
+  const int crow = __builtin_amdgcn_readfirstlane(static_cast<int>(code_row(a, in.code_of)));
+  float4 dr = reinterpret_cast<const float4*>(a.d_raw)[rc];
+  const float zv = MODE == kFromRayZ ? a.z[rc] : 0.0f;
+  uint2 mk[kMaskLayers];
+#pragma unroll
+  for (int l = 0; l < kMaskLayers; ++l)
+    mk[l] = reinterpret_cast<const uint2*>(a.masks)[((tile * kWaves + s.wave) * kMaskLayers + l) * 64 + s.lane];
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  if (!valid) dr = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (crow != cur_code) {
+    if (cur_code >= 0) flush_gcode(s, a, grow, cur_code);
+    cur_code = crow;
+  }
+  // g_code sigma / rgb (lane group 0 carries the wave's 16 samples)
+  {
+    const float t0 = sum16(dr.w), t1 = sum16(dr.x), t2 = sum16(dr.y), t3 = sum16(dr.z);
+    if (s.lane == 15) {
+      atomicAdd(grow + kCbSigma, t0);
+      atomicAdd(grow + kCbRgb, t1);
+      atomicAdd(grow + kCbRgb + 1, t2);
+      atomicAdd(grow + kCbRgb + 2, t3);
+    }
+  }
+  int c = 0;
+  // ---- fc_rgb^T (chunk 0): B = d rgb channel g at k-step 0
+  zero_acc(s);
+  chunk_k0(s, lds, c, s.g == 0 ? dr.x : (s.g == 1 ? dr.y : (s.g == 2 ? dr.z : 0.0f)));
+  c = kTDir2;
+  dbg_acc(s, a, 0, row, valid);
+  // ---- layer_dir2^T (m_v2), layer_dir1^T (m_v1)
+  mask_act(s, mk[3]);
+  zero_acc(s);
+  __builtin_amdgcn_sched_barrier(0);
+  layer256(s, lds, c);
+  dbg_acc(s, a, 1, row, valid);
+  mask_act(s, mk[2]);
+  zero_acc(s);
+  __builtin_amdgcn_sched_barrier(0);
+  layer256(s, lds, c);
+  dbg_acc(s, a, 2, row, valid);
+  // ---- the view-direction rows of layer_dir1^T (narrow chunk, B = m_v1 . d v1 still in act)
+#pragma unroll
+  for (int q = 0; q < 4; ++q) s.acc2[q] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+  chunk_narrow(s, lds, c);
+  c += 1;
+  float gdir[8];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    gdir[r] = s.acc2[0][r] + s.acc2[1][r];
+    gdir[4 + r] = s.acc2[2][r] + s.acc2[3][r];
+  }
+  // ---- fc_out^T: B = d feat (no activation), init = fc_out row 0 (h2 part) x d sigma
+#pragma unroll
+  for (int ob = 0; ob < 16; ++ob) s.act[ob] = s.acc[ob];
+  gcode_add64(s, grow, kCbFeat, s.act);
+#pragma unroll
+  for (int ob = 0; ob < 16; ++ob) {
+    const floatx4 w = *reinterpret_cast<const floatx4*>(clds + kTSig + 64 * s.g + 4 * ob);
+    s.acc[ob] = w * dr.w;
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  layer256(s, lds, c);
+  dbg_acc(s, a, 3, row, valid);
+  // ---- layer_xyz2^T (m_h2): its masked input gradient is the code term's too
+  mask_act(s, mk[1]);
+  gcode_add64(s, grow, kCbXyz2, s.act);
+  zero_acc(s);
+  __builtin_amdgcn_sched_barrier(0);
+  layer256(s, lds, c);
+  dbg_acc(s, a, 4, row, valid);
+  // ---- layer_xyz1^T (m_h1): encoding k-steps 0-7, then 8-15
+  mask_act(s, mk[0]);
+  float genc[16];
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s.acc2[q] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+    chunk_narrow(s, lds, c);
+    c += 1;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      genc[8 * half + r] = s.acc2[0][r] + s.acc2[1][r];
+      genc[8 * half + 4 + r] = s.acc2[2][r] + s.acc2[3][r];
+    }
+  }
+
+  if (a.save && valid) {
+    float* d = a.save + (5 * a.m + row) * 256;
+    for (int t = 0; t < 16; ++t) d[16 * s.g + t] = genc[t];
+    for (int t = 0; t < 8; ++t) d[64 + 8 * s.g + t] = gdir[t];
+  }
+  // ---- encodings -> d pts, d view dir: lane group g owns pairs p = 4 i + g (as the forward)
+  float dx[3] = {0.f, 0.f, 0.f}, dv[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int p = 4 * i + s.g;
+    if (p < 30) {
+      const int d = p % 3, k = p / 3;
+      float sn, cs;
+      sincosf(__fmul_rn(in.x[d], a.fx[k]), &sn, &cs);
+      dx[d] += a.fx[k] * (genc[i] * cs - genc[8 + i] * sn);
+    } else if (s.g == 2) {  // raw inputs x0 (k-step 7), x1 (k-step 15)
+      dx[0] += genc[7];
+      dx[1] += genc[15];
+    } else {                // x2 (k-step 7)
+      dx[2] += genc[7];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int p = 4 * i + s.g, d = p % 3, k = p / 3;
+    float sn, cs;
+    sincosf(__fmul_rn(in.vd[d], a.fd[k]), &sn, &cs);
+    dv[d] += a.fd[k] * (gdir[i] * cs - gdir[3 + i] * sn);
+  }
+  if (s.g < 3) dv[s.g] += gdir[6];
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    dx[d] += __shfl_xor(dx[d], 16);
+    dx[d] += __shfl_xor(dx[d], 32);
+    dv[d] += __shfl_xor(dv[d], 16);
+    dv[d] += __shfl_xor(dv[d], 32);
+  }
+  const int64_t S = a.n_samples;
+  if constexpr (MODE == kFromRayZ) {
+    // pts = ro + rd z (z detached): d ro += d pts, d rd += d pts z.  With S % 16 == 0 the
+    // wave's 16 samples are one ray: sum over them first, one atomic per value.
+    float gro[3], grd[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      gro[d] = valid ? dx[d] : 0.0f;
+      grd[d] = valid ? dx[d] * zv : 0.0f;
+    }
+    const bool one_ray = S % 16 == 0;
+    if (one_ray) {
+#pragma unroll
+      for (int off = 8; off >= 1; off >>= 1)
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+          gro[d] += __shfl_xor(gro[d], off);
+          grd[d] += __shfl_xor(grd[d], off);
+        }
+    }
+    if (valid && s.g == 0 && (!one_ray || s.lane == 0)) {
+      const int64_t ray = rc / S;
+      if (a.d_ro)
+        for (int d = 0; d < 3; ++d) atomicAdd(a.d_ro + 3 * ray + d, gro[d]);
+      if (a.d_rd)
+        for (int d = 0; d < 3; ++d) atomicAdd(a.d_rd + 3 * ray + d, grd[d]);
+    }
+  }
+  if (valid && s.g == 0) {
+    const int64_t ray = rc / S, smp = rc - ray * S;
+    if constexpr (MODE != kFromRayZ) {
+      if (a.d_pts)
+        for (int d = 0; d < 3; ++d) a.d_pts[3 * rc + d] = dx[d];
+    }
+    if (a.d_rd) {
+      // Q1 view direction vd = rd[dray] / |rd[dray]|: d rd[dray] += (g - vd (vd . g)) / |rd[dray]|
+      const int64_t base = (ray / a.chunk_rows) * a.chunk_rows;
+      const int64_t rcnt = min(a.chunk_rows, a.n_rays - base);
+      const int64_t dray = base + ((ray - base) * S + smp) % rcnt;
+      const float d0 = a.rd[3 * dray], d1 = a.rd[3 * dray + 1], d2 = a.rd[3 * dray + 2];
+      const float nrm = sqrtf(d0 * d0 + d1 * d1 + d2 * d2);
+      const float dot = in.vd[0] * dv[0] + in.vd[1] * dv[1] + in.vd[2] * dv[2];
+      for (int d = 0; d < 3; ++d) atomicAdd(a.d_rd + 3 * dray + d, (dv[d] - in.vd[d] * dot) / nrm);
+    }
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kThreads, 2) void field_w16_bwd_kernel(FieldArgs a) {
+  __shared__ __attribute__((aligned(16))) float4 lds[kBwdLdsQuads];
+  float* blds = reinterpret_cast<float*>(lds + kRing * kChunkQuads);
+  State s;
+  s.lane = threadIdx.x & 63;
+  s.g = s.lane >> 4;
+  s.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  s.wsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.packed), 0, kPackedFloats * 4, 0x00020000);
+  s.voff = static_cast<unsigned>(s.wave * 64 + s.lane) * 16u;
+  float* grow = blds + kBGacc + s.wave * kCbStride;
+  for (int k = threadIdx.x; k < kConsts; k += kThreads) blds[k] = a.packed[kStreamFloats + k];
+  for (int k = threadIdx.x; k < kWaves * kCbStride; k += kThreads) blds[kBGacc + k] = 0.0f;
+  __syncthreads();
+  dma_chunk(s, lds, 0);
+  dma_chunk(s, lds, 1);
+  dma_chunk(s, lds, 2);
+  asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  read_a<0>(lds + s.lane, s.pre);
+  int cur_code = -1;
+  const int64_t n_tiles = (a.m + kTile - 1) / kTile;
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) bwd_tile<MODE>(s, a, lds, grow, tile, cur_code);
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  if (cur_code >= 0) flush_gcode(s, a, grow, cur_code);
 }
 
 }  // namespace w16
@@ -514,11 +948,35 @@ int launch_pack_w16(const Params& P, float* packed, hipStream_t st) {
 
 int launch_field_w16(int mode, FieldArgs& a, hipStream_t st) {
   const unsigned grid = static_cast<unsigned>(std::min<int64_t>(cn::ceil_div(a.m, w16::kTile), cu_count_w16()));
-  switch (mode) {
-    case kFromPts: hipLaunchKernelGGL(w16::field_w16_kernel<kFromPts>, dim3(grid), dim3(w16::kThreads), 0, st, a); break;
-    case kFromRayZ: hipLaunchKernelGGL(w16::field_w16_kernel<kFromRayZ>, dim3(grid), dim3(w16::kThreads), 0, st, a); break;
-    default: hipLaunchKernelGGL(w16::field_w16_kernel<kFromEncoded>, dim3(grid), dim3(w16::kThreads), 0, st, a); break;
+  const dim3 b(w16::kThreads);
+  if (a.masks) {
+    if (mode == kFromPts) hipLaunchKernelGGL((w16::field_w16_kernel<kFromPts, true>), dim3(grid), b, 0, st, a);
+    else if (mode == kFromRayZ) hipLaunchKernelGGL((w16::field_w16_kernel<kFromRayZ, true>), dim3(grid), b, 0, st, a);
+    else return CN_EUNSUPPORTED;
+    return cn::launch_status();
   }
+  switch (mode) {
+    case kFromPts: hipLaunchKernelGGL((w16::field_w16_kernel<kFromPts, false>), dim3(grid), b, 0, st, a); break;
+    case kFromRayZ: hipLaunchKernelGGL((w16::field_w16_kernel<kFromRayZ, false>), dim3(grid), b, 0, st, a); break;
+    default: hipLaunchKernelGGL((w16::field_w16_kernel<kFromEncoded, false>), dim3(grid), b, 0, st, a); break;
+  }
+  return cn::launch_status();
+}
+
+int64_t mask_words_w16(int64_t m) { return cn::ceil_div(m, w16::kTile) * w16::kMaskWordsPerTile; }
+
+int launch_pack_w16t(const Params& P, float* packed, hipStream_t st) {
+  hipLaunchKernelGGL(w16::pack_w16t_kernel, dim3(cn::elementwise_grid(w16::kPackedFloats, 256)), dim3(256), 0, st, P,
+                     packed);
+  return cn::launch_status();
+}
+
+int launch_field_w16_bwd(int mode, FieldArgs& a, hipStream_t st) {
+  const unsigned grid = static_cast<unsigned>(std::min<int64_t>(cn::ceil_div(a.m, w16::kTile), cu_count_w16()));
+  const dim3 b(w16::kThreads);
+  if (mode == kFromPts) hipLaunchKernelGGL(w16::field_w16_bwd_kernel<kFromPts>, dim3(grid), b, 0, st, a);
+  else if (mode == kFromRayZ) hipLaunchKernelGGL(w16::field_w16_bwd_kernel<kFromRayZ>, dim3(grid), b, 0, st, a);
+  else return CN_EUNSUPPORTED;
   return cn::launch_status();
 }
 

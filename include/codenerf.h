@@ -57,6 +57,9 @@ typedef void* cn_stream_t; /* hipStream_t */
  *                    (the inference kernel of precision "f32"; exact f32 products as
  *                    CN_FMT_F32, whose kernel remains the training forward). */
 #define CN_FMT_F32_W16 3
+/*   CN_FMT_F32_W16_T the transposed fp32 pack the fused fp32 backward streams
+ *                    (cn_field_backward_fused); not a forward format. */
+#define CN_FMT_F32_W16_T 4
 
 const char* cn_version(void);
 const char* cn_error_string(int code);
@@ -292,6 +295,23 @@ int cn_field_backward_x3(const float* packed_t, const uint32_t* masks, const flo
                          int64_t chunk_rows, const int64_t* code_index, int64_t n_codes,
                          const float* freqs_xyz, const float* freqs_dir, float* g_code, float* d_pts,
                          float* d_ro, float* d_rd, cn_stream_t stream);
+
+/* The same pair in either arithmetic.  fmt CN_FMT_BF16X3 (as above) or CN_FMT_F32_W16: the
+ * fp32 16x16x4 inference kernel (exact fp32 products, the reference's arithmetic) that also
+ * writes its ReLU masks (cn_field_mask_words_fmt(fmt, M) words).  The backward takes the
+ * matching transposed pack (fmt_t CN_FMT_BF16X3_T / CN_FMT_F32_W16_T) and needs one code row
+ * per wave: n_codes == 1, or n_samples % 32 (bf16x3) / % 16 (fp32) == 0. */
+int64_t cn_field_mask_words_fmt(int fmt, int64_t m);
+int cn_radiance_field_masks_fmt(int fmt, const float* packed, const float* code_bias, const int64_t* code_index,
+                                int64_t n_codes, const float* pts, const float* ro, const float* rd,
+                                const float* z, int64_t n_rays, int64_t n_samples, int64_t chunk_rows,
+                                const float* freqs_xyz, const float* freqs_dir, float* raw, uint32_t* masks,
+                                cn_stream_t stream);
+int cn_field_backward_fused(int fmt_t, const float* packed_t, const uint32_t* masks, const float* d_raw,
+                            const float* pts, const float* ro, const float* rd, const float* z, int64_t n_rays,
+                            int64_t n_samples, int64_t chunk_rows, const int64_t* code_index, int64_t n_codes,
+                            const float* freqs_xyz, const float* freqs_dir, float* g_code, float* d_pts,
+                            float* d_ro, float* d_rd, cn_stream_t stream);
 
 /* Backward of cn_code_bias (the code layers, model.py:174-177, and the code
  * halves of layer_xyz2 / fc_out / fc_rgb) from g_code.  dz_s / dz_t (n_codes, 256)

@@ -258,6 +258,26 @@ def decode_relu_masks(words: torch.Tensor, m_rows: int):
     return {k: out[:, l].contiguous() for k, l in (("h1", 0), ("h2", 1), ("v1", 3), ("v2", 4))}
 
 
+def decode_relu_masks_w16(words: torch.Tensor, m_rows: int):
+    """The fp32 16x16x4 kernel's masks (csrc/mlp_f32.hip relu_act) -> {"h1", "h2", "v1", "v2"}.
+
+    Layout: per 128-sample tile, wave w (8), layer l (h1, h2, v1, v2) and lane L, 2 words; bit b of
+    word q is sample tile*128 + 16w + (L & 15), feature 16(8q + (b >> 2)) + 4(L >> 4) + (b & 3).
+    """
+    w = words.detach().cpu().to(torch.int64) & 0xFFFFFFFF
+    tiles = w.numel() // (8 * 4 * 64 * 2)
+    bits = ((w.view(tiles, 8, 4, 64, 2, 1) >> torch.arange(32)) & 1).float()
+    lane = torch.arange(64).view(64, 1, 1)
+    q = torch.arange(2).view(1, 2, 1)
+    b = torch.arange(32).view(1, 1, 32)
+    feat = 16 * (8 * q + (b >> 2)) + 4 * (lane >> 4) + (b & 3)
+    row = (lane & 15).expand(64, 2, 32)
+    out = torch.zeros(tiles, 8, 4, 16, 256)
+    out[:, :, :, row, feat] = bits
+    out = out.permute(0, 1, 3, 2, 4).reshape(tiles * 128, 4, 256)[:m_rows]
+    return {k: out[:, l].contiguous() for k, l in (("h1", 0), ("h2", 1), ("v1", 2), ("v2", 3))}
+
+
 @pytest.mark.parametrize("mode,r,s,chunk,per_ray_codes", [
     ("rayz", 37, 16, 13, False),
     ("pts", 37, 16, 37, False),
@@ -315,17 +335,21 @@ def test_field_backward(dev, mode, r, s, chunk, per_ray_codes, precision):
         close(prm.grad, p[name].grad, what=name)
 
 
-@pytest.mark.parametrize("mode,r,s,chunk,per_ray_codes,fused", [
-    ("rayz", 37, 16, 13, False, True),
-    ("pts", 37, 16, 37, False, True),
-    ("rayz", 20, 32, 20, True, True),
-    ("rayz", 300, 64, 128, False, True),
-    ("rayz", 64, 128, 64, False, True),
-    ("rayz", 20, 9, 20, True, False),   # codes change inside a 32-sample wave: layer-wise fp32 path
+@pytest.mark.parametrize("mode,r,s,chunk,per_ray_codes", [
+    ("rayz", 37, 16, 13, False),
+    ("pts", 37, 16, 37, False),
+    ("rayz", 20, 32, 20, True),
+    ("rayz", 300, 64, 128, False),
+    ("rayz", 64, 128, 64, False),
+    ("rayz", 21, 16, 21, True),   # per-ray codes, 16-sample rays: fused for f32 (16-sample waves) only
+    ("rayz", 20, 9, 20, True),    # codes change inside a wave: layer-wise fp32 path
+    ("pts", 150, 7, 50, False),   # ragged: samples not a multiple of the wave, last tile partial
 ])
-def test_field_backward_eval_fused(dev, monkeypatch, mode, r, s, chunk, per_ray_codes, fused):
-    """Frozen bf16x3 model (the eval step): the 3xbf16 forward with ReLU masks and ONE fused backward
-    launch (cn_field_backward_x3) give the oracle's d ro / d rd / d z_s / d z_t.
+@pytest.mark.parametrize("precision", ["f32", "bf16x3"])
+def test_field_backward_eval_fused(dev, monkeypatch, mode, r, s, chunk, per_ray_codes, precision):
+    """Frozen model (the eval step): the forward with ReLU masks and ONE fused backward launch
+    (cn_field_backward_fused: fp32 16x16x4 for "f32", 3xbf16 for "bf16x3") give the oracle's d ro /
+    d rd / d z_s / d z_t.
 
     Checked three ways: (1) against the oracle with its own ReLU decisions (INDEPENDENT_RTOL);
     (2) every ReLU decision the kernel's forward recorded (decode_relu_masks) equals the oracle's
@@ -350,8 +374,9 @@ def test_field_backward_eval_fused(dev, monkeypatch, mode, r, s, chunk, per_ray_
     o = O()
     m = model(dev, 0)
     p = oracle_params(m)
-    m.precision = "bf16x3"
+    m.precision = precision
     m.requires_grad_(False)
+    fused = (not per_ray_codes) or s % (32 if precision == "bf16x3" else 16) == 0
     g = torch.Generator().manual_seed(r * s + 7)
     ro = torch.randn(r, 3, generator=g) * 0.3 + torch.tensor([0.0, 0.0, 1.3])
     rd = torch.randn(r, 3, generator=g)
@@ -374,7 +399,8 @@ def test_field_backward_eval_fused(dev, monkeypatch, mode, r, s, chunk, per_ray_
         raw_g = nerf._field(m, emb, rd_g, zsg, ztg, chunk, ro=ro_g, z=z.to(dev))
     (raw_g * gout.to(dev)).sum().backward()
     assert calls["fused"] == (1 if fused else 0)
-    masks = decode_relu_masks(calls["masks"], r * s) if fused else None
+    decode = decode_relu_masks if precision == "bf16x3" else decode_relu_masks_w16
+    masks = decode(calls["masks"], r * s) if fused else None
 
     pd = {k: v.detach() for k, v in p.items()}
 
@@ -398,7 +424,7 @@ def test_field_backward_eval_fused(dev, monkeypatch, mode, r, s, chunk, per_ray_
             close(g_, ref, what="d " + what)
         return
     # 2. the kernel's recorded decisions equal the oracle's except inside the 3xbf16 band ...
-    n_dis = check_mask_agreement(masks, pre, MASK_BAND["bf16x3"], "fused forward")
+    n_dis = check_mask_agreement(masks, pre, MASK_BAND[precision], "fused forward")
     print(f"ReLU decisions differing from the oracle (all in-band): {n_dis}")
     # 3. ... and with exactly those decisions the oracle's gradients match tightly
     fed = oracle(masks)
