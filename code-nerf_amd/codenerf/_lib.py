@@ -77,6 +77,11 @@ SIGNATURES = {
                                          _p]),
     "cn_field_backward_fused": (_i, [_i, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p, _i64, _fp, _fp, _p, _p,
                                      _p, _p, _p]),
+    "cn_radiance_field_train_w16": (_i, [_p, _p, _p, _i64, _p, _p, _p, _p, _i64, _i64, _i64, _fp, _fp, _p, _p, _p,
+                                         _p]),
+    "cn_field_backward_train_workspace_floats": (_i64, [_i64]),
+    "cn_field_backward_train": (_i, [_p, ctypes.POINTER(_p), _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p,
+                                     _i64, _fp, _fp, _p, ctypes.POINTER(_p), _p, _p, _p, _p, _p]),
     "cn_field_backward_x3": (_i, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p, _i64, _fp, _fp, _p, _p, _p, _p,
                                   _p]),
     "cn_code_bias_backward": (_i, [ctypes.POINTER(_p), _p, _p, _i64, _p, _p, _p, ctypes.POINTER(_p), _p]),
@@ -89,7 +94,8 @@ SIGNATURES = {
     "cn_gemm_tn": (_i, [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _p]),
     "cn_gemm_nn_x3": (_i, [_p, _i64, _p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _p]),
     "cn_gemm_tn_x3": (_i, [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _p]),
-    "cn_render_loss": (_i, [_p, _p, _p, _i64, _i64, _p, _p, _i64, _i64, _f, _p, _p]),
+    "cn_render_loss_workspace_doubles": (_i64, [_i64]),
+    "cn_render_loss": (_i, [_p, _p, _p, _i64, _i64, _p, _p, _i64, _i64, _f, _p, _p, _p]),
     "cn_render_loss_backward": (_i, [_p, _p, _p, _i64, _i64, _p, _p, _i64, _i64, _f, _p, _p, _p, _p, _p, _p, _p]),
     "cn_adamw_step": (_i, [_p, _p, _p, _p, _i64, ctypes.POINTER(_i64), ctypes.POINTER(_i64),
                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i64),

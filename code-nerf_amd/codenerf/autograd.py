@@ -212,9 +212,20 @@ class RadianceField(torch.autograd.Function):
             ctx.meta = meta
             ctx.save_for_backward(rd, pts, ro, z, z_s, z_t, *params)
             return raw
-        packed = ops.mlp_pack(params, "f32")
-        raw, saved = ops.radiance_field_train(packed, cb, rd, meta.n_samples, meta.chunk_rows, meta.fx, meta.fd,
-                                              pts=pts, ro=ro, z=z, code_index=meta.code_index)
+        # weights trained: the fp32 training forward keeps the activations.  "f32" with fp32 GEMMs
+        # and one code row per 16-sample wave: the 16x16x4 kernel + the fused training backward;
+        # otherwise the 32x32x2 kernel + the layer-wise backward
+        ctx.train_fused = (meta.precision == "f32" and meta.train_precision == "f32"
+                           and ops.fused_backward_supported(z_s.shape[0], meta.n_samples, meta.code_index, "f32"))
+        ctx.masks = None
+        if ctx.train_fused:
+            raw, saved, ctx.masks = ops.radiance_field_train_w16(
+                ops.mlp_pack(params, "f32_w16"), cb, rd, meta.n_samples, meta.chunk_rows, meta.fx, meta.fd, pts=pts,
+                ro=ro, z=z, code_index=meta.code_index)
+        else:
+            raw, saved = ops.radiance_field_train(ops.mlp_pack(params, "f32"), cb, rd, meta.n_samples,
+                                                  meta.chunk_rows, meta.fx, meta.fd, pts=pts, ro=ro, z=z,
+                                                  code_index=meta.code_index)
         ctx.x_enc = ops.encode_inputs(rd, meta.n_samples, meta.chunk_rows, meta.fx, meta.fd, pts=pts, ro=ro, z=z)
         ctx.meta, ctx.acts = meta, saved
         ctx.save_for_backward(rd, pts, ro, z, z_s, z_t, *params)
@@ -239,6 +250,16 @@ class RadianceField(torch.autograd.Function):
             return (None, r["d_rd"], r["d_pts"], r["d_ro"], None, dz_s, dz_t, *([None] * len(params)))
         pg = _param_grad_buffers(params, needs[7:])
         want_z = needs[5] or needs[6]
+        if ctx.train_fused:
+            r = ops.field_backward_train(ops.mlp_pack(params, "f32_w16_t"), params, ctx.masks, ctx.acts, ctx.x_enc,
+                                         g_raw.contiguous(), rd.shape[0], meta.n_samples, meta.chunk_rows,
+                                         z_s.shape[0], meta.fx, meta.fd, rd=rd, pts=pts, ro=ro, z=z,
+                                         code_index=meta.code_index, param_grads=pg, want_pts=needs[2],
+                                         want_ro=needs[3], want_rd=needs[1])
+            ctx.acts = ctx.x_enc = ctx.masks = None
+            dz_s, dz_t = ops.code_bias_backward(params, z_s, z_t, r["g_code"], pg, want_z=want_z)
+            grads = pg if pg is not None else [None] * len(params)
+            return (None, r["d_rd"], r["d_pts"], r["d_ro"], None, dz_s, dz_t, *grads)
         r = ops.field_backward(params, ctx.acts, ctx.x_enc, g_raw.contiguous(), rd.shape[0], meta.n_samples,
                                meta.chunk_rows, z_s.shape[0], meta.fx, meta.fd, rd=rd, pts=pts, ro=ro, z=z,
                                code_index=meta.code_index, param_grads=pg, want_code=want_z or pg is not None,

@@ -417,6 +417,69 @@ def radiance_field_train(packed: Tensor, cb: Tensor, rd: Tensor, n_samples: int,
     return raw, saved
 
 
+def radiance_field_train_w16(packed: Tensor, cb: Tensor, rd: Tensor, n_samples: int, chunk_rows: int,
+                             freqs_xyz: Sequence[float], freqs_dir: Sequence[float], pts: Optional[Tensor] = None,
+                             ro: Optional[Tensor] = None, z: Optional[Tensor] = None,
+                             code_index: Optional[Tensor] = None):
+    """Training forward on the fp32 16x16x4 kernel (packed "f32_w16") -> raw (R,S,4), saved (5, R*S, 256),
+    ReLU masks (the fused training backward's inputs)."""
+    lib = _lib_ready()
+    rd = _cuda(rd, "rd")
+    n = rd.shape[0]
+    if pts is not None:
+        pts = _cuda(pts, "pts")
+        assert pts.shape == (n, n_samples, 3)
+    else:
+        ro, z = _cuda(ro, "ro"), _cuda(z, "z")
+        assert z.shape == (n, n_samples)
+    if code_index is not None:
+        code_index = _cuda(code_index, "code_index", torch.int64)
+    m = n * n_samples
+    raw = torch.empty(n, n_samples, 4, device=rd.device, dtype=torch.float32)
+    saved = torch.empty(5, m, 256, device=rd.device, dtype=torch.float32)
+    masks = torch.empty(int(lib.cn_field_mask_words_fmt(_lib.CN_FMT_F32_W16, m)), device=rd.device, dtype=torch.int32)
+    check(lib.cn_radiance_field_train_w16(ptr(packed), ptr(cb), ptr(code_index), cb.shape[0], ptr(pts), ptr(ro),
+                                          ptr(rd), ptr(z), n, n_samples, chunk_rows, _lib.host_floats(freqs_xyz),
+                                          _lib.host_floats(freqs_dir), ptr(raw), ptr(saved), ptr(masks),
+                                          stream_of(rd)), "cn_radiance_field_train_w16")
+    return raw, saved, masks
+
+
+def field_backward_train(packed_t: Tensor, params: Sequence[Tensor], masks: Tensor, saved: Tensor, x_enc: Tensor,
+                         d_raw: Tensor, n_rays: int, n_samples: int, chunk_rows: int, n_codes: int,
+                         freqs_xyz: Sequence[float], freqs_dir: Sequence[float], rd: Tensor,
+                         pts: Optional[Tensor] = None, ro: Optional[Tensor] = None, z: Optional[Tensor] = None,
+                         code_index: Optional[Tensor] = None, param_grads: Optional[Sequence[Tensor]] = None,
+                         want_pts: bool = False, want_ro: bool = False, want_rd: bool = False):
+    """Fused fp32 training backward (one dX launch + dW GEMMs) -> dict g_code / d_pts / d_ro / d_rd."""
+    lib = _lib_ready()
+    m = n_rays * n_samples
+    params = [_cuda(p.detach(), f"param{i}") for i, p in enumerate(params)]
+    d_raw = _cuda(d_raw, "d_raw")
+    assert d_raw.numel() == 4 * m and saved.shape == (5, m, 256) and x_enc.shape == (m, 90)
+    dev = d_raw.device
+    rd, pts, ro, z = _opt(rd, "rd"), _opt(pts, "pts"), _opt(ro, "ro"), _opt(z, "z")
+    if code_index is not None:
+        code_index = _cuda(code_index, "code_index", torch.int64)
+    ws = torch.empty(int(lib.cn_field_backward_train_workspace_floats(m)), device=dev, dtype=torch.float32)
+    g_code = torch.zeros(n_codes, _lib.CN_CODE_BIAS_STRIDE, device=dev, dtype=torch.float32)
+    d_pts = torch.empty(n_rays, n_samples, 3, device=dev, dtype=torch.float32) if want_pts else None
+    d_ro = torch.zeros(n_rays, 3, device=dev, dtype=torch.float32) if want_ro else None
+    d_rd = torch.zeros(n_rays, 3, device=dev, dtype=torch.float32) if want_rd else None
+    arr, keep = _lib.pointer_array(params)
+    garr, gkeep = (None, None)
+    if param_grads is not None:
+        assert len(param_grads) == _lib.CN_NUM_PARAMS and all(g.is_contiguous() for g in param_grads)
+        garr, gkeep = _lib.pointer_array(list(param_grads))
+    check(lib.cn_field_backward_train(ptr(packed_t), arr, ptr(masks), ptr(saved), ptr(x_enc), ptr(d_raw), ptr(pts),
+                                      ptr(ro), ptr(rd), ptr(z), n_rays, n_samples, chunk_rows, ptr(code_index),
+                                      n_codes, _lib.host_floats(freqs_xyz), _lib.host_floats(freqs_dir), ptr(ws),
+                                      garr, ptr(g_code), ptr(d_pts), ptr(d_ro), ptr(d_rd), stream_of(d_raw)),
+          "cn_field_backward_train")
+    del keep, gkeep
+    return {"g_code": g_code, "d_pts": d_pts, "d_ro": d_ro, "d_rd": d_rd}
+
+
 def mlp_forward_train(packed: Tensor, cb: Tensor, x: Tensor, code_index: Optional[Tensor] = None
                       ) -> Tuple[Tensor, Tensor]:
     """fp32 mlp_forward that also keeps the activations -> raw (M,4), saved (5, M, 256)."""
@@ -680,8 +743,10 @@ def render_loss(rgb_coarse: Optional[Tensor], rgb_fine: Optional[Tensor], target
     n_code = 0 if zs is None else zs.numel()
     assert zt is None or zt.numel() == n_code, "z_s and z_t must have the same size"
     out = torch.empty(6, device=target.device, dtype=torch.float32)
+    nws = int(lib.cn_render_loss_workspace_doubles(n_code))
+    ws = torch.empty(nws, device=target.device, dtype=torch.float64) if nws > 0 else None
     check(lib.cn_render_loss(ptr(rc), ptr(rf), ptr(target), target.shape[1], n, ptr(zs), ptr(zt), n_code, expand,
-                             regularizer_lambda, ptr(out), stream_of(out)), "cn_render_loss")
+                             regularizer_lambda, ptr(ws), ptr(out), stream_of(out)), "cn_render_loss")
     return out
 
 

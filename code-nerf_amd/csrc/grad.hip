@@ -956,3 +956,84 @@ extern "C" int cn_ray_points_backward(const float* g_pts, const float* z, int64_
                      as_stream(stream), g_pts, 3, z, n_rays, n_samples, d_ro, d_rd);
   return launch_status();
 }
+
+// ---------------------------------------------------------------- fused fp32 training backward
+// dX chain, g_code and the ray gradients in ONE fused fp32 launch (field_w16_bwd_kernel<.., true>,
+// which also writes each layer's masked input gradient dPre), then the weight and bias
+// gradients as split-M fp32 MFMA GEMMs dW = dPre^T X over those planes and the forward's saved
+// activations (cn_radiance_field_train_w16).
+extern "C" int64_t cn_field_backward_train_workspace_floats(int64_t m) { return m > 0 ? 5 * m * 256 : -1; }
+
+extern "C" int cn_field_backward_train(const float* packed_t, const float* const* params, const uint32_t* masks,
+                                       const float* saved, const float* x_enc, const float* d_raw, const float* pts,
+                                       const float* ro, const float* rd, const float* z, int64_t n_rays,
+                                       int64_t n_samples, int64_t chunk_rows, const int64_t* code_index,
+                                       int64_t n_codes, const float* freqs_xyz, const float* freqs_dir,
+                                       float* workspace, float* const* grads, float* g_code, float* d_pts,
+                                       float* d_ro, float* d_rd, cn_stream_t stream) {
+  using namespace mlp;
+  CN_CHECK_ARG(packed_t && params && masks && saved && x_enc && d_raw && rd && g_code && workspace);
+  CN_CHECK_ARG(freqs_xyz && freqs_dir && n_rays > 0 && n_samples > 0 && chunk_rows > 0 && n_codes > 0);
+  CN_CHECK_ARG(pts || (ro && z));
+  CN_CHECK_ARG(!d_pts || pts);
+  CN_CHECK_ARG(!d_ro || (ro && z && !pts));
+  CN_CHECK_ARG(code_index || n_codes == 1 || n_codes == n_rays);
+  for (int i = 0; i < CN_NUM_PARAMS; ++i) CN_CHECK_ARG(params[i]);
+  if (!(n_codes == 1 || n_samples % 16 == 0)) return CN_EUNSUPPORTED;  // one code row per 16-sample wave
+  hipStream_t st = as_stream(stream);
+  const int64_t M = n_rays * n_samples;
+  CN_CHECK_ARG(ceil_div(M, 128) <= 0x7fffffff);
+  FieldArgs a = {};
+  a.packed = packed_t;
+  a.code_index = code_index;
+  a.n_codes = n_codes;
+  a.pts = pts;
+  a.ro = ro;
+  a.rd = rd;
+  a.z = z;
+  a.n_rays = n_rays;
+  a.n_samples = n_samples;
+  a.chunk_rows = chunk_rows;
+  a.m = M;
+  for (int i = 0; i < 10; ++i) a.fx[i] = freqs_xyz[i];
+  for (int i = 0; i < 4; ++i) a.fd[i] = freqs_dir[i];
+  a.masks = const_cast<uint32_t*>(masks);
+  a.d_raw = d_raw;
+  a.g_code = g_code;
+  a.d_pts = d_pts;
+  a.d_ro = d_ro;
+  a.d_rd = d_rd;
+  a.dpre = workspace;
+  CN_TRY(launch_field_w16_bwd(pts ? kFromPts : kFromRayZ, a, st));
+  if (!(grads && grads[0])) return CN_OK;
+  auto G = [&](int i) { return grads[i]; };
+  const float* P[5];
+  for (int k = 0; k < 5; ++k) P[k] = workspace + k * M * 256;
+  const float* h1 = saved;
+  const float* h2 = saved + M * 256;
+  const float* feat = saved + 2 * M * 256;
+  const float* v1 = saved + 3 * M * 256;
+  const float* v2 = saved + 4 * M * 256;
+  // fc_rgb (h half): dW += d rgb^T v2
+  CN_TRY(gemm_tn(d_raw, 4, v2, 256, G(kWRgb), 512, M, 3, 256, st));
+  CN_TRY(seg_sum(d_raw, 4, M, 3, M, nullptr, 1, G(kBRgb), 1, st));
+  // layer_dir2
+  CN_TRY(gemm_tn(P[0], 256, v1, 256, G(kWDir2), 256, M, 256, 256, st));
+  CN_TRY(seg_sum(P[0], 256, M, 256, M, nullptr, 1, G(kBDir2), 1, st));
+  // layer_dir1: [feat | dir enc]
+  CN_TRY(gemm_tn(P[1], 256, feat, 256, G(kWDir1), 283, M, 256, 256, st));
+  CN_TRY(gemm_tn(P[1], 256, x_enc + 63, 90, G(kWDir1) + 256, 283, M, 256, 27, st));
+  CN_TRY(seg_sum(P[1], 256, M, 256, M, nullptr, 1, G(kBDir1), 1, st));
+  // fc_out (h half): row 0 from d sigma, rows 1.. from d feat
+  CN_TRY(gemm_tn(d_raw + 3, 4, h2, 256, G(kWOut), 512, M, 1, 256, st));
+  CN_TRY(gemm_tn(P[2], 256, h2, 256, G(kWOut) + 512, 512, M, 256, 256, st));
+  CN_TRY(seg_sum(d_raw + 3, 4, M, 1, M, nullptr, 1, G(kBOut), 1, st));
+  CN_TRY(seg_sum(P[2], 256, M, 256, M, nullptr, 1, G(kBOut) + 1, 1, st));
+  // layer_xyz2 (h half)
+  CN_TRY(gemm_tn(P[3], 256, h1, 256, G(kWXyz2), 512, M, 256, 256, st));
+  CN_TRY(seg_sum(P[3], 256, M, 256, M, nullptr, 1, G(kBXyz2), 1, st));
+  // layer_xyz1
+  CN_TRY(gemm_tn(P[4], 256, x_enc, 90, G(kWXyz1), 63, M, 256, 63, st));
+  CN_TRY(seg_sum(P[4], 256, M, 256, M, nullptr, 1, G(kBXyz1), 1, st));
+  return CN_OK;
+}

@@ -28,12 +28,50 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
   return s;  // valid on thread 0
 }
 
-// out: [loss_coarse, loss_fine, regulariser, total, ||z_s||, ||z_t||]
+// Large code tensors (train: the whole embedding tables, 2 x 2458 x 256): per-block partial sums
+// of squares (double) into partials[2 b], [2 b + 1]; the loss kernel adds them up.
+constexpr int kPartThreads = 256;
+constexpr int64_t kPartElems = 8192;  // code values per partial block
+
+__global__ __launch_bounds__(kPartThreads) void code_sq_partials_kernel(const float* __restrict__ zs,
+                                                                        const float* __restrict__ zt, int64_t n_code,
+                                                                        double* __restrict__ partials) {
+  __shared__ double red[2][kPartThreads / 64];
+  double ss = 0.0, st = 0.0;
+  const int64_t b0 = blockIdx.x * kPartElems, b1 = min(b0 + kPartElems, n_code);
+  for (int64_t i = b0 + threadIdx.x; i < b1; i += kPartThreads) {
+    ss += static_cast<double>(zs[i]) * zs[i];
+    st += static_cast<double>(zt[i]) * zt[i];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    ss += __shfl_xor(ss, o);
+    st += __shfl_xor(st, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = ss;
+    red[1][threadIdx.x >> 6] = st;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a = 0.0, b = 0.0;
+    for (int w = 0; w < kPartThreads / 64; ++w) {
+      a += red[0][w];
+      b += red[1][w];
+    }
+    partials[2 * blockIdx.x] = a;
+    partials[2 * blockIdx.x + 1] = b;
+  }
+}
+
+// out: [loss_coarse, loss_fine, regulariser, total, ||z_s||, ||z_t||].  n_part > 0: the code sums
+// come from the n_part partial pairs instead of z_s / z_t.
 __global__ __launch_bounds__(kThreads) void render_loss_kernel(const float* __restrict__ rgb_c,
                                                                const float* __restrict__ rgb_f,
                                                                const float* __restrict__ target, int64_t ldt,
                                                                int64_t n_rays, const float* __restrict__ zs,
                                                                const float* __restrict__ zt, int64_t n_code,
+                                                               const double* __restrict__ partials, int n_part,
                                                                double expand, float lambda, float* __restrict__ out) {
   __shared__ double red[kThreads / 64];
   double sc = 0.0, sf = 0.0, ss = 0.0, st = 0.0;
@@ -50,9 +88,16 @@ __global__ __launch_bounds__(kThreads) void render_loss_kernel(const float* __re
       sf += static_cast<double>(d) * d;
     }
   }
-  for (int64_t i = threadIdx.x; i < n_code; i += kThreads) {
-    if (zs) ss += static_cast<double>(zs[i]) * zs[i];
-    if (zt) st += static_cast<double>(zt[i]) * zt[i];
+  if (n_part > 0) {
+    for (int i = threadIdx.x; i < n_part; i += kThreads) {
+      ss += partials[2 * i];
+      st += partials[2 * i + 1];
+    }
+  } else {
+    for (int64_t i = threadIdx.x; i < n_code; i += kThreads) {
+      if (zs) ss += static_cast<double>(zs[i]) * zs[i];
+      if (zt) st += static_cast<double>(zt[i]) * zt[i];
+    }
   }
   sc = block_sum(sc, red);
   sf = block_sum(sf, red);
@@ -101,14 +146,25 @@ __global__ void render_loss_backward_kernel(const float* __restrict__ rgb_c, con
 
 }  // namespace
 
+extern "C" int64_t cn_render_loss_workspace_doubles(int64_t n_code) {
+  if (n_code < 0) return -1;
+  return n_code <= 2 * kPartElems ? 0 : 2 * cn::ceil_div(n_code, kPartElems);
+}
+
 extern "C" int cn_render_loss(const float* rgb_coarse, const float* rgb_fine, const float* target,
                               int64_t target_stride, int64_t n_rays, const float* z_s, const float* z_t,
-                              int64_t n_code, int64_t expand, float regularizer_lambda, float* out,
-                              cn_stream_t stream) {
+                              int64_t n_code, int64_t expand, float regularizer_lambda, double* workspace,
+                              float* out, cn_stream_t stream) {
   CN_CHECK_ARG(n_rays > 0 && target && target_stride >= 3 && out && (rgb_coarse || rgb_fine));
   CN_CHECK_ARG(n_code >= 0 && expand >= 1 && (n_code == 0 || (z_s && z_t)));
+  const int64_t ws = cn_render_loss_workspace_doubles(n_code);
+  CN_CHECK_ARG(ws == 0 || workspace);
+  const int n_part = static_cast<int>(ws / 2);
+  if (n_part > 0)
+    hipLaunchKernelGGL(code_sq_partials_kernel, dim3(n_part), dim3(kPartThreads), 0, cn::as_stream(stream), z_s, z_t,
+                       n_code, workspace);
   hipLaunchKernelGGL(render_loss_kernel, dim3(1), dim3(kThreads), 0, cn::as_stream(stream), rgb_coarse, rgb_fine,
-                     target, target_stride, n_rays, z_s, z_t, n_code, static_cast<double>(expand),
+                     target, target_stride, n_rays, z_s, z_t, n_code, workspace, n_part, static_cast<double>(expand),
                      regularizer_lambda, out);
   return cn::launch_status();
 }

@@ -611,6 +611,37 @@ extern "C" int cn_radiance_field_masks_fmt(int fmt, const float* packed, const f
                               : launch_field_w16(pts ? kFromPts : kFromRayZ, a, cn::as_stream(stream));
 }
 
+extern "C" int cn_radiance_field_train_w16(const float* packed, const float* code_bias, const int64_t* code_index,
+                                           int64_t n_codes, const float* pts, const float* ro, const float* rd,
+                                           const float* z, int64_t n_rays, int64_t n_samples, int64_t chunk_rows,
+                                           const float* freqs_xyz, const float* freqs_dir, float* raw, float* save,
+                                           uint32_t* masks, cn_stream_t stream) {
+  CN_CHECK_ARG(packed && code_bias && rd && raw && save && masks && freqs_xyz && freqs_dir);
+  CN_CHECK_ARG(n_rays > 0 && n_samples > 0 && chunk_rows > 0 && n_codes > 0);
+  CN_CHECK_ARG(pts || (ro && z));
+  CN_CHECK_ARG(code_index || n_codes == 1 || n_codes == n_rays);
+  FieldArgs a = {};
+  a.packed = packed;
+  a.code_bias = code_bias;
+  a.code_index = code_index;
+  a.n_codes = n_codes;
+  a.pts = pts;
+  a.ro = ro;
+  a.rd = rd;
+  a.z = z;
+  a.n_rays = n_rays;
+  a.n_samples = n_samples;
+  a.chunk_rows = chunk_rows;
+  a.m = n_rays * n_samples;
+  CN_CHECK_ARG(cn::ceil_div(a.m, kTile) <= 0x7fffffff);
+  for (int i = 0; i < 10; ++i) a.fx[i] = freqs_xyz[i];
+  for (int i = 0; i < 4; ++i) a.fd[i] = freqs_dir[i];
+  a.raw = raw;
+  a.save = save;
+  a.masks = masks;
+  return launch_field_w16(pts ? kFromPts : kFromRayZ, a, cn::as_stream(stream));
+}
+
 extern "C" int cn_field_backward_x3(const float* packed_t, const uint32_t* masks, const float* d_raw,
                                     const float* pts, const float* ro, const float* rd, const float* z,
                                     int64_t n_rays, int64_t n_samples, int64_t chunk_rows,

@@ -44,6 +44,7 @@ struct FieldArgs {
   float* d_pts;          // backward: (m, 3) written (kFromPts)
   float* d_ro;           // backward: (n_rays, 3) accumulated (kFromRayZ)
   float* d_rd;           // backward: (n_rays, 3) accumulated
+  float* dpre;           // fp32 fused training backward: (5, m, 256) masked layer-input gradients
 };
 
 // One sample's inputs: point, unit Q1 view direction, code row.

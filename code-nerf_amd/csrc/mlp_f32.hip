@@ -303,7 +303,19 @@ __device__ __forceinline__ void relu_act(State& s, const FieldArgs& a, int64_t t
     reinterpret_cast<uint2*>(a.masks)[((tile * kWaves + s.wave) * kMaskLayers + ml) * 64 + s.lane] = make_uint2(w0, w1);
 }
 
-template <int MODE, bool MASKS>
+// Training forward: the post-activation rows the weight gradients read (h1, h2, feat, v1, v2 as
+// (5, m, 256) planes, feature 16 ob + 4 g + r: one 16-B store per block per lane).
+template <bool SAVE>
+__device__ __forceinline__ void save_act(const State& s, const FieldArgs& a, int plane, int64_t row, bool valid) {
+  if constexpr (SAVE) {
+    if (!valid) return;
+    float* d = a.save + ((int64_t)plane * a.m + row) * 256 + 4 * s.g;
+#pragma unroll
+    for (int ob = 0; ob < 16; ++ob) *reinterpret_cast<floatx4*>(d + 16 * ob) = s.act[ob];
+  }
+}
+
+template <int MODE, bool MASKS, bool SAVE = false>
 __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4* lds, float* clds, float* crow_lds,
                                           int64_t tile, int& c) {
   const int64_t row = tile * kTile + s.wave * 16 + (s.lane & 15);
@@ -386,6 +398,7 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
     } else {
       relu_act<MASKS>(s, a, tile, layer == kXyz2 ? 0 : (layer == kOut ? 1 : 2));
     }
+    save_act<SAVE>(s, a, layer - kXyz2, row, valid);  // h1, h2, feat, v1
     if (layer == kOut) {
       // sigma = fc_out row 0 . [h2, zs2] + b: the h2 part here, the code part from cn_code_bias
       float sg = 0.0f;
@@ -410,6 +423,7 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
 
   // ---- fc_rgb (256 -> 3): one chunk, 64 k-steps of block 0 in 4 chains
   relu_act<MASKS>(s, a, tile, 3);
+  save_act<SAVE>(s, a, 4, row, valid);  // v2
   {
     float b0 = 0.0f, b1 = 0.0f, b2 = 0.0f, bs = 0.0f;
     if (s.uniform_code) {
@@ -476,7 +490,7 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
   }
 }
 
-template <int MODE, bool MASKS>
+template <int MODE, bool MASKS, bool SAVE = false>
 __global__ __launch_bounds__(kThreads, 2) void field_w16_kernel(FieldArgs a) {
   // ONE LDS object (a second one makes hipcc wait vmcnt(0) before ring reads): the DMA
   // ring, then the constants, then one code-bias row per wave
@@ -504,7 +518,7 @@ __global__ __launch_bounds__(kThreads, 2) void field_w16_kernel(FieldArgs a) {
   int c = 0;
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
     c = 0;
-    field_tile<MODE, MASKS>(s, a, lds, clds, crow_lds, tile, c);
+    field_tile<MODE, MASKS, SAVE>(s, a, lds, clds, crow_lds, tile, c);
   }
   // the last tile prefetched chunks 0..2 of a tile that does not exist: they must land
   // before the workgroup's LDS is released
@@ -718,7 +732,20 @@ __device__ __forceinline__ void dbg_acc(const State& s, const FieldArgs& a, int 
     for (int r = 0; r < 4; ++r) d[16 * ob + r] = s.acc[ob][r];
 }
 
-template <int MODE>
+// Training backward: the masked input gradient of a layer (its dPre, what dW = dPre^T X reads) as
+// plane `plane` of a.dpre: 0 layer_dir2, 1 layer_dir1, 2 fc_out rows 1.. (d feat), 3 layer_xyz2,
+// 4 layer_xyz1.
+template <bool TRAIN>
+__device__ __forceinline__ void save_dpre(const State& s, const FieldArgs& a, int plane, int64_t row, bool valid) {
+  if constexpr (TRAIN) {
+    if (!valid) return;
+    float* d = a.dpre + ((int64_t)plane * a.m + row) * 256 + 4 * s.g;
+#pragma unroll
+    for (int ob = 0; ob < 16; ++ob) *reinterpret_cast<floatx4*>(d + 16 * ob) = s.act[ob];
+  }
+}
+
+template <int MODE, bool TRAIN>
 __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* lds, float* grow, int64_t tile,
                                         int& cur_code) {
   const int64_t row = tile * kTile + s.wave * 16 + (s.lane & 15);
@@ -759,11 +786,13 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   dbg_acc(s, a, 0, row, valid);
   // ---- layer_dir2^T (m_v2), layer_dir1^T (m_v1)
   mask_act(s, mk[3]);
+  save_dpre<TRAIN>(s, a, 0, row, valid);
   zero_acc(s);
   __builtin_amdgcn_sched_barrier(0);
   layer256(s, lds, c);
   dbg_acc(s, a, 1, row, valid);
   mask_act(s, mk[2]);
+  save_dpre<TRAIN>(s, a, 1, row, valid);
   zero_acc(s);
   __builtin_amdgcn_sched_barrier(0);
   layer256(s, lds, c);
@@ -782,6 +811,7 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   // ---- fc_out^T: B = d feat (no activation), init = fc_out row 0 (h2 part) x d sigma
 #pragma unroll
   for (int ob = 0; ob < 16; ++ob) s.act[ob] = s.acc[ob];
+  save_dpre<TRAIN>(s, a, 2, row, valid);
   gcode_add64(s, grow, kCbFeat, s.act);
 #pragma unroll
   for (int ob = 0; ob < 16; ++ob) {
@@ -793,6 +823,7 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   dbg_acc(s, a, 3, row, valid);
   // ---- layer_xyz2^T (m_h2): its masked input gradient is the code term's too
   mask_act(s, mk[1]);
+  save_dpre<TRAIN>(s, a, 3, row, valid);
   gcode_add64(s, grow, kCbXyz2, s.act);
   zero_acc(s);
   __builtin_amdgcn_sched_barrier(0);
@@ -800,6 +831,7 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   dbg_acc(s, a, 4, row, valid);
   // ---- layer_xyz1^T (m_h1): encoding k-steps 0-7, then 8-15
   mask_act(s, mk[0]);
+  save_dpre<TRAIN>(s, a, 4, row, valid);
   float genc[16];
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
@@ -898,7 +930,7 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   }
 }
 
-template <int MODE>
+template <int MODE, bool TRAIN>
 __global__ __launch_bounds__(kThreads, 2) void field_w16_bwd_kernel(FieldArgs a) {
   __shared__ __attribute__((aligned(16))) float4 lds[kBwdLdsQuads];
   float* blds = reinterpret_cast<float*>(lds + kRing * kChunkQuads);
@@ -920,7 +952,8 @@ __global__ __launch_bounds__(kThreads, 2) void field_w16_bwd_kernel(FieldArgs a)
   read_a<0>(lds + s.lane, s.pre);
   int cur_code = -1;
   const int64_t n_tiles = (a.m + kTile - 1) / kTile;
-  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) bwd_tile<MODE>(s, a, lds, grow, tile, cur_code);
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x)
+    bwd_tile<MODE, TRAIN>(s, a, lds, grow, tile, cur_code);
   __builtin_amdgcn_s_waitcnt(0x0F70);
   if (cur_code >= 0) flush_gcode(s, a, grow, cur_code);
 }
@@ -949,6 +982,12 @@ int launch_pack_w16(const Params& P, float* packed, hipStream_t st) {
 int launch_field_w16(int mode, FieldArgs& a, hipStream_t st) {
   const unsigned grid = static_cast<unsigned>(std::min<int64_t>(cn::ceil_div(a.m, w16::kTile), cu_count_w16()));
   const dim3 b(w16::kThreads);
+  if (a.masks && a.save) {
+    if (mode == kFromPts) hipLaunchKernelGGL((w16::field_w16_kernel<kFromPts, true, true>), dim3(grid), b, 0, st, a);
+    else if (mode == kFromRayZ) hipLaunchKernelGGL((w16::field_w16_kernel<kFromRayZ, true, true>), dim3(grid), b, 0, st, a);
+    else return CN_EUNSUPPORTED;
+    return cn::launch_status();
+  }
   if (a.masks) {
     if (mode == kFromPts) hipLaunchKernelGGL((w16::field_w16_kernel<kFromPts, true>), dim3(grid), b, 0, st, a);
     else if (mode == kFromRayZ) hipLaunchKernelGGL((w16::field_w16_kernel<kFromRayZ, true>), dim3(grid), b, 0, st, a);
@@ -974,8 +1013,14 @@ int launch_pack_w16t(const Params& P, float* packed, hipStream_t st) {
 int launch_field_w16_bwd(int mode, FieldArgs& a, hipStream_t st) {
   const unsigned grid = static_cast<unsigned>(std::min<int64_t>(cn::ceil_div(a.m, w16::kTile), cu_count_w16()));
   const dim3 b(w16::kThreads);
-  if (mode == kFromPts) hipLaunchKernelGGL(w16::field_w16_bwd_kernel<kFromPts>, dim3(grid), b, 0, st, a);
-  else if (mode == kFromRayZ) hipLaunchKernelGGL(w16::field_w16_bwd_kernel<kFromRayZ>, dim3(grid), b, 0, st, a);
+  if (a.dpre) {
+    if (mode == kFromPts) hipLaunchKernelGGL((w16::field_w16_bwd_kernel<kFromPts, true>), dim3(grid), b, 0, st, a);
+    else if (mode == kFromRayZ) hipLaunchKernelGGL((w16::field_w16_bwd_kernel<kFromRayZ, true>), dim3(grid), b, 0, st, a);
+    else return CN_EUNSUPPORTED;
+    return cn::launch_status();
+  }
+  if (mode == kFromPts) hipLaunchKernelGGL((w16::field_w16_bwd_kernel<kFromPts, false>), dim3(grid), b, 0, st, a);
+  else if (mode == kFromRayZ) hipLaunchKernelGGL((w16::field_w16_bwd_kernel<kFromRayZ, false>), dim3(grid), b, 0, st, a);
   else return CN_EUNSUPPORTED;
   return cn::launch_status();
 }

@@ -313,6 +313,31 @@ int cn_field_backward_fused(int fmt_t, const float* packed_t, const uint32_t* ma
                             const float* freqs_xyz, const float* freqs_dir, float* g_code, float* d_pts,
                             float* d_ro, float* d_rd, cn_stream_t stream);
 
+/* --- Fused fp32 training step (train.py:92-114; weights trained) ------------------
+ * Forward: cn_radiance_field on a CN_FMT_F32_W16 pack that also writes the ReLU masks
+ * (cn_field_mask_words_fmt(CN_FMT_F32_W16, M) words) and the (5, M, 256) post-activation planes
+ * h1, h2, feat, v1, v2 (cn_radiance_field_train's layout).
+ * Backward: the fused dX chain of cn_field_backward_fused on the CN_FMT_F32_W16_T pack (g_code,
+ * d_pts / d_ro / d_rd as there; g_code required) that also writes every layer's masked input
+ * gradient into workspace (cn_field_backward_train_workspace_floats(M) floats), then the weight
+ * and bias gradients dW = dPre^T X as split-M fp32 MFMA GEMMs over those planes, saved and x_enc
+ * (cn_encode_inputs): grads (18 pointers, or NULL for none) ACCUMULATED as in
+ * cn_field_backward (the code-layer parameters and code halves come from cn_code_bias_backward).
+ * One code row per 16-sample wave: n_codes == 1 or n_samples % 16 == 0, else CN_EUNSUPPORTED. */
+int cn_radiance_field_train_w16(const float* packed, const float* code_bias, const int64_t* code_index,
+                                int64_t n_codes, const float* pts, const float* ro, const float* rd,
+                                const float* z, int64_t n_rays, int64_t n_samples, int64_t chunk_rows,
+                                const float* freqs_xyz, const float* freqs_dir, float* raw, float* save,
+                                uint32_t* masks, cn_stream_t stream);
+int64_t cn_field_backward_train_workspace_floats(int64_t m);
+int cn_field_backward_train(const float* packed_t, const float* const* params, const uint32_t* masks,
+                            const float* saved, const float* x_enc, const float* d_raw, const float* pts,
+                            const float* ro, const float* rd, const float* z, int64_t n_rays, int64_t n_samples,
+                            int64_t chunk_rows, const int64_t* code_index, int64_t n_codes,
+                            const float* freqs_xyz, const float* freqs_dir, float* workspace,
+                            float* const* grads, float* g_code, float* d_pts, float* d_ro, float* d_rd,
+                            cn_stream_t stream);
+
 /* Backward of cn_code_bias (the code layers, model.py:174-177, and the code
  * halves of layer_xyz2 / fc_out / fc_rgb) from g_code.  dz_s / dz_t (n_codes, 256)
  * are written (either may be NULL); grads as in cn_field_backward (accumulated). */
@@ -354,10 +379,13 @@ int cn_ray_points_backward(const float* g_pts, const float* z, int64_t n_rays, i
  *           lambda * (||z_s|| + ||z_t||), their sum, ||z_s||, ||z_t||] (fp32, device), with
  * ||z|| = sqrt(expand * sum z^2) over n_code values (a code row expanded over `expand` rays,
  * eval; or whole tables with expand 1, train).  rgb_*: (n_rays, 3), either may be NULL;
- * target rows of target_stride floats (the first 3 are rgb).  n_code 0: no regulariser. */
+ * target rows of target_stride floats (the first 3 are rgb).  n_code 0: no regulariser.
+ * workspace: cn_render_loss_workspace_doubles(n_code) doubles (0: may be NULL) for the
+ * multi-workgroup sums of large code tensors. */
+int64_t cn_render_loss_workspace_doubles(int64_t n_code);
 int cn_render_loss(const float* rgb_coarse, const float* rgb_fine, const float* target,
                    int64_t target_stride, int64_t n_rays, const float* z_s, const float* z_t,
-                   int64_t n_code, int64_t expand, float regularizer_lambda, float* out,
+                   int64_t n_code, int64_t expand, float regularizer_lambda, double* workspace, float* out,
                    cn_stream_t stream);
 /* Its backward for an upstream gradient *grad_total (device scalar) of the sum, reading
  * the forward's out as stats: d_rgb_* (n_rays, 3) and d_z_* (n_code) WRITTEN (any NULL). */

@@ -228,17 +228,21 @@ def test_render_loss_golden(dev):
         close(t.grad, g[k], 1e-5, k)
 
 
-def test_render_loss_train_regulariser_is_constant(dev):
-    """train.py:106-107: the regulariser over the whole tables' .data has no gradient."""
+@pytest.mark.parametrize("n_obj", [7, 2458])
+def test_render_loss_train_regulariser_is_constant(dev, n_obj):
+    """train.py:106-107: the regulariser over the whole tables' .data has no gradient (2458 objects:
+    the multi-workgroup partial sums)."""
     from codenerf.autograd import render_loss_autograd
     g = torch.Generator().manual_seed(2)
     rc = torch.rand(100, 3, generator=g).to(dev).requires_grad_(True)
     t = torch.rand(100, 4, generator=g).to(dev)
-    tab_s, tab_t = torch.randn(7, 256, generator=g).to(dev), torch.randn(7, 256, generator=g).to(dev)
+    tab_s, tab_t = torch.randn(n_obj, 256, generator=g).to(dev), torch.randn(n_obj, 256, generator=g).to(dev)
     loss, stats = render_loss_autograd(rc, rc, t, tab_s, tab_t, 1, 1e-5)
     loss.backward()
-    ref = 2 * torch.nn.functional.mse_loss(rc.detach()[..., :3], t[..., :3]) + 1e-5 * (tab_s.norm() + tab_t.norm())
-    assert abs(loss.item() - ref.item()) <= 1e-6
+    ref = 2 * torch.nn.functional.mse_loss(rc.detach()[..., :3], t[..., :3]) + 1e-5 * (tab_s.double().norm() +
+                                                                                       tab_t.double().norm())
+    assert abs(loss.item() - ref.item()) <= 1e-6 * max(1.0, ref.item())
+    assert abs(stats[4].item() - tab_s.double().norm().item()) <= 1e-6 * tab_s.double().norm().item()
     close(rc.grad, 2 * 2 * (rc.detach() - t[..., :3]) / 300, 1e-5, "d rgb")
 
 

@@ -120,7 +120,7 @@ def test_train_minibatch_matches_oracle(dev, monkeypatch, chunk, mixed):
     from codenerf import ops, train as T
     from codenerf.nerf import PointSampler
     seen = {"z_fine": None, "saved": [], "w_coarse": None}
-    real_pdf, real_train = ops.sample_pdf, ops.radiance_field_train
+    real_pdf, real_train, real_w16 = ops.sample_pdf, ops.radiance_field_train, ops.radiance_field_train_w16
 
     def spy_pdf(*a, **k):
         r = real_pdf(*a, **k)
@@ -132,8 +132,13 @@ def test_train_minibatch_matches_oracle(dev, monkeypatch, chunk, mixed):
         raw, saved = real_train(*a, **k)
         seen["saved"].append(saved)
         return raw, saved
+    def spy_w16(*a, **k):           # the fused fp32 training path (16-sample waves of one code row)
+        raw, saved, masks = real_w16(*a, **k)
+        seen["saved"].append(saved)
+        return raw, saved, masks
     monkeypatch.setattr(ops, "sample_pdf", spy_pdf)
     monkeypatch.setattr(ops, "radiance_field_train", spy_train)
+    monkeypatch.setattr(ops, "radiance_field_train_w16", spy_w16)
 
     def relu_masks(saved):
         sv = saved.detach().cpu()
