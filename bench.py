@@ -444,8 +444,9 @@ def train_bench(dev, k, iters, world):
             "params": n_params, "loss": float(logs[-1]["total_loss"]), "dtype": "f32",
             "adamw": {"kernel_ms": adamw_ms, "bytes": 28 * n_params,
                       "gbps": 28 * n_params / (adamw_ms * 1e-3) / 1e9},
-            "note": "fp32 training field kernel (activations kept), layer-wise fp32 MFMA backward GEMMs, "
-                    "flat AdamW; train.py's per-chunk psnr read-back included"}
+            "note": "fp32 16x16x4 training forward (activations + ReLU masks kept), ONE fused fp32 dX backward "
+                    "launch per field (masked layer gradients kept), split-M fp32 MFMA dW GEMMs, fused loss, flat "
+                    "AdamW; train.py's per-chunk psnr read-back included"}
 
 
 def cpu_threads() -> int:
