@@ -170,6 +170,109 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(const float* __restrict__ 
     }
 }
 
+// gemm_tn for the 256 x 256 weight gradients (layer_dir2 / layer_dir1 / fc_out / layer_xyz2),
+// row-contiguous operands (lda = ldb = 256): one 512-thread workgroup per CU owns the WHOLE
+// 256 x 256 tile over its slab of M rows, so every dPre / X value crosses HBM once.  The slab
+// streams through a 4-stage LDS ring by LDS-DMA (buffer_load_dword ... lds, 1 KiB = one row per
+// wave-instruction; a stage = 16 rows of A and of B = 32 KiB), three stages in flight, one
+// counted-vmcnt barrier per stage -- the field kernels' scheme.  Wave w: rows 64 (w >> 1) .. of
+// n, columns 128 (w & 1) .. of k = 2 x 4 accumulators of v_mfma_f32_32x32x2_f32 (128 registers),
+// two waves per SIMD; per row pair it reads its 6 operands with ds_read_b32 (a half-wave reads
+// 128 contiguous bytes of one row: conflict free).  Rows past M load as zeros (buffer bounds).
+// The slab's partial tile is flushed with one float atomic per element.
+constexpr int kTwRows = 16;                    // rows of A and of B per stage
+constexpr int kTwStage = 2 * kTwRows * 256;    // floats per stage (A rows, then B rows)
+constexpr int kTwRing = 4;
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+__global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restrict__ A, const float* __restrict__ B,
+                                                            float* __restrict__ C, int64_t ldc, int64_t M,
+                                                            int64_t rows_per_block) {
+  __shared__ __attribute__((aligned(16))) float ring[kTwRing * kTwStage];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int i = lane & 31, h = lane >> 5;
+  const int n0 = (wave >> 1) * 64, k0 = (wave & 1) * 128;
+  const int64_t mb = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t rows = min(rows_per_block, M - mb);
+  const unsigned bytes = static_cast<unsigned>(rows * 256 * 4);
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(A + mb * 256), 0, bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(B + mb * 256), 0, bytes, 0x00020000);
+  const int n_stages = static_cast<int>((rows + kTwRows - 1) / kTwRows);
+  // stage st: wave w moves rows w + 8 j of A and of B (j < kTwRows / 8), 4 B per lane x 4
+  // instructions per row: kTwRows wave-instructions per stage
+  auto dma = [&](int st) {
+    float* slot = ring + (st & (kTwRing - 1)) * kTwStage;
+#pragma unroll
+    for (int j = 0; j < kTwRows / 8; ++j) {
+      const int r = wave + 8 * j;
+      const unsigned row_off = static_cast<unsigned>((st * kTwRows + r) * 1024);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const unsigned soff = __builtin_amdgcn_readfirstlane(row_off + q * 256);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(slot + r * 256 + q * 64), 4, lane * 4u, soff, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr_t)(slot + (kTwRows + r) * 256 + q * 64), 4, lane * 4u,
+                                                 soff, 0, 0);
+      }
+    }
+  };
+  floatx16 acc[2][4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[t][u] = floatx16{0};
+  dma(0);
+  dma(1);
+  dma(2);
+  for (int st = 0; st < n_stages; ++st) {
+    // stage st landed (all but this wave's 2 kTwRows youngest pieces: stages st+1, st+2) and
+    // every wave is done with stage st-1, whose slot then receives stage st+3
+    static_assert(2 * kTwRows == 32, "the vmcnt below counts stages st+1, st+2");
+    asm volatile("s_waitcnt vmcnt(32)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    dma(st + 3);
+    const float* sa = ring + (st & (kTwRing - 1)) * kTwStage + h * 256 + i;
+    const float* sb = sa + kTwRows * 256;
+    // operands of row pair p + 1 are read while pair p's MFMAs run
+    float a[2][2], b[2][4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) a[0][t] = sa[n0 + 32 * t];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) b[0][u] = sb[k0 + 32 * u];
+#pragma unroll
+    for (int p = 0; p < kTwRows / 2; ++p) {
+      const int c = p & 1, nx = c ^ 1;
+      if (p + 1 < kTwRows / 2) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) a[nx][t] = sa[(p + 1) * 512 + n0 + 32 * t];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) b[nx][u] = sb[(p + 1) * 512 + k0 + 32 * u];
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[c][t], b[c][u], acc[t][u], 0, 0, 0);
+    }
+  }
+  // the prefetched stages past the slab must land before the workgroup's LDS is released
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int col = k0 + 32 * u + i;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = n0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
+        atomicAdd(&C[(int64_t)row * ldc + col], acc[t][u][r]);
+      }
+    }
+}
+
 // ---------------------------------------------------------------- 3xbf16 GEMMs
 // The same two products on v_mfma_f32_32x32x16_bf16 with each fp32 operand split
 // x = hi + lo (hi = bf16(x), lo = bf16(x - hi)) and Ah.Bh + Ah.Bl + Al.Bh accumulated in
@@ -725,6 +828,14 @@ int gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, 
     const int64_t nb = ceil_div(M, rows) * tiles;
     hipLaunchKernelGGL(grad::gemm_tn_x3_kernel, dim3(static_cast<unsigned>(nb)), dim3(256), 0, st, A, lda, B, ldb, C,
                        ldc, M, N, K, rows, static_cast<int>(ceil_div(N, grad::kTnTile)), static_cast<int>(tiles));
+    return launch_status();
+  }
+  if (N == 256 && K == 256 && lda == 256 && ldb == 256 && M >= 64 * 1024) {
+    // whole-tile kernel: one workgroup per CU over M / 256 rows each (a multiple of the stage)
+    int64_t rows = ceil_div(M, 256);
+    rows = ceil_div(rows, grad::kTwRows) * grad::kTwRows;
+    hipLaunchKernelGGL(grad::gemm_tn256_kernel, dim3(static_cast<unsigned>(ceil_div(M, rows))), dim3(512), 0, st, A,
+                       B, C, ldc, M, rows);
     return launch_status();
   }
   const int64_t splits = std::max<int64_t>(1, 1024 / tiles);
