@@ -723,15 +723,30 @@ __global__ __launch_bounds__(256) void code_backward_kernel(mlp::Params P, const
   if (j == 0) go[0] = gr[kCbSigma];
   __syncthreads();
   {
-    float a1 = 0.f, a2 = 0.f, a3 = 0.f;
-    for (int k = 0; k < 256; ++k) {
-      a1 = fmaf(P.p[kWSc1][j * 256 + k], zs[k], a1);
-      a2 = fmaf(P.p[kWSc2][j * 256 + k], zs[k], a2);
-      a3 = fmaf(P.p[kWTc1][j * 256 + k], zt[k], a3);
+    // the three code layers (model.py:174-177) recomputed: wave w owns outputs 64 w .. 64 w + 63,
+    // one row at a time with its 64 lanes over k (coalesced 1 KiB rows) and a butterfly sum
+    const int lane = j & 63, w = j >> 6;
+    for (int o = 64 * w; o < 64 * w + 64; ++o) {
+      float a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int k = lane + 64 * q;
+        a1 = fmaf(P.p[kWSc1][o * 256 + k], zs[k], a1);
+        a2 = fmaf(P.p[kWSc2][o * 256 + k], zs[k], a2);
+        a3 = fmaf(P.p[kWTc1][o * 256 + k], zt[k], a3);
+      }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        a1 += __shfl_xor(a1, off);
+        a2 += __shfl_xor(a2, off);
+        a3 += __shfl_xor(a3, off);
+      }
+      if (lane == 0) {
+        s1[o] = fmaxf(a1 + P.p[kBSc1][o], 0.f);
+        s2[o] = fmaxf(a2 + P.p[kBSc2][o], 0.f);
+        t1[o] = fmaxf(a3 + P.p[kBTc1][o], 0.f);
+      }
     }
-    s1[j] = fmaxf(a1 + P.p[kBSc1][j], 0.f);
-    s2[j] = fmaxf(a2 + P.p[kBSc2][j], 0.f);
-    t1[j] = fmaxf(a3 + P.p[kBTc1][j], 0.f);
   }
   __syncthreads();
   // d zs1 = W_xyz2[:, 256:]^T g_x2, d zs2 = W_out[:, 256:]^T g_o, d zt1 = W_rgb[:, 256:]^T g_rgb (masked)
@@ -756,21 +771,25 @@ __global__ __launch_bounds__(256) void code_backward_kernel(mlp::Params P, const
     if (dz_t) dz_t[(int64_t)c * 256 + j] = b;
   }
   if (!G.p[kWSc1]) return;
-  // weight gradients of the code layers and the code halves (row j of each)
-  for (int k = 0; k < 256; ++k) {
-    atomicAdd(&const_cast<float*>(G.p[kWSc1])[j * 256 + k], ds1[j] * zs[k]);
-    atomicAdd(&const_cast<float*>(G.p[kWSc2])[j * 256 + k], ds2[j] * zs[k]);
-    atomicAdd(&const_cast<float*>(G.p[kWTc1])[j * 256 + k], dt1[j] * zt[k]);
-    atomicAdd(&const_cast<float*>(G.p[kWXyz2])[j * 512 + 256 + k], gr[kCbXyz2 + j] * s1[k]);
-    atomicAdd(&const_cast<float*>(G.p[kWOut])[(1 + j) * 512 + 256 + k], go[1 + j] * s2[k]);
+  // weight gradients of the code layers and the code halves: outer products, one row per
+  // iteration with thread j on column j (each wave's atomics hit 256 contiguous bytes)
+  __shared__ float gx2[256], grgb[3];
+  gx2[j] = gr[kCbXyz2 + j];
+  if (j < 3) grgb[j] = gr[kCbRgb + j];
+  __syncthreads();
+  const float zsj = zs[j], ztj = zt[j], s1j = s1[j], s2j = s2[j], t1j = t1[j];
+  for (int r = 0; r < 256; ++r) {
+    atomicAdd(&const_cast<float*>(G.p[kWSc1])[r * 256 + j], ds1[r] * zsj);
+    atomicAdd(&const_cast<float*>(G.p[kWSc2])[r * 256 + j], ds2[r] * zsj);
+    atomicAdd(&const_cast<float*>(G.p[kWTc1])[r * 256 + j], dt1[r] * ztj);
+    atomicAdd(&const_cast<float*>(G.p[kWXyz2])[r * 512 + 256 + j], gx2[r] * s1j);
+    atomicAdd(&const_cast<float*>(G.p[kWOut])[(1 + r) * 512 + 256 + j], go[1 + r] * s2j);
   }
   atomicAdd(&const_cast<float*>(G.p[kBSc1])[j], ds1[j]);
   atomicAdd(&const_cast<float*>(G.p[kBSc2])[j], ds2[j]);
   atomicAdd(&const_cast<float*>(G.p[kBTc1])[j], dt1[j]);
-  atomicAdd(&const_cast<float*>(G.p[kWOut])[256 + j], go[0] * s2[j]);              // fc_out row 0 (sigma)
-  if (j < 3)
-    for (int k = 0; k < 256; ++k)
-      atomicAdd(&const_cast<float*>(G.p[kWRgb])[j * 512 + 256 + k], gr[kCbRgb + j] * t1[k]);
+  atomicAdd(&const_cast<float*>(G.p[kWOut])[256 + j], go[0] * s2j);                // fc_out row 0 (sigma)
+  for (int r = 0; r < 3; ++r) atomicAdd(&const_cast<float*>(G.p[kWRgb])[r * 512 + 256 + j], grgb[r] * t1j);
 }
 
 }  // namespace grad
