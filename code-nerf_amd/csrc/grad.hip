@@ -273,6 +273,42 @@ __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restr
     }
 }
 
+// gemm_tn for a skinny dPre (N = NA <= 4 columns, e.g. d rgb / d sigma of d raw) against a
+// 256-wide X: a streaming pass over X (float4 per lane, 4 rows per 256-thread step) with the
+// 4 x NA partial sums in registers, folded through LDS and flushed with NA x 256 atomics per
+// workgroup.  Bandwidth-bound: X crosses HBM once.
+template <int NA>
+__global__ __launch_bounds__(256) void gemm_tn_skinny_kernel(const float* __restrict__ A, int64_t lda,
+                                                             const float* __restrict__ B, float* __restrict__ C,
+                                                             int64_t ldc, int64_t M, int64_t rows_per_block) {
+  __shared__ float red[4][NA][256];
+  const int t = threadIdx.x, rg = t >> 6, c4 = t & 63;
+  const int64_t mb = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t me = min(M, mb + rows_per_block);
+  float acc[NA][4] = {};
+  for (int64_t m = mb + rg; m < me; m += 4) {
+    const float4 x = reinterpret_cast<const float4*>(B + m * 256)[c4];
+#pragma unroll
+    for (int n = 0; n < NA; ++n) {
+      const float av = A[m * lda + n];
+      acc[n][0] = fmaf(av, x.x, acc[n][0]);
+      acc[n][1] = fmaf(av, x.y, acc[n][1]);
+      acc[n][2] = fmaf(av, x.z, acc[n][2]);
+      acc[n][3] = fmaf(av, x.w, acc[n][3]);
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < NA; ++n)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[rg][n][4 * c4 + j] = acc[n][j];
+  __syncthreads();
+#pragma unroll
+  for (int n = 0; n < NA; ++n) {
+    const float v = (red[0][n][t] + red[1][n][t]) + (red[2][n][t] + red[3][n][t]);
+    atomicAdd(&C[n * ldc + t], v);
+  }
+}
+
 // ---------------------------------------------------------------- 3xbf16 GEMMs
 // The same two products on v_mfma_f32_32x32x16_bf16 with each fp32 operand split
 // x = hi + lo (hi = bf16(x), lo = bf16(x - hi)) and Ah.Bh + Ah.Bl + Al.Bh accumulated in
@@ -792,6 +828,21 @@ __global__ __launch_bounds__(256) void code_backward_kernel(mlp::Params P, const
   for (int r = 0; r < 3; ++r) atomicAdd(&const_cast<float*>(G.p[kWRgb])[r * 512 + 256 + j], grgb[r] * t1j);
 }
 
+// The bias gradients that are column sums of g_code (the per-code sums of the code-bias terms):
+// layer_xyz2 (cols 0..255), fc_out rows 1..256 (256..511) and row 0 (512), fc_rgb (513..515).
+__global__ void gcode_bias_kernel(const float* __restrict__ g_code, int64_t n_codes, float* __restrict__ b_xyz2,
+                                  float* __restrict__ b_out, float* __restrict__ b_rgb) {
+  using namespace mlp;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= kCbRgb + 3) return;
+  float acc = 0.0f;
+  for (int64_t c = 0; c < n_codes; ++c) acc += g_code[c * kCbStride + j];
+  if (j < kCbFeat) b_xyz2[j] += acc;
+  else if (j < kCbSigma) b_out[1 + j - kCbFeat] += acc;
+  else if (j == kCbSigma) b_out[0] += acc;
+  else b_rgb[j - kCbRgb] += acc;
+}
+
 }  // namespace grad
 }  // namespace cn
 
@@ -847,6 +898,17 @@ int gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, 
     const int64_t nb = ceil_div(M, rows) * tiles;
     hipLaunchKernelGGL(grad::gemm_tn_x3_kernel, dim3(static_cast<unsigned>(nb)), dim3(256), 0, st, A, lda, B, ldb, C,
                        ldc, M, N, K, rows, static_cast<int>(ceil_div(N, grad::kTnTile)), static_cast<int>(tiles));
+    return launch_status();
+  }
+  if (N <= 4 && K == 256 && ldb == 256 && (reinterpret_cast<uintptr_t>(B) & 15) == 0 && M >= 64 * 1024) {
+    const int64_t rows = ceil_div(ceil_div(M, 1024), 4) * 4;  // ~1024 workgroups
+    const unsigned grid = static_cast<unsigned>(ceil_div(M, rows));
+    switch (N) {
+      case 1: hipLaunchKernelGGL(grad::gemm_tn_skinny_kernel<1>, dim3(grid), dim3(256), 0, st, A, lda, B, C, ldc, M, rows); break;
+      case 2: hipLaunchKernelGGL(grad::gemm_tn_skinny_kernel<2>, dim3(grid), dim3(256), 0, st, A, lda, B, C, ldc, M, rows); break;
+      case 3: hipLaunchKernelGGL(grad::gemm_tn_skinny_kernel<3>, dim3(grid), dim3(256), 0, st, A, lda, B, C, ldc, M, rows); break;
+      default: hipLaunchKernelGGL(grad::gemm_tn_skinny_kernel<4>, dim3(grid), dim3(256), 0, st, A, lda, B, C, ldc, M, rows); break;
+    }
     return launch_status();
   }
   if (N == 256 && K == 256 && lda == 256 && ldb == 256 && M >= 64 * 1024) {
@@ -1134,9 +1196,20 @@ extern "C" int cn_field_backward_train(const float* packed_t, const float* const
   a.d_ro = d_ro;
   a.d_rd = d_rd;
   a.dpre = workspace;
+  const bool wg = grads && grads[0];
+  if (wg) {
+    a.gbias[0] = grads[kBDir2];
+    a.gbias[1] = grads[kBDir1];
+    a.gbias[2] = grads[kBXyz1];
+  }
   CN_TRY(launch_field_w16_bwd(pts ? kFromPts : kFromRayZ, a, st));
-  if (!(grads && grads[0])) return CN_OK;
+  if (!wg) return CN_OK;
   auto G = [&](int i) { return grads[i]; };
+  // biases: layer_dir2 / layer_dir1 / layer_xyz1 summed in the kernel; the others are g_code's
+  // column sums
+  hipLaunchKernelGGL(grad::gcode_bias_kernel, dim3(3), dim3(256), 0, st, g_code, n_codes, G(kBXyz2), G(kBOut),
+                     G(kBRgb));
+  CN_TRY(launch_status());
   const float* P[5];
   for (int k = 0; k < 5; ++k) P[k] = workspace + k * M * 256;
   const float* h1 = saved;
@@ -1146,24 +1219,17 @@ extern "C" int cn_field_backward_train(const float* packed_t, const float* const
   const float* v2 = saved + 4 * M * 256;
   // fc_rgb (h half): dW += d rgb^T v2
   CN_TRY(gemm_tn(d_raw, 4, v2, 256, G(kWRgb), 512, M, 3, 256, st));
-  CN_TRY(seg_sum(d_raw, 4, M, 3, M, nullptr, 1, G(kBRgb), 1, st));
   // layer_dir2
   CN_TRY(gemm_tn(P[0], 256, v1, 256, G(kWDir2), 256, M, 256, 256, st));
-  CN_TRY(seg_sum(P[0], 256, M, 256, M, nullptr, 1, G(kBDir2), 1, st));
   // layer_dir1: [feat | dir enc]
   CN_TRY(gemm_tn(P[1], 256, feat, 256, G(kWDir1), 283, M, 256, 256, st));
   CN_TRY(gemm_tn(P[1], 256, x_enc + 63, 90, G(kWDir1) + 256, 283, M, 256, 27, st));
-  CN_TRY(seg_sum(P[1], 256, M, 256, M, nullptr, 1, G(kBDir1), 1, st));
   // fc_out (h half): row 0 from d sigma, rows 1.. from d feat
   CN_TRY(gemm_tn(d_raw + 3, 4, h2, 256, G(kWOut), 512, M, 1, 256, st));
   CN_TRY(gemm_tn(P[2], 256, h2, 256, G(kWOut) + 512, 512, M, 256, 256, st));
-  CN_TRY(seg_sum(d_raw + 3, 4, M, 1, M, nullptr, 1, G(kBOut), 1, st));
-  CN_TRY(seg_sum(P[2], 256, M, 256, M, nullptr, 1, G(kBOut) + 1, 1, st));
   // layer_xyz2 (h half)
   CN_TRY(gemm_tn(P[3], 256, h1, 256, G(kWXyz2), 512, M, 256, 256, st));
-  CN_TRY(seg_sum(P[3], 256, M, 256, M, nullptr, 1, G(kBXyz2), 1, st));
   // layer_xyz1
   CN_TRY(gemm_tn(P[4], 256, x_enc, 90, G(kWXyz1), 63, M, 256, 63, st));
-  CN_TRY(seg_sum(P[4], 256, M, 256, M, nullptr, 1, G(kBXyz1), 1, st));
   return CN_OK;
 }

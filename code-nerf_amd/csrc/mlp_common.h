@@ -45,6 +45,7 @@ struct FieldArgs {
   float* d_ro;           // backward: (n_rays, 3) accumulated (kFromRayZ)
   float* d_rd;           // backward: (n_rays, 3) accumulated
   float* dpre;           // fp32 fused training backward: (5, m, 256) masked layer-input gradients
+  float* gbias[3];       // ... and the bias gradients of layer_dir2, layer_dir1, layer_xyz1 (accumulated)
 };
 
 // One sample's inputs: point, unit Q1 view direction, code row.

@@ -554,7 +554,8 @@ constexpr int kTRgb = 0, kTDir2 = 1, kTDir1 = 9, kTDDir = 17, kTOut = 18, kTXyz2
 constexpr int kTSig = 0;  // transposed-pack constants: fc_out row 0 over h2, [g][ob][r]
 // LDS after the ring: constants, one g_code row per wave
 constexpr int kBGacc = kConsts;
-constexpr int kBwdLdsFloats = kBGacc + kWaves * kCbStride;
+constexpr int kBBias = kBGacc + kWaves * kCbStride;  // training: bias-gradient rows dir2 | dir1 | xyz1 (shared)
+constexpr int kBwdLdsFloats = kBBias + 3 * 256;
 constexpr int kBwdLdsQuads = kRing * kChunkQuads + kBwdLdsFloats / 4;
 static_assert(kBwdLdsQuads * 16 <= 160 * 1024, "LDS budget (backward)");
 static_assert(kTXyz1 + 2 == kChunks, "backward chunk schedule");
@@ -732,6 +733,11 @@ __device__ __forceinline__ void dbg_acc(const State& s, const FieldArgs& a, int 
     for (int r = 0; r < 4; ++r) d[16 * ob + r] = s.acc[ob][r];
 }
 
+// Training backward: the workgroup's bias-gradient row l (layer_dir2, layer_dir1, layer_xyz1) in LDS.
+__device__ __forceinline__ float* bias_row(float4* lds, int l) {
+  return reinterpret_cast<float*>(lds + kRing * kChunkQuads) + kBBias + 256 * l;
+}
+
 // Training backward: the masked input gradient of a layer (its dPre, what dW = dPre^T X reads) as
 // plane `plane` of a.dpre: 0 layer_dir2, 1 layer_dir1, 2 fc_out rows 1.. (d feat), 3 layer_xyz2,
 // 4 layer_xyz1.
@@ -787,12 +793,14 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   // ---- layer_dir2^T (m_v2), layer_dir1^T (m_v1)
   mask_act(s, mk[3]);
   save_dpre<TRAIN>(s, a, 0, row, valid);
+  if constexpr (TRAIN) gcode_add64(s, bias_row(lds, 0), 0, s.act);
   zero_acc(s);
   __builtin_amdgcn_sched_barrier(0);
   layer256(s, lds, c);
   dbg_acc(s, a, 1, row, valid);
   mask_act(s, mk[2]);
   save_dpre<TRAIN>(s, a, 1, row, valid);
+  if constexpr (TRAIN) gcode_add64(s, bias_row(lds, 1), 0, s.act);
   zero_acc(s);
   __builtin_amdgcn_sched_barrier(0);
   layer256(s, lds, c);
@@ -832,6 +840,7 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   // ---- layer_xyz1^T (m_h1): encoding k-steps 0-7, then 8-15
   mask_act(s, mk[0]);
   save_dpre<TRAIN>(s, a, 4, row, valid);
+  if constexpr (TRAIN) gcode_add64(s, bias_row(lds, 2), 0, s.act);
   float genc[16];
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
@@ -942,7 +951,7 @@ __global__ __launch_bounds__(kThreads, 2) void field_w16_bwd_kernel(FieldArgs a)
   s.voff = static_cast<unsigned>(s.wave * 64 + s.lane) * 16u;
   float* grow = blds + kBGacc + s.wave * kCbStride;
   for (int k = threadIdx.x; k < kConsts; k += kThreads) blds[k] = a.packed[kStreamFloats + k];
-  for (int k = threadIdx.x; k < kWaves * kCbStride; k += kThreads) blds[kBGacc + k] = 0.0f;
+  for (int k = threadIdx.x; k < kBwdLdsFloats - kBGacc; k += kThreads) blds[kBGacc + k] = 0.0f;
   __syncthreads();
   dma_chunk(s, lds, 0);
   dma_chunk(s, lds, 1);
@@ -956,6 +965,13 @@ __global__ __launch_bounds__(kThreads, 2) void field_w16_bwd_kernel(FieldArgs a)
     bwd_tile<MODE, TRAIN>(s, a, lds, grow, tile, cur_code);
   __builtin_amdgcn_s_waitcnt(0x0F70);
   if (cur_code >= 0) flush_gcode(s, a, grow, cur_code);
+  if constexpr (TRAIN) {
+    __syncthreads();  // every wave's bias atomics landed
+    for (int k = threadIdx.x; k < 3 * 256; k += kThreads) {
+      const float v = blds[kBBias + k];
+      if (v != 0.0f && a.gbias[k >> 8]) atomicAdd(a.gbias[k >> 8] + (k & 255), v);
+    }
+  }
 }
 
 }  // namespace w16

@@ -101,7 +101,8 @@ def test_gemm_nn_strided_a(dev, m, k, lda, precision):
 
 
 @pytest.mark.parametrize("precision", ["f32", "bf16x3"])
-@pytest.mark.parametrize("m,n,k", [(5000, 257, 256), (33, 3, 256), (4096, 256, 63), (65536, 256, 256), (70001, 3, 283)])
+@pytest.mark.parametrize("m,n,k", [(5000, 257, 256), (33, 3, 256), (4096, 256, 63), (65536, 256, 256), (70001, 3, 283),
+                                   (70001, 3, 256), (65537, 1, 256), (131075, 256, 256)])
 def test_gemm_tn_accumulates(dev, m, n, k, precision):
     from codenerf import ops
     g = torch.Generator().manual_seed(m * 3 + n + k)
