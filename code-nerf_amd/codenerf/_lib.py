@@ -94,6 +94,8 @@ SIGNATURES = {
     "cn_gemm_tn": (_i, [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _p]),
     "cn_gemm_nn_x3": (_i, [_p, _i64, _p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _p]),
     "cn_gemm_tn_x3": (_i, [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _p]),
+    "cn_gemm_tn_workspace_floats": (_i64, [_i64, _i64, _i64]),
+    "cn_gemm_tn_ws": (_i, [_i, _p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _p, _p]),
     "cn_render_loss_workspace_doubles": (_i64, [_i64]),
     "cn_render_loss": (_i, [_p, _p, _p, _i64, _i64, _p, _p, _i64, _i64, _f, _p, _p, _p]),
     "cn_render_loss_backward": (_i, [_p, _p, _p, _i64, _i64, _p, _p, _i64, _i64, _f, _p, _p, _p, _p, _p, _p, _p]),

@@ -592,14 +592,21 @@ def gemm_nn(a: Tensor, b: Tensor, mask: Optional[Tensor] = None, precision: str 
     return c
 
 
-def gemm_tn(a: Tensor, b: Tensor, c: Optional[Tensor] = None, precision: str = "f32") -> Tensor:
-    """C += A^T B on the fp32 (or 3xbf16) MFMA tile kernel (C zero-initialised when not given)."""
+def gemm_tn(a: Tensor, b: Tensor, c: Optional[Tensor] = None, precision: str = "f32",
+            deterministic: bool = False) -> Tensor:
+    """C += A^T B on the fp32 (or 3xbf16) MFMA tile kernel (C zero-initialised when not given).
+    deterministic: partial tiles + a fixed-order reduction (cn_gemm_tn_ws) instead of float atomics."""
     lib = _lib_ready()
     a, b = _cuda(a, "A"), _cuda(b, "B")
     (m, n), (m2, k) = a.shape, b.shape
     assert m == m2
     if c is None:
         c = torch.zeros(n, k, device=a.device, dtype=torch.float32)
+    if deterministic:
+        ws = torch.empty(lib.cn_gemm_tn_workspace_floats(m, n, k), device=a.device, dtype=torch.float32)
+        fmt = _lib.FORMATS["bf16x3" if precision == "bf16x3" else "f32"]
+        check(lib.cn_gemm_tn_ws(fmt, ptr(a), n, ptr(b), k, ptr(c), k, m, n, k, ptr(ws), stream_of(a)), "cn_gemm_tn_ws")
+        return c
     fn, name = (lib.cn_gemm_tn_x3, "cn_gemm_tn_x3") if precision == "bf16x3" else (lib.cn_gemm_tn, "cn_gemm_tn")
     check(fn(ptr(a), n, ptr(b), k, ptr(c), k, m, n, k, stream_of(a)), name)
     return c

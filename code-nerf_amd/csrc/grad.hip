@@ -109,6 +109,53 @@ __global__ __launch_bounds__(256) void gemm_nn_kernel(const float* __restrict__ 
     }
 }
 
+// Flush of one 32 x 32 accumulator block (rows row0.., columns col0.. of C): float atomics
+// into C, or -- the deterministic path -- plain stores into this workgroup's partial tile
+// (N x K, row-major) of the workspace, summed in a fixed order by reduce_partials_kernel.
+__device__ __forceinline__ void flush_block(const floatx16& acc, float* C, int64_t ldc, float* part, int N, int K,
+                                            int row0, int col0, int i, int h) {
+  const int col = col0 + i;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = row0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    if (row < N && col < K) {
+      if (part) part[(int64_t)row * K + col] = acc[r];
+      else atomicAdd(&C[(int64_t)row * ldc + col], acc[r]);
+    }
+  }
+}
+
+// C[n][k] += sum_p part[p][n][k], p in order (one thread per element, 4 partial streams per
+// element combined in a fixed tree): the deterministic second pass of the split-M dW GEMMs.
+__global__ __launch_bounds__(256) void reduce_partials_kernel(const float* __restrict__ part, int64_t n_parts,
+                                                              int N, int K, float* __restrict__ C, int64_t ldc) {
+  __shared__ float red[4][64];
+  const int q = threadIdx.x >> 6, t = threadIdx.x & 63;
+  const int64_t nk = (int64_t)N * K;
+  const int64_t e = (int64_t)blockIdx.x * 64 + t;
+  float s = 0.0f;
+  if (e < nk) {
+    const int64_t p0 = n_parts * q / 4, p1 = n_parts * (q + 1) / 4;
+    float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
+    int64_t p = p0;
+    for (; p + 4 <= p1; p += 4) {
+      s0 += part[p * nk + e];
+      s1 += part[(p + 1) * nk + e];
+      s2 += part[(p + 2) * nk + e];
+      s3 += part[(p + 3) * nk + e];
+    }
+    for (; p < p1; ++p) s0 += part[p * nk + e];
+    s = (s0 + s1) + (s2 + s3);
+  }
+  red[q][t] = s;
+  __syncthreads();
+  if (q == 0 && e < nk) {
+    const float v = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+    float* c = C + (e / K) * ldc + e % K;
+    *c += v;
+  }
+}
+
 // gemm_tn: C[n][k] += sum_m A[m][n] B[m][k] (dW = dPre^T X).  No LDS: on
 // v_mfma_f32_32x32x2_f32 lane l's A operand is A[m + (l >> 5)][n + (l & 31)] and its B
 // operand B[m + (l >> 5)][k + (l & 31)], so each half-wave reads 32 consecutive floats of
@@ -121,8 +168,8 @@ constexpr int kTnTile = 128, kTnPairs = 8;
 
 __global__ __launch_bounds__(256) void gemm_tn_kernel(const float* __restrict__ A, int64_t lda,
                                                       const float* __restrict__ B, int64_t ldb,
-                                                      float* __restrict__ C, int64_t ldc, int64_t M,
-                                                      int N, int K, int64_t rows_per_block) {
+                                                      float* __restrict__ C, int64_t ldc, float* __restrict__ part,
+                                                      int64_t M, int N, int K, int64_t rows_per_block) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int i = lane & 31, h = lane >> 5;
   const int n0 = blockIdx.x * kTnTile + (wave >> 1) * 64;
@@ -155,167 +202,35 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(const float* __restrict__ 
       acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[p], b1[p], acc11, 0, 0, 0);
     }
   }
-  const floatx16* accs[4] = {&acc00, &acc01, &acc10, &acc11};
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const floatx16& acc = *accs[2 * t + u];
-      const int col = k0 + 32 * u + i;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = n0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (row < N && col < K) atomicAdd(&C[(int64_t)row * ldc + col], acc[r]);
-      }
-    }
+  float* pt = part ? part + (int64_t)blockIdx.z * N * K : nullptr;
+  flush_block(acc00, C, ldc, pt, N, K, n0, k0, i, h);
+  flush_block(acc01, C, ldc, pt, N, K, n0, k0 + 32, i, h);
+  flush_block(acc10, C, ldc, pt, N, K, n0 + 32, k0, i, h);
+  flush_block(acc11, C, ldc, pt, N, K, n0 + 32, k0 + 32, i, h);
 }
 
 // gemm_tn for the 256 x 256 weight gradients (layer_dir2 / layer_dir1 / fc_out / layer_xyz2),
 // row-contiguous operands (lda = ldb = 256): one 512-thread workgroup per CU owns the WHOLE
 // 256 x 256 tile over its slab of M rows, so every dPre / X value crosses HBM once.  The slab
-// streams through a 4-stage LDS ring by LDS-DMA (buffer_load_dword ... lds, 1 KiB = one row per
+// streams through a 4-stage LDS ring by LDS-DMA (buffer_load_dwordx4 ... lds, 1 KiB = one row per
 // wave-instruction; a stage = 16 rows of A and of B = 32 KiB), three stages in flight, one
 // counted-vmcnt barrier per stage -- the field kernels' scheme.  Wave w: rows 64 (w >> 1) .. of
 // n, columns 128 (w & 1) .. of k = 2 x 4 accumulators of v_mfma_f32_32x32x2_f32 (128 registers),
 // two waves per SIMD; per row pair it reads its 6 operands with ds_read_b32 (a half-wave reads
 // 128 contiguous bytes of one row: conflict free).  Rows past M load as zeros (buffer bounds).
-// The slab's partial tile is flushed with one float atomic per element.
+// The slab's partial tile is flushed with one float atomic per element, or stored to the
+// workspace for the deterministic reduction.  X3: the same stream with 3xbf16 MFMAs (x3_stage).
 constexpr int kTwRows = 16;                    // rows of A and of B per stage
 constexpr int kTwStage = 2 * kTwRows * 256;    // floats per stage (A rows, then B rows)
 constexpr int kTwRing = 4;
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-__global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restrict__ A, const float* __restrict__ B,
-                                                            float* __restrict__ C, int64_t ldc, int64_t M,
-                                                            int64_t rows_per_block) {
-  __shared__ __attribute__((aligned(16))) float ring[kTwRing * kTwStage];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int i = lane & 31, h = lane >> 5;
-  const int n0 = (wave >> 1) * 64, k0 = (wave & 1) * 128;
-  const int64_t mb = (int64_t)blockIdx.x * rows_per_block;
-  const int64_t rows = min(rows_per_block, M - mb);
-  const unsigned bytes = static_cast<unsigned>(rows * 256 * 4);
-  const __amdgpu_buffer_rsrc_t ra =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(A + mb * 256), 0, bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rb =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(B + mb * 256), 0, bytes, 0x00020000);
-  const int n_stages = static_cast<int>((rows + kTwRows - 1) / kTwRows);
-  // stage st: wave w moves rows w + 8 j of A and of B (j < kTwRows / 8), 4 B per lane x 4
-  // instructions per row: kTwRows wave-instructions per stage
-  auto dma = [&](int st) {
-    float* slot = ring + (st & (kTwRing - 1)) * kTwStage;
-#pragma unroll
-    for (int j = 0; j < kTwRows / 8; ++j) {
-      const int r = wave + 8 * j;
-      const unsigned row_off = static_cast<unsigned>((st * kTwRows + r) * 1024);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const unsigned soff = __builtin_amdgcn_readfirstlane(row_off + q * 256);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(slot + r * 256 + q * 64), 4, lane * 4u, soff, 0, 0);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr_t)(slot + (kTwRows + r) * 256 + q * 64), 4, lane * 4u,
-                                                 soff, 0, 0);
-      }
-    }
-  };
-  floatx16 acc[2][4];
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int u = 0; u < 4; ++u) acc[t][u] = floatx16{0};
-  dma(0);
-  dma(1);
-  dma(2);
-  for (int st = 0; st < n_stages; ++st) {
-    // stage st landed (all but this wave's 2 kTwRows youngest pieces: stages st+1, st+2) and
-    // every wave is done with stage st-1, whose slot then receives stage st+3
-    static_assert(2 * kTwRows == 32, "the vmcnt below counts stages st+1, st+2");
-    asm volatile("s_waitcnt vmcnt(32)\n\ts_barrier" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    dma(st + 3);
-    const float* sa = ring + (st & (kTwRing - 1)) * kTwStage + h * 256 + i;
-    const float* sb = sa + kTwRows * 256;
-    // operands of row pair p + 1 are read while pair p's MFMAs run
-    float a[2][2], b[2][4];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) a[0][t] = sa[n0 + 32 * t];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) b[0][u] = sb[k0 + 32 * u];
-#pragma unroll
-    for (int p = 0; p < kTwRows / 2; ++p) {
-      const int c = p & 1, nx = c ^ 1;
-      if (p + 1 < kTwRows / 2) {
-#pragma unroll
-        for (int t = 0; t < 2; ++t) a[nx][t] = sa[(p + 1) * 512 + n0 + 32 * t];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) b[nx][u] = sb[(p + 1) * 512 + k0 + 32 * u];
-      }
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[c][t], b[c][u], acc[t][u], 0, 0, 0);
-    }
-  }
-  // the prefetched stages past the slab must land before the workgroup's LDS is released
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int col = k0 + 32 * u + i;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = n0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
-        atomicAdd(&C[(int64_t)row * ldc + col], acc[t][u][r]);
-      }
-    }
-}
-
-// gemm_tn for a skinny dPre (N = NA <= 4 columns, e.g. d rgb / d sigma of d raw) against a
-// 256-wide X: a streaming pass over X (float4 per lane, 4 rows per 256-thread step) with the
-// 4 x NA partial sums in registers, folded through LDS and flushed with NA x 256 atomics per
-// workgroup.  Bandwidth-bound: X crosses HBM once.
-template <int NA>
-__global__ __launch_bounds__(256) void gemm_tn_skinny_kernel(const float* __restrict__ A, int64_t lda,
-                                                             const float* __restrict__ B, float* __restrict__ C,
-                                                             int64_t ldc, int64_t M, int64_t rows_per_block) {
-  __shared__ float red[4][NA][256];
-  const int t = threadIdx.x, rg = t >> 6, c4 = t & 63;
-  const int64_t mb = (int64_t)blockIdx.x * rows_per_block;
-  const int64_t me = min(M, mb + rows_per_block);
-  float acc[NA][4] = {};
-  for (int64_t m = mb + rg; m < me; m += 4) {
-    const float4 x = reinterpret_cast<const float4*>(B + m * 256)[c4];
-#pragma unroll
-    for (int n = 0; n < NA; ++n) {
-      const float av = A[m * lda + n];
-      acc[n][0] = fmaf(av, x.x, acc[n][0]);
-      acc[n][1] = fmaf(av, x.y, acc[n][1]);
-      acc[n][2] = fmaf(av, x.z, acc[n][2]);
-      acc[n][3] = fmaf(av, x.w, acc[n][3]);
-    }
-  }
-#pragma unroll
-  for (int n = 0; n < NA; ++n)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) red[rg][n][4 * c4 + j] = acc[n][j];
-  __syncthreads();
-#pragma unroll
-  for (int n = 0; n < NA; ++n) {
-    const float v = (red[0][n][t] + red[1][n][t]) + (red[2][n][t] + red[3][n][t]);
-    atomicAdd(&C[n * ldc + t], v);
-  }
-}
-
-// ---------------------------------------------------------------- 3xbf16 GEMMs
-// The same two products on v_mfma_f32_32x32x16_bf16 with each fp32 operand split
-// x = hi + lo (hi = bf16(x), lo = bf16(x - hi)) and Ah.Bh + Ah.Bl + Al.Bh accumulated in
-// fp32 (the dropped Al.Bl and the lo rounding leave ~2^-17 relative error per product,
-// the field kernel's scheme).  On 32x32x16 lane l = 32h + i holds A[row i][k = 8h + j]
-// and B[k = 8h + j][col i], j = 0..7: exactly the 8 consecutive k values the fp32
-// kernels' lanes already load, so one bf16 MFMA triple replaces 8 fp32 MFMAs.
+// 3xbf16 form of one stage (X3: the bf16x3 training step): the stage's 16 rows are ONE k-step of
+// v_mfma_f32_32x32x16_bf16 (lane l = 32h + i: rows 8h .. 8h + 7 of feature i of a block).  Each
+// lane reads its 8 rows per block with ds_read_b32 (a half-wave reads 128 contiguous bytes of a
+// row: conflict free), splits them x = hi + lo and issues Ah.Bh + Ah.Bl + Al.Bh per output block
+// (24 MFMAs per wave and stage).  At 3 bf16 MFMAs per 32x32x16 product the kernel is HBM-bound.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -347,6 +262,158 @@ __device__ __forceinline__ floatx16 mfma3(floatx16 acc, u32x4 ah, u32x4 al, u32x
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_l, b_h, acc, 0, 0, 0);
   return acc;
 }
+
+static_assert(kTwRows == 16, "x3_stage: one stage = one 16-deep k-step");
+__device__ __forceinline__ void x3_stage(const float* slot, int i, int h, int n0, int k0, floatx16 (&acc)[2][4]) {
+  const float* sa = slot + 8 * h * 256 + i;
+  const float* sb = sa + kTwRows * 256;
+  u32x4 ah[2], al[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = sa[j * 256 + n0 + 32 * t];
+    split8(v, ah[t], al[t]);
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = sb[j * 256 + k0 + 32 * u];
+    u32x4 bh, bl;
+    split8(v, bh, bl);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) acc[t][u] = mfma3(acc[t][u], ah[t], al[t], bh, bl);
+  }
+}
+
+template <bool X3>
+__global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restrict__ A, const float* __restrict__ B,
+                                                            float* __restrict__ C, int64_t ldc, float* __restrict__ part,
+                                                            int64_t M, int64_t rows_per_block) {
+  __shared__ __attribute__((aligned(16))) float ring[kTwRing * kTwStage];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int i = lane & 31, h = lane >> 5;
+  const int n0 = (wave >> 1) * 64, k0 = (wave & 1) * 128;
+  const int64_t mb = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t rows = min(rows_per_block, M - mb);
+  const unsigned bytes = static_cast<unsigned>(rows * 256 * 4);
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(A + mb * 256), 0, bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(B + mb * 256), 0, bytes, 0x00020000);
+  const int n_stages = static_cast<int>((rows + kTwRows - 1) / kTwRows);
+  // stage st: wave w moves rows w + 8 j of A and of B (j < kTwRows / 8), one 16-B-per-lane
+  // wave-instruction per 1 KiB row: kTwRows / 4 wave-instructions per stage
+  auto dma = [&](int st) {
+    float* slot = ring + (st & (kTwRing - 1)) * kTwStage;
+#pragma unroll
+    for (int j = 0; j < kTwRows / 8; ++j) {
+      const int r = wave + 8 * j;
+      const unsigned soff = __builtin_amdgcn_readfirstlane(static_cast<unsigned>((st * kTwRows + r) * 1024));
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(slot + r * 256), 16, lane * 16u, soff, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr_t)(slot + (kTwRows + r) * 256), 16, lane * 16u, soff, 0, 0);
+    }
+  };
+  floatx16 acc[2][4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[t][u] = floatx16{0};
+  dma(0);
+  dma(1);
+  dma(2);
+  for (int st = 0; st < n_stages; ++st) {
+    // stage st landed (all but this wave's 2 kTwRows youngest pieces: stages st+1, st+2) and
+    // every wave is done with stage st-1, whose slot then receives stage st+3
+    static_assert(kTwRows / 2 == 8, "the vmcnt below counts stages st+1, st+2");
+    asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    dma(st + 3);
+    if constexpr (X3) {
+      x3_stage(ring + (st & (kTwRing - 1)) * kTwStage, i, h, n0, k0, acc);
+      continue;
+    }
+    const float* sa = ring + (st & (kTwRing - 1)) * kTwStage + h * 256 + i;
+    const float* sb = sa + kTwRows * 256;
+    // operands of row pair p + 1 are read while pair p's MFMAs run
+    float a[2][2], b[2][4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) a[0][t] = sa[n0 + 32 * t];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) b[0][u] = sb[k0 + 32 * u];
+#pragma unroll
+    for (int p = 0; p < kTwRows / 2; ++p) {
+      const int c = p & 1, nx = c ^ 1;
+      if (p + 1 < kTwRows / 2) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) a[nx][t] = sa[(p + 1) * 512 + n0 + 32 * t];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) b[nx][u] = sb[(p + 1) * 512 + k0 + 32 * u];
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[c][t], b[c][u], acc[t][u], 0, 0, 0);
+    }
+  }
+  // the prefetched stages past the slab must land before the workgroup's LDS is released
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  float* pt = part ? part + (int64_t)blockIdx.x * 65536 : nullptr;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) flush_block(acc[t][u], C, ldc, pt, 256, 256, n0 + 32 * t, k0 + 32 * u, i, h);
+}
+
+// gemm_tn for a skinny dPre (N = NA <= 4 columns, e.g. d rgb / d sigma of d raw) against a
+// 256-wide X: a streaming pass over X (float4 per lane, 4 rows per 256-thread step) with the
+// 4 x NA partial sums in registers, folded through LDS and flushed with NA x 256 atomics per
+// workgroup (or stored as the workgroup's partial row block: the deterministic path).
+// Bandwidth-bound: X crosses HBM once.
+template <int NA>
+__global__ __launch_bounds__(256) void gemm_tn_skinny_kernel(const float* __restrict__ A, int64_t lda,
+                                                             const float* __restrict__ B, float* __restrict__ C,
+                                                             int64_t ldc, float* __restrict__ part, int64_t M,
+                                                             int64_t rows_per_block) {
+  __shared__ float red[4][NA][256];
+  const int t = threadIdx.x, rg = t >> 6, c4 = t & 63;
+  const int64_t mb = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t me = min(M, mb + rows_per_block);
+  float acc[NA][4] = {};
+  for (int64_t m = mb + rg; m < me; m += 4) {
+    const float4 x = reinterpret_cast<const float4*>(B + m * 256)[c4];
+#pragma unroll
+    for (int n = 0; n < NA; ++n) {
+      const float av = A[m * lda + n];
+      acc[n][0] = fmaf(av, x.x, acc[n][0]);
+      acc[n][1] = fmaf(av, x.y, acc[n][1]);
+      acc[n][2] = fmaf(av, x.z, acc[n][2]);
+      acc[n][3] = fmaf(av, x.w, acc[n][3]);
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < NA; ++n)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[rg][n][4 * c4 + j] = acc[n][j];
+  __syncthreads();
+#pragma unroll
+  for (int n = 0; n < NA; ++n) {
+    const float v = (red[0][n][t] + red[1][n][t]) + (red[2][n][t] + red[3][n][t]);
+    if (part) part[((int64_t)blockIdx.x * NA + n) * 256 + t] = v;
+    else atomicAdd(&C[n * ldc + t], v);
+  }
+}
+
+// ---------------------------------------------------------------- 3xbf16 GEMMs
+// The same two products on v_mfma_f32_32x32x16_bf16 with each fp32 operand split
+// x = hi + lo (hi = bf16(x), lo = bf16(x - hi)) and Ah.Bh + Ah.Bl + Al.Bh accumulated in
+// fp32 (the dropped Al.Bl and the lo rounding leave ~2^-17 relative error per product,
+// the field kernel's scheme).  On 32x32x16 lane l = 32h + i holds A[row i][k = 8h + j]
+// and B[k = 8h + j][col i], j = 0..7: exactly the 8 consecutive k values the fp32
+// kernels' lanes already load, so one bf16 MFMA triple replaces 8 fp32 MFMAs.
 
 // XCD-aware block order: workgroups are dispatched to the 8 XCDs round-robin, so
 // block b runs on XCD b % 8.  Renumber so each XCD takes a contiguous range of the
@@ -504,8 +571,9 @@ constexpr int kTnRowsX3 = 16, kTnGroupsX3 = 2;
 
 __global__ __launch_bounds__(256) void gemm_tn_x3_kernel(const float* __restrict__ A, int64_t lda,
                                                          const float* __restrict__ B, int64_t ldb,
-                                                         float* __restrict__ C, int64_t ldc, int64_t M, int N,
-                                                         int K, int64_t rows_per_block, int tiles_n, int tiles) {
+                                                         float* __restrict__ C, int64_t ldc, float* __restrict__ part,
+                                                         int64_t M, int N, int K, int64_t rows_per_block, int tiles_n,
+                                                         int tiles) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int i = lane & 31, h = lane >> 5;
   const unsigned v = xcd_order(blockIdx.x, gridDim.x);
@@ -548,19 +616,11 @@ __global__ __launch_bounds__(256) void gemm_tn_x3_kernel(const float* __restrict
       acc11 = mfma3(acc11, a1h, a1l, b1h, b1l);
     }
   }
-  const floatx16* accs[4] = {&acc00, &acc01, &acc10, &acc11};
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const floatx16& acc = *accs[2 * t + u];
-      const int col = k0 + 32 * u + i;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = n0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (row < N && col < K) atomicAdd(&C[(int64_t)row * ldc + col], acc[r]);
-      }
-    }
+  float* pt = part ? part + split * N * K : nullptr;
+  flush_block(acc00, C, ldc, pt, N, K, n0, k0, i, h);
+  flush_block(acc01, C, ldc, pt, N, K, n0, k0 + 32, i, h);
+  flush_block(acc10, C, ldc, pt, N, K, n0 + 32, k0, i, h);
+  flush_block(acc11, C, ldc, pt, N, K, n0 + 32, k0 + 32, i, h);
 }
 
 // out[code(m)][j] += A[m][j] for j < N; code(m) = code_index ? code_index[m / S]
@@ -885,47 +945,92 @@ int gemm_nn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, 
   return launch_status();
 }
 
-int gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M, int N, int K,
-            hipStream_t st, bool x3 = false) {
+// Launch plan of one dW GEMM C += A^T B: the kernel, its rows per workgroup / split and the
+// number of partial N x K tiles it writes on the deterministic path.
+enum TnKind { kTnGeneric, kTnGenericX3, kTnSkinny, kTn256, kTn256X3 };
+struct TnPlan {
+  TnKind kind;
+  int64_t rows, parts;
+};
+
+TnPlan tn_plan(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int N, int K, bool x3) {
+  const bool b16 = (reinterpret_cast<uintptr_t>(B) & 15) == 0;
+  (void)A;
+  if (N <= 4 && K == 256 && ldb == 256 && b16 && M >= 64 * 1024) {
+    // fp32 FMAs in both precisions (bandwidth-bound either way); ~1024 workgroups
+    const int64_t rows = ceil_div(ceil_div(M, 1024), 4) * 4;
+    return {kTnSkinny, rows, ceil_div(M, rows)};
+  }
+  if (N == 256 && K == 256 && lda == 256 && ldb == 256 && M >= 64 * 1024) {
+    // whole-tile kernels: one workgroup per CU over M / 256 rows each (a multiple of the stage)
+    const int64_t rows = ceil_div(ceil_div(M, 256), grad::kTwRows) * grad::kTwRows;
+    return {x3 ? kTn256X3 : kTn256, rows, ceil_div(M, rows)};
+  }
   // about 1024 blocks (4 per CU) over the M split, at least 256 rows each, a multiple of the
   // row group so only the last block has a ragged tail
   const int64_t tiles = ceil_div(N, grad::kTnTile) * ceil_div(K, grad::kTnTile);
-  if (x3) {
-    constexpr int64_t grp = grad::kTnRowsX3 * grad::kTnGroupsX3;
-    const int64_t splits = std::max<int64_t>(1, 1024 / tiles);
-    int64_t rows = std::max<int64_t>(256, ceil_div(M, splits));
-    rows = ceil_div(rows, grp) * grp;
-    const int64_t nb = ceil_div(M, rows) * tiles;
-    hipLaunchKernelGGL(grad::gemm_tn_x3_kernel, dim3(static_cast<unsigned>(nb)), dim3(256), 0, st, A, lda, B, ldb, C,
-                       ldc, M, N, K, rows, static_cast<int>(ceil_div(N, grad::kTnTile)), static_cast<int>(tiles));
-    return launch_status();
-  }
-  if (N <= 4 && K == 256 && ldb == 256 && (reinterpret_cast<uintptr_t>(B) & 15) == 0 && M >= 64 * 1024) {
-    const int64_t rows = ceil_div(ceil_div(M, 1024), 4) * 4;  // ~1024 workgroups
-    const unsigned grid = static_cast<unsigned>(ceil_div(M, rows));
-    switch (N) {
-      case 1: hipLaunchKernelGGL(grad::gemm_tn_skinny_kernel<1>, dim3(grid), dim3(256), 0, st, A, lda, B, C, ldc, M, rows); break;
-      case 2: hipLaunchKernelGGL(grad::gemm_tn_skinny_kernel<2>, dim3(grid), dim3(256), 0, st, A, lda, B, C, ldc, M, rows); break;
-      case 3: hipLaunchKernelGGL(grad::gemm_tn_skinny_kernel<3>, dim3(grid), dim3(256), 0, st, A, lda, B, C, ldc, M, rows); break;
-      default: hipLaunchKernelGGL(grad::gemm_tn_skinny_kernel<4>, dim3(grid), dim3(256), 0, st, A, lda, B, C, ldc, M, rows); break;
-    }
-    return launch_status();
-  }
-  if (N == 256 && K == 256 && lda == 256 && ldb == 256 && M >= 64 * 1024) {
-    // whole-tile kernel: one workgroup per CU over M / 256 rows each (a multiple of the stage)
-    int64_t rows = ceil_div(M, 256);
-    rows = ceil_div(rows, grad::kTwRows) * grad::kTwRows;
-    hipLaunchKernelGGL(grad::gemm_tn256_kernel, dim3(static_cast<unsigned>(ceil_div(M, rows))), dim3(512), 0, st, A,
-                       B, C, ldc, M, rows);
-    return launch_status();
-  }
+  const int64_t grp = x3 ? grad::kTnRowsX3 * grad::kTnGroupsX3 : 2 * grad::kTnPairs;
   const int64_t splits = std::max<int64_t>(1, 1024 / tiles);
   int64_t rows = std::max<int64_t>(256, ceil_div(M, splits));
-  rows = ceil_div(rows, 2 * grad::kTnPairs) * 2 * grad::kTnPairs;
-  dim3 grid(static_cast<unsigned>(ceil_div(N, grad::kTnTile)), static_cast<unsigned>(ceil_div(K, grad::kTnTile)),
-            static_cast<unsigned>(ceil_div(M, rows)));
-  hipLaunchKernelGGL(grad::gemm_tn_kernel, grid, dim3(256), 0, st, A, lda, B, ldb, C, ldc, M, N, K, rows);
+  rows = ceil_div(rows, grp) * grp;
+  return {x3 ? kTnGenericX3 : kTnGeneric, rows, ceil_div(M, rows)};
+}
+
+// ws (optional, tn_plan(..).parts * N * K floats): the deterministic two-pass reduction instead
+// of float atomics.
+int gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M, int N, int K,
+            hipStream_t st, bool x3 = false, float* ws = nullptr) {
+  const TnPlan pl = tn_plan(A, lda, B, ldb, M, N, K, x3);
+  const unsigned nb = static_cast<unsigned>(ceil_div(M, pl.rows));
+  switch (pl.kind) {
+    case kTnSkinny:
+      switch (N) {
+        case 1: hipLaunchKernelGGL(grad::gemm_tn_skinny_kernel<1>, dim3(nb), dim3(256), 0, st, A, lda, B, C, ldc, ws, M, pl.rows); break;
+        case 2: hipLaunchKernelGGL(grad::gemm_tn_skinny_kernel<2>, dim3(nb), dim3(256), 0, st, A, lda, B, C, ldc, ws, M, pl.rows); break;
+        case 3: hipLaunchKernelGGL(grad::gemm_tn_skinny_kernel<3>, dim3(nb), dim3(256), 0, st, A, lda, B, C, ldc, ws, M, pl.rows); break;
+        default: hipLaunchKernelGGL(grad::gemm_tn_skinny_kernel<4>, dim3(nb), dim3(256), 0, st, A, lda, B, C, ldc, ws, M, pl.rows); break;
+      }
+      break;
+    case kTn256:
+      hipLaunchKernelGGL(grad::gemm_tn256_kernel<false>, dim3(nb), dim3(512), 0, st, A, B, C, ldc, ws, M, pl.rows);
+      break;
+    case kTn256X3:
+      hipLaunchKernelGGL(grad::gemm_tn256_kernel<true>, dim3(nb), dim3(512), 0, st, A, B, C, ldc, ws, M, pl.rows);
+      break;
+    case kTnGenericX3: {
+      const int64_t tiles = ceil_div(N, grad::kTnTile) * ceil_div(K, grad::kTnTile);
+      hipLaunchKernelGGL(grad::gemm_tn_x3_kernel, dim3(static_cast<unsigned>(nb * tiles)), dim3(256), 0, st, A, lda, B,
+                         ldb, C, ldc, ws, M, N, K, pl.rows, static_cast<int>(ceil_div(N, grad::kTnTile)),
+                         static_cast<int>(tiles));
+      break;
+    }
+    default: {
+      dim3 grid(static_cast<unsigned>(ceil_div(N, grad::kTnTile)), static_cast<unsigned>(ceil_div(K, grad::kTnTile)), nb);
+      hipLaunchKernelGGL(grad::gemm_tn_kernel, grid, dim3(256), 0, st, A, lda, B, ldb, C, ldc, ws, M, N, K, pl.rows);
+      break;
+    }
+  }
+  if (ws) {
+    const int rc = launch_status();
+    if (rc != CN_OK) return rc;
+    hipLaunchKernelGGL(grad::reduce_partials_kernel, dim3(static_cast<unsigned>(ceil_div((int64_t)N * K, 64))), dim3(256),
+                       0, st, ws, pl.parts, N, K, C, ldc);
+  }
   return launch_status();
+}
+
+// Upper bound of the partial-tile workspace (floats) of gemm_tn(.., ws) for an M x N x K
+// product in either precision, whatever the operand strides / alignment.
+int64_t tn_ws_floats(int64_t M, int N, int K) {
+  static const float* const kAligned = reinterpret_cast<const float*>(256);
+  int64_t best = 0;
+  for (int x3 = 0; x3 < 2; ++x3) {
+    for (int contig = 0; contig < 2; ++contig) {
+      const int64_t lda = contig ? N : N + 1, ldb = contig ? K : K + 1;
+      best = std::max(best, tn_plan(kAligned, lda, kAligned, ldb, M, N, K, x3 != 0).parts * N * K);
+    }
+  }
+  return best;
 }
 
 int seg_sum(const float* A, int64_t lda, int64_t M, int N, int64_t S, const int64_t* code_index, int64_t n_codes,
@@ -956,6 +1061,19 @@ extern "C" int cn_gemm_tn(const float* A, int64_t lda, const float* B, int64_t l
   CN_CHECK_ARG(A && B && C && M > 0 && N > 0 && K > 0 && N <= 65536 && K <= 65536);
   CN_CHECK_ARG(lda >= N && ldb >= K && ldc >= K);
   return gemm_tn(A, lda, B, ldb, C, ldc, M, (int)N, (int)K, as_stream(stream));
+}
+
+extern "C" int64_t cn_gemm_tn_workspace_floats(int64_t M, int64_t N, int64_t K) {
+  if (M <= 0 || N <= 0 || K <= 0 || N > 65536 || K > 65536) return -1;
+  return tn_ws_floats(M, (int)N, (int)K);
+}
+
+extern "C" int cn_gemm_tn_ws(int fmt, const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
+                             int64_t M, int64_t N, int64_t K, float* workspace, cn_stream_t stream) {
+  CN_CHECK_ARG(fmt == CN_FMT_F32 || fmt == CN_FMT_BF16X3);
+  CN_CHECK_ARG(A && B && C && workspace && M > 0 && N > 0 && K > 0 && N <= 65536 && K <= 65536);
+  CN_CHECK_ARG(lda >= N && ldb >= K && ldc >= K);
+  return gemm_tn(A, lda, B, ldb, C, ldc, M, (int)N, (int)K, as_stream(stream), fmt == CN_FMT_BF16X3, workspace);
 }
 
 extern "C" int cn_gemm_nn_x3(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
@@ -1154,7 +1272,18 @@ extern "C" int cn_ray_points_backward(const float* g_pts, const float* z, int64_
 // which also writes each layer's masked input gradient dPre), then the weight and bias
 // gradients as split-M fp32 MFMA GEMMs dW = dPre^T X over those planes and the forward's saved
 // activations (cn_radiance_field_train_w16).
-extern "C" int64_t cn_field_backward_train_workspace_floats(int64_t m) { return m > 0 ? 5 * m * 256 : -1; }
+// dPre planes, then the dW GEMMs' partial tiles (deterministic reduction, reused by each GEMM in
+// stream order).
+static int64_t train_dw_ws_floats(int64_t m) {
+  static const int kShapes[5][2] = {{3, 256}, {256, 256}, {256, 27}, {1, 256}, {256, 63}};
+  int64_t best = 0;
+  for (const auto& sh : kShapes) best = std::max(best, tn_ws_floats(m, sh[0], sh[1]));
+  return best;
+}
+
+extern "C" int64_t cn_field_backward_train_workspace_floats(int64_t m) {
+  return m > 0 ? 5 * m * 256 + train_dw_ws_floats(m) : -1;
+}
 
 extern "C" int cn_field_backward_train(const float* packed_t, const float* const* params, const uint32_t* masks,
                                        const float* saved, const float* x_enc, const float* d_raw, const float* pts,
@@ -1212,24 +1341,25 @@ extern "C" int cn_field_backward_train(const float* packed_t, const float* const
   CN_TRY(launch_status());
   const float* P[5];
   for (int k = 0; k < 5; ++k) P[k] = workspace + k * M * 256;
+  float* ws = workspace + 5 * M * 256;
   const float* h1 = saved;
   const float* h2 = saved + M * 256;
   const float* feat = saved + 2 * M * 256;
   const float* v1 = saved + 3 * M * 256;
   const float* v2 = saved + 4 * M * 256;
   // fc_rgb (h half): dW += d rgb^T v2
-  CN_TRY(gemm_tn(d_raw, 4, v2, 256, G(kWRgb), 512, M, 3, 256, st));
+  CN_TRY(gemm_tn(d_raw, 4, v2, 256, G(kWRgb), 512, M, 3, 256, st, false, ws));
   // layer_dir2
-  CN_TRY(gemm_tn(P[0], 256, v1, 256, G(kWDir2), 256, M, 256, 256, st));
+  CN_TRY(gemm_tn(P[0], 256, v1, 256, G(kWDir2), 256, M, 256, 256, st, false, ws));
   // layer_dir1: [feat | dir enc]
-  CN_TRY(gemm_tn(P[1], 256, feat, 256, G(kWDir1), 283, M, 256, 256, st));
-  CN_TRY(gemm_tn(P[1], 256, x_enc + 63, 90, G(kWDir1) + 256, 283, M, 256, 27, st));
+  CN_TRY(gemm_tn(P[1], 256, feat, 256, G(kWDir1), 283, M, 256, 256, st, false, ws));
+  CN_TRY(gemm_tn(P[1], 256, x_enc + 63, 90, G(kWDir1) + 256, 283, M, 256, 27, st, false, ws));
   // fc_out (h half): row 0 from d sigma, rows 1.. from d feat
-  CN_TRY(gemm_tn(d_raw + 3, 4, h2, 256, G(kWOut), 512, M, 1, 256, st));
-  CN_TRY(gemm_tn(P[2], 256, h2, 256, G(kWOut) + 512, 512, M, 256, 256, st));
+  CN_TRY(gemm_tn(d_raw + 3, 4, h2, 256, G(kWOut), 512, M, 1, 256, st, false, ws));
+  CN_TRY(gemm_tn(P[2], 256, h2, 256, G(kWOut) + 512, 512, M, 256, 256, st, false, ws));
   // layer_xyz2 (h half)
-  CN_TRY(gemm_tn(P[3], 256, h1, 256, G(kWXyz2), 512, M, 256, 256, st));
+  CN_TRY(gemm_tn(P[3], 256, h1, 256, G(kWXyz2), 512, M, 256, 256, st, false, ws));
   // layer_xyz1
-  CN_TRY(gemm_tn(P[4], 256, x_enc, 90, G(kWXyz1), 63, M, 256, 63, st));
+  CN_TRY(gemm_tn(P[4], 256, x_enc, 90, G(kWXyz1), 63, M, 256, 63, st, false, ws));
   return CN_OK;
 }

@@ -321,7 +321,7 @@ int cn_field_backward_fused(int fmt_t, const float* packed_t, const uint32_t* ma
  * d_pts / d_ro / d_rd as there; g_code required) that also writes every layer's masked input
  * gradient into workspace (cn_field_backward_train_workspace_floats(M) floats), then the weight
  * and bias gradients dW = dPre^T X as split-M fp32 MFMA GEMMs over those planes, saved and x_enc
- * (cn_encode_inputs): grads (18 pointers, or NULL for none) ACCUMULATED as in
+ * (cn_encode_inputs), reduced deterministically (cn_gemm_tn_ws) through the rest of workspace: grads (18 pointers, or NULL for none) ACCUMULATED as in
  * cn_field_backward (the code-layer parameters and code halves come from cn_code_bias_backward).
  * One code row per 16-sample wave: n_codes == 1 or n_samples % 16 == 0, else CN_EUNSUPPORTED. */
 int cn_radiance_field_train_w16(const float* packed, const float* code_bias, const int64_t* code_index,
@@ -424,6 +424,13 @@ int cn_gemm_nn_x3(const float* A, int64_t lda, const float* B, int64_t ldb, floa
                   const float* mask, int64_t ldm, int64_t M, int64_t N, int64_t K, cn_stream_t stream);
 int cn_gemm_tn_x3(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M,
                   int64_t N, int64_t K, cn_stream_t stream);
+/* cn_gemm_tn (fmt CN_FMT_F32) or cn_gemm_tn_x3 (CN_FMT_BF16X3), deterministic: each workgroup
+ * stores its partial N x K tile into workspace (cn_gemm_tn_workspace_floats(M, N, K) floats) and
+ * a second pass adds the partials to C in a fixed order, so the result is bitwise reproducible
+ * (the float-atomic flush of cn_gemm_tn is not). */
+int64_t cn_gemm_tn_workspace_floats(int64_t M, int64_t N, int64_t K);
+int cn_gemm_tn_ws(int fmt, const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
+                  int64_t M, int64_t N, int64_t K, float* workspace, cn_stream_t stream);
 
 #ifdef __cplusplus
 }

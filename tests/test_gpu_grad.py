@@ -103,13 +103,19 @@ def test_gemm_nn_strided_a(dev, m, k, lda, precision):
 @pytest.mark.parametrize("precision", ["f32", "bf16x3"])
 @pytest.mark.parametrize("m,n,k", [(5000, 257, 256), (33, 3, 256), (4096, 256, 63), (65536, 256, 256), (70001, 3, 283),
                                    (70001, 3, 256), (65537, 1, 256), (131075, 256, 256)])
-def test_gemm_tn_accumulates(dev, m, n, k, precision):
+@pytest.mark.parametrize("det", [False, True])
+def test_gemm_tn_accumulates(dev, m, n, k, precision, det):
     from codenerf import ops
     g = torch.Generator().manual_seed(m * 3 + n + k)
     a, b = torch.randn(m, n, generator=g), torch.randn(m, k, generator=g)
     c0 = torch.randn(n, k, generator=g)
-    c = ops.gemm_tn(a.to(dev), b.to(dev), c0.to(dev).clone(), precision=precision)
+    ad, bd = a.to(dev), b.to(dev)
+    c = ops.gemm_tn(ad, bd, c0.to(dev).clone(), precision=precision, deterministic=det)
     close(c, c0.double() + a.double().t() @ b.double(), GEMM_TOL[precision], "gemm_tn " + precision)
+    if det:
+        # the partial-tile path is bitwise reproducible
+        c2 = ops.gemm_tn(ad, bd, c0.to(dev).clone(), precision=precision, deterministic=True)
+        assert torch.equal(c, c2), "deterministic gemm_tn differs between two runs"
 
 
 # ---------------------------------------------------------------- element-wise stages

@@ -30,16 +30,21 @@ def main():
             a = torch.randn(M, n, device=dev)
             b = torch.randn(M, k, device=dev)
             fl = 2.0 * M * n * k
-            c = torch.zeros(n, k, device=dev)
-            t_cn = bench(lambda: ops.gemm_tn(a, b, c))
-            t_mm = bench(lambda: torch.mm(a.t(), b))
             ref = torch.mm(a.double().t(), b.double()).float()
-            c.zero_()
-            ops.gemm_tn(a, b, c)
-            err = ((c - ref).abs().max() / ref.abs().max()).item()
-            err_mm = ((torch.mm(a.t(), b) - ref).abs().max() / ref.abs().max()).item()
-            print(f"M={M} N={n} K={k}: cn_gemm_tn {t_cn * 1e3:8.1f} us {fl / t_cn / 1e9:6.1f} TF (rel err {err:.1e}) | "
-                  f"torch.mm {t_mm * 1e3:8.1f} us {fl / t_mm / 1e9:6.1f} TF (rel err {err_mm:.1e})", flush=True)
+            line = [f"M={M} N={n} K={k}:"]
+            for prec in ("f32", "bf16x3"):
+                for det in (False, True):
+                    c = torch.zeros(n, k, device=dev)
+                    t = bench(lambda: ops.gemm_tn(a, b, c, precision=prec, deterministic=det))
+                    c.zero_()
+                    ops.gemm_tn(a, b, c, precision=prec, deterministic=det)
+                    err = ((c - ref).abs().max() / ref.abs().max()).item()
+                    gbs = 4.0 * M * (n + k) / t / 1e6
+                    line.append(f"{prec}{'/det' if det else ''} {t * 1e3:7.1f} us {fl / t / 1e9:6.1f} TF {gbs:6.0f} GB/s "
+                                f"(err {err:.1e})")
+            t_mm = bench(lambda: torch.mm(a.t(), b))
+            line.append(f"torch.mm {t_mm * 1e3:7.1f} us")
+            print(" | ".join(line), flush=True)
 
 
 if __name__ == "__main__":
