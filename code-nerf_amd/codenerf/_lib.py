@@ -79,8 +79,12 @@ SIGNATURES = {
                                      _p, _p, _p]),
     "cn_radiance_field_train_w16": (_i, [_p, _p, _p, _i64, _p, _p, _p, _p, _i64, _i64, _i64, _fp, _fp, _p, _p, _p,
                                          _p]),
+    "cn_radiance_field_train_fmt": (_i, [_i, _p, _p, _p, _i64, _p, _p, _p, _p, _i64, _i64, _i64, _fp, _fp, _p, _p, _p,
+                                         _p]),
     "cn_field_backward_train_workspace_floats": (_i64, [_i64]),
     "cn_field_backward_train": (_i, [_p, ctypes.POINTER(_p), _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p,
+                                     _i64, _fp, _fp, _p, ctypes.POINTER(_p), _p, _p, _p, _p, _p]),
+    "cn_field_backward_train_fmt": (_i, [_i, _p, ctypes.POINTER(_p), _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p,
                                      _i64, _fp, _fp, _p, ctypes.POINTER(_p), _p, _p, _p, _p, _p]),
     "cn_field_backward_x3": (_i, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p, _i64, _fp, _fp, _p, _p, _p, _p,
                                   _p]),

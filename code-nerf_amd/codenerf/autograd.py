@@ -191,8 +191,9 @@ class RadianceField(torch.autograd.Function):
 
     With frozen weights (the eval step) the forward is the field kernel of the model's
     precision writing ReLU masks and the backward ONE fused kernel (cn_field_backward_fused:
-    fp32 16x16x4 for "f32", 3xbf16 for "bf16x3"); with weight gradients the fp32
-    training kernel keeps the activations for the layer-wise backward.
+    fp32 16x16x4 for "f32", 3xbf16 for "bf16x3"); with weight gradients the same kernel pair
+    also keeps the activations and the layer-input gradients for the dW GEMMs
+    (cn_field_backward_train_fmt) when precision == train_precision.
     """
 
     @staticmethod
@@ -212,16 +213,19 @@ class RadianceField(torch.autograd.Function):
             ctx.meta = meta
             ctx.save_for_backward(rd, pts, ro, z, z_s, z_t, *params)
             return raw
-        # weights trained: the fp32 training forward keeps the activations.  "f32" with fp32 GEMMs
-        # and one code row per 16-sample wave: the 16x16x4 kernel + the fused training backward;
-        # otherwise the 32x32x2 kernel + the layer-wise backward
-        ctx.train_fused = (meta.precision == "f32" and meta.train_precision == "f32"
-                           and ops.fused_backward_supported(z_s.shape[0], meta.n_samples, meta.code_index, "f32"))
+        # weights trained: the training forward keeps the activations.  precision == train_precision
+        # ("f32": the 16x16x4 kernel, "bf16x3": the 3xbf16 kernel) with one code row per wave: that
+        # kernel + the fused training backward; otherwise the fp32 32x32x2 kernel + the layer-wise
+        # backward
+        ctx.train_fused = (meta.precision == meta.train_precision and meta.precision in ("f32", "bf16x3")
+                           and ops.fused_backward_supported(z_s.shape[0], meta.n_samples, meta.code_index,
+                                                            meta.precision))
         ctx.masks = None
         if ctx.train_fused:
+            x3 = meta.precision == "bf16x3"
             raw, saved, ctx.masks = ops.radiance_field_train_w16(
-                ops.mlp_pack(params, "f32_w16"), cb, rd, meta.n_samples, meta.chunk_rows, meta.fx, meta.fd, pts=pts,
-                ro=ro, z=z, code_index=meta.code_index)
+                ops.mlp_pack(params, "bf16x3" if x3 else "f32_w16"), cb, rd, meta.n_samples, meta.chunk_rows,
+                meta.fx, meta.fd, pts=pts, ro=ro, z=z, code_index=meta.code_index, precision=meta.precision)
         else:
             raw, saved = ops.radiance_field_train(ops.mlp_pack(params, "f32"), cb, rd, meta.n_samples,
                                                   meta.chunk_rows, meta.fx, meta.fd, pts=pts, ro=ro, z=z,
@@ -251,11 +255,12 @@ class RadianceField(torch.autograd.Function):
         pg = _param_grad_buffers(params, needs[7:])
         want_z = needs[5] or needs[6]
         if ctx.train_fused:
-            r = ops.field_backward_train(ops.mlp_pack(params, "f32_w16_t"), params, ctx.masks, ctx.acts, ctx.x_enc,
-                                         g_raw.contiguous(), rd.shape[0], meta.n_samples, meta.chunk_rows,
-                                         z_s.shape[0], meta.fx, meta.fd, rd=rd, pts=pts, ro=ro, z=z,
+            x3 = meta.precision == "bf16x3"
+            r = ops.field_backward_train(ops.mlp_pack(params, "bf16x3_t" if x3 else "f32_w16_t"), params, ctx.masks,
+                                         ctx.acts, ctx.x_enc, g_raw.contiguous(), rd.shape[0], meta.n_samples,
+                                         meta.chunk_rows, z_s.shape[0], meta.fx, meta.fd, rd=rd, pts=pts, ro=ro, z=z,
                                          code_index=meta.code_index, param_grads=pg, want_pts=needs[2],
-                                         want_ro=needs[3], want_rd=needs[1])
+                                         want_ro=needs[3], want_rd=needs[1], precision=meta.precision)
             ctx.acts = ctx.x_enc = ctx.masks = None
             dz_s, dz_t = ops.code_bias_backward(params, z_s, z_t, r["g_code"], pg, want_z=want_z)
             grads = pg if pg is not None else [None] * len(params)

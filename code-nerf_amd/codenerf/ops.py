@@ -420,9 +420,11 @@ def radiance_field_train(packed: Tensor, cb: Tensor, rd: Tensor, n_samples: int,
 def radiance_field_train_w16(packed: Tensor, cb: Tensor, rd: Tensor, n_samples: int, chunk_rows: int,
                              freqs_xyz: Sequence[float], freqs_dir: Sequence[float], pts: Optional[Tensor] = None,
                              ro: Optional[Tensor] = None, z: Optional[Tensor] = None,
-                             code_index: Optional[Tensor] = None):
-    """Training forward on the fp32 16x16x4 kernel (packed "f32_w16") -> raw (R,S,4), saved (5, R*S, 256),
-    ReLU masks (the fused training backward's inputs)."""
+                             code_index: Optional[Tensor] = None, precision: str = "f32"):
+    """Training forward -> raw (R,S,4), saved (5, R*S, 256), ReLU masks (the fused training backward's
+    inputs): precision "f32" on the fp32 16x16x4 kernel (packed "f32_w16"), "bf16x3" on the 3xbf16
+    kernel (packed "bf16x3")."""
+    fmt = _lib.CN_FMT_BF16X3 if precision == "bf16x3" else _lib.CN_FMT_F32_W16
     lib = _lib_ready()
     rd = _cuda(rd, "rd")
     n = rd.shape[0]
@@ -437,11 +439,11 @@ def radiance_field_train_w16(packed: Tensor, cb: Tensor, rd: Tensor, n_samples: 
     m = n * n_samples
     raw = torch.empty(n, n_samples, 4, device=rd.device, dtype=torch.float32)
     saved = torch.empty(5, m, 256, device=rd.device, dtype=torch.float32)
-    masks = torch.empty(int(lib.cn_field_mask_words_fmt(_lib.CN_FMT_F32_W16, m)), device=rd.device, dtype=torch.int32)
-    check(lib.cn_radiance_field_train_w16(ptr(packed), ptr(cb), ptr(code_index), cb.shape[0], ptr(pts), ptr(ro),
+    masks = torch.empty(int(lib.cn_field_mask_words_fmt(fmt, m)), device=rd.device, dtype=torch.int32)
+    check(lib.cn_radiance_field_train_fmt(fmt, ptr(packed), ptr(cb), ptr(code_index), cb.shape[0], ptr(pts), ptr(ro),
                                           ptr(rd), ptr(z), n, n_samples, chunk_rows, _lib.host_floats(freqs_xyz),
                                           _lib.host_floats(freqs_dir), ptr(raw), ptr(saved), ptr(masks),
-                                          stream_of(rd)), "cn_radiance_field_train_w16")
+                                          stream_of(rd)), "cn_radiance_field_train_fmt")
     return raw, saved, masks
 
 
@@ -450,8 +452,11 @@ def field_backward_train(packed_t: Tensor, params: Sequence[Tensor], masks: Tens
                          freqs_xyz: Sequence[float], freqs_dir: Sequence[float], rd: Tensor,
                          pts: Optional[Tensor] = None, ro: Optional[Tensor] = None, z: Optional[Tensor] = None,
                          code_index: Optional[Tensor] = None, param_grads: Optional[Sequence[Tensor]] = None,
-                         want_pts: bool = False, want_ro: bool = False, want_rd: bool = False):
-    """Fused fp32 training backward (one dX launch + dW GEMMs) -> dict g_code / d_pts / d_ro / d_rd."""
+                         want_pts: bool = False, want_ro: bool = False, want_rd: bool = False,
+                         precision: str = "f32"):
+    """Fused training backward (one dX launch + deterministic dW GEMMs) -> dict g_code / d_pts / d_ro / d_rd.
+    precision "f32" (packed_t "f32_w16_t") or "bf16x3" (packed_t "bf16x3_t", 3xbf16 dW GEMMs)."""
+    fmt_t = _lib.CN_FMT_BF16X3_T if precision == "bf16x3" else _lib.CN_FMT_F32_W16_T
     lib = _lib_ready()
     m = n_rays * n_samples
     params = [_cuda(p.detach(), f"param{i}") for i, p in enumerate(params)]
@@ -471,11 +476,11 @@ def field_backward_train(packed_t: Tensor, params: Sequence[Tensor], masks: Tens
     if param_grads is not None:
         assert len(param_grads) == _lib.CN_NUM_PARAMS and all(g.is_contiguous() for g in param_grads)
         garr, gkeep = _lib.pointer_array(list(param_grads))
-    check(lib.cn_field_backward_train(ptr(packed_t), arr, ptr(masks), ptr(saved), ptr(x_enc), ptr(d_raw), ptr(pts),
-                                      ptr(ro), ptr(rd), ptr(z), n_rays, n_samples, chunk_rows, ptr(code_index),
-                                      n_codes, _lib.host_floats(freqs_xyz), _lib.host_floats(freqs_dir), ptr(ws),
-                                      garr, ptr(g_code), ptr(d_pts), ptr(d_ro), ptr(d_rd), stream_of(d_raw)),
-          "cn_field_backward_train")
+    check(lib.cn_field_backward_train_fmt(fmt_t, ptr(packed_t), arr, ptr(masks), ptr(saved), ptr(x_enc), ptr(d_raw),
+                                          ptr(pts), ptr(ro), ptr(rd), ptr(z), n_rays, n_samples, chunk_rows,
+                                          ptr(code_index), n_codes, _lib.host_floats(freqs_xyz),
+                                          _lib.host_floats(freqs_dir), ptr(ws), garr, ptr(g_code), ptr(d_pts),
+                                          ptr(d_ro), ptr(d_rd), stream_of(d_raw)), "cn_field_backward_train_fmt")
     del keep, gkeep
     return {"g_code": g_code, "d_pts": d_pts, "d_ro": d_ro, "d_rd": d_rd}
 

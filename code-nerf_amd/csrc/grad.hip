@@ -1292,7 +1292,22 @@ extern "C" int cn_field_backward_train(const float* packed_t, const float* const
                                        int64_t n_codes, const float* freqs_xyz, const float* freqs_dir,
                                        float* workspace, float* const* grads, float* g_code, float* d_pts,
                                        float* d_ro, float* d_rd, cn_stream_t stream) {
+  return cn_field_backward_train_fmt(CN_FMT_F32_W16_T, packed_t, params, masks, saved, x_enc, d_raw, pts, ro, rd, z,
+                                     n_rays, n_samples, chunk_rows, code_index, n_codes, freqs_xyz, freqs_dir,
+                                     workspace, grads, g_code, d_pts, d_ro, d_rd, stream);
+}
+
+extern "C" int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, const float* const* params,
+                                           const uint32_t* masks, const float* saved, const float* x_enc,
+                                           const float* d_raw, const float* pts, const float* ro, const float* rd,
+                                           const float* z, int64_t n_rays, int64_t n_samples, int64_t chunk_rows,
+                                           const int64_t* code_index, int64_t n_codes, const float* freqs_xyz,
+                                           const float* freqs_dir, float* workspace, float* const* grads,
+                                           float* g_code, float* d_pts, float* d_ro, float* d_rd,
+                                           cn_stream_t stream) {
   using namespace mlp;
+  CN_CHECK_ARG(fmt_t == CN_FMT_F32_W16_T || fmt_t == CN_FMT_BF16X3_T);
+  const bool x3 = fmt_t == CN_FMT_BF16X3_T;
   CN_CHECK_ARG(packed_t && params && masks && saved && x_enc && d_raw && rd && g_code && workspace);
   CN_CHECK_ARG(freqs_xyz && freqs_dir && n_rays > 0 && n_samples > 0 && chunk_rows > 0 && n_codes > 0);
   CN_CHECK_ARG(pts || (ro && z));
@@ -1300,7 +1315,8 @@ extern "C" int cn_field_backward_train(const float* packed_t, const float* const
   CN_CHECK_ARG(!d_ro || (ro && z && !pts));
   CN_CHECK_ARG(code_index || n_codes == 1 || n_codes == n_rays);
   for (int i = 0; i < CN_NUM_PARAMS; ++i) CN_CHECK_ARG(params[i]);
-  if (!(n_codes == 1 || n_samples % 16 == 0)) return CN_EUNSUPPORTED;  // one code row per 16-sample wave
+  // one code row per wave (32 samples x3, 16 samples w16)
+  if (!(n_codes == 1 || n_samples % (x3 ? 32 : 16) == 0)) return CN_EUNSUPPORTED;
   hipStream_t st = as_stream(stream);
   const int64_t M = n_rays * n_samples;
   CN_CHECK_ARG(ceil_div(M, 128) <= 0x7fffffff);
@@ -1331,7 +1347,8 @@ extern "C" int cn_field_backward_train(const float* packed_t, const float* const
     a.gbias[1] = grads[kBDir1];
     a.gbias[2] = grads[kBXyz1];
   }
-  CN_TRY(launch_field_w16_bwd(pts ? kFromPts : kFromRayZ, a, st));
+  CN_TRY(x3 ? launch_field_x3_bwd(pts ? kFromPts : kFromRayZ, a, st)
+            : launch_field_w16_bwd(pts ? kFromPts : kFromRayZ, a, st));
   if (!wg) return CN_OK;
   auto G = [&](int i) { return grads[i]; };
   // biases: layer_dir2 / layer_dir1 / layer_xyz1 summed in the kernel; the others are g_code's
@@ -1348,18 +1365,18 @@ extern "C" int cn_field_backward_train(const float* packed_t, const float* const
   const float* v1 = saved + 3 * M * 256;
   const float* v2 = saved + 4 * M * 256;
   // fc_rgb (h half): dW += d rgb^T v2
-  CN_TRY(gemm_tn(d_raw, 4, v2, 256, G(kWRgb), 512, M, 3, 256, st, false, ws));
+  CN_TRY(gemm_tn(d_raw, 4, v2, 256, G(kWRgb), 512, M, 3, 256, st, x3, ws));
   // layer_dir2
-  CN_TRY(gemm_tn(P[0], 256, v1, 256, G(kWDir2), 256, M, 256, 256, st, false, ws));
+  CN_TRY(gemm_tn(P[0], 256, v1, 256, G(kWDir2), 256, M, 256, 256, st, x3, ws));
   // layer_dir1: [feat | dir enc]
-  CN_TRY(gemm_tn(P[1], 256, feat, 256, G(kWDir1), 283, M, 256, 256, st, false, ws));
-  CN_TRY(gemm_tn(P[1], 256, x_enc + 63, 90, G(kWDir1) + 256, 283, M, 256, 27, st, false, ws));
+  CN_TRY(gemm_tn(P[1], 256, feat, 256, G(kWDir1), 283, M, 256, 256, st, x3, ws));
+  CN_TRY(gemm_tn(P[1], 256, x_enc + 63, 90, G(kWDir1) + 256, 283, M, 256, 27, st, x3, ws));
   // fc_out (h half): row 0 from d sigma, rows 1.. from d feat
-  CN_TRY(gemm_tn(d_raw + 3, 4, h2, 256, G(kWOut), 512, M, 1, 256, st, false, ws));
-  CN_TRY(gemm_tn(P[2], 256, h2, 256, G(kWOut) + 512, 512, M, 256, 256, st, false, ws));
+  CN_TRY(gemm_tn(d_raw + 3, 4, h2, 256, G(kWOut), 512, M, 1, 256, st, x3, ws));
+  CN_TRY(gemm_tn(P[2], 256, h2, 256, G(kWOut) + 512, 512, M, 256, 256, st, x3, ws));
   // layer_xyz2 (h half)
-  CN_TRY(gemm_tn(P[3], 256, h1, 256, G(kWXyz2), 512, M, 256, 256, st, false, ws));
+  CN_TRY(gemm_tn(P[3], 256, h1, 256, G(kWXyz2), 512, M, 256, 256, st, x3, ws));
   // layer_xyz1
-  CN_TRY(gemm_tn(P[4], 256, x_enc, 90, G(kWXyz1), 63, M, 256, 63, st, false, ws));
+  CN_TRY(gemm_tn(P[4], 256, x_enc, 90, G(kWXyz1), 63, M, 256, 63, st, x3, ws));
   return CN_OK;
 }

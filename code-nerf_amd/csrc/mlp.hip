@@ -616,6 +616,17 @@ extern "C" int cn_radiance_field_train_w16(const float* packed, const float* cod
                                            const float* z, int64_t n_rays, int64_t n_samples, int64_t chunk_rows,
                                            const float* freqs_xyz, const float* freqs_dir, float* raw, float* save,
                                            uint32_t* masks, cn_stream_t stream) {
+  return cn_radiance_field_train_fmt(CN_FMT_F32_W16, packed, code_bias, code_index, n_codes, pts, ro, rd, z, n_rays,
+                                     n_samples, chunk_rows, freqs_xyz, freqs_dir, raw, save, masks, stream);
+}
+
+extern "C" int cn_radiance_field_train_fmt(int fmt, const float* packed, const float* code_bias,
+                                           const int64_t* code_index, int64_t n_codes, const float* pts,
+                                           const float* ro, const float* rd, const float* z, int64_t n_rays,
+                                           int64_t n_samples, int64_t chunk_rows, const float* freqs_xyz,
+                                           const float* freqs_dir, float* raw, float* save, uint32_t* masks,
+                                           cn_stream_t stream) {
+  CN_CHECK_ARG(fmt == CN_FMT_F32_W16 || fmt == CN_FMT_BF16X3);
   CN_CHECK_ARG(packed && code_bias && rd && raw && save && masks && freqs_xyz && freqs_dir);
   CN_CHECK_ARG(n_rays > 0 && n_samples > 0 && chunk_rows > 0 && n_codes > 0);
   CN_CHECK_ARG(pts || (ro && z));
@@ -639,7 +650,8 @@ extern "C" int cn_radiance_field_train_w16(const float* packed, const float* cod
   a.raw = raw;
   a.save = save;
   a.masks = masks;
-  return launch_field_w16(pts ? kFromPts : kFromRayZ, a, cn::as_stream(stream));
+  return fmt == CN_FMT_BF16X3 ? launch_field_x3(pts ? kFromPts : kFromRayZ, a, cn::as_stream(stream))
+                              : launch_field_w16(pts ? kFromPts : kFromRayZ, a, cn::as_stream(stream));
 }
 
 extern "C" int cn_field_backward_x3(const float* packed_t, const uint32_t* masks, const float* d_raw,

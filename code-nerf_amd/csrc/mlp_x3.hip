@@ -165,6 +165,8 @@ struct State {
   unsigned mw[4];         // training forward: ReLU mask words being built for the current layer
   __amdgpu_buffer_rsrc_t wsrc;  // the packed stream as a buffer resource
   unsigned voff;          // this lane's byte offset inside a 1 KiB-per-wave piece row
+  float* sv;              // training: this lane's row of the plane being written (+4h), or null
+  float pend[2];          // training backward: the even piece's values, stored with the odd one
 };
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -232,6 +234,28 @@ __device__ __forceinline__ void conv_all(const float* raw, float* out, float lo,
 template <int J>
 __device__ __forceinline__ void put_mask(unsigned* mw, unsigned mb) {
   mw[J >> 1] |= mb << (16 * (J & 1));
+}
+
+// Training forward: post-activation values 4q..4q+3 of raw slot J (features 32J + 8q + 4h ..
+// + 3, one 16-B store into the plane row s.sv; lo = 0 for a ReLU, -inf for feat).
+template <int J, int Q>
+__device__ __forceinline__ void save_quad(const State& s, float lo) {
+  if (s.sv) {
+    float4 o;
+    o.x = vmax(s.sl[J][4 * Q], lo);
+    o.y = vmax(s.sl[J][4 * Q + 1], lo);
+    o.z = vmax(s.sl[J][4 * Q + 2], lo);
+    o.w = vmax(s.sl[J][4 * Q + 3], lo);
+    *reinterpret_cast<float4*>(s.sv + 32 * J + 8 * Q) = o;
+  }
+}
+
+template <int J>
+__device__ __forceinline__ void save_slot(const State& s, float lo) {
+  save_quad<J, 0>(s, lo);
+  save_quad<J, 1>(s, lo);
+  save_quad<J, 2>(s, lo);
+  save_quad<J, 3>(s, lo);
 }
 
 // One LDS-DMA piece: 1 KiB per wave (16 B per lane) of chunk `cn`, piece `i`
@@ -449,7 +473,7 @@ struct NoFill {
 
 // Convert slot J (raw block of the previous layer) into packed B operands, one
 // pair of values per group; sigma partial alongside.
-template <int J, bool MASKS = false>
+template <int J, bool MASKS = false, bool SAVE = false>
 struct ConvFill {
   State& s;
   float lo;
@@ -458,6 +482,7 @@ struct ConvFill {
   unsigned mb;
   template <int G>
   __device__ __forceinline__ void step() {
+    if constexpr (SAVE && (G & 1)) save_quad<J, G / 2>(s, lo);  // before G == 7 overwrites the slot
 #ifndef CN_ABLATE_NO_FILL
     // w (read asynchronously at the chunk start) is usable only after M_c, so the
     // sigma products of pieces 0-3 are taken in steps 4-7 from the raw values
@@ -559,11 +584,11 @@ __device__ __forceinline__ void run_chunk(State& s, const FieldArgs& a, float4* 
 
 // Chunk J of a 256-input layer: B from slot J, converting slot J+1 meanwhile
 // (the last chunk copies the accumulators out instead).
-template <int J, bool MASKS = false>
+template <int J, bool MASKS = false, bool SAVE = false>
 __device__ __forceinline__ void layer_chunk(State& s, const FieldArgs& a, float4* lds, int& c, const float* blds,
                                             float lo) {
   if constexpr (J < 7) {
-    ConvFill<J + 1, MASKS> f{s, lo, {}, {}, 0u};
+    ConvFill<J + 1, MASKS, SAVE> f{s, lo, {}, {}, 0u};
     lds_read16_async(blds + kSigmaOff + (s.h * 8 + J + 1) * 16, f.w);
     run_chunk<2>(s, a, lds, c, CN_SLOT_B(J), f);
   } else {
@@ -575,8 +600,9 @@ __device__ __forceinline__ void layer_chunk(State& s, const FieldArgs& a, float4
 }
 
 // Bias-initialise the accumulators of `layer` while converting slot 0.
-template <bool MASKS = false>
+template <bool MASKS = false, bool SAVE = false>
 __device__ __forceinline__ void begin_layer(State& s, const FieldArgs& a, const float* blds, int layer, float lo) {
+  if constexpr (SAVE) save_slot<0>(s, lo);
   float w[16];
   lds_read16(blds + kSigmaOff + (s.h * 8) * 16, w);
   float out[16];
@@ -618,7 +644,7 @@ __device__ __forceinline__ void store_masks(State& s, const FieldArgs& a, int64_
 
 // One 128-sample tile: inputs, encodings, the six layers (chunks 0..35 of the
 // stream, which also prefetch chunks 0..2 for the next tile), the raw store.
-template <int MODE, bool MASKS>
+template <int MODE, bool MASKS, bool SAVE>
 __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4* lds, float* blds, int64_t tile) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) s.mw[i] = 0u;
@@ -705,19 +731,21 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
     // activation of the layer that produced the slots: none after fc_out (feat)
     const float lo = layer == kDir1 ? -__builtin_inff() : 0.0f;
     s.sig = 0.0f;
-    begin_layer<MASKS>(s, a, blds, layer, lo);
+    // training: the slots converted in this pass (h1, h2, feat, v1) go to plane layer - kXyz2
+    if constexpr (SAVE) s.sv = valid ? a.save + ((int64_t)(layer - kXyz2) * a.m + row) * 256 + 4 * s.h : nullptr;
+    begin_layer<MASKS, SAVE>(s, a, blds, layer, lo);
     if (layer == kDir1) {
       NoFill nf;
       run_chunk<0>(s, a, lds, c, s.dh[0], s.dl[0], s.dh[1], s.dl[1], nf);
     }
-    layer_chunk<0, MASKS>(s, a, lds, c, blds, lo);
-    layer_chunk<1, MASKS>(s, a, lds, c, blds, lo);
-    layer_chunk<2, MASKS>(s, a, lds, c, blds, lo);
-    layer_chunk<3, MASKS>(s, a, lds, c, blds, lo);
-    layer_chunk<4, MASKS>(s, a, lds, c, blds, lo);
-    layer_chunk<5, MASKS>(s, a, lds, c, blds, lo);
-    layer_chunk<6, MASKS>(s, a, lds, c, blds, lo);
-    layer_chunk<7, MASKS>(s, a, lds, c, blds, lo);
+    layer_chunk<0, MASKS, SAVE>(s, a, lds, c, blds, lo);
+    layer_chunk<1, MASKS, SAVE>(s, a, lds, c, blds, lo);
+    layer_chunk<2, MASKS, SAVE>(s, a, lds, c, blds, lo);
+    layer_chunk<3, MASKS, SAVE>(s, a, lds, c, blds, lo);
+    layer_chunk<4, MASKS, SAVE>(s, a, lds, c, blds, lo);
+    layer_chunk<5, MASKS, SAVE>(s, a, lds, c, blds, lo);
+    layer_chunk<6, MASKS, SAVE>(s, a, lds, c, blds, lo);
+    layer_chunk<7, MASKS, SAVE>(s, a, lds, c, blds, lo);
     // the conversions of this pass were the previous layer's outputs: h1, h2, feat, v1
     if constexpr (MASKS) store_masks(s, a, tile, layer - kXyz2);
     // fc_out's pass converted layer_xyz2's outputs: its partials are sigma's h2 term
@@ -736,6 +764,10 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
       s.acc[0] = bias_mfma((s.h == 0 && i < 3) ? v : 0.0f, ones_b(s.h));
     } else {
       init_acc_per_lane(s, a, kRgb);
+    }
+    if constexpr (SAVE) {
+      s.sv = valid ? a.save + ((int64_t)4 * a.m + row) * 256 + 4 * s.h : nullptr;  // v2
+      save_slot<0>(s, 0.0f);
     }
     {
       float out[16];
@@ -762,6 +794,7 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
   }
 #define CN_RGB_CONV(B)                                                     \
   {                                                                        \
+    if constexpr (SAVE) save_slot<B>(s, 0.0f);                             \
     float out[16];                                                         \
     unsigned mb = 0;                                                       \
     conv_all(s.sl[B], out, 0.0f, nullptr, s.sig, MASKS ? &mb : nullptr);   \
@@ -791,7 +824,7 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
   }
 }
 
-template <int MODE, bool MASKS>
+template <int MODE, bool MASKS, bool SAVE = false>
 __global__ __launch_bounds__(kThreads, 1) void field_x3_kernel(FieldArgs a) {
   // ONE LDS object (a second one makes hipcc wait vmcnt(0) before every ring read):
   // the DMA ring, then the constant vectors and code rows
@@ -803,6 +836,7 @@ __global__ __launch_bounds__(kThreads, 1) void field_x3_kernel(FieldArgs a) {
   s.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   s.wsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.packed), 0, kPackedFloats * 4, 0x00020000);
   s.voff = static_cast<unsigned>(s.wave * 64 + s.lane) * 16u;
+  s.sv = nullptr;
 
   // constant vectors (biases, sigma weights) once per workgroup, then prime the ring
 #pragma unroll
@@ -817,7 +851,7 @@ __global__ __launch_bounds__(kThreads, 1) void field_x3_kernel(FieldArgs a) {
   for (int i = 0; i < kDmaPerWave / 2; ++i) dma_piece(s, lds, 2, i);
 
   const int64_t n_tiles = (a.m + kTile - 1) / kTile;
-  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) field_tile<MODE, MASKS>(s, a, lds, blds, tile);
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) field_tile<MODE, MASKS, SAVE>(s, a, lds, blds, tile);
   // the last tile prefetched chunks 0..2 of a tile that does not exist: they
   // must land before the workgroup's LDS is released
   __builtin_amdgcn_s_waitcnt(0x0F70);
@@ -857,7 +891,8 @@ constexpr int kTSigmaCol = 0, kTZeros = 256;  // transposed-pack constants: fc_o
 // for the lanes of a reduction that hold no sum (lane offset + largest column).
 constexpr int kGaccOff = kConsts;
 constexpr int kDummyOff = kGaccOff + kWaves * kCbStride;
-constexpr int kBwdLdsFloats = kDummyOff + 64 + kCbStride;
+constexpr int kBiasOff = kDummyOff + 64 + kCbStride;  // training: b_dir2, b_dir1, b_xyz1 gradient rows
+constexpr int kBwdLdsFloats = kBiasOff + 3 * 256;
 
 // Accumulator coordinates of A row rho of a block: register and lane half.
 __host__ __device__ constexpr int reg_of_row(int rho) { return (rho & 3) + 4 * (rho >> 3); }
@@ -960,13 +995,34 @@ __device__ __forceinline__ void ds_add(unsigned base, float v) {
 // Row R of block J (lane half h) is feature acc_row(J, R, h); its g_code column
 // sits at gbase + 4 * acc_row(J, R, 0) bytes (gbase carries the 4h and the
 // layer's column offset; lanes that hold no sum point at the dummy row).
+// Lanes that hold no sum carry gbase = kNoSum and stay out of the atomic (EXEC-masked: the LDS
+// then processes 8 lanes per instruction instead of 64).
+constexpr unsigned kNoSum = ~0u;
 template <int J, int R>
 __device__ __forceinline__ void red_add(unsigned gbase, float v) {
-  ds_add<4 * acc_row(J, R, 0)>(gbase, sum8(v));
+#ifdef CN_ABLATE_NO_RED
+  asm volatile("" ::"v"(v), "v"(gbase));
+#else
+  const float t = sum8(v);
+  if (gbase != kNoSum) ds_add<4 * acc_row(J, R, 0)>(gbase, t);
+#endif
 }
 
-// Convert slot J of a backward pass (mask words mw; RED: also sum into g_code).
-template <int J, bool RED>
+// Training backward: masked values of pieces 2q, 2q+1 of slot J (features 32J + 8q + 4h ..
+// + 3) as one 16-B store into the dPre plane row s.sv.
+template <int J, int G>
+__device__ __forceinline__ void save_piece(State& s, float vx, float vy) {
+  if constexpr ((G & 1) == 0) {
+    s.pend[0] = vx;
+    s.pend[1] = vy;
+  } else if (s.sv) {
+    *reinterpret_cast<float4*>(s.sv + 32 * J + 8 * (G / 2)) = make_float4(s.pend[0], s.pend[1], vx, vy);
+  }
+}
+
+// Convert slot J of a backward pass (mask words mw; RED: also sum into the LDS row at gbase --
+// g_code, or a bias gradient row; SAVE: store the masked values into the dPre plane).
+template <int J, bool RED, bool SAVE = false>
 struct ConvMaskFill {
   State& s;
   const unsigned* mw;
@@ -980,6 +1036,7 @@ struct ConvMaskFill {
       red_add<J, 2 * G>(gbase, vx);
       red_add<J, 2 * G + 1>(gbase, vy);
     }
+    if constexpr (SAVE) save_piece<J, G>(s, vx, vy);
     if constexpr (G == 7) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) s.sl[J][i] = out[i];
@@ -987,9 +1044,9 @@ struct ConvMaskFill {
   }
 };
 
-template <int J, bool RED>
+template <int J, bool RED, bool SAVE = false>
 __device__ __forceinline__ void conv_slot(State& s, const unsigned* mw, unsigned gbase) {
-  ConvMaskFill<J, RED> f{s, mw, gbase, {}};
+  ConvMaskFill<J, RED, SAVE> f{s, mw, gbase, {}};
   f.template step<0>();
   f.template step<1>();
   f.template step<2>();
@@ -1027,15 +1084,15 @@ __device__ __forceinline__ void bwd_init(State& s, const float* blds, int off, b
 // One backward pass over 8-block chunks: init, slot 0, chunks 0..6 converting
 // slot J+1, chunk 7 copying the accumulators out (COPY) or leaving them
 // (layer_dir1^T, whose d-dir chunk still reads the slots).
-template <bool RED, bool COPY = true>
+template <bool RED, bool COPY = true, bool SAVE = false>
 __device__ __forceinline__ void bwd_pass(State& s, const FieldArgs& a, float4* lds, int& c, const float* blds,
                                          int init_off, bf16x8 sig_b, const unsigned* mw, unsigned gbase) {
   bwd_init<8>(s, blds, init_off, sig_b);
-  conv_slot<0, RED>(s, mw, gbase);
+  conv_slot<0, RED, SAVE>(s, mw, gbase);
   __builtin_amdgcn_sched_barrier(0);
 #define CN_BWD_CHUNK(J)                                              \
   {                                                                  \
-    ConvMaskFill<(J) + 1, RED> f{s, mw, gbase, {}};                  \
+    ConvMaskFill<(J) + 1, RED, SAVE> f{s, mw, gbase, {}};            \
     run_chunk<RED ? 4 : 2>(s, a, lds, c, CN_SLOT_B(J), f);           \
   }
   CN_BWD_CHUNK(0)
@@ -1084,10 +1141,23 @@ __device__ __forceinline__ void bwd_dir_chunk(State& s, float4* lds, int& c, flo
   ++c;
 }
 
+// Piece G of slot J of layer_xyz1^T's input (m_h1 . d h1); training: its b_xyz1 sums (LDS row
+// at bb) and its dPre plane store.
+template <int J, int G, bool TRAIN>
+__device__ __forceinline__ void x1_piece(State& s, float* out, const unsigned* mw, unsigned bb) {
+  float vx, vy;
+  convm_piece<G>(s.sl[J], out, mw[J >> 1], 16 * (J & 1), vx, vy);
+  if constexpr (TRAIN) {
+    red_add<J, 2 * G>(bb, vx);
+    red_add<J, 2 * G + 1>(bb, vy);
+    save_piece<J, G>(s, vx, vy);
+  }
+}
+
 // layer_xyz1^T chunk Q (k-steps 8Q..8Q+7, blocks 0 and 1): step B reads slot
 // 4Q + B/2 and converts the next slot (4 pieces per step) with mask mw.
-template <int Q>
-__device__ __forceinline__ void bwd_xyz1_chunk(State& s, float4* lds, int& c, const unsigned* mw) {
+template <int Q, bool TRAIN = false>
+__device__ __forceinline__ void bwd_xyz1_chunk(State& s, float4* lds, int& c, const unsigned* mw, unsigned bb = 0) {
   const Dma dma = dma_for(s, lds, c);
   const float4* slot = lds + (c & (kRing - 1)) * kChunkQuads + s.lane;
   const float4* nslot = lds + ((c + 1) & (kRing - 1)) * kChunkQuads;
@@ -1106,11 +1176,10 @@ __device__ __forceinline__ void bwd_xyz1_chunk(State& s, float4* lds, int& c, co
     mfma3(s.acc[1], f2, f3, Bh<SB>(s, TT), Bl<SB>(s, TT));                                              \
     if constexpr (SB + 1 < 8) {                                                                         \
       constexpr int NS = SB + 1, P0 = 4 * TT;                                                           \
-      float vx, vy;                                                                                     \
-      convm_piece<P0>(s.sl[NS], out[NS - kNext], mw[NS >> 1], 16 * (NS & 1), vx, vy);                   \
-      convm_piece<P0 + 1>(s.sl[NS], out[NS - kNext], mw[NS >> 1], 16 * (NS & 1), vx, vy);               \
-      convm_piece<P0 + 2>(s.sl[NS], out[NS - kNext], mw[NS >> 1], 16 * (NS & 1), vx, vy);               \
-      convm_piece<P0 + 3>(s.sl[NS], out[NS - kNext], mw[NS >> 1], 16 * (NS & 1), vx, vy);               \
+      x1_piece<NS, P0, TRAIN>(s, out[NS - kNext], mw, bb);                                              \
+      x1_piece<NS, P0 + 1, TRAIN>(s, out[NS - kNext], mw, bb);                                          \
+      x1_piece<NS, P0 + 2, TRAIN>(s, out[NS - kNext], mw, bb);                                          \
+      x1_piece<NS, P0 + 3, TRAIN>(s, out[NS - kNext], mw, bb);                                          \
       if constexpr (TT == 1) {                                                                          \
         _Pragma("unroll") for (int i = 0; i < 16; ++i) s.sl[NS][i] = out[NS - kNext][i];                \
       }                                                                                                 \
@@ -1165,7 +1234,7 @@ __device__ __forceinline__ void flush_gcode(const State& s, const FieldArgs& a, 
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
-template <int MODE>
+template <int MODE, bool TRAIN>
 __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* lds, float* blds, int64_t tile,
                                          int& cur_code) {
   const int64_t row = tile * kTile + s.wave * 32 + (s.lane & 31);
@@ -1195,16 +1264,29 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
     cur_code = crow0;
   }
   int c = 0;
+#ifdef CN_RED_DUMMY
   const unsigned dummy = lds_addr(blds + kDummyOff) + 4u * s.lane;
+#else
+  const unsigned dummy = kNoSum;
+#endif
   const unsigned gl = lds_addr(blds + kGaccOff + s.wave * kCbStride) + 16u * s.h;  // + 4h floats
   const unsigned gbase = (s.lane & 7) == 7 ? gl : dummy;
   const unsigned gbase0 = ((s.lane & 7) == 7 && s.h == 0) ? gl : dummy;
+  // training: bias gradient rows (b_dir2, b_dir1, b_xyz1) and the dPre plane rows
+  const unsigned bl = lds_addr(blds + kBiasOff) + 16u * s.h;
+  auto bias_base = [&](int k) { return (s.lane & 7) == 7 ? bl + 1024u * k : dummy; };
+  auto plane = [&](int k) { return (TRAIN && valid) ? a.dpre + ((int64_t)k * a.m + row) * 256 + 4 * s.h : nullptr; };
 
   // g_code sigma / rgb: this wave's samples (lane half 1 repeats them)
-  ds_add<4 * kCbSigma>(gbase0, sum8(dr.w));
-  ds_add<4 * kCbRgb>(gbase0, sum8(dr.x));
-  ds_add<4 * (kCbRgb + 1)>(gbase0, sum8(dr.y));
-  ds_add<4 * (kCbRgb + 2)>(gbase0, sum8(dr.z));
+  {
+    const float sw = sum8(dr.w), sx = sum8(dr.x), sy = sum8(dr.y), sz = sum8(dr.z);
+    if (gbase0 != kNoSum) {
+      ds_add<4 * kCbSigma>(gbase0, sw);
+      ds_add<4 * kCbRgb>(gbase0, sx);
+      ds_add<4 * (kCbRgb + 1)>(gbase0, sy);
+      ds_add<4 * (kCbRgb + 2)>(gbase0, sz);
+    }
+  }
   // B operands: d rgb at k-step 0 (lane half 0, k = channel) and the sigma init [dh, dl, dh]
   bf16x8 rh = {}, rl = {}, sig_b = {};
   if (s.h == 0) {
@@ -1233,34 +1315,39 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   }
   // ---- layer_dir2^T (m_v2), layer_dir1^T (m_v1) + its d-dir chunk
   floatx16 acc2;
-  bwd_pass<false, true>(s, a, lds, c, blds, kTZeros, sig_b, mk[3], gbase);
-  bwd_pass<false, false>(s, a, lds, c, blds, kTZeros, sig_b, mk[2], gbase);
+  s.sv = plane(0);
+  bwd_pass<TRAIN, true, TRAIN>(s, a, lds, c, blds, kTZeros, sig_b, mk[3], bias_base(0));
+  s.sv = plane(1);
+  bwd_pass<TRAIN, false, TRAIN>(s, a, lds, c, blds, kTZeros, sig_b, mk[2], bias_base(1));
   bwd_dir_chunk(s, lds, c, acc2);
   // ---- fc_out^T (d feat unmasked, sigma rank-1 init), layer_xyz2^T (m_h2): g_code sums
   const unsigned ones[4] = {~0u, ~0u, ~0u, ~0u};
   for (int l = 0; l < 2; ++l) {
     const unsigned* mw = l == 0 ? ones : mk[1];
-    const unsigned gb = gbase + 4u * (l == 0 ? kCbFeat : kCbXyz2);
-    bwd_pass<true, true>(s, a, lds, c, blds, l == 0 ? kTSigmaCol : kTZeros, sig_b, mw, gb);
+    const unsigned gb = gbase == kNoSum ? kNoSum : gbase + 4u * (l == 0 ? kCbFeat : kCbXyz2);
+    s.sv = plane(2 + l);
+    bwd_pass<true, true, TRAIN>(s, a, lds, c, blds, l == 0 ? kTSigmaCol : kTZeros, sig_b, mw, gb);
   }
   // ---- layer_xyz1^T (m_h1) into acc[0..1]
   bwd_init<2>(s, blds, kTZeros, sig_b);
+  s.sv = plane(4);
+  const unsigned bx1 = bias_base(2);
   {
-    float vx, vy, out[16];
-    convm_piece<0>(s.sl[0], out, mk[0][0], 0, vx, vy);
-    convm_piece<1>(s.sl[0], out, mk[0][0], 0, vx, vy);
-    convm_piece<2>(s.sl[0], out, mk[0][0], 0, vx, vy);
-    convm_piece<3>(s.sl[0], out, mk[0][0], 0, vx, vy);
-    convm_piece<4>(s.sl[0], out, mk[0][0], 0, vx, vy);
-    convm_piece<5>(s.sl[0], out, mk[0][0], 0, vx, vy);
-    convm_piece<6>(s.sl[0], out, mk[0][0], 0, vx, vy);
-    convm_piece<7>(s.sl[0], out, mk[0][0], 0, vx, vy);
+    float out[16];
+    x1_piece<0, 0, TRAIN>(s, out, mk[0], bx1);
+    x1_piece<0, 1, TRAIN>(s, out, mk[0], bx1);
+    x1_piece<0, 2, TRAIN>(s, out, mk[0], bx1);
+    x1_piece<0, 3, TRAIN>(s, out, mk[0], bx1);
+    x1_piece<0, 4, TRAIN>(s, out, mk[0], bx1);
+    x1_piece<0, 5, TRAIN>(s, out, mk[0], bx1);
+    x1_piece<0, 6, TRAIN>(s, out, mk[0], bx1);
+    x1_piece<0, 7, TRAIN>(s, out, mk[0], bx1);
 #pragma unroll
     for (int i = 0; i < 16; ++i) s.sl[0][i] = out[i];
   }
   __builtin_amdgcn_sched_barrier(0);
-  bwd_xyz1_chunk<0>(s, lds, c, mk[0]);
-  bwd_xyz1_chunk<1>(s, lds, c, mk[0]);
+  bwd_xyz1_chunk<0, TRAIN>(s, lds, c, mk[0], bx1);
+  bwd_xyz1_chunk<1, TRAIN>(s, lds, c, mk[0], bx1);
 
   // ---- encodings -> d pts, d view dir (each lane half its own pairs), then the rays
   float dx[3] = {0.f, 0.f, 0.f}, dv[3] = {0.f, 0.f, 0.f};
@@ -1326,7 +1413,7 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   }
 }
 
-template <int MODE>
+template <int MODE, bool TRAIN = false>
 __global__ __launch_bounds__(kThreads, 1) void field_x3_bwd_kernel(FieldArgs a) {
   __shared__ __attribute__((aligned(16))) float4 lds[kLdsQuads + kBwdLdsFloats / 4];
   float* blds = reinterpret_cast<float*>(lds + kLdsQuads);
@@ -1336,6 +1423,7 @@ __global__ __launch_bounds__(kThreads, 1) void field_x3_bwd_kernel(FieldArgs a) 
   s.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   s.wsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.packed), 0, kPackedFloats * 4, 0x00020000);
   s.voff = static_cast<unsigned>(s.wave * 64 + s.lane) * 16u;
+  s.sv = nullptr;
 #pragma unroll
   for (int k = 0; k < kConsts / kThreads; ++k)
     blds[k * kThreads + threadIdx.x] = a.packed[kBiasXyz1 + k * kThreads + threadIdx.x];
@@ -1349,9 +1437,17 @@ __global__ __launch_bounds__(kThreads, 1) void field_x3_bwd_kernel(FieldArgs a) 
   for (int i = 0; i < kDmaPerWave / 2; ++i) dma_piece(s, lds, 2, i);
   int cur_code = -1;
   const int64_t n_tiles = (a.m + kTile - 1) / kTile;
-  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) bwd_tile<MODE>(s, a, lds, blds, tile, cur_code);
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x)
+    bwd_tile<MODE, TRAIN>(s, a, lds, blds, tile, cur_code);
   __builtin_amdgcn_s_waitcnt(0x0F70);
   if (cur_code >= 0) flush_gcode(s, a, blds, cur_code);
+  if constexpr (TRAIN) {
+    __syncthreads();  // every wave's bias sums landed
+    for (int k = threadIdx.x; k < 3 * 256; k += kThreads) {
+      const float v = blds[kBiasOff + k];
+      if (v != 0.0f && a.gbias[k >> 8]) atomicAdd(a.gbias[k >> 8] + (k & 255), v);
+    }
+  }
 }
 
 static_assert(kTChunkX1 + 2 == kChunks, "backward chunk schedule");
@@ -1390,6 +1486,14 @@ int64_t mask_words_x3(int64_t m) { return cn::ceil_div(m, x3::kTile) * x3::kMask
 
 int launch_field_x3_bwd(int mode, FieldArgs& a, hipStream_t st) {
   const unsigned grid = static_cast<unsigned>(std::min<int64_t>(cn::ceil_div(a.m, x3::kTile), cu_count()));
+  if (a.dpre) {
+    switch (mode) {
+      case kFromPts: hipLaunchKernelGGL((x3::field_x3_bwd_kernel<kFromPts, true>), dim3(grid), dim3(x3::kThreads), 0, st, a); break;
+      case kFromRayZ: hipLaunchKernelGGL((x3::field_x3_bwd_kernel<kFromRayZ, true>), dim3(grid), dim3(x3::kThreads), 0, st, a); break;
+      default: return CN_EUNSUPPORTED;
+    }
+    return cn::launch_status();
+  }
   switch (mode) {
     case kFromPts: hipLaunchKernelGGL(x3::field_x3_bwd_kernel<kFromPts>, dim3(grid), dim3(x3::kThreads), 0, st, a); break;
     case kFromRayZ: hipLaunchKernelGGL(x3::field_x3_bwd_kernel<kFromRayZ>, dim3(grid), dim3(x3::kThreads), 0, st, a); break;
@@ -1400,6 +1504,14 @@ int launch_field_x3_bwd(int mode, FieldArgs& a, hipStream_t st) {
 
 int launch_field_x3(int mode, FieldArgs& a, hipStream_t st) {
   const unsigned grid = static_cast<unsigned>(std::min<int64_t>(cn::ceil_div(a.m, x3::kTile), cu_count()));
+  if (a.masks && a.save) {
+    switch (mode) {
+      case kFromPts: hipLaunchKernelGGL((x3::field_x3_kernel<kFromPts, true, true>), dim3(grid), dim3(x3::kThreads), 0, st, a); break;
+      case kFromRayZ: hipLaunchKernelGGL((x3::field_x3_kernel<kFromRayZ, true, true>), dim3(grid), dim3(x3::kThreads), 0, st, a); break;
+      default: return CN_EUNSUPPORTED;
+    }
+    return cn::launch_status();
+  }
   if (a.masks) {
     switch (mode) {
       case kFromPts: hipLaunchKernelGGL((x3::field_x3_kernel<kFromPts, true>), dim3(grid), dim3(x3::kThreads), 0, st, a); break;

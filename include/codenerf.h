@@ -329,6 +329,15 @@ int cn_radiance_field_train_w16(const float* packed, const float* code_bias, con
                                 const float* z, int64_t n_rays, int64_t n_samples, int64_t chunk_rows,
                                 const float* freqs_xyz, const float* freqs_dir, float* raw, float* save,
                                 uint32_t* masks, cn_stream_t stream);
+/* The same pair for either precision: fmt CN_FMT_F32_W16 (fp32 16x16x4) or CN_FMT_BF16X3 (3xbf16
+ * 32x32x16; masks cn_field_mask_words_fmt(CN_FMT_BF16X3, M) words, the same fp32 planes), and
+ * fmt_t the matching transposed pack (CN_FMT_F32_W16_T / CN_FMT_BF16X3_T; the bf16x3 dW GEMMs
+ * are 3xbf16 too).  bf16x3: one code row per 32-sample wave (n_codes == 1 or n_samples % 32 == 0). */
+int cn_radiance_field_train_fmt(int fmt, const float* packed, const float* code_bias, const int64_t* code_index,
+                                int64_t n_codes, const float* pts, const float* ro, const float* rd,
+                                const float* z, int64_t n_rays, int64_t n_samples, int64_t chunk_rows,
+                                const float* freqs_xyz, const float* freqs_dir, float* raw, float* save,
+                                uint32_t* masks, cn_stream_t stream);
 int64_t cn_field_backward_train_workspace_floats(int64_t m);
 int cn_field_backward_train(const float* packed_t, const float* const* params, const uint32_t* masks,
                             const float* saved, const float* x_enc, const float* d_raw, const float* pts,
@@ -337,6 +346,13 @@ int cn_field_backward_train(const float* packed_t, const float* const* params, c
                             const float* freqs_xyz, const float* freqs_dir, float* workspace,
                             float* const* grads, float* g_code, float* d_pts, float* d_ro, float* d_rd,
                             cn_stream_t stream);
+int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, const float* const* params,
+                                const uint32_t* masks, const float* saved, const float* x_enc, const float* d_raw,
+                                const float* pts, const float* ro, const float* rd, const float* z, int64_t n_rays,
+                                int64_t n_samples, int64_t chunk_rows, const int64_t* code_index, int64_t n_codes,
+                                const float* freqs_xyz, const float* freqs_dir, float* workspace,
+                                float* const* grads, float* g_code, float* d_pts, float* d_ro, float* d_rd,
+                                cn_stream_t stream);
 
 /* Backward of cn_code_bias (the code layers, model.py:174-177, and the code
  * halves of layer_xyz2 / fc_out / fc_rgb) from g_code.  dz_s / dz_t (n_codes, 256)

@@ -111,12 +111,15 @@ def _opt_cfg():
                            scheduler_step_size=5000000))
 
 
-@pytest.mark.parametrize("chunk,mixed", [(64, False), (128, True)])
-def test_train_minibatch_matches_oracle(dev, monkeypatch, chunk, mixed):
+@pytest.mark.parametrize("chunk,mixed,precision", [(64, False, "f32"), (128, True, "f32"), (64, False, "bf16x3"),
+                                                    (128, True, "bf16x3")])
+def test_train_minibatch_matches_oracle(dev, monkeypatch, chunk, mixed, precision):
     """One chunk step vs the oracle three ways: (1) fully independent (its own fine depths and
     ReLU decisions) at INDEPENDENT_RTOL; (2) the kernels' discrete decisions -- fine depths and
-    ReLU masks read from the saved activations -- agree with the oracle's up to the fp32 rounding
-    band; (3) with those decisions fed to the oracle, every gradient matches at GRAD_RTOL."""
+    ReLU masks read from the saved activations -- agree with the oracle's up to the precision's
+    rounding band; (3) with those decisions fed to the oracle, every gradient matches at GRAD_RTOL.
+    precision: the field kernels' arithmetic (models' precision = train_precision); bf16x3 runs the
+    3xbf16 fused training pair (32 coarse + 32 fine samples: one code row per 32-sample wave)."""
     from codenerf import ops, train as T
     from codenerf.nerf import PointSampler
     seen = {"z_fine": None, "saved": [], "w_coarse": None}
@@ -132,9 +135,10 @@ def test_train_minibatch_matches_oracle(dev, monkeypatch, chunk, mixed):
         raw, saved = real_train(*a, **k)
         seen["saved"].append(saved)
         return raw, saved
-    def spy_w16(*a, **k):           # the fused fp32 training path (16-sample waves of one code row)
+    def spy_w16(*a, **k):           # the fused training path (one code row per wave)
         raw, saved, masks = real_w16(*a, **k)
         seen["saved"].append(saved)
+        seen["fused"] = k.get("precision", "f32")
         return raw, saved, masks
     monkeypatch.setattr(ops, "sample_pdf", spy_pdf)
     monkeypatch.setattr(ops, "radiance_field_train", spy_train)
@@ -146,15 +150,18 @@ def test_train_minibatch_matches_oracle(dev, monkeypatch, chunk, mixed):
     o = O()
     n_obj, n, lam = 3, 128, 1e-5
     models = _train_models(dev, n_obj)
+    for key in ("nerf_coarse", "nerf_fine"):
+        models[key].precision = models[key].train_precision = precision
+    S = 32 if precision == "bf16x3" else 16
     g = torch.Generator().manual_seed(chunk)
     ro = torch.randn(n, 3, generator=g) * 0.1 + torch.tensor([0.0, 0.0, 1.3])
     rd = torch.randn(n, 3, generator=g) * 0.2 + torch.tensor([0.0, 0.0, -1.0])
     ids = torch.randint(0, n_obj, (n,), generator=g) if mixed else torch.tensor([0] * 64 + [2] * 64)
     tgt = torch.rand(n, 4, generator=g)
     opt, sched = T.prepare_optimizer(_opt_cfg(), models)
-    ps = PointSampler(16, 16, 0.8, 1.8, spacing_mode="lindepth", perturb=False, dtype=torch.float32, device=dev)
+    ps = PointSampler(S, S, 0.8, 1.8, spacing_mode="lindepth", perturb=False, dtype=torch.float32, device=dev)
     emb = embedders(dev)
-    smp, ecfg = o.Sampling(16, 16, 0.8, 1.8), o.EmbedCfg()
+    smp, ecfg = o.Sampling(S, S, 0.8, 1.8), o.EmbedCfg()
     for c0 in range(0, n, chunk):
         sl = slice(c0, c0 + chunk)
         r, d = ro[sl], rd[sl]
@@ -162,6 +169,7 @@ def test_train_minibatch_matches_oracle(dev, monkeypatch, chunk, mixed):
                 "ts": models["embedding"].shape_embedding.weight.detach().cpu().clone(),
                 "tt": models["embedding"].texture_embedding.weight.detach().cpu().clone()}
         seen["saved"].clear()
+        seen["fused"] = None
         logs = T.train_minibatch(models, opt, sched, ps, emb, ro[sl].to(dev), rd[sl].to(dev), ids[sl].to(dev),
                                  tgt[sl].to(dev), lam)
 
@@ -174,7 +182,7 @@ def test_train_minibatch_matches_oracle(dev, monkeypatch, chunk, mixed):
             pts_c, z_c = o.sample_uniform(r, d, smp.bins, None)
             rgb_c, _, _, w_c, _ = o.volume_render(o.forward_pass(pc, ecfg, d, pts_c, zs, zt, masks_c, pre_c), z_c, d)
             if z_f is None:
-                z_f = o.sample_pdf(r, d, w_c.detach()[..., 1:-1], z_c, 16)[1]
+                z_f = o.sample_pdf(r, d, w_c.detach()[..., 1:-1], z_c, S)[1]
             pts_f = r[..., None, :] + d[..., None, :] * z_f[..., :, None]
             rgb_f = o.volume_render(o.forward_pass(pf, ecfg, d, pts_f, zs, zt, masks_f, pre_f), z_f, d)[0]
             lc = torch.nn.functional.mse_loss(rgb_c[..., :3], tgt[sl, :3])
@@ -204,9 +212,10 @@ def test_train_minibatch_matches_oracle(dev, monkeypatch, chunk, mixed):
         #    kernel's z_fine bit for bit, (c) every differing ReLU decision is inside the fp32 band
         w_own, z_c = own[6], own[7]
         assert (seen["w_coarse"] - w_own[..., 1:-1]).abs().max().item() <= 1e-5
-        assert torch.equal(o.sample_pdf(r, d, seen["w_coarse"], z_c, 16)[1], seen["z_fine"])
-        n_dis = (check_mask_agreement(relu_masks(seen["saved"][0]), pre_c, MASK_BAND["f32"], "coarse")
-                 + check_mask_agreement(relu_masks(seen["saved"][1]), pre_f, MASK_BAND["f32"], "fine"))
+        assert seen["fused"] == precision, f"the fused {precision} training path did not run"
+        assert torch.equal(o.sample_pdf(r, d, seen["w_coarse"], z_c, S)[1], seen["z_fine"])
+        n_dis = (check_mask_agreement(relu_masks(seen["saved"][0]), pre_c, MASK_BAND[precision], "coarse")
+                 + check_mask_agreement(relu_masks(seen["saved"][1]), pre_f, MASK_BAND[precision], "fine"))
         z_dis = int((seen["z_fine"] != own[5]).sum())
         print(f"chunk {c0}: differing ReLU decisions (all in-band) {n_dis}, differing fine depths {z_dis}")
         # 3. with exactly those decisions the oracle matches every gradient at GRAD_RTOL ...

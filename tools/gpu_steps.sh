@@ -5,7 +5,9 @@ TAG=${1:-steps}
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
-for job in "eval f32 20" "eval bf16x3 20" "train f32 3"; do
+JOBS=${JOBS:-"eval_f32_20 eval_bf16x3_20 train_f32_3"}
+for jt in $JOBS; do
+  job=$(echo $jt | tr "_" " ")
   t=$(echo $job | tr ' ' '_')
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/$t -o run --output-format csv -- python $R/tools/step_prof.py $job > $O/$t.log 2>&1
   rc=$?; echo "$job rc=$rc"; tail -1 $O/$t.log | cut -c1-400; [ $rc -ne 0 ] && exit $rc

@@ -35,6 +35,7 @@ def main():
         print(bench.eval_bench(dev, rs, emb, models, iters, prec))
     else:
         os.environ["CODENERF_PRECISION"] = prec
+        os.environ["CODENERF_TRAIN_PRECISION"] = prec
         print(bench.train_bench(dev, k, iters, 1))
 
 
