@@ -177,9 +177,18 @@ class _FieldMeta:
         self.code_index = code_index
 
 
-def _param_grad_buffers(params, needs):
+def _param_grad_buffers(params, needs, orig=None):
+    """Zeroed gradient buffers the backward kernels accumulate into: the optimizer's flat-buffer
+    slices when every parameter still has no .grad this step (optim.AdamW.zero_grad), else fresh
+    zeros."""
     if not any(needs):
         return None
+    if orig is not None:
+        slots = [getattr(p, "_cn_grad_slot", None) for p in orig]
+        if all(s is not None and p.grad is None for s, p in zip(slots, orig)):
+            for p in orig:
+                p._cn_grad_slot = None       # one use per zero_grad
+            return slots
     return [torch.zeros_like(p) for p in params]
 
 
@@ -198,6 +207,7 @@ class RadianceField(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, meta, rd, pts, ro, z, z_s, z_t, *params):
+        ctx.orig_params = params
         params = [p.detach() for p in params]
         cb = ops.code_bias(params, z_s, z_t)
         n_rays = rd.shape[0]
@@ -230,7 +240,9 @@ class RadianceField(torch.autograd.Function):
             raw, saved = ops.radiance_field_train(ops.mlp_pack(params, "f32"), cb, rd, meta.n_samples,
                                                   meta.chunk_rows, meta.fx, meta.fd, pts=pts, ro=ro, z=z,
                                                   code_index=meta.code_index)
-        ctx.x_enc = ops.encode_inputs(rd, meta.n_samples, meta.chunk_rows, meta.fx, meta.fd, pts=pts, ro=ro, z=z)
+        # the fused training backward generates the encodings inside its dW kernels
+        ctx.x_enc = None if ctx.train_fused else ops.encode_inputs(rd, meta.n_samples, meta.chunk_rows, meta.fx,
+                                                                   meta.fd, pts=pts, ro=ro, z=z)
         ctx.meta, ctx.acts = meta, saved
         ctx.save_for_backward(rd, pts, ro, z, z_s, z_t, *params)
         return raw
@@ -252,7 +264,8 @@ class RadianceField(torch.autograd.Function):
                 dz_s, dz_t = ops.code_bias_backward(params, z_s, z_t, r["g_code"], None, want_z=True)
             ctx.masks = None
             return (None, r["d_rd"], r["d_pts"], r["d_ro"], None, dz_s, dz_t, *([None] * len(params)))
-        pg = _param_grad_buffers(params, needs[7:])
+        pg = _param_grad_buffers(params, needs[7:], ctx.orig_params)
+        ctx.orig_params = None
         want_z = needs[5] or needs[6]
         if ctx.train_fused:
             x3 = meta.precision == "bf16x3"

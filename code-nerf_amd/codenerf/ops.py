@@ -447,7 +447,8 @@ def radiance_field_train_w16(packed: Tensor, cb: Tensor, rd: Tensor, n_samples: 
     return raw, saved, masks
 
 
-def field_backward_train(packed_t: Tensor, params: Sequence[Tensor], masks: Tensor, saved: Tensor, x_enc: Tensor,
+def field_backward_train(packed_t: Tensor, params: Sequence[Tensor], masks: Tensor, saved: Tensor,
+                         x_enc: Optional[Tensor],
                          d_raw: Tensor, n_rays: int, n_samples: int, chunk_rows: int, n_codes: int,
                          freqs_xyz: Sequence[float], freqs_dir: Sequence[float], rd: Tensor,
                          pts: Optional[Tensor] = None, ro: Optional[Tensor] = None, z: Optional[Tensor] = None,
@@ -461,7 +462,7 @@ def field_backward_train(packed_t: Tensor, params: Sequence[Tensor], masks: Tens
     m = n_rays * n_samples
     params = [_cuda(p.detach(), f"param{i}") for i, p in enumerate(params)]
     d_raw = _cuda(d_raw, "d_raw")
-    assert d_raw.numel() == 4 * m and saved.shape == (5, m, 256) and x_enc.shape == (m, 90)
+    assert d_raw.numel() == 4 * m and saved.shape == (5, m, 256) and (x_enc is None or x_enc.shape == (m, 90))
     dev = d_raw.device
     rd, pts, ro, z = _opt(rd, "rd"), _opt(pts, "pts"), _opt(ro, "ro"), _opt(z, "z")
     if code_index is not None:
@@ -532,7 +533,7 @@ def field_backward(params: Sequence[Tensor], saved: Tensor, x_enc: Tensor, d_raw
     m = n_rays * n_samples
     params = [_cuda(p.detach(), f"param{i}") for i, p in enumerate(params)]
     d_raw = _cuda(d_raw, "d_raw")
-    assert d_raw.numel() == 4 * m and saved.shape == (5, m, 256) and x_enc.shape == (m, 90)
+    assert d_raw.numel() == 4 * m and saved.shape == (5, m, 256) and (x_enc is None or x_enc.shape == (m, 90))
     dev = d_raw.device
     rd, pts, ro, z = _opt(rd, "rd"), _opt(pts, "pts"), _opt(ro, "ro"), _opt(z, "z")
     if code_index is not None:

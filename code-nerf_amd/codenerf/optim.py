@@ -140,12 +140,19 @@ class AdamW(torch.optim.Optimizer):
     # ---- reference API ------------------------------------------------
     def zero_grad(self, set_to_none: bool = True) -> None:
         """train.py:111.  ``set_to_none`` (torch's default) drops the gradients as torch does;
-        otherwise the flat gradient is cleared in one memset and stays attached."""
+        otherwise the flat gradient is cleared in one memset and stays attached.
+
+        Either way the flat gradient is cleared, and each parameter carries its slice as
+        ``p._cn_grad_slot``: a fused backward that finds ``p.grad is None`` accumulates straight
+        into that (zeroed) slice and returns it, so autograd installs it as ``p.grad`` with no
+        per-parameter fill or copy (autograd.RadianceField)."""
+        self._flat["grad"].zero_()
+        for p in self._offs:
+            p._cn_grad_slot = self._view("grad", p)
         if set_to_none:
             for p in self._offs:
                 p.grad = None
         else:
-            self._flat["grad"].zero_()
             for p in self._offs:
                 p.grad = self._view("grad", p)
 

@@ -120,13 +120,15 @@ def train_minibatch(models, optimizer, scheduler, point_sampler, embedders, ro, 
     loss, stats = render_loss_autograd(rgb_coarse, rgb_fine, target_pixels, shape_params, texture_params, 1,
                                        regularizer_lambda)
     loss_coarse, loss_fine, regularization = stats[0], stats[1], stats[2]
-    psnr = mse2psnr(loss_fine.item())
     optimizer.zero_grad()
     loss.backward()
     if is_distributed:
         _average_gradients(optimizer, models)
     optimizer.step()
     scheduler.step()
+    # train.py:105 reads psnr back before the backward; reading the same value once the step is
+    # enqueued keeps the GPU busy through the read-back instead of idling mid-step
+    psnr = mse2psnr(loss_fine.item())
     return {"nerf_loss_coarse": loss_coarse, "nerf_loss_fine": loss_fine, "embedding_loss": regularization,
             "total_loss": loss.detach(), "psnr": psnr}
 

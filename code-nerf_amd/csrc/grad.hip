@@ -623,6 +623,109 @@ __global__ __launch_bounds__(256) void gemm_tn_x3_kernel(const float* __restrict
   flush_block(acc11, C, ldc, pt, N, K, n0 + 32, k0 + 32, i, h);
 }
 
+// gemm_tn against the positional encodings, generated in the kernel: C[n][c] += sum_m A[m][n]
+// enc(m)[c] with enc = the 63 xyz features of the sample point (ENC 0: layer_xyz1's dW) or the 27
+// of its Q1 view direction (ENC 1: layer_dir1's view-direction columns), in
+// PositionalEmbedder.embed order and with encode_inputs_kernel's exact arithmetic -- so the
+// (M, 90) x_enc plane is never written or read.  Register-staged: stage = 16 rows; each thread
+// loads 2 float4 of A and decodes its sample (thread t: sample t >> 5, columns 2 (t & 31) + 0/1)
+// one stage ahead, then writes them into the LDS A image / encoding table behind the stage's
+// MFMAs.  Wave w owns output rows 32 w .. 32 w + 31 and all KB = 2 (xyz) / 1 (dir) column blocks;
+// X3: one 32x32x16 bf16 k-step per stage (3 products), else 8 fp32 32x32x2 row pairs.
+constexpr int kEncRows = 16;
+
+template <int ENC>
+__device__ __forceinline__ float enc_value(const mlp::SampleIn& in, const mlp::FieldArgs& a, int c) {
+  constexpr int K = ENC == 0 ? 63 : 27;
+  if (c >= K) return 0.0f;
+  const float* v = ENC == 0 ? in.x : in.vd;
+  if (c < 3) return v[c];
+  const int b = (c - 3) / 3, comp = (c - 3) % 3;
+  const float arg = __fmul_rn(v[comp], ENC == 0 ? a.fx[b >> 1] : a.fd[b >> 1]);
+  return (b & 1) ? cosf(arg) : sinf(arg);
+}
+
+template <bool X3, int ENC, int MODE>
+__global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __restrict__ A, mlp::FieldArgs a,
+                                                             float* __restrict__ C, int64_t ldc,
+                                                             float* __restrict__ part, int64_t rows_per_block) {
+  constexpr int K = ENC == 0 ? 63 : 27, KB = ENC == 0 ? 2 : 1, EW = 32 * KB;
+  __shared__ __attribute__((aligned(16))) float simg[2][kEncRows * 256];
+  __shared__ __attribute__((aligned(16))) float senc[2][kEncRows * EW];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int i = lane & 31, h = lane >> 5;
+  const int64_t M = a.m;
+  const int64_t mb = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t rows = min(rows_per_block, M - mb);
+  const int n_stages = static_cast<int>((rows + kEncRows - 1) / kEncRows);
+  // staging roles: A rows (tid >> 6) and (tid >> 6) + 8, features 4 (tid & 63); encoding sample
+  // tid >> 5, columns ec, ec + 1 (threads past the table width idle)
+  const int ar = tid >> 6, ac = 4 * (tid & 63);
+  const int es = tid >> 5, ec = 2 * (tid & 31);
+  float4 av[2];
+  float ev[2];
+  auto load = [&](int st) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t r = (int64_t)st * kEncRows + ar + 8 * j;
+      av[j] = r < rows ? *reinterpret_cast<const float4*>(A + (mb + r) * 256 + ac) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    const int64_t r = (int64_t)st * kEncRows + es;
+    ev[0] = ev[1] = 0.0f;
+    if (ec < EW && r < rows) {
+      const mlp::SampleIn in = mlp::decode_sample<MODE>(a, mb + r);
+      ev[0] = enc_value<ENC>(in, a, ec);
+      ev[1] = enc_value<ENC>(in, a, ec + 1);
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) *reinterpret_cast<float4*>(&simg[buf][(ar + 8 * j) * 256 + ac]) = av[j];
+    if (ec < EW) *reinterpret_cast<float2*>(&senc[buf][es * EW + ec]) = make_float2(ev[0], ev[1]);
+  };
+  floatx16 acc[KB];
+#pragma unroll
+  for (int u = 0; u < KB; ++u) acc[u] = floatx16{0};
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int st = 0; st < n_stages; ++st) {
+    const bool more = st + 1 < n_stages;
+    if (more) load(st + 1);
+    const float* sa = simg[st & 1];
+    const float* se = senc[st & 1];
+    if constexpr (X3) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = sa[(8 * h + j) * 256 + 32 * wave + i];
+      u32x4 ah, al;
+      split8(v, ah, al);
+#pragma unroll
+      for (int u = 0; u < KB; ++u) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = se[(8 * h + j) * EW + 32 * u + i];
+        u32x4 bh, bl;
+        split8(v, bh, bl);
+        acc[u] = mfma3(acc[u], ah, al, bh, bl);
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < kEncRows / 2; ++p) {
+        const float x = sa[(2 * p + h) * 256 + 32 * wave + i];
+#pragma unroll
+        for (int u = 0; u < KB; ++u)
+          acc[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(x, se[(2 * p + h) * EW + 32 * u + i], acc[u], 0, 0, 0);
+      }
+    }
+    if (more) store((st + 1) & 1);
+    __syncthreads();
+  }
+  float* pt = part ? part + (int64_t)blockIdx.x * 256 * K : nullptr;
+#pragma unroll
+  for (int u = 0; u < KB; ++u) flush_block(acc[u], C, ldc, pt, 256, K, 32 * wave, 32 * u, i, h);
+}
+
 // out[code(m)][j] += A[m][j] for j < N; code(m) = code_index ? code_index[m / S]
 // : (n_codes == 1 ? 0 : m / S).  Block = 4 waves over kSegRows consecutive rows
 // and 64 columns: lane j of a wave owns column c0 + j (each row read is one
@@ -1033,6 +1136,37 @@ int64_t tn_ws_floats(int64_t M, int N, int K) {
   return best;
 }
 
+// dW of an encoding layer (ENC 0: layer_xyz1 from dPre(xyz1), ENC 1: layer_dir1's view columns
+// from dPre(dir1)) with the encodings generated in the kernel; ws: the deterministic path
+// (enc_ws_parts(M) * 256 * K floats).
+int64_t enc_rows(int64_t M) { return std::max<int64_t>(grad::kEncRows, ceil_div(ceil_div(M, 1024), grad::kEncRows) * grad::kEncRows); }
+int64_t enc_parts(int64_t M) { return ceil_div(M, enc_rows(M)); }
+
+int gemm_tn_enc(int enc, const float* A, const mlp::FieldArgs& a, float* C, int64_t ldc, hipStream_t st, bool x3,
+                float* ws) {
+  const int64_t rows = enc_rows(a.m);
+  const unsigned nb = static_cast<unsigned>(ceil_div(a.m, rows));
+  const int K = enc == 0 ? 63 : 27;
+#define CN_ENC(X3_, E_, M_) \
+  hipLaunchKernelGGL((grad::gemm_tn_enc_kernel<X3_, E_, M_>), dim3(nb), dim3(512), 0, st, A, a, C, ldc, ws, rows)
+  const bool pts = a.pts != nullptr;
+  if (x3) {
+    if (enc == 0) { if (pts) CN_ENC(true, 0, mlp::kFromPts); else CN_ENC(true, 0, mlp::kFromRayZ); }
+    else { if (pts) CN_ENC(true, 1, mlp::kFromPts); else CN_ENC(true, 1, mlp::kFromRayZ); }
+  } else {
+    if (enc == 0) { if (pts) CN_ENC(false, 0, mlp::kFromPts); else CN_ENC(false, 0, mlp::kFromRayZ); }
+    else { if (pts) CN_ENC(false, 1, mlp::kFromPts); else CN_ENC(false, 1, mlp::kFromRayZ); }
+  }
+#undef CN_ENC
+  if (ws) {
+    const int rc = launch_status();
+    if (rc != CN_OK) return rc;
+    hipLaunchKernelGGL(grad::reduce_partials_kernel, dim3(static_cast<unsigned>(ceil_div(256 * K, 64))), dim3(256), 0,
+                       st, ws, static_cast<int64_t>(nb), 256, K, C, ldc);
+  }
+  return launch_status();
+}
+
 int seg_sum(const float* A, int64_t lda, int64_t M, int N, int64_t S, const int64_t* code_index, int64_t n_codes,
             float* out, int64_t out_ld, hipStream_t st) {
   dim3 grid(static_cast<unsigned>(ceil_div(M, grad::kSegRows)), static_cast<unsigned>(ceil_div(N, 64)));
@@ -1278,7 +1412,7 @@ static int64_t train_dw_ws_floats(int64_t m) {
   static const int kShapes[5][2] = {{3, 256}, {256, 256}, {256, 27}, {1, 256}, {256, 63}};
   int64_t best = 0;
   for (const auto& sh : kShapes) best = std::max(best, tn_ws_floats(m, sh[0], sh[1]));
-  return best;
+  return std::max(best, enc_parts(m) * 256 * 63);
 }
 
 extern "C" int64_t cn_field_backward_train_workspace_floats(int64_t m) {
@@ -1308,7 +1442,7 @@ extern "C" int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, con
   using namespace mlp;
   CN_CHECK_ARG(fmt_t == CN_FMT_F32_W16_T || fmt_t == CN_FMT_BF16X3_T);
   const bool x3 = fmt_t == CN_FMT_BF16X3_T;
-  CN_CHECK_ARG(packed_t && params && masks && saved && x_enc && d_raw && rd && g_code && workspace);
+  CN_CHECK_ARG(packed_t && params && masks && saved && d_raw && rd && g_code && workspace);
   CN_CHECK_ARG(freqs_xyz && freqs_dir && n_rays > 0 && n_samples > 0 && chunk_rows > 0 && n_codes > 0);
   CN_CHECK_ARG(pts || (ro && z));
   CN_CHECK_ARG(!d_pts || pts);
@@ -1370,13 +1504,15 @@ extern "C" int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, con
   CN_TRY(gemm_tn(P[0], 256, v1, 256, G(kWDir2), 256, M, 256, 256, st, x3, ws));
   // layer_dir1: [feat | dir enc]
   CN_TRY(gemm_tn(P[1], 256, feat, 256, G(kWDir1), 283, M, 256, 256, st, x3, ws));
-  CN_TRY(gemm_tn(P[1], 256, x_enc + 63, 90, G(kWDir1) + 256, 283, M, 256, 27, st, x3, ws));
+  if (x_enc) CN_TRY(gemm_tn(P[1], 256, x_enc + 63, 90, G(kWDir1) + 256, 283, M, 256, 27, st, x3, ws));
+  else CN_TRY(gemm_tn_enc(1, P[1], a, G(kWDir1) + 256, 283, st, x3, ws));
   // fc_out (h half): row 0 from d sigma, rows 1.. from d feat
   CN_TRY(gemm_tn(d_raw + 3, 4, h2, 256, G(kWOut), 512, M, 1, 256, st, x3, ws));
   CN_TRY(gemm_tn(P[2], 256, h2, 256, G(kWOut) + 512, 512, M, 256, 256, st, x3, ws));
   // layer_xyz2 (h half)
   CN_TRY(gemm_tn(P[3], 256, h1, 256, G(kWXyz2), 512, M, 256, 256, st, x3, ws));
   // layer_xyz1
-  CN_TRY(gemm_tn(P[4], 256, x_enc, 90, G(kWXyz1), 63, M, 256, 63, st, x3, ws));
+  if (x_enc) CN_TRY(gemm_tn(P[4], 256, x_enc, 90, G(kWXyz1), 63, M, 256, 63, st, x3, ws));
+  else CN_TRY(gemm_tn_enc(0, P[4], a, G(kWXyz1), 63, st, x3, ws));
   return CN_OK;
 }

@@ -321,7 +321,8 @@ int cn_field_backward_fused(int fmt_t, const float* packed_t, const uint32_t* ma
  * d_pts / d_ro / d_rd as there; g_code required) that also writes every layer's masked input
  * gradient into workspace (cn_field_backward_train_workspace_floats(M) floats), then the weight
  * and bias gradients dW = dPre^T X as split-M fp32 MFMA GEMMs over those planes, saved and x_enc
- * (cn_encode_inputs), reduced deterministically (cn_gemm_tn_ws) through the rest of workspace: grads (18 pointers, or NULL for none) ACCUMULATED as in
+ * (cn_encode_inputs; or x_enc NULL: the encodings generated inside the dW kernels), reduced
+ * deterministically (cn_gemm_tn_ws) through the rest of workspace: grads (18 pointers, or NULL for none) ACCUMULATED as in
  * cn_field_backward (the code-layer parameters and code halves come from cn_code_bias_backward).
  * One code row per 16-sample wave: n_codes == 1 or n_samples % 16 == 0, else CN_EUNSUPPORTED. */
 int cn_radiance_field_train_w16(const float* packed, const float* code_bias, const int64_t* code_index,

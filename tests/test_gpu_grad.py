@@ -540,3 +540,49 @@ def test_test_time_optimize_runs(dev):
     assert abs(theta.item() - 1.57) > 1e-4 and abs(rho.item() - 1.30) > 1e-4
     assert all(p.requires_grad for mm in models.values() for p in mm.parameters())
 
+
+
+@pytest.mark.parametrize("precision", ["f32", "bf16x3"])
+@pytest.mark.parametrize("mode", ["rayz", "pts"])
+def test_field_backward_train_generated_encodings(dev, mode, precision):
+    """The fused training backward's encoding-layer dW (layer_xyz1, layer_dir1's view columns) with
+    the encodings generated inside the dW kernel (x_enc None, the training path) matches the
+    x_enc-plane GEMMs at GEMM_TOL; every other gradient is the same deterministic computation and
+    must agree bit for bit.  Run twice: the generated path is bitwise reproducible."""
+    from codenerf import ops, synthetic
+    m = model(dev, 0)
+    params = [p.detach() for p in m.param_list()]
+    r, s, chunk = 300, 64, 128
+    g = torch.Generator().manual_seed(5)
+    ro = (torch.randn(r, 3, generator=g) * 0.3 + torch.tensor([0.0, 0.0, 1.3])).to(dev)
+    rd = torch.randn(r, 3, generator=g).to(dev)
+    z = torch.sort(0.8 + torch.rand(r, s, generator=g), dim=-1).values.to(dev)
+    pts = (ro[:, None, :] + rd[:, None, :] * z[..., None]).contiguous() if mode == "pts" else None
+    geo = dict(pts=pts) if mode == "pts" else dict(ro=ro, z=z)
+    gout = torch.randn(r, s, 4, generator=g).to(dev)
+    zs, zt = synthetic.latent_codes(5, 1).to(dev), synthetic.latent_codes(6, 1).to(dev)
+    fx, fd = [2.0 ** k for k in range(10)], [2.0 ** k for k in range(4)]
+    cb = ops.code_bias(params, zs, zt)
+    x3 = precision == "bf16x3"
+    _, saved, masks = ops.radiance_field_train_w16(ops.mlp_pack(params, "bf16x3" if x3 else "f32_w16"), cb, rd, s,
+                                                   chunk, fx, fd, precision=precision, **geo)
+    x_enc = ops.encode_inputs(rd, s, chunk, fx, fd, **geo)
+    packed_t = ops.mlp_pack(params, "bf16x3_t" if x3 else "f32_w16_t")
+    out = {}
+    for name, xe in (("plane", x_enc), ("generated", None), ("generated2", None)):
+        pg = [torch.zeros_like(p) for p in params]
+        ops.field_backward_train(packed_t, params, masks, saved, xe, gout, r, s, chunk, 1, fx, fd, rd=rd,
+                                 param_grads=pg, precision=precision, **geo)
+        out[name] = pg
+    # weights: layer_xyz1 0, layer_xyz2 2, fc_out 4, layer_dir1 12, layer_dir2 14, fc_rgb 16 (dW GEMMs,
+    # deterministic); the biases are float-atomic sums (checked to fp32 rounding)
+    enc_layers, weights = {0, 12}, {0, 2, 4, 12, 14, 16}
+    for k, (a, b) in enumerate(zip(out["generated"], out["plane"])):
+        if k in enc_layers:
+            close(a, b.double(), GEMM_TOL[precision], f"param {k} generated vs plane")
+        elif k in weights:
+            assert torch.equal(a, b), f"param {k}: non-encoding weight gradient changed"
+        else:
+            close(a, b.double(), 1e-5, f"bias {k}")
+        if k in weights:
+            assert torch.equal(a, out["generated2"][k]), f"param {k}: not reproducible"
