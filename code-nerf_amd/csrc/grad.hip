@@ -264,7 +264,13 @@ __device__ __forceinline__ floatx16 mfma3(floatx16 acc, u32x4 ah, u32x4 al, u32x
 }
 
 static_assert(kTwRows == 16, "x3_stage: one stage = one 16-deep k-step");
-__device__ __forceinline__ void x3_stage(const float* slot, int i, int h, int n0, int k0, floatx16 (&acc)[2][4]) {
+__device__ __forceinline__ float sum8v(const float* v) {
+  return ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+}
+
+// bsum[t]: running column sums of A's block t over this lane's rows (the bias gradient dPre^T 1).
+__device__ __forceinline__ void x3_stage(const float* slot, int i, int h, int n0, int k0, floatx16 (&acc)[2][4],
+                                         float (&bsum)[2]) {
   const float* sa = slot + 8 * h * 256 + i;
   const float* sb = sa + kTwRows * 256;
   u32x4 ah[2], al[2];
@@ -273,6 +279,7 @@ __device__ __forceinline__ void x3_stage(const float* slot, int i, int h, int n0
     float v[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = sa[j * 256 + n0 + 32 * t];
+    bsum[t] += sum8v(v);
     split8(v, ah[t], al[t]);
   }
 #pragma unroll
@@ -290,7 +297,8 @@ __device__ __forceinline__ void x3_stage(const float* slot, int i, int h, int n0
 template <bool X3>
 __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restrict__ A, const float* __restrict__ B,
                                                             float* __restrict__ C, int64_t ldc, float* __restrict__ part,
-                                                            int64_t M, int64_t rows_per_block) {
+                                                            float* __restrict__ bias_part, int64_t M,
+                                                            int64_t rows_per_block) {
   __shared__ __attribute__((aligned(16))) float ring[kTwRing * kTwStage];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -321,6 +329,7 @@ __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restr
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int u = 0; u < 4; ++u) acc[t][u] = floatx16{0};
+  float bsum[2] = {0.0f, 0.0f};
   dma(0);
   dma(1);
   dma(2);
@@ -332,7 +341,7 @@ __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restr
     __builtin_amdgcn_sched_barrier(0);
     dma(st + 3);
     if constexpr (X3) {
-      x3_stage(ring + (st & (kTwRing - 1)) * kTwStage, i, h, n0, k0, acc);
+      x3_stage(ring + (st & (kTwRing - 1)) * kTwStage, i, h, n0, k0, acc, bsum);
       continue;
     }
     const float* sa = ring + (st & (kTwRing - 1)) * kTwStage + h * 256 + i;
@@ -366,6 +375,14 @@ __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restr
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int u = 0; u < 4; ++u) flush_block(acc[t][u], C, ldc, pt, 256, 256, n0 + 32 * t, k0 + 32 * u, i, h);
+  // X3 with bias_part: this slab's column sums of A (the waves of column half 0 cover all 256)
+  if (X3 && bias_part && (wave & 1) == 0) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const float b = bsum[t] + __shfl_xor(bsum[t], 32);
+      if (h == 0) bias_part[(int64_t)blockIdx.x * 256 + n0 + 32 * t + i] = b;
+    }
+  }
 }
 
 // gemm_tn for a skinny dPre (N = NA <= 4 columns, e.g. d rgb / d sigma of d raw) against a
@@ -648,7 +665,8 @@ __device__ __forceinline__ float enc_value(const mlp::SampleIn& in, const mlp::F
 template <bool X3, int ENC, int MODE>
 __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __restrict__ A, mlp::FieldArgs a,
                                                              float* __restrict__ C, int64_t ldc,
-                                                             float* __restrict__ part, int64_t rows_per_block) {
+                                                             float* __restrict__ part, float* __restrict__ bias_part,
+                                                             int64_t rows_per_block) {
   constexpr int K = ENC == 0 ? 63 : 27, KB = ENC == 0 ? 2 : 1, EW = 32 * KB;
   __shared__ __attribute__((aligned(16))) float simg[2][kEncRows * 256];
   __shared__ __attribute__((aligned(16))) float senc[2][kEncRows * EW];
@@ -687,6 +705,7 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __rest
   floatx16 acc[KB];
 #pragma unroll
   for (int u = 0; u < KB; ++u) acc[u] = floatx16{0};
+  float bsum = 0.0f;  // column sums of A (feature 32 wave + i) over this lane's rows
   load(0);
   store(0);
   __syncthreads();
@@ -699,6 +718,7 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __rest
       float v[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = sa[(8 * h + j) * 256 + 32 * wave + i];
+      bsum += sum8v(v);
       u32x4 ah, al;
       split8(v, ah, al);
 #pragma unroll
@@ -713,6 +733,7 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __rest
 #pragma unroll
       for (int p = 0; p < kEncRows / 2; ++p) {
         const float x = sa[(2 * p + h) * 256 + 32 * wave + i];
+        bsum += x;
 #pragma unroll
         for (int u = 0; u < KB; ++u)
           acc[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(x, se[(2 * p + h) * EW + 32 * u + i], acc[u], 0, 0, 0);
@@ -724,6 +745,22 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __rest
   float* pt = part ? part + (int64_t)blockIdx.x * 256 * K : nullptr;
 #pragma unroll
   for (int u = 0; u < KB; ++u) flush_block(acc[u], C, ldc, pt, 256, K, 32 * wave, 32 * u, i, h);
+  if (bias_part) {
+    const float b = bsum + __shfl_xor(bsum, 32);
+    if (h == 0) bias_part[(int64_t)blockIdx.x * 256 + 32 * wave + i] = b;
+  }
+}
+
+// Deterministic column sums (bias gradients dPre^T 1) where no dW kernel folds them in:
+// part[b][n] = sum of A[m][n] over block b's rows, in row order.
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ A, int64_t lda, int64_t M, int N,
+                                                     float* __restrict__ part, int64_t rows_per_block) {
+  const int j = threadIdx.x;
+  if (j >= N) return;
+  const int64_t mb = (int64_t)blockIdx.x * rows_per_block, me = min(M, mb + rows_per_block);
+  float s = 0.0f;
+  for (int64_t m = mb; m < me; ++m) s += A[m * lda + j];
+  part[(int64_t)blockIdx.x * N + j] = s;
 }
 
 // out[code(m)][j] += A[m][j] for j < N; code(m) = code_index ? code_index[m / S]
@@ -907,7 +944,8 @@ __global__ void copy_cols_kernel(const float* __restrict__ src, int64_t lds_, fl
 // ---------------------------------------------------------------- code layers (model.py:174-177)
 // Per code row: recompute zs1 / zs2 / zt1, pull the summed code-term gradients g
 // (520-wide, cn_code_bias layout) back through the code halves of layer_xyz2 /
-// fc_out / fc_rgb and the three code layers.  dW / db accumulate with atomics.
+// fc_out / fc_rgb and the three code layers.  dW / db accumulate with atomics.  Rows
+// whose g is all zero (codes no sample used) only write their zero code gradient.
 __global__ __launch_bounds__(256) void code_backward_kernel(mlp::Params P, const float* __restrict__ z_s,
                                                             const float* __restrict__ z_t, const float* __restrict__ g,
                                                             float* __restrict__ dz_s, float* __restrict__ dz_t,
@@ -916,6 +954,14 @@ __global__ __launch_bounds__(256) void code_backward_kernel(mlp::Params P, const
   __shared__ float zs[256], zt[256], s1[256], s2[256], t1[256], ds1[256], ds2[256], dt1[256], go[257];
   const int c = blockIdx.x, j = threadIdx.x;
   const float* gr = g + (int64_t)c * kCbStride;
+  // a code no sample used this step (most rows of a training table) has g = 0: zero code
+  // gradients, no parameter contribution
+  const bool nz = gr[kCbXyz2 + j] != 0.0f || gr[kCbFeat + j] != 0.0f || (j < 8 && gr[kCbSigma + j] != 0.0f);
+  if (!__syncthreads_or(nz)) {
+    if (dz_s) dz_s[(int64_t)c * 256 + j] = 0.0f;
+    if (dz_t) dz_t[(int64_t)c * 256 + j] = 0.0f;
+    return;
+  }
   zs[j] = z_s[(int64_t)c * 256 + j];
   zt[j] = z_t[(int64_t)c * 256 + j];
   go[1 + j] = gr[kCbFeat + j];
@@ -1081,9 +1127,27 @@ TnPlan tn_plan(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t
 
 // ws (optional, tn_plan(..).parts * N * K floats): the deterministic two-pass reduction instead
 // of float atomics.
+// Column sums of A (N <= 256) added to bias in a fixed order (bias_ws: ceil(M / rows) * N floats,
+// rows = max(256, M / 256)).
+int64_t colsum_rows(int64_t M) { return std::max<int64_t>(256, ceil_div(M, 256)); }
+
+int colsum(const float* A, int64_t lda, int64_t M, int N, float* bias, float* bias_ws, hipStream_t st) {
+  const int64_t rows = colsum_rows(M);
+  const unsigned nb = static_cast<unsigned>(ceil_div(M, rows));
+  hipLaunchKernelGGL(grad::colsum_kernel, dim3(nb), dim3(256), 0, st, A, lda, M, N, bias_ws, rows);
+  const int rc = launch_status();
+  if (rc != CN_OK) return rc;
+  hipLaunchKernelGGL(grad::reduce_partials_kernel, dim3(static_cast<unsigned>(ceil_div(N, 64))), dim3(256), 0, st,
+                     bias_ws, static_cast<int64_t>(nb), 1, N, bias, static_cast<int64_t>(N));
+  return launch_status();
+}
+
+// bias (optional, with bias_ws >= 1024 * N floats): also bias += A^T 1 (deterministic; folded into
+// the 3xbf16 whole-tile kernel, a separate column-sum pass otherwise).
 int gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M, int N, int K,
-            hipStream_t st, bool x3 = false, float* ws = nullptr) {
+            hipStream_t st, bool x3 = false, float* ws = nullptr, float* bias = nullptr, float* bias_ws = nullptr) {
   const TnPlan pl = tn_plan(A, lda, B, ldb, M, N, K, x3);
+  const bool fold_bias = bias && pl.kind == kTn256X3;
   const unsigned nb = static_cast<unsigned>(ceil_div(M, pl.rows));
   switch (pl.kind) {
     case kTnSkinny:
@@ -1095,10 +1159,12 @@ int gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, 
       }
       break;
     case kTn256:
-      hipLaunchKernelGGL(grad::gemm_tn256_kernel<false>, dim3(nb), dim3(512), 0, st, A, B, C, ldc, ws, M, pl.rows);
+      hipLaunchKernelGGL(grad::gemm_tn256_kernel<false>, dim3(nb), dim3(512), 0, st, A, B, C, ldc, ws, nullptr, M,
+                         pl.rows);
       break;
     case kTn256X3:
-      hipLaunchKernelGGL(grad::gemm_tn256_kernel<true>, dim3(nb), dim3(512), 0, st, A, B, C, ldc, ws, M, pl.rows);
+      hipLaunchKernelGGL(grad::gemm_tn256_kernel<true>, dim3(nb), dim3(512), 0, st, A, B, C, ldc, ws,
+                         fold_bias ? bias_ws : nullptr, M, pl.rows);
       break;
     case kTnGenericX3: {
       const int64_t tiles = ceil_div(N, grad::kTnTile) * ceil_div(K, grad::kTnTile);
@@ -1118,6 +1184,13 @@ int gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, 
     if (rc != CN_OK) return rc;
     hipLaunchKernelGGL(grad::reduce_partials_kernel, dim3(static_cast<unsigned>(ceil_div((int64_t)N * K, 64))), dim3(256),
                        0, st, ws, pl.parts, N, K, C, ldc);
+  }
+  if (bias) {
+    const int rc = launch_status();
+    if (rc != CN_OK) return rc;
+    if (!fold_bias) return colsum(A, lda, M, N, bias, bias_ws, st);
+    hipLaunchKernelGGL(grad::reduce_partials_kernel, dim3(static_cast<unsigned>(ceil_div(N, 64))), dim3(256), 0, st,
+                       bias_ws, static_cast<int64_t>(nb), 1, N, bias, static_cast<int64_t>(N));
   }
   return launch_status();
 }
@@ -1139,16 +1212,19 @@ int64_t tn_ws_floats(int64_t M, int N, int K) {
 // dW of an encoding layer (ENC 0: layer_xyz1 from dPre(xyz1), ENC 1: layer_dir1's view columns
 // from dPre(dir1)) with the encodings generated in the kernel; ws: the deterministic path
 // (enc_ws_parts(M) * 256 * K floats).
-int64_t enc_rows(int64_t M) { return std::max<int64_t>(grad::kEncRows, ceil_div(ceil_div(M, 1024), grad::kEncRows) * grad::kEncRows); }
+int64_t enc_rows(int64_t M) {
+  return std::max<int64_t>(grad::kEncRows, ceil_div(ceil_div(M, 1024), grad::kEncRows) * grad::kEncRows);
+}
 int64_t enc_parts(int64_t M) { return ceil_div(M, enc_rows(M)); }
 
 int gemm_tn_enc(int enc, const float* A, const mlp::FieldArgs& a, float* C, int64_t ldc, hipStream_t st, bool x3,
-                float* ws) {
+                float* ws, float* bias = nullptr, float* bias_ws = nullptr) {
   const int64_t rows = enc_rows(a.m);
   const unsigned nb = static_cast<unsigned>(ceil_div(a.m, rows));
   const int K = enc == 0 ? 63 : 27;
 #define CN_ENC(X3_, E_, M_) \
-  hipLaunchKernelGGL((grad::gemm_tn_enc_kernel<X3_, E_, M_>), dim3(nb), dim3(512), 0, st, A, a, C, ldc, ws, rows)
+  hipLaunchKernelGGL((grad::gemm_tn_enc_kernel<X3_, E_, M_>), dim3(nb), dim3(512), 0, st, A, a, C, ldc, ws, \
+                     bias ? bias_ws : nullptr, rows)
   const bool pts = a.pts != nullptr;
   if (x3) {
     if (enc == 0) { if (pts) CN_ENC(true, 0, mlp::kFromPts); else CN_ENC(true, 0, mlp::kFromRayZ); }
@@ -1163,6 +1239,12 @@ int gemm_tn_enc(int enc, const float* A, const mlp::FieldArgs& a, float* C, int6
     if (rc != CN_OK) return rc;
     hipLaunchKernelGGL(grad::reduce_partials_kernel, dim3(static_cast<unsigned>(ceil_div(256 * K, 64))), dim3(256), 0,
                        st, ws, static_cast<int64_t>(nb), 256, K, C, ldc);
+  }
+  if (bias) {
+    const int rc = launch_status();
+    if (rc != CN_OK) return rc;
+    hipLaunchKernelGGL(grad::reduce_partials_kernel, dim3(4), dim3(256), 0, st, bias_ws, static_cast<int64_t>(nb), 1,
+                       256, bias, static_cast<int64_t>(256));
   }
   return launch_status();
 }
@@ -1415,8 +1497,11 @@ static int64_t train_dw_ws_floats(int64_t m) {
   return std::max(best, enc_parts(m) * 256 * 63);
 }
 
+// dPre planes | dW partial tiles | bias partial rows (3xbf16: folded into the dW kernels)
+constexpr int64_t kBiasWsFloats = 1024 * 256;
+
 extern "C" int64_t cn_field_backward_train_workspace_floats(int64_t m) {
-  return m > 0 ? 5 * m * 256 + train_dw_ws_floats(m) : -1;
+  return m > 0 ? 5 * m * 256 + train_dw_ws_floats(m) + kBiasWsFloats : -1;
 }
 
 extern "C" int cn_field_backward_train(const float* packed_t, const float* const* params, const uint32_t* masks,
@@ -1476,7 +1561,7 @@ extern "C" int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, con
   a.d_rd = d_rd;
   a.dpre = workspace;
   const bool wg = grads && grads[0];
-  if (wg) {
+  if (wg && !x3) {  // fp32: summed in the fused backward; 3xbf16: folded into the dW GEMMs below
     a.gbias[0] = grads[kBDir2];
     a.gbias[1] = grads[kBDir1];
     a.gbias[2] = grads[kBXyz1];
@@ -1493,6 +1578,8 @@ extern "C" int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, con
   const float* P[5];
   for (int k = 0; k < 5; ++k) P[k] = workspace + k * M * 256;
   float* ws = workspace + 5 * M * 256;
+  float* bws = ws + train_dw_ws_floats(M);
+  auto B = [&](int i) { return x3 ? grads[i] : nullptr; };  // bias folded into this GEMM (3xbf16)
   const float* h1 = saved;
   const float* h2 = saved + M * 256;
   const float* feat = saved + 2 * M * 256;
@@ -1501,9 +1588,9 @@ extern "C" int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, con
   // fc_rgb (h half): dW += d rgb^T v2
   CN_TRY(gemm_tn(d_raw, 4, v2, 256, G(kWRgb), 512, M, 3, 256, st, x3, ws));
   // layer_dir2
-  CN_TRY(gemm_tn(P[0], 256, v1, 256, G(kWDir2), 256, M, 256, 256, st, x3, ws));
+  CN_TRY(gemm_tn(P[0], 256, v1, 256, G(kWDir2), 256, M, 256, 256, st, x3, ws, B(kBDir2), bws));
   // layer_dir1: [feat | dir enc]
-  CN_TRY(gemm_tn(P[1], 256, feat, 256, G(kWDir1), 283, M, 256, 256, st, x3, ws));
+  CN_TRY(gemm_tn(P[1], 256, feat, 256, G(kWDir1), 283, M, 256, 256, st, x3, ws, B(kBDir1), bws));
   if (x_enc) CN_TRY(gemm_tn(P[1], 256, x_enc + 63, 90, G(kWDir1) + 256, 283, M, 256, 27, st, x3, ws));
   else CN_TRY(gemm_tn_enc(1, P[1], a, G(kWDir1) + 256, 283, st, x3, ws));
   // fc_out (h half): row 0 from d sigma, rows 1.. from d feat
@@ -1512,7 +1599,7 @@ extern "C" int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, con
   // layer_xyz2 (h half)
   CN_TRY(gemm_tn(P[3], 256, h1, 256, G(kWXyz2), 512, M, 256, 256, st, x3, ws));
   // layer_xyz1
-  if (x_enc) CN_TRY(gemm_tn(P[4], 256, x_enc, 90, G(kWXyz1), 63, M, 256, 63, st, x3, ws));
-  else CN_TRY(gemm_tn_enc(0, P[4], a, G(kWXyz1), 63, st, x3, ws));
+  if (x_enc) CN_TRY(gemm_tn(P[4], 256, x_enc, 90, G(kWXyz1), 63, M, 256, 63, st, x3, ws, B(kBXyz1), bws));
+  else CN_TRY(gemm_tn_enc(0, P[4], a, G(kWXyz1), 63, st, x3, ws, B(kBXyz1), bws));
   return CN_OK;
 }

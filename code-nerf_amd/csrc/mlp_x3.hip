@@ -891,8 +891,7 @@ constexpr int kTSigmaCol = 0, kTZeros = 256;  // transposed-pack constants: fc_o
 // for the lanes of a reduction that hold no sum (lane offset + largest column).
 constexpr int kGaccOff = kConsts;
 constexpr int kDummyOff = kGaccOff + kWaves * kCbStride;
-constexpr int kBiasOff = kDummyOff + 64 + kCbStride;  // training: b_dir2, b_dir1, b_xyz1 gradient rows
-constexpr int kBwdLdsFloats = kBiasOff + 3 * 256;
+constexpr int kBwdLdsFloats = kDummyOff + 64 + kCbStride;
 
 // Accumulator coordinates of A row rho of a block: register and lane half.
 __host__ __device__ constexpr int reg_of_row(int rho) { return (rho & 3) + 4 * (rho >> 3); }
@@ -1141,23 +1140,18 @@ __device__ __forceinline__ void bwd_dir_chunk(State& s, float4* lds, int& c, flo
   ++c;
 }
 
-// Piece G of slot J of layer_xyz1^T's input (m_h1 . d h1); training: its b_xyz1 sums (LDS row
-// at bb) and its dPre plane store.
+// Piece G of slot J of layer_xyz1^T's input (m_h1 . d h1); training: its dPre plane store.
 template <int J, int G, bool TRAIN>
-__device__ __forceinline__ void x1_piece(State& s, float* out, const unsigned* mw, unsigned bb) {
+__device__ __forceinline__ void x1_piece(State& s, float* out, const unsigned* mw) {
   float vx, vy;
   convm_piece<G>(s.sl[J], out, mw[J >> 1], 16 * (J & 1), vx, vy);
-  if constexpr (TRAIN) {
-    red_add<J, 2 * G>(bb, vx);
-    red_add<J, 2 * G + 1>(bb, vy);
-    save_piece<J, G>(s, vx, vy);
-  }
+  if constexpr (TRAIN) save_piece<J, G>(s, vx, vy);
 }
 
 // layer_xyz1^T chunk Q (k-steps 8Q..8Q+7, blocks 0 and 1): step B reads slot
 // 4Q + B/2 and converts the next slot (4 pieces per step) with mask mw.
 template <int Q, bool TRAIN = false>
-__device__ __forceinline__ void bwd_xyz1_chunk(State& s, float4* lds, int& c, const unsigned* mw, unsigned bb = 0) {
+__device__ __forceinline__ void bwd_xyz1_chunk(State& s, float4* lds, int& c, const unsigned* mw) {
   const Dma dma = dma_for(s, lds, c);
   const float4* slot = lds + (c & (kRing - 1)) * kChunkQuads + s.lane;
   const float4* nslot = lds + ((c + 1) & (kRing - 1)) * kChunkQuads;
@@ -1176,10 +1170,10 @@ __device__ __forceinline__ void bwd_xyz1_chunk(State& s, float4* lds, int& c, co
     mfma3(s.acc[1], f2, f3, Bh<SB>(s, TT), Bl<SB>(s, TT));                                              \
     if constexpr (SB + 1 < 8) {                                                                         \
       constexpr int NS = SB + 1, P0 = 4 * TT;                                                           \
-      x1_piece<NS, P0, TRAIN>(s, out[NS - kNext], mw, bb);                                              \
-      x1_piece<NS, P0 + 1, TRAIN>(s, out[NS - kNext], mw, bb);                                          \
-      x1_piece<NS, P0 + 2, TRAIN>(s, out[NS - kNext], mw, bb);                                          \
-      x1_piece<NS, P0 + 3, TRAIN>(s, out[NS - kNext], mw, bb);                                          \
+      x1_piece<NS, P0, TRAIN>(s, out[NS - kNext], mw);                                                  \
+      x1_piece<NS, P0 + 1, TRAIN>(s, out[NS - kNext], mw);                                              \
+      x1_piece<NS, P0 + 2, TRAIN>(s, out[NS - kNext], mw);                                              \
+      x1_piece<NS, P0 + 3, TRAIN>(s, out[NS - kNext], mw);                                              \
       if constexpr (TT == 1) {                                                                          \
         _Pragma("unroll") for (int i = 0; i < 16; ++i) s.sl[NS][i] = out[NS - kNext][i];                \
       }                                                                                                 \
@@ -1272,9 +1266,7 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   const unsigned gl = lds_addr(blds + kGaccOff + s.wave * kCbStride) + 16u * s.h;  // + 4h floats
   const unsigned gbase = (s.lane & 7) == 7 ? gl : dummy;
   const unsigned gbase0 = ((s.lane & 7) == 7 && s.h == 0) ? gl : dummy;
-  // training: bias gradient rows (b_dir2, b_dir1, b_xyz1) and the dPre plane rows
-  const unsigned bl = lds_addr(blds + kBiasOff) + 16u * s.h;
-  auto bias_base = [&](int k) { return (s.lane & 7) == 7 ? bl + 1024u * k : dummy; };
+  // training: the dPre plane rows (the bias gradients are folded into the dW GEMMs)
   auto plane = [&](int k) { return (TRAIN && valid) ? a.dpre + ((int64_t)k * a.m + row) * 256 + 4 * s.h : nullptr; };
 
   // g_code sigma / rgb: this wave's samples (lane half 1 repeats them)
@@ -1316,9 +1308,9 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   // ---- layer_dir2^T (m_v2), layer_dir1^T (m_v1) + its d-dir chunk
   floatx16 acc2;
   s.sv = plane(0);
-  bwd_pass<TRAIN, true, TRAIN>(s, a, lds, c, blds, kTZeros, sig_b, mk[3], bias_base(0));
+  bwd_pass<false, true, TRAIN>(s, a, lds, c, blds, kTZeros, sig_b, mk[3], gbase);
   s.sv = plane(1);
-  bwd_pass<TRAIN, false, TRAIN>(s, a, lds, c, blds, kTZeros, sig_b, mk[2], bias_base(1));
+  bwd_pass<false, false, TRAIN>(s, a, lds, c, blds, kTZeros, sig_b, mk[2], gbase);
   bwd_dir_chunk(s, lds, c, acc2);
   // ---- fc_out^T (d feat unmasked, sigma rank-1 init), layer_xyz2^T (m_h2): g_code sums
   const unsigned ones[4] = {~0u, ~0u, ~0u, ~0u};
@@ -1331,23 +1323,22 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   // ---- layer_xyz1^T (m_h1) into acc[0..1]
   bwd_init<2>(s, blds, kTZeros, sig_b);
   s.sv = plane(4);
-  const unsigned bx1 = bias_base(2);
   {
     float out[16];
-    x1_piece<0, 0, TRAIN>(s, out, mk[0], bx1);
-    x1_piece<0, 1, TRAIN>(s, out, mk[0], bx1);
-    x1_piece<0, 2, TRAIN>(s, out, mk[0], bx1);
-    x1_piece<0, 3, TRAIN>(s, out, mk[0], bx1);
-    x1_piece<0, 4, TRAIN>(s, out, mk[0], bx1);
-    x1_piece<0, 5, TRAIN>(s, out, mk[0], bx1);
-    x1_piece<0, 6, TRAIN>(s, out, mk[0], bx1);
-    x1_piece<0, 7, TRAIN>(s, out, mk[0], bx1);
+    x1_piece<0, 0, TRAIN>(s, out, mk[0]);
+    x1_piece<0, 1, TRAIN>(s, out, mk[0]);
+    x1_piece<0, 2, TRAIN>(s, out, mk[0]);
+    x1_piece<0, 3, TRAIN>(s, out, mk[0]);
+    x1_piece<0, 4, TRAIN>(s, out, mk[0]);
+    x1_piece<0, 5, TRAIN>(s, out, mk[0]);
+    x1_piece<0, 6, TRAIN>(s, out, mk[0]);
+    x1_piece<0, 7, TRAIN>(s, out, mk[0]);
 #pragma unroll
     for (int i = 0; i < 16; ++i) s.sl[0][i] = out[i];
   }
   __builtin_amdgcn_sched_barrier(0);
-  bwd_xyz1_chunk<0, TRAIN>(s, lds, c, mk[0], bx1);
-  bwd_xyz1_chunk<1, TRAIN>(s, lds, c, mk[0], bx1);
+  bwd_xyz1_chunk<0, TRAIN>(s, lds, c, mk[0]);
+  bwd_xyz1_chunk<1, TRAIN>(s, lds, c, mk[0]);
 
   // ---- encodings -> d pts, d view dir (each lane half its own pairs), then the rays
   float dx[3] = {0.f, 0.f, 0.f}, dv[3] = {0.f, 0.f, 0.f};
@@ -1441,13 +1432,6 @@ __global__ __launch_bounds__(kThreads, 1) void field_x3_bwd_kernel(FieldArgs a) 
     bwd_tile<MODE, TRAIN>(s, a, lds, blds, tile, cur_code);
   __builtin_amdgcn_s_waitcnt(0x0F70);
   if (cur_code >= 0) flush_gcode(s, a, blds, cur_code);
-  if constexpr (TRAIN) {
-    __syncthreads();  // every wave's bias sums landed
-    for (int k = threadIdx.x; k < 3 * 256; k += kThreads) {
-      const float v = blds[kBiasOff + k];
-      if (v != 0.0f && a.gbias[k >> 8]) atomicAdd(a.gbias[k >> 8] + (k & 255), v);
-    }
-  }
 }
 
 static_assert(kTChunkX1 + 2 == kChunks, "backward chunk schedule");
