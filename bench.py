@@ -298,7 +298,8 @@ def run(args):
             result["eval_c5"] = {p: eval_bench(dev, rs, emb, models, args.eval_iters, p) for p in ("f32", "bf16x3")}
             set_precision(args.precision)
         if args.train_iters > 0:
-            result["train_c3"] = train_bench(dev, k, args.train_iters, world)
+            result["train_c3"] = train_bench(dev, k, args.train_iters, world, "f32")
+            result["train_c3"]["bf16x3"] = train_bench(dev, k, args.train_iters, world, "bf16x3")
 
     if rank == 0 and not args.no_cpu_baseline:
         cb, ref_img = cpu_baseline(k, poses[:1])
@@ -373,7 +374,7 @@ def eval_bench(dev, rs, emb, models, iters, precision):
                            "read-back included"}
 
 
-def train_bench(dev, k, iters, world):
+def train_bench(dev, k, iters, world, precision=None):
     """C3 training (srn-cars-code.yml; train.py:64-114): one iteration = 4 images x 4096 random rays,
     chunk 4096 -> 4 optimiser steps, each 64+64 perturbed samples per ray with per-object codes from a
     2458-object table, fwd + bwd into both MLPs and both code tables, flat AdamW (one launch), LambdaLR,
@@ -399,6 +400,9 @@ def train_bench(dev, k, iters, world):
     torch.manual_seed(rank + 1)                   # train.py:29-31: each rank draws its own rays
     np.random.seed(rank + 1)
     models = T.prepare_models(cfg, n_objects, dev)
+    precision = precision or os.environ.get("CODENERF_PRECISION", "f32")
+    for key in ("nerf_coarse", "nerf_fine"):       # field kernels and dW GEMMs in one precision
+        models[key].precision = models[key].train_precision = precision
     opt, sched = T.prepare_optimizer(cfg, models)
     samplers = N.prepare_samplers(cfg, H, W, k, torch.float32, dev)
     embedders = N.prepare_embedders(cfg, torch.float32, dev)
@@ -441,12 +445,14 @@ def train_bench(dev, k, iters, world):
     rays = batch * 4096 * iters * world
     return {"ms_per_iter": dt / iters * 1e3, "rays_per_s": rays / dt, "rays_per_iter_per_rank": batch * 4096,
             "optimizer_steps_per_iter": batch, "samples": "64+64 perturbed", "objects": n_objects,
-            "params": n_params, "loss": float(logs[-1]["total_loss"]), "dtype": "f32",
+            "params": n_params, "loss": float(logs[-1]["total_loss"]), "dtype": precision,
             "adamw": {"kernel_ms": adamw_ms, "bytes": 28 * n_params,
                       "gbps": 28 * n_params / (adamw_ms * 1e-3) / 1e9},
-            "note": "fp32 16x16x4 training forward (activations + ReLU masks kept), ONE fused fp32 dX backward "
-                    "launch per field (masked layer gradients kept), split-M fp32 MFMA dW GEMMs, fused loss, flat "
-                    "AdamW; train.py's per-chunk psnr read-back included"}
+            "note": (("fp32 16x16x4" if precision == "f32" else "3xbf16 32x32x16") +
+                     " training forward (activation planes + ReLU masks kept), ONE fused dX backward launch per field"
+                     " (masked layer-input gradients kept), deterministic split-M dW GEMMs (encodings generated "
+                     "in-kernel" + (", bias column sums folded in" if precision == "bf16x3" else "") +
+                     "), fused loss, flat AdamW; train.py's per-chunk psnr read-back included")}
 
 
 def cpu_threads() -> int:

@@ -36,7 +36,7 @@ def main():
     else:
         os.environ["CODENERF_PRECISION"] = prec
         os.environ["CODENERF_TRAIN_PRECISION"] = prec
-        print(bench.train_bench(dev, k, iters, 1))
+        print(bench.train_bench(dev, k, iters, 1, prec))
 
 
 if __name__ == "__main__":
