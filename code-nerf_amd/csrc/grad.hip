@@ -946,6 +946,8 @@ __global__ void copy_cols_kernel(const float* __restrict__ src, int64_t lds_, fl
 // (520-wide, cn_code_bias layout) back through the code halves of layer_xyz2 /
 // fc_out / fc_rgb and the three code layers.  dW / db accumulate with atomics.  Rows
 // whose g is all zero (codes no sample used) only write their zero code gradient.
+constexpr int kCodeRowSplits = 16;
+
 __global__ __launch_bounds__(256) void code_backward_kernel(mlp::Params P, const float* __restrict__ z_s,
                                                             const float* __restrict__ z_t, const float* __restrict__ g,
                                                             float* __restrict__ dz_s, float* __restrict__ dz_t,
@@ -957,9 +959,10 @@ __global__ __launch_bounds__(256) void code_backward_kernel(mlp::Params P, const
   // a code no sample used this step (most rows of a training table) has g = 0: zero code
   // gradients, no parameter contribution
   const bool nz = gr[kCbXyz2 + j] != 0.0f || gr[kCbFeat + j] != 0.0f || (j < 8 && gr[kCbSigma + j] != 0.0f);
+  const bool lead = blockIdx.y == 0;  // writes dz and the bias / single-row terms
   if (!__syncthreads_or(nz)) {
-    if (dz_s) dz_s[(int64_t)c * 256 + j] = 0.0f;
-    if (dz_t) dz_t[(int64_t)c * 256 + j] = 0.0f;
+    if (lead && dz_s) dz_s[(int64_t)c * 256 + j] = 0.0f;
+    if (lead && dz_t) dz_t[(int64_t)c * 256 + j] = 0.0f;
     return;
   }
   zs[j] = z_s[(int64_t)c * 256 + j];
@@ -1012,8 +1015,8 @@ __global__ __launch_bounds__(256) void code_backward_kernel(mlp::Params P, const
       a = fmaf(P.p[kWSc2][n * 256 + j], ds2[n], a);
       b = fmaf(P.p[kWTc1][n * 256 + j], dt1[n], b);
     }
-    if (dz_s) dz_s[(int64_t)c * 256 + j] = a;
-    if (dz_t) dz_t[(int64_t)c * 256 + j] = b;
+    if (lead && dz_s) dz_s[(int64_t)c * 256 + j] = a;
+    if (lead && dz_t) dz_t[(int64_t)c * 256 + j] = b;
   }
   if (!G.p[kWSc1]) return;
   // weight gradients of the code layers and the code halves: outer products, one row per
@@ -1023,13 +1026,17 @@ __global__ __launch_bounds__(256) void code_backward_kernel(mlp::Params P, const
   if (j < 3) grgb[j] = gr[kCbRgb + j];
   __syncthreads();
   const float zsj = zs[j], ztj = zt[j], s1j = s1[j], s2j = s2[j], t1j = t1[j];
-  for (int r = 0; r < 256; ++r) {
+  // this block's rows of the outer products (blockIdx.y of kCodeRowSplits; the per-code vectors
+  // above are recomputed by each, so the atomics spread over the chip)
+  const int r0 = blockIdx.y * (256 / kCodeRowSplits);
+  for (int r = r0; r < r0 + 256 / kCodeRowSplits; ++r) {
     atomicAdd(&const_cast<float*>(G.p[kWSc1])[r * 256 + j], ds1[r] * zsj);
     atomicAdd(&const_cast<float*>(G.p[kWSc2])[r * 256 + j], ds2[r] * zsj);
     atomicAdd(&const_cast<float*>(G.p[kWTc1])[r * 256 + j], dt1[r] * ztj);
     atomicAdd(&const_cast<float*>(G.p[kWXyz2])[r * 512 + 256 + j], gx2[r] * s1j);
     atomicAdd(&const_cast<float*>(G.p[kWOut])[(1 + r) * 512 + 256 + j], go[1 + r] * s2j);
   }
+  if (!lead) return;
   atomicAdd(&const_cast<float*>(G.p[kBSc1])[j], ds1[j]);
   atomicAdd(&const_cast<float*>(G.p[kBSc2])[j], ds2[j]);
   atomicAdd(&const_cast<float*>(G.p[kBTc1])[j], dt1[j]);
@@ -1458,8 +1465,8 @@ extern "C" int cn_code_bias_backward(const float* const* params, const float* z_
     P.p[i] = params[i];
     G.p[i] = grads ? grads[i] : nullptr;
   }
-  hipLaunchKernelGGL(grad::code_backward_kernel, dim3(static_cast<unsigned>(n_codes)), dim3(256), 0, as_stream(stream), P,
-                     z_s, z_t, g_code, dz_s, dz_t, G);
+  hipLaunchKernelGGL(grad::code_backward_kernel, dim3(static_cast<unsigned>(n_codes), grads ? grad::kCodeRowSplits : 1),
+                     dim3(256), 0, as_stream(stream), P, z_s, z_t, g_code, dz_s, dz_t, G);
   return launch_status();
 }
 
