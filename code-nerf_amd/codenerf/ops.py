@@ -438,7 +438,8 @@ def radiance_field_train_w16(packed: Tensor, cb: Tensor, rd: Tensor, n_samples: 
         code_index = _cuda(code_index, "code_index", torch.int64)
     m = n * n_samples
     raw = torch.empty(n, n_samples, 4, device=rd.device, dtype=torch.float32)
-    saved = torch.empty(5, m, 256, device=rd.device, dtype=torch.float32)
+    # the planes + one scratch row (cn_radiance_field_train_fmt)
+    saved = torch.empty(5 * m * 256 + 256, device=rd.device, dtype=torch.float32)[:5 * m * 256].view(5, m, 256)
     masks = torch.empty(int(lib.cn_field_mask_words_fmt(fmt, m)), device=rd.device, dtype=torch.int32)
     check(lib.cn_radiance_field_train_fmt(fmt, ptr(packed), ptr(cb), ptr(code_index), cb.shape[0], ptr(pts), ptr(ro),
                                           ptr(rd), ptr(z), n, n_samples, chunk_rows, _lib.host_floats(freqs_xyz),

@@ -240,14 +240,12 @@ __device__ __forceinline__ void put_mask(unsigned* mw, unsigned mb) {
 // + 3, one 16-B store into the plane row s.sv; lo = 0 for a ReLU, -inf for feat).
 template <int J, int Q>
 __device__ __forceinline__ void save_quad(const State& s, float lo) {
-  if (s.sv) {
-    float4 o;
-    o.x = vmax(s.sl[J][4 * Q], lo);
-    o.y = vmax(s.sl[J][4 * Q + 1], lo);
-    o.z = vmax(s.sl[J][4 * Q + 2], lo);
-    o.w = vmax(s.sl[J][4 * Q + 3], lo);
-    *reinterpret_cast<float4*>(s.sv + 32 * J + 8 * Q) = o;
-  }
+  float4 o;
+  o.x = vmax(s.sl[J][4 * Q], lo);
+  o.y = vmax(s.sl[J][4 * Q + 1], lo);
+  o.z = vmax(s.sl[J][4 * Q + 2], lo);
+  o.w = vmax(s.sl[J][4 * Q + 3], lo);
+  *reinterpret_cast<float4*>(s.sv + 32 * J + 8 * Q) = o;
 }
 
 template <int J>
@@ -653,6 +651,8 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
   const int64_t row = tile * kTile + s.wave * 32 + (s.lane & 31);
   const bool valid = row < a.m;
   const int64_t rc = valid ? row : a.m - 1;
+  // training: padding lanes store into the scratch row after the planes (no branch per store)
+  float* const scratch = SAVE ? a.save + 5 * a.m * 256 : nullptr;
 
   // ---- per-sample inputs and this wave's code row (ordinary loads; the DMA in
   // flight -- chunks 0..2 of this tile -- retires with them)
@@ -732,7 +732,7 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
     const float lo = layer == kDir1 ? -__builtin_inff() : 0.0f;
     s.sig = 0.0f;
     // training: the slots converted in this pass (h1, h2, feat, v1) go to plane layer - kXyz2
-    if constexpr (SAVE) s.sv = valid ? a.save + ((int64_t)(layer - kXyz2) * a.m + row) * 256 + 4 * s.h : nullptr;
+    if constexpr (SAVE) s.sv = (valid ? a.save + ((int64_t)(layer - kXyz2) * a.m + row) * 256 : scratch) + 4 * s.h;
     begin_layer<MASKS, SAVE>(s, a, blds, layer, lo);
     if (layer == kDir1) {
       NoFill nf;
@@ -766,7 +766,7 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
       init_acc_per_lane(s, a, kRgb);
     }
     if constexpr (SAVE) {
-      s.sv = valid ? a.save + ((int64_t)4 * a.m + row) * 256 + 4 * s.h : nullptr;  // v2
+      s.sv = (valid ? a.save + ((int64_t)4 * a.m + row) * 256 : scratch) + 4 * s.h;  // v2
       save_slot<0>(s, 0.0f);
     }
     {
@@ -887,11 +887,9 @@ static_assert(kChunks % kRing == 0, "cyclic stream: chunk c + 36 reuses chunk c'
 
 constexpr int kTChunkD1 = 9, kTChunkDir = 17, kTChunkOut = 18, kTChunkX2 = 26, kTChunkX1 = 34;
 constexpr int kTSigmaCol = 0, kTZeros = 256;  // transposed-pack constants: fc_out row 0 over h2, zeros
-// LDS after the ring: constants, one g_code row per wave, a shared dummy target
-// for the lanes of a reduction that hold no sum (lane offset + largest column).
+// LDS after the ring: constants, then one g_code row per wave.
 constexpr int kGaccOff = kConsts;
-constexpr int kDummyOff = kGaccOff + kWaves * kCbStride;
-constexpr int kBwdLdsFloats = kDummyOff + 64 + kCbStride;
+constexpr int kBwdLdsFloats = kGaccOff + kWaves * kCbStride;
 
 // Accumulator coordinates of A row rho of a block: register and lane half.
 __host__ __device__ constexpr int reg_of_row(int rho) { return (rho & 3) + 4 * (rho >> 3); }
@@ -985,25 +983,35 @@ __device__ __forceinline__ float sum8(float x) {
   return x;
 }
 
-// LDS float atomic at byte address base + IMM (no return).
-template <int IMM>
+// LDS float atomic at byte address base + IMM (no return) from the lanes of EXEC & {LO, HI}
+// only: the sum holders (lanes 8k + 7) -- the LDS then processes 8 lanes per instruction
+// instead of 64 -- without a branch (EXEC narrowed and restored inside the one asm
+// statement, so the MFMA/VALU interleave around it keeps one basic block).
+constexpr unsigned kHolders = 0x80808080u;
+template <int IMM, unsigned LO = kHolders, unsigned HI = kHolders>
 __device__ __forceinline__ void ds_add(unsigned base, float v) {
-  asm volatile("ds_add_f32 %0, %1 offset:%2" ::"v"(base), "v"(v), "i"(IMM));
+  const unsigned long long mask = (static_cast<unsigned long long>(HI) << 32) | LO;
+  unsigned long long saved;
+  // s_mov only (s_and_saveexec would clobber SCC behind the compiler's back); every call site runs
+  // with all 64 lanes active
+  asm volatile(
+      "s_mov_b64 %0, exec\n\t"
+      "s_mov_b64 exec, %3\n\t"
+      "ds_add_f32 %1, %2 offset:%4\n\t"
+      "s_mov_b64 exec, %0"
+      : "=&s"(saved)
+      : "v"(base), "v"(v), "s"(mask), "i"(IMM)
+      : "memory");
 }
 
-// Row R of block J (lane half h) is feature acc_row(J, R, h); its g_code column
-// sits at gbase + 4 * acc_row(J, R, 0) bytes (gbase carries the 4h and the
-// layer's column offset; lanes that hold no sum point at the dummy row).
-// Lanes that hold no sum carry gbase = kNoSum and stay out of the atomic (EXEC-masked: the LDS
-// then processes 8 lanes per instruction instead of 64).
-constexpr unsigned kNoSum = ~0u;
+// Row R of block J (lane half h) is feature acc_row(J, R, h); its g_code column sits at
+// gbase + 4 * acc_row(J, R, 0) bytes (gbase carries the 4h and the layer's column offset).
 template <int J, int R>
 __device__ __forceinline__ void red_add(unsigned gbase, float v) {
 #ifdef CN_ABLATE_NO_RED
   asm volatile("" ::"v"(v), "v"(gbase));
 #else
-  const float t = sum8(v);
-  if (gbase != kNoSum) ds_add<4 * acc_row(J, R, 0)>(gbase, t);
+  ds_add<4 * acc_row(J, R, 0)>(gbase, sum8(v));
 #endif
 }
 
@@ -1014,7 +1022,7 @@ __device__ __forceinline__ void save_piece(State& s, float vx, float vy) {
   if constexpr ((G & 1) == 0) {
     s.pend[0] = vx;
     s.pend[1] = vy;
-  } else if (s.sv) {
+  } else {
     *reinterpret_cast<float4*>(s.sv + 32 * J + 8 * (G / 2)) = make_float4(s.pend[0], s.pend[1], vx, vy);
   }
 }
@@ -1258,26 +1266,22 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
     cur_code = crow0;
   }
   int c = 0;
-#ifdef CN_RED_DUMMY
-  const unsigned dummy = lds_addr(blds + kDummyOff) + 4u * s.lane;
-#else
-  const unsigned dummy = kNoSum;
-#endif
   const unsigned gl = lds_addr(blds + kGaccOff + s.wave * kCbStride) + 16u * s.h;  // + 4h floats
-  const unsigned gbase = (s.lane & 7) == 7 ? gl : dummy;
-  const unsigned gbase0 = ((s.lane & 7) == 7 && s.h == 0) ? gl : dummy;
+  const unsigned gbase = gl;  // the atomics run on the holder lanes only (ds_add)
   // training: the dPre plane rows (the bias gradients are folded into the dW GEMMs)
-  auto plane = [&](int k) { return (TRAIN && valid) ? a.dpre + ((int64_t)k * a.m + row) * 256 + 4 * s.h : nullptr; };
+  // (padding lanes: the scratch row after the planes -- workspace the dW GEMMs overwrite later)
+  auto plane = [&](int k) {
+    return TRAIN ? (valid ? a.dpre + ((int64_t)k * a.m + row) * 256 : a.dpre + 5 * a.m * 256) + 4 * s.h : nullptr;
+  };
 
   // g_code sigma / rgb: this wave's samples (lane half 1 repeats them)
   {
     const float sw = sum8(dr.w), sx = sum8(dr.x), sy = sum8(dr.y), sz = sum8(dr.z);
-    if (gbase0 != kNoSum) {
-      ds_add<4 * kCbSigma>(gbase0, sw);
-      ds_add<4 * kCbRgb>(gbase0, sx);
-      ds_add<4 * (kCbRgb + 1)>(gbase0, sy);
-      ds_add<4 * (kCbRgb + 2)>(gbase0, sz);
-    }
+    // lane half 0's holders only (half 1 repeats the samples)
+    ds_add<4 * kCbSigma, kHolders, 0u>(gl, sw);
+    ds_add<4 * kCbRgb, kHolders, 0u>(gl, sx);
+    ds_add<4 * (kCbRgb + 1), kHolders, 0u>(gl, sy);
+    ds_add<4 * (kCbRgb + 2), kHolders, 0u>(gl, sz);
   }
   // B operands: d rgb at k-step 0 (lane half 0, k = channel) and the sigma init [dh, dl, dh]
   bf16x8 rh = {}, rl = {}, sig_b = {};
@@ -1316,7 +1320,7 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   const unsigned ones[4] = {~0u, ~0u, ~0u, ~0u};
   for (int l = 0; l < 2; ++l) {
     const unsigned* mw = l == 0 ? ones : mk[1];
-    const unsigned gb = gbase == kNoSum ? kNoSum : gbase + 4u * (l == 0 ? kCbFeat : kCbXyz2);
+    const unsigned gb = gbase + 4u * (l == 0 ? kCbFeat : kCbXyz2);
     s.sv = plane(2 + l);
     bwd_pass<true, true, TRAIN>(s, a, lds, c, blds, l == 0 ? kTSigmaCol : kTZeros, sig_b, mw, gb);
   }

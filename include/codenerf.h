@@ -333,7 +333,8 @@ int cn_radiance_field_train_w16(const float* packed, const float* code_bias, con
 /* The same pair for either precision: fmt CN_FMT_F32_W16 (fp32 16x16x4) or CN_FMT_BF16X3 (3xbf16
  * 32x32x16; masks cn_field_mask_words_fmt(CN_FMT_BF16X3, M) words, the same fp32 planes), and
  * fmt_t the matching transposed pack (CN_FMT_F32_W16_T / CN_FMT_BF16X3_T; the bf16x3 dW GEMMs
- * are 3xbf16 too).  bf16x3: one code row per 32-sample wave (n_codes == 1 or n_samples % 32 == 0). */
+ * are 3xbf16 too).  bf16x3: one code row per 32-sample wave (n_codes == 1 or n_samples % 32 == 0);
+ * its save buffer holds 5 * M * 256 + 256 floats (the last row is scratch for padding lanes). */
 int cn_radiance_field_train_fmt(int fmt, const float* packed, const float* code_bias, const int64_t* code_index,
                                 int64_t n_codes, const float* pts, const float* ro, const float* rd,
                                 const float* z, int64_t n_rays, int64_t n_samples, int64_t chunk_rows,
