@@ -651,14 +651,14 @@ __global__ __launch_bounds__(256) void gemm_tn_x3_kernel(const float* __restrict
 // X3: one 32x32x16 bf16 k-step per stage (3 products), else 8 fp32 32x32x2 row pairs.
 constexpr int kEncRows = 16;
 
+// Encoding column c of a sample whose point (ENC 0) or view direction (ENC 1) is x.
 template <int ENC>
-__device__ __forceinline__ float enc_value(const mlp::SampleIn& in, const mlp::FieldArgs& a, int c) {
+__device__ __forceinline__ float enc_value(const float* x, const mlp::FieldArgs& a, int c) {
   constexpr int K = ENC == 0 ? 63 : 27;
   if (c >= K) return 0.0f;
-  const float* v = ENC == 0 ? in.x : in.vd;
-  if (c < 3) return v[c];
+  if (c < 3) return x[c];
   const int b = (c - 3) / 3, comp = (c - 3) % 3;
-  const float arg = __fmul_rn(v[comp], ENC == 0 ? a.fx[b >> 1] : a.fd[b >> 1]);
+  const float arg = __fmul_rn(x[comp], ENC == 0 ? a.fx[b >> 1] : a.fd[b >> 1]);
   return (b & 1) ? cosf(arg) : sinf(arg);
 }
 
@@ -667,9 +667,10 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __rest
                                                              float* __restrict__ C, int64_t ldc,
                                                              float* __restrict__ part, float* __restrict__ bias_part,
                                                              int64_t rows_per_block) {
-  constexpr int K = ENC == 0 ? 63 : 27, KB = ENC == 0 ? 2 : 1, EW = 32 * KB;
+  constexpr int K = ENC == 0 ? 63 : 27, KB = ENC == 0 ? 2 : 1, EW = 32 * KB, CPT = EW / 32;
   __shared__ __attribute__((aligned(16))) float simg[2][kEncRows * 256];
   __shared__ __attribute__((aligned(16))) float senc[2][kEncRows * EW];
+  __shared__ __attribute__((aligned(16))) float4 xs[3][kEncRows];  // decoded geometry, 3 stages
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int i = lane & 31, h = lane >> 5;
@@ -677,41 +678,66 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __rest
   const int64_t mb = (int64_t)blockIdx.x * rows_per_block;
   const int64_t rows = min(rows_per_block, M - mb);
   const int n_stages = static_cast<int>((rows + kEncRows - 1) / kEncRows);
-  // staging roles: A rows (tid >> 6) and (tid >> 6) + 8, features 4 (tid & 63); encoding sample
-  // tid >> 5, columns ec, ec + 1 (threads past the table width idle)
+  // roles: A rows ar, ar + 8 (features ac..ac+3); encoding sample es, columns ec..ec+CPT-1; threads
+  // 0..15 decode the geometry of stage st + 2 (one sample each: the Q1 map's integer divisions
+  // run once per sample, not once per column)
   const int ar = tid >> 6, ac = 4 * (tid & 63);
-  const int es = tid >> 5, ec = 2 * (tid & 31);
+  const int es = tid >> 5, ec = CPT * (tid & 31);
   float4 av[2];
-  float ev[2];
-  auto load = [&](int st) {
+  float ev[CPT];
+  float4 xv = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto load_a = [&](int st) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int64_t r = (int64_t)st * kEncRows + ar + 8 * j;
       av[j] = r < rows ? *reinterpret_cast<const float4*>(A + (mb + r) * 256 + ac) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    const int64_t r = (int64_t)st * kEncRows + es;
-    ev[0] = ev[1] = 0.0f;
-    if (ec < EW && r < rows) {
+  };
+  auto decode = [&](int st) {
+    const int64_t r = (int64_t)st * kEncRows + tid;
+    if (tid < kEncRows && r < rows) {
       const mlp::SampleIn in = mlp::decode_sample<MODE>(a, mb + r);
-      ev[0] = enc_value<ENC>(in, a, ec);
-      ev[1] = enc_value<ENC>(in, a, ec + 1);
+      const float* v = ENC == 0 ? in.x : in.vd;
+      xv = make_float4(v[0], v[1], v[2], 0.0f);
     }
+  };
+  auto put_x = [&](int st) {
+    if (tid < kEncRows) xs[st % 3][tid] = xv;
+  };
+  auto enc_of = [&](int st) {  // rows past M: their A rows are zero, so any value is harmless
+    const float4 x4 = xs[st % 3][es];
+    const float x[3] = {x4.x, x4.y, x4.z};
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) ev[c] = enc_value<ENC>(x, a, ec + c);
   };
   auto store = [&](int buf) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) *reinterpret_cast<float4*>(&simg[buf][(ar + 8 * j) * 256 + ac]) = av[j];
-    if (ec < EW) *reinterpret_cast<float2*>(&senc[buf][es * EW + ec]) = make_float2(ev[0], ev[1]);
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) senc[buf][es * EW + ec + c] = ev[c];
   };
   floatx16 acc[KB];
 #pragma unroll
   for (int u = 0; u < KB; ++u) acc[u] = floatx16{0};
   float bsum = 0.0f;  // column sums of A (feature 32 wave + i) over this lane's rows
-  load(0);
+  decode(0);
+  put_x(0);
+  decode(1);
+  put_x(1);
+  __syncthreads();
+  load_a(0);
+  enc_of(0);
+  decode(2);
   store(0);
+  put_x(2);
   __syncthreads();
   for (int st = 0; st < n_stages; ++st) {
     const bool more = st + 1 < n_stages;
-    if (more) load(st + 1);
+    if (more) {
+      load_a(st + 1);
+      enc_of(st + 1);
+      decode(st + 3);
+    }
     const float* sa = simg[st & 1];
     const float* se = senc[st & 1];
     if constexpr (X3) {
@@ -739,7 +765,10 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __rest
           acc[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(x, se[(2 * p + h) * EW + 32 * u + i], acc[u], 0, 0, 0);
       }
     }
-    if (more) store((st + 1) & 1);
+    if (more) {
+      store((st + 1) & 1);
+      put_x(st + 3);
+    }
     __syncthreads();
   }
   float* pt = part ? part + (int64_t)blockIdx.x * 256 * K : nullptr;
