@@ -976,38 +976,46 @@ __global__ void copy_cols_kernel(const float* __restrict__ src, int64_t lds_, fl
 // fc_out / fc_rgb and the three code layers.  dW / db accumulate with atomics.  Rows
 // whose g is all zero (codes no sample used) only write their zero code gradient.
 constexpr int kCodeRowSplits = 16;
+constexpr int kCodeThreads = 1024;  // 16 waves: every reduction below is split 4 ways
 
-__global__ __launch_bounds__(256) void code_backward_kernel(mlp::Params P, const float* __restrict__ z_s,
-                                                            const float* __restrict__ z_t, const float* __restrict__ g,
-                                                            float* __restrict__ dz_s, float* __restrict__ dz_t,
-                                                            mlp::Params G) {
+__global__ __launch_bounds__(kCodeThreads) void code_backward_kernel(mlp::Params P, const float* __restrict__ z_s,
+                                                                     const float* __restrict__ z_t,
+                                                                     const float* __restrict__ g,
+                                                                     float* __restrict__ dz_s, float* __restrict__ dz_t,
+                                                                     mlp::Params G) {
   using namespace mlp;
   __shared__ float zs[256], zt[256], s1[256], s2[256], t1[256], ds1[256], ds2[256], dt1[256], go[257];
-  const int c = blockIdx.x, j = threadIdx.x;
+  __shared__ float gx2[256], grgb[3];
+  __shared__ float red[3][4][256];
+  const int c = blockIdx.x, tid = threadIdx.x, j = tid & 255, q = tid >> 8;
   const float* gr = g + (int64_t)c * kCbStride;
   // a code no sample used this step (most rows of a training table) has g = 0: zero code
   // gradients, no parameter contribution
-  const bool nz = gr[kCbXyz2 + j] != 0.0f || gr[kCbFeat + j] != 0.0f || (j < 8 && gr[kCbSigma + j] != 0.0f);
+  const bool nz = q == 0 && (gr[kCbXyz2 + j] != 0.0f || gr[kCbFeat + j] != 0.0f || (j < 8 && gr[kCbSigma + j] != 0.0f));
   const bool lead = blockIdx.y == 0;  // writes dz and the bias / single-row terms
   if (!__syncthreads_or(nz)) {
-    if (lead && dz_s) dz_s[(int64_t)c * 256 + j] = 0.0f;
-    if (lead && dz_t) dz_t[(int64_t)c * 256 + j] = 0.0f;
+    if (q == 0 && lead && dz_s) dz_s[(int64_t)c * 256 + j] = 0.0f;
+    if (q == 0 && lead && dz_t) dz_t[(int64_t)c * 256 + j] = 0.0f;
     return;
   }
-  zs[j] = z_s[(int64_t)c * 256 + j];
-  zt[j] = z_t[(int64_t)c * 256 + j];
-  go[1 + j] = gr[kCbFeat + j];
-  if (j == 0) go[0] = gr[kCbSigma];
+  if (q == 0) {
+    zs[j] = z_s[(int64_t)c * 256 + j];
+    zt[j] = z_t[(int64_t)c * 256 + j];
+    go[1 + j] = gr[kCbFeat + j];
+    gx2[j] = gr[kCbXyz2 + j];
+    if (j == 0) go[0] = gr[kCbSigma];
+    if (j < 3) grgb[j] = gr[kCbRgb + j];
+  }
   __syncthreads();
   {
-    // the three code layers (model.py:174-177) recomputed: wave w owns outputs 64 w .. 64 w + 63,
+    // the three code layers (model.py:174-177) recomputed: wave w owns outputs 16 w .. 16 w + 15,
     // one row at a time with its 64 lanes over k (coalesced 1 KiB rows) and a butterfly sum
-    const int lane = j & 63, w = j >> 6;
-    for (int o = 64 * w; o < 64 * w + 64; ++o) {
+    const int lane = tid & 63, w = tid >> 6;
+    for (int o = 16 * w; o < 16 * w + 16; ++o) {
       float a1 = 0.f, a2 = 0.f, a3 = 0.f;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int k = lane + 64 * q;
+      for (int u = 0; u < 4; ++u) {
+        const int k = lane + 64 * u;
         a1 = fmaf(P.p[kWSc1][o * 256 + k], zs[k], a1);
         a2 = fmaf(P.p[kWSc2][o * 256 + k], zs[k], a2);
         a3 = fmaf(P.p[kWTc1][o * 256 + k], zt[k], a3);
@@ -1025,47 +1033,59 @@ __global__ __launch_bounds__(256) void code_backward_kernel(mlp::Params P, const
       }
     }
   }
-  __syncthreads();
-  // d zs1 = W_xyz2[:, 256:]^T g_x2, d zs2 = W_out[:, 256:]^T g_o, d zt1 = W_rgb[:, 256:]^T g_rgb (masked)
+  // d zs1 = W_xyz2[:, 256:]^T g_x2, d zs2 = W_out[:, 256:]^T g_o, d zt1 = W_rgb[:, 256:]^T g_rgb:
+  // quarter q of the n range per thread, the quarters summed in order
   {
     float a1 = 0.f, a2 = 0.f, a3 = 0.f;
-    for (int n = 0; n < 256; ++n) a1 = fmaf(P.p[kWXyz2][n * 512 + 256 + j], gr[kCbXyz2 + n], a1);
-    for (int n = 0; n < 257; ++n) a2 = fmaf(P.p[kWOut][n * 512 + 256 + j], go[n], a2);
-    for (int n = 0; n < 3; ++n) a3 = fmaf(P.p[kWRgb][n * 512 + 256 + j], gr[kCbRgb + n], a3);
-    ds1[j] = s1[j] > 0.f ? a1 : 0.f;
-    ds2[j] = s2[j] > 0.f ? a2 : 0.f;
-    dt1[j] = t1[j] > 0.f ? a3 : 0.f;
+    for (int n = 64 * q; n < 64 * q + 64; ++n) {
+      a1 = fmaf(P.p[kWXyz2][n * 512 + 256 + j], gx2[n], a1);
+      a2 = fmaf(P.p[kWOut][n * 512 + 256 + j], go[n], a2);
+    }
+    if (q == 3) a2 = fmaf(P.p[kWOut][256 * 512 + 256 + j], go[256], a2);
+    if (q == 0)
+      for (int n = 0; n < 3; ++n) a3 = fmaf(P.p[kWRgb][n * 512 + 256 + j], grgb[n], a3);
+    red[0][q][j] = a1;
+    red[1][q][j] = a2;
+    red[2][q][j] = a3;
   }
   __syncthreads();
-  {
+  if (q == 0) {
+    const float a1 = (red[0][0][j] + red[0][1][j]) + (red[0][2][j] + red[0][3][j]);
+    const float a2 = (red[1][0][j] + red[1][1][j]) + (red[1][2][j] + red[1][3][j]);
+    ds1[j] = s1[j] > 0.f ? a1 : 0.f;
+    ds2[j] = s2[j] > 0.f ? a2 : 0.f;
+    dt1[j] = t1[j] > 0.f ? red[2][0][j] : 0.f;
+  }
+  __syncthreads();
+  if (lead && (dz_s || dz_t)) {
     float a = 0.f, b = 0.f;
-    for (int n = 0; n < 256; ++n) {
+    for (int n = 64 * q; n < 64 * q + 64; ++n) {
       a = fmaf(P.p[kWSc1][n * 256 + j], ds1[n], a);
       a = fmaf(P.p[kWSc2][n * 256 + j], ds2[n], a);
       b = fmaf(P.p[kWTc1][n * 256 + j], dt1[n], b);
     }
-    if (lead && dz_s) dz_s[(int64_t)c * 256 + j] = a;
-    if (lead && dz_t) dz_t[(int64_t)c * 256 + j] = b;
+    red[0][q][j] = a;
+    red[1][q][j] = b;
+  }
+  __syncthreads();
+  if (lead && q == 0) {
+    if (dz_s) dz_s[(int64_t)c * 256 + j] = (red[0][0][j] + red[0][1][j]) + (red[0][2][j] + red[0][3][j]);
+    if (dz_t) dz_t[(int64_t)c * 256 + j] = (red[1][0][j] + red[1][1][j]) + (red[1][2][j] + red[1][3][j]);
   }
   if (!G.p[kWSc1]) return;
-  // weight gradients of the code layers and the code halves: outer products, one row per
-  // iteration with thread j on column j (each wave's atomics hit 256 contiguous bytes)
-  __shared__ float gx2[256], grgb[3];
-  gx2[j] = gr[kCbXyz2 + j];
-  if (j < 3) grgb[j] = gr[kCbRgb + j];
-  __syncthreads();
+  // weight gradients of the code layers and the code halves: outer products over this block's
+  // rows (blockIdx.y of kCodeRowSplits; the per-code vectors above are recomputed by each, so the
+  // atomics spread over the chip), thread (q, j) on rows r0 + q + 4 t, column j
   const float zsj = zs[j], ztj = zt[j], s1j = s1[j], s2j = s2[j], t1j = t1[j];
-  // this block's rows of the outer products (blockIdx.y of kCodeRowSplits; the per-code vectors
-  // above are recomputed by each, so the atomics spread over the chip)
   const int r0 = blockIdx.y * (256 / kCodeRowSplits);
-  for (int r = r0; r < r0 + 256 / kCodeRowSplits; ++r) {
+  for (int r = r0 + q; r < r0 + 256 / kCodeRowSplits; r += 4) {
     atomicAdd(&const_cast<float*>(G.p[kWSc1])[r * 256 + j], ds1[r] * zsj);
     atomicAdd(&const_cast<float*>(G.p[kWSc2])[r * 256 + j], ds2[r] * zsj);
     atomicAdd(&const_cast<float*>(G.p[kWTc1])[r * 256 + j], dt1[r] * ztj);
     atomicAdd(&const_cast<float*>(G.p[kWXyz2])[r * 512 + 256 + j], gx2[r] * s1j);
     atomicAdd(&const_cast<float*>(G.p[kWOut])[(1 + r) * 512 + 256 + j], go[1 + r] * s2j);
   }
-  if (!lead) return;
+  if (!lead || q != 0) return;
   atomicAdd(&const_cast<float*>(G.p[kBSc1])[j], ds1[j]);
   atomicAdd(&const_cast<float*>(G.p[kBSc2])[j], ds2[j]);
   atomicAdd(&const_cast<float*>(G.p[kBTc1])[j], dt1[j]);
@@ -1495,7 +1515,7 @@ extern "C" int cn_code_bias_backward(const float* const* params, const float* z_
     G.p[i] = grads ? grads[i] : nullptr;
   }
   hipLaunchKernelGGL(grad::code_backward_kernel, dim3(static_cast<unsigned>(n_codes), grads ? grad::kCodeRowSplits : 1),
-                     dim3(256), 0, as_stream(stream), P, z_s, z_t, g_code, dz_s, dz_t, G);
+                     dim3(grad::kCodeThreads), 0, as_stream(stream), P, z_s, z_t, g_code, dz_s, dz_t, G);
   return launch_status();
 }
 
