@@ -127,12 +127,12 @@ __device__ __forceinline__ void flush_block(const floatx16& acc, float* C, int64
 
 // C[n][k] += sum_p part[p][n][k], p in order (one thread per element, 4 partial streams per
 // element combined in a fixed tree): the deterministic second pass of the split-M dW GEMMs.
-__global__ __launch_bounds__(256) void reduce_partials_kernel(const float* __restrict__ part, int64_t n_parts,
-                                                              int N, int K, float* __restrict__ C, int64_t ldc) {
-  __shared__ float red[4][64];
+// Block b of a job covers elements 64 b .. 64 b + 63.
+__device__ __forceinline__ void reduce_block(const float* __restrict__ part, int64_t n_parts, int N, int K,
+                                             float* __restrict__ C, int64_t ldc, int64_t b, float (&red)[4][64]) {
   const int q = threadIdx.x >> 6, t = threadIdx.x & 63;
   const int64_t nk = (int64_t)N * K;
-  const int64_t e = (int64_t)blockIdx.x * 64 + t;
+  const int64_t e = b * 64 + t;
   float s = 0.0f;
   if (e < nk) {
     const int64_t p0 = n_parts * q / 4, p1 = n_parts * (q + 1) / 4;
@@ -154,6 +154,33 @@ __global__ __launch_bounds__(256) void reduce_partials_kernel(const float* __res
     float* c = C + (e / K) * ldc + e % K;
     *c += v;
   }
+}
+
+__global__ __launch_bounds__(256) void reduce_partials_kernel(const float* __restrict__ part, int64_t n_parts,
+                                                              int N, int K, float* __restrict__ C, int64_t ldc) {
+  __shared__ float red[4][64];
+  reduce_block(part, n_parts, N, K, C, ldc, blockIdx.x, red);
+}
+
+// Several reductions in one launch (a backward's dW GEMMs queue theirs and flush once).
+struct ReduceJob {
+  const float* part;
+  float* C;
+  int64_t n_parts, ldc, first_block;
+  int N, K;
+};
+constexpr int kMaxReduceJobs = 16;
+struct ReduceJobs {
+  ReduceJob j[kMaxReduceJobs];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void reduce_jobs_kernel(ReduceJobs jobs) {
+  __shared__ float red[4][64];
+  int k = jobs.n - 1;
+  while (k > 0 && (int64_t)blockIdx.x < jobs.j[k].first_block) --k;
+  const ReduceJob& jb = jobs.j[k];
+  reduce_block(jb.part, jb.n_parts, jb.N, jb.K, jb.C, jb.ldc, (int64_t)blockIdx.x - jb.first_block, red);
 }
 
 // gemm_tn: C[n][k] += sum_m A[m][n] B[m][k] (dW = dPre^T X).  No LDS: on
@@ -1183,28 +1210,72 @@ TnPlan tn_plan(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t
 
 // ws (optional, tn_plan(..).parts * N * K floats): the deterministic two-pass reduction instead
 // of float atomics.
+// Deferred fixed-order reductions: with a Reducer, each dW kernel of a backward writes its partial
+// tiles into its own slice of the workspace (bump allocation from `cursor`) and queues the sum;
+// flush() runs every queued sum in ONE launch.  Without one, each sum runs right away.
+struct Reducer {
+  hipStream_t st;
+  float* cursor;
+  grad::ReduceJobs jobs;
+  int64_t blocks;
+  float* take(int64_t n) {
+    float* p = cursor;
+    cursor += ceil_div(n, 64) * 64;
+    return p;
+  }
+  int flush() {
+    if (jobs.n == 0) return CN_OK;
+    hipLaunchKernelGGL(grad::reduce_jobs_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, st, jobs);
+    jobs.n = 0;
+    blocks = 0;
+    return launch_status();
+  }
+};
+
+int reduce(Reducer* rd, const float* part, int64_t parts, int N, int K, float* C, int64_t ldc, hipStream_t st) {
+  const int64_t nblk = ceil_div((int64_t)N * K, 64);
+  if (!rd) {
+    hipLaunchKernelGGL(grad::reduce_partials_kernel, dim3(static_cast<unsigned>(nblk)), dim3(256), 0, st, part, parts,
+                       N, K, C, ldc);
+    return launch_status();
+  }
+  if (rd->jobs.n == grad::kMaxReduceJobs) {
+    const int rc = rd->flush();
+    if (rc != CN_OK) return rc;
+  }
+  rd->jobs.j[rd->jobs.n++] = grad::ReduceJob{part, C, parts, ldc, rd->blocks, N, K};
+  rd->blocks += nblk;
+  return CN_OK;
+}
+
 // Column sums of A (N <= 256) added to bias in a fixed order (bias_ws: ceil(M / rows) * N floats,
 // rows = max(256, M / 256)).
 int64_t colsum_rows(int64_t M) { return std::max<int64_t>(256, ceil_div(M, 256)); }
 
-int colsum(const float* A, int64_t lda, int64_t M, int N, float* bias, float* bias_ws, hipStream_t st) {
+int colsum(const float* A, int64_t lda, int64_t M, int N, float* bias, float* bias_ws, hipStream_t st,
+           Reducer* rd = nullptr) {
   const int64_t rows = colsum_rows(M);
   const unsigned nb = static_cast<unsigned>(ceil_div(M, rows));
+  if (rd) bias_ws = rd->take((int64_t)nb * N);
   hipLaunchKernelGGL(grad::colsum_kernel, dim3(nb), dim3(256), 0, st, A, lda, M, N, bias_ws, rows);
   const int rc = launch_status();
   if (rc != CN_OK) return rc;
-  hipLaunchKernelGGL(grad::reduce_partials_kernel, dim3(static_cast<unsigned>(ceil_div(N, 64))), dim3(256), 0, st,
-                     bias_ws, static_cast<int64_t>(nb), 1, N, bias, static_cast<int64_t>(N));
-  return launch_status();
+  return reduce(rd, bias_ws, nb, 1, N, bias, N, st);
 }
 
 // bias (optional, with bias_ws >= 1024 * N floats): also bias += A^T 1 (deterministic; folded into
 // the 3xbf16 whole-tile kernel, a separate column-sum pass otherwise).
+// rd: the deterministic path with deferred sums (ws / bias_ws are then taken from the reducer).
 int gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M, int N, int K,
-            hipStream_t st, bool x3 = false, float* ws = nullptr, float* bias = nullptr, float* bias_ws = nullptr) {
+            hipStream_t st, bool x3 = false, float* ws = nullptr, float* bias = nullptr, float* bias_ws = nullptr,
+            Reducer* rd = nullptr) {
   const TnPlan pl = tn_plan(A, lda, B, ldb, M, N, K, x3);
   const bool fold_bias = bias && pl.kind == kTn256X3;
   const unsigned nb = static_cast<unsigned>(ceil_div(M, pl.rows));
+  if (rd) {
+    ws = rd->take(pl.parts * N * K);
+    if (fold_bias) bias_ws = rd->take((int64_t)nb * N);
+  }
   switch (pl.kind) {
     case kTnSkinny:
       switch (N) {
@@ -1235,20 +1306,17 @@ int gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, 
       break;
     }
   }
+  int rc = launch_status();
+  if (rc != CN_OK) return rc;
   if (ws) {
-    const int rc = launch_status();
+    rc = reduce(rd, ws, pl.parts, N, K, C, ldc, st);
     if (rc != CN_OK) return rc;
-    hipLaunchKernelGGL(grad::reduce_partials_kernel, dim3(static_cast<unsigned>(ceil_div((int64_t)N * K, 64))), dim3(256),
-                       0, st, ws, pl.parts, N, K, C, ldc);
   }
   if (bias) {
-    const int rc = launch_status();
-    if (rc != CN_OK) return rc;
-    if (!fold_bias) return colsum(A, lda, M, N, bias, bias_ws, st);
-    hipLaunchKernelGGL(grad::reduce_partials_kernel, dim3(static_cast<unsigned>(ceil_div(N, 64))), dim3(256), 0, st,
-                       bias_ws, static_cast<int64_t>(nb), 1, N, bias, static_cast<int64_t>(N));
+    if (!fold_bias) return colsum(A, lda, M, N, bias, bias_ws, st, rd);
+    return reduce(rd, bias_ws, nb, 1, N, bias, N, st);
   }
-  return launch_status();
+  return CN_OK;
 }
 
 // Upper bound of the partial-tile workspace (floats) of gemm_tn(.., ws) for an M x N x K
@@ -1274,10 +1342,14 @@ int64_t enc_rows(int64_t M) {
 int64_t enc_parts(int64_t M) { return ceil_div(M, enc_rows(M)); }
 
 int gemm_tn_enc(int enc, const float* A, const mlp::FieldArgs& a, float* C, int64_t ldc, hipStream_t st, bool x3,
-                float* ws, float* bias = nullptr, float* bias_ws = nullptr) {
+                float* ws, float* bias = nullptr, float* bias_ws = nullptr, Reducer* rd = nullptr) {
   const int64_t rows = enc_rows(a.m);
   const unsigned nb = static_cast<unsigned>(ceil_div(a.m, rows));
   const int K = enc == 0 ? 63 : 27;
+  if (rd) {
+    ws = rd->take((int64_t)nb * 256 * K);
+    if (bias) bias_ws = rd->take((int64_t)nb * 256);
+  }
 #define CN_ENC(X3_, E_, M_) \
   hipLaunchKernelGGL((grad::gemm_tn_enc_kernel<X3_, E_, M_>), dim3(nb), dim3(512), 0, st, A, a, C, ldc, ws, \
                      bias ? bias_ws : nullptr, rows)
@@ -1290,19 +1362,14 @@ int gemm_tn_enc(int enc, const float* A, const mlp::FieldArgs& a, float* C, int6
     else { if (pts) CN_ENC(false, 1, mlp::kFromPts); else CN_ENC(false, 1, mlp::kFromRayZ); }
   }
 #undef CN_ENC
+  int rc = launch_status();
+  if (rc != CN_OK) return rc;
   if (ws) {
-    const int rc = launch_status();
+    rc = reduce(rd, ws, nb, 256, K, C, ldc, st);
     if (rc != CN_OK) return rc;
-    hipLaunchKernelGGL(grad::reduce_partials_kernel, dim3(static_cast<unsigned>(ceil_div(256 * K, 64))), dim3(256), 0,
-                       st, ws, static_cast<int64_t>(nb), 256, K, C, ldc);
   }
-  if (bias) {
-    const int rc = launch_status();
-    if (rc != CN_OK) return rc;
-    hipLaunchKernelGGL(grad::reduce_partials_kernel, dim3(4), dim3(256), 0, st, bias_ws, static_cast<int64_t>(nb), 1,
-                       256, bias, static_cast<int64_t>(256));
-  }
-  return launch_status();
+  if (bias) return reduce(rd, bias_ws, nb, 1, 256, bias, 256, st);
+  return CN_OK;
 }
 
 int seg_sum(const float* A, int64_t lda, int64_t M, int N, int64_t S, const int64_t* code_index, int64_t n_codes,
@@ -1546,18 +1613,16 @@ extern "C" int cn_ray_points_backward(const float* g_pts, const float* z, int64_
 // activations (cn_radiance_field_train_w16).
 // dPre planes, then the dW GEMMs' partial tiles (deterministic reduction, reused by each GEMM in
 // stream order).
+// Every dW GEMM of one backward keeps its partial tiles until the single deferred reduction:
+// the sum of their slices (+ three bias partial blocks and the 64-float alignment of each take).
 static int64_t train_dw_ws_floats(int64_t m) {
-  static const int kShapes[5][2] = {{3, 256}, {256, 256}, {256, 27}, {1, 256}, {256, 63}};
-  int64_t best = 0;
-  for (const auto& sh : kShapes) best = std::max(best, tn_ws_floats(m, sh[0], sh[1]));
-  return std::max(best, enc_parts(m) * 256 * 63);
+  return 4 * tn_ws_floats(m, 256, 256) + tn_ws_floats(m, 3, 256) + tn_ws_floats(m, 1, 256) +
+         std::max(tn_ws_floats(m, 256, 27), enc_parts(m) * 256 * 27) +
+         std::max(tn_ws_floats(m, 256, 63), enc_parts(m) * 256 * 63) + 3 * 1024 * 256 + 16 * 64;
 }
 
-// dPre planes | dW partial tiles | bias partial rows (3xbf16: folded into the dW kernels)
-constexpr int64_t kBiasWsFloats = 1024 * 256;
-
 extern "C" int64_t cn_field_backward_train_workspace_floats(int64_t m) {
-  return m > 0 ? 5 * m * 256 + train_dw_ws_floats(m) + kBiasWsFloats : -1;
+  return m > 0 ? 5 * m * 256 + train_dw_ws_floats(m) : -1;
 }
 
 extern "C" int cn_field_backward_train(const float* packed_t, const float* const* params, const uint32_t* masks,
@@ -1633,8 +1698,10 @@ extern "C" int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, con
   CN_TRY(launch_status());
   const float* P[5];
   for (int k = 0; k < 5; ++k) P[k] = workspace + k * M * 256;
-  float* ws = workspace + 5 * M * 256;
-  float* bws = ws + train_dw_ws_floats(M);
+  // partial tiles of every dW GEMM in their own slices, summed by ONE deferred launch
+  Reducer red{st, workspace + 5 * M * 256, {}, 0};
+  float* const ws = nullptr;
+  float* const bws = nullptr;
   auto B = [&](int i) { return x3 ? grads[i] : nullptr; };  // bias folded into this GEMM (3xbf16)
   const float* h1 = saved;
   const float* h2 = saved + M * 256;
@@ -1642,20 +1709,20 @@ extern "C" int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, con
   const float* v1 = saved + 3 * M * 256;
   const float* v2 = saved + 4 * M * 256;
   // fc_rgb (h half): dW += d rgb^T v2
-  CN_TRY(gemm_tn(d_raw, 4, v2, 256, G(kWRgb), 512, M, 3, 256, st, x3, ws));
+  CN_TRY(gemm_tn(d_raw, 4, v2, 256, G(kWRgb), 512, M, 3, 256, st, x3, ws, nullptr, nullptr, &red));
   // layer_dir2
-  CN_TRY(gemm_tn(P[0], 256, v1, 256, G(kWDir2), 256, M, 256, 256, st, x3, ws, B(kBDir2), bws));
+  CN_TRY(gemm_tn(P[0], 256, v1, 256, G(kWDir2), 256, M, 256, 256, st, x3, ws, B(kBDir2), bws, &red));
   // layer_dir1: [feat | dir enc]
-  CN_TRY(gemm_tn(P[1], 256, feat, 256, G(kWDir1), 283, M, 256, 256, st, x3, ws, B(kBDir1), bws));
-  if (x_enc) CN_TRY(gemm_tn(P[1], 256, x_enc + 63, 90, G(kWDir1) + 256, 283, M, 256, 27, st, x3, ws));
-  else CN_TRY(gemm_tn_enc(1, P[1], a, G(kWDir1) + 256, 283, st, x3, ws));
+  CN_TRY(gemm_tn(P[1], 256, feat, 256, G(kWDir1), 283, M, 256, 256, st, x3, ws, B(kBDir1), bws, &red));
+  if (x_enc) CN_TRY(gemm_tn(P[1], 256, x_enc + 63, 90, G(kWDir1) + 256, 283, M, 256, 27, st, x3, ws, nullptr, nullptr, &red));
+  else CN_TRY(gemm_tn_enc(1, P[1], a, G(kWDir1) + 256, 283, st, x3, ws, nullptr, nullptr, &red));
   // fc_out (h half): row 0 from d sigma, rows 1.. from d feat
-  CN_TRY(gemm_tn(d_raw + 3, 4, h2, 256, G(kWOut), 512, M, 1, 256, st, x3, ws));
-  CN_TRY(gemm_tn(P[2], 256, h2, 256, G(kWOut) + 512, 512, M, 256, 256, st, x3, ws));
+  CN_TRY(gemm_tn(d_raw + 3, 4, h2, 256, G(kWOut), 512, M, 1, 256, st, x3, ws, nullptr, nullptr, &red));
+  CN_TRY(gemm_tn(P[2], 256, h2, 256, G(kWOut) + 512, 512, M, 256, 256, st, x3, ws, nullptr, nullptr, &red));
   // layer_xyz2 (h half)
-  CN_TRY(gemm_tn(P[3], 256, h1, 256, G(kWXyz2), 512, M, 256, 256, st, x3, ws));
+  CN_TRY(gemm_tn(P[3], 256, h1, 256, G(kWXyz2), 512, M, 256, 256, st, x3, ws, nullptr, nullptr, &red));
   // layer_xyz1
-  if (x_enc) CN_TRY(gemm_tn(P[4], 256, x_enc, 90, G(kWXyz1), 63, M, 256, 63, st, x3, ws, B(kBXyz1), bws));
-  else CN_TRY(gemm_tn_enc(0, P[4], a, G(kWXyz1), 63, st, x3, ws, B(kBXyz1), bws));
-  return CN_OK;
+  if (x_enc) CN_TRY(gemm_tn(P[4], 256, x_enc, 90, G(kWXyz1), 63, M, 256, 63, st, x3, ws, B(kBXyz1), bws, &red));
+  else CN_TRY(gemm_tn_enc(0, P[4], a, G(kWXyz1), 63, st, x3, ws, B(kBXyz1), bws, &red));
+  return red.flush();
 }
