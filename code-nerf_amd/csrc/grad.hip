@@ -248,7 +248,7 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(const float* __restrict__ 
 // The slab's partial tile is flushed with one float atomic per element, or stored to the
 // workspace for the deterministic reduction.  X3: the same stream with 3xbf16 MFMAs (x3_stage).
 constexpr int kTwRows = 16;                    // rows of A and of B per stage
-constexpr int kTwStage = 2 * kTwRows * 256;    // floats per stage (A rows, then B rows)
+constexpr int kTwStage = 2 * kTwRows * 256 + 64;  // floats per stage: A rows, B rows, SIG: 16 d raw rows
 constexpr int kTwRing = 4;
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -296,8 +296,11 @@ __device__ __forceinline__ float sum8v(const float* v) {
 }
 
 // bsum[t]: running column sums of A's block t over this lane's rows (the bias gradient dPre^T 1).
+// SIG (fc_out: its sigma row d sigma^T h2 rides on the h2 stream): sacc[u] += sum over this lane's
+// rows of d sigma x B (the stage's d raw rows sit after the B rows).
+template <bool SIG>
 __device__ __forceinline__ void x3_stage(const float* slot, int i, int h, int n0, int k0, floatx16 (&acc)[2][4],
-                                         float (&bsum)[2]) {
+                                         float (&bsum)[2], float (&sacc)[4], bool sig_wave) {
   const float* sa = slot + 8 * h * 256 + i;
   const float* sb = sa + kTwRows * 256;
   u32x4 ah[2], al[2];
@@ -309,11 +312,23 @@ __device__ __forceinline__ void x3_stage(const float* slot, int i, int h, int n0
     bsum[t] += sum8v(v);
     split8(v, ah[t], al[t]);
   }
+  float ds[8];
+  if constexpr (SIG) {
+    const float* sr = slot + 2 * kTwRows * 256 + 8 * h * 4 + 3;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ds[j] = sr[4 * j];
+  }
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     float v[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = sb[j * 256 + k0 + 32 * u];
+    if constexpr (SIG) {
+      if (sig_wave) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sacc[u] = fmaf(ds[j], v[j], sacc[u]);
+      }
+    }
     u32x4 bh, bl;
     split8(v, bh, bl);
 #pragma unroll
@@ -321,10 +336,11 @@ __device__ __forceinline__ void x3_stage(const float* slot, int i, int h, int n0
   }
 }
 
-template <bool X3>
+template <bool X3, bool SIG>
 __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restrict__ A, const float* __restrict__ B,
                                                             float* __restrict__ C, int64_t ldc, float* __restrict__ part,
-                                                            float* __restrict__ bias_part, int64_t M,
+                                                            float* __restrict__ bias_part, const float* __restrict__ draw,
+                                                            float* __restrict__ sig_part, int64_t M,
                                                             int64_t rows_per_block) {
   __shared__ __attribute__((aligned(16))) float ring[kTwRing * kTwStage];
   const int lane = threadIdx.x & 63;
@@ -338,9 +354,12 @@ __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restr
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(A + mb * 256), 0, bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rb =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(B + mb * 256), 0, bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(SIG ? draw + mb * 4 : A), 0, static_cast<unsigned>(SIG ? rows * 16 : 0), 0x00020000);
   const int n_stages = static_cast<int>((rows + kTwRows - 1) / kTwRows);
   // stage st: wave w moves rows w + 8 j of A and of B (j < kTwRows / 8), one 16-B-per-lane
-  // wave-instruction per 1 KiB row: kTwRows / 4 wave-instructions per stage
+  // wave-instruction per 1 KiB row: kTwRows / 4 wave-instructions per stage; SIG: every wave also
+  // moves the stage's 16 d raw rows (256 B, the same bytes: the per-wave vmcnt stays uniform)
   auto dma = [&](int st) {
     float* slot = ring + (st & (kTwRing - 1)) * kTwStage;
 #pragma unroll
@@ -350,7 +369,13 @@ __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restr
       __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(slot + r * 256), 16, lane * 16u, soff, 0, 0);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr_t)(slot + (kTwRows + r) * 256), 16, lane * 16u, soff, 0, 0);
     }
+    if constexpr (SIG) {
+      const unsigned soff = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(st * kTwRows * 16));
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(slot + 2 * kTwRows * 256), 4, lane * 4u, soff, 0, 0);
+    }
   };
+  const bool sig_wave = (wave >> 1) == 0;  // waves 0, 1: columns 0..127, 128..255 of the sigma row
+  float sacc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   floatx16 acc[2][4];
 #pragma unroll
   for (int t = 0; t < 2; ++t)
@@ -364,11 +389,12 @@ __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restr
     // stage st landed (all but this wave's 2 kTwRows youngest pieces: stages st+1, st+2) and
     // every wave is done with stage st-1, whose slot then receives stage st+3
     static_assert(kTwRows / 2 == 8, "the vmcnt below counts stages st+1, st+2");
-    asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+    if constexpr (SIG) asm volatile("s_waitcnt vmcnt(10)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     dma(st + 3);
     if constexpr (X3) {
-      x3_stage(ring + (st & (kTwRing - 1)) * kTwStage, i, h, n0, k0, acc, bsum);
+      x3_stage<SIG>(ring + (st & (kTwRing - 1)) * kTwStage, i, h, n0, k0, acc, bsum, sacc, sig_wave);
       continue;
     }
     const float* sa = ring + (st & (kTwRing - 1)) * kTwStage + h * 256 + i;
@@ -393,6 +419,13 @@ __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restr
 #pragma unroll
         for (int u = 0; u < 4; ++u)
           acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[c][t], b[c][u], acc[t][u], 0, 0, 0);
+      if constexpr (SIG) {
+        if (sig_wave) {
+          const float dsg = sb[kTwRows * 256 - (h * 256 + i) + (2 * p + h) * 4 + 3];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) sacc[u] = fmaf(dsg, b[c][u], sacc[u]);
+        }
+      }
     }
   }
   // the prefetched stages past the slab must land before the workgroup's LDS is released
@@ -408,6 +441,13 @@ __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restr
     for (int t = 0; t < 2; ++t) {
       const float b = bsum[t] + __shfl_xor(bsum[t], 32);
       if (h == 0) bias_part[(int64_t)blockIdx.x * 256 + n0 + 32 * t + i] = b;
+    }
+  }
+  if (SIG && sig_wave) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float v = sacc[u] + __shfl_xor(sacc[u], 32);
+      if (h == 0) sig_part[(int64_t)blockIdx.x * 256 + k0 + 32 * u + i] = v;
     }
   }
 }
@@ -1266,15 +1306,21 @@ int colsum(const float* A, int64_t lda, int64_t M, int N, float* bias, float* bi
 // bias (optional, with bias_ws >= 1024 * N floats): also bias += A^T 1 (deterministic; folded into
 // the 3xbf16 whole-tile kernel, a separate column-sum pass otherwise).
 // rd: the deterministic path with deferred sums (ws / bias_ws are then taken from the reducer).
+// sig / sig_out (optional, with rd; B 256 wide): also sig_out[0..255] += sum_m sig[4 m] B[m][:] -- fc_out's
+// sigma row; sig is column 3 of the (M, 4) d raw rows, which the whole-tile kernels stream whole
+// (draw = sig - 3) beside B -- a skinny pass otherwise.
 int gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M, int N, int K,
             hipStream_t st, bool x3 = false, float* ws = nullptr, float* bias = nullptr, float* bias_ws = nullptr,
-            Reducer* rd = nullptr) {
+            Reducer* rd = nullptr, const float* sig = nullptr, float* sig_out = nullptr) {
   const TnPlan pl = tn_plan(A, lda, B, ldb, M, N, K, x3);
   const bool fold_bias = bias && pl.kind == kTn256X3;
+  const bool fold_sig = sig && rd && (pl.kind == kTn256 || pl.kind == kTn256X3);
   const unsigned nb = static_cast<unsigned>(ceil_div(M, pl.rows));
+  float* sig_ws = nullptr;
   if (rd) {
     ws = rd->take(pl.parts * N * K);
     if (fold_bias) bias_ws = rd->take((int64_t)nb * N);
+    if (fold_sig) sig_ws = rd->take((int64_t)nb * 256);
   }
   switch (pl.kind) {
     case kTnSkinny:
@@ -1286,12 +1332,20 @@ int gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, 
       }
       break;
     case kTn256:
-      hipLaunchKernelGGL(grad::gemm_tn256_kernel<false>, dim3(nb), dim3(512), 0, st, A, B, C, ldc, ws, nullptr, M,
-                         pl.rows);
+      if (fold_sig)
+        hipLaunchKernelGGL((grad::gemm_tn256_kernel<false, true>), dim3(nb), dim3(512), 0, st, A, B, C, ldc, ws,
+                           nullptr, sig - 3, sig_ws, M, pl.rows);
+      else
+        hipLaunchKernelGGL((grad::gemm_tn256_kernel<false, false>), dim3(nb), dim3(512), 0, st, A, B, C, ldc, ws,
+                           nullptr, nullptr, nullptr, M, pl.rows);
       break;
     case kTn256X3:
-      hipLaunchKernelGGL(grad::gemm_tn256_kernel<true>, dim3(nb), dim3(512), 0, st, A, B, C, ldc, ws,
-                         fold_bias ? bias_ws : nullptr, M, pl.rows);
+      if (fold_sig)
+        hipLaunchKernelGGL((grad::gemm_tn256_kernel<true, true>), dim3(nb), dim3(512), 0, st, A, B, C, ldc, ws,
+                           fold_bias ? bias_ws : nullptr, sig - 3, sig_ws, M, pl.rows);
+      else
+        hipLaunchKernelGGL((grad::gemm_tn256_kernel<true, false>), dim3(nb), dim3(512), 0, st, A, B, C, ldc, ws,
+                           fold_bias ? bias_ws : nullptr, nullptr, nullptr, M, pl.rows);
       break;
     case kTnGenericX3: {
       const int64_t tiles = ceil_div(N, grad::kTnTile) * ceil_div(K, grad::kTnTile);
@@ -1310,6 +1364,11 @@ int gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, 
   if (rc != CN_OK) return rc;
   if (ws) {
     rc = reduce(rd, ws, pl.parts, N, K, C, ldc, st);
+    if (rc != CN_OK) return rc;
+  }
+  if (sig) {
+    rc = fold_sig ? reduce(rd, sig_ws, nb, 1, 256, sig_out, 256, st)
+                  : gemm_tn(sig, 4, B, ldb, sig_out, 256, M, 1, 256, st, x3, nullptr, nullptr, nullptr, rd);
     if (rc != CN_OK) return rc;
   }
   if (bias) {
@@ -1717,8 +1776,8 @@ extern "C" int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, con
   if (x_enc) CN_TRY(gemm_tn(P[1], 256, x_enc + 63, 90, G(kWDir1) + 256, 283, M, 256, 27, st, x3, ws, nullptr, nullptr, &red));
   else CN_TRY(gemm_tn_enc(1, P[1], a, G(kWDir1) + 256, 283, st, x3, ws, nullptr, nullptr, &red));
   // fc_out (h half): row 0 from d sigma, rows 1.. from d feat
-  CN_TRY(gemm_tn(d_raw + 3, 4, h2, 256, G(kWOut), 512, M, 1, 256, st, x3, ws, nullptr, nullptr, &red));
-  CN_TRY(gemm_tn(P[2], 256, h2, 256, G(kWOut) + 512, 512, M, 256, 256, st, x3, ws, nullptr, nullptr, &red));
+  CN_TRY(gemm_tn(P[2], 256, h2, 256, G(kWOut) + 512, 512, M, 256, 256, st, x3, ws, nullptr, nullptr, &red, d_raw + 3,
+                 G(kWOut)));
   // layer_xyz2 (h half)
   CN_TRY(gemm_tn(P[3], 256, h1, 256, G(kWXyz2), 512, M, 256, 256, st, x3, ws, nullptr, nullptr, &red));
   // layer_xyz1

@@ -586,3 +586,33 @@ def test_field_backward_train_generated_encodings(dev, mode, precision):
             close(a, b.double(), 1e-5, f"bias {k}")
         if k in weights:
             assert torch.equal(a, out["generated2"][k]), f"param {k}: not reproducible"
+
+
+@pytest.mark.parametrize("precision", ["f32", "bf16x3"])
+def test_field_backward_train_sigma_rgb_rows(dev, precision):
+    """At M >= 65536 the fused training backward folds fc_out's sigma row (d sigma^T h2) into the
+    whole-tile dW kernel's h2 stream; with fc_rgb's rows (d rgb^T v2) it is checked against fp64
+    products of the forward's own saved planes and the d raw it was given (no oracle needed:
+    the planes are the exact operands)."""
+    from codenerf import ops, synthetic
+    m = model(dev, 0)
+    params = [p.detach() for p in m.param_list()]
+    r, s = 1100, 64                              # M = 70400
+    g = torch.Generator().manual_seed(9)
+    ro = (torch.randn(r, 3, generator=g) * 0.3 + torch.tensor([0.0, 0.0, 1.3])).to(dev)
+    rd = torch.randn(r, 3, generator=g).to(dev)
+    z = torch.sort(0.8 + torch.rand(r, s, generator=g), dim=-1).values.to(dev)
+    gout = torch.randn(r, s, 4, generator=g).to(dev)
+    zs, zt = synthetic.latent_codes(5, 1).to(dev), synthetic.latent_codes(6, 1).to(dev)
+    fx, fd = [2.0 ** k for k in range(10)], [2.0 ** k for k in range(4)]
+    cb = ops.code_bias(params, zs, zt)
+    x3 = precision == "bf16x3"
+    _, saved, masks = ops.radiance_field_train_w16(ops.mlp_pack(params, "bf16x3" if x3 else "f32_w16"), cb, rd, s,
+                                                   4096, fx, fd, ro=ro, z=z, precision=precision)
+    pg = [torch.zeros_like(p) for p in params]
+    ops.field_backward_train(ops.mlp_pack(params, "bf16x3_t" if x3 else "f32_w16_t"), params, masks, saved, None,
+                             gout, r, s, 4096, 1, fx, fd, rd=rd, ro=ro, z=z, param_grads=pg, precision=precision)
+    d = gout.reshape(-1, 4).double().cpu()
+    h2, v2 = saved[1].double().cpu(), saved[4].double().cpu()
+    close(pg[4][0, :256], d[:, 3] @ h2, 1e-5, "fc_out sigma row")      # kWOut = 4
+    close(pg[16][:, :256], d[:, :3].t() @ v2, 1e-5, "fc_rgb rows")     # kWRgb = 16
