@@ -78,9 +78,9 @@ def parse_args(argv=None):
     ap.add_argument("--no-extras", action="store_true", help="headline + bf16x3 only (profiling runs)")
     ap.add_argument("--precision", default="f32", choices=sorted(KERNELS),
                     help="headline field-kernel arithmetic (f32 = the reference's precision)")
-    ap.add_argument("--eval-iters", type=int, default=10,
+    ap.add_argument("--eval-iters", type=int, default=40,
                     help="C5: time this many test-time-optimisation iterations (0 = skip)")
-    ap.add_argument("--train-iters", type=int, default=3,
+    ap.add_argument("--train-iters", type=int, default=8,
                     help="C3 training: time this many train.py iterations (4 x 4096 rays each; 0 = skip)")
     return ap.parse_args(argv)
 
