@@ -331,8 +331,9 @@ def eval_bench(dev, rs, emb, models, iters, precision):
     perturbed samples, forward + backward through the HIP kernels into (codes, theta, phi, rho),
     AdamW step.  Weights frozen (their grads are never read by the reference's optimiser)."""
     import numpy as np
-    from codenerf.evaluate import eval_step_loss
+    from codenerf.evaluate import eval_step_loss, step_psnr
     from codenerf.nerf import PointSampler
+    from codenerf.optim import AdamW
     ps = PointSampler(NC, NF, NEAR, FAR, "lindepth", True, torch.float32, dev)
     rs.sample_size = 2048
     target = torch.rand(H * W, 4, generator=torch.Generator().manual_seed(3)).to(dev)
@@ -346,14 +347,16 @@ def eval_bench(dev, rs, emb, models, iters, precision):
     th = torch.tensor([1.57], device=dev).requires_grad_(True)
     ph = torch.tensor([0.0], device=dev).requires_grad_(True)
     rh = torch.tensor([1.3], device=dev).requires_grad_(True)
-    opt = torch.optim.AdamW([{"params": [zs, zt]}, {"params": [th, ph]}, {"params": [rh]}], lr=1e-2)
+    # test_time_optimize's optimiser for val_type AdamW: the flat one-launch AdamW
+    opt = AdamW([{"params": [zs, zt]}, {"params": [th, ph]}, {"params": [rh]}], lr=1e-2)
     np.random.seed(0)
 
     def it():
-        loss, _ = eval_step_loss(th, ph, rh, zs, zt, target, (rs, ps), emb, mods, 1e-5)
+        loss, logs = eval_step_loss(th, ph, rh, zs, zt, target, (rs, ps), emb, mods, 1e-5)
         opt.zero_grad()
         loss.backward()
         opt.step()
+        step_psnr(logs)  # eval.py:159's per-iteration read-back, after the step is enqueued
 
     for _ in range(2):
         it()

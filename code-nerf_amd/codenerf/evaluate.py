@@ -56,12 +56,16 @@ def eval_step_loss(theta, phi, rho, shape_code, texture_code, target_pixels, sam
     rgb_c, rgb_f = out["rgb_coarse"], out["rgb_fine"]
     # mse(coarse) + mse(fine) + lambda (||z_s|| + ||z_t||), the codes expanded over the n rays
     loss, stats = nerf_loss(rgb_c, rgb_f, tp, shape_code, texture_code, n, regularizer_lambda)
-    logs = {"nerf_loss_coarse": stats[0], "nerf_loss_fine": stats[1], "embedding_loss": stats[2],
-            "psnr": mse2psnr(stats[1].item())}
+    logs = {"nerf_loss_coarse": stats[0], "nerf_loss_fine": stats[1], "embedding_loss": stats[2]}
     if gt_pose is not None:
         logs["pose_error"] = ops.pose_error(gt_pose.reshape(1, 4, 4), cam_pose)[1][0]
     logs["cam_pose"] = cam_pose
     return loss, logs
+
+
+def step_psnr(logs: Dict[str, object]) -> float:
+    """eval.py:159: psnr of the fine MSE (mse2psnr, util.py:216-227); one read-back."""
+    return mse2psnr(logs["nerf_loss_fine"].item())
 
 
 def nerf_loss(rgb_c, rgb_f, target, shape_code, texture_code, expand: int, regularizer_lambda: float):
@@ -119,6 +123,7 @@ def test_time_optimize(target_pixels: torch.Tensor, samplers, embedders, models,
             opt.zero_grad()
             loss.backward()
             opt.step()
+            logs["psnr"] = step_psnr(logs)
             logs["total_loss"] = loss.detach()
             history.append(logs)
             if log_every and ((it != 0 and it % log_every == 0) or it == iterations - 1):

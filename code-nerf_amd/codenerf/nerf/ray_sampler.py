@@ -53,7 +53,10 @@ class RaySampler(object):
             return None, sel
         pixel_range = np.arange(0, n)
         select_inds = np.asarray([np.random.permutation(pixel_range)[: self.sample_size] for _ in range(batch)])
-        sel = torch.from_numpy(select_inds.astype(np.int64)).to(self.device, non_blocking=True)
+        sel = torch.from_numpy(select_inds.astype(np.int64))
+        if self.device.type == "cuda":  # pinned: the copy is enqueued, not a host-side wait on the stream
+            sel = sel.pin_memory()
+        sel = sel.to(self.device, non_blocking=True)
         return select_inds, sel
 
     def sample(self, tform_cam2world: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor, np.ndarray]:
