@@ -52,8 +52,10 @@ KERNELS = {"f32": ("field_w16_kernel<kFromRayZ> (fused posenc + CodeNeRF MLP, fp
                     "2 waves/SIMD)", 1, PEAK_FP32_MFMA_TFLOPS),
            "f32_v1": ("field_kernel<kFromRayZ> (fused posenc + CodeNeRF MLP, fp32 v_mfma_f32_32x32x2_f32, "
                       "1 wave/SIMD)", 1, PEAK_FP32_MFMA_TFLOPS),
-           "bf16x3": ("field_x3_kernel<kFromRayZ> (fused posenc + CodeNeRF MLP, 3xbf16 MFMA)", 3,
-                      PEAK_BF16_MFMA_TFLOPS)}
+           "bf16x3": ("field_x3_kernel<kFromRayZ> (fused posenc + CodeNeRF MLP, 3xbf16 32x32x16 MFMA, "
+                      "1 wave/SIMD)", 3, PEAK_BF16_MFMA_TFLOPS),
+           "bf16x3_w16": ("field_x3w_kernel<kFromRayZ> (fused posenc + CodeNeRF MLP, 3xbf16 16x16x32 MFMA, "
+                          "2 waves/SIMD)", 3, PEAK_BF16_MFMA_TFLOPS)}
 
 
 def pose(theta, phi, rho):

@@ -18,9 +18,9 @@ LIB_PATH = os.environ.get("CODENERF_LIB", os.path.join(_HERE, "lib", "libcodener
 
 CN_OK, CN_EINVAL, CN_EUNSUPPORTED = 0, -1, -2
 CN_NUM_PARAMS = 18
-CN_FMT_F32, CN_FMT_BF16X3, CN_FMT_BF16X3_T, CN_FMT_F32_W16, CN_FMT_F32_W16_T = 0, 1, 2, 3, 4
+CN_FMT_F32, CN_FMT_BF16X3, CN_FMT_BF16X3_T, CN_FMT_F32_W16, CN_FMT_F32_W16_T, CN_FMT_BF16X3_W16 = 0, 1, 2, 3, 4, 5
 FORMATS = {"f32": CN_FMT_F32, "bf16x3": CN_FMT_BF16X3, "bf16x3_t": CN_FMT_BF16X3_T, "f32_w16": CN_FMT_F32_W16,
-           "f32_w16_t": CN_FMT_F32_W16_T}
+           "f32_w16_t": CN_FMT_F32_W16_T, "bf16x3_w16": CN_FMT_BF16X3_W16}
 
 
 def kernel_format(precision: str) -> str:

@@ -422,6 +422,7 @@ int make_params(const float* const* params, Params* P) {
 int launch_field(int fmt, int mode, FieldArgs& a, hipStream_t st) {
   if (fmt == CN_FMT_BF16X3) return launch_field_x3(mode, a, st);
   if (fmt == CN_FMT_F32_W16) return launch_field_w16(mode, a, st);
+  if (fmt == CN_FMT_BF16X3_W16) return launch_field_x3w(mode, a, st);
   const unsigned grid = static_cast<unsigned>(cn::ceil_div(a.m, kTile));
   switch (mode) {
     case kFromPts: hipLaunchKernelGGL(field_kernel<kFromPts>, dim3(grid), dim3(kThreads), 0, st, a); break;
@@ -431,7 +432,9 @@ int launch_field(int fmt, int mode, FieldArgs& a, hipStream_t st) {
   return cn::launch_status();
 }
 
-bool valid_fmt(int fmt) { return fmt == CN_FMT_F32 || fmt == CN_FMT_BF16X3 || fmt == CN_FMT_F32_W16; }
+bool valid_fmt(int fmt) {
+  return fmt == CN_FMT_F32 || fmt == CN_FMT_BF16X3 || fmt == CN_FMT_F32_W16 || fmt == CN_FMT_BF16X3_W16;
+}
 bool valid_pack_fmt(int fmt) { return valid_fmt(fmt) || fmt == CN_FMT_BF16X3_T || fmt == CN_FMT_F32_W16_T; }
 
 }  // namespace
@@ -442,6 +445,7 @@ static_assert(kCbStride == CN_CODE_BIAS_STRIDE, "code-bias stride mismatch");
 extern "C" int64_t cn_mlp_packed_floats(int fmt) {
   if (!valid_pack_fmt(fmt)) return -1;
   if (fmt == CN_FMT_F32_W16 || fmt == CN_FMT_F32_W16_T) return packed_floats_w16();
+  if (fmt == CN_FMT_BF16X3_W16) return packed_floats_x3w();
   return fmt == CN_FMT_F32 ? kPackedFloats : packed_floats_x3();
 }
 
@@ -452,6 +456,7 @@ extern "C" int cn_mlp_pack(const float* const* params, int fmt, float* packed, c
   if (fmt == CN_FMT_BF16X3_T) return launch_pack_x3t(P, packed, cn::as_stream(stream));
   if (fmt == CN_FMT_F32_W16) return launch_pack_w16(P, packed, cn::as_stream(stream));
   if (fmt == CN_FMT_F32_W16_T) return launch_pack_w16t(P, packed, cn::as_stream(stream));
+  if (fmt == CN_FMT_BF16X3_W16) return launch_pack_x3w(P, packed, cn::as_stream(stream));
   hipLaunchKernelGGL(pack_kernel, dim3(cn::elementwise_grid(kPackedFloats, 256)), dim3(256), 0,
                      cn::as_stream(stream), P, packed);
   return cn::launch_status();

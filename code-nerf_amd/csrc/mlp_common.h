@@ -131,6 +131,11 @@ int64_t mask_words_w16(int64_t m);
 int launch_pack_w16t(const Params& P, float* packed, hipStream_t st);
 int launch_field_w16_bwd(int mode, FieldArgs& a, hipStream_t st);
 
+// 3xbf16 16x16x32 two-waves-per-SIMD variant (mlp_x3w.hip): inference forward only.
+int64_t packed_floats_x3w();
+int launch_pack_x3w(const Params& P, float* packed, hipStream_t st);
+int launch_field_x3w(int mode, FieldArgs& a, hipStream_t st);
+
 // Pre-encoded rows: the same 2P+2 values gathered from x (base = column offset).
 template <int P, int T = 0>
 __device__ __forceinline__ void gather_pairs(const float* xr, int base, int h, float* out) {

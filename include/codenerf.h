@@ -60,6 +60,11 @@ typedef void* cn_stream_t; /* hipStream_t */
 /*   CN_FMT_F32_W16_T the transposed fp32 pack the fused fp32 backward streams
  *                    (cn_field_backward_fused); not a forward format. */
 #define CN_FMT_F32_W16_T 4
+/*   CN_FMT_BF16X3_W16 the same 3-product bf16 split as CN_FMT_BF16X3 on
+ *                    v_mfma_f32_16x16x32_bf16 at two waves per SIMD (16 samples per wave;
+ *                    cn_mlp_forward / cn_radiance_field only -- the mask-writing forward and
+ *                    the fused backward take CN_FMT_BF16X3 / _T). */
+#define CN_FMT_BF16X3_W16 5
 
 const char* cn_version(void);
 const char* cn_error_string(int code);

@@ -47,6 +47,7 @@ def test_ctypes_table_matches_header(lib_path):
     assert lib.cn_version().decode().startswith("libcodenerf_hip")
     assert lib.cn_mlp_packed_floats(0) == 327424 and lib.cn_mlp_packed_floats(1) == 295936
     assert lib.cn_mlp_packed_floats(3) == 36 * 8192 + 1024
+    assert lib.cn_mlp_packed_floats(5) == 36 * 8192 + 1024   # bf16x3_w16: the same 1.15 MB stream as hi/lo bf16
     assert lib.cn_error_string(-1).decode().startswith("invalid argument")
 
 

@@ -17,7 +17,11 @@ pytestmark = pytest.mark.gpu
 
 TOL_RENDER = 1e-4
 RAW_RTOL = 1e-5
-PRECISIONS = ["f32", "f32_v1", "bf16x3"]
+# the 3xbf16 split drops Wl.Xl and rounds Xl to bf16: ~3 * 2^-18 = 1.1e-5 relative per product at
+# worst; both 3xbf16 kernels (32x32x16 and 16x16x32 accumulation orders) land at 0.99-1.09e-5 on
+# the t3 net (tools/x3w_err.py), so their raw-output bound is 1.5e-5 (rendered outputs keep 1e-4)
+RAW_RTOL_X3 = 1.5e-5
+PRECISIONS = ["f32", "f32_v1", "bf16x3", "bf16x3_w16"]
 
 
 def model_from(dev, params, precision):
@@ -51,7 +55,7 @@ def test_trained_mlp(dev, precision, case):
     scale = ref.abs().max().item()
     err = maxdiff(raw, ref)
     print(f"{precision} {case}: raw max|d| {err:.3e} (max|raw| {scale:.1f}, rel {err / scale:.2e})")
-    assert err <= RAW_RTOL * scale
+    assert err <= (RAW_RTOL_X3 if precision.startswith("bf16x3") else RAW_RTOL) * scale
 
 
 @pytest.mark.parametrize("case", ["t4", "t3"])

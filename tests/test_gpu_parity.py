@@ -40,11 +40,11 @@ def maxdiff(a, b):
     return (a - b).abs().max().item() if a.numel() else 0.0
 
 
-@pytest.fixture(params=["f32", "f32_v1", "bf16x3"])
+@pytest.fixture(params=["f32", "f32_v1", "bf16x3", "bf16x3_w16"])
 def precision(request):
     """Every field kernel is held to the same tolerances: fp32 on 16x16x4 MFMA (two waves per
     SIMD, the default), fp32 on 32x32x2 MFMA (one wave per SIMD, also the training forward) and
-    the opt-in 3xbf16 split."""
+    the opt-in 3xbf16 split on 32x32x16 (one wave per SIMD) and on 16x16x32 (two waves per SIMD)."""
     return request.param
 
 
