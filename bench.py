@@ -298,6 +298,8 @@ def run(args):
                                        "field_launch_ms_avg": sum(f4) / max(1, len(f4))}
         if args.eval_iters > 0:
             result["eval_c5"] = {p: eval_bench(dev, rs, emb, models, args.eval_iters, p) for p in ("f32", "bf16x3")}
+            for p in ("f32", "bf16x3"):
+                result["eval_c5"][p]["graph"] = eval_bench(dev, rs, emb, models, args.eval_iters, p, graph=True)
             set_precision(args.precision)
         if args.train_iters > 0:
             result["train_c3"] = train_bench(dev, k, args.train_iters, world, "f32")
@@ -328,12 +330,12 @@ def traffic_of(prec, samples):
     return None if per_sample is None else per_sample * samples
 
 
-def eval_bench(dev, rs, emb, models, iters, precision):
+def eval_bench(dev, rs, emb, models, iters, precision, graph=False):
     """C5 (srn-cars-code-3080-val.yml): one eval.py:141-167 iteration = 2048 random rays, 64+64
     perturbed samples, forward + backward through the HIP kernels into (codes, theta, phi, rho),
     AdamW step.  Weights frozen (their grads are never read by the reference's optimiser)."""
     import numpy as np
-    from codenerf.evaluate import eval_step_loss, step_psnr
+    from codenerf.evaluate import GraphedEvalStep, eval_step_loss, step_psnr
     from codenerf.nerf import PointSampler
     from codenerf.optim import AdamW
     ps = PointSampler(NC, NF, NEAR, FAR, "lindepth", True, torch.float32, dev)
@@ -353,12 +355,23 @@ def eval_bench(dev, rs, emb, models, iters, precision):
     opt = AdamW([{"params": [zs, zt]}, {"params": [th, ph]}, {"params": [rh]}], lr=1e-2)
     np.random.seed(0)
 
-    def it():
-        loss, logs = eval_step_loss(th, ph, rh, zs, zt, target, (rs, ps), emb, mods, 1e-5)
-        opt.zero_grad()
-        loss.backward()
-        opt.step()
-        step_psnr(logs)  # eval.py:159's per-iteration read-back, after the step is enqueued
+    if graph:
+        # the iteration's forward + backward captured once as a HIP graph (GraphedEvalStep);
+        # the numpy draw, the replay, the flat AdamW and the psnr read-back per iteration
+        graphed = GraphedEvalStep(th, ph, rh, zs, zt, target, (rs, ps), emb, mods, opt, 1e-5)
+
+        def it():
+            _, logs = graphed.step()
+            opt.step()
+            graphed.prefetch()  # the next iteration's numpy draw while the GPU replays this one
+            step_psnr(logs)
+    else:
+        def it():
+            loss, logs = eval_step_loss(th, ph, rh, zs, zt, target, (rs, ps), emb, mods, 1e-5)
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+            step_psnr(logs)  # eval.py:159's per-iteration read-back, after the step is enqueued
 
     for _ in range(2):
         it()
@@ -373,6 +386,8 @@ def eval_bench(dev, rs, emb, models, iters, precision):
         m.precision = prec
     note = ("3xbf16 forward with ReLU masks + one fused 3xbf16 backward launch per field" if precision == "bf16x3"
             else "fp32 16x16x4 forward with ReLU masks + one fused fp32 backward launch per field")
+    if graph:
+        note += "; forward + backward replayed as one captured HIP graph (GraphedEvalStep)"
     return {"ms_per_iter": dt * 1e3, "rays_per_s": 2048 / dt, "rays_per_iter": 2048, "samples": "64+64 perturbed",
             "dtype": precision,
             "note": note + "; fused pose path + loss; host-side numpy ray permutation and eval.py's per-iteration psnr "

@@ -15,11 +15,35 @@ stores the activations the layer-wise backward reads.
 """
 from __future__ import annotations
 
+import weakref
 from typing import Optional, Sequence
 
 import torch
 
 from . import ops
+
+# packed weights per model and format: repacked only when a parameter's storage or version changed
+# (an optimiser step bumps the versions; see optim.AdamW).  Keyed by id() of the model's first
+# parameter (tensors compare elementwise, so no WeakKeyDictionary); the entry leaves with it.
+_PACKS = {}
+
+
+def _packed(owner, params, fmt: str):
+    """ops.mlp_pack(params, fmt), cached while ``params`` are unchanged (frozen weights of the eval
+    loop pack once instead of twice per iteration)."""
+    sig = tuple((p.data_ptr(), p._version) for p in params)
+    key = id(owner)
+    ent = _PACKS.get(key)
+    if ent is None or ent[0]() is not owner:
+        ent = (weakref.ref(owner), {})
+        _PACKS[key] = ent
+        weakref.finalize(owner, _PACKS.pop, key, None)
+    hit = ent[1].get(fmt)
+    if hit is not None and hit[0] == sig:
+        return hit[1]
+    packed = ops.mlp_pack(params, fmt)
+    ent[1][fmt] = (sig, packed)
+    return packed
 
 
 def _needs_grad(*ts) -> bool:
@@ -208,6 +232,7 @@ class RadianceField(torch.autograd.Function):
     @staticmethod
     def forward(ctx, meta, rd, pts, ro, z, z_s, z_t, *params):
         ctx.orig_params = params
+        ctx.owner = params[0]
         params = [p.detach() for p in params]
         cb = ops.code_bias(params, z_s, z_t)
         n_rays = rd.shape[0]
@@ -216,7 +241,7 @@ class RadianceField(torch.autograd.Function):
         ctx.fused = fused
         if fused:
             pack = "bf16x3" if meta.precision == "bf16x3" else "f32_w16"
-            raw, masks = ops.radiance_field_masks(ops.mlp_pack(params, pack), cb, rd, meta.n_samples,
+            raw, masks = ops.radiance_field_masks(_packed(ctx.owner, params, pack), cb, rd, meta.n_samples,
                                                   meta.chunk_rows, meta.fx, meta.fd, pts=pts, ro=ro, z=z,
                                                   code_index=meta.code_index, precision=meta.precision)
             ctx.masks = masks
@@ -234,7 +259,7 @@ class RadianceField(torch.autograd.Function):
         if ctx.train_fused:
             x3 = meta.precision == "bf16x3"
             raw, saved, ctx.masks = ops.radiance_field_train_w16(
-                ops.mlp_pack(params, "bf16x3" if x3 else "f32_w16"), cb, rd, meta.n_samples, meta.chunk_rows,
+                _packed(ctx.owner, params, "bf16x3" if x3 else "f32_w16"), cb, rd, meta.n_samples, meta.chunk_rows,
                 meta.fx, meta.fd, pts=pts, ro=ro, z=z, code_index=meta.code_index, precision=meta.precision)
         else:
             raw, saved = ops.radiance_field_train(ops.mlp_pack(params, "f32"), cb, rd, meta.n_samples,
@@ -255,7 +280,7 @@ class RadianceField(torch.autograd.Function):
         if ctx.fused:
             want_z = needs[5] or needs[6]
             pack_t = "bf16x3_t" if meta.precision == "bf16x3" else "f32_w16_t"
-            r = ops.field_backward_x3(ops.mlp_pack(params, pack_t), ctx.masks, g_raw.contiguous(), rd.shape[0],
+            r = ops.field_backward_x3(_packed(ctx.owner, params, pack_t), ctx.masks, g_raw.contiguous(), rd.shape[0],
                                       meta.n_samples, meta.chunk_rows, z_s.shape[0], meta.fx, meta.fd, rd=rd,
                                       pts=pts, ro=ro, z=z, code_index=meta.code_index, want_pts=needs[2],
                                       want_ro=needs[3], want_rd=needs[1], precision=meta.precision)
@@ -269,7 +294,7 @@ class RadianceField(torch.autograd.Function):
         want_z = needs[5] or needs[6]
         if ctx.train_fused:
             x3 = meta.precision == "bf16x3"
-            r = ops.field_backward_train(ops.mlp_pack(params, "bf16x3_t" if x3 else "f32_w16_t"), params, ctx.masks,
+            r = ops.field_backward_train(_packed(ctx.owner, params, "bf16x3_t" if x3 else "f32_w16_t"), params, ctx.masks,
                                          ctx.acts, ctx.x_enc, g_raw.contiguous(), rd.shape[0], meta.n_samples,
                                          meta.chunk_rows, z_s.shape[0], meta.fx, meta.fd, rd=rd, pts=pts, ro=ro, z=z,
                                          code_index=meta.code_index, param_grads=pg, want_pts=needs[2],
@@ -403,7 +428,8 @@ def volume_render_autograd(raw, z, rd):
 def _code_rows(z_s, z_t):
     """One code row when the per-row codes are an expand() of one row, else one per row."""
     if z_s.dim() == 2 and z_s.stride(0) == 0 and z_t.stride(0) == 0:
-        return z_s[:1], z_t[:1]
+        from .nerf import _expand_base
+        return _expand_base(z_s), _expand_base(z_t)
     return z_s, z_t
 
 

@@ -37,17 +37,19 @@ def pose_spherical(theta: torch.Tensor, phi: torch.Tensor, rho: torch.Tensor) ->
 
 def eval_step_loss(theta, phi, rho, shape_code, texture_code, target_pixels, samplers, embedders, models,
                    regularizer_lambda: float, gt_pose: Optional[torch.Tensor] = None,
-                   t_rand: Optional[torch.Tensor] = None, u: Optional[torch.Tensor] = None
-                   ) -> Tuple[torch.Tensor, Dict[str, object]]:
+                   t_rand: Optional[torch.Tensor] = None, u: Optional[torch.Tensor] = None,
+                   sel: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Dict[str, object]]:
     """One iteration's forward of eval.py:145-163 -> (loss, logs).
 
     ``target_pixels``: (H*W, C) image of the object; rays are drawn by the ray sampler's RNG
     (host numpy as the reference, or rng="device").  ``gt_pose`` (4, 4): the view's pose, for
     the logged pose error (eval.py:161-162).  ``t_rand`` / ``u``: injected stratified / fine
-    uniforms (parity tests), else drawn on the device.  logs: device tensors (read back only
-    when logged) plus psnr, which eval.py:159 reads back every iteration."""
+    uniforms (parity tests), else drawn on the device.  ``sel``: (1, S) device ray indices drawn
+    by the caller (GraphedEvalStep), else the ray sampler draws them.  logs: device tensors (read
+    back only when logged); eval.py:159's per-iteration psnr is read back by the caller once the
+    backward and the optimiser step are enqueued (``step_psnr``)."""
     ray_sampler, point_sampler = samplers
-    ro, rd, select_inds, cam_pose, tp = ray_sampler.sample_spherical(theta, phi, rho, target=target_pixels)
+    ro, rd, select_inds, cam_pose, tp = ray_sampler.sample_spherical(theta, phi, rho, target=target_pixels, sel=sel)
     n = ro.shape[0]
     z_s, z_t = shape_code.expand(n, -1), texture_code.expand(n, -1)
     # predict_radiance_and_render (nerf/__init__.py:74-91) over the whole ray batch
@@ -68,6 +70,81 @@ def step_psnr(logs: Dict[str, object]) -> float:
     return mse2psnr(logs["nerf_loss_fine"].item())
 
 
+class GraphedEvalStep:
+    """One test-time-optimisation iteration's forward and backward (eval.py:145-160) captured ONCE
+    as a HIP graph (torch.cuda.CUDAGraph, i.e. hipGraph on ROCm) and replayed every iteration: the
+    ~60 launches of the fused pose path, the hierarchical render, the fused loss and their
+    backward -- and the Python that issues them -- become one graph launch.
+
+    Per ``step()``: the host draws the ray subset exactly as the reference does
+    (np.random.permutation per iteration, ray_sampler.py:41-42) into a pinned buffer, the graph
+    copies it to the device, renders, takes the loss and its gradients into the optimiser's flat
+    gradient buffer (zeroed inside the graph, so every replay starts from zero as ``zero_grad``
+    would); the caller then runs ``optimizer.step()`` (one flat-AdamW launch; its bias corrections
+    advance on the host as usual).  The stratified / fine-sample uniforms come from torch's
+    device generator, whose graph-safe state advances per replay.
+
+    Needs the flat codenerf.optim.AdamW over (shape_code, texture_code, theta, phi, rho), frozen
+    model weights (the packed weights stay cached across replays) and ``rng="numpy"``.
+    ``t_rand`` / ``u``: fixed uniforms (parity tests), captured as static inputs."""
+
+    def __init__(self, theta, phi, rho, shape_code, texture_code, target_pixels, samplers, embedders, models,
+                 optimizer, regularizer_lambda: float, gt_pose: Optional[torch.Tensor] = None,
+                 t_rand: Optional[torch.Tensor] = None, u: Optional[torch.Tensor] = None, warmup: int = 2):
+        from .optim import AdamW
+        rs = samplers[0]
+        assert rs.rng == "numpy", "GraphedEvalStep draws the rays on the host (rng='numpy')"
+        assert isinstance(optimizer, AdamW), "GraphedEvalStep needs codenerf.optim.AdamW (flat gradients)"
+        assert theta.numel() == 1, "one view per eval step (eval.py:145)"
+        dev = target_pixels.device
+        self.rs, self.opt, self._next = rs, optimizer, None
+        self.h_sel = torch.zeros(1, rs.sample_size, dtype=torch.int64).pin_memory()
+        self.d_sel = torch.zeros(1, rs.sample_size, dtype=torch.int64, device=dev)
+        self.done = torch.cuda.Event()
+        args = (theta, phi, rho, shape_code, texture_code, target_pixels, samplers, embedders, models,
+                regularizer_lambda)
+        kw = dict(gt_pose=gt_pose, t_rand=t_rand, u=u, sel=self.d_sel)
+        grads = self.opt.flat_buffers()["grad"]
+
+        def body():
+            grads.zero_()
+            self.d_sel.copy_(self.h_sel, non_blocking=True)
+            loss, logs = eval_step_loss(*args, **kw)
+            loss.backward()
+            return loss, logs
+
+        # gradients accumulate into the flat slices (attached, not None) inside the graph
+        self.opt.zero_grad(set_to_none=False)
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):          # warm-up outside the capture (lazy inits, weight packs)
+            for _ in range(warmup):
+                body()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        torch.cuda.synchronize(dev)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.loss, self.logs = body()
+        torch.cuda.synchronize(dev)
+
+    def step(self) -> Tuple[torch.Tensor, Dict[str, object]]:
+        """This iteration's rays (host numpy, the reference's call; drawn by prefetch() if it ran),
+        then the replay.  -> (loss, logs): the graph's static output tensors, valid until the next
+        step()."""
+        sel = self._next if self._next is not None else self.rs.draw_host(1)
+        self._next = None
+        self.done.synchronize()                # the previous replay has finished reading h_sel
+        self.h_sel.numpy()[:] = sel
+        self.graph.replay()
+        self.done.record()
+        return self.loss, self.logs
+
+    def prefetch(self) -> None:
+        """Draw the NEXT iteration's rays now, while the GPU runs this one (the same numpy calls in
+        the same order; call it only when another step() follows)."""
+        self._next = self.rs.draw_host(1)
+
+
 def nerf_loss(rgb_c, rgb_f, target, shape_code, texture_code, expand: int, regularizer_lambda: float):
     """eval.py:157-163 -> (loss, stats (6,)) through cn_render_loss (one launch each way)."""
     from .autograd import render_loss_autograd
@@ -86,13 +163,15 @@ def test_time_optimize(target_pixels: torch.Tensor, samplers, embedders, models,
                        regularizer_lambda: float = 1e-5, optimizer: str = "AdamW",
                        init_pose: Tuple[float, float, float] = (1.57, 0.0, 1.30),
                        freeze_models: bool = True, log_every: Optional[int] = None,
-                       gt_pose: Optional[torch.Tensor] = None):
+                       gt_pose: Optional[torch.Tensor] = None, graph: bool = False):
     """eval.py:121-180: optimise codes + (theta, phi, rho) against one image.
 
     ``init_codes``: the embedding tables (z_s, z_t); the start point is their mean (eval.py:121-127).
     ``freeze_models``: the reference leaves the MLP weights requiring grad, so its backward also
     forms weight gradients that its optimiser never reads; they do not change the result, and
     freezing skips those GEMMs.
+    ``graph``: run the iterations as replays of one captured HIP graph (GraphedEvalStep; needs
+    frozen models, val_type AdamW and the numpy ray draw) -- the same arithmetic and draws.
     Returns (shape_code, texture_code, (theta, phi, rho), history, cam_pose of the last iteration).
     """
     dev = target_pixels.device
@@ -114,15 +193,31 @@ def test_time_optimize(target_pixels: torch.Tensor, samplers, embedders, models,
             m.requires_grad_(False)
     history, cam_pose = [], None
     try:
-        for it in range(iterations):
+        graphed = None
+        if graph:
+            assert freeze_models and optimizer == "AdamW", "graph=True needs frozen models and val_type AdamW"
             for m in models.values():
                 m.train()
-            loss, logs = eval_step_loss(theta, phi, rho, shape_code, texture_code, target_pixels, samplers,
-                                        embedders, models, regularizer_lambda, gt_pose=gt_pose)
-            cam_pose = logs.pop("cam_pose")
-            opt.zero_grad()
-            loss.backward()
-            opt.step()
+            graphed = GraphedEvalStep(theta, phi, rho, shape_code, texture_code, target_pixels, samplers,
+                                      embedders, models, opt, regularizer_lambda, gt_pose=gt_pose)
+        for it in range(iterations):
+            if graphed is not None:
+                loss, logs = graphed.step()
+                opt.step()
+                if it + 1 < iterations:
+                    graphed.prefetch()             # host draw overlapping this replay
+                # the graph's outputs are overwritten by the next replay
+                loss, logs = loss.detach().clone(), {k: v.clone() for k, v in logs.items()}
+                cam_pose = logs.pop("cam_pose")
+            else:
+                for m in models.values():
+                    m.train()
+                loss, logs = eval_step_loss(theta, phi, rho, shape_code, texture_code, target_pixels, samplers,
+                                            embedders, models, regularizer_lambda, gt_pose=gt_pose)
+                cam_pose = logs.pop("cam_pose")
+                opt.zero_grad()
+                loss.backward()
+                opt.step()
             logs["psnr"] = step_psnr(logs)
             logs["total_loss"] = loss.detach()
             history.append(logs)

@@ -70,8 +70,19 @@ def _codes(z_s: torch.Tensor, z_t: torch.Tensor):
     if tag is not None and getattr(z_t, "_cn_code_rows", None) is tag and tag.index.shape[0] == z_s.shape[0]:
         return tag.shape_rows, tag.texture_rows, (None if tag.shape_rows.shape[0] == 1 else tag.index)
     if z_s.stride(0) == 0 and z_t.stride(0) == 0:
-        return z_s[:1], z_t[:1], None
+        # an expand() of one code row: hand the field its base row, so the code gradient (already
+        # the sum over the rays, from g_code) lands on it directly instead of through a slice + expand
+        # backward (a zero-filled (R, 256) tensor and a column sum per model and step)
+        return _expand_base(z_s), _expand_base(z_t), None
     return z_s, z_t, None
+
+
+def _expand_base(z: torch.Tensor) -> torch.Tensor:
+    b = z._base
+    if b is not None and b.dim() == 2 and b.shape[0] == 1 and b.shape[1] == z.shape[1] and \
+            b.stride(1) == z.stride(1) and b.data_ptr() == z.data_ptr():
+        return b
+    return z[:1]
 
 
 def _field(model, embedders, rd, z_s, z_t, chunk_rows, pts=None, ro=None, z=None):

@@ -51,13 +51,17 @@ class RaySampler(object):
             sel = ops.random_select(batch, n, self.sample_size, self.seed, self._draws, self.device)
             self._draws += 1
             return None, sel
-        pixel_range = np.arange(0, n)
-        select_inds = np.asarray([np.random.permutation(pixel_range)[: self.sample_size] for _ in range(batch)])
+        select_inds = self.draw_host(batch)
         sel = torch.from_numpy(select_inds.astype(np.int64))
         if self.device.type == "cuda":  # pinned: the copy is enqueued, not a host-side wait on the stream
             sel = sel.pin_memory()
         sel = sel.to(self.device, non_blocking=True)
         return select_inds, sel
+
+    def draw_host(self, batch: int) -> np.ndarray:
+        """ray_sampler.py:41-42's numpy draw alone: per image np.random.permutation(H*W)[:S]."""
+        pixel_range = np.arange(0, self.height * self.width)
+        return np.asarray([np.random.permutation(pixel_range)[: self.sample_size] for _ in range(batch)])
 
     def sample(self, tform_cam2world: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor, np.ndarray]:
         """ray_sampler.py:53-82 -> ro, rd (B*S, 3), select_inds (B, S) (numpy; a device tensor with
@@ -82,14 +86,20 @@ class RaySampler(object):
         return ro, rd, (sel if select_inds is None else select_inds), tgt
 
     def sample_spherical(self, theta: torch.Tensor, phi: torch.Tensor, rho: torch.Tensor,
-                         target: Optional[torch.Tensor] = None):
+                         target: Optional[torch.Tensor] = None, sel: Optional[torch.Tensor] = None):
         """eval.py:145-148 fused: cam_pose = pose_spherical(theta, phi, rho); ro, rd, select_inds =
         sample(cam_pose); target_pixels = target[..., select_inds, :].  theta, phi, rho: (B,) each
         (the reference's (1,) leaves); target: (B, H*W, C) or (H*W, C) for B = 1.
+        ``sel``: (B, S) device indices drawn by the caller (a captured eval step, whose host draw
+        happens outside the graph); else drawn here.
         -> ro, rd (B*S, 3), select_inds, cam_pose (B, 4, 4) (no grad), target rows (B*S, C) | None."""
         from ..autograd import pose_rays_autograd
         batch = theta.numel()
-        select_inds, sel = self.select_inds(batch)
+        if sel is None:
+            select_inds, sel = self.select_inds(batch)
+        else:
+            assert sel.shape == (batch, self.sample_size), "sel must be (B, sample_size)"
+            select_inds = None
         if target is not None:
             target = target.reshape(batch, self.height * self.width, -1)
         ro, rd, cam, tgt = pose_rays_autograd(self.directions, theta, phi, rho, sel=sel, target=target)

@@ -700,10 +700,13 @@ def field_backward_x3(packed_t: Tensor, masks: Tensor, d_raw: Tensor, n_rays: in
     rd, pts, ro, z = _opt(rd, "rd"), _opt(pts, "pts"), _opt(ro, "ro"), _opt(z, "z")
     if code_index is not None:
         code_index = _cuda(code_index, "code_index", torch.int64)
-    g_code = torch.zeros(n_codes, _lib.CN_CODE_BIAS_STRIDE, device=dev, dtype=torch.float32)
+    # the accumulated outputs share one zero-filled buffer (one fill launch instead of three)
+    nc = n_codes * _lib.CN_CODE_BIAS_STRIDE
+    acc = torch.zeros(nc + 3 * n_rays * (int(want_ro) + int(want_rd)), device=dev, dtype=torch.float32)
+    g_code = acc[:nc].view(n_codes, _lib.CN_CODE_BIAS_STRIDE)
+    d_ro = acc[nc:nc + 3 * n_rays].view(n_rays, 3) if want_ro else None
+    d_rd = acc[acc.numel() - 3 * n_rays:].view(n_rays, 3) if want_rd else None
     d_pts = torch.empty(n_rays, n_samples, 3, device=dev, dtype=torch.float32) if want_pts else None
-    d_ro = torch.zeros(n_rays, 3, device=dev, dtype=torch.float32) if want_ro else None
-    d_rd = torch.zeros(n_rays, 3, device=dev, dtype=torch.float32) if want_rd else None
     check(lib.cn_field_backward_fused(fmt_t, ptr(packed_t), ptr(masks), ptr(d_raw), ptr(pts), ptr(ro), ptr(rd),
                                       ptr(z), n_rays, n_samples, chunk_rows, ptr(code_index), n_codes,
                                       _lib.host_floats(freqs_xyz), _lib.host_floats(freqs_dir), ptr(g_code),

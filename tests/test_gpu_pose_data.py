@@ -212,6 +212,78 @@ def test_eval_c5_fused_at_size(dev, precision):
 # ---------------------------------------------------------------- the fused step loss
 
 
+@pytest.mark.parametrize("precision", ["f32", "bf16x3"])
+def test_graphed_eval_step_matches_eager(dev, precision):
+    """GraphedEvalStep (the eval iteration captured once as a HIP graph, replayed per iteration) vs
+    the eager eval_step_loss + backward on the same C5 inputs (the reference's injected uniforms,
+    the same numpy draws), over two replays: loss and every gradient."""
+    from codenerf import synthetic
+    from codenerf.evaluate import GraphedEvalStep, eval_step_loss
+    from codenerf.nerf import PointSampler, RaySampler
+    from codenerf.optim import AdamW
+    g = gload("eval_c5.npz", dev)
+    rs = RaySampler(128, 128, synthetic.srn_intrinsics(128), sample_size=2048, device=dev, datatype=torch.float32)
+    ps = PointSampler(64, 64, 0.8, 1.8, "lindepth", True, torch.float32, dev)
+    models = _eval_models(dev)
+    for m in models.values():
+        m.precision = precision
+
+    def leaves():
+        return [g[k].clone().requires_grad_(True) for k in ("theta", "phi", "rho", "z_s", "z_t")]
+
+    eager = []
+    np.random.seed(17)
+    for _ in range(2):
+        th, ph, rh, zs, zt = lv = leaves()
+        loss, _ = eval_step_loss(th, ph, rh, zs, zt, g["target"], (rs, ps), embedders(dev), models, 1e-5,
+                                 t_rand=g["t_rand"], u=g["u"])
+        loss.backward()
+        eager.append((loss.item(), [t.grad.clone() for t in lv]))
+    th, ph, rh, zs, zt = lv = leaves()
+    opt = AdamW([{"params": [zs, zt]}, {"params": [th, ph]}, {"params": [rh]}], lr=1e-2)
+    np.random.seed(17)
+    step = GraphedEvalStep(th, ph, rh, zs, zt, g["target"], (rs, ps), embedders(dev), models, opt, 1e-5,
+                           t_rand=g["t_rand"], u=g["u"])
+    for i in range(2):
+        loss, _ = step.step()
+        torch.cuda.synchronize()
+        le, ge = eager[i]
+        assert abs(loss.item() - le) <= 1e-6 * max(1.0, abs(le)), (i, loss.item(), le)
+        for name, t, ref in zip(("theta", "phi", "rho", "z_s", "z_t"), lv, ge):
+            close(t.grad, ref, 1e-5, f"replay {i} {name}")
+
+
+def test_time_optimize_graph_matches_eager(dev):
+    """test_time_optimize(graph=True) runs the same iterations as the eager loop (unperturbed
+    samples, the same numpy draws): loss history, codes and pose agree."""
+    from codenerf import synthetic
+    from codenerf.evaluate import test_time_optimize
+    from codenerf.nerf import PointSampler, RaySampler
+    g = gload("eval_c5.npz", dev)
+    out = {}
+    for graph in (False, True):
+        rs = RaySampler(128, 128, synthetic.srn_intrinsics(128), sample_size=2048, device=dev,
+                        datatype=torch.float32)
+        ps = PointSampler(64, 64, 0.8, 1.8, "lindepth", False, torch.float32, dev)
+        codes = (synthetic.latent_codes(5, 4).to(dev), synthetic.latent_codes(6, 4).to(dev))
+        np.random.seed(23)
+        zs, zt, pose, hist, cam = test_time_optimize(g["target"], (rs, ps), embedders(dev), _eval_models(dev), codes,
+                                                     iterations=5, graph=graph)
+        out[graph] = (zs.detach(), zt.detach(), torch.stack([p.detach() for p in pose]), hist, cam)
+    e, q = out[False], out[True]
+    for a, b in zip(e[3], q[3]):
+        assert abs(a["total_loss"] - b["total_loss"]) <= 1e-5 * max(1.0, abs(a["total_loss"])), (a, b)
+        assert abs(a["psnr"] - b["psnr"]) <= 1e-3
+    # AdamW normalises each element's step (lr 1e-2): elements whose gradient is ~0 move by amounts
+    # set by the last bits of the atomically summed g_code, in eager and graphed runs alike, so the
+    # optimised values agree to ~lr-level, not to fp32 rounding (the gradients themselves are
+    # compared at 1e-5 in test_graphed_eval_step_matches_eager)
+    close(q[0], e[0], 2e-3, "z_s")
+    close(q[1], e[1], 2e-3, "z_t")
+    close(q[2], e[2], 2e-3, "pose")
+    close(q[4], e[4], 2e-3, "cam_pose")
+
+
 def test_render_loss_golden(dev):
     """train.py:103-107 / eval.py:157-160 loss terms and gradients vs the reference (loss.npz)."""
     from codenerf.autograd import render_loss_autograd
