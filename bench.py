@@ -305,7 +305,7 @@ def run(args):
             result["train_c3"] = train_bench(dev, k, args.train_iters, world, "f32")
             result["train_c3"]["bf16x3"] = train_bench(dev, k, args.train_iters, world, "bf16x3")
 
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:   # the CPU baseline: rank 0 at N=1 only
         cb, ref_img = cpu_baseline(k, poses[:1])
         result["cpu_baseline"] = cb
         from oracle.codenerf_oracle import mse2psnr
