@@ -415,10 +415,12 @@ __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restr
         for (int u = 0; u < 4; ++u) b[nx][u] = sb[(p + 1) * 512 + k0 + 32 * u];
       }
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < 2; ++t) {
+        bsum[t] += a[c][t];  // the bias gradient's column sum rides on the A stream (VALU beside MFMA)
 #pragma unroll
         for (int u = 0; u < 4; ++u)
           acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[c][t], b[c][u], acc[t][u], 0, 0, 0);
+      }
       if constexpr (SIG) {
         if (sig_wave) {
           const float dsg = sb[kTwRows * 256 - (h * 256 + i) + (2 * p + h) * 4 + 3];
@@ -435,8 +437,9 @@ __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restr
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int u = 0; u < 4; ++u) flush_block(acc[t][u], C, ldc, pt, 256, 256, n0 + 32 * t, k0 + 32 * u, i, h);
-  // X3 with bias_part: this slab's column sums of A (the waves of column half 0 cover all 256)
-  if (X3 && bias_part && (wave & 1) == 0) {
+  // bias_part: this slab's column sums of A, in row order per lane (the waves of column half 0
+  // cover all 256 columns)
+  if (bias_part && (wave & 1) == 0) {
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const float b = bsum[t] + __shfl_xor(bsum[t], 32);
@@ -1313,7 +1316,7 @@ int gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, 
             hipStream_t st, bool x3 = false, float* ws = nullptr, float* bias = nullptr, float* bias_ws = nullptr,
             Reducer* rd = nullptr, const float* sig = nullptr, float* sig_out = nullptr) {
   const TnPlan pl = tn_plan(A, lda, B, ldb, M, N, K, x3);
-  const bool fold_bias = bias && pl.kind == kTn256X3;
+  const bool fold_bias = bias && (pl.kind == kTn256X3 || pl.kind == kTn256);
   const bool fold_sig = sig && rd && (pl.kind == kTn256 || pl.kind == kTn256X3);
   const unsigned nb = static_cast<unsigned>(ceil_div(M, pl.rows));
   float* sig_ws = nullptr;
@@ -1334,10 +1337,10 @@ int gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, 
     case kTn256:
       if (fold_sig)
         hipLaunchKernelGGL((grad::gemm_tn256_kernel<false, true>), dim3(nb), dim3(512), 0, st, A, B, C, ldc, ws,
-                           nullptr, sig - 3, sig_ws, M, pl.rows);
+                           fold_bias ? bias_ws : nullptr, sig - 3, sig_ws, M, pl.rows);
       else
         hipLaunchKernelGGL((grad::gemm_tn256_kernel<false, false>), dim3(nb), dim3(512), 0, st, A, B, C, ldc, ws,
-                           nullptr, nullptr, nullptr, M, pl.rows);
+                           fold_bias ? bias_ws : nullptr, nullptr, nullptr, M, pl.rows);
       break;
     case kTn256X3:
       if (fold_sig)
@@ -1741,11 +1744,9 @@ extern "C" int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, con
   a.d_rd = d_rd;
   a.dpre = workspace;
   const bool wg = grads && grads[0];
-  if (wg && !x3) {  // fp32: summed in the fused backward; 3xbf16: folded into the dW GEMMs below
-    a.gbias[0] = grads[kBDir2];
-    a.gbias[1] = grads[kBDir1];
-    a.gbias[2] = grads[kBXyz1];
-  }
+  // the bias gradients of layer_dir2 / layer_dir1 / layer_xyz1 are column sums of their dPre planes,
+  // folded into the dW kernels below that stream those planes (deterministic partials), so the
+  // fused backward sums none of them (a.gbias stays null)
   CN_TRY(x3 ? launch_field_x3_bwd(pts ? kFromPts : kFromRayZ, a, st)
             : launch_field_w16_bwd(pts ? kFromPts : kFromRayZ, a, st));
   if (!wg) return CN_OK;
@@ -1761,7 +1762,7 @@ extern "C" int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, con
   Reducer red{st, workspace + 5 * M * 256, {}, 0};
   float* const ws = nullptr;
   float* const bws = nullptr;
-  auto B = [&](int i) { return x3 ? grads[i] : nullptr; };  // bias folded into this GEMM (3xbf16)
+  auto B = [&](int i) { return grads[i]; };  // bias folded into this GEMM
   const float* h1 = saved;
   const float* h2 = saved + M * 256;
   const float* feat = saved + 2 * M * 256;

@@ -793,14 +793,14 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   // ---- layer_dir2^T (m_v2), layer_dir1^T (m_v1)
   mask_act(s, mk[3]);
   save_dpre<TRAIN>(s, a, 0, row, valid);
-  if constexpr (TRAIN) gcode_add64(s, bias_row(lds, 0), 0, s.act);
+  if (TRAIN && a.gbias[0]) gcode_add64(s, bias_row(lds, 0), 0, s.act);
   zero_acc(s);
   __builtin_amdgcn_sched_barrier(0);
   layer256(s, lds, c);
   dbg_acc(s, a, 1, row, valid);
   mask_act(s, mk[2]);
   save_dpre<TRAIN>(s, a, 1, row, valid);
-  if constexpr (TRAIN) gcode_add64(s, bias_row(lds, 1), 0, s.act);
+  if (TRAIN && a.gbias[0]) gcode_add64(s, bias_row(lds, 1), 0, s.act);
   zero_acc(s);
   __builtin_amdgcn_sched_barrier(0);
   layer256(s, lds, c);
@@ -840,7 +840,7 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   // ---- layer_xyz1^T (m_h1): encoding k-steps 0-7, then 8-15
   mask_act(s, mk[0]);
   save_dpre<TRAIN>(s, a, 4, row, valid);
-  if constexpr (TRAIN) gcode_add64(s, bias_row(lds, 2), 0, s.act);
+  if (TRAIN && a.gbias[0]) gcode_add64(s, bias_row(lds, 2), 0, s.act);
   float genc[16];
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
