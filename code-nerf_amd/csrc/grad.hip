@@ -714,22 +714,30 @@ __global__ __launch_bounds__(256) void gemm_tn_x3_kernel(const float* __restrict
 // enc(m)[c] with enc = the 63 xyz features of the sample point (ENC 0: layer_xyz1's dW) or the 27
 // of its Q1 view direction (ENC 1: layer_dir1's view-direction columns), in
 // PositionalEmbedder.embed order and with encode_inputs_kernel's exact arithmetic -- so the
-// (M, 90) x_enc plane is never written or read.  Register-staged: stage = 16 rows; each thread
-// loads 2 float4 of A and decodes its sample (thread t: sample t >> 5, columns 2 (t & 31) + 0/1)
-// one stage ahead, then writes them into the LDS A image / encoding table behind the stage's
-// MFMAs.  Wave w owns output rows 32 w .. 32 w + 31 and all KB = 2 (xyz) / 1 (dir) column blocks;
+// (M, 90) x_enc plane is never written or read.  Stage = 16 A rows, moved into a 3-slot LDS ring
+// by LDS-DMA two stages ahead (one counted vmcnt + barrier per stage; until r02 they were
+// register-staged one stage ahead and the kernel ran at ~2-2.7 TB/s, latency-bound); threads
+// 0..15 decode the samples' geometry three stages ahead and 32 threads per sample evaluate its
+// encoding (one sincosf per sin/cos pair) one stage ahead into a double-buffered table.
+// Wave w owns output rows 32 w .. 32 w + 31 and all KB = 2 (xyz) / 1 (dir) column blocks;
 // X3: one 32x32x16 bf16 k-step per stage (3 products), else 8 fp32 32x32x2 row pairs.
 constexpr int kEncRows = 16;
+constexpr int kEncRing = 3;  // A stages in LDS: the one being read, two landing
 
-// Encoding column c of a sample whose point (ENC 0) or view direction (ENC 1) is x.
-template <int ENC>
-__device__ __forceinline__ float enc_value(const float* x, const mlp::FieldArgs& a, int c) {
-  constexpr int K = ENC == 0 ? 63 : 27;
-  if (c >= K) return 0.0f;
-  if (c < 3) return x[c];
-  const int b = (c - 3) / 3, comp = (c - 3) % 3;
-  const float arg = __fmul_rn(x[comp], ENC == 0 ? a.fx[b >> 1] : a.fd[b >> 1]);
-  return (b & 1) ? cosf(arg) : sinf(arg);
+// 8 floats at p + k * S bytes (k = 0..7) of the LDS-DMA ring, one round trip.  Inline asm: hipcc
+// cannot tell these reads from the ring slots the in-flight LDS-DMA pieces fill and would wait
+// vmcnt(0) before them, draining the prefetch; the counted vmcnt + barrier at the top of the
+// stage already guarantee the slot read here has landed.
+template <int S>
+__device__ __forceinline__ void ring_read8(const float* p, float* v) {
+  const unsigned addr = static_cast<unsigned>(reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) void*)p));
+  asm volatile(
+      "ds_read_b32 %0, %8\n\tds_read_b32 %1, %8 offset:%9\n\tds_read_b32 %2, %8 offset:%10\n\t"
+      "ds_read_b32 %3, %8 offset:%11\n\tds_read_b32 %4, %8 offset:%12\n\tds_read_b32 %5, %8 offset:%13\n\t"
+      "ds_read_b32 %6, %8 offset:%14\n\tds_read_b32 %7, %8 offset:%15\n\ts_waitcnt lgkmcnt(0)"
+      : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7])
+      : "v"(addr), "i"(S), "i"(2 * S), "i"(3 * S), "i"(4 * S), "i"(5 * S), "i"(6 * S), "i"(7 * S)
+      : "memory");
 }
 
 template <bool X3, int ENC, int MODE>
@@ -737,8 +745,8 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __rest
                                                              float* __restrict__ C, int64_t ldc,
                                                              float* __restrict__ part, float* __restrict__ bias_part,
                                                              int64_t rows_per_block) {
-  constexpr int K = ENC == 0 ? 63 : 27, KB = ENC == 0 ? 2 : 1, EW = 32 * KB, CPT = EW / 32;
-  __shared__ __attribute__((aligned(16))) float simg[2][kEncRows * 256];
+  constexpr int K = ENC == 0 ? 63 : 27, KB = ENC == 0 ? 2 : 1, EW = 32 * KB;
+  __shared__ __attribute__((aligned(16))) float ring[kEncRing][kEncRows * 256];  // A stages, by LDS-DMA
   __shared__ __attribute__((aligned(16))) float senc[2][kEncRows * EW];
   __shared__ __attribute__((aligned(16))) float4 xs[3][kEncRows];  // decoded geometry, 3 stages
   const int tid = threadIdx.x, lane = tid & 63;
@@ -748,19 +756,46 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __rest
   const int64_t mb = (int64_t)blockIdx.x * rows_per_block;
   const int64_t rows = min(rows_per_block, M - mb);
   const int n_stages = static_cast<int>((rows + kEncRows - 1) / kEncRows);
-  // roles: A rows ar, ar + 8 (features ac..ac+3); encoding sample es, columns ec..ec+CPT-1; threads
-  // 0..15 decode the geometry of stage st + 2 (one sample each: the Q1 map's integer divisions
-  // run once per sample, not once per column)
-  const int ar = tid >> 6, ac = 4 * (tid & 63);
-  const int es = tid >> 5, ec = CPT * (tid & 31);
-  float4 av[2];
-  float ev[CPT];
+  // the slab's A rows as a buffer resource: rows past it (the last stage's tail, the stages the
+  // loop prefetches past the end) read as zeros
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(A + mb * 256), 0, static_cast<unsigned>(rows * 256 * 4), 0x00020000);
+  // roles: encoding sample es (16 per stage), slot j = tid & 31 of its table row: slot j < NP owns
+  // the (sin, cos) pair p = j of PositionalEmbedder's layout (columns 3 + 6 (p / 3) + p % 3 and
+  // that + 3: ONE sincosf), the next slots two of the extra columns each (raw inputs 0..2, zero
+  // padding K..EW-1); threads 0..15 decode the geometry of stage st + 3 (one sample each: the Q1
+  // map's integer divisions run once per sample)
+  constexpr int NP = ENC == 0 ? 30 : 12;                 // 3 components x L frequencies
+  constexpr int NX = (3 + (EW - K) + 1) / 2;             // slots of extra columns
+  static_assert(NP + NX <= 32, "one table row per 32 threads");
+  const int es = tid >> 5, j = tid & 31;
+  // the slot's columns, resolved once: the frequency table is a kernel argument, and reading it
+  // per stage (a per-lane index: a global load) would make every stage wait for the LDS-DMA
+  // pieces in flight
+  int kind = 0, c0 = 0, c1 = 0, comp = 0;  // kind 0 idle, 1 sin/cos pair, 2 extra columns
+  float freq = 0.0f;
+  if (j < NP) {
+    kind = 1;
+    comp = j % 3;
+    c0 = 3 + 6 * (j / 3) + comp;
+    c1 = c0 + 3;
+    freq = ENC == 0 ? a.fx[j / 3] : a.fd[j / 3];
+  } else if (j < NP + NX) {
+    kind = 2;
+    comp = 2 * (j - NP);  // logical extra columns comp, comp + 1: q < 3 raw input q, else column K + q - 3
+    c0 = comp < 3 ? comp : K + comp - 3;
+    c1 = comp + 1 < 3 ? comp + 1 : K + comp - 2;
+  }
+  float ev[2] = {0.0f, 0.0f};
   float4 xv = make_float4(0.f, 0.f, 0.f, 0.f);
-  auto load_a = [&](int st) {
+  // stage st's 16 A rows: wave w moves rows w, w + 8 (1 KiB each, one 16-B-per-lane wave-instruction)
+  auto dma = [&](int st) {
+    float* slot = ring[st % kEncRing];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int64_t r = (int64_t)st * kEncRows + ar + 8 * j;
-      av[j] = r < rows ? *reinterpret_cast<const float4*>(A + (mb + r) * 256 + ac) : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int j = 0; j < kEncRows / 8; ++j) {
+      const int r = wave + 8 * j;
+      const unsigned soff = __builtin_amdgcn_readfirstlane(static_cast<unsigned>((st * kEncRows + r) * 1024));
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(slot + r * 256), 16, lane * 16u, soff, 0, 0);
     }
   };
   auto decode = [&](int st) {
@@ -776,15 +811,19 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __rest
   };
   auto enc_of = [&](int st) {  // rows past M: their A rows are zero, so any value is harmless
     const float4 x4 = xs[st % 3][es];
-    const float x[3] = {x4.x, x4.y, x4.z};
-#pragma unroll
-    for (int c = 0; c < CPT; ++c) ev[c] = enc_value<ENC>(x, a, ec + c);
+    const float x[4] = {x4.x, x4.y, x4.z, 0.0f};
+    if (kind == 1) {
+      sincosf(__fmul_rn(x[comp], freq), &ev[0], &ev[1]);  // the forward's encoding arithmetic
+    } else if (kind == 2) {
+      ev[0] = comp < 3 ? x[comp] : 0.0f;
+      ev[1] = comp + 1 < 3 ? x[comp + 1] : 0.0f;
+    }
   };
-  auto store = [&](int buf) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) *reinterpret_cast<float4*>(&simg[buf][(ar + 8 * j) * 256 + ac]) = av[j];
-#pragma unroll
-    for (int c = 0; c < CPT; ++c) senc[buf][es * EW + ec + c] = ev[c];
+  auto store_enc = [&](int buf) {
+    if (kind != 0) {
+      senc[buf][es * EW + c0] = ev[0];
+      senc[buf][es * EW + c1] = ev[1];
+    }
   };
   floatx16 acc[KB];
 #pragma unroll
@@ -794,26 +833,30 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __rest
   put_x(0);
   decode(1);
   put_x(1);
-  __syncthreads();
-  load_a(0);
-  enc_of(0);
   decode(2);
-  store(0);
   put_x(2);
+  dma(0);
+  dma(1);
   __syncthreads();
+  enc_of(0);
+  store_enc(0);
   for (int st = 0; st < n_stages; ++st) {
+    // stage st landed for every wave (all but this wave's 2 youngest vector-memory ops -- stage
+    // st+1's pieces; the geometry loads of decode(st+2), issued before them, are done too), every
+    // wave is past stage st-1 (its ring slot is free, its senc / xs buffers were read)
+    static_assert(kEncRows / 8 == 2, "the vmcnt below counts one stage of pieces");
+    asm volatile("s_waitcnt vmcnt(2)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (st > 0) put_x(st + 2);
+    decode(st + 3);
+    dma(st + 2);  // always (past the slab: zeros), so every wave's vmcnt above stays exact
     const bool more = st + 1 < n_stages;
-    if (more) {
-      load_a(st + 1);
-      enc_of(st + 1);
-      decode(st + 3);
-    }
-    const float* sa = simg[st & 1];
+    if (more) enc_of(st + 1);
+    const float* sa = ring[st % kEncRing];
     const float* se = senc[st & 1];
     if constexpr (X3) {
       float v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = sa[(8 * h + j) * 256 + 32 * wave + i];
+      ring_read8<1024>(sa + (8 * h) * 256 + 32 * wave + i, v);   // rows 8 h + j
       bsum += sum8v(v);
       u32x4 ah, al;
       split8(v, ah, al);
@@ -826,21 +869,21 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __rest
         acc[u] = mfma3(acc[u], ah, al, bh, bl);
       }
     } else {
+      float xa[8];
+      ring_read8<2048>(sa + h * 256 + 32 * wave + i, xa);          // rows 2 p + h
 #pragma unroll
       for (int p = 0; p < kEncRows / 2; ++p) {
-        const float x = sa[(2 * p + h) * 256 + 32 * wave + i];
+        const float x = xa[p];
         bsum += x;
 #pragma unroll
         for (int u = 0; u < KB; ++u)
           acc[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(x, se[(2 * p + h) * EW + 32 * u + i], acc[u], 0, 0, 0);
       }
     }
-    if (more) {
-      store((st + 1) & 1);
-      put_x(st + 3);
-    }
-    __syncthreads();
+    if (more) store_enc((st + 1) & 1);
   }
+  // the stages prefetched past the slab must land before the workgroup's LDS is released
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   float* pt = part ? part + (int64_t)blockIdx.x * 256 * K : nullptr;
 #pragma unroll
   for (int u = 0; u < KB; ++u) flush_block(acc[u], C, ldc, pt, 256, K, 32 * wave, 32 * u, i, h);
