@@ -364,8 +364,7 @@ def eval_bench(dev, rs, emb, models, iters, precision, graph=False):
         graphed = GraphedEvalStep(th, ph, rh, zs, zt, target, (rs, ps), emb, mods, opt, 1e-5)
 
         def it():
-            _, logs = graphed.step()
-            opt.step()
+            _, logs = graphed.step()  # forward + backward + the flat AdamW update, one replay
             graphed.prefetch()  # the next iteration's numpy draw while the GPU replays this one
             step_psnr(logs)
     else:
@@ -390,7 +389,7 @@ def eval_bench(dev, rs, emb, models, iters, precision, graph=False):
     note = ("3xbf16 forward with ReLU masks + one fused 3xbf16 backward launch per field" if precision == "bf16x3"
             else "fp32 16x16x4 forward with ReLU masks + one fused fp32 backward launch per field")
     if graph:
-        note += "; forward + backward replayed as one captured HIP graph (GraphedEvalStep)"
+        note += "; forward + backward + AdamW replayed as one captured HIP graph (GraphedEvalStep)"
     return {"ms_per_iter": dt * 1e3, "rays_per_s": 2048 / dt, "rays_per_iter": 2048, "samples": "64+64 perturbed",
             "dtype": precision,
             "note": note + "; fused pose path + loss; host-side numpy ray permutation and eval.py's per-iteration psnr "

@@ -106,6 +106,10 @@ SIGNATURES = {
     "cn_adamw_step": (_i, [_p, _p, _p, _p, _i64, ctypes.POINTER(_i64), ctypes.POINTER(_i64),
                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i64),
                            ctypes.c_double, ctypes.c_double, ctypes.c_double, _p]),
+    "cn_adamw_scalars": (_i, [_i64, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                              ctypes.POINTER(_i64), ctypes.c_double, ctypes.c_double, _p]),
+    "cn_adamw_step_dev": (_i, [_p, _p, _p, _p, _i64, ctypes.POINTER(_i64), ctypes.POINTER(_i64), _p,
+                               ctypes.c_double, ctypes.c_double, ctypes.c_double, _p]),
 }
 
 _lib: Optional[ctypes.CDLL] = None

@@ -77,12 +77,14 @@ class GraphedEvalStep:
     backward -- and the Python that issues them -- become one graph launch.
 
     Per ``step()``: the host draws the ray subset exactly as the reference does
-    (np.random.permutation per iteration, ray_sampler.py:41-42) into a pinned buffer, the graph
-    copies it to the device, renders, takes the loss and its gradients into the optimiser's flat
-    gradient buffer (zeroed inside the graph, so every replay starts from zero as ``zero_grad``
-    would); the caller then runs ``optimizer.step()`` (one flat-AdamW launch; its bias corrections
-    advance on the host as usual).  The stratified / fine-sample uniforms come from torch's
-    device generator, whose graph-safe state advances per replay.
+    (np.random.permutation per iteration, ray_sampler.py:41-42) into a pinned buffer and folds
+    the AdamW step's bias-corrected scalars (counting the step as ``optimizer.step()`` would) into
+    another; the graph copies both to the device, renders, takes the loss and its gradients into
+    the optimiser's flat gradient buffer (zeroed inside the graph, as ``zero_grad`` would) and
+    applies the flat AdamW update (cn_adamw_step_dev, scalars read from device memory).  With
+    ``optimizer_in_graph=False`` the caller runs ``optimizer.step()`` after the replay instead.
+    The stratified / fine-sample uniforms come from torch's device generator, whose graph-safe
+    state advances per replay.
 
     Needs the flat codenerf.optim.AdamW over (shape_code, texture_code, theta, phi, rho), frozen
     model weights (the packed weights stay cached across replays) and ``rng="numpy"``.
@@ -90,7 +92,8 @@ class GraphedEvalStep:
 
     def __init__(self, theta, phi, rho, shape_code, texture_code, target_pixels, samplers, embedders, models,
                  optimizer, regularizer_lambda: float, gt_pose: Optional[torch.Tensor] = None,
-                 t_rand: Optional[torch.Tensor] = None, u: Optional[torch.Tensor] = None, warmup: int = 2):
+                 t_rand: Optional[torch.Tensor] = None, u: Optional[torch.Tensor] = None, warmup: int = 2,
+                 optimizer_in_graph: bool = True):
         from .optim import AdamW
         rs = samplers[0]
         assert rs.rng == "numpy", "GraphedEvalStep draws the rays on the host (rng='numpy')"
@@ -105,26 +108,35 @@ class GraphedEvalStep:
                 regularizer_lambda)
         kw = dict(gt_pose=gt_pose, t_rand=t_rand, u=u, sel=self.d_sel)
         grads = self.opt.flat_buffers()["grad"]
-
-        def body():
-            grads.zero_()
-            self.d_sel.copy_(self.h_sel, non_blocking=True)
-            loss, logs = eval_step_loss(*args, **kw)
-            loss.backward()
-            return loss, logs
-
         # gradients accumulate into the flat slices (attached, not None) inside the graph
         self.opt.zero_grad(set_to_none=False)
+        self.opt_in_graph = optimizer_in_graph
+        if optimizer_in_graph:
+            n_seg = len(self.opt._plan(advance=False))
+            self.h_scal = torch.zeros(3 * n_seg, dtype=torch.float32).pin_memory()
+            self.d_scal = torch.zeros(3 * n_seg, dtype=torch.float32, device=dev)
+
+        def body(with_opt: bool):
+            grads.zero_()
+            self.d_sel.copy_(self.h_sel, non_blocking=True)
+            if with_opt:
+                self.d_scal.copy_(self.h_scal, non_blocking=True)
+            loss, logs = eval_step_loss(*args, **kw)
+            loss.backward()
+            if with_opt:
+                self.opt.graph_step(self.d_scal)
+            return loss, logs
+
         side = torch.cuda.Stream(device=dev)
         side.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(side):          # warm-up outside the capture (lazy inits, weight packs)
-            for _ in range(warmup):
-                body()
+        with torch.cuda.stream(side):          # warm-up outside the capture (lazy inits, weight packs);
+            for _ in range(warmup):            # never the update: it would move the parameters
+                body(False)
         torch.cuda.current_stream(dev).wait_stream(side)
         torch.cuda.synchronize(dev)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
-            self.loss, self.logs = body()
+            self.loss, self.logs = body(optimizer_in_graph)
         torch.cuda.synchronize(dev)
 
     def step(self) -> Tuple[torch.Tensor, Dict[str, object]]:
@@ -133,8 +145,10 @@ class GraphedEvalStep:
         step()."""
         sel = self._next if self._next is not None else self.rs.draw_host(1)
         self._next = None
-        self.done.synchronize()                # the previous replay has finished reading h_sel
+        self.done.synchronize()                # the previous replay has finished reading h_sel / h_scal
         self.h_sel.numpy()[:] = sel
+        if self.opt_in_graph:
+            self.opt.graph_scalars(self.h_scal.numpy())
         self.graph.replay()
         self.done.record()
         return self.loss, self.logs
@@ -202,8 +216,7 @@ def test_time_optimize(target_pixels: torch.Tensor, samplers, embedders, models,
                                       embedders, models, opt, regularizer_lambda, gt_pose=gt_pose)
         for it in range(iterations):
             if graphed is not None:
-                loss, logs = graphed.step()
-                opt.step()
+                loss, logs = graphed.step()        # forward, backward and the AdamW update
                 if it + 1 < iterations:
                     graphed.prefetch()             # host draw overlapping this replay
                 # the graph's outputs are overwritten by the next replay

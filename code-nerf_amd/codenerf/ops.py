@@ -743,6 +743,42 @@ def adamw_step(param: Tensor, grad: Tensor, exp_avg: Tensor, exp_avg_sq: Tensor,
                             float(beta1), float(beta2), float(eps), stream_of(param)), "cn_adamw_step")
 
 
+def adamw_scalars(segments, beta1: float, beta2: float, out) -> None:
+    """The per-segment scalars of adamw_step_dev, folded on the host exactly as cn_adamw_step folds
+    them: ``out`` a float32 buffer of 3 * len(segments) (a pinned tensor's numpy view)."""
+    lib = _lib_ready()
+    k = len(segments)
+    assert k >= 1 and out.size >= 3 * k
+
+    def arr(ct, vals):
+        return (ct * k)(*vals)
+    check(lib.cn_adamw_scalars(k, arr(ctypes.c_double, [float(s[2]) for s in segments]),
+                               arr(ctypes.c_double, [float(s[3]) for s in segments]),
+                               arr(ctypes.c_int64, [int(s[4]) for s in segments]), float(beta1), float(beta2),
+                               ctypes.c_void_p(out.ctypes.data)), "cn_adamw_scalars")
+
+
+def adamw_step_dev(param: Tensor, grad: Tensor, exp_avg: Tensor, exp_avg_sq: Tensor, segments, scalars: Tensor,
+                   beta1: float, beta2: float, eps: float) -> None:
+    """adamw_step with the per-segment scalars in device memory (``scalars``: float32, 3 per
+    segment): the graph-capturable form (cn_adamw_step_dev)."""
+    lib = _lib_ready()
+    bufs = [_cuda(t, name) for t, name in ((param, "param"), (grad, "grad"), (exp_avg, "exp_avg"),
+                                          (exp_avg_sq, "exp_avg_sq"))]
+    n = param.numel()
+    assert all(b.data_ptr() == t.data_ptr() and b.numel() == n for b, t in zip(bufs, (param, grad, exp_avg, exp_avg_sq)))
+    k = len(segments)
+    assert k >= 1 and scalars.numel() >= 3 * k and scalars.dtype == torch.float32 and scalars.is_cuda
+    assert all(b % 4 == 0 and e % 4 == 0 and 0 <= b < e <= n for b, e, *_ in segments)
+
+    def arr(ct, vals):
+        return (ct * k)(*vals)
+    check(lib.cn_adamw_step_dev(ptr(param), ptr(grad), ptr(exp_avg), ptr(exp_avg_sq), k,
+                                arr(ctypes.c_int64, [int(s[0]) for s in segments]),
+                                arr(ctypes.c_int64, [int(s[1]) for s in segments]), ptr(scalars),
+                                float(beta1), float(beta2), float(eps), stream_of(param)), "cn_adamw_step_dev")
+
+
 # ------------------------------------------------------------------ the step's loss
 
 

@@ -165,6 +165,17 @@ class AdamW(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         self._sync_grads()
+        betas, eps = self._hyper()
+        segments = self._plan(advance=True)
+        if not segments:
+            return loss
+        f = self._flat
+        ops.adamw_step(f["param"], f["grad"], f["exp_avg"], f["exp_avg_sq"], segments, betas[0], betas[1], eps)
+        # the kernel wrote through raw pointers: tell autograd and the packed-weight caches
+        torch.autograd.graph.increment_version(list(self._offs))
+        return loss
+
+    def _hyper(self):
         g0 = self.param_groups[0]
         betas, eps = tuple(g0["betas"]), float(g0["eps"])
         for g in self.param_groups:
@@ -172,6 +183,11 @@ class AdamW(torch.optim.Optimizer):
                 raise NotImplementedError("codenerf.optim.AdamW: amsgrad / maximize")
             if tuple(g["betas"]) != betas or float(g["eps"]) != eps:
                 raise NotImplementedError("codenerf.optim.AdamW: betas and eps must be shared by all groups")
+        return betas, eps
+
+    def _plan(self, advance: bool):
+        """The step's segments [begin, end, lr, wd, step] over the parameters holding a gradient
+        (state created on first use); ``advance``: count the step, as step() does."""
         segments = []
         for g in self.param_groups:
             lr, wd = float(g["lr"]), float(g["weight_decay"])
@@ -183,21 +199,38 @@ class AdamW(torch.optim.Optimizer):
                     st["step"] = torch.tensor(0.0, dtype=torch.float32)
                     st["exp_avg"] = self._view("exp_avg", p)
                     st["exp_avg_sq"] = self._view("exp_avg_sq", p)
-                st["step"] += 1
-                t = int(st["step"].item())
+                if advance:
+                    st["step"] += 1
+                t = max(1, int(st["step"].item()))
                 off = self._offs[p]
                 end = off + _round_up(p.numel())
                 if segments and segments[-1][1] == off and segments[-1][2:] == [lr, wd, t]:
                     segments[-1][1] = end
                 else:
                     segments.append([off, end, lr, wd, t])
-        if not segments:
-            return loss
+        return segments
+
+    # ---- the captured form (codenerf.evaluate.GraphedEvalStep) ---------------------------
+    def graph_step(self, scalars: torch.Tensor):
+        """Enqueue a graph-capturable step (cn_adamw_step_dev): the same update as step(), its
+        per-segment scalars read from ``scalars`` (device float32, 3 per segment) that
+        graph_scalars() fills before each replay.  Every parameter must hold its flat gradient
+        slice (zero_grad(set_to_none=False)).  Returns the segment count."""
+        betas, eps = self._hyper()
+        segments = self._plan(advance=False)
+        assert segments and scalars.numel() >= 3 * len(segments), "graph_step: scalars too small"
         f = self._flat
-        ops.adamw_step(f["param"], f["grad"], f["exp_avg"], f["exp_avg_sq"], segments, betas[0], betas[1], eps)
-        # the kernel wrote through raw pointers: tell autograd and the packed-weight caches
+        ops.adamw_step_dev(f["param"], f["grad"], f["exp_avg"], f["exp_avg_sq"], segments, scalars, betas[0],
+                           betas[1], eps)
+        return len(segments)
+
+    def graph_scalars(self, out) -> None:
+        """Count one step (as step() does) and write its per-segment scalars into ``out`` (a float32
+        numpy view of the pinned buffer a captured graph copies from)."""
+        betas, _ = self._hyper()
+        segments = self._plan(advance=True)
+        ops.adamw_scalars(segments, betas[0], betas[1], out)
         torch.autograd.graph.increment_version(list(self._offs))
-        return loss
 
     def state_dict(self):
         """torch.optim.AdamW's format; the moments are copied out of the flat buffers."""

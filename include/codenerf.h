@@ -434,6 +434,17 @@ int cn_adamw_step(float* param, const float* grad, float* exp_avg, float* exp_av
                   const int64_t* seg_begin, const int64_t* seg_end, const double* lr, const double* weight_decay,
                   const int64_t* step, double beta1, double beta2, double eps, cn_stream_t stream);
 
+/* The same update with its per-segment scalars read from DEVICE memory, so a captured graph can
+ * replay it with fresh ones: scalars = 3 floats per segment {1 - lr wd, -lr / (1 - beta1^step),
+ * (1 - beta2^step)^0.5}, as cn_adamw_scalars folds them (host, the same double arithmetic as
+ * cn_adamw_step).  Replaces optimizer.step() inside the captured eval iteration
+ * (codenerf.evaluate.GraphedEvalStep; eval.py:165-167). */
+int cn_adamw_scalars(int64_t n_segments, const double* lr, const double* weight_decay, const int64_t* step,
+                     double beta1, double beta2, float* out);
+int cn_adamw_step_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n_segments,
+                      const int64_t* seg_begin, const int64_t* seg_end, const float* scalars, double beta1,
+                      double beta2, double eps, cn_stream_t stream);
+
 /* fp32 MFMA GEMMs the backward is built from (row-major, leading dims in floats):
  *   cn_gemm_nn: C[M][N] = A[M][K] B[K][N], zeroed where mask[m][n] <= 0 (mask may be NULL); K <= 288;
  *   cn_gemm_tn: C[N][K] += sum_m A[M][N] B[M][K] (accumulates). */

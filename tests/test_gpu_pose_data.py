@@ -243,7 +243,7 @@ def test_graphed_eval_step_matches_eager(dev, precision):
     opt = AdamW([{"params": [zs, zt]}, {"params": [th, ph]}, {"params": [rh]}], lr=1e-2)
     np.random.seed(17)
     step = GraphedEvalStep(th, ph, rh, zs, zt, g["target"], (rs, ps), embedders(dev), models, opt, 1e-5,
-                           t_rand=g["t_rand"], u=g["u"])
+                           t_rand=g["t_rand"], u=g["u"], optimizer_in_graph=False)
     for i in range(2):
         loss, _ = step.step()
         torch.cuda.synchronize()
@@ -254,8 +254,13 @@ def test_graphed_eval_step_matches_eager(dev, precision):
 
 
 def test_time_optimize_graph_matches_eager(dev):
-    """test_time_optimize(graph=True) runs the same iterations as the eager loop (unperturbed
-    samples, the same numpy draws): loss history, codes and pose agree."""
+    """test_time_optimize(graph=True) -- forward, backward and the AdamW update in one replay --
+    runs the same iterations as the eager loop (unperturbed samples, the same numpy draws): loss
+    history, codes and pose.  Two iterations: AdamW normalises every element's step, so an element
+    whose gradient is ~0 moves by an amount set by the last bits of the atomically summed g_code
+    (eager runs differ from each other the same way) and the trajectories drift apart at ~lr level
+    over more steps; after two steps they agree to ~1e-6 (a wrong scalar or a missing / extra
+    update moves them by ~lr = 1e-2)."""
     from codenerf import synthetic
     from codenerf.evaluate import test_time_optimize
     from codenerf.nerf import PointSampler, RaySampler
@@ -268,20 +273,15 @@ def test_time_optimize_graph_matches_eager(dev):
         codes = (synthetic.latent_codes(5, 4).to(dev), synthetic.latent_codes(6, 4).to(dev))
         np.random.seed(23)
         zs, zt, pose, hist, cam = test_time_optimize(g["target"], (rs, ps), embedders(dev), _eval_models(dev), codes,
-                                                     iterations=5, graph=graph)
-        out[graph] = (zs.detach(), zt.detach(), torch.stack([p.detach() for p in pose]), hist, cam)
+                                                     iterations=2, graph=graph)
+        out[graph] = (zs.detach(), zt.detach(), torch.cat([p.detach().reshape(-1) for p in pose]), hist, cam)
     e, q = out[False], out[True]
     for a, b in zip(e[3], q[3]):
-        assert abs(a["total_loss"] - b["total_loss"]) <= 1e-5 * max(1.0, abs(a["total_loss"])), (a, b)
-        assert abs(a["psnr"] - b["psnr"]) <= 1e-3
-    # AdamW normalises each element's step (lr 1e-2): elements whose gradient is ~0 move by amounts
-    # set by the last bits of the atomically summed g_code, in eager and graphed runs alike, so the
-    # optimised values agree to ~lr-level, not to fp32 rounding (the gradients themselves are
-    # compared at 1e-5 in test_graphed_eval_step_matches_eager)
-    close(q[0], e[0], 2e-3, "z_s")
-    close(q[1], e[1], 2e-3, "z_t")
-    close(q[2], e[2], 2e-3, "pose")
-    close(q[4], e[4], 2e-3, "cam_pose")
+        assert abs(a["total_loss"] - b["total_loss"]) <= 1e-6 * max(1.0, abs(a["total_loss"])), (a, b)
+        assert abs(a["psnr"] - b["psnr"]) <= 1e-4
+    for name, x, y in (("z_s", q[0], e[0]), ("z_t", q[1], e[1]), ("pose", q[2], e[2]), ("cam_pose", q[4], e[4])):
+        err = (x - y).abs().max().item()
+        assert err <= 1e-4, f"{name}: max |d| {err:.3e}"
 
 
 def test_render_loss_golden(dev):

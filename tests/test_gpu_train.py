@@ -63,6 +63,43 @@ def test_adamw_matches_torch(dev):
     assert float(opt.state[pg[1]]["step"]) == 5.0
 
 
+def test_adamw_graph_step_equals_step(dev):
+    """The graph-capturable update (graph_scalars + graph_step: cn_adamw_scalars folded on the host,
+    cn_adamw_step_dev reading them from device memory) is bit-identical to step()."""
+    import numpy as np
+    from codenerf.optim import AdamW
+    g = torch.Generator().manual_seed(2)
+    shapes = [[(256, 63), (3,)], [(40, 256)]]
+    lrs = [1e-3, 3e-4]
+    base = [[torch.randn(*s, generator=g) * 0.1 for s in grp] for grp in shapes]
+    sets = []
+    for _ in range(2):
+        ps = [[torch.nn.Parameter(t.clone().to(dev)) for t in grp] for grp in base]
+        sets.append((ps, AdamW([{"params": grp, "lr": lr, "weight_decay": 0.05} for grp, lr in zip(ps, lrs)])))
+    (pa, oa), (pb, ob) = sets
+    flat_a = [p for grp in pa for p in grp]
+    flat_b = [p for grp in pb for p in grp]
+    ob.zero_grad(set_to_none=False)
+    scal = torch.zeros(3 * 8, dtype=torch.float32, device=dev)
+    host = np.zeros(3 * 8, dtype=np.float32)
+    for it in range(4):
+        grads = [torch.randn(p.shape, generator=g).to(dev) * 10.0 ** (-it) for p in flat_a]
+        oa.zero_grad()
+        for p, gr in zip(flat_a, grads):
+            p.grad = gr.clone()
+        oa.step()
+        for p, gr in zip(flat_b, grads):
+            p.grad.copy_(gr)
+        ob.graph_scalars(host)
+        scal.copy_(torch.from_numpy(host))
+        ob.graph_step(scal)
+    torch.cuda.synchronize()
+    for a, b in zip(flat_a, flat_b):
+        assert torch.equal(a.detach(), b.detach())
+        assert torch.equal(oa.state[a]["exp_avg"], ob.state[b]["exp_avg"])
+        assert float(oa.state[a]["step"]) == float(ob.state[b]["step"]) == 4.0
+
+
 def test_adamw_state_dict_interop(dev):
     """Optimiser checkpoints (train.py:130-137) move between this AdamW and torch.optim.AdamW."""
     from codenerf.optim import AdamW
