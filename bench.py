@@ -275,7 +275,7 @@ def run(args):
         psnr_img["f32_v1"] = img_v
         result["f32_v1"] = {"value": total_rays / dtv, "unit": "rays/s", "ms_per_step": dtv / args.steps * 1e3,
                             "dtype": "f32", "roofline": roofline("f32_v1", fms_v),
-                            "note": "round-1 fp32 kernel, kept as the training forward (stores activations)"}
+                            "note": "round-1 fp32 kernel, kept as the forward of the layer-wise training path (models whose inference and training precisions differ)"}
     set_precision(args.precision)
 
     if not args.no_extras:
