@@ -48,6 +48,18 @@ struct FieldArgs {
   float* gbias[3];       // ... and the bias gradients of layer_dir2, layer_dir1, layer_xyz1 (accumulated)
 };
 
+// v[i] for a lane-varying i in 0..2 by selects: an indexed read of a private array would
+// place the whole array (and the struct holding it) in scratch memory.
+__device__ __forceinline__ float pick3(const float (&v)[3], int i) {
+  return i == 0 ? v[0] : (i == 1 ? v[1] : v[2]);
+}
+// v[i] += x for a lane-varying i in 0..2, by selects (see pick3).
+__device__ __forceinline__ void add3(float (&v)[3], int i, float x) {
+  v[0] += i == 0 ? x : 0.0f;
+  v[1] += i == 1 ? x : 0.0f;
+  v[2] += i == 2 ? x : 0.0f;
+}
+
 // One sample's inputs: point, unit Q1 view direction, code row.
 struct SampleIn {
   float x[3];

@@ -363,7 +363,7 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
     for (int i = 0; i < 8; ++i) {
       const int p = 4 * i + s.g;
       const int pc = p < 30 ? p : 0;
-      const float arg = __fmul_rn(in.x[pc % 3], a.fx[pc / 3]);
+      const float arg = __fmul_rn(pick3(in.x, pc % 3), a.fx[pc / 3]);
       float sn, cs;
       sincosf(arg, &sn, &cs);
       if (i == 7 && p >= 30) {  // groups 2, 3: raw inputs
@@ -376,7 +376,7 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       const int p = 4 * i + s.g;
-      const float arg = __fmul_rn(in.vd[p % 3], a.fd[p / 3]);
+      const float arg = __fmul_rn(pick3(in.vd, p % 3), a.fd[p / 3]);
       sincosf(arg, &s.denc[i], &s.denc[3 + i]);
     }
     s.denc[6] = s.g == 0 ? in.vd[0] : (s.g == 1 ? in.vd[1] : (s.g == 2 ? in.vd[2] : 0.0f));
@@ -868,8 +868,8 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
     if (p < 30) {
       const int d = p % 3, k = p / 3;
       float sn, cs;
-      sincosf(__fmul_rn(in.x[d], a.fx[k]), &sn, &cs);
-      dx[d] += a.fx[k] * (genc[i] * cs - genc[8 + i] * sn);
+      sincosf(__fmul_rn(pick3(in.x, d), a.fx[k]), &sn, &cs);
+      add3(dx, d, a.fx[k] * (genc[i] * cs - genc[8 + i] * sn));
     } else if (s.g == 2) {  // raw inputs x0 (k-step 7), x1 (k-step 15)
       dx[0] += genc[7];
       dx[1] += genc[15];
@@ -881,10 +881,10 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   for (int i = 0; i < 3; ++i) {
     const int p = 4 * i + s.g, d = p % 3, k = p / 3;
     float sn, cs;
-    sincosf(__fmul_rn(in.vd[d], a.fd[k]), &sn, &cs);
-    dv[d] += a.fd[k] * (gdir[i] * cs - gdir[3 + i] * sn);
+    sincosf(__fmul_rn(pick3(in.vd, d), a.fd[k]), &sn, &cs);
+    add3(dv, d, a.fd[k] * (gdir[i] * cs - gdir[3 + i] * sn));
   }
-  if (s.g < 3) dv[s.g] += gdir[6];
+  add3(dv, s.g, gdir[6]);  // s.g == 3 adds nothing
 #pragma unroll
   for (int d = 0; d < 3; ++d) {
     dx[d] += __shfl_xor(dx[d], 16);

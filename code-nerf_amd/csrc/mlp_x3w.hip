@@ -384,7 +384,7 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
     for (int i = 0; i < 8; ++i) {
       const int p = 4 * i + s.g;
       const int pc = p < 30 ? p : 0;
-      const float arg = __fmul_rn(in.x[pc % 3], a.fx[pc / 3]);
+      const float arg = __fmul_rn(pick3(in.x, pc % 3), a.fx[pc / 3]);
       float sn, cs;
       sincosf(arg, &sn, &cs);
       if (i == 7 && p >= 30) {  // groups 2, 3: raw inputs
@@ -397,7 +397,7 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       const int p = 4 * i + s.g;
-      const float arg = __fmul_rn(in.vd[p % 3], a.fd[p / 3]);
+      const float arg = __fmul_rn(pick3(in.vd, p % 3), a.fd[p / 3]);
       sincosf(arg, &s.denc[i], &s.denc[3 + i]);
     }
     s.denc[6] = s.g == 0 ? in.vd[0] : (s.g == 1 ? in.vd[1] : (s.g == 2 ? in.vd[2] : 0.0f));
