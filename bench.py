@@ -136,7 +136,7 @@ def run(args):
     import codenerf
     from codenerf import synthetic
     from codenerf.models import CodeNeRFModel
-    from codenerf.nerf import PointSampler, PositionalEmbedder, RaySampler, gather_rows, render_rays
+    from codenerf.nerf import PointSampler, PositionalEmbedder, RaySampler, gather_views, render_rays
     from codenerf.utils import split_sizes
     codenerf.load_library()
     info = codenerf.build_info()
@@ -182,9 +182,9 @@ def run(args):
                               chunk_rows=chunk_, coarse_only=coarse_only, events=hook)
             rgb = out["rgb_coarse" if coarse_only else "rgb_fine"]
             if world > 1:
-                rgb = gather_rows(rgb, [p * nv for p in per_], rank)
-                if rgb is not None and len(set(per_)) == 1:     # (rank, view, row) -> (view, rank, row)
-                    rgb = rgb.view(n, nv, per_[0], 3).transpose(0, 1).reshape(nv * n_img_rays, 3)
+                rgb = gather_views(rgb, per_, rank, nv)          # rank 0: (views, H*W, 3)
+                if rgb is not None:
+                    rgb = rgb.reshape(nv * n_img_rays, 3)
             if record:
                 timing["pending"] += hook["field"]
             return rgb
@@ -308,6 +308,8 @@ def run(args):
             result["train_c3"] = train_bench(dev, k, args.train_iters, world, "f32")
             result["train_c3"]["bf16x3"] = train_bench(dev, k, args.train_iters, world, "bf16x3")
 
+    if world > 1 and rank == 0 and psnr_img[args.precision] is not None:
+        result.update(multi_rank_check(psnr_img[args.precision], rs, poses[:1], per, zs, zt, ps, emb, models))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:   # the CPU baseline: rank 0 at N=1 only
         cb, ref_img = cpu_baseline(k, poses[:1])
         result["cpu_baseline"] = cb
@@ -320,6 +322,32 @@ def run(args):
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def multi_rank_check(img, rs, pose1, per, zs, zt, ps, emb, models):
+    """After the timed region, N > 1, rank 0: the gathered first view of the headline's last step
+    against the same view rendered on this GPU alone, (a) with the N-rank split and per-rank chunking
+    (parallel_image_render's semantics: must be identical) and (b) as one 4096-ray-chunked image (the
+    single-GPU render: differs by the Q1 view-direction map wherever the chunking differs)."""
+    from codenerf.nerf import render_rays
+    n_img = H * W
+    with torch.no_grad():
+        ro, rd = rs.get_bundle(pose1)
+        ro, rd = ro.reshape(-1, 3), rd.reshape(-1, 3)
+        parts, s0 = [], 0
+        for p in per:
+            sl = slice(s0, s0 + p)
+            parts.append(render_rays(ro[sl], rd[sl], zs.expand(p, -1), zt.expand(p, -1), ps, emb, models[0],
+                                     models[1], chunk_rows=min(CHUNK, p), coarse_only=True)["rgb_coarse"])
+            s0 += p
+        sharded = torch.cat(parts)
+        single = render_rays(ro, rd, zs.expand(n_img, -1), zt.expand(n_img, -1), ps, emb, models[0], models[1],
+                             chunk_rows=CHUNK, coarse_only=True)["rgb_coarse"]
+    got = img[:n_img]
+    return {"multi_rank_maxdiff": float((got - sharded).abs().max()),
+            "multi_rank_vs_single_chunking_maxdiff": float((got - single).abs().max()),
+            "multi_rank_note": "gathered view 0 vs the same view rendered on rank 0 alone with the N-rank split "
+                               "and per-rank chunks (expected 0) and with one 4096-ray chunking (Q1 view-dir map)"}
 
 
 def traffic_of(prec, samples):

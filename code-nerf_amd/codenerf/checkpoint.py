@@ -9,19 +9,24 @@ the ``module.`` prefix DDP adds is stripped, the optimiser state is restored and
 start iteration returned.
 
 Differences by design:
-* the build never wraps its modules in DDP (codenerf.train), so the ``module.`` prefix
-  is stripped in every mode (the reference strips it only when not distributed, because
-  its distributed modules expect it);
+* the ``module.`` prefix is stripped in every mode and the state loaded into the bare module
+  (``m.module`` of a DDP wrapper): the reference strips it only when not distributed, because
+  its distributed modules are DDP wrappers that expect it.  ``save_checkpoint(ddp_prefix=True)``
+  writes it the way the reference's distributed training does, for the reference to load;
 * the file is read with ``torch.load(weights_only=True)``: the reference's checkpoints
   hold only tensors, numbers, lists and dicts, so nothing executes from the file;
 * the optimiser may be this build's flat AdamW (codenerf.optim), whose state_dict format
-  is torch.optim.AdamW's, or any torch optimiser.
+  is torch.optim.AdamW's, or any torch optimiser;
+* extra keys for an exact resume (the reference's loader reads only its own keys, so it still
+  loads these files): ``cn_next_iter`` (the iteration after the one saved, when the save came after
+  its last chunk), ``cn_scheduler_state_dict`` (the reference does not save the LambdaLR) and
+  ``cn_rng`` (the numpy, torch CPU and torch CUDA generator states, as tensors).
 """
 from __future__ import annotations
 
 from collections import OrderedDict
 from pathlib import Path
-from typing import Dict
+from typing import Dict, Optional
 
 import torch
 import torch.distributed as dist
@@ -40,9 +45,32 @@ def _device_of(models) -> torch.device:
     return torch.device("cpu")
 
 
-def load_checkpoint(cfg, models: Dict[str, torch.nn.Module], optimizer) -> int:
+def _rng_state(device) -> Dict[str, torch.Tensor]:
+    import numpy as np
+    kind, keys, pos, has_gauss, cached = np.random.get_state()
+    out = {"numpy_keys": torch.from_numpy(keys.astype(np.int64)),
+           "numpy_meta": torch.tensor([pos, has_gauss], dtype=torch.int64),
+           "numpy_gauss": torch.tensor([cached], dtype=torch.float64),
+           "torch": torch.get_rng_state()}
+    if device is not None and device.type == "cuda":
+        out["cuda"] = torch.cuda.get_rng_state(device)
+    return out
+
+
+def _set_rng_state(st: Dict[str, torch.Tensor], device) -> None:
+    import numpy as np
+    meta = st["numpy_meta"].tolist()
+    np.random.set_state(("MT19937", st["numpy_keys"].numpy().astype(np.uint32), int(meta[0]), int(meta[1]),
+                         float(st["numpy_gauss"][0])))
+    torch.set_rng_state(st["torch"].cpu())
+    if "cuda" in st and device is not None and device.type == "cuda":
+        torch.cuda.set_rng_state(st["cuda"].cpu(), device)
+
+
+def load_checkpoint(cfg, models: Dict[str, torch.nn.Module], optimizer, extras: Optional[dict] = None) -> int:
     """utils/util.py:175-213 -> the start iteration (0 when ``cfg.load_checkpoint`` is not an
-    existing ``.ckpt`` file)."""
+    existing ``.ckpt`` file).  ``extras``: receives this build's resume keys when the file has them
+    (apply them with ``resume_state``)."""
     start_iter = 0
     is_distributed = bool(getattr(cfg, "is_distributed", False))
     rank = dist.get_rank() if is_distributed else 0
@@ -61,18 +89,46 @@ def load_checkpoint(cfg, models: Dict[str, torch.nn.Module], optimizer) -> int:
         if is_distributed:
             dist.barrier()
         for model_name, model in models.items():
-            model.load_state_dict(_strip_module_prefix(checkpoint[f"model_{model_name}_state_dict"]))
+            getattr(model, "module", model).load_state_dict(
+                _strip_module_prefix(checkpoint[f"model_{model_name}_state_dict"]))
         if optimizer is not None:
             optimizer.load_state_dict(checkpoint["optimizer_state_dict"])
         start_iter = checkpoint["iter"]
+        if extras is not None:
+            extras.update({k: v for k, v in checkpoint.items() if k.startswith("cn_")})
+            extras["device"] = dev
     return start_iter
 
 
-def save_checkpoint(path, iteration: int, models: Dict[str, torch.nn.Module], optimizer) -> None:
-    """train.py:129-138's checkpoint dict, written with torch.save."""
+def resume_state(extras: dict, scheduler, start_iter: int) -> int:
+    """Apply a checkpoint's resume keys (load_checkpoint's ``extras``): the scheduler state, the RNG
+    streams -> the iteration to continue from (``cn_next_iter``, else ``start_iter``)."""
+    if not extras:
+        return start_iter
+    if scheduler is not None and "cn_scheduler_state_dict" in extras:
+        scheduler.load_state_dict(extras["cn_scheduler_state_dict"])
+    if "cn_rng" in extras:
+        _set_rng_state(extras["cn_rng"], extras.get("device"))
+    return int(extras.get("cn_next_iter", start_iter))
+
+
+def save_checkpoint(path, iteration: int, models: Dict[str, torch.nn.Module], optimizer, scheduler=None,
+                    next_iter: Optional[int] = None, ddp_prefix: bool = False, rng: bool = True) -> None:
+    """train.py:129-138's checkpoint dict, written with torch.save (+ the resume keys, see the module
+    docstring).  ``ddp_prefix``: write the model keys with DDP's ``module.`` prefix, as the
+    reference's distributed training does (its distributed load expects them)."""
     checkpoint_dict = {"iter": iteration}
     for name in ("nerf_coarse", "nerf_fine", "embedding"):
         if name in models:
-            checkpoint_dict[f"model_{name}_state_dict"] = models[name].state_dict()
+            sd = models[name].state_dict()
+            if ddp_prefix and not hasattr(models[name], "module"):
+                sd = OrderedDict((f"module.{k}", v) for k, v in sd.items())
+            checkpoint_dict[f"model_{name}_state_dict"] = sd
     checkpoint_dict["optimizer_state_dict"] = optimizer.state_dict()
+    if next_iter is not None:
+        checkpoint_dict["cn_next_iter"] = int(next_iter)
+    if scheduler is not None:
+        checkpoint_dict["cn_scheduler_state_dict"] = scheduler.state_dict()
+    if rng:
+        checkpoint_dict["cn_rng"] = _rng_state(_device_of(models))
     torch.save(checkpoint_dict, str(path))

@@ -13,6 +13,7 @@ one-launch AdamW (codenerf.optim).  torch only routes the tensors.
 """
 from __future__ import annotations
 
+import warnings
 from typing import Dict, Optional, Tuple
 
 import torch
@@ -244,6 +245,62 @@ def test_time_optimize(target_pixels: torch.Tensor, samplers, embedders, models,
     return shape_code, texture_code, (theta, phi, rho), history, cam_pose
 
 
+def _pose_lr(o, key: str) -> float:
+    """eval.py:135-136 reads optimizer.angle_lr / radius_lr; srn-cars-code.yml lacks both, so
+    the reference raises there.  This build substitutes val_lr -- and says so."""
+    if key in o:
+        return o[key] if isinstance(o, dict) else getattr(o, key)
+    if hasattr(o, key):
+        return getattr(o, key)
+    warnings.warn(f"optimizer.{key} is not in the config (the reference's eval.py:135-136 raises for it, SURVEY "
+                  f"Q8); using optimizer.val_lr = {o.val_lr}", stacklevel=3)
+    return o.val_lr
+
+
+def validation_batch(cfg, dataloader, iteration: int) -> Dict[str, torch.Tensor]:
+    """eval.py:103-109: ``set_epoch(iteration)`` when distributed, then the SIXTH batch of a fresh
+    iterator over the validation loader (``islice(iter(loader), 5, None)``).  Every rank draws its
+    own; ``validate`` then broadcasts rank 0's (eval.py:111-115)."""
+    from itertools import islice
+    if getattr(cfg, "is_distributed", False):
+        dataloader.sampler.set_epoch(iteration)
+    return next(islice(iter(dataloader), 5, None))
+
+
+def eval_loop(rank: int, cfg, device=None, resident: bool = True, verbose: bool = True):
+    """eval.py:41-79: seeds ``(rank + 1) + experiment.randomseed``, the val loader and the train split
+    (for the code-table size), models / optimiser / checkpoint, the samplers and embedders from the
+    first validation batch, then ``experiment.iterations // val_batch_size`` validations -> their
+    results (validate's dicts; rank 0 holds loss / psnr / pose_error)."""
+    import numpy as np
+    from .checkpoint import load_checkpoint
+    from .datasets import prepare_dataloader
+    from .train import log_losses, prepare_models, prepare_optimizer
+    seed = (rank + 1) + int(cfg.experiment.randomseed)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    device = torch.device("cuda", rank) if device is None else torch.device(device)
+    torch.cuda.set_device(device)
+    dataloader, _ = prepare_dataloader("val", cfg, device if resident else None)
+    _, train_dataset = prepare_dataloader("train", cfg, None)
+    models = prepare_models(cfg, train_dataset.num_objects, device)
+    optimizer, _ = prepare_optimizer(cfg, models)
+    load_checkpoint(cfg, models, optimizer)
+    first = next(iter(dataloader))
+    (height, width), intrinsic = first["color"][0].shape[:2], first["intrinsic"][0]
+    samplers = nerf.prepare_samplers(cfg, height, width, intrinsic.cpu(), torch.float32, device)
+    embedders = nerf.prepare_embedders(cfg, torch.float32, device)
+    results = []
+    for iteration in range(int(cfg.experiment.iterations) // int(cfg.dataset.val_batch_size)):
+        val_data = validation_batch(cfg, dataloader, iteration)
+        res = validate(cfg, val_data, models, samplers, embedders, device,
+                       log_every=cfg.experiment.val_print_every if verbose else None)
+        if verbose and "psnr" in res:
+            print(log_losses("val", iteration, 0.0, {"loss": res["loss"], "psnr": res["psnr"]}))
+        results.append(res)
+    return results
+
+
 def validate(cfg, val_data: Dict[str, torch.Tensor], models, samplers, embedders, device,
              log_every: Optional[int] = None) -> Dict[str, object]:
     """eval.py:82-205 for one loaded validation view (``color`` (1,H,W,C), ``pose`` (1,4,4)):
@@ -268,13 +325,13 @@ def validate(cfg, val_data: Dict[str, torch.Tensor], models, samplers, embedders
     e, o = cfg.experiment, cfg.optimizer
     zs, zt, (th, ph, rh), history, cam_pose = test_time_optimize(
         color.reshape(-1, color.shape[-1]), samplers, embedders, models, (all_s.detach(), all_t.detach()),
-        e.val_iterations, val_lr=o.val_lr, angle_lr=getattr(o, "angle_lr", o.val_lr),
-        radius_lr=getattr(o, "radius_lr", o.val_lr), regularizer_lambda=e.regularizer_lambda,
-        optimizer=getattr(o, "val_type", "AdamW"), log_every=log_every, gt_pose=gt_pose)
+        e.val_iterations, val_lr=o.val_lr, angle_lr=_pose_lr(o, "angle_lr"), radius_lr=_pose_lr(o, "radius_lr"),
+        regularizer_lambda=e.regularizer_lambda, optimizer=getattr(o, "val_type", "AdamW"), log_every=log_every,
+        gt_pose=gt_pose)
     rgb = nerf.parallel_image_render(cfg, cam_pose, [zs.detach(), zt.detach()], models, samplers, embedders,
                                      device)
     out = {"history": history, "rgb": rgb, "codes": (zs.detach(), zt.detach()),
-           "pose": (float(th), float(ph), float(rh)), "cam_pose": cam_pose}
+           "pose": (th.detach().item(), ph.detach().item(), rh.detach().item()), "cam_pose": cam_pose}
     rank0 = (not is_distributed) or dist.get_rank() == 0
     if rank0:
         assert rgb is not None, "Main process must contain rgb"

@@ -93,8 +93,15 @@ class CodeNeRFModel(torch.nn.Module):
         return ops.code_bias(self.param_list(), z_s, z_t)
 
     # --- reference API ---------------------------------------------------
-    def forward(self, z_s: torch.Tensor, z_t: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
-        """model.py:160-194: per-row codes (M, 256) x2 and encoded rows (M, 90) -> (M, 4)."""
+    def forward(self, z_s: torch.Tensor, z_t: torch.Tensor, x: torch.Tensor = None, *, field=None) -> torch.Tensor:
+        """model.py:160-194: per-row codes (M, 256) x2 and encoded rows (M, 90) -> (M, 4).
+
+        ``field`` (the renderer's fused path, codenerf.nerf._field): keyword arguments of the fused
+        encode + MLP field op over rays / depths instead of encoded rows; ``z_s`` / ``z_t`` are then
+        the distinct code rows.  Routing it through ``forward`` lets a DistributedDataParallel
+        wrapper (util.py:139-142) see the forward it synchronises the gradients of."""
+        if field is not None:
+            return _field_op(self, z_s, z_t, **field)
         self._require_supported()
         if torch.is_grad_enabled() and any(t.requires_grad for t in [z_s, z_t, x] + self.param_list()):
             from ..autograd import mlp_forward_autograd
@@ -102,6 +109,21 @@ class CodeNeRFModel(torch.nn.Module):
         codes_s, codes_t, index = _dedupe_codes(z_s, z_t)
         cb = ops.code_bias(self.param_list(), codes_s, codes_t)
         return ops.mlp_forward(self.packed(), cb, x, index, precision=self.kernel_format())
+
+
+def _field_op(m: CodeNeRFModel, cs, ct, rd, chunk_rows, fx, fd, pts=None, ro=None, z=None, code_index=None):
+    """The fused radiance field (encode + MLP) of ``m`` on distinct code rows cs / ct."""
+    needs_grad = torch.is_grad_enabled() and (
+        any(t is not None and t.requires_grad for t in (rd, cs, ct, pts, ro)) or
+        any(p.requires_grad for p in m.param_list()))
+    if needs_grad:
+        from ..autograd import radiance_field_autograd
+        return radiance_field_autograd(m, rd, cs, ct, chunk_rows, fx, fd, pts=pts, ro=ro, z=z,
+                                       code_index=code_index)
+    cb = m.code_bias(cs, ct)
+    n_samples = pts.shape[1] if pts is not None else z.shape[1]
+    return ops.radiance_field(m.packed(), cb, rd, n_samples, chunk_rows, fx, fd, pts=pts, ro=ro, z=z,
+                              code_index=code_index, precision=m.kernel_format())
 
 
 def _dedupe_codes(z_s: torch.Tensor, z_t: torch.Tensor):
@@ -161,6 +183,6 @@ class ShapeTextureEmbedding(torch.nn.Module):
 
 
 def get_params_tensor(model, is_distributed):
-    """model.py:79-84 (the build's modules are never DDP-wrapped: see codenerf.train)."""
+    """model.py:79-84 (a DDP wrapper or the bare module: both work, whatever ``is_distributed`` says)."""
     m = getattr(model, "module", model)
     return m.get_params_tensor()

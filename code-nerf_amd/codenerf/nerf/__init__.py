@@ -25,7 +25,7 @@ from .volumetric_render import volume_render
 
 __all__ = ["RaySampler", "PointSampler", "PositionalEmbedder", "volume_render", "prepare_samplers",
            "prepare_embedders", "predict_radiance_and_render", "forward_pass", "parallel_image_render",
-           "render_rays"]
+           "render_rays", "gather_rows", "gather_views"]
 
 
 def prepare_samplers(cfg, height: int, width: int, intrinsics, datatype, device) -> Tuple[RaySampler, PointSampler]:
@@ -86,20 +86,16 @@ def _expand_base(z: torch.Tensor) -> torch.Tensor:
 
 
 def _field(model, embedders, rd, z_s, z_t, chunk_rows, pts=None, ro=None, z=None):
+    """The fused field of ``model`` (a CodeNeRFModel or a DDP wrapper of one): through the module's
+    ``forward`` (its ``field`` form), so a DistributedDataParallel wrapper runs its forward
+    bookkeeping and its gradient hooks fire in the backward, as in the reference's DDP training."""
     fx, fd = _check_embedders(embedders)
-    m = _unwrap(model)
     cs, ct, code_index = _codes(z_s, z_t)
-    needs_grad = torch.is_grad_enabled() and (
-        any(t is not None and t.requires_grad for t in (rd, cs, ct, pts, ro)) or
-        any(p.requires_grad for p in m.param_list()))
-    if needs_grad:
-        from ..autograd import radiance_field_autograd
-        return radiance_field_autograd(m, rd, cs, ct, chunk_rows, fx, fd, pts=pts, ro=ro, z=z,
-                                       code_index=code_index)
-    cb = m.code_bias(cs, ct)
-    n_samples = pts.shape[1] if pts is not None else z.shape[1]
-    return ops.radiance_field(m.packed(), cb, rd, n_samples, chunk_rows, fx, fd, pts=pts, ro=ro, z=z,
-                              code_index=code_index, precision=m.kernel_format())
+    if isinstance(model, torch.nn.parallel.DistributedDataParallel):
+        return model(cs, ct, field=dict(rd=rd, chunk_rows=chunk_rows, fx=fx, fd=fd, pts=pts, ro=ro, z=z,
+                                        code_index=code_index))
+    from ..models.model import _field_op
+    return _field_op(_unwrap(model), cs, ct, rd, chunk_rows, fx, fd, pts=pts, ro=ro, z=z, code_index=code_index)
 
 
 def forward_pass(model, embedders, rd: torch.Tensor, pts: torch.Tensor,
@@ -206,6 +202,22 @@ def parallel_image_render(cfg, pose: torch.Tensor, object_embedding, models, sam
         if not is_distributed:
             return rgb
         return gather_rows(rgb, per, rank)
+
+
+def gather_views(rows: torch.Tensor, per: List[int], rank: int, n_views: int) -> Optional[torch.Tensor]:
+    """Many views sharded at once (parallel_image_render's split applied to every view): ``rows`` is
+    this rank's (n_views * per[rank], C) slice rows, view-major.  One all-gather of the padded
+    per-rank blocks (gather_rows), then rank 0 interleaves them back: rank r's view v block is
+    pixels [sum(per[:r]), sum(per[:r+1])) of view v.  Rank 0 -> (n_views, sum(per), C); others None.
+    Uneven shares (Q5: the last rank takes the remainder) are handled."""
+    if rows.shape[0] != n_views * per[rank]:
+        raise ValueError(f"gather_views: {rows.shape[0]} rows, expected {n_views} x {per[rank]}")
+    allrows = gather_rows(rows, [p * n_views for p in per], rank)
+    if allrows is None:
+        return None
+    c = tuple(rows.shape[1:])
+    blocks = allrows.split([p * n_views for p in per])
+    return torch.cat([b.view((n_views, p) + c) for b, p in zip(blocks, per)], dim=1)
 
 
 def gather_rows(rows: torch.Tensor, per: List[int], rank: int) -> Optional[torch.Tensor]:

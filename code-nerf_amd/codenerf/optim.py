@@ -252,8 +252,7 @@ class AdamW(torch.optim.Optimizer):
         if not (dist.is_available() and dist.is_initialized()):
             return
         world = dist.get_world_size(group)
-        if world == 1:
-            return
+        # (world 1 runs the collectives too, as DDP does: the same code path at every size)
         missing = set(self._sync_grads())
         params = list(self._offs)
         # which parameters hold a gradient on SOME rank (DDP reduces those; a parameter no rank
@@ -278,5 +277,5 @@ class AdamW(torch.optim.Optimizer):
     def broadcast_params(self, src: int = 0, group=None) -> None:
         """Start every replica from rank ``src``'s parameters (DDP's construction-time
         broadcast): one broadcast of the flat parameter buffer."""
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        if dist.is_available() and dist.is_initialized():
             dist.broadcast(self._flat["param"], src=src, group=group)

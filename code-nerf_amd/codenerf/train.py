@@ -23,7 +23,8 @@ The loss terms keep the reference's definitions, including the regulariser on
 from __future__ import annotations
 
 from collections import OrderedDict
-from typing import Dict, List
+from pathlib import Path
+from typing import Dict, List, Optional
 
 import torch
 import torch.distributed as dist
@@ -107,6 +108,10 @@ def _average_gradients(optimizer, models) -> None:
         o += p.numel()
 
 
+def _ddp_wrapped(models) -> bool:
+    return any(isinstance(m, torch.nn.parallel.DistributedDataParallel) for m in models.values())
+
+
 def train_minibatch(models, optimizer, scheduler, point_sampler, embedders, ro, rd, object_ids, target_pixels,
                     regularizer_lambda: float, is_distributed: bool = False) -> Dict[str, object]:
     """train.py:92-114 for one chunk -> the losses train.py logs (tensors) and its psnr (float,
@@ -122,8 +127,8 @@ def train_minibatch(models, optimizer, scheduler, point_sampler, embedders, ro, 
     loss_coarse, loss_fine, regularization = stats[0], stats[1], stats[2]
     optimizer.zero_grad()
     loss.backward()
-    if is_distributed:
-        _average_gradients(optimizer, models)
+    if is_distributed and not _ddp_wrapped(models):
+        _average_gradients(optimizer, models)     # (DDP-wrapped modules averaged in the backward)
     optimizer.step()
     scheduler.step()
     # train.py:105 reads psnr back before the backward; reading the same value once the step is
@@ -134,9 +139,10 @@ def train_minibatch(models, optimizer, scheduler, point_sampler, embedders, ro, 
 
 
 def train_iteration(cfg, train_data: Dict[str, torch.Tensor], models, optimizer, scheduler, samplers,
-                    embedders) -> List[Dict[str, object]]:
+                    embedders, on_chunk=None) -> List[Dict[str, object]]:
     """train.py:64-114 for one loaded batch (``color`` (B,H,W,C), ``pose`` (B,4,4), ``object_id``
-    (B,) on the device) -> the per-chunk logs."""
+    (B,) on the device) -> the per-chunk logs.  ``on_chunk(j, num_batches, logs)``: called after
+    chunk j's optimiser step (train.py:116-142's logging / checkpoint / validation slot)."""
     ray_sampler, point_sampler = samplers
     is_distributed = bool(getattr(cfg, "is_distributed", False))
     for m in models.values():
@@ -150,8 +156,116 @@ def train_iteration(cfg, train_data: Dict[str, torch.Tensor], models, optimizer,
     assert chunk <= n_rays * color.shape[0], \
         "Chunksize needs to atleast be less than to the number of rays sampled from a single image"
     logs = []
-    for ro, rd, ids, tp in zip(get_minibatches(ro_batch, chunk), get_minibatches(rd_batch, chunk),
-                               get_minibatches(object_ids, chunk), get_minibatches(target, chunk)):
+    batches = list(zip(get_minibatches(ro_batch, chunk), get_minibatches(rd_batch, chunk),
+                       get_minibatches(object_ids, chunk), get_minibatches(target, chunk)))
+    for j, (ro, rd, ids, tp) in enumerate(batches):
         logs.append(train_minibatch(models, optimizer, scheduler, point_sampler, embedders, ro, rd, ids, tp,
                                     cfg.experiment.regularizer_lambda, is_distributed))
+        if on_chunk is not None:
+            on_chunk(j, len(batches), logs[-1])
     return logs
+
+
+# ---------------------------------------------------------------- the driver loop (train.py:19-142)
+
+def log_losses(mode: str, i: int, time_taken: float, losses: Dict[str, float],
+               learning_rate: Optional[float] = None) -> str:
+    """utils/util.py:238-264's console string (TensorBoard is not rebuilt)."""
+    tag = {"train": "[TRAIN ]", "val": "[VAL   ]"}.get(mode, "[VALOPT]")
+    out = f"{tag} Iter: {i:>8} Time taken: {time_taken:>4.4f} "
+    if learning_rate:
+        out += f"Learning rate: {learning_rate:0.8f} "
+    for key, val in losses.items():
+        out += f"{key}: {float(val):>4.4f} "
+    return out
+
+
+def prepare_experiment(cfg) -> Path:
+    """utils/util.py:44-55: ``experiment.logdir / experiment.id``, with the config written beside."""
+    import yaml
+    logdir_path = Path(cfg.experiment.logdir) / str(cfg.experiment.id)
+    logdir_path.mkdir(parents=True, exist_ok=True)
+    with open(logdir_path / "config.yml", "w") as f:
+        yaml.safe_dump(cfg.to_dict() if hasattr(cfg, "to_dict") else dict(cfg), f)
+    return logdir_path
+
+
+def _main(cfg) -> bool:
+    return (not getattr(cfg, "is_distributed", False)) or dist.get_rank() == 0
+
+
+def train(rank: int, cfg, device=None, resident: bool = True, stop_after: Optional[int] = None,
+          verbose: bool = True) -> Dict[str, object]:
+    """train.py:19-142 on the gfx950 path, with the reference's seeds, data order and cadence.
+
+    * seed ``(rank + 1) + experiment.randomseed`` for numpy and torch (train.py:29-31);
+    * the train / val loaders of utils/util.py:59-90 (``resident``: the split decoded once into HBM,
+      codenerf.datasets.ResidentLoader: the same sampler, the same index order), the models, the
+      optimiser + LambdaLR and the checkpoint (util.py:93-213), the samplers and embedders from the
+      first batch (train.py:51-58);
+    * per iteration: ``set_epoch`` when distributed (train.py:67-68), one batch from a fresh
+      iterator (train.py:70), ``train_iteration``; after each chunk step i = iteration *
+      num_batches + j: the log line every ``print_every`` (rank 0), a checkpoint every
+      ``save_every`` and at the last iteration (rank 0, ``checkpoint{i:5d}.ckpt``), ``validate``
+      every ``validate_every`` (every rank; eval.py:82-205).
+    ``stop_after``: leave the loop after this many iterations (an interrupted run, for resume tests).
+    Checkpoints also carry the RNG streams, the scheduler and the next iteration (extra keys the
+    reference's loader ignores), so a resume continues the uninterrupted run exactly; a reference
+    checkpoint resumes with the reference's semantics (``iter`` again, fresh RNG and scheduler).
+    Returns {"logs": per-chunk losses (floats), "checkpoints": paths, "validation": results,
+    "models", "optimizer", "scheduler"}."""
+    import time
+    import numpy as np
+    from . import checkpoint as C
+    from .datasets import prepare_dataloader
+    from .evaluate import validate, validation_batch
+    seed = (rank + 1) + int(cfg.experiment.randomseed)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    main = _main(cfg)
+    logdir_path = prepare_experiment(cfg) if main else None
+    device = torch.device("cuda", rank) if device is None else torch.device(device)
+    torch.cuda.set_device(device)
+    train_loader, train_dataset = prepare_dataloader("train", cfg, device if resident else None)
+    val_loader, _ = prepare_dataloader("val", cfg, device if resident else None)
+    models = prepare_models(cfg, train_dataset.num_objects, device)
+    optimizer, scheduler = prepare_optimizer(cfg, models)
+    extras: Dict[str, object] = {}
+    start_iter = C.load_checkpoint(cfg, models, optimizer, extras=extras)
+    first = next(iter(train_loader))
+    (height, width), intrinsic = first["color"][0].shape[:2], first["intrinsic"][0]
+    samplers = nerf.prepare_samplers(cfg, height, width, intrinsic.cpu(), torch.float32, device)
+    embedders = nerf.prepare_embedders(cfg, torch.float32, device)
+    start_iter = C.resume_state(extras, scheduler, start_iter)   # after the first-batch draw, as saved
+    out = {"logs": [], "checkpoints": [], "validation": [], "models": models, "optimizer": optimizer,
+           "scheduler": scheduler}
+    total = int(cfg.experiment.iterations) // int(cfg.dataset.train_batch_size)
+    e = cfg.experiment
+    for iteration in range(start_iter, total):
+        if stop_after is not None and iteration - start_iter >= stop_after:
+            break
+        if getattr(cfg, "is_distributed", False):
+            train_loader.sampler.set_epoch(iteration)
+        train_data = next(iter(train_loader))
+        train_data = {k: (v.to(device, non_blocking=True) if torch.is_tensor(v) else v) for k, v in train_data.items()}
+        then = time.time()
+
+        def on_chunk(j, num_batches, lg):
+            i = iteration * num_batches + j
+            out["logs"].append({k: float(v) for k, v in lg.items()})
+            if main and i > 0:
+                if i % e.print_every == 0 and verbose:
+                    print(log_losses("train", i, time.time() - then, out["logs"][-1], scheduler.get_last_lr()[0]))
+                if i % e.save_every == 0 or i == e.iterations - 1:
+                    path = logdir_path / f"checkpoint{i:5d}.ckpt"
+                    C.save_checkpoint(path, iteration, models, optimizer, scheduler=scheduler,
+                                      next_iter=iteration + 1 if j == num_batches - 1 else None)
+                    out["checkpoints"].append(str(path))
+                    if verbose:
+                        print("================== Saved Checkpoint =================")
+            if i > 0 and i % e.validate_every == 0:
+                val_data = validation_batch(cfg, val_loader, i)
+                out["validation"].append(validate(cfg, val_data, models, samplers, embedders, device,
+                                                  log_every=e.val_print_every if verbose else None))
+        train_iteration(cfg, train_data, models, optimizer, scheduler, samplers, embedders, on_chunk=on_chunk)
+    return out

@@ -460,16 +460,21 @@ __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restr
 // 4 x NA partial sums in registers, folded through LDS and flushed with NA x 256 atomics per
 // workgroup (or stored as the workgroup's partial row block: the deterministic path).
 // Bandwidth-bound: X crosses HBM once.
-template <int NA>
+// CS (A = the (M, 4) d raw rows, NA = 3): also the column sums of all 4 columns of A -- g_code's
+// rgb and sigma entries when the code gradient is folded (one code row) -- in row order per row
+// group, the 4 groups added in order: cpart[b * 3 + n] (n < 3) and cpart[3 nb + b] (sigma).
+template <int NA, bool CS = false>
 __global__ __launch_bounds__(256) void gemm_tn_skinny_kernel(const float* __restrict__ A, int64_t lda,
                                                              const float* __restrict__ B, float* __restrict__ C,
                                                              int64_t ldc, float* __restrict__ part, int64_t M,
-                                                             int64_t rows_per_block) {
+                                                             int64_t rows_per_block, float* __restrict__ cpart = nullptr) {
   __shared__ float red[4][NA][256];
+  __shared__ float cred[4][4];
   const int t = threadIdx.x, rg = t >> 6, c4 = t & 63;
   const int64_t mb = (int64_t)blockIdx.x * rows_per_block;
   const int64_t me = min(M, mb + rows_per_block);
   float acc[NA][4] = {};
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
   for (int64_t m = mb + rg; m < me; m += 4) {
     const float4 x = reinterpret_cast<const float4*>(B + m * 256)[c4];
 #pragma unroll
@@ -480,6 +485,18 @@ __global__ __launch_bounds__(256) void gemm_tn_skinny_kernel(const float* __rest
       acc[n][2] = fmaf(av, x.z, acc[n][2]);
       acc[n][3] = fmaf(av, x.w, acc[n][3]);
     }
+    if constexpr (CS) {
+      const float4 a4 = reinterpret_cast<const float4*>(A)[m];
+      cs[0] += a4.x;
+      cs[1] += a4.y;
+      cs[2] += a4.z;
+      cs[3] += a4.w;
+    }
+  }
+  if constexpr (CS) {
+    if (c4 == 0)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) cred[rg][n] = cs[n];
   }
 #pragma unroll
   for (int n = 0; n < NA; ++n)
@@ -491,6 +508,13 @@ __global__ __launch_bounds__(256) void gemm_tn_skinny_kernel(const float* __rest
     const float v = (red[0][n][t] + red[1][n][t]) + (red[2][n][t] + red[3][n][t]);
     if (part) part[((int64_t)blockIdx.x * NA + n) * 256 + t] = v;
     else atomicAdd(&C[n * ldc + t], v);
+  }
+  if constexpr (CS) {
+    if (t < 4) {
+      const float v = (cred[0][t] + cred[1][t]) + (cred[2][t] + cred[3][t]);
+      if (t < 3) cpart[(int64_t)blockIdx.x * 3 + t] = v;
+      else cpart[3 * (int64_t)gridDim.x + blockIdx.x] = v;
+    }
   }
 }
 
@@ -1719,11 +1743,32 @@ extern "C" int cn_ray_points_backward(const float* g_pts, const float* z, int64_
 // dPre planes, then the dW GEMMs' partial tiles (deterministic reduction, reused by each GEMM in
 // stream order).
 // Every dW GEMM of one backward keeps its partial tiles until the single deferred reduction:
-// the sum of their slices (+ three bias partial blocks and the 64-float alignment of each take).
+// the sum of their slices (+ five column-sum partial blocks -- three biases, g_code's feat and xyz2
+// rows -- the small d raw column sums and the 64-float alignment of each take).
 static int64_t train_dw_ws_floats(int64_t m) {
   return 4 * tn_ws_floats(m, 256, 256) + tn_ws_floats(m, 3, 256) + tn_ws_floats(m, 1, 256) +
          std::max(tn_ws_floats(m, 256, 27), enc_parts(m) * 256 * 27) +
-         std::max(tn_ws_floats(m, 256, 63), enc_parts(m) * 256 * 63) + 3 * 1024 * 256 + 16 * 64;
+         std::max(tn_ws_floats(m, 256, 63), enc_parts(m) * 256 * 63) + 5 * 1024 * 256 + 4 * 256 * 4 + 24 * 64;
+}
+
+// fc_rgb's dW (C += d rgb^T v2, d_raw's columns 0..2) and, in the same pass, the d raw column sums
+// g_rgb[0..2] += sum d rgb, g_sig[0] += sum d sigma (g_code's rgb / sigma entries with one code row).
+static int rgb_dw_draw_sums(const float* d_raw, const float* v2, float* C, int64_t ldc, int64_t M, float* g_rgb,
+                            float* g_sig, hipStream_t st, Reducer* rd) {
+  const TnPlan pl = tn_plan(d_raw, 4, v2, 256, M, 3, 256, false);
+  if (pl.kind != kTnSkinny) {
+    CN_TRY(gemm_tn(d_raw, 4, v2, 256, C, ldc, M, 3, 256, st, false, nullptr, g_rgb, nullptr, rd));
+    return colsum(d_raw + 3, 4, M, 1, g_sig, nullptr, st, rd);
+  }
+  const unsigned nb = static_cast<unsigned>(ceil_div(M, pl.rows));
+  float* ws = rd->take(pl.parts * 3 * 256);
+  float* cpart = rd->take(4 * (int64_t)nb);
+  hipLaunchKernelGGL((grad::gemm_tn_skinny_kernel<3, true>), dim3(nb), dim3(256), 0, st, d_raw, 4, v2, C, ldc, ws, M,
+                     pl.rows, cpart);
+  CN_TRY(launch_status());
+  CN_TRY(reduce(rd, ws, pl.parts, 3, 256, C, ldc, st));
+  CN_TRY(reduce(rd, cpart, nb, 1, 3, g_rgb, 3, st));
+  return reduce(rd, cpart + 3 * (int64_t)nb, nb, 1, 1, g_sig, 1, st);
 }
 
 extern "C" int64_t cn_field_backward_train_workspace_floats(int64_t m) {
@@ -1789,16 +1834,25 @@ extern "C" int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, con
   const bool wg = grads && grads[0];
   // the bias gradients of layer_dir2 / layer_dir1 / layer_xyz1 are column sums of their dPre planes,
   // folded into the dW kernels below that stream those planes (deterministic partials), so the
-  // fused backward sums none of them (a.gbias stays null)
+  // fused backward sums none of them (a.gbias stays null).  With ONE code row (a chunk of one
+  // object: every C3 step) g_code is column sums too -- of d feat (plane 2), of layer_xyz2's dPre
+  // (plane 3) and of d raw -- folded the same way, so the fp32 step is deterministic (no float
+  // atomics anywhere in it) and the fused kernel skips its code sums.
+  const bool fold_code = wg && !x3 && n_codes == 1;
+  if (fold_code) a.g_code = nullptr;
   CN_TRY(x3 ? launch_field_x3_bwd(pts ? kFromPts : kFromRayZ, a, st)
             : launch_field_w16_bwd(pts ? kFromPts : kFromRayZ, a, st));
   if (!wg) return CN_OK;
   auto G = [&](int i) { return grads[i]; };
   // biases: layer_dir2 / layer_dir1 / layer_xyz1 summed in the kernel; the others are g_code's
-  // column sums
-  hipLaunchKernelGGL(grad::gcode_bias_kernel, dim3(3), dim3(256), 0, st, g_code, n_codes, G(kBXyz2), G(kBOut),
-                     G(kBRgb));
-  CN_TRY(launch_status());
+  // column sums (after the deferred reduction when g_code itself is folded)
+  if (!fold_code) {
+    hipLaunchKernelGGL(grad::gcode_bias_kernel, dim3(3), dim3(256), 0, st, g_code, n_codes, G(kBXyz2), G(kBOut),
+                       G(kBRgb));
+    CN_TRY(launch_status());
+  }
+  float* const gc_feat = fold_code ? g_code + kCbFeat : nullptr;
+  float* const gc_xyz2 = fold_code ? g_code + kCbXyz2 : nullptr;
   const float* P[5];
   for (int k = 0; k < 5; ++k) P[k] = workspace + k * M * 256;
   // partial tiles of every dW GEMM in their own slices, summed by ONE deferred launch
@@ -1811,8 +1865,9 @@ extern "C" int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, con
   const float* feat = saved + 2 * M * 256;
   const float* v1 = saved + 3 * M * 256;
   const float* v2 = saved + 4 * M * 256;
-  // fc_rgb (h half): dW += d rgb^T v2
-  CN_TRY(gemm_tn(d_raw, 4, v2, 256, G(kWRgb), 512, M, 3, 256, st, x3, ws, nullptr, nullptr, &red));
+  // fc_rgb (h half): dW += d rgb^T v2 (+ g_code's rgb / sigma entries, folded, in the same pass)
+  if (fold_code) CN_TRY(rgb_dw_draw_sums(d_raw, v2, G(kWRgb), 512, M, g_code + kCbRgb, g_code + kCbSigma, st, &red));
+  else CN_TRY(gemm_tn(d_raw, 4, v2, 256, G(kWRgb), 512, M, 3, 256, st, x3, ws, nullptr, nullptr, &red));
   // layer_dir2
   CN_TRY(gemm_tn(P[0], 256, v1, 256, G(kWDir2), 256, M, 256, 256, st, x3, ws, B(kBDir2), bws, &red));
   // layer_dir1: [feat | dir enc]
@@ -1820,12 +1875,18 @@ extern "C" int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, con
   if (x_enc) CN_TRY(gemm_tn(P[1], 256, x_enc + 63, 90, G(kWDir1) + 256, 283, M, 256, 27, st, x3, ws, nullptr, nullptr, &red));
   else CN_TRY(gemm_tn_enc(1, P[1], a, G(kWDir1) + 256, 283, st, x3, ws, nullptr, nullptr, &red));
   // fc_out (h half): row 0 from d sigma, rows 1.. from d feat
-  CN_TRY(gemm_tn(P[2], 256, h2, 256, G(kWOut) + 512, 512, M, 256, 256, st, x3, ws, nullptr, nullptr, &red, d_raw + 3,
+  CN_TRY(gemm_tn(P[2], 256, h2, 256, G(kWOut) + 512, 512, M, 256, 256, st, x3, ws, gc_feat, bws, &red, d_raw + 3,
                  G(kWOut)));
   // layer_xyz2 (h half)
-  CN_TRY(gemm_tn(P[3], 256, h1, 256, G(kWXyz2), 512, M, 256, 256, st, x3, ws, nullptr, nullptr, &red));
+  CN_TRY(gemm_tn(P[3], 256, h1, 256, G(kWXyz2), 512, M, 256, 256, st, x3, ws, gc_xyz2, bws, &red));
   // layer_xyz1
   if (x_enc) CN_TRY(gemm_tn(P[4], 256, x_enc, 90, G(kWXyz1), 63, M, 256, 63, st, x3, ws, B(kBXyz1), bws, &red));
   else CN_TRY(gemm_tn_enc(0, P[4], a, G(kWXyz1), 63, st, x3, ws, B(kBXyz1), bws, &red));
-  return red.flush();
+  CN_TRY(red.flush());
+  if (fold_code) {
+    hipLaunchKernelGGL(grad::gcode_bias_kernel, dim3(3), dim3(256), 0, st, g_code, n_codes, G(kBXyz2), G(kBOut),
+                       G(kBRgb));
+    CN_TRY(launch_status());
+  }
+  return CN_OK;
 }

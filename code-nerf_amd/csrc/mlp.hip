@@ -670,11 +670,6 @@ extern "C" int cn_field_backward_x3(const float* packed_t, const uint32_t* masks
                                  stream);
 }
 
-// Debug hook for tools/debug_w16_bwd.py (not part of the ABI header): when set, the fp32 fused
-// backward dumps its intermediate gradients there ((6, M, 256) floats).
-static float* cn_debug_buffer = nullptr;
-extern "C" void cn_debug_set_buffer(float* p) { cn_debug_buffer = p; }
-
 extern "C" int cn_field_backward_fused(int fmt_t, const float* packed_t, const uint32_t* masks, const float* d_raw,
                                        const float* pts, const float* ro, const float* rd, const float* z,
                                        int64_t n_rays, int64_t n_samples, int64_t chunk_rows,
@@ -712,7 +707,6 @@ extern "C" int cn_field_backward_fused(int fmt_t, const float* packed_t, const u
   a.d_pts = d_pts;
   a.d_ro = d_ro;
   a.d_rd = d_rd;
-  a.save = cn_debug_buffer;  // tools/debug_w16_bwd.py only (NULL otherwise)
   return fmt_t == CN_FMT_BF16X3_T ? launch_field_x3_bwd(pts ? kFromPts : kFromRayZ, a, cn::as_stream(stream))
                                   : launch_field_w16_bwd(pts ? kFromPts : kFromRayZ, a, cn::as_stream(stream));
 }

@@ -64,6 +64,7 @@ __device__ __forceinline__ void add3(float (&v)[3], int i, float x) {
 struct SampleIn {
   float x[3];
   float vd[3];
+  float nrm;        // |rd| of the Q1 direction ray (the backward's d rd scale)
   int64_t code_of;  // ray (or row) whose code applies
 };
 
@@ -92,6 +93,7 @@ __device__ __forceinline__ SampleIn decode_sample(const FieldArgs& a, int64_t rc
     in.vd[0] = __fdiv_rn(d0, nrm);
     in.vd[1] = __fdiv_rn(d1, nrm);
     in.vd[2] = __fdiv_rn(d2, nrm);
+    in.nrm = nrm;
     in.code_of = ray;
   }
   return in;

@@ -41,6 +41,8 @@ namespace mlp {
 namespace w16 {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef unsigned uint4v __attribute__((ext_vector_type(4)));
+typedef unsigned uint2v __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 constexpr int kWaves = 8;
@@ -58,8 +60,12 @@ constexpr int kStreamFloats = kChunks * kChunkQuads * 4;
 // h2, [g][ob][r] = W_out[0][16 ob + 4 g + r])
 constexpr int kCB1 = 0, kCBD1 = 256, kCBD2 = 512, kCSig = 768, kConsts = 1024;
 constexpr int kPackedFloats = kStreamFloats + kConsts;
+// LDS constants: the packed ones, then the encoding frequencies (fx[10] | fd[4] | pad 2): a
+// lane-varying index into the kernel arguments is a global load per use (or a register held
+// across the tile loop), an LDS read is neither
+constexpr int kCFreq = kConsts, kLdsConsts = kConsts + 16;
 // LDS: the ring, the constants, one code-bias row per wave
-constexpr int kLdsQuads = kRing * kChunkQuads + (kConsts + kWaves * kCbStride) / 4;
+constexpr int kLdsQuads = kRing * kChunkQuads + (kLdsConsts + kWaves * kCbStride) / 4;
 
 static_assert(kChunks % kRing == 0, "cyclic stream: chunk c + 36 reuses chunk c's ring slot");
 static_assert(kPiecesPerWave == 4, "4 DMA wave-instructions per chunk per wave");
@@ -149,7 +155,39 @@ struct State {
   bool uniform_code; // all 16 samples of the wave use one code row
   __amdgpu_buffer_rsrc_t wsrc;
   unsigned voff;
+  unsigned poff;     // this lane's byte offset in a (kTile, 256) fp32 plane block: row 16 wave + (lane & 15), col 4 g
+  unsigned gbase;    // backward: this lane's byte offset in a 256-float sum row (rowsum64's features)
 };
+
+// The kernel's LDS constants (after the ring): the packed ones and the encoding frequencies.
+__device__ __forceinline__ void load_consts(const FieldArgs& a, float* clds) {
+  for (int k = threadIdx.x; k < kConsts; k += kThreads) clds[k] = a.packed[kStreamFloats + k];
+  if (threadIdx.x < 16) {
+    const int t = threadIdx.x;
+    clds[kCFreq + t] = t < 10 ? a.fx[t] : (t < 14 ? a.fd[t - 10] : 0.0f);
+  }
+}
+
+// A buffer resource over rows [tile kTile, tile kTile + kTile) of plane `plane` of a (planes, m, 256)
+// fp32 array (wave-uniform base; rows past m fall outside num_records, so their stores are dropped
+// and their loads read 0 -- no per-lane 64-bit address arithmetic, no validity branch).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const float* base, int plane, int64_t m, int64_t tile) {
+  const int64_t r0 = tile * kTile;
+  const int64_t rows = m - r0 < kTile ? m - r0 : kTile;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base) + ((int64_t)plane * m + r0) * 256, 0,
+                                           static_cast<int>(rows * 1024), 0x00020000);
+}
+
+// The tile's mask block: kMaskLayers x 64 uint2 per wave.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mask_rsrc(const unsigned* masks, int64_t tile);
+
+// The 16 blocks' column offsets go in soffset: as part of the VGPR offset, LICM hoists the 16
+// sums out of the tile loop into 16 VGPRs instead of the instruction's immediate field.
+__device__ __forceinline__ void store_plane(const State& s, __amdgpu_buffer_rsrc_t r, const floatx4* v) {
+#pragma unroll
+  for (int ob = 0; ob < 16; ++ob)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, v[ob]), r, s.poff, 64 * ob, 0);
+}
 
 
 // One LDS-DMA piece: 1 KiB of chunk cn (piece p of 4 for this wave).
@@ -283,36 +321,44 @@ __device__ __forceinline__ void bias_code(State& s, const FieldArgs& a, const fl
 constexpr int kMaskLayers = 4;
 constexpr int kMaskWordsPerTile = kWaves * kMaskLayers * 64 * 2;
 
-// act = relu(acc); MASKS: also store the layer's mask bits (slot ml of the tile's mask block).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mask_rsrc(const unsigned* masks, int64_t tile) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned*>(masks) + tile * kMaskWordsPerTile, 0,
+                                           kMaskWordsPerTile * 4, 0x00020000);
+}
+// Byte offset of (wave, layer ml) in a tile's mask block (soffset; the lane's 8 lane B in voffset).
+__device__ __forceinline__ unsigned mask_soff(const State& s, int ml) {
+  return static_cast<unsigned>(s.wave) * kMaskLayers * 512u + 512u * ml;
+}
+
+// act = relu(acc); MASKS: also store the layer's mask bits (slot ml of the tile's mask block): bit
+// 4 ob + r of word ob >> 3 (ob & 7 there).  The words are built by shifting the accumulator left
+// one bit per feature, highest first: a constant 1 << n per bit would be a VOP3 literal, which
+// gfx9 encodings lack, so the compiler kept all 32 of them in VGPRs across the tile loop.
 template <bool MASKS>
 __device__ __forceinline__ void relu_act(State& s, const FieldArgs& a, int64_t tile, int ml) {
-  unsigned w0 = 0, w1 = 0;
 #pragma unroll
   for (int ob = 0; ob < 16; ++ob)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float v = s.acc[ob][r];
-      s.act[ob][r] = fmaxf(v, 0.0f);
-      if constexpr (MASKS) {
-        const unsigned bit = v > 0.0f ? 1u : 0u;
-        if (ob < 8) w0 |= bit << (4 * ob + r);
-        else w1 |= bit << (4 * (ob - 8) + r);
+    for (int r = 0; r < 4; ++r) s.act[ob][r] = fmaxf(s.acc[ob][r], 0.0f);
+  if constexpr (MASKS) {
+    unsigned w[2] = {0u, 0u};
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int k = 31; k >= 0; --k) {
+        const float v = s.acc[8 * h + (k >> 2)][k & 3];
+        w[h] = (w[h] << 1) | (v > 0.0f ? 1u : 0u);
       }
-    }
-  if constexpr (MASKS)
-    reinterpret_cast<uint2*>(a.masks)[((tile * kWaves + s.wave) * kMaskLayers + ml) * 64 + s.lane] = make_uint2(w0, w1);
+    __builtin_amdgcn_raw_buffer_store_b64(uint2v{w[0], w[1]}, mask_rsrc(a.masks, tile), 8u * s.lane,
+                                          mask_soff(s, ml), 0);
+  }
 }
 
 // Training forward: the post-activation rows the weight gradients read (h1, h2, feat, v1, v2 as
 // (5, m, 256) planes, feature 16 ob + 4 g + r: one 16-B store per block per lane).
 template <bool SAVE>
-__device__ __forceinline__ void save_act(const State& s, const FieldArgs& a, int plane, int64_t row, bool valid) {
-  if constexpr (SAVE) {
-    if (!valid) return;
-    float* d = a.save + ((int64_t)plane * a.m + row) * 256 + 4 * s.g;
-#pragma unroll
-    for (int ob = 0; ob < 16; ++ob) *reinterpret_cast<floatx4*>(d + 16 * ob) = s.act[ob];
-  }
+__device__ __forceinline__ void save_act(const State& s, const FieldArgs& a, int plane, int64_t tile) {
+  if constexpr (SAVE) store_plane(s, plane_rsrc(a.save, plane, a.m, tile), s.act);
 }
 
 template <int MODE, bool MASKS, bool SAVE = false>
@@ -363,7 +409,7 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
     for (int i = 0; i < 8; ++i) {
       const int p = 4 * i + s.g;
       const int pc = p < 30 ? p : 0;
-      const float arg = __fmul_rn(pick3(in.x, pc % 3), a.fx[pc / 3]);
+      const float arg = __fmul_rn(pick3(in.x, pc % 3), clds[kCFreq + pc / 3]);
       float sn, cs;
       sincosf(arg, &sn, &cs);
       if (i == 7 && p >= 30) {  // groups 2, 3: raw inputs
@@ -376,7 +422,7 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       const int p = 4 * i + s.g;
-      const float arg = __fmul_rn(pick3(in.vd, p % 3), a.fd[p / 3]);
+      const float arg = __fmul_rn(pick3(in.vd, p % 3), clds[kCFreq + 10 + p / 3]);
       sincosf(arg, &s.denc[i], &s.denc[3 + i]);
     }
     s.denc[6] = s.g == 0 ? in.vd[0] : (s.g == 1 ? in.vd[1] : (s.g == 2 ? in.vd[2] : 0.0f));
@@ -398,7 +444,7 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
     } else {
       relu_act<MASKS>(s, a, tile, layer == kXyz2 ? 0 : (layer == kOut ? 1 : 2));
     }
-    save_act<SAVE>(s, a, layer - kXyz2, row, valid);  // h1, h2, feat, v1
+    save_act<SAVE>(s, a, layer - kXyz2, tile);  // h1, h2, feat, v1
     if (layer == kOut) {
       // sigma = fc_out row 0 . [h2, zs2] + b: the h2 part here, the code part from cn_code_bias
       float sg = 0.0f;
@@ -423,7 +469,7 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
 
   // ---- fc_rgb (256 -> 3): one chunk, 64 k-steps of block 0 in 4 chains
   relu_act<MASKS>(s, a, tile, 3);
-  save_act<SAVE>(s, a, 4, row, valid);  // v2
+  save_act<SAVE>(s, a, 4, tile);  // v2
   {
     float b0 = 0.0f, b1 = 0.0f, b2 = 0.0f, bs = 0.0f;
     if (s.uniform_code) {
@@ -502,15 +548,16 @@ __global__ __launch_bounds__(kThreads, 2) void field_w16_kernel(FieldArgs a) {
   s.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   s.wsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.packed), 0, kPackedFloats * 4, 0x00020000);
   s.voff = static_cast<unsigned>(s.wave * 64 + s.lane) * 16u;
+  s.poff = static_cast<unsigned>(s.wave * 16 + (s.lane & 15)) * 1024u + 16u * s.g;
   s.sig = 0.0f;
-  float* crow_lds = clds + kConsts + s.wave * kCbStride;
+  float* crow_lds = clds + kLdsConsts + s.wave * kCbStride;
 
-  for (int k = threadIdx.x; k < kConsts; k += kThreads) clds[k] = a.packed[kStreamFloats + k];
+  load_consts(a, clds);
   // prime the ring with chunks 0..2, wait for chunk 0 everywhere, read its first fragments
   dma_chunk(s, lds, 0);
   dma_chunk(s, lds, 1);
   dma_chunk(s, lds, 2);
-  asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
   read_a<0>(lds + s.lane, s.pre);
 
@@ -553,7 +600,7 @@ __global__ __launch_bounds__(kThreads, 2) void field_w16_kernel(FieldArgs a) {
 constexpr int kTRgb = 0, kTDir2 = 1, kTDir1 = 9, kTDDir = 17, kTOut = 18, kTXyz2 = 26, kTXyz1 = 34;
 constexpr int kTSig = 0;  // transposed-pack constants: fc_out row 0 over h2, [g][ob][r]
 // LDS after the ring: constants, one g_code row per wave
-constexpr int kBGacc = kConsts;
+constexpr int kBGacc = kLdsConsts;
 constexpr int kBBias = kBGacc + kWaves * kCbStride;  // training: bias-gradient rows dir2 | dir1 | xyz1 (shared)
 constexpr int kBwdLdsFloats = kBBias + 3 * 256;
 constexpr int kBwdLdsQuads = kRing * kChunkQuads + kBwdLdsFloats / 4;
@@ -621,18 +668,62 @@ __device__ __forceinline__ float sum16(float x) {
   return x;
 }
 
-// g_code[col + 16 ob + 4 g + r] += sum over the wave's samples of v[ob][r] (all 64 features of
-// this lane group); row = this wave's g_code row in LDS.
-__device__ __forceinline__ void gcode_add64(const State& s, float* row, int col, const floatx4* v) {
-  const bool holder = (s.lane & 15) == 15;
-  float* base = row + col + 4 * s.g;
+// One butterfly step of rowsum64 over N values: the lane keeps the half of x selected by `hi`
+// (bit s of its row index) and adds the other half of lane i - 2^s (row rotation DPP).
+template <int N, int ROR>
+__device__ __forceinline__ void rowsum_step(const float* x, float* y, bool hi) {
 #pragma unroll
-  for (int ob = 0; ob < 16; ++ob)
+  for (int k = 0; k < N / 2; ++k) {
+    const float keep = hi ? x[k + N / 2] : x[k];
+    const float send = hi ? x[k] : x[k + N / 2];
+    y[k] = keep + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(send), 0x120 + ROR, 0xF, 0xF, false));
+  }
+}
+
+// Sums over the 16 samples of a lane group (the 16 lanes of a DPP row) of the 64 values v[ob][r]:
+// a transpose-reduction in 4 row-rotation steps (60 DPP adds + 120 selects instead of 64 separate
+// 16-lane reductions).  Lane i of the row ends with out[j] = the sum of k = 4 rev4(i) + j, i.e. of
+// features 16 rev4(i) + 4 g + j (j = 0..3), rev4 = the 4-bit reversal of i: step s keeps the half
+// chosen by bit s of i, and lane i - 2^s has the same lower bits and the other bit s.
+__device__ __forceinline__ void rowsum64(const floatx4* v, float* out, int i) {
+  float x0[64], x1[32], x2[16], x3[8];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float t = sum16(v[ob][r]);
-      if (holder) atomicAdd(base + 16 * ob + r, t);
-    }
+  for (int k = 0; k < 64; ++k) x0[k] = v[k >> 2][k & 3];
+  rowsum_step<64, 1>(x0, x1, (i & 1) != 0);
+  rowsum_step<32, 2>(x1, x2, (i & 2) != 0);
+  rowsum_step<16, 4>(x2, x3, (i & 4) != 0);
+  rowsum_step<8, 8>(x3, out, (i & 8) != 0);
+}
+
+__device__ __forceinline__ int rev4(int i) { return ((i & 1) << 3) | ((i & 2) << 1) | ((i & 4) >> 1) | ((i & 8) >> 3); }
+
+__device__ __forceinline__ unsigned lds_addr(const float* p) {
+  return static_cast<unsigned>(reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) float*)(p)));
+}
+
+// row[COL + 16 ob + 4 g + r] += sum over the wave's samples of v[ob][r] (all 64 features of this
+// lane group; `row`: an LDS row, wave-uniform).  The 4 float atomics per lane are issued by inline
+// asm: for a compiler-visible LDS write hipcc cannot rule out the in-flight LDS-DMA ring writes
+// and puts an s_waitcnt vmcnt(0) before it, which drains the weight stream and the plane stores.
+// The address is formed inside the asm from the lane's constant part (s.gbase) and the row's
+// uniform offset, so no per-call address is hoisted out of the tile loop into a VGPR.  The asm is
+// not counted in the compiler's lgkmcnt, so every reader of these rows waits lgkmcnt(0)
+// explicitly (flush_gcode, the kernel's final flush).
+template <int COL>
+__device__ __forceinline__ void gcode_add64(const State& s, float* row, const floatx4* v) {
+  float o[4];
+  rowsum64(v, o, s.lane & 15);
+  const unsigned roff = __builtin_amdgcn_readfirstlane(lds_addr(row));
+  unsigned addr;
+  asm volatile(
+      "v_add_u32 %0, %1, %2\n\t"
+      "ds_add_f32 %0, %3 offset:%7\n\t"
+      "ds_add_f32 %0, %4 offset:%7+4\n\t"
+      "ds_add_f32 %0, %5 offset:%7+8\n\t"
+      "ds_add_f32 %0, %6 offset:%7+12"
+      : "=&v"(addr)
+      : "s"(roff), "v"(s.gbase), "v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]), "i"(4 * COL)
+      : "memory");
 }
 
 // act = acc where the mask bit is set, else +0 (torch's relu backward: grad * (pre > 0)).
@@ -722,17 +813,6 @@ __device__ __forceinline__ void flush_gcode(const State& s, const FieldArgs& a, 
   }
 }
 
-// Debug dump (a.save non-NULL, tools/debug_w16_bwd.py): the accumulators of one backward stage
-// as (M, 256) rows, feature 16 ob + 4 g + r.
-__device__ __forceinline__ void dbg_acc(const State& s, const FieldArgs& a, int stage, int64_t row, bool valid) {
-  if (!a.save || !valid) return;
-  float* d = a.save + ((int64_t)stage * a.m + row) * 256 + 4 * s.g;
-#pragma unroll
-  for (int ob = 0; ob < 16; ++ob)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) d[16 * ob + r] = s.acc[ob][r];
-}
-
 // Training backward: the workgroup's bias-gradient row l (layer_dir2, layer_dir1, layer_xyz1) in LDS.
 __device__ __forceinline__ float* bias_row(float4* lds, int l) {
   return reinterpret_cast<float*>(lds + kRing * kChunkQuads) + kBBias + 256 * l;
@@ -742,15 +822,30 @@ __device__ __forceinline__ float* bias_row(float4* lds, int l) {
 // plane `plane` of a.dpre: 0 layer_dir2, 1 layer_dir1, 2 fc_out rows 1.. (d feat), 3 layer_xyz2,
 // 4 layer_xyz1.
 template <bool TRAIN>
-__device__ __forceinline__ void save_dpre(const State& s, const FieldArgs& a, int plane, int64_t row, bool valid) {
-  if constexpr (TRAIN) {
-    if (!valid) return;
-    float* d = a.dpre + ((int64_t)plane * a.m + row) * 256 + 4 * s.g;
-#pragma unroll
-    for (int ob = 0; ob < 16; ++ob) *reinterpret_cast<floatx4*>(d + 16 * ob) = s.act[ob];
-  }
+__device__ __forceinline__ void save_dpre(const State& s, const FieldArgs& a, int plane, int64_t tile) {
+  if constexpr (TRAIN) store_plane(s, plane_rsrc(a.dpre, plane, a.m, tile), s.act);
 }
 
+// The Q1 view-direction row of sample row rc (nerf/__init__.py:127-128; decode_sample's map).
+__device__ __forceinline__ int64_t q1_dir_ray(const FieldArgs& a, int64_t rc) {
+  const int64_t S = a.n_samples;
+  const int64_t ray = rc / S, smp = rc - ray * S;
+  const int64_t base = (ray / a.chunk_rows) * a.chunk_rows;
+  const int64_t rcnt = min(a.chunk_rows, a.n_rays - base);
+  return base + ((ray - base) * S + smp) % rcnt;
+}
+
+// The tile's ReLU mask words of layer l (slot l of the forward's mask block).
+__device__ __forceinline__ uint2 load_mask(const State& s, const FieldArgs& a, int64_t tile, int l) {
+  const uint2v w = __builtin_amdgcn_raw_buffer_load_b64(mask_rsrc(a.masks, tile), 8u * s.lane, mask_soff(s, l), 0);
+  return make_uint2(w[0], w[1]);
+}
+
+// Live ranges, because this kernel sits at the 256-VGPR cap of two waves per SIMD (act, acc: 128;
+// A fragments and the prefetch: 48): the mask words are loaded a layer pair ahead of their use
+// (the compiler counts the weight stream's DMA pieces in between, so the wait it puts before the
+// use does not drain the stream), the view-direction gradient is finished right after its narrow
+// chunk (3 values to the end instead of 8 + the unit direction), and the code row is wave-uniform.
 template <int MODE, bool TRAIN>
 __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* lds, float* grow, int64_t tile,
                                         int& cur_code) {
@@ -759,23 +854,22 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   const int64_t rc = valid ? row : a.m - 1;
   const float* clds = reinterpret_cast<const float*>(lds + kRing * kChunkQuads);
 
-  // ---- inputs: sample, d raw, masks (h1, h2, v1, v2), code row (wave-uniform: host-checked)
+  // ---- inputs: sample, d raw, masks of v2 and v1, code row (wave-uniform: host-checked)
   const SampleIn in = decode_sample<MODE>(a, rc);
   const int crow = __builtin_amdgcn_readfirstlane(static_cast<int>(code_row(a, in.code_of)));
   float4 dr = reinterpret_cast<const float4*>(a.d_raw)[rc];
-  const float zv = MODE == kFromRayZ ? a.z[rc] : 0.0f;
-  uint2 mk[kMaskLayers];
-#pragma unroll
-  for (int l = 0; l < kMaskLayers; ++l)
-    mk[l] = reinterpret_cast<const uint2*>(a.masks)[((tile * kWaves + s.wave) * kMaskLayers + l) * 64 + s.lane];
+  const uint2 m_v2 = load_mask(s, a, tile, 3), m_v1 = load_mask(s, a, tile, 2);
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   if (!valid) dr = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (crow != cur_code) {
+  // a.g_code NULL: the caller forms g_code from the dPre planes (deterministic column sums folded
+  // into the dW GEMMs; cn_field_backward_train_fmt with one code row) -- no code sums here
+  const bool gc = a.g_code != nullptr;
+  if (gc && crow != cur_code) {
     if (cur_code >= 0) flush_gcode(s, a, grow, cur_code);
     cur_code = crow;
   }
   // g_code sigma / rgb (lane group 0 carries the wave's 16 samples)
-  {
+  if (gc) {
     const float t0 = sum16(dr.w), t1 = sum16(dr.x), t2 = sum16(dr.y), t3 = sum16(dr.z);
     if (s.lane == 15) {
       atomicAdd(grow + kCbSigma, t0);
@@ -789,58 +883,78 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   zero_acc(s);
   chunk_k0(s, lds, c, s.g == 0 ? dr.x : (s.g == 1 ? dr.y : (s.g == 2 ? dr.z : 0.0f)));
   c = kTDir2;
-  dbg_acc(s, a, 0, row, valid);
+  const float dsig = dr.w;
   // ---- layer_dir2^T (m_v2), layer_dir1^T (m_v1)
-  mask_act(s, mk[3]);
-  save_dpre<TRAIN>(s, a, 0, row, valid);
-  if (TRAIN && a.gbias[0]) gcode_add64(s, bias_row(lds, 0), 0, s.act);
+  mask_act(s, m_v2);
+  save_dpre<TRAIN>(s, a, 0, tile);
+  if (TRAIN && a.gbias[0]) gcode_add64<0>(s, bias_row(lds, 0), s.act);
   zero_acc(s);
   __builtin_amdgcn_sched_barrier(0);
   layer256(s, lds, c);
-  dbg_acc(s, a, 1, row, valid);
-  mask_act(s, mk[2]);
-  save_dpre<TRAIN>(s, a, 1, row, valid);
-  if (TRAIN && a.gbias[0]) gcode_add64(s, bias_row(lds, 1), 0, s.act);
+  const uint2 m_h2 = load_mask(s, a, tile, 1), m_h1 = load_mask(s, a, tile, 0);
+  mask_act(s, m_v1);
+  save_dpre<TRAIN>(s, a, 1, tile);
+  if (TRAIN && a.gbias[0]) gcode_add64<0>(s, bias_row(lds, 1), s.act);
   zero_acc(s);
   __builtin_amdgcn_sched_barrier(0);
   layer256(s, lds, c);
-  dbg_acc(s, a, 2, row, valid);
   // ---- the view-direction rows of layer_dir1^T (narrow chunk, B = m_v1 . d v1 still in act)
 #pragma unroll
   for (int q = 0; q < 4; ++q) s.acc2[q] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
   chunk_narrow(s, lds, c);
   c += 1;
-  float gdir[8];
+  // d view dir -> the Q1 direction ray's d rd (its atomics at the end of the tile):
+  // vd = rd[dray] / |rd[dray]|: d rd[dray] += (g - vd (vd . g)) / |rd[dray]|
+  float grd_q1[3] = {0.f, 0.f, 0.f};
+  {
+    float gdir[8];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    gdir[r] = s.acc2[0][r] + s.acc2[1][r];
-    gdir[4 + r] = s.acc2[2][r] + s.acc2[3][r];
+    for (int r = 0; r < 4; ++r) {
+      gdir[r] = s.acc2[0][r] + s.acc2[1][r];
+      gdir[4 + r] = s.acc2[2][r] + s.acc2[3][r];
+    }
+    float dv[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int p = 4 * i + s.g, d = p % 3, k = p / 3;
+      const float f = clds[kCFreq + 10 + k];
+      float sn, cs;
+      sincosf(__fmul_rn(pick3(in.vd, d), f), &sn, &cs);
+      add3(dv, d, f * (gdir[i] * cs - gdir[3 + i] * sn));
+    }
+    add3(dv, s.g, gdir[6]);  // s.g == 3 adds nothing
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      dv[d] += __shfl_xor(dv[d], 16);
+      dv[d] += __shfl_xor(dv[d], 32);
+    }
+    const float dot = in.vd[0] * dv[0] + in.vd[1] * dv[1] + in.vd[2] * dv[2];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) grd_q1[d] = (dv[d] - in.vd[d] * dot) / in.nrm;
   }
   // ---- fc_out^T: B = d feat (no activation), init = fc_out row 0 (h2 part) x d sigma
 #pragma unroll
   for (int ob = 0; ob < 16; ++ob) s.act[ob] = s.acc[ob];
-  save_dpre<TRAIN>(s, a, 2, row, valid);
-  gcode_add64(s, grow, kCbFeat, s.act);
+  save_dpre<TRAIN>(s, a, 2, tile);
+  if (gc) gcode_add64<kCbFeat>(s, grow, s.act);
 #pragma unroll
   for (int ob = 0; ob < 16; ++ob) {
     const floatx4 w = *reinterpret_cast<const floatx4*>(clds + kTSig + 64 * s.g + 4 * ob);
-    s.acc[ob] = w * dr.w;
+    s.acc[ob] = w * dsig;
   }
   __builtin_amdgcn_sched_barrier(0);
   layer256(s, lds, c);
-  dbg_acc(s, a, 3, row, valid);
   // ---- layer_xyz2^T (m_h2): its masked input gradient is the code term's too
-  mask_act(s, mk[1]);
-  save_dpre<TRAIN>(s, a, 3, row, valid);
-  gcode_add64(s, grow, kCbXyz2, s.act);
+  mask_act(s, m_h2);
+  save_dpre<TRAIN>(s, a, 3, tile);
+  if (gc) gcode_add64<kCbXyz2>(s, grow, s.act);
   zero_acc(s);
   __builtin_amdgcn_sched_barrier(0);
   layer256(s, lds, c);
-  dbg_acc(s, a, 4, row, valid);
   // ---- layer_xyz1^T (m_h1): encoding k-steps 0-7, then 8-15
-  mask_act(s, mk[0]);
-  save_dpre<TRAIN>(s, a, 4, row, valid);
-  if (TRAIN && a.gbias[0]) gcode_add64(s, bias_row(lds, 2), 0, s.act);
+  mask_act(s, m_h1);
+  save_dpre<TRAIN>(s, a, 4, tile);
+  if (TRAIN && a.gbias[0]) gcode_add64<0>(s, bias_row(lds, 2), s.act);
   float genc[16];
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
@@ -855,21 +969,17 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
     }
   }
 
-  if (a.save && valid) {
-    float* d = a.save + (5 * a.m + row) * 256;
-    for (int t = 0; t < 16; ++t) d[16 * s.g + t] = genc[t];
-    for (int t = 0; t < 8; ++t) d[64 + 8 * s.g + t] = gdir[t];
-  }
-  // ---- encodings -> d pts, d view dir: lane group g owns pairs p = 4 i + g (as the forward)
-  float dx[3] = {0.f, 0.f, 0.f}, dv[3] = {0.f, 0.f, 0.f};
+  // ---- encodings -> d pts: lane group g owns pairs p = 4 i + g (as the forward)
+  float dx[3] = {0.f, 0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int p = 4 * i + s.g;
     if (p < 30) {
       const int d = p % 3, k = p / 3;
       float sn, cs;
-      sincosf(__fmul_rn(pick3(in.x, d), a.fx[k]), &sn, &cs);
-      add3(dx, d, a.fx[k] * (genc[i] * cs - genc[8 + i] * sn));
+      const float f = clds[kCFreq + k];
+      sincosf(__fmul_rn(pick3(in.x, d), f), &sn, &cs);
+      add3(dx, d, f * (genc[i] * cs - genc[8 + i] * sn));
     } else if (s.g == 2) {  // raw inputs x0 (k-step 7), x1 (k-step 15)
       dx[0] += genc[7];
       dx[1] += genc[15];
@@ -878,24 +988,15 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
     }
   }
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const int p = 4 * i + s.g, d = p % 3, k = p / 3;
-    float sn, cs;
-    sincosf(__fmul_rn(pick3(in.vd, d), a.fd[k]), &sn, &cs);
-    add3(dv, d, a.fd[k] * (gdir[i] * cs - gdir[3 + i] * sn));
-  }
-  add3(dv, s.g, gdir[6]);  // s.g == 3 adds nothing
-#pragma unroll
   for (int d = 0; d < 3; ++d) {
     dx[d] += __shfl_xor(dx[d], 16);
     dx[d] += __shfl_xor(dx[d], 32);
-    dv[d] += __shfl_xor(dv[d], 16);
-    dv[d] += __shfl_xor(dv[d], 32);
   }
   const int64_t S = a.n_samples;
   if constexpr (MODE == kFromRayZ) {
     // pts = ro + rd z (z detached): d ro += d pts, d rd += d pts z.  With S % 16 == 0 the
     // wave's 16 samples are one ray: sum over them first, one atomic per value.
+    const float zv = a.z[rc];
     float gro[3], grd[3];
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
@@ -919,23 +1020,13 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
       if (a.d_rd)
         for (int d = 0; d < 3; ++d) atomicAdd(a.d_rd + 3 * ray + d, grd[d]);
     }
+  } else {
+    if (valid && s.g == 0 && a.d_pts)
+      for (int d = 0; d < 3; ++d) a.d_pts[3 * rc + d] = dx[d];
   }
-  if (valid && s.g == 0) {
-    const int64_t ray = rc / S, smp = rc - ray * S;
-    if constexpr (MODE != kFromRayZ) {
-      if (a.d_pts)
-        for (int d = 0; d < 3; ++d) a.d_pts[3 * rc + d] = dx[d];
-    }
-    if (a.d_rd) {
-      // Q1 view direction vd = rd[dray] / |rd[dray]|: d rd[dray] += (g - vd (vd . g)) / |rd[dray]|
-      const int64_t base = (ray / a.chunk_rows) * a.chunk_rows;
-      const int64_t rcnt = min(a.chunk_rows, a.n_rays - base);
-      const int64_t dray = base + ((ray - base) * S + smp) % rcnt;
-      const float d0 = a.rd[3 * dray], d1 = a.rd[3 * dray + 1], d2 = a.rd[3 * dray + 2];
-      const float nrm = sqrtf(d0 * d0 + d1 * d1 + d2 * d2);
-      const float dot = in.vd[0] * dv[0] + in.vd[1] * dv[1] + in.vd[2] * dv[2];
-      for (int d = 0; d < 3; ++d) atomicAdd(a.d_rd + 3 * dray + d, (dv[d] - in.vd[d] * dot) / nrm);
-    }
+  if (valid && s.g == 0 && a.d_rd) {
+    const int64_t dray = q1_dir_ray(a, rc);
+    for (int d = 0; d < 3; ++d) atomicAdd(a.d_rd + 3 * dray + d, grd_q1[d]);
   }
 }
 
@@ -949,8 +1040,10 @@ __global__ __launch_bounds__(kThreads, 2) void field_w16_bwd_kernel(FieldArgs a)
   s.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   s.wsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.packed), 0, kPackedFloats * 4, 0x00020000);
   s.voff = static_cast<unsigned>(s.wave * 64 + s.lane) * 16u;
+  s.poff = static_cast<unsigned>(s.wave * 16 + (s.lane & 15)) * 1024u + 16u * s.g;
+  s.gbase = static_cast<unsigned>(16 * rev4(s.lane & 15) + 4 * s.g) * 4u;
   float* grow = blds + kBGacc + s.wave * kCbStride;
-  for (int k = threadIdx.x; k < kConsts; k += kThreads) blds[k] = a.packed[kStreamFloats + k];
+  load_consts(a, blds);
   for (int k = threadIdx.x; k < kBwdLdsFloats - kBGacc; k += kThreads) blds[kBGacc + k] = 0.0f;
   __syncthreads();
   dma_chunk(s, lds, 0);
@@ -966,7 +1059,8 @@ __global__ __launch_bounds__(kThreads, 2) void field_w16_bwd_kernel(FieldArgs a)
   __builtin_amdgcn_s_waitcnt(0x0F70);
   if (cur_code >= 0) flush_gcode(s, a, grow, cur_code);
   if constexpr (TRAIN) {
-    __syncthreads();  // every wave's bias atomics landed
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's (asm) bias atomics landed
+    __syncthreads();                     // ... and every other wave's
     for (int k = threadIdx.x; k < 3 * 256; k += kThreads) {
       const float v = blds[kBBias + k];
       if (v != 0.0f && a.gbias[k >> 8]) atomicAdd(a.gbias[k >> 8] + (k & 255), v);

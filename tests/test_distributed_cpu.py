@@ -65,3 +65,37 @@ def test_gather_rows_uneven_shares(world, tmp_path):
     got = np.load(out)
     assert got.shape == (1001, 3)
     assert np.array_equal(got[:, 0], np.arange(1001, dtype=np.float32))
+
+
+def _views_worker(rank, world, port, n_pix, n_views, out_path):
+    import torch.distributed as dist
+    from codenerf.nerf import gather_views
+    from codenerf.utils import split_sizes
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        per, _ = split_sizes(n_pix, world)
+        start = sum(per[:rank])
+        # pixel value = 1000 * view + pixel id, this rank's slice of every view, view-major (bench.py)
+        v = torch.arange(n_views, dtype=torch.float32)[:, None] * 1000
+        px = torch.arange(start, start + per[rank], dtype=torch.float32)[None, :]
+        rows = (v + px).reshape(-1, 1).repeat(1, 3)
+        out = gather_views(rows, per, rank, n_views)
+        if rank == 0:
+            np.save(out_path, out.numpy())
+        else:
+            assert out is None
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_pix", [(2, 16384), (3, 1000), (4, 16384), (4, 1001)])
+def test_gather_views_layout(world, n_pix, tmp_path):
+    """bench.py's multi-view gather (every view split over the ranks as parallel_image_render splits
+    one, nerf/__init__.py:179-218, rank 0 re-interleaving the blocks), with uneven Q5 shares."""
+    out = str(tmp_path / "v.npy")
+    mp.start_processes(_views_worker, args=(world, _free_port(), n_pix, 5, out), nprocs=world, join=True,
+                       start_method="spawn")
+    got = np.load(out)
+    want = (np.arange(5, dtype=np.float32)[:, None] * 1000 + np.arange(n_pix, dtype=np.float32)[None, :])
+    assert got.shape == (5, n_pix, 3)
+    assert np.array_equal(got[..., 0], want) and np.array_equal(got[..., 2], want)

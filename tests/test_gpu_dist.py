@@ -54,3 +54,97 @@ def test_parallel_image_render_rccl(dev, rccl_world1):
     cfg = NS(is_distributed=True, gpus=1, nerf=NS(validation=NS(chunksize=50)))
     rgb = parallel_image_render(cfg, g["pose"], [g["z_s"], g["z_t"]], models, (rs, ps), embedders(dev), dev)
     assert maxdiff(rgb, g["nc8_n1_rgb"]) <= 1e-4
+
+
+def _train_setup(dev, seed=0):
+    from test_gpu_train import _opt_cfg, _train_models
+    torch.manual_seed(seed)
+    return _train_models(dev, 3)
+
+
+def _chunk(dev, n=256, obj=1, seed=4):
+    g = torch.Generator().manual_seed(seed)
+    ro = (torch.randn(n, 3, generator=g) * 0.1 + torch.tensor([0.0, 0.0, 1.3])).to(dev)
+    rd = (torch.randn(n, 3, generator=g) * 0.2 + torch.tensor([0.0, 0.0, -1.0])).to(dev)
+    ids = torch.full((n,), obj, dtype=torch.int64, device=dev)
+    return ro, rd, ids, torch.rand(n, 4, generator=g).to(dev)
+
+
+def test_adamw_allreduce_broadcast_rccl(dev, rccl_world1):
+    """codenerf.optim.AdamW's data-parallel pieces over RCCL (world 1: the collectives run): the
+    flat all-reduce leaves the averaged gradients (here: themselves) and the flags' None-ness, the
+    broadcast leaves the parameters; a step after them equals a step without them."""
+    from codenerf.optim import AdamW
+    g = torch.Generator().manual_seed(0)
+    base = [torch.randn(64, 32, generator=g), torch.randn(7, generator=g), torch.randn(3, 5, generator=g)]
+    runs = []
+    for collective in (False, True):
+        ps = [torch.nn.Parameter(t.clone().to(dev)) for t in base]
+        opt = AdamW([{"params": ps[:2]}, {"params": ps[2:], "lr": 1e-3}], lr=1e-4)
+        if collective:
+            opt.broadcast_params(0)
+        gg = torch.Generator().manual_seed(1)
+        for it in range(3):
+            opt.zero_grad()
+            for i, p in enumerate(ps):
+                gr = torch.randn(p.shape, generator=gg).to(dev)
+                if not (it == 1 and i == 1):      # parameter 1 has no gradient in step 1
+                    p.grad = gr
+            if collective:
+                opt.allreduce_grads()
+                assert (ps[1].grad is None) == (it == 1)
+            opt.step()
+        torch.cuda.synchronize()
+        runs.append([p.detach().clone() for p in ps])
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)
+
+
+def test_ddp_drop_in_rccl(dev, rccl_world1):
+    """INTEGRATION.md's drop-in under the reference's DDP (util.py:139-142): the three modules wrapped in
+    torch.nn.parallel.DistributedDataParallel on an RCCL group, stepped by torch.optim.AdamW (the
+    reference's optimiser, util.py:147-172) through train_minibatch (train.py:96-114): every
+    gradient reaches DDP's hooks (its reducer all-reduces them) and the gradients and the updated
+    parameters equal the unwrapped path's bit for bit (world 1: the average is the gradient)."""
+    from torch.distributed.algorithms.ddp_comm_hooks import default_hooks
+    from torch.nn.parallel import DistributedDataParallel as DDP
+    from codenerf import train as T
+    from codenerf.nerf import PointSampler
+    from test_gpu_train import embedders as embs
+    ps = PointSampler(16, 16, 0.8, 1.8, spacing_mode="lindepth", perturb=False, dtype=torch.float32, device=dev)
+    out = []
+    for wrap in (False, True):
+        models = _train_setup(dev)
+        if wrap:
+            models = {k: DDP(m, device_ids=[dev.index]) for k, m in models.items()}
+        groups = [{"params": list(models["nerf_coarse"].parameters())},
+                  {"params": list(models["nerf_fine"].parameters())},
+                  {"params": list(models["embedding"].parameters()), "lr": 1e-3}]
+        opt = torch.optim.AdamW(groups, lr=1e-4)
+        sched = torch.optim.lr_scheduler.LambdaLR(opt, lambda e: 0.1 ** (e / 5000000))
+        hooked = []
+        if wrap:   # DDP's reducer all-reduces the buckets; count the communication hook's calls
+            def hook(state, bucket):
+                hooked.append(bucket.buffer().numel())
+                return default_hooks.allreduce_hook(None, bucket)
+            for m in models.values():
+                m.register_comm_hook(None, hook)
+        grads = []
+        for step in range(2):
+            ro, rd, ids, tgt = _chunk(dev, obj=step + 1, seed=4 + step)
+            T.train_minibatch(models, opt, sched, ps, embs(dev), ro, rd, ids, tgt, 1e-5, is_distributed=wrap)
+            grads.append({f"{k}.{n}": p.grad.detach().clone() for k, m in models.items()
+                          for n, p in (m.module if wrap else m).named_parameters() if p.grad is not None})
+        torch.cuda.synchronize()
+        params = {f"{k}.{n}": p.detach().clone() for k, m in models.items()
+                  for n, p in (m.module if wrap else m).named_parameters()}
+        out.append((grads, params, hooked))
+    (g0, p0, _), (g1, p1, hooked) = out
+    n_params = sum(v.numel() for v in p1.values())
+    assert sum(hooked) == 2 * n_params, (sum(hooked), n_params)   # every gradient went through the reducer
+    for a, b in zip(g0, g1):
+        assert a.keys() == b.keys()
+        for k in a:
+            assert torch.equal(a[k], b[k]), k
+    for k in p0:
+        assert torch.equal(p0[k], p1[k]), k

@@ -316,3 +316,30 @@ def test_train_iteration_runs(dev):
     assert all(np.isfinite(float(lg["total_loss"])) for lg in logs)
     assert any(not torch.equal(a, b.detach()) for a, b in zip(before, models["nerf_fine"].parameters()))
     assert sched.last_epoch == 3
+
+
+def test_train_minibatch_deterministic(dev):
+    """fp32 chunk steps with one object per chunk (every C3 step) are bit-reproducible: g_code is
+    formed by fixed-order column sums folded into the dW GEMMs (no float atomics in the step), so two
+    identical model sets stepped on the same chunks end bit-identical -- what a checkpoint resume
+    relies on (train.py:129-138 + util.py:175-213)."""
+    from codenerf import train as T
+    from codenerf.nerf import PointSampler
+    runs = []
+    for _ in range(2):
+        torch.manual_seed(3)
+        models = _train_models(dev, 3)
+        opt, sched = T.prepare_optimizer(_opt_cfg(), models)
+        ps = PointSampler(16, 16, 0.8, 1.8, spacing_mode="lindepth", perturb=True, dtype=torch.float32, device=dev)
+        g = torch.Generator().manual_seed(5)
+        for step in range(3):
+            n = 256
+            ro = (torch.randn(n, 3, generator=g) * 0.1 + torch.tensor([0.0, 0.0, 1.3])).to(dev)
+            rd = (torch.randn(n, 3, generator=g) * 0.2 + torch.tensor([0.0, 0.0, -1.0])).to(dev)
+            ids = torch.full((n,), step % 3, dtype=torch.int64, device=dev)
+            tgt = torch.rand(n, 4, generator=g).to(dev)
+            T.train_minibatch(models, opt, sched, ps, embedders(dev), ro, rd, ids, tgt, 1e-5)
+        torch.cuda.synchronize()
+        runs.append({f"{k}.{n_}": p.detach().clone() for k, m in models.items() for n_, p in m.named_parameters()})
+    for k in runs[0]:
+        assert torch.equal(runs[0][k], runs[1][k]), k

@@ -24,7 +24,9 @@ def timed(fn, iters=10):
     return ms[len(ms) // 2]
 
 
-def main(precision="f32", n=8192, s=64):
+def main(precision="f32", n=int(os.environ.get("VT_RAYS", 8192)), s=64):
+    only = set(filter(None, os.environ.get("VT_ONLY", "").split(",")))
+    iters = int(os.environ.get("VT_ITERS", 10))
     from codenerf import ops, synthetic
     from codenerf.models import CodeNeRFModel
     dev = torch.device("cuda", 0)
@@ -43,20 +45,27 @@ def main(precision="f32", n=8192, s=64):
     pkt = ops.mlp_pack(params, "bf16x3_t" if x3 else "f32_w16_t")
     flop = n * s * 572416
     out = {}
-    out["fwd"] = timed(lambda: ops.radiance_field(pk, cb, rd, s, n, fx, fd, ro=ro, z=z,
-                                                  precision="bf16x3" if x3 else "f32_w16"))
+    want = lambda k: not only or k in only
+    if want("fwd"):
+        out["fwd"] = timed(lambda: ops.radiance_field(pk, cb, rd, s, n, fx, fd, ro=ro, z=z,
+                                                  precision="bf16x3" if x3 else "f32_w16"), iters)
     raw, masks = ops.radiance_field_masks(pk, cb, rd, s, n, fx, fd, ro=ro, z=z, precision=precision)
-    out["fwd_masks"] = timed(lambda: ops.radiance_field_masks(pk, cb, rd, s, n, fx, fd, ro=ro, z=z, precision=precision))
-    out["fwd_train"] = timed(lambda: ops.radiance_field_train_w16(pk, cb, rd, s, n, fx, fd, ro=ro, z=z,
-                                                                  precision=precision))
+    if want("fwd_masks"):
+        out["fwd_masks"] = timed(lambda: ops.radiance_field_masks(pk, cb, rd, s, n, fx, fd, ro=ro, z=z,
+                                                                  precision=precision), iters)
+    if want("fwd_train"):
+        out["fwd_train"] = timed(lambda: ops.radiance_field_train_w16(pk, cb, rd, s, n, fx, fd, ro=ro, z=z,
+                                                                      precision=precision), iters)
     d_raw = torch.randn(n, s, 4, generator=g).to(dev) * 1e-3
-    out["bwd_eval"] = timed(lambda: ops.field_backward_x3(pkt, masks, d_raw, n, s, n, 1, fx, fd, rd=rd, ro=ro, z=z,
-                                                          want_ro=True, want_rd=True, precision=precision))
+    if want("bwd_eval"):
+        out["bwd_eval"] = timed(lambda: ops.field_backward_x3(pkt, masks, d_raw, n, s, n, 1, fx, fd, rd=rd, ro=ro, z=z,
+                                                          want_ro=True, want_rd=True, precision=precision), iters)
     _, saved, tmasks = ops.radiance_field_train_w16(pk, cb, rd, s, n, fx, fd, ro=ro, z=z, precision=precision)
     pg = [torch.zeros_like(p) for p in params]
-    out["bwd_train"] = timed(lambda: ops.field_backward_train(pkt, params, tmasks, saved, None, d_raw, n, s, n, 1,
+    if want("bwd_train"):
+        out["bwd_train"] = timed(lambda: ops.field_backward_train(pkt, params, tmasks, saved, None, d_raw, n, s, n, 1,
                                                               fx, fd, rd=rd, ro=ro, z=z, param_grads=pg,
-                                                              want_ro=True, want_rd=True, precision=precision))
+                                                              want_ro=True, want_rd=True, precision=precision), iters)
     for k, v in out.items():
         print(json.dumps({"precision": precision, "variant": k, "samples": n * s, "ms": v,
                           "tflops_fp32_equiv": flop / (v * 1e-3) / 1e12}))
