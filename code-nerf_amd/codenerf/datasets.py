@@ -33,8 +33,15 @@ from . import ops
 
 
 def _decode(path) -> np.ndarray:
+    """imageio.imread of an 8-bit PNG (dataset.py:71): RGB / RGBA / L / LA as stored; a palette
+    image expanded to RGBA when it has transparency, else RGB (imageio's Pillow plugin does the
+    same); anything else (16-bit, float) is refused rather than misread."""
     from PIL import Image
     with Image.open(path) as im:
+        if im.mode == "P":
+            im = im.convert("RGBA" if "transparency" in im.info else "RGB")
+        if im.mode not in ("RGB", "RGBA", "L", "LA"):
+            raise ValueError(f"{path}: PNG mode {im.mode} is not an 8-bit image the SRN loader reads")
         return np.asarray(im)
 
 

@@ -181,12 +181,15 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const float* base, 
 // The tile's mask block: kMaskLayers x 64 uint2 per wave.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t mask_rsrc(const unsigned* masks, int64_t tile);
 
-// The 16 blocks' column offsets go in soffset: as part of the VGPR offset, LICM hoists the 16
-// sums out of the tile loop into 16 VGPRs instead of the instruction's immediate field.
+// The 16 blocks' column offsets fold into the instructions' immediate field because the lane
+// offset is "fresh" here (otherwise LICM hoists the 16 sums out of the tile loop into VGPRs, or,
+// as soffsets, into 16 SGPRs that then spill into VGPR lanes).
+__device__ __forceinline__ int fresh(int v);
 __device__ __forceinline__ void store_plane(const State& s, __amdgpu_buffer_rsrc_t r, const floatx4* v) {
+  const unsigned off = static_cast<unsigned>(fresh(static_cast<int>(s.poff)));
 #pragma unroll
   for (int ob = 0; ob < 16; ++ob)
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, v[ob]), r, s.poff, 64 * ob, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, v[ob]), r, off + 64u * ob, 0, 0);
 }
 
 
@@ -236,10 +239,18 @@ __device__ __forceinline__ void step_pattern() {
   __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
 }
 
+// Nothing to issue at a chunk's barrier.
+struct NoPost {
+  __device__ __forceinline__ void operator()() const {}
+};
+
 // One 16-block chunk of NS k-steps; the B operand of k-step T is getb(T) (compile time).
-// The last k-step reads the next chunk's first fragments into s.pre.
-template <int NS, typename GetB>
-__device__ __forceinline__ void chunk16(State& s, float4* lds, int c, GetB getb) {
+// The last k-step reads the next chunk's first fragments into s.pre.  `post` runs right after
+// the chunk's barrier, before its DMA: the previous layer's plane / mask stores go there (the
+// layer input they save is this layer's B operand, live anyway), so they have a whole chunk until
+// the next barrier's vmcnt counts them -- at the layer epilogue they had half of one.
+template <int NS, typename GetB, typename Post = NoPost>
+__device__ __forceinline__ void chunk16(State& s, float4* lds, int c, GetB getb, Post post = Post{}) {
   const float4* slot = lds + (c & (kRing - 1)) * kChunkQuads + s.lane;
   const float4* nslot = lds + ((c + 1) & (kRing - 1)) * kChunkQuads + s.lane;
   floatx4 a0[4], a1[4];
@@ -255,6 +266,7 @@ __device__ __forceinline__ void chunk16(State& s, float4* lds, int c, GetB getb)
     __builtin_amdgcn_sched_barrier(0);                              \
     if constexpr ((T) == 3) {                                       \
       chunk_barrier();                                              \
+      post();                                                       \
       dma_chunk(s, lds, c + 3);                                     \
     }                                                               \
   }
@@ -287,8 +299,9 @@ struct ArrB {
 };
 
 // A 256-input layer: 8 chunks, B from s.act.
-__device__ __forceinline__ void layer256(State& s, float4* lds, int& c) {
-  chunk16<8>(s, lds, c + 0, ActB<0>{s});
+template <typename Post = NoPost>
+__device__ __forceinline__ void layer256(State& s, float4* lds, int& c, Post post = Post{}) {
+  chunk16<8>(s, lds, c + 0, ActB<0>{s}, post);
   chunk16<8>(s, lds, c + 1, ActB<8>{s});
   chunk16<8>(s, lds, c + 2, ActB<16>{s});
   chunk16<8>(s, lds, c + 3, ActB<24>{s});
@@ -299,10 +312,20 @@ __device__ __forceinline__ void layer256(State& s, float4* lds, int& c) {
   c += 8;
 }
 
-// Bias-initialise the 16 accumulators from a 256-vector (row 16 ob + 4 g + r).
+// A per-lane value the compiler must treat as new here: the lane-derived addresses built from it
+// are formed where they are used instead of being hoisted out of the tile loop (loop-invariant,
+// so LICM would keep e.g. all 16 block addresses of a bias vector in VGPRs for the whole kernel).
+__device__ __forceinline__ int fresh(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+// Bias-initialise the 16 accumulators from a 256-vector (row 16 ob + 4 g + r): one address, the
+// blocks at immediate offsets.
 __device__ __forceinline__ void bias_from(State& s, const float* v) {
+  const floatx4* p = reinterpret_cast<const floatx4*>(v) + fresh(s.g);
 #pragma unroll
-  for (int ob = 0; ob < 16; ++ob) s.acc[ob] = *reinterpret_cast<const floatx4*>(v + 16 * ob + 4 * s.g);
+  for (int ob = 0; ob < 16; ++ob) s.acc[ob] = p[4 * ob];
 }
 
 // The code-bias vector at `off` of this lane's code row: the wave's LDS copy, or (codes
@@ -335,13 +358,13 @@ __device__ __forceinline__ unsigned mask_soff(const State& s, int ml) {
 // one bit per feature, highest first: a constant 1 << n per bit would be a VOP3 literal, which
 // gfx9 encodings lack, so the compiler kept all 32 of them in VGPRs across the tile loop.
 template <bool MASKS>
-__device__ __forceinline__ void relu_act(State& s, const FieldArgs& a, int64_t tile, int ml) {
+__device__ __forceinline__ uint2v relu_act(State& s) {
 #pragma unroll
   for (int ob = 0; ob < 16; ++ob)
 #pragma unroll
     for (int r = 0; r < 4; ++r) s.act[ob][r] = fmaxf(s.acc[ob][r], 0.0f);
+  unsigned w[2] = {0u, 0u};
   if constexpr (MASKS) {
-    unsigned w[2] = {0u, 0u};
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -349,17 +372,31 @@ __device__ __forceinline__ void relu_act(State& s, const FieldArgs& a, int64_t t
         const float v = s.acc[8 * h + (k >> 2)][k & 3];
         w[h] = (w[h] << 1) | (v > 0.0f ? 1u : 0u);
       }
-    __builtin_amdgcn_raw_buffer_store_b64(uint2v{w[0], w[1]}, mask_rsrc(a.masks, tile), 8u * s.lane,
-                                          mask_soff(s, ml), 0);
   }
+  return uint2v{w[0], w[1]};
 }
+
+// The stores a layer's input leaves behind (forward): its ReLU mask words (MASKS, slot ml; ml < 0:
+// none) and, SAVE, its activation plane -- issued at the next chunk barrier (chunk16's `post`).
+template <bool MASKS, bool SAVE>
+struct LayerStores {
+  const State& s;
+  const FieldArgs& a;
+  int64_t tile;
+  int ml, plane;
+  uint2v w;
+  __device__ __forceinline__ void operator()() const {
+    if constexpr (MASKS) {
+      if (ml >= 0)
+        __builtin_amdgcn_raw_buffer_store_b64(w, mask_rsrc(a.masks, tile), 8u * s.lane, mask_soff(s, ml), 0);
+    }
+    if constexpr (SAVE) store_plane(s, plane_rsrc(a.save, plane, a.m, tile), s.act);
+  }
+};
 
 // Training forward: the post-activation rows the weight gradients read (h1, h2, feat, v1, v2 as
 // (5, m, 256) planes, feature 16 ob + 4 g + r: one 16-B store per block per lane).
-template <bool SAVE>
-__device__ __forceinline__ void save_act(const State& s, const FieldArgs& a, int plane, int64_t tile) {
-  if constexpr (SAVE) store_plane(s, plane_rsrc(a.save, plane, a.m, tile), s.act);
-}
+
 
 template <int MODE, bool MASKS, bool SAVE = false>
 __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4* lds, float* clds, float* crow_lds,
@@ -405,9 +442,10 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
 
   // ---- encodings: lane group g owns pairs p = 4 i + g
   if constexpr (MODE != kFromEncoded) {
+    const int g = fresh(s.g);  // the pair indices below are formed here, not held across tiles
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const int p = 4 * i + s.g;
+      const int p = 4 * i + g;
       const int pc = p < 30 ? p : 0;
       const float arg = __fmul_rn(pick3(in.x, pc % 3), clds[kCFreq + pc / 3]);
       float sn, cs;
@@ -421,7 +459,7 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
     }
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      const int p = 4 * i + s.g;
+      const int p = 4 * i + g;
       const float arg = __fmul_rn(pick3(in.vd, p % 3), clds[kCFreq + 10 + p / 3]);
       sincosf(arg, &s.denc[i], &s.denc[3 + i]);
     }
@@ -437,20 +475,23 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
 
   // ---- layer_xyz2, fc_out, layer_dir1 (+ view-dir chunk), layer_dir2
   for (int layer = kXyz2; layer <= kDir2; ++layer) {
-    // activation of the previous layer's outputs: ReLU, none after fc_out (feat)
+    // activation of the previous layer's outputs: ReLU, none after fc_out (feat); its mask words
+    // and its plane (h1, h2, feat, v1) are stored at this layer's first chunk barrier
+    uint2v mw = uint2v{0u, 0u};
     if (layer == kDir1) {
 #pragma unroll
       for (int ob = 0; ob < 16; ++ob) s.act[ob] = s.acc[ob];
     } else {
-      relu_act<MASKS>(s, a, tile, layer == kXyz2 ? 0 : (layer == kOut ? 1 : 2));
+      mw = relu_act<MASKS>(s);
     }
-    save_act<SAVE>(s, a, layer - kXyz2, tile);  // h1, h2, feat, v1
+    const LayerStores<MASKS, SAVE> st{s, a, tile, layer == kXyz2 ? 0 : (layer == kOut ? 1 : (layer == kDir2 ? 2 : -1)),
+                                     layer - kXyz2, mw};
     if (layer == kOut) {
       // sigma = fc_out row 0 . [h2, zs2] + b: the h2 part here, the code part from cn_code_bias
       float sg = 0.0f;
 #pragma unroll
       for (int ob = 0; ob < 16; ++ob) {
-        const floatx4 w = *reinterpret_cast<const floatx4*>(clds + kCSig + 64 * s.g + 4 * ob);
+        const floatx4 w = *reinterpret_cast<const floatx4*>(clds + kCSig + 64 * fresh(s.g) + 4 * ob);
 #pragma unroll
         for (int r = 0; r < 4; ++r) sg = fmaf(w[r], s.act[ob][r], sg);
       }
@@ -460,7 +501,7 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
     else if (layer == kOut) bias_code(s, a, crow_lds, kCbFeat);
     else bias_from(s, clds + (layer == kDir1 ? kCBD1 : kCBD2));
     __builtin_amdgcn_sched_barrier(0);
-    layer256(s, lds, c);
+    layer256(s, lds, c, st);
     if (layer == kDir1) {
       chunk16<7>(s, lds, c, ArrB<0>{s.denc});
       c += 1;
@@ -468,8 +509,7 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
   }
 
   // ---- fc_rgb (256 -> 3): one chunk, 64 k-steps of block 0 in 4 chains
-  relu_act<MASKS>(s, a, tile, 3);
-  save_act<SAVE>(s, a, 4, tile);  // v2
+  const LayerStores<MASKS, SAVE> st_v2{s, a, tile, 3, 4, relu_act<MASKS>(s)};  // v2: at the rgb chunk's barrier
   {
     float b0 = 0.0f, b1 = 0.0f, b2 = 0.0f, bs = 0.0f;
     if (s.uniform_code) {
@@ -515,6 +555,7 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
     __builtin_amdgcn_sched_barrier(0);                                                   \
     if constexpr ((G) == 1) {                                                            \
       chunk_barrier();                                                                   \
+      st_v2();                                                                           \
       dma_chunk(s, lds, c + 3);                                                          \
     }                                                                                    \
   }
@@ -769,7 +810,8 @@ __device__ __forceinline__ void mfma_narrow(State& s, const floatx4* a) {
 }
 
 // A narrow chunk (2 blocks x 64 k-steps, B from s.act) into s.acc2, on chunk16's schedule.
-__device__ __forceinline__ void chunk_narrow(State& s, float4* lds, int c) {
+template <typename Post = NoPost>
+__device__ __forceinline__ void chunk_narrow(State& s, float4* lds, int c, Post post = Post{}) {
   const float4* slot = lds + (c & (kRing - 1)) * kChunkQuads + s.lane;
   const float4* nslot = lds + ((c + 1) & (kRing - 1)) * kChunkQuads + s.lane;
   floatx4 a0[4], a1[4];
@@ -785,6 +827,7 @@ __device__ __forceinline__ void chunk_narrow(State& s, float4* lds, int c) {
     __builtin_amdgcn_sched_barrier(0);                              \
     if constexpr ((T) == 3) {                                       \
       chunk_barrier();                                              \
+      post();                                                       \
       dma_chunk(s, lds, c + 3);                                     \
     }                                                               \
   }
@@ -822,9 +865,15 @@ __device__ __forceinline__ float* bias_row(float4* lds, int l) {
 // plane `plane` of a.dpre: 0 layer_dir2, 1 layer_dir1, 2 fc_out rows 1.. (d feat), 3 layer_xyz2,
 // 4 layer_xyz1.
 template <bool TRAIN>
-__device__ __forceinline__ void save_dpre(const State& s, const FieldArgs& a, int plane, int64_t tile) {
-  if constexpr (TRAIN) store_plane(s, plane_rsrc(a.dpre, plane, a.m, tile), s.act);
-}
+struct DpreStore {
+  const State& s;
+  const FieldArgs& a;
+  int64_t tile;
+  int plane;
+  __device__ __forceinline__ void operator()() const {
+    if constexpr (TRAIN) store_plane(s, plane_rsrc(a.dpre, plane, a.m, tile), s.act);
+  }
+};
 
 // The Q1 view-direction row of sample row rc (nerf/__init__.py:127-128; decode_sample's map).
 __device__ __forceinline__ int64_t q1_dir_ray(const FieldArgs& a, int64_t rc) {
@@ -885,19 +934,19 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   c = kTDir2;
   const float dsig = dr.w;
   // ---- layer_dir2^T (m_v2), layer_dir1^T (m_v1)
+  // (each layer's masked input gradient -- the dW GEMMs' dPre plane -- is stored at the layer's first
+  // chunk barrier: DpreStore as chunk16's `post`)
   mask_act(s, m_v2);
-  save_dpre<TRAIN>(s, a, 0, tile);
   if (TRAIN && a.gbias[0]) gcode_add64<0>(s, bias_row(lds, 0), s.act);
   zero_acc(s);
   __builtin_amdgcn_sched_barrier(0);
-  layer256(s, lds, c);
+  layer256(s, lds, c, DpreStore<TRAIN>{s, a, tile, 0});
   const uint2 m_h2 = load_mask(s, a, tile, 1), m_h1 = load_mask(s, a, tile, 0);
   mask_act(s, m_v1);
-  save_dpre<TRAIN>(s, a, 1, tile);
   if (TRAIN && a.gbias[0]) gcode_add64<0>(s, bias_row(lds, 1), s.act);
   zero_acc(s);
   __builtin_amdgcn_sched_barrier(0);
-  layer256(s, lds, c);
+  layer256(s, lds, c, DpreStore<TRAIN>{s, a, tile, 1});
   // ---- the view-direction rows of layer_dir1^T (narrow chunk, B = m_v1 . d v1 still in act)
 #pragma unroll
   for (int q = 0; q < 4; ++q) s.acc2[q] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -914,15 +963,16 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
       gdir[4 + r] = s.acc2[2][r] + s.acc2[3][r];
     }
     float dv[3] = {0.f, 0.f, 0.f};
+    const int g = fresh(s.g);
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      const int p = 4 * i + s.g, d = p % 3, k = p / 3;
+      const int p = 4 * i + g, d = p % 3, k = p / 3;
       const float f = clds[kCFreq + 10 + k];
       float sn, cs;
       sincosf(__fmul_rn(pick3(in.vd, d), f), &sn, &cs);
       add3(dv, d, f * (gdir[i] * cs - gdir[3 + i] * sn));
     }
-    add3(dv, s.g, gdir[6]);  // s.g == 3 adds nothing
+    add3(dv, g, gdir[6]);  // g == 3 adds nothing
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
       dv[d] += __shfl_xor(dv[d], 16);
@@ -935,32 +985,30 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   // ---- fc_out^T: B = d feat (no activation), init = fc_out row 0 (h2 part) x d sigma
 #pragma unroll
   for (int ob = 0; ob < 16; ++ob) s.act[ob] = s.acc[ob];
-  save_dpre<TRAIN>(s, a, 2, tile);
   if (gc) gcode_add64<kCbFeat>(s, grow, s.act);
 #pragma unroll
   for (int ob = 0; ob < 16; ++ob) {
-    const floatx4 w = *reinterpret_cast<const floatx4*>(clds + kTSig + 64 * s.g + 4 * ob);
+    const floatx4 w = *reinterpret_cast<const floatx4*>(clds + kTSig + 64 * fresh(s.g) + 4 * ob);
     s.acc[ob] = w * dsig;
   }
   __builtin_amdgcn_sched_barrier(0);
-  layer256(s, lds, c);
+  layer256(s, lds, c, DpreStore<TRAIN>{s, a, tile, 2});
   // ---- layer_xyz2^T (m_h2): its masked input gradient is the code term's too
   mask_act(s, m_h2);
-  save_dpre<TRAIN>(s, a, 3, tile);
   if (gc) gcode_add64<kCbXyz2>(s, grow, s.act);
   zero_acc(s);
   __builtin_amdgcn_sched_barrier(0);
-  layer256(s, lds, c);
+  layer256(s, lds, c, DpreStore<TRAIN>{s, a, tile, 3});
   // ---- layer_xyz1^T (m_h1): encoding k-steps 0-7, then 8-15
   mask_act(s, m_h1);
-  save_dpre<TRAIN>(s, a, 4, tile);
   if (TRAIN && a.gbias[0]) gcode_add64<0>(s, bias_row(lds, 2), s.act);
   float genc[16];
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) s.acc2[q] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
-    chunk_narrow(s, lds, c);
+    if (half == 0) chunk_narrow(s, lds, c, DpreStore<TRAIN>{s, a, tile, 4});
+    else chunk_narrow(s, lds, c);
     c += 1;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -971,16 +1019,17 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
 
   // ---- encodings -> d pts: lane group g owns pairs p = 4 i + g (as the forward)
   float dx[3] = {0.f, 0.f, 0.f};
+  const int g = fresh(s.g);
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const int p = 4 * i + s.g;
+    const int p = 4 * i + g;
     if (p < 30) {
       const int d = p % 3, k = p / 3;
       float sn, cs;
       const float f = clds[kCFreq + k];
       sincosf(__fmul_rn(pick3(in.x, d), f), &sn, &cs);
       add3(dx, d, f * (genc[i] * cs - genc[8 + i] * sn));
-    } else if (s.g == 2) {  // raw inputs x0 (k-step 7), x1 (k-step 15)
+    } else if (g == 2) {  // raw inputs x0 (k-step 7), x1 (k-step 15)
       dx[0] += genc[7];
       dx[1] += genc[15];
     } else {                // x2 (k-step 7)

@@ -45,8 +45,9 @@ def _image(seed: int, channels: int) -> np.ndarray:
     return img
 
 
-def write_tree(root: str, name: str = "cars") -> str:
-    """Write the tree under root; returns the dataset basedir (root/srn_<name>)."""
+def write_tree(root: str, name: str = "cars", channels=None) -> str:
+    """Write the tree under root; returns the dataset basedir (root/srn_<name>).  ``channels``: 3 or 4
+    for every PNG (one image shape per split, as the real SRN release), None: alternating."""
     from PIL import Image
     base = os.path.join(root, f"srn_{name}")
     for stage, n_obj in STAGES.items():
@@ -58,7 +59,7 @@ def write_tree(root: str, name: str = "cars") -> str:
             with open(os.path.join(obj, "intrinsics.txt"), "w") as f:
                 f.write(f"{focal} {SIZE // 2}. {SIZE // 2 + 1}. 0.\n0. 0. 0.\n1.\n{SIZE} {SIZE}\n")
             for j in range(VIEWS):
-                ch = 4 if (i + j) % 2 else 3
+                ch = channels or (4 if (i + j) % 2 else 3)
                 Image.fromarray(_image(1000 * i + j + (17 if stage == "val" else 0), ch)).save(
                     os.path.join(obj, "rgb", f"{j:06d}.png"))
                 np.savetxt(os.path.join(obj, "pose", f"{j:06d}.txt"), _pose(i, j).reshape(1, 16), fmt="%.10f")

@@ -96,8 +96,12 @@ def test_save_has_reference_keys(tmp_path):
     path = tmp_path / "checkpoint   12.ckpt"
     save_checkpoint(path, 12, models, opt)
     ck = torch.load(str(path), weights_only=True)
-    assert set(ck) == {"iter", "model_nerf_coarse_state_dict", "model_nerf_fine_state_dict",
-                       "model_embedding_state_dict", "optimizer_state_dict"}
+    # the reference's keys, plus this build's resume keys (cn_*), which the reference's loader ignores
+    assert {k for k in ck if not k.startswith("cn_")} == {"iter", "model_nerf_coarse_state_dict",
+                                                         "model_nerf_fine_state_dict", "model_embedding_state_dict",
+                                                         "optimizer_state_dict"}
+    assert set(ck) - {"iter", "model_nerf_coarse_state_dict", "model_nerf_fine_state_dict",
+                      "model_embedding_state_dict", "optimizer_state_dict"} == {"cn_rng"}
     assert list(ck["model_nerf_coarse_state_dict"]) == list(models["nerf_coarse"].state_dict())
     assert list(ck["model_embedding_state_dict"]) == ["shape_embedding.weight", "texture_embedding.weight"]
     fresh = _models(5)
@@ -105,3 +109,36 @@ def test_save_has_reference_keys(tmp_path):
     for name in models:
         for (k, a), b in zip(models[name].state_dict().items(), fresh[name].state_dict().values()):
             assert torch.equal(a, b), (name, k)
+
+
+def test_save_ddp_prefix_and_rng_roundtrip(tmp_path):
+    """save_checkpoint(ddp_prefix=True) writes the keys the reference's distributed training writes
+    (DDP's ``module.``; its distributed load expects them); load_checkpoint strips them again.  The
+    RNG streams saved with ``rng`` come back through resume_state."""
+    import numpy as np
+    from codenerf.checkpoint import load_checkpoint, resume_state, save_checkpoint
+    models = _models(4)
+    opt = torch.optim.AdamW(_groups(models), lr=1e-4)
+    sched = torch.optim.lr_scheduler.LambdaLR(opt, lambda e: 0.5 ** e)
+    for _ in range(3):
+        sched.step()
+    path = tmp_path / "checkpoint    3.ckpt"
+    np.random.seed(7)
+    torch.manual_seed(7)
+    save_checkpoint(path, 3, models, opt, scheduler=sched, next_iter=4, ddp_prefix=True)
+    want_np, want_t = np.random.rand(3), torch.rand(3)
+    ck = torch.load(str(path), weights_only=True)
+    assert all(k.startswith("module.") for k in ck["model_nerf_fine_state_dict"])
+    fresh = _models(5)
+    opt2 = torch.optim.AdamW(_groups(fresh), lr=1e-4)
+    sched2 = torch.optim.lr_scheduler.LambdaLR(opt2, lambda e: 0.5 ** e)
+    extras = {}
+    assert load_checkpoint(NS(load_checkpoint=str(path)), fresh, opt2, extras=extras) == 3
+    np.random.seed(0)
+    torch.manual_seed(0)
+    assert resume_state(extras, sched2, 3) == 4
+    assert sched2.last_epoch == 3
+    assert np.array_equal(np.random.rand(3), want_np) and torch.equal(torch.rand(3), want_t)
+    for name in models:
+        for a, b in zip(models[name].state_dict().values(), fresh[name].state_dict().values()):
+            assert torch.equal(a, b)

@@ -49,7 +49,7 @@ def _params(out):
 
 @pytest.fixture(scope="module")
 def tree(tmp_path_factory):
-    return srn_tree.write_tree(str(tmp_path_factory.mktemp("srn")))
+    return srn_tree.write_tree(str(tmp_path_factory.mktemp("srn")), channels=4)
 
 
 def test_train_resume_is_exact(tree, tmp_path):
