@@ -366,7 +366,7 @@ def eval_bench(dev, rs, emb, models, iters, precision, graph=False):
     perturbed samples, forward + backward through the HIP kernels into (codes, theta, phi, rho),
     AdamW step.  Weights frozen (their grads are never read by the reference's optimiser)."""
     import numpy as np
-    from codenerf.evaluate import GraphedEvalStep, eval_step_loss, step_psnr
+    from codenerf.evaluate import GraphedEvalStep, eval_step_loss, step_psnr_tensor
     from codenerf.nerf import PointSampler
     from codenerf.optim import AdamW
     ps = PointSampler(NC, NF, NEAR, FAR, "lindepth", True, torch.float32, dev)
@@ -394,14 +394,14 @@ def eval_bench(dev, rs, emb, models, iters, precision, graph=False):
         def it():
             _, logs = graphed.step()  # forward + backward + the flat AdamW update, one replay
             graphed.prefetch()  # the next iteration's numpy draw while the GPU replays this one
-            step_psnr(logs)
+            step_psnr_tensor(logs)  # eval.py:159's psnr, on the device
     else:
         def it():
             loss, logs = eval_step_loss(th, ph, rh, zs, zt, target, (rs, ps), emb, mods, 1e-5)
             opt.zero_grad()
             loss.backward()
             opt.step()
-            step_psnr(logs)  # eval.py:159's per-iteration read-back, after the step is enqueued
+            step_psnr_tensor(logs)  # eval.py:159's per-iteration psnr, on the device (no read-back)
 
     for _ in range(2):
         it()
@@ -420,8 +420,8 @@ def eval_bench(dev, rs, emb, models, iters, precision, graph=False):
         note += "; forward + backward + AdamW replayed as one captured HIP graph (GraphedEvalStep)"
     return {"ms_per_iter": dt * 1e3, "rays_per_s": 2048 / dt, "rays_per_iter": 2048, "samples": "64+64 perturbed",
             "dtype": precision,
-            "note": note + "; fused pose path + loss; host-side numpy ray permutation and eval.py's per-iteration psnr "
-                           "read-back included"}
+            "note": note + "; fused pose path + loss; host-side numpy ray permutation included; eval.py's "
+                           "per-iteration psnr formed on the device"}
 
 
 def train_bench(dev, k, iters, world, precision=None):
@@ -457,9 +457,10 @@ def train_bench(dev, k, iters, world, precision=None):
     samplers = N.prepare_samplers(cfg, H, W, k, torch.float32, dev)
     embedders = N.prepare_embedders(cfg, torch.float32, dev)
     g = torch.Generator().manual_seed(7 + rank)
+    oid = torch.randint(0, n_objects, (batch,), generator=g)
     data = {"color": torch.rand(batch, H, W, 4, generator=g).to(dev),
             "pose": torch.stack([pose(0.4 + 0.5 * i, 0.3, 1.3) for i in range(batch)]).to(dev),
-            "object_id": torch.randint(0, n_objects, (batch,), generator=g).to(dev)}
+            "object_id": oid.to(dev), "object_id_host": oid.numpy()}   # as the resident loader hands them
     T.train_iteration(cfg, data, models, opt, sched, samplers, embedders)        # warm-up
     torch.cuda.synchronize()
     if world > 1:
@@ -501,8 +502,8 @@ def train_bench(dev, k, iters, world, precision=None):
             "note": (("fp32 16x16x4" if precision == "f32" else "3xbf16 32x32x16") +
                      " training forward (activation planes + ReLU masks kept), ONE fused dX backward launch per field"
                      " (masked layer-input gradients kept), deterministic split-M dW GEMMs (encodings generated "
-                     "in-kernel" + (", bias column sums folded in" if precision == "bf16x3" else "") +
-                     "), fused loss, flat AdamW; train.py's per-chunk psnr read-back included")}
+                     "in-kernel, bias and one-object code sums folded in), fused loss, flat AdamW; train.py's "
+                     "per-chunk psnr formed on the device (read when logged), no host sync inside an iteration")}
 
 
 def cpu_threads() -> int:

@@ -149,8 +149,10 @@ class SRNDataset(torch.utils.data.Dataset):
         r = self.resident
         idx = torch.as_tensor(index, dtype=torch.int64).reshape(-1).to(r["images"].device, non_blocking=True)
         color, mask = ops.srn_unpack(r["images"], idx)
+        host_idx = np.asarray(index, dtype=np.int64).reshape(-1)
         return {"object_id": r["object_id"][idx], "intrinsic": r["intrinsic"][idx], "color": color, "mask": mask,
-                "pose": r["pose"][idx]}
+                "pose": r["pose"][idx],
+                "object_id_host": np.asarray([self.rgb_all_filenames[i][0] for i in host_idx], dtype=np.int64)}
 
 
 class ResidentLoader:

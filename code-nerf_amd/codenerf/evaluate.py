@@ -71,6 +71,12 @@ def step_psnr(logs: Dict[str, object]) -> float:
     return mse2psnr(logs["nerf_loss_fine"].item())
 
 
+def step_psnr_tensor(logs: Dict[str, object]) -> torch.Tensor:
+    """eval.py:159's psnr formed on the device (no read-back; float() it when logged)."""
+    from .train import psnr_tensor
+    return psnr_tensor(logs["nerf_loss_fine"])
+
+
 class GraphedEvalStep:
     """One test-time-optimisation iteration's forward and backward (eval.py:145-160) captured ONCE
     as a HIP graph (torch.cuda.CUDAGraph, i.e. hipGraph on ROCm) and replayed every iteration: the
@@ -232,7 +238,7 @@ def test_time_optimize(target_pixels: torch.Tensor, samplers, embedders, models,
                 opt.zero_grad()
                 loss.backward()
                 opt.step()
-            logs["psnr"] = step_psnr(logs)
+            logs["psnr"] = step_psnr_tensor(logs)       # read back with the history (below) or when logged
             logs["total_loss"] = loss.detach()
             history.append(logs)
             if log_every and ((it != 0 and it % log_every == 0) or it == iterations - 1):
@@ -248,9 +254,9 @@ def test_time_optimize(target_pixels: torch.Tensor, samplers, embedders, models,
 def _pose_lr(o, key: str) -> float:
     """eval.py:135-136 reads optimizer.angle_lr / radius_lr; srn-cars-code.yml lacks both, so
     the reference raises there.  This build substitutes val_lr -- and says so."""
-    if key in o:
-        return o[key] if isinstance(o, dict) else getattr(o, key)
-    if hasattr(o, key):
+    if isinstance(o, dict) and key in o:
+        return o[key]
+    if not isinstance(o, dict) and hasattr(o, key):
         return getattr(o, key)
     warnings.warn(f"optimizer.{key} is not in the config (the reference's eval.py:135-136 raises for it, SURVEY "
                   f"Q8); using optimizer.val_lr = {o.val_lr}", stacklevel=3)

@@ -15,6 +15,7 @@ from __future__ import annotations
 import os
 from typing import List, Tuple
 
+import numpy as np
 import torch
 
 from .. import ops
@@ -160,7 +161,16 @@ class ShapeTextureEmbedding(torch.nn.Module):
         object (one per 4096-ray chunk in train.py) instead of once per ray."""
         if object_ids.device.type != "cuda" or object_ids.dim() != 1:
             return self.shape_embedding(object_ids), self.texture_embedding(object_ids)
-        uniq, index = torch.unique(object_ids, return_inverse=True)
+        host = getattr(object_ids, "_cn_host_ids", None)
+        if host is not None and len(host) == object_ids.shape[0]:
+            # the caller knows the ids on the host (codenerf.train: the batch's per-image ids): the
+            # distinct ids go up as a pinned copy and the per-ray index is a device searchsorted --
+            # torch.unique on the device would wait for the GPU (its output size) every chunk
+            uniq_h = np.unique(np.asarray(host, dtype=np.int64))
+            uniq = torch.from_numpy(uniq_h).pin_memory().to(object_ids.device, non_blocking=True)
+            index = torch.searchsorted(uniq, object_ids)
+        else:
+            uniq, index = torch.unique(object_ids, return_inverse=True)
         rows_s, rows_t = self.shape_embedding(uniq), self.texture_embedding(uniq)
         z_s, z_t = rows_s[index], rows_t[index]
         tag = CodeRows(rows_s, rows_t, index)

@@ -26,6 +26,7 @@ from collections import OrderedDict
 from pathlib import Path
 from typing import Dict, List, Optional
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -113,12 +114,19 @@ def _ddp_wrapped(models) -> bool:
 
 
 def train_minibatch(models, optimizer, scheduler, point_sampler, embedders, ro, rd, object_ids, target_pixels,
-                    regularizer_lambda: float, is_distributed: bool = False) -> Dict[str, object]:
+                    regularizer_lambda: float, is_distributed: bool = False, uniforms=None) -> Dict[str, object]:
     """train.py:92-114 for one chunk -> the losses train.py logs (tensors) and its psnr (float,
-    read back every chunk as train.py:105 does)."""
+    read back every chunk as train.py:105 does).  ``uniforms``: (t_rand, u), the stratified / fine
+    draws of point_sampler.py:64,93 injected (parity tests) instead of drawn on the device."""
     target_object_embedding = models["embedding"](object_ids)
-    rgb_coarse, rgb_fine = nerf.predict_radiance_and_render((ro, rd), point_sampler, embedders, models["nerf_coarse"],
-                                                            models["nerf_fine"], target_object_embedding)
+    if uniforms is None:
+        rgb_coarse, rgb_fine = nerf.predict_radiance_and_render((ro, rd), point_sampler, embedders,
+                                                                models["nerf_coarse"], models["nerf_fine"],
+                                                                target_object_embedding)
+    else:
+        out = nerf.render_rays(ro, rd, *target_object_embedding, point_sampler, embedders, models["nerf_coarse"],
+                               models["nerf_fine"], t_rand=uniforms[0], u=uniforms[1])
+        rgb_coarse, rgb_fine = out["rgb_coarse"], out["rgb_fine"]
     # mse coarse + mse fine + lambda (||shape table|| + ||texture table||) on .data (a constant):
     # one cn_render_loss launch forward, one backward into the two rgb tensors
     shape_params, texture_params = get_params_tensor(models["embedding"], is_distributed)
@@ -131,11 +139,18 @@ def train_minibatch(models, optimizer, scheduler, point_sampler, embedders, ro, 
         _average_gradients(optimizer, models)     # (DDP-wrapped modules averaged in the backward)
     optimizer.step()
     scheduler.step()
-    # train.py:105 reads psnr back before the backward; reading the same value once the step is
-    # enqueued keeps the GPU busy through the read-back instead of idling mid-step
-    psnr = mse2psnr(loss_fine.item())
+    # train.py:105's psnr of this chunk, formed on the device (mse2psnr's arithmetic in float64):
+    # the reference's .item() read-back every chunk made the host wait for the GPU and the GPU then
+    # wait for the host's next launches; float() it when it is logged
+    psnr = psnr_tensor(loss_fine)
     return {"nerf_loss_coarse": loss_coarse, "nerf_loss_fine": loss_fine, "embedding_loss": regularization,
             "total_loss": loss.detach(), "psnr": psnr}
+
+
+def psnr_tensor(mse: torch.Tensor) -> torch.Tensor:
+    """utils/util.py:216-227 (mse2psnr) on a device scalar: -10 log10(mse), mse 0 -> 1e-5, float64."""
+    m = mse.detach().double()
+    return -10.0 * torch.log10(torch.where(m == 0, torch.full_like(m, 1e-5), m))
 
 
 def train_iteration(cfg, train_data: Dict[str, torch.Tensor], models, optimizer, scheduler, samplers,
@@ -152,6 +167,12 @@ def train_iteration(cfg, train_data: Dict[str, torch.Tensor], models, optimizer,
     n_rays = ray_sampler.sample_size
     color = train_data["color"]
     object_ids = train_data["object_id"][:, None].expand(-1, n_rays).reshape(-1)
+    # the per-image ids on the host (the resident loader hands them over; else one read per
+    # iteration): the chunks' embedding lookups then need no device sync (ShapeTextureEmbedding)
+    host_ids = train_data.get("object_id_host")
+    if host_ids is None:
+        host_ids = train_data["object_id"].cpu().numpy()
+    host_ids = np.repeat(np.asarray(host_ids, dtype=np.int64), n_rays)
     chunk = cfg.nerf.train.chunksize
     assert chunk <= n_rays * color.shape[0], \
         "Chunksize needs to atleast be less than to the number of rays sampled from a single image"
@@ -159,6 +180,7 @@ def train_iteration(cfg, train_data: Dict[str, torch.Tensor], models, optimizer,
     batches = list(zip(get_minibatches(ro_batch, chunk), get_minibatches(rd_batch, chunk),
                        get_minibatches(object_ids, chunk), get_minibatches(target, chunk)))
     for j, (ro, rd, ids, tp) in enumerate(batches):
+        ids._cn_host_ids = host_ids[j * chunk:j * chunk + ids.shape[0]]
         logs.append(train_minibatch(models, optimizer, scheduler, point_sampler, embedders, ro, rd, ids, tp,
                                     cfg.experiment.regularizer_lambda, is_distributed))
         if on_chunk is not None:
@@ -252,10 +274,11 @@ def train(rank: int, cfg, device=None, resident: bool = True, stop_after: Option
 
         def on_chunk(j, num_batches, lg):
             i = iteration * num_batches + j
-            out["logs"].append({k: float(v) for k, v in lg.items()})
+            out["logs"].append(lg)                 # device scalars: read when printed / returned
             if main and i > 0:
                 if i % e.print_every == 0 and verbose:
-                    print(log_losses("train", i, time.time() - then, out["logs"][-1], scheduler.get_last_lr()[0]))
+                    print(log_losses("train", i, time.time() - then, {k: float(v) for k, v in lg.items()},
+                                     scheduler.get_last_lr()[0]))
                 if i % e.save_every == 0 or i == e.iterations - 1:
                     path = logdir_path / f"checkpoint{i:5d}.ckpt"
                     C.save_checkpoint(path, iteration, models, optimizer, scheduler=scheduler,
@@ -268,4 +291,5 @@ def train(rank: int, cfg, device=None, resident: bool = True, stop_after: Option
                 out["validation"].append(validate(cfg, val_data, models, samplers, embedders, device,
                                                   log_every=e.val_print_every if verbose else None))
         train_iteration(cfg, train_data, models, optimizer, scheduler, samplers, embedders, on_chunk=on_chunk)
+    out["logs"] = [{k: float(v) for k, v in lg.items()} for lg in out["logs"]]
     return out

@@ -1,76 +1,110 @@
 // Volume integration: volume_render (view_synthesis/nerf/volumetric_render.py:36-66).
 //
-// One wavefront per ray; lane l owns a contiguous run of ceil(S/64) samples
-// (one sample per lane at S = 64, so the (S, 4) raw rows and the depths are
-// read as coalesced 1 KiB / 256 B wave loads).  The exclusive prefix of
-// sigma*delta -- transmittance = exp(-[0, cumsum(sigma*delta)[:-1]]) -- is a
-// wave scan over the lanes' run totals followed by the in-run prefix.  The
-// scan accumulates in double, as torch's CPU cumsum does (Q13).
-// Algorithmic bytes per ray: 12 (rd) + 20*S in (raw + z), 4*S + 20 out.
+// The exclusive prefix of sigma*delta -- transmittance = exp(-[0, cumsum(sigma*delta)[:-1]]) --
+// is a scan over the lanes' run totals followed by the in-run prefix (layout below).
 #include "cn_common.h"
 
 namespace {
 
-constexpr int kRaysPerBlock = 4;
-constexpr int kMaxRun = 8;  // S <= 512
+// 16 lanes (one DPP row) per ray, 4 rays per wave, 16 per 256-thread block.  Lane i of a row owns
+// the contiguous run of samples [i run, (i + 1) run), run = ceil(S / 16) <= K; its next sample's
+// depth (z[j + 1] past the run) comes from lane i + 1 by DPP instead of a second load; the
+// exclusive prefix of sigma*delta over the lanes' run totals is a 4-step DPP row scan (in double,
+// as torch's CPU cumsum accumulates, Q13), and the per-ray sums are DPP row reductions -- every
+// cross-lane step stays inside the row, with no LDS traffic.
+// Algorithmic bytes per ray: 12 (rd) + 20*S in (raw + z), 4*S + 20 out.
+constexpr int kRowsPerBlock = 16;
+constexpr int kMaxRun = 32;  // S <= 512
 
-__device__ __forceinline__ double wave_exclusive_scan(double v, int lane) {
-  double incl = v;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const double o = __shfl_up(incl, off);
-    if (lane >= off) incl += o;
-  }
-  return incl - v;
+template <int CTRL>
+__device__ __forceinline__ float dppf(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, true));
+}
+template <int CTRL>
+__device__ __forceinline__ double dppd(double x) {
+  const long long v = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_update_dpp(0, static_cast<int>(v & 0xffffffff), CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, static_cast<int>(v >> 32), CTRL, 0xF, 0xF, true);
+  return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
+}
+// Exclusive prefix over the 16 lanes of the row (row_shr: lane i reads lane i - n, 0 below the row).
+__device__ __forceinline__ double row_exclusive_scan(double v) {
+  double x = v;
+  x += dppd<0x111>(x);
+  x += dppd<0x112>(x);
+  x += dppd<0x114>(x);
+  x += dppd<0x118>(x);
+  return x - v;
+}
+// Exclusive suffix over the row (row_shl: lane i reads lane i + n, 0 past the row).
+__device__ __forceinline__ float row_exclusive_suffix(float v) {
+  float x = v;
+  x += dppf<0x101>(x);
+  x += dppf<0x102>(x);
+  x += dppf<0x104>(x);
+  x += dppf<0x108>(x);
+  return x - v;
+}
+// Sum over the row's 16 lanes, valid in lane 15.
+__device__ __forceinline__ float row_sum(float x) {
+  x += dppf<0x111>(x);
+  x += dppf<0x112>(x);
+  x += dppf<0x114>(x);
+  x += dppf<0x118>(x);
+  return x;
 }
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-  return v;
-}
-
+template <int K>
 __global__ __launch_bounds__(256) void volume_render_kernel(
     const float* __restrict__ raw, const float* __restrict__ z, const float* __restrict__ rd,
     int64_t n_rays, int S_in, float* __restrict__ rgb, float* __restrict__ disp,
     float* __restrict__ acc, float* __restrict__ weights, float* __restrict__ depth) {
-  const int lane = threadIdx.x & 63;
-  const int64_t r = blockIdx.x * (int64_t)kRaysPerBlock + (threadIdx.x >> 6);
-  if (r >= n_rays) return;
+  const int sub = threadIdx.x & 15;
+  const int64_t r = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
+  if (r >= n_rays) return;  // whole rows leave together: the DPP steps never read an exited lane
   // S == 1: the reference's dists = cat(z[1:] - z[:-1], full_like(that[..., :1], 1e10))
   // is EMPTY (both pieces are 0 wide), so no sample contributes (rgb = acc = depth = 0,
   // disp = NaN, weights (R, 0)).  Reproduced by treating the ray as sample-free.
   const int S = S_in == 1 ? 0 : S_in;
-  const int run = (S_in + 63) / 64;
-  const int j0 = lane * run;
+  const int run = (S_in + 15) >> 4;
+  const int j0 = sub * run;
   const float* zr = z + r * S_in;
   const float4* rr = reinterpret_cast<const float4*>(raw) + r * S_in;
   const float d0 = rd[3 * r], d1 = rd[3 * r + 1], d2 = rd[3 * r + 2];
   const float nrm = __fsqrt_rn(__fadd_rn(__fadd_rn(__fmul_rn(d0, d0), __fmul_rn(d1, d1)), __fmul_rn(d2, d2)));
 
-  float sd[kMaxRun], zz[kMaxRun];
-  float4 rv[kMaxRun];
+  float zz[K], sd[K];
+  float4 rv[K];
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    const int j = j0 + i;
+    zz[i] = 0.0f;
+    rv[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i < run && j < S_in) {
+      zz[i] = zr[j];
+      rv[i] = rr[j];
+    }
+  }
+  const float znext = dppf<0x101>(zz[0]);  // the first depth of lane sub + 1's run
   double run_sum = 0.0;  // sum of this run's sigma*delta that feeds later transmittances
 #pragma unroll
-  for (int i = 0; i < kMaxRun; ++i) {
+  for (int i = 0; i < K; ++i) {
     const int j = j0 + i;
     sd[i] = 0.0f;
     if (i < run && j < S) {
-      zz[i] = zr[j];
-      rv[i] = rr[j];
       // dists = [z[1:] - z[:-1], 1e10] (:41-44), delta = dists * |rd| (:45)
-      const float dist = (j + 1 < S) ? __fsub_rn(zr[j + 1], zz[i]) : 1e10f;
-      const float delta = __fmul_rn(dist, nrm);
+      const float zn = (i + 1 < run) ? zz[(i + 1) % K] : znext;
+      const float dist = (j + 1 < S) ? __fsub_rn(zn, zz[i]) : 1e10f;
       const float sigma = cn::softplus20(__fsub_rn(rv[i].w, 1.0f));  // shifted_softplus (:32)
-      sd[i] = __fmul_rn(sigma, delta);
+      sd[i] = __fmul_rn(sigma, __fmul_rn(dist, nrm));
       if (j + 1 < S) run_sum += static_cast<double>(sd[i]);
     }
   }
-  double prefix = wave_exclusive_scan(run_sum, lane);
+  double prefix = row_exclusive_scan(run_sum);
 
   float cr = 0.f, cg = 0.f, cb = 0.f, dep = 0.f, ac = 0.f;
 #pragma unroll
-  for (int i = 0; i < kMaxRun; ++i) {
+  for (int i = 0; i < K; ++i) {
     const int j = j0 + i;
     if (i < run && j < S) {
       const float trans = expf(-static_cast<float>(prefix));      // (:54-57)
@@ -89,12 +123,12 @@ __global__ __launch_bounds__(256) void volume_render_kernel(
       if (j + 1 < S) prefix += static_cast<double>(sd[i]);
     }
   }
-  cr = wave_sum(cr);
-  cg = wave_sum(cg);
-  cb = wave_sum(cb);
-  dep = wave_sum(dep);
-  ac = wave_sum(ac);
-  if (lane == 0) {
+  cr = row_sum(cr);
+  cg = row_sum(cg);
+  cb = row_sum(cb);
+  dep = row_sum(dep);
+  ac = row_sum(ac);
+  if (sub == 15) {
     rgb[3 * r] = cr;
     rgb[3 * r + 1] = cg;
     rgb[3 * r + 2] = cb;
@@ -108,15 +142,25 @@ __global__ __launch_bounds__(256) void volume_render_kernel(
 
 }  // namespace
 
+// Samples per lane the kernels are instantiated for: the smallest that holds ceil(S / 16).
+#define CN_VOLUME_DISPATCH(KERNEL, S, ...)                                                   \
+  do {                                                                                      \
+    const int run_ = static_cast<int>(((S) + 15) / 16);                                    \
+    if (run_ <= 4) hipLaunchKernelGGL(KERNEL<4>, __VA_ARGS__);                             \
+    else if (run_ <= 8) hipLaunchKernelGGL(KERNEL<8>, __VA_ARGS__);                        \
+    else if (run_ <= 12) hipLaunchKernelGGL(KERNEL<12>, __VA_ARGS__);                      \
+    else if (run_ <= 16) hipLaunchKernelGGL(KERNEL<16>, __VA_ARGS__);                      \
+    else hipLaunchKernelGGL(KERNEL<32>, __VA_ARGS__);                                      \
+  } while (0)
+
 extern "C" int cn_volume_render(const float* raw, const float* z, const float* rd, int64_t n_rays,
                                 int64_t n_samples, float* rgb, float* disp, float* acc,
                                 float* weights, float* depth, cn_stream_t stream) {
   CN_CHECK_ARG(raw && z && rd && rgb && disp && acc && depth);
-  CN_CHECK_ARG(n_rays > 0 && n_samples > 0 && n_samples <= 64 * kMaxRun);
-  const unsigned grid = static_cast<unsigned>(cn::ceil_div(n_rays, kRaysPerBlock));
-  hipLaunchKernelGGL(volume_render_kernel, dim3(grid), dim3(64 * kRaysPerBlock), 0,
-                     cn::as_stream(stream), raw, z, rd, n_rays, static_cast<int>(n_samples), rgb,
-                     disp, acc, weights, depth);
+  CN_CHECK_ARG(n_rays > 0 && n_samples > 0 && n_samples <= 16 * kMaxRun);
+  const unsigned grid = static_cast<unsigned>(cn::ceil_div(n_rays, kRowsPerBlock));
+  CN_VOLUME_DISPATCH(volume_render_kernel, n_samples, dim3(grid), dim3(256), 0, cn::as_stream(stream), raw, z, rd,
+                     n_rays, static_cast<int>(n_samples), rgb, disp, acc, weights, depth);
   return cn::launch_status();
 }
 
@@ -124,66 +168,63 @@ extern "C" int cn_volume_render(const float* raw, const float* z, const float* r
 // Gradient of volume_render (volumetric_render.py:36-66) w.r.t. raw and rd.
 // With sd_i = sigma_i delta_i, T_i = exp(-sum_{j<i} sd_j), w_i = (1 - e^{-sd_i}) T_i:
 //   G_i = g_w_i + g_rgb . c_i + g_depth z_i + g_acc          (dL/dw_i)
-//   dL/dsd_i = G_i T_i e^{-sd_i} - sum_{j>i} G_j w_j          (reverse wave scan)
+//   dL/dsd_i = G_i T_i e^{-sd_i} - sum_{j>i} G_j w_j          (reverse row scan)
 //   d raw_i[0:3] = w_i g_rgb 1.002 s(1-s);  d raw_i[3] = dL/dsd_i delta_i softplus'(raw_i[3]-1)
 //   d rd = (sum_i dL/dsd_i sigma_i dist_i) rd/|rd|
 // g_disp folds into g_depth / g_acc through disp = 1/max(1e-10, depth/acc).
-// z is never differentiated (the reference detaches its samples).
+// z is never differentiated (the reference detaches its samples).  Same layout as the forward.
 namespace {
 
-__device__ __forceinline__ float wave_sum_f(float v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-  return v;
-}
-
-__device__ __forceinline__ float wave_exclusive_suffix(float v, int lane) {
-  float incl = v;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const float o = __shfl_down(incl, off);
-    if (lane + off < 64) incl += o;
-  }
-  return incl - v;
-}
-
+template <int K>
 __global__ __launch_bounds__(256) void volume_render_backward_kernel(
     const float* __restrict__ raw, const float* __restrict__ z, const float* __restrict__ rd,
     int64_t n_rays, int S_in, const float* __restrict__ g_rgb, const float* __restrict__ g_disp,
     const float* __restrict__ g_acc, const float* __restrict__ g_w, const float* __restrict__ g_depth,
     float* __restrict__ d_raw, float* __restrict__ d_rd) {
-  const int lane = threadIdx.x & 63;
-  const int64_t r = blockIdx.x * (int64_t)kRaysPerBlock + (threadIdx.x >> 6);
+  const int sub = threadIdx.x & 15;
+  const int64_t r = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
   if (r >= n_rays) return;
   const int S = S_in == 1 ? 0 : S_in;  // see the forward: S == 1 has no contributing sample
-  const int run = (S_in + 63) / 64;
-  const int j0 = lane * run;
+  const int run = (S_in + 15) >> 4;
+  const int j0 = sub * run;
   const float* zr = z + r * S_in;
   const float4* rr = reinterpret_cast<const float4*>(raw) + r * S_in;
   float4* dr = reinterpret_cast<float4*>(d_raw) + r * S_in;
   const float d0 = rd[3 * r], d1 = rd[3 * r + 1], d2 = rd[3 * r + 2];
   const float nrm = __fsqrt_rn(__fadd_rn(__fadd_rn(__fmul_rn(d0, d0), __fmul_rn(d1, d1)), __fmul_rn(d2, d2)));
 
-  float sd[kMaxRun], zz[kMaxRun], dist[kMaxRun], sig[kMaxRun], w[kMaxRun], tr[kMaxRun];
-  float4 rv[kMaxRun];
-  double run_sum = 0.0;
+  float sd[K], zz[K], dist[K], sig[K], w[K], tr[K];
+  float4 rv[K];
 #pragma unroll
-  for (int i = 0; i < kMaxRun; ++i) {
+  for (int i = 0; i < K; ++i) {
     const int j = j0 + i;
-    sd[i] = 0.0f;
-    if (i < run && j < S) {
+    zz[i] = 0.0f;
+    rv[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i < run && j < S_in) {
       zz[i] = zr[j];
       rv[i] = rr[j];
-      dist[i] = (j + 1 < S) ? __fsub_rn(zr[j + 1], zz[i]) : 1e10f;
+    }
+  }
+  const float znext = dppf<0x101>(zz[0]);
+  double run_sum = 0.0;
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    const int j = j0 + i;
+    sd[i] = 0.0f;
+    dist[i] = 0.0f;
+    sig[i] = 0.0f;
+    if (i < run && j < S) {
+      const float zn = (i + 1 < run) ? zz[(i + 1) % K] : znext;
+      dist[i] = (j + 1 < S) ? __fsub_rn(zn, zz[i]) : 1e10f;
       sig[i] = cn::softplus20(__fsub_rn(rv[i].w, 1.0f));
       sd[i] = __fmul_rn(sig[i], __fmul_rn(dist[i], nrm));
       if (j + 1 < S) run_sum += static_cast<double>(sd[i]);
     }
   }
-  double prefix = wave_exclusive_scan(run_sum, lane);
+  double prefix = row_exclusive_scan(run_sum);
   float dep = 0.f, ac = 0.f;
 #pragma unroll
-  for (int i = 0; i < kMaxRun; ++i) {
+  for (int i = 0; i < K; ++i) {
     const int j = j0 + i;
     w[i] = 0.0f;
     tr[i] = 0.0f;
@@ -195,8 +236,9 @@ __global__ __launch_bounds__(256) void volume_render_backward_kernel(
       if (j + 1 < S) prefix += static_cast<double>(sd[i]);
     }
   }
-  dep = wave_sum_f(dep);
-  ac = wave_sum_f(ac);
+  // the ray's depth / acc in every lane of the row (lane 15's row sum, read back by DPP broadcast)
+  dep = __shfl(row_sum(dep), (threadIdx.x & 63) | 15);
+  ac = __shfl(row_sum(ac), (threadIdx.x & 63) | 15);
   const float gr0 = g_rgb ? g_rgb[3 * r] : 0.f, gr1 = g_rgb ? g_rgb[3 * r + 1] : 0.f;
   const float gr2 = g_rgb ? g_rgb[3 * r + 2] : 0.f;
   float gdep = g_depth ? g_depth[r] : 0.f, gacc = g_acc ? g_acc[r] : 0.f;
@@ -209,9 +251,9 @@ __global__ __launch_bounds__(256) void volume_render_backward_kernel(
     }
   }
   // G_i and the per-sample colour gradients
-  float G[kMaxRun], gw_run = 0.f;
+  float G[K], gw_run = 0.f;
 #pragma unroll
-  for (int i = 0; i < kMaxRun; ++i) {
+  for (int i = 0; i < K; ++i) {
     const int j = j0 + i;
     G[i] = 0.0f;
     if (i < run && j < S) {
@@ -224,10 +266,10 @@ __global__ __launch_bounds__(256) void volume_render_backward_kernel(
       gw_run += G[i] * w[i];
     }
   }
-  float suffix = wave_exclusive_suffix(gw_run, lane);  // sum of G_j w_j over later lanes' runs
+  float suffix = row_exclusive_suffix(gw_run);  // sum of G_j w_j over later lanes' runs
   float gnorm = 0.f;
 #pragma unroll
-  for (int i = kMaxRun - 1; i >= 0; --i) {
+  for (int i = K - 1; i >= 0; --i) {
     const int j = j0 + i;
     if (i < run && j < S) {
       const float dsd = G[i] * tr[i] * expf(-sd[i]) - suffix;
@@ -242,8 +284,8 @@ __global__ __launch_bounds__(256) void volume_render_backward_kernel(
       dr[j] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
-  gnorm = wave_sum_f(gnorm);
-  if (lane == 0 && d_rd) {
+  gnorm = row_sum(gnorm);
+  if (sub == 15 && d_rd) {
     const float inv = nrm > 0.f ? gnorm / nrm : 0.f;
     d_rd[3 * r] = inv * d0;
     d_rd[3 * r + 1] = inv * d1;
@@ -259,10 +301,10 @@ extern "C" int cn_volume_render_backward(const float* raw, const float* z, const
                                          const float* g_weights, const float* g_depth,
                                          float* d_raw, float* d_rd, cn_stream_t stream) {
   CN_CHECK_ARG(raw && z && rd && d_raw);
-  CN_CHECK_ARG(n_rays > 0 && n_samples > 0 && n_samples <= 64 * kMaxRun);
-  const unsigned grid = static_cast<unsigned>(cn::ceil_div(n_rays, kRaysPerBlock));
-  hipLaunchKernelGGL(volume_render_backward_kernel, dim3(grid), dim3(64 * kRaysPerBlock), 0,
-                     cn::as_stream(stream), raw, z, rd, n_rays, static_cast<int>(n_samples), g_rgb,
-                     g_disp, g_acc, g_weights, g_depth, d_raw, d_rd);
+  CN_CHECK_ARG(n_rays > 0 && n_samples > 0 && n_samples <= 16 * kMaxRun);
+  const unsigned grid = static_cast<unsigned>(cn::ceil_div(n_rays, kRowsPerBlock));
+  CN_VOLUME_DISPATCH(volume_render_backward_kernel, n_samples, dim3(grid), dim3(256), 0, cn::as_stream(stream), raw,
+                     z, rd, n_rays, static_cast<int>(n_samples), g_rgb, g_disp, g_acc, g_weights, g_depth, d_raw,
+                     d_rd);
   return cn::launch_status();
 }

@@ -17,6 +17,7 @@ the HIP path (tests/test_gpu_*.py).
 """
 from __future__ import annotations
 
+import importlib
 import os
 import sys
 import types
@@ -88,7 +89,7 @@ def main(only=None):
     torch.set_num_threads(8)
     if only:
         for name in only:
-            ROUND2[name](nerf, model_mod, ev)
+            {**ROUND2, **ROUND3}[name](nerf, model_mod, ev)
         return
     pose = lambda th, ph, rh: ev.pose_spherical(torch.tensor([th]), torch.tensor([ph]), torch.tensor([rh]))  # noqa: E731
 
@@ -269,7 +270,7 @@ def main(only=None):
          g_fine_fc_rgb_w=models["nerf_fine"].fc_rgb.weight.grad, g_coarse_fc_out_b=models["nerf_coarse"].fc_out.bias.grad,
          **pw)
     print("split(1024,3) =", util.get_minibatches(torch.arange(10), 4))
-    for fn in ROUND2.values():
+    for fn in list(ROUND2.values()) + list(ROUND3.values()):
         fn(nerf, model_mod, ev)
 
 
@@ -530,8 +531,85 @@ def gen_loss(nerf, model_mod, ev):
          reg=reg, loss=loss, g_rgb_c=rgb_c.grad, g_rgb_f=rgb_f.grad, g_z_s=zs.grad, g_z_t=zt.grad)
 
 
+C3_OBJECTS = 2458                    # SRN cars train objects (BASELINE.json config 3)
+C3_IDS = (17, 1234)                  # the two objects of the chunk (2048 rays each)
+C3_FULL = ("nerf_coarse.layer_dir1.weight", "nerf_coarse.shape_code_layer1.weight", "nerf_fine.fc_rgb.weight",
+           "nerf_fine.fc_out.bias", "nerf_fine.layer_xyz1.weight")
+
+
+def gen_c3train(nerf, model_mod, ev):
+    """C3 training at size (srn-cars-code.yml with 64 + 64 samples): the reference's own chunk step,
+    train.py:96-114 -- embedding lookup, predict_radiance_and_render, mse(coarse) + mse(fine) +
+    lambda (||shape table|| + ||texture table||), zero_grad, backward, AdamW (util.py:157-162 groups:
+    coarse, fine, embedding at embedding_lr), LambdaLR -- on ONE 4096-ray chunk made of two views of
+    two objects of a 2458-object table (2048 rays each, ray_sampler.sample), perturbed samples
+    (uniforms recorded).  Stored: the inputs the test cannot regenerate (rays, ids, targets, draws),
+    the losses, every parameter's gradient norm + a few full gradients, the touched code-table rows'
+    gradients, and the post-step values of the same tensors and rows.  Weights: codenerf.synthetic
+    (seeds 0 / 1), table: synthetic.latent_codes(40 / 41, 2458)."""
+    util = importlib.import_module("view_synthesis.utils.util")
+    K = synthetic.srn_intrinsics(128)
+    rs = nerf.RaySampler(128, 128, K, sample_size=2048, device="cpu", datatype=torch.float32)
+    ps = nerf.PointSampler(64, 64, 0.8, 1.8, spacing_mode="lindepth", perturb=True, dtype=torch.float32,
+                           device="cpu")
+    emb = _embedders(nerf)
+    models = {"nerf_coarse": make_model(model_mod, 0).train(), "nerf_fine": make_model(model_mod, 1).train()}
+    table = model_mod.ShapeTextureEmbedding(C3_OBJECTS, 256, 256)
+    with torch.no_grad():
+        table.shape_embedding.weight.copy_(synthetic.latent_codes(40, C3_OBJECTS))
+        table.texture_embedding.weight.copy_(synthetic.latent_codes(41, C3_OBJECTS))
+    models["embedding"] = table
+    cfg = Cfg(optimizer=Cfg(type="AdamW", lr=1e-4, embedding_lr=1e-3, scheduler_gamma=0.1,
+                            scheduler_step_size=5000000))
+    optimizer, scheduler = util.prepare_optimizer(cfg, models)
+    g = torch.Generator().manual_seed(61)
+    colors = torch.rand(2, 128, 128, 4, generator=g)
+    poses = torch.cat([_pose(ev, 0.5, 0.3, 1.3)[None], _pose(ev, 1.0, -0.6, 1.3)[None]])
+    ids = torch.tensor(C3_IDS)
+    np.random.seed(29)
+    ro, rd, sel = rs.sample(tform_cam2world=poses)                       # train.py:76
+    tgt = torch.cat([colors.flatten(1, 2)[k, sel[k], :] for k in range(2)], dim=0)   # train.py:77-80
+    oid = ids[:, None].expand(-1, 2048).reshape(-1)
+    before = {f"{k}.{n}": p.detach().clone() for k, m in models.items() for n, p in m.named_parameters()}
+    torch.manual_seed(4343)
+    target_object_embedding = models["embedding"](oid)                  # train.py:96-101
+    rgb_c, rgb_f = nerf.predict_radiance_and_render((ro, rd), ps, emb, models["nerf_coarse"], models["nerf_fine"],
+                                                    target_object_embedding)
+    torch.manual_seed(4343)
+    t_rand, u = torch.rand(4096, 64), torch.rand(4096, 64)
+    lc = torch.nn.functional.mse_loss(rgb_c[..., :3], tgt[..., :3])    # train.py:103-108
+    lf = torch.nn.functional.mse_loss(rgb_f[..., :3], tgt[..., :3])
+    sp, tpar = model_mod.get_params_tensor(models["embedding"], False)
+    reg = 1e-5 * (torch.norm(sp, p=2) + torch.norm(tpar, p=2))
+    loss = lc + lf + reg
+    optimizer.zero_grad()                                               # train.py:111-114
+    loss.backward()
+    grads = {f"{k}.{n}": p.grad.detach().clone() for k, m in models.items() for n, p in m.named_parameters()}
+    optimizer.step()
+    scheduler.step()
+    after = {f"{k}.{n}": p.detach().clone() for k, m in models.items() for n, p in m.named_parameters()}
+    # the draws are re-made by the test from the same seed (torch CPU generator); head + sums pin them
+    out = dict(ro=ro, rd=rd, ids=oid, target=tgt, t_rand_head=t_rand[:4], u_head=u[:4],
+               t_rand_sum=t_rand.double().sum(), u_sum=u.double().sum(), select_inds=sel.astype(np.int64),
+               rgb_coarse=rgb_c, rgb_fine=rgb_f, lc=lc, lf=lf, reg=reg, loss=loss)
+    for k in grads:
+        if k.startswith("embedding."):
+            out["grows_" + k] = grads[k][list(C3_IDS)]
+            out["prows_" + k] = after[k][list(C3_IDS)]
+            # every other row: no gradient, weight decay only (AdamW decays every row of the table)
+            out["gnorm_rest_" + k] = grads[k].norm() ** 2 - grads[k][list(C3_IDS)].norm() ** 2
+        else:
+            out["gnorm_" + k] = grads[k].norm()
+            out["pdelta_norm_" + k] = (after[k] - before[k]).norm()
+    for k in C3_FULL:
+        out["g_" + k] = grads[k]
+        out["p_" + k] = after[k]
+    save("train_c3.npz", **out)
+
+
 ROUND2 = {"trained": gen_trained, "chairs": gen_chairs, "lego": gen_lego, "c5": gen_c5, "se3": gen_se3,
           "srn": gen_srn, "loss": gen_loss}
+ROUND3 = {"c3train": gen_c3train}
 
 
 if __name__ == "__main__":

@@ -343,3 +343,72 @@ def test_train_minibatch_deterministic(dev):
         runs.append({f"{k}.{n_}": p.detach().clone() for k, m in models.items() for n_, p in m.named_parameters()})
     for k in runs[0]:
         assert torch.equal(runs[0][k], runs[1][k]), k
+
+
+@pytest.mark.parametrize("precision", ["f32", "bf16x3"])
+def test_train_c3_chunk_at_size(dev, precision):
+    """C3 at size vs the reference's own chunk step (train_c3.npz, make_golden.py gen_c3train:
+    train.py:96-114 on one 4096-ray chunk of two objects of a 2458-object table, 64 + 64 perturbed
+    samples with the reference's draws, AdamW + LambdaLR): the losses, every parameter's gradient
+    (norms; five tensors in full), the two touched code rows' gradients, and the values after the
+    AdamW step -- the touched rows and the full tensors -- while every untouched row only decays."""
+    from codenerf import synthetic, train as T
+    from codenerf.models import CodeNeRFModel, ShapeTextureEmbedding
+    from codenerf.nerf import PointSampler
+    from test_gpu_parity import load
+    g = load("train_c3.npz", dev)
+    n_obj = 2458
+    emb_t = ShapeTextureEmbedding(n_obj, 256, 256)
+    with torch.no_grad():
+        emb_t.shape_embedding.weight.copy_(synthetic.latent_codes(40, n_obj))
+        emb_t.texture_embedding.weight.copy_(synthetic.latent_codes(41, n_obj))
+    models = {"embedding": emb_t.to(dev)}
+    for key, seed in (("nerf_coarse", 0), ("nerf_fine", 1)):
+        m = CodeNeRFModel(hidden_size=256, shape_code_size=256, texture_code_size=256, num_encoding_fn_xyz=10,
+                          num_encoding_fn_dir=4)
+        m.load_state_dict(synthetic.codenerf_params(seed))
+        models[key] = m.to(dev)
+        m.precision = m.train_precision = precision
+    before = {f"{k}.{n}": p.detach().clone() for k, m in models.items() for n, p in m.named_parameters()}
+    opt, sched = T.prepare_optimizer(_opt_cfg(), models)
+    torch.manual_seed(4343)
+    t_rand, u = torch.rand(4096, 64), torch.rand(4096, 64)
+    assert torch.equal(t_rand[:4].to(dev), g["t_rand_head"]) and torch.equal(u[:4].to(dev), g["u_head"])
+    assert abs(t_rand.double().sum().item() - g["t_rand_sum"].item()) < 1e-6
+    ps = PointSampler(64, 64, 0.8, 1.8, spacing_mode="lindepth", perturb=True, dtype=torch.float32, device=dev)
+    logs = T.train_minibatch(models, opt, sched, ps, embedders(dev), g["ro"], g["rd"], g["ids"].long(), g["target"],
+                             1e-5, uniforms=(t_rand.to(dev), u.to(dev)))
+    torch.cuda.synchronize()
+    for k in ("lc", "lf", "reg"):
+        got = {"lc": logs["nerf_loss_coarse"], "lf": logs["nerf_loss_fine"], "reg": logs["embedding_loss"]}[k]
+        assert abs(float(got) - g[k].item()) <= 1e-5 * max(1.0, abs(g[k].item())), k
+    assert abs(float(logs["total_loss"]) - g["loss"].item()) <= 1e-5
+    rtol = 2e-3 if precision == "f32" else 5e-3
+    named = {f"{k}.{n}": p for k, m in models.items() for n, p in m.named_parameters()}
+    ids = [17, 1234]
+    for k, p in named.items():
+        if k.startswith("embedding."):
+            close(p.grad[ids], g["grows_" + k], rtol, "touched rows grad " + k)
+            rest = float(p.grad.norm() ** 2 - p.grad[ids].norm() ** 2)
+            assert abs(rest) <= 1e-12 and g["gnorm_rest_" + k].item() == 0.0, k
+            # after the step: the touched rows moved by about lr; every other row only decays
+            d = (p.detach()[ids] - g["prows_" + k]).abs()
+            assert d.max().item() <= 2.05e-3 and (d > 1e-6).float().mean().item() < 0.01, k
+            mask = torch.ones(n_obj, dtype=torch.bool, device=dev)
+            mask[ids] = False
+            decayed = before[k][mask] * (1 - 1e-3 * 1e-2)
+            assert (p.detach()[mask] - decayed).abs().max().item() <= 1e-7, k
+        else:
+            ref = g["gnorm_" + k].item()
+            assert abs(p.grad.norm().item() - ref) <= rtol * ref + 1e-8, (k, p.grad.norm().item(), ref)
+            dref = g["pdelta_norm_" + k].item()
+            dgot = (p.detach() - before[k]).norm().item()
+            assert abs(dgot - dref) <= 1e-2 * dref + 1e-9, (k, dgot, dref)
+    for k in ("nerf_coarse.layer_dir1.weight", "nerf_coarse.shape_code_layer1.weight", "nerf_fine.fc_rgb.weight",
+              "nerf_fine.fc_out.bias", "nerf_fine.layer_xyz1.weight"):
+        close(named[k].grad, g["g_" + k], rtol, "grad " + k)
+        d = (named[k].detach() - g["p_" + k]).abs()
+        # AdamW's first step moves each element by ~lr * sign(g): elements whose |g| is near eps may
+        # flip; everything else agrees to float rounding
+        assert d.max().item() <= 2.05e-4 and (d > 1e-6).float().mean().item() < 0.01, k
+    assert sched.last_epoch == 1
