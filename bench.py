@@ -506,17 +506,34 @@ def train_bench(dev, k, iters, world, precision=None):
                      "per-chunk psnr formed on the device (read when logged), no host sync inside an iteration")}
 
 
-def cpu_threads() -> int:
-    """Host threads for the CPU baseline: the process's CPU share (cgroup / affinity), not the
-    machine's count -- on the GPU box os.cpu_count() reports the whole host while the job gets
-    OMP_NUM_THREADS (16) cores."""
-    env = os.environ.get("OMP_NUM_THREADS")
-    if env and env.isdigit() and int(env) > 0:
-        return int(env)
+def cgroup_cpus():
+    """The cgroup v2 CPU quota of this job (cpu.max "quota period") in CPUs, or None."""
     try:
-        return len(os.sched_getaffinity(0))
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        return None if quota == "max" else max(1, int(int(quota) / int(period)))
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_share() -> dict:
+    """The host-core figures the CPU baseline states: OMP_NUM_THREADS, the affinity mask, the cgroup
+    quota, os.cpu_count(), and the threads timed = the job's real share of the host: the affinity
+    mask, capped by the cgroup quota when one is set (on the GPU box os.cpu_count() and the mask can
+    show the whole machine while the job's share is a fraction of it)."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    try:
+        aff = len(os.sched_getaffinity(0))
     except AttributeError:
-        return os.cpu_count() or 1
+        aff = os.cpu_count() or 1
+    quota = cgroup_cpus()
+    threads = min(aff, quota) if quota else aff
+    return {"omp_threads": int(env) if env and env.isdigit() else None, "affinity_cores": aff,
+            "cgroup_cpus": quota, "os_cpu_count": os.cpu_count(), "threads_timed": threads}
+
+
+def cpu_threads() -> int:
+    return cpu_share()["threads_timed"]
 
 
 def cpu_baseline(k, pose1):
@@ -524,7 +541,8 @@ def cpu_baseline(k, pose1):
     C2 = 3 full 128x128 images (64 coarse samples), C3 = 3 samples of one 4096-ray chunk at 64+64."""
     from oracle import codenerf_oracle as O
     from codenerf import synthetic
-    threads = cpu_threads()
+    share = cpu_share()
+    threads = share["threads_timed"]
     torch.set_num_threads(threads)
     d = O.ray_directions(H, W, k)
     ro, rd = O.ray_bundle(d, pose1.cpu())
@@ -553,7 +571,7 @@ def cpu_baseline(k, pose1):
              "hierarchical_64_64": {"value": CHUNK / m3, "unit": "rays/s",
                                     "sample": f"C3: median of 3 renders of one 4096-ray chunk at 64+64: "
                                               f"{', '.join(f'{t:.2f}' for t in c3)} s"},
-             "host": host_cpu()}, ref)
+             "host": host_cpu(), "host_cores": share}, ref)
 
 
 def host_cpu() -> str:

@@ -54,6 +54,31 @@ __device__ __forceinline__ float row_sum(float x) {
   return x;
 }
 
+// Load this lane's run of depths and raw rows (zero past S): 16-B vector loads of the depths
+// when the run is a multiple of 4 aligned to 16 B (every S % 4 == 0 with run % 4 == 0: S = 64,
+// 128 -- the C2 / C3 shapes), element loads otherwise.
+template <int K>
+__device__ __forceinline__ void load_run(const float* zr, const float4* rr, int j0, int run, int S_in, float (&zz)[K],
+                                         float4 (&rv)[K]) {
+  if (K % 4 == 0 && run % 4 == 0 && (S_in & 3) == 0 && j0 + run <= S_in) {
+#pragma unroll
+    for (int q = 0; q < K / 4; ++q) {
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (4 * q < run) v = reinterpret_cast<const float4*>(zr + j0)[q];
+      zz[4 * q] = v.x;
+      zz[4 * q + 1] = v.y;
+      zz[4 * q + 2] = v.z;
+      zz[4 * q + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < K; ++i) zz[i] = (i < run && j0 + i < S_in) ? zr[j0 + i] : 0.0f;
+  }
+#pragma unroll
+  for (int i = 0; i < K; ++i)
+    rv[i] = (i < run && j0 + i < S_in) ? rr[j0 + i] : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
 template <int K>
 __global__ __launch_bounds__(256) void volume_render_kernel(
     const float* __restrict__ raw, const float* __restrict__ z, const float* __restrict__ rd,
@@ -73,18 +98,9 @@ __global__ __launch_bounds__(256) void volume_render_kernel(
   const float d0 = rd[3 * r], d1 = rd[3 * r + 1], d2 = rd[3 * r + 2];
   const float nrm = __fsqrt_rn(__fadd_rn(__fadd_rn(__fmul_rn(d0, d0), __fmul_rn(d1, d1)), __fmul_rn(d2, d2)));
 
-  float zz[K], sd[K];
+  float zz[K], sd[K], wv[K];
   float4 rv[K];
-#pragma unroll
-  for (int i = 0; i < K; ++i) {
-    const int j = j0 + i;
-    zz[i] = 0.0f;
-    rv[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (i < run && j < S_in) {
-      zz[i] = zr[j];
-      rv[i] = rr[j];
-    }
-  }
+  load_run<K>(zr, rr, j0, run, S_in, zz, rv);
   const float znext = dppf<0x101>(zz[0]);  // the first depth of lane sub + 1's run
   double run_sum = 0.0;  // sum of this run's sigma*delta that feeds later transmittances
 #pragma unroll
@@ -106,6 +122,7 @@ __global__ __launch_bounds__(256) void volume_render_kernel(
 #pragma unroll
   for (int i = 0; i < K; ++i) {
     const int j = j0 + i;
+    wv[i] = 0.0f;
     if (i < run && j < S) {
       const float trans = expf(-static_cast<float>(prefix));      // (:54-57)
       const float alpha = __fsub_rn(1.0f, expf(-sd[i]));           // (:58)
@@ -119,8 +136,21 @@ __global__ __launch_bounds__(256) void volume_render_kernel(
       cb += w * c2;
       dep += w * zz[i];
       ac += w;
-      if (weights) weights[r * S_in + j] = w;
+      wv[i] = w;
       if (j + 1 < S) prefix += static_cast<double>(sd[i]);
+    }
+  }
+  if (weights) {  // this lane's run of weights: 16-B stores where the run is aligned (see load_run)
+    float* wr = weights + r * S_in;
+    if (K % 4 == 0 && run % 4 == 0 && (S_in & 3) == 0 && j0 + run <= S_in && S > 0) {
+#pragma unroll
+      for (int q = 0; q < K / 4; ++q)
+        if (4 * q < run)
+          reinterpret_cast<float4*>(wr + j0)[q] = make_float4(wv[4 * q], wv[4 * q + 1], wv[4 * q + 2], wv[4 * q + 3]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < K; ++i)
+        if (i < run && j0 + i < S) wr[j0 + i] = wv[i];
     }
   }
   cr = row_sum(cr);
@@ -195,16 +225,7 @@ __global__ __launch_bounds__(256) void volume_render_backward_kernel(
 
   float sd[K], zz[K], dist[K], sig[K], w[K], tr[K];
   float4 rv[K];
-#pragma unroll
-  for (int i = 0; i < K; ++i) {
-    const int j = j0 + i;
-    zz[i] = 0.0f;
-    rv[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (i < run && j < S_in) {
-      zz[i] = zr[j];
-      rv[i] = rr[j];
-    }
-  }
+  load_run<K>(zr, rr, j0, run, S_in, zz, rv);
   const float znext = dppf<0x101>(zz[0]);
   double run_sum = 0.0;
 #pragma unroll

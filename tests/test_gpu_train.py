@@ -374,7 +374,8 @@ def test_train_c3_chunk_at_size(dev, precision):
     torch.manual_seed(4343)
     t_rand, u = torch.rand(4096, 64), torch.rand(4096, 64)
     assert torch.equal(t_rand[:4].to(dev), g["t_rand_head"]) and torch.equal(u[:4].to(dev), g["u_head"])
-    assert abs(t_rand.double().sum().item() - g["t_rand_sum"].item()) < 1e-6
+    assert abs(t_rand.double().sum().item() - g["t_rand_sum"].item()) < 0.02   # stored as float32
+    assert abs(u.double().sum().item() - g["u_sum"].item()) < 0.02
     ps = PointSampler(64, 64, 0.8, 1.8, spacing_mode="lindepth", perturb=True, dtype=torch.float32, device=dev)
     logs = T.train_minibatch(models, opt, sched, ps, embedders(dev), g["ro"], g["rd"], g["ids"].long(), g["target"],
                              1e-5, uniforms=(t_rand.to(dev), u.to(dev)))
