@@ -185,10 +185,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t mask_rsrc(const unsigned* mask
 // offset is "fresh" here (otherwise LICM hoists the 16 sums out of the tile loop into VGPRs, or,
 // as soffsets, into 16 SGPRs that then spill into VGPR lanes).
 __device__ __forceinline__ int fresh(int v);
+template <int B0 = 0, int NB = 16>
 __device__ __forceinline__ void store_plane(const State& s, __amdgpu_buffer_rsrc_t r, const floatx4* v) {
   const unsigned off = static_cast<unsigned>(fresh(static_cast<int>(s.poff)));
 #pragma unroll
-  for (int ob = 0; ob < 16; ++ob)
+  for (int ob = B0; ob < B0 + NB; ++ob)
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, v[ob]), r, off + 64u * ob, 0, 0);
 }
 
@@ -239,16 +240,21 @@ __device__ __forceinline__ void step_pattern() {
   __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
 }
 
-// Nothing to issue at a chunk's barrier.
+// Nothing to issue during a chunk.
 struct NoPost {
-  __device__ __forceinline__ void operator()() const {}
+  template <int T>
+  __device__ __forceinline__ void step() const {}
 };
 
 // One 16-block chunk of NS k-steps; the B operand of k-step T is getb(T) (compile time).
-// The last k-step reads the next chunk's first fragments into s.pre.  `post` runs right after
-// the chunk's barrier, before its DMA: the previous layer's plane / mask stores go there (the
-// layer input they save is this layer's B operand, live anyway), so they have a whole chunk until
-// the next barrier's vmcnt counts them -- at the layer epilogue they had half of one.
+// The last k-step reads the next chunk's first fragments into s.pre.  `post.step<T>()` runs after
+// k-step T's MFMAs (after the barrier and the DMA at T = 3): the previous layer's plane / mask
+// stores go in the k-steps after the barrier, a few per step (the layer input they save is this
+// layer's B operand, live anyway).  Issued all at once -- at the layer epilogue or right after a
+// barrier -- the 16 stores of every wave of the CU queued behind each other and stalled the
+// waves' instruction issue (PMC: SQ_WAIT_INST_ANY +11 % over the mask-only forward, r03f); spread
+// out they overlap the MFMAs.  They complete in issue order after this chunk's DMA, so the next
+// barrier's counted vmcnt still sees the ring's pieces in order.
 template <int NS, typename GetB, typename Post = NoPost>
 __device__ __forceinline__ void chunk16(State& s, float4* lds, int c, GetB getb, Post post = Post{}) {
   const float4* slot = lds + (c & (kRing - 1)) * kChunkQuads + s.lane;
@@ -266,9 +272,9 @@ __device__ __forceinline__ void chunk16(State& s, float4* lds, int c, GetB getb,
     __builtin_amdgcn_sched_barrier(0);                              \
     if constexpr ((T) == 3) {                                       \
       chunk_barrier();                                              \
-      post();                                                       \
       dma_chunk(s, lds, c + 3);                                     \
     }                                                               \
+    post.template step<(T)>();                                      \
   }
   CN_STEP(0, a0, a1)
   CN_STEP(1, a1, a0)
@@ -377,7 +383,8 @@ __device__ __forceinline__ uint2v relu_act(State& s) {
 }
 
 // The stores a layer's input leaves behind (forward): its ReLU mask words (MASKS, slot ml; ml < 0:
-// none) and, SAVE, its activation plane -- issued at the next chunk barrier (chunk16's `post`).
+// none) and, SAVE, its activation plane -- 4 blocks per k-step in k-steps 4..7 of the next layer's
+// first chunk (chunk16's `post`), the mask words with the first of them.
 template <bool MASKS, bool SAVE>
 struct LayerStores {
   const State& s;
@@ -385,12 +392,17 @@ struct LayerStores {
   int64_t tile;
   int ml, plane;
   uint2v w;
-  __device__ __forceinline__ void operator()() const {
+  template <int B0, int NB>
+  __device__ __forceinline__ void blocks() const {
     if constexpr (MASKS) {
-      if (ml >= 0)
+      if (B0 == 0 && ml >= 0)
         __builtin_amdgcn_raw_buffer_store_b64(w, mask_rsrc(a.masks, tile), 8u * s.lane, mask_soff(s, ml), 0);
     }
-    if constexpr (SAVE) store_plane(s, plane_rsrc(a.save, plane, a.m, tile), s.act);
+    if constexpr (SAVE) store_plane<B0, NB>(s, plane_rsrc(a.save, plane, a.m, tile), s.act);
+  }
+  template <int T>
+  __device__ __forceinline__ void step() const {
+    if constexpr (T >= 4) blocks<4 * (T - 4), 4>();
   }
 };
 
@@ -555,9 +567,9 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
     __builtin_amdgcn_sched_barrier(0);                                                   \
     if constexpr ((G) == 1) {                                                            \
       chunk_barrier();                                                                   \
-      st_v2();                                                                           \
       dma_chunk(s, lds, c + 3);                                                          \
     }                                                                                    \
+    if constexpr ((G) >= 2) st_v2.template blocks<8 * ((G) - 2), 8>();                  \
   }
     CN_RGB(0, a0, a1)
     CN_RGB(1, a1, a0)
@@ -827,9 +839,9 @@ __device__ __forceinline__ void chunk_narrow(State& s, float4* lds, int c, Post 
     __builtin_amdgcn_sched_barrier(0);                              \
     if constexpr ((T) == 3) {                                       \
       chunk_barrier();                                              \
-      post();                                                       \
       dma_chunk(s, lds, c + 3);                                     \
     }                                                               \
+    post.template step<(T)>();                                      \
   }
   CN_NSTEP(0, a0, a1)
   CN_NSTEP(1, a1, a0)
@@ -870,8 +882,9 @@ struct DpreStore {
   const FieldArgs& a;
   int64_t tile;
   int plane;
-  __device__ __forceinline__ void operator()() const {
-    if constexpr (TRAIN) store_plane(s, plane_rsrc(a.dpre, plane, a.m, tile), s.act);
+  template <int T>
+  __device__ __forceinline__ void step() const {  // 4 blocks per k-step in k-steps 4..7 (see chunk16)
+    if constexpr (TRAIN && T >= 4) store_plane<4 * (T - 4), 4>(s, plane_rsrc(a.dpre, plane, a.m, tile), s.act);
   }
 };
 

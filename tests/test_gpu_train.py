@@ -393,8 +393,7 @@ def test_train_c3_chunk_at_size(dev, precision):
             rest = float(p.grad.norm() ** 2 - p.grad[ids].norm() ** 2)
             assert abs(rest) <= 1e-12 and g["gnorm_rest_" + k].item() == 0.0, k
             # after the step: the touched rows moved by about lr; every other row only decays
-            d = (p.detach()[ids] - g["prows_" + k]).abs()
-            assert d.max().item() <= 2.05e-3 and (d > 1e-6).float().mean().item() < 0.01, k
+            _post_step_close(p.detach()[ids], g["prows_" + k], g["grows_" + k], 1e-3, rtol, k)
             mask = torch.ones(n_obj, dtype=torch.bool, device=dev)
             mask[ids] = False
             decayed = before[k][mask] * (1 - 1e-3 * 1e-2)
@@ -408,8 +407,16 @@ def test_train_c3_chunk_at_size(dev, precision):
     for k in ("nerf_coarse.layer_dir1.weight", "nerf_coarse.shape_code_layer1.weight", "nerf_fine.fc_rgb.weight",
               "nerf_fine.fc_out.bias", "nerf_fine.layer_xyz1.weight"):
         close(named[k].grad, g["g_" + k], rtol, "grad " + k)
-        d = (named[k].detach() - g["p_" + k]).abs()
-        # AdamW's first step moves each element by ~lr * sign(g): elements whose |g| is near eps may
-        # flip; everything else agrees to float rounding
-        assert d.max().item() <= 2.05e-4 and (d > 1e-6).float().mean().item() < 0.01, k
+        _post_step_close(named[k].detach(), g["p_" + k], g["g_" + k], 1e-4, rtol, k)
     assert sched.last_epoch == 1
+
+
+def _post_step_close(got, ref, g_ref, lr, rtol, what):
+    """AdamW's first step moves each element by lr g / (|g| + eps) (+ decay): where the reference's
+    |g| is well above both eps (1e-8) and the gradient tolerance (rtol x the tensor's max) that is
+    lr * sign(g) and must agree to float rounding; elsewhere the quotient follows the gradient's last
+    digits, so only the step's bound holds."""
+    d = (got - ref).abs()
+    firm = g_ref.abs() > max(1e-6, 10 * rtol * g_ref.abs().max().item())
+    assert d[firm].max().item() <= 1e-6, (what, d[firm].max().item())
+    assert d.max().item() <= 2.05 * lr, (what, d.max().item())

@@ -24,6 +24,7 @@ def short(name):
 def main(root, subs=()):
     per = collections.defaultdict(lambda: collections.defaultdict(dict))
     dur = collections.defaultdict(dict)
+    gdur = collections.defaultdict(dict)   # durations of the launches GRBM_GUI_ACTIVE was read on
     for f in sorted(glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True)):
         for r in csv.DictReader(open(f)):
             k = short(r["Kernel_Name"])
@@ -32,6 +33,8 @@ def main(root, subs=()):
             key = (f, int(r["Dispatch_Id"]))
             per[k][r["Counter_Name"]][key] = per[k][r["Counter_Name"]].get(key, 0.0) + float(r["Counter_Value"])
             dur[k][key] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+            if r["Counter_Name"] == "GRBM_GUI_ACTIVE":
+                gdur[k][key] = dur[k][key]
     out = {}
     for k in per:
         row = {}
@@ -45,7 +48,10 @@ def main(root, subs=()):
         row["launches"] = len(ds)
         if "GRBM_GUI_ACTIVE" in row:
             cyc = row["GRBM_GUI_ACTIVE"] / 8.0
-            row["clock_ghz"] = cyc / (row["kernel_us"] * 1e3)
+            gd = [gdur[k][d] for d in sorted(gdur[k])]
+            gd = gd[1:] if len(gd) > 1 else gd
+            row["kernel_us_grbm_pass"] = sum(gd) / len(gd)
+            row["clock_ghz"] = cyc / (row["kernel_us_grbm_pass"] * 1e3)
             if "SQ_VALU_MFMA_BUSY_CYCLES" in row:
                 row["mfma_busy"] = row["SQ_VALU_MFMA_BUSY_CYCLES"] / (cyc * 1024)
         if "SQ_WAVE_CYCLES" in row and row["SQ_WAVE_CYCLES"]:
