@@ -326,3 +326,38 @@ def test_srn_item_restatement(tmp_path):
             for k in ("color", "mask", "pose", "intrinsic", "object_id"):
                 ref = g[f"{stage}_{i}_{k}"]
                 assert np.array_equal(np.asarray(item[k]), ref), (stage, i, k)
+
+
+def test_train_c3_chunk_gradients():
+    """C3 at size (train_c3.npz): the reference's own train.py:96-114 chunk step -- 4096 rays of two
+    objects of a 2458-object table, 64 + 64 perturbed samples -- through the oracle's autograd: the
+    losses, every parameter gradient's norm, five full gradients and the touched code rows."""
+    g = load("train_c3.npz")
+    torch.manual_seed(4343)
+    t_rand, u = torch.rand(4096, 64), torch.rand(4096, 64)
+    same(t_rand[:4], g["t_rand_head"])
+    pc, pf = synthetic.codenerf_params(0), synthetic.codenerf_params(1)
+    ts, tt = synthetic.latent_codes(40, 2458).requires_grad_(True), synthetic.latent_codes(41, 2458).requires_grad_(True)
+    for p in list(pc.values()) + list(pf.values()):
+        p.requires_grad_(True)
+    ids = g["ids"].long()
+    out = O.predict_radiance_and_render(g["ro"], g["rd"], O.Sampling(64, 64, 0.8, 1.8), O.EmbedCfg(), pc, pf,
+                                        ts[ids], tt[ids], t_rand, u)
+    tgt = g["target"]
+    lc = torch.nn.functional.mse_loss(out["rgb_coarse"][..., :3], tgt[..., :3])
+    lf = torch.nn.functional.mse_loss(out["rgb_fine"][..., :3], tgt[..., :3])
+    reg = 1e-5 * (torch.norm(ts.data.reshape(-1), p=2) + torch.norm(tt.data.reshape(-1), p=2))
+    (lc + lf + reg).backward()
+    same(lc.detach(), g["lc"], 1e-7)
+    same(lf.detach(), g["lf"], 1e-7)
+    same(reg, g["reg"], 1e-9)
+    named = {**{f"nerf_coarse.{k}": v for k, v in pc.items()}, **{f"nerf_fine.{k}": v for k, v in pf.items()}}
+    for k, p in named.items():
+        ref = g["gnorm_" + k].item()
+        assert abs(p.grad.norm().item() - ref) <= 1e-5 * ref + 1e-9, k
+    for k in ("nerf_coarse.layer_dir1.weight", "nerf_coarse.shape_code_layer1.weight", "nerf_fine.fc_rgb.weight",
+              "nerf_fine.fc_out.bias", "nerf_fine.layer_xyz1.weight"):
+        same(named[k].grad, g["g_" + k], 1e-5 * g["g_" + k].abs().max().item())
+    for t, k in ((ts, "shape_embedding"), (tt, "texture_embedding")):
+        ref = g[f"grows_embedding.{k}.weight"]
+        same(t.grad[[17, 1234]], ref, 1e-5 * ref.abs().max().item())
