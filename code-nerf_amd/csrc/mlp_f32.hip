@@ -185,12 +185,17 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t mask_rsrc(const unsigned* mask
 // offset is "fresh" here (otherwise LICM hoists the 16 sums out of the tile loop into VGPRs, or,
 // as soffsets, into 16 SGPRs that then spill into VGPR lanes).
 __device__ __forceinline__ int fresh(int v);
+#ifdef CN_ABLATE_PLANE_NT
+constexpr int kPlaneCPol = 2;   // experiment: non-temporal (streaming) plane stores
+#else
+constexpr int kPlaneCPol = 0;
+#endif
 template <int B0 = 0, int NB = 16>
 __device__ __forceinline__ void store_plane(const State& s, __amdgpu_buffer_rsrc_t r, const floatx4* v) {
   const unsigned off = static_cast<unsigned>(fresh(static_cast<int>(s.poff)));
 #pragma unroll
   for (int ob = B0; ob < B0 + NB; ++ob)
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, v[ob]), r, off + 64u * ob, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, v[ob]), r, off + 64u * ob, 0, kPlaneCPol);
 }
 
 
