@@ -247,20 +247,21 @@ __device__ __forceinline__ void step_pattern() {
 
 // Nothing to issue during a chunk.
 struct NoPost {
-  template <int T>
+  template <int CI, int T>
   __device__ __forceinline__ void step() const {}
 };
 
 // One 16-block chunk of NS k-steps; the B operand of k-step T is getb(T) (compile time).
-// The last k-step reads the next chunk's first fragments into s.pre.  `post.step<T>()` runs after
-// k-step T's MFMAs (after the barrier and the DMA at T = 3): the previous layer's plane / mask
-// stores go in the k-steps after the barrier, a few per step (the layer input they save is this
-// layer's B operand, live anyway).  Issued all at once -- at the layer epilogue or right after a
-// barrier -- the 16 stores of every wave of the CU queued behind each other and stalled the
-// waves' instruction issue (PMC: SQ_WAIT_INST_ANY +11 % over the mask-only forward, r03f); spread
-// out they overlap the MFMAs.  They complete in issue order after this chunk's DMA, so the next
+// The last k-step reads the next chunk's first fragments into s.pre.  `post.step<CI, T>()` runs
+// after k-step T's MFMAs (after the barrier and the DMA at T = 3) of the layer's chunk CI: the
+// previous layer's plane / mask stores go there, spread over the layer (the layer input they save
+// is this layer's B operand, live anyway).  Issued in bursts -- 16 per wave at the epilogue or
+// after a barrier -- the stores of the CU's 8 waves queued in the vector-memory path with the
+// weight stream's DMA and cost each wave ~250 cycles of issue stall and waitcnt per store (PMC,
+// r03g: SQ_WAIT_INST_ANY +77 M and SQ_WAIT_ANY +55 M quad-cycles over the mask-only forward for
+// 2.09 M stores); two per chunk they overlap the MFMAs.  They follow the chunk's DMA, so the next
 // barrier's counted vmcnt still sees the ring's pieces in order.
-template <int NS, typename GetB, typename Post = NoPost>
+template <int NS, int CI = 0, typename GetB, typename Post = NoPost>
 __device__ __forceinline__ void chunk16(State& s, float4* lds, int c, GetB getb, Post post = Post{}) {
   const float4* slot = lds + (c & (kRing - 1)) * kChunkQuads + s.lane;
   const float4* nslot = lds + ((c + 1) & (kRing - 1)) * kChunkQuads + s.lane;
@@ -279,7 +280,7 @@ __device__ __forceinline__ void chunk16(State& s, float4* lds, int c, GetB getb,
       chunk_barrier();                                              \
       dma_chunk(s, lds, c + 3);                                     \
     }                                                               \
-    post.template step<(T)>();                                      \
+    post.template step<CI, (T)>();                                  \
   }
   CN_STEP(0, a0, a1)
   CN_STEP(1, a1, a0)
@@ -312,14 +313,14 @@ struct ArrB {
 // A 256-input layer: 8 chunks, B from s.act.
 template <typename Post = NoPost>
 __device__ __forceinline__ void layer256(State& s, float4* lds, int& c, Post post = Post{}) {
-  chunk16<8>(s, lds, c + 0, ActB<0>{s}, post);
-  chunk16<8>(s, lds, c + 1, ActB<8>{s});
-  chunk16<8>(s, lds, c + 2, ActB<16>{s});
-  chunk16<8>(s, lds, c + 3, ActB<24>{s});
-  chunk16<8>(s, lds, c + 4, ActB<32>{s});
-  chunk16<8>(s, lds, c + 5, ActB<40>{s});
-  chunk16<8>(s, lds, c + 6, ActB<48>{s});
-  chunk16<8>(s, lds, c + 7, ActB<56>{s});
+  chunk16<8, 0>(s, lds, c + 0, ActB<0>{s}, post);
+  chunk16<8, 1>(s, lds, c + 1, ActB<8>{s}, post);
+  chunk16<8, 2>(s, lds, c + 2, ActB<16>{s}, post);
+  chunk16<8, 3>(s, lds, c + 3, ActB<24>{s}, post);
+  chunk16<8, 4>(s, lds, c + 4, ActB<32>{s}, post);
+  chunk16<8, 5>(s, lds, c + 5, ActB<40>{s}, post);
+  chunk16<8, 6>(s, lds, c + 6, ActB<48>{s}, post);
+  chunk16<8, 7>(s, lds, c + 7, ActB<56>{s}, post);
   c += 8;
 }
 
@@ -388,8 +389,8 @@ __device__ __forceinline__ uint2v relu_act(State& s) {
 }
 
 // The stores a layer's input leaves behind (forward): its ReLU mask words (MASKS, slot ml; ml < 0:
-// none) and, SAVE, its activation plane -- 4 blocks per k-step in k-steps 4..7 of the next layer's
-// first chunk (chunk16's `post`), the mask words with the first of them.
+// none) and, SAVE, its activation plane -- two blocks per chunk of the next layer, at k-step 4
+// (chunk16's `post`), the mask words with the first of them.
 template <bool MASKS, bool SAVE>
 struct LayerStores {
   const State& s;
@@ -405,9 +406,9 @@ struct LayerStores {
     }
     if constexpr (SAVE) store_plane<B0, NB>(s, plane_rsrc(a.save, plane, a.m, tile), s.act);
   }
-  template <int T>
+  template <int CI, int T>
   __device__ __forceinline__ void step() const {
-    if constexpr (T >= 4) blocks<4 * (T - 4), 4>();
+    if constexpr (T == 4) blocks<2 * CI, 2>();
   }
 };
 
@@ -827,7 +828,7 @@ __device__ __forceinline__ void mfma_narrow(State& s, const floatx4* a) {
 }
 
 // A narrow chunk (2 blocks x 64 k-steps, B from s.act) into s.acc2, on chunk16's schedule.
-template <typename Post = NoPost>
+template <int CI = 0, typename Post = NoPost>
 __device__ __forceinline__ void chunk_narrow(State& s, float4* lds, int c, Post post = Post{}) {
   const float4* slot = lds + (c & (kRing - 1)) * kChunkQuads + s.lane;
   const float4* nslot = lds + ((c + 1) & (kRing - 1)) * kChunkQuads + s.lane;
@@ -846,7 +847,7 @@ __device__ __forceinline__ void chunk_narrow(State& s, float4* lds, int c, Post 
       chunk_barrier();                                              \
       dma_chunk(s, lds, c + 3);                                     \
     }                                                               \
-    post.template step<(T)>();                                      \
+    post.template step<CI, (T)>();                                  \
   }
   CN_NSTEP(0, a0, a1)
   CN_NSTEP(1, a1, a0)
@@ -887,9 +888,18 @@ struct DpreStore {
   const FieldArgs& a;
   int64_t tile;
   int plane;
-  template <int T>
-  __device__ __forceinline__ void step() const {  // 4 blocks per k-step in k-steps 4..7 (see chunk16)
-    if constexpr (TRAIN && T >= 4) store_plane<4 * (T - 4), 4>(s, plane_rsrc(a.dpre, plane, a.m, tile), s.act);
+  // two blocks per chunk of a 256-wide layer (see chunk16); in the xyz1 layer's two narrow chunks
+  // (NARROW): eight per chunk, two per k-step 4..7
+  bool narrow = false;
+  template <int CI, int T>
+  __device__ __forceinline__ void step() const {
+    if constexpr (TRAIN) {
+      if (narrow) {
+        if constexpr (T >= 4) store_plane<8 * CI + 2 * (T - 4), 2>(s, plane_rsrc(a.dpre, plane, a.m, tile), s.act);
+      } else if constexpr (T == 4) {
+        store_plane<2 * CI, 2>(s, plane_rsrc(a.dpre, plane, a.m, tile), s.act);
+      }
+    }
   }
 };
 
@@ -1025,8 +1035,8 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   for (int half = 0; half < 2; ++half) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) s.acc2[q] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
-    if (half == 0) chunk_narrow(s, lds, c, DpreStore<TRAIN>{s, a, tile, 4});
-    else chunk_narrow(s, lds, c);
+    if (half == 0) chunk_narrow<0>(s, lds, c, DpreStore<TRAIN>{s, a, tile, 4, true});
+    else chunk_narrow<1>(s, lds, c, DpreStore<TRAIN>{s, a, tile, 4, true});
     c += 1;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
