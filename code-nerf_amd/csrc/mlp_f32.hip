@@ -185,10 +185,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t mask_rsrc(const unsigned* mask
 // offset is "fresh" here (otherwise LICM hoists the 16 sums out of the tile loop into VGPRs, or,
 // as soffsets, into 16 SGPRs that then spill into VGPR lanes).
 __device__ __forceinline__ int fresh(int v);
-#ifdef CN_ABLATE_PLANE_NT
-constexpr int kPlaneCPol = 2;   // experiment: non-temporal (streaming) plane stores
-#else
+// Plane stores are non-temporal (cpol 2): the 400 MB of planes per C3 chunk never fit the L2, and
+// write-back stores evicted the weight stream (forward FETCH 58 -> 6 MB per launch, the backward
+// that reads them 1.5 % faster; r03i). CN_ABLATE_PLANE_WB restores write-back for A/B runs.
+#ifdef CN_ABLATE_PLANE_WB
 constexpr int kPlaneCPol = 0;
+#else
+constexpr int kPlaneCPol = 2;
 #endif
 template <int B0 = 0, int NB = 16>
 __device__ __forceinline__ void store_plane(const State& s, __amdgpu_buffer_rsrc_t r, const floatx4* v) {

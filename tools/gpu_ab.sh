@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of library variants (tools/build_ablations.sh) on the training kernels: HIP-event timing of
 # the field variants, then per variant one FETCH_SIZE and one MFMA-busy PMC pass.
-#   VARIANTS="base PLANE_NT" tools/gpu_ab.sh <tag>
+#   VARIANTS="base PLANE_WB" tools/gpu_ab.sh <tag>
 R=$GRAFT_REPO_ROOT
 TAG=${1:-ab}
 O=$R/gpurun_out/$TAG

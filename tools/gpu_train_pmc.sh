@@ -18,7 +18,7 @@ PASSES=${PMC_PASSES:-"SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE|FETCH_SIZE|WRITE_
 IFS='|' read -ra PASS_LIST <<< "$PASSES"
 for c in "${PASS_LIST[@]}"; do
   tag=$(echo $c | tr ' ' '_')
-  timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $c --kernel-include-regex "field_w16|field_x3" -d $O/pmc_$tag -o run --output-format csv -- python $R/tools/variant_timing.py $PREC > $O/pmc_$tag.log 2>&1
+  timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $c --kernel-include-regex "${PMC_REGEX:-field_w16|field_x3|gemm_tn|reduce_jobs}" -d $O/pmc_$tag -o run --output-format csv -- python $R/tools/variant_timing.py $PREC > $O/pmc_$tag.log 2>&1
   rc=$?; echo "$c rc=$rc"; [ $rc -ne 0 ] && { tail -5 $O/pmc_$tag.log; exit $rc; }
 done
 python $R/tools/pmc_kernels.py $O > $O/pmc_summary.txt && cat $O/pmc_summary.txt
