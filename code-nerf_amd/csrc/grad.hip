@@ -336,19 +336,46 @@ __device__ __forceinline__ void x3_stage(const float* slot, int i, int h, int n0
   }
 }
 
-template <bool X3, bool SIG>
+// DIRS (layer_dir1 only): its 27 view-encoding columns folded into the [feat] pass.  The view
+// direction of sample row k of a chunk of rcnt rays is ray k mod rcnt's (Q1, decode_sample), so the
+// 16 rows j rcnt + d0 .. + 15 of one sample index j share the directions d0 .. d0 + 15 of every j.
+// A stage ("unit") is such a row block, units are ordered (direction group g of 16, j) and each
+// workgroup streams a contiguous run of units; it sums its dPre rows per direction (column sums per
+// stage row) and stores them per (workgroup, group) run into gsum slot (workgroup + g), 16 x 256
+// floats.  dir_enc_dw_kernel then forms dW[:, 256:283] = sum_d dsum[d]^T enc(d) and the bias from
+// them -- the encodings are evaluated once per direction instead of once per sample, and the
+// (M, 256) dPre plane is streamed once instead of twice (by gemm_tn_enc_kernel as well).
+struct DirFold {
+  unsigned n_rays, n_samples, chunk_rows;  // rays, samples per ray, Q1 chunk (multiples of 16)
+  unsigned units_per_block, total_units;   // 16-row units: total = n_rays / 16 * n_samples
+  float* gsum;                             // (workgroups + n_rays / 16) slots of 16 x 256
+};
+
+// First row of unit u (direction group g = u / S, sample index j = u % S).
+__device__ __forceinline__ unsigned dir_unit_row(const DirFold& d, unsigned u) {
+  const unsigned S = d.n_samples, g = u / S, j = u - g * S, D = 16 * g;
+  const unsigned base = (D / d.chunk_rows) * d.chunk_rows;
+  const unsigned rcnt = min(d.chunk_rows, d.n_rays - base);
+  return base * S + j * rcnt + (D - base);
+}
+
+template <bool X3, bool SIG, bool DIRS = false>
 __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restrict__ A, const float* __restrict__ B,
                                                             float* __restrict__ C, int64_t ldc, float* __restrict__ part,
                                                             float* __restrict__ bias_part, const float* __restrict__ draw,
                                                             float* __restrict__ sig_part, int64_t M,
-                                                            int64_t rows_per_block) {
+                                                            int64_t rows_per_block, DirFold dir = {}) {
+  static_assert(!(DIRS && (X3 || SIG)), "the direction fold is the fp32 layer_dir1 pass");
   __shared__ __attribute__((aligned(16))) float ring[kTwRing * kTwStage];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int i = lane & 31, h = lane >> 5;
   const int n0 = (wave >> 1) * 64, k0 = (wave & 1) * 128;
-  const int64_t mb = (int64_t)blockIdx.x * rows_per_block;
-  const int64_t rows = min(rows_per_block, M - mb);
+  // DIRS: the whole plane as one resource (host: M * 1 KiB + 1 KiB < 4 GiB), units u0 .. u1 - 1
+  const int64_t mb = DIRS ? 0 : (int64_t)blockIdx.x * rows_per_block;
+  const int64_t rows = DIRS ? M : min(rows_per_block, M - mb);
+  const unsigned u0 = DIRS ? blockIdx.x * dir.units_per_block : 0u;
+  const unsigned u1 = DIRS ? min(u0 + dir.units_per_block, dir.total_units) : 0u;
   const unsigned bytes = static_cast<unsigned>(rows * 256 * 4);
   const __amdgpu_buffer_rsrc_t ra =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(A + mb * 256), 0, bytes, 0x00020000);
@@ -356,16 +383,22 @@ __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restr
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(B + mb * 256), 0, bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(SIG ? draw + mb * 4 : A), 0, static_cast<unsigned>(SIG ? rows * 16 : 0), 0x00020000);
-  const int n_stages = static_cast<int>((rows + kTwRows - 1) / kTwRows);
+  const int n_stages = DIRS ? static_cast<int>(u1 - u0) : static_cast<int>((rows + kTwRows - 1) / kTwRows);
   // stage st: wave w moves rows w + 8 j of A and of B (j < kTwRows / 8), one 16-B-per-lane
   // wave-instruction per 1 KiB row: kTwRows / 4 wave-instructions per stage; SIG: every wave also
   // moves the stage's 16 d raw rows (256 B, the same bytes: the per-wave vmcnt stays uniform)
   auto dma = [&](int st) {
     float* slot = ring + (st & (kTwRing - 1)) * kTwStage;
+    // DIRS: the unit's first row; units past the run's end (prefetch) read as zeros
+    unsigned row0 = static_cast<unsigned>(st * kTwRows);
+    if constexpr (DIRS) {
+      const unsigned u = u0 + static_cast<unsigned>(st);
+      row0 = u < dir.total_units ? dir_unit_row(dir, u) : static_cast<unsigned>(M);
+    }
 #pragma unroll
     for (int j = 0; j < kTwRows / 8; ++j) {
       const int r = wave + 8 * j;
-      const unsigned soff = __builtin_amdgcn_readfirstlane(static_cast<unsigned>((st * kTwRows + r) * 1024));
+      const unsigned soff = __builtin_amdgcn_readfirstlane((row0 + static_cast<unsigned>(r)) * 1024u);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(slot + r * 256), 16, lane * 16u, soff, 0, 0);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_ptr_t)(slot + (kTwRows + r) * 256), 16, lane * 16u, soff, 0, 0);
     }
@@ -382,14 +415,23 @@ __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restr
 #pragma unroll
     for (int u = 0; u < 4; ++u) acc[t][u] = floatx16{0};
   float bsum[2] = {0.0f, 0.0f};
+  // DIRS: per-direction column sums of the current unit run, rows 2 p + h of columns n0 + 32 t + i
+  // (both waves of a pair sum both column blocks -- a select by wave would become an indexed
+  // private array, which the compiler moves to LDS -- and wave 2 q + t stores block t); flushed:
+  // the previous stage stored them
+  float dsum[DIRS ? 8 : 1][2] = {};
+  const int tw = wave & 1;
+  bool flushed = false;
   dma(0);
   dma(1);
   dma(2);
   for (int st = 0; st < n_stages; ++st) {
     // stage st landed (all but this wave's 2 kTwRows youngest pieces: stages st+1, st+2) and
-    // every wave is done with stage st-1, whose slot then receives stage st+3
+    // every wave is done with stage st-1, whose slot then receives stage st+3; after a DIRS flush
+    // its 8 stores are the youngest 8 vector-memory ops as well
     static_assert(kTwRows / 2 == 8, "the vmcnt below counts stages st+1, st+2");
     if constexpr (SIG) asm volatile("s_waitcnt vmcnt(10)\n\ts_barrier" ::: "memory");
+    else if (DIRS && flushed) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     dma(st + 3);
@@ -416,7 +458,9 @@ __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restr
       }
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        bsum[t] += a[c][t];  // the bias gradient's column sum rides on the A stream (VALU beside MFMA)
+        // the bias gradient's column sum (DIRS: per direction) rides on the A stream (VALU beside MFMA)
+        if constexpr (DIRS) dsum[p][t] += a[c][t];
+        else bsum[t] += a[c][t];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
           acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[c][t], b[c][u], acc[t][u], 0, 0, 0);
@@ -426,6 +470,20 @@ __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restr
           const float dsg = sb[kTwRows * 256 - (h * 256 + i) + (2 * p + h) * 4 + 3];
 #pragma unroll
           for (int u = 0; u < 4; ++u) sacc[u] = fmaf(dsg, b[c][u], sacc[u]);
+        }
+      }
+    }
+    if constexpr (DIRS) {
+      // the run of direction group g ends with this stage: its sums go to slot (workgroup + g)
+      const unsigned u = u0 + static_cast<unsigned>(st);
+      flushed = st + 1 == n_stages || (u + 1) % dir.n_samples == 0;
+      if (flushed) {
+        float* gs = dir.gsum + (int64_t)(blockIdx.x + u / dir.n_samples) * 4096 + h * 256 + n0 + 32 * tw + i;
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+          gs[p * 512] = tw ? dsum[p][1] : dsum[p][0];
+          dsum[p][0] = 0.0f;
+          dsum[p][1] = 0.0f;
         }
       }
     }
@@ -915,6 +973,63 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __rest
     const float b = bsum + __shfl_xor(bsum, 32);
     if (h == 0) bias_part[(int64_t)blockIdx.x * 256 + 32 * wave + i] = b;
   }
+}
+
+// The second half of the DIRS fold (gemm_tn256_kernel): workgroup w of this kernel takes direction
+// groups kDirGroups w .. + kDirGroups - 1; per group it adds the gsum slots of the tn256 workgroups
+// whose unit runs cover it (in workgroup order), evaluates the 16 directions' encodings with
+// gemm_tn_enc_kernel's arithmetic (PositionalEmbedder order: raw 0..2, then per frequency sin 3,
+// cos 3) and accumulates thread n's row of dW: part[w][n][k] = sum_d dsum[d][n] enc(d)[k], k < 27;
+// the bias (enc 1) into bias_part[w][n].  Fixed order throughout: deterministic.
+constexpr int kDirGroups = 4;
+__global__ __launch_bounds__(256) void dir_enc_dw_kernel(mlp::FieldArgs a, DirFold dir, float* __restrict__ part,
+                                                         float* __restrict__ bias_part) {
+  __shared__ float encl[16][28];
+  const int n = threadIdx.x;
+  const unsigned S = dir.n_samples, U = dir.units_per_block, n_groups = dir.n_rays / 16;
+  float acc[28];
+#pragma unroll
+  for (int k = 0; k < 28; ++k) acc[k] = 0.0f;
+  for (int q = 0; q < kDirGroups; ++q) {
+    const unsigned g = blockIdx.x * kDirGroups + q;
+    if (g >= n_groups) break;
+    float ds[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) ds[r] = 0.0f;
+    const unsigned b0 = g * S / U, b1 = ((g + 1) * S - 1) / U;
+    for (unsigned b = b0; b <= b1; ++b) {
+      const float* gs = dir.gsum + (int64_t)(b + g) * 4096 + n;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) ds[r] += gs[r * 256];
+    }
+    __syncthreads();  // the previous group's encodings are read
+    if (n < 16 * 12) {
+      const int r = n / 12, p = n - 12 * (n / 12), comp = p % 3, c0 = 3 + 6 * (p / 3) + comp;
+      float vd[3];
+      mlp::view_dir(a, 16 * (int64_t)g + r, vd);
+      float s, c;
+      sincosf(__fmul_rn(mlp::pick3(vd, comp), a.fd[p / 3]), &s, &c);
+      encl[r][c0] = s;
+      encl[r][c0 + 3] = c;
+    } else if (n < 16 * 13) {
+      const int r = n - 16 * 12;
+      float vd[3];
+      mlp::view_dir(a, 16 * (int64_t)g + r, vd);
+      encl[r][0] = vd[0];
+      encl[r][1] = vd[1];
+      encl[r][2] = vd[2];
+      encl[r][27] = 1.0f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+#pragma unroll
+      for (int k = 0; k < 28; ++k) acc[k] = fmaf(ds[r], encl[r][k], acc[k]);
+  }
+  float* pt = part + (int64_t)blockIdx.x * 256 * 27 + n * 27;
+#pragma unroll
+  for (int k = 0; k < 27; ++k) pt[k] = acc[k];
+  bias_part[(int64_t)blockIdx.x * 256 + n] = acc[27];
 }
 
 // Deterministic column sums (bias gradients dPre^T 1) where no dW kernel folds them in:
@@ -1751,6 +1866,38 @@ static int64_t train_dw_ws_floats(int64_t m) {
          std::max(tn_ws_floats(m, 256, 63), enc_parts(m) * 256 * 63) + 5 * 1024 * 256 + 4 * 256 * 4 + 24 * 64;
 }
 
+// layer_dir1's dW (C: [feat | 27 view-encoding columns], ldc 283) and bias in one pass over its dPre
+// plane (the DIRS fold: gemm_tn256_kernel<false, false, true> + dir_enc_dw_kernel).  Needs the
+// whole-tile plan, whole direction groups (n_rays and the Q1 chunk multiples of 16) and at most
+// `budget` floats of reducer workspace; CN_EUNSUPPORTED otherwise, before anything is launched
+// (the caller then runs the [feat] GEMM and gemm_tn_enc separately).
+static int dir1_dw_folded(const float* dpre, const float* feat, float* C, float* bias, const mlp::FieldArgs& a,
+                          hipStream_t st, Reducer* rd, int64_t budget) {
+  const int64_t M = a.m;
+  const TnPlan pl = tn_plan(dpre, 256, feat, 256, M, 256, 256, false);
+  const int64_t rc = std::min(a.chunk_rows, a.n_rays);
+  if (pl.kind != kTn256 || a.n_rays % 16 || rc % 16 || M * 1024 + 64 * 1024 >= (int64_t(1) << 32))
+    return CN_EUNSUPPORTED;
+  const int64_t total = M / 16, per = ceil_div(total, 256), nb = ceil_div(total, per), groups = a.n_rays / 16;
+  const int64_t nd = ceil_div(groups, grad::kDirGroups);
+  const int64_t need = (nb + groups) * 4096 + nb * 65536 + nd * 256 * 28 + 4 * 64;
+  if (nb > pl.parts || need > budget) return CN_EUNSUPPORTED;
+  grad::DirFold d{static_cast<unsigned>(a.n_rays), static_cast<unsigned>(a.n_samples),
+                  static_cast<unsigned>(rc), static_cast<unsigned>(per),
+                  static_cast<unsigned>(total), rd->take((nb + groups) * 4096)};
+  float* ws = rd->take(nb * 65536);
+  hipLaunchKernelGGL((grad::gemm_tn256_kernel<false, false, true>), dim3(static_cast<unsigned>(nb)), dim3(512), 0, st,
+                     dpre, feat, C, 283, ws, nullptr, nullptr, nullptr, M, 0, d);
+  CN_TRY(launch_status());
+  float* ep = rd->take(nd * 256 * 27);
+  float* bp = rd->take(nd * 256);
+  hipLaunchKernelGGL(grad::dir_enc_dw_kernel, dim3(static_cast<unsigned>(nd)), dim3(256), 0, st, a, d, ep, bp);
+  CN_TRY(launch_status());
+  CN_TRY(reduce(rd, ws, nb, 256, 256, C, 283, st));
+  CN_TRY(reduce(rd, ep, nd, 256, 27, C + 256, 283, st));
+  return reduce(rd, bp, nd, 1, 256, bias, 256, st);
+}
+
 // fc_rgb's dW (C += d rgb^T v2, d_raw's columns 0..2) and, in the same pass, the d raw column sums
 // g_rgb[0..2] += sum d rgb, g_sig[0] += sum d sigma (g_code's rgb / sigma entries with one code row).
 static int rgb_dw_draw_sums(const float* d_raw, const float* v2, float* C, int64_t ldc, int64_t M, float* g_rgb,
@@ -1871,9 +2018,15 @@ extern "C" int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, con
   // layer_dir2
   CN_TRY(gemm_tn(P[0], 256, v1, 256, G(kWDir2), 256, M, 256, 256, st, x3, ws, B(kBDir2), bws, &red));
   // layer_dir1: [feat | dir enc]
-  CN_TRY(gemm_tn(P[1], 256, feat, 256, G(kWDir1), 283, M, 256, 256, st, x3, ws, B(kBDir1), bws, &red));
-  if (x_enc) CN_TRY(gemm_tn(P[1], 256, x_enc + 63, 90, G(kWDir1) + 256, 283, M, 256, 27, st, x3, ws, nullptr, nullptr, &red));
-  else CN_TRY(gemm_tn_enc(1, P[1], a, G(kWDir1) + 256, 283, st, x3, ws, nullptr, nullptr, &red));
+  const int64_t dir1_budget = tn_ws_floats(M, 256, 256) + std::max(tn_ws_floats(M, 256, 27), enc_parts(M) * 256 * 27);
+  const int folded = x3 || x_enc ? CN_EUNSUPPORTED
+                                 : dir1_dw_folded(P[1], feat, G(kWDir1), B(kBDir1), a, st, &red, dir1_budget);
+  if (folded != CN_OK) {
+    if (folded != CN_EUNSUPPORTED) return folded;
+    CN_TRY(gemm_tn(P[1], 256, feat, 256, G(kWDir1), 283, M, 256, 256, st, x3, ws, B(kBDir1), bws, &red));
+    if (x_enc) CN_TRY(gemm_tn(P[1], 256, x_enc + 63, 90, G(kWDir1) + 256, 283, M, 256, 27, st, x3, ws, nullptr, nullptr, &red));
+    else CN_TRY(gemm_tn_enc(1, P[1], a, G(kWDir1) + 256, 283, st, x3, ws, nullptr, nullptr, &red));
+  }
   // fc_out (h half): row 0 from d sigma, rows 1.. from d feat
   CN_TRY(gemm_tn(P[2], 256, h2, 256, G(kWOut) + 512, 512, M, 256, 256, st, x3, ws, gc_feat, bws, &red, d_raw + 3,
                  G(kWOut)));

@@ -68,6 +68,16 @@ struct SampleIn {
   int64_t code_of;  // ray (or row) whose code applies
 };
 
+// Unit view direction of ray dray (rd normalised with the reference's op order); returns |rd|.
+__device__ __forceinline__ float view_dir(const FieldArgs& a, int64_t dray, float (&vd)[3]) {
+  const float d0 = a.rd[3 * dray], d1 = a.rd[3 * dray + 1], d2 = a.rd[3 * dray + 2];
+  const float nrm = __fsqrt_rn(__fadd_rn(__fadd_rn(__fmul_rn(d0, d0), __fmul_rn(d1, d1)), __fmul_rn(d2, d2)));
+  vd[0] = __fdiv_rn(d0, nrm);
+  vd[1] = __fdiv_rn(d1, nrm);
+  vd[2] = __fdiv_rn(d2, nrm);
+  return nrm;
+}
+
 template <int MODE>
 __device__ __forceinline__ SampleIn decode_sample(const FieldArgs& a, int64_t rc) {
   SampleIn in;
@@ -88,12 +98,7 @@ __device__ __forceinline__ SampleIn decode_sample(const FieldArgs& a, int64_t rc
     const int64_t base = (ray / a.chunk_rows) * a.chunk_rows;
     const int64_t rcnt = min(a.chunk_rows, a.n_rays - base);
     const int64_t dray = base + ((ray - base) * S + smp) % rcnt;
-    const float d0 = a.rd[3 * dray], d1 = a.rd[3 * dray + 1], d2 = a.rd[3 * dray + 2];
-    const float nrm = __fsqrt_rn(__fadd_rn(__fadd_rn(__fmul_rn(d0, d0), __fmul_rn(d1, d1)), __fmul_rn(d2, d2)));
-    in.vd[0] = __fdiv_rn(d0, nrm);
-    in.vd[1] = __fdiv_rn(d1, nrm);
-    in.vd[2] = __fdiv_rn(d2, nrm);
-    in.nrm = nrm;
+    in.nrm = view_dir(a, dray, in.vd);
     in.code_of = ray;
   }
   return in;

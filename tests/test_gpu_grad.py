@@ -588,6 +588,52 @@ def test_field_backward_train_generated_encodings(dev, mode, precision):
             assert torch.equal(a, out["generated2"][k]), f"param {k}: not reproducible"
 
 
+@pytest.mark.parametrize("mode,r,s,chunk", [("rayz", 1056, 64, 256),   # 5 Q1 chunks, the last 32 rays
+                                             ("rayz", 1056, 80, 4096),  # unit runs straddle direction groups
+                                             ("pts", 4096, 24, 1024),
+                                             ("rayz", 1050, 64, 256)])  # n_rays % 16 != 0: unfolded path
+def test_field_backward_train_dir1_fold(dev, mode, r, s, chunk):
+    """At M >= 65536 (fp32) layer_dir1's view-encoding dW and bias come from per-direction column
+    sums of its dPre plane taken during the [feat] pass (gemm_tn256_kernel DIRS +
+    dir_enc_dw_kernel): the Q1 map makes rows j rcnt + d of a chunk share direction d.  Checked
+    against the x_enc-plane GEMMs (the encodings as the forward made them) at GEMM_TOL; every other
+    gradient is the same computation, bit for bit; two runs are bitwise identical."""
+    from codenerf import ops, synthetic
+    m = model(dev, 0)
+    params = [p.detach() for p in m.param_list()]
+    g = torch.Generator().manual_seed(r + s)
+    ro = (torch.randn(r, 3, generator=g) * 0.3 + torch.tensor([0.0, 0.0, 1.3])).to(dev)
+    rd = torch.randn(r, 3, generator=g).to(dev)
+    z = torch.sort(0.8 + torch.rand(r, s, generator=g), dim=-1).values.to(dev)
+    pts = (ro[:, None, :] + rd[:, None, :] * z[..., None]).contiguous() if mode == "pts" else None
+    geo = dict(pts=pts) if mode == "pts" else dict(ro=ro, z=z)
+    gout = torch.randn(r, s, 4, generator=g).to(dev)
+    zs, zt = synthetic.latent_codes(5, 1).to(dev), synthetic.latent_codes(6, 1).to(dev)
+    fx, fd = [2.0 ** k for k in range(10)], [2.0 ** k for k in range(4)]
+    cb = ops.code_bias(params, zs, zt)
+    _, saved, masks = ops.radiance_field_train_w16(ops.mlp_pack(params, "f32_w16"), cb, rd, s, chunk, fx, fd,
+                                                   precision="f32", **geo)
+    x_enc = ops.encode_inputs(rd, s, chunk, fx, fd, **geo)
+    packed_t = ops.mlp_pack(params, "f32_w16_t")
+    out = {}
+    for name, xe in (("plane", x_enc), ("folded", None), ("folded2", None)):
+        pg = [torch.zeros_like(p) for p in params]
+        ops.field_backward_train(packed_t, params, masks, saved, xe, gout, r, s, chunk, 1, fx, fd, rd=rd,
+                                 param_grads=pg, precision="f32", **geo)
+        out[name] = pg
+    # layer_xyz1 0 (generated encodings), layer_dir1 12 / its bias 13 (the fold) vs the plane GEMMs
+    for k, (a, b) in enumerate(zip(out["folded"], out["plane"])):
+        if k in (0, 12):
+            close(a, b.double(), GEMM_TOL["f32"], f"param {k} folded vs plane")
+        elif k == 13:
+            close(a, b.double(), 1e-5, "layer_dir1 bias")
+        elif k in (2, 4, 14, 16):
+            assert torch.equal(a, b), f"param {k}: weight gradient outside the fold changed"
+        else:
+            close(a, b.double(), 1e-5, f"bias {k}")
+        assert torch.equal(a, out["folded2"][k]), f"param {k}: not reproducible"
+
+
 @pytest.mark.parametrize("precision", ["f32", "bf16x3"])
 def test_field_backward_train_sigma_rgb_rows(dev, precision):
     """At M >= 65536 the fused training backward folds fc_out's sigma row (d sigma^T h2) into the
