@@ -127,15 +127,61 @@ __device__ __forceinline__ void flush_block(const floatx16& acc, float* C, int64
 
 // C[n][k] += sum_p part[p][n][k], p in order (one thread per element, 4 partial streams per
 // element combined in a fixed tree): the deterministic second pass of the split-M dW GEMMs.
-// Block b of a job covers elements 64 b .. 64 b + 63.
+// Block b of a job covers elements 64 b .. 64 b + 63, or 256 b .. 256 b + 255 with a float4 per
+// thread (reduce_vec4: N K % 4 == 0 and a 16-B aligned workspace; 16-B loads, a quarter of the blocks).  Either way element e's
+// partials are added in the same order -- four interleaved chains per quarter of the parts, the
+// quarters then pairwise -- so both forms give the same bits.
+__host__ __device__ __forceinline__ bool reduce_vec4(const float* part, int64_t nk) {
+  return nk % 4 == 0 && (reinterpret_cast<uintptr_t>(part) & 15) == 0;
+}
+
+__device__ __forceinline__ void reduce_add(float* __restrict__ C, int64_t ldc, int K, int64_t e, float v) {
+  C[(e / K) * ldc + e % K] += v;
+}
+
 __device__ __forceinline__ void reduce_block(const float* __restrict__ part, int64_t n_parts, int N, int K,
-                                             float* __restrict__ C, int64_t ldc, int64_t b, float (&red)[4][64]) {
+                                             float* __restrict__ C, int64_t ldc, int64_t b, float4 (&red)[4][64]) {
   const int q = threadIdx.x >> 6, t = threadIdx.x & 63;
   const int64_t nk = (int64_t)N * K;
+  const int64_t p0 = n_parts * q / 4, p1 = n_parts * (q + 1) / 4;
+  if (reduce_vec4(part, nk)) {
+    const int64_t e = b * 256 + 4 * t;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (e < nk) {
+      float4 s0 = s, s1 = s, s2 = s, s3 = s;
+      const float4* pp = reinterpret_cast<const float4*>(part + e);
+      const int64_t st = nk / 4;
+      int64_t p = p0;
+      for (; p + 4 <= p1; p += 4) {
+        const float4 x0 = pp[p * st], x1 = pp[(p + 1) * st], x2 = pp[(p + 2) * st], x3 = pp[(p + 3) * st];
+        s0.x += x0.x; s0.y += x0.y; s0.z += x0.z; s0.w += x0.w;
+        s1.x += x1.x; s1.y += x1.y; s1.z += x1.z; s1.w += x1.w;
+        s2.x += x2.x; s2.y += x2.y; s2.z += x2.z; s2.w += x2.w;
+        s3.x += x3.x; s3.y += x3.y; s3.z += x3.z; s3.w += x3.w;
+      }
+      for (; p < p1; ++p) {
+        const float4 x0 = pp[p * st];
+        s0.x += x0.x; s0.y += x0.y; s0.z += x0.z; s0.w += x0.w;
+      }
+      s.x = (s0.x + s1.x) + (s2.x + s3.x);
+      s.y = (s0.y + s1.y) + (s2.y + s3.y);
+      s.z = (s0.z + s1.z) + (s2.z + s3.z);
+      s.w = (s0.w + s1.w) + (s2.w + s3.w);
+    }
+    red[q][t] = s;
+    __syncthreads();
+    if (q == 0 && e < nk) {
+      const float4 r0 = red[0][t], r1 = red[1][t], r2 = red[2][t], r3 = red[3][t];
+      reduce_add(C, ldc, K, e, (r0.x + r1.x) + (r2.x + r3.x));
+      reduce_add(C, ldc, K, e + 1, (r0.y + r1.y) + (r2.y + r3.y));
+      reduce_add(C, ldc, K, e + 2, (r0.z + r1.z) + (r2.z + r3.z));
+      reduce_add(C, ldc, K, e + 3, (r0.w + r1.w) + (r2.w + r3.w));
+    }
+    return;
+  }
   const int64_t e = b * 64 + t;
   float s = 0.0f;
   if (e < nk) {
-    const int64_t p0 = n_parts * q / 4, p1 = n_parts * (q + 1) / 4;
     float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
     int64_t p = p0;
     for (; p + 4 <= p1; p += 4) {
@@ -147,18 +193,14 @@ __device__ __forceinline__ void reduce_block(const float* __restrict__ part, int
     for (; p < p1; ++p) s0 += part[p * nk + e];
     s = (s0 + s1) + (s2 + s3);
   }
-  red[q][t] = s;
+  red[q][t].x = s;
   __syncthreads();
-  if (q == 0 && e < nk) {
-    const float v = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
-    float* c = C + (e / K) * ldc + e % K;
-    *c += v;
-  }
+  if (q == 0 && e < nk) reduce_add(C, ldc, K, e, (red[0][t].x + red[1][t].x) + (red[2][t].x + red[3][t].x));
 }
 
 __global__ __launch_bounds__(256) void reduce_partials_kernel(const float* __restrict__ part, int64_t n_parts,
                                                               int N, int K, float* __restrict__ C, int64_t ldc) {
-  __shared__ float red[4][64];
+  __shared__ float4 red[4][64];
   reduce_block(part, n_parts, N, K, C, ldc, blockIdx.x, red);
 }
 
@@ -176,7 +218,7 @@ struct ReduceJobs {
 };
 
 __global__ __launch_bounds__(256) void reduce_jobs_kernel(ReduceJobs jobs) {
-  __shared__ float red[4][64];
+  __shared__ float4 red[4][64];
   int k = jobs.n - 1;
   while (k > 0 && (int64_t)blockIdx.x < jobs.j[k].first_block) --k;
   const ReduceJob& jb = jobs.j[k];
@@ -351,14 +393,6 @@ struct DirFold {
   float* gsum;                             // (workgroups + n_rays / 16) slots of 16 x 256
 };
 
-// First row of unit u (direction group g = u / S, sample index j = u % S).
-__device__ __forceinline__ unsigned dir_unit_row(const DirFold& d, unsigned u) {
-  const unsigned S = d.n_samples, g = u / S, j = u - g * S, D = 16 * g;
-  const unsigned base = (D / d.chunk_rows) * d.chunk_rows;
-  const unsigned rcnt = min(d.chunk_rows, d.n_rays - base);
-  return base * S + j * rcnt + (D - base);
-}
-
 template <bool X3, bool SIG, bool DIRS = false>
 __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restrict__ A, const float* __restrict__ B,
                                                             float* __restrict__ C, int64_t ldc, float* __restrict__ part,
@@ -387,13 +421,30 @@ __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restr
   // stage st: wave w moves rows w + 8 j of A and of B (j < kTwRows / 8), one 16-B-per-lane
   // wave-instruction per 1 KiB row: kTwRows / 4 wave-instructions per stage; SIG: every wave also
   // moves the stage's 16 d raw rows (256 B, the same bytes: the per-wave vmcnt stays uniform)
+  // DIRS: the DMA's unit cursor (dma() runs for st = 0, 1, 2, ... in order): sample index dj of
+  // direction group dg, whose chunk's first row and ray count are dbase * S / drcnt
+  unsigned dj = 0, dg = 0, dbase = 0, drcnt = 0;
+  if constexpr (DIRS) {
+    dg = u0 / dir.n_samples;
+    dj = u0 - dg * dir.n_samples;
+    dbase = (16 * dg / dir.chunk_rows) * dir.chunk_rows;
+    drcnt = min(dir.chunk_rows, dir.n_rays - dbase);
+  }
   auto dma = [&](int st) {
     float* slot = ring + (st & (kTwRing - 1)) * kTwStage;
     // DIRS: the unit's first row; units past the run's end (prefetch) read as zeros
     unsigned row0 = static_cast<unsigned>(st * kTwRows);
     if constexpr (DIRS) {
-      const unsigned u = u0 + static_cast<unsigned>(st);
-      row0 = u < dir.total_units ? dir_unit_row(dir, u) : static_cast<unsigned>(M);
+      row0 = u0 + static_cast<unsigned>(st) < dir.total_units ? dbase * dir.n_samples + dj * drcnt + (16 * dg - dbase)
+                                                               : static_cast<unsigned>(M);
+      if (++dj == dir.n_samples) {
+        dj = 0;
+        ++dg;
+        if (16 * dg >= dbase + drcnt) {  // the next Q1 chunk
+          dbase += drcnt;
+          drcnt = min(dir.chunk_rows, dir.n_rays - dbase);
+        }
+      }
     }
 #pragma unroll
     for (int j = 0; j < kTwRows / 8; ++j) {
@@ -981,7 +1032,7 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __rest
 // gemm_tn_enc_kernel's arithmetic (PositionalEmbedder order: raw 0..2, then per frequency sin 3,
 // cos 3) and accumulates thread n's row of dW: part[w][n][k] = sum_d dsum[d][n] enc(d)[k], k < 27;
 // the bias (enc 1) into bias_part[w][n].  Fixed order throughout: deterministic.
-constexpr int kDirGroups = 4;
+constexpr int kDirGroups = 1;
 __global__ __launch_bounds__(256) void dir_enc_dw_kernel(mlp::FieldArgs a, DirFold dir, float* __restrict__ part,
                                                          float* __restrict__ bias_part) {
   __shared__ float encl[16][28];
@@ -1263,25 +1314,36 @@ __global__ __launch_bounds__(kCodeThreads) void code_backward_kernel(mlp::Params
     // the three code layers (model.py:174-177) recomputed: wave w owns outputs 16 w .. 16 w + 15,
     // one row at a time with its 64 lanes over k (coalesced 1 KiB rows) and a butterfly sum
     const int lane = tid & 63, w = tid >> 6;
-    for (int o = 16 * w; o < 16 * w + 16; ++o) {
-      float a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    // four rows at a time: their 48 loads are in flight together (a row at a time was 16 serial
+    // memory latencies per wave); each row's sums in the same order as before
+    for (int ob = 16 * w; ob < 16 * w + 16; ob += 4) {
+      float a1[4], a2[4], a3[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int k = lane + 64 * u;
-        a1 = fmaf(P.p[kWSc1][o * 256 + k], zs[k], a1);
-        a2 = fmaf(P.p[kWSc2][o * 256 + k], zs[k], a2);
-        a3 = fmaf(P.p[kWTc1][o * 256 + k], zt[k], a3);
+      for (int x = 0; x < 4; ++x) {
+        const int o = ob + x;
+        a1[x] = a2[x] = a3[x] = 0.f;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int k = lane + 64 * u;
+          a1[x] = fmaf(P.p[kWSc1][o * 256 + k], zs[k], a1[x]);
+          a2[x] = fmaf(P.p[kWSc2][o * 256 + k], zs[k], a2[x]);
+          a3[x] = fmaf(P.p[kWTc1][o * 256 + k], zt[k], a3[x]);
+        }
       }
 #pragma unroll
-      for (int off = 32; off > 0; off >>= 1) {
-        a1 += __shfl_xor(a1, off);
-        a2 += __shfl_xor(a2, off);
-        a3 += __shfl_xor(a3, off);
-      }
-      if (lane == 0) {
-        s1[o] = fmaxf(a1 + P.p[kBSc1][o], 0.f);
-        s2[o] = fmaxf(a2 + P.p[kBSc2][o], 0.f);
-        t1[o] = fmaxf(a3 + P.p[kBTc1][o], 0.f);
+      for (int x = 0; x < 4; ++x) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+          a1[x] += __shfl_xor(a1[x], off);
+          a2[x] += __shfl_xor(a2[x], off);
+          a3[x] += __shfl_xor(a3[x], off);
+        }
+        if (lane == 0) {
+          const int o = ob + x;
+          s1[o] = fmaxf(a1[x] + P.p[kBSc1][o], 0.f);
+          s2[o] = fmaxf(a2[x] + P.p[kBSc2][o], 0.f);
+          t1[o] = fmaxf(a3[x] + P.p[kBTc1][o], 0.f);
+        }
       }
     }
   }
@@ -1289,6 +1351,7 @@ __global__ __launch_bounds__(kCodeThreads) void code_backward_kernel(mlp::Params
   // quarter q of the n range per thread, the quarters summed in order
   {
     float a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll 16
     for (int n = 64 * q; n < 64 * q + 64; ++n) {
       a1 = fmaf(P.p[kWXyz2][n * 512 + 256 + j], gx2[n], a1);
       a2 = fmaf(P.p[kWOut][n * 512 + 256 + j], go[n], a2);
@@ -1311,6 +1374,7 @@ __global__ __launch_bounds__(kCodeThreads) void code_backward_kernel(mlp::Params
   __syncthreads();
   if (lead && (dz_s || dz_t)) {
     float a = 0.f, b = 0.f;
+#pragma unroll 16
     for (int n = 64 * q; n < 64 * q + 64; ++n) {
       a = fmaf(P.p[kWSc1][n * 256 + j], ds1[n], a);
       a = fmaf(P.p[kWSc2][n * 256 + j], ds2[n], a);
@@ -1458,7 +1522,7 @@ struct Reducer {
 };
 
 int reduce(Reducer* rd, const float* part, int64_t parts, int N, int K, float* C, int64_t ldc, hipStream_t st) {
-  const int64_t nblk = ceil_div((int64_t)N * K, 64);
+  const int64_t nk = (int64_t)N * K, nblk = ceil_div(nk, grad::reduce_vec4(part, nk) ? 256 : 64);  // reduce_block's
   if (!rd) {
     hipLaunchKernelGGL(grad::reduce_partials_kernel, dim3(static_cast<unsigned>(nblk)), dim3(256), 0, st, part, parts,
                        N, K, C, ldc);
