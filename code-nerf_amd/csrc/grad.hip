@@ -485,7 +485,12 @@ __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restr
     else if (DIRS && flushed) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
+#ifdef CN_ABLATE_TN_NODMA
+    if (st == 0) dma(st + 3);  // experiment: the ring is never refilled (the vmcnt stays counted)
+    else asm volatile("" ::: "memory");
+#else
     dma(st + 3);
+#endif
     if constexpr (X3) {
       x3_stage<SIG>(ring + (st & (kTwRing - 1)) * kTwStage, i, h, n0, k0, acc, bsum, sacc, sig_wave);
       continue;
@@ -510,8 +515,10 @@ __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restr
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         // the bias gradient's column sum (DIRS: per direction) rides on the A stream (VALU beside MFMA)
+#ifndef CN_ABLATE_TN_NOBSUM
         if constexpr (DIRS) dsum[p][t] += a[c][t];
         else bsum[t] += a[c][t];
+#endif
 #pragma unroll
         for (int u = 0; u < 4; ++u)
           acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[c][t], b[c][u], acc[t][u], 0, 0, 0);
@@ -542,6 +549,9 @@ __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restr
   // the prefetched stages past the slab must land before the workgroup's LDS is released
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   float* pt = part ? part + (int64_t)blockIdx.x * 65536 : nullptr;
+#ifdef CN_ABLATE_TN_NOFLUSH
+  if (blockIdx.x == 0 && acc[0][0][0] == 12345.0f)  // experiment: no partial tile written
+#endif
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
