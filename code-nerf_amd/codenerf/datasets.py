@@ -96,9 +96,9 @@ class SRNDataset(torch.utils.data.Dataset):
         k[0, 2], k[1, 2] = cx - crop_w, cy - crop_h
         return object_index, pose.astype(np.float32), k.astype(np.float32), (height, width, crop_h, crop_w)
 
-    def _cropped_u8(self, index) -> np.ndarray:
+    def _cropped_u8(self, index, geo=None) -> np.ndarray:
         _, rgb_filename = self.rgb_all_filenames[index]
-        _, _, _, (height, width, crop_h, crop_w) = self._geometry(index)
+        _, _, _, (height, width, crop_h, crop_w) = geo if geo is not None else self._geometry(index)
         rgb = _decode(rgb_filename)
         return np.ascontiguousarray(rgb[crop_w:width - crop_w, crop_h:height - crop_h, ...])
 
@@ -111,31 +111,51 @@ class SRNDataset(torch.utils.data.Dataset):
                 "mask": (mask / 255.0).astype(np.float32), "pose": pose}
 
     # ---- HBM-resident store ----------------------------------------------------------
-    def load_resident(self, device, threads: Optional[int] = None) -> Dict[str, torch.Tensor]:
-        """Decode every view once (thread pool) into pinned host memory and upload ONE uint8
-        (n_views, h, w, c) tensor + poses / intrinsics / object ids to ``device``."""
+    def load_resident(self, device, threads: Optional[int] = None, chunk_views: int = 256) -> Dict[str, torch.Tensor]:
+        """Decode every view once (thread pool; each view's geometry read once) and upload ONE uint8
+        (n_views, h, w, c) tensor + poses / intrinsics / object ids to ``device``.  The pixels go
+        up in slices of ``chunk_views`` views through two small pinned staging buffers (decode of
+        one slice overlaps the upload of the previous), which are released afterwards: no
+        split-sized pinned host block stays cached for the run."""
         n = len(self)
         assert n > 0, "empty split"
-        geo = [self._geometry(i) for i in range(n)]
+        dev = torch.device(device)
+        pinned = dev.type == "cuda"
         threads = threads or min(16, os.cpu_count() or 1)
         with ThreadPoolExecutor(max_workers=threads) as pool:
-            first = self._cropped_u8(0)
+            geo = list(pool.map(self._geometry, range(n)))
+            first = self._cropped_u8(0, geo[0])
             h, w = first.shape[:2]
             c = first.shape[2] if first.ndim == 3 else 1
-            host = torch.empty((n, h, w, c), dtype=torch.uint8, pin_memory=torch.cuda.is_available())
-            host[0].copy_(torch.from_numpy(first.reshape(h, w, c)))
+            images = torch.empty((n, h, w, c), dtype=torch.uint8, device=dev)
+            per = max(1, min(chunk_views, n))
+            stage = [torch.empty((per, h, w, c), dtype=torch.uint8, pin_memory=pinned) for _ in range(2)]
+            done = [None, None]
+            for k, s0 in enumerate(range(0, n, per)):
+                s1 = min(n, s0 + per)
+                buf = stage[k % 2]
+                if done[k % 2] is not None:
+                    done[k % 2].synchronize()      # the upload that last read this buffer finished
 
-            def fill(i):
-                a = self._cropped_u8(i)
-                if a.shape[:2] != (h, w) or (a.shape[2] if a.ndim == 3 else 1) != c:
-                    raise ValueError(f"view {i} is {a.shape}, the split's first view is {(h, w, c)}: the resident "
-                                     "store needs one image shape per split")
-                host[i].copy_(torch.from_numpy(a.reshape(h, w, c)))
+                def fill(i, buf=buf, s0=s0):
+                    a = first if i == 0 else self._cropped_u8(i, geo[i])
+                    if a.shape[:2] != (h, w) or (a.shape[2] if a.ndim == 3 else 1) != c:
+                        raise ValueError(f"view {i} is {a.shape}, the split's first view is {(h, w, c)}: the "
+                                         "resident store needs one image shape per split")
+                    buf[i - s0].copy_(torch.from_numpy(a.reshape(h, w, c)))
 
-            list(pool.map(fill, range(1, n)))
-        dev = torch.device(device)
+                list(pool.map(fill, range(s0, s1)))
+                images[s0:s1].copy_(buf[: s1 - s0], non_blocking=pinned)
+                if pinned:
+                    done[k % 2] = torch.cuda.Event()
+                    done[k % 2].record()
+            if pinned:
+                torch.cuda.current_stream(dev).synchronize()
+        del stage, done
+        if pinned and hasattr(torch._C, "_host_emptyCache"):
+            torch._C._host_emptyCache()            # hand the staging buffers back to the OS
         self.resident = {
-            "images": host.to(dev, non_blocking=True),
+            "images": images,
             "pose": torch.from_numpy(np.stack([g[1] for g in geo])).to(dev),
             "intrinsic": torch.from_numpy(np.stack([g[2] for g in geo])).to(dev),
             "object_id": torch.tensor([g[0] for g in geo], dtype=torch.int64, device=dev),

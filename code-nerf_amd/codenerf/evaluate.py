@@ -91,7 +91,8 @@ class GraphedEvalStep:
     applies the flat AdamW update (cn_adamw_step_dev, scalars read from device memory).  With
     ``optimizer_in_graph=False`` the caller runs ``optimizer.step()`` after the replay instead.
     The stratified / fine-sample uniforms come from torch's device generator, whose graph-safe
-    state advances per replay.
+    state advances per replay; the warm-up iterations' draws are rolled back (the generator state
+    is restored before capture), so replay i draws what eager iteration i would.
 
     Needs the flat codenerf.optim.AdamW over (shape_code, texture_code, theta, phi, rho), frozen
     model weights (the packed weights stay cached across replays) and ``rng="numpy"``.
@@ -134,6 +135,7 @@ class GraphedEvalStep:
                 self.opt.graph_step(self.d_scal)
             return loss, logs
 
+        rng_state = torch.cuda.get_rng_state(dev)
         side = torch.cuda.Stream(device=dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):          # warm-up outside the capture (lazy inits, weight packs);
@@ -141,6 +143,7 @@ class GraphedEvalStep:
                 body(False)
         torch.cuda.current_stream(dev).wait_stream(side)
         torch.cuda.synchronize(dev)
+        torch.cuda.set_rng_state(rng_state, dev)  # the warm-up's t_rand / u draws never happened
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.loss, self.logs = body(optimizer_in_graph)

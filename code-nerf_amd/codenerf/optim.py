@@ -219,6 +219,9 @@ class AdamW(torch.optim.Optimizer):
         betas, eps = self._hyper()
         segments = self._plan(advance=False)
         assert segments and scalars.numel() >= 3 * len(segments), "graph_step: scalars too small"
+        # the bounds are baked into the captured launch: graph_scalars() checks every later plan
+        # has exactly these (a changed lr / wd / step pattern can merge or split segments)
+        self._graph_bounds = [(b, e) for b, e, *_ in segments]
         f = self._flat
         ops.adamw_step_dev(f["param"], f["grad"], f["exp_avg"], f["exp_avg_sq"], segments, scalars, betas[0],
                            betas[1], eps)
@@ -229,6 +232,11 @@ class AdamW(torch.optim.Optimizer):
         numpy view of the pinned buffer a captured graph copies from)."""
         betas, _ = self._hyper()
         segments = self._plan(advance=True)
+        bounds = getattr(self, "_graph_bounds", None)
+        if bounds is not None and [(b, e) for b, e, *_ in segments] != bounds:
+            raise RuntimeError("graph_scalars: the step's segments differ from the captured graph_step's "
+                               f"({len(segments)} vs {len(bounds)}); per-group lr / weight_decay / step changes "
+                               "that merge or split segments need a new capture")
         ops.adamw_scalars(segments, betas[0], betas[1], out)
         torch.autograd.graph.increment_version(list(self._offs))
 

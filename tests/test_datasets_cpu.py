@@ -73,3 +73,19 @@ def test_resident_loader_draws_dataloader_order(batch_size):
     got = [next(iter(rl)).tolist() for _ in range(6)]
     assert got == ref
     assert len(rl) == len(dl)
+
+
+@pytest.mark.parametrize("chunk_views", [1, 3, 1000])
+def test_load_resident_cpu_slices(tmp_path, chunk_views):
+    """load_resident's sliced upload (two staging buffers, chunk_views views each) fills every view
+    with the crop __getitem__ decodes, whatever the slice size; geometry tensors match item order."""
+    from codenerf.datasets import SRNDataset
+    root = srn_tree.write_tree(str(tmp_path), channels=4)
+    ds = SRNDataset(root, "train")
+    r = ds.load_resident("cpu", threads=2, chunk_views=chunk_views)
+    assert r["images"].shape[0] == len(ds)
+    for i in range(len(ds)):
+        item = ds[i]
+        rgb = r["images"][i].numpy()
+        assert np.array_equal((rgb / 255.0).astype(np.float32), item["color"]), i
+        assert np.array_equal(r["pose"][i].numpy(), item["pose"]) and int(r["object_id"][i]) == item["object_id"]

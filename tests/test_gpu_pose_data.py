@@ -253,10 +253,11 @@ def test_graphed_eval_step_matches_eager(dev, precision):
             close(t.grad, ref, 1e-5, f"replay {i} {name}")
 
 
-def test_time_optimize_graph_matches_eager(dev):
+@pytest.mark.parametrize("perturb", [False, True])
+def test_time_optimize_graph_matches_eager(dev, perturb):
     """test_time_optimize(graph=True) -- forward, backward and the AdamW update in one replay --
-    runs the same iterations as the eager loop (unperturbed samples, the same numpy draws): loss
-    history, codes and pose.  Two iterations: AdamW normalises every element's step, so an element
+    runs the same iterations as the eager loop (the same numpy draws; perturbed: the same device
+    uniforms, since the graph's warm-up draws are rolled back): loss history, codes and pose.  Two iterations: AdamW normalises every element's step, so an element
     whose gradient is ~0 moves by an amount set by the last bits of the atomically summed g_code
     (eager runs differ from each other the same way) and the trajectories drift apart at ~lr level
     over more steps; after two steps they agree to ~1e-6 (a wrong scalar or a missing / extra
@@ -269,10 +270,12 @@ def test_time_optimize_graph_matches_eager(dev):
     for graph in (False, True):
         rs = RaySampler(128, 128, synthetic.srn_intrinsics(128), sample_size=2048, device=dev,
                         datatype=torch.float32)
-        ps = PointSampler(64, 64, 0.8, 1.8, "lindepth", False, torch.float32, dev)
+        ps = PointSampler(64, 64, 0.8, 1.8, "lindepth", perturb, torch.float32, dev)
         codes = (synthetic.latent_codes(5, 4).to(dev), synthetic.latent_codes(6, 4).to(dev))
+        models = _eval_models(dev)
         np.random.seed(23)
-        zs, zt, pose, hist, cam = test_time_optimize(g["target"], (rs, ps), embedders(dev), _eval_models(dev), codes,
+        torch.manual_seed(31)
+        zs, zt, pose, hist, cam = test_time_optimize(g["target"], (rs, ps), embedders(dev), models, codes,
                                                      iterations=2, graph=graph)
         out[graph] = (zs.detach(), zt.detach(), torch.cat([p.detach().reshape(-1) for p in pose]), hist, cam)
     e, q = out[False], out[True]

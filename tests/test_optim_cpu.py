@@ -75,6 +75,21 @@ def test_step_needs_the_gpu():
         opt.step()
 
 
+def test_graph_scalars_refuses_changed_segments():
+    """A captured graph_step bakes its segment bounds into the launch: a later lr change that merges
+    two groups' segments must stop graph_scalars instead of shifting scalars onto the wrong slices."""
+    ps = _params()
+    opt = _opt(ps)
+    for p in ps:
+        p.grad = torch.ones_like(p)
+    opt._sync_grads()
+    opt._graph_bounds = [(b, e) for b, e, *_ in opt._plan(advance=False)]   # as graph_step records them
+    assert len(opt._graph_bounds) == 2
+    opt.param_groups[1]["lr"] = opt.param_groups[0]["lr"]                  # the two groups now merge
+    with pytest.raises(RuntimeError, match="need a new capture"):
+        opt.graph_scalars(np.zeros(6, dtype=np.float32))
+
+
 def test_refuses_unsupported_options():
     from codenerf.optim import AdamW
     with pytest.raises(NotImplementedError):
