@@ -1654,8 +1654,13 @@ int64_t tn_ws_floats(int64_t M, int N, int K) {
 // dW of an encoding layer (ENC 0: layer_xyz1 from dPre(xyz1), ENC 1: layer_dir1's view columns
 // from dPre(dir1)) with the encodings generated in the kernel; ws: the deterministic path
 // (enc_ws_parts(M) * 256 * K floats).
+#ifdef CN_ABLATE_ENC512
+constexpr int64_t kEncBlocks = 512;  // experiment: one round of two workgroups per CU
+#else
+constexpr int64_t kEncBlocks = 1024;
+#endif
 int64_t enc_rows(int64_t M) {
-  return std::max<int64_t>(grad::kEncRows, ceil_div(ceil_div(M, 1024), grad::kEncRows) * grad::kEncRows);
+  return std::max<int64_t>(grad::kEncRows, ceil_div(ceil_div(M, kEncBlocks), grad::kEncRows) * grad::kEncRows);
 }
 int64_t enc_parts(int64_t M) { return ceil_div(M, enc_rows(M)); }
 

@@ -86,9 +86,9 @@ __global__ void pack_kernel(Params P, float* __restrict__ packed) {
 constexpr int kCbThreads = 512;
 constexpr int kCbSlices = 17;
 
-__device__ __forceinline__ float wave_dot256(const float* __restrict__ w, const float* v, int lane) {
-  const float4 a = reinterpret_cast<const float4*>(w)[lane];
-  const float4 b = reinterpret_cast<const float4*>(v)[lane];
+// The dot of a 256-float row with v as 64 lanes x float4 (w, x: this lane's quarter), summed by a
+// butterfly: every lane ends with the total.
+__device__ __forceinline__ float wave_dot4(float4 a, float4 b) {
   float s = fmaf(a.x, b.x, fmaf(a.y, b.y, fmaf(a.z, b.z, a.w * b.w)));
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
@@ -106,14 +106,27 @@ __global__ __launch_bounds__(kCbThreads) void code_bias_kernel(Params P, const f
   if (t < kCode) z[t] = (l == 2 ? z_t : z_s)[c * kCode + t];
   __syncthreads();
   {
+    // rows wave + 8 i: eight rows' loads in flight per round (no branch between them), the lane-0
+    // writes after; bias + ReLU once per output below
     const float* W = P.p[l == 0 ? kWSc1 : (l == 1 ? kWSc2 : kWTc1)];
-    const float* B = P.p[l == 0 ? kBSc1 : (l == 1 ? kBSc2 : kBTc1)];
-#pragma unroll 8
-    for (int i = 0; i < kCode / kW; ++i) {
-      const int j = wave + i * kW;
-      const float a = wave_dot256(W + j * kCode, z, lane);
-      if (lane == 0) hv[j] = fmaxf(a + B[j], 0.f);
+    const float4 zv = reinterpret_cast<const float4*>(z)[lane];
+#pragma unroll
+    for (int i0 = 0; i0 < kCode / kW; i0 += 8) {
+      float4 wv[8];
+#pragma unroll
+      for (int x = 0; x < 8; ++x) wv[x] = reinterpret_cast<const float4*>(W + (wave + (i0 + x) * kW) * kCode)[lane];
+      float d[8];
+#pragma unroll
+      for (int x = 0; x < 8; ++x) d[x] = wave_dot4(wv[x], zv);
+      if (lane == 0)
+#pragma unroll
+        for (int x = 0; x < 8; ++x) hv[wave + (i0 + x) * kW] = d[x];
     }
+  }
+  __syncthreads();
+  if (t < kCode) {
+    const float* B = P.p[l == 0 ? kBSc1 : (l == 1 ? kBSc2 : kBTc1)];
+    hv[t] = fmaxf(hv[t] + B[t], 0.f);
   }
   __syncthreads();
   float* o = out + c * kCbStride;
@@ -121,22 +134,31 @@ __global__ __launch_bounds__(kCbThreads) void code_bias_kernel(Params P, const f
   if (l == 0) { r0 = 32 * q; nr = 32; }
   else if (l == 1) { r0 = 32 * (q - 8); nr = q == 15 ? 33 : 32; }
   else { r0 = 0; nr = 3; }
-  for (int r = r0 + wave; r < r0 + nr; r += kW) {
+  // at most 5 rows per wave (33 / 8): all their loads first, then the dots
+  const float4 hq = reinterpret_cast<const float4*>(hv)[lane];
+  float4 wv[5];
+  float bv[5];
+  int dst[5];
+#pragma unroll
+  for (int x = 0; x < 5; ++x) {
+    const int r = min(r0 + wave + x * kW, r0 + nr - 1);  // rows past the slice repeat its last (not stored)
     const float* w;
-    float b;
-    int dst;
     if (l == 0) {
-      w = P.p[kWXyz2] + r * (kHidden + kCode) + kHidden; b = P.p[kBXyz2][r]; dst = kCbXyz2 + r;
+      w = P.p[kWXyz2] + r * (kHidden + kCode) + kHidden; bv[x] = P.p[kBXyz2][r]; dst[x] = kCbXyz2 + r;
     } else if (l == 1) {
       // slice rows 0..255 map to fc_out rows 1..256 (feat); row 256 -> fc_out row 0 (sigma)
       const int i = r == kCode ? 0 : r + 1;
-      w = P.p[kWOut] + i * (kHidden + kCode) + kHidden; b = P.p[kBOut][i];
-      dst = i == 0 ? kCbSigma : kCbFeat + i - 1;
+      w = P.p[kWOut] + i * (kHidden + kCode) + kHidden; bv[x] = P.p[kBOut][i];
+      dst[x] = i == 0 ? kCbSigma : kCbFeat + i - 1;
     } else {
-      w = P.p[kWRgb] + r * (kHidden + kCode) + kHidden; b = P.p[kBRgb][r]; dst = kCbRgb + r;
+      w = P.p[kWRgb] + r * (kHidden + kCode) + kHidden; bv[x] = P.p[kBRgb][r]; dst[x] = kCbRgb + r;
     }
-    const float a = wave_dot256(w, hv, lane);
-    if (lane == 0) o[dst] = a + b;
+    wv[x] = reinterpret_cast<const float4*>(w)[lane];
+  }
+#pragma unroll
+  for (int x = 0; x < 5; ++x) {
+    const float a = wave_dot4(wv[x], hq);
+    if (lane == 0 && wave + x * kW < nr) o[dst[x]] = a + bv[x];
   }
   if (l == 2 && t >= 3 && t < kCbStride - kCbRgb) o[kCbRgb + t] = 0.f;  // pad 516..519
 }
