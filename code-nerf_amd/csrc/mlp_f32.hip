@@ -598,8 +598,16 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
   }
 }
 
+#ifdef CN_ABLATE_WGTIME
+// experiment: each workgroup's start / end wall clock (100 MHz), read by cn_debug_wgtime
+__device__ long long g_wgtime[2048][2];
+#endif
+
 template <int MODE, bool MASKS, bool SAVE = false>
 __global__ __launch_bounds__(kThreads, 2) void field_w16_kernel(FieldArgs a) {
+#ifdef CN_ABLATE_WGTIME
+  const long long t_start = wall_clock64();
+#endif
   // ONE LDS object (a second one makes hipcc wait vmcnt(0) before ring reads): the DMA
   // ring, then the constants, then one code-bias row per wave
   __shared__ __attribute__((aligned(16))) float4 lds[kLdsQuads];
@@ -632,6 +640,12 @@ __global__ __launch_bounds__(kThreads, 2) void field_w16_kernel(FieldArgs a) {
   // the last tile prefetched chunks 0..2 of a tile that does not exist: they must land
   // before the workgroup's LDS is released
   __builtin_amdgcn_s_waitcnt(0x0F70);
+#ifdef CN_ABLATE_WGTIME
+  if (threadIdx.x == 0 && blockIdx.x < 2048) {
+    g_wgtime[blockIdx.x][0] = t_start;
+    g_wgtime[blockIdx.x][1] = wall_clock64();
+  }
+#endif
 }
 
 
@@ -1217,3 +1231,11 @@ int launch_field_w16_bwd(int mode, FieldArgs& a, hipStream_t st) {
 
 }  // namespace mlp
 }  // namespace cn
+
+#ifdef CN_ABLATE_WGTIME
+// experiment: copy the last field_w16_kernel launch's per-workgroup (start, end) wall clocks
+extern "C" int cn_debug_wgtime(long long* out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(cn::mlp::w16::g_wgtime), sizeof(long long) * 2 * std::min(n, 2048)) ==
+                 hipSuccess ? 0 : -1;
+}
+#endif
