@@ -433,7 +433,11 @@ __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restr
   auto dma = [&](int st) {
     float* slot = ring + (st & (kTwRing - 1)) * kTwStage;
     // DIRS: the unit's first row; units past the run's end (prefetch) read as zeros
+#ifdef CN_ABLATE_TN_L2DMA
+    unsigned row0 = static_cast<unsigned>((st & 3) * kTwRows);  // experiment: 4 stages of rows, L2-resident
+#else
     unsigned row0 = static_cast<unsigned>(st * kTwRows);
+#endif
     if constexpr (DIRS) {
       row0 = u0 + static_cast<unsigned>(st) < dir.total_units ? dbase * dir.n_samples + dj * drcnt + (16 * dg - dbase)
                                                                : static_cast<unsigned>(M);

@@ -58,8 +58,7 @@ __device__ __forceinline__ float row_sum(float x) {
 // when the run is a multiple of 4 aligned to 16 B (every S % 4 == 0 with run % 4 == 0: S = 64,
 // 128 -- the C2 / C3 shapes), element loads otherwise.
 template <int K>
-__device__ __forceinline__ void load_run(const float* zr, const float4* rr, int j0, int run, int S_in, float (&zz)[K],
-                                         float4 (&rv)[K]) {
+__device__ __forceinline__ void load_depths(const float* zr, int j0, int run, int S_in, float (&zz)[K]) {
   if (K % 4 == 0 && run % 4 == 0 && (S_in & 3) == 0 && j0 + run <= S_in) {
 #pragma unroll
     for (int q = 0; q < K / 4; ++q) {
@@ -74,9 +73,49 @@ __device__ __forceinline__ void load_run(const float* zr, const float4* rr, int 
 #pragma unroll
     for (int i = 0; i < K; ++i) zz[i] = (i < run && j0 + i < S_in) ? zr[j0 + i] : 0.0f;
   }
+}
+
+template <int K>
+__device__ __forceinline__ void load_run(const float* zr, const float4* rr, int j0, int run, int S_in, float (&zz)[K],
+                                         float4 (&rv)[K]) {
+  load_depths<K>(zr, j0, run, S_in, zz);
 #pragma unroll
   for (int i = 0; i < K; ++i)
     rv[i] = (i < run && j0 + i < S_in) ? rr[j0 + i] : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+// Raw rows through LDS (K <= 8, i.e. S <= 128): a lane's run of float4 samples is 16 run bytes
+// apart from its neighbour's, so per-lane loads of it touch every cache line four (eight) times.
+// The wave's four rays' rows are ONE contiguous (4 S) float4 block: lane l copies quads
+// l + 64 t with coalesced 16-B loads into LDS slot pad(q) = q + q / 4 (a padding quad after every
+// four: runs of four then sit 5 quads apart, conflict-free across a 16-lane group), and each lane
+// then reads its own run from there.  The backward stores d raw back the same way.
+constexpr int kLdsMaxK = 8;
+__device__ __forceinline__ int pad4(int q) { return q + (q >> 2); }
+
+template <int K>
+__device__ __forceinline__ void stage_rows_in(const float4* __restrict__ src, int nq, float4* sl, int lane) {
+#pragma unroll
+  for (int t = 0; t < K; ++t) {
+    const int q = lane + 64 * t;
+    if (q < nq) sl[pad4(q)] = src[q];
+  }
+}
+
+template <int K>
+__device__ __forceinline__ void stage_rows_out(float4* __restrict__ dst, int nq, const float4* sl, int lane) {
+#pragma unroll
+  for (int t = 0; t < K; ++t) {
+    const int q = lane + 64 * t;
+    if (q < nq) dst[q] = sl[pad4(q)];
+  }
+}
+
+// This lane's run of raw rows from the wave's LDS copy (q0: the run's first quad in the wave block).
+template <int K>
+__device__ __forceinline__ void load_raw_lds(const float4* sl, int q0, int j0, int run, int S_in, float4 (&rv)[K]) {
+#pragma unroll
+  for (int i = 0; i < K; ++i) rv[i] = (i < run && j0 + i < S_in) ? sl[pad4(q0 + i)] : make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
 template <int K>
@@ -84,8 +123,17 @@ __global__ __launch_bounds__(256) void volume_render_kernel(
     const float* __restrict__ raw, const float* __restrict__ z, const float* __restrict__ rd,
     int64_t n_rays, int S_in, float* __restrict__ rgb, float* __restrict__ disp,
     float* __restrict__ acc, float* __restrict__ weights, float* __restrict__ depth) {
-  const int sub = threadIdx.x & 15;
+  constexpr bool kLds = K <= kLdsMaxK;
+  __shared__ float4 slds[kLds ? 4 * 80 * K : 1];  // per wave: 4 rays x <= 16 K quads, padded 5 / 4
+  const int sub = threadIdx.x & 15, lane = threadIdx.x & 63;
   const int64_t r = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
+  const int64_t rw0 = r - (lane >> 4);  // the wave's first ray
+  float4* sl = slds + (kLds ? (threadIdx.x >> 6) * 80 * K : 0);
+  if constexpr (kLds) {
+    if (rw0 < n_rays)
+      stage_rows_in<K>(reinterpret_cast<const float4*>(raw) + rw0 * S_in,
+                       static_cast<int>(min<int64_t>(4, n_rays - rw0)) * S_in, sl, lane);
+  }
   if (r >= n_rays) return;  // whole rows leave together: the DPP steps never read an exited lane
   // S == 1: the reference's dists = cat(z[1:] - z[:-1], full_like(that[..., :1], 1e10))
   // is EMPTY (both pieces are 0 wide), so no sample contributes (rgb = acc = depth = 0,
@@ -100,7 +148,12 @@ __global__ __launch_bounds__(256) void volume_render_kernel(
 
   float zz[K], sd[K], wv[K];
   float4 rv[K];
-  load_run<K>(zr, rr, j0, run, S_in, zz, rv);
+  if constexpr (kLds) {
+    load_depths<K>(zr, j0, run, S_in, zz);
+    load_raw_lds<K>(sl, (lane >> 4) * S_in + j0, j0, run, S_in, rv);
+  } else {
+    load_run<K>(zr, rr, j0, run, S_in, zz, rv);
+  }
   const float znext = dppf<0x101>(zz[0]);  // the first depth of lane sub + 1's run
   double run_sum = 0.0;  // sum of this run's sigma*delta that feeds later transmittances
 #pragma unroll
@@ -211,9 +264,20 @@ __global__ __launch_bounds__(256) void volume_render_backward_kernel(
     int64_t n_rays, int S_in, const float* __restrict__ g_rgb, const float* __restrict__ g_disp,
     const float* __restrict__ g_acc, const float* __restrict__ g_w, const float* __restrict__ g_depth,
     float* __restrict__ d_raw, float* __restrict__ d_rd) {
-  const int sub = threadIdx.x & 15;
-  const int64_t r = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
-  if (r >= n_rays) return;
+  constexpr bool kLds = K <= kLdsMaxK;
+  __shared__ float4 slds[kLds ? 4 * 80 * K : 1];  // per wave: raw in, then d raw out (forward's layout)
+  const int sub = threadIdx.x & 15, lane = threadIdx.x & 63;
+  const int64_t r_ = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
+  const int64_t rw0 = r_ - (lane >> 4);
+  if (rw0 >= n_rays) return;  // the whole wave
+  const int nq = static_cast<int>(min<int64_t>(4, n_rays - rw0)) * S_in;  // the wave's valid quads
+  float4* sl = slds + (kLds ? (threadIdx.x >> 6) * 80 * K : 0);
+  if constexpr (kLds) stage_rows_in<K>(reinterpret_cast<const float4*>(raw) + rw0 * S_in, nq, sl, lane);
+  // LDS path: a row past n_rays stays alive (as a copy of the last ray, nothing stored) so the
+  // wave's coalesced d raw copy-out runs in every lane; else it leaves here
+  const bool live = r_ < n_rays;
+  if (!kLds && !live) return;
+  const int64_t r = live ? r_ : n_rays - 1;
   const int S = S_in == 1 ? 0 : S_in;  // see the forward: S == 1 has no contributing sample
   const int run = (S_in + 15) >> 4;
   const int j0 = sub * run;
@@ -225,7 +289,14 @@ __global__ __launch_bounds__(256) void volume_render_backward_kernel(
 
   float sd[K], zz[K], dist[K], sig[K], w[K], tr[K];
   float4 rv[K];
-  load_run<K>(zr, rr, j0, run, S_in, zz, rv);
+  const int q0 = (lane >> 4) * S_in + j0;  // this run's first quad in the wave block
+  if constexpr (kLds) {
+    load_depths<K>(zr, j0, run, S_in, zz);
+    if (live) load_raw_lds<K>(sl, q0, j0, run, S_in, rv);
+    else load_run<K>(zr, rr, j0, run, S_in, zz, rv);  // the last ray again (not in this wave's block)
+  } else {
+    load_run<K>(zr, rr, j0, run, S_in, zz, rv);
+  }
   const float znext = dppf<0x101>(zz[0]);
   double run_sum = 0.0;
 #pragma unroll
@@ -299,14 +370,23 @@ __global__ __launch_bounds__(256) void volume_render_backward_kernel(
       const float dsp = x > 20.0f ? 1.0f : cn::sigmoidf_(x);
       float4 o = rv[i];
       o.w = dsd * (dist[i] * nrm) * dsp;
-      dr[j] = o;
+      if (kLds) {
+        if (live) sl[pad4(q0 + i)] = o;
+      } else {
+        dr[j] = o;
+      }
       gnorm += dsd * sig[i] * dist[i];
     } else if (i < run && j < S_in) {
-      dr[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (kLds) {
+        if (live) sl[pad4(q0 + i)] = make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+        dr[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
     }
   }
+  if constexpr (kLds) stage_rows_out<K>(reinterpret_cast<float4*>(d_raw) + rw0 * S_in, nq, sl, lane);
   gnorm = row_sum(gnorm);
-  if (sub == 15 && d_rd) {
+  if (live && sub == 15 && d_rd) {
     const float inv = nrm > 0.f ? gnorm / nrm : 0.f;
     d_rd[3 * r] = inv * d0;
     d_rd[3 * r + 1] = inv * d1;
