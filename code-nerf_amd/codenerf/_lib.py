@@ -89,6 +89,8 @@ SIGNATURES = {
     "cn_field_backward_x3": (_i, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p, _i64, _fp, _fp, _p, _p, _p, _p,
                                   _p]),
     "cn_code_bias_backward": (_i, [ctypes.POINTER(_p), _p, _p, _i64, _p, _p, _p, ctypes.POINTER(_p), _p]),
+    "cn_code_bias_backward_workspace_floats": (_i64, [_i64]),
+    "cn_code_bias_backward_ws": (_i, [ctypes.POINTER(_p), _p, _p, _i64, _p, _p, _p, ctypes.POINTER(_p), _p, _p]),
     "cn_volume_render_backward": (_i, [_p, _p, _p, _i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p]),
     "cn_ray_bundle_backward": (_i, [_p, _i64, _i64, _p, _p, _p, _p]),
     "cn_gather_rays_backward": (_i, [_p, _p, _i64, _i64, _p, _i64, _p, _p, _p]),

@@ -564,8 +564,11 @@ def field_backward(params: Sequence[Tensor], saved: Tensor, x_enc: Tensor, d_raw
 
 
 def code_bias_backward(params: Sequence[Tensor], z_s: Tensor, z_t: Tensor, g_code: Tensor,
-                       param_grads: Optional[Sequence[Tensor]] = None, want_z: bool = True):
-    """Backward of code_bias (model.py:174-177 + the code halves) -> dz_s, dz_t (n_codes, 256) or None."""
+                       param_grads: Optional[Sequence[Tensor]] = None, want_z: bool = True,
+                       single_launch: bool = False):
+    """Backward of code_bias (model.py:174-177 + the code halves) -> dz_s, dz_t (n_codes, 256) or None.
+    The two-launch form (cn_code_bias_backward_ws) unless single_launch (cn_code_bias_backward):
+    bitwise the same results."""
     lib = _lib_ready()
     params = [_cuda(p.detach(), f"param{i}") for i, p in enumerate(params)]
     z_s, z_t, g_code = _cuda(z_s.detach(), "z_s"), _cuda(z_t.detach(), "z_t"), _cuda(g_code, "g_code")
@@ -576,8 +579,13 @@ def code_bias_backward(params: Sequence[Tensor], z_s: Tensor, z_t: Tensor, g_cod
     garr, gkeep = (None, None)
     if param_grads is not None:
         garr, gkeep = _lib.pointer_array(list(param_grads))
-    check(lib.cn_code_bias_backward(arr, ptr(z_s), ptr(z_t), n, ptr(g_code), ptr(dz_s), ptr(dz_t), garr,
-                                    stream_of(g_code)), "cn_code_bias_backward")
+    if single_launch:
+        check(lib.cn_code_bias_backward(arr, ptr(z_s), ptr(z_t), n, ptr(g_code), ptr(dz_s), ptr(dz_t), garr,
+                                        stream_of(g_code)), "cn_code_bias_backward")
+    else:
+        ws = torch.empty(lib.cn_code_bias_backward_workspace_floats(n), device=g_code.device, dtype=torch.float32)
+        check(lib.cn_code_bias_backward_ws(arr, ptr(z_s), ptr(z_t), n, ptr(g_code), ptr(dz_s), ptr(dz_t), garr,
+                                           ptr(ws), stream_of(g_code)), "cn_code_bias_backward_ws")
     del keep, gkeep
     return dz_s, dz_t
 

@@ -1423,6 +1423,169 @@ __global__ __launch_bounds__(kCodeThreads) void code_backward_kernel(mlp::Params
   for (int r = 0; r < 3; ++r) atomicAdd(&const_cast<float*>(G.p[kWRgb])[r * 512 + 256 + j], grgb[r] * t1j);
 }
 
+// The same backward in two launches (cn_code_bias_backward_ws).  code_backward_kernel recomputes
+// the three code layers and the three 256-long reductions in each of its 16 workgroups per code
+// (about 2 MiB of L2 reads per workgroup: ~55 us for one code).  Here workgroup y of
+// code_layers_dz_kernel forms outputs 16 y .. 16 y + 15 of s1 / s2 / t1 and of ds1 / ds2 / dt1
+// into the workspace (per code: s1 s2 t1 ds1 ds2 dt1, 6 x 256 floats), and workgroup y of
+// code_outer_kernel forms dz_s / dz_t for columns 16 y .. and the outer products of rows 16 y ..
+// Every sum keeps code_backward_kernel's order: bitwise the same results.
+constexpr int kCodeSlices = 16;  // workgroups per code, 16 outputs each
+
+// Whether any sample used code row gr (all its code-term gradients zero otherwise), as
+// code_backward_kernel tests it; every thread of the block gets the answer.
+__device__ __forceinline__ bool code_row_used(const float* __restrict__ gr, int tid) {
+  using namespace mlp;
+  const bool nz = tid < 256 && (gr[kCbXyz2 + tid] != 0.0f || gr[kCbFeat + tid] != 0.0f ||
+                                (tid < 8 && gr[kCbSigma + tid] != 0.0f));
+  return __syncthreads_or(nz);
+}
+
+__global__ __launch_bounds__(256) void code_layers_dz_kernel(mlp::Params P, const float* __restrict__ z_s,
+                                                             const float* __restrict__ z_t,
+                                                             const float* __restrict__ g, float* __restrict__ ws) {
+  using namespace mlp;
+  __shared__ float zs[256], zt[256], gx2[256], go[257], grgb[3], sv[3][16];
+  __shared__ float red[3][4][16];
+  const int c = blockIdx.x, y = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const float* gr = g + (int64_t)c * kCbStride;
+  if (!code_row_used(gr, tid)) return;  // code_outer_kernel writes its zero dz
+  zs[tid] = z_s[(int64_t)c * 256 + tid];
+  zt[tid] = z_t[(int64_t)c * 256 + tid];
+  gx2[tid] = gr[kCbXyz2 + tid];
+  go[1 + tid] = gr[kCbFeat + tid];
+  if (tid == 0) go[0] = gr[kCbSigma];
+  if (tid < 3) grgb[tid] = gr[kCbRgb + tid];
+  __syncthreads();
+  float* wc = ws + (int64_t)c * 6 * 256;
+  {
+    // outputs o = 16 y + 4 w + x: lanes over k (k = lane + 64 u), butterfly sum
+    float a1[4], a2[4], a3[4];
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      const int o = 16 * y + 4 * w + x;
+      a1[x] = a2[x] = a3[x] = 0.f;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = lane + 64 * u;
+        a1[x] = fmaf(P.p[kWSc1][o * 256 + k], zs[k], a1[x]);
+        a2[x] = fmaf(P.p[kWSc2][o * 256 + k], zs[k], a2[x]);
+        a3[x] = fmaf(P.p[kWTc1][o * 256 + k], zt[k], a3[x]);
+      }
+    }
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        a1[x] += __shfl_xor(a1[x], off);
+        a2[x] += __shfl_xor(a2[x], off);
+        a3[x] += __shfl_xor(a3[x], off);
+      }
+      if (lane == 0) {
+        const int i = 4 * w + x, o = 16 * y + i;
+        sv[0][i] = fmaxf(a1[x] + P.p[kBSc1][o], 0.f);
+        sv[1][i] = fmaxf(a2[x] + P.p[kBSc2][o], 0.f);
+        sv[2][i] = fmaxf(a3[x] + P.p[kBTc1][o], 0.f);
+      }
+    }
+  }
+  // ds1 / ds2 / dt1 for j = 16 y + jj: thread (quarter q, vector v, jj), the quarter's 64 n in order
+  {
+    const int q = tid >> 6, v = (tid >> 4) & 3, jj = tid & 15, j = 16 * y + jj;
+    float a = 0.f;
+    if (v == 0) {
+#pragma unroll 16
+      for (int n = 64 * q; n < 64 * q + 64; ++n) a = fmaf(P.p[kWXyz2][n * 512 + 256 + j], gx2[n], a);
+    } else if (v == 1) {
+#pragma unroll 16
+      for (int n = 64 * q; n < 64 * q + 64; ++n) a = fmaf(P.p[kWOut][n * 512 + 256 + j], go[n], a);
+      if (q == 3) a = fmaf(P.p[kWOut][256 * 512 + 256 + j], go[256], a);
+    } else if (v == 2 && q == 0) {
+      for (int n = 0; n < 3; ++n) a = fmaf(P.p[kWRgb][n * 512 + 256 + j], grgb[n], a);
+    }
+    if (v < 3) red[v][q][jj] = a;
+  }
+  __syncthreads();
+  if (tid < 48) {
+    const int v = tid >> 4, jj = tid & 15, j = 16 * y + jj;
+    const float sum = v == 2 ? red[2][0][jj] : (red[v][0][jj] + red[v][1][jj]) + (red[v][2][jj] + red[v][3][jj]);
+    wc[v * 256 + j] = sv[v][jj];
+    wc[(3 + v) * 256 + j] = sv[v][jj] > 0.f ? sum : 0.f;
+  }
+}
+
+__global__ __launch_bounds__(256) void code_outer_kernel(mlp::Params P, const float* __restrict__ z_s,
+                                                         const float* __restrict__ z_t, const float* __restrict__ g,
+                                                         const float* __restrict__ ws, float* __restrict__ dz_s,
+                                                         float* __restrict__ dz_t, mlp::Params G) {
+  using namespace mlp;
+  __shared__ float s1[256], s2[256], t1[256], ds1[256], ds2[256], dt1[256], go[257], gx2[256], grgb[3];
+  __shared__ float red[2][4][16];
+  const int c = blockIdx.x, y = blockIdx.y, tid = threadIdx.x;
+  const float* gr = g + (int64_t)c * kCbStride;
+  if (!code_row_used(gr, tid)) {
+    if (tid < 16 && dz_s) dz_s[(int64_t)c * 256 + 16 * y + tid] = 0.0f;
+    if (tid < 16 && dz_t) dz_t[(int64_t)c * 256 + 16 * y + tid] = 0.0f;
+    return;
+  }
+  const float* wc = ws + (int64_t)c * 6 * 256;
+  s1[tid] = wc[tid];
+  s2[tid] = wc[256 + tid];
+  t1[tid] = wc[512 + tid];
+  ds1[tid] = wc[768 + tid];
+  ds2[tid] = wc[1024 + tid];
+  dt1[tid] = wc[1280 + tid];
+  gx2[tid] = gr[kCbXyz2 + tid];
+  go[1 + tid] = gr[kCbFeat + tid];
+  if (tid == 0) go[0] = gr[kCbSigma];
+  if (tid < 3) grgb[tid] = gr[kCbRgb + tid];
+  __syncthreads();
+  if (dz_s || dz_t) {
+    // columns j = 16 y + jj: thread (quarter q, vector v, jj), code_backward_kernel's chains
+    const int q = tid >> 6, v = (tid >> 4) & 3, jj = tid & 15, j = 16 * y + jj;
+    float a = 0.f;
+    if (v == 0) {
+#pragma unroll 16
+      for (int n = 64 * q; n < 64 * q + 64; ++n) {
+        a = fmaf(P.p[kWSc1][n * 256 + j], ds1[n], a);
+        a = fmaf(P.p[kWSc2][n * 256 + j], ds2[n], a);
+      }
+    } else if (v == 1) {
+#pragma unroll 16
+      for (int n = 64 * q; n < 64 * q + 64; ++n) a = fmaf(P.p[kWTc1][n * 256 + j], dt1[n], a);
+    }
+    if (v < 2) red[v][q][jj] = a;
+    __syncthreads();
+    if (tid < 32) {
+      const int vv = tid >> 4, k = tid & 15;
+      const float sum = (red[vv][0][k] + red[vv][1][k]) + (red[vv][2][k] + red[vv][3][k]);
+      float* dz = vv == 0 ? dz_s : dz_t;
+      if (dz) dz[(int64_t)c * 256 + 16 * y + k] = sum;
+    }
+  }
+  if (!G.p[kWSc1]) return;
+  // rows r = 16 y .. 16 y + 15 of the outer products, column j = tid; the bias / single-row terms
+  // of columns 16 y ..
+  const int j = tid;
+  const float zsj = z_s[(int64_t)c * 256 + j], ztj = z_t[(int64_t)c * 256 + j];
+  const float s1j = s1[j], s2j = s2[j];
+  for (int r = 16 * y; r < 16 * y + 16; ++r) {
+    atomicAdd(&const_cast<float*>(G.p[kWSc1])[r * 256 + j], ds1[r] * zsj);
+    atomicAdd(&const_cast<float*>(G.p[kWSc2])[r * 256 + j], ds2[r] * zsj);
+    atomicAdd(&const_cast<float*>(G.p[kWTc1])[r * 256 + j], dt1[r] * ztj);
+    atomicAdd(&const_cast<float*>(G.p[kWXyz2])[r * 512 + 256 + j], gx2[r] * s1j);
+    atomicAdd(&const_cast<float*>(G.p[kWOut])[(1 + r) * 512 + 256 + j], go[1 + r] * s2j);
+  }
+  if (tid < 16) {
+    const int jb = 16 * y + tid;
+    atomicAdd(&const_cast<float*>(G.p[kBSc1])[jb], ds1[jb]);
+    atomicAdd(&const_cast<float*>(G.p[kBSc2])[jb], ds2[jb]);
+    atomicAdd(&const_cast<float*>(G.p[kBTc1])[jb], dt1[jb]);
+    atomicAdd(&const_cast<float*>(G.p[kWOut])[256 + jb], go[0] * s2[jb]);  // fc_out row 0 (sigma)
+    for (int r = 0; r < 3; ++r) atomicAdd(&const_cast<float*>(G.p[kWRgb])[r * 512 + 256 + jb], grgb[r] * t1[jb]);
+  }
+}
+
 // The bias gradients that are column sums of g_code (the per-code sums of the code-bias terms):
 // layer_xyz2 (cols 0..255), fc_out rows 1..256 (256..511) and row 0 (512), fc_rgb (513..515).
 __global__ void gcode_bias_kernel(const float* __restrict__ g_code, int64_t n_codes, float* __restrict__ b_xyz2,
@@ -1910,6 +2073,29 @@ extern "C" int cn_code_bias_backward(const float* const* params, const float* z_
   }
   hipLaunchKernelGGL(grad::code_backward_kernel, dim3(static_cast<unsigned>(n_codes), grads ? grad::kCodeRowSplits : 1),
                      dim3(grad::kCodeThreads), 0, as_stream(stream), P, z_s, z_t, g_code, dz_s, dz_t, G);
+  return launch_status();
+}
+
+extern "C" int64_t cn_code_bias_backward_workspace_floats(int64_t n_codes) {
+  return n_codes > 0 ? n_codes * 6 * 256 : -1;
+}
+
+extern "C" int cn_code_bias_backward_ws(const float* const* params, const float* z_s, const float* z_t,
+                                        int64_t n_codes, const float* g_code, float* dz_s, float* dz_t,
+                                        float* const* grads, float* workspace, cn_stream_t stream) {
+  using namespace mlp;
+  CN_CHECK_ARG(params && z_s && z_t && g_code && workspace && n_codes > 0 && n_codes < (1ll << 31));
+  Params P, G = {};
+  for (int i = 0; i < CN_NUM_PARAMS; ++i) {
+    CN_CHECK_ARG(params[i]);
+    P.p[i] = params[i];
+    G.p[i] = grads ? grads[i] : nullptr;
+  }
+  hipStream_t st = as_stream(stream);
+  const dim3 grid(static_cast<unsigned>(n_codes), grad::kCodeSlices);
+  hipLaunchKernelGGL(grad::code_layers_dz_kernel, grid, dim3(256), 0, st, P, z_s, z_t, g_code, workspace);
+  CN_TRY(launch_status());
+  hipLaunchKernelGGL(grad::code_outer_kernel, grid, dim3(256), 0, st, P, z_s, z_t, g_code, workspace, dz_s, dz_t, G);
   return launch_status();
 }
 

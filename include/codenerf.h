@@ -367,6 +367,14 @@ int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, const float* c
 int cn_code_bias_backward(const float* const* params, const float* z_s, const float* z_t, int64_t n_codes,
                           const float* g_code, float* dz_s, float* dz_t, float* const* grads,
                           cn_stream_t stream);
+/* The same backward in two launches with a caller-provided workspace
+ * (cn_code_bias_backward_workspace_floats(n_codes) floats): each code's layers and
+ * reductions are formed once, split over 16 workgroups, instead of once per workgroup.
+ * Bitwise the same results as cn_code_bias_backward. */
+int64_t cn_code_bias_backward_workspace_floats(int64_t n_codes);
+int cn_code_bias_backward_ws(const float* const* params, const float* z_s, const float* z_t, int64_t n_codes,
+                             const float* g_code, float* dz_s, float* dz_t, float* const* grads, float* workspace,
+                             cn_stream_t stream);
 
 /* Backward of volume_render (volumetric_render.py:36-66) w.r.t. raw and rd
  * (z is detached in the reference).  Any of g_rgb (R,3), g_disp, g_acc, g_depth

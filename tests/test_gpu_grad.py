@@ -662,3 +662,31 @@ def test_field_backward_train_sigma_rgb_rows(dev, precision):
     h2, v2 = saved[1].double().cpu(), saved[4].double().cpu()
     close(pg[4][0, :256], d[:, 3] @ h2, 1e-5, "fc_out sigma row")      # kWOut = 4
     close(pg[16][:, :256], d[:, :3].t() @ v2, 1e-5, "fc_rgb rows")     # kWRgb = 16
+
+
+@pytest.mark.parametrize("n_codes,want_grads", [(1, True), (5, True), (5, False)])
+def test_code_bias_backward_two_launch_bitwise(dev, n_codes, want_grads):
+    """cn_code_bias_backward_ws (code layers split over 16 workgroups per code, two launches) gives
+    bitwise the results of the single-launch cn_code_bias_backward: dz_s, dz_t and every accumulated
+    parameter gradient; a code no sample used (g row zero) gets dz = 0 and contributes nothing."""
+    from codenerf import ops, synthetic
+    m = model(dev, 0)
+    params = [p.detach() for p in m.param_list()]
+    g = torch.Generator().manual_seed(n_codes)
+    zs, zt = synthetic.latent_codes(5, n_codes).to(dev), synthetic.latent_codes(6, n_codes).to(dev)
+    stride = ops.code_bias(params, zs, zt).shape[1]
+    gc = (torch.randn(n_codes, stride, generator=g) * 1e-2).to(dev)
+    if n_codes > 1:
+        gc[1] = 0.0                                   # an unused code row
+    out = {}
+    for single in (True, False):
+        pg = [torch.full_like(p, 0.5) for p in params] if want_grads else None
+        dz_s, dz_t = ops.code_bias_backward(params, zs, zt, gc, pg, want_z=True, single_launch=single)
+        out[single] = (dz_s, dz_t, pg)
+    a, b = out[True], out[False]
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    if n_codes > 1:
+        assert not b[0][1].any() and not b[1][1].any()
+    if want_grads:
+        for k, (x, y) in enumerate(zip(a[2], b[2])):
+            assert torch.equal(x, y), f"param {k}"
