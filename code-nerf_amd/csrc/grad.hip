@@ -2129,10 +2129,18 @@ extern "C" int cn_ray_points_backward(const float* g_pts, const float* z, int64_
 // Every dW GEMM of one backward keeps its partial tiles until the single deferred reduction:
 // the sum of their slices (+ five column-sum partial blocks -- three biases, g_code's feat and xyz2
 // rows -- the small d raw column sums and the 64-float alignment of each take).
+// The DIRS fold's own slices (dir1_dw_folded, n_samples >= 32): gsum slots for <= 256 workgroups +
+// m / 512 direction groups, and the encoding / bias partials of those groups.
+static int64_t dirs_ws_floats(int64_t m) {
+  const int64_t groups = ceil_div(m, 512);
+  return (256 + groups) * 4096 + ceil_div(groups, grad::kDirGroups) * 256 * 28 + 4 * 64;
+}
+
 static int64_t train_dw_ws_floats(int64_t m) {
   return 4 * tn_ws_floats(m, 256, 256) + tn_ws_floats(m, 3, 256) + tn_ws_floats(m, 1, 256) +
          std::max(tn_ws_floats(m, 256, 27), enc_parts(m) * 256 * 27) +
-         std::max(tn_ws_floats(m, 256, 63), enc_parts(m) * 256 * 63) + 5 * 1024 * 256 + 4 * 256 * 4 + 24 * 64;
+         std::max(tn_ws_floats(m, 256, 63), enc_parts(m) * 256 * 63) + 5 * 1024 * 256 + 4 * 256 * 4 + 24 * 64 +
+         dirs_ws_floats(m);
 }
 
 // layer_dir1's dW (C: [feat | 27 view-encoding columns], ldc 283) and bias in one pass over its dPre
@@ -2145,7 +2153,7 @@ static int dir1_dw_folded(const float* dpre, const float* feat, float* C, float*
   const int64_t M = a.m;
   const TnPlan pl = tn_plan(dpre, 256, feat, 256, M, 256, 256, false);
   const int64_t rc = std::min(a.chunk_rows, a.n_rays);
-  if (pl.kind != kTn256 || a.n_rays % 16 || rc % 16 || M * 1024 + 64 * 1024 >= (int64_t(1) << 32))
+  if (pl.kind != kTn256 || a.n_rays % 16 || rc % 16 || a.n_samples < 32 || M * 1024 + 64 * 1024 >= (int64_t(1) << 32))
     return CN_EUNSUPPORTED;
   const int64_t total = M / 16, per = ceil_div(total, 256), nb = ceil_div(total, per), groups = a.n_rays / 16;
   const int64_t nd = ceil_div(groups, grad::kDirGroups);
@@ -2287,7 +2295,8 @@ extern "C" int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, con
   // layer_dir2
   CN_TRY(gemm_tn(P[0], 256, v1, 256, G(kWDir2), 256, M, 256, 256, st, x3, ws, B(kBDir2), bws, &red));
   // layer_dir1: [feat | dir enc]
-  const int64_t dir1_budget = tn_ws_floats(M, 256, 256) + std::max(tn_ws_floats(M, 256, 27), enc_parts(M) * 256 * 27);
+  const int64_t dir1_budget =
+      tn_ws_floats(M, 256, 256) + std::max(tn_ws_floats(M, 256, 27), enc_parts(M) * 256 * 27) + dirs_ws_floats(M);
   const int folded = x3 || x_enc ? CN_EUNSUPPORTED
                                  : dir1_dw_folded(P[1], feat, G(kWDir1), B(kBDir1), a, st, &red, dir1_budget);
   if (folded != CN_OK) {

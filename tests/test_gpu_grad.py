@@ -590,7 +590,8 @@ def test_field_backward_train_generated_encodings(dev, mode, precision):
 
 @pytest.mark.parametrize("mode,r,s,chunk", [("rayz", 1056, 64, 256),   # 5 Q1 chunks, the last 32 rays
                                              ("rayz", 1056, 80, 4096),  # unit runs straddle direction groups
-                                             ("pts", 4096, 24, 1024),
+                                             ("pts", 4096, 32, 1024),
+                                             ("rayz", 4096, 24, 1024),  # S < 32: unfolded path
                                              ("rayz", 1050, 64, 256)])  # n_rays % 16 != 0: unfolded path
 def test_field_backward_train_dir1_fold(dev, mode, r, s, chunk):
     """At M >= 65536 (fp32) layer_dir1's view-encoding dW and bias come from per-direction column
