@@ -406,8 +406,15 @@ __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restr
   const int i = lane & 31, h = lane >> 5;
   const int n0 = (wave >> 1) * 64, k0 = (wave & 1) * 128;
   // DIRS: the whole plane as one resource (host: M * 1 KiB + 1 KiB < 4 GiB), units u0 .. u1 - 1
-  const int64_t mb = DIRS ? 0 : (int64_t)blockIdx.x * rows_per_block;
-  const int64_t rows = DIRS ? M : min(rows_per_block, M - mb);
+#ifdef CN_ABLATE_TN_INTERLEAVE
+  // experiment (plain form): workgroup b takes stages b, b + nb, ... of the whole plane, so the
+  // concurrent reads of all workgroups are one contiguous region
+  constexpr bool kIlv = !DIRS && !SIG;
+#else
+  constexpr bool kIlv = false;
+#endif
+  const int64_t mb = (DIRS || kIlv) ? 0 : (int64_t)blockIdx.x * rows_per_block;
+  const int64_t rows = (DIRS || kIlv) ? M : min(rows_per_block, M - mb);
   const unsigned u0 = DIRS ? blockIdx.x * dir.units_per_block : 0u;
   const unsigned u1 = DIRS ? min(u0 + dir.units_per_block, dir.total_units) : 0u;
   const unsigned bytes = static_cast<unsigned>(rows * 256 * 4);
@@ -417,7 +424,9 @@ __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restr
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(B + mb * 256), 0, bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(SIG ? draw + mb * 4 : A), 0, static_cast<unsigned>(SIG ? rows * 16 : 0), 0x00020000);
-  const int n_stages = DIRS ? static_cast<int>(u1 - u0) : static_cast<int>((rows + kTwRows - 1) / kTwRows);
+  const int n_stages = DIRS ? static_cast<int>(u1 - u0)
+                      : kIlv ? static_cast<int>((rows_per_block + kTwRows - 1) / kTwRows)
+                             : static_cast<int>((rows + kTwRows - 1) / kTwRows);
   // stage st: wave w moves rows w + 8 j of A and of B (j < kTwRows / 8), one 16-B-per-lane
   // wave-instruction per 1 KiB row: kTwRows / 4 wave-instructions per stage; SIG: every wave also
   // moves the stage's 16 d raw rows (256 B, the same bytes: the per-wave vmcnt stays uniform)
@@ -435,9 +444,15 @@ __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restr
     // DIRS: the unit's first row; units past the run's end (prefetch) read as zeros
 #ifdef CN_ABLATE_TN_L2DMA
     unsigned row0 = static_cast<unsigned>((st & 3) * kTwRows);  // experiment: 4 stages of rows, L2-resident
+#elif defined(CN_ABLATE_TN_STAGGER)
+    // experiment: workgroup b walks its slab from stage b mod n_stages (wrapping), so the 256
+    // slabs' concurrent reads sit at different offsets instead of one 1.5-MiB-strided comb
+    const int stw = st < n_stages ? (st + static_cast<int>(blockIdx.x) % n_stages) % n_stages : st;
+    unsigned row0 = static_cast<unsigned>(stw * kTwRows);
 #else
     unsigned row0 = static_cast<unsigned>(st * kTwRows);
 #endif
+    if constexpr (kIlv) row0 = static_cast<unsigned>((st * gridDim.x + blockIdx.x) * kTwRows);
     if constexpr (DIRS) {
       row0 = u0 + static_cast<unsigned>(st) < dir.total_units ? dbase * dir.n_samples + dj * drcnt + (16 * dg - dbase)
                                                                : static_cast<unsigned>(M);
