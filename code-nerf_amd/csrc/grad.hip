@@ -1836,11 +1836,10 @@ int64_t tn_ws_floats(int64_t M, int N, int K) {
 // dW of an encoding layer (ENC 0: layer_xyz1 from dPre(xyz1), ENC 1: layer_dir1's view columns
 // from dPre(dir1)) with the encodings generated in the kernel; ws: the deterministic path
 // (enc_ws_parts(M) * 256 * K floats).
-#ifdef CN_ABLATE_ENC512
-constexpr int64_t kEncBlocks = 512;  // experiment: one round of two workgroups per CU
-#else
-constexpr int64_t kEncBlocks = 1024;
-#endif
+// about one round of two workgroups per CU: each workgroup's prologue (three geometry stages, two
+// DMA stages) and partial tile are paid half as often as with 1024 (r03k: 144.8 -> 135.3 us per
+// layer_xyz1 launch of 393 Ki rows)
+constexpr int64_t kEncBlocks = 512;
 int64_t enc_rows(int64_t M) {
   return std::max<int64_t>(grad::kEncRows, ceil_div(ceil_div(M, kEncBlocks), grad::kEncRows) * grad::kEncRows);
 }
