@@ -46,4 +46,12 @@ __device__ __forceinline__ float softplus20(float x) {
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 
+// sigmoid on the hardware exp2 / reciprocal (v_exp_f32, v_rcp_f32: 1 ulp each) instead of the
+// libm expf and the IEEE division (~25 instructions).  The argument rounding of -x log2(e) moves
+// e^-x by <= |x| 2^-24 relative, so the result stays within ~2e-7 of the exact sigmoid
+// (saturated where |x| is large); volume_render's colours and their gradients use it.
+__device__ __forceinline__ float sigmoid_hw(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -1.44269504088896341f));
+}
+
 }  // namespace cn

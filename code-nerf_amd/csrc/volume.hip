@@ -118,11 +118,12 @@ __device__ __forceinline__ void load_raw_lds(const float4* sl, int q0, int j0, i
   for (int i = 0; i < K; ++i) rv[i] = (i < run && j0 + i < S_in) ? sl[pad4(q0 + i)] : make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
-template <int K>
+template <int K, bool FULL>
 __global__ __launch_bounds__(256) void volume_render_kernel(
     const float* __restrict__ raw, const float* __restrict__ z, const float* __restrict__ rd,
     int64_t n_rays, int S_in, float* __restrict__ rgb, float* __restrict__ disp,
     float* __restrict__ acc, float* __restrict__ weights, float* __restrict__ depth) {
+  if (FULL) S_in = 16 * K;  // the host dispatches FULL only for S == 16 K: lets every bound fold
   constexpr bool kLds = K <= kLdsMaxK;
   __shared__ float4 slds[kLds ? 4 * 80 * K : 1];  // per wave: 4 rays x <= 16 K quads, padded 5 / 4
   const int sub = threadIdx.x & 15, lane = threadIdx.x & 63;
@@ -138,8 +139,9 @@ __global__ __launch_bounds__(256) void volume_render_kernel(
   // S == 1: the reference's dists = cat(z[1:] - z[:-1], full_like(that[..., :1], 1e10))
   // is EMPTY (both pieces are 0 wide), so no sample contributes (rgb = acc = depth = 0,
   // disp = NaN, weights (R, 0)).  Reproduced by treating the ray as sample-free.
-  const int S = S_in == 1 ? 0 : S_in;
-  const int run = (S_in + 15) >> 4;
+  // FULL (S_in == 16 K: every lane's run is K samples): the run / bounds tests fold away
+  const int S = FULL ? 16 * K : (S_in == 1 ? 0 : S_in);
+  const int run = FULL ? K : (S_in + 15) >> 4;
   const int j0 = sub * run;
   const float* zr = z + r * S_in;
   const float4* rr = reinterpret_cast<const float4*>(raw) + r * S_in;
@@ -181,9 +183,9 @@ __global__ __launch_bounds__(256) void volume_render_kernel(
       const float alpha = __fsub_rn(1.0f, expf(-sd[i]));           // (:58)
       const float w = __fmul_rn(alpha, trans);                     // (:59)
       // widened_sigmoid (:28): sigmoid(x) * 1.002 - 0.001
-      const float c0 = __fsub_rn(__fmul_rn(cn::sigmoidf_(rv[i].x), 1.002f), 0.001f);
-      const float c1 = __fsub_rn(__fmul_rn(cn::sigmoidf_(rv[i].y), 1.002f), 0.001f);
-      const float c2 = __fsub_rn(__fmul_rn(cn::sigmoidf_(rv[i].z), 1.002f), 0.001f);
+      const float c0 = __fsub_rn(__fmul_rn(cn::sigmoid_hw(rv[i].x), 1.002f), 0.001f);
+      const float c1 = __fsub_rn(__fmul_rn(cn::sigmoid_hw(rv[i].y), 1.002f), 0.001f);
+      const float c2 = __fsub_rn(__fmul_rn(cn::sigmoid_hw(rv[i].z), 1.002f), 0.001f);
       cr += w * c0;
       cg += w * c1;
       cb += w * c2;
@@ -226,14 +228,17 @@ __global__ __launch_bounds__(256) void volume_render_kernel(
 }  // namespace
 
 // Samples per lane the kernels are instantiated for: the smallest that holds ceil(S / 16).
+// S = 64 / 128 (every C2-C5 shape) take the FULL instances.
 #define CN_VOLUME_DISPATCH(KERNEL, S, ...)                                                   \
   do {                                                                                      \
     const int run_ = static_cast<int>(((S) + 15) / 16);                                    \
-    if (run_ <= 4) hipLaunchKernelGGL(KERNEL<4>, __VA_ARGS__);                             \
-    else if (run_ <= 8) hipLaunchKernelGGL(KERNEL<8>, __VA_ARGS__);                        \
-    else if (run_ <= 12) hipLaunchKernelGGL(KERNEL<12>, __VA_ARGS__);                      \
-    else if (run_ <= 16) hipLaunchKernelGGL(KERNEL<16>, __VA_ARGS__);                      \
-    else hipLaunchKernelGGL(KERNEL<32>, __VA_ARGS__);                                      \
+    if ((S) == 64) hipLaunchKernelGGL((KERNEL<4, true>), __VA_ARGS__);                     \
+    else if ((S) == 128) hipLaunchKernelGGL((KERNEL<8, true>), __VA_ARGS__);               \
+    else if (run_ <= 4) hipLaunchKernelGGL((KERNEL<4, false>), __VA_ARGS__);               \
+    else if (run_ <= 8) hipLaunchKernelGGL((KERNEL<8, false>), __VA_ARGS__);               \
+    else if (run_ <= 12) hipLaunchKernelGGL((KERNEL<12, false>), __VA_ARGS__);             \
+    else if (run_ <= 16) hipLaunchKernelGGL((KERNEL<16, false>), __VA_ARGS__);             \
+    else hipLaunchKernelGGL((KERNEL<32, false>), __VA_ARGS__);                             \
   } while (0)
 
 extern "C" int cn_volume_render(const float* raw, const float* z, const float* rd, int64_t n_rays,
@@ -258,12 +263,13 @@ extern "C" int cn_volume_render(const float* raw, const float* z, const float* r
 // z is never differentiated (the reference detaches its samples).  Same layout as the forward.
 namespace {
 
-template <int K>
+template <int K, bool FULL>
 __global__ __launch_bounds__(256) void volume_render_backward_kernel(
     const float* __restrict__ raw, const float* __restrict__ z, const float* __restrict__ rd,
     int64_t n_rays, int S_in, const float* __restrict__ g_rgb, const float* __restrict__ g_disp,
     const float* __restrict__ g_acc, const float* __restrict__ g_w, const float* __restrict__ g_depth,
     float* __restrict__ d_raw, float* __restrict__ d_rd) {
+  if (FULL) S_in = 16 * K;  // as in the forward
   constexpr bool kLds = K <= kLdsMaxK;
   __shared__ float4 slds[kLds ? 4 * 80 * K : 1];  // per wave: raw in, then d raw out (forward's layout)
   const int sub = threadIdx.x & 15, lane = threadIdx.x & 63;
@@ -278,8 +284,8 @@ __global__ __launch_bounds__(256) void volume_render_backward_kernel(
   const bool live = r_ < n_rays;
   if (!kLds && !live) return;
   const int64_t r = live ? r_ : n_rays - 1;
-  const int S = S_in == 1 ? 0 : S_in;  // see the forward: S == 1 has no contributing sample
-  const int run = (S_in + 15) >> 4;
+  const int S = FULL ? 16 * K : (S_in == 1 ? 0 : S_in);  // see the forward: S == 1 has no contributing sample
+  const int run = FULL ? K : (S_in + 15) >> 4;
   const int j0 = sub * run;
   const float* zr = z + r * S_in;
   const float4* rr = reinterpret_cast<const float4*>(raw) + r * S_in;
@@ -349,7 +355,7 @@ __global__ __launch_bounds__(256) void volume_render_backward_kernel(
     const int j = j0 + i;
     G[i] = 0.0f;
     if (i < run && j < S) {
-      const float s0 = cn::sigmoidf_(rv[i].x), s1 = cn::sigmoidf_(rv[i].y), s2 = cn::sigmoidf_(rv[i].z);
+      const float s0 = cn::sigmoid_hw(rv[i].x), s1 = cn::sigmoid_hw(rv[i].y), s2 = cn::sigmoid_hw(rv[i].z);
       const float c0 = s0 * 1.002f - 0.001f, c1 = s1 * 1.002f - 0.001f, c2 = s2 * 1.002f - 0.001f;
       G[i] = gr0 * c0 + gr1 * c1 + gr2 * c2 + gdep * zz[i] + gacc + (g_w ? g_w[r * S_in + j] : 0.f);
       rv[i].x = w[i] * gr0 * 1.002f * s0 * (1.0f - s0);  // reuse rv for d_raw[0:3]
@@ -367,7 +373,7 @@ __global__ __launch_bounds__(256) void volume_render_backward_kernel(
       const float dsd = G[i] * tr[i] * expf(-sd[i]) - suffix;
       suffix += G[i] * w[i];
       const float x = rv[i].w - 1.0f;
-      const float dsp = x > 20.0f ? 1.0f : cn::sigmoidf_(x);
+      const float dsp = x > 20.0f ? 1.0f : cn::sigmoid_hw(x);
       float4 o = rv[i];
       o.w = dsd * (dist[i] * nrm) * dsp;
       if (kLds) {
