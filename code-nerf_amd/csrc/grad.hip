@@ -393,6 +393,12 @@ struct DirFold {
   float* gsum;                             // (workgroups + n_rays / 16) slots of 16 x 256
 };
 
+#ifdef CN_ABLATE_TN_WAITPROF
+// experiment: per (workgroup, wave): shader clocks at the stage barrier, in the DMA issue, in the
+// whole loop, and the stage count (read by cn_debug_tnprof)
+__device__ long long g_tnprof[1024][8][4];
+#endif
+
 template <bool X3, bool SIG, bool DIRS = false>
 __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restrict__ A, const float* __restrict__ B,
                                                             float* __restrict__ C, int64_t ldc, float* __restrict__ part,
@@ -485,6 +491,10 @@ __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restr
 #pragma unroll
     for (int u = 0; u < 4; ++u) acc[t][u] = floatx16{0};
   float bsum[2] = {0.0f, 0.0f};
+#ifdef CN_ABLATE_TN_WAITPROF
+  long long prof_bar = 0, prof_dma = 0;
+  const long long prof_t0 = clock64();
+#endif
   // DIRS: per-direction column sums of the current unit run, rows 2 p + h of columns n0 + 32 t + i
   // (both waves of a pair sum both column blocks -- a select by wave would become an indexed
   // private array, which the compiler moves to LDS -- and wave 2 q + t stores block t); flushed:
@@ -500,15 +510,26 @@ __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restr
     // every wave is done with stage st-1, whose slot then receives stage st+3; after a DIRS flush
     // its 8 stores are the youngest 8 vector-memory ops as well
     static_assert(kTwRows / 2 == 8, "the vmcnt below counts stages st+1, st+2");
+#ifdef CN_ABLATE_TN_WAITPROF
+    const long long tp0 = clock64();
+#endif
     if constexpr (SIG) asm volatile("s_waitcnt vmcnt(10)\n\ts_barrier" ::: "memory");
     else if (DIRS && flushed) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
+#ifdef CN_ABLATE_TN_WAITPROF
+    const long long tp1 = clock64();
+    prof_bar += tp1 - tp0;
+#endif
 #ifdef CN_ABLATE_TN_NODMA
     if (st == 0) dma(st + 3);  // experiment: the ring is never refilled (the vmcnt stays counted)
     else asm volatile("" ::: "memory");
 #else
     dma(st + 3);
+#endif
+#ifdef CN_ABLATE_TN_WAITPROF
+    __builtin_amdgcn_sched_barrier(0);
+    prof_dma += clock64() - tp1;
 #endif
     if constexpr (X3) {
       x3_stage<SIG>(ring + (st & (kTwRing - 1)) * kTwStage, i, h, n0, k0, acc, bsum, sacc, sig_wave);
@@ -567,6 +588,14 @@ __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restr
   }
   // the prefetched stages past the slab must land before the workgroup's LDS is released
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef CN_ABLATE_TN_WAITPROF
+  if (lane == 0 && blockIdx.x < 1024) {
+    g_tnprof[blockIdx.x][wave][0] = prof_bar;
+    g_tnprof[blockIdx.x][wave][1] = prof_dma;
+    g_tnprof[blockIdx.x][wave][2] = clock64() - prof_t0;
+    g_tnprof[blockIdx.x][wave][3] = n_stages;
+  }
+#endif
   float* pt = part ? part + (int64_t)blockIdx.x * 65536 : nullptr;
 #ifdef CN_ABLATE_TN_NOFLUSH
   if (blockIdx.x == 0 && acc[0][0][0] == 12345.0f)  // experiment: no partial tile written
@@ -2089,6 +2118,13 @@ extern "C" int cn_code_bias_backward(const float* const* params, const float* z_
                      dim3(grad::kCodeThreads), 0, as_stream(stream), P, z_s, z_t, g_code, dz_s, dz_t, G);
   return launch_status();
 }
+
+#ifdef CN_ABLATE_TN_WAITPROF
+extern "C" int cn_debug_tnprof(long long* out, int n_blocks) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(cn::grad::g_tnprof), sizeof(long long) * 32 * std::min(n_blocks, 1024)) ==
+                 hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" int64_t cn_code_bias_backward_workspace_floats(int64_t n_codes) {
   return n_codes > 0 ? n_codes * 6 * 256 : -1;
