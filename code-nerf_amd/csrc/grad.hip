@@ -399,14 +399,13 @@ struct DirFold {
 __device__ long long g_tnprof[1024][8][4];
 #endif
 
-template <bool X3, bool SIG, bool DIRS = false>
-__global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restrict__ A, const float* __restrict__ B,
-                                                            float* __restrict__ C, int64_t ldc, float* __restrict__ part,
-                                                            float* __restrict__ bias_part, const float* __restrict__ draw,
-                                                            float* __restrict__ sig_part, int64_t M,
-                                                            int64_t rows_per_block, DirFold dir = {}) {
+template <bool X3, bool SIG, bool DIRS>
+__device__ __forceinline__ void tn256_body(float* ring, const float* __restrict__ A, const float* __restrict__ B,
+                                           float* __restrict__ C, int64_t ldc, float* __restrict__ part,
+                                           float* __restrict__ bias_part, const float* __restrict__ draw,
+                                           float* __restrict__ sig_part, int64_t M, int64_t rows_per_block,
+                                           const DirFold& dir, const unsigned blk, const unsigned nblk) {
   static_assert(!(DIRS && (X3 || SIG)), "the direction fold is the fp32 layer_dir1 pass");
-  __shared__ __attribute__((aligned(16))) float ring[kTwRing * kTwStage];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int i = lane & 31, h = lane >> 5;
@@ -419,9 +418,9 @@ __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restr
 #else
   constexpr bool kIlv = false;
 #endif
-  const int64_t mb = (DIRS || kIlv) ? 0 : (int64_t)blockIdx.x * rows_per_block;
+  const int64_t mb = (DIRS || kIlv) ? 0 : (int64_t)blk * rows_per_block;
   const int64_t rows = (DIRS || kIlv) ? M : min(rows_per_block, M - mb);
-  const unsigned u0 = DIRS ? blockIdx.x * dir.units_per_block : 0u;
+  const unsigned u0 = DIRS ? blk * dir.units_per_block : 0u;
   const unsigned u1 = DIRS ? min(u0 + dir.units_per_block, dir.total_units) : 0u;
   const unsigned bytes = static_cast<unsigned>(rows * 256 * 4);
   const __amdgpu_buffer_rsrc_t ra =
@@ -453,12 +452,12 @@ __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restr
 #elif defined(CN_ABLATE_TN_STAGGER)
     // experiment: workgroup b walks its slab from stage b mod n_stages (wrapping), so the 256
     // slabs' concurrent reads sit at different offsets instead of one 1.5-MiB-strided comb
-    const int stw = st < n_stages ? (st + static_cast<int>(blockIdx.x) % n_stages) % n_stages : st;
+    const int stw = st < n_stages ? (st + static_cast<int>(blk) % n_stages) % n_stages : st;
     unsigned row0 = static_cast<unsigned>(stw * kTwRows);
 #else
     unsigned row0 = static_cast<unsigned>(st * kTwRows);
 #endif
-    if constexpr (kIlv) row0 = static_cast<unsigned>((st * gridDim.x + blockIdx.x) * kTwRows);
+    if constexpr (kIlv) row0 = static_cast<unsigned>((st * nblk + blk) * kTwRows);
     if constexpr (DIRS) {
       row0 = u0 + static_cast<unsigned>(st) < dir.total_units ? dbase * dir.n_samples + dj * drcnt + (16 * dg - dbase)
                                                                : static_cast<unsigned>(M);
@@ -576,7 +575,7 @@ __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restr
       const unsigned u = u0 + static_cast<unsigned>(st);
       flushed = st + 1 == n_stages || (u + 1) % dir.n_samples == 0;
       if (flushed) {
-        float* gs = dir.gsum + (int64_t)(blockIdx.x + u / dir.n_samples) * 4096 + h * 256 + n0 + 32 * tw + i;
+        float* gs = dir.gsum + (int64_t)(blk + u / dir.n_samples) * 4096 + h * 256 + n0 + 32 * tw + i;
 #pragma unroll
         for (int p = 0; p < 8; ++p) {
           gs[p * 512] = tw ? dsum[p][1] : dsum[p][0];
@@ -589,16 +588,16 @@ __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restr
   // the prefetched stages past the slab must land before the workgroup's LDS is released
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #ifdef CN_ABLATE_TN_WAITPROF
-  if (lane == 0 && blockIdx.x < 1024) {
-    g_tnprof[blockIdx.x][wave][0] = prof_bar;
-    g_tnprof[blockIdx.x][wave][1] = prof_dma;
-    g_tnprof[blockIdx.x][wave][2] = clock64() - prof_t0;
-    g_tnprof[blockIdx.x][wave][3] = n_stages;
+  if (lane == 0 && blk < 1024) {
+    g_tnprof[blk][wave][0] = prof_bar;
+    g_tnprof[blk][wave][1] = prof_dma;
+    g_tnprof[blk][wave][2] = clock64() - prof_t0;
+    g_tnprof[blk][wave][3] = n_stages;
   }
 #endif
-  float* pt = part ? part + (int64_t)blockIdx.x * 65536 : nullptr;
+  float* pt = part ? part + (int64_t)blk * 65536 : nullptr;
 #ifdef CN_ABLATE_TN_NOFLUSH
-  if (blockIdx.x == 0 && acc[0][0][0] == 12345.0f)  // experiment: no partial tile written
+  if (blk == 0 && acc[0][0][0] == 12345.0f)  // experiment: no partial tile written
 #endif
 #pragma unroll
   for (int t = 0; t < 2; ++t)
@@ -610,15 +609,68 @@ __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restr
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const float b = bsum[t] + __shfl_xor(bsum[t], 32);
-      if (h == 0) bias_part[(int64_t)blockIdx.x * 256 + n0 + 32 * t + i] = b;
+      if (h == 0) bias_part[(int64_t)blk * 256 + n0 + 32 * t + i] = b;
     }
   }
   if (SIG && sig_wave) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const float v = sacc[u] + __shfl_xor(sacc[u], 32);
-      if (h == 0) sig_part[(int64_t)blockIdx.x * 256 + k0 + 32 * u + i] = v;
+      if (h == 0) sig_part[(int64_t)blk * 256 + k0 + 32 * u + i] = v;
     }
+  }
+}
+// One dW GEMM per launch (gemm_tn's whole-tile plan).
+template <bool X3, bool SIG, bool DIRS = false>
+__global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restrict__ A, const float* __restrict__ B,
+                                                            float* __restrict__ C, int64_t ldc, float* __restrict__ part,
+                                                            float* __restrict__ bias_part, const float* __restrict__ draw,
+                                                            float* __restrict__ sig_part, int64_t M,
+                                                            int64_t rows_per_block, DirFold dir = {}) {
+  __shared__ __attribute__((aligned(16))) float ring[kTwRing * kTwStage];
+  tn256_body<X3, SIG, DIRS>(ring, A, B, C, ldc, part, bias_part, draw, sig_part, M, rows_per_block, dir, blockIdx.x,
+                            gridDim.x);
+}
+
+// Several whole-tile dW GEMMs in ONE launch (a training backward's four 256 x 256 layers): job k
+// owns workgroups first_block .. first_block + n_blocks - 1 and splits its M rows over them.  Fewer
+// workgroups per GEMM means fewer partial tiles (each 256 KiB, written at the end and read back by
+// the deterministic reduction) and one launch's prologue and tail instead of four; the jobs' block
+// counts are weighted by their per-row cost so they end together.
+struct TnJob {
+  const float* A;
+  const float* B;
+  float* part;       // n_blocks partial 256 x 256 tiles
+  float* bias_part;  // optional: n_blocks x 256 column sums of A
+  const float* draw; // SIG: the (M, 4) d raw rows
+  float* sig_part;   // SIG: n_blocks x 256
+  int64_t M, rows_per_block;
+  int kind;          // 0 plain, 1 SIG (fc_out's sigma row), 2 DIRS (layer_dir1's view-encoding fold)
+  int first_block, n_blocks;
+  DirFold dir;
+};
+constexpr int kMaxTnJobs = 4;
+struct TnJobs {
+  TnJob j[kMaxTnJobs];
+  int n;
+};
+
+template <bool X3>
+__global__ __launch_bounds__(512, 2) void gemm_tn256_jobs_kernel(TnJobs jobs) {
+  __shared__ __attribute__((aligned(16))) float ring[kTwRing * kTwStage];
+  int k = jobs.n - 1;
+  while (k > 0 && static_cast<int>(blockIdx.x) < jobs.j[k].first_block) --k;
+  const TnJob& j = jobs.j[k];
+  const unsigned blk = blockIdx.x - static_cast<unsigned>(j.first_block), nblk = static_cast<unsigned>(j.n_blocks);
+  if (j.kind == 1) {
+    tn256_body<X3, true, false>(ring, j.A, j.B, nullptr, 0, j.part, j.bias_part, j.draw, j.sig_part, j.M,
+                                j.rows_per_block, j.dir, blk, nblk);
+  } else if (!X3 && j.kind == 2) {
+    tn256_body<false, false, true>(ring, j.A, j.B, nullptr, 0, j.part, j.bias_part, nullptr, nullptr, j.M,
+                                   j.rows_per_block, j.dir, blk, nblk);
+  } else {
+    tn256_body<X3, false, false>(ring, j.A, j.B, nullptr, 0, j.part, j.bias_part, nullptr, nullptr, j.M,
+                                 j.rows_per_block, j.dir, blk, nblk);
   }
 }
 
@@ -2225,6 +2277,124 @@ static int dir1_dw_folded(const float* dpre, const float* feat, float* C, float*
   return reduce(rd, bp, nd, 1, 256, bias, 256, st);
 }
 
+// The whole-tile dW GEMMs of one training backward, queued and launched as ONE
+// gemm_tn256_jobs_kernel (TnJobs).  add() records a GEMM C += A^T B (+ its bias column sums, the
+// sigma row, the DIRS view-encoding fold); launch() splits the grid over the jobs in proportion to
+// their rows times their per-row cost, takes each job's partial tiles from the reducer and queues
+// the fixed-order sums (same partial order within a job: deterministic).  The costs belong to the
+// layer slot, not to the job's kind, so a job's split -- and its summation order -- does not depend
+// on whether another slot takes the DIRS fold.  CN_TN_JOBS=0 in the environment launches the GEMMs
+// one by one (A/B); CN_TN_COST="c0,c1,c2,c3" overrides the slot costs.
+struct TnBatch {
+  struct Pending {
+    const float* A;
+    const float* B;
+    int64_t M;
+    int kind;
+    float* C;
+    int64_t ldc;
+    float* bias;      // += column sums of A (kinds 0, 1)
+    const float* sig; // kind 1: d sigma (column 3 of the (M, 4) d raw rows)
+    float* sig_out;
+    mlp::FieldArgs a; // kind 2: the geometry (view directions) of the rows
+    float cost;       // per-row cost of the slot (relative)
+  };
+  Pending p[grad::kMaxTnJobs];
+  int n = 0;
+};
+
+static bool tn_jobs_enabled() {
+  static const int on = [] {
+    const char* e = getenv("CN_TN_JOBS");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return on != 0;
+}
+
+// The training backward's slot costs: layer_dir2, layer_dir1 (DIRS where it applies), fc_out
+// (SIG), layer_xyz2 -- r03 per-launch times 375.5, 387.6, 394.7, 375.5 us.
+static const float* tn_slot_cost() {
+  static float w[4] = {1.0f, 1.03f, 1.05f, 1.0f};
+  static const bool init = [] {
+    const char* e = getenv("CN_TN_COST");
+    if (e) sscanf(e, "%f,%f,%f,%f", &w[0], &w[1], &w[2], &w[3]);
+    return true;
+  }();
+  (void)init;
+  return w;
+}
+
+// DIRS fold applicability (dir1_dw_folded's conditions, without the workspace budget).
+static bool dirs_foldable(const mlp::FieldArgs& a) {
+  const int64_t rc = std::min(a.chunk_rows, a.n_rays);
+  return a.n_rays % 16 == 0 && rc % 16 == 0 && a.n_samples >= 32 && a.m * 1024 + 64 * 1024 < (int64_t(1) << 32) &&
+         a.m >= 64 * 1024;
+}
+
+static int tn_batch_launch(TnBatch& b, bool x3, hipStream_t st, Reducer* rd) {
+  if (b.n == 0) return CN_OK;
+  double total = 0.0;
+  for (int k = 0; k < b.n; ++k) total += b.p[k].cost * static_cast<double>(b.p[k].M);
+  constexpr int kGrid = 256;  // one workgroup per CU (the ring fills the LDS)
+  grad::TnJobs jobs = {};
+  jobs.n = b.n;
+  int first = 0;
+  for (int k = 0; k < b.n; ++k) {
+    const TnBatch::Pending& q = b.p[k];
+    int want = static_cast<int>(kGrid * q.cost * static_cast<double>(q.M) / total + 0.5);
+    want = std::max(1, std::min(want, kGrid - first - (b.n - 1 - k)));
+    if (k == b.n - 1) want = std::max(1, kGrid - first);
+    grad::TnJob& j = jobs.j[k];
+    j.A = q.A;
+    j.B = q.B;
+    j.M = q.M;
+    j.kind = q.kind;
+    j.first_block = first;
+    if (q.kind == 2) {
+      const int64_t rc = std::min(q.a.chunk_rows, q.a.n_rays);
+      const int64_t total_u = q.M / 16, per = ceil_div(total_u, want), nb = ceil_div(total_u, per);
+      const int64_t groups = q.a.n_rays / 16;
+      j.n_blocks = static_cast<int>(nb);
+      j.rows_per_block = 0;
+      j.dir = grad::DirFold{static_cast<unsigned>(q.a.n_rays), static_cast<unsigned>(q.a.n_samples),
+                            static_cast<unsigned>(rc), static_cast<unsigned>(per), static_cast<unsigned>(total_u),
+                            rd->take((nb + groups) * 4096)};
+    } else {
+      const int64_t rows = ceil_div(ceil_div(q.M, want), grad::kTwRows) * grad::kTwRows;
+      j.n_blocks = static_cast<int>(ceil_div(q.M, rows));
+      j.rows_per_block = rows;
+    }
+    j.part = rd->take((int64_t)j.n_blocks * 65536);
+    j.bias_part = (q.bias && q.kind != 2) ? rd->take((int64_t)j.n_blocks * 256) : nullptr;  // DIRS: dir_enc_dw's
+    j.draw = q.kind == 1 ? q.sig - 3 : nullptr;
+    j.sig_part = q.kind == 1 ? rd->take((int64_t)j.n_blocks * 256) : nullptr;
+    first += j.n_blocks;
+  }
+  if (x3) hipLaunchKernelGGL(grad::gemm_tn256_jobs_kernel<true>, dim3(static_cast<unsigned>(first)), dim3(512), 0, st, jobs);
+  else hipLaunchKernelGGL(grad::gemm_tn256_jobs_kernel<false>, dim3(static_cast<unsigned>(first)), dim3(512), 0, st, jobs);
+  CN_TRY(launch_status());
+  for (int k = 0; k < b.n; ++k) {
+    const TnBatch::Pending& q = b.p[k];
+    const grad::TnJob& j = jobs.j[k];
+    if (q.kind == 2) {
+      const int64_t groups = q.a.n_rays / 16, nd = ceil_div(groups, grad::kDirGroups);
+      float* ep = rd->take(nd * 256 * 27);
+      float* bp = rd->take(nd * 256);
+      hipLaunchKernelGGL(grad::dir_enc_dw_kernel, dim3(static_cast<unsigned>(nd)), dim3(256), 0, st, q.a, j.dir, ep, bp);
+      CN_TRY(launch_status());
+      CN_TRY(reduce(rd, j.part, j.n_blocks, 256, 256, q.C, q.ldc, st));
+      CN_TRY(reduce(rd, ep, nd, 256, 27, q.C + 256, q.ldc, st));
+      CN_TRY(reduce(rd, bp, nd, 1, 256, q.bias, 256, st));
+      continue;
+    }
+    CN_TRY(reduce(rd, j.part, j.n_blocks, 256, 256, q.C, q.ldc, st));
+    if (q.kind == 1) CN_TRY(reduce(rd, j.sig_part, j.n_blocks, 1, 256, q.sig_out, 256, st));
+    if (q.bias) CN_TRY(reduce(rd, j.bias_part, j.n_blocks, 1, 256, q.bias, 256, st));
+  }
+  b.n = 0;
+  return CN_OK;
+}
+
 // fc_rgb's dW (C += d rgb^T v2, d_raw's columns 0..2) and, in the same pass, the d raw column sums
 // g_rgb[0..2] += sum d rgb, g_sig[0] += sum d sigma (g_code's rgb / sigma entries with one code row).
 static int rgb_dw_draw_sums(const float* d_raw, const float* v2, float* C, int64_t ldc, int64_t M, float* g_rgb,
@@ -2342,24 +2512,42 @@ extern "C" int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, con
   // fc_rgb (h half): dW += d rgb^T v2 (+ g_code's rgb / sigma entries, folded, in the same pass)
   if (fold_code) CN_TRY(rgb_dw_draw_sums(d_raw, v2, G(kWRgb), 512, M, g_code + kCbRgb, g_code + kCbSigma, st, &red));
   else CN_TRY(gemm_tn(d_raw, 4, v2, 256, G(kWRgb), 512, M, 3, 256, st, x3, ws, nullptr, nullptr, &red));
-  // layer_dir2
-  CN_TRY(gemm_tn(P[0], 256, v1, 256, G(kWDir2), 256, M, 256, 256, st, x3, ws, B(kBDir2), bws, &red));
-  // layer_dir1: [feat | dir enc]
-  const int64_t dir1_budget =
-      tn_ws_floats(M, 256, 256) + std::max(tn_ws_floats(M, 256, 27), enc_parts(M) * 256 * 27) + dirs_ws_floats(M);
-  const int folded = x3 || x_enc ? CN_EUNSUPPORTED
-                                 : dir1_dw_folded(P[1], feat, G(kWDir1), B(kBDir1), a, st, &red, dir1_budget);
-  if (folded != CN_OK) {
-    if (folded != CN_EUNSUPPORTED) return folded;
-    CN_TRY(gemm_tn(P[1], 256, feat, 256, G(kWDir1), 283, M, 256, 256, st, x3, ws, B(kBDir1), bws, &red));
-    if (x_enc) CN_TRY(gemm_tn(P[1], 256, x_enc + 63, 90, G(kWDir1) + 256, 283, M, 256, 27, st, x3, ws, nullptr, nullptr, &red));
-    else CN_TRY(gemm_tn_enc(1, P[1], a, G(kWDir1) + 256, 283, st, x3, ws, nullptr, nullptr, &red));
+  if (tn_jobs_enabled() && M >= 64 * 1024) {
+    // the four 256 x 256 layers as ONE whole-tile launch (TnBatch): layer_dir2, layer_dir1 [feat]
+    // (+ its view-encoding columns by the DIRS fold where it applies), fc_out (+ sigma row),
+    // layer_xyz2
+    TnBatch tb;
+    const bool dirs = !x3 && !x_enc && dirs_foldable(a);
+    const float* c = tn_slot_cost();
+    tb.p[tb.n++] = {P[0], v1, M, 0, G(kWDir2), 256, B(kBDir2), nullptr, nullptr, {}, c[0]};
+    tb.p[tb.n++] = {P[1], feat, M, dirs ? 2 : 0, G(kWDir1), 283, B(kBDir1), nullptr, nullptr, a, c[1]};
+    tb.p[tb.n++] = {P[2], h2, M, 1, G(kWOut) + 512, 512, gc_feat, d_raw + 3, G(kWOut), {}, c[2]};
+    tb.p[tb.n++] = {P[3], h1, M, 0, G(kWXyz2), 512, gc_xyz2, nullptr, nullptr, {}, c[3]};
+    CN_TRY(tn_batch_launch(tb, x3, st, &red));
+    if (!dirs) {
+      if (x_enc) CN_TRY(gemm_tn(P[1], 256, x_enc + 63, 90, G(kWDir1) + 256, 283, M, 256, 27, st, x3, ws, nullptr, nullptr, &red));
+      else CN_TRY(gemm_tn_enc(1, P[1], a, G(kWDir1) + 256, 283, st, x3, ws, nullptr, nullptr, &red));
+    }
+  } else {
+    // layer_dir2
+    CN_TRY(gemm_tn(P[0], 256, v1, 256, G(kWDir2), 256, M, 256, 256, st, x3, ws, B(kBDir2), bws, &red));
+    // layer_dir1: [feat | dir enc]
+    const int64_t dir1_budget =
+        tn_ws_floats(M, 256, 256) + std::max(tn_ws_floats(M, 256, 27), enc_parts(M) * 256 * 27) + dirs_ws_floats(M);
+    const int folded = x3 || x_enc ? CN_EUNSUPPORTED
+                                   : dir1_dw_folded(P[1], feat, G(kWDir1), B(kBDir1), a, st, &red, dir1_budget);
+    if (folded != CN_OK) {
+      if (folded != CN_EUNSUPPORTED) return folded;
+      CN_TRY(gemm_tn(P[1], 256, feat, 256, G(kWDir1), 283, M, 256, 256, st, x3, ws, B(kBDir1), bws, &red));
+      if (x_enc) CN_TRY(gemm_tn(P[1], 256, x_enc + 63, 90, G(kWDir1) + 256, 283, M, 256, 27, st, x3, ws, nullptr, nullptr, &red));
+      else CN_TRY(gemm_tn_enc(1, P[1], a, G(kWDir1) + 256, 283, st, x3, ws, nullptr, nullptr, &red));
+    }
+    // fc_out (h half): row 0 from d sigma, rows 1.. from d feat
+    CN_TRY(gemm_tn(P[2], 256, h2, 256, G(kWOut) + 512, 512, M, 256, 256, st, x3, ws, gc_feat, bws, &red, d_raw + 3,
+                   G(kWOut)));
+    // layer_xyz2 (h half)
+    CN_TRY(gemm_tn(P[3], 256, h1, 256, G(kWXyz2), 512, M, 256, 256, st, x3, ws, gc_xyz2, bws, &red));
   }
-  // fc_out (h half): row 0 from d sigma, rows 1.. from d feat
-  CN_TRY(gemm_tn(P[2], 256, h2, 256, G(kWOut) + 512, 512, M, 256, 256, st, x3, ws, gc_feat, bws, &red, d_raw + 3,
-                 G(kWOut)));
-  // layer_xyz2 (h half)
-  CN_TRY(gemm_tn(P[3], 256, h1, 256, G(kWXyz2), 512, M, 256, 256, st, x3, ws, gc_xyz2, bws, &red));
   // layer_xyz1
   if (x_enc) CN_TRY(gemm_tn(P[4], 256, x_enc, 90, G(kWXyz1), 63, M, 256, 63, st, x3, ws, B(kBXyz1), bws, &red));
   else CN_TRY(gemm_tn_enc(0, P[4], a, G(kWXyz1), 63, st, x3, ws, B(kBXyz1), bws, &red));

@@ -694,4 +694,7 @@ def test_code_bias_backward_two_launch_bitwise(dev, n_codes, want_grads):
             if n_codes == 1:
                 assert torch.equal(x, y), f"param {k}"
             else:
-                close(x - 0.5, (y - 0.5).double(), 1e-6, f"param {k}")
+                # each of the n_codes atomic adds onto the 0.5 fill rounds at the fill's ulp (2^-24
+                # near 0.5): two orders differ by up to n_codes ulps, whatever the gradient's scale
+                err = (x.double() - y.double()).abs().max().item()
+                assert err <= n_codes * 2.0 ** -23, f"param {k}: max err {err:.3e}"
