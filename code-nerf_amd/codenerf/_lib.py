@@ -104,6 +104,7 @@ SIGNATURES = {
     "cn_gemm_tn_ws": (_i, [_i, _p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _p, _p]),
     "cn_render_loss_workspace_doubles": (_i64, [_i64]),
     "cn_render_loss": (_i, [_p, _p, _p, _i64, _i64, _p, _p, _i64, _i64, _f, _p, _p, _p]),
+    "cn_render_loss_psnr": (_i, [_p, _p, _p, _i64, _i64, _p, _p, _i64, _i64, _f, _p, _p, _p, _p]),
     "cn_render_loss_backward": (_i, [_p, _p, _p, _i64, _i64, _p, _p, _i64, _i64, _f, _p, _p, _p, _p, _p, _p, _p]),
     "cn_adamw_step": (_i, [_p, _p, _p, _p, _i64, ctypes.POINTER(_i64), ctypes.POINTER(_i64),
                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i64),

@@ -355,9 +355,9 @@ class RenderLoss(torch.autograd.Function):
     [coarse, fine, regulariser, total, ||z_s||, ||z_t||] (not differentiable)."""
 
     @staticmethod
-    def forward(ctx, rgb_c, rgb_f, target, z_s, z_t, expand, lam):
+    def forward(ctx, rgb_c, rgb_f, target, z_s, z_t, expand, lam, psnr=None):
         ctx.set_materialize_grads(False)
-        stats = ops.render_loss(rgb_c, rgb_f, target, z_s, z_t, expand, lam)
+        stats = ops.render_loss(rgb_c, rgb_f, target, z_s, z_t, expand, lam, psnr=psnr)
         ctx.save_for_backward(rgb_c, rgb_f, target, z_s, z_t, stats)
         ctx.expand, ctx.lam = expand, lam
         ctx.mark_non_differentiable(stats)
@@ -366,21 +366,23 @@ class RenderLoss(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_total, _g_stats):
         if g_total is None:
-            return (None,) * 7
+            return (None,) * 8
         rgb_c, rgb_f, target, z_s, z_t, stats = ctx.saved_tensors
         want = ctx.needs_input_grad[:2] + ctx.needs_input_grad[3:5]
         d = ops.render_loss_backward(rgb_c, rgb_f, target, z_s, z_t, ctx.expand, ctx.lam, stats,
                                      g_total.reshape(1).contiguous(), want)
-        return d[0], d[1], None, d[2], d[3], None, None
+        return d[0], d[1], None, d[2], d[3], None, None, None
 
 
-def render_loss_autograd(rgb_c, rgb_f, target, z_s=None, z_t=None, expand: int = 1, lam: float = 0.0):
-    """-> (total loss, stats (6,)).  The regulariser is differentiated only where z_s / z_t require grad."""
+def render_loss_autograd(rgb_c, rgb_f, target, z_s=None, z_t=None, expand: int = 1, lam: float = 0.0,
+                         psnr=None):
+    """-> (total loss, stats (6,)).  The regulariser is differentiated only where z_s / z_t require grad.
+    ``psnr`` (float64 device scalar, optional): mse2psnr of the fine loss, written by the same launch."""
     tgt = target.detach()
     if not _needs_grad(rgb_c, rgb_f, z_s, z_t):
-        stats = ops.render_loss(_d(rgb_c), _d(rgb_f), tgt, _d(z_s), _d(z_t), expand, lam)
+        stats = ops.render_loss(_d(rgb_c), _d(rgb_f), tgt, _d(z_s), _d(z_t), expand, lam, psnr=psnr)
         return stats[3], stats
-    return RenderLoss.apply(rgb_c, rgb_f, tgt, z_s, z_t, expand, lam)
+    return RenderLoss.apply(rgb_c, rgb_f, tgt, z_s, z_t, expand, lam, psnr)
 
 
 # ------------------------------------------------------------------ entry points used by the package

@@ -58,8 +58,9 @@ def eval_step_loss(theta, phi, rho, shape_code, texture_code, target_pixels, sam
                            chunk_rows=n, t_rand=t_rand, u=u)
     rgb_c, rgb_f = out["rgb_coarse"], out["rgb_fine"]
     # mse(coarse) + mse(fine) + lambda (||z_s|| + ||z_t||), the codes expanded over the n rays
-    loss, stats = nerf_loss(rgb_c, rgb_f, tp, shape_code, texture_code, n, regularizer_lambda)
-    logs = {"nerf_loss_coarse": stats[0], "nerf_loss_fine": stats[1], "embedding_loss": stats[2]}
+    psnr = torch.empty((), dtype=torch.float64, device=tp.device)   # eval.py:159's psnr, by the loss launch
+    loss, stats = nerf_loss(rgb_c, rgb_f, tp, shape_code, texture_code, n, regularizer_lambda, psnr=psnr)
+    logs = {"nerf_loss_coarse": stats[0], "nerf_loss_fine": stats[1], "embedding_loss": stats[2], "psnr": psnr}
     if gt_pose is not None:
         logs["pose_error"] = ops.pose_error(gt_pose.reshape(1, 4, 4), cam_pose)[1][0]
     logs["cam_pose"] = cam_pose
@@ -72,7 +73,10 @@ def step_psnr(logs: Dict[str, object]) -> float:
 
 
 def step_psnr_tensor(logs: Dict[str, object]) -> torch.Tensor:
-    """eval.py:159's psnr formed on the device (no read-back; float() it when logged)."""
+    """eval.py:159's psnr on the device (no read-back; float() it when logged): the loss launch's own
+    (eval_step_loss), else formed from the fine MSE."""
+    if "psnr" in logs:
+        return logs["psnr"]
     from .train import psnr_tensor
     return psnr_tensor(logs["nerf_loss_fine"])
 
@@ -169,10 +173,12 @@ class GraphedEvalStep:
         self._next = self.rs.draw_host(1)
 
 
-def nerf_loss(rgb_c, rgb_f, target, shape_code, texture_code, expand: int, regularizer_lambda: float):
-    """eval.py:157-163 -> (loss, stats (6,)) through cn_render_loss (one launch each way)."""
+def nerf_loss(rgb_c, rgb_f, target, shape_code, texture_code, expand: int, regularizer_lambda: float, psnr=None):
+    """eval.py:157-163 -> (loss, stats (6,)) through cn_render_loss (one launch each way); ``psnr``: the
+    fine loss's mse2psnr written by the same launch."""
     from .autograd import render_loss_autograd
-    return render_loss_autograd(rgb_c, rgb_f, target, shape_code, texture_code, expand, regularizer_lambda)
+    return render_loss_autograd(rgb_c, rgb_f, target, shape_code, texture_code, expand, regularizer_lambda,
+                                psnr=psnr)
 
 
 def _optimizer(kind: str, groups, lr: float):

@@ -163,6 +163,20 @@ class ShapeTextureEmbedding(torch.nn.Module):
             return self.shape_embedding(object_ids), self.texture_embedding(object_ids)
         host = getattr(object_ids, "_cn_host_ids", None)
         if host is not None and len(host) == object_ids.shape[0]:
+            uniq_h = np.unique(np.asarray(host, dtype=np.int64))
+            if uniq_h.shape[0] == 1:
+                # one object (every train.py chunk of one image): its table rows as views and the
+                # per-ray codes as their expand -- no id upload, no index search, no gathers; the
+                # field kernels take the one code row (nerf._codes)
+                k = int(uniq_h[0])
+                rows_s = self.shape_embedding.weight.narrow(0, k, 1)
+                rows_t = self.texture_embedding.weight.narrow(0, k, 1)
+                n = object_ids.shape[0]
+                z_s, z_t = rows_s.expand(n, -1), rows_t.expand(n, -1)
+                tag = CodeRows(rows_s, rows_t, None)
+                z_s._cn_code_rows = tag
+                z_t._cn_code_rows = tag
+                return z_s, z_t
             # the caller knows the ids on the host (codenerf.train: the batch's per-image ids): the
             # distinct ids go up as a pinned copy and the per-ray index is a device searchsorted --
             # torch.unique on the device would wait for the GPU (its output size) every chunk

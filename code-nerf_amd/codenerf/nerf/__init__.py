@@ -67,8 +67,11 @@ def _codes(z_s: torch.Tensor, z_t: torch.Tensor):
     the distinct rows when the codes came from ShapeTextureEmbedding (train), one row when
     they are an expand() of one row (eval / render), else one row per ray."""
     tag = getattr(z_s, "_cn_code_rows", None)
-    if tag is not None and getattr(z_t, "_cn_code_rows", None) is tag and tag.index.shape[0] == z_s.shape[0]:
-        return tag.shape_rows, tag.texture_rows, (None if tag.shape_rows.shape[0] == 1 else tag.index)
+    if tag is not None and getattr(z_t, "_cn_code_rows", None) is tag:
+        if tag.index is None and tag.shape_rows.shape[0] == 1:      # one object: every ray's row 0
+            return tag.shape_rows, tag.texture_rows, None
+        if tag.index is not None and tag.index.shape[0] == z_s.shape[0]:
+            return tag.shape_rows, tag.texture_rows, (None if tag.shape_rows.shape[0] == 1 else tag.index)
     if z_s.stride(0) == 0 and z_t.stride(0) == 0:
         # an expand() of one code row: hand the field its base row, so the code gradient (already
         # the sum over the rays, from g_code) lands on it directly instead of through a slice + expand

@@ -792,9 +792,10 @@ def adamw_step_dev(param: Tensor, grad: Tensor, exp_avg: Tensor, exp_avg_sq: Ten
 
 def render_loss(rgb_coarse: Optional[Tensor], rgb_fine: Optional[Tensor], target: Tensor,
                 z_s: Optional[Tensor] = None, z_t: Optional[Tensor] = None, expand: int = 1,
-                regularizer_lambda: float = 0.0) -> Tensor:
+                regularizer_lambda: float = 0.0, psnr: Optional[Tensor] = None) -> Tensor:
     """train.py:103-108 / eval.py:157-163 in one launch -> (6,) [loss_coarse, loss_fine, regulariser,
-    total, ||z_s||, ||z_t||]; ``||z||`` over z's elements times ``expand`` (expanded rows)."""
+    total, ||z_s||, ||z_t||]; ``||z||`` over z's elements times ``expand`` (expanded rows).
+    ``psnr`` (a float64 device scalar): also mse2psnr of the fine loss, written by the same launch."""
     lib = _lib_ready()
     rc, rf = _opt(rgb_coarse, "rgb_coarse"), _opt(rgb_fine, "rgb_fine")
     target = _cuda(target, "target")
@@ -806,6 +807,12 @@ def render_loss(rgb_coarse: Optional[Tensor], rgb_fine: Optional[Tensor], target
     out = torch.empty(6, device=target.device, dtype=torch.float32)
     nws = int(lib.cn_render_loss_workspace_doubles(n_code))
     ws = torch.empty(nws, device=target.device, dtype=torch.float64) if nws > 0 else None
+    if psnr is not None:
+        assert psnr.is_cuda and psnr.dtype == torch.float64 and psnr.numel() == 1, "psnr: a float64 device scalar"
+        check(lib.cn_render_loss_psnr(ptr(rc), ptr(rf), ptr(target), target.shape[1], n, ptr(zs), ptr(zt), n_code,
+                                      expand, regularizer_lambda, ptr(ws), ptr(out), ptr(psnr), stream_of(out)),
+              "cn_render_loss_psnr")
+        return out
     check(lib.cn_render_loss(ptr(rc), ptr(rf), ptr(target), target.shape[1], n, ptr(zs), ptr(zt), n_code, expand,
                              regularizer_lambda, ptr(ws), ptr(out), stream_of(out)), "cn_render_loss")
     return out

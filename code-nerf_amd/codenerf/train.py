@@ -130,8 +130,12 @@ def train_minibatch(models, optimizer, scheduler, point_sampler, embedders, ro, 
     # mse coarse + mse fine + lambda (||shape table|| + ||texture table||) on .data (a constant):
     # one cn_render_loss launch forward, one backward into the two rgb tensors
     shape_params, texture_params = get_params_tensor(models["embedding"], is_distributed)
+    # train.py:105's psnr of this chunk, written on the device by the loss launch itself (mse2psnr's
+    # arithmetic in float64): the reference's .item() read-back every chunk made the host wait for
+    # the GPU and the GPU then wait for the host's next launches; float() it when it is logged
+    psnr = torch.empty((), dtype=torch.float64, device=target_pixels.device)
     loss, stats = render_loss_autograd(rgb_coarse, rgb_fine, target_pixels, shape_params, texture_params, 1,
-                                       regularizer_lambda)
+                                       regularizer_lambda, psnr=psnr)
     loss_coarse, loss_fine, regularization = stats[0], stats[1], stats[2]
     optimizer.zero_grad()
     loss.backward()
@@ -139,10 +143,6 @@ def train_minibatch(models, optimizer, scheduler, point_sampler, embedders, ro, 
         _average_gradients(optimizer, models)     # (DDP-wrapped modules averaged in the backward)
     optimizer.step()
     scheduler.step()
-    # train.py:105's psnr of this chunk, formed on the device (mse2psnr's arithmetic in float64):
-    # the reference's .item() read-back every chunk made the host wait for the GPU and the GPU then
-    # wait for the host's next launches; float() it when it is logged
-    psnr = psnr_tensor(loss_fine)
     return {"nerf_loss_coarse": loss_coarse, "nerf_loss_fine": loss_fine, "embedding_loss": regularization,
             "total_loss": loss.detach(), "psnr": psnr}
 

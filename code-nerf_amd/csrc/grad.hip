@@ -640,20 +640,111 @@ __global__ __launch_bounds__(512, 2) void gemm_tn256_kernel(const float* __restr
 struct TnJob {
   const float* A;
   const float* B;
-  float* part;       // n_blocks partial 256 x 256 tiles
-  float* bias_part;  // optional: n_blocks x 256 column sums of A
-  const float* draw; // SIG: the (M, 4) d raw rows
+  float* part;       // n_blocks partial tiles (256 x 256; RGB: 3 x 256)
+  float* bias_part;  // optional: n_blocks x 256 column sums of A (RGB: the d raw column sums, 4 per block)
+  const float* draw; // SIG, RGB: the (M, 4) d raw rows
   float* sig_part;   // SIG: n_blocks x 256
   int64_t M, rows_per_block;
-  int kind;          // 0 plain, 1 SIG (fc_out's sigma row), 2 DIRS (layer_dir1's view-encoding fold)
+  int kind;          // 0 plain, 1 SIG (fc_out's sigma row), 2 DIRS (layer_dir1's view-encoding fold), 3 RGB
   int first_block, n_blocks;
   DirFold dir;
 };
-constexpr int kMaxTnJobs = 4;
+constexpr int kMaxTnJobs = 5;
 struct TnJobs {
   TnJob j[kMaxTnJobs];
   int n;
 };
+
+// RGB (kind 3): fc_rgb's dW, C += d rgb^T v2 (3 x 256), and the column sums of the d raw rows
+// (g_code's rgb / sigma entries with one code row) -- gemm_tn_skinny_kernel<3, true>'s work as a
+// role of the whole-tile launch.  It is a bandwidth pass (1 KiB of v2 per row, 24 FMAs per row per
+// 256 threads), so it runs on a few workgroups beside the MFMA-bound GEMMs instead of taking the
+// whole chip for its own ~80 us: a deep LDS-DMA ring (kRgbRing stages of 16 v2 rows + their 16 d
+// raw rows, all but one in flight, ~100 KiB per CU) keeps one CU's loads streaming.  Thread t sums
+// column t & 255 over rows 8 (t >> 8) .. + 7 of every stage; the two halves and the per-row d raw
+// sums (threads 0, 256) are added in a fixed order at the end: deterministic.
+constexpr int kRgbRing = 7;
+constexpr int kRgbStage = kTwRows * 256 + kTwRows * 4;
+static_assert(kRgbRing * kRgbStage <= kTwRing * kTwStage, "the RGB ring lives in the whole-tile ring's LDS");
+
+__device__ __forceinline__ void rgb_body(float* ring, const float* __restrict__ draw, const float* __restrict__ v2,
+                                         float* __restrict__ part, float* __restrict__ cpart, int64_t M,
+                                         int64_t rows_per_block, const unsigned blk, const unsigned nblk) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t mb = (int64_t)blk * rows_per_block;
+  const int64_t rows = min(rows_per_block, M - mb);
+  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(v2 + mb * 256), 0,
+                                                                      static_cast<unsigned>(rows * 1024), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(draw + mb * 4), 0,
+                                                                      static_cast<unsigned>(rows * 16), 0x00020000);
+  const int n_stages = static_cast<int>((rows + kTwRows - 1) / kTwRows);
+  // stage st: wave w moves v2 rows w, w + 8 (1 KiB each) and -- every wave, the same 256 bytes, so the
+  // per-wave vmcnt stays uniform -- the stage's 16 d raw rows; rows past the slab read as zeros
+  auto dma = [&](int st) {
+    float* slot = ring + (st % kRgbRing) * kRgbStage;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int r = wave + 8 * j;
+      const unsigned soff = __builtin_amdgcn_readfirstlane(static_cast<unsigned>((st * kTwRows + r) * 1024));
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (lds_ptr_t)(slot + r * 256), 16, lane * 16u, soff, 0, 0);
+    }
+    const unsigned soff = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(st * kTwRows * 16));
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rr, (lds_ptr_t)(slot + kTwRows * 256), 4, lane * 4u, soff, 0, 0);
+  };
+  const int c = tid & 255, hh = tid >> 8;
+  float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
+  float cs[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int st = 0; st < kRgbRing - 1; ++st) dma(st);
+  for (int st = 0; st < n_stages; ++st) {
+    // stage st landed (all but this wave's pieces of stages st+1 .. st+kRgbRing-2: 3 each) and every
+    // wave is past stage st-1, whose slot then receives stage st+kRgbRing-1
+    static_assert(3 * (kRgbRing - 2) == 15, "the vmcnt below");
+    asm volatile("s_waitcnt vmcnt(15)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    dma(st + kRgbRing - 1);
+    const float* slot = ring + (st % kRgbRing) * kRgbStage;
+    const float* sv = slot + 8 * hh * 256 + c;
+    const float4* sd = reinterpret_cast<const float4*>(slot + kTwRows * 256) + 8 * hh;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v = sv[j * 256];
+      const float4 d = sd[j];
+      a0 = fmaf(d.x, v, a0);
+      a1 = fmaf(d.y, v, a1);
+      a2 = fmaf(d.z, v, a2);
+      if (c == 0) {
+        cs[0] += d.x;
+        cs[1] += d.y;
+        cs[2] += d.z;
+        cs[3] += d.w;
+      }
+    }
+  }
+  // the prefetched stages past the slab land, then the halves meet in the (free) ring
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (hh == 1) {
+    ring[c] = a0;
+    ring[256 + c] = a1;
+    ring[512 + c] = a2;
+    if (c == 0)
+      for (int n = 0; n < 4; ++n) ring[768 + n] = cs[n];
+  }
+  __syncthreads();
+  if (hh == 0) {
+    float* pt = part + (int64_t)blk * 3 * 256;
+    pt[c] = a0 + ring[c];
+    pt[256 + c] = a1 + ring[256 + c];
+    pt[512 + c] = a2 + ring[512 + c];
+    if (c == 0) {
+      for (int n = 0; n < 3; ++n) cpart[(int64_t)blk * 3 + n] = cs[n] + ring[768 + n];
+      cpart[3 * (int64_t)nblk + blk] = cs[3] + ring[771];
+    }
+  }
+}
+
 
 template <bool X3>
 __global__ __launch_bounds__(512, 2) void gemm_tn256_jobs_kernel(TnJobs jobs) {
@@ -668,6 +759,8 @@ __global__ __launch_bounds__(512, 2) void gemm_tn256_jobs_kernel(TnJobs jobs) {
   } else if (!X3 && j.kind == 2) {
     tn256_body<false, false, true>(ring, j.A, j.B, nullptr, 0, j.part, j.bias_part, nullptr, nullptr, j.M,
                                    j.rows_per_block, j.dir, blk, nblk);
+  } else if (!X3 && j.kind == 3) {
+    rgb_body(ring, j.draw, j.B, j.part, j.bias_part, j.M, j.rows_per_block, blk, nblk);
   } else {
     tn256_body<X3, false, false>(ring, j.A, j.B, nullptr, 0, j.part, j.bias_part, nullptr, nullptr, j.M,
                                  j.rows_per_block, j.dir, blk, nblk);
@@ -2284,7 +2377,7 @@ static int dir1_dw_folded(const float* dpre, const float* feat, float* C, float*
 // the fixed-order sums (same partial order within a job: deterministic).  The costs belong to the
 // layer slot, not to the job's kind, so a job's split -- and its summation order -- does not depend
 // on whether another slot takes the DIRS fold.  CN_TN_JOBS=0 in the environment launches the GEMMs
-// one by one (A/B); CN_TN_COST="c0,c1,c2,c3" overrides the slot costs.
+// one by one (A/B); CN_TN_COST="c0,c1,c2,c3,c4" overrides the slot costs.
 struct TnBatch {
   struct Pending {
     const float* A;
@@ -2312,12 +2405,16 @@ static bool tn_jobs_enabled() {
 }
 
 // The training backward's slot costs: layer_dir2, layer_dir1 (DIRS where it applies), fc_out
-// (SIG), layer_xyz2 -- r03 per-launch times 375.5, 387.6, 394.7, 375.5 us.
+// (SIG), layer_xyz2 -- r03 per-launch times 375.5, 387.6, 394.7, 375.5 us -- and the RGB pass: an
+// RGB workgroup streams ~40 GB/s of v2 beside the GEMMs (r03l: 6 of them, cost 0.1, held the
+// launch 1.70 ms; 4 (0.07) 2.5 ms; 8-9 (0.14) balanced; r03n: 0.15 / 0.18 / 0.24 gave 41.5 / 41.7 /
+// 41.7 ms per C3 iteration), 1 KiB per row, ~0.12 of a whole-tile row.  Kept a little above that:
+// a late RGB workgroup holds up the whole launch, a spare one costs 1/256 of it.
 static const float* tn_slot_cost() {
-  static float w[4] = {1.0f, 1.03f, 1.05f, 1.0f};
+  static float w[5] = {1.0f, 1.03f, 1.05f, 1.0f, 0.16f};
   static const bool init = [] {
     const char* e = getenv("CN_TN_COST");
-    if (e) sscanf(e, "%f,%f,%f,%f", &w[0], &w[1], &w[2], &w[3]);
+    if (e) sscanf(e, "%f,%f,%f,%f,%f", &w[0], &w[1], &w[2], &w[3], &w[4]);
     return true;
   }();
   (void)init;
@@ -2364,6 +2461,14 @@ static int tn_batch_launch(TnBatch& b, bool x3, hipStream_t st, Reducer* rd) {
       j.n_blocks = static_cast<int>(ceil_div(q.M, rows));
       j.rows_per_block = rows;
     }
+    if (q.kind == 3) {  // RGB: 3 x 256 partials, 4 d raw column sums per block
+      j.part = rd->take((int64_t)j.n_blocks * 3 * 256);
+      j.bias_part = rd->take((int64_t)j.n_blocks * 4);
+      j.draw = q.sig;
+      j.sig_part = nullptr;
+      first += j.n_blocks;
+      continue;
+    }
     j.part = rd->take((int64_t)j.n_blocks * 65536);
     j.bias_part = (q.bias && q.kind != 2) ? rd->take((int64_t)j.n_blocks * 256) : nullptr;  // DIRS: dir_enc_dw's
     j.draw = q.kind == 1 ? q.sig - 3 : nullptr;
@@ -2385,6 +2490,12 @@ static int tn_batch_launch(TnBatch& b, bool x3, hipStream_t st, Reducer* rd) {
       CN_TRY(reduce(rd, j.part, j.n_blocks, 256, 256, q.C, q.ldc, st));
       CN_TRY(reduce(rd, ep, nd, 256, 27, q.C + 256, q.ldc, st));
       CN_TRY(reduce(rd, bp, nd, 1, 256, q.bias, 256, st));
+      continue;
+    }
+    if (q.kind == 3) {
+      CN_TRY(reduce(rd, j.part, j.n_blocks, 3, 256, q.C, q.ldc, st));
+      CN_TRY(reduce(rd, j.bias_part, j.n_blocks, 1, 3, q.bias, 3, st));
+      CN_TRY(reduce(rd, j.bias_part + 3 * (int64_t)j.n_blocks, j.n_blocks, 1, 1, q.sig_out, 1, st));
       continue;
     }
     CN_TRY(reduce(rd, j.part, j.n_blocks, 256, 256, q.C, q.ldc, st));
@@ -2509,10 +2620,17 @@ extern "C" int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, con
   const float* feat = saved + 2 * M * 256;
   const float* v1 = saved + 3 * M * 256;
   const float* v2 = saved + 4 * M * 256;
-  // fc_rgb (h half): dW += d rgb^T v2 (+ g_code's rgb / sigma entries, folded, in the same pass)
-  if (fold_code) CN_TRY(rgb_dw_draw_sums(d_raw, v2, G(kWRgb), 512, M, g_code + kCbRgb, g_code + kCbSigma, st, &red));
-  else CN_TRY(gemm_tn(d_raw, 4, v2, 256, G(kWRgb), 512, M, 3, 256, st, x3, ws, nullptr, nullptr, &red));
-  if (tn_jobs_enabled() && M >= 64 * 1024) {
+  const bool jobs = tn_jobs_enabled() && M >= 64 * 1024;
+  // fc_rgb (h half): dW += d rgb^T v2 (+ g_code's rgb / sigma entries, folded, in the same pass); as
+  // the batched launch's RGB role where that runs (fp32, folded code)
+  const bool rgb_role = jobs && fold_code && !x3;
+  if (rgb_role) {
+  } else if (fold_code) {
+    CN_TRY(rgb_dw_draw_sums(d_raw, v2, G(kWRgb), 512, M, g_code + kCbRgb, g_code + kCbSigma, st, &red));
+  } else {
+    CN_TRY(gemm_tn(d_raw, 4, v2, 256, G(kWRgb), 512, M, 3, 256, st, x3, ws, nullptr, nullptr, &red));
+  }
+  if (jobs) {
     // the four 256 x 256 layers as ONE whole-tile launch (TnBatch): layer_dir2, layer_dir1 [feat]
     // (+ its view-encoding columns by the DIRS fold where it applies), fc_out (+ sigma row),
     // layer_xyz2
@@ -2523,6 +2641,8 @@ extern "C" int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, con
     tb.p[tb.n++] = {P[1], feat, M, dirs ? 2 : 0, G(kWDir1), 283, B(kBDir1), nullptr, nullptr, a, c[1]};
     tb.p[tb.n++] = {P[2], h2, M, 1, G(kWOut) + 512, 512, gc_feat, d_raw + 3, G(kWOut), {}, c[2]};
     tb.p[tb.n++] = {P[3], h1, M, 0, G(kWXyz2), 512, gc_xyz2, nullptr, nullptr, {}, c[3]};
+    if (rgb_role)
+      tb.p[tb.n++] = {d_raw, v2, M, 3, G(kWRgb), 512, g_code + kCbRgb, d_raw, g_code + kCbSigma, {}, c[4]};
     CN_TRY(tn_batch_launch(tb, x3, st, &red));
     if (!dirs) {
       if (x_enc) CN_TRY(gemm_tn(P[1], 256, x_enc + 63, 90, G(kWDir1) + 256, 283, M, 256, 27, st, x3, ws, nullptr, nullptr, &red));
@@ -2548,7 +2668,8 @@ extern "C" int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, con
     // layer_xyz2 (h half)
     CN_TRY(gemm_tn(P[3], 256, h1, 256, G(kWXyz2), 512, M, 256, 256, st, x3, ws, gc_xyz2, bws, &red));
   }
-  // layer_xyz1
+  // layer_xyz1 (its own launch: as a role of the batched launch it ran no faster per CU -- it is
+  // compute work, not a bandwidth pass that could hide beside the GEMMs; r03m)
   if (x_enc) CN_TRY(gemm_tn(P[4], 256, x_enc, 90, G(kWXyz1), 63, M, 256, 63, st, x3, ws, B(kBXyz1), bws, &red));
   else CN_TRY(gemm_tn_enc(0, P[4], a, G(kWXyz1), 63, st, x3, ws, B(kBXyz1), bws, &red));
   CN_TRY(red.flush());

@@ -72,7 +72,8 @@ __global__ __launch_bounds__(kThreads) void render_loss_kernel(const float* __re
                                                                int64_t n_rays, const float* __restrict__ zs,
                                                                const float* __restrict__ zt, int64_t n_code,
                                                                const double* __restrict__ partials, int n_part,
-                                                               double expand, float lambda, float* __restrict__ out) {
+                                                               double expand, float lambda, float* __restrict__ out,
+                                                               double* __restrict__ psnr) {
   __shared__ double red[kThreads / 64];
   double sc = 0.0, sf = 0.0, ss = 0.0, st = 0.0;
   const int64_t n = n_rays * 3;
@@ -114,6 +115,10 @@ __global__ __launch_bounds__(kThreads) void render_loss_kernel(const float* __re
     out[3] = (lc + lf) + reg;
     out[4] = ns;
     out[5] = nt;
+    if (psnr) {  // mse2psnr (util.py:216-227) of the fine loss, float64
+      const double m = static_cast<double>(rgb_f ? lf : lc);
+      psnr[0] = -10.0 * log10(m == 0.0 ? 1e-5 : m);
+    }
   }
 }
 
@@ -155,6 +160,14 @@ extern "C" int cn_render_loss(const float* rgb_coarse, const float* rgb_fine, co
                               int64_t target_stride, int64_t n_rays, const float* z_s, const float* z_t,
                               int64_t n_code, int64_t expand, float regularizer_lambda, double* workspace,
                               float* out, cn_stream_t stream) {
+  return cn_render_loss_psnr(rgb_coarse, rgb_fine, target, target_stride, n_rays, z_s, z_t, n_code, expand,
+                             regularizer_lambda, workspace, out, nullptr, stream);
+}
+
+extern "C" int cn_render_loss_psnr(const float* rgb_coarse, const float* rgb_fine, const float* target,
+                                   int64_t target_stride, int64_t n_rays, const float* z_s, const float* z_t,
+                                   int64_t n_code, int64_t expand, float regularizer_lambda, double* workspace,
+                                   float* out, double* psnr, cn_stream_t stream) {
   CN_CHECK_ARG(n_rays > 0 && target && target_stride >= 3 && out && (rgb_coarse || rgb_fine));
   CN_CHECK_ARG(n_code >= 0 && expand >= 1 && (n_code == 0 || (z_s && z_t)));
   const int64_t ws = cn_render_loss_workspace_doubles(n_code);
@@ -165,7 +178,7 @@ extern "C" int cn_render_loss(const float* rgb_coarse, const float* rgb_fine, co
                        n_code, workspace);
   hipLaunchKernelGGL(render_loss_kernel, dim3(1), dim3(kThreads), 0, cn::as_stream(stream), rgb_coarse, rgb_fine,
                      target, target_stride, n_rays, z_s, z_t, n_code, workspace, n_part, static_cast<double>(expand),
-                     regularizer_lambda, out);
+                     regularizer_lambda, out, psnr);
   return cn::launch_status();
 }
 

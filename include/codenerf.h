@@ -418,6 +418,13 @@ int cn_render_loss(const float* rgb_coarse, const float* rgb_fine, const float* 
                    int64_t target_stride, int64_t n_rays, const float* z_s, const float* z_t,
                    int64_t n_code, int64_t expand, float regularizer_lambda, double* workspace, float* out,
                    cn_stream_t stream);
+/* The same, plus psnr[0] = mse2psnr of the fine loss (of the coarse one without rgb_fine) in
+ * float64 on the device -- utils/util.py:216-227 (-10 log10(mse), mse 0 -> 1e-5), the psnr
+ * train.py:105 / eval.py:160 log -- so the caller needs no launches and no read-back for it. */
+int cn_render_loss_psnr(const float* rgb_coarse, const float* rgb_fine, const float* target,
+                        int64_t target_stride, int64_t n_rays, const float* z_s, const float* z_t,
+                        int64_t n_code, int64_t expand, float regularizer_lambda, double* workspace,
+                        float* out, double* psnr, cn_stream_t stream);
 /* Its backward for an upstream gradient *grad_total (device scalar) of the sum, reading
  * the forward's out as stats: d_rgb_* (n_rays, 3) and d_z_* (n_code) WRITTEN (any NULL). */
 int cn_render_loss_backward(const float* rgb_coarse, const float* rgb_fine, const float* target,
