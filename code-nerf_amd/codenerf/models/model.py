@@ -134,6 +134,36 @@ def _dedupe_codes(z_s: torch.Tensor, z_t: torch.Tensor):
     return z_s, z_t, None
 
 
+class _TableRow(torch.autograd.Function):
+    """Row k of the shape and texture tables (nn.Embedding's lookup of one id) whose backward adds the
+    row gradients into the tables' gradient buffers directly: the optimiser's zeroed flat-buffer slice
+    when the table has no .grad yet this step (optim.AdamW.zero_grad), else a fresh zero table -- one
+    small add per table instead of torch's dense zero fill + scatter + copy into .grad."""
+
+    @staticmethod
+    def forward(ctx, w_s, w_t, k):
+        ctx.k = k
+        ctx.tables = (w_s, w_t)
+        return w_s.detach().narrow(0, k, 1), w_t.detach().narrow(0, k, 1)   # views: no copy
+
+    @staticmethod
+    def backward(ctx, g_s, g_t):
+        out = []
+        for w, g, need in zip(ctx.tables, (g_s, g_t), ctx.needs_input_grad[:2]):
+            if not need or g is None:
+                out.append(None)
+                continue
+            slot = getattr(w, "_cn_grad_slot", None)
+            if slot is not None and w.grad is None:
+                w._cn_grad_slot = None            # one use per zero_grad
+                buf = slot
+            else:
+                buf = torch.zeros_like(w)
+            buf[ctx.k:ctx.k + 1].add_(g)
+            out.append(buf)
+        return out[0], out[1], None
+
+
 class CodeRows:
     """The distinct code rows behind per-ray codes: z_s = shape_rows[index], z_t = texture_rows[index]."""
 
@@ -169,8 +199,7 @@ class ShapeTextureEmbedding(torch.nn.Module):
                 # per-ray codes as their expand -- no id upload, no index search, no gathers; the
                 # field kernels take the one code row (nerf._codes)
                 k = int(uniq_h[0])
-                rows_s = self.shape_embedding.weight.narrow(0, k, 1)
-                rows_t = self.texture_embedding.weight.narrow(0, k, 1)
+                rows_s, rows_t = _TableRow.apply(self.shape_embedding.weight, self.texture_embedding.weight, k)
                 n = object_ids.shape[0]
                 z_s, z_t = rows_s.expand(n, -1), rows_t.expand(n, -1)
                 tag = CodeRows(rows_s, rows_t, None)

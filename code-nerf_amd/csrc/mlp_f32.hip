@@ -152,6 +152,9 @@ struct State {
   float sig;         // sigma partial (this lane group's 64 features)
   int lane, g, wave;
   int crow;          // this lane's code-bias row
+#ifdef CN_ABLATE_PROLOGUE
+  long long prolog;  // experiment: shader clocks from a tile's start to its first chunk, summed over tiles
+#endif
   bool uniform_code; // all 16 samples of the wave use one code row
   __amdgpu_buffer_rsrc_t wsrc;
   unsigned voff;
@@ -425,6 +428,9 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
   const int64_t row = tile * kTile + s.wave * 16 + (s.lane & 15);
   const bool valid = row < a.m;
   const int64_t rc = valid ? row : a.m - 1;
+#ifdef CN_ABLATE_PROLOGUE
+  const long long tp0 = clock64();
+#endif
 
   // ---- per-sample inputs, code row (ordinary loads: the in-flight DMA retires with them)
   const SampleIn in = decode_sample<MODE>(a, rc);
@@ -489,6 +495,9 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
   s.denc[7] = 0.0f;
 
   // ---- layer_xyz1 (63 -> 256): 2 chunks of encoding k-steps
+#ifdef CN_ABLATE_PROLOGUE
+  s.prolog += clock64() - tp0;
+#endif
   bias_from(s, clds + kCB1);
   chunk16<8>(s, lds, c + 0, ArrB<0>{enc});
   chunk16<8>(s, lds, c + 1, ArrB<8>{enc});
@@ -602,6 +611,11 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
 // experiment: each workgroup's start / end wall clock (100 MHz), read by cn_debug_wgtime
 __device__ long long g_wgtime[2048][2];
 #endif
+#ifdef CN_ABLATE_PROLOGUE
+// experiment: per (workgroup, wave) of the last fp32 field launch (forward or backward): tile
+// prologue clocks (summed), the tile loop's clocks, the tile count; read by cn_debug_prologue
+__device__ long long g_prolog[2048][8][3];
+#endif
 
 template <int MODE, bool MASKS, bool SAVE = false>
 __global__ __launch_bounds__(kThreads, 2) void field_w16_kernel(FieldArgs a) {
@@ -633,10 +647,25 @@ __global__ __launch_bounds__(kThreads, 2) void field_w16_kernel(FieldArgs a) {
 
   const int64_t n_tiles = (a.m + kTile - 1) / kTile;
   int c = 0;
+#ifdef CN_ABLATE_PROLOGUE
+  s.prolog = 0;
+  const long long tl0 = clock64();
+  int nt = 0;
+#endif
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
     c = 0;
     field_tile<MODE, MASKS, SAVE>(s, a, lds, clds, crow_lds, tile, c);
+#ifdef CN_ABLATE_PROLOGUE
+    ++nt;
+#endif
   }
+#ifdef CN_ABLATE_PROLOGUE
+  if (s.lane == 0 && blockIdx.x < 2048) {
+    g_prolog[blockIdx.x][s.wave][0] = s.prolog;
+    g_prolog[blockIdx.x][s.wave][1] = clock64() - tl0;
+    g_prolog[blockIdx.x][s.wave][2] = nt;
+  }
+#endif
   // the last tile prefetched chunks 0..2 of a tile that does not exist: they must land
   // before the workgroup's LDS is released
   __builtin_amdgcn_s_waitcnt(0x0F70);
@@ -949,6 +978,9 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   const float* clds = reinterpret_cast<const float*>(lds + kRing * kChunkQuads);
 
   // ---- inputs: sample, d raw, masks of v2 and v1, code row (wave-uniform: host-checked)
+#ifdef CN_ABLATE_PROLOGUE
+  const long long tp0 = clock64();
+#endif
   const SampleIn in = decode_sample<MODE>(a, rc);
   const int crow = __builtin_amdgcn_readfirstlane(static_cast<int>(code_row(a, in.code_of)));
   float4 dr = reinterpret_cast<const float4*>(a.d_raw)[rc];
@@ -974,6 +1006,9 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   }
   int c = 0;
   // ---- fc_rgb^T (chunk 0): B = d rgb channel g at k-step 0
+#ifdef CN_ABLATE_PROLOGUE
+  s.prolog += clock64() - tp0;
+#endif
   zero_acc(s);
   chunk_k0(s, lds, c, s.g == 0 ? dr.x : (s.g == 1 ? dr.y : (s.g == 2 ? dr.z : 0.0f)));
   c = kTDir2;
@@ -1148,8 +1183,24 @@ __global__ __launch_bounds__(kThreads, 2) void field_w16_bwd_kernel(FieldArgs a)
   read_a<0>(lds + s.lane, s.pre);
   int cur_code = -1;
   const int64_t n_tiles = (a.m + kTile - 1) / kTile;
-  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x)
+#ifdef CN_ABLATE_PROLOGUE
+  s.prolog = 0;
+  const long long tl0 = clock64();
+  int nt = 0;
+#endif
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
     bwd_tile<MODE, TRAIN>(s, a, lds, grow, tile, cur_code);
+#ifdef CN_ABLATE_PROLOGUE
+    ++nt;
+#endif
+  }
+#ifdef CN_ABLATE_PROLOGUE
+  if (s.lane == 0 && blockIdx.x < 2048) {
+    g_prolog[blockIdx.x][s.wave][0] = s.prolog;
+    g_prolog[blockIdx.x][s.wave][1] = clock64() - tl0;
+    g_prolog[blockIdx.x][s.wave][2] = nt;
+  }
+#endif
   __builtin_amdgcn_s_waitcnt(0x0F70);
   if (cur_code >= 0) flush_gcode(s, a, grow, cur_code);
   if constexpr (TRAIN) {
@@ -1232,6 +1283,13 @@ int launch_field_w16_bwd(int mode, FieldArgs& a, hipStream_t st) {
 }  // namespace mlp
 }  // namespace cn
 
+#ifdef CN_ABLATE_PROLOGUE
+// experiment: copy g_prolog of the last fp32 field launch (n workgroups x 8 waves x 3)
+extern "C" int cn_debug_prologue(long long* out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(cn::mlp::w16::g_prolog), sizeof(long long) * 24 * std::min(n, 2048)) ==
+                 hipSuccess ? 0 : -1;
+}
+#endif
 #ifdef CN_ABLATE_WGTIME
 // experiment: copy the last field_w16_kernel launch's per-workgroup (start, end) wall clocks
 extern "C" int cn_debug_wgtime(long long* out, int n) {
