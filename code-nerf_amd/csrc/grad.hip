@@ -1123,7 +1123,6 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __rest
     c1 = comp + 1 < 3 ? comp + 1 : K + comp - 2;
   }
   float ev[2] = {0.0f, 0.0f};
-  float4 xv = make_float4(0.f, 0.f, 0.f, 0.f);
   // stage st's 16 A rows: wave w moves rows w, w + 8 (1 KiB each, one 16-B-per-lane wave-instruction)
   auto dma = [&](int st) {
     float* slot = ring[st % kEncRing];
@@ -1134,16 +1133,60 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __rest
       __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(slot + r * 256), 16, lane * 16u, soff, 0, 0);
     }
   };
+  // decode(st) only ISSUES the loads of stage st's geometry (threads 0..15 of wave 0): the point's
+  // depth / origin / direction (ENC 0) or the Q1 direction ray's rd (ENC 1); put_x(st), one stage
+  // later -- after the next barrier's counted vmcnt has seen them land -- forms the point (decode_
+  // sample's arithmetic: ro + rd z) or the unit direction and puts it in the table.  Formed in
+  // decode itself, the arithmetic made wave 0 wait vmcnt(0) for its loads AND the ring's in-flight
+  // pieces every stage, and every other wave then waited at the barrier (r03q ISA).
+  float g0 = 0.0f, g1[3] = {0.f, 0.f, 0.f}, g2[3] = {0.f, 0.f, 0.f};
+  bool gvalid = false;  // rows past the slab: a zero table row (their A rows are zero too)
+  const bool idx32 = M < (int64_t(1) << 31) && a.n_rays < (int64_t(1) << 31);
   auto decode = [&](int st) {
     const int64_t r = (int64_t)st * kEncRows + tid;
-    if (tid < kEncRows && r < rows) {
-      const mlp::SampleIn in = mlp::decode_sample<MODE>(a, mb + r);
-      const float* v = ENC == 0 ? in.x : in.vd;
-      xv = make_float4(v[0], v[1], v[2], 0.0f);
+    gvalid = tid < kEncRows && r < rows;
+    if (gvalid) {
+      const int64_t rc = mb + r;
+      const int64_t S = a.n_samples;
+      const int64_t ray = idx32 ? static_cast<int64_t>(static_cast<unsigned>(rc) / static_cast<unsigned>(S)) : rc / S;
+      if constexpr (ENC == 0) {
+        if constexpr (MODE == mlp::kFromPts) {
+#pragma unroll
+          for (int c = 0; c < 3; ++c) g1[c] = a.pts[3 * rc + c];
+        } else {
+          g0 = a.z[rc];
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            g1[c] = a.ro[3 * ray + c];
+            g2[c] = a.rd[3 * ray + c];
+          }
+        }
+      } else {
+        // Q1 (nerf/__init__.py:127-128): row k = r S + s of a chunk of rcnt rays takes ray k mod rcnt's
+        const int64_t smp = rc - ray * S;
+        const int64_t base = (ray / a.chunk_rows) * a.chunk_rows;
+        const int64_t rcnt = min(a.chunk_rows, a.n_rays - base);
+        const int64_t dray = base + ((ray - base) * S + smp) % rcnt;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) g2[c] = a.rd[3 * dray + c];
+      }
     }
   };
   auto put_x = [&](int st) {
-    if (tid < kEncRows) xs[st % 3][tid] = xv;
+    if (tid < kEncRows) {
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (!gvalid) {
+      } else if constexpr (ENC == 0 && MODE == mlp::kFromPts) {
+        v = make_float4(g1[0], g1[1], g1[2], 0.0f);
+      } else if constexpr (ENC == 0) {
+        v = make_float4(mul_add_rn(g2[0], g0, g1[0]), mul_add_rn(g2[1], g0, g1[1]), mul_add_rn(g2[2], g0, g1[2]), 0.0f);
+      } else {  // view_dir's normalisation, the reference's op order
+        const float nrm = __fsqrt_rn(__fadd_rn(__fadd_rn(__fmul_rn(g2[0], g2[0]), __fmul_rn(g2[1], g2[1])),
+                                               __fmul_rn(g2[2], g2[2])));
+        v = make_float4(__fdiv_rn(g2[0], nrm), __fdiv_rn(g2[1], nrm), __fdiv_rn(g2[2], nrm), 0.0f);
+      }
+      xs[st % 3][tid] = v;
+    }
   };
   auto enc_of = [&](int st) {  // rows past M: their A rows are zero, so any value is harmless
     const float4 x4 = xs[st % 3][es];
