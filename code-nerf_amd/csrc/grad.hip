@@ -1224,7 +1224,8 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __rest
     // st+1's pieces; the geometry loads of decode(st+2), issued before them, are done too), every
     // wave is past stage st-1 (its ring slot is free, its senc / xs buffers were read)
     static_assert(kEncRows / 8 == 2, "the vmcnt below counts one stage of pieces");
-    asm volatile("s_waitcnt vmcnt(2)\n\ts_barrier" ::: "memory");
+    // (lgkmcnt(0): this wave's table writes of the previous stage are done before the barrier)
+    asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     if (st > 0) put_x(st + 2);
     decode(st + 3);
@@ -1248,15 +1249,18 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __rest
         acc[u] = mfma3(acc[u], ah, al, bh, bl);
       }
     } else {
-      float xa[8];
+      // the stage's A values and its encoding operands, each read in one round trip before the
+      // MFMAs (read per row pair, the B operands exposed an LDS wait before every MFMA pair)
+      float xa[8], xb[KB][8];
       ring_read8<2048>(sa + h * 256 + 32 * wave + i, xa);          // rows 2 p + h
+#pragma unroll
+      for (int u = 0; u < KB; ++u) ring_read8<2 * EW * 4>(se + h * EW + 32 * u + i, xb[u]);
 #pragma unroll
       for (int p = 0; p < kEncRows / 2; ++p) {
         const float x = xa[p];
         bsum += x;
 #pragma unroll
-        for (int u = 0; u < KB; ++u)
-          acc[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(x, se[(2 * p + h) * EW + 32 * u + i], acc[u], 0, 0, 0);
+        for (int u = 0; u < KB; ++u) acc[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(x, xb[u][p], acc[u], 0, 0, 0);
       }
     }
     if (more) store_enc((st + 1) & 1);

@@ -47,6 +47,10 @@ def main():
     nb = min(256, (n * s + 127) // 128)
     out = {"rays": n, "samples": s}
     for _ in range(3):
+        ops.radiance_field(packed, cb, rd, s, 4096, fx, fd, ro=ro, z=z, precision="f32_w16")
+    torch.cuda.synchronize()
+    out["forward_inference"] = read(fn, nb)
+    for _ in range(3):
         raw, saved, masks = ops.radiance_field_train_w16(packed, cb, rd, s, 4096, fx, fd, ro=ro, z=z, precision="f32")
     torch.cuda.synchronize()
     out["forward_train"] = read(fn, nb)
