@@ -211,7 +211,7 @@ class ShapeTextureEmbedding(torch.nn.Module):
             # torch.unique on the device would wait for the GPU (its output size) every chunk
             uniq_h = np.unique(np.asarray(host, dtype=np.int64))
             uniq = torch.from_numpy(uniq_h).pin_memory().to(object_ids.device, non_blocking=True)
-            index = torch.searchsorted(uniq, object_ids)
+            index = torch.searchsorted(uniq, object_ids.contiguous())
         else:
             uniq, index = torch.unique(object_ids, return_inverse=True)
         rows_s, rows_t = self.shape_embedding(uniq), self.texture_embedding(uniq)

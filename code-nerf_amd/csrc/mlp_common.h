@@ -60,6 +60,28 @@ __device__ __forceinline__ void add3(float (&v)[3], int i, float x) {
   v[2] += i == 2 ? x : 0.0f;
 }
 
+// sin / cos of an encoding argument without branches, for |x| <= kFastSinBound: Cody-Waite
+// reduction by pi/2 in three fp32 parts with FMAs, then the Cephes sinf / cosf polynomials on
+// [-pi/4, pi/4] (max 1.5 ulp against float64 sin / cos over |x| <= 2^14, 0.34 ulp mean; ocml's
+// sincosf is of the same class but branches into its large-argument path, which keeps the field
+// kernels from interleaving the encodings with the first layer's MFMAs).  Callers check the bound
+// (positional encodings: |x| 2^(L-1) of scene coordinates; beyond it they take sincosf).
+constexpr float kFastSinBound = 16384.0f;
+__device__ __forceinline__ void fast_sincosf(float x, float& sn, float& cs) {
+  const float j = __builtin_rintf(x * 0.636619772367581343f);
+  float r = fmaf(-j, 1.57079637050628662109375f, x);
+  r = fmaf(-j, -4.37113900018624283e-8f, r);
+  r = fmaf(-j, -1.71512451000591636e-15f, r);
+  const float z = r * r;
+  const float s = fmaf(r * z, fmaf(z, fmaf(z, -1.9515295891e-4f, 8.3321608736e-3f), -1.6666654611e-1f), r);
+  const float c = fmaf(z * z, fmaf(z, fmaf(z, 2.443315711809948e-5f, -1.388731625493765e-3f), 4.166664568298827e-2f),
+                       fmaf(-0.5f, z, 1.0f));
+  const int q = static_cast<int>(j) & 3;
+  const float s1 = (q & 1) ? c : s, c1 = (q & 1) ? s : c;
+  sn = (q & 2) ? -s1 : s1;
+  cs = ((q + 1) & 2) ? -c1 : c1;
+}
+
 // One sample's inputs: point, unit Q1 view direction, code row.
 struct SampleIn {
   float x[3];

@@ -62,7 +62,7 @@ constexpr int kCB1 = 0, kCBD1 = 256, kCBD2 = 512, kCSig = 768, kConsts = 1024;
 constexpr int kPackedFloats = kStreamFloats + kConsts;
 // LDS constants: the packed ones, then the encoding frequencies (fx[10] | fd[4] | pad 2): a
 // lane-varying index into the kernel arguments is a global load per use (or a register held
-// across the tile loop), an LDS read is neither
+// across the tile loop), an LDS read is neither; the pad holds the largest |fx| and |fd|
 constexpr int kCFreq = kConsts, kLdsConsts = kConsts + 16;
 // LDS: the ring, the constants, one code-bias row per wave
 constexpr int kLdsQuads = kRing * kChunkQuads + (kLdsConsts + kWaves * kCbStride) / 4;
@@ -167,7 +167,12 @@ __device__ __forceinline__ void load_consts(const FieldArgs& a, float* clds) {
   for (int k = threadIdx.x; k < kConsts; k += kThreads) clds[k] = a.packed[kStreamFloats + k];
   if (threadIdx.x < 16) {
     const int t = threadIdx.x;
-    clds[kCFreq + t] = t < 10 ? a.fx[t] : (t < 14 ? a.fd[t - 10] : 0.0f);
+    float mx = 0.0f, md = 0.0f;  // the largest |frequency| of each encoding (fast_sincosf's range check)
+#pragma unroll
+    for (int k = 0; k < 10; ++k) mx = fmaxf(mx, fabsf(a.fx[k]));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) md = fmaxf(md, fabsf(a.fd[k]));
+    clds[kCFreq + t] = t < 10 ? a.fx[t] : (t < 14 ? a.fd[t - 10] : (t == 14 ? mx : md));
   }
 }
 
@@ -251,6 +256,22 @@ __device__ __forceinline__ void step_pattern() {
   __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
 }
 
+// A k-step with VALU work of its own (LazyXyz): the A reads and 2-3 VALU instructions between
+// consecutive MFMAs, the remainder after the last.
+__device__ __forceinline__ void lazy_step_pattern() {
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+  }
+#pragma unroll
+  for (int m = 0; m < 12; ++m) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+  }
+}
+
 // Nothing to issue during a chunk.
 struct NoPost {
   template <int CI, int T>
@@ -280,7 +301,9 @@ __device__ __forceinline__ void chunk16(State& s, float4* lds, int c, GetB getb,
     if constexpr ((T) + 1 < NS) read_a<(T) + 1>(slot, NXT);         \
     else read_a<0>(nslot, s.pre);                                   \
     mfma_step(s, CUR, getb.template at<(T)>());                     \
-    step_pattern();                                                 \
+    getb.template prep<(T)>();                                      \
+    if constexpr (GetB::kLazy) lazy_step_pattern();                 \
+    else step_pattern();                                            \
     __builtin_amdgcn_sched_barrier(0);                              \
     if constexpr ((T) == 3) {                                       \
       chunk_barrier();                                              \
@@ -308,12 +331,77 @@ struct ActB {
     constexpr int t = K0 + T;
     return s.act[t >> 2][t & 3];
   }
+  static constexpr bool kLazy = false;
+  template <int T>
+  __device__ __forceinline__ void prep() const {}
 };
 template <int K0>
 struct ArrB {
   const float* v;
   template <int T>
   __device__ __forceinline__ float at() const { return v[K0 + T]; }
+  static constexpr bool kLazy = false;
+  template <int T>
+  __device__ __forceinline__ void prep() const {}
+};
+
+// layer_xyz1's B operands computed where they are consumed: in its first chunk, k-step T's MFMAs
+// use the sine of pair T (lane group g: pair p = 4 T + g) and, issued after them, the (sin, cos) of
+// pair T + 1 is evaluated (fast_sincosf, branch-free), so its VALU fills the MFMAs' shadow instead
+// of a tile prologue that both waves of every SIMD ran at once with the matrix pipe idle (~2.7 % of
+// the inference forward's tile time, r03s).  The second chunk consumes the cosines and evaluates
+// the three view-direction pairs and the raw direction component the view-dir chunk takes later.
+struct LazyXyz {
+  float (&enc)[16];
+  float (&denc)[8];
+  const float (&x)[3];
+  const float (&vd)[3];
+  const float (&fr)[11];  // this lane group's frequencies: pairs 0..7 (xyz), 0..2 (view direction)
+  int g;
+  bool second;            // the chunk of the cosines (k-steps 8..15)
+  static constexpr bool kLazy = true;
+  template <int T>
+  __device__ __forceinline__ float at() const { return second ? enc[8 + T] : enc[T]; }
+  // c ? a : b on the bits (lane-varying selects written as ternaries came out as EXEC-masked
+  // branches here, which split the k-step's block and stopped the MFMA / VALU interleave)
+  static __device__ __forceinline__ float bsel(bool c, float a, float b) {
+    const int m = -static_cast<int>(c);
+    return __int_as_float((__float_as_int(a) & m) | (__float_as_int(b) & ~m));
+  }
+  static __device__ __forceinline__ float sel3(const float (&v)[3], int c) {
+    return bsel(c == 0, v[0], bsel(c == 1, v[1], v[2]));
+  }
+  // sin / cos of pair I of this lane group (I < 7, or groups 0, 1 at I = 7); groups 2, 3 take raw
+  // inputs at I = 7 (col_enc_xyz).  p = 4 I + g: p % 3 = (I % 3 + g) mod 3, p / 3 = (11 p) >> 5
+  // (exact for p < 32), no divisions.
+  template <int I>
+  __device__ __forceinline__ void pair() const {
+    const int p = 4 * I + g;
+    const int c0 = I % 3 + g;
+    const int comp = c0 >= 3 ? c0 - 3 : c0;
+    float sn, cs;
+    fast_sincosf(__fmul_rn(sel3(x, comp), fr[I]), sn, cs);
+    if constexpr (I == 7) {
+      const bool raw = p >= 30;
+      sn = bsel(raw, bsel(g == 2, x[0], x[2]), sn);
+      cs = bsel(raw, bsel(g == 2, x[1], 0.0f), cs);
+    }
+    enc[I] = sn;
+    enc[8 + I] = cs;
+  }
+  template <int T>
+  __device__ __forceinline__ void prep() const {
+    if (!second) {
+      if constexpr (T + 1 < 8) pair<T + 1>();
+    } else if constexpr (T < 3) {
+      const int c0 = T + g;
+      const int comp = c0 >= 3 ? c0 - 3 : c0;
+      fast_sincosf(__fmul_rn(sel3(vd, comp), fr[8 + T]), denc[T], denc[3 + T]);
+    } else if constexpr (T == 3) {
+      denc[6] = bsel(g == 3, 0.0f, sel3(vd, g));
+      denc[7] = 0.0f;
+    }
+  }
 };
 
 // A 256-input layer: 8 chunks, B from s.act.
@@ -467,40 +555,71 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
     if (j < kCbStride) crow_lds[j] = cbr[k];
   }
 
-  // ---- encodings: lane group g owns pairs p = 4 i + g
+  // ---- encodings (lane group g owns pairs p = 4 i + g) and layer_xyz1 (63 -> 256): 2 chunks of
+  // encoding k-steps.  Lazily (LazyXyz) when every lane's arguments are in fast_sincosf's range,
+  // else all evaluated up front with sincosf.
+  bool lazy = false;
   if constexpr (MODE != kFromEncoded) {
-    const int g = fresh(s.g);  // the pair indices below are formed here, not held across tiles
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int p = 4 * i + g;
-      const int pc = p < 30 ? p : 0;
-      const float arg = __fmul_rn(pick3(in.x, pc % 3), clds[kCFreq + pc / 3]);
-      float sn, cs;
-      sincosf(arg, &sn, &cs);
-      if (i == 7 && p >= 30) {  // groups 2, 3: raw inputs
-        sn = s.g == 2 ? in.x[0] : in.x[2];
-        cs = s.g == 2 ? in.x[1] : 0.0f;
-      }
-      enc[i] = sn;
-      enc[8 + i] = cs;
-    }
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const int p = 4 * i + g;
-      const float arg = __fmul_rn(pick3(in.vd, p % 3), clds[kCFreq + 10 + p / 3]);
-      sincosf(arg, &s.denc[i], &s.denc[3 + i]);
-    }
-    s.denc[6] = s.g == 0 ? in.vd[0] : (s.g == 1 ? in.vd[1] : (s.g == 2 ? in.vd[2] : 0.0f));
+    const float xa = fmaxf(fmaxf(fabsf(in.x[0]), fabsf(in.x[1])), fabsf(in.x[2])) * clds[kCFreq + 14];
+    const float da = fmaxf(fmaxf(fabsf(in.vd[0]), fabsf(in.vd[1])), fabsf(in.vd[2])) * clds[kCFreq + 15];
+    const bool ok = xa <= kFastSinBound && da <= kFastSinBound;  // false for NaN
+    lazy = __builtin_amdgcn_readfirstlane(__ballot(!ok) == 0 ? 1 : 0) != 0;
   }
-  s.denc[7] = 0.0f;
-
-  // ---- layer_xyz1 (63 -> 256): 2 chunks of encoding k-steps
+  if (lazy) {
+    if constexpr (MODE != kFromEncoded) {
+      // the frequencies of this lane group's pairs, read once here: an LDS read inside the k-steps
+      // made each wait lgkmcnt(0) on the next k-step's A fragments too
+      const int g = fresh(s.g);
+      float fr[11];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int p = 4 * i + g;
+        fr[i] = clds[kCFreq + ((p < 30 ? p : 0) * 11 >> 5)];  // (11 p) >> 5 = p / 3 for p < 32
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i) fr[8 + i] = clds[kCFreq + 10 + ((4 * i + g) * 11 >> 5)];
+      const LazyXyz l0{enc, s.denc, in.x, in.vd, fr, g, false};
+      l0.pair<0>();
 #ifdef CN_ABLATE_PROLOGUE
-  s.prolog += clock64() - tp0;
+      s.prolog += clock64() - tp0;
 #endif
-  bias_from(s, clds + kCB1);
-  chunk16<8>(s, lds, c + 0, ArrB<0>{enc});
-  chunk16<8>(s, lds, c + 1, ArrB<8>{enc});
+      bias_from(s, clds + kCB1);
+      chunk16<8>(s, lds, c + 0, l0);
+      chunk16<8>(s, lds, c + 1, LazyXyz{enc, s.denc, in.x, in.vd, fr, g, true});
+    }
+  } else {
+    if constexpr (MODE != kFromEncoded) {
+      const int g = fresh(s.g);  // the pair indices below are formed here, not held across tiles
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int p = 4 * i + g;
+        const int pc = p < 30 ? p : 0;
+        const float arg = __fmul_rn(pick3(in.x, pc % 3), clds[kCFreq + pc / 3]);
+        float sn, cs;
+        sincosf(arg, &sn, &cs);
+        if (i == 7 && p >= 30) {  // groups 2, 3: raw inputs
+          sn = s.g == 2 ? in.x[0] : in.x[2];
+          cs = s.g == 2 ? in.x[1] : 0.0f;
+        }
+        enc[i] = sn;
+        enc[8 + i] = cs;
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int p = 4 * i + g;
+        const float arg = __fmul_rn(pick3(in.vd, p % 3), clds[kCFreq + 10 + p / 3]);
+        sincosf(arg, &s.denc[i], &s.denc[3 + i]);
+      }
+      s.denc[6] = s.g == 0 ? in.vd[0] : (s.g == 1 ? in.vd[1] : (s.g == 2 ? in.vd[2] : 0.0f));
+    }
+    s.denc[7] = 0.0f;
+#ifdef CN_ABLATE_PROLOGUE
+    s.prolog += clock64() - tp0;
+#endif
+    bias_from(s, clds + kCB1);
+    chunk16<8>(s, lds, c + 0, ArrB<0>{enc});
+    chunk16<8>(s, lds, c + 1, ArrB<8>{enc});
+  }
   c += 2;
 
   // ---- layer_xyz2, fc_out, layer_dir1 (+ view-dir chunk), layer_dir2
