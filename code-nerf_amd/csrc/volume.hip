@@ -6,15 +6,18 @@
 
 namespace {
 
-// 16 lanes (one DPP row) per ray, 4 rays per wave, 16 per 256-thread block.  Lane i of a row owns
-// the contiguous run of samples [i run, (i + 1) run), run = ceil(S / 16) <= K; its next sample's
-// depth (z[j + 1] past the run) comes from lane i + 1 by DPP instead of a second load; the
-// exclusive prefix of sigma*delta over the lanes' run totals is a 4-step DPP row scan (in double,
-// as torch's CPU cumsum accumulates, Q13), and the per-ray sums are DPP row reductions -- every
-// cross-lane step stays inside the row, with no LDS traffic.
+// L lanes per ray: 16 (one DPP row; 4 rays per wave, 16 per 256-thread block) for S <= 128, 64
+// (the whole wave; 4 rays per block) above, so a lane's run stays <= 8 samples in registers at
+// every S <= 512.  Lane i of a ray owns the contiguous run of samples [i run, (i + 1) run),
+// run = ceil(S / L) <= K; its next sample's depth (z[j + 1] past the run) comes from lane i + 1 by
+// DPP (a lane shuffle when L = 64) instead of a second load; the exclusive prefix of sigma*delta
+// over the lanes' run totals is a 4-step DPP row scan (in double, as torch's CPU cumsum
+// accumulates, Q13) plus, for L = 64, the earlier rows' totals read back as scalars; the per-ray
+// sums are DPP row reductions (plus the row totals for L = 64) -- no LDS traffic in any
+// cross-lane step.
 // Algorithmic bytes per ray: 12 (rd) + 20*S in (raw + z), 4*S + 20 out.
-constexpr int kRowsPerBlock = 16;
-constexpr int kMaxRun = 32;  // S <= 512
+constexpr int kMaxRun = 8;
+constexpr int kMaxSamples = 64 * kMaxRun;  // 512
 
 template <int CTRL>
 __device__ __forceinline__ float dppf(float x) {
@@ -27,23 +30,21 @@ __device__ __forceinline__ double dppd(double x) {
   const int hi = __builtin_amdgcn_update_dpp(0, static_cast<int>(v >> 32), CTRL, 0xF, 0xF, true);
   return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
 }
-// Exclusive prefix over the 16 lanes of the row (row_shr: lane i reads lane i - n, 0 below the row).
-__device__ __forceinline__ double row_exclusive_scan(double v) {
-  double x = v;
+// Inclusive prefix over the 16 lanes of the row (row_shr: lane i reads lane i - n, 0 below the row).
+__device__ __forceinline__ double row_inclusive_scan(double x) {
   x += dppd<0x111>(x);
   x += dppd<0x112>(x);
   x += dppd<0x114>(x);
   x += dppd<0x118>(x);
-  return x - v;
+  return x;
 }
-// Exclusive suffix over the row (row_shl: lane i reads lane i + n, 0 past the row).
-__device__ __forceinline__ float row_exclusive_suffix(float v) {
-  float x = v;
+// Inclusive suffix over the row (row_shl: lane i reads lane i + n, 0 past the row).
+__device__ __forceinline__ float row_inclusive_suffix(float x) {
   x += dppf<0x101>(x);
   x += dppf<0x102>(x);
   x += dppf<0x104>(x);
   x += dppf<0x108>(x);
-  return x - v;
+  return x;
 }
 // Sum over the row's 16 lanes, valid in lane 15.
 __device__ __forceinline__ float row_sum(float x) {
@@ -54,9 +55,73 @@ __device__ __forceinline__ float row_sum(float x) {
   return x;
 }
 
-// Load this lane's run of depths and raw rows (zero past S): 16-B vector loads of the depths
-// when the run is a multiple of 4 aligned to 16 B (every S % 4 == 0 with run % 4 == 0: S = 64,
-// 128 -- the C2 / C3 shapes), element loads otherwise.
+__device__ __forceinline__ float lanef(float x, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
+}
+__device__ __forceinline__ double laned(double x, int l) {
+  const long long v = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_readlane(static_cast<int>(v & 0xffffffff), l);
+  const int hi = __builtin_amdgcn_readlane(static_cast<int>(v >> 32), l);
+  return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
+}
+
+// The ray-level cross-lane steps over its L lanes.  L = 16: the row steps.  L = 64 (one ray per
+// wave): the row step, then the other rows' totals -- uniform, read back by readlane -- added in
+// a fixed order.
+template <int L>
+__device__ __forceinline__ double ray_exclusive_scan(double v) {
+  const double x = row_inclusive_scan(v);
+  if constexpr (L == 16) {
+    return x - v;
+  } else {
+    const int row = (threadIdx.x & 63) >> 4;
+    const double t0 = laned(x, 15), t1 = laned(x, 31), t2 = laned(x, 47);
+    double off = 0.0;
+    if (row > 0) off += t0;
+    if (row > 1) off += t1;
+    if (row > 2) off += t2;
+    return (x - v) + off;
+  }
+}
+template <int L>
+__device__ __forceinline__ float ray_exclusive_suffix(float v) {
+  const float x = row_inclusive_suffix(v);
+  if constexpr (L == 16) {
+    return x - v;
+  } else {  // row totals: the inclusive suffix in each row's lane 0
+    const int row = (threadIdx.x & 63) >> 4;
+    const float t1 = lanef(x, 16), t2 = lanef(x, 32), t3 = lanef(x, 48);
+    float off = 0.0f;
+    if (row < 3) off += t3;
+    if (row < 2) off += t2;
+    if (row < 1) off += t1;
+    return (x - v) + off;
+  }
+}
+// The ray's sum over its L lanes: valid in lane 15 of the row (L = 16) / every lane (L = 64).
+template <int L>
+__device__ __forceinline__ float ray_sum(float x) {
+  x = row_sum(x);
+  if constexpr (L == 64) x = ((lanef(x, 15) + lanef(x, 31)) + lanef(x, 47)) + lanef(x, 63);
+  return x;
+}
+// ... valid in every lane of the ray.
+template <int L>
+__device__ __forceinline__ float ray_sum_all(float x) {
+  if constexpr (L == 16) return __shfl(row_sum(x), (threadIdx.x & 63) | 15);
+  else return ray_sum<64>(x);
+}
+// Lane + 1's value (the next run's first depth); 0 (L = 16) or the lane's own value (L = 64) past
+// the ray's last lane, where it is never used.
+template <int L>
+__device__ __forceinline__ float next_lane(float x) {
+  if constexpr (L == 16) return dppf<0x101>(x);
+  else return __shfl_down(x, 1);
+}
+
+// Load this lane's run of depths (zero past S): 16-B vector loads when the run is a multiple of
+// 4 aligned to 16 B (every S % 4 == 0 with run % 4 == 0: S = 64, 128 -- the C2 / C3 shapes),
+// element loads otherwise.
 template <int K>
 __device__ __forceinline__ void load_depths(const float* zr, int j0, int run, int S_in, float (&zz)[K]) {
   if (K % 4 == 0 && run % 4 == 0 && (S_in & 3) == 0 && j0 + run <= S_in) {
@@ -84,13 +149,12 @@ __device__ __forceinline__ void load_run(const float* zr, const float4* rr, int 
     rv[i] = (i < run && j0 + i < S_in) ? rr[j0 + i] : make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
-// Raw rows through LDS (K <= 8, i.e. S <= 128): a lane's run of float4 samples is 16 run bytes
-// apart from its neighbour's, so per-lane loads of it touch every cache line four (eight) times.
-// The wave's four rays' rows are ONE contiguous (4 S) float4 block: lane l copies quads
-// l + 64 t with coalesced 16-B loads into LDS slot pad(q) = q + q / 4 (a padding quad after every
-// four: runs of four then sit 5 quads apart, conflict-free across a 16-lane group), and each lane
-// then reads its own run from there.  The backward stores d raw back the same way.
-constexpr int kLdsMaxK = 8;
+// Raw rows through LDS: a lane's run of float4 samples is 16 run bytes apart from its
+// neighbour's, so per-lane loads of it touch every cache line run times.  The wave's rays' rows
+// (64 / L of them) are ONE contiguous (64 / L) S float4 block: lane l copies quads l + 64 t with
+// coalesced 16-B loads into LDS slot pad(q) = q + q / 4 (a padding quad after every four: runs of
+// four then sit 5 quads apart, conflict-free across a 16-lane group), and each lane then reads
+// its own run from there.  The backward stores d raw back the same way.  <= 64 K quads per wave.
 __device__ __forceinline__ int pad4(int q) { return q + (q >> 2); }
 
 template <int K>
@@ -118,45 +182,38 @@ __device__ __forceinline__ void load_raw_lds(const float4* sl, int q0, int j0, i
   for (int i = 0; i < K; ++i) rv[i] = (i < run && j0 + i < S_in) ? sl[pad4(q0 + i)] : make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
-template <int K, bool FULL>
+template <int K, bool FULL, int L>
 __global__ __launch_bounds__(256) void volume_render_kernel(
     const float* __restrict__ raw, const float* __restrict__ z, const float* __restrict__ rd,
     int64_t n_rays, int S_in, float* __restrict__ rgb, float* __restrict__ disp,
     float* __restrict__ acc, float* __restrict__ weights, float* __restrict__ depth) {
-  if (FULL) S_in = 16 * K;  // the host dispatches FULL only for S == 16 K: lets every bound fold
-  constexpr bool kLds = K <= kLdsMaxK;
-  __shared__ float4 slds[kLds ? 4 * 80 * K : 1];  // per wave: 4 rays x <= 16 K quads, padded 5 / 4
-  const int sub = threadIdx.x & 15, lane = threadIdx.x & 63;
-  const int64_t r = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
-  const int64_t rw0 = r - (lane >> 4);  // the wave's first ray
-  float4* sl = slds + (kLds ? (threadIdx.x >> 6) * 80 * K : 0);
-  if constexpr (kLds) {
-    if (rw0 < n_rays)
-      stage_rows_in<K>(reinterpret_cast<const float4*>(raw) + rw0 * S_in,
-                       static_cast<int>(min<int64_t>(4, n_rays - rw0)) * S_in, sl, lane);
-  }
-  if (r >= n_rays) return;  // whole rows leave together: the DPP steps never read an exited lane
+  static_assert(K <= kMaxRun && (L == 16 || L == 64) && (!FULL || L == 16), "instance");
+  if (FULL) S_in = L * K;  // the host dispatches FULL only for S == 16 K: lets every bound fold
+  __shared__ float4 slds[4 * 80 * K];  // per wave: <= 64 K quads, padded 5 / 4
+  const int sub = threadIdx.x & (L - 1), lane = threadIdx.x & 63;
+  const int64_t r = ((int64_t)blockIdx.x * 256 + threadIdx.x) / L;
+  const int64_t rw0 = r - lane / L;  // the wave's first ray
+  float4* sl = slds + (threadIdx.x >> 6) * 80 * K;
+  if (rw0 < n_rays)
+    stage_rows_in<K>(reinterpret_cast<const float4*>(raw) + rw0 * S_in,
+                     static_cast<int>(min<int64_t>(64 / L, n_rays - rw0)) * S_in, sl, lane);
+  if (r >= n_rays) return;  // whole rays leave together: the cross-lane steps never read an exited lane
   // S == 1: the reference's dists = cat(z[1:] - z[:-1], full_like(that[..., :1], 1e10))
   // is EMPTY (both pieces are 0 wide), so no sample contributes (rgb = acc = depth = 0,
   // disp = NaN, weights (R, 0)).  Reproduced by treating the ray as sample-free.
   // FULL (S_in == 16 K: every lane's run is K samples): the run / bounds tests fold away
-  const int S = FULL ? 16 * K : (S_in == 1 ? 0 : S_in);
-  const int run = FULL ? K : (S_in + 15) >> 4;
+  const int S = FULL ? L * K : (S_in == 1 ? 0 : S_in);
+  const int run = FULL ? K : (S_in + L - 1) / L;
   const int j0 = sub * run;
   const float* zr = z + r * S_in;
-  const float4* rr = reinterpret_cast<const float4*>(raw) + r * S_in;
   const float d0 = rd[3 * r], d1 = rd[3 * r + 1], d2 = rd[3 * r + 2];
   const float nrm = __fsqrt_rn(__fadd_rn(__fadd_rn(__fmul_rn(d0, d0), __fmul_rn(d1, d1)), __fmul_rn(d2, d2)));
 
   float zz[K], sd[K], wv[K];
   float4 rv[K];
-  if constexpr (kLds) {
-    load_depths<K>(zr, j0, run, S_in, zz);
-    load_raw_lds<K>(sl, (lane >> 4) * S_in + j0, j0, run, S_in, rv);
-  } else {
-    load_run<K>(zr, rr, j0, run, S_in, zz, rv);
-  }
-  const float znext = dppf<0x101>(zz[0]);  // the first depth of lane sub + 1's run
+  load_depths<K>(zr, j0, run, S_in, zz);
+  load_raw_lds<K>(sl, (lane / L) * S_in + j0, j0, run, S_in, rv);
+  const float znext = next_lane<L>(zz[0]);  // the first depth of lane sub + 1's run
   double run_sum = 0.0;  // sum of this run's sigma*delta that feeds later transmittances
 #pragma unroll
   for (int i = 0; i < K; ++i) {
@@ -171,7 +228,7 @@ __global__ __launch_bounds__(256) void volume_render_kernel(
       if (j + 1 < S) run_sum += static_cast<double>(sd[i]);
     }
   }
-  double prefix = row_exclusive_scan(run_sum);
+  double prefix = ray_exclusive_scan<L>(run_sum);
 
   float cr = 0.f, cg = 0.f, cb = 0.f, dep = 0.f, ac = 0.f;
 #pragma unroll
@@ -195,7 +252,7 @@ __global__ __launch_bounds__(256) void volume_render_kernel(
       if (j + 1 < S) prefix += static_cast<double>(sd[i]);
     }
   }
-  if (weights) {  // this lane's run of weights: 16-B stores where the run is aligned (see load_run)
+  if (weights) {  // this lane's run of weights: 16-B stores where the run is aligned (see load_depths)
     float* wr = weights + r * S_in;
     if (K % 4 == 0 && run % 4 == 0 && (S_in & 3) == 0 && j0 + run <= S_in && S > 0) {
 #pragma unroll
@@ -208,12 +265,12 @@ __global__ __launch_bounds__(256) void volume_render_kernel(
         if (i < run && j0 + i < S) wr[j0 + i] = wv[i];
     }
   }
-  cr = row_sum(cr);
-  cg = row_sum(cg);
-  cb = row_sum(cb);
-  dep = row_sum(dep);
-  ac = row_sum(ac);
-  if (sub == 15) {
+  cr = ray_sum<L>(cr);
+  cg = ray_sum<L>(cg);
+  cb = ray_sum<L>(cb);
+  dep = ray_sum<L>(dep);
+  ac = ray_sum<L>(ac);
+  if (sub == (L == 16 ? 15 : 63)) {
     rgb[3 * r] = cr;
     rgb[3 * r + 1] = cg;
     rgb[3 * r + 2] = cb;
@@ -227,28 +284,27 @@ __global__ __launch_bounds__(256) void volume_render_kernel(
 
 }  // namespace
 
-// Samples per lane the kernels are instantiated for: the smallest that holds ceil(S / 16).
-// S = 64 / 128 (every C2-C5 shape) take the FULL instances.
-#define CN_VOLUME_DISPATCH(KERNEL, S, ...)                                                   \
-  do {                                                                                      \
-    const int run_ = static_cast<int>(((S) + 15) / 16);                                    \
-    if ((S) == 64) hipLaunchKernelGGL((KERNEL<4, true>), __VA_ARGS__);                     \
-    else if ((S) == 128) hipLaunchKernelGGL((KERNEL<8, true>), __VA_ARGS__);               \
-    else if (run_ <= 4) hipLaunchKernelGGL((KERNEL<4, false>), __VA_ARGS__);               \
-    else if (run_ <= 8) hipLaunchKernelGGL((KERNEL<8, false>), __VA_ARGS__);               \
-    else if (run_ <= 12) hipLaunchKernelGGL((KERNEL<12, false>), __VA_ARGS__);             \
-    else if (run_ <= 16) hipLaunchKernelGGL((KERNEL<16, false>), __VA_ARGS__);             \
-    else hipLaunchKernelGGL((KERNEL<32, false>), __VA_ARGS__);                             \
+// Instances: S = 64 / 128 (every C2-C5 coarse / merged shape) take the FULL 16-lane ones; other
+// S <= 128 the 16-lane ones with run <= 4 / 8; S <= 512 (the 32 + 160 and 64 + 128 merged
+// shapes: S = 192) the 64-lane ones with run <= 4 / 8.
+#define CN_VOLUME_DISPATCH(KERNEL, S, N, STREAM, ...)                                                      \
+  do {                                                                                                      \
+    const dim3 g16(static_cast<unsigned>(cn::ceil_div((N), 16))), g64(static_cast<unsigned>(cn::ceil_div((N), 4))); \
+    if ((S) == 64) hipLaunchKernelGGL((KERNEL<4, true, 16>), g16, dim3(256), 0, STREAM, __VA_ARGS__);      \
+    else if ((S) == 128) hipLaunchKernelGGL((KERNEL<8, true, 16>), g16, dim3(256), 0, STREAM, __VA_ARGS__); \
+    else if ((S) <= 64) hipLaunchKernelGGL((KERNEL<4, false, 16>), g16, dim3(256), 0, STREAM, __VA_ARGS__); \
+    else if ((S) <= 128) hipLaunchKernelGGL((KERNEL<8, false, 16>), g16, dim3(256), 0, STREAM, __VA_ARGS__); \
+    else if ((S) <= 256) hipLaunchKernelGGL((KERNEL<4, false, 64>), g64, dim3(256), 0, STREAM, __VA_ARGS__); \
+    else hipLaunchKernelGGL((KERNEL<8, false, 64>), g64, dim3(256), 0, STREAM, __VA_ARGS__);                \
   } while (0)
 
 extern "C" int cn_volume_render(const float* raw, const float* z, const float* rd, int64_t n_rays,
                                 int64_t n_samples, float* rgb, float* disp, float* acc,
                                 float* weights, float* depth, cn_stream_t stream) {
   CN_CHECK_ARG(raw && z && rd && rgb && disp && acc && depth);
-  CN_CHECK_ARG(n_rays > 0 && n_samples > 0 && n_samples <= 16 * kMaxRun);
-  const unsigned grid = static_cast<unsigned>(cn::ceil_div(n_rays, kRowsPerBlock));
-  CN_VOLUME_DISPATCH(volume_render_kernel, n_samples, dim3(grid), dim3(256), 0, cn::as_stream(stream), raw, z, rd,
-                     n_rays, static_cast<int>(n_samples), rgb, disp, acc, weights, depth);
+  CN_CHECK_ARG(n_rays > 0 && n_samples > 0 && n_samples <= kMaxSamples);
+  CN_VOLUME_DISPATCH(volume_render_kernel, n_samples, n_rays, cn::as_stream(stream), raw, z, rd, n_rays,
+                     static_cast<int>(n_samples), rgb, disp, acc, weights, depth);
   return cn::launch_status();
 }
 
@@ -256,54 +312,48 @@ extern "C" int cn_volume_render(const float* raw, const float* z, const float* r
 // Gradient of volume_render (volumetric_render.py:36-66) w.r.t. raw and rd.
 // With sd_i = sigma_i delta_i, T_i = exp(-sum_{j<i} sd_j), w_i = (1 - e^{-sd_i}) T_i:
 //   G_i = g_w_i + g_rgb . c_i + g_depth z_i + g_acc          (dL/dw_i)
-//   dL/dsd_i = G_i T_i e^{-sd_i} - sum_{j>i} G_j w_j          (reverse row scan)
+//   dL/dsd_i = G_i T_i e^{-sd_i} - sum_{j>i} G_j w_j          (reverse ray scan)
 //   d raw_i[0:3] = w_i g_rgb 1.002 s(1-s);  d raw_i[3] = dL/dsd_i delta_i softplus'(raw_i[3]-1)
 //   d rd = (sum_i dL/dsd_i sigma_i dist_i) rd/|rd|
 // g_disp folds into g_depth / g_acc through disp = 1/max(1e-10, depth/acc).
 // z is never differentiated (the reference detaches its samples).  Same layout as the forward.
 namespace {
 
-template <int K, bool FULL>
+template <int K, bool FULL, int L>
 __global__ __launch_bounds__(256) void volume_render_backward_kernel(
     const float* __restrict__ raw, const float* __restrict__ z, const float* __restrict__ rd,
     int64_t n_rays, int S_in, const float* __restrict__ g_rgb, const float* __restrict__ g_disp,
     const float* __restrict__ g_acc, const float* __restrict__ g_w, const float* __restrict__ g_depth,
     float* __restrict__ d_raw, float* __restrict__ d_rd) {
-  if (FULL) S_in = 16 * K;  // as in the forward
-  constexpr bool kLds = K <= kLdsMaxK;
-  __shared__ float4 slds[kLds ? 4 * 80 * K : 1];  // per wave: raw in, then d raw out (forward's layout)
-  const int sub = threadIdx.x & 15, lane = threadIdx.x & 63;
-  const int64_t r_ = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
-  const int64_t rw0 = r_ - (lane >> 4);
+  static_assert(K <= kMaxRun && (L == 16 || L == 64) && (!FULL || L == 16), "instance");
+  if (FULL) S_in = L * K;  // as in the forward
+  __shared__ float4 slds[4 * 80 * K];  // per wave: raw in, then d raw out (forward's layout)
+  const int sub = threadIdx.x & (L - 1), lane = threadIdx.x & 63;
+  const int64_t r_ = ((int64_t)blockIdx.x * 256 + threadIdx.x) / L;
+  const int64_t rw0 = r_ - lane / L;
   if (rw0 >= n_rays) return;  // the whole wave
-  const int nq = static_cast<int>(min<int64_t>(4, n_rays - rw0)) * S_in;  // the wave's valid quads
-  float4* sl = slds + (kLds ? (threadIdx.x >> 6) * 80 * K : 0);
-  if constexpr (kLds) stage_rows_in<K>(reinterpret_cast<const float4*>(raw) + rw0 * S_in, nq, sl, lane);
-  // LDS path: a row past n_rays stays alive (as a copy of the last ray, nothing stored) so the
-  // wave's coalesced d raw copy-out runs in every lane; else it leaves here
+  const int nq = static_cast<int>(min<int64_t>(64 / L, n_rays - rw0)) * S_in;  // the wave's valid quads
+  float4* sl = slds + (threadIdx.x >> 6) * 80 * K;
+  stage_rows_in<K>(reinterpret_cast<const float4*>(raw) + rw0 * S_in, nq, sl, lane);
+  // a ray past n_rays (L = 16 only) stays alive as a copy of the last ray, nothing stored, so the
+  // wave's coalesced d raw copy-out runs in every lane
   const bool live = r_ < n_rays;
-  if (!kLds && !live) return;
   const int64_t r = live ? r_ : n_rays - 1;
-  const int S = FULL ? 16 * K : (S_in == 1 ? 0 : S_in);  // see the forward: S == 1 has no contributing sample
-  const int run = FULL ? K : (S_in + 15) >> 4;
+  const int S = FULL ? L * K : (S_in == 1 ? 0 : S_in);  // see the forward: S == 1 has no contributing sample
+  const int run = FULL ? K : (S_in + L - 1) / L;
   const int j0 = sub * run;
   const float* zr = z + r * S_in;
   const float4* rr = reinterpret_cast<const float4*>(raw) + r * S_in;
-  float4* dr = reinterpret_cast<float4*>(d_raw) + r * S_in;
   const float d0 = rd[3 * r], d1 = rd[3 * r + 1], d2 = rd[3 * r + 2];
   const float nrm = __fsqrt_rn(__fadd_rn(__fadd_rn(__fmul_rn(d0, d0), __fmul_rn(d1, d1)), __fmul_rn(d2, d2)));
 
   float sd[K], zz[K], dist[K], sig[K], w[K], tr[K];
   float4 rv[K];
-  const int q0 = (lane >> 4) * S_in + j0;  // this run's first quad in the wave block
-  if constexpr (kLds) {
-    load_depths<K>(zr, j0, run, S_in, zz);
-    if (live) load_raw_lds<K>(sl, q0, j0, run, S_in, rv);
-    else load_run<K>(zr, rr, j0, run, S_in, zz, rv);  // the last ray again (not in this wave's block)
-  } else {
-    load_run<K>(zr, rr, j0, run, S_in, zz, rv);
-  }
-  const float znext = dppf<0x101>(zz[0]);
+  const int q0 = (lane / L) * S_in + j0;  // this run's first quad in the wave block
+  load_depths<K>(zr, j0, run, S_in, zz);
+  if (live) load_raw_lds<K>(sl, q0, j0, run, S_in, rv);
+  else load_run<K>(zr, rr, j0, run, S_in, zz, rv);  // the last ray again (not in this wave's block)
+  const float znext = next_lane<L>(zz[0]);
   double run_sum = 0.0;
 #pragma unroll
   for (int i = 0; i < K; ++i) {
@@ -319,7 +369,7 @@ __global__ __launch_bounds__(256) void volume_render_backward_kernel(
       if (j + 1 < S) run_sum += static_cast<double>(sd[i]);
     }
   }
-  double prefix = row_exclusive_scan(run_sum);
+  double prefix = ray_exclusive_scan<L>(run_sum);
   float dep = 0.f, ac = 0.f;
 #pragma unroll
   for (int i = 0; i < K; ++i) {
@@ -334,9 +384,9 @@ __global__ __launch_bounds__(256) void volume_render_backward_kernel(
       if (j + 1 < S) prefix += static_cast<double>(sd[i]);
     }
   }
-  // the ray's depth / acc in every lane of the row (lane 15's row sum, read back by DPP broadcast)
-  dep = __shfl(row_sum(dep), (threadIdx.x & 63) | 15);
-  ac = __shfl(row_sum(ac), (threadIdx.x & 63) | 15);
+  // the ray's depth / acc in every lane of the ray
+  dep = ray_sum_all<L>(dep);
+  ac = ray_sum_all<L>(ac);
   const float gr0 = g_rgb ? g_rgb[3 * r] : 0.f, gr1 = g_rgb ? g_rgb[3 * r + 1] : 0.f;
   const float gr2 = g_rgb ? g_rgb[3 * r + 2] : 0.f;
   float gdep = g_depth ? g_depth[r] : 0.f, gacc = g_acc ? g_acc[r] : 0.f;
@@ -364,7 +414,7 @@ __global__ __launch_bounds__(256) void volume_render_backward_kernel(
       gw_run += G[i] * w[i];
     }
   }
-  float suffix = row_exclusive_suffix(gw_run);  // sum of G_j w_j over later lanes' runs
+  float suffix = ray_exclusive_suffix<L>(gw_run);  // sum of G_j w_j over later lanes' runs
   float gnorm = 0.f;
 #pragma unroll
   for (int i = K - 1; i >= 0; --i) {
@@ -376,23 +426,15 @@ __global__ __launch_bounds__(256) void volume_render_backward_kernel(
       const float dsp = x > 20.0f ? 1.0f : cn::sigmoid_hw(x);
       float4 o = rv[i];
       o.w = dsd * (dist[i] * nrm) * dsp;
-      if (kLds) {
-        if (live) sl[pad4(q0 + i)] = o;
-      } else {
-        dr[j] = o;
-      }
+      if (live) sl[pad4(q0 + i)] = o;
       gnorm += dsd * sig[i] * dist[i];
     } else if (i < run && j < S_in) {
-      if (kLds) {
-        if (live) sl[pad4(q0 + i)] = make_float4(0.f, 0.f, 0.f, 0.f);
-      } else {
-        dr[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-      }
+      if (live) sl[pad4(q0 + i)] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
-  if constexpr (kLds) stage_rows_out<K>(reinterpret_cast<float4*>(d_raw) + rw0 * S_in, nq, sl, lane);
-  gnorm = row_sum(gnorm);
-  if (live && sub == 15 && d_rd) {
+  stage_rows_out<K>(reinterpret_cast<float4*>(d_raw) + rw0 * S_in, nq, sl, lane);
+  gnorm = ray_sum<L>(gnorm);
+  if (live && sub == (L == 16 ? 15 : 63) && d_rd) {
     const float inv = nrm > 0.f ? gnorm / nrm : 0.f;
     d_rd[3 * r] = inv * d0;
     d_rd[3 * r + 1] = inv * d1;
@@ -408,10 +450,8 @@ extern "C" int cn_volume_render_backward(const float* raw, const float* z, const
                                          const float* g_weights, const float* g_depth,
                                          float* d_raw, float* d_rd, cn_stream_t stream) {
   CN_CHECK_ARG(raw && z && rd && d_raw);
-  CN_CHECK_ARG(n_rays > 0 && n_samples > 0 && n_samples <= 16 * kMaxRun);
-  const unsigned grid = static_cast<unsigned>(cn::ceil_div(n_rays, kRowsPerBlock));
-  CN_VOLUME_DISPATCH(volume_render_backward_kernel, n_samples, dim3(grid), dim3(256), 0, cn::as_stream(stream), raw,
-                     z, rd, n_rays, static_cast<int>(n_samples), g_rgb, g_disp, g_acc, g_weights, g_depth, d_raw,
-                     d_rd);
+  CN_CHECK_ARG(n_rays > 0 && n_samples > 0 && n_samples <= kMaxSamples);
+  CN_VOLUME_DISPATCH(volume_render_backward_kernel, n_samples, n_rays, cn::as_stream(stream), raw, z, rd, n_rays,
+                     static_cast<int>(n_samples), g_rgb, g_disp, g_acc, g_weights, g_depth, d_raw, d_rd);
   return cn::launch_status();
 }

@@ -121,7 +121,7 @@ def test_gemm_tn_accumulates(dev, m, n, k, precision, det):
 # ---------------------------------------------------------------- element-wise stages
 
 
-@pytest.mark.parametrize("s", [2, 7, 24, 64, 129])
+@pytest.mark.parametrize("s", [2, 7, 24, 64, 128, 129, 192, 300, 512])
 def test_volume_render_backward(dev, s):
     from codenerf.nerf import volume_render
     o = O()

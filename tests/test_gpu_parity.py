@@ -159,7 +159,7 @@ def test_volume_render(dev):
         assert maxdiff(a[fin], ref[fin]) <= tol, k
 
 
-@pytest.mark.parametrize("s", [1, 7, 64, 65, 192, 300])
+@pytest.mark.parametrize("s", [1, 7, 64, 65, 128, 129, 192, 256, 300, 512])
 def test_volume_render_sizes(dev, s):
     from oracle import codenerf_oracle as O
     from codenerf import ops
@@ -170,9 +170,12 @@ def test_volume_render_sizes(dev, s):
     rd = torch.randn(n, 3)
     ref = O.volume_render(raw, z, rd)
     got = ops.volume_render(raw.to(dev), z.to(dev), rd.to(dev))
+    # the per-ray sums (rgb, depth ~2, acc) are S-term fp32 sums in a lane-tree order vs torch's
+    # sequential one: the bound grows with S past 256 (S = 512: 1e-5, ~40 ulp of a depth of 2)
+    tol = 5e-6 * max(1.0, s / 256)
     for a, b in zip(got, ref):
         fin = torch.isfinite(b)
-        assert maxdiff(a.cpu()[fin], b[fin]) <= 5e-6
+        assert maxdiff(a.cpu()[fin], b[fin]) <= tol
 
 
 # ---------------------------------------------------------------- MLP
