@@ -30,8 +30,9 @@
 // pipe never waits on a chunk boundary.  The stream is cyclic across tiles.
 //
 // sigma (fc_out row 0) is an fp32 dot product over layer_xyz2's outputs taken in the
-// xyz2 epilogue (64 FMAs per lane + a 4-group butterfly); fc_rgb is one 16-row block
-// (rows 0..2 real) over 64 k-steps, accumulated in 4 interleaved chains.
+// xyz2 epilogue (32 packed FMAs per lane + a 4-group butterfly); fc_rgb the same way for its
+// 3 rows (96 packed FMAs per lane, weights from the rgb chunk's ring slot) -- as one 16-row
+// MFMA block over 64 k-steps (CN_ABLATE_RGB_MFMA) 13 of its 16 rows were padding.
 #include <algorithm>
 
 #include "mlp_common.h"
@@ -56,6 +57,7 @@ constexpr int kPiecesPerWave = kChunkQuads / (64 * kWaves);   // 4 x 1 KiB per w
 // the stream: xyz1 2 | xyz2 8 | fc_out 8 | dir1 8 | dir1 view-dir 1 | dir2 8 | rgb 1
 constexpr int kCL2 = 2, kCL3 = 10, kCL4 = 18, kCDir = 26, kCL5 = 27, kCRgb = 35, kChunks = 36;
 constexpr int kStreamFloats = kChunks * kChunkQuads * 4;
+constexpr int kRgbValu = 64 * 64;  // float offset of fc_rgb's VALU-form rows inside the rgb chunk
 // constants after the stream: b_xyz1 | b_dir1 | b_dir2 | sigma weights (fc_out row 0 over
 // h2, [g][ob][r] = W_out[0][16 ob + 4 g + r])
 constexpr int kCB1 = 0, kCBD1 = 256, kCBD2 = 512, kCSig = 768, kConsts = 1024;
@@ -113,11 +115,16 @@ __global__ void pack_w16_kernel(Params P, float* __restrict__ packed) {
     } else {
       const int c = idx / (kChunkQuads * 4), rem = idx % (kChunkQuads * 4);
       if (c == kCRgb) {
-        // fc_rgb: 64 k-steps of block 0, [k-step quad][lane][k-step & 3]
+        // fc_rgb: 64 k-steps of block 0, [k-step quad][lane][k-step & 3] (the MFMA form,
+        // CN_ABLATE_RGB_MFMA), then at kRgbValu rows 0..2 over v2 for the VALU form,
+        // [row][g][ob][r] = W_rgb[row][16 ob + 4 g + r]
         if (rem < 64 * 64) {
           const int lane = (rem % 256) / 4, t = 4 * (rem / 256) + rem % 4;
           const int i = lane & 15, g = lane >> 4;
           if (i < 3) v = P.p[kWRgb][i * (kHidden + kCode) + col_acc(t, g)];
+        } else if (rem >= kRgbValu && rem < kRgbValu + 3 * 256) {
+          const int t = rem - kRgbValu, i = t >> 8, g = (t >> 6) & 3, ob = (t >> 2) & 15, r = t & 3;
+          v = P.p[kWRgb][i * (kHidden + kCode) + 16 * ob + 4 * g + r];
         }
       } else {
         const int s = rem / (kStepQuads * 4), q = (rem % (kStepQuads * 4)) / 256;
@@ -637,14 +644,16 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
                                      layer - kXyz2, mw};
     if (layer == kOut) {
       // sigma = fc_out row 0 . [h2, zs2] + b: the h2 part here, the code part from cn_code_bias
-      float sg = 0.0f;
+      // (two packed chains: 32 v_pk_fma_f32 instead of one 64-deep fmaf chain)
+      typedef float float2v __attribute__((ext_vector_type(2)));
+      float2v s0{0.0f, 0.0f}, s1{0.0f, 0.0f};
 #pragma unroll
       for (int ob = 0; ob < 16; ++ob) {
         const floatx4 w = *reinterpret_cast<const floatx4*>(clds + kCSig + 64 * fresh(s.g) + 4 * ob);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) sg = fmaf(w[r], s.act[ob][r], sg);
+        s0 = __builtin_elementwise_fma(float2v{w[0], w[1]}, float2v{s.act[ob][0], s.act[ob][1]}, s0);
+        s1 = __builtin_elementwise_fma(float2v{w[2], w[3]}, float2v{s.act[ob][2], s.act[ob][3]}, s1);
       }
-      s.sig = sg;
+      s.sig = (s0[0] + s0[1]) + (s1[0] + s1[1]);
     }
     if (layer == kXyz2) bias_code(s, a, crow_lds, kCbXyz2);
     else if (layer == kOut) bias_code(s, a, crow_lds, kCbFeat);
@@ -682,6 +691,59 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
     sg += __shfl_xor(sg, 32);
     s.sig = sg + bs;
   }
+#ifndef CN_ABLATE_RGB_MFMA
+  // fc_rgb on the VALU: 3 of the 16 MFMA rows were real, so the chunk's 64 MFMAs per wave (4 k
+  // pipe cycles per SIMD and tile) became 96 packed FMAs per lane over this lane group's 64 v2
+  // features, weights read from the rgb chunk's slot (it has landed: the chunk is current), then
+  // the 4-group butterfly as for sigma.  The chunk keeps its place in the stream, its barrier and
+  // the next tile's DMA.
+  {
+    typedef float float2v __attribute__((ext_vector_type(2)));
+    const floatx4* wr = reinterpret_cast<const floatx4*>(lds + (c & (kRing - 1)) * kChunkQuads) +
+                        (kRgbValu / 4 + 16 * fresh(s.g));
+    const float4* nslot = lds + ((c + 1) & (kRing - 1)) * kChunkQuads + s.lane;
+    float2v p[3][2];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) p[i][0] = p[i][1] = float2v{0.0f, 0.0f};
+    auto blocks = [&](auto b0) {
+      constexpr int B0 = decltype(b0)::value;
+#pragma unroll
+      for (int ob = B0; ob < B0 + 8; ++ob) {
+        const float2v x0{s.act[ob][0], s.act[ob][1]}, x1{s.act[ob][2], s.act[ob][3]};
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const floatx4 w = wr[64 * i + ob];
+          p[i][0] = __builtin_elementwise_fma(float2v{w[0], w[1]}, x0, p[i][0]);
+          p[i][1] = __builtin_elementwise_fma(float2v{w[2], w[3]}, x1, p[i][1]);
+        }
+      }
+    };
+    blocks(std::integral_constant<int, 0>{});
+    chunk_barrier();
+    dma_chunk(s, lds, c + 3);
+    st_v2.template blocks<0, 8>();
+    blocks(std::integral_constant<int, 8>{});
+    st_v2.template blocks<8, 8>();
+    read_a<0>(nslot, s.pre);
+    c += 1;
+    float rgb[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      float v = (p[i][0][0] + p[i][0][1]) + (p[i][1][0] + p[i][1][1]);
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      rgb[i] = v;
+    }
+    if (valid && s.g == 0) {
+      float4 o;
+      o.x = rgb[0] + s.acc[0][0];  // the code-bias terms (lane group 0's acc[0], set above)
+      o.y = rgb[1] + s.acc[0][1];
+      o.z = rgb[2] + s.acc[0][2];
+      o.w = s.sig;
+      reinterpret_cast<float4*>(a.raw)[row] = o;
+    }
+  }
+#else
   {
     const float4* slot = lds + (c & (kRing - 1)) * kChunkQuads + s.lane;
     const float4* nslot = lds + ((c + 1) & (kRing - 1)) * kChunkQuads + s.lane;
@@ -724,6 +786,7 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
     o.w = s.sig;
     reinterpret_cast<float4*>(a.raw)[row] = o;
   }
+#endif
 }
 
 #ifdef CN_ABLATE_WGTIME
