@@ -226,7 +226,8 @@ def run(args):
                 "launches_timed": len(field_ms), "flop_per_launch": flop_per_launch,
                 "samples_per_launch": samples_per_launch, "flop_per_sample": FLOP_PER_SAMPLE,
                 "mfma_passes": passes, "fp32_equiv_tflops": algo_tf,
-                "timing": "HIP events on the launching (current) stream around every field launch of the timed steps"}
+                "timing": "HIP events on the launching (current) stream around every field launch of the timed steps",
+                "traffic_source": traffic_source(prec)}
 
     # ---- headline: C2 in the reference's precision
     set_precision(args.precision)
@@ -359,6 +360,18 @@ def traffic_of(prec, samples):
     with open(tpath) as f:
         per_sample = json.load(f).get(prec, {}).get("hbm_bytes_per_sample")
     return None if per_sample is None else per_sample * samples
+
+
+def traffic_source(prec):
+    """Where `traffic` comes from: it is NOT a counter read in this run (PMC passes cannot share a
+    run with the timing), but the per-sample HBM bytes of the kernel's own PMC passes, scaled."""
+    tpath = os.path.join(ROOT, "profiles", "field_kernel_traffic.json")
+    if not os.path.exists(tpath):
+        return None
+    with open(tpath) as f:
+        rec = json.load(f).get(prec, {})
+    return (f"rocprofv3 FETCH_SIZE / WRITE_SIZE passes ({rec.get('measured_round', '?')}, {rec.get('raw', '?')}), "
+            "per-sample bytes x this launch's samples; profiles/field_kernel_traffic.json")
 
 
 def eval_bench(dev, rs, emb, models, iters, precision, graph=False):

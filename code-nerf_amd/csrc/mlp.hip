@@ -345,7 +345,8 @@ __device__ __forceinline__ void finish_layer(State& s) {
 #pragma unroll
     for (int ob = 0; ob < 8; ++ob)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) s.act[ob][r] = fmaxf(s.acc[ob][r], 0.0f);
+      for (int r = 0; r < 16; ++r)  // ReLU as v_max_i32 on the bits (fmaxf: canonicalize + max)
+        s.act[ob][r] = __int_as_float(max(__float_as_int(s.acc[ob][r]), 0));
   }
 }
 

@@ -470,12 +470,18 @@ __device__ __forceinline__ unsigned mask_soff(const State& s, int ml) {
 // 4 ob + r of word ob >> 3 (ob & 7 there).  The words are built by shifting the accumulator left
 // one bit per feature, highest first: a constant 1 << n per bit would be a VOP3 literal, which
 // gfx9 encodings lack, so the compiler kept all 32 of them in VGPRs across the tile loop.
+// The ReLU is a signed-integer max on the bits (v_max_i32; -0 and negatives -> +0): fmaxf on an
+// MFMA result came out as two v_max_f32 per value (a canonicalize, then the max).
 template <bool MASKS>
 __device__ __forceinline__ uint2v relu_act(State& s) {
 #pragma unroll
   for (int ob = 0; ob < 16; ++ob)
 #pragma unroll
+#ifdef CN_ABLATE_RELU_FMAX
     for (int r = 0; r < 4; ++r) s.act[ob][r] = fmaxf(s.acc[ob][r], 0.0f);
+#else
+    for (int r = 0; r < 4; ++r) s.act[ob][r] = __int_as_float(max(__float_as_int(s.acc[ob][r]), 0));
+#endif
   unsigned w[2] = {0u, 0u};
   if constexpr (MASKS) {
 #pragma unroll
