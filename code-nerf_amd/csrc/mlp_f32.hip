@@ -652,13 +652,33 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
       // sigma = fc_out row 0 . [h2, zs2] + b: the h2 part here, the code part from cn_code_bias
       // (two packed chains: 32 v_pk_fma_f32 instead of one 64-deep fmaf chain)
       typedef float float2v __attribute__((ext_vector_type(2)));
+      // the weights in two batches of 8 LDS reads issued together (one wait per batch; read one at
+      // a time, each FMA pair waited on its own read while both waves of the SIMD sat here)
       float2v s0{0.0f, 0.0f}, s1{0.0f, 0.0f};
+#ifdef CN_ABLATE_SIGMA_SERIAL
 #pragma unroll
       for (int ob = 0; ob < 16; ++ob) {
         const floatx4 w = *reinterpret_cast<const floatx4*>(clds + kCSig + 64 * fresh(s.g) + 4 * ob);
         s0 = __builtin_elementwise_fma(float2v{w[0], w[1]}, float2v{s.act[ob][0], s.act[ob][1]}, s0);
         s1 = __builtin_elementwise_fma(float2v{w[2], w[3]}, float2v{s.act[ob][2], s.act[ob][3]}, s1);
       }
+#else
+      const floatx4* wsig = reinterpret_cast<const floatx4*>(clds + kCSig) + 16 * fresh(s.g);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        floatx4 w[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w[k] = wsig[8 * h + k];
+        __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int ob = 8 * h + k;
+          s0 = __builtin_elementwise_fma(float2v{w[k][0], w[k][1]}, float2v{s.act[ob][0], s.act[ob][1]}, s0);
+          s1 = __builtin_elementwise_fma(float2v{w[k][2], w[k][3]}, float2v{s.act[ob][2], s.act[ob][3]}, s1);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
+      }
+#endif
       s.sig = (s0[0] + s0[1]) + (s1[0] + s1[1]);
     }
     if (layer == kXyz2) bias_code(s, a, crow_lds, kCbXyz2);
