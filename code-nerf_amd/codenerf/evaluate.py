@@ -287,13 +287,10 @@ def eval_loop(rank: int, cfg, device=None, resident: bool = True, verbose: bool 
     (for the code-table size), models / optimiser / checkpoint, the samplers and embedders from the
     first validation batch, then ``experiment.iterations // val_batch_size`` validations -> their
     results (validate's dicts; rank 0 holds loss / psnr / pose_error)."""
-    import numpy as np
     from .checkpoint import load_checkpoint
     from .datasets import prepare_dataloader
-    from .train import log_losses, prepare_models, prepare_optimizer
-    seed = (rank + 1) + int(cfg.experiment.randomseed)
-    np.random.seed(seed)
-    torch.manual_seed(seed)
+    from .train import log_losses, prepare_models, prepare_optimizer, seed_rank
+    seed_rank(rank, cfg)
     device = torch.device("cuda", rank) if device is None else torch.device(device)
     torch.cuda.set_device(device)
     dataloader, _ = prepare_dataloader("val", cfg, device if resident else None)
@@ -356,3 +353,29 @@ def validate(cfg, val_data: Dict[str, torch.Tensor], models, samplers, embedders
         out["psnr"] = mse2psnr(out["loss"])
         out["pose_error"] = float(ops.pose_error(gt_pose.reshape(1, 4, 4), cam_pose)[1][0])
     return out
+
+
+# ---------------------------------------------------------------- process launch (eval.py:208-242)
+
+def _eval_rank(rank: int, cfg) -> None:
+    eval_loop(rank, cfg)
+
+
+def main(cfg, backend: Optional[str] = None, port: int = 29500) -> None:
+    """eval.py:222-242: ``eval_loop`` on ``cfg.gpus`` ranks (one spawned process per GPU, RCCL) or on
+    one (codenerf.train.launch)."""
+    from .train import launch
+    launch(_eval_rank, cfg, backend=backend, port=port)
+
+
+if __name__ == "__main__":
+    import argparse
+    from .config import load_config
+    parser = argparse.ArgumentParser()
+    parser.add_argument("-c", "--config", type=str, required=True, help="Path to (.yml) config file.")
+    parser.add_argument("--load-checkpoint", type=str, required=True, help="Path to load saved checkpoint from.")
+    parser.add_argument("-g", "--gpus", default=1, type=int, help="Number of gpus per node")
+    parser.add_argument("--distributed", action="store_true", dest="is_distributed",
+                        help="Run the models in DataDistributedParallel")
+    a = parser.parse_args()
+    main(load_config(a.config, gpus=a.gpus, is_distributed=a.is_distributed, load_checkpoint=a.load_checkpoint))

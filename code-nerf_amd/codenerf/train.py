@@ -154,16 +154,21 @@ def psnr_tensor(mse: torch.Tensor) -> torch.Tensor:
 
 
 def train_iteration(cfg, train_data: Dict[str, torch.Tensor], models, optimizer, scheduler, samplers,
-                    embedders, on_chunk=None) -> List[Dict[str, object]]:
+                    embedders, on_chunk=None, start_chunk: int = 0, after_draw=None) -> List[Dict[str, object]]:
     """train.py:64-114 for one loaded batch (``color`` (B,H,W,C), ``pose`` (B,4,4), ``object_id``
     (B,) on the device) -> the per-chunk logs.  ``on_chunk(j, num_batches, logs)``: called after
-    chunk j's optimiser step (train.py:116-142's logging / checkpoint / validation slot)."""
+    chunk j's optimiser step (train.py:116-142's logging / checkpoint / validation slot).
+    ``start_chunk`` / ``after_draw()``: a mid-iteration resume -- the batch's ray draw is made as
+    usual, ``after_draw`` then restores the generators saved after chunk ``start_chunk - 1`` and
+    the chunks before ``start_chunk`` are skipped."""
     ray_sampler, point_sampler = samplers
     is_distributed = bool(getattr(cfg, "is_distributed", False))
     for m in models.values():
         m.train()
     # sample + the per-image target gather (train.py:76-80) in one cn_pose_rays launch
     ro_batch, rd_batch, select_inds, target = ray_sampler.sample_pixels(train_data["pose"], train_data["color"])
+    if after_draw is not None:
+        after_draw()
     n_rays = ray_sampler.sample_size
     color = train_data["color"]
     object_ids = train_data["object_id"][:, None].expand(-1, n_rays).reshape(-1)
@@ -180,6 +185,8 @@ def train_iteration(cfg, train_data: Dict[str, torch.Tensor], models, optimizer,
     batches = list(zip(get_minibatches(ro_batch, chunk), get_minibatches(rd_batch, chunk),
                        get_minibatches(object_ids, chunk), get_minibatches(target, chunk)))
     for j, (ro, rd, ids, tp) in enumerate(batches):
+        if j < start_chunk:
+            continue
         ids._cn_host_ids = host_ids[j * chunk:j * chunk + ids.shape[0]]
         logs.append(train_minibatch(models, optimizer, scheduler, point_sampler, embedders, ro, rd, ids, tp,
                                     cfg.experiment.regularizer_lambda, is_distributed))
@@ -216,8 +223,76 @@ def _main(cfg) -> bool:
     return (not getattr(cfg, "is_distributed", False)) or dist.get_rank() == 0
 
 
+def seed_rank(rank: int, cfg) -> int:
+    """train.py:28-31 / eval.py:44-47: numpy and torch seeded with ``(rank + 1) + randomseed``, so
+    every process samples different rays -> the seed."""
+    seed = (rank + 1) + int(cfg.experiment.randomseed)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    return seed
+
+
+def next_train_batch(cfg, train_loader, iteration: int):
+    """train.py:67-70: ``set_epoch(iteration)`` when distributed, then the first batch of a fresh
+    iterator over the train loader."""
+    if getattr(cfg, "is_distributed", False):
+        train_loader.sampler.set_epoch(iteration)
+    return next(iter(train_loader))
+
+
+class LogBook:
+    """The driver's per-chunk logs without holding the run: entries arrive as device scalars (no
+    read-back per chunk), are read back together when printed or every ``flush_every`` chunks (one
+    copy for the lot), and only the last ``keep`` host-float entries are retained (None: all)."""
+
+    def __init__(self, keep: Optional[int] = 1000, flush_every: int = 64):
+        from collections import deque
+        self.keep, self.flush_every = keep, flush_every
+        self.pending: List[Dict[str, object]] = []
+        self.entries = deque(maxlen=keep)
+        self.count = 0
+
+    def add(self, lg: Dict[str, object]) -> None:
+        self.pending.append(lg)
+        self.count += 1
+        if len(self.pending) >= self.flush_every:
+            self.flush()
+
+    def flush(self) -> None:
+        if not self.pending:
+            return
+        keys = [list(lg) for lg in self.pending]
+        vals = [v for lg in self.pending for v in lg.values()]
+        dev = [v.detach().reshape(()).double() for v in vals if torch.is_tensor(v)]
+        host = iter(torch.stack(dev).cpu().tolist()) if dev else iter(())
+        flat = [next(host) if torch.is_tensor(v) else float(v) for v in vals]
+        o = 0
+        for ks in keys:
+            self.entries.append(dict(zip(ks, flat[o:o + len(ks)])))
+            o += len(ks)
+        self.pending = []
+
+    def last(self) -> Dict[str, float]:
+        self.flush()
+        return self.entries[-1]
+
+    def as_list(self) -> List[Dict[str, float]]:
+        self.flush()
+        return list(self.entries)
+
+
+def _validation_summary(res: Dict[str, object], iteration: int) -> Dict[str, object]:
+    """What the driver keeps of a validation (host scalars): the reference logs loss / psnr and writes
+    the images to TensorBoard, keeping nothing."""
+    out = {"iteration": iteration, "pose": res.get("pose")}
+    for k in ("loss", "psnr", "pose_error"):
+        if k in res:
+            out[k] = float(res[k])
+    return out
+
+
 def train(rank: int, cfg, device=None, resident: bool = True, stop_after: Optional[int] = None,
-          verbose: bool = True) -> Dict[str, object]:
+          verbose: bool = True, keep_logs: Optional[int] = 1000, keep_validation: bool = False) -> Dict[str, object]:
     """train.py:19-142 on the gfx950 path, with the reference's seeds, data order and cadence.
 
     * seed ``(rank + 1) + experiment.randomseed`` for numpy and torch (train.py:29-31);
@@ -227,24 +302,34 @@ def train(rank: int, cfg, device=None, resident: bool = True, stop_after: Option
       first batch (train.py:51-58);
     * per iteration: ``set_epoch`` when distributed (train.py:67-68), one batch from a fresh
       iterator (train.py:70), ``train_iteration``; after each chunk step i = iteration *
-      num_batches + j: the log line every ``print_every`` (rank 0), a checkpoint every
-      ``save_every`` and at the last iteration (rank 0, ``checkpoint{i:5d}.ckpt``), ``validate``
-      every ``validate_every`` (every rank; eval.py:82-205).
+      num_batches + j: the log line every ``print_every`` (rank 0), ``validate`` every
+      ``validate_every`` (every rank; eval.py:82-205), a checkpoint every ``save_every`` and at the
+      last iteration (rank 0, ``checkpoint{i:5d}.ckpt``).
     ``stop_after``: leave the loop after this many iterations (an interrupted run, for resume tests).
-    Checkpoints also carry the RNG streams, the scheduler and the next iteration (extra keys the
-    reference's loader ignores), so a resume continues the uninterrupted run exactly; a reference
-    checkpoint resumes with the reference's semantics (``iter`` again, fresh RNG and scheduler).
-    Returns {"logs": per-chunk losses (floats), "checkpoints": paths, "validation": results,
-    "models", "optimizer", "scheduler"}."""
+
+    Exact resume: a checkpoint carries the scheduler, a cursor (iteration, next chunk) and EVERY
+    rank's generator states (gathered at the save): the states after the save step -- taken after
+    that step's validation, so the file is written once the validation has run (the reference
+    writes it just before) -- and the states at the start of the iteration.  A resume from a save
+    after chunk j < last replays the iteration's batch and ray draw from the latter, restores the
+    former and continues at chunk j + 1; one at an iteration's end continues with the next.  Each
+    rank restores its own states.  The continuation is bit-identical to the uninterrupted run
+    where the step itself is deterministic: one object per chunk (every runnable config:
+    chunksize <= num_random_rays), see DESIGN.md section 4.  A reference checkpoint resumes with
+    the reference's semantics (``iter`` again, fresh RNG and scheduler).
+
+    Memory: the per-chunk logs are read back in batches and only the last ``keep_logs`` kept
+    (LogBook); a validation keeps its host scalars (``keep_validation``: also its history, codes and
+    image).  Returns {"logs": host-float dicts (the last ``keep_logs``), "num_logs", "checkpoints":
+    paths, "validation": summaries, "models", "optimizer", "scheduler"}."""
     import time
-    import numpy as np
     from . import checkpoint as C
     from .datasets import prepare_dataloader
     from .evaluate import validate, validation_batch
-    seed = (rank + 1) + int(cfg.experiment.randomseed)
-    np.random.seed(seed)
-    torch.manual_seed(seed)
+    seed_rank(rank, cfg)
     main = _main(cfg)
+    is_distributed = bool(getattr(cfg, "is_distributed", False))
+    world = dist.get_world_size() if is_distributed else 1
     logdir_path = prepare_experiment(cfg) if main else None
     device = torch.device("cuda", rank) if device is None else torch.device(device)
     torch.cuda.set_device(device)
@@ -258,38 +343,112 @@ def train(rank: int, cfg, device=None, resident: bool = True, stop_after: Option
     (height, width), intrinsic = first["color"][0].shape[:2], first["intrinsic"][0]
     samplers = nerf.prepare_samplers(cfg, height, width, intrinsic.cpu(), torch.float32, device)
     embedders = nerf.prepare_embedders(cfg, torch.float32, device)
-    start_iter = C.resume_state(extras, scheduler, start_iter)   # after the first-batch draw, as saved
+    ray_sampler = samplers[0]
+    # after the first-batch draw, as saved
+    point = C.resume_point(extras, scheduler, start_iter, rank=dist.get_rank() if is_distributed else 0,
+                           world_size=world)
+    if point.chunk == 0 and point.rng is not None:
+        C.set_rng_state(point.rng, device, ray_sampler)
+    book = LogBook(keep_logs)
     out = {"logs": [], "checkpoints": [], "validation": [], "models": models, "optimizer": optimizer,
            "scheduler": scheduler}
     total = int(cfg.experiment.iterations) // int(cfg.dataset.train_batch_size)
     e = cfg.experiment
-    for iteration in range(start_iter, total):
-        if stop_after is not None and iteration - start_iter >= stop_after:
+    for iteration in range(point.iteration, total):
+        if stop_after is not None and iteration - point.iteration >= stop_after:
             break
-        if getattr(cfg, "is_distributed", False):
-            train_loader.sampler.set_epoch(iteration)
-        train_data = next(iter(train_loader))
+        resume_chunk = point.chunk if iteration == point.iteration else 0
+        if resume_chunk:
+            C.set_rng_state(point.iter_rng, device, ray_sampler)
+        iter_rng = C.rng_state(device, ray_sampler)     # replayed by a resume from inside this iteration
+        train_data = next_train_batch(cfg, train_loader, iteration)
         train_data = {k: (v.to(device, non_blocking=True) if torch.is_tensor(v) else v) for k, v in train_data.items()}
         then = time.time()
 
         def on_chunk(j, num_batches, lg):
             i = iteration * num_batches + j
-            out["logs"].append(lg)                 # device scalars: read when printed / returned
-            if main and i > 0:
-                if i % e.print_every == 0 and verbose:
-                    print(log_losses("train", i, time.time() - then, {k: float(v) for k, v in lg.items()},
-                                     scheduler.get_last_lr()[0]))
-                if i % e.save_every == 0 or i == e.iterations - 1:
+            book.add(lg)                           # device scalars: read in batches (LogBook)
+            if main and i > 0 and i % e.print_every == 0 and verbose:
+                print(log_losses("train", i, time.time() - then, book.last(), scheduler.get_last_lr()[0]))
+            if i > 0 and i % e.validate_every == 0:
+                val_data = validation_batch(cfg, val_loader, i)
+                res = validate(cfg, val_data, models, samplers, embedders, device,
+                               log_every=e.val_print_every if verbose else None)
+                out["validation"].append(res if keep_validation else _validation_summary(res, i))
+            if i > 0 and (i % e.save_every == 0 or i == e.iterations - 1):
+                # every rank's generators after this step (and its validation), and at the iteration's start
+                states = C.gather_rng_states({"now": C.rng_state(device, ray_sampler), "iter_start": iter_rng})
+                if main:
+                    cursor = (iteration + 1, 0) if j == num_batches - 1 else (iteration, j + 1)
                     path = logdir_path / f"checkpoint{i:5d}.ckpt"
-                    C.save_checkpoint(path, iteration, models, optimizer, scheduler=scheduler,
-                                      next_iter=iteration + 1 if j == num_batches - 1 else None)
+                    C.save_checkpoint(path, iteration, models, optimizer, scheduler=scheduler, cursor=cursor,
+                                      rng_ranks=states)
                     out["checkpoints"].append(str(path))
                     if verbose:
                         print("================== Saved Checkpoint =================")
-            if i > 0 and i % e.validate_every == 0:
-                val_data = validation_batch(cfg, val_loader, i)
-                out["validation"].append(validate(cfg, val_data, models, samplers, embedders, device,
-                                                  log_every=e.val_print_every if verbose else None))
-        train_iteration(cfg, train_data, models, optimizer, scheduler, samplers, embedders, on_chunk=on_chunk)
-    out["logs"] = [{k: float(v) for k, v in lg.items()} for lg in out["logs"]]
+
+        after_draw = (lambda: C.set_rng_state(point.rng, device, ray_sampler)) if resume_chunk else None
+        train_iteration(cfg, train_data, models, optimizer, scheduler, samplers, embedders, on_chunk=on_chunk,
+                        start_chunk=resume_chunk, after_draw=after_draw)
+    out["logs"] = book.as_list()
+    out["num_logs"] = book.count
     return out
+
+
+# ---------------------------------------------------------------- process launch (train.py:145-179)
+
+def init_process(rank: int, fn, cfg, backend: str = "gloo", port: int = 29500, init_method: Optional[str] = None):
+    """train.py:145-156 / eval.py:208-219: rendezvous at 127.0.0.1:``port`` (the reference's 29500),
+    ``init_process_group(backend, rank, world_size=cfg.gpus)`` -- on "nccl" (RCCL) bound to
+    ``cuda:rank`` -- then ``fn(rank, cfg)`` and ``destroy_process_group``.  This runs in a freshly
+    spawned process: nothing has touched the GPU before it."""
+    import os
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    kw = {}
+    if backend == "nccl":
+        torch.cuda.set_device(rank)
+        kw["device_id"] = torch.device("cuda", rank)
+    if init_method is not None:
+        kw["init_method"] = init_method
+    dist.init_process_group(backend, rank=rank, world_size=int(cfg.gpus), **kw)
+    try:
+        fn(rank, cfg)
+    finally:
+        dist.destroy_process_group()
+
+
+def launch(fn, cfg, backend: Optional[str] = None, port: int = 29500, init_method: Optional[str] = None) -> None:
+    """train.py:159-179's dispatch: with ``cfg.is_distributed`` and ``cfg.gpus`` > 1, one process per
+    rank (``start_method="spawn"``: started before this process makes any GPU call, so each child
+    initialises HIP itself) running ``init_process`` over ``backend`` (default "nccl", i.e. RCCL);
+    otherwise ``fn(0, cfg)`` in this process."""
+    gpus = int(getattr(cfg, "gpus", 1))
+    if gpus > 1 and getattr(cfg, "is_distributed", False):
+        import torch.multiprocessing as mp
+        mp.start_processes(init_process, args=(fn, cfg, backend or "nccl", port, init_method), nprocs=gpus,
+                           join=True, start_method="spawn")
+    else:
+        fn(0, cfg)
+
+
+def _train_rank(rank: int, cfg) -> None:
+    train(rank, cfg)
+
+
+def main(cfg, backend: Optional[str] = None, port: int = 29500) -> None:
+    """train.py:159-179: ``train`` on ``cfg.gpus`` ranks (one process per GPU over RCCL) or on one."""
+    launch(_train_rank, cfg, backend=backend, port=port)
+
+
+if __name__ == "__main__":
+    import argparse
+    from .config import load_config
+    parser = argparse.ArgumentParser()
+    parser.add_argument("-c", "--config", type=str, required=True, help="Path to (.yml) config file.")
+    parser.add_argument("--load-checkpoint", type=str, default="", help="Path to load saved checkpoint from.")
+    parser.add_argument("-g", "--gpus", default=1, type=int, help="Number of gpus per node")
+    parser.add_argument("--distributed", action="store_true", dest="is_distributed",
+                        help="Run the models in DataDistributedParallel")
+    a = parser.parse_args()
+    main(load_config(a.config, gpus=a.gpus, is_distributed=a.is_distributed, load_checkpoint=a.load_checkpoint))

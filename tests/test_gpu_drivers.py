@@ -73,6 +73,39 @@ def test_train_resume_is_exact(tree, tmp_path):
     assert full["scheduler"].last_epoch == resumed["scheduler"].last_epoch == 5
 
 
+def test_train_resume_mid_iteration_with_validation(tree, tmp_path):
+    """A periodic save inside an iteration (2 chunks per iteration, the save after chunk 0) that
+    coincides with a validation step, and one at an iteration's end: resuming from
+    either continues the uninterrupted run bit for bit -- the cursor replays the iteration's ray
+    draw, the generators are those after the save step's validation."""
+    from codenerf.train import train
+    dev = torch.device("cuda", 0)
+    kw = dict(iterations=4, save_every=4, validate_every=4, val_iterations=2)
+
+    def cfg(name, **extra):
+        c = _cfg(tree, str(tmp_path / name), **kw)
+        c.nerf.train.chunksize = 64                            # 128 rays per image -> 2 chunks
+        return c | extra
+
+    full = train(0, cfg("full"), device=dev, verbose=False)
+    assert full["num_logs"] == 8 and len(full["validation"]) == 1
+    assert set(full["validation"][0]) >= {"iteration", "loss", "psnr", "pose_error"}
+    names = [os.path.basename(p) for p in full["checkpoints"]]
+    assert names == ["checkpoint    3.ckpt", "checkpoint    4.ckpt"], names   # i == iterations-1, i % 4
+    ck3 = torch.load(full["checkpoints"][0], weights_only=True)
+    ck4 = torch.load(full["checkpoints"][1], weights_only=True)
+    assert ck3["cn_cursor"].tolist() == [2, 0] and ck3["cn_next_iter"] == 2
+    assert ck4["cn_cursor"].tolist() == [2, 1] and "cn_next_iter" not in ck4 and ck4["iter"] == 2
+    a = _params(full)
+    for path, first in ((full["checkpoints"][1], 5), (full["checkpoints"][0], 4)):
+        res = train(0, cfg("res" + str(first), load_checkpoint=path), device=dev, verbose=False)
+        assert res["logs"] == full["logs"][first:], first
+        b = _params(res)
+        for k in a:
+            assert torch.equal(a[k], b[k]), (first, k)
+        assert res["scheduler"].last_epoch == full["scheduler"].last_epoch == 8
+
+
 def test_train_checkpoint_cadence_and_reference_format(tree, tmp_path):
     """save_every / the last iteration (train.py:129) write checkpoint{i:5d}.ckpt with the reference's
     keys; one holding ONLY those keys (as the reference writes it) loads and resumes the reference's
