@@ -84,6 +84,9 @@ def parse_args(argv=None):
                     help="C5: time this many test-time-optimisation iterations (0 = skip)")
     ap.add_argument("--train-iters", type=int, default=8,
                     help="C3 training: time this many train.py iterations (4 x 4096 rays each; 0 = skip)")
+    ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
+                    help="process-group backend for N > 1 (nccl = RCCL; gloo: test harness only)")
+    ap.add_argument("--quiet", action="store_true", help="return the result without printing it (tests)")
     return ap.parse_args(argv)
 
 
@@ -129,8 +132,11 @@ def run(args):
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
-        rccl_world = dist.get_world_size()
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+            rccl_world = dist.get_world_size()
+        else:       # gloo: the multi-rank test harness (ranks sharing one GPU; tests/test_gpu_multirank.py)
+            dist.init_process_group("gloo", rank=rank, world_size=world)
     dev = torch.device("cuda", local)
 
     import codenerf
@@ -178,9 +184,19 @@ def run(args):
             rd = rd.reshape(nv, -1, 3)[:, start_:start_ + per_[rank]].reshape(-1, 3)
             r = ro.shape[0]
             hook = {} if record else None
-            out = render_rays(ro, rd, zs.expand(r, -1), zt.expand(r, -1), ps_, emb, models[0], models[1],
-                              chunk_rows=chunk_, coarse_only=coarse_only, events=hook)
-            rgb = out["rgb_coarse" if coarse_only else "rgb_fine"]
+            key = "rgb_coarse" if coarse_only else "rgb_fine"
+            if per_[rank] % chunk_ == 0:
+                # the views' slices concatenated: every chunk lies inside one view, so one pass has
+                # parallel_image_render's per-view chunking (the Q1 view-direction map) exactly
+                rgb = render_rays(ro, rd, zs.expand(r, -1), zt.expand(r, -1), ps_, emb, models[0], models[1],
+                                  chunk_rows=chunk_, coarse_only=coarse_only, events=hook)[key]
+            else:
+                # a ragged last chunk per view (e.g. 3 ranks: 5461 rays per view): chunking restarts at
+                # every view as parallel_image_render's does, so one pass per view
+                p_ = per_[rank]
+                rgb = torch.cat([render_rays(ro[v * p_:(v + 1) * p_], rd[v * p_:(v + 1) * p_], zs.expand(p_, -1),
+                                             zt.expand(p_, -1), ps_, emb, models[0], models[1], chunk_rows=chunk_,
+                                             coarse_only=coarse_only, events=hook)[key] for v in range(nv)])
             if world > 1:
                 rgb = gather_views(rgb, per_, rank, nv)          # rank 0: (views, H*W, 3)
                 if rgb is not None:
@@ -207,7 +223,7 @@ def run(args):
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         if world > 1:
-            t = torch.tensor([dt], device=dev, dtype=torch.float64)
+            t = torch.tensor([dt], device=dev if args.backend == "nccl" else "cpu", dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
         ms = [a.elapsed_time(b) for a, b in timing["pending"]]
@@ -319,10 +335,11 @@ def run(args):
             if im is not None:
                 mse = float(((im[:n_img_rays].float().cpu() - ref_img) ** 2).mean())
                 result.setdefault("psnr_vs_ref", {})[prec] = mse2psnr(mse)
-    if rank == 0:
+    if rank == 0 and not args.quiet:
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return result if rank == 0 else None
 
 
 def multi_rank_check(img, rs, pose1, per, zs, zt, ps, emb, models):

@@ -544,8 +544,12 @@ def gen_c3train(nerf, model_mod, ev):
     coarse, fine, embedding at embedding_lr), LambdaLR -- on ONE 4096-ray chunk made of two views of
     two objects of a 2458-object table (2048 rays each, ray_sampler.sample), perturbed samples
     (uniforms recorded).  Stored: the inputs the test cannot regenerate (rays, ids, targets, draws),
-    the losses, every parameter's gradient norm + a few full gradients, the touched code-table rows'
-    gradients, and the post-step values of the same tensors and rows.  Weights: codenerf.synthetic
+    the losses, and element-wise evidence for every parameter: nerf_fine's gradients and post-step
+    values in full; for nerf_coarse (size: the full set would double the fixture) the full five
+    tensors of round 3 plus, for EVERY tensor, C3_PROJ seeded Gaussian projections of its gradient
+    and of its post-step change (proj_seed: the test regenerates the same directions) -- a
+    projection sees any error pattern (sign, swapped block) of a size a norm would miss; the
+    touched code-table rows' gradients and post-step values.  Weights: codenerf.synthetic
     (seeds 0 / 1), table: synthetic.latent_codes(40 / 41, 2458)."""
     util = importlib.import_module("view_synthesis.utils.util")
     K = synthetic.srn_intrinsics(128)
@@ -604,7 +608,29 @@ def gen_c3train(nerf, model_mod, ev):
     for k in C3_FULL:
         out["g_" + k] = grads[k]
         out["p_" + k] = after[k]
+    for idx, k in enumerate(sorted(grads)):
+        if k.startswith("embedding."):
+            continue
+        if k.startswith("nerf_fine."):
+            out["g_" + k] = grads[k]
+            out["p_" + k] = after[k]
+        r = proj_directions(idx, grads[k].shape)
+        out["gproj_" + k] = proj(r, grads[k])
+        out["pproj_" + k] = proj(r, after[k] - before[k])
     save("train_c3.npz", **out)
+
+
+C3_PROJ = 16
+
+
+def proj_directions(idx: int, shape) -> torch.Tensor:
+    """C3_PROJ seeded N(0, 1) directions for parameter ``idx`` (sorted-name order), float32 CPU."""
+    return torch.randn((C3_PROJ,) + tuple(shape), generator=torch.Generator().manual_seed(7000 + idx))
+
+
+def proj(r: torch.Tensor, t: torch.Tensor) -> np.ndarray:
+    """<r_k, t> for every direction, accumulated in float64."""
+    return (r.double() * t.detach().double()[None]).reshape(r.shape[0], -1).sum(1).numpy()
 
 
 ROUND2 = {"trained": gen_trained, "chairs": gen_chairs, "lego": gen_lego, "c5": gen_c5, "se3": gen_se3,

@@ -11,6 +11,7 @@ import numpy as np
 import pytest
 import torch
 
+from conftest import margin
 from test_gpu_parity import dev, embedders, load, maxdiff  # noqa: F401
 
 pytestmark = pytest.mark.gpu
@@ -22,6 +23,9 @@ RAW_RTOL = 1e-5
 # the t3 net (tools/x3w_err.py), so their raw-output bound is 1.5e-5 (rendered outputs keep 1e-4)
 RAW_RTOL_X3 = 1.5e-5
 PRECISIONS = ["f32", "f32_v1", "bf16x3", "bf16x3_w16"]
+# C5 at-size gradient bound (max |g - g_ref| over the tensor's largest |g_ref|; d theta / phi / rho
+# relative to max(1e-2, |g_ref|)); the achieved values are recorded (conftest.margin)
+C5_GRAD_RTOL = {"f32": 2e-3, "bf16x3": 2e-3}
 
 
 def model_from(dev, params, precision):
@@ -77,8 +81,8 @@ def test_trained_render_c2_c3(dev, precision, case):
     d = {k: maxdiff(o[a], g[f"{case}_{k}"]) for a, k in [("rgb_coarse", "rgb_c"), ("depth_coarse", "depth_c"),
                                                         ("acc_coarse", "acc_c"), ("rgb_fine", "rgb_f"),
                                                         ("depth_fine", "depth_f"), ("acc_fine", "acc_f")]}
-    print(f"{precision} {case}: max |d| vs reference {d}")
-    assert max(d.values()) <= TOL_RENDER, d
+    for k, v in d.items():
+        margin(f"render_trained_{case}[{precision}]", k, v, TOL_RENDER)
 
 
 # ---------------------------------------------------------------- C4: chairs, rank slices
@@ -110,11 +114,12 @@ def test_chairs_c4_rank_slices(dev, precision, n_ranks):
             outs.append(render_rays(ro[sl], rd[sl], g["z_s"].expand(n, -1)[sl], g["z_t"].expand(n, -1)[sl], ps,
                                     embedders(dev), mc, mf, chunk_rows=4096))
     rgb = torch.cat([o["rgb_fine"] for o in outs])
-    assert maxdiff(rgb, g[f"n{n_ranks}_rgb"]) <= TOL_RENDER
+    tag = f"chairs_c4_n{n_ranks}[{precision}]"
+    margin(tag, "rgb_f", maxdiff(rgb, g[f"n{n_ranks}_rgb"]), TOL_RENDER)
     if n_ranks == 1:
-        assert maxdiff(outs[0]["depth_fine"], g["depth_f"]) <= TOL_RENDER
-        assert maxdiff(outs[0]["acc_fine"], g["acc_f"]) <= TOL_RENDER
-        assert maxdiff(outs[0]["rgb_coarse"], g["rgb_c"]) <= TOL_RENDER
+        margin(tag, "depth_f", maxdiff(outs[0]["depth_fine"], g["depth_f"]), TOL_RENDER)
+        margin(tag, "acc_f", maxdiff(outs[0]["acc_fine"], g["acc_f"]), TOL_RENDER)
+        margin(tag, "rgb_c", maxdiff(outs[0]["rgb_coarse"], g["rgb_c"]), TOL_RENDER)
         assert outs[0]["z_fine"].shape == (n, 160)
 
 
@@ -170,7 +175,7 @@ def test_lego_c1_leaf_ops(dev, tag):
         o = render_rays(ro, rd, zs, zt, ps, emb, mc, mf, chunk_rows=8192, t_rand=t_rand, u=u)
     for a, k in [("rgb_coarse", "rgb_c"), ("acc_coarse", "acc_c"), ("depth_coarse", "depth_c"), ("rgb_fine", "rgb_f"),
                  ("depth_fine", "depth_f"), ("acc_fine", "acc_f")]:
-        assert maxdiff(o[a], g[f"{tag}_{k}"]) <= TOL_RENDER, k
+        margin(f"lego_c1[{tag}]", k, maxdiff(o[a], g[f"{tag}_{k}"]), TOL_RENDER)
 
 
 # ---------------------------------------------------------------- C5: one eval step at size
@@ -185,7 +190,6 @@ def test_eval_c5_step_at_size(dev, frozen, precision):
     from codenerf import synthetic
     from codenerf.evaluate import pose_spherical
     from codenerf.nerf import PointSampler, RaySampler, render_rays
-    from test_gpu_grad import close
     g = load("eval_c5.npz", dev)
     rs = RaySampler(128, 128, synthetic.srn_intrinsics(128), sample_size=2048, device=dev, datatype=torch.float32)
     ps = PointSampler(64, 64, 0.8, 1.8, "lindepth", True, torch.float32, dev)
@@ -206,24 +210,30 @@ def test_eval_c5_step_at_size(dev, frozen, precision):
     o = render_rays(ro, rd, zse, zte, ps, embedders(dev), models["nerf_coarse"], models["nerf_fine"], chunk_rows=n,
                     t_rand=g["t_rand"], u=g["u"])
     rgb_c, rgb_f = o["rgb_coarse"], o["rgb_fine"]
-    assert maxdiff(rgb_c, g["rgb_coarse"]) <= TOL_RENDER
-    assert maxdiff(rgb_f, g["rgb_fine"]) <= TOL_RENDER
+    tag = f"eval_c5[{precision},{'frozen' if frozen else 'weights'}]"
+    margin(tag, "rgb_c", maxdiff(rgb_c, g["rgb_coarse"]), TOL_RENDER)
+    margin(tag, "rgb_f", maxdiff(rgb_f, g["rgb_fine"]), TOL_RENDER)
     lc = torch.nn.functional.mse_loss(rgb_c[..., :3], tp[..., :3])
     lf = torch.nn.functional.mse_loss(rgb_f[..., :3], tp[..., :3])
     loss = lc + lf + 1e-5 * (torch.norm(zse, p=2) + torch.norm(zte, p=2))
     loss.backward()
-    assert abs(loss.item() - g["loss"].item()) <= 1e-5
+    margin(tag, "loss", abs(loss.item() - g["loss"].item()), 1e-5)
+    rtol = C5_GRAD_RTOL[precision]
     for name, t in [("theta", theta), ("phi", phi), ("rho", rho)]:
         ref = g["g_" + name].cpu()
-        err = (t.grad.cpu() - ref).abs().max().item()
-        print(f"{name}: grad {t.grad.item():.6e} ref {ref.item():.6e}")
-        assert err <= 2e-3 * max(1e-2, ref.abs().max().item()), name
-    close(zs.grad, g["g_z_s"], 2e-3, "g_z_s")
-    close(zt.grad, g["g_z_t"], 2e-3, "g_z_t")
+        margin(tag, "d " + name, (t.grad.cpu() - ref).abs().max().item() / max(1e-2, ref.abs().max().item()), rtol)
+    for name, t in [("z_s", zs), ("z_t", zt)]:
+        ref = g["g_" + name].cpu()
+        margin(tag, "d " + name, (t.grad.cpu() - ref).abs().max().item() / ref.abs().max().item(), rtol)
     if not frozen:
-        close(models["nerf_fine"].fc_rgb.weight.grad, g["g_fine_fc_rgb_w"], 2e-3, "fine fc_rgb.weight")
-        close(models["nerf_coarse"].layer_xyz1.weight.grad, g["g_coarse_layer_xyz1_w"], 2e-3, "coarse layer_xyz1")
+        for what, t, key in [("fine fc_rgb.weight", models["nerf_fine"].fc_rgb.weight, "g_fine_fc_rgb_w"),
+                             ("coarse layer_xyz1.weight", models["nerf_coarse"].layer_xyz1.weight,
+                              "g_coarse_layer_xyz1_w")]:
+            ref = g[key].cpu()
+            margin(tag, "d " + what, (t.grad.cpu() - ref).abs().max().item() / ref.abs().max().item(), rtol)
+        worst = (0.0, "")
         for key, mm in models.items():
             for nm, prm in mm.named_parameters():
                 ref = g[f"gnorm_{key}.{nm}"].item()
-                assert abs(prm.grad.norm().item() - ref) <= 2e-3 * ref + 1e-8, (key, nm)
+                worst = max(worst, (abs(prm.grad.norm().item() - ref) / (ref + 1e-8), f"{key}.{nm}"))
+        margin(tag, "weight-grad norms (worst: %s)" % worst[1], worst[0], rtol)

@@ -220,6 +220,80 @@ def test_forward_pass_q1(dev, precision, r, s):
     assert maxdiff(got, ref) <= 1e-4
 
 
+# The field kernels' encodings take the lazy fast_sincosf path only when every lane's largest
+# argument |x| * 2^9 stays <= 2^14, i.e. |x| <= 32 at L = 10 (csrc/mlp_f32.hip, bound in
+# mlp_common.h); past it the wave evaluates every pair with sincosf up front.  Raw outputs with
+# |x| ~ 100 are larger, so the bound is relative to the largest |raw| (as test_trained_mlp's).
+LARGE_ARG_RTOL = {"f32": 1e-5, "f32_v1": 1e-5, "bf16x3": 1.5e-5, "bf16x3_w16": 1.5e-5}
+
+
+def _large_arg_case(case, r, s, seed):
+    g = torch.Generator().manual_seed(seed)
+    rd = torch.randn(r, 3, generator=g)
+    pts = torch.randn(r, s, 3, generator=g)
+    if case == "far":
+        pts = pts * 40.0                               # (almost) every lane past the 2^14 argument bound
+    else:
+        pts[37, 5] = torch.tensor([45.0, -38.0, 41.0])  # ONE sample of one wave far out: a mixed tile
+    return rd, pts
+
+
+@pytest.mark.parametrize("case", ["far", "mixed"])
+def test_field_large_arguments_inference(dev, precision, case):
+    """The inference field kernels past the fast-sincos argument bound, vs the oracle."""
+    from oracle import codenerf_oracle as O
+    from codenerf import synthetic
+    from codenerf.nerf import forward_pass
+    from conftest import margin
+    r, s = 300, 64
+    rd, pts = _large_arg_case(case, r, s, 11)
+    zs, zt = synthetic.latent_codes(3, r), synthetic.latent_codes(4, r)
+    ref = O.forward_pass(synthetic.codenerf_params(0), O.EmbedCfg(), rd, pts, zs, zt)
+    mdl, = models(dev, (0,), precision)
+    with torch.no_grad():
+        got = forward_pass(mdl, embedders(dev), rd.to(dev), pts.to(dev), (zs.to(dev), zt.to(dev)))
+    scale = ref.abs().max().item()
+    margin(f"large_args_inference_{case}[{precision}]", "raw rel", maxdiff(got, ref) / scale, LARGE_ARG_RTOL[precision],
+           max_abs_x=float(pts.abs().max()))
+
+
+@pytest.mark.parametrize("case", ["far", "mixed"])
+@pytest.mark.parametrize("train_precision", ["f32", "bf16x3"])
+@pytest.mark.parametrize("mode", ["pts", "rayz"])
+def test_field_large_arguments_training(dev, train_precision, case, mode):
+    """The training forwards (fp32 w16 and 3xbf16: activation planes + ReLU masks) past the
+    fast-sincos argument bound: raw and the saved post-activation planes vs the oracle's."""
+    from oracle import codenerf_oracle as O
+    from codenerf import ops, synthetic
+    from conftest import margin
+    r, s = 300, 64
+    rd, pts = _large_arg_case(case, r, s, 12)
+    geo = dict(pts=pts.to(dev))
+    if mode == "rayz":       # pts = ro + rd z formed in the kernel: far rays from far origins
+        z = torch.sort(0.8 + torch.rand(r, s, generator=torch.Generator().manual_seed(3)), dim=-1).values
+        ro = pts[:, 0, :].clone()
+        pts = ro[:, None, :] + rd[:, None, :] * z[..., None]
+        geo = dict(ro=ro.to(dev), z=z.to(dev))
+    params_d = synthetic.codenerf_params(0)
+    mdl, = models(dev, (0,), "f32")
+    params = [p.detach() for p in mdl.param_list()]
+    zs, zt = synthetic.latent_codes(5, 1), synthetic.latent_codes(6, 1)
+    cb = ops.code_bias(params, zs.to(dev), zt.to(dev))
+    fx, fd = [2.0 ** k for k in range(10)], [2.0 ** k for k in range(4)]
+    x3 = train_precision == "bf16x3"
+    raw, saved, _ = ops.radiance_field_train_w16(ops.mlp_pack(params, "bf16x3" if x3 else "f32_w16"), cb,
+                                                 rd.to(dev), s, r, fx, fd, precision=train_precision, **geo)
+    pre = {}
+    ref = O.forward_pass(params_d, O.EmbedCfg(), rd, pts, zs.expand(r, -1), zt.expand(r, -1), pre_out=pre)
+    tag = f"large_args_training_{case}_{mode}[{train_precision}]"
+    rt = LARGE_ARG_RTOL[train_precision]
+    margin(tag, "raw rel", maxdiff(raw, ref) / ref.abs().max().item(), rt, max_abs_x=float(pts.abs().max()))
+    # the first saved plane is h1 = relu(layer_xyz1(enc)): the encodings' own consumer
+    h1 = torch.relu(pre["h1"]) if "h1" in pre else None
+    if h1 is not None:
+        margin(tag, "h1 plane rel", maxdiff(saved[0], h1) / h1.abs().max().item(), rt)
+
+
 # ---------------------------------------------------------------- rendering
 
 
@@ -281,8 +355,9 @@ def test_render_full_golden(dev, precision):
     d = {k: maxdiff(o[a], g[k]) for a, k in [("rgb_coarse", "rgb_c"), ("depth_coarse", "depth_c"),
                                              ("acc_coarse", "acc_c"), ("rgb_fine", "rgb_f"),
                                              ("depth_fine", "depth_f"), ("acc_fine", "acc_f")]}
-    print("max |d| vs reference:", d)
-    assert max(d.values()) <= TOL_RENDER, d
+    from conftest import margin
+    for k, v in d.items():
+        margin(f"render_full_c2c3[{precision}]", k, v, TOL_RENDER)
     # size-independent properties at full size
     assert bool((o["acc_fine"] <= 1.0 + 1e-6).all())
     assert bool((o["z_fine"][:, 1:] >= o["z_fine"][:, :-1]).all())
