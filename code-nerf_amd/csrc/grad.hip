@@ -13,6 +13,7 @@
 
 #include "cn_common.h"
 #include "mlp_common.h"
+#include "cn_instrument.h"
 
 namespace cn {
 namespace grad {
@@ -393,7 +394,7 @@ struct DirFold {
   float* gsum;                             // (workgroups + n_rays / 16) slots of 16 x 256
 };
 
-#ifdef CN_ABLATE_TN_WAITPROF
+#ifdef CN_PROBE_TN_WAITPROF
 // experiment: per (workgroup, wave): shader clocks at the stage barrier, in the DMA issue, in the
 // whole loop, and the stage count (read by cn_debug_tnprof)
 __device__ long long g_tnprof[1024][8][4];
@@ -411,13 +412,7 @@ __device__ __forceinline__ void tn256_body(float* ring, const float* __restrict_
   const int i = lane & 31, h = lane >> 5;
   const int n0 = (wave >> 1) * 64, k0 = (wave & 1) * 128;
   // DIRS: the whole plane as one resource (host: M * 1 KiB + 1 KiB < 4 GiB), units u0 .. u1 - 1
-#ifdef CN_ABLATE_TN_INTERLEAVE
-  // experiment (plain form): workgroup b takes stages b, b + nb, ... of the whole plane, so the
-  // concurrent reads of all workgroups are one contiguous region
-  constexpr bool kIlv = !DIRS && !SIG;
-#else
   constexpr bool kIlv = false;
-#endif
   const int64_t mb = (DIRS || kIlv) ? 0 : (int64_t)blk * rows_per_block;
   const int64_t rows = (DIRS || kIlv) ? M : min(rows_per_block, M - mb);
   const unsigned u0 = DIRS ? blk * dir.units_per_block : 0u;
@@ -447,16 +442,7 @@ __device__ __forceinline__ void tn256_body(float* ring, const float* __restrict_
   auto dma = [&](int st) {
     float* slot = ring + (st & (kTwRing - 1)) * kTwStage;
     // DIRS: the unit's first row; units past the run's end (prefetch) read as zeros
-#ifdef CN_ABLATE_TN_L2DMA
-    unsigned row0 = static_cast<unsigned>((st & 3) * kTwRows);  // experiment: 4 stages of rows, L2-resident
-#elif defined(CN_ABLATE_TN_STAGGER)
-    // experiment: workgroup b walks its slab from stage b mod n_stages (wrapping), so the 256
-    // slabs' concurrent reads sit at different offsets instead of one 1.5-MiB-strided comb
-    const int stw = st < n_stages ? (st + static_cast<int>(blk) % n_stages) % n_stages : st;
-    unsigned row0 = static_cast<unsigned>(stw * kTwRows);
-#else
     unsigned row0 = static_cast<unsigned>(st * kTwRows);
-#endif
     if constexpr (kIlv) row0 = static_cast<unsigned>((st * nblk + blk) * kTwRows);
     if constexpr (DIRS) {
       row0 = u0 + static_cast<unsigned>(st) < dir.total_units ? dbase * dir.n_samples + dj * drcnt + (16 * dg - dbase)
@@ -490,7 +476,7 @@ __device__ __forceinline__ void tn256_body(float* ring, const float* __restrict_
 #pragma unroll
     for (int u = 0; u < 4; ++u) acc[t][u] = floatx16{0};
   float bsum[2] = {0.0f, 0.0f};
-#ifdef CN_ABLATE_TN_WAITPROF
+#ifdef CN_PROBE_TN_WAITPROF
   long long prof_bar = 0, prof_dma = 0;
   const long long prof_t0 = clock64();
 #endif
@@ -509,24 +495,19 @@ __device__ __forceinline__ void tn256_body(float* ring, const float* __restrict_
     // every wave is done with stage st-1, whose slot then receives stage st+3; after a DIRS flush
     // its 8 stores are the youngest 8 vector-memory ops as well
     static_assert(kTwRows / 2 == 8, "the vmcnt below counts stages st+1, st+2");
-#ifdef CN_ABLATE_TN_WAITPROF
+#ifdef CN_PROBE_TN_WAITPROF
     const long long tp0 = clock64();
 #endif
     if constexpr (SIG) asm volatile("s_waitcnt vmcnt(10)\n\ts_barrier" ::: "memory");
     else if (DIRS && flushed) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-#ifdef CN_ABLATE_TN_WAITPROF
+#ifdef CN_PROBE_TN_WAITPROF
     const long long tp1 = clock64();
     prof_bar += tp1 - tp0;
 #endif
-#ifdef CN_ABLATE_TN_NODMA
-    if (st == 0) dma(st + 3);  // experiment: the ring is never refilled (the vmcnt stays counted)
-    else asm volatile("" ::: "memory");
-#else
     dma(st + 3);
-#endif
-#ifdef CN_ABLATE_TN_WAITPROF
+#ifdef CN_PROBE_TN_WAITPROF
     __builtin_amdgcn_sched_barrier(0);
     prof_dma += clock64() - tp1;
 #endif
@@ -554,10 +535,8 @@ __device__ __forceinline__ void tn256_body(float* ring, const float* __restrict_
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         // the bias gradient's column sum (DIRS: per direction) rides on the A stream (VALU beside MFMA)
-#ifndef CN_ABLATE_TN_NOBSUM
         if constexpr (DIRS) dsum[p][t] += a[c][t];
         else bsum[t] += a[c][t];
-#endif
 #pragma unroll
         for (int u = 0; u < 4; ++u)
           acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[c][t], b[c][u], acc[t][u], 0, 0, 0);
@@ -587,7 +566,7 @@ __device__ __forceinline__ void tn256_body(float* ring, const float* __restrict_
   }
   // the prefetched stages past the slab must land before the workgroup's LDS is released
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#ifdef CN_ABLATE_TN_WAITPROF
+#ifdef CN_PROBE_TN_WAITPROF
   if (lane == 0 && blk < 1024) {
     g_tnprof[blk][wave][0] = prof_bar;
     g_tnprof[blk][wave][1] = prof_dma;
@@ -596,9 +575,6 @@ __device__ __forceinline__ void tn256_body(float* ring, const float* __restrict_
   }
 #endif
   float* pt = part ? part + (int64_t)blk * 65536 : nullptr;
-#ifdef CN_ABLATE_TN_NOFLUSH
-  if (blk == 0 && acc[0][0][0] == 12345.0f)  // experiment: no partial tile written
-#endif
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -2311,7 +2287,7 @@ extern "C" int cn_code_bias_backward(const float* const* params, const float* z_
   return launch_status();
 }
 
-#ifdef CN_ABLATE_TN_WAITPROF
+#ifdef CN_PROBE_TN_WAITPROF
 extern "C" int cn_debug_tnprof(long long* out, int n_blocks) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(cn::grad::g_tnprof), sizeof(long long) * 32 * std::min(n_blocks, 1024)) ==
                  hipSuccess ? 0 : -1;

@@ -32,10 +32,11 @@
 // sigma (fc_out row 0) is an fp32 dot product over layer_xyz2's outputs taken in the
 // xyz2 epilogue (32 packed FMAs per lane + a 4-group butterfly); fc_rgb the same way for its
 // 3 rows (96 packed FMAs per lane, weights from the rgb chunk's ring slot) -- as one 16-row
-// MFMA block over 64 k-steps (CN_ABLATE_RGB_MFMA) 13 of its 16 rows were padding.
+// MFMA block over 64 k-steps (r03, removed) 13 of its 16 rows were padding.
 #include <algorithm>
 
 #include "mlp_common.h"
+#include "cn_instrument.h"
 
 namespace cn {
 namespace mlp {
@@ -115,8 +116,9 @@ __global__ void pack_w16_kernel(Params P, float* __restrict__ packed) {
     } else {
       const int c = idx / (kChunkQuads * 4), rem = idx % (kChunkQuads * 4);
       if (c == kCRgb) {
-        // fc_rgb: 64 k-steps of block 0, [k-step quad][lane][k-step & 3] (the MFMA form,
-        // CN_ABLATE_RGB_MFMA), then at kRgbValu rows 0..2 over v2 for the VALU form,
+        // fc_rgb: 64 k-steps of block 0, [k-step quad][lane][k-step & 3] (the former MFMA form,
+        // not read any more; the chunk keeps its size and place in the stream), then at kRgbValu
+        // rows 0..2 over v2 for the VALU form,
         // [row][g][ob][r] = W_rgb[row][16 ob + 4 g + r]
         if (rem < 64 * 64) {
           const int lane = (rem % 256) / 4, t = 4 * (rem / 256) + rem % 4;
@@ -159,7 +161,7 @@ struct State {
   float sig;         // sigma partial (this lane group's 64 features)
   int lane, g, wave;
   int crow;          // this lane's code-bias row
-#ifdef CN_ABLATE_PROLOGUE
+#ifdef CN_PROBE_PROLOGUE
   long long prolog;  // experiment: shader clocks from a tile's start to its first chunk, summed over tiles
 #endif
   bool uniform_code; // all 16 samples of the wave use one code row
@@ -202,12 +204,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t mask_rsrc(const unsigned* mask
 __device__ __forceinline__ int fresh(int v);
 // Plane stores are non-temporal (cpol 2): the 400 MB of planes per C3 chunk never fit the L2, and
 // write-back stores evicted the weight stream (forward FETCH 58 -> 6 MB per launch, the backward
-// that reads them 1.5 % faster; r03i). CN_ABLATE_PLANE_WB restores write-back for A/B runs.
-#ifdef CN_ABLATE_PLANE_WB
-constexpr int kPlaneCPol = 0;
-#else
+// that reads them 1.5 % faster; r03i).
 constexpr int kPlaneCPol = 2;
-#endif
 template <int B0 = 0, int NB = 16>
 __device__ __forceinline__ void store_plane(const State& s, __amdgpu_buffer_rsrc_t r, const floatx4* v) {
   const unsigned off = static_cast<unsigned>(fresh(static_cast<int>(s.poff)));
@@ -477,11 +475,7 @@ __device__ __forceinline__ uint2v relu_act(State& s) {
 #pragma unroll
   for (int ob = 0; ob < 16; ++ob)
 #pragma unroll
-#ifdef CN_ABLATE_RELU_FMAX
-    for (int r = 0; r < 4; ++r) s.act[ob][r] = fmaxf(s.acc[ob][r], 0.0f);
-#else
     for (int r = 0; r < 4; ++r) s.act[ob][r] = __int_as_float(max(__float_as_int(s.acc[ob][r]), 0));
-#endif
   unsigned w[2] = {0u, 0u};
   if constexpr (MASKS) {
 #pragma unroll
@@ -529,7 +523,7 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
   const int64_t row = tile * kTile + s.wave * 16 + (s.lane & 15);
   const bool valid = row < a.m;
   const int64_t rc = valid ? row : a.m - 1;
-#ifdef CN_ABLATE_PROLOGUE
+#ifdef CN_PROBE_PROLOGUE
   const long long tp0 = clock64();
 #endif
 
@@ -593,7 +587,7 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
       for (int i = 0; i < 3; ++i) fr[8 + i] = clds[kCFreq + 10 + ((4 * i + g) * 11 >> 5)];
       const LazyXyz l0{enc, s.denc, in.x, in.vd, fr, g, false};
       l0.pair<0>();
-#ifdef CN_ABLATE_PROLOGUE
+#ifdef CN_PROBE_PROLOGUE
       s.prolog += clock64() - tp0;
 #endif
       bias_from(s, clds + kCB1);
@@ -626,7 +620,7 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
       s.denc[6] = s.g == 0 ? in.vd[0] : (s.g == 1 ? in.vd[1] : (s.g == 2 ? in.vd[2] : 0.0f));
     }
     s.denc[7] = 0.0f;
-#ifdef CN_ABLATE_PROLOGUE
+#ifdef CN_PROBE_PROLOGUE
     s.prolog += clock64() - tp0;
 #endif
     bias_from(s, clds + kCB1);
@@ -655,14 +649,6 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
       // the weights in two batches of 8 LDS reads issued together (one wait per batch; read one at
       // a time, each FMA pair waited on its own read while both waves of the SIMD sat here)
       float2v s0{0.0f, 0.0f}, s1{0.0f, 0.0f};
-#ifdef CN_ABLATE_SIGMA_SERIAL
-#pragma unroll
-      for (int ob = 0; ob < 16; ++ob) {
-        const floatx4 w = *reinterpret_cast<const floatx4*>(clds + kCSig + 64 * fresh(s.g) + 4 * ob);
-        s0 = __builtin_elementwise_fma(float2v{w[0], w[1]}, float2v{s.act[ob][0], s.act[ob][1]}, s0);
-        s1 = __builtin_elementwise_fma(float2v{w[2], w[3]}, float2v{s.act[ob][2], s.act[ob][3]}, s1);
-      }
-#else
       const floatx4* wsig = reinterpret_cast<const floatx4*>(clds + kCSig) + 16 * fresh(s.g);
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -678,7 +664,6 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
         }
         __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
       }
-#endif
       s.sig = (s0[0] + s0[1]) + (s1[0] + s1[1]);
     }
     if (layer == kXyz2) bias_code(s, a, crow_lds, kCbXyz2);
@@ -717,7 +702,6 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
     sg += __shfl_xor(sg, 32);
     s.sig = sg + bs;
   }
-#ifndef CN_ABLATE_RGB_MFMA
   // fc_rgb on the VALU: 3 of the 16 MFMA rows were real, so the chunk's 64 MFMAs per wave (4 k
   // pipe cycles per SIMD and tile) became 96 packed FMAs per lane over this lane group's 64 v2
   // features, weights read from the rgb chunk's slot (it has landed: the chunk is current), then
@@ -769,57 +753,13 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
       reinterpret_cast<float4*>(a.raw)[row] = o;
     }
   }
-#else
-  {
-    const float4* slot = lds + (c & (kRing - 1)) * kChunkQuads + s.lane;
-    const float4* nslot = lds + ((c + 1) & (kRing - 1)) * kChunkQuads + s.lane;
-    floatx4 a0[4], a1[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) a0[q] = s.pre[q];
-    // k-step quads 0..3 arrived in s.pre; quads 4q'..4q'+3 are read one group ahead
-#define CN_RGB(G, CUR, NXT)                                                              \
-  {                                                                                      \
-    if constexpr ((G) < 3) {                                                             \
-      _Pragma("unroll") for (int q = 0; q < 4; ++q) NXT[q] = *reinterpret_cast<const floatx4*>(slot + (4 * ((G) + 1) + q) * 64); \
-    } else {                                                                             \
-      read_a<0>(nslot, s.pre);                                                           \
-    }                                                                                    \
-    _Pragma("unroll") for (int q = 0; q < 4; ++q)                                        \
-    _Pragma("unroll") for (int j = 0; j < 4; ++j) {                                      \
-      s.acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(CUR[q][j], s.act[4 * (G) + q][j], s.acc[j], 0, 0, 0); \
-    }                                                                                    \
-    step_pattern();                                                                      \
-    __builtin_amdgcn_sched_barrier(0);                                                   \
-    if constexpr ((G) == 1) {                                                            \
-      chunk_barrier();                                                                   \
-      dma_chunk(s, lds, c + 3);                                                          \
-    }                                                                                    \
-    if constexpr ((G) >= 2) st_v2.template blocks<8 * ((G) - 2), 8>();                  \
-  }
-    CN_RGB(0, a0, a1)
-    CN_RGB(1, a1, a0)
-    CN_RGB(2, a0, a1)
-    CN_RGB(3, a1, a0)
-#undef CN_RGB
-    c += 1;
-  }
-  if (valid && s.g == 0) {
-    const floatx4 r = (s.acc[0] + s.acc[1]) + (s.acc[2] + s.acc[3]);
-    float4 o;
-    o.x = r[0];
-    o.y = r[1];
-    o.z = r[2];
-    o.w = s.sig;
-    reinterpret_cast<float4*>(a.raw)[row] = o;
-  }
-#endif
 }
 
-#ifdef CN_ABLATE_WGTIME
+#ifdef CN_PROBE_WGTIME
 // experiment: each workgroup's start / end wall clock (100 MHz), read by cn_debug_wgtime
 __device__ long long g_wgtime[2048][2];
 #endif
-#ifdef CN_ABLATE_PROLOGUE
+#ifdef CN_PROBE_PROLOGUE
 // experiment: per (workgroup, wave) of the last fp32 field launch (forward or backward): tile
 // prologue clocks (summed), the tile loop's clocks, the tile count; read by cn_debug_prologue
 __device__ long long g_prolog[2048][8][3];
@@ -827,7 +767,7 @@ __device__ long long g_prolog[2048][8][3];
 
 template <int MODE, bool MASKS, bool SAVE = false>
 __global__ __launch_bounds__(kThreads, 2) void field_w16_kernel(FieldArgs a) {
-#ifdef CN_ABLATE_WGTIME
+#ifdef CN_PROBE_WGTIME
   const long long t_start = wall_clock64();
 #endif
   // ONE LDS object (a second one makes hipcc wait vmcnt(0) before ring reads): the DMA
@@ -855,7 +795,7 @@ __global__ __launch_bounds__(kThreads, 2) void field_w16_kernel(FieldArgs a) {
 
   const int64_t n_tiles = (a.m + kTile - 1) / kTile;
   int c = 0;
-#ifdef CN_ABLATE_PROLOGUE
+#ifdef CN_PROBE_PROLOGUE
   s.prolog = 0;
   const long long tl0 = clock64();
   int nt = 0;
@@ -863,11 +803,11 @@ __global__ __launch_bounds__(kThreads, 2) void field_w16_kernel(FieldArgs a) {
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
     c = 0;
     field_tile<MODE, MASKS, SAVE>(s, a, lds, clds, crow_lds, tile, c);
-#ifdef CN_ABLATE_PROLOGUE
+#ifdef CN_PROBE_PROLOGUE
     ++nt;
 #endif
   }
-#ifdef CN_ABLATE_PROLOGUE
+#ifdef CN_PROBE_PROLOGUE
   if (s.lane == 0 && blockIdx.x < 2048) {
     g_prolog[blockIdx.x][s.wave][0] = s.prolog;
     g_prolog[blockIdx.x][s.wave][1] = clock64() - tl0;
@@ -877,7 +817,7 @@ __global__ __launch_bounds__(kThreads, 2) void field_w16_kernel(FieldArgs a) {
   // the last tile prefetched chunks 0..2 of a tile that does not exist: they must land
   // before the workgroup's LDS is released
   __builtin_amdgcn_s_waitcnt(0x0F70);
-#ifdef CN_ABLATE_WGTIME
+#ifdef CN_PROBE_WGTIME
   if (threadIdx.x == 0 && blockIdx.x < 2048) {
     g_wgtime[blockIdx.x][0] = t_start;
     g_wgtime[blockIdx.x][1] = wall_clock64();
@@ -1186,7 +1126,7 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   const float* clds = reinterpret_cast<const float*>(lds + kRing * kChunkQuads);
 
   // ---- inputs: sample, d raw, masks of v2 and v1, code row (wave-uniform: host-checked)
-#ifdef CN_ABLATE_PROLOGUE
+#ifdef CN_PROBE_PROLOGUE
   const long long tp0 = clock64();
 #endif
   const SampleIn in = decode_sample<MODE>(a, rc);
@@ -1214,7 +1154,7 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   }
   int c = 0;
   // ---- fc_rgb^T (chunk 0): B = d rgb channel g at k-step 0
-#ifdef CN_ABLATE_PROLOGUE
+#ifdef CN_PROBE_PROLOGUE
   s.prolog += clock64() - tp0;
 #endif
   zero_acc(s);
@@ -1391,18 +1331,18 @@ __global__ __launch_bounds__(kThreads, 2) void field_w16_bwd_kernel(FieldArgs a)
   read_a<0>(lds + s.lane, s.pre);
   int cur_code = -1;
   const int64_t n_tiles = (a.m + kTile - 1) / kTile;
-#ifdef CN_ABLATE_PROLOGUE
+#ifdef CN_PROBE_PROLOGUE
   s.prolog = 0;
   const long long tl0 = clock64();
   int nt = 0;
 #endif
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
     bwd_tile<MODE, TRAIN>(s, a, lds, grow, tile, cur_code);
-#ifdef CN_ABLATE_PROLOGUE
+#ifdef CN_PROBE_PROLOGUE
     ++nt;
 #endif
   }
-#ifdef CN_ABLATE_PROLOGUE
+#ifdef CN_PROBE_PROLOGUE
   if (s.lane == 0 && blockIdx.x < 2048) {
     g_prolog[blockIdx.x][s.wave][0] = s.prolog;
     g_prolog[blockIdx.x][s.wave][1] = clock64() - tl0;
@@ -1491,14 +1431,14 @@ int launch_field_w16_bwd(int mode, FieldArgs& a, hipStream_t st) {
 }  // namespace mlp
 }  // namespace cn
 
-#ifdef CN_ABLATE_PROLOGUE
+#ifdef CN_PROBE_PROLOGUE
 // experiment: copy g_prolog of the last fp32 field launch (n workgroups x 8 waves x 3)
 extern "C" int cn_debug_prologue(long long* out, int n) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(cn::mlp::w16::g_prolog), sizeof(long long) * 24 * std::min(n, 2048)) ==
                  hipSuccess ? 0 : -1;
 }
 #endif
-#ifdef CN_ABLATE_WGTIME
+#ifdef CN_PROBE_WGTIME
 // experiment: copy the last field_w16_kernel launch's per-workgroup (start, end) wall clocks
 extern "C" int cn_debug_wgtime(long long* out, int n) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(cn::mlp::w16::g_wgtime), sizeof(long long) * 2 * std::min(n, 2048)) ==

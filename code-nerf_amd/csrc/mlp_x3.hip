@@ -260,11 +260,9 @@ __device__ __forceinline__ void save_slot(const State& s, float lo) {
 // (piece i of chunk cn covers quads [i*256, i*256+256) of the chunk; this wave
 // moves quads i*256 + wave*64 + lane).
 __device__ __forceinline__ void dma_piece(const State& s, float4* lds, int cn, int i) {
-#ifndef CN_ABLATE_NO_DMA
   const unsigned soff = __builtin_amdgcn_readfirstlane((unsigned)(cn * kChunkQuads + i * 256) * 16u);
   __builtin_amdgcn_raw_ptr_buffer_load_lds(s.wsrc, (lds_ptr_t)(lds + (cn & (kRing - 1)) * kChunkQuads + i * 256 + s.wave * 64),
                                            16, s.voff, soff, 0, 0);
-#endif
 }
 
 // The pieces running chunk c issues: groups 0-3 pieces 4-7 of chunk c+2, groups
@@ -293,16 +291,8 @@ __device__ __forceinline__ Dma dma_for(const State& s, float4* lds, int c) {
 // statement, so no LDS read can be scheduled across it.
 template <int OUT>
 __device__ __forceinline__ void chunk_barrier() {
-#if defined(CN_ABLATE_NO_BARRIER)
-  asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" ::"n"(OUT) : "memory");
-#elif defined(CN_ABLATE_NO_DMA)
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#else
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(OUT) : "memory");
-#endif
-#ifndef CN_ABLATE_NO_MC_FENCE
   __builtin_amdgcn_sched_barrier(0);  // nothing (ring reads included) is scheduled above the wait
-#endif
 }
 constexpr int kMidOut = 8;  // chunk c+2's pieces are younger than chunk c+1's at M_c
 
@@ -375,14 +365,7 @@ __device__ __forceinline__ floatx16 bias_mfma(float v, bf16x8 one) {
   const __bf16 hi = static_cast<__bf16>(v);
   f[0] = hi;
   f[1] = static_cast<__bf16>(v - static_cast<float>(hi));
-#ifdef CN_ABLATE_NO_MFMA
-  floatx16 r = {};
-  r[0] = v;
-  asm volatile("" ::"v"(f), "v"(one));
-  return r;
-#else
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(f, one, floatx16{0}, 0, 0, 0);
-#endif
 }
 
 __device__ __forceinline__ bf16x8 ones_b(int h) {
@@ -430,13 +413,9 @@ __device__ __forceinline__ void init_acc_per_lane(State& s, const FieldArgs& a, 
 }
 
 __device__ __forceinline__ void mfma3(floatx16& acc, bf16x8 ah, bf16x8 al, bf16x8 bh, bf16x8 bl) {
-#ifdef CN_ABLATE_NO_MFMA
-  asm volatile("" ::"v"(ah), "v"(al), "v"(bh), "v"(bl));
-#else
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
-#endif
 }
 
 // A fragments {hi, lo} of blocks (2P, 2P+1) of k-step T of the chunk in `slot`.
@@ -481,7 +460,6 @@ struct ConvFill {
   template <int G>
   __device__ __forceinline__ void step() {
     if constexpr (SAVE && (G & 1)) save_quad<J, G / 2>(s, lo);  // before G == 7 overwrites the slot
-#ifndef CN_ABLATE_NO_FILL
     // w (read asynchronously at the chunk start) is usable only after M_c, so the
     // sigma products of pieces 0-3 are taken in steps 4-7 from the raw values
     if constexpr (G < 4) {
@@ -493,10 +471,6 @@ struct ConvFill {
       s.sig = fmaf(w[2 * K], v0, s.sig);
       s.sig = fmaf(w[2 * K + 1], v1, s.sig);
     }
-#else
-    out[2 * G] = s.sl[J][2 * G];
-    out[2 * G + 1] = s.sl[J][2 * G + 1];
-#endif
     if constexpr (G == 7) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) s.sl[J][i] = out[i];
@@ -683,13 +657,8 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
 
   // ---- encodings (VALU)
   if constexpr (MODE != kFromEncoded) {
-#ifndef CN_ABLATE_NO_ENC
     encode_pairs<15, 10>(in.x, a.fx, s.h, enc);
     encode_pairs<6, 4>(in.vd, a.fd, s.h, dv);
-#else
-    for (int i = 0; i < 32; ++i) enc[i] = in.x[i % 3] * (float)(i + 1);
-    for (int i = 0; i < 16; ++i) dv[i] = in.vd[i % 3] * (float)(i + 1);
-#endif
   }
   dv[14] = 0.0f;
   dv[15] = 0.0f;
@@ -1008,11 +977,7 @@ __device__ __forceinline__ void ds_add(unsigned base, float v) {
 // gbase + 4 * acc_row(J, R, 0) bytes (gbase carries the 4h and the layer's column offset).
 template <int J, int R>
 __device__ __forceinline__ void red_add(unsigned gbase, float v) {
-#ifdef CN_ABLATE_NO_RED
-  asm volatile("" ::"v"(v), "v"(gbase));
-#else
   ds_add<4 * acc_row(J, R, 0)>(gbase, sum8(v));
-#endif
 }
 
 // Training backward: masked values of pieces 2q, 2q+1 of slot J (features 32J + 8q + 4h ..
@@ -1079,12 +1044,7 @@ __device__ __forceinline__ void bwd_init(State& s, const float* blds, int off, b
       f[1] = hi;
       f[2] = static_cast<__bf16>(v[b] - static_cast<float>(hi));
     }
-#ifdef CN_ABLATE_NO_MFMA
-    s.acc[b] = floatx16{};
-    asm volatile("" ::"v"(f), "v"(sig_b));
-#else
     s.acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f, sig_b, floatx16{0}, 0, 0, 0);
-#endif
   }
 }
 

@@ -226,9 +226,6 @@ __device__ __forceinline__ void sigma_h2(State& s, const float* clds) {
 
 // One LDS-DMA piece: 1 KiB of chunk cn (piece p of 4 for this wave).
 __device__ __forceinline__ void dma_piece(const State& s, float4* lds, int cn, int p) {
-#ifdef CN_ABLATE_NO_DMA
-  return;
-#endif
   const int src = cn < kChunks ? cn : cn - kChunks;
   const unsigned soff = __builtin_amdgcn_readfirstlane((unsigned)(src * kChunkQuads + p * 64 * kWaves) * 16u);
   __builtin_amdgcn_raw_ptr_buffer_load_lds(
@@ -244,13 +241,7 @@ __device__ __forceinline__ void dma_chunk(const State& s, float4* lds, int cn) {
 // M_c: chunk c+1 landed for every wave (all but this wave's 4 youngest DMA pieces --
 // chunk c+2's -- retired), every wave past chunk c-1, this wave's LDS reads returned.
 __device__ __forceinline__ void chunk_barrier() {
-#if defined(CN_ABLATE_NO_BARRIER)
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#elif defined(CN_ABLATE_NO_DMA)
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#else
   asm volatile("s_waitcnt vmcnt(4)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#endif
   __builtin_amdgcn_sched_barrier(0);
 }
 

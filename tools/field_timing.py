@@ -1,6 +1,6 @@
 """Time the C2 field-kernel launch (1,048,576 samples) of the library at $CODENERF_LIB.
 
-Kernel-development harness (ablation builds etc.); prints one JSON line.
+Kernel-development harness (variant builds etc.); prints one JSON line.
     CODENERF_LIB=... python tools/field_timing.py [--precision bf16x3] [--iters 20]
 """
 import argparse

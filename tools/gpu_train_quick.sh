@@ -18,8 +18,8 @@ for p in ${TRAIN_PRECISIONS:-f32}; do
   rc=$?; echo "train $p rc=$rc"; tail -1 $O/train_$p.json | cut -c1-400; [ $rc -ne 0 ] && { tail -5 $O/train_$p.err; exit $rc; }
   python $R/tools/kstats.py $O/train_$p/run_kernel_stats.csv > $O/train_${p}_kstats.txt; head -25 $O/train_${p}_kstats.txt
 done
-for v in ${EXTRA_LIBS}; do   # ablation builds (tools/build_ablations.sh) of the f32 iteration
-  CODENERF_LIB=$R/code-nerf_amd/codenerf/lib/ablate/lib_$v.so timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/train_f32_$v -o run --output-format csv -- python $R/tools/train_timing.py --precision f32 --iters ${TRAIN_ITERS:-8} > $O/train_f32_$v.json 2> $O/train_f32_$v.err
+for v in ${EXTRA_LIBS}; do   # variant builds (tools/build_variants.sh) of the f32 iteration
+  CODENERF_LIB=$R/code-nerf_amd/codenerf/lib/variants/lib_$v.so timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/train_f32_$v -o run --output-format csv -- python $R/tools/train_timing.py --precision f32 --iters ${TRAIN_ITERS:-8} > $O/train_f32_$v.json 2> $O/train_f32_$v.err
   rc=$?; echo "train f32 $v rc=$rc"; tail -1 $O/train_f32_$v.json | cut -c1-300; [ $rc -ne 0 ] && { tail -5 $O/train_f32_$v.err; exit $rc; }
   python $R/tools/kstats.py $O/train_f32_$v/run_kernel_stats.csv > $O/train_f32_${v}_kstats.txt; head -12 $O/train_f32_${v}_kstats.txt
 done

@@ -1,6 +1,6 @@
 """Share of the fp32 field kernels' tile loop spent in the tile prologue (sample inputs, code row,
 encodings: from a tile's start to its first chunk), training forward and training backward at the
-C3 chunk-field size.  Library built with -DCN_ABLATE_PROLOGUE (tools/build_ablations.sh PROLOGUE):
+C3 chunk-field size.  Library built with -DCN_PROBE_PROLOGUE (tools/build_variants.sh PROLOGUE):
     CODENERF_LIB=.../lib_PROLOGUE.so python tools/prologue.py [--rays 6144] [--samples 64]"""
 import argparse
 import ctypes

@@ -1,5 +1,5 @@
 """HIP-event timing of one whole-tile dW GEMM (gemm_tn256_kernel + its fixed-order reduction, the
-deterministic cn_gemm_tn_ws path) at the C3 chunk size, for the library at $CODENERF_LIB (ablation
+deterministic cn_gemm_tn_ws path) at the C3 chunk size, for the library at $CODENERF_LIB (a variant
 builds).   CODENERF_LIB=... python tools/tn_timing.py [--m 393216] [--iters 20]"""
 import argparse
 import json

@@ -1,4 +1,4 @@
-"""Where the whole-tile dW GEMM's waves spend their clocks (library built with -DCN_ABLATE_TN_WAITPROF,
+"""Where the whole-tile dW GEMM's waves spend their clocks (library built with -DCN_PROBE_TN_WAITPROF,
 optionally with TN_NODMA): per stage, the clocks at the counted-vmcnt barrier and in the DMA issue,
 against the whole loop.   CODENERF_LIB=.../lib_TN_WAITPROF.so python tools/tnprof.py [--m 393216]"""
 import argparse

@@ -1,5 +1,5 @@
 """Per-workgroup start / end of the training forward field_w16_kernel<.., true, true> (library built with
--DCN_ABLATE_WGTIME, tools/build_ablations.sh WGTIME): how evenly the persistent grid's static tile
+-DCN_PROBE_WGTIME, tools/build_variants.sh WGTIME): how evenly the persistent grid's static tile
 round-robin finishes.   CODENERF_LIB=.../lib_WGTIME.so python tools/wgtime.py [--rays 4096 8192 6144]"""
 import argparse
 import ctypes
