@@ -90,10 +90,17 @@ class GraphedEvalStep:
     Per ``step()``: the host draws the ray subset exactly as the reference does
     (np.random.permutation per iteration, ray_sampler.py:41-42) into a pinned buffer and folds
     the AdamW step's bias-corrected scalars (counting the step as ``optimizer.step()`` would) into
-    another; the graph copies both to the device, renders, takes the loss and its gradients into
-    the optimiser's flat gradient buffer (zeroed inside the graph, as ``zero_grad`` would) and
-    applies the flat AdamW update (cn_adamw_step_dev, scalars read from device memory).  With
-    ``optimizer_in_graph=False`` the caller runs ``optimizer.step()`` after the replay instead.
+    another; both are copied to fixed device buffers on the stream (outside the graph), then one
+    replay renders, takes the loss and its gradients into the optimiser's flat gradient buffer
+    (zeroed inside the graph, as ``zero_grad`` would) and applies the flat AdamW update
+    (cn_adamw_step_dev, scalars read from device memory).  With ``optimizer_in_graph=False`` the
+    caller runs ``optimizer.step()`` after the replay instead.
+    The pinned buffers alternate between two sets, each reused only once the copy that read it two
+    steps earlier has finished: the host never waits for the replay it just launched, so it draws
+    and enqueues the next iteration while the GPU runs this one.  (A first form copied from ONE
+    pinned set inside the graph and had to wait for each replay to end before refilling it: the
+    GPU then idled for the host's wake-up, draw and graph launch every iteration -- slower than
+    the eager loop)
     The stratified / fine-sample uniforms come from torch's device generator, whose graph-safe
     state advances per replay; the warm-up iterations' draws are rolled back (the generator state
     is restored before capture), so replay i draws what eager iteration i would.
@@ -113,9 +120,10 @@ class GraphedEvalStep:
         assert theta.numel() == 1, "one view per eval step (eval.py:145)"
         dev = target_pixels.device
         self.rs, self.opt, self._next = rs, optimizer, None
-        self.h_sel = torch.zeros(1, rs.sample_size, dtype=torch.int64).pin_memory()
+        self.h_sel = [torch.zeros(1, rs.sample_size, dtype=torch.int64).pin_memory() for _ in range(2)]
         self.d_sel = torch.zeros(1, rs.sample_size, dtype=torch.int64, device=dev)
-        self.done = torch.cuda.Event()
+        self.copied = [None, None]             # events: the copies that last read each pinned set
+        self.k = 0
         args = (theta, phi, rho, shape_code, texture_code, target_pixels, samplers, embedders, models,
                 regularizer_lambda)
         kw = dict(gt_pose=gt_pose, t_rand=t_rand, u=u, sel=self.d_sel)
@@ -125,14 +133,11 @@ class GraphedEvalStep:
         self.opt_in_graph = optimizer_in_graph
         if optimizer_in_graph:
             n_seg = len(self.opt._plan(advance=False))
-            self.h_scal = torch.zeros(3 * n_seg, dtype=torch.float32).pin_memory()
+            self.h_scal = [torch.zeros(3 * n_seg, dtype=torch.float32).pin_memory() for _ in range(2)]
             self.d_scal = torch.zeros(3 * n_seg, dtype=torch.float32, device=dev)
 
         def body(with_opt: bool):
             grads.zero_()
-            self.d_sel.copy_(self.h_sel, non_blocking=True)
-            if with_opt:
-                self.d_scal.copy_(self.h_scal, non_blocking=True)
             loss, logs = eval_step_loss(*args, **kw)
             loss.backward()
             if with_opt:
@@ -159,12 +164,19 @@ class GraphedEvalStep:
         step()."""
         sel = self._next if self._next is not None else self.rs.draw_host(1)
         self._next = None
-        self.done.synchronize()                # the previous replay has finished reading h_sel / h_scal
-        self.h_sel.numpy()[:] = sel
+        k = self.k
+        self.k ^= 1
+        if self.copied[k] is not None:
+            self.copied[k].synchronize()       # the copies of two steps ago have read this set
+        self.h_sel[k].numpy()[:] = sel
+        self.d_sel.copy_(self.h_sel[k], non_blocking=True)
         if self.opt_in_graph:
-            self.opt.graph_scalars(self.h_scal.numpy())
+            self.opt.graph_scalars(self.h_scal[k].numpy())
+            self.d_scal.copy_(self.h_scal[k], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.copied[k] = ev
         self.graph.replay()
-        self.done.record()
         return self.loss, self.logs
 
     def prefetch(self) -> None:

@@ -197,6 +197,9 @@ __global__ __launch_bounds__(256) void volume_render_kernel(
   if (rw0 < n_rays)
     stage_rows_in<K>(reinterpret_cast<const float4*>(raw) + rw0 * S_in,
                      static_cast<int>(min<int64_t>(64 / L, n_rays - rw0)) * S_in, sl, lane);
+  // lanes read quads other lanes wrote: keep the staging stores ahead of the reads (no instruction;
+  // LDS operations of one wave then execute in program order)
+  __builtin_amdgcn_wave_barrier();
   if (r >= n_rays) return;  // whole rays leave together: the cross-lane steps never read an exited lane
   // S == 1: the reference's dists = cat(z[1:] - z[:-1], full_like(that[..., :1], 1e10))
   // is EMPTY (both pieces are 0 wide), so no sample contributes (rgb = acc = depth = 0,
@@ -335,6 +338,7 @@ __global__ __launch_bounds__(256) void volume_render_backward_kernel(
   const int nq = static_cast<int>(min<int64_t>(64 / L, n_rays - rw0)) * S_in;  // the wave's valid quads
   float4* sl = slds + (threadIdx.x >> 6) * 80 * K;
   stage_rows_in<K>(reinterpret_cast<const float4*>(raw) + rw0 * S_in, nq, sl, lane);
+  __builtin_amdgcn_wave_barrier();  // cross-lane LDS reads follow (see the forward)
   // a ray past n_rays (L = 16 only) stays alive as a copy of the last ray, nothing stored, so the
   // wave's coalesced d raw copy-out runs in every lane
   const bool live = r_ < n_rays;
@@ -432,6 +436,7 @@ __global__ __launch_bounds__(256) void volume_render_backward_kernel(
       if (live) sl[pad4(q0 + i)] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
+  __builtin_amdgcn_wave_barrier();  // the copy-out reads quads other lanes wrote
   stage_rows_out<K>(reinterpret_cast<float4*>(d_raw) + rw0 * S_in, nq, sl, lane);
   gnorm = ray_sum<L>(gnorm);
   if (live && sub == (L == 16 ? 15 : 63) && d_rd) {
