@@ -45,7 +45,6 @@ struct FieldArgs {
   float* d_ro;           // backward: (n_rays, 3) accumulated (kFromRayZ)
   float* d_rd;           // backward: (n_rays, 3) accumulated
   float* dpre;           // fp32 fused training backward: (5, m, 256) masked layer-input gradients
-  float* gbias[3];       // ... and the bias gradients of layer_dir2, layer_dir1, layer_xyz1 (accumulated)
 };
 
 // v[i] for a lane-varying i in 0..2 by selects: an indexed read of a private array would

@@ -854,8 +854,7 @@ constexpr int kTRgb = 0, kTDir2 = 1, kTDir1 = 9, kTDDir = 17, kTOut = 18, kTXyz2
 constexpr int kTSig = 0;  // transposed-pack constants: fc_out row 0 over h2, [g][ob][r]
 // LDS after the ring: constants, one g_code row per wave
 constexpr int kBGacc = kLdsConsts;
-constexpr int kBBias = kBGacc + kWaves * kCbStride;  // training: bias-gradient rows dir2 | dir1 | xyz1 (shared)
-constexpr int kBwdLdsFloats = kBBias + 3 * 256;
+constexpr int kBwdLdsFloats = kBGacc + kWaves * kCbStride;
 constexpr int kBwdLdsQuads = kRing * kChunkQuads + kBwdLdsFloats / 4;
 static_assert(kBwdLdsQuads * 16 <= 160 * 1024, "LDS budget (backward)");
 static_assert(kTXyz1 + 2 == kChunks, "backward chunk schedule");
@@ -992,6 +991,90 @@ __device__ __forceinline__ void mask_act(State& s, uint2 m) {
   }
 }
 
+// The lazy form (the field backward's masked layers): act = the raw gradients (the previous layer's
+// accumulators), then value t is masked in place in the shadow of the MFMAs of k-step t - 1 (MaskB,
+// NarrowMask) -- at the layer boundary, where both waves of a SIMD meet with the matrix pipe idle,
+// only value 0 (a 256-wide layer) or block pair 0 (the narrow xyz1 chunks) is masked.
+template <int t>
+__device__ __forceinline__ void mask_one(State& s, uint2 m) {
+  const unsigned w = t < 32 ? m.x : m.y;
+  const unsigned keep = static_cast<unsigned>(__builtin_amdgcn_sbfe(static_cast<int>(w), t & 31, 1));
+  s.act[t >> 2][t & 3] = __uint_as_float(__float_as_uint(s.act[t >> 2][t & 3]) & keep);
+}
+
+__device__ __forceinline__ void raw_act(State& s) {
+#pragma unroll
+  for (int ob = 0; ob < 16; ++ob) s.act[ob] = s.acc[ob];
+}
+
+// B of a masked 256-wide layer: k-step T reads value K0 + T (masked by then), and its prep masks
+// value K0 + T + 1 (the last k-step of a chunk: the next chunk's first value).
+template <int K0>
+struct MaskB {
+  State& s;
+  uint2 m;
+  template <int T>
+  __device__ __forceinline__ float at() const {
+    constexpr int t = K0 + T;
+    return s.act[t >> 2][t & 3];
+  }
+  static constexpr bool kLazy = true;
+  template <int T>
+  __device__ __forceinline__ void prep() const {
+    if constexpr (K0 + T + 1 < 64) mask_one<K0 + T + 1>(s, m);
+  }
+};
+
+// The narrow chunks' lazy mask: k-step T reads blocks 2 T, 2 T + 1 (values 8 T .. 8 T + 7); the
+// first chunk masks the next k-step's eight values after its MFMAs, the second finds them all masked.
+struct NarrowMask {
+  State& s;
+  uint2 m;
+  bool active;
+  template <int T>
+  __device__ __forceinline__ void step() const {
+    if constexpr (T + 1 < 8) {
+      if (active) {
+        mask_one<8 * T + 8>(s, m);
+        mask_one<8 * T + 9>(s, m);
+        mask_one<8 * T + 10>(s, m);
+        mask_one<8 * T + 11>(s, m);
+        mask_one<8 * T + 12>(s, m);
+        mask_one<8 * T + 13>(s, m);
+        mask_one<8 * T + 14>(s, m);
+        mask_one<8 * T + 15>(s, m);
+      }
+    }
+  }
+};
+struct NoPrep {
+  template <int T>
+  __device__ __forceinline__ void step() const {}
+};
+
+// The mask words as new values (an empty asm): the bit tests of a chunk are formed in that chunk.
+// Without it the optimiser merged them with the other uses of the same words (the eager g_code
+// form, the other chunks) and kept up to 64 tested bits live across the layer: 116-152 B/lane of
+// scratch at the 256-VGPR cap.
+__device__ __forceinline__ uint2 fresh_mask(uint2 m) {
+  asm volatile("" : "+v"(m.x), "+v"(m.y));
+  return m;
+}
+
+// A 256-input layer whose B is the lazily masked act (MaskB; value 0 masked by the caller).
+template <typename Post = NoPost>
+__device__ __forceinline__ void layer256_masked(State& s, float4* lds, int& c, uint2 m, Post post = Post{}) {
+  chunk16<8, 0>(s, lds, c + 0, MaskB<0>{s, fresh_mask(m)}, post);
+  chunk16<8, 1>(s, lds, c + 1, MaskB<8>{s, fresh_mask(m)}, post);
+  chunk16<8, 2>(s, lds, c + 2, MaskB<16>{s, fresh_mask(m)}, post);
+  chunk16<8, 3>(s, lds, c + 3, MaskB<24>{s, fresh_mask(m)}, post);
+  chunk16<8, 4>(s, lds, c + 4, MaskB<32>{s, fresh_mask(m)}, post);
+  chunk16<8, 5>(s, lds, c + 5, MaskB<40>{s, fresh_mask(m)}, post);
+  chunk16<8, 6>(s, lds, c + 6, MaskB<48>{s, fresh_mask(m)}, post);
+  chunk16<8, 7>(s, lds, c + 7, MaskB<56>{s, fresh_mask(m)}, post);
+  c += 8;
+}
+
 __device__ __forceinline__ void zero_acc(State& s) {
 #pragma unroll
   for (int ob = 0; ob < 16; ++ob) s.acc[ob] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -1022,8 +1105,8 @@ __device__ __forceinline__ void mfma_narrow(State& s, const floatx4* a) {
 }
 
 // A narrow chunk (2 blocks x 64 k-steps, B from s.act) into s.acc2, on chunk16's schedule.
-template <int CI = 0, typename Post = NoPost>
-__device__ __forceinline__ void chunk_narrow(State& s, float4* lds, int c, Post post = Post{}) {
+template <int CI = 0, typename Post = NoPost, typename Prep = NoPrep>
+__device__ __forceinline__ void chunk_narrow(State& s, float4* lds, int c, Post post = Post{}, Prep prep = Prep{}) {
   const float4* slot = lds + (c & (kRing - 1)) * kChunkQuads + s.lane;
   const float4* nslot = lds + ((c + 1) & (kRing - 1)) * kChunkQuads + s.lane;
   floatx4 a0[4], a1[4];
@@ -1035,7 +1118,8 @@ __device__ __forceinline__ void chunk_narrow(State& s, float4* lds, int c, Post 
     if constexpr ((T) + 1 < 8) read_a<(T) + 1>(slot, NXT);          \
     else read_a<0>(nslot, s.pre);                                   \
     mfma_narrow<(T)>(s, CUR);                                       \
-    step_pattern();                                                 \
+    prep.template step<(T)>();                                      \
+    lazy_step_pattern();                                            \
     __builtin_amdgcn_sched_barrier(0);                              \
     if constexpr ((T) == 3) {                                       \
       chunk_barrier();                                              \
@@ -1068,11 +1152,6 @@ __device__ __forceinline__ void flush_gcode(const State& s, const FieldArgs& a, 
   }
 }
 
-// Training backward: the workgroup's bias-gradient row l (layer_dir2, layer_dir1, layer_xyz1) in LDS.
-__device__ __forceinline__ float* bias_row(float4* lds, int l) {
-  return reinterpret_cast<float*>(lds + kRing * kChunkQuads) + kBBias + 256 * l;
-}
-
 // Training backward: the masked input gradient of a layer (its dPre, what dW = dPre^T X reads) as
 // plane `plane` of a.dpre: 0 layer_dir2, 1 layer_dir1, 2 fc_out rows 1.. (d feat), 3 layer_xyz2,
 // 4 layer_xyz1.
@@ -1082,16 +1161,19 @@ struct DpreStore {
   const FieldArgs& a;
   int64_t tile;
   int plane;
-  // two blocks per chunk of a 256-wide layer (see chunk16); in the xyz1 layer's two narrow chunks
-  // (NARROW): eight per chunk, two per k-step 4..7
+  // two blocks per chunk of a 256-wide layer (see chunk16) -- at k-step 4, or with `late` (a lazily
+  // masked layer: the chunk's last values are masked during k-steps 4..6) at k-step 7, in the same
+  // place relative to the chunk's DMA; in the xyz1 layer's two narrow chunks (NARROW): eight per
+  // chunk, two per k-step 4..7 (the first chunk stores blocks it masked four k-steps earlier)
   bool narrow = false;
+  bool late = false;
   template <int CI, int T>
   __device__ __forceinline__ void step() const {
     if constexpr (TRAIN) {
       if (narrow) {
         if constexpr (T >= 4) store_plane<8 * CI + 2 * (T - 4), 2>(s, plane_rsrc(a.dpre, plane, a.m, tile), s.act);
-      } else if constexpr (T == 4) {
-        store_plane<2 * CI, 2>(s, plane_rsrc(a.dpre, plane, a.m, tile), s.act);
+      } else if constexpr (T == 4 || T == 7) {
+        if (late == (T == 7)) store_plane<2 * CI, 2>(s, plane_rsrc(a.dpre, plane, a.m, tile), s.act);
       }
     }
   }
@@ -1132,7 +1214,7 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   const SampleIn in = decode_sample<MODE>(a, rc);
   const int crow = __builtin_amdgcn_readfirstlane(static_cast<int>(code_row(a, in.code_of)));
   float4 dr = reinterpret_cast<const float4*>(a.d_raw)[rc];
-  const uint2 m_v2 = load_mask(s, a, tile, 3), m_v1 = load_mask(s, a, tile, 2);
+  const uint2 m_v2 = load_mask(s, a, tile, 3);
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   if (!valid) dr = make_float4(0.f, 0.f, 0.f, 0.f);
   // a.g_code NULL: the caller forms g_code from the dPre planes (deterministic column sums folded
@@ -1164,17 +1246,20 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   // ---- layer_dir2^T (m_v2), layer_dir1^T (m_v1)
   // (each layer's masked input gradient -- the dW GEMMs' dPre plane -- is stored at the layer's first
   // chunk barrier: DpreStore as chunk16's `post`)
-  mask_act(s, m_v2);
-  if (TRAIN && a.gbias[0]) gcode_add64<0>(s, bias_row(lds, 0), s.act);
+  // (masked lazily: MaskB; their stores late)
+  raw_act(s);
+  mask_one<0>(s, m_v2);
+  zero_acc(s);
+  const uint2 m_v1 = load_mask(s, a, tile, 2);
+  __builtin_amdgcn_sched_barrier(0);
+  layer256_masked(s, lds, c, m_v2, DpreStore<TRAIN>{s, a, tile, 0, false, true});
+  raw_act(s);
+  mask_one<0>(s, m_v1);
   zero_acc(s);
   __builtin_amdgcn_sched_barrier(0);
-  layer256(s, lds, c, DpreStore<TRAIN>{s, a, tile, 0});
-  const uint2 m_h2 = load_mask(s, a, tile, 1), m_h1 = load_mask(s, a, tile, 0);
-  mask_act(s, m_v1);
-  if (TRAIN && a.gbias[0]) gcode_add64<0>(s, bias_row(lds, 1), s.act);
-  zero_acc(s);
+  const uint2 m_h2 = load_mask(s, a, tile, 1);
   __builtin_amdgcn_sched_barrier(0);
-  layer256(s, lds, c, DpreStore<TRAIN>{s, a, tile, 1});
+  layer256_masked(s, lds, c, m_v1, DpreStore<TRAIN>{s, a, tile, 1, false, true});
   // ---- the view-direction rows of layer_dir1^T (narrow chunk, B = m_v1 . d v1 still in act)
 #pragma unroll
   for (int q = 0; q < 4; ++q) s.acc2[q] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -1214,6 +1299,7 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
 #pragma unroll
   for (int ob = 0; ob < 16; ++ob) s.act[ob] = s.acc[ob];
   if (gc) gcode_add64<kCbFeat>(s, grow, s.act);
+  const uint2 m_h1 = load_mask(s, a, tile, 0);
 #pragma unroll
   for (int ob = 0; ob < 16; ++ob) {
     const floatx4 w = *reinterpret_cast<const floatx4*>(clds + kTSig + 64 * fresh(s.g) + 4 * ob);
@@ -1221,21 +1307,34 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   }
   __builtin_amdgcn_sched_barrier(0);
   layer256(s, lds, c, DpreStore<TRAIN>{s, a, tile, 2});
-  // ---- layer_xyz2^T (m_h2): its masked input gradient is the code term's too
-  mask_act(s, m_h2);
-  if (gc) gcode_add64<kCbXyz2>(s, grow, s.act);
+  // ---- layer_xyz2^T (m_h2): its masked input gradient is the code term's too (g_code in the kernel:
+  // masked here at once for the row sums; the lazy masking then finds every value masked already)
+  if (gc) {
+    mask_act(s, m_h2);
+    gcode_add64<kCbXyz2>(s, grow, s.act);
+  } else {
+    raw_act(s);
+    mask_one<0>(s, m_h2);
+  }
   zero_acc(s);
   __builtin_amdgcn_sched_barrier(0);
-  layer256(s, lds, c, DpreStore<TRAIN>{s, a, tile, 3});
-  // ---- layer_xyz1^T (m_h1): encoding k-steps 0-7, then 8-15
-  mask_act(s, m_h1);
-  if (TRAIN && a.gbias[0]) gcode_add64<0>(s, bias_row(lds, 2), s.act);
+  layer256_masked(s, lds, c, m_h2, DpreStore<TRAIN>{s, a, tile, 3, false, true});
+  // ---- layer_xyz1^T (m_h1): encoding k-steps 0-7, then 8-15 (masked lazily in the first chunk)
+  raw_act(s);
+  mask_one<0>(s, m_h1);
+  mask_one<1>(s, m_h1);
+  mask_one<2>(s, m_h1);
+  mask_one<3>(s, m_h1);
+  mask_one<4>(s, m_h1);
+  mask_one<5>(s, m_h1);
+  mask_one<6>(s, m_h1);
+  mask_one<7>(s, m_h1);
   float genc[16];
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) s.acc2[q] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
-    if (half == 0) chunk_narrow<0>(s, lds, c, DpreStore<TRAIN>{s, a, tile, 4, true});
+    if (half == 0) chunk_narrow<0>(s, lds, c, DpreStore<TRAIN>{s, a, tile, 4, true}, NarrowMask{s, m_h1, true});
     else chunk_narrow<1>(s, lds, c, DpreStore<TRAIN>{s, a, tile, 4, true});
     c += 1;
 #pragma unroll
@@ -1351,14 +1450,6 @@ __global__ __launch_bounds__(kThreads, 2) void field_w16_bwd_kernel(FieldArgs a)
 #endif
   __builtin_amdgcn_s_waitcnt(0x0F70);
   if (cur_code >= 0) flush_gcode(s, a, grow, cur_code);
-  if constexpr (TRAIN) {
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's (asm) bias atomics landed
-    __syncthreads();                     // ... and every other wave's
-    for (int k = threadIdx.x; k < 3 * 256; k += kThreads) {
-      const float v = blds[kBBias + k];
-      if (v != 0.0f && a.gbias[k >> 8]) atomicAdd(a.gbias[k >> 8] + (k & 255), v);
-    }
-  }
 }
 
 }  // namespace w16
