@@ -234,12 +234,8 @@ def gather_rows(rows: torch.Tensor, per: List[int], rank: int) -> Optional[torch
         dist.all_gather_into_tensor(allrows, padded)
         parts = list(allrows.split(width))
     else:
-        # gloo (the reference's init_process default): its all_gather takes host tensors only, so
-        # device rows are staged through host memory and the result returns to the rows' device
-        host = padded.cpu() if padded.is_cuda else padded
-        parts = [torch.zeros_like(host) for _ in range(world)]
-        dist.all_gather(parts, host)
-        parts = [p.to(rows.device) for p in parts] if padded.is_cuda and rank == 0 else parts
+        parts = [torch.zeros_like(padded) for _ in range(world)]
+        dist.all_gather(parts, padded)
     if rank != 0:
         return None
     return torch.cat([p[: per[i]] for i, p in enumerate(parts)], dim=0)

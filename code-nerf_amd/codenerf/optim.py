@@ -267,7 +267,7 @@ class AdamW(torch.optim.Optimizer):
         # touched keeps grad None, so step() skips it exactly as torch's AdamW would)
         flags = torch.tensor([0 if p in missing else 1 for p in params], dtype=torch.int32,
                              device=self._flat["grad"].device)
-        _all_reduce(flags, dist.ReduceOp.SUM, group)
+        dist.all_reduce(flags, op=dist.ReduceOp.SUM, group=group)
         anywhere = flags.cpu().tolist()
         for p, cnt in zip(params, anywhere):
             if p in missing:
@@ -279,28 +279,11 @@ class AdamW(torch.optim.Optimizer):
         if dist.get_backend(group) == dist.Backend.NCCL:
             dist.all_reduce(grad, op=dist.ReduceOp.AVG, group=group)
         else:
-            _all_reduce(grad, dist.ReduceOp.SUM, group)
+            dist.all_reduce(grad, op=dist.ReduceOp.SUM, group=group)
             grad.div_(world)
 
     def broadcast_params(self, src: int = 0, group=None) -> None:
         """Start every replica from rank ``src``'s parameters (DDP's construction-time
         broadcast): one broadcast of the flat parameter buffer."""
         if dist.is_available() and dist.is_initialized():
-            flat = self._flat["param"]
-            if dist.get_backend(group) != dist.Backend.NCCL and flat.is_cuda:
-                host = flat.cpu()                 # gloo: host tensors (see _all_reduce)
-                dist.broadcast(host, src=src, group=group)
-                flat.copy_(host)
-            else:
-                dist.broadcast(flat, src=src, group=group)
-
-
-def _all_reduce(t: torch.Tensor, op, group=None) -> None:
-    """dist.all_reduce; on a non-NCCL group (gloo: the reference's init_process default) device
-    tensors are staged through host memory, which every gloo build accepts."""
-    if dist.get_backend(group) != dist.Backend.NCCL and t.is_cuda:
-        host = t.cpu()
-        dist.all_reduce(host, op=op, group=group)
-        t.copy_(host)
-    else:
-        dist.all_reduce(t, op=op, group=group)
+            dist.broadcast(self._flat["param"], src=src, group=group)

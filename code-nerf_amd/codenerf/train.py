@@ -32,7 +32,7 @@ import torch.distributed as dist
 
 from . import nerf
 from .models import CodeNeRFModel, ShapeTextureEmbedding, get_params_tensor
-from .optim import AdamW, _all_reduce
+from .optim import AdamW
 from .autograd import render_loss_autograd
 from .utils import get_minibatches, mse2psnr
 
@@ -77,9 +77,7 @@ def broadcast_parameters(models, src: int = 0) -> None:
     starts from rank ``src``'s parameters (one coalesced broadcast)."""
     params = [p for m in models.values() for p in m.parameters()]
     flat = torch.cat([p.detach().reshape(-1) for p in params])
-    host = flat.cpu() if dist.get_backend() != dist.Backend.NCCL and flat.is_cuda else flat
-    dist.broadcast(host, src=src)                # (gloo: staged through host memory)
-    flat = host.to(flat.device)
+    dist.broadcast(flat, src=src)
     o = 0
     with torch.no_grad():
         for p in params:
@@ -97,8 +95,8 @@ def _average_gradients(optimizer, models) -> None:
     dev = params[0].device
     flat = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in params])
     flags = torch.tensor([int(p.grad is not None) for p in params], dtype=torch.int32, device=dev)
-    _all_reduce(flags, dist.ReduceOp.SUM)
-    _all_reduce(flat, dist.ReduceOp.SUM)
+    dist.all_reduce(flags)
+    dist.all_reduce(flat)
     flat.div_(dist.get_world_size())
     o = 0
     for p, cnt in zip(params, flags.cpu().tolist()):

@@ -23,9 +23,14 @@ RAW_RTOL = 1e-5
 # the t3 net (tools/x3w_err.py), so their raw-output bound is 1.5e-5 (rendered outputs keep 1e-4)
 RAW_RTOL_X3 = 1.5e-5
 PRECISIONS = ["f32", "f32_v1", "bf16x3", "bf16x3_w16"]
-# C5 at-size gradient bound (max |g - g_ref| over the tensor's largest |g_ref|; d theta / phi / rho
-# relative to max(1e-2, |g_ref|)); the achieved values are recorded (conftest.margin)
-C5_GRAD_RTOL = {"f32": 2e-3, "bf16x3": 2e-3}
+# C5 at-size gradient bounds (max |g - g_ref| over the tensor's largest |g_ref|; d theta / phi / rho
+# relative to max(1e-2, |g_ref|)), about twice the achieved values (r04b, profiles/r04): the pose and
+# code gradients at <= 4.7e-5, so 1e-4; the weight gradients (not frozen): fine fc_rgb 3.9e-6 and the
+# norms 2.7e-5 against 1e-4, coarse layer_xyz1 3.2e-4 -- its input is the encodings of every sample,
+# where the fine depths that moved across a bin (test_train_c3_decisions_at_size counts them for the
+# C3 step) enter directly
+C5_GRAD_RTOL = {"f32": 1e-4, "bf16x3": 1e-4}
+C5_XYZ1_RTOL = 6.5e-4
 
 
 def model_from(dev, params, precision):
@@ -226,11 +231,11 @@ def test_eval_c5_step_at_size(dev, frozen, precision):
         ref = g["g_" + name].cpu()
         margin(tag, "d " + name, (t.grad.cpu() - ref).abs().max().item() / ref.abs().max().item(), rtol)
     if not frozen:
-        for what, t, key in [("fine fc_rgb.weight", models["nerf_fine"].fc_rgb.weight, "g_fine_fc_rgb_w"),
-                             ("coarse layer_xyz1.weight", models["nerf_coarse"].layer_xyz1.weight,
-                              "g_coarse_layer_xyz1_w")]:
+        for what, t, key, bound in [("fine fc_rgb.weight", models["nerf_fine"].fc_rgb.weight, "g_fine_fc_rgb_w", rtol),
+                                    ("coarse layer_xyz1.weight", models["nerf_coarse"].layer_xyz1.weight,
+                                     "g_coarse_layer_xyz1_w", C5_XYZ1_RTOL)]:
             ref = g[key].cpu()
-            margin(tag, "d " + what, (t.grad.cpu() - ref).abs().max().item() / ref.abs().max().item(), rtol)
+            margin(tag, "d " + what, (t.grad.cpu() - ref).abs().max().item() / ref.abs().max().item(), bound)
         worst = (0.0, "")
         for key, mm in models.items():
             for nm, prm in mm.named_parameters():

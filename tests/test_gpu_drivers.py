@@ -80,7 +80,9 @@ def test_train_resume_mid_iteration_with_validation(tree, tmp_path):
     draw, the generators are those after the save step's validation."""
     from codenerf.train import train
     dev = torch.device("cuda", 0)
-    kw = dict(iterations=4, save_every=4, validate_every=4, val_iterations=2)
+    # iterations >= 6: validate picks the val loader's SIXTH batch (eval.py:103-109), and the loader
+    # yields ``iterations`` of them (util.py:59-90)
+    kw = dict(iterations=6, save_every=4, validate_every=4, val_iterations=2)
 
     def cfg(name, **extra):
         c = _cfg(tree, str(tmp_path / name), **kw)
@@ -88,22 +90,23 @@ def test_train_resume_mid_iteration_with_validation(tree, tmp_path):
         return c | extra
 
     full = train(0, cfg("full"), device=dev, verbose=False)
-    assert full["num_logs"] == 8 and len(full["validation"]) == 1
+    assert full["num_logs"] == 12 and [v["iteration"] for v in full["validation"]] == [4, 8]
     assert set(full["validation"][0]) >= {"iteration", "loss", "psnr", "pose_error"}
     names = [os.path.basename(p) for p in full["checkpoints"]]
-    assert names == ["checkpoint    3.ckpt", "checkpoint    4.ckpt"], names   # i == iterations-1, i % 4
-    ck3 = torch.load(full["checkpoints"][0], weights_only=True)
-    ck4 = torch.load(full["checkpoints"][1], weights_only=True)
-    assert ck3["cn_cursor"].tolist() == [2, 0] and ck3["cn_next_iter"] == 2
+    # i % save_every == 0 and i == iterations - 1 (train.py:129, i counts chunks)
+    assert names == ["checkpoint    4.ckpt", "checkpoint    5.ckpt", "checkpoint    8.ckpt"], names
+    ck4, ck5 = (torch.load(p, weights_only=True) for p in full["checkpoints"][:2])
     assert ck4["cn_cursor"].tolist() == [2, 1] and "cn_next_iter" not in ck4 and ck4["iter"] == 2
+    assert ck5["cn_cursor"].tolist() == [3, 0] and ck5["cn_next_iter"] == 3
     a = _params(full)
-    for path, first in ((full["checkpoints"][1], 5), (full["checkpoints"][0], 4)):
+    # after chunk 0 of iteration 2 (with that step's validation), after an iteration's last chunk
+    for path, first in ((full["checkpoints"][0], 5), (full["checkpoints"][1], 6)):
         res = train(0, cfg("res" + str(first), load_checkpoint=path), device=dev, verbose=False)
         assert res["logs"] == full["logs"][first:], first
         b = _params(res)
         for k in a:
             assert torch.equal(a[k], b[k]), (first, k)
-        assert res["scheduler"].last_epoch == full["scheduler"].last_epoch == 8
+        assert res["scheduler"].last_epoch == full["scheduler"].last_epoch == 12
 
 
 def test_train_checkpoint_cadence_and_reference_format(tree, tmp_path):

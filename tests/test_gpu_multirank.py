@@ -2,8 +2,8 @@
 "what's missing" 2): two freshly spawned processes (start_method "spawn", as bench.py and
 codenerf.train.launch start ranks) form a world-size-2 gloo group, both on the test box's one GPU
 (RCCL refuses two ranks on one device; on a node every rank has its own GPU and the group is RCCL).
-gloo's collectives take host tensors: the product stages device tensors through host memory on a
-gloo group (codenerf.nerf.gather_rows, codenerf.optim._all_reduce).
+This torch build's gloo takes device tensors in every collective the product uses (tools/gloo_probe.py,
+profiles/r04/gloo_probe.jsonl), so the product code runs unchanged on the gloo group.
 
 (a) parallel_image_render (nerf/__init__.py:137-226) of C4 chairs with 2 ranks: rank 0's gathered
     image vs the reference's 2-rank image (render_chairs.npz ``n2_rgb``) at 1e-4;

@@ -225,6 +225,10 @@ def test_forward_pass_q1(dev, precision, r, s):
 # mlp_common.h); past it the wave evaluates every pair with sincosf up front.  Raw outputs with
 # |x| ~ 100 are larger, so the bound is relative to the largest |raw| (as test_trained_mlp's).
 LARGE_ARG_RTOL = {"f32": 1e-5, "f32_v1": 1e-5, "bf16x3": 1.5e-5, "bf16x3_w16": 1.5e-5}
+# the training forwards' first activation plane: h1 = relu(layer_xyz1(enc)) with the raw point among
+# its inputs (|x| ~ 180 here), so 3xbf16's ~2^-17 relative error per product reaches 1.5e-5 of the
+# plane's largest value (r04b: 1.52e-5 for bf16x3, 7.8e-7 for fp32)
+LARGE_ARG_H1_RTOL = {"f32": 2e-6, "bf16x3": 3e-5}
 
 
 def _large_arg_case(case, r, s, seed):
@@ -291,7 +295,7 @@ def test_field_large_arguments_training(dev, train_precision, case, mode):
     # the first saved plane is h1 = relu(layer_xyz1(enc)): the encodings' own consumer
     h1 = torch.relu(pre["h1"]) if "h1" in pre else None
     if h1 is not None:
-        margin(tag, "h1 plane rel", maxdiff(saved[0], h1) / h1.abs().max().item(), rt)
+        margin(tag, "h1 plane rel", maxdiff(saved[0], h1) / h1.abs().max().item(), LARGE_ARG_H1_RTOL[train_precision])
 
 
 # ---------------------------------------------------------------- rendering

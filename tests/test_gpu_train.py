@@ -299,7 +299,9 @@ def test_host_id_lookup_bitwise(dev, mixed):
     """The production embedding lookups (codenerf.train hands each chunk's ids over from the host:
     one object -> _TableRow views writing the optimiser's gradient slot; several -> host unique +
     device searchsorted) against the torch.unique lookup: after three chunk steps every gradient
-    and every parameter -- the code tables included -- is bit-identical."""
+    and every parameter -- the code tables included -- is bit-identical for one-object chunks (the
+    deterministic step); with several objects per chunk the code gradients are float-atomic sums
+    (DESIGN.md section 4), so the two agree to fp32 reassociation."""
     from codenerf import train as T
     from codenerf.nerf import PointSampler
     runs = []
@@ -329,9 +331,15 @@ def test_host_id_lookup_bitwise(dev, mixed):
     for a, b in zip(g0, g1):
         assert a.keys() == b.keys()
         for k in a:
-            assert torch.equal(a[k], b[k]), ("grad", k)
+            if mixed:
+                close(b[k], a[k], 1e-5, ("grad", k))
+            else:
+                assert torch.equal(a[k], b[k]), ("grad", k)
     for k in p0:
-        assert torch.equal(p0[k], p1[k]), ("param", k)
+        if mixed:
+            assert (p0[k] - p1[k]).abs().max().item() <= 2.05 * 3 * 1e-3, ("param", k)   # 3 steps, |step| <= lr
+        else:
+            assert torch.equal(p0[k], p1[k]), ("param", k)
 
 
 def test_train_iteration_runs(dev):
@@ -392,11 +400,15 @@ def test_train_minibatch_deterministic(dev):
         assert torch.equal(runs[0][k], runs[1][k]), k
 
 
-# C3 at-size bounds (max |g - g_ref| relative to the tensor's largest |g_ref|; projections relative
-# to the tensor's norm), per precision; the achieved values are recorded (conftest.margin)
-C3_GRAD_RTOL = {"f32": 2e-3, "bf16x3": 5e-3}
-C3_PROJ_RTOL = {"f32": 2e-3, "bf16x3": 5e-3}
-C3_STEP_PROJ = 2e-2
+# C3 at-size bounds, per precision, at about twice the achieved error (profiles/r04/parity_margins.json):
+# max |g - g_ref| relative to the tensor's largest |g_ref| (full tensors), projections relative to the
+# tensor's norm, post-step projections relative to lr sqrt(n).  They sit above GRAD_RTOL (2e-4) because
+# the run is independent of the reference's discrete decisions: test_train_c3_decisions_at_size counts
+# the fine depths and ReLU decisions that differ and shows that with the kernels' decisions the
+# reference's arithmetic (the oracle) matches every gradient at GRAD_RTOL.
+C3_GRAD_RTOL = {"f32": 1e-3, "bf16x3": 1.4e-3}
+C3_PROJ_RTOL = {"f32": 1.2e-3, "bf16x3": 3.8e-3}
+C3_STEP_PROJ = {"f32": 6e-3, "bf16x3": 2.7e-2}
 
 
 def _proj_directions(idx, shape):
@@ -409,6 +421,37 @@ def _proj(r, t):
 
 
 _C3_RESULTS = {}
+C3_OBJECTS = 2458
+C3_IDS = [17, 1234]
+
+
+def _c3_setup(dev, precision):
+    """train_c3.npz's chunk step inputs (make_golden.py gen_c3train): the models before the step, the
+    optimiser, the reference's stratified / fine uniforms, the point sampler."""
+    from codenerf import synthetic, train as T
+    from codenerf.models import CodeNeRFModel, ShapeTextureEmbedding
+    from codenerf.nerf import PointSampler
+    from test_gpu_parity import load
+    g = load("train_c3.npz", dev)
+    emb_t = ShapeTextureEmbedding(C3_OBJECTS, 256, 256)
+    with torch.no_grad():
+        emb_t.shape_embedding.weight.copy_(synthetic.latent_codes(40, C3_OBJECTS))
+        emb_t.texture_embedding.weight.copy_(synthetic.latent_codes(41, C3_OBJECTS))
+    models = {"embedding": emb_t.to(dev)}
+    for key, seed in (("nerf_coarse", 0), ("nerf_fine", 1)):
+        m = CodeNeRFModel(hidden_size=256, shape_code_size=256, texture_code_size=256, num_encoding_fn_xyz=10,
+                          num_encoding_fn_dir=4)
+        m.load_state_dict(synthetic.codenerf_params(seed))
+        models[key] = m.to(dev)
+        m.precision = m.train_precision = precision
+    opt, sched = T.prepare_optimizer(_opt_cfg(), models)
+    torch.manual_seed(4343)
+    t_rand, u = torch.rand(4096, 64), torch.rand(4096, 64)
+    assert torch.equal(t_rand[:4].to(dev), g["t_rand_head"]) and torch.equal(u[:4].to(dev), g["u_head"])
+    assert abs(t_rand.double().sum().item() - g["t_rand_sum"].item()) < 0.02   # stored as float32
+    assert abs(u.double().sum().item() - g["u_sum"].item()) < 0.02
+    ps = PointSampler(64, 64, 0.8, 1.8, spacing_mode="lindepth", perturb=True, dtype=torch.float32, device=dev)
+    return g, models, opt, sched, t_rand, u, ps
 
 
 @pytest.mark.parametrize("host_ids", [False, True])
@@ -420,36 +463,15 @@ def test_train_c3_chunk_at_size(dev, precision, host_ids):
     gradients and post-step values in full; for nerf_coarse five tensors in full and 16 seeded
     projections of EVERY tensor's gradient and post-step change; the two touched code rows'
     gradients and values, every untouched row only decayed.  ``host_ids``: the chunk's object ids
-    also handed over from the host (``_cn_host_ids``, as train_iteration does: the production
-    lookup) -- the result must equal the device-id path bit for bit.  Achieved errors are recorded
-    (conftest.margin)."""
-    from codenerf import synthetic, train as T
-    from codenerf.models import CodeNeRFModel, ShapeTextureEmbedding
-    from codenerf.nerf import PointSampler
+    also handed over from the host (``_cn_host_ids``, as train_iteration does); with two objects in
+    the chunk the code gradients are float-atomic sums (determinism scope), so
+    the two lookups agree to fp32 reassociation, not bit for bit.  Achieved errors are recorded
+    (conftest.margin), per tensor for the full ones."""
+    from codenerf import train as T
     from conftest import margin
-    from test_gpu_parity import load
     tag = f"c3_train[{precision}{',host_ids' if host_ids else ''}]"
-    g = load("train_c3.npz", dev)
-    n_obj = 2458
-    emb_t = ShapeTextureEmbedding(n_obj, 256, 256)
-    with torch.no_grad():
-        emb_t.shape_embedding.weight.copy_(synthetic.latent_codes(40, n_obj))
-        emb_t.texture_embedding.weight.copy_(synthetic.latent_codes(41, n_obj))
-    models = {"embedding": emb_t.to(dev)}
-    for key, seed in (("nerf_coarse", 0), ("nerf_fine", 1)):
-        m = CodeNeRFModel(hidden_size=256, shape_code_size=256, texture_code_size=256, num_encoding_fn_xyz=10,
-                          num_encoding_fn_dir=4)
-        m.load_state_dict(synthetic.codenerf_params(seed))
-        models[key] = m.to(dev)
-        m.precision = m.train_precision = precision
+    g, models, opt, sched, t_rand, u, ps = _c3_setup(dev, precision)
     before = {f"{k}.{n}": p.detach().clone() for k, m in models.items() for n, p in m.named_parameters()}
-    opt, sched = T.prepare_optimizer(_opt_cfg(), models)
-    torch.manual_seed(4343)
-    t_rand, u = torch.rand(4096, 64), torch.rand(4096, 64)
-    assert torch.equal(t_rand[:4].to(dev), g["t_rand_head"]) and torch.equal(u[:4].to(dev), g["u_head"])
-    assert abs(t_rand.double().sum().item() - g["t_rand_sum"].item()) < 0.02   # stored as float32
-    assert abs(u.double().sum().item() - g["u_sum"].item()) < 0.02
-    ps = PointSampler(64, 64, 0.8, 1.8, spacing_mode="lindepth", perturb=True, dtype=torch.float32, device=dev)
     ids_t = g["ids"].long()
     if host_ids:
         ids_t._cn_host_ids = g["ids"].long().cpu().numpy()
@@ -462,8 +484,9 @@ def test_train_c3_chunk_at_size(dev, precision, host_ids):
         margin(tag, "loss " + k, abs(float(v) - g[k].item()), 1e-5 * max(1.0, abs(g[k].item())))
     rtol, prtol = C3_GRAD_RTOL[precision], C3_PROJ_RTOL[precision]
     named = {f"{k}.{n}": p for k, m in models.items() for n, p in m.named_parameters()}
-    ids = [17, 1234]
+    ids = C3_IDS
     worst = {"grad": (0.0, ""), "proj": (0.0, ""), "firm_step": (0.0, ""), "step_proj": (0.0, "")}
+    per_tensor = {}
     flips = 0
     for idx, k in enumerate(sorted(named)):
         p = named[k]
@@ -477,7 +500,7 @@ def test_train_c3_chunk_at_size(dev, precision, host_ids):
             fs, nf = _post_step(p.detach()[ids], g["prows_" + k], ref, 1e-3, rtol)
             margin(tag, "touched rows firm post-step " + k, fs, 1e-6)
             flips += nf
-            mask = torch.ones(n_obj, dtype=torch.bool, device=dev)
+            mask = torch.ones(C3_OBJECTS, dtype=torch.bool, device=dev)
             mask[ids] = False
             decayed = before[k][mask] * (1 - 1e-3 * 1e-2)
             assert (p.detach()[mask] - decayed).abs().max().item() <= 1e-7, k
@@ -486,6 +509,7 @@ def test_train_c3_chunk_at_size(dev, precision, host_ids):
         if "g_" + k in g:                                    # full tensors
             ref = g["g_" + k]
             e = (p.grad - ref).abs().max().item() / max(ref.abs().max().item(), 1e-12)
+            per_tensor[k] = e
             worst["grad"] = max(worst["grad"], (e, k))
             fs, nf = _post_step(p.detach(), g["p_" + k], ref, lr, rtol)
             worst["firm_step"] = max(worst["firm_step"], (fs, k))
@@ -498,16 +522,22 @@ def test_train_c3_chunk_at_size(dev, precision, host_ids):
         # scale is lr sqrt(n); only elements whose gradient sign is undetermined at rtol can differ
         dp = (_proj(r, p.detach() - before[k]) - g["pproj_" + k].cpu()).abs().max().item()
         worst["step_proj"] = max(worst["step_proj"], (dp / (lr * p.numel() ** 0.5), k))
-    margin(tag, "grad full tensors (worst: %s)" % worst["grad"][1], worst["grad"][0], rtol)
+    margin(tag, "grad full tensors (worst: %s)" % worst["grad"][1], worst["grad"][0], rtol,
+           per_tensor={k: float(f"{v:.3e}") for k, v in per_tensor.items()},
+           above_grad_rtol=sorted(k for k, v in per_tensor.items() if v > GRAD_RTOL))
     margin(tag, "grad projections (worst: %s)" % worst["proj"][1], worst["proj"][0], prtol)
     margin(tag, "firm post-step (worst: %s)" % worst["firm_step"][1], worst["firm_step"][0], 1e-6,
            sign_undetermined_elements=flips)
-    margin(tag, "post-step projections (worst: %s)" % worst["step_proj"][1], worst["step_proj"][0], C3_STEP_PROJ)
+    margin(tag, "post-step projections (worst: %s)" % worst["step_proj"][1], worst["step_proj"][0],
+           C3_STEP_PROJ[precision])
     assert sched.last_epoch == 1
     if host_ids and precision in _C3_RESULTS:          # the device-id case ran first (parametrize order)
+        e = 0.0
         for k, p in named.items():
             a, b = _C3_RESULTS[precision][k]
-            assert torch.equal(a, p.grad) and torch.equal(b, p.detach()), ("host-id vs device-id lookup", k)
+            e = max(e, (a - p.grad).abs().max().item() / max(a.abs().max().item(), 1e-30))
+            assert (b - p.detach()).abs().max().item() <= 2.05 * (1e-3 if k.startswith("embedding.") else 1e-4), k
+        margin(tag, "host-id vs device-id lookup (two objects: float-atomic code sums)", e, 1e-5)
     elif not host_ids:
         _C3_RESULTS[precision] = {k: (p.grad.detach().clone(), p.detach().clone()) for k, p in named.items()}
 
@@ -522,3 +552,106 @@ def _post_step(got, ref, g_ref, lr, rtol):
     firm = g_ref.abs() > max(1e-6, 10 * rtol * g_ref.abs().max().item())
     assert d.max().item() <= 2.05 * lr, d.max().item()
     return (d[firm].max().item() if firm.any() else 0.0), int(((~firm) & (d > 1e-6)).sum().item())
+
+
+def test_train_c3_decisions_at_size(dev, monkeypatch):
+    """Why the at-size C3 bounds sit above GRAD_RTOL, with counts: the same chunk step (fp32) also
+    run by the oracle (the reference's op sequence on the CPU, pinned by the fixture itself here) on
+    its OWN discrete decisions and on the KERNELS' -- fine depths from sample_pdf and ReLU masks read
+    from the saved activation planes.  (1) the oracle's own run reproduces the reference's gradients
+    (the oracle is the reference at size); (2) the kernels' decisions that differ from the oracle's --
+    fine depths, ReLU signs -- are counted, every differing ReLU inside the fp32 band of its
+    pre-activation; (3) fed those decisions, the oracle matches every kernel gradient at GRAD_RTOL;
+    so the at-size gaps are the moved decisions, not the arithmetic."""
+    from codenerf import ops, train as T
+    from conftest import margin
+    o = O()
+    seen = {"z_fine": None, "w_coarse": None, "saved": []}
+    real_pdf, real_w16 = ops.sample_pdf, ops.radiance_field_train_w16
+
+    def spy_pdf(*a, **k):
+        r = real_pdf(*a, **k)
+        seen["z_fine"] = r[1].detach().cpu()
+        seen["w_coarse"] = a[2].detach().cpu().clone()
+        return r
+
+    def spy_w16(*a, **k):
+        raw, saved, masks = real_w16(*a, **k)
+        sv = saved.detach()
+        seen["saved"].append({name: (sv[i] > 0).cpu().float() for name, i in (("h1", 0), ("h2", 1), ("v1", 3), ("v2", 4))})
+        return raw, saved, masks
+    monkeypatch.setattr(ops, "sample_pdf", spy_pdf)
+    monkeypatch.setattr(ops, "radiance_field_train_w16", spy_w16)
+    g, models, opt, sched, t_rand, u, ps = _c3_setup(dev, "f32")
+    snap = {"pc": oracle_params(models["nerf_coarse"]), "pf": oracle_params(models["nerf_fine"]),
+            "ts": models["embedding"].shape_embedding.weight.detach().cpu().clone(),
+            "tt": models["embedding"].texture_embedding.weight.detach().cpu().clone()}
+    T.train_minibatch(models, opt, sched, ps, embedders(dev), g["ro"], g["rd"], g["ids"].long(), g["target"], 1e-5,
+                      uniforms=(t_rand.to(dev), u.to(dev)))
+    torch.cuda.synchronize()
+    assert len(seen["saved"]) == 2, "the fused fp32 training forward ran for both fields"
+    got = {f"{key}.{name}": prm.grad.detach().cpu() for key in ("nerf_coarse", "nerf_fine")
+           for name, prm in models[key].named_parameters()}
+    got["shape table"] = models["embedding"].shape_embedding.weight.grad[C3_IDS].cpu()
+    got["texture table"] = models["embedding"].texture_embedding.weight.grad[C3_IDS].cpu()
+    ro, rd, ids, tgt = g["ro"].cpu(), g["rd"].cpu(), g["ids"].long().cpu(), g["target"].cpu()
+    smp, ecfg = o.Sampling(64, 64, 0.8, 1.8), o.EmbedCfg()
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+
+    def oracle_step(masks_c=None, masks_f=None, z_f=None, pre_c=None, pre_f=None):
+        pc = {k: v.detach().clone().requires_grad_(True) for k, v in snap["pc"].items()}
+        pf = {k: v.detach().clone().requires_grad_(True) for k, v in snap["pf"].items()}
+        ts, tt = snap["ts"].clone().requires_grad_(True), snap["tt"].clone().requires_grad_(True)
+        zs, zt = ts[ids], tt[ids]
+        pts_c, z_c = o.sample_uniform(ro, rd, smp.bins, t_rand)
+        rgb_c, _, _, w_c, _ = o.volume_render(o.forward_pass(pc, ecfg, rd, pts_c, zs, zt, masks_c, pre_c), z_c, rd)
+        if z_f is None:
+            z_f = o.sample_pdf(ro, rd, w_c.detach()[..., 1:-1], z_c, 64, u)[1]
+        pts_f = ro[..., None, :] + rd[..., None, :] * z_f[..., :, None]
+        rgb_f = o.volume_render(o.forward_pass(pf, ecfg, rd, pts_f, zs, zt, masks_f, pre_f), z_f, rd)[0]
+        lc = torch.nn.functional.mse_loss(rgb_c[..., :3], tgt[..., :3])
+        lf = torch.nn.functional.mse_loss(rgb_f[..., :3], tgt[..., :3])
+        loss = lc + lf + 1e-5 * (torch.norm(ts.detach(), p=2) + torch.norm(tt.detach(), p=2))
+        loss.backward()
+        out = {f"nerf_coarse.{k}": v.grad for k, v in pc.items()}
+        out.update({f"nerf_fine.{k}": v.grad for k, v in pf.items()})
+        out["shape table"], out["texture table"] = ts.grad[C3_IDS], tt.grad[C3_IDS]
+        return out, z_f, w_c.detach(), z_c
+
+    # 1. the oracle on its own decisions IS the reference at size
+    pre_c, pre_f = {}, {}
+    own, z_own, w_own, z_c = oracle_step(pre_c=pre_c, pre_f=pre_f)
+    e_ref = 0.0
+    for k in own:
+        key = "g_" + k if ("g_" + k) in g else None
+        if key is not None:
+            ref = g[key].cpu()
+            e_ref = max(e_ref, (own[k] - ref).abs().max().item() / ref.abs().max().item())
+    margin("c3_decisions[f32]", "oracle (own decisions) vs reference, full tensors", e_ref, 2e-5)
+    # 2. the kernels' discrete decisions against the oracle's
+    assert (seen["w_coarse"] - w_own[..., 1:-1]).abs().max().item() <= 1e-5
+    assert torch.equal(o.sample_pdf(ro, rd, seen["w_coarse"], z_c, 64, u)[1], seen["z_fine"])
+    z_dis = int((seen["z_fine"] != z_own).sum())
+    z_far = int(((seen["z_fine"] - z_own).abs() > 1e-4).sum())
+    pre_f_k = {}
+    oracle_step(z_f=seen["z_fine"], pre_f=pre_f_k)
+    n_dis_c = check_mask_agreement(seen["saved"][0], pre_c, MASK_BAND["f32"], "coarse")
+    n_dis_f = check_mask_agreement(seen["saved"][1], pre_f_k, MASK_BAND["f32"], "fine")
+    # 3. fed the kernels' decisions, the oracle matches every gradient at GRAD_RTOL
+    fed = oracle_step(seen["saved"][0], seen["saved"][1], seen["z_fine"])[0]
+    worst, worst_own = (0.0, ""), (0.0, "")
+    for k in got:
+        scale = fed[k].abs().max().item()
+        e = (got[k].double() - fed[k].double()).abs().max().item() / max(scale, 1e-30)
+        worst = max(worst, (e, k))
+        e_own = (got[k].double() - own[k].double()).abs().max().item() / max(own[k].abs().max().item(), 1e-30)
+        worst_own = max(worst_own, (e_own, k))
+        explained_by_kinks(got[k], own[k], fed[k], k)
+    n_samples = {"coarse": 4096 * 64, "fine": 4096 * 128}
+    margin("c3_decisions[f32]", "kernels vs oracle on the kernels' decisions (worst: %s)" % worst[1], worst[0],
+           GRAD_RTOL, fine_depths_differing=z_dis, fine_depths_differing_over_1em4=z_far,
+           fine_depths=4096 * 128, relu_decisions_differing_coarse=n_dis_c,
+           relu_decisions_differing_fine=n_dis_f, relu_decisions_coarse=4 * 256 * n_samples["coarse"],
+           relu_decisions_fine=4 * 256 * n_samples["fine"])
+    margin("c3_decisions[f32]", "kernels vs oracle on its own decisions (worst: %s)" % worst_own[1], worst_own[0],
+           C3_GRAD_RTOL["f32"])
