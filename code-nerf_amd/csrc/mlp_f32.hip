@@ -156,6 +156,7 @@ struct State {
   floatx4 act[16];   // layer input: block ob register r = input feature 16 ob + 4 g + r
   floatx4 acc[16];   // layer output accumulators
   floatx4 pre[4];    // the next chunk's first A fragments (read during this chunk's last k-step)
+  unsigned mw[2];    // forward: the ReLU mask words of the layer input being activated (LazyAct)
   floatx4 acc2[4];   // backward: the narrow chunks' accumulators (2 blocks x 2 chains)
   float denc[8];     // view-direction encoding, k-steps of the view-dir chunk
   float sig;         // sigma partial (this lane group's 64 features)
@@ -450,8 +451,11 @@ __device__ __forceinline__ void bias_code(State& s, const FieldArgs& a, const fl
   }
 }
 
-// ReLU masks for the fused backward: 4 layers (h1, h2, v1, v2) x 64 bits per lane (bit 4 ob + r
-// of feature 16 ob + 4 g + r: pre-activation > 0), one 8-B store per lane per layer.
+// ReLU masks for the fused backward: 4 layers (h1, h2, v1, v2) x 64 bits per lane (value t = 4 ob + r,
+// feature 16 ob + 4 g + r, pre-activation > 0: bit 31 - (t & 31) of word t >> 5), one 8-B store per
+// lane per layer.  The words are built by shifting left one bit per value in increasing t: a constant
+// 1 << n per bit would be a VOP3 literal, which gfx9 encodings lack, so the compiler kept them all in
+// VGPRs across the tile loop.
 constexpr int kMaskLayers = 4;
 constexpr int kMaskWordsPerTile = kWaves * kMaskLayers * 64 * 2;
 
@@ -464,10 +468,7 @@ __device__ __forceinline__ unsigned mask_soff(const State& s, int ml) {
   return static_cast<unsigned>(s.wave) * kMaskLayers * 512u + 512u * ml;
 }
 
-// act = relu(acc); MASKS: also store the layer's mask bits (slot ml of the tile's mask block): bit
-// 4 ob + r of word ob >> 3 (ob & 7 there).  The words are built by shifting the accumulator left
-// one bit per feature, highest first: a constant 1 << n per bit would be a VOP3 literal, which
-// gfx9 encodings lack, so the compiler kept all 32 of them in VGPRs across the tile loop.
+// act = relu(acc); MASKS: also the layer's mask words (kMaskLayers' bit order).
 // The ReLU is a signed-integer max on the bits (v_max_i32; -0 and negatives -> +0): fmaxf on an
 // MFMA result came out as two v_max_f32 per value (a canonicalize, then the max).
 template <bool MASKS>
@@ -481,7 +482,7 @@ __device__ __forceinline__ uint2v relu_act(State& s) {
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int k = 31; k >= 0; --k) {
+      for (int k = 0; k < 32; ++k) {
         const float v = s.acc[8 * h + (k >> 2)][k & 3];
         w[h] = (w[h] << 1) | (v > 0.0f ? 1u : 0u);
       }
@@ -512,6 +513,75 @@ struct LayerStores {
     if constexpr (T == 4) blocks<2 * CI, 2>();
   }
 };
+
+// The lazy form of relu_act for the 256-wide layers' inputs: act = the previous layer's accumulators
+// as they are, then value t is activated in place in the shadow of the MFMAs of k-step t - 1 (LazyAct)
+// -- at the layer boundary, where both waves of a SIMD meet with the matrix pipe idle, only value 0.
+// The ReLU is the signed-integer max against `floor` (0; INT_MIN for feat, which has no activation),
+// and MASKS sets the value's bit (pre-activation > 0, torch's relu-backward mask) in s.mw.
+template <int t, bool MASKS>
+__device__ __forceinline__ void act_one(State& s, int floor) {
+  const float x = s.act[t >> 2][t & 3];
+  s.act[t >> 2][t & 3] = __int_as_float(max(__float_as_int(x), floor));
+  if constexpr (MASKS) {
+    // t ascending; the empty asm keeps the shift chain a chain (reassociated into 64 independent
+    // select-of-(1 << t) terms it held 20-30 more VGPRs)
+    unsigned w = (s.mw[t >> 5] << 1) | (x > 0.0f ? 1u : 0u);
+    asm volatile("" : "+v"(w));
+    s.mw[t >> 5] = w;
+  }
+}
+
+template <int K0, bool MASKS>
+struct LazyAct {
+  State& s;
+  int floor;
+  template <int T>
+  __device__ __forceinline__ float at() const {
+    constexpr int t = K0 + T;
+    return s.act[t >> 2][t & 3];
+  }
+  static constexpr bool kLazy = true;
+  template <int T>
+  __device__ __forceinline__ void prep() const {
+    if constexpr (K0 + T + 1 < 64) act_one<K0 + T + 1, MASKS>(s, floor);
+  }
+};
+
+// The stores a lazily activated layer input leaves behind: its activation plane (SAVE), two blocks per
+// chunk at k-step 7 (their last values are activated during k-steps 4..6), and its mask words (MASKS,
+// slot ml >= 0) once complete, at the last chunk's k-step 7 -- both after the chunk's DMA, as before.
+template <bool MASKS, bool SAVE>
+struct LazyStores {
+  const State& s;
+  const FieldArgs& a;
+  int64_t tile;
+  int ml, plane;
+  template <int CI, int T>
+  __device__ __forceinline__ void step() const {
+    if constexpr (T == 7) {
+      if constexpr (SAVE) store_plane<2 * CI, 2>(s, plane_rsrc(a.save, plane, a.m, tile), s.act);
+      if constexpr (MASKS && CI == 7) {
+        if (ml >= 0)
+          __builtin_amdgcn_raw_buffer_store_b64(uint2v{s.mw[0], s.mw[1]}, mask_rsrc(a.masks, tile), 8u * s.lane,
+                                                mask_soff(s, ml), 0);
+      }
+    }
+  }
+};
+
+template <bool MASKS, typename Post>
+__device__ __forceinline__ void layer256_lazy(State& s, float4* lds, int& c, int floor, Post post) {
+  chunk16<8, 0>(s, lds, c + 0, LazyAct<0, MASKS>{s, floor}, post);
+  chunk16<8, 1>(s, lds, c + 1, LazyAct<8, MASKS>{s, floor}, post);
+  chunk16<8, 2>(s, lds, c + 2, LazyAct<16, MASKS>{s, floor}, post);
+  chunk16<8, 3>(s, lds, c + 3, LazyAct<24, MASKS>{s, floor}, post);
+  chunk16<8, 4>(s, lds, c + 4, LazyAct<32, MASKS>{s, floor}, post);
+  chunk16<8, 5>(s, lds, c + 5, LazyAct<40, MASKS>{s, floor}, post);
+  chunk16<8, 6>(s, lds, c + 6, LazyAct<48, MASKS>{s, floor}, post);
+  chunk16<8, 7>(s, lds, c + 7, LazyAct<56, MASKS>{s, floor}, post);
+  c += 8;
+}
 
 // Training forward: the post-activation rows the weight gradients read (h1, h2, feat, v1, v2 as
 // (5, m, 256) planes, feature 16 ob + 4 g + r: one 16-B store per block per lane).
@@ -633,15 +703,21 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
   for (int layer = kXyz2; layer <= kDir2; ++layer) {
     // activation of the previous layer's outputs: ReLU, none after fc_out (feat); its mask words
     // and its plane (h1, h2, feat, v1) are stored at this layer's first chunk barrier
-    uint2v mw = uint2v{0u, 0u};
-    if (layer == kDir1) {
+    // (lazily: LazyAct; sigma's dot product below needs all of h2 at once, so fc_out's input is
+    // also activated here -- LazyAct's ReLU then leaves it unchanged)
+    const int floor = layer == kDir1 ? INT_MIN : 0;
 #pragma unroll
-      for (int ob = 0; ob < 16; ++ob) s.act[ob] = s.acc[ob];
-    } else {
-      mw = relu_act<MASKS>(s);
+    for (int ob = 0; ob < 16; ++ob) s.act[ob] = s.acc[ob];
+    s.mw[0] = s.mw[1] = 0u;
+    if (layer == kOut) {
+#pragma unroll
+      for (int ob = 0; ob < 16; ++ob)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s.act[ob][r] = __int_as_float(max(__float_as_int(s.act[ob][r]), 0));
     }
-    const LayerStores<MASKS, SAVE> st{s, a, tile, layer == kXyz2 ? 0 : (layer == kOut ? 1 : (layer == kDir2 ? 2 : -1)),
-                                     layer - kXyz2, mw};
+    act_one<0, MASKS>(s, floor);
+    const LazyStores<MASKS, SAVE> st{s, a, tile, layer == kXyz2 ? 0 : (layer == kOut ? 1 : (layer == kDir2 ? 2 : -1)),
+                                    layer - kXyz2};
     if (layer == kOut) {
       // sigma = fc_out row 0 . [h2, zs2] + b: the h2 part here, the code part from cn_code_bias
       // (two packed chains: 32 v_pk_fma_f32 instead of one 64-deep fmaf chain)
@@ -670,7 +746,7 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
     else if (layer == kOut) bias_code(s, a, crow_lds, kCbFeat);
     else bias_from(s, clds + (layer == kDir1 ? kCBD1 : kCBD2));
     __builtin_amdgcn_sched_barrier(0);
-    layer256(s, lds, c, st);
+    layer256_lazy<MASKS>(s, lds, c, floor, st);
     if (layer == kDir1) {
       chunk16<7>(s, lds, c, ArrB<0>{s.denc});
       c += 1;
@@ -985,7 +1061,7 @@ __device__ __forceinline__ void mask_act(State& s, uint2 m) {
     const unsigned w = ob < 8 ? m.x : m.y;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const unsigned keep = static_cast<unsigned>(__builtin_amdgcn_sbfe(static_cast<int>(w), 4 * (ob & 7) + r, 1));
+      const unsigned keep = static_cast<unsigned>(__builtin_amdgcn_sbfe(static_cast<int>(w), 31 - 4 * (ob & 7) - r, 1));
       s.act[ob][r] = __uint_as_float(__float_as_uint(s.acc[ob][r]) & keep);
     }
   }
@@ -998,7 +1074,7 @@ __device__ __forceinline__ void mask_act(State& s, uint2 m) {
 template <int t>
 __device__ __forceinline__ void mask_one(State& s, uint2 m) {
   const unsigned w = t < 32 ? m.x : m.y;
-  const unsigned keep = static_cast<unsigned>(__builtin_amdgcn_sbfe(static_cast<int>(w), t & 31, 1));
+  const unsigned keep = static_cast<unsigned>(__builtin_amdgcn_sbfe(static_cast<int>(w), 31 - (t & 31), 1));
   s.act[t >> 2][t & 3] = __uint_as_float(__float_as_uint(s.act[t >> 2][t & 3]) & keep);
 }
 
