@@ -618,16 +618,20 @@ def test_train_c3_decisions_at_size(dev, monkeypatch):
         out["shape table"], out["texture table"] = ts.grad[C3_IDS], tt.grad[C3_IDS]
         return out, z_f, w_c.detach(), z_c
 
-    # 1. the oracle on its own decisions IS the reference at size
+    # 1. the oracle on its own decisions: the reference's op sequence, on this host's CPU (other
+    #    threads / BLAS blocking than the container that wrote the fixture) -- at size it differs
+    #    from the reference by the same kind of moved decisions (r04d: 3.0e-4), which is the
+    #    problem's conditioning, not the kernels'
     pre_c, pre_f = {}, {}
     own, z_own, w_own, z_c = oracle_step(pre_c=pre_c, pre_f=pre_f)
-    e_ref = 0.0
+    e_ref, per = (0.0, ""), {}
     for k in own:
-        key = "g_" + k if ("g_" + k) in g else None
-        if key is not None:
-            ref = g[key].cpu()
-            e_ref = max(e_ref, (own[k] - ref).abs().max().item() / ref.abs().max().item())
-    margin("c3_decisions[f32]", "oracle (own decisions) vs reference, full tensors", e_ref, 2e-5)
+        if ("g_" + k) in g:
+            ref = g["g_" + k].cpu()
+            per[k] = (own[k] - ref).abs().max().item() / ref.abs().max().item()
+            e_ref = max(e_ref, (per[k], k))
+    margin("c3_decisions[f32]", "CPU oracle (own decisions) vs reference, full tensors (worst: %s)" % e_ref[1],
+           e_ref[0], C3_GRAD_RTOL["f32"], per_tensor={k: float(f"{v:.3e}") for k, v in per.items()})
     # 2. the kernels' discrete decisions against the oracle's
     assert (seen["w_coarse"] - w_own[..., 1:-1]).abs().max().item() <= 1e-5
     assert torch.equal(o.sample_pdf(ro, rd, seen["w_coarse"], z_c, 64, u)[1], seen["z_fine"])
