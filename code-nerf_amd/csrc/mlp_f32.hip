@@ -168,7 +168,8 @@ struct State {
   bool uniform_code; // all 16 samples of the wave use one code row
   __amdgpu_buffer_rsrc_t wsrc;
   unsigned voff;
-  unsigned poff;     // this lane's byte offset in a (kTile, 256) fp32 plane block: row 16 wave + (lane & 15), col 4 g
+  unsigned poff;     // this lane's byte offset in a (kTile, 256) fp32 plane block (store_plane): row
+                     // 16 wave + (lane & 7), byte 64 ((lane >> 3) & 1) + 16 g
   unsigned gbase;    // backward: this lane's byte offset in a 256-float sum row (rowsum64's features)
 };
 
@@ -205,14 +206,30 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t mask_rsrc(const unsigned* mask
 __device__ __forceinline__ int fresh(int v);
 // Plane stores are non-temporal (cpol 2): the 400 MB of planes per C3 chunk never fit the L2, and
 // write-back stores evicted the weight stream (forward FETCH 58 -> 6 MB per launch, the backward
-// that reads them 1.5 % faster; r03i).
+// that reads them 1.5 % faster; r03i).  A lane holds 16 B of a row per block, so block ob alone is 16
+// rows x 64 B -- half of every 128-B line it touches, and non-temporal half lines cost the memory side
+// 1.29x their bytes at 3.1 TB/s (tools/write_probe.hip, r04).  So blocks are stored in pairs as whole
+// lines: the pair's first instruction writes rows 0..7 of the wave's 16 (lane i = lane & 15 < 8: its
+// own block b; i >= 8: block b + 1 of row i - 8, fetched by one row_ror:8 DPP move whose bank mask
+// keeps the lanes i < 8), the second rows 8..15 (the mirror); bytes 128 (b / 2) .. + 127 of 8 rows per
+// instruction.  Eight DPP moves per pair, in the MFMA shadow like the stores themselves.
 constexpr int kPlaneCPol = 2;
 template <int B0 = 0, int NB = 16>
 __device__ __forceinline__ void store_plane(const State& s, __amdgpu_buffer_rsrc_t r, const floatx4* v) {
+  static_assert(B0 % 2 == 0 && NB % 2 == 0, "blocks go out in pairs");
   const unsigned off = static_cast<unsigned>(fresh(static_cast<int>(s.poff)));
 #pragma unroll
-  for (int ob = B0; ob < B0 + NB; ++ob)
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, v[ob]), r, off + 64u * ob, 0, kPlaneCPol);
+  for (int b = B0; b < B0 + NB; b += 2) {
+    floatx4 lo, hi;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      // row_ror:8 = 0x128; bank mask 0xc: lanes 8..15 of each row of 16, 0x3: lanes 0..7
+      lo[q] = __builtin_amdgcn_update_dpp(v[b][q], v[b + 1][q], 0x128, 0xf, 0xc, false);
+      hi[q] = __builtin_amdgcn_update_dpp(v[b + 1][q], v[b][q], 0x128, 0xf, 0x3, false);
+    }
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, lo), r, off + 64u * b, 0, kPlaneCPol);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, hi), r, off + 8192u + 64u * b, 0, kPlaneCPol);
+  }
 }
 
 
@@ -856,7 +873,7 @@ __global__ __launch_bounds__(kThreads, 2) void field_w16_kernel(FieldArgs a) {
   s.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   s.wsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.packed), 0, kPackedFloats * 4, 0x00020000);
   s.voff = static_cast<unsigned>(s.wave * 64 + s.lane) * 16u;
-  s.poff = static_cast<unsigned>(s.wave * 16 + (s.lane & 15)) * 1024u + 16u * s.g;
+  s.poff = static_cast<unsigned>(s.wave * 16 + (s.lane & 7)) * 1024u + 64u * ((s.lane >> 3) & 1) + 16u * s.g;
   s.sig = 0.0f;
   float* crow_lds = clds + kLdsConsts + s.wave * kCbStride;
 
@@ -1492,7 +1509,7 @@ __global__ __launch_bounds__(kThreads, 2) void field_w16_bwd_kernel(FieldArgs a)
   s.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   s.wsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.packed), 0, kPackedFloats * 4, 0x00020000);
   s.voff = static_cast<unsigned>(s.wave * 64 + s.lane) * 16u;
-  s.poff = static_cast<unsigned>(s.wave * 16 + (s.lane & 15)) * 1024u + 16u * s.g;
+  s.poff = static_cast<unsigned>(s.wave * 16 + (s.lane & 7)) * 1024u + 64u * ((s.lane >> 3) & 1) + 16u * s.g;
   s.gbase = static_cast<unsigned>(16 * rev4(s.lane & 15) + 4 * s.g) * 4u;
   float* grow = blds + kBGacc + s.wave * kCbStride;
   load_consts(a, blds);

@@ -16,6 +16,9 @@
 //               spread them over k-steps 4..7 of the next chunk)
 //   rows_nt     one contiguous 1 KiB row per 64 lanes per instruction, NT (the alternative layout:
 //               a wave writes whole rows)
+//   lines_nt    the planes' layout written as whole 128-B lines: instruction k of a pair writes rows
+//               8 h .. 8 h + 7 x bytes 128 k .. 128 k + 127 (lane i = lane & 15 < 8 its own block 2 k,
+//               lane i >= 8 block 2 k + 1 of row i - 8: one row_ror:8 DPP exchange), NT
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -58,6 +61,22 @@ __global__ __launch_bounds__(256) void plane(float* out, long n_blocks) {
   }
 }
 
+// lines_nt: the DPP-exchanged form of the plane store (16 instructions per 16-row block as plane<>)
+__global__ __launch_bounds__(256) void lines(float* out, long n_blocks) {
+  const long wave = (long(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  if (wave >= n_blocks) return;
+  const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(out + wave * 4096, 0, 16384, 0x00020000);
+  const unsigned off = static_cast<unsigned>(i & 7) * 1024u + 64u * (i >> 3) + 16u * g;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const float x = __builtin_amdgcn_update_dpp(0.0f, float(lane + k), 0x128, 0xf, 0xf, false);  // row_ror:8
+    const f32x4 a = f32x4{x, 2.f, 3.f, float(k)};
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, a), r, off + 128u * k, 0, 2);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, a), r, off + 8192u + 128u * k, 0, 2);
+  }
+}
+
 template <int CPOL>
 __global__ __launch_bounds__(256) void rows(float* out, long n_blocks) {
   const long wave = (long(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
@@ -88,8 +107,8 @@ int main() {
   CHECK(hipEventCreate(&a));
   CHECK(hipEventCreate(&b));
   const int reps = 3;
-  const char* names[] = {"lanes16", "lanes64", "plane_wb", "plane_nt", "plane_nt_4", "rows_nt", "rows_wb"};
-  for (int which = 0; which < 7; ++which) {
+  const char* names[] = {"lanes16", "lanes64", "plane_wb", "plane_nt", "plane_nt_4", "rows_nt", "rows_wb", "lines_nt"};
+  for (int which = 0; which < 8; ++which) {
     float best = 1e30f;
     for (int rep = 0; rep < reps + 1; ++rep) {
       CHECK(hipEventRecord(a));
@@ -100,7 +119,8 @@ int main() {
         case 3: plane<2, 0><<<n_blk / 4, 256>>>(out, n_blk); break;
         case 4: plane<2, 1><<<n_blk / 4, 256>>>(out, n_blk); break;
         case 5: rows<2><<<n_blk / 4, 256>>>(out, n_blk); break;
-        default: rows<0><<<n_blk / 4, 256>>>(out, n_blk); break;
+        case 6: rows<0><<<n_blk / 4, 256>>>(out, n_blk); break;
+        default: lines<<<n_blk / 4, 256>>>(out, n_blk); break;
       }
       CHECK(hipGetLastError());
       CHECK(hipEventRecord(b));
