@@ -490,39 +490,46 @@ __device__ __forceinline__ void tn256_body(float* ring, const float* __restrict_
   dma(0);
   dma(1);
   dma(2);
+  // operands of row pair p + 1 are read while pair p's MFMAs run -- across stages too: the last pair
+  // of stage st reads stage st+1's first, so the barrier is followed by MFMAs, not by LDS latency
+  float a[2][2], b[2][4];
   for (int st = 0; st < n_stages; ++st) {
-    // stage st landed (all but this wave's 2 kTwRows youngest pieces: stages st+1, st+2) and
-    // every wave is done with stage st-1, whose slot then receives stage st+3; after a DIRS flush
-    // its 8 stores are the youngest 8 vector-memory ops as well
-    static_assert(kTwRows / 2 == 8, "the vmcnt below counts stages st+1, st+2");
+    // stages st AND st+1 landed (all but this wave's kTwRows / 4 youngest pieces: stage st+2's) and
+    // every wave is done with stage st-1, whose slot then receives stage st+3 (issued after this
+    // stage's first row pair, beside its MFMAs); after a DIRS flush its 8 stores are the youngest 8
+    // vector-memory ops as well.  Waiting for st+1 here (it was issued two stages ago) is what lets
+    // the last row pair prefetch from it.
+    static_assert(kTwRows / 4 == 4, "the vmcnt below counts stage st+2");
 #ifdef CN_PROBE_TN_WAITPROF
     const long long tp0 = clock64();
 #endif
-    if constexpr (SIG) asm volatile("s_waitcnt vmcnt(10)\n\ts_barrier" ::: "memory");
-    else if (DIRS && flushed) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+    if constexpr (SIG) asm volatile("s_waitcnt vmcnt(5)\n\ts_barrier" ::: "memory");
+    else if (DIRS && flushed) asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
 #ifdef CN_PROBE_TN_WAITPROF
     const long long tp1 = clock64();
     prof_bar += tp1 - tp0;
 #endif
-    dma(st + 3);
-#ifdef CN_PROBE_TN_WAITPROF
-    __builtin_amdgcn_sched_barrier(0);
-    prof_dma += clock64() - tp1;
-#endif
     if constexpr (X3) {
+      dma(st + 3);
+#ifdef CN_PROBE_TN_WAITPROF
+      __builtin_amdgcn_sched_barrier(0);
+      prof_dma += clock64() - tp1;
+#endif
       x3_stage<SIG>(ring + (st & (kTwRing - 1)) * kTwStage, i, h, n0, k0, acc, bsum, sacc, sig_wave);
       continue;
     }
     const float* sa = ring + (st & (kTwRing - 1)) * kTwStage + h * 256 + i;
     const float* sb = sa + kTwRows * 256;
-    // operands of row pair p + 1 are read while pair p's MFMAs run
-    float a[2][2], b[2][4];
+    const float* sa1 = ring + ((st + 1) & (kTwRing - 1)) * kTwStage + h * 256 + i;  // stage st+1
+    const float* sb1 = sa1 + kTwRows * 256;
+    if (st == 0) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t) a[0][t] = sa[n0 + 32 * t];
+      for (int t = 0; t < 2; ++t) a[0][t] = sa[n0 + 32 * t];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) b[0][u] = sb[k0 + 32 * u];
+      for (int u = 0; u < 4; ++u) b[0][u] = sb[k0 + 32 * u];
+    }
 #pragma unroll
     for (int p = 0; p < kTwRows / 2; ++p) {
       const int c = p & 1, nx = c ^ 1;
@@ -531,6 +538,12 @@ __device__ __forceinline__ void tn256_body(float* ring, const float* __restrict_
         for (int t = 0; t < 2; ++t) a[nx][t] = sa[(p + 1) * 512 + n0 + 32 * t];
 #pragma unroll
         for (int u = 0; u < 4; ++u) b[nx][u] = sb[(p + 1) * 512 + k0 + 32 * u];
+      } else {
+        // stage st+1's first pair (past the last stage: slot st+1 holds zeros or a stale stage; unused)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) a[nx][t] = sa1[n0 + 32 * t];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) b[nx][u] = sb1[k0 + 32 * u];
       }
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
@@ -547,6 +560,18 @@ __device__ __forceinline__ void tn256_body(float* ring, const float* __restrict_
 #pragma unroll
           for (int u = 0; u < 4; ++u) sacc[u] = fmaf(dsg, b[c][u], sacc[u]);
         }
+      }
+      if (p == 0) {
+        __builtin_amdgcn_sched_barrier(0);
+#ifdef CN_PROBE_TN_WAITPROF
+        const long long td0 = clock64();
+#endif
+        dma(st + 3);  // beside the first pair's MFMAs
+#ifdef CN_PROBE_TN_WAITPROF
+        __builtin_amdgcn_sched_barrier(0);
+        prof_dma += clock64() - td0;
+#endif
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
     if constexpr (DIRS) {
