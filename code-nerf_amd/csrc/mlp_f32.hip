@@ -156,7 +156,6 @@ struct State {
   floatx4 act[16];   // layer input: block ob register r = input feature 16 ob + 4 g + r
   floatx4 acc[16];   // layer output accumulators
   floatx4 pre[4];    // the next chunk's first A fragments (read during this chunk's last k-step)
-  unsigned mw[2];    // forward: the ReLU mask words of the layer input being activated (LazyAct)
   floatx4 acc2[4];   // backward: the narrow chunks' accumulators (2 blocks x 2 chains)
   float denc[8];     // view-direction encoding, k-steps of the view-dir chunk
   float sig;         // sigma partial (this lane group's 64 features)
@@ -168,8 +167,7 @@ struct State {
   bool uniform_code; // all 16 samples of the wave use one code row
   __amdgpu_buffer_rsrc_t wsrc;
   unsigned voff;
-  unsigned poff;     // this lane's byte offset in a (kTile, 256) fp32 plane block (store_plane): row
-                     // 16 wave + (lane & 7), byte 64 ((lane >> 3) & 1) + 16 g
+  unsigned poff;     // this lane's byte offset in a (kTile, 256) fp32 plane block: row 16 wave + (lane & 15), col 4 g
   unsigned gbase;    // backward: this lane's byte offset in a 256-float sum row (rowsum64's features)
 };
 
@@ -206,30 +204,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t mask_rsrc(const unsigned* mask
 __device__ __forceinline__ int fresh(int v);
 // Plane stores are non-temporal (cpol 2): the 400 MB of planes per C3 chunk never fit the L2, and
 // write-back stores evicted the weight stream (forward FETCH 58 -> 6 MB per launch, the backward
-// that reads them 1.5 % faster; r03i).  A lane holds 16 B of a row per block, so block ob alone is 16
-// rows x 64 B -- half of every 128-B line it touches, and non-temporal half lines cost the memory side
-// 1.29x their bytes at 3.1 TB/s (tools/write_probe.hip, r04).  So blocks are stored in pairs as whole
-// lines: the pair's first instruction writes rows 0..7 of the wave's 16 (lane i = lane & 15 < 8: its
-// own block b; i >= 8: block b + 1 of row i - 8, fetched by one row_ror:8 DPP move whose bank mask
-// keeps the lanes i < 8), the second rows 8..15 (the mirror); bytes 128 (b / 2) .. + 127 of 8 rows per
-// instruction.  Eight DPP moves per pair, in the MFMA shadow like the stores themselves.
+// that reads them 1.5 % faster; r03i).
 constexpr int kPlaneCPol = 2;
 template <int B0 = 0, int NB = 16>
 __device__ __forceinline__ void store_plane(const State& s, __amdgpu_buffer_rsrc_t r, const floatx4* v) {
-  static_assert(B0 % 2 == 0 && NB % 2 == 0, "blocks go out in pairs");
   const unsigned off = static_cast<unsigned>(fresh(static_cast<int>(s.poff)));
 #pragma unroll
-  for (int b = B0; b < B0 + NB; b += 2) {
-    floatx4 lo, hi;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      // row_ror:8 = 0x128; bank mask 0xc: lanes 8..15 of each row of 16, 0x3: lanes 0..7
-      lo[q] = __builtin_amdgcn_update_dpp(v[b][q], v[b + 1][q], 0x128, 0xf, 0xc, false);
-      hi[q] = __builtin_amdgcn_update_dpp(v[b + 1][q], v[b][q], 0x128, 0xf, 0x3, false);
-    }
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, lo), r, off + 64u * b, 0, kPlaneCPol);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, hi), r, off + 8192u + 64u * b, 0, kPlaneCPol);
-  }
+  for (int ob = B0; ob < B0 + NB; ++ob)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, v[ob]), r, off + 64u * ob, 0, kPlaneCPol);
 }
 
 
@@ -468,11 +450,8 @@ __device__ __forceinline__ void bias_code(State& s, const FieldArgs& a, const fl
   }
 }
 
-// ReLU masks for the fused backward: 4 layers (h1, h2, v1, v2) x 64 bits per lane (value t = 4 ob + r,
-// feature 16 ob + 4 g + r, pre-activation > 0: bit 31 - (t & 31) of word t >> 5), one 8-B store per
-// lane per layer.  The words are built by shifting left one bit per value in increasing t: a constant
-// 1 << n per bit would be a VOP3 literal, which gfx9 encodings lack, so the compiler kept them all in
-// VGPRs across the tile loop.
+// ReLU masks for the fused backward: 4 layers (h1, h2, v1, v2) x 64 bits per lane (bit 4 ob + r
+// of feature 16 ob + 4 g + r: pre-activation > 0), one 8-B store per lane per layer.
 constexpr int kMaskLayers = 4;
 constexpr int kMaskWordsPerTile = kWaves * kMaskLayers * 64 * 2;
 
@@ -485,7 +464,10 @@ __device__ __forceinline__ unsigned mask_soff(const State& s, int ml) {
   return static_cast<unsigned>(s.wave) * kMaskLayers * 512u + 512u * ml;
 }
 
-// act = relu(acc); MASKS: also the layer's mask words (kMaskLayers' bit order).
+// act = relu(acc); MASKS: also store the layer's mask bits (slot ml of the tile's mask block): bit
+// 4 ob + r of word ob >> 3 (ob & 7 there).  The words are built by shifting the accumulator left
+// one bit per feature, highest first: a constant 1 << n per bit would be a VOP3 literal, which
+// gfx9 encodings lack, so the compiler kept all 32 of them in VGPRs across the tile loop.
 // The ReLU is a signed-integer max on the bits (v_max_i32; -0 and negatives -> +0): fmaxf on an
 // MFMA result came out as two v_max_f32 per value (a canonicalize, then the max).
 template <bool MASKS>
@@ -499,7 +481,7 @@ __device__ __forceinline__ uint2v relu_act(State& s) {
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int k = 0; k < 32; ++k) {
+      for (int k = 31; k >= 0; --k) {
         const float v = s.acc[8 * h + (k >> 2)][k & 3];
         w[h] = (w[h] << 1) | (v > 0.0f ? 1u : 0u);
       }
@@ -530,75 +512,6 @@ struct LayerStores {
     if constexpr (T == 4) blocks<2 * CI, 2>();
   }
 };
-
-// The lazy form of relu_act for the 256-wide layers' inputs: act = the previous layer's accumulators
-// as they are, then value t is activated in place in the shadow of the MFMAs of k-step t - 1 (LazyAct)
-// -- at the layer boundary, where both waves of a SIMD meet with the matrix pipe idle, only value 0.
-// The ReLU is the signed-integer max against `floor` (0; INT_MIN for feat, which has no activation),
-// and MASKS sets the value's bit (pre-activation > 0, torch's relu-backward mask) in s.mw.
-template <int t, bool MASKS>
-__device__ __forceinline__ void act_one(State& s, int floor) {
-  const float x = s.act[t >> 2][t & 3];
-  s.act[t >> 2][t & 3] = __int_as_float(max(__float_as_int(x), floor));
-  if constexpr (MASKS) {
-    // t ascending; the empty asm keeps the shift chain a chain (reassociated into 64 independent
-    // select-of-(1 << t) terms it held 20-30 more VGPRs)
-    unsigned w = (s.mw[t >> 5] << 1) | (x > 0.0f ? 1u : 0u);
-    asm volatile("" : "+v"(w));
-    s.mw[t >> 5] = w;
-  }
-}
-
-template <int K0, bool MASKS>
-struct LazyAct {
-  State& s;
-  int floor;
-  template <int T>
-  __device__ __forceinline__ float at() const {
-    constexpr int t = K0 + T;
-    return s.act[t >> 2][t & 3];
-  }
-  static constexpr bool kLazy = true;
-  template <int T>
-  __device__ __forceinline__ void prep() const {
-    if constexpr (K0 + T + 1 < 64) act_one<K0 + T + 1, MASKS>(s, floor);
-  }
-};
-
-// The stores a lazily activated layer input leaves behind: its activation plane (SAVE), two blocks per
-// chunk at k-step 7 (their last values are activated during k-steps 4..6), and its mask words (MASKS,
-// slot ml >= 0) once complete, at the last chunk's k-step 7 -- both after the chunk's DMA, as before.
-template <bool MASKS, bool SAVE>
-struct LazyStores {
-  const State& s;
-  const FieldArgs& a;
-  int64_t tile;
-  int ml, plane;
-  template <int CI, int T>
-  __device__ __forceinline__ void step() const {
-    if constexpr (T == 7) {
-      if constexpr (SAVE) store_plane<2 * CI, 2>(s, plane_rsrc(a.save, plane, a.m, tile), s.act);
-      if constexpr (MASKS && CI == 7) {
-        if (ml >= 0)
-          __builtin_amdgcn_raw_buffer_store_b64(uint2v{s.mw[0], s.mw[1]}, mask_rsrc(a.masks, tile), 8u * s.lane,
-                                                mask_soff(s, ml), 0);
-      }
-    }
-  }
-};
-
-template <bool MASKS, typename Post>
-__device__ __forceinline__ void layer256_lazy(State& s, float4* lds, int& c, int floor, Post post) {
-  chunk16<8, 0>(s, lds, c + 0, LazyAct<0, MASKS>{s, floor}, post);
-  chunk16<8, 1>(s, lds, c + 1, LazyAct<8, MASKS>{s, floor}, post);
-  chunk16<8, 2>(s, lds, c + 2, LazyAct<16, MASKS>{s, floor}, post);
-  chunk16<8, 3>(s, lds, c + 3, LazyAct<24, MASKS>{s, floor}, post);
-  chunk16<8, 4>(s, lds, c + 4, LazyAct<32, MASKS>{s, floor}, post);
-  chunk16<8, 5>(s, lds, c + 5, LazyAct<40, MASKS>{s, floor}, post);
-  chunk16<8, 6>(s, lds, c + 6, LazyAct<48, MASKS>{s, floor}, post);
-  chunk16<8, 7>(s, lds, c + 7, LazyAct<56, MASKS>{s, floor}, post);
-  c += 8;
-}
 
 // Training forward: the post-activation rows the weight gradients read (h1, h2, feat, v1, v2 as
 // (5, m, 256) planes, feature 16 ob + 4 g + r: one 16-B store per block per lane).
@@ -720,21 +633,15 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
   for (int layer = kXyz2; layer <= kDir2; ++layer) {
     // activation of the previous layer's outputs: ReLU, none after fc_out (feat); its mask words
     // and its plane (h1, h2, feat, v1) are stored at this layer's first chunk barrier
-    // (lazily: LazyAct; sigma's dot product below needs all of h2 at once, so fc_out's input is
-    // also activated here -- LazyAct's ReLU then leaves it unchanged)
-    const int floor = layer == kDir1 ? INT_MIN : 0;
+    uint2v mw = uint2v{0u, 0u};
+    if (layer == kDir1) {
 #pragma unroll
-    for (int ob = 0; ob < 16; ++ob) s.act[ob] = s.acc[ob];
-    s.mw[0] = s.mw[1] = 0u;
-    if (layer == kOut) {
-#pragma unroll
-      for (int ob = 0; ob < 16; ++ob)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) s.act[ob][r] = __int_as_float(max(__float_as_int(s.act[ob][r]), 0));
+      for (int ob = 0; ob < 16; ++ob) s.act[ob] = s.acc[ob];
+    } else {
+      mw = relu_act<MASKS>(s);
     }
-    act_one<0, MASKS>(s, floor);
-    const LazyStores<MASKS, SAVE> st{s, a, tile, layer == kXyz2 ? 0 : (layer == kOut ? 1 : (layer == kDir2 ? 2 : -1)),
-                                    layer - kXyz2};
+    const LayerStores<MASKS, SAVE> st{s, a, tile, layer == kXyz2 ? 0 : (layer == kOut ? 1 : (layer == kDir2 ? 2 : -1)),
+                                     layer - kXyz2, mw};
     if (layer == kOut) {
       // sigma = fc_out row 0 . [h2, zs2] + b: the h2 part here, the code part from cn_code_bias
       // (two packed chains: 32 v_pk_fma_f32 instead of one 64-deep fmaf chain)
@@ -763,7 +670,7 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
     else if (layer == kOut) bias_code(s, a, crow_lds, kCbFeat);
     else bias_from(s, clds + (layer == kDir1 ? kCBD1 : kCBD2));
     __builtin_amdgcn_sched_barrier(0);
-    layer256_lazy<MASKS>(s, lds, c, floor, st);
+    layer256(s, lds, c, st);
     if (layer == kDir1) {
       chunk16<7>(s, lds, c, ArrB<0>{s.denc});
       c += 1;
@@ -873,7 +780,7 @@ __global__ __launch_bounds__(kThreads, 2) void field_w16_kernel(FieldArgs a) {
   s.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   s.wsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.packed), 0, kPackedFloats * 4, 0x00020000);
   s.voff = static_cast<unsigned>(s.wave * 64 + s.lane) * 16u;
-  s.poff = static_cast<unsigned>(s.wave * 16 + (s.lane & 7)) * 1024u + 64u * ((s.lane >> 3) & 1) + 16u * s.g;
+  s.poff = static_cast<unsigned>(s.wave * 16 + (s.lane & 15)) * 1024u + 16u * s.g;
   s.sig = 0.0f;
   float* crow_lds = clds + kLdsConsts + s.wave * kCbStride;
 
@@ -1078,94 +985,10 @@ __device__ __forceinline__ void mask_act(State& s, uint2 m) {
     const unsigned w = ob < 8 ? m.x : m.y;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const unsigned keep = static_cast<unsigned>(__builtin_amdgcn_sbfe(static_cast<int>(w), 31 - 4 * (ob & 7) - r, 1));
+      const unsigned keep = static_cast<unsigned>(__builtin_amdgcn_sbfe(static_cast<int>(w), 4 * (ob & 7) + r, 1));
       s.act[ob][r] = __uint_as_float(__float_as_uint(s.acc[ob][r]) & keep);
     }
   }
-}
-
-// The lazy form (the field backward's masked layers): act = the raw gradients (the previous layer's
-// accumulators), then value t is masked in place in the shadow of the MFMAs of k-step t - 1 (MaskB,
-// NarrowMask) -- at the layer boundary, where both waves of a SIMD meet with the matrix pipe idle,
-// only value 0 (a 256-wide layer) or block pair 0 (the narrow xyz1 chunks) is masked.
-template <int t>
-__device__ __forceinline__ void mask_one(State& s, uint2 m) {
-  const unsigned w = t < 32 ? m.x : m.y;
-  const unsigned keep = static_cast<unsigned>(__builtin_amdgcn_sbfe(static_cast<int>(w), 31 - (t & 31), 1));
-  s.act[t >> 2][t & 3] = __uint_as_float(__float_as_uint(s.act[t >> 2][t & 3]) & keep);
-}
-
-__device__ __forceinline__ void raw_act(State& s) {
-#pragma unroll
-  for (int ob = 0; ob < 16; ++ob) s.act[ob] = s.acc[ob];
-}
-
-// B of a masked 256-wide layer: k-step T reads value K0 + T (masked by then), and its prep masks
-// value K0 + T + 1 (the last k-step of a chunk: the next chunk's first value).
-template <int K0>
-struct MaskB {
-  State& s;
-  uint2 m;
-  template <int T>
-  __device__ __forceinline__ float at() const {
-    constexpr int t = K0 + T;
-    return s.act[t >> 2][t & 3];
-  }
-  static constexpr bool kLazy = true;
-  template <int T>
-  __device__ __forceinline__ void prep() const {
-    if constexpr (K0 + T + 1 < 64) mask_one<K0 + T + 1>(s, m);
-  }
-};
-
-// The narrow chunks' lazy mask: k-step T reads blocks 2 T, 2 T + 1 (values 8 T .. 8 T + 7); the
-// first chunk masks the next k-step's eight values after its MFMAs, the second finds them all masked.
-struct NarrowMask {
-  State& s;
-  uint2 m;
-  bool active;
-  template <int T>
-  __device__ __forceinline__ void step() const {
-    if constexpr (T + 1 < 8) {
-      if (active) {
-        mask_one<8 * T + 8>(s, m);
-        mask_one<8 * T + 9>(s, m);
-        mask_one<8 * T + 10>(s, m);
-        mask_one<8 * T + 11>(s, m);
-        mask_one<8 * T + 12>(s, m);
-        mask_one<8 * T + 13>(s, m);
-        mask_one<8 * T + 14>(s, m);
-        mask_one<8 * T + 15>(s, m);
-      }
-    }
-  }
-};
-struct NoPrep {
-  template <int T>
-  __device__ __forceinline__ void step() const {}
-};
-
-// The mask words as new values (an empty asm): the bit tests of a chunk are formed in that chunk.
-// Without it the optimiser merged them with the other uses of the same words (the eager g_code
-// form, the other chunks) and kept up to 64 tested bits live across the layer: 116-152 B/lane of
-// scratch at the 256-VGPR cap.
-__device__ __forceinline__ uint2 fresh_mask(uint2 m) {
-  asm volatile("" : "+v"(m.x), "+v"(m.y));
-  return m;
-}
-
-// A 256-input layer whose B is the lazily masked act (MaskB; value 0 masked by the caller).
-template <typename Post = NoPost>
-__device__ __forceinline__ void layer256_masked(State& s, float4* lds, int& c, uint2 m, Post post = Post{}) {
-  chunk16<8, 0>(s, lds, c + 0, MaskB<0>{s, fresh_mask(m)}, post);
-  chunk16<8, 1>(s, lds, c + 1, MaskB<8>{s, fresh_mask(m)}, post);
-  chunk16<8, 2>(s, lds, c + 2, MaskB<16>{s, fresh_mask(m)}, post);
-  chunk16<8, 3>(s, lds, c + 3, MaskB<24>{s, fresh_mask(m)}, post);
-  chunk16<8, 4>(s, lds, c + 4, MaskB<32>{s, fresh_mask(m)}, post);
-  chunk16<8, 5>(s, lds, c + 5, MaskB<40>{s, fresh_mask(m)}, post);
-  chunk16<8, 6>(s, lds, c + 6, MaskB<48>{s, fresh_mask(m)}, post);
-  chunk16<8, 7>(s, lds, c + 7, MaskB<56>{s, fresh_mask(m)}, post);
-  c += 8;
 }
 
 __device__ __forceinline__ void zero_acc(State& s) {
@@ -1198,8 +1021,8 @@ __device__ __forceinline__ void mfma_narrow(State& s, const floatx4* a) {
 }
 
 // A narrow chunk (2 blocks x 64 k-steps, B from s.act) into s.acc2, on chunk16's schedule.
-template <int CI = 0, typename Post = NoPost, typename Prep = NoPrep>
-__device__ __forceinline__ void chunk_narrow(State& s, float4* lds, int c, Post post = Post{}, Prep prep = Prep{}) {
+template <int CI = 0, typename Post = NoPost>
+__device__ __forceinline__ void chunk_narrow(State& s, float4* lds, int c, Post post = Post{}) {
   const float4* slot = lds + (c & (kRing - 1)) * kChunkQuads + s.lane;
   const float4* nslot = lds + ((c + 1) & (kRing - 1)) * kChunkQuads + s.lane;
   floatx4 a0[4], a1[4];
@@ -1211,8 +1034,7 @@ __device__ __forceinline__ void chunk_narrow(State& s, float4* lds, int c, Post 
     if constexpr ((T) + 1 < 8) read_a<(T) + 1>(slot, NXT);          \
     else read_a<0>(nslot, s.pre);                                   \
     mfma_narrow<(T)>(s, CUR);                                       \
-    prep.template step<(T)>();                                      \
-    lazy_step_pattern();                                            \
+    step_pattern();                                                 \
     __builtin_amdgcn_sched_barrier(0);                              \
     if constexpr ((T) == 3) {                                       \
       chunk_barrier();                                              \
@@ -1254,19 +1076,16 @@ struct DpreStore {
   const FieldArgs& a;
   int64_t tile;
   int plane;
-  // two blocks per chunk of a 256-wide layer (see chunk16) -- at k-step 4, or with `late` (a lazily
-  // masked layer: the chunk's last values are masked during k-steps 4..6) at k-step 7, in the same
-  // place relative to the chunk's DMA; in the xyz1 layer's two narrow chunks (NARROW): eight per
-  // chunk, two per k-step 4..7 (the first chunk stores blocks it masked four k-steps earlier)
+  // two blocks per chunk of a 256-wide layer (see chunk16); in the xyz1 layer's two narrow chunks
+  // (NARROW): eight per chunk, two per k-step 4..7
   bool narrow = false;
-  bool late = false;
   template <int CI, int T>
   __device__ __forceinline__ void step() const {
     if constexpr (TRAIN) {
       if (narrow) {
         if constexpr (T >= 4) store_plane<8 * CI + 2 * (T - 4), 2>(s, plane_rsrc(a.dpre, plane, a.m, tile), s.act);
-      } else if constexpr (T == 4 || T == 7) {
-        if (late == (T == 7)) store_plane<2 * CI, 2>(s, plane_rsrc(a.dpre, plane, a.m, tile), s.act);
+      } else if constexpr (T == 4) {
+        store_plane<2 * CI, 2>(s, plane_rsrc(a.dpre, plane, a.m, tile), s.act);
       }
     }
   }
@@ -1307,7 +1126,7 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   const SampleIn in = decode_sample<MODE>(a, rc);
   const int crow = __builtin_amdgcn_readfirstlane(static_cast<int>(code_row(a, in.code_of)));
   float4 dr = reinterpret_cast<const float4*>(a.d_raw)[rc];
-  const uint2 m_v2 = load_mask(s, a, tile, 3);
+  const uint2 m_v2 = load_mask(s, a, tile, 3), m_v1 = load_mask(s, a, tile, 2);
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   if (!valid) dr = make_float4(0.f, 0.f, 0.f, 0.f);
   // a.g_code NULL: the caller forms g_code from the dPre planes (deterministic column sums folded
@@ -1339,20 +1158,15 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   // ---- layer_dir2^T (m_v2), layer_dir1^T (m_v1)
   // (each layer's masked input gradient -- the dW GEMMs' dPre plane -- is stored at the layer's first
   // chunk barrier: DpreStore as chunk16's `post`)
-  // (masked lazily: MaskB; their stores late)
-  raw_act(s);
-  mask_one<0>(s, m_v2);
-  zero_acc(s);
-  const uint2 m_v1 = load_mask(s, a, tile, 2);
-  __builtin_amdgcn_sched_barrier(0);
-  layer256_masked(s, lds, c, m_v2, DpreStore<TRAIN>{s, a, tile, 0, false, true});
-  raw_act(s);
-  mask_one<0>(s, m_v1);
+  mask_act(s, m_v2);
   zero_acc(s);
   __builtin_amdgcn_sched_barrier(0);
-  const uint2 m_h2 = load_mask(s, a, tile, 1);
+  layer256(s, lds, c, DpreStore<TRAIN>{s, a, tile, 0});
+  const uint2 m_h2 = load_mask(s, a, tile, 1), m_h1 = load_mask(s, a, tile, 0);
+  mask_act(s, m_v1);
+  zero_acc(s);
   __builtin_amdgcn_sched_barrier(0);
-  layer256_masked(s, lds, c, m_v1, DpreStore<TRAIN>{s, a, tile, 1, false, true});
+  layer256(s, lds, c, DpreStore<TRAIN>{s, a, tile, 1});
   // ---- the view-direction rows of layer_dir1^T (narrow chunk, B = m_v1 . d v1 still in act)
 #pragma unroll
   for (int q = 0; q < 4; ++q) s.acc2[q] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -1392,7 +1206,6 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
 #pragma unroll
   for (int ob = 0; ob < 16; ++ob) s.act[ob] = s.acc[ob];
   if (gc) gcode_add64<kCbFeat>(s, grow, s.act);
-  const uint2 m_h1 = load_mask(s, a, tile, 0);
 #pragma unroll
   for (int ob = 0; ob < 16; ++ob) {
     const floatx4 w = *reinterpret_cast<const floatx4*>(clds + kTSig + 64 * fresh(s.g) + 4 * ob);
@@ -1400,34 +1213,20 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   }
   __builtin_amdgcn_sched_barrier(0);
   layer256(s, lds, c, DpreStore<TRAIN>{s, a, tile, 2});
-  // ---- layer_xyz2^T (m_h2): its masked input gradient is the code term's too (g_code in the kernel:
-  // masked here at once for the row sums; the lazy masking then finds every value masked already)
-  if (gc) {
-    mask_act(s, m_h2);
-    gcode_add64<kCbXyz2>(s, grow, s.act);
-  } else {
-    raw_act(s);
-    mask_one<0>(s, m_h2);
-  }
+  // ---- layer_xyz2^T (m_h2): its masked input gradient is the code term's too
+  mask_act(s, m_h2);
+  if (gc) gcode_add64<kCbXyz2>(s, grow, s.act);
   zero_acc(s);
   __builtin_amdgcn_sched_barrier(0);
-  layer256_masked(s, lds, c, m_h2, DpreStore<TRAIN>{s, a, tile, 3, false, true});
-  // ---- layer_xyz1^T (m_h1): encoding k-steps 0-7, then 8-15 (masked lazily in the first chunk)
-  raw_act(s);
-  mask_one<0>(s, m_h1);
-  mask_one<1>(s, m_h1);
-  mask_one<2>(s, m_h1);
-  mask_one<3>(s, m_h1);
-  mask_one<4>(s, m_h1);
-  mask_one<5>(s, m_h1);
-  mask_one<6>(s, m_h1);
-  mask_one<7>(s, m_h1);
+  layer256(s, lds, c, DpreStore<TRAIN>{s, a, tile, 3});
+  // ---- layer_xyz1^T (m_h1): encoding k-steps 0-7, then 8-15
+  mask_act(s, m_h1);
   float genc[16];
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) s.acc2[q] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
-    if (half == 0) chunk_narrow<0>(s, lds, c, DpreStore<TRAIN>{s, a, tile, 4, true}, NarrowMask{s, m_h1, true});
+    if (half == 0) chunk_narrow<0>(s, lds, c, DpreStore<TRAIN>{s, a, tile, 4, true});
     else chunk_narrow<1>(s, lds, c, DpreStore<TRAIN>{s, a, tile, 4, true});
     c += 1;
 #pragma unroll
@@ -1509,7 +1308,7 @@ __global__ __launch_bounds__(kThreads, 2) void field_w16_bwd_kernel(FieldArgs a)
   s.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   s.wsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.packed), 0, kPackedFloats * 4, 0x00020000);
   s.voff = static_cast<unsigned>(s.wave * 64 + s.lane) * 16u;
-  s.poff = static_cast<unsigned>(s.wave * 16 + (s.lane & 7)) * 1024u + 64u * ((s.lane >> 3) & 1) + 16u * s.g;
+  s.poff = static_cast<unsigned>(s.wave * 16 + (s.lane & 15)) * 1024u + 16u * s.g;
   s.gbase = static_cast<unsigned>(16 * rev4(s.lane & 15) + 4 * s.g) * 4u;
   float* grow = blds + kBGacc + s.wave * kCbStride;
   load_consts(a, blds);

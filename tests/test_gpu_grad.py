@@ -268,13 +268,12 @@ def decode_relu_masks(words: torch.Tensor, m_rows: int):
 def decode_relu_masks_w16(words: torch.Tensor, m_rows: int):
     """The fp32 16x16x4 kernel's masks (csrc/mlp_f32.hip relu_act) -> {"h1", "h2", "v1", "v2"}.
 
-    Layout: per 128-sample tile, wave w (8), layer l (h1, h2, v1, v2) and lane L, 2 words; bit 31 - b
-    of word q is sample tile*128 + 16w + (L & 15), feature 16(8q + (b >> 2)) + 4(L >> 4) + (b & 3)
-    (the words are built by shifting left one value at a time, value 32 q + b in increasing order).
+    Layout: per 128-sample tile, wave w (8), layer l (h1, h2, v1, v2) and lane L, 2 words; bit b of
+    word q is sample tile*128 + 16w + (L & 15), feature 16(8q + (b >> 2)) + 4(L >> 4) + (b & 3).
     """
     w = words.detach().cpu().to(torch.int64) & 0xFFFFFFFF
     tiles = w.numel() // (8 * 4 * 64 * 2)
-    bits = ((w.view(tiles, 8, 4, 64, 2, 1) >> (31 - torch.arange(32))) & 1).float()
+    bits = ((w.view(tiles, 8, 4, 64, 2, 1) >> torch.arange(32)) & 1).float()
     lane = torch.arange(64).view(64, 1, 1)
     q = torch.arange(2).view(1, 2, 1)
     b = torch.arange(32).view(1, 1, 32)
