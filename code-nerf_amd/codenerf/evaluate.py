@@ -213,7 +213,10 @@ def test_time_optimize(target_pixels: torch.Tensor, samplers, embedders, models,
     forms weight gradients that its optimiser never reads; they do not change the result, and
     freezing skips those GEMMs.
     ``graph``: run the iterations as replays of one captured HIP graph (GraphedEvalStep; needs
-    frozen models, val_type AdamW and the numpy ray draw) -- the same arithmetic and draws.
+    frozen models, val_type AdamW and the numpy ray draw) -- the same arithmetic and draws.  Off by
+    default: the eager loop is GPU-bound (C5 3.585 ms eager vs 3.592 ms replayed, DESIGN.md section 8
+    item 3); the graph pays only where the host is the bottleneck.
+
     Returns (shape_code, texture_code, (theta, phi, rho), history, cam_pose of the last iteration).
     """
     dev = target_pixels.device
