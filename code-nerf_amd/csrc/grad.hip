@@ -493,6 +493,7 @@ __device__ __forceinline__ void tn256_body(float* ring, const float* __restrict_
   // operands of row pair p + 1 are read while pair p's MFMAs run -- across stages too: the last pair
   // of stage st reads stage st+1's first, so the barrier is followed by MFMAs, not by LDS latency
   float a[2][2], b[2][4];
+  float dsg[2] = {0.0f, 0.0f};  // SIG: the pair's d sigma (d raw column 3), read with its operands
   for (int st = 0; st < n_stages; ++st) {
     // stages st AND st+1 landed (all but this wave's kTwRows / 4 youngest pieces: stage st+2's) and
     // every wave is done with stage st-1, whose slot then receives stage st+3 (issued after this
@@ -503,6 +504,10 @@ __device__ __forceinline__ void tn256_body(float* ring, const float* __restrict_
 #ifdef CN_PROBE_TN_WAITPROF
     const long long tp0 = clock64();
 #endif
+    // lgkmcnt(0) as the compiler's own wait (it does not read the asm's): the next stage's first
+    // operands, read during the last pair, have landed, so nothing is owed at the loop header and the
+    // first MFMAs start at once
+    __builtin_amdgcn_s_waitcnt(0xC07F);
     if constexpr (SIG) asm volatile("s_waitcnt vmcnt(5)\n\ts_barrier" ::: "memory");
     else if (DIRS && flushed) asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
@@ -529,6 +534,7 @@ __device__ __forceinline__ void tn256_body(float* ring, const float* __restrict_
       for (int t = 0; t < 2; ++t) a[0][t] = sa[n0 + 32 * t];
 #pragma unroll
       for (int u = 0; u < 4; ++u) b[0][u] = sb[k0 + 32 * u];
+      if constexpr (SIG) dsg[0] = sb[kTwRows * 256 - (h * 256 + i) + h * 4 + 3];
     }
 #pragma unroll
     for (int p = 0; p < kTwRows / 2; ++p) {
@@ -538,13 +544,20 @@ __device__ __forceinline__ void tn256_body(float* ring, const float* __restrict_
         for (int t = 0; t < 2; ++t) a[nx][t] = sa[(p + 1) * 512 + n0 + 32 * t];
 #pragma unroll
         for (int u = 0; u < 4; ++u) b[nx][u] = sb[(p + 1) * 512 + k0 + 32 * u];
+        if constexpr (SIG) dsg[nx] = sb[kTwRows * 256 - (h * 256 + i) + (2 * (p + 1) + h) * 4 + 3];
       } else {
         // stage st+1's first pair (past the last stage: slot st+1 holds zeros or a stale stage; unused)
 #pragma unroll
         for (int t = 0; t < 2; ++t) a[nx][t] = sa1[n0 + 32 * t];
 #pragma unroll
         for (int u = 0; u < 4; ++u) b[nx][u] = sb1[k0 + 32 * u];
+        if constexpr (SIG) dsg[nx] = sb1[kTwRows * 256 - (h * 256 + i) + h * 4 + 3];
       }
+#ifndef CN_TN_SINK_READS
+      // keep the next pair's reads above this pair's MFMAs: left to itself the scheduler sinks them
+      // below, and every pair then opens with an exposed LDS round trip (lgkmcnt(0) before its MFMAs)
+      __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         // the bias gradient's column sum (DIRS: per direction) rides on the A stream (VALU beside MFMA)
@@ -555,11 +568,9 @@ __device__ __forceinline__ void tn256_body(float* ring, const float* __restrict_
           acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[c][t], b[c][u], acc[t][u], 0, 0, 0);
       }
       if constexpr (SIG) {
-        if (sig_wave) {
-          const float dsg = sb[kTwRows * 256 - (h * 256 + i) + (2 * p + h) * 4 + 3];
+        // every wave (no branch in the MFMA stream); only the sig waves' sums are stored
 #pragma unroll
-          for (int u = 0; u < 4; ++u) sacc[u] = fmaf(dsg, b[c][u], sacc[u]);
-        }
+        for (int u = 0; u < 4; ++u) sacc[u] = fmaf(dsg[c], b[c][u], sacc[u]);
       }
       if (p == 0) {
         __builtin_amdgcn_sched_barrier(0);

@@ -35,6 +35,45 @@ __global__ void sample_uniform_kernel(const float* __restrict__ ro, const float*
   }
 }
 
+// The same for nc % 4 == 0 (every config: 32 / 64 coarse samples) and 16-B aligned buffers: one
+// lane per 4 consecutive samples of a ray -- 16-B loads of the bins / bounds / draws and 16-B stores
+// of z (a wave stores 1 KiB per instruction; pts as 3 x 16 B per lane, 3 KiB contiguous per wave),
+// 32-bit index math (n_rays * nc / 4 < 2^32, checked by the host) instead of a 64-bit divide per
+// sample, and one pass over a grid that covers the work (no grid-stride loop).  Bitwise the same
+// arithmetic per sample.
+__global__ __launch_bounds__(256) void sample_uniform4_kernel(const float* __restrict__ ro, const float* __restrict__ rd,
+                                                              unsigned n4, unsigned nc4, const float4* __restrict__ zb,
+                                                              const float4* __restrict__ lower,
+                                                              const float4* __restrict__ upper,
+                                                              const float4* __restrict__ t_rand, float4* __restrict__ z_out,
+                                                              float4* __restrict__ pts_out) {
+  const unsigned q = blockIdx.x * 256u + threadIdx.x;
+  if (q >= n4) return;
+  const unsigned r = q / nc4, i4 = q - r * nc4;
+  float4 z;
+  if (t_rand) {
+    const float4 lo = lower[i4], up = upper[i4], t = t_rand[q];
+    z.x = __fadd_rn(lo.x, __fmul_rn(__fsub_rn(up.x, lo.x), t.x));
+    z.y = __fadd_rn(lo.y, __fmul_rn(__fsub_rn(up.y, lo.y), t.y));
+    z.z = __fadd_rn(lo.z, __fmul_rn(__fsub_rn(up.z, lo.z), t.z));
+    z.w = __fadd_rn(lo.w, __fmul_rn(__fsub_rn(up.w, lo.w), t.w));
+  } else {
+    z = zb[i4];
+  }
+  z_out[q] = z;
+  if (pts_out) {
+    const float o0 = ro[3 * r], o1 = ro[3 * r + 1], o2 = ro[3 * r + 2];
+    const float d0 = rd[3 * r], d1 = rd[3 * r + 1], d2 = rd[3 * r + 2];
+    float4* po = pts_out + 3 * static_cast<size_t>(q);
+    po[0] = make_float4(cn::mul_add_rn(d0, z.x, o0), cn::mul_add_rn(d1, z.x, o1), cn::mul_add_rn(d2, z.x, o2),
+                        cn::mul_add_rn(d0, z.y, o0));
+    po[1] = make_float4(cn::mul_add_rn(d1, z.y, o1), cn::mul_add_rn(d2, z.y, o2), cn::mul_add_rn(d0, z.z, o0),
+                        cn::mul_add_rn(d1, z.z, o1));
+    po[2] = make_float4(cn::mul_add_rn(d2, z.z, o2), cn::mul_add_rn(d0, z.w, o0), cn::mul_add_rn(d1, z.w, o1),
+                        cn::mul_add_rn(d2, z.w, o2));
+  }
+}
+
 // pts = ro[..., None, :] + rd[..., None, :] * z[..., :, None] (point_sampler.py:70, :118).
 __global__ void ray_points_kernel(const float* __restrict__ ro, const float* __restrict__ rd,
                                   const float* __restrict__ z, int64_t n_rays, int64_t s,
@@ -178,6 +217,17 @@ extern "C" int cn_sample_uniform(const float* ro, const float* rd, int64_t n_ray
   CN_CHECK_ARG(t_rand ? (lower && upper) : (z_bins != nullptr));
   CN_CHECK_ARG(!pts_out || (ro && rd));
   const int64_t n = n_rays * nc;
+  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (nc % 4 == 0 && n / 4 < (int64_t(1) << 32) - 256 && al16(z_out) && al16(pts_out) &&
+      (t_rand ? (al16(t_rand) && al16(lower) && al16(upper)) : al16(z_bins))) {
+    const unsigned n4 = static_cast<unsigned>(n / 4);
+    hipLaunchKernelGGL(sample_uniform4_kernel, dim3(static_cast<unsigned>(cn::ceil_div(n / 4, 256))), dim3(256), 0,
+                       cn::as_stream(stream), ro, rd, n4, static_cast<unsigned>(nc / 4),
+                       reinterpret_cast<const float4*>(z_bins), reinterpret_cast<const float4*>(lower),
+                       reinterpret_cast<const float4*>(upper), reinterpret_cast<const float4*>(t_rand),
+                       reinterpret_cast<float4*>(z_out), reinterpret_cast<float4*>(pts_out));
+    return cn::launch_status();
+  }
   hipLaunchKernelGGL(sample_uniform_kernel, dim3(cn::elementwise_grid(n, 256)), dim3(256), 0,
                      cn::as_stream(stream), ro, rd, n_rays, z_bins, lower, upper, nc, t_rand,
                      z_out, pts_out);

@@ -19,6 +19,18 @@ namespace {
 constexpr int kMaxRun = 8;
 constexpr int kMaxSamples = 64 * kMaxRun;  // 512
 
+// Raw rows, depths and weights cross the kernel once: non-temporal 16-B loads and stores (streamed
+// past the caches) -- the C2 launch 91 -> 86 us alone, 83 -> 74 us with the grouped launch (r04,
+// tools/volume_timing.py, HIP-event medians).
+typedef float nt_f4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 nt_load4(const float4* p) {
+  const nt_f4 v = __builtin_nontemporal_load(reinterpret_cast<const nt_f4*>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void nt_store4(float4 v, float4* p) {
+  __builtin_nontemporal_store(nt_f4{v.x, v.y, v.z, v.w}, reinterpret_cast<nt_f4*>(p));
+}
+
 template <int CTRL>
 __device__ __forceinline__ float dppf(float x) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, true));
@@ -128,7 +140,7 @@ __device__ __forceinline__ void load_depths(const float* zr, int j0, int run, in
 #pragma unroll
     for (int q = 0; q < K / 4; ++q) {
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (4 * q < run) v = reinterpret_cast<const float4*>(zr + j0)[q];
+      if (4 * q < run) v = nt_load4(reinterpret_cast<const float4*>(zr + j0) + q);
       zz[4 * q] = v.x;
       zz[4 * q + 1] = v.y;
       zz[4 * q + 2] = v.z;
@@ -157,12 +169,13 @@ __device__ __forceinline__ void load_run(const float* zr, const float4* rr, int 
 // its own run from there.  The backward stores d raw back the same way.  <= 64 K quads per wave.
 __device__ __forceinline__ int pad4(int q) { return q + (q >> 2); }
 
+
 template <int K>
 __device__ __forceinline__ void stage_rows_in(const float4* __restrict__ src, int nq, float4* sl, int lane) {
 #pragma unroll
   for (int t = 0; t < K; ++t) {
     const int q = lane + 64 * t;
-    if (q < nq) sl[pad4(q)] = src[q];
+    if (q < nq) sl[pad4(q)] = nt_load4(src + q);
   }
 }
 
@@ -182,25 +195,12 @@ __device__ __forceinline__ void load_raw_lds(const float4* sl, int q0, int j0, i
   for (int i = 0; i < K; ++i) rv[i] = (i < run && j0 + i < S_in) ? sl[pad4(q0 + i)] : make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
+// One lane's part of a ray (lane sub of its L): the run's depths zz and raw rows rv loaded, |rd| = nrm.
 template <int K, bool FULL, int L>
-__global__ __launch_bounds__(256) void volume_render_kernel(
-    const float* __restrict__ raw, const float* __restrict__ z, const float* __restrict__ rd,
-    int64_t n_rays, int S_in, float* __restrict__ rgb, float* __restrict__ disp,
-    float* __restrict__ acc, float* __restrict__ weights, float* __restrict__ depth) {
-  static_assert(K <= kMaxRun && (L == 16 || L == 64) && (!FULL || L == 16), "instance");
-  if (FULL) S_in = L * K;  // the host dispatches FULL only for S == 16 K: lets every bound fold
-  __shared__ float4 slds[4 * 80 * K];  // per wave: <= 64 K quads, padded 5 / 4
-  const int sub = threadIdx.x & (L - 1), lane = threadIdx.x & 63;
-  const int64_t r = ((int64_t)blockIdx.x * 256 + threadIdx.x) / L;
-  const int64_t rw0 = r - lane / L;  // the wave's first ray
-  float4* sl = slds + (threadIdx.x >> 6) * 80 * K;
-  if (rw0 < n_rays)
-    stage_rows_in<K>(reinterpret_cast<const float4*>(raw) + rw0 * S_in,
-                     static_cast<int>(min<int64_t>(64 / L, n_rays - rw0)) * S_in, sl, lane);
-  // lanes read quads other lanes wrote: keep the staging stores ahead of the reads (no instruction;
-  // LDS operations of one wave then execute in program order)
-  __builtin_amdgcn_wave_barrier();
-  if (r >= n_rays) return;  // whole rays leave together: the cross-lane steps never read an exited lane
+__device__ __forceinline__ void render_run(const float (&zz)[K], const float4 (&rv)[K], int S_in, int64_t r, float nrm,
+                                           float* __restrict__ rgb, float* __restrict__ disp, float* __restrict__ acc,
+                                           float* __restrict__ weights, float* __restrict__ depth) {
+  const int sub = threadIdx.x & (L - 1);
   // S == 1: the reference's dists = cat(z[1:] - z[:-1], full_like(that[..., :1], 1e10))
   // is EMPTY (both pieces are 0 wide), so no sample contributes (rgb = acc = depth = 0,
   // disp = NaN, weights (R, 0)).  Reproduced by treating the ray as sample-free.
@@ -208,14 +208,7 @@ __global__ __launch_bounds__(256) void volume_render_kernel(
   const int S = FULL ? L * K : (S_in == 1 ? 0 : S_in);
   const int run = FULL ? K : (S_in + L - 1) / L;
   const int j0 = sub * run;
-  const float* zr = z + r * S_in;
-  const float d0 = rd[3 * r], d1 = rd[3 * r + 1], d2 = rd[3 * r + 2];
-  const float nrm = __fsqrt_rn(__fadd_rn(__fadd_rn(__fmul_rn(d0, d0), __fmul_rn(d1, d1)), __fmul_rn(d2, d2)));
-
-  float zz[K], sd[K], wv[K];
-  float4 rv[K];
-  load_depths<K>(zr, j0, run, S_in, zz);
-  load_raw_lds<K>(sl, (lane / L) * S_in + j0, j0, run, S_in, rv);
+  float sd[K], wv[K];
   const float znext = next_lane<L>(zz[0]);  // the first depth of lane sub + 1's run
   double run_sum = 0.0;  // sum of this run's sigma*delta that feeds later transmittances
 #pragma unroll
@@ -261,7 +254,8 @@ __global__ __launch_bounds__(256) void volume_render_kernel(
 #pragma unroll
       for (int q = 0; q < K / 4; ++q)
         if (4 * q < run)
-          reinterpret_cast<float4*>(wr + j0)[q] = make_float4(wv[4 * q], wv[4 * q + 1], wv[4 * q + 2], wv[4 * q + 3]);
+          nt_store4(make_float4(wv[4 * q], wv[4 * q + 1], wv[4 * q + 2], wv[4 * q + 3]),
+                                      reinterpret_cast<float4*>(wr + j0) + q);
     } else {
 #pragma unroll
       for (int i = 0; i < K; ++i)
@@ -282,6 +276,86 @@ __global__ __launch_bounds__(256) void volume_render_kernel(
     // (:63) torch.max propagates NaN: disp is NaN when acc == 0
     const float q = dep / ac;
     disp[r] = (q != q) ? q : 1.0f / fmaxf(1e-10f, q);
+  }
+}
+
+template <int K, bool FULL, int L>
+__global__ __launch_bounds__(256) void volume_render_kernel(
+    const float* __restrict__ raw, const float* __restrict__ z, const float* __restrict__ rd,
+    int64_t n_rays, int S_in, float* __restrict__ rgb, float* __restrict__ disp,
+    float* __restrict__ acc, float* __restrict__ weights, float* __restrict__ depth) {
+  static_assert(K <= kMaxRun && (L == 16 || L == 64) && (!FULL || L == 16), "instance");
+  if (FULL) S_in = L * K;  // the host dispatches FULL only for S == 16 K: lets every bound fold
+  __shared__ float4 slds[4 * 80 * K];  // per wave: <= 64 K quads, padded 5 / 4
+  const int sub = threadIdx.x & (L - 1), lane = threadIdx.x & 63;
+  const int64_t r = ((int64_t)blockIdx.x * 256 + threadIdx.x) / L;
+  const int64_t rw0 = r - lane / L;  // the wave's first ray
+  float4* sl = slds + (threadIdx.x >> 6) * 80 * K;
+  if (rw0 < n_rays)
+    stage_rows_in<K>(reinterpret_cast<const float4*>(raw) + rw0 * S_in,
+                     static_cast<int>(min<int64_t>(64 / L, n_rays - rw0)) * S_in, sl, lane);
+  // lanes read quads other lanes wrote: keep the staging stores ahead of the reads (no instruction;
+  // LDS operations of one wave then execute in program order)
+  __builtin_amdgcn_wave_barrier();
+  if (r >= n_rays) return;  // whole rays leave together: the cross-lane steps never read an exited lane
+  const int run = FULL ? K : (S_in + L - 1) / L;
+  const int j0 = sub * run;
+  const float* zr = z + r * S_in;
+  const float d0 = rd[3 * r], d1 = rd[3 * r + 1], d2 = rd[3 * r + 2];
+  const float nrm = __fsqrt_rn(__fadd_rn(__fadd_rn(__fmul_rn(d0, d0), __fmul_rn(d1, d1)), __fmul_rn(d2, d2)));
+  float zz[K];
+  float4 rv[K];
+  load_depths<K>(zr, j0, run, S_in, zz);
+  load_raw_lds<K>(sl, (lane / L) * S_in + j0, j0, run, S_in, rv);
+  render_run<K, FULL, L>(zz, rv, S_in, r, nrm, rgb, disp, acc, weights, depth);
+}
+
+// S = 16 K with n_rays % 4 == 0 (the C2 / C3 shapes): wave w renders G groups of 4 rays, groups
+// w + g W of the grid's W waves.  Every group's raw rows, depths and directions are loaded up front,
+// so the later groups' loads are in flight while the wave integrates the earlier ones.
+template <int K, int G>
+__global__ __launch_bounds__(256) void volume_render_groups_kernel(
+    const float* __restrict__ raw, const float* __restrict__ z, const float* __restrict__ rd, int64_t n_rays,
+    float* __restrict__ rgb, float* __restrict__ disp, float* __restrict__ acc, float* __restrict__ weights,
+    float* __restrict__ depth) {
+  constexpr int L = 16, S = L * K;
+  __shared__ float4 slds[4 * 80 * K];
+  const int lane = threadIdx.x & 63, sub = lane & 15;
+  float4* sl = slds + (threadIdx.x >> 6) * 80 * K;
+  const int64_t n_waves = (int64_t)gridDim.x * 4, wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  float4 stg[G][K];
+  float zz[G][K], dv[G][3];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    // past the end: a copy of the last group (no branch around the loads, so the arrays stay in registers)
+    const int64_t rw0 = min(4 * (wave + g * n_waves), n_rays - 4);
+    const float4* src = reinterpret_cast<const float4*>(raw) + rw0 * S;
+#pragma unroll
+    for (int t = 0; t < K; ++t) stg[g][t] = nt_load4(src + lane + 64 * t);
+    const int64_t r = rw0 + lane / L;
+    float zl[K];
+    load_depths<K>(z + r * S, sub * K, K, S, zl);
+#pragma unroll
+    for (int i = 0; i < K; ++i) zz[g][i] = zl[i];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) dv[g][d] = rd[3 * r + d];
+  }
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const int64_t rw0 = 4 * (wave + g * n_waves);
+    if (rw0 >= n_rays) continue;  // wave-uniform
+#pragma unroll
+    for (int t = 0; t < K; ++t) sl[pad4(lane + 64 * t)] = stg[g][t];
+    __builtin_amdgcn_wave_barrier();
+    float4 rv[K];
+    load_raw_lds<K>(sl, (lane / L) * S + sub * K, sub * K, K, S, rv);
+    __builtin_amdgcn_wave_barrier();
+    float zg[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) zg[i] = zz[g][i];
+    const float nrm = __fsqrt_rn(__fadd_rn(__fadd_rn(__fmul_rn(dv[g][0], dv[g][0]), __fmul_rn(dv[g][1], dv[g][1])),
+                                           __fmul_rn(dv[g][2], dv[g][2])));
+    render_run<K, true, L>(zg, rv, S, rw0 + lane / L, nrm, rgb, disp, acc, weights, depth);
   }
 }
 
@@ -306,6 +380,13 @@ extern "C" int cn_volume_render(const float* raw, const float* z, const float* r
                                 float* weights, float* depth, cn_stream_t stream) {
   CN_CHECK_ARG(raw && z && rd && rgb && disp && acc && depth);
   CN_CHECK_ARG(n_rays > 0 && n_samples > 0 && n_samples <= kMaxSamples);
+  if (n_samples == 64 && n_rays % 4 == 0) {  // C2 / C5 coarse: two ray groups per wave
+    constexpr int G = 2;
+    const int64_t waves = cn::ceil_div(n_rays / 4, G);
+    hipLaunchKernelGGL((volume_render_groups_kernel<4, G>), dim3(static_cast<unsigned>(cn::ceil_div(waves, 4))),
+                       dim3(256), 0, cn::as_stream(stream), raw, z, rd, n_rays, rgb, disp, acc, weights, depth);
+    return cn::launch_status();
+  }
   CN_VOLUME_DISPATCH(volume_render_kernel, n_samples, n_rays, cn::as_stream(stream), raw, z, rd, n_rays,
                      static_cast<int>(n_samples), rgb, disp, acc, weights, depth);
   return cn::launch_status();

@@ -110,6 +110,36 @@ def test_points(dev, tag):
         assert maxdiff(pf, g[tag + "_ptsf"]) <= 2e-6
 
 
+@pytest.mark.parametrize("nc", [6, 13, 64])
+@pytest.mark.parametrize("perturb", [False, True])
+def test_sample_uniform_shapes_vs_oracle(dev, nc, perturb):
+    """cn_sample_uniform's two forms: nc % 4 == 0 (16-B lanes, 64) and the per-sample kernel (6, 13),
+    with and without the perturbed draw, bit-exact vs the oracle on the same inputs; plus an
+    unaligned output (offset by one float) that must take the per-sample form and agree."""
+    from codenerf import ops
+    from codenerf.nerf import PointSampler
+    from oracle import codenerf_oracle as O
+    g = torch.Generator().manual_seed(nc)
+    R = 1000
+    ro = torch.randn(R, 3, generator=g)
+    rd = torch.randn(R, 3, generator=g)
+    ps = PointSampler(nc, 8, 0.8, 1.8, spacing_mode="lindepth", perturb=perturb, dtype=torch.float32, device=dev)
+    t_rand = torch.rand(R, nc, generator=g) if perturb else None
+    t_dev = None if t_rand is None else t_rand.to(dev)
+    pts, z = ops.sample_uniform(ro.to(dev), rd.to(dev), ps.z_vals, ps.lower, ps.upper, t_dev)
+    pts_o, z_o = O.sample_uniform(ro, rd, O.Sampling(nc, 8, 0.8, 1.8).bins, t_rand)
+    assert torch.equal(z.cpu(), z_o) and torch.equal(pts.cpu(), pts_o)
+    zbuf = torch.empty(R * nc + 1, device=dev)
+    pbuf = torch.empty(R * nc * 3 + 1, device=dev)
+    ro_d, rd_d = ro.to(dev), rd.to(dev)
+    ops.check(ops._lib_ready().cn_sample_uniform(ops.ptr(ro_d), ops.ptr(rd_d), R, ops.ptr(ps.z_vals),
+                                                 ops.ptr(ps.lower), ops.ptr(ps.upper), nc, ops.ptr(t_dev),
+                                                 ops.ptr(zbuf[1:]), ops.ptr(pbuf[1:]), ops.stream_of(zbuf)),
+              "cn_sample_uniform")
+    torch.cuda.synchronize()
+    assert torch.equal(zbuf[1:].view(R, nc).cpu(), z_o) and torch.equal(pbuf[1:].view(R, nc, 3).cpu(), pts_o)
+
+
 def test_sample_pdf_strided_weights_and_indices(dev):
     """weights[..., 1:-1] view (nerf/__init__.py:87) and searchsorted indices vs the oracle."""
     from oracle import codenerf_oracle as O
@@ -176,6 +206,31 @@ def test_volume_render_sizes(dev, s):
     for a, b in zip(got, ref):
         fin = torch.isfinite(b)
         assert maxdiff(a.cpu()[fin], b[fin]) <= tol
+
+
+@pytest.mark.parametrize("n", [4, 1028, 262144])
+def test_volume_render_grouped_path(dev, n):
+    """S = 64 with n_rays % 4 == 0 takes the grouped launch (two ray groups per wave, the second's loads
+    in flight during the first's integration, the grid's last wave past the end); n + 1 rays take the
+    per-group kernel.  The first n rays must agree bit for bit (same arithmetic per ray), and with the
+    oracle at test_volume_render_sizes' bound (n = 262144: the C2 launch, checked on a ray sample)."""
+    from oracle import codenerf_oracle as O
+    from codenerf import ops
+    g = torch.Generator().manual_seed(n)
+    raw = torch.randn(n + 1, 64, 4, generator=g) * 2
+    z = torch.sort(1 + torch.rand(n + 1, 64, generator=g), -1).values
+    rd = torch.randn(n + 1, 3, generator=g)
+    grouped = ops.volume_render(raw[:n].to(dev), z[:n].to(dev), rd[:n].to(dev))
+    single = ops.volume_render(raw.to(dev), z.to(dev), rd.to(dev))
+    for a, b in zip(grouped, single):
+        fa, fb = a.cpu(), b[:n].cpu()
+        assert torch.equal(torch.isnan(fa), torch.isnan(fb))
+        assert torch.equal(fa[~torch.isnan(fa)], fb[~torch.isnan(fb)])
+    pick = torch.randperm(n, generator=g)[:4096] if n > 4096 else torch.arange(n)
+    ref = O.volume_render(raw[pick], z[pick], rd[pick])
+    for a, b in zip(grouped, ref):
+        fin = torch.isfinite(b)
+        assert maxdiff(a.cpu()[pick][fin], b[fin]) <= 5e-6
 
 
 # ---------------------------------------------------------------- MLP

@@ -1,5 +1,6 @@
 """HIP-event timing of the C2 volume_render launch (262,144 rays x 64 samples) in isolation, with and
-without the weights output, and right after a C2 field launch (the bench's order).
+without the weights output, and of the C2 sample_uniform launch (z only, as the bench; perturbed;
+with points).
     python tools/volume_timing.py [--rays 262144] [--samples 64] [--iters 20]"""
 import argparse
 import json
@@ -43,6 +44,14 @@ def main():
     for w in (True, False):
         med, best = timed(lambda: ops.volume_render(raw, z, rd, want_weights=w), args.iters)
         out["weights" if w else "no_weights"] = {"median_us": med, "min_us": best, "TBps": nbytes(w) / (med * 1e-6) / 1e12}
+    from codenerf.nerf import PointSampler
+    ps = PointSampler(s, s, 0.8, 1.8, spacing_mode="lindepth", perturb=False, dtype=torch.float32, device=dev)
+    ro = torch.randn(n, 3, generator=g).to(dev)
+    t_rand = torch.rand(n, s, generator=g).to(dev)
+    for name, t, pts in (("uniform_z", None, False), ("uniform_z_perturbed", t_rand, False), ("uniform_pts", None, True)):
+        med, best = timed(lambda: ops.sample_uniform(ro, rd, ps.z_vals, ps.lower, ps.upper, t, want_pts=pts), args.iters)
+        b = n * (24 if pts else 0) + n * s * (4 + (4 if t is not None else 0) + (12 if pts else 0))
+        out[name] = {"median_us": med, "min_us": best, "TBps": b / (med * 1e-6) / 1e12}
     print(json.dumps(out))
 
 
