@@ -1204,7 +1204,7 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __rest
     const float4 x4 = xs[st % 3][es];
     const float x[4] = {x4.x, x4.y, x4.z, 0.0f};
     if (kind == 1) {
-      sincosf(__fmul_rn(x[comp], freq), &ev[0], &ev[1]);  // the forward's encoding arithmetic
+      mlp::enc_sincosf(__fmul_rn(x[comp], freq), ev[0], ev[1]);  // the forward's encoding arithmetic
     } else if (kind == 2) {
       ev[0] = comp < 3 ? x[comp] : 0.0f;
       ev[1] = comp + 1 < 3 ? x[comp + 1] : 0.0f;
@@ -1321,7 +1321,7 @@ __global__ __launch_bounds__(256) void dir_enc_dw_kernel(mlp::FieldArgs a, DirFo
       float vd[3];
       mlp::view_dir(a, 16 * (int64_t)g + r, vd);
       float s, c;
-      sincosf(__fmul_rn(mlp::pick3(vd, comp), a.fd[p / 3]), &s, &c);
+      mlp::enc_sincosf(__fmul_rn(mlp::pick3(vd, comp), a.fd[p / 3]), s, c);
       encl[r][c0] = s;
       encl[r][c0 + 3] = c;
     } else if (n < 16 * 13) {

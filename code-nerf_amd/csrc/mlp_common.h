@@ -81,6 +81,14 @@ __device__ __forceinline__ void fast_sincosf(float x, float& sn, float& cs) {
   cs = ((q + 1) & 2) ? -c1 : c1;
 }
 
+// An encoding's (sin, cos) for the dW kernels that regenerate the encodings: fast_sincosf inside
+// its bound -- the arithmetic the field kernels' lazy path used for every in-range wave (and, unlike
+// ocml's sincosf, ~20 VALU instructions without a branch) -- ocml's sincosf beyond it, per lane.
+__device__ __forceinline__ void enc_sincosf(float x, float& sn, float& cs) {
+  if (fabsf(x) <= kFastSinBound) fast_sincosf(x, sn, cs);
+  else sincosf(x, &sn, &cs);
+}
+
 // One sample's inputs: point, unit Q1 view direction, code row.
 struct SampleIn {
   float x[3];
