@@ -1094,8 +1094,13 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __rest
                                                              float* __restrict__ part, float* __restrict__ bias_part,
                                                              int64_t rows_per_block) {
   constexpr int K = ENC == 0 ? 63 : 27, KB = ENC == 0 ? 2 : 1, EW = 32 * KB;
-  __shared__ __attribute__((aligned(16))) float ring[kEncRing][kEncRows * 256];  // A stages, by LDS-DMA
-  __shared__ __attribute__((aligned(16))) float senc[2][kEncRows * EW];
+  // row strides (floats) of the A ring and the encoding table: the two rows a wave's half-waves
+  // read together (fp32: rows 2 p and 2 p + 1; x3: rows j and 8 + j) sit 32 banks apart -- with
+  // 256 / 64-float rows they hit the same banks (a 2-way conflict on every read)
+  constexpr int RS = X3 ? 260 : 288;
+  constexpr int ES = X3 ? EW + 4 : (EW % 64 == 0 ? EW + 32 : EW);
+  __shared__ __attribute__((aligned(16))) float ring[kEncRing][kEncRows * RS];  // A stages, by LDS-DMA
+  __shared__ __attribute__((aligned(16))) float senc[2][kEncRows * ES];
   __shared__ __attribute__((aligned(16))) float4 xs[3][kEncRows];  // decoded geometry, 3 stages
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1142,7 +1147,7 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __rest
     for (int j = 0; j < kEncRows / 8; ++j) {
       const int r = wave + 8 * j;
       const unsigned soff = __builtin_amdgcn_readfirstlane(static_cast<unsigned>((st * kEncRows + r) * 1024));
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(slot + r * 256), 16, lane * 16u, soff, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(slot + r * RS), 16, lane * 16u, soff, 0, 0);
     }
   };
   // decode(st) only ISSUES the loads of stage st's geometry (threads 0..15 of wave 0): the point's
@@ -1212,8 +1217,8 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __rest
   };
   auto store_enc = [&](int buf) {
     if (kind != 0) {
-      senc[buf][es * EW + c0] = ev[0];
-      senc[buf][es * EW + c1] = ev[1];
+      senc[buf][es * ES + c0] = ev[0];
+      senc[buf][es * ES + c1] = ev[1];
     }
   };
   floatx16 acc[KB];
@@ -1248,14 +1253,14 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __rest
     const float* se = senc[st & 1];
     if constexpr (X3) {
       float v[8];
-      ring_read8<1024>(sa + (8 * h) * 256 + 32 * wave + i, v);   // rows 8 h + j
+      ring_read8<RS * 4>(sa + (8 * h) * RS + 32 * wave + i, v);   // rows 8 h + j
       bsum += sum8v(v);
       u32x4 ah, al;
       split8(v, ah, al);
 #pragma unroll
       for (int u = 0; u < KB; ++u) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = se[(8 * h + j) * EW + 32 * u + i];
+        for (int j = 0; j < 8; ++j) v[j] = se[(8 * h + j) * ES + 32 * u + i];
         u32x4 bh, bl;
         split8(v, bh, bl);
         acc[u] = mfma3(acc[u], ah, al, bh, bl);
@@ -1264,9 +1269,9 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __rest
       // the stage's A values and its encoding operands, each read in one round trip before the
       // MFMAs (read per row pair, the B operands exposed an LDS wait before every MFMA pair)
       float xa[8], xb[KB][8];
-      ring_read8<2048>(sa + h * 256 + 32 * wave + i, xa);          // rows 2 p + h
+      ring_read8<2 * RS * 4>(sa + h * RS + 32 * wave + i, xa);          // rows 2 p + h
 #pragma unroll
-      for (int u = 0; u < KB; ++u) ring_read8<2 * EW * 4>(se + h * EW + 32 * u + i, xb[u]);
+      for (int u = 0; u < KB; ++u) ring_read8<2 * ES * 4>(se + h * ES + 32 * u + i, xb[u]);
 #pragma unroll
       for (int p = 0; p < kEncRows / 2; ++p) {
         const float x = xa[p];
