@@ -553,11 +553,9 @@ __device__ __forceinline__ void tn256_body(float* ring, const float* __restrict_
         for (int u = 0; u < 4; ++u) b[nx][u] = sb1[k0 + 32 * u];
         if constexpr (SIG) dsg[nx] = sb1[kTwRows * 256 - (h * 256 + i) + h * 4 + 3];
       }
-#ifndef CN_TN_SINK_READS
       // keep the next pair's reads above this pair's MFMAs: left to itself the scheduler sinks them
       // below, and every pair then opens with an exposed LDS round trip (lgkmcnt(0) before its MFMAs)
       __builtin_amdgcn_sched_barrier(0);
-#endif
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         // the bias gradient's column sum (DIRS: per direction) rides on the A stream (VALU beside MFMA)
