@@ -29,6 +29,12 @@ def _cuda(t: Tensor, name: str, dtype=torch.float32) -> Tensor:
     return t.contiguous()
 
 
+def _aligned16(t: Tensor) -> Tensor:
+    """t itself when its data pointer is 16-B aligned (what the kernels' vector accesses need; every
+    fresh allocation is), else an aligned copy (a contiguous view at an odd element offset)."""
+    return t if t.data_ptr() % 16 == 0 else t.clone()
+
+
 def _lib_ready():
     return _lib.load()
 
@@ -233,6 +239,7 @@ def volume_render(raw: Tensor, z: Tensor, rd: Tensor, want_weights: bool = True)
     """volume_render (volumetric_render.py:36-66) -> rgb, disp, acc, weights, depth."""
     lib = _lib_ready()
     raw, z, rd = _cuda(raw, "radiance_field"), _cuda(z, "depth_values"), _cuda(rd, "ray_directions")
+    raw, z = _aligned16(raw), _aligned16(z)
     n, s = z.shape
     assert raw.shape == (n, s, 4), "radiance_field must be (num_rays, num_samples, 4)"
     assert rd.shape == (n, 3), "ray_directions must be (num_rays, 3)"
@@ -350,6 +357,7 @@ def volume_render_backward(raw: Tensor, z: Tensor, rd: Tensor, g_rgb=None, g_dis
     """Gradient of volume_render (volumetric_render.py:36-66) -> d_raw (R,S,4), d_rd (R,3) or None."""
     lib = _lib_ready()
     raw, z, rd = _cuda(raw, "radiance_field"), _cuda(z, "depth_values"), _cuda(rd, "ray_directions")
+    raw, z = _aligned16(raw), _aligned16(z)
     n, s = z.shape
     assert raw.shape == (n, s, 4) and rd.shape == (n, 3)
     g_rgb, g_disp, g_acc, g_depth = (_opt(g_rgb, "g_rgb"), _opt(g_disp, "g_disp"), _opt(g_acc, "g_acc"),

@@ -26,6 +26,9 @@ inline int launch_status() {
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // Grid for a grid-stride elementwise kernel: at most 256 CUs x 8 blocks.
+// NULL counts as aligned (an optional output).
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
 inline unsigned elementwise_grid(int64_t n, int block) {
   int64_t g = ceil_div(n, block);
   if (g > 2048) g = 2048;

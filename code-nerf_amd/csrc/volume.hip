@@ -380,6 +380,7 @@ extern "C" int cn_volume_render(const float* raw, const float* z, const float* r
                                 float* weights, float* depth, cn_stream_t stream) {
   CN_CHECK_ARG(raw && z && rd && rgb && disp && acc && depth);
   CN_CHECK_ARG(n_rays > 0 && n_samples > 0 && n_samples <= kMaxSamples);
+  CN_CHECK_ARG(cn::aligned16(raw) && cn::aligned16(z) && cn::aligned16(weights));
   if (n_samples == 64 && n_rays % 4 == 0) {  // C2 / C5 coarse: two ray groups per wave
     constexpr int G = 2;
     const int64_t waves = cn::ceil_div(n_rays / 4, G);
@@ -537,6 +538,7 @@ extern "C" int cn_volume_render_backward(const float* raw, const float* z, const
                                          float* d_raw, float* d_rd, cn_stream_t stream) {
   CN_CHECK_ARG(raw && z && rd && d_raw);
   CN_CHECK_ARG(n_rays > 0 && n_samples > 0 && n_samples <= kMaxSamples);
+  CN_CHECK_ARG(cn::aligned16(raw) && cn::aligned16(z) && cn::aligned16(d_raw));
   CN_VOLUME_DISPATCH(volume_render_backward_kernel, n_samples, n_rays, cn::as_stream(stream), raw, z, rd, n_rays,
                      static_cast<int>(n_samples), g_rgb, g_disp, g_acc, g_weights, g_depth, d_raw, d_rd);
   return cn::launch_status();

@@ -169,7 +169,8 @@ int cn_posenc(const float* x, int64_t m, int64_t d, const float* freqs, int64_t 
 
 /* volume_render, volumetric_render.py:36-66.
  * raw: (n_rays, n_samples, 4); z: (n_rays, n_samples); rd: (n_rays, 3);
- * rgb: (n_rays, 3); disp, acc, depth: (n_rays); weights: (n_rays, n_samples) or NULL. */
+ * rgb: (n_rays, 3); disp, acc, depth: (n_rays); weights: (n_rays, n_samples) or NULL.
+ * raw, z and weights are read / written with 16-B vector accesses: 16-B aligned, or CN_EINVAL. */
 int cn_volume_render(const float* raw, const float* z, const float* rd, int64_t n_rays,
                      int64_t n_samples, float* rgb, float* disp, float* acc, float* weights,
                      float* depth, cn_stream_t stream);
@@ -379,7 +380,7 @@ int cn_code_bias_backward_ws(const float* const* params, const float* z_s, const
 /* Backward of volume_render (volumetric_render.py:36-66) w.r.t. raw and rd
  * (z is detached in the reference).  Any of g_rgb (R,3), g_disp, g_acc, g_depth
  * (R), g_weights (R,S) may be NULL (zero).  d_raw (R,S,4) and d_rd (R,3, may be
- * NULL) are written. */
+ * NULL) are written.  raw, z and d_raw 16-B aligned, or CN_EINVAL. */
 int cn_volume_render_backward(const float* raw, const float* z, const float* rd, int64_t n_rays,
                               int64_t n_samples, const float* g_rgb, const float* g_disp,
                               const float* g_acc, const float* g_weights, const float* g_depth,

@@ -233,6 +233,31 @@ def test_volume_render_grouped_path(dev, n):
         assert maxdiff(a.cpu()[pick][fin], b[fin]) <= 5e-6
 
 
+def test_volume_render_unaligned_inputs(dev):
+    """raw / z as contiguous views at an odd element offset: the C ABI refuses them (CN_EINVAL, no
+    launch: its 16-B vector accesses need aligned rows), the Python op realigns them and returns the
+    aligned inputs' results bit for bit."""
+    from codenerf import ops
+    n, s = 256, 64
+    g = torch.Generator().manual_seed(3)
+    raw = (torch.randn(n, s, 4, generator=g) * 2).to(dev)
+    z = torch.sort(1 + torch.rand(n, s, generator=g), -1).values.to(dev)
+    rd = torch.randn(n, 3, generator=g).to(dev)
+    rbuf = torch.empty(n * s * 4 + 1, device=dev)
+    zbuf = torch.empty(n * s + 1, device=dev)
+    raw_u, z_u = rbuf[1:].view(n, s, 4), zbuf[1:].view(n, s)
+    raw_u.copy_(raw)
+    z_u.copy_(z)
+    assert raw_u.data_ptr() % 16 == 4 and z_u.is_contiguous()
+    outs = [torch.empty(n, 3, device=dev)] + [torch.empty(n, device=dev) for _ in range(3)]
+    rc = ops._lib_ready().cn_volume_render(ops.ptr(raw_u), ops.ptr(z_u), ops.ptr(rd), n, s, ops.ptr(outs[0]),
+                                           ops.ptr(outs[1]), ops.ptr(outs[2]), None, ops.ptr(outs[3]),
+                                           ops.stream_of(rd))
+    assert rc != 0, "an unaligned raw row must be refused"
+    for a, b in zip(ops.volume_render(raw_u, z_u, rd), ops.volume_render(raw, z, rd)):
+        assert torch.equal(torch.nan_to_num(a, nan=7.0), torch.nan_to_num(b, nan=7.0))
+
+
 # ---------------------------------------------------------------- MLP
 
 
