@@ -470,7 +470,7 @@ def field_backward_train(packed_t: Tensor, params: Sequence[Tensor], masks: Tens
     lib = _lib_ready()
     m = n_rays * n_samples
     params = [_cuda(p.detach(), f"param{i}") for i, p in enumerate(params)]
-    d_raw = _cuda(d_raw, "d_raw")
+    d_raw = _aligned16(_cuda(d_raw, "d_raw"))
     assert d_raw.numel() == 4 * m and saved.shape == (5, m, 256) and (x_enc is None or x_enc.shape == (m, 90))
     dev = d_raw.device
     rd, pts, ro, z = _opt(rd, "rd"), _opt(pts, "pts"), _opt(ro, "ro"), _opt(z, "z")
@@ -541,7 +541,7 @@ def field_backward(params: Sequence[Tensor], saved: Tensor, x_enc: Tensor, d_raw
     lib = _lib_ready()
     m = n_rays * n_samples
     params = [_cuda(p.detach(), f"param{i}") for i, p in enumerate(params)]
-    d_raw = _cuda(d_raw, "d_raw")
+    d_raw = _aligned16(_cuda(d_raw, "d_raw"))
     assert d_raw.numel() == 4 * m and saved.shape == (5, m, 256) and (x_enc is None or x_enc.shape == (m, 90))
     dev = d_raw.device
     rd, pts, ro, z = _opt(rd, "rd"), _opt(pts, "pts"), _opt(ro, "ro"), _opt(z, "z")
@@ -710,7 +710,7 @@ def field_backward_x3(packed_t: Tensor, masks: Tensor, d_raw: Tensor, n_rays: in
     fmt_t = _lib.CN_FMT_BF16X3_T if precision == "bf16x3" else _lib.CN_FMT_F32_W16_T
     lib = _lib_ready()
     m = n_rays * n_samples
-    d_raw = _cuda(d_raw, "d_raw")
+    d_raw = _aligned16(_cuda(d_raw, "d_raw"))
     assert d_raw.numel() == 4 * m
     dev = d_raw.device
     rd, pts, ro, z = _opt(rd, "rd"), _opt(pts, "pts"), _opt(ro, "ro"), _opt(z, "z")

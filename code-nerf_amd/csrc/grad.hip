@@ -2643,6 +2643,7 @@ extern "C" int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, con
   for (int i = 0; i < 4; ++i) a.fd[i] = freqs_dir[i];
   a.masks = const_cast<uint32_t*>(masks);
   a.d_raw = d_raw;
+  CN_CHECK_ARG(cn::aligned16(d_raw));  // float4 rows (include/codenerf.h)
   a.g_code = g_code;
   a.d_pts = d_pts;
   a.d_ro = d_ro;

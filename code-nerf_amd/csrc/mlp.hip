@@ -509,6 +509,7 @@ extern "C" int cn_mlp_forward(const float* packed, int fmt, const float* code_bi
   a.x = x;
   a.m = m;
   a.raw = raw;
+  CN_CHECK_ARG(cn::aligned16(raw));  // float4 rows (include/codenerf.h)
   return launch_field(fmt, kFromEncoded, a, cn::as_stream(stream));
 }
 
@@ -538,6 +539,7 @@ extern "C" int cn_radiance_field(const float* packed, int fmt, const float* code
   for (int i = 0; i < 10; ++i) a.fx[i] = freqs_xyz[i];
   for (int i = 0; i < 4; ++i) a.fd[i] = freqs_dir[i];
   a.raw = raw;
+  CN_CHECK_ARG(cn::aligned16(raw));  // float4 rows (include/codenerf.h)
   return launch_field(fmt, pts ? kFromPts : kFromRayZ, a, cn::as_stream(stream));
 }
 
@@ -567,6 +569,7 @@ extern "C" int cn_radiance_field_train(const float* packed, const float* code_bi
   for (int i = 0; i < 10; ++i) a.fx[i] = freqs_xyz[i];
   for (int i = 0; i < 4; ++i) a.fd[i] = freqs_dir[i];
   a.raw = raw;
+  CN_CHECK_ARG(cn::aligned16(raw));  // float4 rows (include/codenerf.h)
   a.save = save;
   return launch_field(CN_FMT_F32, pts ? kFromPts : kFromRayZ, a, cn::as_stream(stream));
 }
@@ -585,6 +588,7 @@ extern "C" int cn_mlp_forward_train(const float* packed, const float* code_bias,
   a.x = x;
   a.m = m;
   a.raw = raw;
+  CN_CHECK_ARG(cn::aligned16(raw));  // float4 rows (include/codenerf.h)
   a.save = save;
   return launch_field(CN_FMT_F32, kFromEncoded, a, cn::as_stream(stream));
 }
@@ -634,6 +638,7 @@ extern "C" int cn_radiance_field_masks_fmt(int fmt, const float* packed, const f
   for (int i = 0; i < 10; ++i) a.fx[i] = freqs_xyz[i];
   for (int i = 0; i < 4; ++i) a.fd[i] = freqs_dir[i];
   a.raw = raw;
+  CN_CHECK_ARG(cn::aligned16(raw));  // float4 rows (include/codenerf.h)
   a.masks = masks;
   return fmt == CN_FMT_BF16X3 ? launch_field_x3(pts ? kFromPts : kFromRayZ, a, cn::as_stream(stream))
                               : launch_field_w16(pts ? kFromPts : kFromRayZ, a, cn::as_stream(stream));
@@ -676,6 +681,7 @@ extern "C" int cn_radiance_field_train_fmt(int fmt, const float* packed, const f
   for (int i = 0; i < 10; ++i) a.fx[i] = freqs_xyz[i];
   for (int i = 0; i < 4; ++i) a.fd[i] = freqs_dir[i];
   a.raw = raw;
+  CN_CHECK_ARG(cn::aligned16(raw));  // float4 rows (include/codenerf.h)
   a.save = save;
   a.masks = masks;
   return fmt == CN_FMT_BF16X3 ? launch_field_x3(pts ? kFromPts : kFromRayZ, a, cn::as_stream(stream))
@@ -726,6 +732,7 @@ extern "C" int cn_field_backward_fused(int fmt_t, const float* packed_t, const u
   for (int i = 0; i < 4; ++i) a.fd[i] = freqs_dir[i];
   a.masks = const_cast<uint32_t*>(masks);
   a.d_raw = d_raw;
+  CN_CHECK_ARG(cn::aligned16(d_raw));  // float4 rows (include/codenerf.h)
   a.g_code = g_code;
   a.d_pts = d_pts;
   a.d_ro = d_ro;

@@ -177,6 +177,9 @@ int cn_volume_render(const float* raw, const float* z, const float* rd, int64_t 
 
 /* --- Code-conditioned MLP: view_synthesis/models/model.py -------------- */
 
+/* Every field entry point below stores raw / reads d_raw as one 16-B row per sample: raw and d_raw
+ * must be 16-B aligned, or the call returns CN_EINVAL without a launch. */
+
 /* Floats needed for one packed model of format fmt (cn_mlp_pack output); -1 for a bad fmt. */
 int64_t cn_mlp_packed_floats(int fmt);
 
