@@ -3,7 +3,7 @@
 # MFMA busy, instruction mix, wait states, LDS.   tools/gpu_enc_pmc.sh <tag>
 R=$GRAFT_REPO_ROOT; TAG=${1:-encpmc}; O=$R/gpurun_out/$TAG; mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
-PASSES="SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE|SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_WAVES|SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS|SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_LDS_IDX_ACTIVE|FETCH_SIZE"
+PASSES=${PMC_PASSES:-"SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE|SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_WAVES|SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS|SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_LDS_IDX_ACTIVE|FETCH_SIZE"}
 IFS='|' read -ra PASS_LIST <<< "$PASSES"
 for c in "${PASS_LIST[@]}"; do
   tag=$(echo $c | tr ' ' '_')
