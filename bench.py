@@ -524,7 +524,14 @@ def train_bench(dev, k, iters, world, precision=None):
     torch.cuda.synchronize()
     adamw_ms = e0.elapsed_time(e1) / 20
     rays = batch * 4096 * iters * world
+    # the MLP work of one iteration per rank: forward + dX + dW (3 x 572,416 FLOP) per sample evaluation,
+    # (64 coarse + 128 merged fine) samples per ray; against the dense MFMA peak of the precision's pipe
+    # (3xbf16: three bf16 products per fp32 one, so its figure is in fp32-equivalent TFLOP/s)
+    flop_iter = 3.0 * FLOP_PER_SAMPLE * batch * 4096 * (64 + 128)
+    tflops = flop_iter / (dt / iters) / 1e12
+    peak = PEAK_FP32_MFMA_TFLOPS if precision == "f32" else PEAK_BF16_MFMA_TFLOPS / 3.0
     return {"ms_per_iter": dt / iters * 1e3, "rays_per_s": rays / dt, "rays_per_iter_per_rank": batch * 4096,
+            "mlp_tflop_per_iter": flop_iter / 1e12, "achieved_tflops": tflops, "frac_of_peak": tflops / peak,
             "optimizer_steps_per_iter": batch, "samples": "64+64 perturbed", "objects": n_objects,
             "params": n_params, "loss": float(logs[-1]["total_loss"]), "dtype": precision,
             "adamw": {"kernel_ms": adamw_ms, "bytes": 28 * n_params,
