@@ -310,7 +310,8 @@ __global__ __launch_bounds__(256) void volume_render_kernel(
   render_run<K, FULL, L>(zz, rv, S_in, r, nrm, rgb, disp, acc, weights, depth);
 }
 
-// S = 16 K with n_rays % 4 == 0 (the C2 / C3 shapes): wave w renders G groups of 4 rays, groups
+// S = 16 K with n_rays % 4 == 0 (dispatched for S = 64: the C2 / C3 / C5 coarse launches; at K = 8
+// the staged rows would cost the occupancy): wave w renders G groups of 4 rays, groups
 // w + g W of the grid's W waves.  Every group's raw rows, depths and directions are loaded up front,
 // so the later groups' loads are in flight while the wave integrates the earlier ones.
 template <int K, int G>
