@@ -175,8 +175,9 @@ def sample_uniform(ro: Tensor, rd: Tensor, z_bins: Tensor, lower: Tensor, upper:
         assert t_rand.shape == (n, nc), "t_rand must be (num_rays, num_coarse)"
     z = torch.empty(n, nc, device=ro.device, dtype=torch.float32)
     pts = torch.empty(n, nc, 3, device=ro.device, dtype=torch.float32) if want_pts else None
-    check(lib.cn_sample_uniform(ptr(ro), ptr(rd), n, ptr(z_bins), ptr(lower), ptr(upper), nc, ptr(t_rand),
-                                ptr(z), ptr(pts), stream_of(z)), "cn_sample_uniform")
+    if n:      # no rays: empty outputs, as torch's ops give (the C ABI refuses n_rays == 0)
+        check(lib.cn_sample_uniform(ptr(ro), ptr(rd), n, ptr(z_bins), ptr(lower), ptr(upper), nc, ptr(t_rand),
+                                    ptr(z), ptr(pts), stream_of(z)), "cn_sample_uniform")
     return pts, z
 
 
@@ -187,7 +188,8 @@ def ray_points(ro: Tensor, rd: Tensor, z: Tensor) -> Tensor:
     n, s = z.shape
     assert ro.shape == (n, 3) and rd.shape == (n, 3), "ro / rd must be (num_rays, 3)"
     pts = torch.empty(n, s, 3, device=z.device, dtype=torch.float32)
-    check(lib.cn_ray_points(ptr(ro), ptr(rd), ptr(z), n, s, ptr(pts), stream_of(z)), "cn_ray_points")
+    if n * s:
+        check(lib.cn_ray_points(ptr(ro), ptr(rd), ptr(z), n, s, ptr(pts), stream_of(z)), "cn_ray_points")
     return pts
 
 
@@ -212,8 +214,9 @@ def sample_pdf(ro: Tensor, rd: Tensor, weights: Tensor, z: Tensor, num_fine: int
         u_stride = num_fine if u.dim() == 2 else 0
     zo = torch.empty(n, nc + num_fine, device=z.device, dtype=torch.float32)
     pts = torch.empty(n, nc + num_fine, 3, device=z.device, dtype=torch.float32) if want_pts else None
-    check(lib.cn_sample_pdf(ptr(ro), ptr(rd), ptr(weights), w_stride, ptr(z), n, nc, num_fine, ptr(u), u_stride, ptr(zo),
-                            ptr(pts), stream_of(zo)), "cn_sample_pdf")
+    if n:
+        check(lib.cn_sample_pdf(ptr(ro), ptr(rd), ptr(weights), w_stride, ptr(z), n, nc, num_fine, ptr(u), u_stride,
+                                ptr(zo), ptr(pts), stream_of(zo)), "cn_sample_pdf")
     return pts, zo
 
 
@@ -227,8 +230,9 @@ def posenc(x: Tensor, freqs: Sequence[float], include_input: bool) -> Tensor:
     assert x.dim() == 2, "tensor must be (N, num_dim)"
     m, d = x.shape
     out = torch.empty(m, d * (int(include_input) + 2 * len(freqs)), device=x.device, dtype=torch.float32)
-    check(lib.cn_posenc(ptr(x), m, d, _lib.host_floats(freqs), len(freqs), int(include_input), ptr(out),
-                        stream_of(x)), "cn_posenc")
+    if m:
+        check(lib.cn_posenc(ptr(x), m, d, _lib.host_floats(freqs), len(freqs), int(include_input), ptr(out),
+                            stream_of(x)), "cn_posenc")
     return out
 
 
@@ -249,8 +253,9 @@ def volume_render(raw: Tensor, z: Tensor, rd: Tensor, want_weights: bool = True)
     acc = torch.empty_like(disp)
     depth = torch.empty_like(disp)
     w = torch.empty(n, s, device=dev, dtype=torch.float32) if want_weights else None
-    check(lib.cn_volume_render(ptr(raw), ptr(z), ptr(rd), n, s, ptr(rgb), ptr(disp), ptr(acc), ptr(w), ptr(depth),
-                               stream_of(raw)), "cn_volume_render")
+    if n:
+        check(lib.cn_volume_render(ptr(raw), ptr(z), ptr(rd), n, s, ptr(rgb), ptr(disp), ptr(acc), ptr(w), ptr(depth),
+                                   stream_of(raw)), "cn_volume_render")
     if w is not None and s == 1:
         w = w[:, :0]          # the reference's S == 1 weights are (R, 0) (see volume.hip)
     return rgb, disp, acc, w, depth
@@ -312,9 +317,10 @@ def mlp_forward(packed: Tensor, cb: Tensor, x: Tensor, code_index: Optional[Tens
     else:
         assert n_codes in (1, m), "codes must be one row or one row per sample"
     raw = torch.empty(m, 4, device=x.device, dtype=torch.float32)
-    check(lib.cn_mlp_forward(ptr(packed), _fmt(precision), ptr(cb), ptr(code_index), n_codes, ptr(x), m, ptr(raw),
-                             stream_of(x)),
-          "cn_mlp_forward")
+    if m:
+        check(lib.cn_mlp_forward(ptr(packed), _fmt(precision), ptr(cb), ptr(code_index), n_codes, ptr(x), m, ptr(raw),
+                                 stream_of(x)),
+              "cn_mlp_forward")
     return raw
 
 
@@ -339,9 +345,10 @@ def radiance_field(packed: Tensor, cb: Tensor, rd: Tensor, n_samples: int, chunk
         assert n_codes in (1, n), "codes must be one row or one row per ray"
     assert len(freqs_xyz) == 10 and len(freqs_dir) == 4, "the field kernel implements L_xyz=10, L_dir=4"
     raw = torch.empty(n, n_samples, 4, device=rd.device, dtype=torch.float32)
-    check(lib.cn_radiance_field(ptr(packed), _fmt(precision), ptr(cb), ptr(code_index), n_codes, ptr(pts), ptr(ro), ptr(rd), ptr(z),
-                                n, n_samples, chunk_rows, _lib.host_floats(freqs_xyz), _lib.host_floats(freqs_dir),
-                                ptr(raw), stream_of(rd)), "cn_radiance_field")
+    if n:
+        check(lib.cn_radiance_field(ptr(packed), _fmt(precision), ptr(cb), ptr(code_index), n_codes, ptr(pts), ptr(ro),
+                                    ptr(rd), ptr(z), n, n_samples, chunk_rows, _lib.host_floats(freqs_xyz),
+                                    _lib.host_floats(freqs_dir), ptr(raw), stream_of(rd)), "cn_radiance_field")
     return raw
 
 

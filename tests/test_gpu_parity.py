@@ -233,6 +233,28 @@ def test_volume_render_grouped_path(dev, n):
         assert maxdiff(a.cpu()[pick][fin], b[fin]) <= 5e-6
 
 
+def test_leaf_ops_empty_batch(dev):
+    """Zero rays through the leaf ops gives torch's empty outputs -- the oracle's (torch ops) shapes --
+    instead of an error (the C ABI refuses n_rays == 0; the Python layer launches nothing)."""
+    from oracle import codenerf_oracle as O
+    from codenerf import ops
+    from codenerf.nerf import PointSampler
+    e3, e64 = torch.empty(0, 3), torch.empty(0, 64)
+    ref = O.volume_render(torch.empty(0, 64, 4), e64, e3)
+    got = ops.volume_render(torch.empty(0, 64, 4, device=dev), e64.to(dev), e3.to(dev))
+    assert [tuple(t.shape) for t in got] == [tuple(t.shape) for t in ref]
+    ps = PointSampler(64, 64, 0.8, 1.8, spacing_mode="lindepth", perturb=False, dtype=torch.float32, device=dev)
+    pts, z = ops.sample_uniform(e3.to(dev), e3.to(dev), ps.z_vals, ps.lower, ps.upper)
+    pts_o, z_o = O.sample_uniform(e3, e3, O.Sampling(64, 64, 0.8, 1.8).bins)
+    assert pts.shape == pts_o.shape and z.shape == z_o.shape
+    pf, zf = ops.sample_pdf(e3.to(dev), e3.to(dev), torch.empty(0, 62, device=dev), e64.to(dev), 64,
+                            u=ps.u_lin)
+    assert pf.shape == (0, 128, 3) and zf.shape == (0, 128)
+    enc = ops.posenc(e3.to(dev), [2.0 ** k for k in range(10)], True)
+    assert enc.shape == O.posenc(e3, O.frequency_bands(10, True), True).shape
+    assert ops.ray_points(e3.to(dev), e3.to(dev), e64.to(dev)).shape == (0, 64, 3)
+
+
 def test_volume_render_unaligned_inputs(dev):
     """raw / z as contiguous views at an odd element offset: the C ABI refuses them (CN_EINVAL, no
     launch: its 16-B vector accesses need aligned rows), the Python op realigns them and returns the
