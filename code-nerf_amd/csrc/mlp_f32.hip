@@ -169,6 +169,7 @@ struct State {
   unsigned voff;
   unsigned poff;     // this lane's byte offset in a (kTile, 256) fp32 plane block: row 16 wave + (lane & 15), col 4 g
   unsigned gbase;    // backward: this lane's byte offset in a 256-float sum row (rowsum64's features)
+  int cbase;         // no-geometry backward: chunk counter at the tile's first chunk (stream_src)
 };
 
 // The kernel's LDS constants (after the ring): the packed ones and the encoding frequencies.
@@ -215,18 +216,32 @@ __device__ __forceinline__ void store_plane(const State& s, __amdgpu_buffer_rsrc
 }
 
 
+// The packed chunk the chunk counter cn streams.  The forward and the geometry backward run the
+// whole 36-chunk stream from cn = 0 in every tile.  NG: the no-geometry training backward streams
+// 33 of the transposed pack's chunks (not the view-direction chunk kNoGeoSkip, nor the two
+// layer_xyz1^T chunks at the end); 33 is not a multiple of the ring, so its counter runs on across
+// tiles (ring slot cn & 3) and s.cbase is the counter at the tile's first chunk.
+constexpr int kNoGeoSkip = 17, kNoGeoChunks = kChunks - 3;
+__device__ __forceinline__ int stream_src_ng(const State& s, int cn) {
+  int k = cn - s.cbase;
+  if (k >= kNoGeoChunks) k -= kNoGeoChunks;
+  return k + (k >= kNoGeoSkip ? 1 : 0);
+}
+
 // One LDS-DMA piece: 1 KiB of chunk cn (piece p of 4 for this wave).
+template <bool NG = false>
 __device__ __forceinline__ void dma_piece(const State& s, float4* lds, int cn, int p) {
-  const int src = cn < kChunks ? cn : cn - kChunks;
+  const int src = NG ? stream_src_ng(s, cn) : (cn < kChunks ? cn : cn - kChunks);
   const unsigned soff = __builtin_amdgcn_readfirstlane((unsigned)(src * kChunkQuads + p * 64 * kWaves) * 16u);
   __builtin_amdgcn_raw_ptr_buffer_load_lds(
       s.wsrc, (lds_ptr_t)(lds + (cn & (kRing - 1)) * kChunkQuads + p * 64 * kWaves + s.wave * 64), 16, s.voff,
       soff, 0, 0);
 }
 
+template <bool NG = false>
 __device__ __forceinline__ void dma_chunk(const State& s, float4* lds, int cn) {
 #pragma unroll
-  for (int p = 0; p < kPiecesPerWave; ++p) dma_piece(s, lds, cn, p);
+  for (int p = 0; p < kPiecesPerWave; ++p) dma_piece<NG>(s, lds, cn, p);
 }
 
 // M_c: chunk c+1 landed for every wave (all but this wave's 4 youngest DMA pieces --
@@ -293,7 +308,7 @@ struct NoPost {
 // r03g: SQ_WAIT_INST_ANY +77 M and SQ_WAIT_ANY +55 M quad-cycles over the mask-only forward for
 // 2.09 M stores); two per chunk they overlap the MFMAs.  They follow the chunk's DMA, so the next
 // barrier's counted vmcnt still sees the ring's pieces in order.
-template <int NS, int CI = 0, typename GetB, typename Post = NoPost>
+template <int NS, int CI = 0, bool NG = false, typename GetB, typename Post = NoPost>
 __device__ __forceinline__ void chunk16(State& s, float4* lds, int c, GetB getb, Post post = Post{}) {
   const float4* slot = lds + (c & (kRing - 1)) * kChunkQuads + s.lane;
   const float4* nslot = lds + ((c + 1) & (kRing - 1)) * kChunkQuads + s.lane;
@@ -312,7 +327,7 @@ __device__ __forceinline__ void chunk16(State& s, float4* lds, int c, GetB getb,
     __builtin_amdgcn_sched_barrier(0);                              \
     if constexpr ((T) == 3) {                                       \
       chunk_barrier();                                              \
-      dma_chunk(s, lds, c + 3);                                     \
+      dma_chunk<NG>(s, lds, c + 3);                                 \
     }                                                               \
     post.template step<CI, (T)>();                                  \
   }
@@ -410,16 +425,16 @@ struct LazyXyz {
 };
 
 // A 256-input layer: 8 chunks, B from s.act.
-template <typename Post = NoPost>
+template <bool NG = false, typename Post = NoPost>
 __device__ __forceinline__ void layer256(State& s, float4* lds, int& c, Post post = Post{}) {
-  chunk16<8, 0>(s, lds, c + 0, ActB<0>{s}, post);
-  chunk16<8, 1>(s, lds, c + 1, ActB<8>{s}, post);
-  chunk16<8, 2>(s, lds, c + 2, ActB<16>{s}, post);
-  chunk16<8, 3>(s, lds, c + 3, ActB<24>{s}, post);
-  chunk16<8, 4>(s, lds, c + 4, ActB<32>{s}, post);
-  chunk16<8, 5>(s, lds, c + 5, ActB<40>{s}, post);
-  chunk16<8, 6>(s, lds, c + 6, ActB<48>{s}, post);
-  chunk16<8, 7>(s, lds, c + 7, ActB<56>{s}, post);
+  chunk16<8, 0, NG>(s, lds, c + 0, ActB<0>{s}, post);
+  chunk16<8, 1, NG>(s, lds, c + 1, ActB<8>{s}, post);
+  chunk16<8, 2, NG>(s, lds, c + 2, ActB<16>{s}, post);
+  chunk16<8, 3, NG>(s, lds, c + 3, ActB<24>{s}, post);
+  chunk16<8, 4, NG>(s, lds, c + 4, ActB<32>{s}, post);
+  chunk16<8, 5, NG>(s, lds, c + 5, ActB<40>{s}, post);
+  chunk16<8, 6, NG>(s, lds, c + 6, ActB<48>{s}, post);
+  chunk16<8, 7, NG>(s, lds, c + 7, ActB<56>{s}, post);
   c += 8;
 }
 
@@ -858,6 +873,7 @@ constexpr int kBwdLdsFloats = kBGacc + kWaves * kCbStride;
 constexpr int kBwdLdsQuads = kRing * kChunkQuads + kBwdLdsFloats / 4;
 static_assert(kBwdLdsQuads * 16 <= 160 * 1024, "LDS budget (backward)");
 static_assert(kTXyz1 + 2 == kChunks, "backward chunk schedule");
+static_assert(kTDDir == kNoGeoSkip && kTDDir + 1 == kTOut, "no-geometry stream: skips the view-dir chunk");
 
 __global__ void pack_w16t_kernel(Params P, float* __restrict__ packed) {
   constexpr int kX2 = kHidden + kCode, kD1 = kCode + kDimDir;
@@ -997,16 +1013,29 @@ __device__ __forceinline__ void zero_acc(State& s) {
 }
 
 // fc_rgb^T: only k-step 0 of chunk c is real; the chunk's barrier and DMA, then its 16 MFMAs.
-__device__ __forceinline__ void chunk_k0(State& s, float4* lds, int c, float b) {
+// X1STORE (no-geometry training backward): s.act still holds the PREVIOUS tile's layer_xyz1 dPre
+// (m_h1 . d h1, plane 4), which the geometry kernel stored beside its layer_xyz1^T chunks; here its
+// 16 stores go out after the DMA, one beside each MFMA (rsrc x1 covers no rows before the first tile:
+// the stores are dropped).
+template <bool X1STORE = false>
+__device__ __forceinline__ void chunk_k0(State& s, float4* lds, int c, float b, __amdgpu_buffer_rsrc_t x1) {
   const float4* nslot = lds + ((c + 1) & (kRing - 1)) * kChunkQuads + s.lane;
   floatx4 a0[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) a0[q] = s.pre[q];
   __builtin_amdgcn_sched_barrier(0);
   chunk_barrier();
-  dma_chunk(s, lds, c + 3);
+  dma_chunk<X1STORE>(s, lds, c + 3);
   read_a<0>(nslot, s.pre);
+  if constexpr (X1STORE) store_plane<0, 16>(s, x1, s.act);
   mfma_step(s, a0, b);
+  if constexpr (X1STORE) {
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      __builtin_amdgcn_sched_group_barrier(0x040, 1, 0);  // VMEM write
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+    }
+  }
   __builtin_amdgcn_sched_barrier(0);
 }
 
@@ -1111,9 +1140,17 @@ __device__ __forceinline__ uint2 load_mask(const State& s, const FieldArgs& a, i
 // (the compiler counts the weight stream's DMA pieces in between, so the wait it puts before the
 // use does not drain the stream), the view-direction gradient is finished right after its narrow
 // chunk (3 values to the end instead of 8 + the unit direction), and the code row is wave-uniform.
-template <int MODE, bool TRAIN>
+//
+// NOGEO (the training backward with no d ro / d rd / d pts wanted -- train.py's rays are data,
+// ray_sampler.py:53-82): the view-direction chunk, both layer_xyz1^T chunks and the encoding / ray
+// epilogue only feed those outputs, so they are not streamed or run (33 chunks per tile instead of
+// 36).  The one thing training needs from that schedule, layer_xyz1's dPre plane (m_h1 . d h1), is
+// left in s.act at the tile's end and stored beside the next tile's fc_rgb^T MFMAs (chunk_k0), the
+// last tile's after the tile loop.  crun: the running chunk counter (stream_src); prev: the tile
+// whose plane 4 is pending (-1: none).
+template <int MODE, bool TRAIN, bool NOGEO = false>
 __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* lds, float* grow, int64_t tile,
-                                        int& cur_code) {
+                                        int& cur_code, int& crun, int64_t& prev) {
   const int64_t row = tile * kTile + s.wave * 16 + (s.lane & 15);
   const bool valid = row < a.m;
   const int64_t rc = valid ? row : a.m - 1;
@@ -1146,14 +1183,24 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
       atomicAdd(grow + kCbRgb + 2, t3);
     }
   }
-  int c = 0;
+  int c = NOGEO ? crun : 0;
+  s.cbase = c;
   // ---- fc_rgb^T (chunk 0): B = d rgb channel g at k-step 0
 #ifdef CN_PROBE_PROLOGUE
   s.prolog += clock64() - tp0;
 #endif
   zero_acc(s);
-  chunk_k0(s, lds, c, s.g == 0 ? dr.x : (s.g == 1 ? dr.y : (s.g == 2 ? dr.z : 0.0f)));
-  c = kTDir2;
+  {
+    const float b = s.g == 0 ? dr.x : (s.g == 1 ? dr.y : (s.g == 2 ? dr.z : 0.0f));
+    if constexpr (NOGEO) {
+      const __amdgpu_buffer_rsrc_t x1 =
+          prev >= 0 ? plane_rsrc(a.dpre, 4, a.m, prev) : __builtin_amdgcn_make_buffer_rsrc(a.dpre, 0, 0, 0x00020000);
+      chunk_k0<true>(s, lds, c, b, x1);
+    } else {
+      chunk_k0(s, lds, c, b, s.wsrc);  // (no stores: x1 unused)
+    }
+  }
+  c += kTDir2;
   const float dsig = dr.w;
   // ---- layer_dir2^T (m_v2), layer_dir1^T (m_v1)
   // (each layer's masked input gradient -- the dW GEMMs' dPre plane -- is stored at the layer's first
@@ -1161,21 +1208,21 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   mask_act(s, m_v2);
   zero_acc(s);
   __builtin_amdgcn_sched_barrier(0);
-  layer256(s, lds, c, DpreStore<TRAIN>{s, a, tile, 0});
+  layer256<NOGEO>(s, lds, c, DpreStore<TRAIN>{s, a, tile, 0});
   const uint2 m_h2 = load_mask(s, a, tile, 1), m_h1 = load_mask(s, a, tile, 0);
   mask_act(s, m_v1);
   zero_acc(s);
   __builtin_amdgcn_sched_barrier(0);
-  layer256(s, lds, c, DpreStore<TRAIN>{s, a, tile, 1});
+  layer256<NOGEO>(s, lds, c, DpreStore<TRAIN>{s, a, tile, 1});
   // ---- the view-direction rows of layer_dir1^T (narrow chunk, B = m_v1 . d v1 still in act)
-#pragma unroll
-  for (int q = 0; q < 4; ++q) s.acc2[q] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
-  chunk_narrow(s, lds, c);
-  c += 1;
   // d view dir -> the Q1 direction ray's d rd (its atomics at the end of the tile):
   // vd = rd[dray] / |rd[dray]|: d rd[dray] += (g - vd (vd . g)) / |rd[dray]|
   float grd_q1[3] = {0.f, 0.f, 0.f};
-  {
+  if constexpr (!NOGEO) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s.acc2[q] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+    chunk_narrow(s, lds, c);
+    c += 1;
     float gdir[8];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -1212,15 +1259,21 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
     s.acc[ob] = w * dsig;
   }
   __builtin_amdgcn_sched_barrier(0);
-  layer256(s, lds, c, DpreStore<TRAIN>{s, a, tile, 2});
+  layer256<NOGEO>(s, lds, c, DpreStore<TRAIN>{s, a, tile, 2});
   // ---- layer_xyz2^T (m_h2): its masked input gradient is the code term's too
   mask_act(s, m_h2);
   if (gc) gcode_add64<kCbXyz2>(s, grow, s.act);
   zero_acc(s);
   __builtin_amdgcn_sched_barrier(0);
-  layer256(s, lds, c, DpreStore<TRAIN>{s, a, tile, 3});
+  layer256<NOGEO>(s, lds, c, DpreStore<TRAIN>{s, a, tile, 3});
   // ---- layer_xyz1^T (m_h1): encoding k-steps 0-7, then 8-15
   mask_act(s, m_h1);
+  if constexpr (NOGEO) {
+    // its dPre plane goes out beside the next tile's fc_rgb^T (or after the tile loop)
+    crun = c;
+    prev = tile;
+    return;
+  }
   float genc[16];
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
@@ -1298,8 +1351,9 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   }
 }
 
-template <int MODE, bool TRAIN>
+template <int MODE, bool TRAIN, bool NOGEO = false>
 __global__ __launch_bounds__(kThreads, 2) void field_w16_bwd_kernel(FieldArgs a) {
+  static_assert(!NOGEO || TRAIN, "the no-geometry schedule is the training backward's");
   __shared__ __attribute__((aligned(16))) float4 lds[kBwdLdsQuads];
   float* blds = reinterpret_cast<float*>(lds + kRing * kChunkQuads);
   State s;
@@ -1310,6 +1364,7 @@ __global__ __launch_bounds__(kThreads, 2) void field_w16_bwd_kernel(FieldArgs a)
   s.voff = static_cast<unsigned>(s.wave * 64 + s.lane) * 16u;
   s.poff = static_cast<unsigned>(s.wave * 16 + (s.lane & 15)) * 1024u + 16u * s.g;
   s.gbase = static_cast<unsigned>(16 * rev4(s.lane & 15) + 4 * s.g) * 4u;
+  s.cbase = 0;
   float* grow = blds + kBGacc + s.wave * kCbStride;
   load_consts(a, blds);
   for (int k = threadIdx.x; k < kBwdLdsFloats - kBGacc; k += kThreads) blds[kBGacc + k] = 0.0f;
@@ -1327,11 +1382,16 @@ __global__ __launch_bounds__(kThreads, 2) void field_w16_bwd_kernel(FieldArgs a)
   const long long tl0 = clock64();
   int nt = 0;
 #endif
+  int crun = 0;
+  int64_t prev = -1;
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
-    bwd_tile<MODE, TRAIN>(s, a, lds, grow, tile, cur_code);
+    bwd_tile<MODE, TRAIN, NOGEO>(s, a, lds, grow, tile, cur_code, crun, prev);
 #ifdef CN_PROBE_PROLOGUE
     ++nt;
 #endif
+  }
+  if constexpr (NOGEO) {
+    if (prev >= 0) store_plane<0, 16>(s, plane_rsrc(a.dpre, 4, a.m, prev), s.act);
   }
 #ifdef CN_PROBE_PROLOGUE
   if (s.lane == 0 && blockIdx.x < 2048) {
@@ -1396,9 +1456,26 @@ int launch_pack_w16t(const Params& P, float* packed, hipStream_t st) {
   return cn::launch_status();
 }
 
+// CN_BWD_NOGEO=0 keeps the geometry schedule in training too (A/B timing; the weight and code
+// gradients are bitwise the same either way)
+bool nogeo_enabled() {
+  static const int on = [] {
+    const char* e = getenv("CN_BWD_NOGEO");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return on != 0;
+}
+
 int launch_field_w16_bwd(int mode, FieldArgs& a, hipStream_t st) {
   const unsigned grid = static_cast<unsigned>(std::min<int64_t>(cn::ceil_div(a.m, w16::kTile), cu_count_w16()));
   const dim3 b(w16::kThreads);
+  // training with no geometry gradient wanted (train.py: the rays are data): the 33-chunk schedule
+  if (a.dpre && !a.d_pts && !a.d_ro && !a.d_rd && nogeo_enabled()) {
+    if (mode == kFromPts) hipLaunchKernelGGL((w16::field_w16_bwd_kernel<kFromPts, true, true>), dim3(grid), b, 0, st, a);
+    else if (mode == kFromRayZ) hipLaunchKernelGGL((w16::field_w16_bwd_kernel<kFromRayZ, true, true>), dim3(grid), b, 0, st, a);
+    else return CN_EUNSUPPORTED;
+    return cn::launch_status();
+  }
   if (a.dpre) {
     if (mode == kFromPts) hipLaunchKernelGGL((w16::field_w16_bwd_kernel<kFromPts, true>), dim3(grid), b, 0, st, a);
     else if (mode == kFromRayZ) hipLaunchKernelGGL((w16::field_w16_bwd_kernel<kFromRayZ, true>), dim3(grid), b, 0, st, a);

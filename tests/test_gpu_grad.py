@@ -665,6 +665,63 @@ def test_field_backward_train_sigma_rgb_rows(dev, precision):
     close(pg[16][:, :256], d[:, :3].t() @ v2, 1e-5, "fc_rgb rows")     # kWRgb = 16
 
 
+@pytest.mark.parametrize("precision", ["f32", "bf16x3"])
+@pytest.mark.parametrize("mode,r,s,n_codes", [("rayz", 1050, 64, 1),    # 525 tiles: 2-3 per workgroup, ragged
+                                              ("rayz", 4096, 64, 1),    # C3-shaped: 8 tiles per workgroup
+                                              ("pts", 777, 48, 1),
+                                              ("rayz", 5, 16, 1),       # one (partial) tile
+                                              ("rayz", 300, 24, 1),     # S % 16 != 0
+                                              ("rayz", 1024, 64, 3)])   # in-kernel g_code sums
+def test_field_backward_train_nogeo_bitwise(dev, precision, mode, r, s, n_codes):
+    """train.py's rays are data (ray_sampler.py:53-82), so the training backward is asked for no d ro /
+    d rd / d pts, and the fused kernel then skips the geometry-only chunks (view-direction rows of
+    layer_dir1^T, both layer_xyz1^T chunks) and the encoding epilogue, storing layer_xyz1's dPre plane
+    beside the next tile's fc_rgb^T.  Every weight and code gradient must be bitwise those of the
+    geometry schedule on the same chunk (one code row: deterministic throughout; several: the per-code
+    sums are float atomics, so g_code and the three biases formed from it agree to fp32 rounding)."""
+    from codenerf import ops, synthetic
+    if precision == "bf16x3" and s % 32:
+        pytest.skip("3xbf16 fused backward: one code row per 32-sample wave")
+    m = model(dev, 0)
+    params = [p.detach() for p in m.param_list()]
+    g = torch.Generator().manual_seed(r + s + n_codes)
+    ro = (torch.randn(r, 3, generator=g) * 0.3 + torch.tensor([0.0, 0.0, 1.3])).to(dev)
+    rd = torch.randn(r, 3, generator=g).to(dev)
+    z = torch.sort(0.8 + torch.rand(r, s, generator=g), dim=-1).values.to(dev)
+    pts = (ro[:, None, :] + rd[:, None, :] * z[..., None]).contiguous() if mode == "pts" else None
+    geo = dict(pts=pts) if mode == "pts" else dict(ro=ro, z=z)
+    gout = torch.randn(r, s, 4, generator=g).to(dev)
+    zs, zt = synthetic.latent_codes(5, n_codes).to(dev), synthetic.latent_codes(6, n_codes).to(dev)
+    code_index = (torch.arange(r) * n_codes // r).to(dev) if n_codes > 1 else None
+    fx, fd = [2.0 ** k for k in range(10)], [2.0 ** k for k in range(4)]
+    cb = ops.code_bias(params, zs, zt)
+    x3 = precision == "bf16x3"
+    chunk = 256
+    _, saved, masks = ops.radiance_field_train_w16(ops.mlp_pack(params, "bf16x3" if x3 else "f32_w16"), cb, rd, s,
+                                                   chunk, fx, fd, precision=precision, code_index=code_index, **geo)
+    packed_t = ops.mlp_pack(params, "bf16x3_t" if x3 else "f32_w16_t")
+    want = dict(want_pts=True) if mode == "pts" else dict(want_ro=True, want_rd=True)
+    out = {}
+    for name, w in (("geo", want), ("nogeo", {}), ("nogeo2", {})):
+        pg = [torch.zeros_like(p) for p in params]
+        res = ops.field_backward_train(packed_t, params, masks, saved, None, gout, r, s, chunk, n_codes, fx, fd, rd=rd,
+                                       code_index=code_index, param_grads=pg, precision=precision, **w, **geo)
+        out[name] = (pg, res["g_code"])
+    torch.cuda.synchronize()
+    atomic = n_codes > 1 or x3       # the per-code sums / biases of g_code: float atomics
+    code_biases = {3, 5, 17}          # b_xyz2, b_out, b_rgb: column sums of g_code
+    for other in ("nogeo", "nogeo2"):
+        for k, (a, b) in enumerate(zip(out[other][0], out["geo"][0])):
+            if atomic and k in code_biases:
+                close(a, b.double(), 1e-5, f"bias {k}")
+            else:
+                assert torch.equal(a, b), f"param {k}: {other} differs from the geometry schedule"
+        if atomic:
+            close(out[other][1], out["geo"][1].double(), 1e-5, "g_code")
+        else:
+            assert torch.equal(out[other][1], out["geo"][1]), f"g_code: {other}"
+
+
 @pytest.mark.parametrize("n_codes,want_grads", [(1, True), (5, True), (5, False)])
 def test_code_bias_backward_two_launch_bitwise(dev, n_codes, want_grads):
     """cn_code_bias_backward_ws (code layers split over 16 workgroups per code, two launches) gives
