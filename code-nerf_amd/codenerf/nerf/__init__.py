@@ -223,13 +223,18 @@ def gather_views(rows: torch.Tensor, per: List[int], rank: int, n_views: int) ->
     return torch.cat([b.view((n_views, p) + c) for b, p in zip(blocks, per)], dim=1)
 
 
-def gather_rows(rows: torch.Tensor, per: List[int], rank: int) -> Optional[torch.Tensor]:
-    """Pad every rank's rows to the largest share, all-gather, trim on rank 0 (nerf/__init__.py:212-224)."""
+def gather_rows(rows: torch.Tensor, per: List[int], rank: int, single_tensor: bool = True) -> Optional[torch.Tensor]:
+    """Pad every rank's rows to the largest share, all-gather, trim on rank 0 (nerf/__init__.py:212-224).
+
+    ``single_tensor`` (default): ONE ``all_gather_into_tensor`` into a (world * width, ...) buffer --
+    RCCL's native form, and what gloo runs too, so the multi-rank tests exercise the branch a
+    multi-GPU node executes; False: the reference's list ``all_gather`` (kept for backends without
+    the single-tensor collective)."""
     world = len(per)
     width = max(per)
     padded = torch.zeros((width,) + tuple(rows.shape[1:]), dtype=rows.dtype, device=rows.device)
     padded[: rows.shape[0]] = rows
-    if dist.get_backend() == "nccl":
+    if single_tensor:
         allrows = torch.empty((world * width,) + tuple(rows.shape[1:]), dtype=rows.dtype, device=rows.device)
         dist.all_gather_into_tensor(allrows, padded)
         parts = list(allrows.split(width))

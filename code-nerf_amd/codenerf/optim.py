@@ -90,6 +90,17 @@ class AdamW(torch.optim.Optimizer):
                 if grad is not None:
                     flat["grad"][off:off + k].copy_(grad.reshape(-1))
                     p.grad = flat["grad"][off:off + k].view_as(p)
+        # the gradient buffer carries one has-grad flag per parameter after its end (allreduce_grads:
+        # one collective for both); flat["grad"] is the gradient part
+        n_flags = _round_up(len(offs))
+        self._grad_ext = torch.zeros(n + n_flags, device=dev, dtype=torch.float32)
+        self._grad_ext[:n].copy_(flat["grad"])
+        flat["grad"] = self._grad_ext[:n]
+        with torch.no_grad():
+            for p, off in offs.items():
+                if p.grad is not None:
+                    p.grad = flat["grad"][off:off + p.numel()].view_as(p)
+        self._flag_cache = {}
         self._flat, self._offs, self._starts = flat, offs, starts
         self._adopt_state()
 
@@ -254,33 +265,41 @@ class AdamW(torch.optim.Optimizer):
     # ---- data parallel ------------------------------------------------
     def allreduce_grads(self, group=None) -> None:
         """Average the gradients over the process group (the reference's DDP, util.py:139-142):
-        ONE all-reduce of the flat gradient buffer (plus one of a per-parameter has-grad flag).
-        A gradient missing on this rank counts as zero; a parameter without a gradient on every
-        rank keeps ``grad = None``."""
+        ONE all-reduce (SUM, then a division by the world size -- the same arithmetic on RCCL and
+        gloo) of the flat gradient buffer with a per-parameter has-grad flag appended to it.  A
+        gradient missing on this rank counts as zero; a parameter without a gradient on every rank
+        keeps ``grad = None``.
+
+        No host synchronisation when every parameter holds a gradient here (every training step
+        of the reference: each chunk runs both models and both code tables): the flags are a
+        cached device tensor per has-grad pattern, copied into the buffer's tail, and only a rank
+        that lacks some gradient reads the reduced flags back (to know whether another rank has
+        it).  Every rank always issues the same single collective, whatever its pattern."""
         if not (dist.is_available() and dist.is_initialized()):
             return
         world = dist.get_world_size(group)
-        # (world 1 runs the collectives too, as DDP does: the same code path at every size)
+        # (world 1 runs the collective too, as DDP does: the same code path at every size)
         missing = set(self._sync_grads())
         params = list(self._offs)
-        # which parameters hold a gradient on SOME rank (DDP reduces those; a parameter no rank
-        # touched keeps grad None, so step() skips it exactly as torch's AdamW would)
-        flags = torch.tensor([0 if p in missing else 1 for p in params], dtype=torch.int32,
-                             device=self._flat["grad"].device)
-        dist.all_reduce(flags, op=dist.ReduceOp.SUM, group=group)
-        anywhere = flags.cpu().tolist()
-        for p, cnt in zip(params, anywhere):
-            if p in missing:
-                view = self._view("grad", p)
-                view.zero_()
-                if cnt > 0:
-                    p.grad = view
-        grad = self._flat["grad"]
-        if dist.get_backend(group) == dist.Backend.NCCL:
-            dist.all_reduce(grad, op=dist.ReduceOp.AVG, group=group)
-        else:
-            dist.all_reduce(grad, op=dist.ReduceOp.SUM, group=group)
-            grad.div_(world)
+        n = self._flat["grad"].numel()
+        ext = self._grad_ext
+        pattern = tuple(p not in missing for p in params)
+        flags = self._flag_cache.get(pattern)
+        if flags is None:
+            flags = torch.tensor([1.0 if f else 0.0 for f in pattern], dtype=torch.float32).to(ext.device)
+            self._flag_cache[pattern] = flags
+        ext[n:n + len(params)].copy_(flags)
+        for p in missing:
+            self._view("grad", p).zero_()
+        dist.all_reduce(ext, op=dist.ReduceOp.SUM, group=group)
+        ext.div_(world)
+        if missing:
+            # which of this rank's missing parameters hold a gradient on SOME rank (DDP reduces
+            # those; a parameter no rank touched keeps grad None, so step() skips it as torch does)
+            anywhere = ext[n:n + len(params)].cpu().tolist()
+            for i, p in enumerate(params):
+                if p in missing and anywhere[i] > 0:
+                    p.grad = self._view("grad", p)
 
     def broadcast_params(self, src: int = 0, group=None) -> None:
         """Start every replica from rank ``src``'s parameters (DDP's construction-time

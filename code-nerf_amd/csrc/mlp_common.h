@@ -178,6 +178,8 @@ int launch_field_w16(int mode, FieldArgs& a, hipStream_t st);  // a.masks: also 
 int64_t mask_words_w16(int64_t m);
 int launch_pack_w16t(const Params& P, float* packed, hipStream_t st);
 int launch_field_w16_bwd(int mode, FieldArgs& a, hipStream_t st);
+// The training backwards' no-geometry schedule (no d ro / d rd / d pts wanted) unless CN_BWD_NOGEO=0.
+bool nogeo_enabled();
 
 // 3xbf16 16x16x32 two-waves-per-SIMD variant (mlp_x3w.hip): inference forward only.
 int64_t packed_floats_x3w();

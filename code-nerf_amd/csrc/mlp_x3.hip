@@ -43,6 +43,7 @@
 // is a single unrolled 16-k-step layer (a fully unrolled kernel is
 // instruction-fetch bound).
 #include <algorithm>
+#include <type_traits>
 
 #include "mlp_common.h"
 
@@ -167,6 +168,7 @@ struct State {
   unsigned voff;          // this lane's byte offset inside a 1 KiB-per-wave piece row
   float* sv;              // training: this lane's row of the plane being written (+4h), or null
   float pend[2];          // training backward: the even piece's values, stored with the odd one
+  int cbase;              // no-geometry backward: chunk counter at the tile's first chunk (DmaNoGeo)
 };
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -284,6 +286,39 @@ __device__ __forceinline__ Dma dma_for(const State& s, float4* lds, int c) {
   const int cb = c + 3 < kChunks ? c + 3 : c + 3 - kChunks;
   return Dma{s, lds, ca, cb};
 }
+// The default chunk stream: the 36 chunks from c = 0 in every tile.
+struct DmaFull {
+  static __device__ __forceinline__ Dma make(const State& s, float4* lds, int c) { return dma_for(s, lds, c); }
+};
+
+// The no-geometry training backward's stream: 33 of the transposed pack's 36 chunks (not the
+// view-direction chunk kNoGeoSkip, nor the two layer_xyz1^T chunks).  33 is not a multiple of the
+// ring, so the chunk counter runs on across tiles: ring slot = counter & 3, packed chunk = the
+// counter's position in the tile's stream (s.cbase: the counter at the tile's first chunk).
+constexpr int kNoGeoSkip = 17, kNoGeoChunks = kChunks - 3;
+__device__ __forceinline__ void dma_piece_ng(const State& s, float4* lds, int cn, int i) {
+  int k = cn - s.cbase;
+  if (k >= kNoGeoChunks) k -= kNoGeoChunks;
+  const int src = k + (k >= kNoGeoSkip ? 1 : 0);
+  const unsigned soff = __builtin_amdgcn_readfirstlane((unsigned)(src * kChunkQuads + i * 256) * 16u);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(s.wsrc, (lds_ptr_t)(lds + (cn & (kRing - 1)) * kChunkQuads + i * 256 + s.wave * 64),
+                                           16, s.voff, soff, 0, 0);
+}
+struct DmaNoGeoPieces {
+  const State& s;
+  float4* lds;
+  int ca, cb;  // c+2, c+3 (running counters)
+  template <int G>
+  __device__ __forceinline__ void piece() const {
+    if constexpr (G < 4) dma_piece_ng(s, lds, ca, 4 + G);
+    else dma_piece_ng(s, lds, cb, G - 4);
+  }
+};
+struct DmaNoGeo {
+  static __device__ __forceinline__ DmaNoGeoPieces make(const State& s, float4* lds, int c) {
+    return DmaNoGeoPieces{s, lds, c + 2, c + 3};
+  }
+};
 
 // M_c: chunk c+1 landed for every wave (all but this wave's OUT youngest DMA
 // pieces retired), every wave is past chunk c-1, and every LDS read of this
@@ -507,12 +542,12 @@ struct CopyFill {
 // (independent of the chunk) placed in group g's MFMA issue gaps; group g also
 // issues one DMA piece; M_c sits between groups 3 and 4.  SELF: group 0's
 // fragments are read here (first chunk of a tile) instead of arriving in s.pre.
-template <int NV, bool SELF, bool PREF, typename Fill>
+template <int NV, bool SELF, bool PREF, typename D = DmaFull, typename Fill>
 __device__ __forceinline__ void chunk_mfma(State& s, float4* lds, int c, bf16x8 bh0, bf16x8 bl0, bf16x8 bh1,
                                            bf16x8 bl1, Fill& fill) {
   const float4* slot = lds + (c & (kRing - 1)) * kChunkQuads;
   const float4* nslot = lds + ((c + 1) & (kRing - 1)) * kChunkQuads;
-  const Dma dma = dma_for(s, lds, c);
+  const auto dma = D::make(s, lds, c);
   bf16x8 a0[4], a1[4];
   if constexpr (SELF) {
     load_a<0, 0>(s, slot, a0);
@@ -547,10 +582,10 @@ __device__ __forceinline__ void chunk_mfma(State& s, float4* lds, int c, bf16x8 
 }
 
 // Chunk c's MFMAs (with its DMA pieces and M_c inside).
-template <int NV, bool SELF = false, typename Fill>
+template <int NV, bool SELF = false, typename D = DmaFull, typename Fill>
 __device__ __forceinline__ void run_chunk(State& s, const FieldArgs& a, float4* lds, int& c, bf16x8 bh0, bf16x8 bl0,
                                           bf16x8 bh1, bf16x8 bl1, Fill& fill) {
-  chunk_mfma<NV, SELF, true>(s, lds, c, bh0, bl0, bh1, bl1, fill);
+  chunk_mfma<NV, SELF, true, D>(s, lds, c, bh0, bl0, bh1, bl1, fill);
   ++c;
 }
 
@@ -1051,7 +1086,7 @@ __device__ __forceinline__ void bwd_init(State& s, const float* blds, int off, b
 // One backward pass over 8-block chunks: init, slot 0, chunks 0..6 converting
 // slot J+1, chunk 7 copying the accumulators out (COPY) or leaving them
 // (layer_dir1^T, whose d-dir chunk still reads the slots).
-template <bool RED, bool COPY = true, bool SAVE = false>
+template <bool RED, bool COPY = true, bool SAVE = false, typename D = DmaFull>
 __device__ __forceinline__ void bwd_pass(State& s, const FieldArgs& a, float4* lds, int& c, const float* blds,
                                          int init_off, bf16x8 sig_b, const unsigned* mw, unsigned gbase) {
   bwd_init<8>(s, blds, init_off, sig_b);
@@ -1060,7 +1095,7 @@ __device__ __forceinline__ void bwd_pass(State& s, const FieldArgs& a, float4* l
 #define CN_BWD_CHUNK(J)                                              \
   {                                                                  \
     ConvMaskFill<(J) + 1, RED, SAVE> f{s, mw, gbase, {}};            \
-    run_chunk<RED ? 4 : 2>(s, a, lds, c, CN_SLOT_B(J), f);           \
+    run_chunk<RED ? 4 : 2, false, D>(s, a, lds, c, CN_SLOT_B(J), f); \
   }
   CN_BWD_CHUNK(0)
   CN_BWD_CHUNK(1)
@@ -1072,12 +1107,12 @@ __device__ __forceinline__ void bwd_pass(State& s, const FieldArgs& a, float4* l
 #undef CN_BWD_CHUNK
   if constexpr (COPY) {
     CopyFill f{s};
-    run_chunk<6>(s, a, lds, c, CN_SLOT_B(7), f);
+    run_chunk<6, false, D>(s, a, lds, c, CN_SLOT_B(7), f);
     copy_acc(s, 6);
     copy_acc(s, 7);
   } else {
     NoFill f;
-    run_chunk<0>(s, a, lds, c, CN_SLOT_B(7), f);
+    run_chunk<0, false, D>(s, a, lds, c, CN_SLOT_B(7), f);
   }
 }
 
@@ -1196,9 +1231,32 @@ __device__ __forceinline__ void flush_gcode(const State& s, const FieldArgs& a, 
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
-template <int MODE, bool TRAIN>
+// layer_xyz1's dPre plane (m_h1 . d h1, the raw d h1 in the slots) without its chunks (NOGEO).
+template <int J = 0>
+__device__ __forceinline__ void store_x1_plane(State& s, const unsigned* mw) {
+  if constexpr (J < 8) {
+#pragma unroll
+    for (int g = 0; g < 8; g += 2) {
+      const int off = 16 * (J & 1);
+      const float4 v = make_float4(masked(s.sl[J][2 * g], mw[J >> 1], off + 2 * g),
+                                   masked(s.sl[J][2 * g + 1], mw[J >> 1], off + 2 * g + 1),
+                                   masked(s.sl[J][2 * g + 2], mw[J >> 1], off + 2 * g + 2),
+                                   masked(s.sl[J][2 * g + 3], mw[J >> 1], off + 2 * g + 3));
+      *reinterpret_cast<float4*>(s.sv + 32 * J + 8 * (g / 2)) = v;
+    }
+    store_x1_plane<J + 1>(s, mw);
+  }
+}
+
+// NOGEO (the training backward with no d ro / d rd / d pts wanted -- train.py's rays are data,
+// ray_sampler.py:53-82): the d-dir chunk, both layer_xyz1^T chunks and the encoding / ray epilogue
+// only feed those outputs, so they are not streamed or run (33 chunks per tile, DmaNoGeo; layer_dir1^T
+// copies its d feat out itself).  layer_xyz1's dPre plane is stored from the slots at the tile's end.
+// crun: the running chunk counter.
+template <int MODE, bool TRAIN, bool NOGEO = false>
 __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* lds, float* blds, int64_t tile,
-                                         int& cur_code) {
+                                         int& cur_code, int& crun) {
+  using D = typename std::conditional<NOGEO, DmaNoGeo, DmaFull>::type;
   const int64_t row = tile * kTile + s.wave * 32 + (s.lane & 31);
   const bool valid = row < a.m;
   const int64_t rc = valid ? row : a.m - 1;
@@ -1225,7 +1283,8 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
     if (cur_code >= 0) flush_gcode(s, a, blds, cur_code);
     cur_code = crow0;
   }
-  int c = 0;
+  int c = NOGEO ? crun : 0;
+  s.cbase = c;
   const unsigned gl = lds_addr(blds + kGaccOff + s.wave * kCbStride) + 16u * s.h;  // + 4h floats
   const unsigned gbase = gl;  // the atomics run on the holder lanes only (ds_add)
   // training: the dPre plane rows (the bias gradients are folded into the dW GEMMs)
@@ -1264,7 +1323,7 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   {
     bwd_init<8>(s, blds, kTZeros, sig_b);
     CopyFill f{s};
-    chunk_mfma<6, true, true>(s, lds, c, rh, rl, z8, z8, f);
+    chunk_mfma<6, true, true, D>(s, lds, c, rh, rl, z8, z8, f);
     ++c;
     copy_acc(s, 6);
     copy_acc(s, 7);
@@ -1272,17 +1331,23 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   // ---- layer_dir2^T (m_v2), layer_dir1^T (m_v1) + its d-dir chunk
   floatx16 acc2;
   s.sv = plane(0);
-  bwd_pass<false, true, TRAIN>(s, a, lds, c, blds, kTZeros, sig_b, mk[3], gbase);
+  bwd_pass<false, true, TRAIN, D>(s, a, lds, c, blds, kTZeros, sig_b, mk[3], gbase);
   s.sv = plane(1);
-  bwd_pass<false, false, TRAIN>(s, a, lds, c, blds, kTZeros, sig_b, mk[2], gbase);
-  bwd_dir_chunk(s, lds, c, acc2);
+  bwd_pass<false, NOGEO, TRAIN, D>(s, a, lds, c, blds, kTZeros, sig_b, mk[2], gbase);
+  if constexpr (!NOGEO) bwd_dir_chunk(s, lds, c, acc2);
   // ---- fc_out^T (d feat unmasked, sigma rank-1 init), layer_xyz2^T (m_h2): g_code sums
   const unsigned ones[4] = {~0u, ~0u, ~0u, ~0u};
   for (int l = 0; l < 2; ++l) {
     const unsigned* mw = l == 0 ? ones : mk[1];
     const unsigned gb = gbase + 4u * (l == 0 ? kCbFeat : kCbXyz2);
     s.sv = plane(2 + l);
-    bwd_pass<true, true, TRAIN>(s, a, lds, c, blds, l == 0 ? kTSigmaCol : kTZeros, sig_b, mw, gb);
+    bwd_pass<true, true, TRAIN, D>(s, a, lds, c, blds, l == 0 ? kTSigmaCol : kTZeros, sig_b, mw, gb);
+  }
+  if constexpr (NOGEO) {
+    s.sv = plane(4);
+    store_x1_plane(s, mk[0]);
+    crun = c;
+    return;
   }
   // ---- layer_xyz1^T (m_h1) into acc[0..1]
   bwd_init<2>(s, blds, kTZeros, sig_b);
@@ -1368,8 +1433,9 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   }
 }
 
-template <int MODE, bool TRAIN = false>
+template <int MODE, bool TRAIN = false, bool NOGEO = false>
 __global__ __launch_bounds__(kThreads, 1) void field_x3_bwd_kernel(FieldArgs a) {
+  static_assert(!NOGEO || TRAIN, "the no-geometry schedule is the training backward's");
   __shared__ __attribute__((aligned(16))) float4 lds[kLdsQuads + kBwdLdsFloats / 4];
   float* blds = reinterpret_cast<float*>(lds + kLdsQuads);
   State s;
@@ -1379,6 +1445,7 @@ __global__ __launch_bounds__(kThreads, 1) void field_x3_bwd_kernel(FieldArgs a) 
   s.wsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.packed), 0, kPackedFloats * 4, 0x00020000);
   s.voff = static_cast<unsigned>(s.wave * 64 + s.lane) * 16u;
   s.sv = nullptr;
+  s.cbase = 0;
 #pragma unroll
   for (int k = 0; k < kConsts / kThreads; ++k)
     blds[k * kThreads + threadIdx.x] = a.packed[kBiasXyz1 + k * kThreads + threadIdx.x];
@@ -1392,13 +1459,15 @@ __global__ __launch_bounds__(kThreads, 1) void field_x3_bwd_kernel(FieldArgs a) 
   for (int i = 0; i < kDmaPerWave / 2; ++i) dma_piece(s, lds, 2, i);
   int cur_code = -1;
   const int64_t n_tiles = (a.m + kTile - 1) / kTile;
+  int crun = 0;
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x)
-    bwd_tile<MODE, TRAIN>(s, a, lds, blds, tile, cur_code);
+    bwd_tile<MODE, TRAIN, NOGEO>(s, a, lds, blds, tile, cur_code, crun);
   __builtin_amdgcn_s_waitcnt(0x0F70);
   if (cur_code >= 0) flush_gcode(s, a, blds, cur_code);
 }
 
 static_assert(kTChunkX1 + 2 == kChunks, "backward chunk schedule");
+static_assert(kTChunkDir == kNoGeoSkip && kTChunkDir + 1 == kTChunkOut, "no-geometry stream: skips the d-dir chunk");
 static_assert(kBwdLdsFloats * 4 + kLdsQuads * 16 <= 160 * 1024, "LDS budget");
 
 }  // namespace x3
@@ -1434,6 +1503,14 @@ int64_t mask_words_x3(int64_t m) { return cn::ceil_div(m, x3::kTile) * x3::kMask
 
 int launch_field_x3_bwd(int mode, FieldArgs& a, hipStream_t st) {
   const unsigned grid = static_cast<unsigned>(std::min<int64_t>(cn::ceil_div(a.m, x3::kTile), cu_count()));
+  if (a.dpre && !a.d_pts && !a.d_ro && !a.d_rd && nogeo_enabled()) {
+    switch (mode) {
+      case kFromPts: hipLaunchKernelGGL((x3::field_x3_bwd_kernel<kFromPts, true, true>), dim3(grid), dim3(x3::kThreads), 0, st, a); break;
+      case kFromRayZ: hipLaunchKernelGGL((x3::field_x3_bwd_kernel<kFromRayZ, true, true>), dim3(grid), dim3(x3::kThreads), 0, st, a); break;
+      default: return CN_EUNSUPPORTED;
+    }
+    return cn::launch_status();
+  }
   if (a.dpre) {
     switch (mode) {
       case kFromPts: hipLaunchKernelGGL((x3::field_x3_bwd_kernel<kFromPts, true>), dim3(grid), dim3(x3::kThreads), 0, st, a); break;

@@ -39,7 +39,7 @@ def test_parallel_image_render_gloo(world, nc, nf, tmp_path):
     assert np.abs(res["rgb"] - g[f"nc{nc}_n{world}_rgb"]).max() <= 1e-5
 
 
-def _gather_worker(rank, world, port, out_path):
+def _gather_worker(rank, world, port, out_path, single_tensor):
     import torch.distributed as dist
     from codenerf.nerf import gather_rows
     from codenerf.utils import split_sizes
@@ -48,7 +48,7 @@ def _gather_worker(rank, world, port, out_path):
         per, _ = split_sizes(1001, world)
         start = sum(per[:rank])
         rows = torch.arange(start, start + per[rank], dtype=torch.float32)[:, None].repeat(1, 3)
-        out = gather_rows(rows, per, rank)
+        out = gather_rows(rows, per, rank, single_tensor=single_tensor)
         if rank == 0:
             np.save(out_path, out.numpy())
         else:
@@ -57,10 +57,13 @@ def _gather_worker(rank, world, port, out_path):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_gather_rows_uneven_shares(world, tmp_path):
+@pytest.mark.parametrize("single_tensor", [True, False])
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_gather_rows_uneven_shares(world, single_tensor, tmp_path):
+    """gather_rows' two branches: all_gather_into_tensor (the default, RCCL's form, run on gloo here) and
+    the list all_gather, with uneven Q5 shares."""
     out = str(tmp_path / "g.npy")
-    mp.start_processes(_gather_worker, args=(world, _free_port(), out), nprocs=world, join=True,
+    mp.start_processes(_gather_worker, args=(world, _free_port(), out, single_tensor), nprocs=world, join=True,
                        start_method="spawn")
     got = np.load(out)
     assert got.shape == (1001, 3)

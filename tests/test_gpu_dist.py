@@ -148,3 +148,35 @@ def test_ddp_drop_in_rccl(dev, rccl_world1):
             assert torch.equal(a[k], b[k]), k
     for k in p0:
         assert torch.equal(p0[k], p1[k]), k
+
+
+def test_train_minibatch_no_host_sync_rccl(dev, rccl_world1):
+    """The data-parallel chunk step (train.py:96-114 + util.py:139-142's gradient average) over RCCL
+    runs with no host synchronisation: AdamW.allreduce_grads issues ONE all-reduce of the flat
+    gradient with its has-grad flags appended (a cached device tensor) and reads nothing back when
+    every parameter holds a gradient; torch's sync debug mode "error" raises on any sync."""
+    import numpy as np
+    from codenerf import train as T
+    from codenerf.nerf import PointSampler
+    from test_gpu_train import _opt_cfg, embedders as embs
+    models = _train_setup(dev)
+    cfg = _opt_cfg()
+    cfg.is_distributed = True
+    opt, sched = T.prepare_optimizer(cfg, models)
+    ps = PointSampler(16, 16, 0.8, 1.8, spacing_mode="lindepth", perturb=False, dtype=torch.float32, device=dev)
+    e = embs(dev)
+    chunks = []
+    for step in range(3):
+        ro, rd, ids, tgt = _chunk(dev, obj=1, seed=4 + step)
+        ids._cn_host_ids = np.full(ids.shape[0], 1, dtype=np.int64)
+        chunks.append((ro, rd, ids, tgt))
+    T.train_minibatch(models, opt, sched, ps, e, *chunks[0], 1e-5, is_distributed=True)   # first call: caches
+    torch.cuda.synchronize()
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        for c in chunks[1:]:
+            out = T.train_minibatch(models, opt, sched, ps, e, *c, 1e-5, is_distributed=True)
+    finally:
+        torch.cuda.set_sync_debug_mode(0)
+    torch.cuda.synchronize()
+    assert np.isfinite(float(out["psnr"])) and np.isfinite(float(out["total_loss"]))

@@ -126,6 +126,60 @@ def _train_worker(rank, world, port, out_dir):
         dist.destroy_process_group()
 
 
+def _nosync_worker(rank, world, port, out_dir):
+    """train_minibatch on 2 gloo ranks under torch's sync debug mode "error": the product code between
+    the collectives must not synchronise (gloo itself stages device tensors through the host, so the
+    mode is lifted for the duration of its all-reduce only)."""
+    import numpy as np
+    import torch.distributed as dist
+    from codenerf import train as T
+    from test_gpu_train import embedders
+    dev = _init(rank, world, port)
+    try:
+        models, opt, sched, ps = _setup(dev, True)
+        opt.broadcast_params(0)
+        e = embedders(dev)
+        chunks = []
+        for k in range(3):
+            ro, rd, ids, tgt = _chunk(dev, 4096, 20 + 2 * k + rank)
+            ids._cn_host_ids = np.full(ids.shape[0], 1, dtype=np.int64)
+            chunks.append((ro, rd, ids, tgt))
+        T.train_minibatch(models, opt, sched, ps, e, *chunks[0], 1e-5, is_distributed=True)
+        torch.cuda.synchronize()
+        real = dist.all_reduce
+        calls = []
+
+        def gloo_all_reduce(*a, **k):
+            calls.append(a[0].numel())
+            torch.cuda.set_sync_debug_mode(0)
+            try:
+                return real(*a, **k)
+            finally:
+                torch.cuda.set_sync_debug_mode("error")
+        dist.all_reduce = gloo_all_reduce
+        torch.cuda.set_sync_debug_mode("error")
+        try:
+            for c in chunks[1:]:
+                T.train_minibatch(models, opt, sched, ps, e, *c, 1e-5, is_distributed=True)
+        finally:
+            torch.cuda.set_sync_debug_mode(0)
+            dist.all_reduce = real
+        torch.cuda.synchronize()
+        assert len(calls) == 2, calls                          # ONE collective per optimiser step
+        torch.save({f"{k}.{n}": p.detach().cpu() for k, m in models.items() for n, p in m.named_parameters()},
+                   os.path.join(out_dir, f"nosync{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_train_minibatch_two_ranks_no_host_sync(tmp_path):
+    """the per-step has-grad read-back is gone from AdamW.allreduce_grads."""
+    _spawn(_nosync_worker, 2, str(tmp_path))
+    got = [torch.load(str(tmp_path / f"nosync{r}.pt"), weights_only=True) for r in range(2)]
+    for k in got[0]:
+        assert torch.equal(got[0][k], got[1][k]), ("ranks differ", k)
+
+
 def test_train_allreduce_two_ranks(tmp_path):
     """Two data-parallel chunk steps on 2 ranks vs one process averaging both chunks' gradients."""
     from codenerf import train as T
@@ -178,3 +232,121 @@ def test_bench_gather_views_multi_rank(tmp_path, world):
     res = json.load(open(tmp_path / "bench.json"))
     assert res["n_gpus"] == world and res["value"] > 0
     margin(f"bench_multi_rank_n{world}[f32]", "multi_rank_maxdiff", res["multi_rank_maxdiff"], 0.0)
+
+
+def _eval_setup(cfg, dev, rank):
+    """eval.py:41-79 as codenerf.evaluate.eval_loop runs it: seeds, loaders, models, the optimiser's
+    broadcast of rank 0's parameters (no checkpoint here), samplers and embedders."""
+    from codenerf import nerf
+    from codenerf.datasets import prepare_dataloader
+    from codenerf.train import prepare_models, prepare_optimizer, seed_rank
+    seed_rank(rank, cfg)
+    loader, _ = prepare_dataloader("val", cfg, dev)
+    _, train_dataset = prepare_dataloader("train", cfg, None)
+    models = prepare_models(cfg, train_dataset.num_objects, dev)
+    prepare_optimizer(cfg, models)
+    first = next(iter(loader))
+    (h, w), k = first["color"][0].shape[:2], first["intrinsic"][0]
+    samplers = nerf.prepare_samplers(cfg, h, w, k.cpu(), torch.float32, dev)
+    return loader, models, samplers, nerf.prepare_embedders(cfg, torch.float32, dev)
+
+
+def _eval_cfg(tree, logdir, world):
+    from test_gpu_drivers import _cfg
+    cfg = _cfg(tree, logdir, iterations=6, val_iterations=3)
+    cfg.is_distributed, cfg.gpus = world > 1, world
+    cfg.nerf.point_sampler.perturb = False     # a deterministic render to compare the gather bit for bit
+    return cfg
+
+
+def _eval_worker(rank, world, port, tree, out_dir):
+    import numpy as np
+    import torch.distributed as dist
+    from codenerf.evaluate import validate
+    dev = _init(rank, world, port)
+    try:
+        cfg = _eval_cfg(tree, os.path.join(out_dir, "e"), world)
+        loader, models, samplers, embedders = _eval_setup(cfg, dev, rank)
+        val = next(iter(loader))
+        val = {"color": val["color"].clone(), "pose": val["pose"].clone()}
+        if rank == 1:       # a different view on rank 1: validate must broadcast rank 0's (eval.py:111-115)
+            val["color"] = val["color"].flip(1).contiguous()
+        st = {"np": np.random.get_state(), "cpu": torch.get_rng_state(), "cuda": torch.cuda.get_rng_state(dev)}
+        res = validate(cfg, val, models, samplers, embedders, dev)
+        out = {"np_keys": torch.from_numpy(st["np"][1].astype(np.int64)), "np_pos": st["np"][2],
+               "np_hg": st["np"][3], "np_g": st["np"][4],
+               "cpu_rng": st["cpu"], "cuda_rng": st["cuda"].cpu(), "zs": res["codes"][0].cpu(),
+               "zt": res["codes"][1].cpu(), "cam_pose": res["cam_pose"].cpu(),
+               "losses": torch.tensor([h["total_loss"] for h in res["history"]], dtype=torch.float64)}
+        if rank == 0:
+            out.update(rgb=res["rgb"].cpu(), loss=res["loss"], psnr=res["psnr"], pose_error=res["pose_error"],
+                       color=val["color"].cpu(), gt_pose=val["pose"].cpu(),
+                       state={f"{k}.{n}": v.cpu() for k, m in models.items() for n, v in m.state_dict().items()})
+        else:
+            assert res["rgb"] is None and "loss" not in res
+        torch.save(out, os.path.join(out_dir, f"eval{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_validate_two_ranks_q6(tmp_path):
+    """eval.py:82-205 on two ranks (C5's multi-GPU eval): rank 0's view broadcast, every rank
+    optimising codes and pose on its own ray draws (seed (r + 1) + randomseed), then
+    parallel_image_render (nerf/__init__.py:137-226) with each rank rendering its Q5 slice from ITS OWN
+    pose and codes.  Checked against a single process: (1) each rank's slice, rendered from that rank's
+    optimised pose and codes, equals rank 0's gathered rows bit for bit; (2) re-running each rank's
+    test_time_optimize from its recorded RNG state reproduces its first loss bit for bit and its pose
+    and codes to 1e-5 (the eval backward's per-code and per-ray sums are float atomics, so later
+    iterations match to rounding); (3) rank 0's loss / psnr / pose error are finite and the loss is
+    the gathered image's MSE."""
+    import numpy as np
+    from srn_tree import write_tree
+    from codenerf.evaluate import _pose_lr, test_time_optimize
+    from codenerf.nerf import render_rays
+    from codenerf.utils import split_sizes
+    tree = write_tree(str(tmp_path / "srn"), channels=4)
+    _spawn(_eval_worker, 2, tree, str(tmp_path))
+    got = [torch.load(str(tmp_path / f"eval{r}.pt"), weights_only=True) for r in range(2)]
+    dev = torch.device("cuda", 0)
+    cfg = _eval_cfg(tree, str(tmp_path / "single"), 1)
+    _, models, (rs, ps), emb = _eval_setup(cfg, dev, 0)
+    state = got[0]["state"]
+    for k, m in models.items():
+        m.load_state_dict({n[len(k) + 1:]: v for n, v in state.items() if n.startswith(k + ".")})
+    color = got[0]["color"].to(dev, torch.float32)
+    target = color.reshape(-1, color.shape[-1])
+    gt_pose = got[0]["gt_pose"].to(dev, torch.float32)
+    emb_t = models["embedding"]
+    all_s, all_t = emb_t.get_all_embeddings(device=dev)
+    e, o = cfg.experiment, cfg.optimizer
+    rows = []
+    per, _ = split_sizes(target.shape[0], 2)
+    for r in range(2):
+        g = got[r]
+        np.random.set_state(("MT19937", g["np_keys"].numpy().astype(np.uint32), int(g["np_pos"]), int(g["np_hg"]),
+                             float(g["np_g"])))
+        torch.set_rng_state(g["cpu_rng"])
+        torch.cuda.set_rng_state(g["cuda_rng"], dev)
+        zs, zt, _, hist, cam = test_time_optimize(target, (rs, ps), emb, models, (all_s.detach(), all_t.detach()),
+                                                  e.val_iterations, val_lr=o.val_lr, angle_lr=_pose_lr(o, "angle_lr"),
+                                                  radius_lr=_pose_lr(o, "radius_lr"),
+                                                  regularizer_lambda=e.regularizer_lambda, gt_pose=gt_pose)
+        assert hist[0]["total_loss"] == g["losses"][0].item(), r
+        assert (cam.cpu() - g["cam_pose"]).abs().max().item() <= 1e-5, r
+        assert (zs.detach().cpu() - g["zs"]).abs().max().item() <= 1e-5, r
+        assert (zt.detach().cpu() - g["zt"]).abs().max().item() <= 1e-5, r
+        # rank r's Q5 slice from its own optimised pose and codes, the validation chunking
+        ro, rd = rs.get_bundle(tform_cam2world=g["cam_pose"].to(dev))
+        ro, rd = ro.reshape(-1, 3), rd.reshape(-1, 3)
+        sl = slice(sum(per[:r]), sum(per[:r + 1]))
+        n = ro.shape[0]
+        with torch.no_grad():
+            out = render_rays(ro[sl], rd[sl], g["zs"].to(dev).expand(n, -1)[sl], g["zt"].to(dev).expand(n, -1)[sl],
+                              ps, emb, models["nerf_coarse"], models["nerf_fine"], cfg.nerf.validation.chunksize)
+        rows.append(out["rgb_fine"].cpu())
+    assert not torch.equal(got[0]["cam_pose"], got[1]["cam_pose"])      # the ranks optimised independently
+    want = torch.cat(rows)
+    assert torch.equal(got[0]["rgb"], want)
+    assert np.isfinite([got[0]["loss"], got[0]["psnr"], got[0]["pose_error"]]).all()
+    mse = ((got[0]["rgb"].double() - got[0]["color"].reshape(-1, 4)[:, :3].double()) ** 2).mean().item()
+    assert abs(got[0]["loss"] - mse) <= 1e-6 * max(1.0, mse)

@@ -114,16 +114,20 @@ def _dp_worker(rank, world, port, out):
         ps = _params(seed=rank)                  # replicas start apart (train.py:29-31 seeds by rank)
         opt = _opt(ps)
         opt.broadcast_params(0)
-        for p in ps:
-            p.grad = torch.full_like(p, float(rank + 1))
-        if rank == 1:
-            ps[3].grad = None                    # absent on one rank: counts as zero
-        ps[1].grad = None                        # absent on every rank: stays None (step skips it)
-        opt.allreduce_grads()
-        assert ps[1].grad is None
+        steps = []
+        # three rounds of has-grad patterns: (missing on rank 1 only, missing everywhere), the same
+        # again (the cached flags), then a new one (missing on rank 0 only)
+        for missing_here, missing_all in (({3} if rank == 1 else set(), {1}), ({3} if rank == 1 else set(), {1}),
+                                          ({2} if rank == 0 else set(), set())):
+            for i, p in enumerate(ps):
+                p.grad = None if (i in missing_here or i in missing_all) else torch.full_like(p, float(rank + 1))
+            opt.allreduce_grads()
+            for i in missing_all:
+                assert ps[i].grad is None
+            steps.append(torch.cat([(p.grad if p.grad is not None else torch.full_like(p, -7.0)).reshape(-1)
+                                    for p in ps]).numpy())
         np.savez(out.format(rank), params=torch.cat([p.detach().reshape(-1) for p in ps]).numpy(),
-                 grads=torch.cat([(p.grad if p.grad is not None else torch.full_like(p, -7.0)).reshape(-1)
-                                  for p in ps]).numpy())
+                 grads=np.stack(steps))
         # the torch-optimiser fallback: ranks with DIFFERENT missing gradients issue the same
         # all-reduce sizes (no hang) and the same flags
         from types import SimpleNamespace
@@ -143,19 +147,29 @@ def _dp_worker(rank, world, port, out):
         dist.destroy_process_group()
 
 
-def test_allreduce_and_broadcast_gloo(tmp_path):
-    world = 2
+@pytest.mark.parametrize("world", [2, 3])
+def test_allreduce_and_broadcast_gloo(world, tmp_path):
+    """AdamW.allreduce_grads (util.py:139-142's DDP average): one SUM all-reduce of the flat gradient
+    with the has-grad flags in its tail, divided by the world size -- the arithmetic on every backend;
+    a gradient missing on a rank counts as zero, one missing everywhere stays None; changing patterns
+    between steps (the per-pattern flag cache) reduce correctly."""
     out = str(tmp_path / "r{}.npz")
     mp.start_processes(_dp_worker, args=(world, _free_port(), out), nprocs=world, join=True, start_method="spawn")
-    r0, r1 = np.load(out.format(0)), np.load(out.format(1))
+    res = [np.load(out.format(r)) for r in range(world)]
     ref = torch.cat([p.detach().reshape(-1) for p in _params(seed=0)]).numpy()
-    assert np.array_equal(r0["params"], ref) and np.array_equal(r1["params"], ref)
     sizes = [int(np.prod(s)) for s in SHAPES]
-    exp = np.concatenate([np.full(n, 1.5, np.float32) for n in sizes])
-    o3 = sum(sizes[:3])
-    exp[o3:o3 + sizes[3]] = 0.5                   # (1 + 0) / 2
-    exp[sizes[0]:sizes[0] + sizes[1]] = -7.0      # no rank had it: grad None
-    assert np.array_equal(r0["grads"], exp) and np.array_equal(r1["grads"], exp)
+    offs = np.concatenate([[0], np.cumsum(sizes)])
+    full = np.float32(sum(range(1, world + 1))) / np.float32(world)
+    exp = np.stack([np.full(offs[-1], full, np.float32) for _ in range(3)])
+    for st in (0, 1):
+        exp[st, offs[3]:offs[4]] = np.float32(sum(r + 1 for r in range(world) if r != 1)) / np.float32(world)
+        exp[st, offs[1]:offs[2]] = -7.0       # no rank had it: grad None
+    exp[2, offs[2]:offs[3]] = np.float32(sum(r + 1 for r in range(world) if r != 0)) / np.float32(world)
+    for r in res:
+        assert np.array_equal(r["params"], ref)
+        assert np.array_equal(r["grads"], exp)
+    if world != 2:
+        return
     f0, f1 = np.load(out.format(0) + ".fallback.npz"), np.load(out.format(1) + ".fallback.npz")
     ref10 = torch.cat([q.detach().reshape(-1) for q in _params(seed=10)]).numpy()
     assert np.array_equal(f0["params"], ref10) and np.array_equal(f1["params"], ref10)   # broadcast from rank 0
