@@ -266,7 +266,10 @@ def run(args):
         "dtype": "f32" if args.precision == "f32" else args.precision,
         "data": "synthetic (hash-initialised CodeNeRFModel weights, one latent code pair, spherical poses)",
         "config": {"workload": "C2: srn-cars-code, one held-out car, 128x128 views, 64 coarse samples/ray, "
-                               "chunk 4096, lindepth near 0.8 far 1.8, fused HIP render",
+                               "chunk 4096, lindepth near 0.8 far 1.8, perturb=False (parity mode: the "
+                               "deterministic depths the golden renders pin; the perturbed form is the "
+                               "'perturbed' line), fused HIP render",
+                   "perturb": False,
                    "images_per_step": views, "images_per_rank_step": B, "rays_per_image": n_img_rays,
                    "samples_per_ray": NC,
                    "parallelism": f"ray-sharded x{n} + RCCL all-gather" if n > 1 else "single GPU"},
@@ -296,6 +299,15 @@ def run(args):
     set_precision(args.precision)
 
     if not args.no_extras:
+        # ---- C2 as srn-cars-code.yml's validation render configures it (perturb: True, Q4): stratified
+        # depths from the device RNG (torch.rand_like on the GPU, point_sampler.py:61-65)
+        ps_p = PointSampler(NC, NF, NEAR, FAR, "lindepth", True, torch.float32, dev)
+        kp = max(1, args.steps // 4)
+        dtp, fp_, _ = timed(kp, 1, lambda rec: render_step(rec, True, ps_p))
+        result["perturbed"] = {"value": total_rays / args.steps * kp / dtp, "unit": "rays/s",
+                               "ms_per_step": dtp / kp * 1e3, "steps": kp, "dtype": args.precision,
+                               "field_launch_ms_avg": sum(fp_) / max(1, len(fp_)),
+                               "note": "C2 with perturb=True (stratified depths drawn on the device per step)"}
         # ---- C3: 64+64 hierarchical render, same views
         k3 = max(1, args.steps // 4)
         dth, f3, _ = timed(k3, 1, lambda rec: render_step(rec, False))

@@ -20,7 +20,7 @@ from typing import Optional, Sequence
 
 import torch
 
-from . import ops
+from . import _lib, ops
 
 # packed weights per model and format: repacked only when a parameter's storage or version changed
 # (an optimiser step bumps the versions; see optim.AdamW).  Keyed by id() of the model's first
@@ -28,9 +28,8 @@ from . import ops
 _PACKS = {}
 
 
-def _packed(owner, params, fmt: str):
-    """ops.mlp_pack(params, fmt), cached while ``params`` are unchanged (frozen weights of the eval
-    loop pack once instead of twice per iteration)."""
+def _pack_cache(owner, params):
+    """(the owner's cache dict, the weights' signature): packs stay valid while ``params`` are unchanged."""
     sig = tuple((p.data_ptr(), p._version) for p in params)
     key = id(owner)
     ent = _PACKS.get(key)
@@ -38,12 +37,34 @@ def _packed(owner, params, fmt: str):
         ent = (weakref.ref(owner), {})
         _PACKS[key] = ent
         weakref.finalize(owner, _PACKS.pop, key, None)
-    hit = ent[1].get(fmt)
+    return ent[1], sig
+
+
+def _packed(owner, params, fmt: str):
+    """ops.mlp_pack(params, fmt), cached while ``params`` are unchanged (frozen weights of the eval
+    loop pack once instead of twice per iteration)."""
+    cache, sig = _pack_cache(owner, params)
+    hit = cache.get(fmt)
     if hit is not None and hit[0] == sig:
         return hit[1]
     packed = ops.mlp_pack(params, fmt)
-    ent[1][fmt] = (sig, packed)
+    cache[fmt] = (sig, packed)
     return packed
+
+
+def _prepare_w16(owner, params, z_s, z_t, n_zero: int):
+    """The fp32 training step's per-model preparation in ONE launch (ops.field_prepare): the code terms,
+    the forward and backward packs where the cache lacks them (after every optimiser step), and a
+    zeroed g_code accumulator for the fused backward -> (cb, packed "f32_w16", zero)."""
+    cache, sig = _pack_cache(owner, params)
+    have = {f: (cache.get(f) is not None and cache[f][0] == sig) for f in ("f32_w16", "f32_w16_t")}
+    cb, pk, pkt, zero = ops.field_prepare(params, z_s, z_t, pack=not have["f32_w16"], pack_t=not have["f32_w16_t"],
+                                          n_zero=n_zero)
+    if pk is not None:
+        cache["f32_w16"] = (sig, pk)
+    if pkt is not None:
+        cache["f32_w16_t"] = (sig, pkt)
+    return cb, cache["f32_w16"][1], zero
 
 
 def _needs_grad(*ts) -> bool:
@@ -234,11 +255,20 @@ class RadianceField(torch.autograd.Function):
         ctx.orig_params = params
         ctx.owner = params[0]
         params = [p.detach() for p in params]
-        cb = ops.code_bias(params, z_s, z_t)
         n_rays = rd.shape[0]
         fused = (meta.precision in ("bf16x3", "f32") and not any(ctx.needs_input_grad[7:])
                  and ops.fused_backward_supported(z_s.shape[0], meta.n_samples, meta.code_index, meta.precision))
         ctx.fused = fused
+        ctx.g_code = None
+        train_w16 = (not fused and meta.precision == meta.train_precision == "f32"
+                     and ops.fused_backward_supported(z_s.shape[0], meta.n_samples, meta.code_index, "f32"))
+        if train_w16:
+            # the fp32 training step: code terms, both packs and the backward's zeroed g_code, one launch
+            nc = z_s.shape[0]
+            cb, packed_w16, zero = _prepare_w16(ctx.owner, params, z_s, z_t, nc * _lib.CN_CODE_BIAS_STRIDE)
+            ctx.g_code = zero.view(nc, _lib.CN_CODE_BIAS_STRIDE)
+        else:
+            cb = ops.code_bias(params, z_s, z_t)
         if fused:
             pack = "bf16x3" if meta.precision == "bf16x3" else "f32_w16"
             raw, masks = ops.radiance_field_masks(_packed(ctx.owner, params, pack), cb, rd, meta.n_samples,
@@ -259,7 +289,7 @@ class RadianceField(torch.autograd.Function):
         if ctx.train_fused:
             x3 = meta.precision == "bf16x3"
             raw, saved, ctx.masks = ops.radiance_field_train_w16(
-                _packed(ctx.owner, params, "bf16x3" if x3 else "f32_w16"), cb, rd, meta.n_samples, meta.chunk_rows,
+                packed_w16 if train_w16 else _packed(ctx.owner, params, "bf16x3"), cb, rd, meta.n_samples, meta.chunk_rows,
                 meta.fx, meta.fd, pts=pts, ro=ro, z=z, code_index=meta.code_index, precision=meta.precision)
         else:
             raw, saved = ops.radiance_field_train(ops.mlp_pack(params, "f32"), cb, rd, meta.n_samples,
@@ -298,8 +328,9 @@ class RadianceField(torch.autograd.Function):
                                          ctx.acts, ctx.x_enc, g_raw.contiguous(), rd.shape[0], meta.n_samples,
                                          meta.chunk_rows, z_s.shape[0], meta.fx, meta.fd, rd=rd, pts=pts, ro=ro, z=z,
                                          code_index=meta.code_index, param_grads=pg, want_pts=needs[2],
-                                         want_ro=needs[3], want_rd=needs[1], precision=meta.precision)
-            ctx.acts = ctx.x_enc = ctx.masks = None
+                                         want_ro=needs[3], want_rd=needs[1], precision=meta.precision,
+                                         g_code=ctx.g_code)
+            ctx.acts = ctx.x_enc = ctx.masks = ctx.g_code = None
             dz_s, dz_t = ops.code_bias_backward(params, z_s, z_t, r["g_code"], pg, want_z=want_z)
             grads = pg if pg is not None else [None] * len(params)
             return (None, r["d_rd"], r["d_pts"], r["d_ro"], None, dz_s, dz_t, *grads)

@@ -304,6 +304,28 @@ def code_bias(params: Sequence[Tensor], z_s: Tensor, z_t: Tensor) -> Tensor:
     return out
 
 
+def field_prepare(params: Sequence[Tensor], z_s: Tensor, z_t: Tensor, pack: bool = True, pack_t: bool = True,
+                  n_zero: int = 0):
+    """cn_field_prepare: code_bias(params, z_s, z_t), the fp32 forward / backward packs ("f32_w16",
+    "f32_w16_t"; each only if asked) and a zeroed (n_zero,) buffer in ONE launch -> (cb, packed or None,
+    packed_t or None, zero or None); bitwise the separate calls' outputs."""
+    lib = _lib_ready()
+    params = [_cuda(p.detach(), f"param{i}") for i, p in enumerate(params)]
+    z_s, z_t = _cuda(z_s.detach(), "z_s"), _cuda(z_t.detach(), "z_t")
+    assert z_s.shape == z_t.shape and z_s.dim() == 2 and z_s.shape[1] == 256, "codes must be (n, 256)"
+    dev = z_s.device
+    cb = torch.empty(z_s.shape[0], _lib.CN_CODE_BIAS_STRIDE, device=dev, dtype=torch.float32)
+    nf = mlp_packed_floats("f32_w16")
+    packed = torch.empty(nf, device=dev, dtype=torch.float32) if pack else None
+    packed_t = torch.empty(nf, device=dev, dtype=torch.float32) if pack_t else None
+    zero = torch.empty(n_zero, device=dev, dtype=torch.float32) if n_zero else None
+    arr, keep = _lib.pointer_array(params)
+    check(lib.cn_field_prepare(arr, ptr(z_s), ptr(z_t), z_s.shape[0], ptr(cb), ptr(packed), ptr(packed_t), ptr(zero),
+                               n_zero, stream_of(cb)), "cn_field_prepare")
+    del keep
+    return cb, packed, packed_t, zero
+
+
 def mlp_forward(packed: Tensor, cb: Tensor, x: Tensor, code_index: Optional[Tensor] = None,
                 precision: str = "f32") -> Tensor:
     """CodeNeRFModel.forward on pre-encoded rows (model.py:160-194): (M, 90) -> (M, 4)."""
@@ -470,9 +492,10 @@ def field_backward_train(packed_t: Tensor, params: Sequence[Tensor], masks: Tens
                          pts: Optional[Tensor] = None, ro: Optional[Tensor] = None, z: Optional[Tensor] = None,
                          code_index: Optional[Tensor] = None, param_grads: Optional[Sequence[Tensor]] = None,
                          want_pts: bool = False, want_ro: bool = False, want_rd: bool = False,
-                         precision: str = "f32"):
+                         precision: str = "f32", g_code: Optional[Tensor] = None):
     """Fused training backward (one dX launch + deterministic dW GEMMs) -> dict g_code / d_pts / d_ro / d_rd.
-    precision "f32" (packed_t "f32_w16_t") or "bf16x3" (packed_t "bf16x3_t", 3xbf16 dW GEMMs)."""
+    precision "f32" (packed_t "f32_w16_t") or "bf16x3" (packed_t "bf16x3_t", 3xbf16 dW GEMMs).
+    ``g_code``: a zeroed (n_codes, CN_CODE_BIAS_STRIDE) accumulator (field_prepare's), else allocated."""
     fmt_t = _lib.CN_FMT_BF16X3_T if precision == "bf16x3" else _lib.CN_FMT_F32_W16_T
     lib = _lib_ready()
     m = n_rays * n_samples
@@ -484,7 +507,10 @@ def field_backward_train(packed_t: Tensor, params: Sequence[Tensor], masks: Tens
     if code_index is not None:
         code_index = _cuda(code_index, "code_index", torch.int64)
     ws = torch.empty(int(lib.cn_field_backward_train_workspace_floats(m)), device=dev, dtype=torch.float32)
-    g_code = torch.zeros(n_codes, _lib.CN_CODE_BIAS_STRIDE, device=dev, dtype=torch.float32)
+    if g_code is None:
+        g_code = torch.zeros(n_codes, _lib.CN_CODE_BIAS_STRIDE, device=dev, dtype=torch.float32)
+    else:
+        assert g_code.shape == (n_codes, _lib.CN_CODE_BIAS_STRIDE) and g_code.is_contiguous()
     d_pts = torch.empty(n_rays, n_samples, 3, device=dev, dtype=torch.float32) if want_pts else None
     d_ro = torch.zeros(n_rays, 3, device=dev, dtype=torch.float32) if want_ro else None
     d_rd = torch.zeros(n_rays, 3, device=dev, dtype=torch.float32) if want_rd else None

@@ -136,12 +136,17 @@ __host__ __device__ __forceinline__ bool reduce_vec4(const float* part, int64_t 
   return nk % 4 == 0 && (reinterpret_cast<uintptr_t>(part) & 15) == 0;
 }
 
-__device__ __forceinline__ void reduce_add(float* __restrict__ C, int64_t ldc, int K, int64_t e, float v) {
+__device__ __forceinline__ void reduce_add(float* __restrict__ C, int64_t ldc, int K, int64_t e, float v,
+                                           float* __restrict__ C2 = nullptr) {
   C[(e / K) * ldc + e % K] += v;
+  if (C2) C2[(e / K) * ldc + e % K] += v;
 }
 
+// C (and C2, when set: a second target of the same layout) += the fixed-order sum of the n_parts
+// partial (N, K) tiles, elements of block b.
 __device__ __forceinline__ void reduce_block(const float* __restrict__ part, int64_t n_parts, int N, int K,
-                                             float* __restrict__ C, int64_t ldc, int64_t b, float4 (&red)[4][64]) {
+                                             float* __restrict__ C, int64_t ldc, int64_t b, float4 (&red)[4][64],
+                                             float* __restrict__ C2 = nullptr) {
   const int q = threadIdx.x >> 6, t = threadIdx.x & 63;
   const int64_t nk = (int64_t)N * K;
   const int64_t p0 = n_parts * q / 4, p1 = n_parts * (q + 1) / 4;
@@ -173,10 +178,10 @@ __device__ __forceinline__ void reduce_block(const float* __restrict__ part, int
     __syncthreads();
     if (q == 0 && e < nk) {
       const float4 r0 = red[0][t], r1 = red[1][t], r2 = red[2][t], r3 = red[3][t];
-      reduce_add(C, ldc, K, e, (r0.x + r1.x) + (r2.x + r3.x));
-      reduce_add(C, ldc, K, e + 1, (r0.y + r1.y) + (r2.y + r3.y));
-      reduce_add(C, ldc, K, e + 2, (r0.z + r1.z) + (r2.z + r3.z));
-      reduce_add(C, ldc, K, e + 3, (r0.w + r1.w) + (r2.w + r3.w));
+      reduce_add(C, ldc, K, e, (r0.x + r1.x) + (r2.x + r3.x), C2);
+      reduce_add(C, ldc, K, e + 1, (r0.y + r1.y) + (r2.y + r3.y), C2);
+      reduce_add(C, ldc, K, e + 2, (r0.z + r1.z) + (r2.z + r3.z), C2);
+      reduce_add(C, ldc, K, e + 3, (r0.w + r1.w) + (r2.w + r3.w), C2);
     }
     return;
   }
@@ -196,7 +201,7 @@ __device__ __forceinline__ void reduce_block(const float* __restrict__ part, int
   }
   red[q][t].x = s;
   __syncthreads();
-  if (q == 0 && e < nk) reduce_add(C, ldc, K, e, (red[0][t].x + red[1][t].x) + (red[2][t].x + red[3][t].x));
+  if (q == 0 && e < nk) reduce_add(C, ldc, K, e, (red[0][t].x + red[1][t].x) + (red[2][t].x + red[3][t].x), C2);
 }
 
 __global__ __launch_bounds__(256) void reduce_partials_kernel(const float* __restrict__ part, int64_t n_parts,
@@ -211,6 +216,7 @@ struct ReduceJob {
   float* C;
   int64_t n_parts, ldc, first_block;
   int N, K;
+  float* C2;  // a second target (g_code's entries that are also bias gradients), or null
 };
 constexpr int kMaxReduceJobs = 16;
 struct ReduceJobs {
@@ -223,7 +229,7 @@ __global__ __launch_bounds__(256) void reduce_jobs_kernel(ReduceJobs jobs) {
   int k = jobs.n - 1;
   while (k > 0 && (int64_t)blockIdx.x < jobs.j[k].first_block) --k;
   const ReduceJob& jb = jobs.j[k];
-  reduce_block(jb.part, jb.n_parts, jb.N, jb.K, jb.C, jb.ldc, (int64_t)blockIdx.x - jb.first_block, red);
+  reduce_block(jb.part, jb.n_parts, jb.N, jb.K, jb.C, jb.ldc, (int64_t)blockIdx.x - jb.first_block, red, jb.C2);
 }
 
 // gemm_tn: C[n][k] += sum_m A[m][n] B[m][k] (dW = dPre^T X).  No LDS: on
@@ -1100,6 +1106,7 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __rest
   __shared__ __attribute__((aligned(16))) float ring[kEncRing][kEncRows * RS];  // A stages, by LDS-DMA
   __shared__ __attribute__((aligned(16))) float senc[2][kEncRows * ES];
   __shared__ __attribute__((aligned(16))) float4 xs[3][kEncRows];  // decoded geometry, 3 stages
+  __shared__ int xfast[3];  // ENC 0, fp32: the stage's 16 points all inside fast_sincosf's bound (below)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int i = lane & 31, h = lane >> 5;
@@ -1187,6 +1194,21 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __rest
       }
     }
   };
+  // The encodings the forward multiplied (ENC 0, fp32): field_w16_kernel evaluates a 16-sample wave's
+  // (sin, cos) pairs with fast_sincosf when every sample's max |x| * max |f_xyz| is inside kFastSinBound
+  // (and its view direction's too: |vd| <= 1, so that holds whenever max |f_dir| is), else every pair of
+  // the wave with ocml's sincosf.  The forward's waves are 16-row groups aligned to 16 rows, and so is
+  // every stage here (rows_per_block is a multiple of kEncRows): the stage takes the same choice.  The
+  // 3xbf16 forward always calls sincosf (enc_pair), and so does X3 here.  (A wave whose view direction is
+  // NaN -- a zero-length ray -- took sincosf in the forward; its outputs are NaN either way.)
+  float fast_freq_max = 0.0f, dir_freq_max = 0.0f;   // load_consts' mx / md
+#pragma unroll
+  for (int k = 0; k < 10; ++k) fast_freq_max = fmaxf(fast_freq_max, fabsf(a.fx[k]));
+#pragma unroll
+  for (int k = 0; k < 4; ++k) dir_freq_max = fmaxf(dir_freq_max, fabsf(a.fd[k]));
+  // |vd_d| <= 1 up to the rounding of the normalisation (a few ulp): the margin keeps this true only
+  // where the forward's per-sample test cannot fail (every embedder's max |f_dir| is far below it)
+  const bool dir_fast = dir_freq_max * 1.0001f <= mlp::kFastSinBound;
   auto put_x = [&](int st) {
     if (tid < kEncRows) {
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1201,13 +1223,31 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __rest
         v = make_float4(__fdiv_rn(g2[0], nrm), __fdiv_rn(g2[1], nrm), __fdiv_rn(g2[2], nrm), 0.0f);
       }
       xs[st % 3][tid] = v;
+      if constexpr (ENC == 0 && !X3) {
+        // the forward's test: max |x_d| * max |f| <= kFastSinBound (false for NaN); rows past the
+        // slab are zeros and pass
+        const float xa = fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fabsf(v.z)) * fast_freq_max;
+        const bool ok = xa <= mlp::kFastSinBound;
+        const unsigned long long bad = __ballot(!ok);  // lanes 0..15 of wave 0: the stage's rows
+        if (tid == 0) xfast[st % 3] = (bad & 0xFFFFull) == 0 && dir_fast;
+      }
     }
   };
   auto enc_of = [&](int st) {  // rows past M: their A rows are zero, so any value is harmless
     const float4 x4 = xs[st % 3][es];
     const float x[4] = {x4.x, x4.y, x4.z, 0.0f};
     if (kind == 1) {
-      mlp::enc_sincosf(__fmul_rn(x[comp], freq), ev[0], ev[1]);  // the forward's encoding arithmetic
+      const float arg = __fmul_rn(x[comp], freq);
+      if constexpr (X3) {
+        sincosf(arg, &ev[0], &ev[1]);                 // the 3xbf16 forward's (enc_pair)
+      } else if constexpr (ENC == 0) {
+        if (xfast[st % 3]) mlp::fast_sincosf(arg, ev[0], ev[1]);   // the forward's choice for this wave
+        else sincosf(arg, &ev[0], &ev[1]);
+      } else {
+        // view columns: fast inside the bound, per lane -- the forward's whenever its wave's points
+        // were inside theirs (every sample of the runnable configs: |x| <= 2^14 / 2^9 = 32)
+        mlp::enc_sincosf(arg, ev[0], ev[1]);
+      }
     } else if (kind == 2) {
       ev[0] = comp < 3 ? x[comp] : 0.0f;
       ev[1] = comp + 1 < 3 ? x[comp + 1] : 0.0f;
@@ -1949,7 +1989,9 @@ struct Reducer {
   }
 };
 
-int reduce(Reducer* rd, const float* part, int64_t parts, int N, int K, float* C, int64_t ldc, hipStream_t st) {
+int reduce(Reducer* rd, const float* part, int64_t parts, int N, int K, float* C, int64_t ldc, hipStream_t st,
+           float* C2 = nullptr) {
+  if (C2 && !rd) return CN_EINVAL;  // a second target: the queued form only
   const int64_t nk = (int64_t)N * K, nblk = ceil_div(nk, grad::reduce_vec4(part, nk) ? 256 : 64);  // reduce_block's
   if (!rd) {
     hipLaunchKernelGGL(grad::reduce_partials_kernel, dim3(static_cast<unsigned>(nblk)), dim3(256), 0, st, part, parts,
@@ -1960,7 +2002,7 @@ int reduce(Reducer* rd, const float* part, int64_t parts, int N, int K, float* C
     const int rc = rd->flush();
     if (rc != CN_OK) return rc;
   }
-  rd->jobs.j[rd->jobs.n++] = grad::ReduceJob{part, C, parts, ldc, rd->blocks, N, K};
+  rd->jobs.j[rd->jobs.n++] = grad::ReduceJob{part, C, parts, ldc, rd->blocks, N, K, C2};
   rd->blocks += nblk;
   return CN_OK;
 }
@@ -2453,6 +2495,8 @@ struct TnBatch {
     float* sig_out;
     mlp::FieldArgs a; // kind 2: the geometry (view directions) of the rows
     float cost;       // per-row cost of the slot (relative)
+    float* bias2;     // a second target of the bias sums (g_code entries that are bias gradients), or null
+    float* sig2;      // the same for sig_out
   };
   Pending p[grad::kMaxTnJobs];
   int n = 0;
@@ -2556,13 +2600,13 @@ static int tn_batch_launch(TnBatch& b, bool x3, hipStream_t st, Reducer* rd) {
     }
     if (q.kind == 3) {
       CN_TRY(reduce(rd, j.part, j.n_blocks, 3, 256, q.C, q.ldc, st));
-      CN_TRY(reduce(rd, j.bias_part, j.n_blocks, 1, 3, q.bias, 3, st));
-      CN_TRY(reduce(rd, j.bias_part + 3 * (int64_t)j.n_blocks, j.n_blocks, 1, 1, q.sig_out, 1, st));
+      CN_TRY(reduce(rd, j.bias_part, j.n_blocks, 1, 3, q.bias, 3, st, q.bias2));
+      CN_TRY(reduce(rd, j.bias_part + 3 * (int64_t)j.n_blocks, j.n_blocks, 1, 1, q.sig_out, 1, st, q.sig2));
       continue;
     }
     CN_TRY(reduce(rd, j.part, j.n_blocks, 256, 256, q.C, q.ldc, st));
     if (q.kind == 1) CN_TRY(reduce(rd, j.sig_part, j.n_blocks, 1, 256, q.sig_out, 256, st));
-    if (q.bias) CN_TRY(reduce(rd, j.bias_part, j.n_blocks, 1, 256, q.bias, 256, st));
+    if (q.bias) CN_TRY(reduce(rd, j.bias_part, j.n_blocks, 1, 256, q.bias, 256, st, q.bias2));
   }
   b.n = 0;
   return CN_OK;
@@ -2687,6 +2731,7 @@ extern "C" int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, con
   // fc_rgb (h half): dW += d rgb^T v2 (+ g_code's rgb / sigma entries, folded, in the same pass); as
   // the batched launch's RGB role where that runs (fp32, folded code)
   const bool rgb_role = jobs && fold_code && !x3;
+  const bool dual_code = rgb_role;  // the g_code sums also land in the bias gradients (below)
   if (rgb_role) {
   } else if (fold_code) {
     CN_TRY(rgb_dw_draw_sums(d_raw, v2, G(kWRgb), 512, M, g_code + kCbRgb, g_code + kCbSigma, st, &red));
@@ -2700,12 +2745,19 @@ extern "C" int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, con
     TnBatch tb;
     const bool dirs = !x3 && !x_enc && dirs_foldable(a);
     const float* c = tn_slot_cost();
-    tb.p[tb.n++] = {P[0], v1, M, 0, G(kWDir2), 256, B(kBDir2), nullptr, nullptr, {}, c[0]};
-    tb.p[tb.n++] = {P[1], feat, M, dirs ? 2 : 0, G(kWDir1), 283, B(kBDir1), nullptr, nullptr, a, c[1]};
-    tb.p[tb.n++] = {P[2], h2, M, 1, G(kWOut) + 512, 512, gc_feat, d_raw + 3, G(kWOut), {}, c[2]};
-    tb.p[tb.n++] = {P[3], h1, M, 0, G(kWXyz2), 512, gc_xyz2, nullptr, nullptr, {}, c[3]};
+    // with one code row the g_code entries summed here ARE the bias gradients of layer_xyz2, fc_out
+    // and fc_rgb (gcode_bias_kernel's column sums over one row): the reductions add each sum to both
+    // (bias2 / sig2), bitwise gcode_bias_kernel's 0 + g then b + that, and that launch is not needed
+    float* const b_xyz2 = dual_code ? G(kBXyz2) : nullptr;
+    float* const b_feat = dual_code ? G(kBOut) + 1 : nullptr;
+    tb.p[tb.n++] = {P[0], v1, M, 0, G(kWDir2), 256, B(kBDir2), nullptr, nullptr, {}, c[0], nullptr, nullptr};
+    tb.p[tb.n++] = {P[1], feat, M, dirs ? 2 : 0, G(kWDir1), 283, B(kBDir1), nullptr, nullptr, a, c[1], nullptr,
+                    nullptr};
+    tb.p[tb.n++] = {P[2], h2, M, 1, G(kWOut) + 512, 512, gc_feat, d_raw + 3, G(kWOut), {}, c[2], b_feat, nullptr};
+    tb.p[tb.n++] = {P[3], h1, M, 0, G(kWXyz2), 512, gc_xyz2, nullptr, nullptr, {}, c[3], b_xyz2, nullptr};
     if (rgb_role)
-      tb.p[tb.n++] = {d_raw, v2, M, 3, G(kWRgb), 512, g_code + kCbRgb, d_raw, g_code + kCbSigma, {}, c[4]};
+      tb.p[tb.n++] = {d_raw, v2, M, 3, G(kWRgb), 512, g_code + kCbRgb, d_raw, g_code + kCbSigma, {}, c[4],
+                      dual_code ? G(kBRgb) : nullptr, dual_code ? G(kBOut) : nullptr};
     CN_TRY(tn_batch_launch(tb, x3, st, &red));
     if (!dirs) {
       if (x_enc) CN_TRY(gemm_tn(P[1], 256, x_enc + 63, 90, G(kWDir1) + 256, 283, M, 256, 27, st, x3, ws, nullptr, nullptr, &red));
@@ -2736,7 +2788,7 @@ extern "C" int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, con
   if (x_enc) CN_TRY(gemm_tn(P[4], 256, x_enc, 90, G(kWXyz1), 63, M, 256, 63, st, x3, ws, B(kBXyz1), bws, &red));
   else CN_TRY(gemm_tn_enc(0, P[4], a, G(kWXyz1), 63, st, x3, ws, B(kBXyz1), bws, &red));
   CN_TRY(red.flush());
-  if (fold_code) {
+  if (fold_code && !dual_code) {
     hipLaunchKernelGGL(grad::gcode_bias_kernel, dim3(3), dim3(256), 0, st, g_code, n_codes, G(kBXyz2), G(kBOut),
                        G(kBRgb));
     CN_TRY(launch_status());

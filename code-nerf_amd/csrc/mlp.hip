@@ -72,95 +72,12 @@ __global__ void pack_kernel(Params P, float* __restrict__ packed) {
 }
 
 // ---------------------------------------------------------------- code bias
-// Per code row: the three code layers (model.py:174-177), then the code halves
-// of layer_xyz2 / fc_out / fc_rgb plus their biases.  Each code row is spread
-// over kCbSlices workgroups so the 1.5 MiB of weight rows are read by many CUs
-// at once (one CU per code was latency bound, ~85 us): slice q < 8 forms
-// xyz2 rows 32q..32q+31, slices 8..15 fc_out rows (slice 15 also row 256),
-// slice 16 the three fc_rgb rows.  Each slice first forms the one code-layer
-// vector it consumes (s1, s2 or t1; 256 dots, L2-resident weights after the
-// first slice touches them).  Every output is one wave-wide dot product: 64
-// lanes read a 256-float weight row as one coalesced float4 each, then a
-// butterfly sum.
-
-constexpr int kCbThreads = 512;
-constexpr int kCbSlices = 17;
-
-// The dot of a 256-float row with v as 64 lanes x float4 (w, x: this lane's quarter), summed by a
-// butterfly: every lane ends with the total.
-__device__ __forceinline__ float wave_dot4(float4 a, float4 b) {
-  float s = fmaf(a.x, b.x, fmaf(a.y, b.y, fmaf(a.z, b.z, a.w * b.w)));
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-  return s;
-}
+// (code_bias_block, mlp_common.h: one workgroup of kCbThreads per (code, slice))
 
 __global__ __launch_bounds__(kCbThreads) void code_bias_kernel(Params P, const float* __restrict__ z_s,
                                                                const float* __restrict__ z_t,
                                                                float* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) float z[kCode], hv[kCode];
-  const int64_t c = blockIdx.x / kCbSlices;
-  const int q = blockIdx.x % kCbSlices, t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  constexpr int kW = kCbThreads / 64;
-  const int l = q < 8 ? 0 : (q < 16 ? 1 : 2);  // 0: s1 -> xyz2, 1: s2 -> fc_out, 2: t1 -> fc_rgb
-  if (t < kCode) z[t] = (l == 2 ? z_t : z_s)[c * kCode + t];
-  __syncthreads();
-  {
-    // rows wave + 8 i: eight rows' loads in flight per round (no branch between them), the lane-0
-    // writes after; bias + ReLU once per output below
-    const float* W = P.p[l == 0 ? kWSc1 : (l == 1 ? kWSc2 : kWTc1)];
-    const float4 zv = reinterpret_cast<const float4*>(z)[lane];
-#pragma unroll
-    for (int i0 = 0; i0 < kCode / kW; i0 += 8) {
-      float4 wv[8];
-#pragma unroll
-      for (int x = 0; x < 8; ++x) wv[x] = reinterpret_cast<const float4*>(W + (wave + (i0 + x) * kW) * kCode)[lane];
-      float d[8];
-#pragma unroll
-      for (int x = 0; x < 8; ++x) d[x] = wave_dot4(wv[x], zv);
-      if (lane == 0)
-#pragma unroll
-        for (int x = 0; x < 8; ++x) hv[wave + (i0 + x) * kW] = d[x];
-    }
-  }
-  __syncthreads();
-  if (t < kCode) {
-    const float* B = P.p[l == 0 ? kBSc1 : (l == 1 ? kBSc2 : kBTc1)];
-    hv[t] = fmaxf(hv[t] + B[t], 0.f);
-  }
-  __syncthreads();
-  float* o = out + c * kCbStride;
-  int r0, nr;
-  if (l == 0) { r0 = 32 * q; nr = 32; }
-  else if (l == 1) { r0 = 32 * (q - 8); nr = q == 15 ? 33 : 32; }
-  else { r0 = 0; nr = 3; }
-  // at most 5 rows per wave (33 / 8): all their loads first, then the dots
-  const float4 hq = reinterpret_cast<const float4*>(hv)[lane];
-  float4 wv[5];
-  float bv[5];
-  int dst[5];
-#pragma unroll
-  for (int x = 0; x < 5; ++x) {
-    const int r = min(r0 + wave + x * kW, r0 + nr - 1);  // rows past the slice repeat its last (not stored)
-    const float* w;
-    if (l == 0) {
-      w = P.p[kWXyz2] + r * (kHidden + kCode) + kHidden; bv[x] = P.p[kBXyz2][r]; dst[x] = kCbXyz2 + r;
-    } else if (l == 1) {
-      // slice rows 0..255 map to fc_out rows 1..256 (feat); row 256 -> fc_out row 0 (sigma)
-      const int i = r == kCode ? 0 : r + 1;
-      w = P.p[kWOut] + i * (kHidden + kCode) + kHidden; bv[x] = P.p[kBOut][i];
-      dst[x] = i == 0 ? kCbSigma : kCbFeat + i - 1;
-    } else {
-      w = P.p[kWRgb] + r * (kHidden + kCode) + kHidden; bv[x] = P.p[kBRgb][r]; dst[x] = kCbRgb + r;
-    }
-    wv[x] = reinterpret_cast<const float4*>(w)[lane];
-  }
-#pragma unroll
-  for (int x = 0; x < 5; ++x) {
-    const float a = wave_dot4(wv[x], hq);
-    if (lane == 0 && wave + x * kW < nr) o[dst[x]] = a + bv[x];
-  }
-  if (l == 2 && t >= 3 && t < kCbStride - kCbRgb) o[kCbRgb + t] = 0.f;  // pad 516..519
+  code_bias_block(P, z_s, z_t, out, blockIdx.x);
 }
 
 // ---------------------------------------------------------------- field kernel
@@ -493,6 +410,17 @@ extern "C" int cn_code_bias(const float* const* params, const float* z_s, const 
   hipLaunchKernelGGL(code_bias_kernel, dim3(static_cast<unsigned>(n_codes * kCbSlices)), dim3(kCbThreads), 0,
                      cn::as_stream(stream), P, z_s, z_t, code_bias);
   return cn::launch_status();
+}
+
+extern "C" int cn_field_prepare(const float* const* params, const float* z_s, const float* z_t, int64_t n_codes,
+                                float* code_bias, float* packed, float* packed_t, float* zero, int64_t n_zero,
+                                cn_stream_t stream) {
+  Params P;
+  if (make_params(params, &P) != CN_OK) return CN_EINVAL;
+  CN_CHECK_ARG(n_zero >= 0 && (n_zero == 0 || zero));
+  CN_CHECK_ARG(!code_bias || (z_s && z_t && n_codes > 0 && n_codes * kCbSlices + 256 <= 0x7fffffff));
+  return launch_field_prepare_w16(P, z_s, z_t, n_codes, code_bias, packed, packed_t, zero, n_zero,
+                                  cn::as_stream(stream));
 }
 
 extern "C" int cn_mlp_forward(const float* packed, int fmt, const float* code_bias,

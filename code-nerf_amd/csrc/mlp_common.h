@@ -162,6 +162,99 @@ __device__ __forceinline__ void encode_pairs(const float* x, const float* f, int
   }
 }
 
+// ---------------------------------------------------------------- code bias (model.py:174-192)
+// Per code row: the three code layers (model.py:174-177), then the code halves
+// of layer_xyz2 / fc_out / fc_rgb plus their biases.  Each code row is spread
+// over kCbSlices workgroups so the 1.5 MiB of weight rows are read by many CUs
+// at once (one CU per code was latency bound, ~85 us): slice q < 8 forms
+// xyz2 rows 32q..32q+31, slices 8..15 fc_out rows (slice 15 also row 256),
+// slice 16 the three fc_rgb rows.  Each slice first forms the one code-layer
+// vector it consumes (s1, s2 or t1; 256 dots, L2-resident weights after the
+// first slice touches them).  Every output is one wave-wide dot product: 64
+// lanes read a 256-float weight row as one coalesced float4 each, then a
+// butterfly sum.
+
+constexpr int kCbThreads = 512;
+constexpr int kCbSlices = 17;
+
+// The dot of a 256-float row with v as 64 lanes x float4 (w, x: this lane's quarter), summed by a
+// butterfly: every lane ends with the total.
+__device__ __forceinline__ float wave_dot4(float4 a, float4 b) {
+  float s = fmaf(a.x, b.x, fmaf(a.y, b.y, fmaf(a.z, b.z, a.w * b.w)));
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  return s;
+}
+
+// Workgroup `blk` (= code * kCbSlices + slice) of the code-bias launch (cn_code_bias; also a role of
+// the one-launch step preparation, cn_field_prepare).
+__device__ __forceinline__ void code_bias_block(const Params& P, const float* __restrict__ z_s,
+                                                const float* __restrict__ z_t, float* __restrict__ out, int64_t blk) {
+  __shared__ __attribute__((aligned(16))) float z[kCode], hv[kCode];
+  const int64_t c = blk / kCbSlices;
+  const int q = static_cast<int>(blk % kCbSlices), t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  constexpr int kW = kCbThreads / 64;
+  const int l = q < 8 ? 0 : (q < 16 ? 1 : 2);  // 0: s1 -> xyz2, 1: s2 -> fc_out, 2: t1 -> fc_rgb
+  if (t < kCode) z[t] = (l == 2 ? z_t : z_s)[c * kCode + t];
+  __syncthreads();
+  {
+    // rows wave + 8 i: eight rows' loads in flight per round (no branch between them), the lane-0
+    // writes after; bias + ReLU once per output below
+    const float* W = P.p[l == 0 ? kWSc1 : (l == 1 ? kWSc2 : kWTc1)];
+    const float4 zv = reinterpret_cast<const float4*>(z)[lane];
+#pragma unroll
+    for (int i0 = 0; i0 < kCode / kW; i0 += 8) {
+      float4 wv[8];
+#pragma unroll
+      for (int x = 0; x < 8; ++x) wv[x] = reinterpret_cast<const float4*>(W + (wave + (i0 + x) * kW) * kCode)[lane];
+      float d[8];
+#pragma unroll
+      for (int x = 0; x < 8; ++x) d[x] = wave_dot4(wv[x], zv);
+      if (lane == 0)
+#pragma unroll
+        for (int x = 0; x < 8; ++x) hv[wave + (i0 + x) * kW] = d[x];
+    }
+  }
+  __syncthreads();
+  if (t < kCode) {
+    const float* B = P.p[l == 0 ? kBSc1 : (l == 1 ? kBSc2 : kBTc1)];
+    hv[t] = fmaxf(hv[t] + B[t], 0.f);
+  }
+  __syncthreads();
+  float* o = out + c * kCbStride;
+  int r0, nr;
+  if (l == 0) { r0 = 32 * q; nr = 32; }
+  else if (l == 1) { r0 = 32 * (q - 8); nr = q == 15 ? 33 : 32; }
+  else { r0 = 0; nr = 3; }
+  // at most 5 rows per wave (33 / 8): all their loads first, then the dots
+  const float4 hq = reinterpret_cast<const float4*>(hv)[lane];
+  float4 wv[5];
+  float bv[5];
+  int dst[5];
+#pragma unroll
+  for (int x = 0; x < 5; ++x) {
+    const int r = min(r0 + wave + x * kW, r0 + nr - 1);  // rows past the slice repeat its last (not stored)
+    const float* w;
+    if (l == 0) {
+      w = P.p[kWXyz2] + r * (kHidden + kCode) + kHidden; bv[x] = P.p[kBXyz2][r]; dst[x] = kCbXyz2 + r;
+    } else if (l == 1) {
+      // slice rows 0..255 map to fc_out rows 1..256 (feat); row 256 -> fc_out row 0 (sigma)
+      const int i = r == kCode ? 0 : r + 1;
+      w = P.p[kWOut] + i * (kHidden + kCode) + kHidden; bv[x] = P.p[kBOut][i];
+      dst[x] = i == 0 ? kCbSigma : kCbFeat + i - 1;
+    } else {
+      w = P.p[kWRgb] + r * (kHidden + kCode) + kHidden; bv[x] = P.p[kBRgb][r]; dst[x] = kCbRgb + r;
+    }
+    wv[x] = reinterpret_cast<const float4*>(w)[lane];
+  }
+#pragma unroll
+  for (int x = 0; x < 5; ++x) {
+    const float a = wave_dot4(wv[x], hq);
+    if (lane == 0 && wave + x * kW < nr) o[dst[x]] = a + bv[x];
+  }
+  if (l == 2 && t >= 3 && t < kCbStride - kCbRgb) o[kCbRgb + t] = 0.f;  // pad 516..519
+}
+
 // 3xbf16 variant (mlp_x3.hip): forward (optionally writing ReLU masks) and the
 // fused backward over the transposed pack.
 int64_t packed_floats_x3();
@@ -177,6 +270,9 @@ int launch_pack_w16(const Params& P, float* packed, hipStream_t st);
 int launch_field_w16(int mode, FieldArgs& a, hipStream_t st);  // a.masks: also the ReLU masks
 int64_t mask_words_w16(int64_t m);
 int launch_pack_w16t(const Params& P, float* packed, hipStream_t st);
+// code_bias + the CN_FMT_F32_W16 / _T packs + a zeroed buffer in one launch (any of them null: skipped)
+int launch_field_prepare_w16(const Params& P, const float* z_s, const float* z_t, int64_t n_codes, float* code_bias,
+                             float* packed, float* packed_t, float* zero, int64_t n_zero, hipStream_t st);
 int launch_field_w16_bwd(int mode, FieldArgs& a, hipStream_t st);
 // The training backwards' no-geometry schedule (no d ro / d rd / d pts wanted) unless CN_BWD_NOGEO=0.
 bool nogeo_enabled();

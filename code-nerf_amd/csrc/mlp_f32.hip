@@ -101,8 +101,10 @@ __host__ __device__ constexpr int col_enc_dir(int s, int g) {
 
 // ---------------------------------------------------------------- packing
 
-__global__ void pack_w16_kernel(Params P, float* __restrict__ packed) {
-  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < kPackedFloats; idx += gridDim.x * blockDim.x) {
+// Elements idx0, idx0 + stride, ... of the CN_FMT_F32_W16 pack (pack_w16_kernel; a role of
+// field_prepare_kernel).
+__device__ __forceinline__ void pack_w16_range(const Params& P, float* __restrict__ packed, int idx0, int stride) {
+  for (int idx = idx0; idx < kPackedFloats; idx += stride) {
     float v = 0.0f;
     if (idx >= kStreamFloats) {
       const int j = idx - kStreamFloats;
@@ -148,6 +150,10 @@ __global__ void pack_w16_kernel(Params P, float* __restrict__ packed) {
     }
     packed[idx] = v;
   }
+}
+
+__global__ void pack_w16_kernel(Params P, float* __restrict__ packed) {
+  pack_w16_range(P, packed, blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x);
 }
 
 // ---------------------------------------------------------------- kernel state
@@ -875,9 +881,11 @@ static_assert(kBwdLdsQuads * 16 <= 160 * 1024, "LDS budget (backward)");
 static_assert(kTXyz1 + 2 == kChunks, "backward chunk schedule");
 static_assert(kTDDir == kNoGeoSkip && kTDDir + 1 == kTOut, "no-geometry stream: skips the view-dir chunk");
 
-__global__ void pack_w16t_kernel(Params P, float* __restrict__ packed) {
+// Elements idx0, idx0 + stride, ... of the CN_FMT_F32_W16_T pack (pack_w16t_kernel; a role of
+// field_prepare_kernel).
+__device__ __forceinline__ void pack_w16t_range(const Params& P, float* __restrict__ packed, int idx0, int stride) {
   constexpr int kX2 = kHidden + kCode, kD1 = kCode + kDimDir;
-  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < kPackedFloats; idx += gridDim.x * blockDim.x) {
+  for (int idx = idx0; idx < kPackedFloats; idx += stride) {
     float v = 0.0f;
     if (idx >= kStreamFloats) {
       const int t = idx - kStreamFloats;
@@ -925,6 +933,54 @@ __global__ void pack_w16t_kernel(Params P, float* __restrict__ packed) {
     }
     packed[idx] = v;
   }
+}
+
+__global__ void pack_w16t_kernel(Params P, float* __restrict__ packed) {
+  pack_w16t_range(P, packed, blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x);
+}
+
+// What a training or eval step computes from the weights and codes before its field kernels, in ONE
+// launch (cn_field_prepare): the per-code terms (code_bias_block, blocks [0, nb_cb)), the forward and
+// backward packs (each over nb_pack blocks, grid-stride) and a zeroed buffer (the backward's g_code
+// accumulator; blocks after the packs).  Four launches per model and chunk before (code_bias,
+// pack_w16, pack_w16t, a torch fill); the roles write disjoint outputs from the same inputs.
+struct Prepare {
+  Params P;
+  const float* z_s;
+  const float* z_t;
+  float* code_bias;
+  float* packed;     // CN_FMT_F32_W16 or null
+  float* packed_t;   // CN_FMT_F32_W16_T or null
+  float* zero;
+  int64_t n_zero;
+  unsigned nb_cb, nb_pack, nb_zero;
+};
+constexpr int kPrepThreads = 512;
+static_assert(kPrepThreads == kCbThreads, "code_bias_block's workgroup size");
+
+__global__ __launch_bounds__(kPrepThreads) void field_prepare_kernel(Prepare p) {
+  unsigned b = blockIdx.x;
+  if (b < p.nb_cb) {
+    code_bias_block(p.P, p.z_s, p.z_t, p.code_bias, b);
+    return;
+  }
+  b -= p.nb_cb;
+  if (p.packed) {
+    if (b < p.nb_pack) {
+      pack_w16_range(p.P, p.packed, b * kPrepThreads + threadIdx.x, p.nb_pack * kPrepThreads);
+      return;
+    }
+    b -= p.nb_pack;
+  }
+  if (p.packed_t) {
+    if (b < p.nb_pack) {
+      pack_w16t_range(p.P, p.packed_t, b * kPrepThreads + threadIdx.x, p.nb_pack * kPrepThreads);
+      return;
+    }
+    b -= p.nb_pack;
+  }
+  for (int64_t i = (int64_t)b * kPrepThreads + threadIdx.x; i < p.n_zero; i += (int64_t)p.nb_zero * kPrepThreads)
+    p.zero[i] = 0.0f;
 }
 
 // Sum over each row of 16 lanes (the 16 samples of one lane group); lane 16 g + 15 holds it.
@@ -1449,6 +1505,18 @@ int launch_field_w16(int mode, FieldArgs& a, hipStream_t st) {
 }
 
 int64_t mask_words_w16(int64_t m) { return cn::ceil_div(m, w16::kTile) * w16::kMaskWordsPerTile; }
+
+int launch_field_prepare_w16(const Params& P, const float* z_s, const float* z_t, int64_t n_codes, float* code_bias,
+                             float* packed, float* packed_t, float* zero, int64_t n_zero, hipStream_t st) {
+  w16::Prepare p{P, z_s, z_t, code_bias, packed, packed_t, zero, n_zero, 0u, 0u, 0u};
+  p.nb_cb = code_bias ? static_cast<unsigned>(n_codes * kCbSlices) : 0u;
+  p.nb_pack = 64;  // 64 x 512 threads over each pack's 327,680 floats: 10 elements per thread
+  p.nb_zero = n_zero > 0 ? static_cast<unsigned>(std::min<int64_t>(cn::ceil_div(n_zero, w16::kPrepThreads), 64)) : 0u;
+  const unsigned grid = p.nb_cb + (packed ? p.nb_pack : 0u) + (packed_t ? p.nb_pack : 0u) + p.nb_zero;
+  if (grid == 0) return CN_OK;
+  hipLaunchKernelGGL(w16::field_prepare_kernel, dim3(grid), dim3(w16::kPrepThreads), 0, st, p);
+  return cn::launch_status();
+}
 
 int launch_pack_w16t(const Params& P, float* packed, hipStream_t st) {
   hipLaunchKernelGGL(w16::pack_w16t_kernel, dim3(cn::elementwise_grid(w16::kPackedFloats, 256)), dim3(256), 0, st, P,

@@ -198,6 +198,15 @@ int cn_mlp_pack(const float* const* params, int fmt, float* packed, cn_stream_t 
 int cn_code_bias(const float* const* params, const float* z_s, const float* z_t,
                  int64_t n_codes, float* code_bias, cn_stream_t stream);
 
+/* Everything a step needs from a model's weights and codes before its fp32 field kernels, in ONE
+ * launch (what the reference recomputes inside every CodeNeRFModel.forward, model.py:160-194):
+ * code_bias as cn_code_bias (NULL: skipped), packed / packed_t as cn_mlp_pack with CN_FMT_F32_W16
+ * / CN_FMT_F32_W16_T (each NULL: skipped), and zero[0 .. n_zero) set to 0 (the fused backward's
+ * g_code accumulator).  Bitwise the outputs of the separate calls. */
+int cn_field_prepare(const float* const* params, const float* z_s, const float* z_t, int64_t n_codes,
+                     float* code_bias, float* packed, float* packed_t, float* zero, int64_t n_zero,
+                     cn_stream_t stream);
+
 /* CodeNeRFModel.forward(z_s, z_t, x), model.py:160-194, for pre-encoded rows.
  * x: (m, 90) = [xyz 63 | dir 27]; code row of row i = code_index ? code_index[i]
  * : (n_codes == 1 ? 0 : i); raw: (m, 4) = [rgb_raw(3), sigma_raw]. */

@@ -543,12 +543,15 @@ def test_test_time_optimize_runs(dev):
 
 
 @pytest.mark.parametrize("precision", ["f32", "bf16x3"])
-@pytest.mark.parametrize("mode", ["rayz", "pts"])
-def test_field_backward_train_generated_encodings(dev, mode, precision):
+@pytest.mark.parametrize("mode,far", [("rayz", False), ("pts", False), ("pts", True), ("rayz", True)])
+def test_field_backward_train_generated_encodings(dev, mode, far, precision):
     """The fused training backward's encoding-layer dW (layer_xyz1, layer_dir1's view columns) with
     the encodings generated inside the dW kernel (x_enc None, the training path) matches the
     x_enc-plane GEMMs at GEMM_TOL; every other gradient is the same deterministic computation and
-    must agree bit for bit.  Run twice: the generated path is bitwise reproducible."""
+    must agree bit for bit.  Run twice: the generated path is bitwise reproducible.  ``far``: samples
+    past fast_sincosf's argument bound (pts: ONE sample of one 16-sample wave -- a mixed wave, which
+    the fp32 forward and its dW kernel evaluate with sincosf throughout; rayz: one far ray), so both
+    per-stage choices of the dW kernel run."""
     from codenerf import ops, synthetic
     m = model(dev, 0)
     params = [p.detach() for p in m.param_list()]
@@ -557,7 +560,11 @@ def test_field_backward_train_generated_encodings(dev, mode, precision):
     ro = (torch.randn(r, 3, generator=g) * 0.3 + torch.tensor([0.0, 0.0, 1.3])).to(dev)
     rd = torch.randn(r, 3, generator=g).to(dev)
     z = torch.sort(0.8 + torch.rand(r, s, generator=g), dim=-1).values.to(dev)
+    if far and mode == "rayz":
+        ro[37] = torch.tensor([45.0, -38.0, 41.0], device=dev)
     pts = (ro[:, None, :] + rd[:, None, :] * z[..., None]).contiguous() if mode == "pts" else None
+    if far and mode == "pts":
+        pts[37, 5] = torch.tensor([45.0, -38.0, 41.0], device=dev)
     geo = dict(pts=pts) if mode == "pts" else dict(ro=ro, z=z)
     gout = torch.randn(r, s, 4, generator=g).to(dev)
     zs, zt = synthetic.latent_codes(5, 1).to(dev), synthetic.latent_codes(6, 1).to(dev)
@@ -755,3 +762,23 @@ def test_code_bias_backward_two_launch_bitwise(dev, n_codes, want_grads):
                 # near 0.5): two orders differ by up to n_codes ulps, whatever the gradient's scale
                 err = (x.double() - y.double()).abs().max().item()
                 assert err <= n_codes * 2.0 ** -23, f"param {k}: max err {err:.3e}"
+
+
+@pytest.mark.parametrize("n_codes", [1, 5])
+@pytest.mark.parametrize("pack,pack_t", [(True, True), (False, True), (False, False)])
+def test_field_prepare_bitwise(dev, n_codes, pack, pack_t):
+    """cn_field_prepare (the fp32 training step's one pre-field launch per model: code terms, both packs,
+    a zeroed g_code) equals the separate cn_code_bias / cn_mlp_pack calls bit for bit."""
+    from codenerf import ops, synthetic
+    m = model(dev, 2)
+    params = [p.detach() for p in m.param_list()]
+    zs, zt = synthetic.latent_codes(7, n_codes).to(dev), synthetic.latent_codes(8, n_codes).to(dev)
+    nz = n_codes * 520 + 3
+    cb, pk, pkt, zero = ops.field_prepare(params, zs, zt, pack=pack, pack_t=pack_t, n_zero=nz)
+    assert torch.equal(cb, ops.code_bias(params, zs, zt))
+    assert (pk is None) == (not pack) and (pkt is None) == (not pack_t)
+    if pack:
+        assert torch.equal(pk, ops.mlp_pack(params, "f32_w16"))
+    if pack_t:
+        assert torch.equal(pkt, ops.mlp_pack(params, "f32_w16_t"))
+    assert zero.shape == (nz,) and not zero.any()

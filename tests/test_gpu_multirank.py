@@ -300,6 +300,7 @@ def test_validate_two_ranks_q6(tmp_path):
     iterations match to rounding); (3) rank 0's loss / psnr / pose error are finite and the loss is
     the gathered image's MSE."""
     import numpy as np
+    sys.path.insert(0, os.path.join(HERE, "golden"))
     from srn_tree import write_tree
     from codenerf.evaluate import _pose_lr, test_time_optimize
     from codenerf.nerf import render_rays
