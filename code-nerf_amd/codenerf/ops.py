@@ -396,6 +396,8 @@ def volume_render_backward(raw: Tensor, z: Tensor, rd: Tensor, g_rgb=None, g_dis
     g_weights = _opt(g_weights, "g_weights")
     d_raw = torch.empty_like(raw)
     d_rd = torch.empty_like(rd) if want_rd else None
+    if n == 0:      # no rays: empty gradients (the C ABI refuses n_rays == 0), as the forward
+        return d_raw, d_rd
     check(lib.cn_volume_render_backward(ptr(raw), ptr(z), ptr(rd), n, s, ptr(g_rgb), ptr(g_disp), ptr(g_acc),
                                         ptr(g_weights), ptr(g_depth), ptr(d_raw), ptr(d_rd), stream_of(raw)),
           "cn_volume_render_backward")
@@ -447,6 +449,8 @@ def radiance_field_train(packed: Tensor, cb: Tensor, rd: Tensor, n_samples: int,
         code_index = _cuda(code_index, "code_index", torch.int64)
     raw = torch.empty(n, n_samples, 4, device=rd.device, dtype=torch.float32)
     saved = torch.empty(5, n * n_samples, 256, device=rd.device, dtype=torch.float32)
+    if n * n_samples == 0:
+        return raw, saved
     check(lib.cn_radiance_field_train(ptr(packed), ptr(cb), ptr(code_index), cb.shape[0], ptr(pts), ptr(ro), ptr(rd),
                                       ptr(z), n, n_samples, chunk_rows, _lib.host_floats(freqs_xyz),
                                       _lib.host_floats(freqs_dir), ptr(raw), ptr(saved), stream_of(rd)),
@@ -475,6 +479,9 @@ def radiance_field_train_w16(packed: Tensor, cb: Tensor, rd: Tensor, n_samples: 
         code_index = _cuda(code_index, "code_index", torch.int64)
     m = n * n_samples
     raw = torch.empty(n, n_samples, 4, device=rd.device, dtype=torch.float32)
+    if m == 0:
+        return (raw, torch.empty(5, 0, 256, device=rd.device, dtype=torch.float32),
+                torch.empty(0, device=rd.device, dtype=torch.int32))
     # the planes + one scratch row (cn_radiance_field_train_fmt)
     saved = torch.empty(5 * m * 256 + 256, device=rd.device, dtype=torch.float32)[:5 * m * 256].view(5, m, 256)
     masks = torch.empty(int(lib.cn_field_mask_words_fmt(fmt, m)), device=rd.device, dtype=torch.int32)
@@ -506,7 +513,7 @@ def field_backward_train(packed_t: Tensor, params: Sequence[Tensor], masks: Tens
     rd, pts, ro, z = _opt(rd, "rd"), _opt(pts, "pts"), _opt(ro, "ro"), _opt(z, "z")
     if code_index is not None:
         code_index = _cuda(code_index, "code_index", torch.int64)
-    ws = torch.empty(int(lib.cn_field_backward_train_workspace_floats(m)), device=dev, dtype=torch.float32)
+    ws = torch.empty(max(0, int(lib.cn_field_backward_train_workspace_floats(m))), device=dev, dtype=torch.float32)
     if g_code is None:
         g_code = torch.zeros(n_codes, _lib.CN_CODE_BIAS_STRIDE, device=dev, dtype=torch.float32)
     else:
@@ -514,6 +521,8 @@ def field_backward_train(packed_t: Tensor, params: Sequence[Tensor], masks: Tens
     d_pts = torch.empty(n_rays, n_samples, 3, device=dev, dtype=torch.float32) if want_pts else None
     d_ro = torch.zeros(n_rays, 3, device=dev, dtype=torch.float32) if want_ro else None
     d_rd = torch.zeros(n_rays, 3, device=dev, dtype=torch.float32) if want_rd else None
+    if m == 0:      # no samples: nothing accumulates (the C ABI refuses n_rays == 0)
+        return {"g_code": g_code, "d_pts": d_pts, "d_ro": d_ro, "d_rd": d_rd}
     arr, keep = _lib.pointer_array(params)
     garr, gkeep = (None, None)
     if param_grads is not None:
@@ -553,6 +562,8 @@ def encode_inputs(rd: Tensor, n_samples: int, chunk_rows: int, freqs_xyz: Sequen
     n = rd.shape[0]
     pts, ro, z = _opt(pts, "pts"), _opt(ro, "ro"), _opt(z, "z")
     x = torch.empty(n * n_samples, 90, device=rd.device, dtype=torch.float32)
+    if n * n_samples == 0:
+        return x
     check(lib.cn_encode_inputs(ptr(pts), ptr(ro), ptr(rd), ptr(z), n, n_samples, chunk_rows,
                                _lib.host_floats(freqs_xyz), _lib.host_floats(freqs_dir), ptr(x), stream_of(rd)),
           "cn_encode_inputs")
@@ -580,12 +591,17 @@ def field_backward(params: Sequence[Tensor], saved: Tensor, x_enc: Tensor, d_raw
     rd, pts, ro, z = _opt(rd, "rd"), _opt(pts, "pts"), _opt(ro, "ro"), _opt(z, "z")
     if code_index is not None:
         code_index = _cuda(code_index, "code_index", torch.int64)
-    ws = torch.empty(int(lib.cn_field_backward_workspace_floats(m)), device=dev, dtype=torch.float32)
+    ws = torch.empty(max(0, int(lib.cn_field_backward_workspace_floats(m))), device=dev, dtype=torch.float32)
     out = {}
     g_code = torch.zeros(n_codes, _lib.CN_CODE_BIAS_STRIDE, device=dev, dtype=torch.float32) if want_code else None
     d_pts = torch.empty(n_rays, n_samples, 3, device=dev, dtype=torch.float32) if want_pts else None
     d_ro = torch.zeros(n_rays, 3, device=dev, dtype=torch.float32) if want_ro else None
     d_rd = torch.zeros(n_rays, 3, device=dev, dtype=torch.float32) if want_rd else None
+    if m == 0:      # no samples: zero sums (the C ABI refuses n_rays == 0)
+        out.update(g_code=g_code, d_pts=d_pts, d_ro=d_ro, d_rd=d_rd)
+        if want_x:
+            out["d_x"] = torch.empty(0, 90, device=dev, dtype=torch.float32)
+        return out
     arr, keep = _lib.pointer_array(params)
     garr, gkeep = (None, None)
     if param_grads is not None:
@@ -719,6 +735,8 @@ def radiance_field_masks(packed: Tensor, cb: Tensor, rd: Tensor, n_samples: int,
         code_index = _cuda(code_index, "code_index", torch.int64)
     m = n * n_samples
     raw = torch.empty(n, n_samples, 4, device=rd.device, dtype=torch.float32)
+    if m == 0:
+        return raw, torch.empty(0, device=rd.device, dtype=torch.int32)
     masks = torch.empty(int(lib.cn_field_mask_words_fmt(fmt, m)), device=rd.device, dtype=torch.int32)
     check(lib.cn_radiance_field_masks_fmt(fmt, ptr(packed), ptr(cb), ptr(code_index), cb.shape[0], ptr(pts), ptr(ro),
                                           ptr(rd), ptr(z), n, n_samples, chunk_rows, _lib.host_floats(freqs_xyz),
@@ -756,6 +774,8 @@ def field_backward_x3(packed_t: Tensor, masks: Tensor, d_raw: Tensor, n_rays: in
     d_ro = acc[nc:nc + 3 * n_rays].view(n_rays, 3) if want_ro else None
     d_rd = acc[acc.numel() - 3 * n_rays:].view(n_rays, 3) if want_rd else None
     d_pts = torch.empty(n_rays, n_samples, 3, device=dev, dtype=torch.float32) if want_pts else None
+    if m == 0:      # no samples: zero sums (the C ABI refuses n_rays == 0)
+        return {"g_code": g_code, "d_pts": d_pts, "d_ro": d_ro, "d_rd": d_rd}
     check(lib.cn_field_backward_fused(fmt_t, ptr(packed_t), ptr(masks), ptr(d_raw), ptr(pts), ptr(ro), ptr(rd),
                                       ptr(z), n_rays, n_samples, chunk_rows, ptr(code_index), n_codes,
                                       _lib.host_floats(freqs_xyz), _lib.host_floats(freqs_dir), ptr(g_code),

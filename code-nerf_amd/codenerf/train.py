@@ -292,7 +292,7 @@ def _validation_summary(res: Dict[str, object], iteration: int) -> Dict[str, obj
 
 
 def train(rank: int, cfg, device=None, resident: bool = True, stop_after: Optional[int] = None,
-          verbose: bool = True, keep_logs: Optional[int] = 1000, keep_validation: bool = False) -> Dict[str, object]:
+          verbose: bool = True, keep_logs: Optional[int] = None, keep_validation: bool = False) -> Dict[str, object]:
     """train.py:19-142 on the gfx950 path, with the reference's seeds, data order and cadence.
 
     * seed ``(rank + 1) + experiment.randomseed`` for numpy and torch (train.py:29-31);
@@ -318,10 +318,11 @@ def train(rank: int, cfg, device=None, resident: bool = True, stop_after: Option
     chunksize <= num_random_rays), see DESIGN.md section 4.  A reference checkpoint resumes with
     the reference's semantics (``iter`` again, fresh RNG and scheduler).
 
-    Memory: the per-chunk logs are read back in batches and only the last ``keep_logs`` kept
-    (LogBook); a validation keeps its host scalars (``keep_validation``: also its history, codes and
-    image).  Returns {"logs": host-float dicts (the last ``keep_logs``), "num_logs", "checkpoints":
-    paths, "validation": summaries, "models", "optimizer", "scheduler"}."""
+    Memory: the per-chunk logs are read back in batches; ``keep_logs`` (None, the library default:
+    all) caps how many of the last ones are kept (LogBook; the command line keeps 1000); a validation
+    keeps its host scalars (``keep_validation``: also its history, codes and image).  Returns {"logs":
+    host-float dicts, "num_logs", "first_log_index" (the chunk index of logs[0]: 0 unless capped),
+    "checkpoints": paths, "validation": summaries, "models", "optimizer", "scheduler"}."""
     import time
     from . import checkpoint as C
     from .datasets import prepare_dataloader
@@ -392,6 +393,7 @@ def train(rank: int, cfg, device=None, resident: bool = True, stop_after: Option
                         start_chunk=resume_chunk, after_draw=after_draw)
     out["logs"] = book.as_list()
     out["num_logs"] = book.count
+    out["first_log_index"] = book.count - len(out["logs"])
     return out
 
 
@@ -433,7 +435,7 @@ def launch(fn, cfg, backend: Optional[str] = None, port: int = 29500, init_metho
 
 
 def _train_rank(rank: int, cfg) -> None:
-    train(rank, cfg)
+    train(rank, cfg, keep_logs=1000)     # the command line: a long run keeps the last 1000 chunk logs
 
 
 def main(cfg, backend: Optional[str] = None, port: int = 29500) -> None:

@@ -351,3 +351,47 @@ def test_validate_two_ranks_q6(tmp_path):
     assert np.isfinite([got[0]["loss"], got[0]["psnr"], got[0]["pose_error"]]).all()
     mse = ((got[0]["rgb"].double() - got[0]["color"].reshape(-1, 4)[:, :3].double()) ** 2).mean().item()
     assert abs(got[0]["loss"] - mse) <= 1e-6 * max(1.0, mse)
+
+
+def _train_driver_worker(rank, world, port, tree, out_dir, tag, ckpt):
+    import torch.distributed as dist
+    from codenerf.train import train
+    from test_gpu_drivers import _cfg
+    dev = _init(rank, world, port)
+    try:
+        cfg = _cfg(tree, os.path.join(out_dir, tag), iterations=6, save_every=4, validate_every=1000)
+        cfg.nerf.train.chunksize = 64                    # 128 rays per image -> 2 chunks per iteration
+        cfg.is_distributed, cfg.gpus = True, world
+        if ckpt:
+            cfg = cfg | {"load_checkpoint": ckpt}
+        out = train(rank, cfg, device=dev, verbose=False)
+        torch.save({"params": {f"{k}.{n}": p.detach().cpu() for k, m in out["models"].items()
+                               for n, p in m.named_parameters()},
+                    "logs": torch.tensor([[lg[k] for k in sorted(lg)] for lg in out["logs"]], dtype=torch.float64),
+                    "ckpts": list(out["checkpoints"])}, os.path.join(out_dir, f"{tag}{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_train_driver_two_ranks_mid_iteration_resume(tmp_path):
+    """codenerf.train.train on 2 ranks: a save after chunk 0 of iteration 2 (i = 4; the
+    driver gathers every rank's RNG streams into it with all_gather_object), then both ranks resume
+    from it -- each restores its own streams and the cursor -- and must end with the uninterrupted
+    2-rank run's parameters and chunk logs, bit for bit, on both ranks."""
+    sys.path.insert(0, os.path.join(HERE, "golden"))
+    from srn_tree import write_tree
+    tree = write_tree(str(tmp_path / "srn"), channels=4)
+    _spawn(_train_driver_worker, 2, tree, str(tmp_path), "full", "")
+    full = [torch.load(str(tmp_path / f"full{r}.pt"), weights_only=True) for r in range(2)]
+    ck = [p for p in full[0]["ckpts"] if p.endswith("    4.ckpt")]
+    assert ck, full[0]["ckpts"]
+    _spawn(_train_driver_worker, 2, tree, str(tmp_path), "res", ck[0])
+    res = [torch.load(str(tmp_path / f"res{r}.pt"), weights_only=True) for r in range(2)]
+    n_after = res[0]["logs"].shape[0]
+    assert n_after == full[0]["logs"].shape[0] - 5            # chunks 5.. of 12
+    for r in range(2):
+        assert torch.equal(res[r]["logs"], full[r]["logs"][5:]), r
+        for k, v in full[r]["params"].items():
+            assert torch.equal(res[r]["params"][k], v), (r, k)
+    for k, v in full[0]["params"].items():
+        assert torch.equal(full[1]["params"][k], v), ("ranks differ", k)

@@ -255,6 +255,32 @@ def test_leaf_ops_empty_batch(dev):
     assert ops.ray_points(e3.to(dev), e3.to(dev), e64.to(dev)).shape == (0, 64, 3)
 
 
+@pytest.mark.parametrize("precision", ["f32", "bf16x3"])
+def test_zero_ray_batch_backward(dev, precision):
+    """A zero-ray batch through the differentiable path -- volume_render and the fused field forward /
+    backward of both precisions, training (weights with gradients) and eval (frozen) -- returns empty
+    or zero gradients instead of the C ABI's CN_EINVAL."""
+    from codenerf.nerf import forward_pass, volume_render
+    mdl, = models(dev, (0,), precision)
+    mdl.train_precision = precision
+    for frozen in (False, True):
+        mdl.requires_grad_(not frozen)
+        rd = torch.empty(0, 3, device=dev, requires_grad=True)
+        pts = torch.empty(0, 64, 3, device=dev, requires_grad=True)
+        zs = torch.randn(1, 256, device=dev).expand(0, -1).requires_grad_(True)
+        zt = torch.randn(1, 256, device=dev).expand(0, -1).requires_grad_(True)
+        raw = forward_pass(mdl, embedders(dev), rd, pts, (zs, zt))
+        assert raw.shape == (0, 64, 4)
+        z = torch.empty(0, 64, device=dev)
+        rgb, disp, acc, w, depth = volume_render(raw, z, rd)
+        (rgb.sum() + disp.sum() + acc.sum() + depth.sum()).backward()
+        assert pts.grad is None or pts.grad.shape == (0, 64, 3)
+        if not frozen:
+            assert all(p.grad is None or not p.grad.any() for p in mdl.parameters())
+            mdl.zero_grad()
+    mdl.requires_grad_(True)
+
+
 def test_volume_render_unaligned_inputs(dev):
     """raw / z as contiguous views at an odd element offset: the C ABI refuses them (CN_EINVAL, no
     launch: its 16-B vector accesses need aligned rows), the Python op realigns them and returns the
