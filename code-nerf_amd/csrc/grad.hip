@@ -1092,6 +1092,69 @@ __device__ __forceinline__ void ring_read8(const float* p, float* v) {
       : "memory");
 }
 
+// The second half of the DIRS fold (gemm_tn256_kernel): workgroup w of this kernel takes direction
+// groups kDirGroups w .. + kDirGroups - 1; per group it adds the gsum slots of the tn256 workgroups
+// whose unit runs cover it (in workgroup order), evaluates the 16 directions' encodings with
+// gemm_tn_enc_kernel's arithmetic (PositionalEmbedder order: raw 0..2, then per frequency sin 3,
+// cos 3) and accumulates thread n's row of dW: part[w][n][k] = sum_d dsum[d][n] enc(d)[k], k < 27;
+// the bias (enc 1) into bias_part[w][n].  Fixed order throughout: deterministic.
+constexpr int kDirGroups = 1;
+// Workgroup blk of that launch; threads 0..255 work (a 512-thread caller's upper half only takes
+// part in the barriers: the role rides in gemm_tn_enc_kernel's launch).
+__device__ __forceinline__ void dir_enc_dw_block(const mlp::FieldArgs& a, const DirFold& dir, float* __restrict__ part,
+                                                 float* __restrict__ bias_part, unsigned blk) {
+  __shared__ float encl[16][28];
+  const int n = threadIdx.x;
+  const bool act = n < 256;
+  const unsigned S = dir.n_samples, U = dir.units_per_block, n_groups = dir.n_rays / 16;
+  float acc[28];
+#pragma unroll
+  for (int k = 0; k < 28; ++k) acc[k] = 0.0f;
+  for (int q = 0; q < kDirGroups; ++q) {
+    const unsigned g = blk * kDirGroups + q;
+    if (g >= n_groups) break;
+    float ds[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) ds[r] = 0.0f;
+    const unsigned b0 = g * S / U, b1 = ((g + 1) * S - 1) / U;
+    if (act) {
+      for (unsigned b = b0; b <= b1; ++b) {
+        const float* gs = dir.gsum + (int64_t)(b + g) * 4096 + n;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) ds[r] += gs[r * 256];
+      }
+    }
+    __syncthreads();  // the previous group's encodings are read
+    if (n < 16 * 12) {
+      const int r = n / 12, p = n - 12 * (n / 12), comp = p % 3, c0 = 3 + 6 * (p / 3) + comp;
+      float vd[3];
+      mlp::view_dir(a, 16 * (int64_t)g + r, vd);
+      float s, c;
+      mlp::enc_sincosf(__fmul_rn(mlp::pick3(vd, comp), a.fd[p / 3]), s, c);
+      encl[r][c0] = s;
+      encl[r][c0 + 3] = c;
+    } else if (n < 16 * 13) {
+      const int r = n - 16 * 12;
+      float vd[3];
+      mlp::view_dir(a, 16 * (int64_t)g + r, vd);
+      encl[r][0] = vd[0];
+      encl[r][1] = vd[1];
+      encl[r][2] = vd[2];
+      encl[r][27] = 1.0f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+#pragma unroll
+      for (int k = 0; k < 28; ++k) acc[k] = fmaf(ds[r], encl[r][k], acc[k]);
+  }
+  if (!act) return;
+  float* pt = part + (int64_t)blk * 256 * 27 + n * 27;
+#pragma unroll
+  for (int k = 0; k < 27; ++k) pt[k] = acc[k];
+  bias_part[(int64_t)blk * 256 + n] = acc[27];
+}
+
 // Lane-varying selects on the bits (a ternary chain on a lane-varying index becomes EXEC-masked
 // branches, which would split the MFMA / VALU interleave below into blocks).
 struct LazyPick {
@@ -1104,11 +1167,26 @@ struct LazyPick {
   }
 };
 
+// The DIRS fold's second half as a role of this launch (gemm_tn_enc_kernel's first n workgroups run
+// dir_enc_dw_block instead of a separate 256-workgroup launch): both only need the batched dW launch's
+// outputs (gsum / dPre planes), and their partials go to the same deferred reduction.
+struct DirRole {
+  DirFold dir;
+  float* part;
+  float* bias_part;
+  unsigned n;  // workgroups of the role (0: none)
+};
+
 template <bool X3, int ENC, int MODE>
 __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __restrict__ A, mlp::FieldArgs a,
                                                              float* __restrict__ C, int64_t ldc,
                                                              float* __restrict__ part, float* __restrict__ bias_part,
-                                                             int64_t rows_per_block) {
+                                                             int64_t rows_per_block, DirRole dr) {
+  if (blockIdx.x < dr.n) {
+    dir_enc_dw_block(a, dr.dir, dr.part, dr.bias_part, blockIdx.x);
+    return;
+  }
+  const unsigned blk = blockIdx.x - dr.n;
   constexpr int K = ENC == 0 ? 63 : 27, KB = ENC == 0 ? 2 : 1, EW = 32 * KB;
   // row strides (floats) of the A ring and the encoding table: the two rows a wave's half-waves
   // read together (fp32: rows 2 p and 2 p + 1; x3: rows j and 8 + j) sit 32 banks apart -- with
@@ -1123,7 +1201,7 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __rest
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int i = lane & 31, h = lane >> 5;
   const int64_t M = a.m;
-  const int64_t mb = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t mb = (int64_t)blk * rows_per_block;
   const int64_t rows = min(rows_per_block, M - mb);
   const int n_stages = static_cast<int>((rows + kEncRows - 1) / kEncRows);
   // the slab's A rows as a buffer resource: rows past it (the last stage's tail, the stages the
@@ -1385,70 +1463,18 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __rest
   }
   // the stages prefetched past the slab must land before the workgroup's LDS is released
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  float* pt = part ? part + (int64_t)blockIdx.x * 256 * K : nullptr;
+  float* pt = part ? part + (int64_t)blk * 256 * K : nullptr;
 #pragma unroll
   for (int u = 0; u < KB; ++u) flush_block(acc[u], C, ldc, pt, 256, K, 32 * wave, 32 * u, i, h);
   if (bias_part) {
     const float b = bsum + __shfl_xor(bsum, 32);
-    if (h == 0) bias_part[(int64_t)blockIdx.x * 256 + 32 * wave + i] = b;
+    if (h == 0) bias_part[(int64_t)blk * 256 + 32 * wave + i] = b;
   }
 }
 
-// The second half of the DIRS fold (gemm_tn256_kernel): workgroup w of this kernel takes direction
-// groups kDirGroups w .. + kDirGroups - 1; per group it adds the gsum slots of the tn256 workgroups
-// whose unit runs cover it (in workgroup order), evaluates the 16 directions' encodings with
-// gemm_tn_enc_kernel's arithmetic (PositionalEmbedder order: raw 0..2, then per frequency sin 3,
-// cos 3) and accumulates thread n's row of dW: part[w][n][k] = sum_d dsum[d][n] enc(d)[k], k < 27;
-// the bias (enc 1) into bias_part[w][n].  Fixed order throughout: deterministic.
-constexpr int kDirGroups = 1;
 __global__ __launch_bounds__(256) void dir_enc_dw_kernel(mlp::FieldArgs a, DirFold dir, float* __restrict__ part,
                                                          float* __restrict__ bias_part) {
-  __shared__ float encl[16][28];
-  const int n = threadIdx.x;
-  const unsigned S = dir.n_samples, U = dir.units_per_block, n_groups = dir.n_rays / 16;
-  float acc[28];
-#pragma unroll
-  for (int k = 0; k < 28; ++k) acc[k] = 0.0f;
-  for (int q = 0; q < kDirGroups; ++q) {
-    const unsigned g = blockIdx.x * kDirGroups + q;
-    if (g >= n_groups) break;
-    float ds[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) ds[r] = 0.0f;
-    const unsigned b0 = g * S / U, b1 = ((g + 1) * S - 1) / U;
-    for (unsigned b = b0; b <= b1; ++b) {
-      const float* gs = dir.gsum + (int64_t)(b + g) * 4096 + n;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) ds[r] += gs[r * 256];
-    }
-    __syncthreads();  // the previous group's encodings are read
-    if (n < 16 * 12) {
-      const int r = n / 12, p = n - 12 * (n / 12), comp = p % 3, c0 = 3 + 6 * (p / 3) + comp;
-      float vd[3];
-      mlp::view_dir(a, 16 * (int64_t)g + r, vd);
-      float s, c;
-      mlp::enc_sincosf(__fmul_rn(mlp::pick3(vd, comp), a.fd[p / 3]), s, c);
-      encl[r][c0] = s;
-      encl[r][c0 + 3] = c;
-    } else if (n < 16 * 13) {
-      const int r = n - 16 * 12;
-      float vd[3];
-      mlp::view_dir(a, 16 * (int64_t)g + r, vd);
-      encl[r][0] = vd[0];
-      encl[r][1] = vd[1];
-      encl[r][2] = vd[2];
-      encl[r][27] = 1.0f;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 16; ++r)
-#pragma unroll
-      for (int k = 0; k < 28; ++k) acc[k] = fmaf(ds[r], encl[r][k], acc[k]);
-  }
-  float* pt = part + (int64_t)blockIdx.x * 256 * 27 + n * 27;
-#pragma unroll
-  for (int k = 0; k < 27; ++k) pt[k] = acc[k];
-  bias_part[(int64_t)blockIdx.x * 256 + n] = acc[27];
+  dir_enc_dw_block(a, dir, part, bias_part, blockIdx.x);
 }
 
 // Deterministic column sums (bias gradients dPre^T 1) where no dW kernel folds them in:
@@ -2187,7 +2213,8 @@ int64_t enc_rows(int64_t M) {
 int64_t enc_parts(int64_t M) { return ceil_div(M, enc_rows(M)); }
 
 int gemm_tn_enc(int enc, const float* A, const mlp::FieldArgs& a, float* C, int64_t ldc, hipStream_t st, bool x3,
-                float* ws, float* bias = nullptr, float* bias_ws = nullptr, Reducer* rd = nullptr) {
+                float* ws, float* bias = nullptr, float* bias_ws = nullptr, Reducer* rd = nullptr,
+                grad::DirRole dr = {}) {
   const int64_t rows = enc_rows(a.m);
   const unsigned nb = static_cast<unsigned>(ceil_div(a.m, rows));
   const int K = enc == 0 ? 63 : 27;
@@ -2196,8 +2223,8 @@ int gemm_tn_enc(int enc, const float* A, const mlp::FieldArgs& a, float* C, int6
     if (bias) bias_ws = rd->take((int64_t)nb * 256);
   }
 #define CN_ENC(X3_, E_, M_) \
-  hipLaunchKernelGGL((grad::gemm_tn_enc_kernel<X3_, E_, M_>), dim3(nb), dim3(512), 0, st, A, a, C, ldc, ws, \
-                     bias ? bias_ws : nullptr, rows)
+  hipLaunchKernelGGL((grad::gemm_tn_enc_kernel<X3_, E_, M_>), dim3(nb + dr.n), dim3(512), 0, st, A, a, C, ldc, ws, \
+                     bias ? bias_ws : nullptr, rows, dr)
   const bool pts = a.pts != nullptr;
   if (x3) {
     if (enc == 0) { if (pts) CN_ENC(true, 0, mlp::kFromPts); else CN_ENC(true, 0, mlp::kFromRayZ); }
@@ -2565,6 +2592,15 @@ struct TnBatch {
   int n = 0;
 };
 
+// CN_DIR_IN_ENC=0: the DIRS fold's dir_enc_dw pass as its own launch again (A/B; bitwise the same)
+static bool dir_in_enc_enabled() {
+  static const int on = [] {
+    const char* e = getenv("CN_DIR_IN_ENC");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return on != 0;
+}
+
 static bool tn_jobs_enabled() {
   static const int on = [] {
     const char* e = getenv("CN_TN_JOBS");
@@ -2597,7 +2633,9 @@ static bool dirs_foldable(const mlp::FieldArgs& a) {
          a.m >= 64 * 1024;
 }
 
-static int tn_batch_launch(TnBatch& b, bool x3, hipStream_t st, Reducer* rd) {
+// dir_out: when set, the DIRS fold's dir_enc_dw work is not launched here but returned as a role
+// for the next gemm_tn_enc launch (its partials' reductions are queued here either way).
+static int tn_batch_launch(TnBatch& b, bool x3, hipStream_t st, Reducer* rd, grad::DirRole* dir_out = nullptr) {
   if (b.n == 0) return CN_OK;
   double total = 0.0;
   for (int k = 0; k < b.n; ++k) total += b.p[k].cost * static_cast<double>(b.p[k].M);
@@ -2654,8 +2692,13 @@ static int tn_batch_launch(TnBatch& b, bool x3, hipStream_t st, Reducer* rd) {
       const int64_t groups = q.a.n_rays / 16, nd = ceil_div(groups, grad::kDirGroups);
       float* ep = rd->take(nd * 256 * 27);
       float* bp = rd->take(nd * 256);
-      hipLaunchKernelGGL(grad::dir_enc_dw_kernel, dim3(static_cast<unsigned>(nd)), dim3(256), 0, st, q.a, j.dir, ep, bp);
-      CN_TRY(launch_status());
+      if (dir_out) {
+        *dir_out = grad::DirRole{j.dir, ep, bp, static_cast<unsigned>(nd)};
+      } else {
+        hipLaunchKernelGGL(grad::dir_enc_dw_kernel, dim3(static_cast<unsigned>(nd)), dim3(256), 0, st, q.a, j.dir, ep,
+                           bp);
+        CN_TRY(launch_status());
+      }
       CN_TRY(reduce(rd, j.part, j.n_blocks, 256, 256, q.C, q.ldc, st));
       CN_TRY(reduce(rd, ep, nd, 256, 27, q.C + 256, q.ldc, st));
       CN_TRY(reduce(rd, bp, nd, 1, 256, q.bias, 256, st));
@@ -2791,6 +2834,7 @@ extern "C" int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, con
   const float* v1 = saved + 3 * M * 256;
   const float* v2 = saved + 4 * M * 256;
   const bool jobs = tn_jobs_enabled() && M >= 64 * 1024;
+  grad::DirRole dir_role = {};
   // fc_rgb (h half): dW += d rgb^T v2 (+ g_code's rgb / sigma entries, folded, in the same pass); as
   // the batched launch's RGB role where that runs (fp32, folded code)
   const bool rgb_role = jobs && fold_code && !x3;
@@ -2821,7 +2865,9 @@ extern "C" int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, con
     if (rgb_role)
       tb.p[tb.n++] = {d_raw, v2, M, 3, G(kWRgb), 512, g_code + kCbRgb, d_raw, g_code + kCbSigma, {}, c[4],
                       dual_code ? G(kBRgb) : nullptr, dual_code ? G(kBOut) : nullptr};
-    CN_TRY(tn_batch_launch(tb, x3, st, &red));
+    // the DIRS fold's per-direction pass rides in layer_xyz1's encoding dW launch (below) when that
+    // is a gemm_tn_enc launch: one launch fewer per field and chunk
+    CN_TRY(tn_batch_launch(tb, x3, st, &red, dirs && !x_enc && dir_in_enc_enabled() ? &dir_role : nullptr));
     if (!dirs) {
       if (x_enc) CN_TRY(gemm_tn(P[1], 256, x_enc + 63, 90, G(kWDir1) + 256, 283, M, 256, 27, st, x3, ws, nullptr, nullptr, &red));
       else CN_TRY(gemm_tn_enc(1, P[1], a, G(kWDir1) + 256, 283, st, x3, ws, nullptr, nullptr, &red));
@@ -2849,7 +2895,7 @@ extern "C" int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, con
   // layer_xyz1 (its own launch: as a role of the batched launch it ran no faster per CU -- it is
   // compute work, not a bandwidth pass that could hide beside the GEMMs; r03m)
   if (x_enc) CN_TRY(gemm_tn(P[4], 256, x_enc, 90, G(kWXyz1), 63, M, 256, 63, st, x3, ws, B(kBXyz1), bws, &red));
-  else CN_TRY(gemm_tn_enc(0, P[4], a, G(kWXyz1), 63, st, x3, ws, B(kBXyz1), bws, &red));
+  else CN_TRY(gemm_tn_enc(0, P[4], a, G(kWXyz1), 63, st, x3, ws, B(kBXyz1), bws, &red, dir_role));
   CN_TRY(red.flush());
   if (fold_code && !dual_code) {
     hipLaunchKernelGGL(grad::gcode_bias_kernel, dim3(3), dim3(256), 0, st, g_code, n_codes, G(kBXyz2), G(kBOut),

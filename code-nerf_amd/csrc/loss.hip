@@ -31,7 +31,9 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
 // Large code tensors (train: the whole embedding tables, 2 x 2458 x 256): per-block partial sums
 // of squares (double) into partials[2 b], [2 b + 1]; the loss kernel adds them up.
 constexpr int kPartThreads = 256;
-constexpr int64_t kPartElems = 8192;  // code values per partial block
+// code values per partial block: 1024 (4 per thread, one float4 each) -- 615 blocks for the C3
+// tables instead of 77 blocks looping 32 times (11 -> ~3 us; the loss kernel adds the partials)
+constexpr int64_t kPartElems = 1024;
 
 __global__ __launch_bounds__(kPartThreads) void code_sq_partials_kernel(const float* __restrict__ zs,
                                                                         const float* __restrict__ zt, int64_t n_code,
@@ -39,9 +41,18 @@ __global__ __launch_bounds__(kPartThreads) void code_sq_partials_kernel(const fl
   __shared__ double red[2][kPartThreads / 64];
   double ss = 0.0, st = 0.0;
   const int64_t b0 = blockIdx.x * kPartElems, b1 = min(b0 + kPartElems, n_code);
-  for (int64_t i = b0 + threadIdx.x; i < b1; i += kPartThreads) {
-    ss += static_cast<double>(zs[i]) * zs[i];
-    st += static_cast<double>(zt[i]) * zt[i];
+  // all of a thread's loads first, then the products (four values per thread)
+  float vs[kPartElems / kPartThreads], vt[kPartElems / kPartThreads];
+#pragma unroll
+  for (int k = 0; k < kPartElems / kPartThreads; ++k) {
+    const int64_t i = b0 + threadIdx.x + k * kPartThreads;
+    vs[k] = i < b1 ? zs[i] : 0.0f;
+    vt[k] = i < b1 ? zt[i] : 0.0f;
+  }
+#pragma unroll
+  for (int k = 0; k < kPartElems / kPartThreads; ++k) {
+    ss += static_cast<double>(vs[k]) * vs[k];
+    st += static_cast<double>(vt[k]) * vt[k];
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -77,16 +88,27 @@ __global__ __launch_bounds__(kThreads) void render_loss_kernel(const float* __re
   __shared__ double red[kThreads / 64];
   double sc = 0.0, sf = 0.0, ss = 0.0, st = 0.0;
   const int64_t n = n_rays * 3;
-  for (int64_t i = threadIdx.x; i < n; i += kThreads) {
-    const int64_t r = i / 3, c = i - 3 * r;
-    const float t = target[r * ldt + c];
-    if (rgb_c) {
-      const float d = rgb_c[i] - t;
-      sc += static_cast<double>(d) * d;
+  // four elements per thread and round, their loads issued together (one at a time the 12 rounds of
+  // a 4096-ray chunk were 12 serial memory latencies); the same per-thread summation order
+  constexpr int kU = 4;
+  for (int64_t i0 = threadIdx.x; i0 < n; i0 += kU * kThreads) {
+    float t[kU], c[kU], f[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t i = i0 + u * kThreads;
+      const bool ok = i < n;
+      const int64_t ii = ok ? i : 0;
+      const int64_t r = ii / 3, cc = ii - 3 * r;
+      t[u] = target[r * ldt + cc];
+      c[u] = rgb_c ? rgb_c[ii] : 0.0f;
+      f[u] = rgb_f ? rgb_f[ii] : 0.0f;
+      if (!ok) t[u] = c[u] = f[u] = 0.0f;
     }
-    if (rgb_f) {
-      const float d = rgb_f[i] - t;
-      sf += static_cast<double>(d) * d;
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const float dc = c[u] - t[u], df = f[u] - t[u];
+      if (rgb_c) sc += static_cast<double>(dc) * dc;
+      if (rgb_f) sf += static_cast<double>(df) * df;
     }
   }
   if (n_part > 0) {
