@@ -256,6 +256,9 @@ class RadianceField(torch.autograd.Function):
         ctx.owner = params[0]
         params = [p.detach() for p in params]
         n_rays = rd.shape[0]
+        ctx.empty = n_rays == 0 or z_s.shape[0] == 0
+        if ctx.empty:      # a zero-ray batch: empty raw, and no gradient flows back (backward)
+            return torch.empty(n_rays, meta.n_samples, 4, device=rd.device, dtype=torch.float32)
         fused = (meta.precision in ("bf16x3", "f32") and not any(ctx.needs_input_grad[7:])
                  and ops.fused_backward_supported(z_s.shape[0], meta.n_samples, meta.code_index, meta.precision))
         ctx.fused = fused
@@ -304,6 +307,8 @@ class RadianceField(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_raw):
+        if ctx.empty:
+            return (None,) * len(ctx.needs_input_grad)
         rd, pts, ro, z, z_s, z_t, *params = ctx.saved_tensors
         needs = ctx.needs_input_grad
         meta = ctx.meta

@@ -1155,18 +1155,6 @@ __device__ __forceinline__ void dir_enc_dw_block(const mlp::FieldArgs& a, const 
   bias_part[(int64_t)blk * 256 + n] = acc[27];
 }
 
-// Lane-varying selects on the bits (a ternary chain on a lane-varying index becomes EXEC-masked
-// branches, which would split the MFMA / VALU interleave below into blocks).
-struct LazyPick {
-  static __device__ __forceinline__ float bsel(bool c, float a, float b) {
-    const int m = -static_cast<int>(c);
-    return __int_as_float((__float_as_int(a) & m) | (__float_as_int(b) & ~m));
-  }
-  static __device__ __forceinline__ float sel3(float v0, float v1, float v2, int c) {
-    return bsel(c == 0, v0, bsel(c == 1, v1, v2));
-  }
-};
-
 // The DIRS fold's second half as a role of this launch (gemm_tn_enc_kernel's first n workgroups run
 // dir_enc_dw_block instead of a separate 256-workgroup launch): both only need the batched dW launch's
 // outputs (gsum / dPre planes), and their partials go to the same deferred reduction.
@@ -1376,59 +1364,9 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __rest
     decode(st + 3);
     dma(st + 2);  // always (past the slab: zeros), so every wave's vmcnt above stays exact
     const bool more = st + 1 < n_stages;
-#if defined(CN_ENC_INTERLEAVE)
-    // ENC 0, fp32, every point of the next stage inside fast_sincosf's bound (the flag is
-    // stage-uniform): the next stage's encodings branch-free between this stage's MFMAs (2-3 VALU per
-    // MFMA) instead of a VALU block before them -- in this loop the VALU otherwise adds to the matrix
-    // time
-    constexpr bool kInter = ENC == 0 && !X3;
-    const bool inter = kInter && more && xfast[(st + 1) % 3];
-#else
-    constexpr bool kInter = false;
-    const bool inter = false;
-#endif
-#if defined(CN_ENC_STAGGER)
-    const bool late = wave >= 4;   // waves 4-7 (the SIMD partners of 0-3) form the encodings after their MFMAs
-#else
-    const bool late = false;
-#endif
-    if (more && !inter && !late) enc_of(st + 1);
+    if (more) enc_of(st + 1);
     const float* sa = ring[st % kEncRing];
     const float* se = senc[st & 1];
-    if constexpr (kInter) {
-      if (inter) {
-        float xa[8], xb[KB][8];
-        ring_read8<2 * RS * 4>(sa + h * RS + 32 * wave + i, xa);
-#pragma unroll
-        for (int u = 0; u < KB; ++u) ring_read8<2 * ES * 4>(se + h * ES + 32 * u + i, xb[u]);
-        const float4 x4 = xs[(st + 1) % 3][es];
-        const float xc = LazyPick::sel3(x4.x, x4.y, x4.z, comp);
-        const float arg = __fmul_rn(xc, freq);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int p = 0; p < kEncRows / 2; ++p) {
-          const float x = xa[p];
-          bsum += x;
-#pragma unroll
-          for (int u = 0; u < KB; ++u) acc[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(x, xb[u][p], acc[u], 0, 0, 0);
-        }
-        float sn, cs;
-        mlp::fast_sincosf(arg, sn, cs);
-        // kind 1: the pair; kind 2: raw inputs comp, comp + 1 (or zero padding); kind 0: unused
-        const float r0 = comp < 3 ? LazyPick::sel3(x4.x, x4.y, x4.z, comp) : 0.0f;
-        const float r1 = comp + 1 < 3 ? LazyPick::sel3(x4.x, x4.y, x4.z, comp + 1) : 0.0f;
-        ev[0] = LazyPick::bsel(kind == 1, sn, r0);
-        ev[1] = LazyPick::bsel(kind == 1, cs, r1);
-#pragma unroll
-        for (int m = 0; m < 16; ++m) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
-          __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);   // VALU
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        store_enc((st + 1) & 1);
-        continue;
-      }
-    }
     if constexpr (X3) {
       float v[8];
       ring_read8<RS * 4>(sa + (8 * h) * RS + 32 * wave + i, v);   // rows 8 h + j
@@ -1458,7 +1396,6 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __rest
         for (int u = 0; u < KB; ++u) acc[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(x, xb[u][p], acc[u], 0, 0, 0);
       }
     }
-    if (more && late) enc_of(st + 1);
     if (more) store_enc((st + 1) & 1);
   }
   // the stages prefetched past the slab must land before the workgroup's LDS is released

@@ -234,7 +234,7 @@ def test_bench_gather_views_multi_rank(tmp_path, world):
     margin(f"bench_multi_rank_n{world}[f32]", "multi_rank_maxdiff", res["multi_rank_maxdiff"], 0.0)
 
 
-def _eval_setup(cfg, dev, rank):
+def _eval_setup(cfg, dev, rank, intrinsic=None):
     """eval.py:41-79 as codenerf.evaluate.eval_loop runs it: seeds, loaders, models, the optimiser's
     broadcast of rank 0's parameters (no checkpoint here), samplers and embedders."""
     from codenerf import nerf
@@ -247,8 +247,10 @@ def _eval_setup(cfg, dev, rank):
     prepare_optimizer(cfg, models)
     first = next(iter(loader))
     (h, w), k = first["color"][0].shape[:2], first["intrinsic"][0]
+    if intrinsic is not None:        # the single-process emulation: the ranks' samplers (eval.py:66-76)
+        k = intrinsic
     samplers = nerf.prepare_samplers(cfg, h, w, k.cpu(), torch.float32, dev)
-    return loader, models, samplers, nerf.prepare_embedders(cfg, torch.float32, dev)
+    return loader, models, samplers, nerf.prepare_embedders(cfg, torch.float32, dev), k.cpu()
 
 
 def _eval_cfg(tree, logdir, world):
@@ -266,7 +268,7 @@ def _eval_worker(rank, world, port, tree, out_dir):
     dev = _init(rank, world, port)
     try:
         cfg = _eval_cfg(tree, os.path.join(out_dir, "e"), world)
-        loader, models, samplers, embedders = _eval_setup(cfg, dev, rank)
+        loader, models, samplers, embedders, k = _eval_setup(cfg, dev, rank)
         val = next(iter(loader))
         val = {"color": val["color"].clone(), "pose": val["pose"].clone()}
         if rank == 1:       # a different view on rank 1: validate must broadcast rank 0's (eval.py:111-115)
@@ -277,7 +279,8 @@ def _eval_worker(rank, world, port, tree, out_dir):
                "np_hg": st["np"][3], "np_g": st["np"][4],
                "cpu_rng": st["cpu"], "cuda_rng": st["cuda"].cpu(), "zs": res["codes"][0].cpu(),
                "zt": res["codes"][1].cpu(), "cam_pose": res["cam_pose"].cpu(),
-               "losses": torch.tensor([h["total_loss"] for h in res["history"]], dtype=torch.float64)}
+               "losses": torch.tensor([h["total_loss"] for h in res["history"]], dtype=torch.float64),
+               "intrinsic": k}    # this rank's samplers' (its own first batch's, eval.py:66-76)
         if rank == 0:
             out.update(rgb=res["rgb"].cpu(), loss=res["loss"], psnr=res["psnr"], pose_error=res["pose_error"],
                        color=val["color"].cpu(), gt_pose=val["pose"].cpu(),
@@ -293,7 +296,8 @@ def test_validate_two_ranks_q6(tmp_path):
     """eval.py:82-205 on two ranks (C5's multi-GPU eval): rank 0's view broadcast, every rank
     optimising codes and pose on its own ray draws (seed (r + 1) + randomseed), then
     parallel_image_render (nerf/__init__.py:137-226) with each rank rendering its Q5 slice from ITS OWN
-    pose and codes.  Checked against a single process: (1) each rank's slice, rendered from that rank's
+    pose and codes (and, as eval.py:66-76 builds them, its own samplers from its own first validation
+    batch).  Checked against a single process: (1) each rank's slice, rendered from that rank's
     optimised pose and codes, equals rank 0's gathered rows bit for bit; (2) re-running each rank's
     test_time_optimize from its recorded RNG state reproduces its first loss bit for bit and its pose
     and codes to 1e-5 (the eval backward's per-code and per-ray sums are float atomics, so later
@@ -310,7 +314,8 @@ def test_validate_two_ranks_q6(tmp_path):
     got = [torch.load(str(tmp_path / f"eval{r}.pt"), weights_only=True) for r in range(2)]
     dev = torch.device("cuda", 0)
     cfg = _eval_cfg(tree, str(tmp_path / "single"), 1)
-    _, models, (rs, ps), emb = _eval_setup(cfg, dev, 0)
+    from codenerf import nerf
+    _, models, _, emb, _ = _eval_setup(cfg, dev, 0)
     state = got[0]["state"]
     for k, m in models.items():
         m.load_state_dict({n[len(k) + 1:]: v for n, v in state.items() if n.startswith(k + ".")})
@@ -324,6 +329,8 @@ def test_validate_two_ranks_q6(tmp_path):
     per, _ = split_sizes(target.shape[0], 2)
     for r in range(2):
         g = got[r]
+        h, w = got[0]["color"].shape[1:3]
+        rs, ps = nerf.prepare_samplers(cfg, h, w, g["intrinsic"], torch.float32, dev)
         np.random.set_state(("MT19937", g["np_keys"].numpy().astype(np.uint32), int(g["np_pos"]), int(g["np_hg"]),
                              float(g["np_g"])))
         torch.set_rng_state(g["cpu_rng"])
