@@ -60,6 +60,7 @@ SIGNATURES = {
     "cn_mlp_pack": (_i, [ctypes.POINTER(_p), _i, _p, _p]),
     "cn_code_bias": (_i, [ctypes.POINTER(_p), _p, _p, _i64, _p, _p]),
     "cn_field_prepare": (_i, [ctypes.POINTER(_p), _p, _p, _i64, _p, _p, _p, _p, _i64, _p]),
+    "cn_field_train_saved_floats": (_i64, [_i, _i64]),
     "cn_mlp_forward": (_i, [_p, _i, _p, _p, _i64, _p, _i64, _p, _p]),
     "cn_radiance_field": (_i, [_p, _i, _p, _p, _i64, _p, _p, _p, _p, _i64, _i64, _i64, _fp, _fp, _p, _p]),
     "cn_radiance_field_train": (_i, [_p, _p, _p, _i64, _p, _p, _p, _p, _i64, _i64, _i64, _fp, _fp, _p, _p, _p]),

@@ -326,6 +326,21 @@ def field_prepare(params: Sequence[Tensor], z_s: Tensor, z_t: Tensor, pack: bool
     return cb, packed, packed_t, zero
 
 
+def xenc_columns():
+    """The fp32 training forward's encoding plane (cn_field_train_saved_floats): column c' (0..63) ->
+    PositionalEmbedder column (position_embed.py:44-53), -1 for the padding slot (mlp_common.h
+    xenc_col: lane group g = c' // 16 holds layer_xyz1's k-steps t = c' % 16)."""
+    out = []
+    for cp in range(64):
+        t, g = cp & 15, cp >> 4
+        i, p = t & 7, 4 * (t & 7) + g
+        if p < 30:
+            out.append((3 if t < 8 else 6) + 6 * (p // 3) + p % 3)
+        else:
+            out.append((0 if g == 2 else 2) if t < 8 else (1 if g == 2 else -1))
+    return out
+
+
 def mlp_forward(packed: Tensor, cb: Tensor, x: Tensor, code_index: Optional[Tensor] = None,
                 precision: str = "f32") -> Tensor:
     """CodeNeRFModel.forward on pre-encoded rows (model.py:160-194): (M, 90) -> (M, 4)."""
@@ -482,8 +497,10 @@ def radiance_field_train_w16(packed: Tensor, cb: Tensor, rd: Tensor, n_samples: 
     if m == 0:
         return (raw, torch.empty(5, 0, 256, device=rd.device, dtype=torch.float32),
                 torch.empty(0, device=rd.device, dtype=torch.int32))
-    # the planes + one scratch row (cn_radiance_field_train_fmt)
-    saved = torch.empty(5 * m * 256 + 256, device=rd.device, dtype=torch.float32)[:5 * m * 256].view(5, m, 256)
+    # the planes (+ fp32: the encoding plane) + one scratch row (cn_radiance_field_train_fmt); ``saved`` is
+    # the (5, m, 256) planes view, the backward finds the encoding plane after them in the same storage
+    buf = torch.empty(int(lib.cn_field_train_saved_floats(fmt, m)), device=rd.device, dtype=torch.float32)
+    saved = buf[:5 * m * 256].view(5, m, 256)
     masks = torch.empty(int(lib.cn_field_mask_words_fmt(fmt, m)), device=rd.device, dtype=torch.int32)
     check(lib.cn_radiance_field_train_fmt(fmt, ptr(packed), ptr(cb), ptr(code_index), cb.shape[0], ptr(pts), ptr(ro),
                                           ptr(rd), ptr(z), n, n_samples, chunk_rows, _lib.host_floats(freqs_xyz),

@@ -1409,6 +1409,95 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __rest
   }
 }
 
+// layer_xyz1's dW from the encodings the fp32 training forward multiplied (its (M, 64) encoding plane,
+// cn_radiance_field_train_fmt): C[n][xenc_col(c')] = sum_m A[m][n] X[m][c'], and the bias column
+// sums of A.  Both operands move by LDS-DMA into 3-slot rings, two 16-row stages ahead: A's rows
+// as 1 KiB dwordx4 pieces, X's 256-B rows as dword pieces (each wave two of each per stage), so the
+// loop is one counted vmcnt + barrier, the ring reads and the MFMAs -- no geometry decode and no
+// sin / cos per stage (gemm_tn_enc_kernel's VALU, which in this loop adds to the matrix time), and
+// the encodings are exactly the forward's (lazy fast_sincosf or ocml sincosf, per wave).
+// Wave w: output rows 32 w .. + 31, both 32-column blocks (c' 0..63); fp32 32x32x2.
+constexpr int kXRS = 288, kXES = 96;   // LDS row strides (floats): 32 banks between a pair's rows
+__global__ __launch_bounds__(512, 1) void gemm_tn_xenc_kernel(const float* __restrict__ A, const float* __restrict__ X,
+                                                              int64_t M, float* __restrict__ part,
+                                                              float* __restrict__ bias_part, int64_t rows_per_block,
+                                                              mlp::FieldArgs a, DirRole dr) {
+  if (blockIdx.x < dr.n) {
+    dir_enc_dw_block(a, dr.dir, dr.part, dr.bias_part, blockIdx.x);
+    return;
+  }
+  const unsigned blk = blockIdx.x - dr.n;
+  __shared__ __attribute__((aligned(16))) float ring[kEncRing][kEncRows * kXRS];
+  __shared__ __attribute__((aligned(16))) float xring[kEncRing][kEncRows * kXES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int i = lane & 31, h = lane >> 5;
+  const int64_t mb = (int64_t)blk * rows_per_block;
+  const int64_t rows = min(rows_per_block, M - mb);
+  const int n_stages = static_cast<int>((rows + kEncRows - 1) / kEncRows);
+  // the slab's rows as buffer resources: rows past it (the tail, the stages prefetched past the end)
+  // read as zeros
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(A + mb * 256), 0, static_cast<unsigned>(rows * 256 * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(X + mb * 64), 0, static_cast<unsigned>(rows * 64 * 4), 0x00020000);
+  // stage st: wave w moves A rows w, w + 8 and X rows w, w + 8 (4 vector-memory ops per wave)
+  auto dma = [&](int st) {
+    float* slot = ring[st % kEncRing];
+    float* xslot = xring[st % kEncRing];
+#pragma unroll
+    for (int j = 0; j < kEncRows / 8; ++j) {
+      const int r = wave + 8 * j;
+      const unsigned soff = __builtin_amdgcn_readfirstlane(static_cast<unsigned>((st * kEncRows + r) * 1024));
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(slot + r * kXRS), 16, lane * 16u, soff, 0, 0);
+      const unsigned xoff = __builtin_amdgcn_readfirstlane(static_cast<unsigned>((st * kEncRows + r) * 256));
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_t)(xslot + r * kXES), 4, lane * 4u, xoff, 0, 0);
+    }
+  };
+  floatx16 acc[2] = {floatx16{0}, floatx16{0}};
+  float bsum = 0.0f;  // column sums of A (feature 32 wave + i) over this lane's rows
+  dma(0);
+  dma(1);
+  for (int st = 0; st < n_stages; ++st) {
+    // stage st landed for every wave (all but this wave's 4 youngest vector-memory ops -- stage
+    // st+1's -- retired), every wave is past stage st-1 (its ring slots are free)
+    static_assert(kEncRows / 8 == 2, "the vmcnt below counts one stage of pieces");
+    asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    dma(st + 2);  // always (past the slab: zeros), so every wave's vmcnt above stays exact
+    const float* sa = ring[st % kEncRing];
+    const float* sx = xring[st % kEncRing];
+    float xa[8], xb[2][8];
+    ring_read8<2 * kXRS * 4>(sa + h * kXRS + 32 * wave + i, xa);   // rows 2 p + h
+#pragma unroll
+    for (int u = 0; u < 2; ++u) ring_read8<2 * kXES * 4>(sx + h * kXES + 32 * u + i, xb[u]);
+#pragma unroll
+    for (int p = 0; p < kEncRows / 2; ++p) {
+      const float x = xa[p];
+      bsum += x;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) acc[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(x, xb[u][p], acc[u], 0, 0, 0);
+    }
+  }
+  // the stages prefetched past the slab must land before the workgroup's LDS is released
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // the partial tile in PositionalEmbedder column order (part: (256, 63) per workgroup)
+  float* pt = part + (int64_t)blk * 256 * 63;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int col = mlp::xenc_col(32 * u + i);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (col >= 0) pt[(int64_t)row * 63 + col] = acc[u][r];
+    }
+  }
+  if (bias_part) {
+    const float b = bsum + __shfl_xor(bsum, 32);
+    if (h == 0) bias_part[(int64_t)blk * 256 + 32 * wave + i] = b;
+  }
+}
+
 __global__ __launch_bounds__(256) void dir_enc_dw_kernel(mlp::FieldArgs a, DirFold dir, float* __restrict__ part,
                                                          float* __restrict__ bias_part) {
   dir_enc_dw_block(a, dir, part, bias_part, blockIdx.x);
@@ -2181,6 +2270,22 @@ int gemm_tn_enc(int enc, const float* A, const mlp::FieldArgs& a, float* C, int6
   return CN_OK;
 }
 
+// layer_xyz1's dW (+ bias) from the fp32 training forward's encoding plane (gemm_tn_xenc_kernel), with the
+// DIRS fold's per-direction role riding in the same launch (dr); partials through the reducer.
+int gemm_tn_xenc(const float* A, const float* X, const mlp::FieldArgs& a, float* C, int64_t ldc, hipStream_t st,
+                 float* bias, Reducer* rd, grad::DirRole dr) {
+  const int64_t rows = enc_rows(a.m);
+  const unsigned nb = static_cast<unsigned>(ceil_div(a.m, rows));
+  float* ws = rd->take((int64_t)nb * 256 * 63);
+  float* bws = bias ? rd->take((int64_t)nb * 256) : nullptr;
+  hipLaunchKernelGGL(grad::gemm_tn_xenc_kernel, dim3(nb + dr.n), dim3(512), 0, st, A, X, a.m, ws, bws, rows, a, dr);
+  int rc = launch_status();
+  if (rc != CN_OK) return rc;
+  rc = reduce(rd, ws, nb, 256, 63, C, ldc, st);
+  if (rc != CN_OK) return rc;
+  return bias ? reduce(rd, bws, nb, 1, 256, bias, 256, st) : CN_OK;
+}
+
 int seg_sum(const float* A, int64_t lda, int64_t M, int N, int64_t S, const int64_t* code_index, int64_t n_codes,
             float* out, int64_t out_ld, hipStream_t st) {
   dim3 grid(static_cast<unsigned>(ceil_div(M, grad::kSegRows)), static_cast<unsigned>(ceil_div(N, 64)));
@@ -2529,6 +2634,16 @@ struct TnBatch {
   int n = 0;
 };
 
+// CN_XENC_PLANE=0: layer_xyz1's dW regenerates the encodings (gemm_tn_enc_kernel) instead of reading the
+// forward's encoding plane (A/B)
+static bool xenc_plane_enabled() {
+  static const int on = [] {
+    const char* e = getenv("CN_XENC_PLANE");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return on != 0;
+}
+
 // CN_DIR_IN_ENC=0: the DIRS fold's dir_enc_dw pass as its own launch again (A/B; bitwise the same)
 static bool dir_in_enc_enabled() {
   static const int on = [] {
@@ -2832,6 +2947,8 @@ extern "C" int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, con
   // layer_xyz1 (its own launch: as a role of the batched launch it ran no faster per CU -- it is
   // compute work, not a bandwidth pass that could hide beside the GEMMs; r03m)
   if (x_enc) CN_TRY(gemm_tn(P[4], 256, x_enc, 90, G(kWXyz1), 63, M, 256, 63, st, x3, ws, B(kBXyz1), bws, &red));
+  else if (!x3 && xenc_plane_enabled())   // the fp32 forward's own encodings (saved's encoding plane)
+    CN_TRY(gemm_tn_xenc(P[4], saved + 5 * M * 256, a, G(kWXyz1), 63, st, B(kBXyz1), &red, dir_role));
   else CN_TRY(gemm_tn_enc(0, P[4], a, G(kWXyz1), 63, st, x3, ws, B(kBXyz1), bws, &red, dir_role));
   CN_TRY(red.flush());
   if (fold_code && !dual_code) {

@@ -612,8 +612,16 @@ extern "C" int cn_radiance_field_train_fmt(int fmt, const float* packed, const f
   CN_CHECK_ARG(cn::aligned16(raw));  // float4 rows (include/codenerf.h)
   a.save = save;
   a.masks = masks;
+  // fp32: the encoding plane follows the five activation planes (cn_field_train_saved_floats)
+  if (fmt == CN_FMT_F32_W16) a.xenc = save + 5 * a.m * 256;
   return fmt == CN_FMT_BF16X3 ? launch_field_x3(pts ? kFromPts : kFromRayZ, a, cn::as_stream(stream))
                               : launch_field_w16(pts ? kFromPts : kFromRayZ, a, cn::as_stream(stream));
+}
+
+extern "C" int64_t cn_field_train_saved_floats(int fmt, int64_t m) {
+  if (m <= 0 || !(fmt == CN_FMT_F32_W16 || fmt == CN_FMT_BF16X3)) return -1;
+  // five (m, 256) activation planes; fp32: then the (m, 64) encoding plane; a 256-float scratch row
+  return 5 * m * 256 + (fmt == CN_FMT_F32_W16 ? 64 * m : 0) + 256;
 }
 
 extern "C" int cn_field_backward_x3(const float* packed_t, const uint32_t* masks, const float* d_raw,

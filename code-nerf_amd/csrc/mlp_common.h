@@ -45,7 +45,18 @@ struct FieldArgs {
   float* d_ro;           // backward: (n_rays, 3) accumulated (kFromRayZ)
   float* d_rd;           // backward: (n_rays, 3) accumulated
   float* dpre;           // fp32 fused training backward: (5, m, 256) masked layer-input gradients
+  float* xenc;           // fp32 training forward: (m, 64) the positional encodings it multiplied (xenc_col)
 };
+
+// Column c' of the fp32 training forward's encoding plane (64 floats per sample: lane group g's 16
+// k-step values of layer_xyz1 at 16 g + t) -> PositionalEmbedder column (position_embed.py:44-53:
+// x_d -> d, sin(f_k x_d) -> 3 + 6k + d, cos -> 6 + 6k + d), or -1 for the padding slot; the field
+// kernel's feature map for layer_xyz1's k-steps (mlp_f32.hip col_enc_xyz).
+__host__ __device__ constexpr int xenc_col(int cp) {
+  const int t = cp & 15, g = cp >> 4, i = t & 7, p = 4 * i + g;
+  if (p < 30) return (t < 8 ? 3 : 6) + 6 * (p / 3) + p % 3;
+  return t < 8 ? (g == 2 ? 0 : 2) : (g == 2 ? 1 : -1);
+}
 
 // v[i] for a lane-varying i in 0..2 by selects: an indexed read of a private array would
 // place the whole array (and the struct holding it) in scratch memory.

@@ -71,6 +71,10 @@ constexpr int kCFreq = kConsts, kLdsConsts = kConsts + 16;
 constexpr int kLdsQuads = kRing * kChunkQuads + (kLdsConsts + kWaves * kCbStride) / 4;
 
 static_assert(kChunks % kRing == 0, "cyclic stream: chunk c + 36 reuses chunk c's ring slot");
+__host__ __device__ constexpr int col_enc_xyz(int t, int g);
+constexpr bool xenc_map_ok(int cp = 0) {
+  return cp == 64 || (xenc_col(cp) == col_enc_xyz(cp & 15, cp >> 4) && xenc_map_ok(cp + 1));
+}
 static_assert(kPiecesPerWave == 4, "4 DMA wave-instructions per chunk per wave");
 static_assert(kLdsQuads * 16 <= 160 * 1024, "LDS budget");
 
@@ -88,6 +92,8 @@ __host__ __device__ constexpr int col_enc_xyz(int t, int g) {
   if (p < 30) return (t < 8 ? 3 : 6) + 6 * (p / 3) + p % 3;
   return t < 8 ? (g == 2 ? 0 : 2) : (g == 2 ? 1 : -1);
 }
+
+static_assert(xenc_map_ok(), "the encoding plane's column map is layer_xyz1's k-step feature map");
 
 // View-direction encoding column (27 wide) at k-step s (0..6) of the view-dir chunk:
 // sines of pairs p = 4i + g at s = i (i < 3), cosines at s = 3 + i, raw component g at s = 6.
@@ -302,6 +308,8 @@ __device__ __forceinline__ void lazy_step_pattern() {
 struct NoPost {
   template <int CI, int T>
   __device__ __forceinline__ void step() const {}
+  template <int CI>
+  __device__ __forceinline__ void before_dma() const {}
 };
 
 // One 16-block chunk of NS k-steps; the B operand of k-step T is getb(T) (compile time).
@@ -333,6 +341,7 @@ __device__ __forceinline__ void chunk16(State& s, float4* lds, int c, GetB getb,
     __builtin_amdgcn_sched_barrier(0);                              \
     if constexpr ((T) == 3) {                                       \
       chunk_barrier();                                              \
+      post.template before_dma<CI>();                               \
       dma_chunk<NG>(s, lds, c + 3);                                 \
     }                                                               \
     post.template step<CI, (T)>();                                  \
@@ -532,6 +541,35 @@ struct LayerStores {
   __device__ __forceinline__ void step() const {
     if constexpr (T == 4) blocks<2 * CI, 2>();
   }
+  template <int CI>
+  __device__ __forceinline__ void before_dma() const {}
+};
+
+// Training forward: the encodings layer_xyz1 multiplied (enc[16]: this lane group's k-step values),
+// as the (m, 64) encoding plane -- row = sample, lane group g's 16 values at 16 g (xenc_col) -- which
+// the backward's layer_xyz1 dW reads instead of regenerating them.  Four 16-B stores per lane,
+// issued in layer_xyz1's second chunk right after its barrier and before its DMA: at the next
+// barrier the counted vmcnt then leaves the ring's pieces in flight, not these.
+struct XencStore {
+  const State& s;
+  const FieldArgs& a;
+  int64_t tile;
+  const float (&enc)[16];
+  template <int CI, int T>
+  __device__ __forceinline__ void step() const {}
+  template <int CI>
+  __device__ __forceinline__ void before_dma() const {
+    const int64_t r0 = tile * kTile;
+    const int64_t rows = a.m - r0 < kTile ? a.m - r0 : kTile;
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(a.xenc + r0 * 64, 0, static_cast<int>(rows * 256),
+                                                                      0x00020000);
+    const unsigned off = static_cast<unsigned>(fresh((s.wave * 16 + (s.lane & 15)) * 256 + 64 * s.g));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const floatx4 v{enc[4 * q], enc[4 * q + 1], enc[4 * q + 2], enc[4 * q + 3]};
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, v), r, off + 16u * q, 0, kPlaneCPol);
+    }
+  }
 };
 
 // Training forward: the post-activation rows the weight gradients read (h1, h2, feat, v1, v2 as
@@ -613,7 +651,10 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
 #endif
       bias_from(s, clds + kCB1);
       chunk16<8>(s, lds, c + 0, l0);
-      chunk16<8>(s, lds, c + 1, LazyXyz{enc, s.denc, in.x, in.vd, fr, g, true});
+      if constexpr (SAVE)
+        chunk16<8, 0>(s, lds, c + 1, LazyXyz{enc, s.denc, in.x, in.vd, fr, g, true}, XencStore{s, a, tile, enc});
+      else
+        chunk16<8>(s, lds, c + 1, LazyXyz{enc, s.denc, in.x, in.vd, fr, g, true});
     }
   } else {
     if constexpr (MODE != kFromEncoded) {
@@ -646,7 +687,10 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
 #endif
     bias_from(s, clds + kCB1);
     chunk16<8>(s, lds, c + 0, ArrB<0>{enc});
-    chunk16<8>(s, lds, c + 1, ArrB<8>{enc});
+    if constexpr (SAVE)
+      chunk16<8, 0>(s, lds, c + 1, ArrB<8>{enc}, XencStore{s, a, tile, enc});
+    else
+      chunk16<8>(s, lds, c + 1, ArrB<8>{enc});
   }
   c += 2;
 
@@ -1174,6 +1218,8 @@ struct DpreStore {
       }
     }
   }
+  template <int CI>
+  __device__ __forceinline__ void before_dma() const {}
 };
 
 // The Q1 view-direction row of sample row rc (nerf/__init__.py:127-128; decode_sample's map).

@@ -333,13 +333,17 @@ int cn_field_backward_fused(int fmt_t, const float* packed_t, const uint32_t* ma
 
 /* --- Fused fp32 training step (train.py:92-114; weights trained) ------------------
  * Forward: cn_radiance_field on a CN_FMT_F32_W16 pack that also writes the ReLU masks
- * (cn_field_mask_words_fmt(CN_FMT_F32_W16, M) words) and the (5, M, 256) post-activation planes
- * h1, h2, feat, v1, v2 (cn_radiance_field_train's layout).
+ * (cn_field_mask_words_fmt(CN_FMT_F32_W16, M) words), the (5, M, 256) post-activation planes
+ * h1, h2, feat, v1, v2 (cn_radiance_field_train's layout) and after them, at save + 5 M 256, the
+ * (M, 64) encoding plane: the positional encodings layer_xyz1 multiplied, 16 per lane group in the
+ * kernel's k-step order (column c' -> PositionalEmbedder column of the mlp_common.h map, one padding
+ * slot).  save holds cn_field_train_saved_floats(CN_FMT_F32_W16, M) floats.
  * Backward: the fused dX chain of cn_field_backward_fused on the CN_FMT_F32_W16_T pack (g_code,
  * d_pts / d_ro / d_rd as there; g_code required) that also writes every layer's masked input
  * gradient into workspace (cn_field_backward_train_workspace_floats(M) floats), then the weight
  * and bias gradients dW = dPre^T X as split-M fp32 MFMA GEMMs over those planes, saved and x_enc
- * (cn_encode_inputs; or x_enc NULL: the encodings generated inside the dW kernels), reduced
+ * (cn_encode_inputs; or x_enc NULL: the forward's own encodings from saved's encoding plane, fp32,
+ * or generated inside the dW kernels, bf16x3), reduced
  * deterministically (cn_gemm_tn_ws) through the rest of workspace: grads (18 pointers, or NULL for none) ACCUMULATED as in
  * cn_field_backward (the code-layer parameters and code halves come from cn_code_bias_backward).
  * One code row per 16-sample wave: n_codes == 1 or n_samples % 16 == 0, else CN_EUNSUPPORTED. */
@@ -352,7 +356,9 @@ int cn_radiance_field_train_w16(const float* packed, const float* code_bias, con
  * 32x32x16; masks cn_field_mask_words_fmt(CN_FMT_BF16X3, M) words, the same fp32 planes), and
  * fmt_t the matching transposed pack (CN_FMT_F32_W16_T / CN_FMT_BF16X3_T; the bf16x3 dW GEMMs
  * are 3xbf16 too).  bf16x3: one code row per 32-sample wave (n_codes == 1 or n_samples % 32 == 0);
- * its save buffer holds 5 * M * 256 + 256 floats (the last row is scratch for padding lanes). */
+ * its save buffer holds 5 * M * 256 + 256 floats (the last row is scratch for padding lanes).
+ * cn_field_train_saved_floats: the save buffer's floats for fmt and M (-1: bad arguments). */
+int64_t cn_field_train_saved_floats(int fmt, int64_t m);
 int cn_radiance_field_train_fmt(int fmt, const float* packed, const float* code_bias, const int64_t* code_index,
                                 int64_t n_codes, const float* pts, const float* ro, const float* rd,
                                 const float* z, int64_t n_rays, int64_t n_samples, int64_t chunk_rows,

@@ -782,3 +782,47 @@ def test_field_prepare_bitwise(dev, n_codes, pack, pack_t):
     if pack_t:
         assert torch.equal(pkt, ops.mlp_pack(params, "f32_w16_t"))
     assert zero.shape == (nz,) and not zero.any()
+
+
+@pytest.mark.parametrize("far", [False, True])
+@pytest.mark.parametrize("mode", ["rayz", "pts"])
+def test_training_forward_encoding_plane(dev, mode, far):
+    """The fp32 training forward's (M, 64) encoding plane (after the five activation planes; the
+    layer_xyz1 dW reads it instead of regenerating the encodings): mapped through xenc_col it is the
+    positional encoding of the sample points (position_embed.py:44-53) -- the oracle's to 2e-6 (both
+    within ~2 ulp of sin / cos) -- and the padding slot is zero.  ``far``: one 16-sample wave with a
+    point past fast_sincosf's bound (that wave takes ocml's sincosf throughout)."""
+    from codenerf import ops, synthetic
+    from oracle import codenerf_oracle as Or
+    m_ = model(dev, 0)
+    params = [p.detach() for p in m_.param_list()]
+    r, s = 300, 64
+    g = torch.Generator().manual_seed(17)
+    ro = (torch.randn(r, 3, generator=g) * 0.3 + torch.tensor([0.0, 0.0, 1.3]))
+    rd = torch.randn(r, 3, generator=g)
+    z = torch.sort(0.8 + torch.rand(r, s, generator=g), dim=-1).values
+    pts = ro[:, None, :] + rd[:, None, :] * z[..., None]
+    if far:
+        pts[37, 5] = torch.tensor([45.0, -38.0, 41.0])
+    geo = dict(pts=pts.to(dev)) if mode == "pts" or far else dict(ro=ro.to(dev), z=z.to(dev))
+    if mode == "rayz" and far:
+        ro2 = ro.clone()
+        ro2[37] = torch.tensor([45.0, -38.0, 41.0])
+        pts = ro2[:, None, :] + rd[:, None, :] * z[..., None]
+        geo = dict(ro=ro2.to(dev), z=z.to(dev))
+    zs, zt = synthetic.latent_codes(5, 1).to(dev), synthetic.latent_codes(6, 1).to(dev)
+    fx, fd = [2.0 ** k for k in range(10)], [2.0 ** k for k in range(4)]
+    cb = ops.code_bias(params, zs, zt)
+    _, saved, _ = ops.radiance_field_train_w16(ops.mlp_pack(params, "f32_w16"), cb, rd.to(dev), s, r, fx, fd,
+                                               precision="f32", **geo)
+    m = r * s
+    plane = torch.empty(0, device=dev).set_(saved.untyped_storage(), 5 * m * 256, (m, 64)).cpu()
+    cols = ops.xenc_columns()
+    ref = Or.posenc(pts.reshape(-1, 3), Or.frequency_bands(10, True), True)
+    got = torch.zeros(m, 63)
+    for cp, c in enumerate(cols):
+        if c >= 0:
+            got[:, c] = plane[:, cp]
+        else:
+            assert not plane[:, cp].any(), "padding slot"
+    assert (got - ref).abs().max().item() <= 2e-6
