@@ -265,11 +265,18 @@ class RadianceField(torch.autograd.Function):
         ctx.g_code = None
         train_w16 = (not fused and meta.precision == meta.train_precision == "f32"
                      and ops.fused_backward_supported(z_s.shape[0], meta.n_samples, meta.code_index, "f32"))
+        ctx.acc = None
         if train_w16:
             # the fp32 training step: code terms, both packs and the backward's zeroed g_code, one launch
             nc = z_s.shape[0]
             cb, packed_w16, zero = _prepare_w16(ctx.owner, params, z_s, z_t, nc * _lib.CN_CODE_BIAS_STRIDE)
             ctx.g_code = zero.view(nc, _lib.CN_CODE_BIAS_STRIDE)
+        elif fused:
+            # the eval step (frozen weights, packs cached): the code terms and the fused backward's zeroed
+            # accumulators (g_code, d ro, d rd) in one launch
+            n_acc = ops.field_backward_x3_acc_floats(z_s.shape[0], n_rays, ctx.needs_input_grad[3],
+                                                     ctx.needs_input_grad[1])
+            cb, _, _, ctx.acc = ops.field_prepare(params, z_s, z_t, pack=False, pack_t=False, n_zero=n_acc)
         else:
             cb = ops.code_bias(params, z_s, z_t)
         if fused:
@@ -318,7 +325,8 @@ class RadianceField(torch.autograd.Function):
             r = ops.field_backward_x3(_packed(ctx.owner, params, pack_t), ctx.masks, g_raw.contiguous(), rd.shape[0],
                                       meta.n_samples, meta.chunk_rows, z_s.shape[0], meta.fx, meta.fd, rd=rd,
                                       pts=pts, ro=ro, z=z, code_index=meta.code_index, want_pts=needs[2],
-                                      want_ro=needs[3], want_rd=needs[1], precision=meta.precision)
+                                      want_ro=needs[3], want_rd=needs[1], precision=meta.precision, acc=ctx.acc)
+            ctx.acc = None
             dz_s = dz_t = None
             if want_z:
                 dz_s, dz_t = ops.code_bias_backward(params, z_s, z_t, r["g_code"], None, want_z=True)

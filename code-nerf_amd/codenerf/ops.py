@@ -768,13 +768,21 @@ def fused_backward_supported(n_codes: int, n_samples: int, code_index: Optional[
     return n_codes == 1 or n_samples % (32 if precision == "bf16x3" else 16) == 0
 
 
+def field_backward_x3_acc_floats(n_codes: int, n_rays: int, want_ro: bool, want_rd: bool) -> int:
+    """Floats of field_backward_x3's zeroed accumulator buffer: g_code, then d ro / d rd if wanted."""
+    return n_codes * _lib.CN_CODE_BIAS_STRIDE + 3 * n_rays * (int(want_ro) + int(want_rd))
+
+
 def field_backward_x3(packed_t: Tensor, masks: Tensor, d_raw: Tensor, n_rays: int, n_samples: int,
                       chunk_rows: int, n_codes: int, freqs_xyz: Sequence[float], freqs_dir: Sequence[float],
                       rd: Tensor, pts: Optional[Tensor] = None, ro: Optional[Tensor] = None,
                       z: Optional[Tensor] = None, code_index: Optional[Tensor] = None, want_pts: bool = False,
-                      want_ro: bool = False, want_rd: bool = False, precision: str = "bf16x3"):
+                      want_ro: bool = False, want_rd: bool = False, precision: str = "bf16x3",
+                      acc: Optional[Tensor] = None):
     """Fused backward of forward_pass + CodeNeRFModel.forward (frozen weights) -> g_code / d_pts / d_ro / d_rd.
-    precision "bf16x3" (packed_t "bf16x3_t") or "f32" (packed_t "f32_w16_t", masks of the f32_w16 forward)."""
+    precision "bf16x3" (packed_t "bf16x3_t") or "f32" (packed_t "f32_w16_t", masks of the f32_w16 forward).
+    ``acc``: a zeroed buffer of field_backward_x3_acc_floats(...) floats for the accumulated outputs
+    (field_prepare's), else one is allocated and filled."""
     fmt_t = _lib.CN_FMT_BF16X3_T if precision == "bf16x3" else _lib.CN_FMT_F32_W16_T
     lib = _lib_ready()
     m = n_rays * n_samples
@@ -786,7 +794,11 @@ def field_backward_x3(packed_t: Tensor, masks: Tensor, d_raw: Tensor, n_rays: in
         code_index = _cuda(code_index, "code_index", torch.int64)
     # the accumulated outputs share one zero-filled buffer (one fill launch instead of three)
     nc = n_codes * _lib.CN_CODE_BIAS_STRIDE
-    acc = torch.zeros(nc + 3 * n_rays * (int(want_ro) + int(want_rd)), device=dev, dtype=torch.float32)
+    n_acc = field_backward_x3_acc_floats(n_codes, n_rays, want_ro, want_rd)
+    if acc is None:
+        acc = torch.zeros(n_acc, device=dev, dtype=torch.float32)
+    else:
+        assert acc.numel() == n_acc and acc.is_contiguous()
     g_code = acc[:nc].view(n_codes, _lib.CN_CODE_BIAS_STRIDE)
     d_ro = acc[nc:nc + 3 * n_rays].view(n_rays, 3) if want_ro else None
     d_rd = acc[acc.numel() - 3 * n_rays:].view(n_rays, 3) if want_rd else None

@@ -136,7 +136,7 @@ class AdamW(torch.optim.Optimizer):
     def _sync_grads(self) -> List[torch.Tensor]:
         """Move every gradient into the flat buffer (autograd may have installed a new
         tensor) and point ``.grad`` at it; returns the parameters without a gradient."""
-        missing = []
+        missing, dst, src, moved = [], [], [], []
         with torch.no_grad():
             for p in self._offs:
                 if p.grad is None:
@@ -144,7 +144,14 @@ class AdamW(torch.optim.Optimizer):
                     continue
                 view = self._view("grad", p)
                 if p.grad.data_ptr() != view.data_ptr():
-                    view.copy_(p.grad)
+                    dst.append(view)
+                    src.append(p.grad)
+                    moved.append((p, view))
+            if dst:
+                # one multi-tensor launch for all of them (the eval loop's five leaf gradients --
+                # codes and pose -- were five copy launches per iteration)
+                torch._foreach_copy_(dst, src)
+                for p, view in moved:
                     p.grad = view
         return missing
 
