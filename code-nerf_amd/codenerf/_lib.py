@@ -39,6 +39,14 @@ _f = ctypes.c_float
 _i = ctypes.c_int
 _fp = ctypes.POINTER(ctypes.c_float)
 
+
+
+class FieldPrep(ctypes.Structure):
+    """cn_field_prep (include/codenerf.h): one model's part of cn_field_prepare_models."""
+    _fields_ = [("params", ctypes.POINTER(_p)), ("code_bias", _p), ("packed", _p), ("packed_t", _p), ("zero", _p),
+                ("n_zero", _i64)]
+
+
 # name -> (restype, argtypes); mirrors include/codenerf.h one to one.
 SIGNATURES = {
     "cn_version": (ctypes.c_char_p, []),
@@ -60,6 +68,7 @@ SIGNATURES = {
     "cn_mlp_pack": (_i, [ctypes.POINTER(_p), _i, _p, _p]),
     "cn_code_bias": (_i, [ctypes.POINTER(_p), _p, _p, _i64, _p, _p]),
     "cn_field_prepare": (_i, [ctypes.POINTER(_p), _p, _p, _i64, _p, _p, _p, _p, _i64, _p]),
+    "cn_field_prepare_models": (_i, [ctypes.POINTER(FieldPrep), _i, _p, _p, _i64, _p]),
     "cn_field_train_saved_floats": (_i64, [_i, _i64]),
     "cn_mlp_forward": (_i, [_p, _i, _p, _p, _i64, _p, _i64, _p, _p]),
     "cn_radiance_field": (_i, [_p, _i, _p, _p, _i64, _p, _p, _p, _p, _i64, _i64, _i64, _fp, _fp, _p, _p]),
@@ -92,7 +101,7 @@ SIGNATURES = {
                                   _p]),
     "cn_code_bias_backward": (_i, [ctypes.POINTER(_p), _p, _p, _i64, _p, _p, _p, ctypes.POINTER(_p), _p]),
     "cn_code_bias_backward_workspace_floats": (_i64, [_i64]),
-    "cn_code_bias_backward_ws": (_i, [ctypes.POINTER(_p), _p, _p, _i64, _p, _p, _p, ctypes.POINTER(_p), _p, _p]),
+    "cn_code_bias_backward_ws": (_i, [ctypes.POINTER(_p), _p, _p, _i64, _p, _p, _p, ctypes.POINTER(_p), _p, _i, _p]),
     "cn_volume_render_backward": (_i, [_p, _p, _p, _i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p]),
     "cn_ray_bundle_backward": (_i, [_p, _i64, _i64, _p, _p, _p, _p]),
     "cn_gather_rays_backward": (_i, [_p, _p, _i64, _i64, _p, _i64, _p, _p, _p]),

@@ -67,6 +67,62 @@ def _prepare_w16(owner, params, z_s, z_t, n_zero: int):
     return cb, cache["f32_w16"][1], zero
 
 
+def _zkey(z_s, z_t):
+    return (z_s.data_ptr(), z_s._version, tuple(z_s.shape), z_t.data_ptr(), z_t._version, tuple(z_t.shape))
+
+
+def _prep_plan(meta, n_codes: int, n_rays: int, needs):
+    """The pre-field launch RadianceField.forward makes -> (mode, n_zero): "train_w16" (code terms, the
+    fp32 packs where missing, a zeroed g_code), "fused" (the eval step: code terms and the fused
+    backward's zeroed accumulators) or (None, 0) (code_bias alone).  ``needs``: its needs_input_grad."""
+    if n_rays == 0 or n_codes == 0:
+        return None, 0
+    if (meta.precision in ("bf16x3", "f32") and not any(needs[7:])
+            and ops.fused_backward_supported(n_codes, meta.n_samples, meta.code_index, meta.precision)):
+        return "fused", ops.field_backward_x3_acc_floats(n_codes, n_rays, needs[3], needs[1])
+    if (meta.precision == meta.train_precision == "f32"
+            and ops.fused_backward_supported(n_codes, meta.n_samples, meta.code_index, "f32")):
+        return "train_w16", n_codes * _lib.CN_CODE_BIAS_STRIDE
+    return None, 0
+
+
+def prefetch_prepares(fields, z_s, z_t) -> bool:
+    """The pre-field launches of a render's two fields (coarse and fine, on the same code rows) as ONE
+    cn_field_prepare_models launch before the coarse field; each field's RadianceField.forward then
+    takes its part (_take_prepared) instead of launching its own.  ``fields``: [(model, meta, n_rays,
+    needs)] as RadianceField.apply will see them.  False (nothing launched) unless both plan one."""
+    entries = []
+    for model, meta, n_rays, needs in fields:
+        mode, n_zero = _prep_plan(meta, z_s.shape[0], n_rays, needs)
+        if mode is None:
+            return False
+        orig = model.param_list()
+        params = [p.detach() for p in orig]
+        cache, sig = _pack_cache(orig[0], params)
+        have = {f: (cache.get(f) is not None and cache[f][0] == sig) for f in ("f32_w16", "f32_w16_t")}
+        pack = mode == "train_w16" and not have["f32_w16"]
+        pack_t = mode == "train_w16" and not have["f32_w16_t"]
+        entries.append((cache, sig, mode, n_zero, params, pack, pack_t))
+    outs = ops.field_prepare_models([(e[4], e[5], e[6], e[3]) for e in entries], z_s, z_t)
+    key = _zkey(z_s, z_t)
+    for (cache, sig, mode, n_zero, _, _, _), (cb, pk, pkt, zero) in zip(entries, outs):
+        if pk is not None:
+            cache["f32_w16"] = (sig, pk)
+        if pkt is not None:
+            cache["f32_w16_t"] = (sig, pkt)
+        cache["prep"] = ((sig, mode, n_zero, key), (cb, zero))
+    return True
+
+
+def _take_prepared(owner, params, z_s, z_t, mode, n_zero):
+    """This field's part of a prefetch_prepares launch -> (cb, zero), or None (none, or stale)."""
+    cache, sig = _pack_cache(owner, params)
+    ent = cache.pop("prep", None)
+    if ent is None or ent[0] != (sig, mode, n_zero, _zkey(z_s, z_t)):
+        return None
+    return ent[1]
+
+
 def _needs_grad(*ts) -> bool:
     return torch.is_grad_enabled() and any(isinstance(t, torch.Tensor) and t.requires_grad for t in ts)
 
@@ -214,12 +270,24 @@ def _c(t):
 class _FieldMeta:
     """Non-tensor arguments of the field Functions."""
 
-    def __init__(self, n_samples, chunk_rows, fx, fd, code_index=None, precision="f32", train_precision="f32"):
+    def __init__(self, n_samples, chunk_rows, fx, fd, code_index=None, precision="f32", train_precision="f32",
+                 sink=None):
         self.n_samples, self.chunk_rows = n_samples, chunk_rows
         self.precision = precision
         self.train_precision = train_precision
         self.fx, self.fd = list(fx) if fx is not None else None, list(fd) if fd is not None else None
         self.code_index = code_index
+        self.sink = sink       # models.model.CodeGradSink of the code rows, or None
+
+
+def _code_grads(meta, params, z_s, z_t, g_code, pg, want_z):
+    """cn_code_bias_backward_ws -> (dz_s, dz_t); (None, None) when they were added in place into the code
+    tables' gradient rows (meta.sink: the coarse and fine fields of a one-object chunk add up there)."""
+    rows = meta.sink.rows() if (want_z and meta.sink is not None) else None
+    if rows is not None:
+        ops.code_bias_backward(params, z_s, z_t, g_code, pg, dz_into=rows)
+        return None, None
+    return ops.code_bias_backward(params, z_s, z_t, g_code, pg, want_z=want_z)
 
 
 def _param_grad_buffers(params, needs, orig=None):
@@ -259,24 +327,28 @@ class RadianceField(torch.autograd.Function):
         ctx.empty = n_rays == 0 or z_s.shape[0] == 0
         if ctx.empty:      # a zero-ray batch: empty raw, and no gradient flows back (backward)
             return torch.empty(n_rays, meta.n_samples, 4, device=rd.device, dtype=torch.float32)
-        fused = (meta.precision in ("bf16x3", "f32") and not any(ctx.needs_input_grad[7:])
-                 and ops.fused_backward_supported(z_s.shape[0], meta.n_samples, meta.code_index, meta.precision))
-        ctx.fused = fused
+        mode, n_zero = _prep_plan(meta, z_s.shape[0], n_rays, ctx.needs_input_grad)
+        fused = ctx.fused = mode == "fused"
+        train_w16 = mode == "train_w16"
         ctx.g_code = None
-        train_w16 = (not fused and meta.precision == meta.train_precision == "f32"
-                     and ops.fused_backward_supported(z_s.shape[0], meta.n_samples, meta.code_index, "f32"))
         ctx.acc = None
+        # a render's two fields may have been prepared together (prefetch_prepares)
+        pre = _take_prepared(ctx.owner, params, z_s, z_t, mode, n_zero) if mode else None
         if train_w16:
             # the fp32 training step: code terms, both packs and the backward's zeroed g_code, one launch
             nc = z_s.shape[0]
-            cb, packed_w16, zero = _prepare_w16(ctx.owner, params, z_s, z_t, nc * _lib.CN_CODE_BIAS_STRIDE)
+            if pre is not None:
+                (cb, zero), packed_w16 = pre, _packed(ctx.owner, params, "f32_w16")
+            else:
+                cb, packed_w16, zero = _prepare_w16(ctx.owner, params, z_s, z_t, n_zero)
             ctx.g_code = zero.view(nc, _lib.CN_CODE_BIAS_STRIDE)
         elif fused:
             # the eval step (frozen weights, packs cached): the code terms and the fused backward's zeroed
             # accumulators (g_code, d ro, d rd) in one launch
-            n_acc = ops.field_backward_x3_acc_floats(z_s.shape[0], n_rays, ctx.needs_input_grad[3],
-                                                     ctx.needs_input_grad[1])
-            cb, _, _, ctx.acc = ops.field_prepare(params, z_s, z_t, pack=False, pack_t=False, n_zero=n_acc)
+            if pre is not None:
+                cb, ctx.acc = pre
+            else:
+                cb, _, _, ctx.acc = ops.field_prepare(params, z_s, z_t, pack=False, pack_t=False, n_zero=n_zero)
         else:
             cb = ops.code_bias(params, z_s, z_t)
         if fused:
@@ -329,7 +401,7 @@ class RadianceField(torch.autograd.Function):
             ctx.acc = None
             dz_s = dz_t = None
             if want_z:
-                dz_s, dz_t = ops.code_bias_backward(params, z_s, z_t, r["g_code"], None, want_z=True)
+                dz_s, dz_t = _code_grads(meta, params, z_s, z_t, r["g_code"], None, True)
             ctx.masks = None
             return (None, r["d_rd"], r["d_pts"], r["d_ro"], None, dz_s, dz_t, *([None] * len(params)))
         pg = _param_grad_buffers(params, needs[7:], ctx.orig_params)
@@ -344,7 +416,7 @@ class RadianceField(torch.autograd.Function):
                                          want_ro=needs[3], want_rd=needs[1], precision=meta.precision,
                                          g_code=ctx.g_code)
             ctx.acts = ctx.x_enc = ctx.masks = ctx.g_code = None
-            dz_s, dz_t = ops.code_bias_backward(params, z_s, z_t, r["g_code"], pg, want_z=want_z)
+            dz_s, dz_t = _code_grads(meta, params, z_s, z_t, r["g_code"], pg, want_z)
             grads = pg if pg is not None else [None] * len(params)
             return (None, r["d_rd"], r["d_pts"], r["d_ro"], None, dz_s, dz_t, *grads)
         r = ops.field_backward(params, ctx.acts, ctx.x_enc, g_raw.contiguous(), rd.shape[0], meta.n_samples,
@@ -354,7 +426,7 @@ class RadianceField(torch.autograd.Function):
                                precision=meta.train_precision)
         dz_s = dz_t = None
         if r["g_code"] is not None:
-            dz_s, dz_t = ops.code_bias_backward(params, z_s, z_t, r["g_code"], pg, want_z=want_z)
+            dz_s, dz_t = _code_grads(meta, params, z_s, z_t, r["g_code"], pg, want_z)
         ctx.acts = ctx.x_enc = None
         grads = pg if pg is not None else [None] * len(params)
         return (None, r["d_rd"], r["d_pts"], r["d_ro"], None, dz_s, dz_t, *grads)
@@ -484,10 +556,33 @@ def mlp_forward_autograd(model, z_s, z_t, x):
     return MLPForward.apply(getattr(model, "train_precision", "f32"), x, cs, ct, *model.param_list())
 
 
+def _field_meta(model, cs, ct, n_samples, chunk_rows, fx, fd, code_index):
+    sink = getattr(cs, "_cn_sink", None)
+    return _FieldMeta(n_samples, chunk_rows, fx, fd, code_index=code_index,
+                      precision=getattr(model, "precision", "f32"),
+                      train_precision=getattr(model, "train_precision", "f32"),
+                      sink=sink if sink is not None and getattr(ct, "_cn_sink", None) is sink else None)
+
+
 def radiance_field_autograd(model, rd, z_s, z_t, chunk_rows, fx, fd, pts=None, ro=None, z=None, code_index=None):
     cs, ct = (z_s, z_t) if code_index is not None else _code_rows(z_s, z_t)
     n_samples = pts.shape[1] if pts is not None else z.shape[1]
-    meta = _FieldMeta(n_samples, chunk_rows, fx, fd, code_index=code_index,
-                      precision=getattr(model, "precision", "f32"),
-                      train_precision=getattr(model, "train_precision", "f32"))
+    meta = _field_meta(model, cs, ct, n_samples, chunk_rows, fx, fd, code_index)
     return RadianceField.apply(meta, rd, pts, ro, _d(z), cs, ct, *model.param_list())
+
+
+def prefetch_render_prepares(coarse, fine, rd, ro, cs, ct, n_coarse, n_fine, chunk_rows, fx, fd,
+                             code_index=None) -> bool:
+    """render_rays' hook: both fields' pre-field launches in one (prefetch_prepares) when both run the
+    differentiable field on the rays-and-depths form (coarse n_coarse, fine n_fine samples per ray)."""
+    if not torch.is_grad_enabled():
+        return False
+    fields = []
+    for model, n_s in ((coarse, n_coarse), (fine, n_fine)):
+        params = model.param_list()
+        needs = (False, rd.requires_grad, False, ro.requires_grad, False, cs.requires_grad, ct.requires_grad,
+                 *[p.requires_grad for p in params])
+        if not any(needs):
+            return False                  # _field_op takes the no-grad path
+        fields.append((model, _field_meta(model, cs, ct, n_s, chunk_rows, fx, fd, code_index), rd.shape[0], needs))
+    return prefetch_prepares(fields, cs, ct)

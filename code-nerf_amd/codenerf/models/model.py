@@ -134,34 +134,80 @@ def _dedupe_codes(z_s: torch.Tensor, z_t: torch.Tensor):
     return z_s, z_t, None
 
 
+class CodeGradSink:
+    """The code-table gradient rows the field backwards add into in place (cn_code_bias_backward_ws with
+    accumulate_dz): row k of the shape and of the texture table's zeroed flat gradient slice
+    (optim.AdamW.zero_grad), claimed by the first field backward that asks and handed to the tables as
+    their .grad by _TableRow.backward.  Per model and step this replaces an add of the coarse and fine
+    code gradients and one into the table row (nn.Embedding's backward, model.py:102-105)."""
+
+    __slots__ = ("tables", "k", "bufs")
+
+    def __init__(self, tables, k: int):
+        self.tables, self.k, self.bufs = tables, k, None
+
+    def rows(self):
+        """-> (shape row, texture row) views (1, code size) of the claimed gradient buffers, or None when a
+        table is frozen, already has a .grad or has no zeroed slot (the gradients then flow through
+        autograd as usual)."""
+        if self.bufs is None:
+            slots = [getattr(w, "_cn_grad_slot", None) for w in self.tables]
+            if not all(s is not None and w.requires_grad and w.grad is None and s.is_contiguous()
+                       for s, w in zip(slots, self.tables)):
+                return None
+            for w in self.tables:
+                w._cn_grad_slot = None            # one use per zero_grad
+            self.bufs = slots
+        return tuple(b[self.k:self.k + 1] for b in self.bufs)
+
+    def take(self):
+        """-> the claimed buffers or None, dropping the sink's references to them (AccumulateGrad then
+        adopts them as .grad without a copy)."""
+        b, self.bufs = self.bufs, None
+        return b
+
+
 class _TableRow(torch.autograd.Function):
     """Row k of the shape and texture tables (nn.Embedding's lookup of one id) whose backward adds the
     row gradients into the tables' gradient buffers directly: the optimiser's zeroed flat-buffer slice
     when the table has no .grad yet this step (optim.AdamW.zero_grad), else a fresh zero table -- one
-    small add per table instead of torch's dense zero fill + scatter + copy into .grad."""
+    small add per table instead of torch's dense zero fill + scatter + copy into .grad.  With a
+    CodeGradSink the field backwards have already added theirs in place: the claimed buffers are
+    returned as they are (plus any gradient that still came through autograd)."""
 
     @staticmethod
-    def forward(ctx, w_s, w_t, k):
+    def forward(ctx, w_s, w_t, k, sink=None):
+        ctx.set_materialize_grads(False)
         ctx.k = k
         ctx.tables = (w_s, w_t)
+        ctx.sink = sink
         return w_s.detach().narrow(0, k, 1), w_t.detach().narrow(0, k, 1)   # views: no copy
 
     @staticmethod
     def backward(ctx, g_s, g_t):
+        sunk = ctx.sink.take() if ctx.sink is not None else None
         out = []
-        for w, g, need in zip(ctx.tables, (g_s, g_t), ctx.needs_input_grad[:2]):
-            if not need or g is None:
+        for i, (w, g, need) in enumerate(zip(ctx.tables, (g_s, g_t), ctx.needs_input_grad[:2])):
+            if not need:
                 out.append(None)
                 continue
-            slot = getattr(w, "_cn_grad_slot", None)
-            if slot is not None and w.grad is None:
-                w._cn_grad_slot = None            # one use per zero_grad
-                buf = slot
+            if sunk is not None:
+                buf = sunk[i]
+            elif g is None:
+                out.append(None)
+                continue
             else:
-                buf = torch.zeros_like(w)
-            buf[ctx.k:ctx.k + 1].add_(g)
+                slot = getattr(w, "_cn_grad_slot", None)
+                if slot is not None and w.grad is None:
+                    w._cn_grad_slot = None            # one use per zero_grad
+                    buf = slot
+                else:
+                    buf = torch.zeros_like(w)
+            if g is not None:
+                buf[ctx.k:ctx.k + 1].add_(g)
             out.append(buf)
-        return out[0], out[1], None
+        sunk = buf = None
+        return out[0], out[1], None, None
 
 
 class CodeRows:
@@ -199,7 +245,10 @@ class ShapeTextureEmbedding(torch.nn.Module):
                 # per-ray codes as their expand -- no id upload, no index search, no gathers; the
                 # field kernels take the one code row (nerf._codes)
                 k = int(uniq_h[0])
-                rows_s, rows_t = _TableRow.apply(self.shape_embedding.weight, self.texture_embedding.weight, k)
+                tables = (self.shape_embedding.weight, self.texture_embedding.weight)
+                sink = CodeGradSink(tables, k)
+                rows_s, rows_t = _TableRow.apply(*tables, k, sink)
+                rows_s._cn_sink = rows_t._cn_sink = sink
                 n = object_ids.shape[0]
                 z_s, z_t = rows_s.expand(n, -1), rows_t.expand(n, -1)
                 tag = CodeRows(rows_s, rows_t, None)

@@ -142,6 +142,14 @@ def render_rays(ro: torch.Tensor, rd: torch.Tensor, z_s: torch.Tensor, z_t: torc
         t_rand = torch.rand(n, ps.num_samples_coarse, dtype=torch.float32, device=ro.device)
     _, z_c = ops.sample_uniform(ro.detach(), rd.detach(), ps.z_vals, ps.lower, ps.upper,
                                 t_rand if ps.perturb else None, want_pts=False)
+    if fine_model is not None and not coarse_only:
+        # the two differentiable fields' pre-field launches (code terms, packs, zeroed accumulators) as
+        # one launch; each field takes its part (no launch when either runs without gradients)
+        from ..autograd import prefetch_render_prepares
+        fx, fd = _check_embedders(embedders)
+        cs, ct, code_index = _codes(z_s, z_t)
+        prefetch_render_prepares(_unwrap(coarse_model), _unwrap(fine_model), rd, ro, cs, ct, ps.num_samples_coarse,
+                                 ps.num_samples_coarse + ps.num_samples_fine, chunk_rows, fx, fd, code_index)
     # pts = ro + rd z is formed inside the field kernel (z detached, point_sampler.py:115); with
     # gradients on, the field's backward returns d ro / d rd through both the points and the view dirs
     raw_c = timed_field(coarse_model, embedders, rd, z_s, z_t, chunk_rows, ro=ro, z=z_c)

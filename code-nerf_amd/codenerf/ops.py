@@ -326,6 +326,34 @@ def field_prepare(params: Sequence[Tensor], z_s: Tensor, z_t: Tensor, pack: bool
     return cb, packed, packed_t, zero
 
 
+def field_prepare_models(models: Sequence[Tuple[Sequence[Tensor], bool, bool, int]], z_s: Tensor, z_t: Tensor):
+    """cn_field_prepare_models: field_prepare for one or two models (params, pack, pack_t, n_zero) on the
+    same codes in ONE launch -> [(cb, packed or None, packed_t or None, zero or None)] per model; bitwise
+    each model's field_prepare."""
+    lib = _lib_ready()
+    assert 1 <= len(models) <= 2, "one or two models"
+    z_s, z_t = _cuda(z_s.detach(), "z_s"), _cuda(z_t.detach(), "z_t")
+    assert z_s.shape == z_t.shape and z_s.dim() == 2 and z_s.shape[1] == 256, "codes must be (n, 256)"
+    dev = z_s.device
+    nf = mlp_packed_floats("f32_w16")
+    outs, keep = [], []
+    preps = (_lib.FieldPrep * len(models))()
+    for k, (params, pack, pack_t, n_zero) in enumerate(models):
+        params = [_cuda(p.detach(), f"param{i}") for i, p in enumerate(params)]
+        cb = torch.empty(z_s.shape[0], _lib.CN_CODE_BIAS_STRIDE, device=dev, dtype=torch.float32)
+        packed = torch.empty(nf, device=dev, dtype=torch.float32) if pack else None
+        packed_t = torch.empty(nf, device=dev, dtype=torch.float32) if pack_t else None
+        zero = torch.empty(n_zero, device=dev, dtype=torch.float32) if n_zero else None
+        arr, k_arr = _lib.pointer_array(params)
+        keep += [params, arr, k_arr]
+        preps[k] = _lib.FieldPrep(arr, ptr(cb), ptr(packed), ptr(packed_t), ptr(zero), n_zero)
+        outs.append((cb, packed, packed_t, zero))
+    check(lib.cn_field_prepare_models(preps, len(models), ptr(z_s), ptr(z_t), z_s.shape[0], stream_of(z_s)),
+          "cn_field_prepare_models")
+    del keep
+    return outs
+
+
 def xenc_columns():
     """The fp32 training forward's encoding plane (cn_field_train_saved_floats): column c' (0..63) ->
     PositionalEmbedder column (position_embed.py:44-53), -1 for the padding slot (mlp_common.h
@@ -639,16 +667,24 @@ def field_backward(params: Sequence[Tensor], saved: Tensor, x_enc: Tensor, d_raw
 
 def code_bias_backward(params: Sequence[Tensor], z_s: Tensor, z_t: Tensor, g_code: Tensor,
                        param_grads: Optional[Sequence[Tensor]] = None, want_z: bool = True,
-                       single_launch: bool = False):
+                       single_launch: bool = False, dz_into: Optional[Tuple[Tensor, Tensor]] = None):
     """Backward of code_bias (model.py:174-177 + the code halves) -> dz_s, dz_t (n_codes, 256) or None.
     The two-launch form (cn_code_bias_backward_ws) unless single_launch (cn_code_bias_backward):
-    bitwise the same results."""
+    bitwise the same results.  ``dz_into`` (two contiguous (n_codes, 256) device tensors, two-launch
+    form): the code gradients are ADDED into them (accumulate_dz) and returned."""
     lib = _lib_ready()
     params = [_cuda(p.detach(), f"param{i}") for i, p in enumerate(params)]
     z_s, z_t, g_code = _cuda(z_s.detach(), "z_s"), _cuda(z_t.detach(), "z_t"), _cuda(g_code, "g_code")
     n = z_s.shape[0]
-    dz_s = torch.empty_like(z_s) if want_z else None
-    dz_t = torch.empty_like(z_t) if want_z else None
+    if dz_into is not None:
+        assert not single_launch, "dz_into: the two-launch form"
+        for d in dz_into:
+            assert d.is_cuda and d.dtype == torch.float32 and d.is_contiguous() and d.shape == z_s.shape, \
+                "dz_into: contiguous (n_codes, 256) fp32 device tensors"
+        dz_s, dz_t = dz_into
+    else:
+        dz_s = torch.empty_like(z_s) if want_z else None
+        dz_t = torch.empty_like(z_t) if want_z else None
     arr, keep = _lib.pointer_array(params)
     garr, gkeep = (None, None)
     if param_grads is not None:
@@ -659,7 +695,8 @@ def code_bias_backward(params: Sequence[Tensor], z_s: Tensor, z_t: Tensor, g_cod
     else:
         ws = torch.empty(lib.cn_code_bias_backward_workspace_floats(n), device=g_code.device, dtype=torch.float32)
         check(lib.cn_code_bias_backward_ws(arr, ptr(z_s), ptr(z_t), n, ptr(g_code), ptr(dz_s), ptr(dz_t), garr,
-                                           ptr(ws), stream_of(g_code)), "cn_code_bias_backward_ws")
+                                           ptr(ws), int(dz_into is not None), stream_of(g_code)),
+              "cn_code_bias_backward_ws")
     del keep, gkeep
     return dz_s, dz_t
 

@@ -126,12 +126,14 @@ __device__ __forceinline__ void flush_block(const floatx16& acc, float* C, int64
   }
 }
 
-// C[n][k] += sum_p part[p][n][k], p in order (one thread per element, 4 partial streams per
-// element combined in a fixed tree): the deterministic second pass of the split-M dW GEMMs.
-// Block b of a job covers elements 64 b .. 64 b + 63, or 256 b .. 256 b + 255 with a float4 per
-// thread (reduce_vec4: N K % 4 == 0 and a 16-B aligned workspace; 16-B loads, a quarter of the blocks).  Either way element e's
-// partials are added in the same order -- four interleaved chains per quarter of the parts, the
-// quarters then pairwise -- so both forms give the same bits.
+// C[n][k] += sum_p part[p][n][k] in a fixed order: the deterministic second pass of the split-M dW
+// GEMMs.  The parts are split into G groups (4, or 16 for many parts: reduce_groups), each summed as
+// four interleaved chains by one lane per element, the groups then combined in a pairwise tree.  Block
+// b of a job covers reduce_block_elems(G, vec4) elements: a float per lane, or a float4 per lane
+// (reduce_vec4: N K % 4 == 0 and a 16-B aligned workspace; 16-B loads, a quarter of the blocks).
+// Either way element e's partials are added in the same order, so both forms give the same bits.
+constexpr int kReduceBatch = 16;   // partials per quarter loaded together (C3's jobs: 12-16)
+
 __host__ __device__ __forceinline__ bool reduce_vec4(const float* part, int64_t nk) {
   return nk % 4 == 0 && (reinterpret_cast<uintptr_t>(part) & 15) == 0;
 }
@@ -142,72 +144,113 @@ __device__ __forceinline__ void reduce_add(float* __restrict__ C, int64_t ldc, i
   if (C2) C2[(e / K) * ldc + e % K] += v;
 }
 
+// One part group's chains: parts p0 .. p1 - 1 added in order into four interleaved chains (groups of
+// four parts into s0..s3, the tail into s0), combined (s0 + s1) + (s2 + s3).  The loads go out
+// kReduceBatch at a time (one memory latency per batch instead of one per group of four); the additions
+// keep the loop's order, so the bits do not depend on the batching.
+template <typename V, typename Load>
+__device__ __forceinline__ V reduce_chains(int64_t p0, int64_t p1, V zero, Load load) {
+  V s0 = zero, s1 = zero, s2 = zero, s3 = zero;
+  const int64_t g4 = p0 + ((p1 - p0) & ~int64_t(3));   // end of the groups of four
+  for (int64_t base = p0; base < p1; base += kReduceBatch) {
+    V x[kReduceBatch];
+#pragma unroll
+    for (int u = 0; u < kReduceBatch; ++u) x[u] = base + u < p1 ? load(base + u) : zero;
+    // static chain selection (a dynamically chosen reference would put the chains in scratch): part
+    // base + u of a full group of four goes to chain u & 3, a tail part (p >= g4) to s0
+#pragma unroll
+    for (int u = 0; u < kReduceBatch; ++u) {
+      const int64_t p = base + u;
+      const bool full = p < g4, tail = !full && p < p1;
+      if ((u & 3) == 0) {
+        s0 = (full || tail) ? s0 + x[u] : s0;
+      } else {
+        V& c = (u & 3) == 1 ? s1 : (u & 3) == 2 ? s2 : s3;
+        c = full ? c + x[u] : c;
+        s0 = tail ? s0 + x[u] : s0;
+      }
+    }
+  }
+  return (s0 + s1) + (s2 + s3);
+}
+
+__device__ __forceinline__ float4& operator+=(float4& a, const float4& b) {
+  a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+  return a;
+}
+__device__ __forceinline__ float4 operator+(float4 a, const float4& b) { return a += b; }
+
+// The G part groups' sums combined in a fixed pairwise tree: (r0 + r1) + (r2 + r3) for G = 4; for
+// G = 16 the same over the four quads.
+template <int G, typename V>
+__device__ __forceinline__ V reduce_tree(const V* r) {
+  if constexpr (G == 4) {
+    return (r[0] + r[1]) + (r[2] + r[3]);
+  } else {
+    static_assert(G == 16, "part groups: 4 or 16");
+    return (((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]))) +
+           (((r[8] + r[9]) + (r[10] + r[11])) + ((r[12] + r[13]) + (r[14] + r[15])));
+  }
+}
+
+// Elements per reduce block: 256 threads = G part groups x 256 / G lanes, a float4 (reduce_vec4) or a
+// float per lane.
+__host__ __device__ constexpr int reduce_block_elems(int G, bool vec4) { return (256 / G) * (vec4 ? 4 : 1); }
+// Part groups of a reduction over n_parts partials: 4 (each group's partials in one or two load
+// batches up to 64 parts), 16 past that (layer_xyz1's 512 encoding partials: 32 per group instead of
+// 128 in eight dependent batches -- that job held the whole reduce launch).
+__host__ __device__ constexpr int reduce_groups(int64_t n_parts) { return n_parts > 4 * kReduceBatch ? 16 : 4; }
+
 // C (and C2, when set: a second target of the same layout) += the fixed-order sum of the n_parts
-// partial (N, K) tiles, elements of block b.
+// partial (N, K) tiles, elements of block b; G part groups (reduce_groups).
+template <int G>
 __device__ __forceinline__ void reduce_block(const float* __restrict__ part, int64_t n_parts, int N, int K,
-                                             float* __restrict__ C, int64_t ldc, int64_t b, float4 (&red)[4][64],
+                                             float* __restrict__ C, int64_t ldc, int64_t b, float4 (&red)[16][64],
                                              float* __restrict__ C2 = nullptr) {
-  const int q = threadIdx.x >> 6, t = threadIdx.x & 63;
+  constexpr int L = 256 / G;   // lanes per part group
+  const int q = threadIdx.x / L, t = threadIdx.x % L;
   const int64_t nk = (int64_t)N * K;
-  const int64_t p0 = n_parts * q / 4, p1 = n_parts * (q + 1) / 4;
+  const int64_t p0 = n_parts * q / G, p1 = n_parts * (q + 1) / G;
   if (reduce_vec4(part, nk)) {
-    const int64_t e = b * 256 + 4 * t;
+    const int64_t e = b * reduce_block_elems(G, true) + 4 * t;
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
     if (e < nk) {
-      float4 s0 = s, s1 = s, s2 = s, s3 = s;
       const float4* pp = reinterpret_cast<const float4*>(part + e);
       const int64_t st = nk / 4;
-      int64_t p = p0;
-      for (; p + 4 <= p1; p += 4) {
-        const float4 x0 = pp[p * st], x1 = pp[(p + 1) * st], x2 = pp[(p + 2) * st], x3 = pp[(p + 3) * st];
-        s0.x += x0.x; s0.y += x0.y; s0.z += x0.z; s0.w += x0.w;
-        s1.x += x1.x; s1.y += x1.y; s1.z += x1.z; s1.w += x1.w;
-        s2.x += x2.x; s2.y += x2.y; s2.z += x2.z; s2.w += x2.w;
-        s3.x += x3.x; s3.y += x3.y; s3.z += x3.z; s3.w += x3.w;
-      }
-      for (; p < p1; ++p) {
-        const float4 x0 = pp[p * st];
-        s0.x += x0.x; s0.y += x0.y; s0.z += x0.z; s0.w += x0.w;
-      }
-      s.x = (s0.x + s1.x) + (s2.x + s3.x);
-      s.y = (s0.y + s1.y) + (s2.y + s3.y);
-      s.z = (s0.z + s1.z) + (s2.z + s3.z);
-      s.w = (s0.w + s1.w) + (s2.w + s3.w);
+      s = reduce_chains(p0, p1, s, [&](int64_t p) { return pp[p * st]; });
     }
     red[q][t] = s;
     __syncthreads();
     if (q == 0 && e < nk) {
-      const float4 r0 = red[0][t], r1 = red[1][t], r2 = red[2][t], r3 = red[3][t];
-      reduce_add(C, ldc, K, e, (r0.x + r1.x) + (r2.x + r3.x), C2);
-      reduce_add(C, ldc, K, e + 1, (r0.y + r1.y) + (r2.y + r3.y), C2);
-      reduce_add(C, ldc, K, e + 2, (r0.z + r1.z) + (r2.z + r3.z), C2);
-      reduce_add(C, ldc, K, e + 3, (r0.w + r1.w) + (r2.w + r3.w), C2);
+      float4 r[G];
+#pragma unroll
+      for (int g = 0; g < G; ++g) r[g] = red[g][t];
+      const float4 v = reduce_tree<G>(r);
+      reduce_add(C, ldc, K, e, v.x, C2);
+      reduce_add(C, ldc, K, e + 1, v.y, C2);
+      reduce_add(C, ldc, K, e + 2, v.z, C2);
+      reduce_add(C, ldc, K, e + 3, v.w, C2);
     }
     return;
   }
-  const int64_t e = b * 64 + t;
+  const int64_t e = b * reduce_block_elems(G, false) + t;
   float s = 0.0f;
-  if (e < nk) {
-    float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
-    int64_t p = p0;
-    for (; p + 4 <= p1; p += 4) {
-      s0 += part[p * nk + e];
-      s1 += part[(p + 1) * nk + e];
-      s2 += part[(p + 2) * nk + e];
-      s3 += part[(p + 3) * nk + e];
-    }
-    for (; p < p1; ++p) s0 += part[p * nk + e];
-    s = (s0 + s1) + (s2 + s3);
-  }
+  if (e < nk) s = reduce_chains(p0, p1, 0.0f, [&](int64_t p) { return part[p * nk + e]; });
   red[q][t].x = s;
   __syncthreads();
-  if (q == 0 && e < nk) reduce_add(C, ldc, K, e, (red[0][t].x + red[1][t].x) + (red[2][t].x + red[3][t].x), C2);
+  if (q == 0 && e < nk) {
+    float r[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) r[g] = red[g][t].x;
+    reduce_add(C, ldc, K, e, reduce_tree<G>(r), C2);
+  }
 }
 
 __global__ __launch_bounds__(256) void reduce_partials_kernel(const float* __restrict__ part, int64_t n_parts,
                                                               int N, int K, float* __restrict__ C, int64_t ldc) {
-  __shared__ float4 red[4][64];
-  reduce_block(part, n_parts, N, K, C, ldc, blockIdx.x, red);
+  __shared__ float4 red[16][64];
+  if (reduce_groups(n_parts) == 16) reduce_block<16>(part, n_parts, N, K, C, ldc, blockIdx.x, red);
+  else reduce_block<4>(part, n_parts, N, K, C, ldc, blockIdx.x, red);
 }
 
 // Several reductions in one launch (a backward's dW GEMMs queue theirs and flush once).
@@ -225,11 +268,13 @@ struct ReduceJobs {
 };
 
 __global__ __launch_bounds__(256) void reduce_jobs_kernel(ReduceJobs jobs) {
-  __shared__ float4 red[4][64];
+  __shared__ float4 red[16][64];
   int k = jobs.n - 1;
   while (k > 0 && (int64_t)blockIdx.x < jobs.j[k].first_block) --k;
   const ReduceJob& jb = jobs.j[k];
-  reduce_block(jb.part, jb.n_parts, jb.N, jb.K, jb.C, jb.ldc, (int64_t)blockIdx.x - jb.first_block, red, jb.C2);
+  const int64_t b = (int64_t)blockIdx.x - jb.first_block;
+  if (reduce_groups(jb.n_parts) == 16) reduce_block<16>(jb.part, jb.n_parts, jb.N, jb.K, jb.C, jb.ldc, b, red, jb.C2);
+  else reduce_block<4>(jb.part, jb.n_parts, jb.N, jb.K, jb.C, jb.ldc, b, red, jb.C2);
 }
 
 // gemm_tn: C[n][k] += sum_m A[m][n] B[m][k] (dW = dPre^T X).  No LDS: on
@@ -1832,11 +1877,14 @@ __global__ __launch_bounds__(kCodeThreads) void code_backward_kernel(mlp::Params
 // The same backward in two launches (cn_code_bias_backward_ws).  code_backward_kernel recomputes
 // the three code layers and the three 256-long reductions in each of its 16 workgroups per code
 // (about 2 MiB of L2 reads per workgroup: ~55 us for one code).  Here workgroup y of
-// code_layers_dz_kernel forms outputs 16 y .. 16 y + 15 of s1 / s2 / t1 and of ds1 / ds2 / dt1
-// into the workspace (per code: s1 s2 t1 ds1 ds2 dt1, 6 x 256 floats), and workgroup y of
-// code_outer_kernel forms dz_s / dz_t for columns 16 y .. and the outer products of rows 16 y ..
-// Every sum keeps code_backward_kernel's order: bitwise the same results.
-constexpr int kCodeSlices = 16;  // workgroups per code, 16 outputs each
+// code_layers_dz_kernel forms outputs R y .. R y + R - 1 (R = kCodeRows) of s1 / s2 / t1 and of
+// ds1 / ds2 / dt1 into the workspace (per code: s1 s2 t1 ds1 ds2 dt1, 6 x 256 floats), and workgroup
+// y of code_outer_kernel forms dz_s / dz_t for columns R y .. and the outer products of rows R y ..
+// Every sum keeps code_backward_kernel's order: bitwise the same results.  64 workgroups per code
+// (4 rows each): the per-workgroup chains are latency-bound, so more and shorter ones.
+constexpr int kCodeSlices = 64;                  // workgroups per code
+constexpr int kCodeRows = 256 / kCodeSlices;     // outputs / outer-product rows per workgroup
+static_assert(256 % kCodeSlices == 0 && kCodeRows <= 16, "phase-2 thread map: 16 columns per (quarter, vector)");
 
 // Whether any sample used code row gr (all its code-term gradients zero otherwise), as
 // code_backward_kernel tests it; every thread of the block gets the answer.
@@ -1851,7 +1899,8 @@ __global__ __launch_bounds__(256) void code_layers_dz_kernel(mlp::Params P, cons
                                                              const float* __restrict__ z_t,
                                                              const float* __restrict__ g, float* __restrict__ ws) {
   using namespace mlp;
-  __shared__ float zs[256], zt[256], gx2[256], go[257], grgb[3], sv[3][16];
+  constexpr int kPerWave = (kCodeRows + 3) / 4;  // outputs per wave (waves past kCodeRows idle)
+  __shared__ float zs[256], zt[256], gx2[256], go[257], grgb[3], sv[3][kCodeRows];
   __shared__ float red[3][4][16];
   const int c = blockIdx.x, y = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const float* gr = g + (int64_t)c * kCbStride;
@@ -1865,11 +1914,11 @@ __global__ __launch_bounds__(256) void code_layers_dz_kernel(mlp::Params P, cons
   __syncthreads();
   float* wc = ws + (int64_t)c * 6 * 256;
   {
-    // outputs o = 16 y + 4 w + x: lanes over k (k = lane + 64 u), butterfly sum
-    float a1[4], a2[4], a3[4];
+    // outputs o = R y + kPerWave w + x: lanes over k (k = lane + 64 u), butterfly sum
+    float a1[kPerWave], a2[kPerWave], a3[kPerWave];
 #pragma unroll
-    for (int x = 0; x < 4; ++x) {
-      const int o = 16 * y + 4 * w + x;
+    for (int x = 0; x < kPerWave; ++x) {
+      const int i = kPerWave * w + x, o = kCodeRows * y + (i < kCodeRows ? i : 0);
       a1[x] = a2[x] = a3[x] = 0.f;
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -1880,58 +1929,68 @@ __global__ __launch_bounds__(256) void code_layers_dz_kernel(mlp::Params P, cons
       }
     }
 #pragma unroll
-    for (int x = 0; x < 4; ++x) {
+    for (int x = 0; x < kPerWave; ++x) {
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) {
         a1[x] += __shfl_xor(a1[x], off);
         a2[x] += __shfl_xor(a2[x], off);
         a3[x] += __shfl_xor(a3[x], off);
       }
-      if (lane == 0) {
-        const int i = 4 * w + x, o = 16 * y + i;
+      const int i = kPerWave * w + x;
+      if (lane == 0 && i < kCodeRows) {
+        const int o = kCodeRows * y + i;
         sv[0][i] = fmaxf(a1[x] + P.p[kBSc1][o], 0.f);
         sv[1][i] = fmaxf(a2[x] + P.p[kBSc2][o], 0.f);
         sv[2][i] = fmaxf(a3[x] + P.p[kBTc1][o], 0.f);
       }
     }
   }
-  // ds1 / ds2 / dt1 for j = 16 y + jj: thread (quarter q, vector v, jj), the quarter's 64 n in order
+  // ds1 / ds2 / dt1 for j = R y + jj: thread (quarter q, vector v, jj), the quarter's 64 n in order
   {
-    const int q = tid >> 6, v = (tid >> 4) & 3, jj = tid & 15, j = 16 * y + jj;
+    const int q = tid >> 6, v = (tid >> 4) & 3, jj = tid & 15, j = kCodeRows * y + jj;
     float a = 0.f;
-    if (v == 0) {
+    if (jj < kCodeRows) {
+      if (v == 0) {
 #pragma unroll 16
-      for (int n = 64 * q; n < 64 * q + 64; ++n) a = fmaf(P.p[kWXyz2][n * 512 + 256 + j], gx2[n], a);
-    } else if (v == 1) {
+        for (int n = 64 * q; n < 64 * q + 64; ++n) a = fmaf(P.p[kWXyz2][n * 512 + 256 + j], gx2[n], a);
+      } else if (v == 1) {
 #pragma unroll 16
-      for (int n = 64 * q; n < 64 * q + 64; ++n) a = fmaf(P.p[kWOut][n * 512 + 256 + j], go[n], a);
-      if (q == 3) a = fmaf(P.p[kWOut][256 * 512 + 256 + j], go[256], a);
-    } else if (v == 2 && q == 0) {
-      for (int n = 0; n < 3; ++n) a = fmaf(P.p[kWRgb][n * 512 + 256 + j], grgb[n], a);
+        for (int n = 64 * q; n < 64 * q + 64; ++n) a = fmaf(P.p[kWOut][n * 512 + 256 + j], go[n], a);
+        if (q == 3) a = fmaf(P.p[kWOut][256 * 512 + 256 + j], go[256], a);
+      } else if (v == 2 && q == 0) {
+        for (int n = 0; n < 3; ++n) a = fmaf(P.p[kWRgb][n * 512 + 256 + j], grgb[n], a);
+      }
+      if (v < 3) red[v][q][jj] = a;
     }
-    if (v < 3) red[v][q][jj] = a;
   }
   __syncthreads();
-  if (tid < 48) {
-    const int v = tid >> 4, jj = tid & 15, j = 16 * y + jj;
+  if (tid < 48 && (tid & 15) < kCodeRows) {
+    const int v = tid >> 4, jj = tid & 15, j = kCodeRows * y + jj;
     const float sum = v == 2 ? red[2][0][jj] : (red[v][0][jj] + red[v][1][jj]) + (red[v][2][jj] + red[v][3][jj]);
     wc[v * 256 + j] = sv[v][jj];
     wc[(3 + v) * 256 + j] = sv[v][jj] > 0.f ? sum : 0.f;
   }
 }
 
+// G[i] += v (returnless float atomic: one code -> one writer per element, the plain sum's bits)
+__device__ __forceinline__ void grad_add(const float* p, int64_t i, float v) {
+  atomicAdd(const_cast<float*>(p) + i, v);
+}
+
+// accumulate: dz_s / dz_t += the code gradients (the shape / texture tables' gradient rows), else =.
 __global__ __launch_bounds__(256) void code_outer_kernel(mlp::Params P, const float* __restrict__ z_s,
                                                          const float* __restrict__ z_t, const float* __restrict__ g,
                                                          const float* __restrict__ ws, float* __restrict__ dz_s,
-                                                         float* __restrict__ dz_t, mlp::Params G) {
+                                                         float* __restrict__ dz_t, mlp::Params G, int accumulate) {
   using namespace mlp;
   __shared__ float s1[256], s2[256], t1[256], ds1[256], ds2[256], dt1[256], go[257], gx2[256], grgb[3];
   __shared__ float red[2][4][16];
   const int c = blockIdx.x, y = blockIdx.y, tid = threadIdx.x;
+  const int r0 = kCodeRows * y;
   const float* gr = g + (int64_t)c * kCbStride;
   if (!code_row_used(gr, tid)) {
-    if (tid < 16 && dz_s) dz_s[(int64_t)c * 256 + 16 * y + tid] = 0.0f;
-    if (tid < 16 && dz_t) dz_t[(int64_t)c * 256 + 16 * y + tid] = 0.0f;
+    if (!accumulate && tid < kCodeRows && dz_s) dz_s[(int64_t)c * 256 + r0 + tid] = 0.0f;
+    if (!accumulate && tid < kCodeRows && dz_t) dz_t[(int64_t)c * 256 + r0 + tid] = 0.0f;
     return;
   }
   const float* wc = ws + (int64_t)c * 6 * 256;
@@ -1947,48 +2006,54 @@ __global__ __launch_bounds__(256) void code_outer_kernel(mlp::Params P, const fl
   if (tid < 3) grgb[tid] = gr[kCbRgb + tid];
   __syncthreads();
   if (dz_s || dz_t) {
-    // columns j = 16 y + jj: thread (quarter q, vector v, jj), code_backward_kernel's chains
-    const int q = tid >> 6, v = (tid >> 4) & 3, jj = tid & 15, j = 16 * y + jj;
+    // columns j = R y + jj: thread (quarter q, vector v, jj), code_backward_kernel's chains
+    const int q = tid >> 6, v = (tid >> 4) & 3, jj = tid & 15, j = r0 + jj;
     float a = 0.f;
-    if (v == 0) {
+    if (jj < kCodeRows) {
+      if (v == 0) {
 #pragma unroll 16
-      for (int n = 64 * q; n < 64 * q + 64; ++n) {
-        a = fmaf(P.p[kWSc1][n * 256 + j], ds1[n], a);
-        a = fmaf(P.p[kWSc2][n * 256 + j], ds2[n], a);
+        for (int n = 64 * q; n < 64 * q + 64; ++n) {
+          a = fmaf(P.p[kWSc1][n * 256 + j], ds1[n], a);
+          a = fmaf(P.p[kWSc2][n * 256 + j], ds2[n], a);
+        }
+      } else if (v == 1) {
+#pragma unroll 16
+        for (int n = 64 * q; n < 64 * q + 64; ++n) a = fmaf(P.p[kWTc1][n * 256 + j], dt1[n], a);
       }
-    } else if (v == 1) {
-#pragma unroll 16
-      for (int n = 64 * q; n < 64 * q + 64; ++n) a = fmaf(P.p[kWTc1][n * 256 + j], dt1[n], a);
+      if (v < 2) red[v][q][jj] = a;
     }
-    if (v < 2) red[v][q][jj] = a;
     __syncthreads();
-    if (tid < 32) {
+    if (tid < 32 && (tid & 15) < kCodeRows) {
       const int vv = tid >> 4, k = tid & 15;
       const float sum = (red[vv][0][k] + red[vv][1][k]) + (red[vv][2][k] + red[vv][3][k]);
       float* dz = vv == 0 ? dz_s : dz_t;
-      if (dz) dz[(int64_t)c * 256 + 16 * y + k] = sum;
+      if (dz) {
+        float* d = dz + (int64_t)c * 256 + r0 + k;
+        *d = accumulate ? *d + sum : sum;
+      }
     }
   }
   if (!G.p[kWSc1]) return;
-  // rows r = 16 y .. 16 y + 15 of the outer products, column j = tid; the bias / single-row terms
-  // of columns 16 y ..
+  // rows r0 .. r0 + R - 1 of the outer products, column j = tid; the bias / single-row terms of
+  // columns r0 ..
   const int j = tid;
   const float zsj = z_s[(int64_t)c * 256 + j], ztj = z_t[(int64_t)c * 256 + j];
   const float s1j = s1[j], s2j = s2[j];
-  for (int r = 16 * y; r < 16 * y + 16; ++r) {
-    atomicAdd(&const_cast<float*>(G.p[kWSc1])[r * 256 + j], ds1[r] * zsj);
-    atomicAdd(&const_cast<float*>(G.p[kWSc2])[r * 256 + j], ds2[r] * zsj);
-    atomicAdd(&const_cast<float*>(G.p[kWTc1])[r * 256 + j], dt1[r] * ztj);
-    atomicAdd(&const_cast<float*>(G.p[kWXyz2])[r * 512 + 256 + j], gx2[r] * s1j);
-    atomicAdd(&const_cast<float*>(G.p[kWOut])[(1 + r) * 512 + 256 + j], go[1 + r] * s2j);
+#pragma unroll
+  for (int r = r0; r < r0 + kCodeRows; ++r) {
+    grad_add(G.p[kWSc1], r * 256 + j, ds1[r] * zsj);
+    grad_add(G.p[kWSc2], r * 256 + j, ds2[r] * zsj);
+    grad_add(G.p[kWTc1], r * 256 + j, dt1[r] * ztj);
+    grad_add(G.p[kWXyz2], r * 512 + 256 + j, gx2[r] * s1j);
+    grad_add(G.p[kWOut], (1 + r) * 512 + 256 + j, go[1 + r] * s2j);
   }
-  if (tid < 16) {
-    const int jb = 16 * y + tid;
-    atomicAdd(&const_cast<float*>(G.p[kBSc1])[jb], ds1[jb]);
-    atomicAdd(&const_cast<float*>(G.p[kBSc2])[jb], ds2[jb]);
-    atomicAdd(&const_cast<float*>(G.p[kBTc1])[jb], dt1[jb]);
-    atomicAdd(&const_cast<float*>(G.p[kWOut])[256 + jb], go[0] * s2[jb]);  // fc_out row 0 (sigma)
-    for (int r = 0; r < 3; ++r) atomicAdd(&const_cast<float*>(G.p[kWRgb])[r * 512 + 256 + jb], grgb[r] * t1[jb]);
+  if (tid < kCodeRows) {
+    const int jb = r0 + tid;
+    grad_add(G.p[kBSc1], jb, ds1[jb]);
+    grad_add(G.p[kBSc2], jb, ds2[jb]);
+    grad_add(G.p[kBTc1], jb, dt1[jb]);
+    grad_add(G.p[kWOut], 256 + jb, go[0] * s2[jb]);  // fc_out row 0 (sigma)
+    for (int r = 0; r < 3; ++r) grad_add(G.p[kWRgb], r * 512 + 256 + jb, grgb[r] * t1[jb]);
   }
 }
 
@@ -2107,7 +2172,8 @@ struct Reducer {
 int reduce(Reducer* rd, const float* part, int64_t parts, int N, int K, float* C, int64_t ldc, hipStream_t st,
            float* C2 = nullptr) {
   if (C2 && !rd) return CN_EINVAL;  // a second target: the queued form only
-  const int64_t nk = (int64_t)N * K, nblk = ceil_div(nk, grad::reduce_vec4(part, nk) ? 256 : 64);  // reduce_block's
+  const int64_t nk = (int64_t)N * K;
+  const int64_t nblk = ceil_div(nk, grad::reduce_block_elems(grad::reduce_groups(parts), grad::reduce_vec4(part, nk)));
   if (!rd) {
     hipLaunchKernelGGL(grad::reduce_partials_kernel, dim3(static_cast<unsigned>(nblk)), dim3(256), 0, st, part, parts,
                        N, K, C, ldc);
@@ -2513,9 +2579,11 @@ extern "C" int64_t cn_code_bias_backward_workspace_floats(int64_t n_codes) {
 
 extern "C" int cn_code_bias_backward_ws(const float* const* params, const float* z_s, const float* z_t,
                                         int64_t n_codes, const float* g_code, float* dz_s, float* dz_t,
-                                        float* const* grads, float* workspace, cn_stream_t stream) {
+                                        float* const* grads, float* workspace, int accumulate_dz,
+                                        cn_stream_t stream) {
   using namespace mlp;
   CN_CHECK_ARG(params && z_s && z_t && g_code && workspace && n_codes > 0 && n_codes < (1ll << 31));
+  CN_CHECK_ARG(accumulate_dz == 0 || accumulate_dz == 1);
   Params P, G = {};
   for (int i = 0; i < CN_NUM_PARAMS; ++i) {
     CN_CHECK_ARG(params[i]);
@@ -2526,7 +2594,8 @@ extern "C" int cn_code_bias_backward_ws(const float* const* params, const float*
   const dim3 grid(static_cast<unsigned>(n_codes), grad::kCodeSlices);
   hipLaunchKernelGGL(grad::code_layers_dz_kernel, grid, dim3(256), 0, st, P, z_s, z_t, g_code, workspace);
   CN_TRY(launch_status());
-  hipLaunchKernelGGL(grad::code_outer_kernel, grid, dim3(256), 0, st, P, z_s, z_t, g_code, workspace, dz_s, dz_t, G);
+  hipLaunchKernelGGL(grad::code_outer_kernel, grid, dim3(256), 0, st, P, z_s, z_t, g_code, workspace, dz_s, dz_t, G,
+                     accumulate_dz);
   return launch_status();
 }
 

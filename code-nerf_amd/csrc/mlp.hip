@@ -415,12 +415,26 @@ extern "C" int cn_code_bias(const float* const* params, const float* z_s, const 
 extern "C" int cn_field_prepare(const float* const* params, const float* z_s, const float* z_t, int64_t n_codes,
                                 float* code_bias, float* packed, float* packed_t, float* zero, int64_t n_zero,
                                 cn_stream_t stream) {
-  Params P;
-  if (make_params(params, &P) != CN_OK) return CN_EINVAL;
-  CN_CHECK_ARG(n_zero >= 0 && (n_zero == 0 || zero));
-  CN_CHECK_ARG(!code_bias || (z_s && z_t && n_codes > 0 && n_codes * kCbSlices + 256 <= 0x7fffffff));
-  return launch_field_prepare_w16(P, z_s, z_t, n_codes, code_bias, packed, packed_t, zero, n_zero,
-                                  cn::as_stream(stream));
+  const cn_field_prep m = {params, code_bias, packed, packed_t, zero, n_zero};
+  return cn_field_prepare_models(&m, 1, z_s, z_t, n_codes, stream);
+}
+
+extern "C" int cn_field_prepare_models(const cn_field_prep* models, int n_models, const float* z_s, const float* z_t,
+                                       int64_t n_codes, cn_stream_t stream) {
+  CN_CHECK_ARG(models && n_models >= 1 && n_models <= 2);
+  PrepareModel pm[2];
+  for (int k = 0; k < n_models; ++k) {
+    const cn_field_prep& m = models[k];
+    if (make_params(m.params, &pm[k].P) != CN_OK) return CN_EINVAL;
+    CN_CHECK_ARG(m.n_zero >= 0 && (m.n_zero == 0 || m.zero));
+    CN_CHECK_ARG(!m.code_bias || (z_s && z_t && n_codes > 0 && n_codes * kCbSlices + 256 <= 0x7fffffff));
+    pm[k].code_bias = m.code_bias;
+    pm[k].packed = m.packed;
+    pm[k].packed_t = m.packed_t;
+    pm[k].zero = m.zero;
+    pm[k].n_zero = m.n_zero;
+  }
+  return launch_field_prepare_w16(pm, n_models, z_s, z_t, n_codes, cn::as_stream(stream));
 }
 
 extern "C" int cn_mlp_forward(const float* packed, int fmt, const float* code_bias,

@@ -281,9 +281,18 @@ int launch_pack_w16(const Params& P, float* packed, hipStream_t st);
 int launch_field_w16(int mode, FieldArgs& a, hipStream_t st);  // a.masks: also the ReLU masks
 int64_t mask_words_w16(int64_t m);
 int launch_pack_w16t(const Params& P, float* packed, hipStream_t st);
-// code_bias + the CN_FMT_F32_W16 / _T packs + a zeroed buffer in one launch (any of them null: skipped)
-int launch_field_prepare_w16(const Params& P, const float* z_s, const float* z_t, int64_t n_codes, float* code_bias,
-                             float* packed, float* packed_t, float* zero, int64_t n_zero, hipStream_t st);
+// code_bias + the CN_FMT_F32_W16 / _T packs + a zeroed buffer (any of them null: skipped), for one or
+// two models on the same codes, in one launch
+struct PrepareModel {
+  Params P;
+  float* code_bias;
+  float* packed;
+  float* packed_t;
+  float* zero;
+  int64_t n_zero;
+};
+int launch_field_prepare_w16(const PrepareModel* models, int n_models, const float* z_s, const float* z_t,
+                             int64_t n_codes, hipStream_t st);
 int launch_field_w16_bwd(int mode, FieldArgs& a, hipStream_t st);
 // The training backwards' no-geometry schedule (no d ro / d rd / d pts wanted) unless CN_BWD_NOGEO=0.
 bool nogeo_enabled();

@@ -1002,8 +1002,18 @@ struct Prepare {
 constexpr int kPrepThreads = 512;
 static_assert(kPrepThreads == kCbThreads, "code_bias_block's workgroup size");
 
-__global__ __launch_bounds__(kPrepThreads) void field_prepare_kernel(Prepare p) {
-  unsigned b = blockIdx.x;
+// Up to two models' preparations in one launch (a render's coarse and fine fields share the codes):
+// blocks first[1] .. belong to the second.
+constexpr int kMaxPrepModels = 2;
+struct PrepareSet {
+  Prepare p[kMaxPrepModels];
+  unsigned first[kMaxPrepModels];
+};
+
+__global__ __launch_bounds__(kPrepThreads) void field_prepare_kernel(PrepareSet set) {
+  const int k = blockIdx.x >= set.first[1] ? 1 : 0;
+  const Prepare& p = set.p[k];
+  unsigned b = blockIdx.x - set.first[k];
   if (b < p.nb_cb) {
     code_bias_block(p.P, p.z_s, p.z_t, p.code_bias, b);
     return;
@@ -1552,15 +1562,25 @@ int launch_field_w16(int mode, FieldArgs& a, hipStream_t st) {
 
 int64_t mask_words_w16(int64_t m) { return cn::ceil_div(m, w16::kTile) * w16::kMaskWordsPerTile; }
 
-int launch_field_prepare_w16(const Params& P, const float* z_s, const float* z_t, int64_t n_codes, float* code_bias,
-                             float* packed, float* packed_t, float* zero, int64_t n_zero, hipStream_t st) {
-  w16::Prepare p{P, z_s, z_t, code_bias, packed, packed_t, zero, n_zero, 0u, 0u, 0u};
-  p.nb_cb = code_bias ? static_cast<unsigned>(n_codes * kCbSlices) : 0u;
-  p.nb_pack = 64;  // 64 x 512 threads over each pack's 327,680 floats: 10 elements per thread
-  p.nb_zero = n_zero > 0 ? static_cast<unsigned>(std::min<int64_t>(cn::ceil_div(n_zero, w16::kPrepThreads), 64)) : 0u;
-  const unsigned grid = p.nb_cb + (packed ? p.nb_pack : 0u) + (packed_t ? p.nb_pack : 0u) + p.nb_zero;
+int launch_field_prepare_w16(const PrepareModel* models, int n_models, const float* z_s, const float* z_t,
+                             int64_t n_codes, hipStream_t st) {
+  if (n_models < 1 || n_models > w16::kMaxPrepModels) return CN_EINVAL;
+  w16::PrepareSet set = {};
+  unsigned grid = 0;
+  for (int k = 0; k < n_models; ++k) {
+    const PrepareModel& m = models[k];
+    w16::Prepare& p = set.p[k];
+    p = w16::Prepare{m.P, z_s, z_t, m.code_bias, m.packed, m.packed_t, m.zero, m.n_zero, 0u, 0u, 0u};
+    p.nb_cb = m.code_bias ? static_cast<unsigned>(n_codes * kCbSlices) : 0u;
+    p.nb_pack = 64;  // 64 x 512 threads over each pack's 327,680 floats: 10 elements per thread
+    p.nb_zero = m.n_zero > 0 ? static_cast<unsigned>(std::min<int64_t>(cn::ceil_div(m.n_zero, w16::kPrepThreads), 64))
+                             : 0u;
+    set.first[k] = grid;
+    grid += p.nb_cb + (m.packed ? p.nb_pack : 0u) + (m.packed_t ? p.nb_pack : 0u) + p.nb_zero;
+  }
+  if (n_models == 1) set.first[1] = grid;   // no block reaches the second slot
   if (grid == 0) return CN_OK;
-  hipLaunchKernelGGL(w16::field_prepare_kernel, dim3(grid), dim3(w16::kPrepThreads), 0, st, p);
+  hipLaunchKernelGGL(w16::field_prepare_kernel, dim3(grid), dim3(w16::kPrepThreads), 0, st, set);
   return cn::launch_status();
 }
 

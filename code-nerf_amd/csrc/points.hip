@@ -2,9 +2,10 @@
 //
 // sample_uniform is a pure stream (12 B ray + 4 B bin in, 16 B per sample out).
 // sample_pdf gives one wavefront to one ray: the ray's cdf, bins and merged
-// depth list live in LDS, searchsorted is a binary search there, and the
-// final sort is a rank sort (every value counts the values that precede it),
-// which handles unsorted perturbed fine samples and ties without a network.
+// depth list live in LDS, the cdf is a wave scan (exact in double, so the
+// sequential loop's bits), searchsorted is a binary search there, and the
+// final sort a bitonic network over (value, position) keys -- the stable sort
+// of the unsorted perturbed fine samples, ties included.
 #include "cn_common.h"
 
 namespace {
@@ -125,7 +126,34 @@ __device__ float torch_cpu_row_sum(const float* x, int n) {
   return fin;
 }
 
+// torch_cpu_row_sum for one wave (every lane returns it): the eight column chains of the n >= 8 path
+// run in lanes 0..7, every lane then folds the scalar tail and the eight chains in torch's order.
+__device__ float torch_cpu_row_sum_wave(const float* x, int n, int lane) {
+  if (n < 8) return torch_cpu_row_sum(x, n);
+  const int nv = n / 8, s = nv / 4;
+  float p = 0.0f;
+  if (lane < 8) {
+    const int k = lane;
+    float a[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    for (int i = 0; i < s; ++i)
+      for (int j = 0; j < 4; ++j) a[j] = __fadd_rn(a[j], x[(4 * i + j) * 8 + k]);
+    p = a[0];
+    for (int i = 4 * s; i < nv; ++i) p = __fadd_rn(p, x[8 * i + k]);
+    p = __fadd_rn(__fadd_rn(__fadd_rn(p, a[1]), a[2]), a[3]);
+  }
+  float fin = 0.0f;
+  for (int k = 8 * nv; k < n; ++k) fin = __fadd_rn(fin, x[k]);
+  for (int k = 0; k < 8; ++k) fin = __fadd_rn(fin, __shfl(p, k));
+  return fin;
+}
+
 // point_sampler.py:84-118, one wave per ray.
+//   pdf / cdf: torch's CPU cumsum adds the fp32 pdf in double and rounds every prefix.  When every
+//   nonzero |pdf| >= 2^-28 (so all are multiples of 2^-51) and sum |pdf| < 1.5 (every prefix below
+//   2^2), each double prefix is EXACT -- whatever the order of the additions -- so a wave scan gives
+//   the sequential loop's bits; a ray outside those bounds takes the sequential loop in lane 0.
+//   sort(cat(z, samples)) (:116): a bitonic network in LDS over (value, position) keys padded to a
+//   power of two with +inf -- ties ordered by position, i.e. the stable sort -- and coalesced stores.
 __global__ __launch_bounds__(256) void sample_pdf_kernel(
     const float* __restrict__ ro, const float* __restrict__ rd, const float* __restrict__ weights,
     int64_t w_stride, const float* __restrict__ z, int64_t n_rays, int nc, int nf,
@@ -134,6 +162,7 @@ __global__ __launch_bounds__(256) void sample_pdf_kernel(
   __shared__ float s_cdf[kPdfWaves][256];
   __shared__ float s_mid[kPdfWaves][256];
   __shared__ float s_val[kPdfWaves][kPdfMaxN];
+  __shared__ int s_idx[kPdfWaves][kPdfMaxN];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int64_t r_raw = blockIdx.x * (int64_t)kPdfWaves + wv;
@@ -142,11 +171,14 @@ __global__ __launch_bounds__(256) void sample_pdf_kernel(
   float* cdf = s_cdf[wv];
   float* mid = s_mid[wv];
   float* val = s_val[wv];
+  int* idx = s_idx[wv];
   const float* zr = z + r * nc;
   const float* wr = weights + r * w_stride;
   const int nw = nc - 2;      // pdf entries
   const int ncdf = nc - 1;    // cdf / bins entries
   const int n = nc + nf;
+  int n2 = 1;
+  while (n2 < n) n2 <<= 1;
 
   // bins = 0.5 * (z[1:] + z[:-1]) (:85); coarse depths into the merge list
   for (int j = lane; j < ncdf; j += 64) mid[j] = __fmul_rn(0.5f, __fadd_rn(zr[j + 1], zr[j]));
@@ -155,16 +187,47 @@ __global__ __launch_bounds__(256) void sample_pdf_kernel(
   // w = weights + 1e-5 (:86), staged in cdf[1..nw]
   for (int j = lane; j < nw; j += 64) cdf[j + 1] = __fadd_rn(wr[j], 1e-5f);
   __syncthreads();
-  if (lane == 0) {
-    // pdf = w / sum(w) (:87) with torch's CPU summation order, then
-    // cdf = [0, cumsum(pdf)] (:88-89): torch's CPU cumsum accumulates in double
-    // and rounds every prefix.  A few hundred scalar ops per ray.
-    const float total = torch_cpu_row_sum(cdf + 1, nw);
-    double acc = 0.0;
-    cdf[0] = 0.0f;
-    for (int j = 1; j <= nw; ++j) {
-      acc += static_cast<double>(__fdiv_rn(cdf[j], total));
-      cdf[j] = static_cast<float>(acc);
+  {
+    // pdf = w / sum(w) (:87), cdf = [0, cumsum(pdf)] (:88-89)
+    const float total = torch_cpu_row_sum_wave(cdf + 1, nw, lane);
+    float pdf[4];            // entries lane + 64 q (nw <= 254)
+    bool ok = true;
+    float asum = 0.0f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = lane + 64 * q;
+      pdf[q] = j < nw ? __fdiv_rn(cdf[j + 1], total) : 0.0f;
+      const float a = fabsf(pdf[q]);
+      ok = ok && (a == 0.0f || a >= 0x1p-28f);     // false for NaN
+      asum += a;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) asum += __shfl_xor(asum, off);
+    ok = __all(ok) && asum < 1.5f;
+    if (ok) {
+      double carry = 0.0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (64 * q >= nw) break;                    // wave-uniform
+        const int j = lane + 64 * q;
+        double v = static_cast<double>(pdf[q]);
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+          const double t = __shfl_up(v, off);
+          if (lane >= off) v += t;
+        }
+        v += carry;
+        if (j < nw) cdf[j + 1] = static_cast<float>(v);
+        carry = __shfl(v, 63);
+      }
+      if (lane == 0) cdf[0] = 0.0f;
+    } else if (lane == 0) {
+      double acc = 0.0;
+      cdf[0] = 0.0f;
+      for (int j = 1; j <= nw; ++j) {
+        acc += static_cast<double>(__fdiv_rn(cdf[j], total));
+        cdf[j] = static_cast<float>(acc);
+      }
     }
   }
   __syncthreads();
@@ -186,21 +249,37 @@ __global__ __launch_bounds__(256) void sample_pdf_kernel(
     const float b0 = mid[below], b1 = mid[above];
     val[nc + i] = __fadd_rn(b0, __fmul_rn(t, __fsub_rn(b1, b0)));
   }
+  for (int i = lane; i < n2; i += 64) {
+    idx[i] = i;
+    if (i >= n) val[i] = __builtin_inff();
+  }
   __syncthreads();
-  if (!valid) return;
 
-  // sort(cat(z, samples)) (:116): stable rank of every value
-  for (int i = lane; i < n; i += 64) {
-    const float v = val[i];
-    int pos = 0;
-    for (int k = 0; k < n; ++k) {
-      const float w = val[k];
-      pos += (w < v) || (w == v && k < i);
+  // sort(cat(z, samples)) (:116): bitonic over (value, position)
+  for (int k = 2; k <= n2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int t = lane; t < (n2 >> 1); t += 64) {
+        const int a = 2 * t - (t & (j - 1)), b = a + j;
+        const float va = val[a], vb = val[b];
+        const int ia = idx[a], ib = idx[b];
+        const bool a_after = va > vb || (va == vb && ia > ib);
+        if (a_after == ((a & k) == 0)) {
+          val[a] = vb;
+          val[b] = va;
+          idx[a] = ib;
+          idx[b] = ia;
+        }
+      }
+      __syncthreads();
     }
-    float* zo = z_out + r * n;
-    zo[pos] = v;
+  }
+  if (!valid) return;
+  float* zo = z_out + r * n;
+  for (int p = lane; p < n; p += 64) {
+    const float v = val[p];
+    zo[p] = v;
     if (pts_out) {
-      float* po = pts_out + (r * n + pos) * 3;
+      float* po = pts_out + (r * n + p) * 3;
 #pragma unroll
       for (int j = 0; j < 3; ++j) po[j] = cn::mul_add_rn(rd[3 * r + j], v, ro[3 * r + j]);
     }

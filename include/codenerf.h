@@ -207,6 +207,22 @@ int cn_field_prepare(const float* const* params, const float* z_s, const float* 
                      float* code_bias, float* packed, float* packed_t, float* zero, int64_t n_zero,
                      cn_stream_t stream);
 
+/* One model's part of cn_field_prepare_models: the arguments of cn_field_prepare. */
+typedef struct cn_field_prep {
+  const float* const* params;
+  float* code_bias;
+  float* packed;
+  float* packed_t;
+  float* zero;
+  int64_t n_zero;
+} cn_field_prep;
+
+/* cn_field_prepare for n_models (1 or 2) models on the same codes in ONE launch: a render's coarse
+ * and fine fields (nerf/__init__.py:74-91 runs both on one object's codes) prepared together before
+ * the coarse field.  Bitwise each model's cn_field_prepare. */
+int cn_field_prepare_models(const cn_field_prep* models, int n_models, const float* z_s, const float* z_t,
+                            int64_t n_codes, cn_stream_t stream);
+
 /* CodeNeRFModel.forward(z_s, z_t, x), model.py:160-194, for pre-encoded rows.
  * x: (m, 90) = [xyz 63 | dir 27]; code row of row i = code_index ? code_index[i]
  * : (n_codes == 1 ? 0 : i); raw: (m, 4) = [rgb_raw(3), sigma_raw]. */
@@ -388,12 +404,15 @@ int cn_code_bias_backward(const float* const* params, const float* z_s, const fl
                           cn_stream_t stream);
 /* The same backward in two launches with a caller-provided workspace
  * (cn_code_bias_backward_workspace_floats(n_codes) floats): each code's layers and
- * reductions are formed once, split over 16 workgroups, instead of once per workgroup.
- * Bitwise the same results as cn_code_bias_backward. */
+ * reductions are formed once, split over 64 workgroups, instead of once per workgroup.
+ * Bitwise the same results as cn_code_bias_backward.  accumulate_dz = 1: dz_s / dz_t +=
+ * the code gradients instead of = (the training step points them at the code tables'
+ * gradient rows, so the coarse and fine fields' code gradients add up in place --
+ * ShapeTextureEmbedding.forward in model.py:102-105 is the lookup they flow back to). */
 int64_t cn_code_bias_backward_workspace_floats(int64_t n_codes);
 int cn_code_bias_backward_ws(const float* const* params, const float* z_s, const float* z_t, int64_t n_codes,
                              const float* g_code, float* dz_s, float* dz_t, float* const* grads, float* workspace,
-                             cn_stream_t stream);
+                             int accumulate_dz, cn_stream_t stream);
 
 /* Backward of volume_render (volumetric_render.py:36-66) w.r.t. raw and rd
  * (z is detached in the reference).  Any of g_rgb (R,3), g_disp, g_acc, g_depth

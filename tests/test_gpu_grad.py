@@ -731,10 +731,11 @@ def test_field_backward_train_nogeo_bitwise(dev, precision, mode, r, s, n_codes)
 
 @pytest.mark.parametrize("n_codes,want_grads", [(1, True), (5, True), (5, False)])
 def test_code_bias_backward_two_launch_bitwise(dev, n_codes, want_grads):
-    """cn_code_bias_backward_ws (code layers split over 16 workgroups per code, two launches) gives
+    """cn_code_bias_backward_ws (code layers split over 64 workgroups per code, two launches) gives
     bitwise the results of the single-launch cn_code_bias_backward: dz_s, dz_t, and with one code
     every accumulated parameter gradient (with several codes both add their float atomics in no
-    fixed order: 1e-6 relative); a code no sample used (g row zero) gets dz = 0."""
+    fixed order: 1e-6 relative); a code no sample used (g row zero) gets dz = 0.  accumulate_dz
+    (dz_into): the same dz added onto what the rows held, bit for bit, an unused code's rows kept."""
     from codenerf import ops, synthetic
     m = model(dev, 0)
     params = [p.detach() for p in m.param_list()]
@@ -753,6 +754,11 @@ def test_code_bias_backward_two_launch_bitwise(dev, n_codes, want_grads):
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
     if n_codes > 1:
         assert not b[0][1].any() and not b[1][1].any()
+    base = [(torch.randn(n_codes, 256, generator=g) * 1e-2).to(dev) for _ in range(2)]
+    into = [t.clone() for t in base]
+    r = ops.code_bias_backward(params, zs, zt, gc, None, dz_into=tuple(into))
+    assert r[0] is into[0] and r[1] is into[1]
+    assert torch.equal(into[0], base[0] + b[0]) and torch.equal(into[1], base[1] + b[1])
     if want_grads:
         for k, (x, y) in enumerate(zip(a[2], b[2])):
             if n_codes == 1:
@@ -782,6 +788,23 @@ def test_field_prepare_bitwise(dev, n_codes, pack, pack_t):
     if pack_t:
         assert torch.equal(pkt, ops.mlp_pack(params, "f32_w16_t"))
     assert zero.shape == (nz,) and not zero.any()
+
+
+@pytest.mark.parametrize("n_codes", [1, 3])
+def test_field_prepare_models_bitwise(dev, n_codes):
+    """cn_field_prepare_models (a render's coarse and fine fields prepared in one launch) equals each
+    model's cn_field_prepare bit for bit, with different pack / zero requests per model."""
+    from codenerf import ops, synthetic
+    ps = [[p.detach() for p in model(dev, s).param_list()] for s in (3, 4)]
+    zs, zt = synthetic.latent_codes(9, n_codes).to(dev), synthetic.latent_codes(10, n_codes).to(dev)
+    reqs = [(ps[0], True, False, n_codes * 520), (ps[1], False, True, 777)]
+    got = ops.field_prepare_models(reqs, zs, zt)
+    for (params, pack, pack_t, nz), out in zip(reqs, got):
+        ref = ops.field_prepare(params, zs, zt, pack=pack, pack_t=pack_t, n_zero=nz)
+        for a, b in zip(out, ref):
+            assert (a is None) == (b is None)
+            if a is not None:
+                assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("far", [False, True])

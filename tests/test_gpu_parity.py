@@ -156,6 +156,46 @@ def test_sample_pdf_strided_weights_and_indices(dev):
     assert maxdiff(zf, zf_ref) == 0.0   # same sum order, double cumsum, same searchsorted -> same bits
 
 
+@pytest.mark.parametrize("n,nc,nf", [(37, 3, 5), (130, 13, 7), (257, 64, 64), (100, 64, 128), (64, 128, 128),
+                                     (33, 256, 256)])
+def test_sample_pdf_scan_and_sort_bitwise(dev, n, nc, nf):
+    """cn_sample_pdf's wave-parallel cdf (a double scan, exact inside its bounds) and bitonic merge sort vs
+    the oracle, bit for bit: per-ray weight regimes in one launch -- heavy-tailed, all zero (uniform pdf),
+    one spike of 1e9 (pdf entries below 2^-28: the sequential cumsum fallback) and random scale --, depth
+    lists with repeated values and draws quantised to 1/8 (ties between coarse and fine depths and among
+    the fine ones), n not a multiple of the 4 rays per workgroup."""
+    from oracle import codenerf_oracle as O
+    from codenerf import ops
+    g = torch.Generator().manual_seed(nc * 1000 + nf)
+    ro, rd = torch.randn(n, 3, generator=g), torch.randn(n, 3, generator=g)
+    w = torch.rand(n, nc, generator=g) ** 4
+    kind = torch.arange(n) % 4
+    w[kind == 1] = 0.0
+    spike = w[kind == 2]
+    spike.zero_()
+    spike[:, nc // 2] = 1e9
+    w[kind == 2] = spike
+    w[kind == 3] *= torch.rand(n, 1, generator=g)[kind == 3] * 50.0
+    z = O.depth_bins(nc, 0.8, 1.8, "lindepth")["z"].expand(n, nc).contiguous()
+    z[::5, 1:] = torch.maximum(z[::5, 1:], z[::5, :-1]).clone()
+    z[::5, nc // 2] = z[::5, nc // 2 - 1] if nc > 2 else z[::5, nc // 2]
+    u = torch.rand(n, nf, generator=g)
+    u[::3] = torch.floor(u[::3] * 8.0) / 8.0
+    pf_ref, zf_ref = O.sample_pdf(ro, rd, w[..., 1:-1], z, nf, u)
+    pf, zf = ops.sample_pdf(ro.to(dev), rd.to(dev), w.to(dev)[..., 1:-1], z.to(dev), nf, u.to(dev))
+    assert torch.equal(zf.cpu(), zf_ref)
+    assert torch.equal(pf.cpu(), pf_ref)
+    # u = None: the kernel's linspace(0, 1, nf) -- torch's symmetric two-half formula, each op rounded
+    # (linspace01); torch's own vectorised CPU linspace may differ by an ulp for nf >= 64, so the
+    # oracle gets the kernel's u
+    i = torch.arange(nf, dtype=torch.float32)
+    step = torch.tensor(1.0) / float(max(nf - 1, 1))
+    u_lin = torch.where(i < nf // 2, step * i, 1.0 - step * (nf - 1 - i)) if nf > 1 else torch.zeros(1)
+    _, zl_ref = O.sample_pdf(ro, rd, w[..., 1:-1], z, nf, u_lin.expand(n, nf).contiguous())
+    _, zl = ops.sample_pdf(ro.to(dev), rd.to(dev), w.to(dev)[..., 1:-1], z.to(dev), nf, None, want_pts=False)
+    assert torch.equal(zl.cpu(), zl_ref)
+
+
 # ---------------------------------------------------------------- encoding
 
 

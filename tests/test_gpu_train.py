@@ -342,6 +342,93 @@ def test_host_id_lookup_bitwise(dev, mixed):
             assert torch.equal(p0[k], p1[k]), ("param", k)
 
 
+@pytest.mark.parametrize("precision,off", [("f32", "sink"), ("bf16x3", "sink"), ("f32", "prefetch")])
+def test_step_fusions_bitwise(dev, monkeypatch, precision, off):
+    """The training step's launch merges against the plain route, three steps of one-object chunks, every
+    gradient and parameter bit-identical:
+    * "sink": both fields' code backwards add their dz into the code tables' gradient rows in place
+      (CodeGradSink, accumulate_dz; two such launches per step, the tables' .grad the optimiser's flat
+      slices) vs dz returned, summed by autograd and added into the row (3xbf16: to 1e-5, its fused
+      backward's g_code is a float-atomic sum);
+    * "prefetch": both fields' pre-field launches as one (cn_field_prepare_models, once per step, no
+      per-field cn_field_prepare) vs one per field."""
+    from codenerf import autograd as A, ops, train as T
+    from codenerf.models import model as M
+    from codenerf.nerf import PointSampler
+    real_cb, real_pm, real_fp = ops.code_bias_backward, ops.field_prepare_models, ops.field_prepare
+    calls = {"sunk": [], "models": 0, "single": 0}
+
+    def spy_cb(*a, **k):
+        calls["sunk"].append(k.get("dz_into") is not None)
+        return real_cb(*a, **k)
+
+    def spy_pm(*a, **k):
+        calls["models"] += 1
+        return real_pm(*a, **k)
+
+    def spy_fp(*a, **k):
+        calls["single"] += 1
+        return real_fp(*a, **k)
+    monkeypatch.setattr(ops, "code_bias_backward", spy_cb)
+    monkeypatch.setattr(ops, "field_prepare_models", spy_pm)
+    monkeypatch.setattr(ops, "field_prepare", spy_fp)
+    S = 32 if precision == "bf16x3" else 16
+    runs = []
+    for on in (True, False):
+        if not on and off == "sink":
+            monkeypatch.setattr(M.CodeGradSink, "rows", lambda self: None)
+        if not on and off == "prefetch":
+            monkeypatch.setattr(A, "prefetch_render_prepares", lambda *a, **k: False)
+        calls.update(sunk=[], models=0, single=0)
+        torch.manual_seed(3)
+        models = _train_models(dev, 4)
+        for key in ("nerf_coarse", "nerf_fine"):
+            models[key].precision = models[key].train_precision = precision
+        opt, sched = T.prepare_optimizer(_opt_cfg(), models)
+        ps = PointSampler(S, S, 0.8, 1.8, spacing_mode="lindepth", perturb=False, dtype=torch.float32, device=dev)
+        g = torch.Generator().manual_seed(5)
+        grads = []
+        for step in range(3):
+            n = 192
+            ro = (torch.randn(n, 3, generator=g) * 0.1 + torch.tensor([0.0, 0.0, 1.3])).to(dev)
+            rd = (torch.randn(n, 3, generator=g) * 0.2 + torch.tensor([0.0, 0.0, -1.0])).to(dev)
+            ids_h = torch.full((n,), (step * 3) % 4)
+            ids = ids_h.to(dev)
+            ids._cn_host_ids = ids_h.numpy()
+            tgt = torch.rand(n, 4, generator=g).to(dev)
+            T.train_minibatch(models, opt, sched, ps, embedders(dev), ro, rd, ids, tgt, 1e-5)
+            grads.append({f"{k}.{n_}": p.grad.detach().clone() for k, m in models.items()
+                          for n_, p in m.named_parameters() if p.grad is not None})
+            if on and off == "sink":
+                flat = opt.flat_buffers()["grad"]
+                lo, hi = flat.data_ptr(), flat.data_ptr() + flat.numel() * 4
+                for w in (models["embedding"].shape_embedding.weight, models["embedding"].texture_embedding.weight):
+                    assert lo <= w.grad.data_ptr() < hi, "the table's .grad is not the optimiser's flat slice"
+        if off == "sink":
+            assert calls["sunk"] == [on] * 6, calls
+        elif precision == "f32":
+            assert (calls["models"], calls["single"]) == ((3, 0) if on else (0, 6)), calls
+        torch.cuda.synchronize()
+        params = {f"{k}.{n_}": p.detach().clone() for k, m in models.items() for n_, p in m.named_parameters()}
+        runs.append((grads, params))
+    (g0, p0), (g1, p1) = runs
+    for step, (a, b) in enumerate(zip(g0, g1)):
+        assert a.keys() == b.keys()
+        for k in a:
+            if precision == "f32":
+                assert torch.equal(a[k], b[k]), ("grad", k)
+            elif step == 0:
+                # the 3xbf16 backward sums g_code with LDS float atomics: not bit-reproducible, and after
+                # a step the runs' parameters differ in their last bits (the later steps' ReLU decisions
+                # may then differ too), so only the first step's gradients are compared, to 1e-5
+                close(b[k], a[k], 1e-5, ("grad", k))
+    for k in p0:
+        if precision == "f32":
+            assert torch.equal(p0[k], p1[k]), ("param", k)
+        else:
+            assert (p0[k] - p1[k]).abs().max().item() <= 2.05 * 3 * 1e-3, ("param", k)
+
+
 def test_train_iteration_runs(dev):
     from codenerf import nerf as N, synthetic, train as T
     from codenerf.evaluate import pose_spherical
