@@ -408,6 +408,7 @@ def eval_bench(dev, rs, emb, models, iters, precision, graph=False):
     perturbed samples, forward + backward through the HIP kernels into (codes, theta, phi, rho),
     AdamW step.  Weights frozen (their grads are never read by the reference's optimiser)."""
     import numpy as np
+    from codenerf.autograd import backward_from
     from codenerf.evaluate import GraphedEvalStep, eval_step_loss, step_psnr_tensor
     from codenerf.nerf import PointSampler
     from codenerf.optim import AdamW
@@ -441,7 +442,7 @@ def eval_bench(dev, rs, emb, models, iters, precision, graph=False):
         def it():
             loss, logs = eval_step_loss(th, ph, rh, zs, zt, target, (rs, ps), emb, mods, 1e-5)
             opt.zero_grad()
-            loss.backward()
+            backward_from(loss)
             opt.step()
             step_psnr_tensor(logs)  # eval.py:159's per-iteration psnr, on the device (no read-back)
 

@@ -44,7 +44,12 @@ _fp = ctypes.POINTER(ctypes.c_float)
 class FieldPrep(ctypes.Structure):
     """cn_field_prep (include/codenerf.h): one model's part of cn_field_prepare_models."""
     _fields_ = [("params", ctypes.POINTER(_p)), ("code_bias", _p), ("packed", _p), ("packed_t", _p), ("zero", _p),
-                ("n_zero", _i64)]
+                ("n_zero", _i64), ("code_act", _p)]
+
+
+class CodeDzJob(ctypes.Structure):
+    """cn_code_dz_job (include/codenerf.h): one field's part of cn_code_dz."""
+    _fields_ = [("params", ctypes.POINTER(_p)), ("g_code", _p), ("workspace", _p)]
 
 
 # name -> (restype, argtypes); mirrors include/codenerf.h one to one.
@@ -101,6 +106,8 @@ SIGNATURES = {
                                   _p]),
     "cn_code_bias_backward": (_i, [ctypes.POINTER(_p), _p, _p, _i64, _p, _p, _p, ctypes.POINTER(_p), _p]),
     "cn_code_bias_backward_workspace_floats": (_i64, [_i64]),
+    "cn_code_bias_backward_act": (_i, [ctypes.POINTER(_p), _p, _p, _i64, _p, _p, ctypes.POINTER(_p), _p, _p]),
+    "cn_code_dz": (_i, [ctypes.POINTER(CodeDzJob), _i, _i64, _p, _p, _i, _p]),
     "cn_code_bias_backward_ws": (_i, [ctypes.POINTER(_p), _p, _p, _i64, _p, _p, _p, ctypes.POINTER(_p), _p, _i, _p]),
     "cn_volume_render_backward": (_i, [_p, _p, _p, _i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p]),
     "cn_ray_bundle_backward": (_i, [_p, _i64, _i64, _p, _p, _p, _p]),

@@ -55,16 +55,16 @@ def _packed(owner, params, fmt: str):
 def _prepare_w16(owner, params, z_s, z_t, n_zero: int):
     """The fp32 training step's per-model preparation in ONE launch (ops.field_prepare): the code terms,
     the forward and backward packs where the cache lacks them (after every optimiser step), and a
-    zeroed g_code accumulator for the fused backward -> (cb, packed "f32_w16", zero)."""
+    zeroed g_code accumulator for the fused backward -> (cb, packed "f32_w16", zero, code-layer activations)."""
     cache, sig = _pack_cache(owner, params)
     have = {f: (cache.get(f) is not None and cache[f][0] == sig) for f in ("f32_w16", "f32_w16_t")}
-    cb, pk, pkt, zero = ops.field_prepare(params, z_s, z_t, pack=not have["f32_w16"], pack_t=not have["f32_w16_t"],
-                                          n_zero=n_zero)
+    ((cb, pk, pkt, zero, act),) = ops.field_prepare_models(
+        [(params, not have["f32_w16"], not have["f32_w16_t"], n_zero)], z_s, z_t, want_act=True)
     if pk is not None:
         cache["f32_w16"] = (sig, pk)
     if pkt is not None:
         cache["f32_w16_t"] = (sig, pkt)
-    return cb, cache["f32_w16"][1], zero
+    return cb, cache["f32_w16"][1], zero, act
 
 
 def _zkey(z_s, z_t):
@@ -103,24 +103,37 @@ def prefetch_prepares(fields, z_s, z_t) -> bool:
         pack = mode == "train_w16" and not have["f32_w16"]
         pack_t = mode == "train_w16" and not have["f32_w16_t"]
         entries.append((cache, sig, mode, n_zero, params, pack, pack_t))
-    outs = ops.field_prepare_models([(e[4], e[5], e[6], e[3]) for e in entries], z_s, z_t)
+    outs = ops.field_prepare_models([(e[4], e[5], e[6], e[3]) for e in entries], z_s, z_t, want_act=True)
     key = _zkey(z_s, z_t)
-    for (cache, sig, mode, n_zero, _, _, _), (cb, pk, pkt, zero) in zip(entries, outs):
+    for (cache, sig, mode, n_zero, _, _, _), (cb, pk, pkt, zero, act) in zip(entries, outs):
         if pk is not None:
             cache["f32_w16"] = (sig, pk)
         if pkt is not None:
             cache["f32_w16_t"] = (sig, pkt)
-        cache["prep"] = ((sig, mode, n_zero, key), (cb, zero))
+        cache["prep"] = ((sig, mode, n_zero, key), (cb, zero, act))
     return True
 
 
 def _take_prepared(owner, params, z_s, z_t, mode, n_zero):
-    """This field's part of a prefetch_prepares launch -> (cb, zero), or None (none, or stale)."""
+    """This field's part of a prefetch_prepares launch -> (cb, zero, act), or None (none, or stale)."""
     cache, sig = _pack_cache(owner, params)
     ent = cache.pop("prep", None)
     if ent is None or ent[0] != (sig, mode, n_zero, _zkey(z_s, z_t)):
         return None
     return ent[1]
+
+
+_ONES = {}
+
+
+def backward_from(loss) -> None:
+    """loss.backward() for a scalar loss with a cached device 1.0 as its seed gradient: torch's
+    ones_like seed is a fill launch per step (train.py:111, eval.py:160)."""
+    key = (loss.device, loss.dtype)
+    one = _ONES.get(key)
+    if one is None:
+        one = _ONES[key] = torch.ones((), device=loss.device, dtype=loss.dtype)
+    loss.backward(one if loss.dim() == 0 else one.expand_as(loss))
 
 
 def _needs_grad(*ts) -> bool:
@@ -280,9 +293,19 @@ class _FieldMeta:
         self.sink = sink       # models.model.CodeGradSink of the code rows, or None
 
 
-def _code_grads(meta, params, z_s, z_t, g_code, pg, want_z):
-    """cn_code_bias_backward_ws -> (dz_s, dz_t); (None, None) when they were added in place into the code
-    tables' gradient rows (meta.sink: the coarse and fine fields of a one-object chunk add up there)."""
+def _code_grads(meta, params, z_s, z_t, g_code, pg, want_z, act=None):
+    """The code backward -> (dz_s, dz_t); (None, None) when they go in place into the code tables'
+    gradient rows (meta.sink: the coarse and fine fields of a one-object chunk add up there).  With the
+    forward's code-layer activations (act, from the preparation launch): cn_code_bias_backward_act now
+    and cn_code_dz -- for a sink deferred, so both fields' dz are one launch (CodeGradSink.flush);
+    otherwise the recomputing two-launch form (cn_code_bias_backward_ws)."""
+    if act is not None:
+        ws = ops.code_ds_outer(params, z_s, z_t, act, g_code, pg)
+        if not want_z:
+            return None, None
+        if meta.sink is not None and meta.sink.defer(params, g_code, ws):
+            return None, None
+        return ops.code_dz([(params, g_code, ws)], z_s.shape[0])
     rows = meta.sink.rows() if (want_z and meta.sink is not None) else None
     if rows is not None:
         ops.code_bias_backward(params, z_s, z_t, g_code, pg, dz_into=rows)
@@ -332,23 +355,24 @@ class RadianceField(torch.autograd.Function):
         train_w16 = mode == "train_w16"
         ctx.g_code = None
         ctx.acc = None
+        ctx.code_act = None        # the code layers' activations (the code backward's operand)
         # a render's two fields may have been prepared together (prefetch_prepares)
         pre = _take_prepared(ctx.owner, params, z_s, z_t, mode, n_zero) if mode else None
         if train_w16:
             # the fp32 training step: code terms, both packs and the backward's zeroed g_code, one launch
             nc = z_s.shape[0]
             if pre is not None:
-                (cb, zero), packed_w16 = pre, _packed(ctx.owner, params, "f32_w16")
+                (cb, zero, ctx.code_act), packed_w16 = pre, _packed(ctx.owner, params, "f32_w16")
             else:
-                cb, packed_w16, zero = _prepare_w16(ctx.owner, params, z_s, z_t, n_zero)
+                cb, packed_w16, zero, ctx.code_act = _prepare_w16(ctx.owner, params, z_s, z_t, n_zero)
             ctx.g_code = zero.view(nc, _lib.CN_CODE_BIAS_STRIDE)
         elif fused:
             # the eval step (frozen weights, packs cached): the code terms and the fused backward's zeroed
             # accumulators (g_code, d ro, d rd) in one launch
-            if pre is not None:
-                cb, ctx.acc = pre
-            else:
-                cb, _, _, ctx.acc = ops.field_prepare(params, z_s, z_t, pack=False, pack_t=False, n_zero=n_zero)
+            if pre is None:
+                pre = ops.field_prepare_models([(params, False, False, n_zero)], z_s, z_t, want_act=True)[0]
+                pre = (pre[0], pre[3], pre[4])
+            cb, ctx.acc, ctx.code_act = pre
         else:
             cb = ops.code_bias(params, z_s, z_t)
         if fused:
@@ -401,7 +425,8 @@ class RadianceField(torch.autograd.Function):
             ctx.acc = None
             dz_s = dz_t = None
             if want_z:
-                dz_s, dz_t = _code_grads(meta, params, z_s, z_t, r["g_code"], None, True)
+                dz_s, dz_t = _code_grads(meta, params, z_s, z_t, r["g_code"], None, True, ctx.code_act)
+            ctx.code_act = None
             ctx.masks = None
             return (None, r["d_rd"], r["d_pts"], r["d_ro"], None, dz_s, dz_t, *([None] * len(params)))
         pg = _param_grad_buffers(params, needs[7:], ctx.orig_params)
@@ -415,8 +440,8 @@ class RadianceField(torch.autograd.Function):
                                          code_index=meta.code_index, param_grads=pg, want_pts=needs[2],
                                          want_ro=needs[3], want_rd=needs[1], precision=meta.precision,
                                          g_code=ctx.g_code)
-            ctx.acts = ctx.x_enc = ctx.masks = ctx.g_code = None
-            dz_s, dz_t = _code_grads(meta, params, z_s, z_t, r["g_code"], pg, want_z)
+            act, ctx.acts, ctx.x_enc, ctx.masks, ctx.g_code, ctx.code_act = ctx.code_act, None, None, None, None, None
+            dz_s, dz_t = _code_grads(meta, params, z_s, z_t, r["g_code"], pg, want_z, act)
             grads = pg if pg is not None else [None] * len(params)
             return (None, r["d_rd"], r["d_pts"], r["d_ro"], None, dz_s, dz_t, *grads)
         r = ops.field_backward(params, ctx.acts, ctx.x_enc, g_raw.contiguous(), rd.shape[0], meta.n_samples,

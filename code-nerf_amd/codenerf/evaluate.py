@@ -20,6 +20,7 @@ import torch
 import torch.distributed as dist
 
 from . import nerf, ops
+from .autograd import backward_from
 from .utils import mse2psnr
 
 
@@ -139,7 +140,7 @@ class GraphedEvalStep:
         def body(with_opt: bool):
             grads.zero_()
             loss, logs = eval_step_loss(*args, **kw)
-            loss.backward()
+            backward_from(loss)
             if with_opt:
                 self.opt.graph_step(self.d_scal)
             return loss, logs
@@ -260,7 +261,7 @@ def test_time_optimize(target_pixels: torch.Tensor, samplers, embedders, models,
                                             embedders, models, regularizer_lambda, gt_pose=gt_pose)
                 cam_pose = logs.pop("cam_pose")
                 opt.zero_grad()
-                loss.backward()
+                backward_from(loss)
                 opt.step()
             logs["psnr"] = step_psnr_tensor(logs)       # read back with the history (below) or when logged
             logs["total_loss"] = loss.detach()

@@ -141,10 +141,10 @@ class CodeGradSink:
     their .grad by _TableRow.backward.  Per model and step this replaces an add of the coarse and fine
     code gradients and one into the table row (nn.Embedding's backward, model.py:102-105)."""
 
-    __slots__ = ("tables", "k", "bufs")
+    __slots__ = ("tables", "k", "bufs", "pending")
 
     def __init__(self, tables, k: int):
-        self.tables, self.k, self.bufs = tables, k, None
+        self.tables, self.k, self.bufs, self.pending = tables, k, None, []
 
     def rows(self):
         """-> (shape row, texture row) views (1, code size) of the claimed gradient buffers, or None when a
@@ -160,9 +160,26 @@ class CodeGradSink:
             self.bufs = slots
         return tuple(b[self.k:self.k + 1] for b in self.bufs)
 
+    def defer(self, params, g_code, workspace) -> bool:
+        """Queue a field's dz (cn_code_dz job: its parameters, g_code and cn_code_bias_backward_act's
+        workspace) for flush(); False (nothing queued) when rows() has no buffers to give."""
+        if self.rows() is None:
+            return False
+        self.pending.append((params, g_code, workspace))
+        return True
+
+    def flush(self) -> None:
+        """The queued fields' dz added into the claimed rows: ONE cn_code_dz launch for a render's two
+        fields (in the order they were queued)."""
+        from .. import ops
+        while self.pending:
+            jobs, self.pending = self.pending[:2], self.pending[2:]
+            ops.code_dz(jobs, 1, dz_into=self.rows())
+
     def take(self):
-        """-> the claimed buffers or None, dropping the sink's references to them (AccumulateGrad then
-        adopts them as .grad without a copy)."""
+        """-> the claimed buffers or None (after flush()), dropping the sink's references to them
+        (AccumulateGrad then adopts them as .grad without a copy)."""
+        self.flush()
         b, self.bufs = self.bufs, None
         return b
 

@@ -326,10 +326,12 @@ def field_prepare(params: Sequence[Tensor], z_s: Tensor, z_t: Tensor, pack: bool
     return cb, packed, packed_t, zero
 
 
-def field_prepare_models(models: Sequence[Tuple[Sequence[Tensor], bool, bool, int]], z_s: Tensor, z_t: Tensor):
+def field_prepare_models(models: Sequence[Tuple[Sequence[Tensor], bool, bool, int]], z_s: Tensor, z_t: Tensor,
+                         want_act: bool = False):
     """cn_field_prepare_models: field_prepare for one or two models (params, pack, pack_t, n_zero) on the
     same codes in ONE launch -> [(cb, packed or None, packed_t or None, zero or None)] per model; bitwise
-    each model's field_prepare."""
+    each model's field_prepare.  ``want_act``: each tuple also carries the code-layer activations
+    (n_codes, 768) (code_ds_outer's operand) as a fifth entry."""
     lib = _lib_ready()
     assert 1 <= len(models) <= 2, "one or two models"
     z_s, z_t = _cuda(z_s.detach(), "z_s"), _cuda(z_t.detach(), "z_t")
@@ -344,10 +346,11 @@ def field_prepare_models(models: Sequence[Tuple[Sequence[Tensor], bool, bool, in
         packed = torch.empty(nf, device=dev, dtype=torch.float32) if pack else None
         packed_t = torch.empty(nf, device=dev, dtype=torch.float32) if pack_t else None
         zero = torch.empty(n_zero, device=dev, dtype=torch.float32) if n_zero else None
+        act = torch.empty(z_s.shape[0], 768, device=dev, dtype=torch.float32) if want_act else None
         arr, k_arr = _lib.pointer_array(params)
         keep += [params, arr, k_arr]
-        preps[k] = _lib.FieldPrep(arr, ptr(cb), ptr(packed), ptr(packed_t), ptr(zero), n_zero)
-        outs.append((cb, packed, packed_t, zero))
+        preps[k] = _lib.FieldPrep(arr, ptr(cb), ptr(packed), ptr(packed_t), ptr(zero), n_zero, ptr(act))
+        outs.append((cb, packed, packed_t, zero, act) if want_act else (cb, packed, packed_t, zero))
     check(lib.cn_field_prepare_models(preps, len(models), ptr(z_s), ptr(z_t), z_s.shape[0], stream_of(z_s)),
           "cn_field_prepare_models")
     del keep
@@ -698,6 +701,55 @@ def code_bias_backward(params: Sequence[Tensor], z_s: Tensor, z_t: Tensor, g_cod
                                            ptr(ws), int(dz_into is not None), stream_of(g_code)),
               "cn_code_bias_backward_ws")
     del keep, gkeep
+    return dz_s, dz_t
+
+
+def code_ds_outer(params: Sequence[Tensor], z_s: Tensor, z_t: Tensor, code_act: Tensor, g_code: Tensor,
+                  param_grads: Optional[Sequence[Tensor]] = None) -> Tensor:
+    """cn_code_bias_backward_act: the code backward's first half on the forward's code-layer activations
+    (field_prepare_models(..., want_act=True)) -> its workspace (the masked ds1 / ds2 / dt1, for code_dz);
+    the code layers' and code halves' gradients are added into ``param_grads``."""
+    lib = _lib_ready()
+    params = [_cuda(p.detach(), f"param{i}") for i, p in enumerate(params)]
+    z_s, z_t, g_code = _cuda(z_s.detach(), "z_s"), _cuda(z_t.detach(), "z_t"), _cuda(g_code, "g_code")
+    code_act = _cuda(code_act, "code_act")
+    n = z_s.shape[0]
+    assert code_act.numel() == n * 768, "code_act: (n_codes, 768)"
+    ws = torch.empty(lib.cn_code_bias_backward_workspace_floats(n), device=g_code.device, dtype=torch.float32)
+    arr, keep = _lib.pointer_array(params)
+    garr, gkeep = _lib.pointer_array(list(param_grads)) if param_grads is not None else (None, None)
+    check(lib.cn_code_bias_backward_act(arr, ptr(z_s), ptr(z_t), n, ptr(code_act), ptr(g_code), garr, ptr(ws),
+                                        stream_of(g_code)), "cn_code_bias_backward_act")
+    del keep, gkeep
+    return ws
+
+
+def code_dz(jobs: Sequence[Tuple[Sequence[Tensor], Tensor, Tensor]], n_codes: int,
+            dz_into: Optional[Tuple[Tensor, Tensor]] = None):
+    """cn_code_dz: dz_s, dz_t of one or two fields' code backwards [(params, g_code, code_ds_outer's
+    workspace)] on the same codes, summed in job order -> fresh (n_codes, 256) tensors, or ADDED into
+    ``dz_into`` (contiguous (n_codes, 256) device tensors) and those returned."""
+    lib = _lib_ready()
+    assert 1 <= len(jobs) <= 2, "one or two jobs"
+    dev = jobs[0][1].device
+    if dz_into is not None:
+        for d in dz_into:
+            assert d.is_cuda and d.dtype == torch.float32 and d.is_contiguous() and d.shape == (n_codes, 256), \
+                "dz_into: contiguous (n_codes, 256) fp32 device tensors"
+        dz_s, dz_t = dz_into
+    else:
+        dz_s = torch.empty(n_codes, 256, device=dev, dtype=torch.float32)
+        dz_t = torch.empty(n_codes, 256, device=dev, dtype=torch.float32)
+    arr = (_lib.CodeDzJob * len(jobs))()
+    keep = []
+    for k, (params, g_code, ws) in enumerate(jobs):
+        params = [_cuda(p.detach(), f"param{i}") for i, p in enumerate(params)]
+        pa, pk = _lib.pointer_array(params)
+        keep += [params, pa, pk]
+        arr[k] = _lib.CodeDzJob(pa, ptr(_cuda(g_code, "g_code")), ptr(ws))
+    check(lib.cn_code_dz(arr, len(jobs), n_codes, ptr(dz_s), ptr(dz_t), int(dz_into is not None), stream_of(dz_s)),
+          "cn_code_dz")
+    del keep
     return dz_s, dz_t
 
 

@@ -33,7 +33,7 @@ import torch.distributed as dist
 from . import nerf
 from .models import CodeNeRFModel, ShapeTextureEmbedding, get_params_tensor
 from .optim import AdamW
-from .autograd import render_loss_autograd
+from .autograd import backward_from, render_loss_autograd
 from .utils import get_minibatches, mse2psnr
 
 
@@ -138,7 +138,7 @@ def train_minibatch(models, optimizer, scheduler, point_sampler, embedders, ro, 
                                        regularizer_lambda, psnr=psnr)
     loss_coarse, loss_fine, regularization = stats[0], stats[1], stats[2]
     optimizer.zero_grad()
-    loss.backward()
+    backward_from(loss)
     if is_distributed and not _ddp_wrapped(models):
         _average_gradients(optimizer, models)     # (DDP-wrapped modules averaged in the backward)
     optimizer.step()

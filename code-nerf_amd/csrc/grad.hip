@@ -2057,6 +2057,170 @@ __global__ __launch_bounds__(256) void code_outer_kernel(mlp::Params P, const fl
   }
 }
 
+// The code backward on the forward's own code-layer activations (act: s1 | s2 | t1 per code, written by
+// the preparation launch, cn_field_prepare_models), in two kernels whose second may serve both fields of
+// a render at once:
+//   code_ds_outer_kernel: workgroup y forms ds1 / ds2 / dt1 for rows R y .. (masked by act > 0) into the
+//     workspace and the outer products / bias terms of those rows -- no code layer is recomputed;
+//   code_dz_kernel: dz_s / dz_t for columns R y .. from every row's ds, for one or two (model, g_code,
+//     workspace) jobs added in job order.
+// Each 256-long dot is split over the 16 lanes of a DPP row (16 n each, all loads in flight) and summed
+// by a 16-lane butterfly: one memory round trip per chain instead of four.
+
+// Sum over the 16 lanes of this lane's row group (every lane of the group gets it); fixed order.
+__device__ __forceinline__ float sum16_bfly(float x) {
+#pragma unroll
+  for (int off = 8; off > 0; off >>= 1) x += __shfl_xor(x, off, 16);
+  return x;
+}
+
+__global__ __launch_bounds__(256) void code_ds_outer_kernel(mlp::Params P, const float* __restrict__ z_s,
+                                                            const float* __restrict__ z_t, const float* __restrict__ g,
+                                                            const float* __restrict__ act, float* __restrict__ ws,
+                                                            mlp::Params G) {
+  using namespace mlp;
+  static_assert(kCodeRows == 4, "thread map: 8 row groups of 16 lanes = 2 vectors x 4 rows");
+  __shared__ float gx2[256], go[257], grgb[3], ds[3][kCodeRows];
+  const int c = blockIdx.x, y = blockIdx.y, tid = threadIdx.x;
+  const int r0 = kCodeRows * y;
+  const float* gr = g + (int64_t)c * kCbStride;
+  if (!code_row_used(gr, tid)) return;  // code_dz_kernel skips the code too
+  gx2[tid] = gr[kCbXyz2 + tid];
+  go[1 + tid] = gr[kCbFeat + tid];
+  if (tid == 0) go[0] = gr[kCbSigma];
+  if (tid < 3) grgb[tid] = gr[kCbRgb + tid];
+  __syncthreads();
+  const float* a = act + (int64_t)c * 3 * 256;
+  if (tid < 128) {
+    // group o = tid / 16: vector v = o / 4 (0: layer_xyz2's code half . gx2, 1: fc_out's . go), row i = o % 4;
+    // lane p of the group: n = 16 p .. 16 p + 15 (fc_out's row 256 term last, in lane 15)
+    const int o = tid >> 4, v = o >> 2, i = o & 3, pl = tid & 15, j = r0 + i;
+    const float* W = P.p[v == 0 ? kWXyz2 : kWOut] + 256 + j;
+    const float* gv = v == 0 ? gx2 : go;
+    float wv[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) wv[u] = W[(16 * pl + u) * 512];
+    float acc = 0.f;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) acc = fmaf(wv[u], gv[16 * pl + u], acc);
+    if (v == 1 && pl == 15) acc = fmaf(P.p[kWOut][256 * 512 + 256 + j], go[256], acc);
+    const float sum = sum16_bfly(acc);
+    if (pl == 0) {
+      const float d = a[v * 256 + j] > 0.f ? sum : 0.f;
+      ds[v][i] = d;
+      ws[(int64_t)c * 6 * 256 + (3 + v) * 256 + j] = d;
+    }
+  } else if (tid < 128 + kCodeRows) {
+    const int i = tid - 128, j = r0 + i;
+    float acc = 0.f;
+    for (int n = 0; n < 3; ++n) acc = fmaf(P.p[kWRgb][n * 512 + 256 + j], grgb[n], acc);
+    const float d = a[512 + j] > 0.f ? acc : 0.f;
+    ds[2][i] = d;
+    ws[(int64_t)c * 6 * 256 + 5 * 256 + j] = d;
+  }
+  __syncthreads();
+  if (!G.p[kWSc1]) return;
+  const int j = tid;
+  const float zsj = z_s[(int64_t)c * 256 + j], ztj = z_t[(int64_t)c * 256 + j];
+  const float s1j = a[j], s2j = a[256 + j];
+#pragma unroll
+  for (int i = 0; i < kCodeRows; ++i) {
+    const int r = r0 + i;
+    grad_add(G.p[kWSc1], r * 256 + j, ds[0][i] * zsj);
+    grad_add(G.p[kWSc2], r * 256 + j, ds[1][i] * zsj);
+    grad_add(G.p[kWTc1], r * 256 + j, ds[2][i] * ztj);
+    grad_add(G.p[kWXyz2], r * 512 + 256 + j, gx2[r] * s1j);
+    grad_add(G.p[kWOut], (1 + r) * 512 + 256 + j, go[1 + r] * s2j);
+  }
+  if (tid < kCodeRows) {
+    const int jb = r0 + tid;
+    grad_add(G.p[kBSc1], jb, ds[0][tid]);
+    grad_add(G.p[kBSc2], jb, ds[1][tid]);
+    grad_add(G.p[kBTc1], jb, ds[2][tid]);
+    grad_add(G.p[kWOut], 256 + jb, go[0] * a[256 + jb]);  // fc_out row 0 (sigma)
+    for (int r = 0; r < 3; ++r) grad_add(G.p[kWRgb], r * 512 + 256 + jb, grgb[r] * a[512 + jb]);
+  }
+}
+
+struct DzJob {
+  mlp::Params P;
+  const float* g;
+  const float* ws;
+};
+constexpr int kMaxDzJobs = 2;
+struct DzJobs {
+  DzJob j[kMaxDzJobs];
+  int n;
+};
+
+// accumulate: dz += each job's code gradient (in job order), else dz = their sum (0 for a code no job
+// used).  Group o = tid / 16 of the block: job o / 8, vector (o / 4) % 2 (dz_s: W_sc1^T ds1 + W_sc2^T
+// ds2; dz_t: W_tc1^T dt1), column r0 + o % 4; its lane p takes n = 16 p .. 16 p + 15.
+__global__ __launch_bounds__(256) void code_dz_kernel(DzJobs jobs, float* __restrict__ dz_s, float* __restrict__ dz_t,
+                                                      int accumulate) {
+  using namespace mlp;
+  static_assert(kCodeRows == 4 && kMaxDzJobs == 2, "thread map: 2 jobs x 2 vectors x 4 columns x 16 lanes");
+  __shared__ float dsv[kMaxDzJobs][3][256];
+  __shared__ float part[kMaxDzJobs][2][kCodeRows];
+  const int c = blockIdx.x, y = blockIdx.y, tid = threadIdx.x;
+  const int r0 = kCodeRows * y;
+  bool used[kMaxDzJobs] = {false, false};
+  for (int jb = 0; jb < jobs.n; ++jb) {
+    used[jb] = code_row_used(jobs.j[jb].g + (int64_t)c * kCbStride, tid);
+    if (used[jb]) {
+      const float* wc = jobs.j[jb].ws + (int64_t)c * 6 * 256;
+      dsv[jb][0][tid] = wc[768 + tid];
+      dsv[jb][1][tid] = wc[1024 + tid];
+      dsv[jb][2][tid] = wc[1280 + tid];
+    }
+  }
+  __syncthreads();
+  {
+    const int o = tid >> 4, jb = o >> 3, vv = (o >> 2) & 1, k = o & 3, pl = tid & 15, j = r0 + k;
+    if (jb < jobs.n && used[jb]) {     // uniform over the 16-lane group
+      const Params& Pj = jobs.j[jb].P;
+      float acc = 0.f;
+      if (vv == 0) {
+        float w1[16], w2[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          w1[u] = Pj.p[kWSc1][(16 * pl + u) * 256 + j];
+          w2[u] = Pj.p[kWSc2][(16 * pl + u) * 256 + j];
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          acc = fmaf(w1[u], dsv[jb][0][16 * pl + u], acc);
+          acc = fmaf(w2[u], dsv[jb][1][16 * pl + u], acc);
+        }
+      } else {
+        float w1[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) w1[u] = Pj.p[kWTc1][(16 * pl + u) * 256 + j];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) acc = fmaf(w1[u], dsv[jb][2][16 * pl + u], acc);
+      }
+      const float sum = sum16_bfly(acc);
+      if (pl == 0) part[jb][vv][k] = sum;
+    }
+  }
+  __syncthreads();
+  if (tid < 2 * kCodeRows) {
+    const int vv = tid / kCodeRows, k = tid % kCodeRows;
+    float* dz = vv == 0 ? dz_s : dz_t;
+    if (dz) {
+      float* d = dz + (int64_t)c * 256 + r0 + k;
+      bool has = accumulate != 0;
+      float cur = has ? *d : 0.f;
+      for (int jb = 0; jb < jobs.n; ++jb) {
+        if (!used[jb]) continue;
+        cur = has ? cur + part[jb][vv][k] : part[jb][vv][k];
+        has = true;
+      }
+      *d = cur;
+    }
+  }
+}
+
 // The bias gradients that are column sums of g_code (the per-code sums of the code-bias terms):
 // layer_xyz2 (cols 0..255), fc_out rows 1..256 (256..511) and row 0 (512), fc_rgb (513..515).
 __global__ void gcode_bias_kernel(const float* __restrict__ g_code, int64_t n_codes, float* __restrict__ b_xyz2,
@@ -2572,6 +2736,44 @@ extern "C" int cn_debug_tnprof(long long* out, int n_blocks) {
                  hipSuccess ? 0 : -1;
 }
 #endif
+
+extern "C" int cn_code_bias_backward_act(const float* const* params, const float* z_s, const float* z_t,
+                                         int64_t n_codes, const float* code_act, const float* g_code,
+                                         float* const* grads, float* workspace, cn_stream_t stream) {
+  using namespace mlp;
+  CN_CHECK_ARG(params && z_s && z_t && code_act && g_code && workspace && n_codes > 0 && n_codes < (1ll << 31));
+  Params P, G = {};
+  for (int i = 0; i < CN_NUM_PARAMS; ++i) {
+    CN_CHECK_ARG(params[i]);
+    P.p[i] = params[i];
+    G.p[i] = grads ? grads[i] : nullptr;
+  }
+  hipLaunchKernelGGL(grad::code_ds_outer_kernel, dim3(static_cast<unsigned>(n_codes), grad::kCodeSlices), dim3(256), 0,
+                     as_stream(stream), P, z_s, z_t, g_code, code_act, workspace, G);
+  return launch_status();
+}
+
+extern "C" int cn_code_dz(const cn_code_dz_job* jobs, int n_jobs, int64_t n_codes, float* dz_s, float* dz_t,
+                          int accumulate, cn_stream_t stream) {
+  using namespace mlp;
+  CN_CHECK_ARG(jobs && n_jobs >= 1 && n_jobs <= grad::kMaxDzJobs && n_codes > 0 && n_codes < (1ll << 31));
+  CN_CHECK_ARG(accumulate == 0 || accumulate == 1);
+  grad::DzJobs dj = {};
+  dj.n = n_jobs;
+  for (int k = 0; k < n_jobs; ++k) {
+    CN_CHECK_ARG(jobs[k].params && jobs[k].g_code && jobs[k].workspace);
+    for (int i = 0; i < CN_NUM_PARAMS; ++i) {
+      CN_CHECK_ARG(jobs[k].params[i]);
+      dj.j[k].P.p[i] = jobs[k].params[i];
+    }
+    dj.j[k].g = jobs[k].g_code;
+    dj.j[k].ws = jobs[k].workspace;
+  }
+  if (!dz_s && !dz_t) return CN_OK;
+  hipLaunchKernelGGL(grad::code_dz_kernel, dim3(static_cast<unsigned>(n_codes), grad::kCodeSlices), dim3(256), 0,
+                     as_stream(stream), dj, dz_s, dz_t, accumulate);
+  return launch_status();
+}
 
 extern "C" int64_t cn_code_bias_backward_workspace_floats(int64_t n_codes) {
   return n_codes > 0 ? n_codes * 6 * 256 : -1;

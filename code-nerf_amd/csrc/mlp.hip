@@ -415,7 +415,7 @@ extern "C" int cn_code_bias(const float* const* params, const float* z_s, const 
 extern "C" int cn_field_prepare(const float* const* params, const float* z_s, const float* z_t, int64_t n_codes,
                                 float* code_bias, float* packed, float* packed_t, float* zero, int64_t n_zero,
                                 cn_stream_t stream) {
-  const cn_field_prep m = {params, code_bias, packed, packed_t, zero, n_zero};
+  const cn_field_prep m = {params, code_bias, packed, packed_t, zero, n_zero, nullptr};
   return cn_field_prepare_models(&m, 1, z_s, z_t, n_codes, stream);
 }
 
@@ -428,7 +428,9 @@ extern "C" int cn_field_prepare_models(const cn_field_prep* models, int n_models
     if (make_params(m.params, &pm[k].P) != CN_OK) return CN_EINVAL;
     CN_CHECK_ARG(m.n_zero >= 0 && (m.n_zero == 0 || m.zero));
     CN_CHECK_ARG(!m.code_bias || (z_s && z_t && n_codes > 0 && n_codes * kCbSlices + 256 <= 0x7fffffff));
+    CN_CHECK_ARG(!m.code_act || m.code_bias);
     pm[k].code_bias = m.code_bias;
+    pm[k].code_act = m.code_act;
     pm[k].packed = m.packed;
     pm[k].packed_t = m.packed_t;
     pm[k].zero = m.zero;

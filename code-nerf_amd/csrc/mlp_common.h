@@ -199,8 +199,11 @@ __device__ __forceinline__ float wave_dot4(float4 a, float4 b) {
 
 // Workgroup `blk` (= code * kCbSlices + slice) of the code-bias launch (cn_code_bias; also a role of
 // the one-launch step preparation, cn_field_prepare).
+// act (optional, (n_codes, 768)): the code-layer activations s1 | s2 | t1 (post-ReLU), written by the
+// first slice of each layer -- the code backward's ReLU masks and outer-product operands.
 __device__ __forceinline__ void code_bias_block(const Params& P, const float* __restrict__ z_s,
-                                                const float* __restrict__ z_t, float* __restrict__ out, int64_t blk) {
+                                                const float* __restrict__ z_t, float* __restrict__ out, int64_t blk,
+                                                float* __restrict__ act = nullptr) {
   __shared__ __attribute__((aligned(16))) float z[kCode], hv[kCode];
   const int64_t c = blk / kCbSlices;
   const int q = static_cast<int>(blk % kCbSlices), t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -230,6 +233,7 @@ __device__ __forceinline__ void code_bias_block(const Params& P, const float* __
   if (t < kCode) {
     const float* B = P.p[l == 0 ? kBSc1 : (l == 1 ? kBSc2 : kBTc1)];
     hv[t] = fmaxf(hv[t] + B[t], 0.f);
+    if (act && (q == 0 || q == 8 || q == 16)) act[c * 3 * kCode + l * kCode + t] = hv[t];
   }
   __syncthreads();
   float* o = out + c * kCbStride;
@@ -286,6 +290,7 @@ int launch_pack_w16t(const Params& P, float* packed, hipStream_t st);
 struct PrepareModel {
   Params P;
   float* code_bias;
+  float* code_act;   // (n_codes, 768) code-layer activations, or null
   float* packed;
   float* packed_t;
   float* zero;

@@ -993,6 +993,7 @@ struct Prepare {
   const float* z_s;
   const float* z_t;
   float* code_bias;
+  float* code_act;   // code-layer activations (code_bias_block) or null
   float* packed;     // CN_FMT_F32_W16 or null
   float* packed_t;   // CN_FMT_F32_W16_T or null
   float* zero;
@@ -1015,7 +1016,7 @@ __global__ __launch_bounds__(kPrepThreads) void field_prepare_kernel(PrepareSet 
   const Prepare& p = set.p[k];
   unsigned b = blockIdx.x - set.first[k];
   if (b < p.nb_cb) {
-    code_bias_block(p.P, p.z_s, p.z_t, p.code_bias, b);
+    code_bias_block(p.P, p.z_s, p.z_t, p.code_bias, b, p.code_act);
     return;
   }
   b -= p.nb_cb;
@@ -1570,7 +1571,8 @@ int launch_field_prepare_w16(const PrepareModel* models, int n_models, const flo
   for (int k = 0; k < n_models; ++k) {
     const PrepareModel& m = models[k];
     w16::Prepare& p = set.p[k];
-    p = w16::Prepare{m.P, z_s, z_t, m.code_bias, m.packed, m.packed_t, m.zero, m.n_zero, 0u, 0u, 0u};
+    p = w16::Prepare{m.P, z_s, z_t, m.code_bias, m.code_bias ? m.code_act : nullptr, m.packed, m.packed_t, m.zero,
+                     m.n_zero, 0u, 0u, 0u};
     p.nb_cb = m.code_bias ? static_cast<unsigned>(n_codes * kCbSlices) : 0u;
     p.nb_pack = 64;  // 64 x 512 threads over each pack's 327,680 floats: 10 elements per thread
     p.nb_zero = m.n_zero > 0 ? static_cast<unsigned>(std::min<int64_t>(cn::ceil_div(m.n_zero, w16::kPrepThreads), 64))

@@ -4,8 +4,9 @@
 // sample_pdf gives one wavefront to one ray: the ray's cdf, bins and merged
 // depth list live in LDS, the cdf is a wave scan (exact in double, so the
 // sequential loop's bits), searchsorted is a binary search there, and the
-// final sort a bitonic network over (value, position) keys -- the stable sort
-// of the unsorted perturbed fine samples, ties included.
+// final sort a bitonic network over (value, position) keys in the wave's
+// registers -- the stable sort of the unsorted perturbed fine samples, ties
+// included.
 #include "cn_common.h"
 
 namespace {
@@ -147,13 +148,78 @@ __device__ float torch_cpu_row_sum_wave(const float* x, int n, int lane) {
   return fin;
 }
 
+// sort(cat(z, samples)) (:116) of one ray in its wave's registers: a bitonic network over N2 (value,
+// position) keys, element e = lane + 64 h in lane `lane`, slot h; keys past n are +inf at positions past
+// n, so ties order by position -- the stable sort.  Partners 64 or more apart sit in the same lane
+// (a register exchange), nearer ones in lane ^ j (a cross-lane shuffle): no LDS, no barrier.  Then the
+// sorted depths (and points) stored in order, coalesced.
+template <int N2>
+__device__ __forceinline__ void sort_store(const float* val, int n, int lane, float* __restrict__ zo,
+                                           float* __restrict__ po, const float* o, const float* d) {
+  constexpr int E = N2 / 64;
+  float v[E];
+  int ix[E];
+#pragma unroll
+  for (int h = 0; h < E; ++h) {
+    const int e = lane + 64 * h;
+    v[h] = e < n ? val[e] : __builtin_inff();
+    ix[h] = e;
+  }
+#pragma unroll
+  for (int k = 2; k <= N2; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      if (j >= 64) {
+#pragma unroll
+        for (int h = 0; h < E; ++h) {
+          const int hp = h ^ (j >> 6);
+          if (hp > h) {
+            const bool up = ((lane + 64 * h) & k) == 0;
+            const bool after = v[h] > v[hp] || (v[h] == v[hp] && ix[h] > ix[hp]);
+            if (after == up) {
+              const float tv = v[h];
+              const int ti = ix[h];
+              v[h] = v[hp];
+              ix[h] = ix[hp];
+              v[hp] = tv;
+              ix[hp] = ti;
+            }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int h = 0; h < E; ++h) {
+          const float pv = __shfl_xor(v[h], j);
+          const int pi = __shfl_xor(ix[h], j);
+          const bool up = ((lane + 64 * h) & k) == 0, lower = (lane & j) == 0;
+          const bool after = v[h] > pv || (v[h] == pv && ix[h] > pi);
+          if (after == (lower == up)) {      // the lower slot of an ascending pair keeps the smaller key
+            v[h] = pv;
+            ix[h] = pi;
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < E; ++h) {
+    const int e = lane + 64 * h;
+    if (e < n) {
+      zo[e] = v[h];
+      if (po) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) po[3 * e + j] = cn::mul_add_rn(d[j], v[h], o[j]);
+      }
+    }
+  }
+}
+
 // point_sampler.py:84-118, one wave per ray.
 //   pdf / cdf: torch's CPU cumsum adds the fp32 pdf in double and rounds every prefix.  When every
 //   nonzero |pdf| >= 2^-28 (so all are multiples of 2^-51) and sum |pdf| < 1.5 (every prefix below
 //   2^2), each double prefix is EXACT -- whatever the order of the additions -- so a wave scan gives
 //   the sequential loop's bits; a ray outside those bounds takes the sequential loop in lane 0.
-//   sort(cat(z, samples)) (:116): a bitonic network in LDS over (value, position) keys padded to a
-//   power of two with +inf -- ties ordered by position, i.e. the stable sort -- and coalesced stores.
+//   sort(cat(z, samples)) (:116): sort_store, a bitonic network in registers.
 __global__ __launch_bounds__(256) void sample_pdf_kernel(
     const float* __restrict__ ro, const float* __restrict__ rd, const float* __restrict__ weights,
     int64_t w_stride, const float* __restrict__ z, int64_t n_rays, int nc, int nf,
@@ -162,7 +228,6 @@ __global__ __launch_bounds__(256) void sample_pdf_kernel(
   __shared__ float s_cdf[kPdfWaves][256];
   __shared__ float s_mid[kPdfWaves][256];
   __shared__ float s_val[kPdfWaves][kPdfMaxN];
-  __shared__ int s_idx[kPdfWaves][kPdfMaxN];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int64_t r_raw = blockIdx.x * (int64_t)kPdfWaves + wv;
@@ -171,13 +236,12 @@ __global__ __launch_bounds__(256) void sample_pdf_kernel(
   float* cdf = s_cdf[wv];
   float* mid = s_mid[wv];
   float* val = s_val[wv];
-  int* idx = s_idx[wv];
   const float* zr = z + r * nc;
   const float* wr = weights + r * w_stride;
   const int nw = nc - 2;      // pdf entries
   const int ncdf = nc - 1;    // cdf / bins entries
   const int n = nc + nf;
-  int n2 = 1;
+  int n2 = 64;
   while (n2 < n) n2 <<= 1;
 
   // bins = 0.5 * (z[1:] + z[:-1]) (:85); coarse depths into the merge list
@@ -249,40 +313,16 @@ __global__ __launch_bounds__(256) void sample_pdf_kernel(
     const float b0 = mid[below], b1 = mid[above];
     val[nc + i] = __fadd_rn(b0, __fmul_rn(t, __fsub_rn(b1, b0)));
   }
-  for (int i = lane; i < n2; i += 64) {
-    idx[i] = i;
-    if (i >= n) val[i] = __builtin_inff();
-  }
   __syncthreads();
-
-  // sort(cat(z, samples)) (:116): bitonic over (value, position)
-  for (int k = 2; k <= n2; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int t = lane; t < (n2 >> 1); t += 64) {
-        const int a = 2 * t - (t & (j - 1)), b = a + j;
-        const float va = val[a], vb = val[b];
-        const int ia = idx[a], ib = idx[b];
-        const bool a_after = va > vb || (va == vb && ia > ib);
-        if (a_after == ((a & k) == 0)) {
-          val[a] = vb;
-          val[b] = va;
-          idx[a] = ib;
-          idx[b] = ia;
-        }
-      }
-      __syncthreads();
-    }
-  }
-  if (!valid) return;
+  if (!valid) return;                       // no barrier below
   float* zo = z_out + r * n;
-  for (int p = lane; p < n; p += 64) {
-    const float v = val[p];
-    zo[p] = v;
-    if (pts_out) {
-      float* po = pts_out + (r * n + p) * 3;
-#pragma unroll
-      for (int j = 0; j < 3; ++j) po[j] = cn::mul_add_rn(rd[3 * r + j], v, ro[3 * r + j]);
-    }
+  const float* o = pts_out ? ro + 3 * r : nullptr;
+  const float* d = pts_out ? rd + 3 * r : nullptr;
+  switch (n2) {
+    case 64: sort_store<64>(val, n, lane, zo, pts_out ? pts_out + r * n * 3 : nullptr, o, d); break;
+    case 128: sort_store<128>(val, n, lane, zo, pts_out ? pts_out + r * n * 3 : nullptr, o, d); break;
+    case 256: sort_store<256>(val, n, lane, zo, pts_out ? pts_out + r * n * 3 : nullptr, o, d); break;
+    default: sort_store<512>(val, n, lane, zo, pts_out ? pts_out + r * n * 3 : nullptr, o, d); break;
   }
 }
 

@@ -207,7 +207,9 @@ int cn_field_prepare(const float* const* params, const float* z_s, const float* 
                      float* code_bias, float* packed, float* packed_t, float* zero, int64_t n_zero,
                      cn_stream_t stream);
 
-/* One model's part of cn_field_prepare_models: the arguments of cn_field_prepare. */
+/* One model's part of cn_field_prepare_models: the arguments of cn_field_prepare, and code_act
+ * (optional, with code_bias; (n_codes, 768)): the code layers' activations s1 | s2 | t1 after the
+ * ReLU (model.py:174-177) as this launch formed them, for cn_code_bias_backward_act. */
 typedef struct cn_field_prep {
   const float* const* params;
   float* code_bias;
@@ -215,6 +217,7 @@ typedef struct cn_field_prep {
   float* packed_t;
   float* zero;
   int64_t n_zero;
+  float* code_act;
 } cn_field_prep;
 
 /* cn_field_prepare for n_models (1 or 2) models on the same codes in ONE launch: a render's coarse
@@ -410,6 +413,23 @@ int cn_code_bias_backward(const float* const* params, const float* z_s, const fl
  * gradient rows, so the coarse and fine fields' code gradients add up in place --
  * ShapeTextureEmbedding.forward in model.py:102-105 is the lookup they flow back to). */
 int64_t cn_code_bias_backward_workspace_floats(int64_t n_codes);
+/* The code backward on the forward's code-layer activations (code_act of cn_field_prepare_models),
+ * first half: ds1 / ds2 / dt1 (ReLU-masked by code_act) into the workspace
+ * (cn_code_bias_backward_workspace_floats) and the code layers' / code halves' parameter gradients
+ * added into grads (optional) -- no code layer is recomputed.  cn_code_dz forms dz from it. */
+int cn_code_bias_backward_act(const float* const* params, const float* z_s, const float* z_t, int64_t n_codes,
+                              const float* code_act, const float* g_code, float* const* grads, float* workspace,
+                              cn_stream_t stream);
+/* One field's part of cn_code_dz: its parameters, g_code and cn_code_bias_backward_act's workspace. */
+typedef struct cn_code_dz_job {
+  const float* const* params;
+  const float* g_code;
+  const float* workspace;
+} cn_code_dz_job;
+/* dz_s / dz_t (n_codes, 256; either may be NULL) of 1 or 2 jobs on the same codes (a render's coarse and
+ * fine fields, nerf/__init__.py:74-91), summed in job order; accumulate = 1: added to what dz holds. */
+int cn_code_dz(const cn_code_dz_job* jobs, int n_jobs, int64_t n_codes, float* dz_s, float* dz_t, int accumulate,
+               cn_stream_t stream);
 int cn_code_bias_backward_ws(const float* const* params, const float* z_s, const float* z_t, int64_t n_codes,
                              const float* g_code, float* dz_s, float* dz_t, float* const* grads, float* workspace,
                              int accumulate_dz, cn_stream_t stream);

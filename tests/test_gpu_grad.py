@@ -790,6 +790,61 @@ def test_field_prepare_bitwise(dev, n_codes, pack, pack_t):
     assert zero.shape == (nz,) and not zero.any()
 
 
+@pytest.mark.parametrize("n_codes,want_grads", [(1, True), (4, True), (4, False)])
+def test_code_backward_on_forward_activations(dev, n_codes, want_grads):
+    """The code backward on the preparation launch's code-layer activations (cn_code_bias_backward_act +
+    cn_code_dz): the activations are relu(W z + b) of the code layers (1e-6), dz and every parameter
+    gradient agree with the recomputing two-launch form to fp32 rounding (the two dot orders of the
+    activations differ in the last bits), an unused code gets dz = 0, and cn_code_dz over two fields
+    equals the one-field launches added in the same order, bit for bit."""
+    from codenerf import ops, synthetic
+    m = model(dev, 0)
+    params = [p.detach() for p in m.param_list()]
+    pd = {n: p.detach() for n, p in m.named_parameters()}
+    g = torch.Generator().manual_seed(40 + n_codes)
+    zs, zt = synthetic.latent_codes(11, n_codes).to(dev), synthetic.latent_codes(12, n_codes).to(dev)
+    ((cb, _, _, _, act),) = ops.field_prepare_models([(params, False, False, 0)], zs, zt, want_act=True)
+    assert torch.equal(cb, ops.code_bias(params, zs, zt))
+    ref_act = torch.cat([torch.relu(zs @ pd["shape_code_layer1.weight"].T + pd["shape_code_layer1.bias"]),
+                         torch.relu(zs @ pd["shape_code_layer2.weight"].T + pd["shape_code_layer2.bias"]),
+                         torch.relu(zt @ pd["texture_code_layer1.weight"].T + pd["texture_code_layer1.bias"])], 1)
+    close(act, ref_act, 1e-6, "code_act")
+    gc = (torch.randn(n_codes, cb.shape[1], generator=g) * 1e-2).to(dev)
+    if n_codes > 1:
+        gc[1] = 0.0
+    pg_old = [torch.full_like(p, 0.5) for p in params] if want_grads else None
+    dz_old = ops.code_bias_backward(params, zs, zt, gc, pg_old, want_z=True)
+    pg_new = [torch.full_like(p, 0.5) for p in params] if want_grads else None
+    ws = ops.code_ds_outer(params, zs, zt, act, gc, pg_new)
+    dz_new = ops.code_dz([(params, gc, ws)], n_codes)
+    for a, b, k in zip(dz_new, dz_old, ("dz_s", "dz_t")):
+        close(a, b, 1e-5, k)
+    if n_codes > 1:
+        assert not dz_new[0][1].any() and not dz_new[1][1].any()
+    if want_grads:
+        for k, (x, y) in enumerate(zip(pg_new, pg_old)):
+            close(x - 0.5, y - 0.5, 1e-5, f"param {k}")
+    # two fields in one cn_code_dz launch == the one-field launches in the same order
+    m2 = model(dev, 1)
+    params2 = [p.detach() for p in m2.param_list()]
+    ((_, _, _, _, act2),) = ops.field_prepare_models([(params2, False, False, 0)], zs, zt, want_act=True)
+    gc2 = (torch.randn(n_codes, cb.shape[1], generator=g) * 1e-2).to(dev)
+    ws2 = ops.code_ds_outer(params2, zs, zt, act2, gc2)
+    both = ops.code_dz([(params, gc, ws), (params2, gc2, ws2)], n_codes)
+    base = [(torch.randn(n_codes, 256, generator=g) * 1e-2).to(dev) for _ in range(2)]
+    into = tuple(t.clone() for t in base)
+    ops.code_dz([(params, gc, ws), (params2, gc2, ws2)], n_codes, dz_into=into)
+    one = ops.code_dz([(params, gc, ws)], n_codes)
+    seq = ops.code_dz([(params2, gc2, ws2)], n_codes, dz_into=tuple(t.clone() for t in one))
+    for a, b in zip(both, seq):
+        assert torch.equal(a, b)
+    step = tuple(t.clone() for t in base)
+    ops.code_dz([(params, gc, ws)], n_codes, dz_into=step)
+    ops.code_dz([(params2, gc2, ws2)], n_codes, dz_into=step)
+    for a, b in zip(into, step):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("n_codes", [1, 3])
 def test_field_prepare_models_bitwise(dev, n_codes):
     """cn_field_prepare_models (a render's coarse and fine fields prepared in one launch) equals each

@@ -346,32 +346,28 @@ def test_host_id_lookup_bitwise(dev, mixed):
 def test_step_fusions_bitwise(dev, monkeypatch, precision, off):
     """The training step's launch merges against the plain route, three steps of one-object chunks, every
     gradient and parameter bit-identical:
-    * "sink": both fields' code backwards add their dz into the code tables' gradient rows in place
-      (CodeGradSink, accumulate_dz; two such launches per step, the tables' .grad the optimiser's flat
-      slices) vs dz returned, summed by autograd and added into the row (3xbf16: to 1e-5, its fused
-      backward's g_code is a float-atomic sum);
-    * "prefetch": both fields' pre-field launches as one (cn_field_prepare_models, once per step, no
-      per-field cn_field_prepare) vs one per field."""
+    * "sink": both fields' code gradients added into the code tables' gradient rows in place
+      (CodeGradSink: fp32, one two-field cn_code_dz launch per step; 3xbf16, each field's
+      accumulate_dz launch), the tables' .grad the optimiser's flat slices, vs dz returned, summed by
+      autograd and added into the row (3xbf16: to 1e-5, its fused backward's g_code is a float-atomic
+      sum);
+    * "prefetch": both fields' pre-field launches as one (cn_field_prepare_models, once per step) vs one
+      per field."""
     from codenerf import autograd as A, ops, train as T
     from codenerf.models import model as M
     from codenerf.nerf import PointSampler
-    real_cb, real_pm, real_fp = ops.code_bias_backward, ops.field_prepare_models, ops.field_prepare
-    calls = {"sunk": [], "models": 0, "single": 0}
+    real_dz, real_pm = ops.code_dz, ops.field_prepare_models
+    calls = {"sunk": [], "models": []}
 
-    def spy_cb(*a, **k):
-        calls["sunk"].append(k.get("dz_into") is not None)
-        return real_cb(*a, **k)
+    def spy_dz(jobs, *a, **k):
+        calls["sunk"].append((len(jobs), k.get("dz_into") is not None))
+        return real_dz(jobs, *a, **k)
 
-    def spy_pm(*a, **k):
-        calls["models"] += 1
-        return real_pm(*a, **k)
-
-    def spy_fp(*a, **k):
-        calls["single"] += 1
-        return real_fp(*a, **k)
-    monkeypatch.setattr(ops, "code_bias_backward", spy_cb)
+    def spy_pm(models, *a, **k):
+        calls["models"].append(len(models))
+        return real_pm(models, *a, **k)
+    monkeypatch.setattr(ops, "code_dz", spy_dz)
     monkeypatch.setattr(ops, "field_prepare_models", spy_pm)
-    monkeypatch.setattr(ops, "field_prepare", spy_fp)
     S = 32 if precision == "bf16x3" else 16
     runs = []
     for on in (True, False):
@@ -379,7 +375,7 @@ def test_step_fusions_bitwise(dev, monkeypatch, precision, off):
             monkeypatch.setattr(M.CodeGradSink, "rows", lambda self: None)
         if not on and off == "prefetch":
             monkeypatch.setattr(A, "prefetch_render_prepares", lambda *a, **k: False)
-        calls.update(sunk=[], models=0, single=0)
+        calls.update(sunk=[], models=[])
         torch.manual_seed(3)
         models = _train_models(dev, 4)
         for key in ("nerf_coarse", "nerf_fine"):
@@ -404,10 +400,11 @@ def test_step_fusions_bitwise(dev, monkeypatch, precision, off):
                 lo, hi = flat.data_ptr(), flat.data_ptr() + flat.numel() * 4
                 for w in (models["embedding"].shape_embedding.weight, models["embedding"].texture_embedding.weight):
                     assert lo <= w.grad.data_ptr() < hi, "the table's .grad is not the optimiser's flat slice"
-        if off == "sink":
-            assert calls["sunk"] == [on] * 6, calls
-        elif precision == "f32":
-            assert (calls["models"], calls["single"]) == ((3, 0) if on else (0, 6)), calls
+        if off == "sink" and precision == "f32":
+            # sink: one two-field dz launch per step into the table rows; else one per field, returned
+            assert calls["sunk"] == ([(2, True)] * 3 if on else [(1, False)] * 6), calls
+        elif off == "prefetch":
+            assert calls["models"] == ([2] * 3 if on else [1] * 6), calls
         torch.cuda.synchronize()
         params = {f"{k}.{n_}": p.detach().clone() for k, m in models.items() for n_, p in m.named_parameters()}
         runs.append((grads, params))
