@@ -109,7 +109,7 @@ SIGNATURES = {
     "cn_code_bias_backward_act": (_i, [ctypes.POINTER(_p), _p, _p, _i64, _p, _p, ctypes.POINTER(_p), _p, _p]),
     "cn_code_dz": (_i, [ctypes.POINTER(CodeDzJob), _i, _i64, _p, _p, _i, _p]),
     "cn_code_bias_backward_ws": (_i, [ctypes.POINTER(_p), _p, _p, _i64, _p, _p, _p, ctypes.POINTER(_p), _p, _i, _p]),
-    "cn_volume_render_backward": (_i, [_p, _p, _p, _i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p]),
+    "cn_volume_render_backward": (_i, [_p, _p, _p, _i64, _i64, _p, _p, _p, _p, _p, _p, _p, _i, _p]),
     "cn_ray_bundle_backward": (_i, [_p, _i64, _i64, _p, _p, _p, _p]),
     "cn_gather_rays_backward": (_i, [_p, _p, _i64, _i64, _p, _i64, _p, _p, _p]),
     "cn_posenc_backward": (_i, [_p, _i64, _i64, _fp, _i64, _i, _p, _p, _p]),
@@ -123,7 +123,7 @@ SIGNATURES = {
     "cn_render_loss_workspace_doubles": (_i64, [_i64]),
     "cn_render_loss": (_i, [_p, _p, _p, _i64, _i64, _p, _p, _i64, _i64, _f, _p, _p, _p]),
     "cn_render_loss_psnr": (_i, [_p, _p, _p, _i64, _i64, _p, _p, _i64, _i64, _f, _p, _p, _p, _p]),
-    "cn_render_loss_backward": (_i, [_p, _p, _p, _i64, _i64, _p, _p, _i64, _i64, _f, _p, _p, _p, _p, _p, _p, _p]),
+    "cn_render_loss_backward": (_i, [_p, _p, _p, _i64, _i64, _p, _p, _i64, _i64, _f, _p, _p, _p, _p, _p, _p, _i, _p]),
     "cn_adamw_step": (_i, [_p, _p, _p, _p, _i64, ctypes.POINTER(_i64), ctypes.POINTER(_i64),
                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i64),
                            ctypes.c_double, ctypes.c_double, ctypes.c_double, _p]),

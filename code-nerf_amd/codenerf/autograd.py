@@ -90,7 +90,8 @@ def prefetch_prepares(fields, z_s, z_t) -> bool:
     """The pre-field launches of a render's two fields (coarse and fine, on the same code rows) as ONE
     cn_field_prepare_models launch before the coarse field; each field's RadianceField.forward then
     takes its part (_take_prepared) instead of launching its own.  ``fields``: [(model, meta, n_rays,
-    needs)] as RadianceField.apply will see them.  False (nothing launched) unless both plan one."""
+    needs)] as RadianceField.apply will see them.  -> [(mode, zeroed buffer)] per field, or False
+    (nothing launched) unless both plan one."""
     entries = []
     for model, meta, n_rays, needs in fields:
         mode, n_zero = _prep_plan(meta, z_s.shape[0], n_rays, needs)
@@ -111,7 +112,7 @@ def prefetch_prepares(fields, z_s, z_t) -> bool:
         if pkt is not None:
             cache["f32_w16_t"] = (sig, pkt)
         cache["prep"] = ((sig, mode, n_zero, key), (cb, zero, act))
-    return True
+    return [(e[2], o[3]) for e, o in zip(entries, outs)]
 
 
 def _take_prepared(owner, params, z_s, z_t, mode, n_zero):
@@ -134,6 +135,52 @@ def backward_from(loss) -> None:
     if one is None:
         one = _ONES[key] = torch.ones((), device=loss.device, dtype=loss.dtype)
     loss.backward(one if loss.dim() == 0 else one.expand_as(loss))
+
+
+def _leaf_sink(ts):
+    """The gradient buffers a backward may add the gradients of leaves ``ts`` into in place, as
+    AccumulateGrad would: each leaf's .grad when it has one (dense, contiguous, fp32), else the
+    optimiser's zeroed flat slot (optim.AdamW.zero_grad), installed as its .grad here.  None when a leaf
+    does not qualify (not a leaf, hooks, no slot): its gradients then go through autograd."""
+    if not ts:
+        return None
+    for t in ts:
+        if not (isinstance(t, torch.Tensor) and t.is_leaf and t.requires_grad) or t._backward_hooks \
+                or getattr(t, "_post_accumulate_grad_hooks", None):
+            return None
+        g = t.grad
+        if g is None:
+            slot = getattr(t, "_cn_grad_slot", None)
+            if slot is None or not slot.is_contiguous() or slot.shape != t.shape:
+                return None
+        elif not (g.layout == torch.strided and g.is_contiguous() and g.dtype == torch.float32
+                  and g.device == t.device):
+            return None
+    out = []
+    for t in ts:
+        if t.grad is None:
+            t.grad, t._cn_grad_slot = t._cn_grad_slot, None      # one use per zero_grad
+        out.append(t.grad)
+    return out
+
+
+class RaySink:
+    """The ray gradients of a pose's rays (PoseRays) added up in place: ``buf`` = (d ro, d rd) (R, 3)
+    zeroed buffers -- set by render_rays' prefetch (the fine field's zeroed accumulators) -- into which
+    both volume renders and both fused field backwards add, returning no gradient; PoseRays.backward
+    reads the sum.  Replaces four (R, 3) autograd adds per eval step (eval.py:145-163)."""
+
+    __slots__ = ("buf",)
+
+    def __init__(self):
+        self.buf = None
+
+
+def _ray_sink(rd, ro=None):
+    s = getattr(rd, "_cn_ray_sink", None)
+    if s is None or (ro is not None and getattr(ro, "_cn_ray_sink", None) is not s):
+        return None
+    return s
 
 
 def _needs_grad(*ts) -> bool:
@@ -192,9 +239,11 @@ class PoseRays(torch.autograd.Function):
     or a c2w (B, 4, 4) -- gradient d c2w, as get_bundle + gather's autograd."""
 
     @staticmethod
-    def forward(ctx, dirs, theta, phi, rho, c2w, sel, target):
+    def forward(ctx, dirs, theta, phi, rho, c2w, sel, target, sink=None):
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(dirs, theta, phi, rho, sel)
+        ctx.sink = sink
+        ctx.leaves = (theta, phi, rho)
         ctx.angles = theta is not None
         ctx.shapes = (theta.shape, phi.shape, rho.shape) if ctx.angles else None
         ctx.batch = theta.numel() if ctx.angles else c2w.shape[0]
@@ -206,7 +255,13 @@ class PoseRays(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_ro, g_rd, _g_c2w, _g_tgt):
-        none = [None] * 7
+        none = [None] * 8
+        sink, ctx.sink = ctx.sink, None
+        if sink is not None and sink.buf is not None:
+            # the consumers that added their ray gradients in place (RaySink), plus any that did not
+            s_ro, s_rd = sink.buf
+            g_ro = s_ro if g_ro is None else s_ro + g_ro
+            g_rd = s_rd if g_rd is None else s_rd + g_rd
         if g_ro is None and g_rd is None:
             return tuple(none)
         dirs, theta, phi, rho, sel = ctx.saved_tensors
@@ -215,8 +270,17 @@ class PoseRays(torch.autograd.Function):
             return tuple(none)
         if not ctx.angles and not want_c2w:
             return tuple(none)
+        # the angle gradients straight into the optimiser's zeroed slots (autograd installs them as .grad)
+        out = None
+        if ctx.angles and all(ctx.needs_input_grad[1:4]):
+            slots = [getattr(t, "_cn_grad_slot", None) if (t.is_leaf and t.grad is None) else None
+                     for t in ctx.leaves]
+            if all(sl is not None and sl.is_contiguous() for sl in slots):
+                for t in ctx.leaves:
+                    t._cn_grad_slot = None
+                out = [sl.view(-1) for sl in slots]
         (dt, dp, dr), d_c2w = ops.pose_rays_backward(dirs, ctx.batch, _c(g_ro), _c(g_rd), theta, phi, rho,
-                                                     select_inds=sel, want_c2w=want_c2w)
+                                                     select_inds=sel, want_c2w=want_c2w, out=out)
         if ctx.angles:
             for i, (g, sh) in enumerate(zip((dt, dp, dr), ctx.shapes)):
                 none[1 + i] = g.view(sh) if ctx.needs_input_grad[1 + i] else None
@@ -261,6 +325,7 @@ class VolumeRender(torch.autograd.Function):
     def forward(ctx, raw, z, rd):
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(raw, z, rd)
+        ctx.ray_sink = _ray_sink(rd)
         return ops.volume_render(raw, z, rd)
 
     @staticmethod
@@ -268,9 +333,11 @@ class VolumeRender(torch.autograd.Function):
         if all(g is None for g in (g_rgb, g_disp, g_acc, g_w, g_depth)):
             return None, None, None
         raw, z, rd = ctx.saved_tensors
+        sink, ctx.ray_sink = ctx.ray_sink, None
+        into = sink.buf[1] if (sink is not None and sink.buf is not None and ctx.needs_input_grad[2]) else None
         d_raw, d_rd = ops.volume_render_backward(raw, z, rd, _c(g_rgb), _c(g_disp), _c(g_acc), _c(g_w), _c(g_depth),
-                                                 want_rd=ctx.needs_input_grad[2])
-        return d_raw, None, d_rd
+                                                 want_rd=ctx.needs_input_grad[2], d_rd_into=into)
+        return d_raw, None, (None if into is not None else d_rd)
 
 
 def _c(t):
@@ -284,26 +351,32 @@ class _FieldMeta:
     """Non-tensor arguments of the field Functions."""
 
     def __init__(self, n_samples, chunk_rows, fx, fd, code_index=None, precision="f32", train_precision="f32",
-                 sink=None):
+                 sink=None, ray_sink=None):
         self.n_samples, self.chunk_rows = n_samples, chunk_rows
         self.precision = precision
         self.train_precision = train_precision
         self.fx, self.fd = list(fx) if fx is not None else None, list(fd) if fd is not None else None
         self.code_index = code_index
         self.sink = sink       # models.model.CodeGradSink of the code rows, or None
+        self.ray_sink = ray_sink   # RaySink of the rays, or None
 
 
-def _code_grads(meta, params, z_s, z_t, g_code, pg, want_z, act=None):
+def _code_grads(meta, params, z_s, z_t, g_code, pg, want_z, act=None, leaves=None):
     """The code backward -> (dz_s, dz_t); (None, None) when they go in place into the code tables'
     gradient rows (meta.sink: the coarse and fine fields of a one-object chunk add up there).  With the
     forward's code-layer activations (act, from the preparation launch): cn_code_bias_backward_act now
-    and cn_code_dz -- for a sink deferred, so both fields' dz are one launch (CodeGradSink.flush);
-    otherwise the recomputing two-launch form (cn_code_bias_backward_ws)."""
+    and cn_code_dz -- for a sink deferred, so both fields' dz are one launch (CodeGradSink.flush), for
+    leaf codes (``leaves``, the eval step) added into their .grad (_leaf_sink); otherwise the recomputing
+    two-launch form (cn_code_bias_backward_ws)."""
     if act is not None:
         ws = ops.code_ds_outer(params, z_s, z_t, act, g_code, pg)
         if not want_z:
             return None, None
         if meta.sink is not None and meta.sink.defer(params, g_code, ws):
+            return None, None
+        bufs = _leaf_sink(leaves)           # leaf codes (the eval step): added into their .grad in place
+        if bufs is not None:
+            ops.code_dz([(params, g_code, ws)], z_s.shape[0], dz_into=tuple(bufs))
             return None, None
         return ops.code_dz([(params, g_code, ws)], z_s.shape[0])
     rows = meta.sink.rows() if (want_z and meta.sink is not None) else None
@@ -345,6 +418,7 @@ class RadianceField(torch.autograd.Function):
     def forward(ctx, meta, rd, pts, ro, z, z_s, z_t, *params):
         ctx.orig_params = params
         ctx.owner = params[0]
+        ctx.z_leaves = (z_s, z_t)
         params = [p.detach() for p in params]
         n_rays = rd.shape[0]
         ctx.empty = n_rays == 0 or z_s.shape[0] == 0
@@ -415,20 +489,26 @@ class RadianceField(torch.autograd.Function):
         rd, pts, ro, z, z_s, z_t, *params = ctx.saved_tensors
         needs = ctx.needs_input_grad
         meta = ctx.meta
+        leaves, ctx.z_leaves = ctx.z_leaves, None
         if ctx.fused:
             want_z = needs[5] or needs[6]
             pack_t = "bf16x3_t" if meta.precision == "bf16x3" else "f32_w16_t"
+            # the rays' gradients added in place into the pose's RaySink (no autograd sums)
+            rs = meta.ray_sink
+            ray_into = rs.buf if (rs is not None and rs.buf is not None and needs[1] and needs[3]) else None
             r = ops.field_backward_x3(_packed(ctx.owner, params, pack_t), ctx.masks, g_raw.contiguous(), rd.shape[0],
                                       meta.n_samples, meta.chunk_rows, z_s.shape[0], meta.fx, meta.fd, rd=rd,
                                       pts=pts, ro=ro, z=z, code_index=meta.code_index, want_pts=needs[2],
-                                      want_ro=needs[3], want_rd=needs[1], precision=meta.precision, acc=ctx.acc)
+                                      want_ro=needs[3], want_rd=needs[1], precision=meta.precision, acc=ctx.acc,
+                                      ray_into=ray_into)
             ctx.acc = None
             dz_s = dz_t = None
             if want_z:
-                dz_s, dz_t = _code_grads(meta, params, z_s, z_t, r["g_code"], None, True, ctx.code_act)
+                dz_s, dz_t = _code_grads(meta, params, z_s, z_t, r["g_code"], None, True, ctx.code_act, leaves)
             ctx.code_act = None
             ctx.masks = None
-            return (None, r["d_rd"], r["d_pts"], r["d_ro"], None, dz_s, dz_t, *([None] * len(params)))
+            d_ro, d_rd = (None, None) if ray_into is not None else (r["d_ro"], r["d_rd"])
+            return (None, d_rd, r["d_pts"], d_ro, None, dz_s, dz_t, *([None] * len(params)))
         pg = _param_grad_buffers(params, needs[7:], ctx.orig_params)
         ctx.orig_params = None
         want_z = needs[5] or needs[6]
@@ -441,7 +521,7 @@ class RadianceField(torch.autograd.Function):
                                          want_ro=needs[3], want_rd=needs[1], precision=meta.precision,
                                          g_code=ctx.g_code)
             act, ctx.acts, ctx.x_enc, ctx.masks, ctx.g_code, ctx.code_act = ctx.code_act, None, None, None, None, None
-            dz_s, dz_t = _code_grads(meta, params, z_s, z_t, r["g_code"], pg, want_z, act)
+            dz_s, dz_t = _code_grads(meta, params, z_s, z_t, r["g_code"], pg, want_z, act, leaves)
             grads = pg if pg is not None else [None] * len(params)
             return (None, r["d_rd"], r["d_pts"], r["d_ro"], None, dz_s, dz_t, *grads)
         r = ops.field_backward(params, ctx.acts, ctx.x_enc, g_raw.contiguous(), rd.shape[0], meta.n_samples,
@@ -501,17 +581,25 @@ class RenderLoss(torch.autograd.Function):
         stats = ops.render_loss(rgb_c, rgb_f, target, z_s, z_t, expand, lam, psnr=psnr)
         ctx.save_for_backward(rgb_c, rgb_f, target, z_s, z_t, stats)
         ctx.expand, ctx.lam = expand, lam
+        ctx.z_leaves = (z_s, z_t) if z_s is not None and z_t is not None else None
         ctx.mark_non_differentiable(stats)
         return stats[3], stats
 
     @staticmethod
     def backward(ctx, g_total, _g_stats):
+        leaves, ctx.z_leaves = ctx.z_leaves, None
         if g_total is None:
             return (None,) * 8
         rgb_c, rgb_f, target, z_s, z_t, stats = ctx.saved_tensors
         want = ctx.needs_input_grad[:2] + ctx.needs_input_grad[3:5]
+        # the codes' gradient straight into their .grad (the eval step's leaf codes, _leaf_sink): the field
+        # backwards then add theirs there too, no autograd sums
+        bufs = _leaf_sink(leaves) if (want[2] and want[3]) else None
         d = ops.render_loss_backward(rgb_c, rgb_f, target, z_s, z_t, ctx.expand, ctx.lam, stats,
-                                     g_total.reshape(1).contiguous(), want)
+                                     g_total.reshape(1).contiguous(), want,
+                                     dz_into=None if bufs is None else tuple(b.view(-1) for b in bufs))
+        if bufs is not None:
+            return d[0], d[1], None, None, None, None, None, None
         return d[0], d[1], None, d[2], d[3], None, None, None
 
 
@@ -540,7 +628,10 @@ def pose_rays_autograd(dirs, theta=None, phi=None, rho=None, c2w=None, sel=None,
     tgt = None if target is None else target.detach()
     if not _needs_grad(theta, phi, rho, c2w):
         return ops.pose_rays(dirs, _d(theta), _d(phi), _d(rho), c2w=_d(c2w), select_inds=sel, target=tgt)
-    return PoseRays.apply(dirs.detach(), theta, phi, rho, c2w, sel, tgt)
+    sink = RaySink()
+    ro, rd, c2w_out, tgt_out = PoseRays.apply(dirs.detach(), theta, phi, rho, c2w, sel, tgt, sink)
+    ro._cn_ray_sink = rd._cn_ray_sink = sink
+    return ro, rd, c2w_out, tgt_out
 
 
 def gather_rays_autograd(ro, rd, sel):
@@ -581,18 +672,19 @@ def mlp_forward_autograd(model, z_s, z_t, x):
     return MLPForward.apply(getattr(model, "train_precision", "f32"), x, cs, ct, *model.param_list())
 
 
-def _field_meta(model, cs, ct, n_samples, chunk_rows, fx, fd, code_index):
+def _field_meta(model, cs, ct, n_samples, chunk_rows, fx, fd, code_index, rd=None, ro=None):
     sink = getattr(cs, "_cn_sink", None)
     return _FieldMeta(n_samples, chunk_rows, fx, fd, code_index=code_index,
                       precision=getattr(model, "precision", "f32"),
                       train_precision=getattr(model, "train_precision", "f32"),
-                      sink=sink if sink is not None and getattr(ct, "_cn_sink", None) is sink else None)
+                      sink=sink if sink is not None and getattr(ct, "_cn_sink", None) is sink else None,
+                      ray_sink=_ray_sink(rd, ro) if (rd is not None and ro is not None) else None)
 
 
 def radiance_field_autograd(model, rd, z_s, z_t, chunk_rows, fx, fd, pts=None, ro=None, z=None, code_index=None):
     cs, ct = (z_s, z_t) if code_index is not None else _code_rows(z_s, z_t)
     n_samples = pts.shape[1] if pts is not None else z.shape[1]
-    meta = _field_meta(model, cs, ct, n_samples, chunk_rows, fx, fd, code_index)
+    meta = _field_meta(model, cs, ct, n_samples, chunk_rows, fx, fd, code_index, rd, ro)
     return RadianceField.apply(meta, rd, pts, ro, _d(z), cs, ct, *model.param_list())
 
 
@@ -610,4 +702,11 @@ def prefetch_render_prepares(coarse, fine, rd, ro, cs, ct, n_coarse, n_fine, chu
         if not any(needs):
             return False                  # _field_op takes the no-grad path
         fields.append((model, _field_meta(model, cs, ct, n_s, chunk_rows, fx, fd, code_index), rd.shape[0], needs))
-    return prefetch_prepares(fields, cs, ct)
+    done = prefetch_prepares(fields, cs, ct)
+    sink = _ray_sink(rd, ro)
+    if done and sink is not None and rd.requires_grad and ro.requires_grad and all(m == "fused" for m, _ in done):
+        # the rays' gradient sums live in the fine field's zeroed d ro / d rd accumulators
+        # (field_backward_x3's layout: g_code, d ro, d rd)
+        acc, n = done[1][1], rd.shape[0]
+        sink.buf = (acc[acc.numel() - 6 * n:acc.numel() - 3 * n].view(n, 3), acc[acc.numel() - 3 * n:].view(n, 3))
+    return bool(done)

@@ -123,15 +123,21 @@ def pose_rays(dirs: Tensor, theta: Optional[Tensor] = None, phi: Optional[Tensor
 
 def pose_rays_backward(dirs: Tensor, batch: int, g_ro: Optional[Tensor], g_rd: Optional[Tensor],
                        theta: Optional[Tensor] = None, phi: Optional[Tensor] = None, rho: Optional[Tensor] = None,
-                       select_inds: Optional[Tensor] = None, want_c2w: bool = False):
-    """Backward of pose_rays -> (d_theta, d_phi, d_rho (B,) each | None, d_c2w (B,4,4) | None)."""
+                       select_inds: Optional[Tensor] = None, want_c2w: bool = False, out=None):
+    """Backward of pose_rays -> (d_theta, d_phi, d_rho (B,) each | None, d_c2w (B,4,4) | None).  ``out``:
+    three (B,) contiguous device tensors the angle gradients are written into (e.g. the optimiser's
+    gradient slots)."""
     lib = _lib_ready()
     dirs = _cuda(dirs, "directions")
     hw = dirs.numel() // 3
     s = hw if select_inds is None else select_inds.shape[1]
     g_ro, g_rd = _opt(g_ro, "g_ro"), _opt(g_rd, "g_rd")
     angles = theta is not None
-    d = [torch.empty(batch, device=dirs.device, dtype=torch.float32) if angles else None for _ in range(3)]
+    if out is not None and angles:
+        assert all(t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.numel() == batch for t in out)
+        d = list(out)
+    else:
+        d = [torch.empty(batch, device=dirs.device, dtype=torch.float32) if angles else None for _ in range(3)]
     d_c2w = torch.empty(batch, 4, 4, device=dirs.device, dtype=torch.float32) if want_c2w else None
     check(lib.cn_pose_rays_backward(ptr(theta), ptr(phi), ptr(rho), batch, ptr(dirs), hw, ptr(select_inds), s,
                                     ptr(g_ro), ptr(g_rd), ptr(d_c2w), ptr(d[0]), ptr(d[1]), ptr(d[2]),
@@ -428,8 +434,10 @@ def _opt(t: Optional[Tensor], name: str) -> Optional[Tensor]:
 
 
 def volume_render_backward(raw: Tensor, z: Tensor, rd: Tensor, g_rgb=None, g_disp=None, g_acc=None,
-                           g_weights=None, g_depth=None, want_rd: bool = True) -> Tuple[Tensor, Optional[Tensor]]:
-    """Gradient of volume_render (volumetric_render.py:36-66) -> d_raw (R,S,4), d_rd (R,3) or None."""
+                           g_weights=None, g_depth=None, want_rd: bool = True,
+                           d_rd_into: Optional[Tensor] = None) -> Tuple[Tensor, Optional[Tensor]]:
+    """Gradient of volume_render (volumetric_render.py:36-66) -> d_raw (R,S,4), d_rd (R,3) or None.
+    ``d_rd_into`` (a contiguous (R, 3) device tensor): d rd ADDED into it (accumulate_rd) and returned."""
     lib = _lib_ready()
     raw, z, rd = _cuda(raw, "radiance_field"), _cuda(z, "depth_values"), _cuda(rd, "ray_directions")
     raw, z = _aligned16(raw), _aligned16(z)
@@ -441,12 +449,16 @@ def volume_render_backward(raw: Tensor, z: Tensor, rd: Tensor, g_rgb=None, g_dis
         g_weights = None
     g_weights = _opt(g_weights, "g_weights")
     d_raw = torch.empty_like(raw)
-    d_rd = torch.empty_like(rd) if want_rd else None
+    if d_rd_into is not None:
+        assert d_rd_into.is_cuda and d_rd_into.is_contiguous() and d_rd_into.shape == (n, 3)
+        d_rd = d_rd_into
+    else:
+        d_rd = torch.empty_like(rd) if want_rd else None
     if n == 0:      # no rays: empty gradients (the C ABI refuses n_rays == 0), as the forward
         return d_raw, d_rd
     check(lib.cn_volume_render_backward(ptr(raw), ptr(z), ptr(rd), n, s, ptr(g_rgb), ptr(g_disp), ptr(g_acc),
-                                        ptr(g_weights), ptr(g_depth), ptr(d_raw), ptr(d_rd), stream_of(raw)),
-          "cn_volume_render_backward")
+                                        ptr(g_weights), ptr(g_depth), ptr(d_raw), ptr(d_rd),
+                                        int(d_rd_into is not None), stream_of(raw)), "cn_volume_render_backward")
     return d_raw, d_rd
 
 
@@ -867,11 +879,12 @@ def field_backward_x3(packed_t: Tensor, masks: Tensor, d_raw: Tensor, n_rays: in
                       rd: Tensor, pts: Optional[Tensor] = None, ro: Optional[Tensor] = None,
                       z: Optional[Tensor] = None, code_index: Optional[Tensor] = None, want_pts: bool = False,
                       want_ro: bool = False, want_rd: bool = False, precision: str = "bf16x3",
-                      acc: Optional[Tensor] = None):
+                      acc: Optional[Tensor] = None, ray_into: Optional[Tuple[Tensor, Tensor]] = None):
     """Fused backward of forward_pass + CodeNeRFModel.forward (frozen weights) -> g_code / d_pts / d_ro / d_rd.
     precision "bf16x3" (packed_t "bf16x3_t") or "f32" (packed_t "f32_w16_t", masks of the f32_w16 forward).
     ``acc``: a zeroed buffer of field_backward_x3_acc_floats(...) floats for the accumulated outputs
-    (field_prepare's), else one is allocated and filled."""
+    (field_prepare's), else one is allocated and filled.  ``ray_into`` ((R, 3) d ro, d rd device tensors,
+    with want_ro and want_rd): the ray gradients are ADDED into those (the kernel's atomics) instead."""
     fmt_t = _lib.CN_FMT_BF16X3_T if precision == "bf16x3" else _lib.CN_FMT_F32_W16_T
     lib = _lib_ready()
     m = n_rays * n_samples
@@ -891,6 +904,9 @@ def field_backward_x3(packed_t: Tensor, masks: Tensor, d_raw: Tensor, n_rays: in
     g_code = acc[:nc].view(n_codes, _lib.CN_CODE_BIAS_STRIDE)
     d_ro = acc[nc:nc + 3 * n_rays].view(n_rays, 3) if want_ro else None
     d_rd = acc[acc.numel() - 3 * n_rays:].view(n_rays, 3) if want_rd else None
+    if ray_into is not None:
+        assert want_ro and want_rd and all(t.is_cuda and t.is_contiguous() and t.shape == (n_rays, 3) for t in ray_into)
+        d_ro, d_rd = ray_into
     d_pts = torch.empty(n_rays, n_samples, 3, device=dev, dtype=torch.float32) if want_pts else None
     if m == 0:      # no samples: zero sums (the C ABI refuses n_rays == 0)
         return {"g_code": g_code, "d_pts": d_pts, "d_ro": d_ro, "d_rd": d_rd}
@@ -998,8 +1014,9 @@ def render_loss(rgb_coarse: Optional[Tensor], rgb_fine: Optional[Tensor], target
 
 
 def render_loss_backward(rgb_coarse, rgb_fine, target, z_s, z_t, expand, regularizer_lambda, stats, grad_total,
-                         want=(True, True, True, True)):
-    """Backward of render_loss -> (d_rgb_coarse, d_rgb_fine, d_z_s, d_z_t), None where not wanted."""
+                         want=(True, True, True, True), dz_into: Optional[Tuple[Tensor, Tensor]] = None):
+    """Backward of render_loss -> (d_rgb_coarse, d_rgb_fine, d_z_s, d_z_t), None where not wanted.
+    ``dz_into`` (two contiguous device tensors of z_s's / z_t's size): d z ADDED into them and returned."""
     lib = _lib_ready()
     rc, rf = _opt(rgb_coarse, "rgb_coarse"), _opt(rgb_fine, "rgb_fine")
     target = _cuda(target, "target")
@@ -1007,9 +1024,14 @@ def render_loss_backward(rgb_coarse, rgb_fine, target, z_s, z_t, expand, regular
     zs, zt = _opt(z_s, "z_s"), _opt(z_t, "z_t")
     n_code = 0 if zs is None else zs.numel()
     outs = [torch.empty_like(t) if (w and t is not None) else None for w, t in zip(want, (rc, rf, zs, zt))]
+    if dz_into is not None:
+        for d in dz_into:
+            assert d.is_cuda and d.dtype == torch.float32 and d.is_contiguous() and d.numel() == n_code
+        outs[2], outs[3] = dz_into
     check(lib.cn_render_loss_backward(ptr(rc), ptr(rf), ptr(target), target.shape[1], n, ptr(zs), ptr(zt), n_code,
                                       expand, regularizer_lambda, ptr(stats), ptr(_cuda(grad_total, "grad")),
-                                      *[ptr(o) for o in outs], stream_of(target)), "cn_render_loss_backward")
+                                      *[ptr(o) for o in outs], int(dz_into is not None), stream_of(target)),
+          "cn_render_loss_backward")
     return tuple(outs)
 
 

@@ -152,7 +152,7 @@ __global__ void render_loss_backward_kernel(const float* __restrict__ rgb_c, con
                                             int64_t n_code, float expand, float lambda,
                                             const float* __restrict__ stats, const float* __restrict__ grad,
                                             float* __restrict__ d_rgb_c, float* __restrict__ d_rgb_f,
-                                            float* __restrict__ d_zs, float* __restrict__ d_zt) {
+                                            float* __restrict__ d_zs, float* __restrict__ d_zt, int accumulate_z) {
   const float g = *grad;
   const int64_t n = n_rays * 3;
   const float k = __fdiv_rn(2.0f, static_cast<float>(n));
@@ -166,8 +166,13 @@ __global__ void render_loss_backward_kernel(const float* __restrict__ rgb_c, con
   const float ks = stats[4] > 0.0f ? g * lambda * expand / stats[4] : 0.0f;
   const float kt = stats[5] > 0.0f ? g * lambda * expand / stats[5] : 0.0f;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n_code; i += (int64_t)gridDim.x * blockDim.x) {
-    if (d_zs) d_zs[i] = ks * zs[i];
-    if (d_zt) d_zt[i] = kt * zt[i];
+    if (accumulate_z) {
+      if (d_zs) d_zs[i] += ks * zs[i];
+      if (d_zt) d_zt[i] += kt * zt[i];
+    } else {
+      if (d_zs) d_zs[i] = ks * zs[i];
+      if (d_zt) d_zt[i] = kt * zt[i];
+    }
   }
 }
 
@@ -208,14 +213,15 @@ extern "C" int cn_render_loss_backward(const float* rgb_coarse, const float* rgb
                                        int64_t target_stride, int64_t n_rays, const float* z_s, const float* z_t,
                                        int64_t n_code, int64_t expand, float regularizer_lambda, const float* stats,
                                        const float* grad_total, float* d_rgb_coarse, float* d_rgb_fine,
-                                       float* d_z_s, float* d_z_t, cn_stream_t stream) {
+                                       float* d_z_s, float* d_z_t, int accumulate_z, cn_stream_t stream) {
   CN_CHECK_ARG(n_rays > 0 && target && target_stride >= 3 && stats && grad_total);
+  CN_CHECK_ARG(accumulate_z == 0 || accumulate_z == 1);
   CN_CHECK_ARG((!d_rgb_coarse || rgb_coarse) && (!d_rgb_fine || rgb_fine));
   CN_CHECK_ARG((!d_z_s && !d_z_t) || (z_s && z_t && n_code > 0 && expand >= 1));
   const int64_t n = std::max<int64_t>(n_rays * 3, n_code);
   hipLaunchKernelGGL(render_loss_backward_kernel, dim3(cn::elementwise_grid(n, 256)), dim3(256), 0,
                      cn::as_stream(stream), rgb_coarse, rgb_fine, target, target_stride, n_rays, z_s, z_t, n_code,
                      static_cast<float>(expand), regularizer_lambda, stats, grad_total, d_rgb_coarse, d_rgb_fine,
-                     d_z_s, d_z_t);
+                     d_z_s, d_z_t, accumulate_z);
   return cn::launch_status();
 }

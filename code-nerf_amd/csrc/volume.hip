@@ -410,7 +410,7 @@ __global__ __launch_bounds__(256) void volume_render_backward_kernel(
     const float* __restrict__ raw, const float* __restrict__ z, const float* __restrict__ rd,
     int64_t n_rays, int S_in, const float* __restrict__ g_rgb, const float* __restrict__ g_disp,
     const float* __restrict__ g_acc, const float* __restrict__ g_w, const float* __restrict__ g_depth,
-    float* __restrict__ d_raw, float* __restrict__ d_rd) {
+    float* __restrict__ d_raw, float* __restrict__ d_rd, int accumulate_rd) {
   static_assert(K <= kMaxRun && (L == 16 || L == 64) && (!FULL || L == 16), "instance");
   if (FULL) S_in = L * K;  // as in the forward
   __shared__ float4 slds[4 * 80 * K];  // per wave: raw in, then d raw out (forward's layout)
@@ -524,9 +524,15 @@ __global__ __launch_bounds__(256) void volume_render_backward_kernel(
   gnorm = ray_sum<L>(gnorm);
   if (live && sub == (L == 16 ? 15 : 63) && d_rd) {
     const float inv = nrm > 0.f ? gnorm / nrm : 0.f;
-    d_rd[3 * r] = inv * d0;
-    d_rd[3 * r + 1] = inv * d1;
-    d_rd[3 * r + 2] = inv * d2;
+    if (accumulate_rd) {      // one writer per ray: the caller's running sum of the ray's gradients
+      d_rd[3 * r] += inv * d0;
+      d_rd[3 * r + 1] += inv * d1;
+      d_rd[3 * r + 2] += inv * d2;
+    } else {
+      d_rd[3 * r] = inv * d0;
+      d_rd[3 * r + 1] = inv * d1;
+      d_rd[3 * r + 2] = inv * d2;
+    }
   }
 }
 
@@ -536,11 +542,12 @@ extern "C" int cn_volume_render_backward(const float* raw, const float* z, const
                                          int64_t n_rays, int64_t n_samples, const float* g_rgb,
                                          const float* g_disp, const float* g_acc,
                                          const float* g_weights, const float* g_depth,
-                                         float* d_raw, float* d_rd, cn_stream_t stream) {
-  CN_CHECK_ARG(raw && z && rd && d_raw);
+                                         float* d_raw, float* d_rd, int accumulate_rd, cn_stream_t stream) {
+  CN_CHECK_ARG(raw && z && rd && d_raw && (accumulate_rd == 0 || accumulate_rd == 1));
   CN_CHECK_ARG(n_rays > 0 && n_samples > 0 && n_samples <= kMaxSamples);
   CN_CHECK_ARG(cn::aligned16(raw) && cn::aligned16(z) && cn::aligned16(d_raw));
   CN_VOLUME_DISPATCH(volume_render_backward_kernel, n_samples, n_rays, cn::as_stream(stream), raw, z, rd, n_rays,
-                     static_cast<int>(n_samples), g_rgb, g_disp, g_acc, g_weights, g_depth, d_raw, d_rd);
+                     static_cast<int>(n_samples), g_rgb, g_disp, g_acc, g_weights, g_depth, d_raw, d_rd,
+                     accumulate_rd);
   return cn::launch_status();
 }

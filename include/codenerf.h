@@ -437,11 +437,13 @@ int cn_code_bias_backward_ws(const float* const* params, const float* z_s, const
 /* Backward of volume_render (volumetric_render.py:36-66) w.r.t. raw and rd
  * (z is detached in the reference).  Any of g_rgb (R,3), g_disp, g_acc, g_depth
  * (R), g_weights (R,S) may be NULL (zero).  d_raw (R,S,4) and d_rd (R,3, may be
- * NULL) are written.  raw, z and d_raw 16-B aligned, or CN_EINVAL. */
+ * NULL) are written -- d_rd added to instead with accumulate_rd = 1 (a running sum
+ * of the rays' gradients over their consumers).  raw, z and d_raw 16-B aligned, or
+ * CN_EINVAL. */
 int cn_volume_render_backward(const float* raw, const float* z, const float* rd, int64_t n_rays,
                               int64_t n_samples, const float* g_rgb, const float* g_disp,
                               const float* g_acc, const float* g_weights, const float* g_depth,
-                              float* d_raw, float* d_rd, cn_stream_t stream);
+                              float* d_raw, float* d_rd, int accumulate_rd, cn_stream_t stream);
 
 /* Backward of get_bundle (ray_sampler.py:95-98): d_c2w (batch, 4, 4) rows 0..2
  * ACCUMULATED from g_ro / g_rd (batch*hw, 3), either may be NULL (not both). */
@@ -484,12 +486,13 @@ int cn_render_loss_psnr(const float* rgb_coarse, const float* rgb_fine, const fl
                         int64_t n_code, int64_t expand, float regularizer_lambda, double* workspace,
                         float* out, double* psnr, cn_stream_t stream);
 /* Its backward for an upstream gradient *grad_total (device scalar) of the sum, reading
- * the forward's out as stats: d_rgb_* (n_rays, 3) and d_z_* (n_code) WRITTEN (any NULL). */
+ * the forward's out as stats: d_rgb_* (n_rays, 3) and d_z_* (n_code) WRITTEN (any NULL);
+ * accumulate_z = 1: d_z_* added to (the codes' running gradient). */
 int cn_render_loss_backward(const float* rgb_coarse, const float* rgb_fine, const float* target,
                             int64_t target_stride, int64_t n_rays, const float* z_s, const float* z_t,
                             int64_t n_code, int64_t expand, float regularizer_lambda, const float* stats,
                             const float* grad_total, float* d_rgb_coarse, float* d_rgb_fine, float* d_z_s,
-                            float* d_z_t, cn_stream_t stream);
+                            float* d_z_t, int accumulate_z, cn_stream_t stream);
 
 /* --- Training step: the optimiser (train.py:111-114, utils/util.py:147-172) ---
  * torch.optim.AdamW.step (decoupled weight decay; amsgrad / maximize off) over ONE

@@ -209,6 +209,50 @@ def test_eval_c5_fused_at_size(dev, precision):
     close(zt.grad, g["g_z_t"], 2e-3, "g_z_t")
 
 
+@pytest.mark.parametrize("precision", ["f32", "bf16x3"])
+def test_eval_step_in_place_gradients(dev, monkeypatch, precision):
+    """The eval step's gradient sinks (C5 inputs, the flat AdamW's zeroed slots handed out by zero_grad):
+    the codes' gradients added in place into their .grad by the loss and both fields (_leaf_sink), the
+    rays' by both volume renders and both fields into the fine field's zeroed accumulators (RaySink),
+    the pose angles' written into their slots -- every leaf's .grad is then its flat slice (no autograd
+    adds, no copy into the flat buffer) -- against the route through autograd: the loss bit for bit, the
+    code gradients to 1e-6 (same sums, same order), the angles to 1e-5 (the ray sums' atomics round
+    differently)."""
+    from codenerf import autograd as A, synthetic
+    from codenerf.evaluate import eval_step_loss
+    from codenerf.nerf import PointSampler, RaySampler
+    from codenerf.optim import AdamW
+    g = gload("eval_c5.npz", dev)
+    rs = RaySampler(128, 128, synthetic.srn_intrinsics(128), sample_size=2048, device=dev, datatype=torch.float32)
+    ps = PointSampler(64, 64, 0.8, 1.8, "lindepth", True, torch.float32, dev)
+    models = _eval_models(dev)
+    for m in models.values():
+        m.precision = precision
+    out = []
+    for on in (True, False):
+        if not on:
+            monkeypatch.setattr(A, "_leaf_sink", lambda ts: None)
+            monkeypatch.setattr(A, "_ray_sink", lambda rd, ro=None: None)
+        lv = [g[k].clone().requires_grad_(True) for k in ("theta", "phi", "rho", "z_s", "z_t")]
+        opt = AdamW([{"params": lv[3:]}, {"params": lv[:2]}, {"params": lv[2:3]}], lr=1e-2)
+        opt.zero_grad()
+        np.random.seed(17)
+        loss, _ = eval_step_loss(*lv, g["target"], (rs, ps), embedders(dev), models, 1e-5, t_rand=g["t_rand"],
+                                 u=g["u"])
+        A.backward_from(loss)
+        torch.cuda.synchronize()
+        if on:
+            flat = opt.flat_buffers()["grad"]
+            lo, hi = flat.data_ptr(), flat.data_ptr() + 4 * flat.numel()
+            for t in lv:
+                assert lo <= t.grad.data_ptr() < hi, "a leaf's .grad is not its flat slice"
+        out.append((loss.item(), [t.grad.clone() for t in lv]))
+    (l0, g0), (l1, g1) = out
+    assert l0 == l1
+    for name, a, b in zip(("theta", "phi", "rho", "z_s", "z_t"), g0, g1):
+        close(a, b, 1e-6 if name.startswith("z") else 1e-5, name)
+
+
 # ---------------------------------------------------------------- the fused step loss
 
 
