@@ -137,33 +137,6 @@ def backward_from(loss) -> None:
     loss.backward(one if loss.dim() == 0 else one.expand_as(loss))
 
 
-def _leaf_sink(ts):
-    """The gradient buffers a backward may add the gradients of leaves ``ts`` into in place, as
-    AccumulateGrad would: each leaf's .grad when it has one (dense, contiguous, fp32), else the
-    optimiser's zeroed flat slot (optim.AdamW.zero_grad), installed as its .grad here.  None when a leaf
-    does not qualify (not a leaf, hooks, no slot): its gradients then go through autograd."""
-    if not ts:
-        return None
-    for t in ts:
-        if not (isinstance(t, torch.Tensor) and t.is_leaf and t.requires_grad) or t._backward_hooks \
-                or getattr(t, "_post_accumulate_grad_hooks", None):
-            return None
-        g = t.grad
-        if g is None:
-            slot = getattr(t, "_cn_grad_slot", None)
-            if slot is None or not slot.is_contiguous() or slot.shape != t.shape:
-                return None
-        elif not (g.layout == torch.strided and g.is_contiguous() and g.dtype == torch.float32
-                  and g.device == t.device):
-            return None
-    out = []
-    for t in ts:
-        if t.grad is None:
-            t.grad, t._cn_grad_slot = t._cn_grad_slot, None      # one use per zero_grad
-        out.append(t.grad)
-    return out
-
-
 class RaySink:
     """The ray gradients of a pose's rays (PoseRays) added up in place: ``buf`` = (d ro, d rd) (R, 3)
     zeroed buffers -- set by render_rays' prefetch (the fine field's zeroed accumulators) -- into which
@@ -361,22 +334,17 @@ class _FieldMeta:
         self.ray_sink = ray_sink   # RaySink of the rays, or None
 
 
-def _code_grads(meta, params, z_s, z_t, g_code, pg, want_z, act=None, leaves=None):
+def _code_grads(meta, params, z_s, z_t, g_code, pg, want_z, act=None):
     """The code backward -> (dz_s, dz_t); (None, None) when they go in place into the code tables'
     gradient rows (meta.sink: the coarse and fine fields of a one-object chunk add up there).  With the
     forward's code-layer activations (act, from the preparation launch): cn_code_bias_backward_act now
-    and cn_code_dz -- for a sink deferred, so both fields' dz are one launch (CodeGradSink.flush), for
-    leaf codes (``leaves``, the eval step) added into their .grad (_leaf_sink); otherwise the recomputing
-    two-launch form (cn_code_bias_backward_ws)."""
+    and cn_code_dz -- for a sink deferred, so both fields' dz are one launch (CodeGradSink.flush);
+    otherwise the recomputing two-launch form (cn_code_bias_backward_ws)."""
     if act is not None:
         ws = ops.code_ds_outer(params, z_s, z_t, act, g_code, pg)
         if not want_z:
             return None, None
         if meta.sink is not None and meta.sink.defer(params, g_code, ws):
-            return None, None
-        bufs = _leaf_sink(leaves)           # leaf codes (the eval step): added into their .grad in place
-        if bufs is not None:
-            ops.code_dz([(params, g_code, ws)], z_s.shape[0], dz_into=tuple(bufs))
             return None, None
         return ops.code_dz([(params, g_code, ws)], z_s.shape[0])
     rows = meta.sink.rows() if (want_z and meta.sink is not None) else None
@@ -418,7 +386,6 @@ class RadianceField(torch.autograd.Function):
     def forward(ctx, meta, rd, pts, ro, z, z_s, z_t, *params):
         ctx.orig_params = params
         ctx.owner = params[0]
-        ctx.z_leaves = (z_s, z_t)
         params = [p.detach() for p in params]
         n_rays = rd.shape[0]
         ctx.empty = n_rays == 0 or z_s.shape[0] == 0
@@ -489,7 +456,6 @@ class RadianceField(torch.autograd.Function):
         rd, pts, ro, z, z_s, z_t, *params = ctx.saved_tensors
         needs = ctx.needs_input_grad
         meta = ctx.meta
-        leaves, ctx.z_leaves = ctx.z_leaves, None
         if ctx.fused:
             want_z = needs[5] or needs[6]
             pack_t = "bf16x3_t" if meta.precision == "bf16x3" else "f32_w16_t"
@@ -504,7 +470,7 @@ class RadianceField(torch.autograd.Function):
             ctx.acc = None
             dz_s = dz_t = None
             if want_z:
-                dz_s, dz_t = _code_grads(meta, params, z_s, z_t, r["g_code"], None, True, ctx.code_act, leaves)
+                dz_s, dz_t = _code_grads(meta, params, z_s, z_t, r["g_code"], None, True, ctx.code_act)
             ctx.code_act = None
             ctx.masks = None
             d_ro, d_rd = (None, None) if ray_into is not None else (r["d_ro"], r["d_rd"])
@@ -521,7 +487,7 @@ class RadianceField(torch.autograd.Function):
                                          want_ro=needs[3], want_rd=needs[1], precision=meta.precision,
                                          g_code=ctx.g_code)
             act, ctx.acts, ctx.x_enc, ctx.masks, ctx.g_code, ctx.code_act = ctx.code_act, None, None, None, None, None
-            dz_s, dz_t = _code_grads(meta, params, z_s, z_t, r["g_code"], pg, want_z, act, leaves)
+            dz_s, dz_t = _code_grads(meta, params, z_s, z_t, r["g_code"], pg, want_z, act)
             grads = pg if pg is not None else [None] * len(params)
             return (None, r["d_rd"], r["d_pts"], r["d_ro"], None, dz_s, dz_t, *grads)
         r = ops.field_backward(params, ctx.acts, ctx.x_enc, g_raw.contiguous(), rd.shape[0], meta.n_samples,
@@ -581,24 +547,25 @@ class RenderLoss(torch.autograd.Function):
         stats = ops.render_loss(rgb_c, rgb_f, target, z_s, z_t, expand, lam, psnr=psnr)
         ctx.save_for_backward(rgb_c, rgb_f, target, z_s, z_t, stats)
         ctx.expand, ctx.lam = expand, lam
-        ctx.z_leaves = (z_s, z_t) if z_s is not None and z_t is not None else None
+        sink = getattr(z_s, "_cn_sink", None) if z_s is not None else None
+        ctx.code_sink = sink if (sink is not None and getattr(z_t, "_cn_sink", None) is sink) else None
         ctx.mark_non_differentiable(stats)
         return stats[3], stats
 
     @staticmethod
     def backward(ctx, g_total, _g_stats):
-        leaves, ctx.z_leaves = ctx.z_leaves, None
+        sink, ctx.code_sink = ctx.code_sink, None
         if g_total is None:
             return (None,) * 8
         rgb_c, rgb_f, target, z_s, z_t, stats = ctx.saved_tensors
         want = ctx.needs_input_grad[:2] + ctx.needs_input_grad[3:5]
-        # the codes' gradient straight into their .grad (the eval step's leaf codes, _leaf_sink): the field
-        # backwards then add theirs there too, no autograd sums
-        bufs = _leaf_sink(leaves) if (want[2] and want[3]) else None
+        # the code rows' gradient added in place into their CodeGradSink (the eval step's codes): the field
+        # backwards add theirs there too, no autograd sums
+        rows = sink.rows() if (sink is not None and want[2] and want[3]) else None
         d = ops.render_loss_backward(rgb_c, rgb_f, target, z_s, z_t, ctx.expand, ctx.lam, stats,
                                      g_total.reshape(1).contiguous(), want,
-                                     dz_into=None if bufs is None else tuple(b.view(-1) for b in bufs))
-        if bufs is not None:
+                                     dz_into=None if rows is None else tuple(r.reshape(-1) for r in rows))
+        if rows is not None:
             return d[0], d[1], None, None, None, None, None, None
         return d[0], d[1], None, d[2], d[3], None, None, None
 

@@ -53,7 +53,12 @@ def eval_step_loss(theta, phi, rho, shape_code, texture_code, target_pixels, sam
     ray_sampler, point_sampler = samplers
     ro, rd, select_inds, cam_pose, tp = ray_sampler.sample_spherical(theta, phi, rho, target=target_pixels, sel=sel)
     n = ro.shape[0]
+    # the code rows, with their gradient summed in place (code_rows_with_sink), expanded over the rays
+    from .models.model import CodeRows, code_rows_with_sink
+    shape_code, texture_code = code_rows_with_sink(shape_code, texture_code)
     z_s, z_t = shape_code.expand(n, -1), texture_code.expand(n, -1)
+    if shape_code.dim() == 2 and shape_code.shape[0] == 1:
+        z_s._cn_code_rows = z_t._cn_code_rows = CodeRows(shape_code, texture_code, None)
     # predict_radiance_and_render (nerf/__init__.py:74-91) over the whole ray batch
     out = nerf.render_rays(ro, rd, z_s, z_t, point_sampler, embedders, models["nerf_coarse"], models["nerf_fine"],
                            chunk_rows=n, t_rand=t_rand, u=u)

@@ -213,6 +213,9 @@ class _TableRow(torch.autograd.Function):
             elif g is None:
                 out.append(None)
                 continue
+            elif w.shape[0] == 1:
+                out.append(g)                     # a one-row "table" (the eval step's code leaf): g is its grad
+                continue
             else:
                 slot = getattr(w, "_cn_grad_slot", None)
                 if slot is not None and w.grad is None:
@@ -225,6 +228,20 @@ class _TableRow(torch.autograd.Function):
             out.append(buf)
         sunk = buf = None
         return out[0], out[1], None, None
+
+
+def code_rows_with_sink(z_s: torch.Tensor, z_t: torch.Tensor):
+    """One code row each (1, C) -- the eval step's optimised leaf codes -- as _TableRow views carrying a
+    CodeGradSink (eval.py:145-163): the loss and both fields add their code gradients in place into the
+    leaves' zeroed optimiser slots, handed back to autograd as the leaves' gradients.  The rows are
+    returned unchanged when they do not need it (no gradient, more than one row)."""
+    if not (torch.is_grad_enabled() and z_s.requires_grad and z_t.requires_grad and z_s.is_leaf and z_t.is_leaf
+            and z_s.dim() == 2 and z_t.dim() == 2 and z_s.shape[0] == 1 and z_t.shape[0] == 1):
+        return z_s, z_t
+    sink = CodeGradSink((z_s, z_t), 0)
+    rows_s, rows_t = _TableRow.apply(z_s, z_t, 0, sink)
+    rows_s._cn_sink = rows_t._cn_sink = sink
+    return rows_s, rows_t
 
 
 class CodeRows:

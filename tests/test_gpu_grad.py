@@ -717,14 +717,17 @@ def test_field_backward_train_nogeo_bitwise(dev, precision, mode, r, s, n_codes)
     torch.cuda.synchronize()
     atomic = n_codes > 1 or x3       # the per-code sums / biases of g_code: float atomics
     code_biases = {3, 5, 17}          # b_xyz2, b_out, b_rgb: column sums of g_code
+    # float-atomic sums over ~67k samples whose partial sums exceed the total (cancellation): two orders
+    # agree to 1e-5 of the total's magnitude in fp32, to 1e-4 in 3xbf16 (larger per-sample terms)
+    tol = 1e-4 if x3 else 1e-5
     for other in ("nogeo", "nogeo2"):
         for k, (a, b) in enumerate(zip(out[other][0], out["geo"][0])):
             if atomic and k in code_biases:
-                close(a, b.double(), 1e-5, f"bias {k}")
+                close(a, b.double(), tol, f"bias {k}")
             else:
                 assert torch.equal(a, b), f"param {k}: {other} differs from the geometry schedule"
         if atomic:
-            close(out[other][1], out["geo"][1].double(), 1e-5, "g_code")
+            close(out[other][1], out["geo"][1].double(), tol, "g_code")
         else:
             assert torch.equal(out[other][1], out["geo"][1]), f"g_code: {other}"
 

@@ -212,14 +212,17 @@ def test_eval_c5_fused_at_size(dev, precision):
 @pytest.mark.parametrize("precision", ["f32", "bf16x3"])
 def test_eval_step_in_place_gradients(dev, monkeypatch, precision):
     """The eval step's gradient sinks (C5 inputs, the flat AdamW's zeroed slots handed out by zero_grad):
-    the codes' gradients added in place into their .grad by the loss and both fields (_leaf_sink), the
-    rays' by both volume renders and both fields into the fine field's zeroed accumulators (RaySink),
-    the pose angles' written into their slots -- every leaf's .grad is then its flat slice (no autograd
-    adds, no copy into the flat buffer) -- against the route through autograd: the loss bit for bit, the
-    code gradients to 1e-6 (same sums, same order), the angles to 1e-5 (the ray sums' atomics round
-    differently)."""
+    the codes' gradients added in place into the leaves' slots by the loss and both fields (one dz launch
+    for both; code_rows_with_sink's CodeGradSink), the rays' by both volume renders and both fields into
+    the fine field's zeroed accumulators (RaySink), the pose angles' written into their slots -- every
+    leaf's .grad is then its flat slice (no autograd adds, no copy into the flat buffer) -- against the
+    route through autograd: the loss bit for bit, the code gradients to 1e-6 (the same sums in the same
+    order, of g_code's float-atomic sums -- not bit-reproducible run to run), the angles to 1e-5 (the ray
+    sums' atomics round differently).  torch.autograd.grad through the sinks returns the same code
+    gradients."""
     from codenerf import autograd as A, synthetic
     from codenerf.evaluate import eval_step_loss
+    from codenerf.models import model as M
     from codenerf.nerf import PointSampler, RaySampler
     from codenerf.optim import AdamW
     g = gload("eval_c5.npz", dev)
@@ -231,7 +234,7 @@ def test_eval_step_in_place_gradients(dev, monkeypatch, precision):
     out = []
     for on in (True, False):
         if not on:
-            monkeypatch.setattr(A, "_leaf_sink", lambda ts: None)
+            monkeypatch.setattr(M.CodeGradSink, "rows", lambda self: None)
             monkeypatch.setattr(A, "_ray_sink", lambda rd, ro=None: None)
         lv = [g[k].clone().requires_grad_(True) for k in ("theta", "phi", "rho", "z_s", "z_t")]
         opt = AdamW([{"params": lv[3:]}, {"params": lv[:2]}, {"params": lv[2:3]}], lr=1e-2)
@@ -251,6 +254,16 @@ def test_eval_step_in_place_gradients(dev, monkeypatch, precision):
     assert l0 == l1
     for name, a, b in zip(("theta", "phi", "rho", "z_s", "z_t"), g0, g1):
         close(a, b, 1e-6 if name.startswith("z") else 1e-5, name)
+    # torch.autograd.grad (no .grad accumulation) through the sinks: the same code gradients
+    monkeypatch.undo()
+    lv = [g[k].clone().requires_grad_(True) for k in ("theta", "phi", "rho", "z_s", "z_t")]
+    opt = AdamW([{"params": lv[3:]}, {"params": lv[:2]}, {"params": lv[2:3]}], lr=1e-2)
+    opt.zero_grad()
+    np.random.seed(17)
+    loss, _ = eval_step_loss(*lv, g["target"], (rs, ps), embedders(dev), models, 1e-5, t_rand=g["t_rand"], u=g["u"])
+    gz = torch.autograd.grad(loss, lv[3:])
+    for name, a, b in zip(("z_s", "z_t"), gz, g0[3:]):
+        close(a, b, 1e-6, "autograd.grad " + name)
 
 
 # ---------------------------------------------------------------- the fused step loss
