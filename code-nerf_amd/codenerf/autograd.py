@@ -595,9 +595,14 @@ def pose_rays_autograd(dirs, theta=None, phi=None, rho=None, c2w=None, sel=None,
     tgt = None if target is None else target.detach()
     if not _needs_grad(theta, phi, rho, c2w):
         return ops.pose_rays(dirs, _d(theta), _d(phi), _d(rho), c2w=_d(c2w), select_inds=sel, target=tgt)
-    sink = RaySink()
+    # the eval step (pose leaves optimised by eval.py:145-167): the rays' consumers sum their gradients in
+    # place (RaySink; torch.autograd.grad w.r.t. these rays themselves then sees none -- w.r.t. the pose
+    # leaves it is exact)
+    leaves = theta is not None and all(t is not None and t.is_leaf and t.requires_grad for t in (theta, phi, rho))
+    sink = RaySink() if leaves else None
     ro, rd, c2w_out, tgt_out = PoseRays.apply(dirs.detach(), theta, phi, rho, c2w, sel, tgt, sink)
-    ro._cn_ray_sink = rd._cn_ray_sink = sink
+    if sink is not None:
+        ro._cn_ray_sink = rd._cn_ray_sink = sink
     return ro, rd, c2w_out, tgt_out
 
 
