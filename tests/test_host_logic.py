@@ -108,3 +108,51 @@ def test_bench_refuses_more_gpus_than_visible():
                        capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode != 0
     assert "needs 64 visible GPUs" in (r.stderr + r.stdout)
+
+
+def test_code_grad_sink_claims_zeroed_slots_once():
+    """CodeGradSink (the in-place code-gradient rows): it claims the tables' zeroed optimiser slots only
+    when every table is trainable, has no .grad yet and carries a slot; it hands out row k of each;
+    queued dz jobs need those rows; take() drops its references; a second sink after the claim gets
+    none (one use per zero_grad).  Host logic only (no launch)."""
+    from codenerf.models.model import CodeGradSink
+    ws = [torch.nn.Parameter(torch.randn(5, 4)) for _ in range(2)]
+    assert CodeGradSink(ws, 2).rows() is None                  # no slots handed out
+    for w in ws:
+        w._cn_grad_slot = torch.zeros(5, 4)
+    frozen = [torch.randn(5, 4), ws[1]]
+    frozen[0]._cn_grad_slot = torch.zeros(5, 4)
+    assert CodeGradSink(frozen, 2).rows() is None              # a table without requires_grad
+    ws[1].grad = torch.zeros(5, 4)
+    assert CodeGradSink(ws, 2).rows() is None                  # a table that already has a gradient
+    assert ws[0]._cn_grad_slot is not None                     # nothing claimed on the way
+    ws[1].grad = None
+    slots = [w._cn_grad_slot for w in ws]
+    sink = CodeGradSink(ws, 2)
+    rows = sink.rows()
+    assert rows is not None and all(r.shape == (1, 4) for r in rows)
+    for r, s in zip(rows, slots):
+        assert r.data_ptr() == s[2:3].data_ptr()
+    assert all(w._cn_grad_slot is None for w in ws)            # claimed: one use per zero_grad
+    assert sink.rows()[0].data_ptr() == rows[0].data_ptr()     # the same rows on every ask
+    assert CodeGradSink(ws, 1).rows() is None                  # another sink finds no slot
+    b = sink.take()                                            # nothing queued: no launch
+    assert b is not None and b[0] is slots[0] and sink.bufs is None and sink.pending == []
+
+
+def test_prep_plan_modes():
+    """The pre-field launch RadianceField.forward plans (autograd._prep_plan): the eval step's fused
+    mode with its accumulators (g_code, then d ro / d rd as wanted), the fp32 training mode with a
+    zeroed g_code, none for an empty batch or a format the fused kernels do not take."""
+    from codenerf import _lib, autograd as A
+    meta = A._FieldMeta(64, 4096, [1.0] * 10, [1.0] * 4, precision="f32", train_precision="f32")
+    frozen = (False, True, False, True, False, True, True) + (False,) * 18
+    train = (False, False, False, False, False, True, True) + (True,) * 18
+    stride = _lib.CN_CODE_BIAS_STRIDE
+    assert A._prep_plan(meta, 1, 2048, frozen) == ("fused", stride + 6 * 2048)
+    assert A._prep_plan(meta, 1, 2048, frozen[:3] + (False,) + frozen[4:]) == ("fused", stride + 3 * 2048)
+    assert A._prep_plan(meta, 1, 4096, train) == ("train_w16", stride)
+    assert A._prep_plan(meta, 0, 4096, train) == (None, 0)
+    assert A._prep_plan(meta, 1, 0, train) == (None, 0)
+    meta_v1 = A._FieldMeta(64, 4096, [1.0] * 10, [1.0] * 4, precision="f32_v1", train_precision="f32")
+    assert A._prep_plan(meta_v1, 1, 4096, train) == (None, 0)
