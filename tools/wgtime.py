@@ -16,6 +16,7 @@ import torch  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rays", type=int, nargs="+", default=[4096, 8192, 6144])
+    ap.add_argument("--infer", action="store_true", help="the inference kernel (C2: 262144 rays = one bench step)")
     args = ap.parse_args()
     from codenerf import ops, synthetic
     from codenerf.models import CodeNeRFModel
@@ -36,7 +37,10 @@ def main():
         rd = torch.randn(n, 3, generator=g).to(dev)
         z = (0.8 + torch.rand(n, s, generator=g).sort(-1).values).to(dev)
         for _ in range(3):
-            ops.radiance_field_train_w16(packed, cb, rd, s, 4096, fx, fd, ro=ro, z=z, precision="f32")
+            if args.infer:
+                ops.radiance_field(packed, cb, rd, s, 4096, fx, fd, ro=ro, z=z, precision="f32")
+            else:
+                ops.radiance_field_train_w16(packed, cb, rd, s, 4096, fx, fd, ro=ro, z=z, precision="f32")
         torch.cuda.synchronize()
         buf = np.zeros((2048, 2), dtype=np.int64)
         assert fn(buf.ctypes.data, 2048) == 0
