@@ -80,7 +80,11 @@ __global__ __launch_bounds__(256) void pose_rays_kernel(const float* __restrict_
 //   d/dphi:   R00 -cp, R10 -sp, R01 st sp, R11 -st cp, R02 -ct sp, R12 ct cp,
 //             t0 -rho ct sp, t1 rho ct cp
 //   d/drho:   t0 ct cp, t1 ct sp, t2 st
-__global__ __launch_bounds__(256) void pose_rays_backward_kernel(const float* __restrict__ th_,
+// 1024 threads per pose: two rays per thread for the eval step's 2048, every load of a thread's rays
+// issued before its FMAs (the index, then the direction gather: two memory round trips in all; the
+// 256-thread loop took two per ray, 10.4 us per call).
+constexpr int kPoseBwdThreads = 1024;
+__global__ __launch_bounds__(kPoseBwdThreads) void pose_rays_backward_kernel(const float* __restrict__ th_,
                                                                  const float* __restrict__ ph_,
                                                                  const float* __restrict__ rho_,
                                                                  const float* __restrict__ dirs, int64_t hw,
@@ -89,24 +93,45 @@ __global__ __launch_bounds__(256) void pose_rays_backward_kernel(const float* __
                                                                  const float* __restrict__ g_rd,
                                                                  float* __restrict__ d_c2w, float* __restrict__ d_th,
                                                                  float* __restrict__ d_ph, float* __restrict__ d_rho) {
-  __shared__ float red[12][4];
+  constexpr int kW = kPoseBwdThreads / 64;
+  __shared__ float red[12][kW];
   const int64_t b = blockIdx.x;
   float acc[12] = {0};
-  for (int64_t i = threadIdx.x; i < s; i += blockDim.x) {
-    const int64_t q = b * s + i;
-    const int64_t p = sel ? sel[q] : i;
-    if (p < 0 || p >= hw) continue;
-    const float d0 = dirs[3 * p], d1 = dirs[3 * p + 1], d2 = dirs[3 * p + 2];
+  constexpr int kU = 2;   // rays per thread and round, loaded together
+  for (int64_t i0 = threadIdx.x; i0 < s; i0 += kU * kPoseBwdThreads) {
+    int64_t p[kU];
+    bool ok[kU];
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const float g = g_rd ? g_rd[3 * q + j] : 0.0f;
-      acc[4 * j + 0] = fmaf(g, d0, acc[4 * j + 0]);
-      acc[4 * j + 1] = fmaf(g, d1, acc[4 * j + 1]);
-      acc[4 * j + 2] = fmaf(g, d2, acc[4 * j + 2]);
-      acc[4 * j + 3] += g_ro ? g_ro[3 * q + j] : 0.0f;
+    for (int u = 0; u < kU; ++u) {
+      const int64_t i = i0 + u * kPoseBwdThreads;
+      ok[u] = i < s;
+      p[u] = ok[u] ? (sel ? sel[b * s + i] : i) : 0;
+      ok[u] = ok[u] && p[u] >= 0 && p[u] < hw;
+    }
+    float d[kU][3], gr[kU][3], go[kU][3];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t q = b * s + i0 + u * kPoseBwdThreads, pp = ok[u] ? p[u] : 0;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        d[u][j] = dirs[3 * pp + j];
+        gr[u][j] = (ok[u] && g_rd) ? g_rd[3 * q + j] : 0.0f;
+        go[u][j] = (ok[u] && g_ro) ? g_ro[3 * q + j] : 0.0f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      if (!ok[u]) continue;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        acc[4 * j + 0] = fmaf(gr[u][j], d[u][0], acc[4 * j + 0]);
+        acc[4 * j + 1] = fmaf(gr[u][j], d[u][1], acc[4 * j + 1]);
+        acc[4 * j + 2] = fmaf(gr[u][j], d[u][2], acc[4 * j + 2]);
+        acc[4 * j + 3] += go[u][j];
+      }
     }
   }
-  // wave butterfly, then the 4 waves through LDS
+  // wave butterfly, then the waves through LDS (a fixed pairwise tree)
 #pragma unroll
   for (int k = 0; k < 12; ++k) {
 #pragma unroll
@@ -120,7 +145,16 @@ __global__ __launch_bounds__(256) void pose_rays_backward_kernel(const float* __
   if (threadIdx.x != 0) return;
   float G[12];
 #pragma unroll
-  for (int k = 0; k < 12; ++k) G[k] = (red[k][0] + red[k][1]) + (red[k][2] + red[k][3]);
+  for (int k = 0; k < 12; ++k) {
+    float t[kW];
+#pragma unroll
+    for (int w = 0; w < kW; ++w) t[w] = red[k][w];
+#pragma unroll
+    for (int n = kW / 2; n > 0; n >>= 1)
+#pragma unroll
+      for (int w = 0; w < n; ++w) t[w] = t[w] + t[w + n];
+    G[k] = t[0];
+  }
   if (d_c2w) {
 #pragma unroll
     for (int k = 0; k < 12; ++k) d_c2w[16 * b + k] = G[k];
@@ -336,7 +370,7 @@ extern "C" int cn_pose_rays_backward(const float* theta, const float* phi, const
   CN_CHECK_ARG(batch > 0 && batch < (1ll << 31) && hw > 0 && dirs && (g_ro || g_rd) && (d_c2w || want_angles));
   CN_CHECK_ARG(select_inds ? (sample_size > 0 && sample_size <= hw) : sample_size == hw);
   CN_CHECK_ARG(!want_angles || (theta && phi && rho));
-  hipLaunchKernelGGL(pose_rays_backward_kernel, dim3(static_cast<unsigned>(batch)), dim3(256), 0,
+  hipLaunchKernelGGL(pose_rays_backward_kernel, dim3(static_cast<unsigned>(batch)), dim3(kPoseBwdThreads), 0,
                      cn::as_stream(stream), want_angles ? theta : nullptr, phi, rho, dirs, hw, select_inds,
                      sample_size, g_ro, g_rd, d_c2w, d_theta, d_phi, d_rho);
   return cn::launch_status();
