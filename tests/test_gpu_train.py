@@ -349,7 +349,7 @@ def test_step_fusions_bitwise(dev, monkeypatch, precision, off):
     * "sink": both fields' code gradients added into the code tables' gradient rows in place
       (CodeGradSink: fp32, one two-field cn_code_dz launch per step; 3xbf16, each field's
       accumulate_dz launch), the tables' .grad the optimiser's flat slices, vs dz returned, summed by
-      autograd and added into the row (3xbf16: to 1e-5, its fused backward's g_code is a float-atomic
+      autograd and added into the row (3xbf16: to 1e-4, its fused backward's g_code is a float-atomic
       sum);
     * "prefetch": both fields' pre-field launches as one (cn_field_prepare_models, once per step) vs one
       per field."""
@@ -415,10 +415,12 @@ def test_step_fusions_bitwise(dev, monkeypatch, precision, off):
             if precision == "f32":
                 assert torch.equal(a[k], b[k]), ("grad", k)
             elif step == 0:
-                # the 3xbf16 backward sums g_code with LDS float atomics: not bit-reproducible, and after
-                # a step the runs' parameters differ in their last bits (the later steps' ReLU decisions
-                # may then differ too), so only the first step's gradients are compared, to 1e-5
-                close(b[k], a[k], 1e-5, ("grad", k))
+                # the 3xbf16 backward sums g_code with LDS float atomics: not bit-reproducible (two orders
+                # of those ~10^4-term sums, and the biases formed from them, agree to ~1e-5 of the total;
+                # test_field_backward_train_nogeo_bitwise saw 1.3e-5), and after a step the runs'
+                # parameters differ in their last bits (later ReLU decisions may then differ too), so only
+                # the first step's gradients are compared, to 1e-4
+                close(b[k], a[k], 1e-4, ("grad", k))
     for k in p0:
         if precision == "f32":
             assert torch.equal(p0[k], p1[k]), ("param", k)
