@@ -332,6 +332,9 @@ def run(args):
             if world == 1:
                 for p in ("f32", "bf16x3"):
                     result["eval_c5"][p]["graph"] = eval_bench(dev, rs, emb, models, args.eval_iters, p, graph=True)
+            else:
+                # the optional ray-sharded mode: one C5 optimisation strong-scaled over the ranks
+                result["eval_c5_sharded"] = eval_bench(dev, rs, emb, models, args.eval_iters, "f32", sharded=True)
             set_precision(args.precision)
         if args.train_iters > 0:
             result["train_c3"] = train_bench(dev, k, args.train_iters, world, "f32")
@@ -403,10 +406,13 @@ def traffic_source(prec):
             "per-sample bytes x this launch's samples; profiles/field_kernel_traffic.json")
 
 
-def eval_bench(dev, rs, emb, models, iters, precision, graph=False):
+def eval_bench(dev, rs, emb, models, iters, precision, graph=False, sharded=False):
     """C5 (srn-cars-code-3080-val.yml): one eval.py:141-167 iteration = 2048 random rays, 64+64
     perturbed samples, forward + backward through the HIP kernels into (codes, theta, phi, rho),
-    AdamW step.  Weights frozen (their grads are never read by the reference's optimiser)."""
+    AdamW step.  Weights frozen (their grads are never read by the reference's optimiser).
+    ``sharded`` (N > 1): the optional ray-sharded mode -- ONE optimisation, each iteration's 2048 rays
+    split over the ranks, the gradients summed by one all-reduce (codenerf.evaluate.sharded_eval_step);
+    timed between barriers, the max over ranks."""
     import numpy as np
     from codenerf.autograd import backward_from
     from codenerf.evaluate import GraphedEvalStep, eval_step_loss, step_psnr_tensor
@@ -429,7 +435,14 @@ def eval_bench(dev, rs, emb, models, iters, precision, graph=False):
     opt = AdamW([{"params": [zs, zt]}, {"params": [th, ph]}, {"params": [rh]}], lr=1e-2)
     np.random.seed(0)
 
-    if graph:
+    if sharded:
+        from codenerf.evaluate import sharded_eval_step, sync_shard_state
+        sync_shard_state((rs, ps), 0)         # every rank draws rank 0's rays and uniforms
+
+        def it():
+            _, logs = sharded_eval_step(th, ph, rh, zs, zt, target, (rs, ps), emb, mods, opt, 1e-5)
+            step_psnr_tensor(logs)
+    elif graph:
         # the iteration's forward + backward captured once as a HIP graph (GraphedEvalStep);
         # the numpy draw, the replay, the flat AdamW and the psnr read-back per iteration
         graphed = GraphedEvalStep(th, ph, rh, zs, zt, target, (rs, ps), emb, mods, opt, 1e-5)
@@ -449,11 +462,19 @@ def eval_bench(dev, rs, emb, models, iters, precision, graph=False):
     for _ in range(2):
         it()
     torch.cuda.synchronize()
+    if sharded:
+        dist.barrier()
     t0 = time.perf_counter()
     for _ in range(iters):
         it()
     torch.cuda.synchronize()
+    if sharded:
+        dist.barrier()
     dt = (time.perf_counter() - t0) / iters
+    if sharded:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
     for m, prec in saved:
         m.requires_grad_(True)
         m.precision = prec
@@ -461,8 +482,15 @@ def eval_bench(dev, rs, emb, models, iters, precision, graph=False):
             else "fp32 16x16x4 forward with ReLU masks + one fused fp32 backward launch per field")
     if graph:
         note += "; forward + backward + AdamW replayed as one captured HIP graph (GraphedEvalStep)"
+    extra = {}
+    if sharded:
+        world = dist.get_world_size()
+        note += (f"; ray-sharded over {world} ranks (one optimisation; 2048 / {world} rays per rank and iteration, "
+                 "one all-reduce of the 515 code / pose gradient floats; each share is its own Q1 chunk, so this "
+                 "mode is reported beside the reference's per-rank optimisation, Q6)")
+        extra = {"scaling": "strong", "n_ranks": world, "rays_per_rank_per_iter": 2048 // world}
     return {"ms_per_iter": dt * 1e3, "rays_per_s": 2048 / dt, "rays_per_iter": 2048, "samples": "64+64 perturbed",
-            "dtype": precision,
+            "dtype": precision, **extra,
             "note": note + "; fused pose path + loss; host-side numpy ray permutation included; eval.py's "
                            "per-iteration psnr formed on the device"}
 

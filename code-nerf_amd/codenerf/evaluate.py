@@ -40,16 +40,20 @@ def pose_spherical(theta: torch.Tensor, phi: torch.Tensor, rho: torch.Tensor) ->
 def eval_step_loss(theta, phi, rho, shape_code, texture_code, target_pixels, samplers, embedders, models,
                    regularizer_lambda: float, gt_pose: Optional[torch.Tensor] = None,
                    t_rand: Optional[torch.Tensor] = None, u: Optional[torch.Tensor] = None,
-                   sel: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Dict[str, object]]:
+                   sel: Optional[torch.Tensor] = None,
+                   rows_total: Optional[int] = None) -> Tuple[torch.Tensor, Dict[str, object]]:
     """One iteration's forward of eval.py:145-163 -> (loss, logs).
 
     ``target_pixels``: (H*W, C) image of the object; rays are drawn by the ray sampler's RNG
     (host numpy as the reference, or rng="device").  ``gt_pose`` (4, 4): the view's pose, for
     the logged pose error (eval.py:161-162).  ``t_rand`` / ``u``: injected stratified / fine
     uniforms (parity tests), else drawn on the device.  ``sel``: (1, S) device ray indices drawn
-    by the caller (GraphedEvalStep), else the ray sampler draws them.  logs: device tensors (read
-    back only when logged); eval.py:159's per-iteration psnr is read back by the caller once the
-    backward and the optimiser step are enqueued (``step_psnr``)."""
+    by the caller (GraphedEvalStep), else the ray sampler draws them.  ``rows_total``: this call renders
+    one rank's share of an iteration of ``rows_total`` rays (sharded_eval_step): the regulariser
+    expands the codes over all ``rows_total`` rows and the loss is weighted by share / rows_total, so
+    the ranks' losses sum to the whole iteration's.  logs: device tensors (read back only when
+    logged; the per-share means when sharded); eval.py:159's per-iteration psnr is read back by the
+    caller once the backward and the optimiser step are enqueued (``step_psnr``)."""
     ray_sampler, point_sampler = samplers
     ro, rd, select_inds, cam_pose, tp = ray_sampler.sample_spherical(theta, phi, rho, target=target_pixels, sel=sel)
     n = ro.shape[0]
@@ -65,7 +69,10 @@ def eval_step_loss(theta, phi, rho, shape_code, texture_code, target_pixels, sam
     rgb_c, rgb_f = out["rgb_coarse"], out["rgb_fine"]
     # mse(coarse) + mse(fine) + lambda (||z_s|| + ||z_t||), the codes expanded over the n rays
     psnr = torch.empty((), dtype=torch.float64, device=tp.device)   # eval.py:159's psnr, by the loss launch
-    loss, stats = nerf_loss(rgb_c, rgb_f, tp, shape_code, texture_code, n, regularizer_lambda, psnr=psnr)
+    expand = n if rows_total is None else rows_total
+    loss, stats = nerf_loss(rgb_c, rgb_f, tp, shape_code, texture_code, expand, regularizer_lambda, psnr=psnr)
+    if expand != n:
+        loss = loss * (n / expand)
     logs = {"nerf_loss_coarse": stats[0], "nerf_loss_fine": stats[1], "embedding_loss": stats[2], "psnr": psnr}
     if gt_pose is not None:
         logs["pose_error"] = ops.pose_error(gt_pose.reshape(1, 4, 4), cam_pose)[1][0]
@@ -85,6 +92,111 @@ def step_psnr_tensor(logs: Dict[str, object]) -> torch.Tensor:
         return logs["psnr"]
     from .train import psnr_tensor
     return psnr_tensor(logs["nerf_loss_fine"])
+
+
+def sync_shard_state(samplers, src: int = 0, group=None) -> None:
+    """Put the ranks of a ray-sharded eval (sharded_eval_step) in step with rank ``src``: its random
+    streams -- numpy's global state (the ray draw, ray_sampler.py:41-42), torch's CPU and
+    current-device generators (the stratified / fine uniforms), the ray sampler's device-Philox
+    counter -- and its ray sampler's camera (focal, principal point: eval.py:66-76 builds each rank's
+    samplers from its own first validation batch, while a sharded step renders ONE view, rank
+    ``src``'s).  One object broadcast; the other ranks continue with rank ``src``'s streams."""
+    import numpy as np
+    rs = samplers[0]
+    rank = dist.get_rank(group)
+    state = [None]
+    if rank == src:
+        cuda = torch.cuda.get_rng_state() if torch.cuda.is_available() and torch.cuda.is_initialized() else None
+        state = [dict(np=np.random.get_state(), cpu=torch.get_rng_state(), cuda=cuda, draws=(rs.seed, rs._draws),
+                      camera=(rs.height, rs.width, rs.focal_length, rs.cx, rs.cy), k=rs.intrinsics.cpu())]
+    dist.broadcast_object_list(state, src=src, group=group)
+    if rank == src:
+        return
+    st = state[0]
+    np.random.set_state(st["np"])
+    torch.set_rng_state(st["cpu"])
+    if st["cuda"] is not None:
+        torch.cuda.set_rng_state(st["cuda"])
+    rs.seed, rs._draws = st["draws"]
+    h, w, focal, cx, cy = st["camera"]
+    assert (h, w) == (rs.height, rs.width), "ray-sharded eval: the ranks' images differ in size"
+    if (focal, cx, cy) != (rs.focal_length, rs.cx, rs.cy):
+        rs.focal_length, rs.cx, rs.cy = focal, cx, cy
+        rs.intrinsics = st["k"].to(rs.device)
+        rs.directions = ops.ray_directions(h, w, focal, cx, cy, rs.device)
+
+
+def shard_draws(samplers, n_rays: int):
+    """The random inputs of one ray-sharded eval iteration, drawn in full on every rank in the order
+    the unsharded step draws them (eval_step_loss: the ray subset, then render_rays' stratified and
+    fine uniforms from torch's device generator) -> (sel (1, n_rays) device int64, t_rand | None,
+    u | None).  With the ranks' streams in step (sync_shard_state), every rank holds the same draws."""
+    rs, ps = samplers
+    assert n_rays == rs.sample_size, "one view's sample_size rays per iteration (eval.py:145)"
+    _, sel = rs.select_inds(1)
+    t_rand = u = None
+    if ps.perturb:
+        t_rand = torch.rand(n_rays, ps.num_samples_coarse, dtype=torch.float32, device=sel.device)
+        u = torch.rand(n_rays, ps.num_samples_fine, dtype=torch.float32, device=sel.device)
+    return sel, t_rand, u
+
+
+def shard_of(n_rays: int, world: int, rank: int) -> slice:
+    """Rank ``rank``'s rows of an ``n_rays`` iteration: parallel_image_render's Q5 split
+    (utils.split_sizes: truncating, the last rank takes the remainder)."""
+    from .utils import split_sizes
+    per, _ = split_sizes(n_rays, world)
+    start = sum(per[:rank])
+    return slice(start, start + per[rank])
+
+
+def _allreduce_sum(optimizer, params, group) -> None:
+    """Sum the parameters' gradients over the group: the flat AdamW's one all-reduce (no average),
+    else one all-reduce of the gradients concatenated."""
+    from .optim import AdamW
+    if isinstance(optimizer, AdamW):
+        optimizer.allreduce_grads(group, average=False)
+        return
+    grads = [p.grad for p in params]
+    flat = torch.cat([g.reshape(-1) for g in grads])
+    dist.all_reduce(flat, group=group)
+    torch._foreach_copy_(grads, [f.view_as(g) for f, g in zip(flat.split([g.numel() for g in grads]), grads)])
+
+
+def sharded_eval_step(theta, phi, rho, shape_code, texture_code, target_pixels, samplers, embedders, models,
+                      optimizer, regularizer_lambda: float, gt_pose: Optional[torch.Tensor] = None,
+                      group=None) -> Tuple[torch.Tensor, Dict[str, object]]:
+    """One test-time-optimisation iteration with its ray batch split over the ranks (SURVEY.md 8(e)'s
+    optional sharded C5 mode, a build extension: eval.py runs one independent optimisation per rank,
+    Q6, which stays the default).  Every rank draws the iteration's rays and uniforms in full
+    (shard_draws; the streams put in step by sync_shard_state), renders its Q5 share of the rays, weights
+    its loss by share / rays (eval_step_loss ``rows_total``), runs the backward, and ONE all-reduce
+    sums the code / pose gradients (515 floats; a second one the two MSE terms for the logs); the
+    optimiser step then runs on identical gradients, so the parameters stay identical on every rank.
+    Semantics: the gradient of the whole batch's loss, except that each share is rendered as its own
+    chunk, so the Q1 view-direction map (nerf/__init__.py:127-128) pairs samples with rays of the
+    share rather than of the whole batch -- the reason this mode is reported beside, not instead of,
+    the reference's.  -> (total loss, logs) of the whole iteration; logs as eval_step_loss's."""
+    rs, _ = samplers
+    n_rays = rs.sample_size
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    sel, t_rand, u = shard_draws(samplers, n_rays)
+    sl = shard_of(n_rays, world, rank)
+    n = sl.stop - sl.start
+    loss, logs = eval_step_loss(theta, phi, rho, shape_code, texture_code, target_pixels, samplers, embedders,
+                                models, regularizer_lambda, gt_pose=gt_pose,
+                                t_rand=None if t_rand is None else t_rand[sl], u=None if u is None else u[sl],
+                                sel=sel[:, sl], rows_total=n_rays)
+    optimizer.zero_grad()
+    backward_from(loss)
+    params = [shape_code, texture_code, theta, phi, rho]
+    _allreduce_sum(optimizer, params, group)
+    mse = torch.stack([logs["nerf_loss_coarse"], logs["nerf_loss_fine"]]) * (n / n_rays)
+    dist.all_reduce(mse, group=group)
+    optimizer.step()
+    from .train import psnr_tensor
+    logs.update(nerf_loss_coarse=mse[0], nerf_loss_fine=mse[1], psnr=psnr_tensor(mse[1]))
+    return mse[0] + mse[1] + logs["embedding_loss"], logs
 
 
 class GraphedEvalStep:
@@ -211,7 +323,8 @@ def test_time_optimize(target_pixels: torch.Tensor, samplers, embedders, models,
                        regularizer_lambda: float = 1e-5, optimizer: str = "AdamW",
                        init_pose: Tuple[float, float, float] = (1.57, 0.0, 1.30),
                        freeze_models: bool = True, log_every: Optional[int] = None,
-                       gt_pose: Optional[torch.Tensor] = None, graph: bool = False):
+                       gt_pose: Optional[torch.Tensor] = None, graph: bool = False, shard_rays: bool = False,
+                       group=None):
     """eval.py:121-180: optimise codes + (theta, phi, rho) against one image.
 
     ``init_codes``: the embedding tables (z_s, z_t); the start point is their mean (eval.py:121-127).
@@ -222,6 +335,9 @@ def test_time_optimize(target_pixels: torch.Tensor, samplers, embedders, models,
     frozen models, val_type AdamW and the numpy ray draw) -- the same arithmetic and draws.  Off by
     default: the eager loop is GPU-bound (C5 3.585 ms eager vs 3.592 ms replayed, DESIGN.md section 8
     item 3); the graph pays only where the host is the bottleneck.
+    ``shard_rays`` (with an initialised process group of more than one rank): every iteration's ray
+    batch split over the ranks (sharded_eval_step; the caller puts the ranks' random streams in step
+    first, sync_shard_state) -- one optimisation shared by all ranks instead of one per rank (Q6).
 
     Returns (shape_code, texture_code, (theta, phi, rho), history, cam_pose of the last iteration).
     """
@@ -243,6 +359,8 @@ def test_time_optimize(target_pixels: torch.Tensor, samplers, embedders, models,
             saved[k] = [p.requires_grad for p in m.parameters()]
             m.requires_grad_(False)
     history, cam_pose = [], None
+    sharded = bool(shard_rays) and dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+    assert not (sharded and graph), "graph=True runs one rank's whole batch; shard_rays needs the eager step"
     try:
         graphed = None
         if graph:
@@ -258,6 +376,13 @@ def test_time_optimize(target_pixels: torch.Tensor, samplers, embedders, models,
                     graphed.prefetch()             # host draw overlapping this replay
                 # the graph's outputs are overwritten by the next replay
                 loss, logs = loss.detach().clone(), {k: v.clone() for k, v in logs.items()}
+                cam_pose = logs.pop("cam_pose")
+            elif sharded:
+                for m in models.values():
+                    m.train()
+                loss, logs = sharded_eval_step(theta, phi, rho, shape_code, texture_code, target_pixels, samplers,
+                                               embedders, models, opt, regularizer_lambda, gt_pose=gt_pose,
+                                               group=group)
                 cam_pose = logs.pop("cam_pose")
             else:
                 for m in models.values():
@@ -335,7 +460,7 @@ def eval_loop(rank: int, cfg, device=None, resident: bool = True, verbose: bool 
 
 
 def validate(cfg, val_data: Dict[str, torch.Tensor], models, samplers, embedders, device,
-             log_every: Optional[int] = None) -> Dict[str, object]:
+             log_every: Optional[int] = None, shard_rays: Optional[bool] = None) -> Dict[str, object]:
     """eval.py:82-205 for one loaded validation view (``color`` (1,H,W,C), ``pose`` (1,4,4)):
 
     1. rank 0's view is broadcast to every rank (eval.py:111-115);
@@ -344,14 +469,23 @@ def validate(cfg, val_data: Dict[str, torch.Tensor], models, samplers, embedders
     3. the whole view rendered from the optimised pose with ``parallel_image_render`` (sharded
        over the ranks, one all-gather) and its MSE / PSNR against the target on rank 0
        (eval.py:182-205).
+    ``shard_rays`` (default: the config's ``experiment.val_shard_rays``, else False = the reference's
+    Q6): with several ranks, step 2 runs as ONE optimisation with every iteration's rays split over the
+    ranks (sharded_eval_step), every rank continuing with rank 0's random streams and camera
+    (sync_shard_state).
     Returns {"history", "rgb" (H*W,3) on rank 0, "loss", "psnr", "pose_error", "codes", "pose"}."""
     is_distributed = bool(getattr(cfg, "is_distributed", False))
+    if shard_rays is None:
+        shard_rays = bool(getattr(cfg.experiment, "val_shard_rays", False))
+    shard_rays = shard_rays and is_distributed
     color = val_data["color"].to(device, torch.float32)
     gt_pose = val_data["pose"].to(device, torch.float32)
     if is_distributed:
         color, gt_pose = color.contiguous(), gt_pose.contiguous()
         dist.broadcast(color, 0)
         dist.broadcast(gt_pose, 0)
+        if shard_rays:
+            sync_shard_state(samplers, 0)
     emb = models["embedding"]
     emb = getattr(emb, "module", emb)
     all_s, all_t = emb.get_all_embeddings(device=device)
@@ -360,7 +494,7 @@ def validate(cfg, val_data: Dict[str, torch.Tensor], models, samplers, embedders
         color.reshape(-1, color.shape[-1]), samplers, embedders, models, (all_s.detach(), all_t.detach()),
         e.val_iterations, val_lr=o.val_lr, angle_lr=_pose_lr(o, "angle_lr"), radius_lr=_pose_lr(o, "radius_lr"),
         regularizer_lambda=e.regularizer_lambda, optimizer=getattr(o, "val_type", "AdamW"), log_every=log_every,
-        gt_pose=gt_pose)
+        gt_pose=gt_pose, shard_rays=shard_rays)
     rgb = nerf.parallel_image_render(cfg, cam_pose, [zs.detach(), zt.detach()], models, samplers, embedders,
                                      device)
     out = {"history": history, "rgb": rgb, "codes": (zs.detach(), zt.detach()),

@@ -90,15 +90,17 @@ class RaySampler(object):
         """eval.py:145-148 fused: cam_pose = pose_spherical(theta, phi, rho); ro, rd, select_inds =
         sample(cam_pose); target_pixels = target[..., select_inds, :].  theta, phi, rho: (B,) each
         (the reference's (1,) leaves); target: (B, H*W, C) or (H*W, C) for B = 1.
-        ``sel``: (B, S) device indices drawn by the caller (a captured eval step, whose host draw
-        happens outside the graph); else drawn here.
+        ``sel``: (B, S') device indices drawn by the caller (a captured eval step, whose host draw
+        happens outside the graph; S' = sample_size, or a rank's share of them in the ray-sharded
+        eval step); else drawn here.
         -> ro, rd (B*S, 3), select_inds, cam_pose (B, 4, 4) (no grad), target rows (B*S, C) | None."""
         from ..autograd import pose_rays_autograd
         batch = theta.numel()
         if sel is None:
             select_inds, sel = self.select_inds(batch)
         else:
-            assert sel.shape == (batch, self.sample_size), "sel must be (B, sample_size)"
+            assert sel.dim() == 2 and sel.shape[0] == batch and 0 < sel.shape[1] <= self.sample_size, \
+                "sel must be (B, S') with S' <= sample_size"
             select_inds = None
         if target is not None:
             target = target.reshape(batch, self.height * self.width, -1)

@@ -270,10 +270,12 @@ class AdamW(torch.optim.Optimizer):
         self._adopt_state()
 
     # ---- data parallel ------------------------------------------------
-    def allreduce_grads(self, group=None) -> None:
+    def allreduce_grads(self, group=None, average: bool = True) -> None:
         """Average the gradients over the process group (the reference's DDP, util.py:139-142):
         ONE all-reduce (SUM, then a division by the world size -- the same arithmetic on RCCL and
-        gloo) of the flat gradient buffer with a per-parameter has-grad flag appended to it.  A
+        gloo) of the flat gradient buffer with a per-parameter has-grad flag appended to it
+        (``average=False``: the plain sum, for losses the ranks already weighted -- the ray-sharded
+        eval step, codenerf.evaluate.sharded_eval_step).  A
         gradient missing on this rank counts as zero; a parameter without a gradient on every rank
         keeps ``grad = None``.
 
@@ -299,7 +301,8 @@ class AdamW(torch.optim.Optimizer):
         for p in missing:
             self._view("grad", p).zero_()
         dist.all_reduce(ext, op=dist.ReduceOp.SUM, group=group)
-        ext.div_(world)
+        if average:
+            ext.div_(world)
         if missing:
             # which of this rank's missing parameters hold a gradient on SOME rank (DDP reduces
             # those; a parameter no rank touched keeps grad None, so step() skips it as torch does)

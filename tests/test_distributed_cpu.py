@@ -102,3 +102,48 @@ def test_gather_views_layout(world, n_pix, tmp_path):
     want = (np.arange(5, dtype=np.float32)[:, None] * 1000 + np.arange(n_pix, dtype=np.float32)[None, :])
     assert got.shape == (5, n_pix, 3)
     assert np.array_equal(got[..., 0], want) and np.array_equal(got[..., 2], want)
+
+
+def _shard_sync_worker(rank, world, port, out_path):
+    import torch.distributed as dist
+    from types import SimpleNamespace as NS
+    from codenerf.evaluate import shard_of, sync_shard_state
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        np.random.seed(100 + rank)              # per-rank streams, as eval.py seeds them ((r + 1) + seed)
+        torch.manual_seed(200 + rank)
+        rs = NS(seed=7, _draws=3 + rank, height=8, width=8, focal_length=70.0, cx=4.0, cy=5.0,
+                intrinsics=torch.eye(4), device=torch.device("cpu"))
+        sync_shard_state((rs, None), 0)
+        draw = np.random.permutation(64)[:16]   # the ray draw every rank makes next (shard_draws)
+        u = torch.rand(5)
+        sl = shard_of(16, world, rank)
+        rows = torch.zeros(16)
+        rows[sl] = 1.0 + rank
+        dist.all_reduce(rows)                   # every row owned by exactly one rank
+        torch.save({"draw": torch.from_numpy(draw), "u": u, "draws": rs._draws, "rows": rows,
+                    "share": sl.stop - sl.start}, f"{out_path}.{rank}")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_ray_sharded_eval_state_sync(world, tmp_path):
+    """The ray-sharded eval step's host logic (codenerf.evaluate.sharded_eval_step): after
+    sync_shard_state every rank continues with rank 0's numpy / torch streams and ray-sampler counter,
+    so all ranks draw the same rays and uniforms; shard_of gives each row to exactly one rank with
+    parallel_image_render's Q5 split."""
+    from codenerf.utils import split_sizes
+    out = str(tmp_path / "s")
+    mp.start_processes(_shard_sync_worker, args=(world, _free_port(), out), nprocs=world, join=True,
+                       start_method="spawn")
+    got = [torch.load(f"{out}.{r}", weights_only=True) for r in range(world)]
+    for g in got[1:]:
+        assert torch.equal(g["draw"], got[0]["draw"]) and torch.equal(g["u"], got[0]["u"])
+        assert g["draws"] == 3
+    np.random.seed(100)
+    assert np.array_equal(got[0]["draw"].numpy(), np.random.permutation(64)[:16])
+    per, _ = split_sizes(16, world)
+    assert [g["share"] for g in got] == per
+    want = torch.cat([torch.full((p,), 1.0 + r) for r, p in enumerate(per)])
+    assert torch.equal(got[0]["rows"], want)

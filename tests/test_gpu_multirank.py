@@ -210,13 +210,15 @@ def test_train_allreduce_two_ranks(tmp_path):
         assert torch.equal(got[0][k], want[k]), ("vs the averaged single process", k)
 
 
-def _bench_worker(rank, world, port, out_dir):
+_BENCH_HEADLINE = ["--steps", "2", "--warmup", "1", "--images-per-step", "2", "--no-extras"]
+
+
+def _bench_worker(rank, world, port, out_dir, argv=_BENCH_HEADLINE):
     os.environ.update(RANK=str(rank), LOCAL_RANK="0", WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
     sys.path.insert(0, ROOT)
     import bench
-    res = bench.run(bench.parse_args(["--steps", "2", "--warmup", "1", "--images-per-step", "2", "--no-extras",
-                                      "--no-cpu-baseline", "--backend", "gloo", "--quiet"]))
+    res = bench.run(bench.parse_args(list(argv) + ["--no-cpu-baseline", "--backend", "gloo", "--quiet"]))
     if rank == 0:
         with open(os.path.join(out_dir, "bench.json"), "w") as f:
             json.dump(res, f)
@@ -232,6 +234,17 @@ def test_bench_gather_views_multi_rank(tmp_path, world):
     res = json.load(open(tmp_path / "bench.json"))
     assert res["n_gpus"] == world and res["value"] > 0
     margin(f"bench_multi_rank_n{world}[f32]", "multi_rank_maxdiff", res["multi_rank_maxdiff"], 0.0)
+
+
+def test_bench_eval_sharded_two_ranks(tmp_path):
+    """bench.py's side lines at 2 ranks, with the ray-sharded C5 line (eval_c5_sharded: one optimisation,
+    its 2048 rays per iteration split over the ranks) beside the per-rank C5 lines."""
+    _spawn(_bench_worker, 2, str(tmp_path), ["--steps", "1", "--warmup", "0", "--images-per-step", "1",
+                                              "--eval-iters", "2", "--train-iters", "0"])
+    res = json.load(open(tmp_path / "bench.json"))
+    sh = res["eval_c5_sharded"]
+    assert sh["n_ranks"] == 2 and sh["scaling"] == "strong" and sh["rays_per_s"] > 0
+    assert res["eval_c5"]["f32"]["rays_per_s"] > 0
 
 
 def _eval_setup(cfg, dev, rank, intrinsic=None):
@@ -358,6 +371,126 @@ def test_validate_two_ranks_q6(tmp_path):
     assert np.isfinite([got[0]["loss"], got[0]["psnr"], got[0]["pose_error"]]).all()
     mse = ((got[0]["rgb"].double() - got[0]["color"].reshape(-1, 4)[:, :3].double()) ** 2).mean().item()
     assert abs(got[0]["loss"] - mse) <= 1e-6 * max(1.0, mse)
+
+
+def _shard_worker(rank, world, port, tree, out_dir):
+    import numpy as np
+    import torch.distributed as dist
+    from codenerf.evaluate import _pose_lr, sync_shard_state, test_time_optimize, validate
+    dev = _init(rank, world, port)
+    try:
+        cfg = _eval_cfg(tree, os.path.join(out_dir, "s"), world)
+        cfg.nerf.point_sampler.perturb = True        # the stratified / fine uniforms are sliced too
+        loader, models, samplers, embedders, _ = _eval_setup(cfg, dev, rank)
+        val = next(iter(loader))
+        color = val["color"].to(dev, torch.float32).contiguous()
+        gt_pose = val["pose"].to(dev, torch.float32).contiguous()
+        dist.broadcast(color, 0)
+        dist.broadcast(gt_pose, 0)
+        sync_shard_state(samplers, 0)                 # rank 0's streams and camera on every rank
+        st = {"np": np.random.get_state(), "cpu": torch.get_rng_state(), "cuda": torch.cuda.get_rng_state(dev)}
+        emb = models["embedding"]
+        all_s, all_t = emb.get_all_embeddings(device=dev)
+        e, o = cfg.experiment, cfg.optimizer
+        zs, zt, pose, hist, cam = test_time_optimize(
+            color.reshape(-1, color.shape[-1]), samplers, embedders, models, (all_s.detach(), all_t.detach()),
+            e.val_iterations, val_lr=o.val_lr, angle_lr=_pose_lr(o, "angle_lr"), radius_lr=_pose_lr(o, "radius_lr"),
+            regularizer_lambda=e.regularizer_lambda, gt_pose=gt_pose, shard_rays=True)
+        out = {"np_keys": torch.from_numpy(st["np"][1].astype(np.int64)), "np_pos": st["np"][2],
+               "np_hg": st["np"][3], "np_g": st["np"][4], "cpu_rng": st["cpu"], "cuda_rng": st["cuda"].cpu(),
+               "zs": zs.detach().cpu(), "zt": zt.detach().cpu(), "cam_pose": cam.cpu(),
+               "pose": torch.cat([v.detach().cpu() for v in pose]),
+               "losses": torch.tensor([h["total_loss"] for h in hist], dtype=torch.float64),
+               "intrinsic": samplers[0].intrinsics.cpu()}
+        # end to end: validate's sharded mode (view broadcast, state sync, shared optimisation, gather)
+        res = validate(cfg, {"color": val["color"], "pose": val["pose"]}, models, samplers, embedders, dev,
+                       shard_rays=True)
+        out.update(v_zs=res["codes"][0].cpu(), v_cam=res["cam_pose"].cpu())
+        if rank == 0:
+            out.update(color=color.cpu(), gt_pose=gt_pose.cpu(), v_loss=res["loss"], v_psnr=res["psnr"],
+                       v_pose_error=res["pose_error"], v_rgb_rows=res["rgb"].shape[0],
+                       state={f"{k}.{n}": v.cpu() for k, m in models.items() for n, v in m.state_dict().items()})
+        torch.save(out, os.path.join(out_dir, f"shard{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_eval_ray_sharded_two_ranks(tmp_path):
+    """The optional ray-sharded C5 mode (codenerf.evaluate.sharded_eval_step) on two
+    ranks: ONE test-time optimisation whose every iteration's rays are split over the ranks (Q5 shares),
+    the code / pose gradients summed by one all-reduce.  (1) Both ranks end with bit-identical codes and
+    pose and the same loss history (they step on the same summed gradients).  (2) A single process that
+    draws the same rays and uniforms (rank 0's recorded streams), renders the two shares one after the
+    other, sums their gradients and steps reproduces the first iteration's loss bit for bit and the
+    final pose and codes to 1e-5 (the eval backward's per-code sums are float atomics).  (3) validate's
+    sharded mode runs end to end: identical codes on both ranks, a finite loss / psnr / pose error and
+    the whole gathered view on rank 0."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(HERE, "golden"))
+    from srn_tree import write_tree
+    from codenerf import nerf
+    from codenerf.autograd import backward_from
+    from codenerf.evaluate import _optimizer, _pose_lr, eval_step_loss, shard_draws, shard_of
+    tree = write_tree(str(tmp_path / "srn"), channels=4)
+    _spawn(_shard_worker, 2, tree, str(tmp_path))
+    got = [torch.load(str(tmp_path / f"shard{r}.pt"), weights_only=True) for r in range(2)]
+    for key in ("zs", "zt", "pose", "cam_pose", "losses", "v_zs", "v_cam"):
+        assert torch.equal(got[0][key], got[1][key]), key
+    # (2) the single-process emulation
+    dev = torch.device("cuda", 0)
+    cfg = _eval_cfg(tree, str(tmp_path / "single"), 1)
+    cfg.nerf.point_sampler.perturb = True
+    _, models, _, emb, _ = _eval_setup(cfg, dev, 0)
+    g0 = got[0]
+    for k, m in models.items():
+        m.load_state_dict({n[len(k) + 1:]: v for n, v in g0["state"].items() if n.startswith(k + ".")})
+        m.requires_grad_(False)
+        m.train()
+    color = g0["color"].to(dev)
+    target = color.reshape(-1, color.shape[-1])
+    gt_pose = g0["gt_pose"].to(dev)
+    h, w = color.shape[1:3]
+    rs, ps = nerf.prepare_samplers(cfg, h, w, g0["intrinsic"], torch.float32, dev)
+    np.random.set_state(("MT19937", g0["np_keys"].numpy().astype(np.uint32), int(g0["np_pos"]), int(g0["np_hg"]),
+                         float(g0["np_g"])))
+    torch.set_rng_state(g0["cpu_rng"])
+    torch.cuda.set_rng_state(g0["cuda_rng"], dev)
+    all_s, all_t = models["embedding"].get_all_embeddings(device=dev)
+    zs = all_s.detach().mean(dim=0, keepdim=True).clone().requires_grad_(True)
+    zt = all_t.detach().mean(dim=0, keepdim=True).clone().requires_grad_(True)
+    th, ph, rh = (torch.tensor([v], device=dev).requires_grad_(True) for v in (1.57, 0.0, 1.30))
+    e, o = cfg.experiment, cfg.optimizer
+    opt = _optimizer("AdamW", [{"params": [zs, zt]}, {"params": [th, ph], "lr": _pose_lr(o, "angle_lr")},
+                               {"params": [rh], "lr": _pose_lr(o, "radius_lr")}], o.val_lr)
+    params, n_rays, losses = [zs, zt, th, ph, rh], rs.sample_size, []
+    for _ in range(e.val_iterations):
+        sel, t_rand, u = shard_draws((rs, ps), n_rays)
+        gsum, mse = None, None
+        for r in range(2):
+            sl = shard_of(n_rays, 2, r)
+            loss, logs = eval_step_loss(th, ph, rh, zs, zt, target, (rs, ps), emb, models, e.regularizer_lambda,
+                                        gt_pose=gt_pose, t_rand=t_rand[sl], u=u[sl], sel=sel[:, sl],
+                                        rows_total=n_rays)
+            opt.zero_grad()
+            backward_from(loss)
+            g = [p.grad.detach().clone() for p in params]
+            m = torch.stack([logs["nerf_loss_coarse"], logs["nerf_loss_fine"]]) * ((sl.stop - sl.start) / n_rays)
+            gsum = g if gsum is None else [a + b for a, b in zip(gsum, g)]
+            mse = m if mse is None else mse + m
+        with torch.no_grad():
+            for p, g in zip(params, gsum):
+                p.grad.copy_(g)
+        opt.step()
+        losses.append(float(mse[0] + mse[1] + logs["embedding_loss"]))
+    assert losses[0] == g0["losses"][0].item()
+    from conftest import margin
+    pose = torch.cat([v.detach().cpu() for v in (th, ph, rh)])
+    for name, a, b in (("zs", zs.detach().cpu(), g0["zs"]), ("zt", zt.detach().cpu(), g0["zt"]),
+                       ("pose", pose, g0["pose"])):
+        margin("eval_ray_sharded_two_ranks", name, (a - b).abs().max().item(), 1e-5)
+    # (3) validate's sharded mode
+    assert np.isfinite([g0["v_loss"], g0["v_psnr"], g0["v_pose_error"]]).all()
+    assert g0["v_rgb_rows"] == h * w
 
 
 def _train_driver_worker(rank, world, port, tree, out_dir, tag, ckpt):
