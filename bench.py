@@ -482,13 +482,19 @@ def eval_bench(dev, rs, emb, models, iters, precision, graph=False, sharded=Fals
             else "fp32 16x16x4 forward with ReLU masks + one fused fp32 backward launch per field")
     if graph:
         note += "; forward + backward + AdamW replayed as one captured HIP graph (GraphedEvalStep)"
-    extra = {}
+    # the MLP work of one iteration: forward + dX (2 x 572,416 FLOP; frozen weights, no dW) per sample
+    # evaluation, 64 coarse + 128 merged fine samples per ray, as train_bench's accounting
+    flop_iter = 2.0 * FLOP_PER_SAMPLE * 2048 * (64 + 128)
+    tflops = flop_iter / dt / 1e12
+    peak = PEAK_FP32_MFMA_TFLOPS if precision == "f32" else PEAK_BF16_MFMA_TFLOPS / 3.0
+    extra = {"mlp_tflop_per_iter": flop_iter / 1e12, "achieved_tflops": tflops, "frac_of_peak": tflops / peak}
     if sharded:
         world = dist.get_world_size()
         note += (f"; ray-sharded over {world} ranks (one optimisation; 2048 / {world} rays per rank and iteration, "
                  "one all-reduce of the 515 code / pose gradient floats; each share is its own Q1 chunk, so this "
                  "mode is reported beside the reference's per-rank optimisation, Q6)")
-        extra = {"scaling": "strong", "n_ranks": world, "rays_per_rank_per_iter": 2048 // world}
+        extra.update(scaling="strong", n_ranks=world, rays_per_rank_per_iter=2048 // world,
+                     frac_of_peak=tflops / (peak * world))
     return {"ms_per_iter": dt * 1e3, "rays_per_s": 2048 / dt, "rays_per_iter": 2048, "samples": "64+64 perturbed",
             "dtype": precision, **extra,
             "note": note + "; fused pose path + loss; host-side numpy ray permutation included; eval.py's "
