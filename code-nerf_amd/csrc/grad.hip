@@ -3127,9 +3127,10 @@ extern "C" int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, con
   // folded into the dW kernels below that stream those planes (deterministic partials), so the
   // fused backward sums none of them (a.gbias stays null).  With ONE code row (a chunk of one
   // object: every C3 step) g_code is column sums too -- of d feat (plane 2), of layer_xyz2's dPre
-  // (plane 3) and of d raw -- folded the same way, so the fp32 step is deterministic (no float
-  // atomics anywhere in it) and the fused kernel skips its code sums.
-  const bool fold_code = wg && !x3 && n_codes == 1;
+  // (plane 3) and of d raw -- folded the same way, so the step is deterministic in both precisions
+  // (no float atomics anywhere in it) and the fused kernel skips its code sums (fp32) or leaves its
+  // LDS sums unflushed (3xbf16).
+  const bool fold_code = wg && n_codes == 1;
   if (fold_code) a.g_code = nullptr;
   CN_TRY(x3 ? launch_field_x3_bwd(pts ? kFromPts : kFromRayZ, a, st)
             : launch_field_w16_bwd(pts ? kFromPts : kFromRayZ, a, st));

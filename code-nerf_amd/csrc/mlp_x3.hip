@@ -1214,7 +1214,9 @@ __device__ __forceinline__ void posenc_bwd(const float* x, const float* f, int h
   }
 }
 
-// Flush this wave's g_code row (LDS) into g_code[code] and zero it.
+// Flush this wave's g_code row (LDS) into g_code[code] and zero it.  g_code null (a training chunk of
+// one code row: its sums are the dPre planes' column sums, folded into the dW GEMMs in a fixed order):
+// the row is only cleared.
 __device__ __forceinline__ void flush_gcode(const State& s, const FieldArgs& a, float* blds, int code) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   float* row = blds + kGaccOff + s.wave * kCbStride;
@@ -1224,7 +1226,7 @@ __device__ __forceinline__ void flush_gcode(const State& s, const FieldArgs& a, 
     if (j < kCbStride) {
       float v;
       asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_addr(row + j)) : "memory");
-      if (v != 0.0f) atomicAdd(a.g_code + (int64_t)code * kCbStride + j, v);
+      if (v != 0.0f && a.g_code) atomicAdd(a.g_code + (int64_t)code * kCbStride + j, v);
       asm volatile("ds_write_b32 %0, %1" ::"v"(lds_addr(row + j)), "v"(0.0f) : "memory");
     }
   }

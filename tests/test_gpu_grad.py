@@ -684,8 +684,9 @@ def test_field_backward_train_nogeo_bitwise(dev, precision, mode, r, s, n_codes)
     d rd / d pts, and the fused kernel then skips the geometry-only chunks (view-direction rows of
     layer_dir1^T, both layer_xyz1^T chunks) and the encoding epilogue, storing layer_xyz1's dPre plane
     beside the next tile's fc_rgb^T.  Every weight and code gradient must be bitwise those of the
-    geometry schedule on the same chunk (one code row: deterministic throughout; several: the per-code
-    sums are float atomics, so g_code and the three biases formed from it agree to fp32 rounding)."""
+    geometry schedule on the same chunk (one code row: deterministic throughout, in both precisions --
+    g_code is the dPre planes' column sums folded into the dW GEMMs; several: the per-code sums are float
+    atomics, so g_code and the three biases formed from it agree to fp32 rounding)."""
     from codenerf import ops, synthetic
     if precision == "bf16x3" and s % 32:
         pytest.skip("3xbf16 fused backward: one code row per 32-sample wave")
@@ -715,7 +716,7 @@ def test_field_backward_train_nogeo_bitwise(dev, precision, mode, r, s, n_codes)
                                        code_index=code_index, param_grads=pg, precision=precision, **w, **geo)
         out[name] = (pg, res["g_code"])
     torch.cuda.synchronize()
-    atomic = n_codes > 1 or x3       # the per-code sums / biases of g_code: float atomics
+    atomic = n_codes > 1             # the per-code sums / biases of g_code: float atomics
     code_biases = {3, 5, 17}          # b_xyz2, b_out, b_rgb: column sums of g_code
     # float-atomic sums over ~67k samples whose partial sums exceed the total (cancellation): two orders
     # agree to 1e-5 of the total's magnitude in fp32, to 1e-4 in 3xbf16 (larger per-sample terms)

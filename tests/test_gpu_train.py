@@ -349,8 +349,7 @@ def test_step_fusions_bitwise(dev, monkeypatch, precision, off):
     * "sink": both fields' code gradients added into the code tables' gradient rows in place
       (CodeGradSink: fp32, one two-field cn_code_dz launch per step; 3xbf16, each field's
       accumulate_dz launch), the tables' .grad the optimiser's flat slices, vs dz returned, summed by
-      autograd and added into the row (3xbf16: to 1e-4, its fused backward's g_code is a float-atomic
-      sum);
+      autograd and added into the row;
     * "prefetch": both fields' pre-field launches as one (cn_field_prepare_models, once per step) vs one
       per field."""
     from codenerf import autograd as A, ops, train as T
@@ -412,20 +411,9 @@ def test_step_fusions_bitwise(dev, monkeypatch, precision, off):
     for step, (a, b) in enumerate(zip(g0, g1)):
         assert a.keys() == b.keys()
         for k in a:
-            if precision == "f32":
-                assert torch.equal(a[k], b[k]), ("grad", k)
-            elif step == 0:
-                # the 3xbf16 backward sums g_code with LDS float atomics: not bit-reproducible (two orders
-                # of those ~10^4-term sums, and the biases formed from them, agree to ~1e-5 of the total;
-                # test_field_backward_train_nogeo_bitwise saw 1.3e-5), and after a step the runs'
-                # parameters differ in their last bits (later ReLU decisions may then differ too), so only
-                # the first step's gradients are compared, to 1e-4
-                close(b[k], a[k], 1e-4, ("grad", k))
+            assert torch.equal(a[k], b[k]), ("grad", step, k)
     for k in p0:
-        if precision == "f32":
-            assert torch.equal(p0[k], p1[k]), ("param", k)
-        else:
-            assert (p0[k] - p1[k]).abs().max().item() <= 2.05 * 3 * 1e-3, ("param", k)
+        assert torch.equal(p0[k], p1[k]), ("param", k)
 
 
 def test_train_iteration_runs(dev):
@@ -459,10 +447,11 @@ def test_train_iteration_runs(dev):
     assert sched.last_epoch == 3
 
 
-def test_train_minibatch_deterministic(dev):
-    """fp32 chunk steps with one object per chunk (every C3 step) are bit-reproducible: g_code is
-    formed by fixed-order column sums folded into the dW GEMMs (no float atomics in the step), so two
-    identical model sets stepped on the same chunks end bit-identical -- what a checkpoint resume
+@pytest.mark.parametrize("precision", ["f32", "bf16x3"])
+def test_train_minibatch_deterministic(dev, precision):
+    """Chunk steps with one object per chunk (every C3 step) are bit-reproducible in both precisions:
+    g_code is formed by fixed-order column sums folded into the dW GEMMs (no float atomics in the step),
+    so two identical model sets stepped on the same chunks end bit-identical -- what a checkpoint resume
     relies on (train.py:129-138 + util.py:175-213)."""
     from codenerf import train as T
     from codenerf.nerf import PointSampler
@@ -470,8 +459,11 @@ def test_train_minibatch_deterministic(dev):
     for _ in range(2):
         torch.manual_seed(3)
         models = _train_models(dev, 3)
+        for key in ("nerf_coarse", "nerf_fine"):
+            models[key].precision = models[key].train_precision = precision
         opt, sched = T.prepare_optimizer(_opt_cfg(), models)
-        ps = PointSampler(16, 16, 0.8, 1.8, spacing_mode="lindepth", perturb=True, dtype=torch.float32, device=dev)
+        S = 32 if precision == "bf16x3" else 16     # the 3xbf16 backward: one code row per 32-sample wave
+        ps = PointSampler(S, S, 0.8, 1.8, spacing_mode="lindepth", perturb=True, dtype=torch.float32, device=dev)
         g = torch.Generator().manual_seed(5)
         for step in range(3):
             n = 256
