@@ -93,6 +93,9 @@ SIGNATURES = {
                                          _p]),
     "cn_field_backward_fused": (_i, [_i, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p, _i64, _fp, _fp, _p, _p,
                                      _p, _p, _p]),
+    "cn_field_backward_fused_workspace_floats": (_i64, [_i, _i64, _i64]),
+    "cn_field_backward_fused_ws": (_i, [_i, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p, _i64, _fp, _fp, _p,
+                                        _p, _p, _p, _p, _p]),
     "cn_radiance_field_train_w16": (_i, [_p, _p, _p, _i64, _p, _p, _p, _p, _i64, _i64, _i64, _fp, _fp, _p, _p, _p,
                                          _p]),
     "cn_radiance_field_train_fmt": (_i, [_i, _p, _p, _p, _i64, _p, _p, _p, _p, _i64, _i64, _i64, _fp, _fp, _p, _p, _p,

@@ -879,12 +879,15 @@ def field_backward_x3(packed_t: Tensor, masks: Tensor, d_raw: Tensor, n_rays: in
                       rd: Tensor, pts: Optional[Tensor] = None, ro: Optional[Tensor] = None,
                       z: Optional[Tensor] = None, code_index: Optional[Tensor] = None, want_pts: bool = False,
                       want_ro: bool = False, want_rd: bool = False, precision: str = "bf16x3",
-                      acc: Optional[Tensor] = None, ray_into: Optional[Tuple[Tensor, Tensor]] = None):
+                      acc: Optional[Tensor] = None, ray_into: Optional[Tuple[Tensor, Tensor]] = None,
+                      deterministic: bool = True):
     """Fused backward of forward_pass + CodeNeRFModel.forward (frozen weights) -> g_code / d_pts / d_ro / d_rd.
     precision "bf16x3" (packed_t "bf16x3_t") or "f32" (packed_t "f32_w16_t", masks of the f32_w16 forward).
     ``acc``: a zeroed buffer of field_backward_x3_acc_floats(...) floats for the accumulated outputs
     (field_prepare's), else one is allocated and filled.  ``ray_into`` ((R, 3) d ro, d rd device tensors,
-    with want_ro and want_rd): the ray gradients are ADDED into those (the kernel's atomics) instead."""
+    with want_ro and want_rd): the ray gradients are ADDED into those instead.  ``deterministic`` (default):
+    with one code row and S % 32 (bf16x3) / % 16 (f32) == 0, cn_field_backward_fused_ws's form without
+    float atomics, so repeated backwards give the same bits (False: the float-atomic kernel)."""
     fmt_t = _lib.CN_FMT_BF16X3_T if precision == "bf16x3" else _lib.CN_FMT_F32_W16_T
     lib = _lib_ready()
     m = n_rays * n_samples
@@ -910,10 +913,17 @@ def field_backward_x3(packed_t: Tensor, masks: Tensor, d_raw: Tensor, n_rays: in
     d_pts = torch.empty(n_rays, n_samples, 3, device=dev, dtype=torch.float32) if want_pts else None
     if m == 0:      # no samples: zero sums (the C ABI refuses n_rays == 0)
         return {"g_code": g_code, "d_pts": d_pts, "d_ro": d_ro, "d_rd": d_rd}
-    check(lib.cn_field_backward_fused(fmt_t, ptr(packed_t), ptr(masks), ptr(d_raw), ptr(pts), ptr(ro), ptr(rd),
-                                      ptr(z), n_rays, n_samples, chunk_rows, ptr(code_index), n_codes,
-                                      _lib.host_floats(freqs_xyz), _lib.host_floats(freqs_dir), ptr(g_code),
-                                      ptr(d_pts), ptr(d_ro), ptr(d_rd), stream_of(d_raw)), "cn_field_backward_fused")
+    # one code row, every wave inside one ray: the deterministic form (no float atomics; its partials in a
+    # workspace, summed in a fixed order by two short launches), else the float-atomic kernel
+    ws = None
+    if deterministic and n_codes == 1 and n_samples % (32 if precision == "bf16x3" else 16) == 0:
+        ws = torch.empty(int(lib.cn_field_backward_fused_workspace_floats(fmt_t, n_rays, n_samples)), device=dev,
+                         dtype=torch.float32)
+    check(lib.cn_field_backward_fused_ws(fmt_t, ptr(packed_t), ptr(masks), ptr(d_raw), ptr(pts), ptr(ro), ptr(rd),
+                                         ptr(z), n_rays, n_samples, chunk_rows, ptr(code_index), n_codes,
+                                         _lib.host_floats(freqs_xyz), _lib.host_floats(freqs_dir), ptr(g_code),
+                                         ptr(d_pts), ptr(d_ro), ptr(d_rd), ptr(ws), stream_of(d_raw)),
+          "cn_field_backward_fused_ws")
     return {"g_code": g_code, "d_pts": d_pts, "d_ro": d_ro, "d_rd": d_rd}
 
 

@@ -2236,6 +2236,52 @@ __global__ void gcode_bias_kernel(const float* __restrict__ g_code, int64_t n_co
   else b_rgb[j - kCbRgb] += acc;
 }
 
+// The deterministic fused eval backward's ray gradients (cn_field_backward_fused_ws): one wave per
+// ray r adds, in a fixed order (each lane its strided share, then a butterfly), the ray's wave rows of
+// ray_part (d ro, d rd of its points: S / ws rows) and the Q1 view-direction terms of q1_part (the S
+// samples k of r's chunk with k mod rcnt = r - base, nerf/__init__.py:127-128), then
+// d ro[r] += points' d ro and d rd[r] += points' d rd + Q1 d rd.
+__global__ __launch_bounds__(256) void ray_grad_reduce_kernel(const float* __restrict__ ray_part,
+                                                              const float* __restrict__ q1_part, int64_t n_rays,
+                                                              int64_t S, int64_t chunk_rows, int wave_samples,
+                                                              float* __restrict__ d_ro, float* __restrict__ d_rd) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= n_rays) return;  // wave-uniform
+  float v[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) v[i] = 0.0f;
+  if (ray_part) {
+    const int64_t nb = S / wave_samples;
+    for (int64_t b = lane; b < nb; b += 64) {
+      const float* p = ray_part + (r * nb + b) * 6;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) v[i] += p[i];
+    }
+  }
+  if (q1_part) {
+    const int64_t base = (r / chunk_rows) * chunk_rows;
+    const int64_t rcnt = min(chunk_rows, n_rays - base);
+    const int64_t k0 = base * S + (r - base);
+    for (int64_t j = lane; j < S; j += 64) {
+      const float* q = q1_part + 3 * (k0 + j * rcnt);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) v[6 + i] += q[i];
+    }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1)
+#pragma unroll
+    for (int i = 0; i < 9; ++i) v[i] += __shfl_xor(v[i], off);
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      if (d_ro) d_ro[3 * r + i] += v[i];
+      if (d_rd) d_rd[3 * r + i] += v[3 + i] + v[6 + i];
+    }
+  }
+}
+
 }  // namespace grad
 }  // namespace cn
 
@@ -3059,6 +3105,58 @@ static int rgb_dw_draw_sums(const float* d_raw, const float* v2, float* C, int64
   CN_TRY(reduce(rd, ws, pl.parts, 3, 256, C, ldc, st));
   CN_TRY(reduce(rd, cpart, nb, 1, 3, g_rgb, 3, st));
   return reduce(rd, cpart + 3 * (int64_t)nb, nb, 1, 1, g_sig, 1, st);
+}
+
+// ---- the fused eval backward without float atomics (one code row, every wave inside one ray)
+
+static int64_t fused_ws_layout(int fmt_t, int64_t m, int64_t* ray_off, int64_t* q1_off) {
+  const int64_t ws = fmt_t == CN_FMT_BF16X3_T ? 32 : 16;
+  // the launch's grid is at most one workgroup per 128-sample tile and kMaxBwdBlocks
+  const int64_t gc = std::min<int64_t>(ceil_div(m, 128), mlp::kMaxBwdBlocks) * mlp::kMaxBwdWaves * mlp::kCbStride;
+  const int64_t rp = ceil_div(m, ws) * 6;
+  if (ray_off) *ray_off = gc;
+  if (q1_off) *q1_off = gc + ceil_div(rp, 4) * 4;
+  return gc + ceil_div(rp, 4) * 4 + 3 * m;
+}
+
+extern "C" int64_t cn_field_backward_fused_workspace_floats(int fmt_t, int64_t n_rays, int64_t n_samples) {
+  if (!(fmt_t == CN_FMT_BF16X3_T || fmt_t == CN_FMT_F32_W16_T) || n_rays <= 0 || n_samples <= 0) return -1;
+  return fused_ws_layout(fmt_t, n_rays * n_samples, nullptr, nullptr);
+}
+
+extern "C" int cn_field_backward_fused_ws(int fmt_t, const float* packed_t, const uint32_t* masks,
+                                          const float* d_raw, const float* pts, const float* ro, const float* rd,
+                                          const float* z, int64_t n_rays, int64_t n_samples, int64_t chunk_rows,
+                                          const int64_t* code_index, int64_t n_codes, const float* freqs_xyz,
+                                          const float* freqs_dir, float* g_code, float* d_pts, float* d_ro,
+                                          float* d_rd, float* workspace, cn_stream_t stream) {
+  mlp::FieldArgs a;
+  CN_TRY(mlp::fused_backward_args(fmt_t, packed_t, masks, d_raw, pts, ro, rd, z, n_rays, n_samples, chunk_rows,
+                                  code_index, n_codes, freqs_xyz, freqs_dir, g_code, d_pts, d_ro, d_rd, a));
+  hipStream_t st = as_stream(stream);
+  const int mode = pts ? mlp::kFromPts : mlp::kFromRayZ;
+  const bool x3 = fmt_t == CN_FMT_BF16X3_T;
+  const int wave_samples = x3 ? 32 : 16;
+  // the deterministic form needs one code row (g_code: one row per workgroup) and every wave inside
+  // one ray (the ray rows); otherwise the float-atomic kernel
+  const bool det = workspace && n_codes == 1 && n_samples % wave_samples == 0;
+  if (det) {
+    int64_t ray_off = 0, q1_off = 0;
+    fused_ws_layout(fmt_t, a.m, &ray_off, &q1_off);
+    a.gc_part = workspace;
+    a.ray_part = mode == mlp::kFromRayZ && (d_ro || d_rd) ? workspace + ray_off : nullptr;
+    a.q1_part = d_rd ? workspace + q1_off : nullptr;
+  }
+  CN_TRY(x3 ? mlp::launch_field_x3_bwd(mode, a, st) : mlp::launch_field_w16_bwd(mode, a, st));
+  if (!det) return CN_OK;
+  // g_code += the waves' rows, in (workgroup, wave) order (the dW GEMMs' fixed-order reduction)
+  CN_TRY(reduce(nullptr, a.gc_part, a.n_blocks * (x3 ? 4 : 8), 1, mlp::kCbStride, g_code, mlp::kCbStride, st));
+  if (a.ray_part || a.q1_part) {
+    hipLaunchKernelGGL(grad::ray_grad_reduce_kernel, dim3(static_cast<unsigned>(ceil_div(n_rays, 4))), dim3(256), 0,
+                       st, a.ray_part, a.q1_part, n_rays, n_samples, chunk_rows, wave_samples, d_ro, d_rd);
+    CN_TRY(launch_status());
+  }
+  return CN_OK;
 }
 
 extern "C" int64_t cn_field_backward_train_workspace_floats(int64_t m) {

@@ -651,12 +651,14 @@ extern "C" int cn_field_backward_x3(const float* packed_t, const uint32_t* masks
                                  stream);
 }
 
-extern "C" int cn_field_backward_fused(int fmt_t, const float* packed_t, const uint32_t* masks, const float* d_raw,
-                                       const float* pts, const float* ro, const float* rd, const float* z,
-                                       int64_t n_rays, int64_t n_samples, int64_t chunk_rows,
-                                       const int64_t* code_index, int64_t n_codes, const float* freqs_xyz,
-                                       const float* freqs_dir, float* g_code, float* d_pts, float* d_ro,
-                                       float* d_rd, cn_stream_t stream) {
+namespace cn {
+namespace mlp {
+// cn_field_backward_fused's checks and kernel arguments (shared with cn_field_backward_fused_ws).
+int fused_backward_args(int fmt_t, const float* packed_t, const uint32_t* masks, const float* d_raw,
+                        const float* pts, const float* ro, const float* rd, const float* z, int64_t n_rays,
+                        int64_t n_samples, int64_t chunk_rows, const int64_t* code_index, int64_t n_codes,
+                        const float* freqs_xyz, const float* freqs_dir, float* g_code, float* d_pts, float* d_ro,
+                        float* d_rd, FieldArgs& a) {
   CN_CHECK_ARG(fmt_t == CN_FMT_BF16X3_T || fmt_t == CN_FMT_F32_W16_T);
   CN_CHECK_ARG(packed_t && masks && d_raw && rd && g_code && freqs_xyz && freqs_dir);
   CN_CHECK_ARG(n_rays > 0 && n_samples > 0 && chunk_rows > 0 && n_codes > 0);
@@ -667,7 +669,7 @@ extern "C" int cn_field_backward_fused(int fmt_t, const float* packed_t, const u
   // one code row per wave (32 samples x3, 16 samples w16): a single code, or every wave inside one ray
   const int wave_samples = fmt_t == CN_FMT_BF16X3_T ? 32 : 16;
   if (!(n_codes == 1 || n_samples % wave_samples == 0)) return CN_EUNSUPPORTED;
-  FieldArgs a = {};
+  a = FieldArgs{};
   a.packed = packed_t;
   a.code_index = code_index;
   a.n_codes = n_codes;
@@ -689,6 +691,21 @@ extern "C" int cn_field_backward_fused(int fmt_t, const float* packed_t, const u
   a.d_pts = d_pts;
   a.d_ro = d_ro;
   a.d_rd = d_rd;
+  return CN_OK;
+}
+}  // namespace mlp
+}  // namespace cn
+
+extern "C" int cn_field_backward_fused(int fmt_t, const float* packed_t, const uint32_t* masks, const float* d_raw,
+                                       const float* pts, const float* ro, const float* rd, const float* z,
+                                       int64_t n_rays, int64_t n_samples, int64_t chunk_rows,
+                                       const int64_t* code_index, int64_t n_codes, const float* freqs_xyz,
+                                       const float* freqs_dir, float* g_code, float* d_pts, float* d_ro,
+                                       float* d_rd, cn_stream_t stream) {
+  FieldArgs a;
+  const int rc = fused_backward_args(fmt_t, packed_t, masks, d_raw, pts, ro, rd, z, n_rays, n_samples, chunk_rows,
+                                     code_index, n_codes, freqs_xyz, freqs_dir, g_code, d_pts, d_ro, d_rd, a);
+  if (rc != CN_OK) return rc;
   return fmt_t == CN_FMT_BF16X3_T ? launch_field_x3_bwd(pts ? kFromPts : kFromRayZ, a, cn::as_stream(stream))
                                   : launch_field_w16_bwd(pts ? kFromPts : kFromRayZ, a, cn::as_stream(stream));
 }

@@ -46,7 +46,17 @@ struct FieldArgs {
   float* d_rd;           // backward: (n_rays, 3) accumulated
   float* dpre;           // fp32 fused training backward: (5, m, 256) masked layer-input gradients
   float* xenc;           // fp32 training forward: (m, 64) the positional encodings it multiplied (xenc_col)
+  // fused eval backward, deterministic form (cn_field_backward_fused_ws: one code row, every wave inside
+  // one ray): no float atomics -- partials a fixed-order reduction adds up afterwards
+  float* gc_part;        // (blocks x waves, kCbStride): each wave's g_code row
+  float* ray_part;       // (m / wave samples, 6): each wave's d ro, d rd of its ray (the points' part)
+  float* q1_part;        // (m, 3): each sample's d rd of its Q1 view-direction ray
+  int64_t n_blocks;      // set by the backward launchers: the grid they launched
 };
+
+// The most workgroups a fused backward launches in the deterministic form, and its most waves per
+// workgroup (gc_part holds kMaxBwdBlocks x kMaxBwdWaves rows).
+constexpr int64_t kMaxBwdBlocks = 512, kMaxBwdWaves = 8;
 
 // Column c' of the fp32 training forward's encoding plane (64 floats per sample: lane group g's 16
 // k-step values of layer_xyz1 at 16 g + t) -> PositionalEmbedder column (position_embed.py:44-53:
@@ -299,6 +309,12 @@ struct PrepareModel {
 int launch_field_prepare_w16(const PrepareModel* models, int n_models, const float* z_s, const float* z_t,
                              int64_t n_codes, hipStream_t st);
 int launch_field_w16_bwd(int mode, FieldArgs& a, hipStream_t st);
+// cn_field_backward_fused's argument checks, into a (mlp.hip).
+int fused_backward_args(int fmt_t, const float* packed_t, const uint32_t* masks, const float* d_raw,
+                        const float* pts, const float* ro, const float* rd, const float* z, int64_t n_rays,
+                        int64_t n_samples, int64_t chunk_rows, const int64_t* code_index, int64_t n_codes,
+                        const float* freqs_xyz, const float* freqs_dir, float* g_code, float* d_pts, float* d_ro,
+                        float* d_rd, FieldArgs& a);
 // The training backwards' no-geometry schedule (no d ro / d rd / d pts wanted) unless CN_BWD_NOGEO=0.
 bool nogeo_enabled();
 

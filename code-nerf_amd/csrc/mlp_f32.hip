@@ -1261,7 +1261,7 @@ __device__ __forceinline__ uint2 load_mask(const State& s, const FieldArgs& a, i
 // left in s.act at the tile's end and stored beside the next tile's fc_rgb^T MFMAs (chunk_k0), the
 // last tile's after the tile loop.  crun: the running chunk counter (stream_src); prev: the tile
 // whose plane 4 is pending (-1: none).
-template <int MODE, bool TRAIN, bool NOGEO = false>
+template <int MODE, bool TRAIN, bool NOGEO = false, bool DET = false>
 __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* lds, float* grow, int64_t tile,
                                         int& cur_code, int& crun, int64_t& prev) {
   const int64_t row = tile * kTile + s.wave * 16 + (s.lane & 15);
@@ -1361,6 +1361,11 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
     const float dot = in.vd[0] * dv[0] + in.vd[1] * dv[1] + in.vd[2] * dv[2];
 #pragma unroll
     for (int d = 0; d < 3; ++d) grd_q1[d] = (dv[d] - in.vd[d] * dot) / in.nrm;
+    if constexpr (DET) {
+      // deterministic form: this sample's Q1 term as its q1_part row, here (not live to the tile's end)
+      if (valid && s.g == 0 && a.d_rd)
+        for (int d = 0; d < 3; ++d) a.q1_part[3 * rc + d] = grd_q1[d];
+    }
   }
   // ---- fc_out^T: B = d feat (no activation), init = fc_out row 0 (h2 part) x d sigma
 #pragma unroll
@@ -1449,22 +1454,36 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
     }
     if (valid && s.g == 0 && (!one_ray || s.lane == 0)) {
       const int64_t ray = rc / S;
-      if (a.d_ro)
-        for (int d = 0; d < 3; ++d) atomicAdd(a.d_ro + 3 * ray + d, gro[d]);
-      if (a.d_rd)
-        for (int d = 0; d < 3; ++d) atomicAdd(a.d_rd + 3 * ray + d, grd[d]);
+      if constexpr (DET) {
+        // deterministic form (one ray per wave, host-checked): the wave's sums as its row of ray_part
+        // (lane 0's rc is the wave's first sample, a multiple of 16)
+        if (a.ray_part) {
+          float* p = a.ray_part + (rc >> 4) * 6;
+          for (int d = 0; d < 3; ++d) {
+            p[d] = gro[d];
+            p[3 + d] = grd[d];
+          }
+        }
+      } else {
+        if (a.d_ro)
+          for (int d = 0; d < 3; ++d) atomicAdd(a.d_ro + 3 * ray + d, gro[d]);
+        if (a.d_rd)
+          for (int d = 0; d < 3; ++d) atomicAdd(a.d_rd + 3 * ray + d, grd[d]);
+      }
     }
   } else {
     if (valid && s.g == 0 && a.d_pts)
       for (int d = 0; d < 3; ++d) a.d_pts[3 * rc + d] = dx[d];
   }
-  if (valid && s.g == 0 && a.d_rd) {
-    const int64_t dray = q1_dir_ray(a, rc);
-    for (int d = 0; d < 3; ++d) atomicAdd(a.d_rd + 3 * dray + d, grd_q1[d]);
+  if constexpr (!DET) {
+    if (valid && s.g == 0 && a.d_rd) {
+      const int64_t dray = q1_dir_ray(a, rc);
+      for (int d = 0; d < 3; ++d) atomicAdd(a.d_rd + 3 * dray + d, grd_q1[d]);
+    }
   }
 }
 
-template <int MODE, bool TRAIN, bool NOGEO = false>
+template <int MODE, bool TRAIN, bool NOGEO = false, bool DET = false>
 __global__ __launch_bounds__(kThreads, 2) void field_w16_bwd_kernel(FieldArgs a) {
   static_assert(!NOGEO || TRAIN, "the no-geometry schedule is the training backward's");
   __shared__ __attribute__((aligned(16))) float4 lds[kBwdLdsQuads];
@@ -1498,7 +1517,7 @@ __global__ __launch_bounds__(kThreads, 2) void field_w16_bwd_kernel(FieldArgs a)
   int crun = 0;
   int64_t prev = -1;
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
-    bwd_tile<MODE, TRAIN, NOGEO>(s, a, lds, grow, tile, cur_code, crun, prev);
+    bwd_tile<MODE, TRAIN, NOGEO, DET>(s, a, lds, grow, tile, cur_code, crun, prev);
 #ifdef CN_PROBE_PROLOGUE
     ++nt;
 #endif
@@ -1514,7 +1533,19 @@ __global__ __launch_bounds__(kThreads, 2) void field_w16_bwd_kernel(FieldArgs a)
   }
 #endif
   __builtin_amdgcn_s_waitcnt(0x0F70);
-  if (cur_code >= 0) flush_gcode(s, a, grow, cur_code);
+  if constexpr (DET) {
+    // deterministic form (one code row, host-checked): this wave's g_code row into its gc_part row
+    // (every wave writes its row, zeros included)
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS atomics landed
+    float* out = a.gc_part + ((int64_t)blockIdx.x * kWaves + s.wave) * kCbStride;
+#pragma unroll
+    for (int k = 0; k < (kCbStride + 63) / 64; ++k) {
+      const int j = s.lane + 64 * k;
+      if (j < kCbStride) out[j] = grow[j];
+    }
+  } else if (cur_code >= 0) {
+    flush_gcode(s, a, grow, cur_code);
+  }
 }
 
 }  // namespace w16
@@ -1603,7 +1634,9 @@ bool nogeo_enabled() {
 }
 
 int launch_field_w16_bwd(int mode, FieldArgs& a, hipStream_t st) {
-  const unsigned grid = static_cast<unsigned>(std::min<int64_t>(cn::ceil_div(a.m, w16::kTile), cu_count_w16()));
+  const unsigned grid = static_cast<unsigned>(
+      std::min<int64_t>(std::min<int64_t>(cn::ceil_div(a.m, w16::kTile), cu_count_w16()), kMaxBwdBlocks));
+  a.n_blocks = grid;
   const dim3 b(w16::kThreads);
   // training with no geometry gradient wanted (train.py: the rays are data): the 33-chunk schedule
   if (a.dpre && !a.d_pts && !a.d_ro && !a.d_rd && nogeo_enabled()) {
@@ -1615,6 +1648,12 @@ int launch_field_w16_bwd(int mode, FieldArgs& a, hipStream_t st) {
   if (a.dpre) {
     if (mode == kFromPts) hipLaunchKernelGGL((w16::field_w16_bwd_kernel<kFromPts, true>), dim3(grid), b, 0, st, a);
     else if (mode == kFromRayZ) hipLaunchKernelGGL((w16::field_w16_bwd_kernel<kFromRayZ, true>), dim3(grid), b, 0, st, a);
+    else return CN_EUNSUPPORTED;
+    return cn::launch_status();
+  }
+  if (a.gc_part) {   // the eval backward without float atomics (cn_field_backward_fused_ws)
+    if (mode == kFromPts) hipLaunchKernelGGL((w16::field_w16_bwd_kernel<kFromPts, false, false, true>), dim3(grid), b, 0, st, a);
+    else if (mode == kFromRayZ) hipLaunchKernelGGL((w16::field_w16_bwd_kernel<kFromRayZ, false, false, true>), dim3(grid), b, 0, st, a);
     else return CN_EUNSUPPORTED;
     return cn::launch_status();
   }

@@ -1255,7 +1255,7 @@ __device__ __forceinline__ void store_x1_plane(State& s, const unsigned* mw) {
 // only feed those outputs, so they are not streamed or run (33 chunks per tile, DmaNoGeo; layer_dir1^T
 // copies its d feat out itself).  layer_xyz1's dPre plane is stored from the slots at the tile's end.
 // crun: the running chunk counter.
-template <int MODE, bool TRAIN, bool NOGEO = false>
+template <int MODE, bool TRAIN, bool NOGEO = false, bool DET = false>
 __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* lds, float* blds, int64_t tile,
                                          int& cur_code, int& crun) {
   using D = typename std::conditional<NOGEO, DmaNoGeo, DmaFull>::type;
@@ -1410,10 +1410,22 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
     }
     if (valid && s.h == 0 && (!one_ray || (s.lane & 31) == 0)) {
       const int64_t ray = rc / S;
-      if (a.d_ro)
-        for (int d = 0; d < 3; ++d) atomicAdd(a.d_ro + 3 * ray + d, gro[d]);
-      if (a.d_rd)
-        for (int d = 0; d < 3; ++d) atomicAdd(a.d_rd + 3 * ray + d, grd[d]);
+      if constexpr (DET) {
+        // deterministic form (one ray per wave, host-checked): the wave's sums as its row of ray_part
+        // (lane 0's rc is the wave's first sample, a multiple of 32)
+        if (a.ray_part) {
+          float* p = a.ray_part + (rc >> 5) * 6;
+          for (int d = 0; d < 3; ++d) {
+            p[d] = gro[d];
+            p[3 + d] = grd[d];
+          }
+        }
+      } else {
+        if (a.d_ro)
+          for (int d = 0; d < 3; ++d) atomicAdd(a.d_ro + 3 * ray + d, gro[d]);
+        if (a.d_rd)
+          for (int d = 0; d < 3; ++d) atomicAdd(a.d_rd + 3 * ray + d, grd[d]);
+      }
     }
   }
   if (valid && s.h == 0) {
@@ -1430,12 +1442,16 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
       const float d0 = a.rd[3 * dray], d1 = a.rd[3 * dray + 1], d2 = a.rd[3 * dray + 2];
       const float nrm = sqrtf(d0 * d0 + d1 * d1 + d2 * d2);
       const float dot = in.vd[0] * dv[0] + in.vd[1] * dv[1] + in.vd[2] * dv[2];
-      for (int d = 0; d < 3; ++d) atomicAdd(a.d_rd + 3 * dray + d, (dv[d] - in.vd[d] * dot) / nrm);
+      if constexpr (DET) {
+        for (int d = 0; d < 3; ++d) a.q1_part[3 * rc + d] = (dv[d] - in.vd[d] * dot) / nrm;
+      } else {
+        for (int d = 0; d < 3; ++d) atomicAdd(a.d_rd + 3 * dray + d, (dv[d] - in.vd[d] * dot) / nrm);
+      }
     }
   }
 }
 
-template <int MODE, bool TRAIN = false, bool NOGEO = false>
+template <int MODE, bool TRAIN = false, bool NOGEO = false, bool DET = false>
 __global__ __launch_bounds__(kThreads, 1) void field_x3_bwd_kernel(FieldArgs a) {
   static_assert(!NOGEO || TRAIN, "the no-geometry schedule is the training backward's");
   __shared__ __attribute__((aligned(16))) float4 lds[kLdsQuads + kBwdLdsFloats / 4];
@@ -1463,9 +1479,22 @@ __global__ __launch_bounds__(kThreads, 1) void field_x3_bwd_kernel(FieldArgs a) 
   const int64_t n_tiles = (a.m + kTile - 1) / kTile;
   int crun = 0;
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x)
-    bwd_tile<MODE, TRAIN, NOGEO>(s, a, lds, blds, tile, cur_code, crun);
+    bwd_tile<MODE, TRAIN, NOGEO, DET>(s, a, lds, blds, tile, cur_code, crun);
   __builtin_amdgcn_s_waitcnt(0x0F70);
-  if (cur_code >= 0) flush_gcode(s, a, blds, cur_code);
+  if constexpr (DET) {
+    // deterministic form (one code row, host-checked): this wave's g_code row into its gc_part row
+    // (every wave writes its row, zeros included)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const float* row = blds + kGaccOff + s.wave * kCbStride;
+    float* out = a.gc_part + ((int64_t)blockIdx.x * kWaves + s.wave) * kCbStride;
+#pragma unroll
+    for (int k = 0; k < (kCbStride + 63) / 64; ++k) {
+      const int j = s.lane + 64 * k;
+      if (j < kCbStride) out[j] = row[j];
+    }
+  } else if (cur_code >= 0) {
+    flush_gcode(s, a, blds, cur_code);
+  }
 }
 
 static_assert(kTChunkX1 + 2 == kChunks, "backward chunk schedule");
@@ -1504,7 +1533,9 @@ int launch_pack_x3t(const Params& P, float* packed, hipStream_t st) {
 int64_t mask_words_x3(int64_t m) { return cn::ceil_div(m, x3::kTile) * x3::kMaskWordsPerTile; }
 
 int launch_field_x3_bwd(int mode, FieldArgs& a, hipStream_t st) {
-  const unsigned grid = static_cast<unsigned>(std::min<int64_t>(cn::ceil_div(a.m, x3::kTile), cu_count()));
+  const unsigned grid = static_cast<unsigned>(
+      std::min<int64_t>(std::min<int64_t>(cn::ceil_div(a.m, x3::kTile), cu_count()), kMaxBwdBlocks));
+  a.n_blocks = grid;
   if (a.dpre && !a.d_pts && !a.d_ro && !a.d_rd && nogeo_enabled()) {
     switch (mode) {
       case kFromPts: hipLaunchKernelGGL((x3::field_x3_bwd_kernel<kFromPts, true, true>), dim3(grid), dim3(x3::kThreads), 0, st, a); break;
@@ -1517,6 +1548,14 @@ int launch_field_x3_bwd(int mode, FieldArgs& a, hipStream_t st) {
     switch (mode) {
       case kFromPts: hipLaunchKernelGGL((x3::field_x3_bwd_kernel<kFromPts, true>), dim3(grid), dim3(x3::kThreads), 0, st, a); break;
       case kFromRayZ: hipLaunchKernelGGL((x3::field_x3_bwd_kernel<kFromRayZ, true>), dim3(grid), dim3(x3::kThreads), 0, st, a); break;
+      default: return CN_EUNSUPPORTED;
+    }
+    return cn::launch_status();
+  }
+  if (a.gc_part) {   // the eval backward without float atomics (cn_field_backward_fused_ws)
+    switch (mode) {
+      case kFromPts: hipLaunchKernelGGL((x3::field_x3_bwd_kernel<kFromPts, false, false, true>), dim3(grid), dim3(x3::kThreads), 0, st, a); break;
+      case kFromRayZ: hipLaunchKernelGGL((x3::field_x3_bwd_kernel<kFromRayZ, false, false, true>), dim3(grid), dim3(x3::kThreads), 0, st, a); break;
       default: return CN_EUNSUPPORTED;
     }
     return cn::launch_status();

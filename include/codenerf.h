@@ -349,6 +349,18 @@ int cn_field_backward_fused(int fmt_t, const float* packed_t, const uint32_t* ma
                             int64_t n_samples, int64_t chunk_rows, const int64_t* code_index, int64_t n_codes,
                             const float* freqs_xyz, const float* freqs_dir, float* g_code, float* d_pts,
                             float* d_ro, float* d_rd, cn_stream_t stream);
+/* The same backward without float atomics (eval.py:145-160's backward, bit-reproducible): with
+ * n_codes == 1 and n_samples % 32 (bf16x3) / % 16 (fp32) == 0 the kernel writes per-workgroup g_code
+ * rows and per-wave / per-sample ray-gradient terms into workspace
+ * (cn_field_backward_fused_workspace_floats(fmt_t, n_rays, n_samples) floats, 16-B aligned), and two
+ * short launches add them into g_code, d_ro and d_rd in a fixed order (g_code / d_ro / d_rd are still
+ * ACCUMULATED).  Other shapes, or workspace NULL, run cn_field_backward_fused. */
+int64_t cn_field_backward_fused_workspace_floats(int fmt_t, int64_t n_rays, int64_t n_samples);
+int cn_field_backward_fused_ws(int fmt_t, const float* packed_t, const uint32_t* masks, const float* d_raw,
+                               const float* pts, const float* ro, const float* rd, const float* z, int64_t n_rays,
+                               int64_t n_samples, int64_t chunk_rows, const int64_t* code_index, int64_t n_codes,
+                               const float* freqs_xyz, const float* freqs_dir, float* g_code, float* d_pts,
+                               float* d_ro, float* d_rd, float* workspace, cn_stream_t stream);
 
 /* --- Fused fp32 training step (train.py:92-114; weights trained) ------------------
  * Forward: cn_radiance_field on a CN_FMT_F32_W16 pack that also writes the ReLU masks

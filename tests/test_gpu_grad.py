@@ -733,6 +733,51 @@ def test_field_backward_train_nogeo_bitwise(dev, precision, mode, r, s, n_codes)
             assert torch.equal(out[other][1], out["geo"][1]), f"g_code: {other}"
 
 
+@pytest.mark.parametrize("precision", ["f32", "bf16x3"])
+@pytest.mark.parametrize("mode,r,s,chunk", [("rayz", 300, 64, 128),   # 3 Q1 chunks, the last one short
+                                            ("rayz", 64, 128, 64),
+                                            ("rayz", 2048, 64, 2048),  # C5's coarse pass
+                                            ("pts", 37, 32, 37)])
+def test_fused_backward_deterministic(dev, precision, mode, r, s, chunk):
+    """The eval backward without float atomics (cn_field_backward_fused_ws, the default of
+    ops.field_backward_x3 for one code row and whole waves per ray): per-wave g_code rows, per-wave
+    ray rows and per-sample Q1 terms summed in a fixed order.  Two runs give the same bits; the
+    float-atomic kernel agrees to fp32 reassociation; d ro / d rd are ADDED into given tensors."""
+    from codenerf import ops, synthetic
+    m = model(dev, 0)
+    params = [p.detach() for p in m.param_list()]
+    x3 = precision == "bf16x3"
+    g = torch.Generator().manual_seed(r + s + chunk)
+    ro = (torch.randn(r, 3, generator=g) * 0.3 + torch.tensor([0.0, 0.0, 1.3])).to(dev)
+    rd = torch.randn(r, 3, generator=g).to(dev)
+    z = torch.sort(0.8 + torch.rand(r, s, generator=g), dim=-1).values.to(dev)
+    pts = (ro[:, None, :] + rd[:, None, :] * z[..., None]).contiguous() if mode == "pts" else None
+    geo = dict(pts=pts) if mode == "pts" else dict(ro=ro, z=z)
+    gout = torch.randn(r, s, 4, generator=g).to(dev)
+    zs, zt = synthetic.latent_codes(5, 1).to(dev), synthetic.latent_codes(6, 1).to(dev)
+    fx, fd = [2.0 ** k for k in range(10)], [2.0 ** k for k in range(4)]
+    cb = ops.code_bias(params, zs, zt)
+    _, masks = ops.radiance_field_masks(ops.mlp_pack(params, "bf16x3" if x3 else "f32_w16"), cb, rd, s, chunk, fx,
+                                        fd, precision=precision, **geo)
+    packed_t = ops.mlp_pack(params, "bf16x3_t" if x3 else "f32_w16_t")
+    want = dict(want_pts=True, want_rd=True) if mode == "pts" else dict(want_ro=True, want_rd=True)
+
+    def run(det, **kw):
+        out = ops.field_backward_x3(packed_t, masks, gout, r, s, chunk, 1, fx, fd, rd, precision=precision,
+                                    deterministic=det, **geo, **want, **kw)
+        return {k: v.clone() for k, v in out.items() if v is not None}
+    a, b, c = run(True), run(True), run(False)
+    torch.cuda.synchronize()
+    for k in a:
+        assert torch.equal(a[k], b[k]), f"{k}: two deterministic runs differ"
+        close(a[k], c[k].double(), 1e-5, f"{k} vs the float-atomic kernel")
+    if mode == "rayz":
+        base = (torch.randn(r, 3, generator=g).to(dev), torch.randn(r, 3, generator=g).to(dev))
+        into = (base[0].clone(), base[1].clone())
+        run(True, ray_into=into)
+        assert torch.equal(into[0], base[0] + a["d_ro"]) and torch.equal(into[1], base[1] + a["d_rd"])
+
+
 @pytest.mark.parametrize("n_codes,want_grads", [(1, True), (5, True), (5, False)])
 def test_code_bias_backward_two_launch_bitwise(dev, n_codes, want_grads):
     """cn_code_bias_backward_ws (code layers split over 64 workgroups per code, two launches) gives

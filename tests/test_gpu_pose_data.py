@@ -216,10 +216,9 @@ def test_eval_step_in_place_gradients(dev, monkeypatch, precision):
     for both; code_rows_with_sink's CodeGradSink), the rays' by both volume renders and both fields into
     the fine field's zeroed accumulators (RaySink), the pose angles' written into their slots -- every
     leaf's .grad is then its flat slice (no autograd adds, no copy into the flat buffer) -- against the
-    route through autograd: the loss bit for bit, the code gradients to 1e-6 (the same sums in the same
-    order, of g_code's float-atomic sums -- not bit-reproducible run to run), the angles to 1e-5 (the ray
-    sums' atomics round differently).  torch.autograd.grad through the sinks returns the same code
-    gradients."""
+    route through autograd: the loss and every gradient bit for bit (the same sums in the same order, and
+    the eval backward's g_code / ray sums are fixed-order, cn_field_backward_fused_ws).
+    torch.autograd.grad through the sinks returns the same code gradients."""
     from codenerf import autograd as A, synthetic
     from codenerf.evaluate import eval_step_loss
     from codenerf.models import model as M
@@ -253,7 +252,7 @@ def test_eval_step_in_place_gradients(dev, monkeypatch, precision):
     (l0, g0), (l1, g1) = out
     assert l0 == l1
     for name, a, b in zip(("theta", "phi", "rho", "z_s", "z_t"), g0, g1):
-        close(a, b, 1e-6 if name.startswith("z") else 1e-5, name)
+        assert torch.equal(a, b), (name, (a - b).abs().max().item())
     # torch.autograd.grad (no .grad accumulation) through the sinks: the same code gradients
     monkeypatch.undo()
     lv = [g[k].clone().requires_grad_(True) for k in ("theta", "phi", "rho", "z_s", "z_t")]
@@ -263,7 +262,7 @@ def test_eval_step_in_place_gradients(dev, monkeypatch, precision):
     loss, _ = eval_step_loss(*lv, g["target"], (rs, ps), embedders(dev), models, 1e-5, t_rand=g["t_rand"], u=g["u"])
     gz = torch.autograd.grad(loss, lv[3:])
     for name, a, b in zip(("z_s", "z_t"), gz, g0[3:]):
-        close(a, b, 1e-6, "autograd.grad " + name)
+        assert torch.equal(a, b), ("autograd.grad " + name, (a - b).abs().max().item())
 
 
 # ---------------------------------------------------------------- the fused step loss
