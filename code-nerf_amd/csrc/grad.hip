@@ -2241,10 +2241,25 @@ __global__ void gcode_bias_kernel(const float* __restrict__ g_code, int64_t n_co
 // ray_part (d ro, d rd of its points: S / ws rows) and the Q1 view-direction terms of q1_part (the S
 // samples k of r's chunk with k mod rcnt = r - base, nerf/__init__.py:127-128), then
 // d ro[r] += points' d ro and d rd[r] += points' d rd + Q1 d rd.
+// Blocks past the rays' (gc_blocks of them) add each backward workgroup's wave rows of gc_part in wave
+// order into gc_rows (one row per workgroup), which reduce_partials_kernel then sums in block order.
 __global__ __launch_bounds__(256) void ray_grad_reduce_kernel(const float* __restrict__ ray_part,
                                                               const float* __restrict__ q1_part, int64_t n_rays,
                                                               int64_t S, int64_t chunk_rows, int wave_samples,
-                                                              float* __restrict__ d_ro, float* __restrict__ d_rd) {
+                                                              float* __restrict__ d_ro, float* __restrict__ d_rd,
+                                                              const float* __restrict__ gc_part, int gc_waves,
+                                                              float* __restrict__ gc_rows) {
+  const int64_t ray_blocks = (n_rays + 3) / 4;
+  if ((int64_t)blockIdx.x >= ray_blocks) {
+    const int64_t b = (int64_t)blockIdx.x - ray_blocks;
+    const float* rows = gc_part + b * gc_waves * mlp::kCbStride;
+    for (int j = threadIdx.x; j < mlp::kCbStride; j += 256) {
+      float v = rows[j];
+      for (int w = 1; w < gc_waves; ++w) v += rows[(int64_t)w * mlp::kCbStride + j];
+      gc_rows[b * mlp::kCbStride + j] = v;
+    }
+    return;
+  }
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (r >= n_rays) return;  // wave-uniform
@@ -3109,19 +3124,22 @@ static int rgb_dw_draw_sums(const float* d_raw, const float* v2, float* C, int64
 
 // ---- the fused eval backward without float atomics (one code row, every wave inside one ray)
 
-static int64_t fused_ws_layout(int fmt_t, int64_t m, int64_t* ray_off, int64_t* q1_off) {
+static int64_t fused_ws_layout(int fmt_t, int64_t m, int64_t* ray_off, int64_t* q1_off, int64_t* rows_off) {
   const int64_t ws = fmt_t == CN_FMT_BF16X3_T ? 32 : 16;
   // the launch's grid is at most one workgroup per 128-sample tile and kMaxBwdBlocks
-  const int64_t gc = std::min<int64_t>(ceil_div(m, 128), mlp::kMaxBwdBlocks) * mlp::kMaxBwdWaves * mlp::kCbStride;
-  const int64_t rp = ceil_div(m, ws) * 6;
-  if (ray_off) *ray_off = gc;
-  if (q1_off) *q1_off = gc + ceil_div(rp, 4) * 4;
-  return gc + ceil_div(rp, 4) * 4 + 3 * m;
+  const int64_t blocks = std::min<int64_t>(ceil_div(m, 128), mlp::kMaxBwdBlocks);
+  const int64_t gc = blocks * mlp::kMaxBwdWaves * mlp::kCbStride;
+  const int64_t rows = blocks * mlp::kCbStride;
+  const int64_t rp = ceil_div(ceil_div(m, ws) * 6, 4) * 4;
+  if (rows_off) *rows_off = gc;
+  if (ray_off) *ray_off = gc + rows;
+  if (q1_off) *q1_off = gc + rows + rp;
+  return gc + rows + rp + 3 * m;
 }
 
 extern "C" int64_t cn_field_backward_fused_workspace_floats(int fmt_t, int64_t n_rays, int64_t n_samples) {
   if (!(fmt_t == CN_FMT_BF16X3_T || fmt_t == CN_FMT_F32_W16_T) || n_rays <= 0 || n_samples <= 0) return -1;
-  return fused_ws_layout(fmt_t, n_rays * n_samples, nullptr, nullptr);
+  return fused_ws_layout(fmt_t, n_rays * n_samples, nullptr, nullptr, nullptr);
 }
 
 extern "C" int cn_field_backward_fused_ws(int fmt_t, const float* packed_t, const uint32_t* masks,
@@ -3140,23 +3158,24 @@ extern "C" int cn_field_backward_fused_ws(int fmt_t, const float* packed_t, cons
   // the deterministic form needs one code row (g_code: one row per workgroup) and every wave inside
   // one ray (the ray rows); otherwise the float-atomic kernel
   const bool det = workspace && n_codes == 1 && n_samples % wave_samples == 0;
+  int64_t ray_off = 0, q1_off = 0, rows_off = 0;
   if (det) {
-    int64_t ray_off = 0, q1_off = 0;
-    fused_ws_layout(fmt_t, a.m, &ray_off, &q1_off);
+    fused_ws_layout(fmt_t, a.m, &ray_off, &q1_off, &rows_off);
     a.gc_part = workspace;
     a.ray_part = mode == mlp::kFromRayZ && (d_ro || d_rd) ? workspace + ray_off : nullptr;
     a.q1_part = d_rd ? workspace + q1_off : nullptr;
   }
   CN_TRY(x3 ? mlp::launch_field_x3_bwd(mode, a, st) : mlp::launch_field_w16_bwd(mode, a, st));
   if (!det) return CN_OK;
-  // g_code += the waves' rows, in (workgroup, wave) order (the dW GEMMs' fixed-order reduction)
-  CN_TRY(reduce(nullptr, a.gc_part, a.n_blocks * (x3 ? 4 : 8), 1, mlp::kCbStride, g_code, mlp::kCbStride, st));
-  if (a.ray_part || a.q1_part) {
-    hipLaunchKernelGGL(grad::ray_grad_reduce_kernel, dim3(static_cast<unsigned>(ceil_div(n_rays, 4))), dim3(256), 0,
-                       st, a.ray_part, a.q1_part, n_rays, n_samples, chunk_rows, wave_samples, d_ro, d_rd);
-    CN_TRY(launch_status());
-  }
-  return CN_OK;
+  // one launch: the rays' sums, and each workgroup's wave rows added in wave order (gc_rows); then
+  // g_code += those rows in block order (the dW GEMMs' fixed-order reduction)
+  float* gc_rows = workspace + rows_off;
+  const int64_t ray_blocks = a.ray_part || a.q1_part ? ceil_div(n_rays, 4) : 0;
+  hipLaunchKernelGGL(grad::ray_grad_reduce_kernel, dim3(static_cast<unsigned>(ray_blocks + a.n_blocks)), dim3(256), 0,
+                     st, a.ray_part, a.q1_part, ray_blocks ? n_rays : 0, n_samples, chunk_rows, wave_samples, d_ro,
+                     d_rd, a.gc_part, x3 ? 4 : 8, gc_rows);
+  CN_TRY(launch_status());
+  return reduce(nullptr, gc_rows, a.n_blocks, 1, mlp::kCbStride, g_code, mlp::kCbStride, st);
 }
 
 extern "C" int64_t cn_field_backward_train_workspace_floats(int64_t m) {
