@@ -82,6 +82,26 @@ def test_backward_workspace_layout(lib_path):
     assert lib.cn_field_backward_dx_offset(0) == -1
 
 
+def test_deterministic_eval_backward_workspace(lib_path):
+    """cn_field_backward_fused_workspace_floats: the deterministic eval backward's partials -- up to 8 wave
+    rows of 520 g_code floats per workgroup (one per 128-sample tile, at most 512), the workgroups'
+    rows, 6 floats per wave of 16 (fp32) / 32 (3xbf16) samples, 3 per sample -- and -1 for bad
+    arguments; the ws entry refuses the arguments cn_field_backward_fused refuses, before any launch."""
+    from codenerf import _lib
+    lib = _lib.load(lib_path)
+    up4 = lambda n: (n + 3) // 4 * 4
+    for fmt_t, ws in ((_lib.CN_FMT_F32_W16_T, 16), (_lib.CN_FMT_BF16X3_T, 32)):
+        for n_rays, s in ((1, 32), (2048, 64), (2048, 128), (37, 64), (100000, 64)):
+            m = n_rays * s
+            blocks = min((m + 127) // 128, 512)
+            want = blocks * 8 * 520 + blocks * 520 + up4((m + ws - 1) // ws * 6) + 3 * m
+            assert lib.cn_field_backward_fused_workspace_floats(fmt_t, n_rays, s) == want, (fmt_t, n_rays, s)
+        assert lib.cn_field_backward_fused_workspace_floats(fmt_t, 0, 64) == -1
+    assert lib.cn_field_backward_fused_workspace_floats(_lib.CN_FMT_F32_W16, 16, 64) == -1   # not a transposed pack
+    args = [_lib.CN_FMT_F32_W16_T] + [None] * 7 + [1, 64, 1, None, 1, None, None, None, None, None, None, None, None]
+    assert lib.cn_field_backward_fused_ws(*args) == _lib.CN_EINVAL
+
+
 def test_library_built_from_this_tree(lib_path):
     """cn_version() carries the hash of the sources it was compiled from (codenerf/provenance.py)."""
     from codenerf import _lib, provenance
