@@ -327,6 +327,7 @@ def run(args):
                                        "field_launch_ms_avg": sum(f4) / max(1, len(f4))}
         if args.eval_iters > 0:
             result["eval_c5"] = {p: eval_bench(dev, rs, emb, models, args.eval_iters, p) for p in ("f32", "bf16x3")}
+            result["eval_c5_chairs"] = eval_bench(dev, rs, emb, models, args.eval_iters, "f32", shape="chairs")
             # the HIP-graph form at N = 1 only: C5 is a per-replica loop, and a capture beside a live
             # RCCL communicator (its watchdog thread queries events) is a risk the scaling lines need not take
             if world == 1:
@@ -339,6 +340,9 @@ def run(args):
         if args.train_iters > 0:
             result["train_c3"] = train_bench(dev, k, args.train_iters, world, "f32")
             result["train_c3"]["bf16x3"] = train_bench(dev, k, args.train_iters, world, "bf16x3")
+            # the reference's own runnable training configurations, fp32
+            result["train_cars_code"] = train_bench(dev, k, args.train_iters, world, "f32", shape="cars_code")
+            result["train_3080"] = train_bench(dev, k, 4 * args.train_iters, world, "f32", shape="3080")
 
     if world > 1 and rank == 0 and psnr_img[args.precision] is not None:
         result.update(multi_rank_check(psnr_img[args.precision], rs, poses[:1], per, zs, zt, ps, emb, models))
@@ -406,7 +410,13 @@ def traffic_source(prec):
             "per-sample bytes x this launch's samples; profiles/field_kernel_traffic.json")
 
 
-def eval_bench(dev, rs, emb, models, iters, precision, graph=False, sharded=False):
+# The eval shapes: C5 (srn-cars-code-3080-val.yml:47-52, BASELINE config 5) and the chairs eval of
+# srn-chairs-code.yml:47-54 (4096 rays, 32 + 128, near 1.25 / far 2.75).
+EVAL_SHAPES = {"c5": dict(rays=2048, nc=64, nf=64, near=NEAR, far=FAR, rho=1.3),
+               "chairs": dict(rays=4096, nc=32, nf=128, near=1.25, far=2.75, rho=2.0)}
+
+
+def eval_bench(dev, rs, emb, models, iters, precision, graph=False, sharded=False, shape="c5"):
     """C5 (srn-cars-code-3080-val.yml): one eval.py:141-167 iteration = 2048 random rays, 64+64
     perturbed samples, forward + backward through the HIP kernels into (codes, theta, phi, rho),
     AdamW step.  Weights frozen (their grads are never read by the reference's optimiser).
@@ -418,8 +428,10 @@ def eval_bench(dev, rs, emb, models, iters, precision, graph=False, sharded=Fals
     from codenerf.evaluate import GraphedEvalStep, eval_step_loss, step_psnr_tensor
     from codenerf.nerf import PointSampler
     from codenerf.optim import AdamW
-    ps = PointSampler(NC, NF, NEAR, FAR, "lindepth", True, torch.float32, dev)
-    rs.sample_size = 2048
+    sh = EVAL_SHAPES[shape]
+    n_rays = sh["rays"]
+    ps = PointSampler(sh["nc"], sh["nf"], sh["near"], sh["far"], "lindepth", True, torch.float32, dev)
+    rs.sample_size = n_rays
     target = torch.rand(H * W, 4, generator=torch.Generator().manual_seed(3)).to(dev)
     mods = {"nerf_coarse": models[0], "nerf_fine": models[1]}
     saved = [(m, m.precision) for m in models]
@@ -430,7 +442,7 @@ def eval_bench(dev, rs, emb, models, iters, precision, graph=False, sharded=Fals
     zt = (torch.randn(1, 256, generator=torch.Generator().manual_seed(5)) * 0.3).to(dev).requires_grad_(True)
     th = torch.tensor([1.57], device=dev).requires_grad_(True)
     ph = torch.tensor([0.0], device=dev).requires_grad_(True)
-    rh = torch.tensor([1.3], device=dev).requires_grad_(True)
+    rh = torch.tensor([sh["rho"]], device=dev).requires_grad_(True)
     # test_time_optimize's optimiser for val_type AdamW: the flat one-launch AdamW
     opt = AdamW([{"params": [zs, zt]}, {"params": [th, ph]}, {"params": [rh]}], lr=1e-2)
     np.random.seed(0)
@@ -484,32 +496,43 @@ def eval_bench(dev, rs, emb, models, iters, precision, graph=False, sharded=Fals
         note += "; forward + backward + AdamW replayed as one captured HIP graph (GraphedEvalStep)"
     # the MLP work of one iteration: forward + dX (2 x 572,416 FLOP; frozen weights, no dW) per sample
     # evaluation, 64 coarse + 128 merged fine samples per ray, as train_bench's accounting
-    flop_iter = 2.0 * FLOP_PER_SAMPLE * 2048 * (64 + 128)
+    flop_iter = 2.0 * FLOP_PER_SAMPLE * n_rays * (2 * sh["nc"] + sh["nf"])
     tflops = flop_iter / dt / 1e12
     peak = PEAK_FP32_MFMA_TFLOPS if precision == "f32" else PEAK_BF16_MFMA_TFLOPS / 3.0
     extra = {"mlp_tflop_per_iter": flop_iter / 1e12, "achieved_tflops": tflops, "frac_of_peak": tflops / peak}
     if sharded:
         world = dist.get_world_size()
-        note += (f"; ray-sharded over {world} ranks (one optimisation; 2048 / {world} rays per rank and iteration, "
+        note += (f"; ray-sharded over {world} ranks (one optimisation; {n_rays} / {world} rays per rank and iteration, "
                  "one all-reduce of the 515 code / pose gradient floats; each share is its own Q1 chunk, so this "
                  "mode is reported beside the reference's per-rank optimisation, Q6)")
-        extra.update(scaling="strong", n_ranks=world, rays_per_rank_per_iter=2048 // world,
+        extra.update(scaling="strong", n_ranks=world, rays_per_rank_per_iter=n_rays // world,
                      frac_of_peak=tflops / (peak * world))
-    return {"ms_per_iter": dt * 1e3, "rays_per_s": 2048 / dt, "rays_per_iter": 2048, "samples": "64+64 perturbed",
+    return {"ms_per_iter": dt * 1e3, "rays_per_s": n_rays / dt, "rays_per_iter": n_rays,
+            "samples": f"{sh['nc']}+{sh['nf']} perturbed", "near_far": [sh["near"], sh["far"]],
             "dtype": precision, **extra,
             "note": note + "; fused pose path + loss; host-side numpy ray permutation included; eval.py's "
                            "per-iteration psnr formed on the device"}
 
 
-def train_bench(dev, k, iters, world, precision=None):
-    """C3 training (srn-cars-code.yml; train.py:64-114): one iteration = 4 images x 4096 random rays,
-    chunk 4096 -> 4 optimiser steps, each 64+64 perturbed samples per ray with per-object codes from a
-    2458-object table, fwd + bwd into both MLPs and both code tables, flat AdamW (one launch), LambdaLR,
-    and with N ranks one RCCL all-reduce of the flat gradient per step (DDP's average)."""
+# The training shapes: C3 (BASELINE config 3: srn-cars-code.yml with 64 + 64), and the reference's own
+# runnable configurations srn-cars-code.yml:18,45-48,63 (4 images x 4096 rays, 32 + 128, chunk 4096) and
+# srn-cars-code-3080.yml:18,45-48,62 (1 image x 4096 rays, 64 + 128, chunk 1024).
+TRAIN_SHAPES = {"c3": dict(batch=4, nc=64, nf=64, chunk=4096),
+                "cars_code": dict(batch=4, nc=32, nf=128, chunk=4096),
+                "3080": dict(batch=1, nc=64, nf=128, chunk=1024)}
+
+
+def train_bench(dev, k, iters, world, precision=None, shape="c3"):
+    """Training (train.py:64-114) at one of TRAIN_SHAPES: one iteration = batch images x 4096 random
+    rays, cut into chunks -> one optimiser step per chunk, each Nc + Nf perturbed samples per ray with
+    per-object codes from a 2458-object table, fwd + bwd into both MLPs and both code tables, flat AdamW
+    (one launch), LambdaLR, and with N ranks one RCCL all-reduce of the flat gradient per step (DDP's
+    average)."""
     import numpy as np
     from types import SimpleNamespace as NS
     from codenerf import nerf as N, train as T
-    n_objects, batch = 2458, 4
+    sh = TRAIN_SHAPES[shape]
+    n_objects, batch = 2458, sh["batch"]
     cfg = NS(is_distributed=world > 1,
              models=NS(embedding=NS(shape_code_size=256, texture_code_size=256), nerf_coarse=NS(hidden_size=256),
                        nerf_fine=NS(hidden_size=256)),
@@ -517,9 +540,9 @@ def train_bench(dev, k, iters, world, precision=None):
                                  num_encoding_fn_dir=4, include_input_dir=True, log_sampling_dir=True,
                                  use_viewdirs=True),
                      ray_sampler=NS(num_random_rays=4096),
-                     point_sampler=NS(num_coarse=NC, num_fine=NF, near_limit=NEAR, far_limit=FAR,
+                     point_sampler=NS(num_coarse=sh["nc"], num_fine=sh["nf"], near_limit=NEAR, far_limit=FAR,
                                       spacing_mode="lindepth", perturb=True),
-                     train=NS(chunksize=4096)),
+                     train=NS(chunksize=sh["chunk"])),
              optimizer=NS(type="AdamW", lr=1e-4, embedding_lr=1e-3, scheduler_gamma=0.1,
                           scheduler_step_size=5000000),
              experiment=NS(regularizer_lambda=1e-5))
@@ -574,12 +597,17 @@ def train_bench(dev, k, iters, world, precision=None):
     # the MLP work of one iteration per rank: forward + dX + dW (3 x 572,416 FLOP) per sample evaluation,
     # (64 coarse + 128 merged fine) samples per ray; against the dense MFMA peak of the precision's pipe
     # (3xbf16: three bf16 products per fp32 one, so its figure is in fp32-equivalent TFLOP/s)
-    flop_iter = 3.0 * FLOP_PER_SAMPLE * batch * 4096 * (64 + 128)
+    flop_iter = 3.0 * FLOP_PER_SAMPLE * batch * 4096 * (2 * sh["nc"] + sh["nf"])
     tflops = flop_iter / (dt / iters) / 1e12
     peak = PEAK_FP32_MFMA_TFLOPS if precision == "f32" else PEAK_BF16_MFMA_TFLOPS / 3.0
+    steps = batch * 4096 // sh["chunk"]
     return {"ms_per_iter": dt / iters * 1e3, "rays_per_s": rays / dt, "rays_per_iter_per_rank": batch * 4096,
             "mlp_tflop_per_iter": flop_iter / 1e12, "achieved_tflops": tflops, "frac_of_peak": tflops / peak,
-            "optimizer_steps_per_iter": batch, "samples": "64+64 perturbed", "objects": n_objects,
+            "optimizer_steps_per_iter": steps, "chunk": sh["chunk"],
+            "samples": f"{sh['nc']}+{sh['nf']} perturbed ({2 * sh['nc'] + sh['nf']} field samples per ray)",
+            "tiles_per_cu": {"coarse": sh["chunk"] * sh["nc"] // 128 / 256,
+                             "fine": sh["chunk"] * (sh["nc"] + sh["nf"]) // 128 / 256},
+            "objects": n_objects,
             "params": n_params, "loss": float(logs[-1]["total_loss"]), "dtype": precision,
             "adamw": {"kernel_ms": adamw_ms, "bytes": 28 * n_params,
                       "gbps": 28 * n_params / (adamw_ms * 1e-3) / 1e9},
@@ -636,6 +664,10 @@ def cpu_baseline(k, pose1):
     pc, pf = synthetic.codenerf_params(0), synthetic.codenerf_params(1)
     c2, ref = [], None
     with torch.no_grad():
+        # one untimed warm-up chunk (thread pool start, page-in of the weights, the host's clock ramp):
+        # the r05 line's first timed image was 52 % slower than its last without it
+        O.render_image(ro[:CHUNK], rd[:CHUNK], zs[:CHUNK], zt[:CHUNK], O.Sampling(NC, NF, NEAR, FAR), O.EmbedCfg(),
+                       pc, pf, CHUNK, coarse_only=True)
         for _ in range(3):
             t0 = time.perf_counter()
             out = O.render_image(ro, rd, zs, zt, O.Sampling(NC, NF, NEAR, FAR), O.EmbedCfg(), pc, pf, CHUNK,
@@ -649,10 +681,15 @@ def cpu_baseline(k, pose1):
                            pc, pf, CHUNK)
             c3.append(time.perf_counter() - t0)
     m2, m3 = sorted(c2)[1], sorted(c3)[1]
+
+    def spread(ts, rays):
+        return {"min": rays / max(ts), "median": rays / sorted(ts)[1], "max": rays / min(ts),
+                "spread": (max(ts) - min(ts)) / sorted(ts)[1]}
     return ({"value": nr / m2, "unit": "rays/s", "cores": threads, "kind": "port",
-             "sample": f"C2: median of 3 full 128x128 images (16384 rays x 64 coarse samples, chunk 4096): "
-                       f"{', '.join(f'{t:.2f}' for t in c2)} s",
-             "hierarchical_64_64": {"value": CHUNK / m3, "unit": "rays/s",
+             "sample": f"C2: median of 3 full 128x128 images (16384 rays x 64 coarse samples, chunk 4096) after "
+                       f"one untimed warm-up chunk: {', '.join(f'{t:.2f}' for t in c2)} s",
+             "rays_per_s": spread(c2, nr),
+             "hierarchical_64_64": {"value": CHUNK / m3, "unit": "rays/s", "rays_per_s": spread(c3, CHUNK),
                                     "sample": f"C3: median of 3 renders of one 4096-ray chunk at 64+64: "
                                               f"{', '.join(f'{t:.2f}' for t in c3)} s"},
              "host": host_cpu(), "host_cores": share}, ref)

@@ -149,6 +149,24 @@ class RaySink:
         self.buf = None
 
 
+_RAY_SINKS = [False]
+
+
+class eval_ray_sinks:
+    """Context in which pose_rays_autograd attaches a RaySink to the rays of leaf (theta, phi, rho):
+    the eval step (evaluate.eval_step_loss) only.  Outside it the rays' consumers return their
+    gradients through autograd as usual, so torch.autograd.grad / hooks on the rays see them."""
+
+    def __enter__(self):
+        self.prev = _RAY_SINKS[0]
+        _RAY_SINKS[0] = True
+        return self
+
+    def __exit__(self, *exc):
+        _RAY_SINKS[0] = self.prev
+        return False
+
+
 def _ray_sink(rd, ro=None):
     s = getattr(rd, "_cn_ray_sink", None)
     if s is None or (ro is not None and getattr(ro, "_cn_ray_sink", None) is not s):
@@ -595,11 +613,11 @@ def pose_rays_autograd(dirs, theta=None, phi=None, rho=None, c2w=None, sel=None,
     tgt = None if target is None else target.detach()
     if not _needs_grad(theta, phi, rho, c2w):
         return ops.pose_rays(dirs, _d(theta), _d(phi), _d(rho), c2w=_d(c2w), select_inds=sel, target=tgt)
-    # the eval step (pose leaves optimised by eval.py:145-167): the rays' consumers sum their gradients in
-    # place (RaySink; torch.autograd.grad w.r.t. these rays themselves then sees none -- w.r.t. the pose
-    # leaves it is exact)
+    # the eval step (pose leaves optimised by eval.py:145-167, inside eval_ray_sinks()): the rays' consumers
+    # sum their gradients in place (RaySink; torch.autograd.grad w.r.t. these rays themselves then sees
+    # none -- w.r.t. the pose leaves it is exact).  Elsewhere the rays' gradients flow through autograd.
     leaves = theta is not None and all(t is not None and t.is_leaf and t.requires_grad for t in (theta, phi, rho))
-    sink = RaySink() if leaves else None
+    sink = RaySink() if (leaves and _RAY_SINKS[0]) else None
     ro, rd, c2w_out, tgt_out = PoseRays.apply(dirs.detach(), theta, phi, rho, c2w, sel, tgt, sink)
     if sink is not None:
         ro._cn_ray_sink = rd._cn_ray_sink = sink

@@ -54,8 +54,11 @@ def eval_step_loss(theta, phi, rho, shape_code, texture_code, target_pixels, sam
     the ranks' losses sum to the whole iteration's.  logs: device tensors (read back only when
     logged; the per-share means when sharded); eval.py:159's per-iteration psnr is read back by the
     caller once the backward and the optimiser step are enqueued (``step_psnr``)."""
+    from .autograd import eval_ray_sinks
     ray_sampler, point_sampler = samplers
-    ro, rd, select_inds, cam_pose, tp = ray_sampler.sample_spherical(theta, phi, rho, target=target_pixels, sel=sel)
+    with eval_ray_sinks():            # the rays' gradients summed in place (autograd.RaySink)
+        ro, rd, select_inds, cam_pose, tp = ray_sampler.sample_spherical(theta, phi, rho, target=target_pixels,
+                                                                         sel=sel)
     n = ro.shape[0]
     # the code rows, with their gradient summed in place (code_rows_with_sink), expanded over the rays
     from .models.model import CodeRows, code_rows_with_sink
@@ -157,6 +160,9 @@ def _allreduce_sum(optimizer, params, group) -> None:
     if isinstance(optimizer, AdamW):
         optimizer.allreduce_grads(group, average=False)
         return
+    for p in params:              # a parameter without a gradient on this rank reduces zeros
+        if p.grad is None:
+            p.grad = torch.zeros_like(p)
     grads = [p.grad for p in params]
     flat = torch.cat([g.reshape(-1) for g in grads])
     dist.all_reduce(flat, group=group)

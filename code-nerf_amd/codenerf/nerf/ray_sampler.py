@@ -93,7 +93,9 @@ class RaySampler(object):
         ``sel``: (B, S') device indices drawn by the caller (a captured eval step, whose host draw
         happens outside the graph; S' = sample_size, or a rank's share of them in the ray-sharded
         eval step); else drawn here.
-        -> ro, rd (B*S, 3), select_inds, cam_pose (B, 4, 4) (no grad), target rows (B*S, C) | None."""
+        -> ro, rd (B*S, 3), select_inds, cam_pose (B, 4, 4) (no grad), target rows (B*S, C) | None.
+        Inside evaluate.eval_step_loss (autograd.eval_ray_sinks) the rays' consumers add their gradients
+        in place and return none for ro / rd; elsewhere the rays' gradients flow through autograd."""
         from ..autograd import pose_rays_autograd
         batch = theta.numel()
         if sel is None:

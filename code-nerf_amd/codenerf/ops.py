@@ -569,6 +569,13 @@ def field_backward_train(packed_t: Tensor, params: Sequence[Tensor], masks: Tens
     params = [_cuda(p.detach(), f"param{i}") for i, p in enumerate(params)]
     d_raw = _aligned16(_cuda(d_raw, "d_raw"))
     assert d_raw.numel() == 4 * m and saved.shape == (5, m, 256) and (x_enc is None or x_enc.shape == (m, 90))
+    if m and precision != "bf16x3" and x_enc is None:
+        # the fp32 backward reads the forward's encoding plane at saved + 5 M 256 (cn_field_backward_train_fmt):
+        # ``saved`` must be radiance_field_train_w16's view of its whole save buffer, not a copy of the planes
+        need = 4 * int(lib.cn_field_train_saved_floats(_lib.CN_FMT_F32_W16, m))
+        assert saved.is_contiguous() and saved.storage_offset() == 0 and \
+            saved.untyped_storage().nbytes() >= need, \
+            "field_backward_train: saved must be the training forward's own buffer (planes + encoding plane)"
     dev = d_raw.device
     rd, pts, ro, z = _opt(rd, "rd"), _opt(pts, "pts"), _opt(ro, "ro"), _opt(z, "z")
     if code_index is not None:

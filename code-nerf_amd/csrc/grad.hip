@@ -13,7 +13,6 @@
 
 #include "cn_common.h"
 #include "mlp_common.h"
-#include "cn_instrument.h"
 
 namespace cn {
 namespace grad {
@@ -445,11 +444,6 @@ struct DirFold {
   float* gsum;                             // (workgroups + n_rays / 16) slots of 16 x 256
 };
 
-#ifdef CN_PROBE_TN_WAITPROF
-// experiment: per (workgroup, wave): shader clocks at the stage barrier, in the DMA issue, in the
-// whole loop, and the stage count (read by cn_debug_tnprof)
-__device__ long long g_tnprof[1024][8][4];
-#endif
 
 template <bool X3, bool SIG, bool DIRS>
 __device__ __forceinline__ void tn256_body(float* ring, const float* __restrict__ A, const float* __restrict__ B,
@@ -527,10 +521,6 @@ __device__ __forceinline__ void tn256_body(float* ring, const float* __restrict_
 #pragma unroll
     for (int u = 0; u < 4; ++u) acc[t][u] = floatx16{0};
   float bsum[2] = {0.0f, 0.0f};
-#ifdef CN_PROBE_TN_WAITPROF
-  long long prof_bar = 0, prof_dma = 0;
-  const long long prof_t0 = clock64();
-#endif
   // DIRS: per-direction column sums of the current unit run, rows 2 p + h of columns n0 + 32 t + i
   // (both waves of a pair sum both column blocks -- a select by wave would become an indexed
   // private array, which the compiler moves to LDS -- and wave 2 q + t stores block t); flushed:
@@ -552,9 +542,6 @@ __device__ __forceinline__ void tn256_body(float* ring, const float* __restrict_
     // vector-memory ops as well.  Waiting for st+1 here (it was issued two stages ago) is what lets
     // the last row pair prefetch from it.
     static_assert(kTwRows / 4 == 4, "the vmcnt below counts stage st+2");
-#ifdef CN_PROBE_TN_WAITPROF
-    const long long tp0 = clock64();
-#endif
     // lgkmcnt(0) as the compiler's own wait (it does not read the asm's): the next stage's first
     // operands, read during the last pair, have landed, so nothing is owed at the loop header and the
     // first MFMAs start at once
@@ -563,16 +550,8 @@ __device__ __forceinline__ void tn256_body(float* ring, const float* __restrict_
     else if (DIRS && flushed) asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-#ifdef CN_PROBE_TN_WAITPROF
-    const long long tp1 = clock64();
-    prof_bar += tp1 - tp0;
-#endif
     if constexpr (X3) {
       dma(st + 3);
-#ifdef CN_PROBE_TN_WAITPROF
-      __builtin_amdgcn_sched_barrier(0);
-      prof_dma += clock64() - tp1;
-#endif
       x3_stage<SIG>(ring + (st & (kTwRing - 1)) * kTwStage, i, h, n0, k0, acc, bsum, sacc, sig_wave);
       continue;
     }
@@ -623,14 +602,7 @@ __device__ __forceinline__ void tn256_body(float* ring, const float* __restrict_
       }
       if (p == 0) {
         __builtin_amdgcn_sched_barrier(0);
-#ifdef CN_PROBE_TN_WAITPROF
-        const long long td0 = clock64();
-#endif
         dma(st + 3);  // beside the first pair's MFMAs
-#ifdef CN_PROBE_TN_WAITPROF
-        __builtin_amdgcn_sched_barrier(0);
-        prof_dma += clock64() - td0;
-#endif
         __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -651,14 +623,6 @@ __device__ __forceinline__ void tn256_body(float* ring, const float* __restrict_
   }
   // the prefetched stages past the slab must land before the workgroup's LDS is released
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#ifdef CN_PROBE_TN_WAITPROF
-  if (lane == 0 && blk < 1024) {
-    g_tnprof[blk][wave][0] = prof_bar;
-    g_tnprof[blk][wave][1] = prof_dma;
-    g_tnprof[blk][wave][2] = clock64() - prof_t0;
-    g_tnprof[blk][wave][3] = n_stages;
-  }
-#endif
   float* pt = part ? part + (int64_t)blk * 65536 : nullptr;
 #pragma unroll
   for (int t = 0; t < 2; ++t)
@@ -2791,12 +2755,6 @@ extern "C" int cn_code_bias_backward(const float* const* params, const float* z_
   return launch_status();
 }
 
-#ifdef CN_PROBE_TN_WAITPROF
-extern "C" int cn_debug_tnprof(long long* out, int n_blocks) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(cn::grad::g_tnprof), sizeof(long long) * 32 * std::min(n_blocks, 1024)) ==
-                 hipSuccess ? 0 : -1;
-}
-#endif
 
 extern "C" int cn_code_bias_backward_act(const float* const* params, const float* z_s, const float* z_t,
                                          int64_t n_codes, const float* code_act, const float* g_code,

@@ -36,7 +36,6 @@
 #include <algorithm>
 
 #include "mlp_common.h"
-#include "cn_instrument.h"
 
 namespace cn {
 namespace mlp {
@@ -173,9 +172,6 @@ struct State {
   float sig;         // sigma partial (this lane group's 64 features)
   int lane, g, wave;
   int crow;          // this lane's code-bias row
-#ifdef CN_PROBE_PROLOGUE
-  long long prolog;  // experiment: shader clocks from a tile's start to its first chunk, summed over tiles
-#endif
   bool uniform_code; // all 16 samples of the wave use one code row
   __amdgpu_buffer_rsrc_t wsrc;
   unsigned voff;
@@ -582,9 +578,6 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
   const int64_t row = tile * kTile + s.wave * 16 + (s.lane & 15);
   const bool valid = row < a.m;
   const int64_t rc = valid ? row : a.m - 1;
-#ifdef CN_PROBE_PROLOGUE
-  const long long tp0 = clock64();
-#endif
 
   // ---- per-sample inputs, code row (ordinary loads: the in-flight DMA retires with them)
   const SampleIn in = decode_sample<MODE>(a, rc);
@@ -646,9 +639,6 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
       for (int i = 0; i < 3; ++i) fr[8 + i] = clds[kCFreq + 10 + ((4 * i + g) * 11 >> 5)];
       const LazyXyz l0{enc, s.denc, in.x, in.vd, fr, g, false};
       l0.pair<0>();
-#ifdef CN_PROBE_PROLOGUE
-      s.prolog += clock64() - tp0;
-#endif
       bias_from(s, clds + kCB1);
       chunk16<8>(s, lds, c + 0, l0);
       if constexpr (SAVE)
@@ -682,9 +672,6 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
       s.denc[6] = s.g == 0 ? in.vd[0] : (s.g == 1 ? in.vd[1] : (s.g == 2 ? in.vd[2] : 0.0f));
     }
     s.denc[7] = 0.0f;
-#ifdef CN_PROBE_PROLOGUE
-    s.prolog += clock64() - tp0;
-#endif
     bias_from(s, clds + kCB1);
     chunk16<8>(s, lds, c + 0, ArrB<0>{enc});
     if constexpr (SAVE)
@@ -820,21 +807,9 @@ __device__ __forceinline__ void field_tile(State& s, const FieldArgs& a, float4*
   }
 }
 
-#ifdef CN_PROBE_WGTIME
-// experiment: each workgroup's start / end wall clock (100 MHz), read by cn_debug_wgtime
-__device__ long long g_wgtime[2048][2];
-#endif
-#ifdef CN_PROBE_PROLOGUE
-// experiment: per (workgroup, wave) of the last fp32 field launch (forward or backward): tile
-// prologue clocks (summed), the tile loop's clocks, the tile count; read by cn_debug_prologue
-__device__ long long g_prolog[2048][8][3];
-#endif
 
 template <int MODE, bool MASKS, bool SAVE = false>
 __global__ __launch_bounds__(kThreads, 2) void field_w16_kernel(FieldArgs a) {
-#ifdef CN_PROBE_WGTIME
-  const long long t_start = wall_clock64();
-#endif
   // ONE LDS object (a second one makes hipcc wait vmcnt(0) before ring reads): the DMA
   // ring, then the constants, then one code-bias row per wave
   __shared__ __attribute__((aligned(16))) float4 lds[kLdsQuads];
@@ -860,34 +835,13 @@ __global__ __launch_bounds__(kThreads, 2) void field_w16_kernel(FieldArgs a) {
 
   const int64_t n_tiles = (a.m + kTile - 1) / kTile;
   int c = 0;
-#ifdef CN_PROBE_PROLOGUE
-  s.prolog = 0;
-  const long long tl0 = clock64();
-  int nt = 0;
-#endif
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
     c = 0;
     field_tile<MODE, MASKS, SAVE>(s, a, lds, clds, crow_lds, tile, c);
-#ifdef CN_PROBE_PROLOGUE
-    ++nt;
-#endif
   }
-#ifdef CN_PROBE_PROLOGUE
-  if (s.lane == 0 && blockIdx.x < 2048) {
-    g_prolog[blockIdx.x][s.wave][0] = s.prolog;
-    g_prolog[blockIdx.x][s.wave][1] = clock64() - tl0;
-    g_prolog[blockIdx.x][s.wave][2] = nt;
-  }
-#endif
   // the last tile prefetched chunks 0..2 of a tile that does not exist: they must land
   // before the workgroup's LDS is released
   __builtin_amdgcn_s_waitcnt(0x0F70);
-#ifdef CN_PROBE_WGTIME
-  if (threadIdx.x == 0 && blockIdx.x < 2048) {
-    g_wgtime[blockIdx.x][0] = t_start;
-    g_wgtime[blockIdx.x][1] = wall_clock64();
-  }
-#endif
 }
 
 
@@ -1270,9 +1224,6 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   const float* clds = reinterpret_cast<const float*>(lds + kRing * kChunkQuads);
 
   // ---- inputs: sample, d raw, masks of v2 and v1, code row (wave-uniform: host-checked)
-#ifdef CN_PROBE_PROLOGUE
-  const long long tp0 = clock64();
-#endif
   const SampleIn in = decode_sample<MODE>(a, rc);
   const int crow = __builtin_amdgcn_readfirstlane(static_cast<int>(code_row(a, in.code_of)));
   float4 dr = reinterpret_cast<const float4*>(a.d_raw)[rc];
@@ -1299,9 +1250,6 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   int c = NOGEO ? crun : 0;
   s.cbase = c;
   // ---- fc_rgb^T (chunk 0): B = d rgb channel g at k-step 0
-#ifdef CN_PROBE_PROLOGUE
-  s.prolog += clock64() - tp0;
-#endif
   zero_acc(s);
   {
     const float b = s.g == 0 ? dr.x : (s.g == 1 ? dr.y : (s.g == 2 ? dr.z : 0.0f));
@@ -1509,29 +1457,14 @@ __global__ __launch_bounds__(kThreads, 2) void field_w16_bwd_kernel(FieldArgs a)
   read_a<0>(lds + s.lane, s.pre);
   int cur_code = -1;
   const int64_t n_tiles = (a.m + kTile - 1) / kTile;
-#ifdef CN_PROBE_PROLOGUE
-  s.prolog = 0;
-  const long long tl0 = clock64();
-  int nt = 0;
-#endif
   int crun = 0;
   int64_t prev = -1;
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
     bwd_tile<MODE, TRAIN, NOGEO, DET>(s, a, lds, grow, tile, cur_code, crun, prev);
-#ifdef CN_PROBE_PROLOGUE
-    ++nt;
-#endif
   }
   if constexpr (NOGEO) {
     if (prev >= 0) store_plane<0, 16>(s, plane_rsrc(a.dpre, 4, a.m, prev), s.act);
   }
-#ifdef CN_PROBE_PROLOGUE
-  if (s.lane == 0 && blockIdx.x < 2048) {
-    g_prolog[blockIdx.x][s.wave][0] = s.prolog;
-    g_prolog[blockIdx.x][s.wave][1] = clock64() - tl0;
-    g_prolog[blockIdx.x][s.wave][2] = nt;
-  }
-#endif
   __builtin_amdgcn_s_waitcnt(0x0F70);
   if constexpr (DET) {
     // deterministic form (one code row, host-checked): this wave's g_code row into its gc_part row
@@ -1666,17 +1599,3 @@ int launch_field_w16_bwd(int mode, FieldArgs& a, hipStream_t st) {
 }  // namespace mlp
 }  // namespace cn
 
-#ifdef CN_PROBE_PROLOGUE
-// experiment: copy g_prolog of the last fp32 field launch (n workgroups x 8 waves x 3)
-extern "C" int cn_debug_prologue(long long* out, int n) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(cn::mlp::w16::g_prolog), sizeof(long long) * 24 * std::min(n, 2048)) ==
-                 hipSuccess ? 0 : -1;
-}
-#endif
-#ifdef CN_PROBE_WGTIME
-// experiment: copy the last field_w16_kernel launch's per-workgroup (start, end) wall clocks
-extern "C" int cn_debug_wgtime(long long* out, int n) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(cn::mlp::w16::g_wgtime), sizeof(long long) * 2 * std::min(n, 2048)) ==
-                 hipSuccess ? 0 : -1;
-}
-#endif

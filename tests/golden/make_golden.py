@@ -89,7 +89,7 @@ def main(only=None):
     torch.set_num_threads(8)
     if only:
         for name in only:
-            {**ROUND2, **ROUND3}[name](nerf, model_mod, ev)
+            {**ROUND2, **ROUND3, **ROUND6}[name](nerf, model_mod, ev)
         return
     pose = lambda th, ph, rh: ev.pose_spherical(torch.tensor([th]), torch.tensor([ph]), torch.tensor([rh]))  # noqa: E731
 
@@ -270,7 +270,7 @@ def main(only=None):
          g_fine_fc_rgb_w=models["nerf_fine"].fc_rgb.weight.grad, g_coarse_fc_out_b=models["nerf_coarse"].fc_out.bias.grad,
          **pw)
     print("split(1024,3) =", util.get_minibatches(torch.arange(10), 4))
-    for fn in list(ROUND2.values()) + list(ROUND3.values()):
+    for fn in list(ROUND2.values()) + list(ROUND3.values()) + list(ROUND6.values()):
         fn(nerf, model_mod, ev)
 
 
@@ -622,6 +622,140 @@ def gen_c3train(nerf, model_mod, ev):
 
 C3_PROJ = 16
 
+# The reference's runnable training shapes (round 6): one chunk step each, like gen_c3train but with
+# ONE object per chunk (train_batch_size images of num_random_rays each, chunk <= num_random_rays: a
+# chunk is always a slice of one image).  (config file, Nc, Nf, near, far, rays drawn per image, chunk,
+# object id, pose).  Stored like train_c3.npz minus the full nerf_fine tensors (size): C3_FULL in full,
+# 16 projections of every tensor's gradient and post-step change, the touched code rows.
+TRAIN_SHAPES = {
+    "train_cars_code": ("config/srn-cars-code.yml:45-48,63", 32, 128, 0.8, 1.8, 4096, 4096, 611, (0.7, -0.4, 1.3)),
+    "train_3080": ("config/srn-cars-code-3080.yml:45-48,62", 64, 128, 0.8, 1.8, 4096, 1024, 2001, (0.9, 1.1, 1.3)),
+}
+
+
+def gen_train_shape(nerf, model_mod, ev, name):
+    """train.py:76-114 at one of TRAIN_SHAPES: ray_sampler.sample of one view (num_random_rays), the
+    target gather, get_minibatches' FIRST chunk, then the chunk step (embedding lookup,
+    predict_radiance_and_render with perturbed samples -- draws re-made by the tests from
+    torch.manual_seed(4343): t_rand (chunk, Nc) then u (chunk, Nf) -- losses, zero_grad, backward, AdamW +
+    LambdaLR).  Weights: codenerf.synthetic seeds 0 / 1; tables synthetic.latent_codes(40 / 41, 2458)."""
+    util = importlib.import_module("view_synthesis.utils.util")
+    _src, nc, nf, near, far, n_rays, chunk, oid_v, cam = TRAIN_SHAPES[name]
+    K = synthetic.srn_intrinsics(128)
+    rs = nerf.RaySampler(128, 128, K, sample_size=n_rays, device="cpu", datatype=torch.float32)
+    ps = nerf.PointSampler(nc, nf, near, far, spacing_mode="lindepth", perturb=True, dtype=torch.float32,
+                           device="cpu")
+    emb = _embedders(nerf)
+    models = {"nerf_coarse": make_model(model_mod, 0).train(), "nerf_fine": make_model(model_mod, 1).train()}
+    table = model_mod.ShapeTextureEmbedding(C3_OBJECTS, 256, 256)
+    with torch.no_grad():
+        table.shape_embedding.weight.copy_(synthetic.latent_codes(40, C3_OBJECTS))
+        table.texture_embedding.weight.copy_(synthetic.latent_codes(41, C3_OBJECTS))
+    models["embedding"] = table
+    cfg = Cfg(optimizer=Cfg(type="AdamW", lr=1e-4, embedding_lr=1e-3, scheduler_gamma=0.1,
+                            scheduler_step_size=5000000))
+    optimizer, scheduler = util.prepare_optimizer(cfg, models)
+    g = torch.Generator().manual_seed(62)
+    colors = torch.rand(1, 128, 128, 4, generator=g)
+    poses = _pose(ev, *cam)[None]
+    np.random.seed(30)
+    ro_b, rd_b, sel = rs.sample(tform_cam2world=poses)                    # train.py:76
+    tgt_b = colors.flatten(1, 2)[0, sel[0], :]                            # train.py:77-80
+    ro, rd, tgt = util.get_minibatches(ro_b, chunk)[0], util.get_minibatches(rd_b, chunk)[0], \
+        util.get_minibatches(tgt_b, chunk)[0]                             # train.py:84-85
+    oid = torch.full((chunk,), oid_v, dtype=torch.int64)
+    before = {f"{k}.{n}": p.detach().clone() for k, m in models.items() for n, p in m.named_parameters()}
+    torch.manual_seed(4343)
+    rgb_c, rgb_f = nerf.predict_radiance_and_render((ro, rd), ps, emb, models["nerf_coarse"], models["nerf_fine"],
+                                                    models["embedding"](oid))
+    torch.manual_seed(4343)
+    t_rand, u = torch.rand(chunk, nc), torch.rand(chunk, nf)
+    lc = torch.nn.functional.mse_loss(rgb_c[..., :3], tgt[..., :3])
+    lf = torch.nn.functional.mse_loss(rgb_f[..., :3], tgt[..., :3])
+    sp, tpar = model_mod.get_params_tensor(models["embedding"], False)
+    reg = 1e-5 * (torch.norm(sp, p=2) + torch.norm(tpar, p=2))
+    loss = lc + lf + reg
+    optimizer.zero_grad()
+    loss.backward()
+    grads = {f"{k}.{n}": p.grad.detach().clone() for k, m in models.items() for n, p in m.named_parameters()}
+    optimizer.step()
+    scheduler.step()
+    after = {f"{k}.{n}": p.detach().clone() for k, m in models.items() for n, p in m.named_parameters()}
+    out = dict(nc=nc, nf=nf, near=np.float32(near), far=np.float32(far), chunk=chunk,
+               ro=ro, rd=rd, ids=oid, target=tgt, t_rand_head=t_rand[:4], u_head=u[:4],
+               t_rand_sum=t_rand.double().sum(), u_sum=u.double().sum(), select_inds=sel.astype(np.int64),
+               rgb_coarse=rgb_c, rgb_fine=rgb_f, lc=lc, lf=lf, reg=reg, loss=loss)
+    for k in grads:
+        if k.startswith("embedding."):
+            out["grows_" + k] = grads[k][[oid_v]]
+            out["prows_" + k] = after[k][[oid_v]]
+            out["gnorm_rest_" + k] = grads[k].norm() ** 2 - grads[k][[oid_v]].norm() ** 2
+        else:
+            out["gnorm_" + k] = grads[k].norm()
+            out["pdelta_norm_" + k] = (after[k] - before[k]).norm()
+    for k in C3_FULL:
+        out["g_" + k] = grads[k]
+        out["p_" + k] = after[k]
+    for idx, k in enumerate(sorted(grads)):
+        if k.startswith("embedding."):
+            continue
+        r = proj_directions(idx, grads[k].shape)
+        out["gproj_" + k] = proj(r, grads[k])
+        out["pproj_" + k] = proj(r, after[k] - before[k])
+    save(name + ".npz", **out)
+
+
+def gen_train_cars_code(nerf, model_mod, ev):
+    gen_train_shape(nerf, model_mod, ev, "train_cars_code")
+
+
+def gen_train_3080(nerf, model_mod, ev):
+    gen_train_shape(nerf, model_mod, ev, "train_3080")
+
+
+def gen_c5_chairs(nerf, model_mod, ev):
+    """eval.py:141-168 at srn-chairs-code.yml:47-54's shape: num_random_rays 4096 of a 128x128 view, 32
+    coarse + 128 fine perturbed samples, near 1.25 / far 2.75, the whole batch in one
+    predict_radiance_and_render; gradients into theta, phi, rho and both codes (weights require grad, as
+    in eval.py).  The draws are re-made by the tests from torch.manual_seed(4244): t_rand (4096, 32), then
+    u (4096, 128); head and sums stored."""
+    K = synthetic.srn_intrinsics(128)
+    rs = nerf.RaySampler(128, 128, K, sample_size=4096, device="cpu", datatype=torch.float32)
+    ps = nerf.PointSampler(32, 128, 1.25, 2.75, spacing_mode="lindepth", perturb=True, dtype=torch.float32,
+                           device="cpu")
+    emb = _embedders(nerf)
+    models = {"nerf_coarse": make_model(model_mod, 0), "nerf_fine": make_model(model_mod, 1)}
+    for mm in models.values():
+        mm.train()
+    g = torch.Generator().manual_seed(32)
+    target = torch.rand(128 * 128, 4, generator=g)
+    theta = torch.tensor([1.1]).requires_grad_(True)
+    phi = torch.tensor([-0.5]).requires_grad_(True)
+    rho = torch.tensor([2.0]).requires_grad_(True)
+    zs = synthetic.latent_codes(7, 1).clone().requires_grad_(True)
+    zt = synthetic.latent_codes(8, 1).clone().requires_grad_(True)
+    np.random.seed(18)
+    c2w = ev.pose_spherical(theta, phi, rho)[None, :]
+    ro, rd, sel = rs.sample(tform_cam2world=c2w)
+    tp = target[None][..., sel, :].squeeze()
+    zse, zte = zs.expand(ro.shape[0], -1), zt.expand(ro.shape[0], -1)
+    torch.manual_seed(4244)
+    rgb_c, rgb_f = nerf.predict_radiance_and_render((ro, rd), ps, emb, models["nerf_coarse"], models["nerf_fine"],
+                                                    (zse, zte))
+    torch.manual_seed(4244)
+    t_rand, u = torch.rand(4096, 32), torch.rand(4096, 128)
+    lc = torch.nn.functional.mse_loss(rgb_c[..., :3], tp[..., :3])
+    lf = torch.nn.functional.mse_loss(rgb_f[..., :3], tp[..., :3])
+    loss = lc + lf + 1e-5 * (torch.norm(zse, p=2) + torch.norm(zte, p=2))
+    loss.backward()
+    pw = {f"gnorm_{k}.{n}": p.grad.norm() for k, mm in models.items() for n, p in mm.named_parameters()}
+    save("eval_c5_chairs.npz", target=target,
+         select_inds=sel.astype(np.int64), theta=theta, phi=phi, rho=rho, z_s=zs, z_t=zt,
+         t_rand_head=t_rand[:4], u_head=u[:4], t_rand_sum=t_rand.double().sum(), u_sum=u.double().sum(),
+         rgb_coarse=rgb_c, rgb_fine=rgb_f, loss=loss, g_theta=theta.grad, g_phi=phi.grad, g_rho=rho.grad,
+         g_z_s=zs.grad, g_z_t=zt.grad, g_fine_fc_rgb_w=models["nerf_fine"].fc_rgb.weight.grad,
+         g_coarse_layer_xyz1_w=models["nerf_coarse"].layer_xyz1.weight.grad, **pw)
+
 
 def proj_directions(idx: int, shape) -> torch.Tensor:
     """C3_PROJ seeded N(0, 1) directions for parameter ``idx`` (sorted-name order), float32 CPU."""
@@ -636,6 +770,7 @@ def proj(r: torch.Tensor, t: torch.Tensor) -> np.ndarray:
 ROUND2 = {"trained": gen_trained, "chairs": gen_chairs, "lego": gen_lego, "c5": gen_c5, "se3": gen_se3,
           "srn": gen_srn, "loss": gen_loss}
 ROUND3 = {"c3train": gen_c3train}
+ROUND6 = {"train_cars_code": gen_train_cars_code, "train_3080": gen_train_3080, "c5_chairs": gen_c5_chairs}
 
 
 if __name__ == "__main__":

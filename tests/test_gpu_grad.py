@@ -720,8 +720,9 @@ def test_field_backward_train_nogeo_bitwise(dev, precision, mode, r, s, n_codes)
     atomic = n_codes > 1             # the per-code sums / biases of g_code: float atomics
     code_biases = {3, 5, 17}          # b_xyz2, b_out, b_rgb: column sums of g_code
     # float-atomic sums over ~67k samples whose partial sums exceed the total (cancellation): two orders
-    # agree to 1e-5 of the total's magnitude in fp32, to 1e-4 in 3xbf16 (larger per-sample terms)
-    tol = 1e-4 if x3 else 1e-5
+    # agree to 1e-5 of the total's magnitude in fp32; 3xbf16 (larger per-sample terms) measured 1.27e-5
+    # (gpurun_out/r05n), bound at 2x that
+    tol = 2.6e-5 if x3 else 1e-5
     for other in ("nogeo", "nogeo2"):
         for k, (a, b) in enumerate(zip(out[other][0], out["geo"][0])):
             if atomic and k in code_biases:
@@ -729,6 +730,11 @@ def test_field_backward_train_nogeo_bitwise(dev, precision, mode, r, s, n_codes)
             else:
                 assert torch.equal(a, b), f"param {k}: {other} differs from the geometry schedule"
         if atomic:
+            from conftest import margin
+            err = (out[other][1].double() - out["geo"][1].double()).abs().max().item()
+            scale = max(out["geo"][1].abs().max().item(), 1e-30)
+            margin(f"nogeo_bitwise[{precision},{r}x{s},codes{n_codes}]", f"g_code {other} vs geo (rel. max)",
+                   err / scale, tol + 1e-7 / scale)
             close(out[other][1], out["geo"][1].double(), tol, "g_code")
         else:
             assert torch.equal(out[other][1], out["geo"][1]), f"g_code: {other}"

@@ -209,6 +209,45 @@ def test_eval_c5_fused_at_size(dev, precision):
     close(zt.grad, g["g_z_t"], 2e-3, "g_z_t")
 
 
+C5_CHAIRS_RTOL = 2e-3      # as C5's; margins recorded (profiles/r06/parity_margins.json)
+
+
+def test_eval_c5_chairs_fused_at_size(dev):
+    """eval.py:141-168 at srn-chairs-code.yml's shape (make_golden.py gen_c5_chairs: num_random_rays 4096
+    of a 128x128 view, 32 + 128 perturbed samples -- a 160-sample fine pass -- near 1.25 / far 2.75, the
+    reference's draws re-made from its seed) through eval_step_loss's fused path, fp32: rendered rgb,
+    loss and d(theta, phi, rho, z_s, z_t) vs the reference; a second run bit for bit."""
+    from codenerf import synthetic
+    from codenerf.evaluate import eval_step_loss
+    from codenerf.nerf import PointSampler, RaySampler
+    from conftest import margin
+    g = gload("eval_c5_chairs.npz", dev)
+    torch.manual_seed(4244)
+    t_rand, u = torch.rand(4096, 32), torch.rand(4096, 128)
+    assert torch.equal(t_rand[:4].to(dev), g["t_rand_head"]) and torch.equal(u[:4].to(dev), g["u_head"])
+    t_rand, u = t_rand.to(dev), u.to(dev)
+    rs = RaySampler(128, 128, synthetic.srn_intrinsics(128), sample_size=4096, device=dev, datatype=torch.float32)
+    ps = PointSampler(32, 128, 1.25, 2.75, "lindepth", True, torch.float32, dev)
+    models = _eval_models(dev)
+    runs = []
+    for rep in range(2):
+        lv = [g[k].clone().requires_grad_(True) for k in ("theta", "phi", "rho", "z_s", "z_t")]
+        np.random.seed(18)
+        loss, logs = eval_step_loss(*lv, g["target"], (rs, ps), embedders(dev), models, 1e-5, t_rand=t_rand, u=u)
+        loss.backward()
+        torch.cuda.synchronize()
+        runs.append((loss.item(), [t.grad.clone() for t in lv]))
+    assert runs[0][0] == runs[1][0]
+    for a, b in zip(runs[0][1], runs[1][1]):
+        assert torch.equal(a, b)
+    tag = "eval_c5_chairs[f32]"
+    margin(tag, "loss", abs(runs[0][0] - g["loss"].item()), 1e-5)
+    for name, t in zip(("theta", "phi", "rho", "z_s", "z_t"), runs[0][1]):
+        ref = g["g_" + name]
+        scale = max(1e-2, ref.abs().max().item()) if name in ("theta", "phi", "rho") else ref.abs().max().item()
+        margin(tag, "d " + name, (t - ref).abs().max().item() / scale, C5_CHAIRS_RTOL)
+
+
 @pytest.mark.parametrize("precision", ["f32", "bf16x3"])
 def test_eval_step_in_place_gradients(dev, monkeypatch, precision):
     """The eval step's gradient sinks (C5 inputs, the flat AdamW's zeroed slots handed out by zero_grad):

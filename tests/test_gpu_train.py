@@ -620,6 +620,101 @@ def test_train_c3_chunk_at_size(dev, precision, host_ids):
         _C3_RESULTS[precision] = {k: (p.grad.detach().clone(), p.detach().clone()) for k, p in named.items()}
 
 
+# The reference's runnable training shapes (round 6; make_golden.py gen_train_shape, one object per
+# chunk): bounds as C3's -- set from the first GPU run's margins (profiles/r06/parity_margins.json).
+SHAPE_GRAD_RTOL = {"train_cars_code": 1e-3, "train_3080": 1e-3}
+SHAPE_PROJ_RTOL = {"train_cars_code": 1.2e-3, "train_3080": 1.2e-3}
+SHAPE_STEP_PROJ = {"train_cars_code": 6e-3, "train_3080": 6e-3}
+
+
+@pytest.mark.parametrize("name", ["train_cars_code", "train_3080"])
+def test_train_shape_chunk_at_size(dev, name):
+    """The reference's own runnable training shapes, one chunk step each vs the reference
+    (make_golden.py gen_train_shape): srn-cars-code.yml (Nc 32 / Nf 128: a 160-sample fine pass,
+    chunk 4096) and srn-cars-code-3080.yml (64 / 128: 192 fine samples, chunk 1024 -- the first chunk
+    of a 4096-ray draw), perturbed samples with the reference's draws, one object per chunk (the
+    deterministic path every runnable config takes), AdamW + LambdaLR.  fp32 (the reference's
+    precision) through train_minibatch: losses, rendered rgb, five gradients in full, 16 projections of
+    every gradient and post-step change, the touched code row (gradient and post-step), every other row
+    only decayed.  Run twice: the step is bit-reproducible."""
+    from codenerf import synthetic, train as T
+    from codenerf.models import CodeNeRFModel, ShapeTextureEmbedding
+    from codenerf.nerf import PointSampler
+    from conftest import margin
+    from test_gpu_parity import load
+    g = load(name + ".npz", dev)
+    nc, nf, chunk = int(g["nc"].item()), int(g["nf"].item()), int(g["chunk"].item())
+    near, far = float(g["near"].item()), float(g["far"].item())
+    torch.manual_seed(4343)
+    t_rand, u = torch.rand(chunk, nc), torch.rand(chunk, nf)
+    assert torch.equal(t_rand[:4].to(dev), g["t_rand_head"]) and torch.equal(u[:4].to(dev), g["u_head"])
+    runs = []
+    for rep in range(2):
+        emb_t = ShapeTextureEmbedding(C3_OBJECTS, 256, 256)
+        with torch.no_grad():
+            emb_t.shape_embedding.weight.copy_(synthetic.latent_codes(40, C3_OBJECTS))
+            emb_t.texture_embedding.weight.copy_(synthetic.latent_codes(41, C3_OBJECTS))
+        models = {"embedding": emb_t.to(dev)}
+        for key, seed in (("nerf_coarse", 0), ("nerf_fine", 1)):
+            m = CodeNeRFModel(hidden_size=256, shape_code_size=256, texture_code_size=256, num_encoding_fn_xyz=10,
+                              num_encoding_fn_dir=4)
+            m.load_state_dict(synthetic.codenerf_params(seed))
+            models[key] = m.to(dev)
+        opt, sched = T.prepare_optimizer(_opt_cfg(), models)
+        ps = PointSampler(nc, nf, near, far, spacing_mode="lindepth", perturb=True, dtype=torch.float32, device=dev)
+        before = {f"{k}.{n}": p.detach().clone() for k, m in models.items() for n, p in m.named_parameters()}
+        ids_t = g["ids"].long()
+        ids_t._cn_host_ids = g["ids"].long().cpu().numpy()
+        logs = T.train_minibatch(models, opt, sched, ps, embedders(dev), g["ro"], g["rd"], ids_t, g["target"],
+                                 1e-5, uniforms=(t_rand.to(dev), u.to(dev)))
+        torch.cuda.synchronize()
+        named = {f"{k}.{n}": p for k, m in models.items() for n, p in m.named_parameters()}
+        runs.append({k: (p.grad.detach().clone(), p.detach().clone()) for k, p in named.items()})
+    for k in runs[0]:
+        assert torch.equal(runs[0][k][0], runs[1][k][0]) and torch.equal(runs[0][k][1], runs[1][k][1]), \
+            ("not bit-reproducible", k)
+    tag = f"{name}[f32]"
+    for k, key in (("lc", "nerf_loss_coarse"), ("lf", "nerf_loss_fine"), ("reg", "embedding_loss"),
+                   ("loss", "total_loss")):
+        margin(tag, "loss " + k, abs(float(logs[key]) - g[k].item()), 1e-5 * max(1.0, abs(g[k].item())))
+    rtol, prtol = SHAPE_GRAD_RTOL[name], SHAPE_PROJ_RTOL[name]
+    oid = int(g["ids"][0].item())
+    worst = {"grad": (0.0, ""), "proj": (0.0, ""), "firm_step": (0.0, ""), "step_proj": (0.0, "")}
+    flips = 0
+    for idx, k in enumerate(sorted(named)):
+        p = named[k]
+        if k.startswith("embedding."):
+            ref = g["grows_" + k]
+            margin(tag, "touched row grad " + k, (p.grad[[oid]] - ref).abs().max().item() / ref.abs().max().item(),
+                   rtol)
+            assert float(p.grad.norm() ** 2 - p.grad[[oid]].norm() ** 2) == 0.0, k
+            fs, nf_ = _post_step(p.detach()[[oid]], g["prows_" + k], ref, 1e-3, rtol)
+            margin(tag, "touched row firm post-step " + k, fs, 1e-6)
+            flips += nf_
+            mask = torch.ones(C3_OBJECTS, dtype=torch.bool, device=dev)
+            mask[oid] = False
+            assert (p.detach()[mask] - before[k][mask] * (1 - 1e-3 * 1e-2)).abs().max().item() <= 1e-7, k
+            continue
+        lr = 1e-4
+        if "g_" + k in g:
+            ref = g["g_" + k]
+            worst["grad"] = max(worst["grad"], ((p.grad - ref).abs().max().item() / ref.abs().max().item(), k))
+            fs, nf_ = _post_step(p.detach(), g["p_" + k], ref, lr, rtol)
+            worst["firm_step"] = max(worst["firm_step"], (fs, k))
+            flips += nf_
+        r = _proj_directions(idx, p.shape)
+        gn = max(g["gnorm_" + k].item(), 1e-12)
+        worst["proj"] = max(worst["proj"], ((_proj(r, p.grad) - g["gproj_" + k].cpu()).abs().max().item() / gn, k))
+        dp = (_proj(r, p.detach() - before[k]) - g["pproj_" + k].cpu()).abs().max().item()
+        worst["step_proj"] = max(worst["step_proj"], (dp / (lr * p.numel() ** 0.5), k))
+    margin(tag, "grad full tensors (worst: %s)" % worst["grad"][1], worst["grad"][0], rtol)
+    margin(tag, "grad projections (worst: %s)" % worst["proj"][1], worst["proj"][0], prtol)
+    margin(tag, "firm post-step (worst: %s)" % worst["firm_step"][1], worst["firm_step"][0], 1e-6,
+           sign_undetermined_elements=flips)
+    margin(tag, "post-step projections (worst: %s)" % worst["step_proj"][1], worst["step_proj"][0],
+           SHAPE_STEP_PROJ[name])
+
+
 def _post_step(got, ref, g_ref, lr, rtol):
     """AdamW's first step moves each element by lr g / (|g| + eps) (+ decay): where the reference's
     |g| is well above both eps (1e-8) and the gradient tolerance (rtol x the tensor's max) that is

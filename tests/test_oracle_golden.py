@@ -361,3 +361,89 @@ def test_train_c3_chunk_gradients():
     for t, k in ((ts, "shape_embedding"), (tt, "texture_embedding")):
         ref = g[f"grows_embedding.{k}.weight"]
         same(t.grad[[17, 1234]], ref, 1e-5 * ref.abs().max().item())
+
+
+# ---------------------------------------------------------------- round 6: the reference's runnable shapes
+
+
+@pytest.mark.parametrize("name", ["train_cars_code", "train_3080"])
+def test_train_shape_chunk_gradients(name):
+    """train.py:76-114 at srn-cars-code.yml (32 + 128, chunk 4096) and srn-cars-code-3080.yml (64 + 128,
+    the first 1024-ray chunk of a 4096-ray draw): the reference's own chunk step (make_golden.py
+    gen_train_shape, one object per chunk) through the oracle's autograd -- losses, every gradient's
+    norm and its 16 projections, five full gradients, the touched code row."""
+    g = load(name + ".npz")
+    nc, nf, chunk = int(g["nc"]), int(g["nf"]), int(g["chunk"])
+    torch.manual_seed(4343)
+    t_rand, u = torch.rand(chunk, nc), torch.rand(chunk, nf)
+    same(t_rand[:4], g["t_rand_head"])
+    same(u[:4], g["u_head"])
+    pc, pf = synthetic.codenerf_params(0), synthetic.codenerf_params(1)
+    ts, tt = synthetic.latent_codes(40, 2458).requires_grad_(True), synthetic.latent_codes(41, 2458).requires_grad_(True)
+    for p in list(pc.values()) + list(pf.values()):
+        p.requires_grad_(True)
+    ids = g["ids"].long()
+    smp = O.Sampling(nc, nf, float(g["near"]), float(g["far"]))
+    out = O.predict_radiance_and_render(g["ro"], g["rd"], smp, O.EmbedCfg(), pc, pf, ts[ids], tt[ids], t_rand, u)
+    tgt = g["target"]
+    lc = torch.nn.functional.mse_loss(out["rgb_coarse"][..., :3], tgt[..., :3])
+    lf = torch.nn.functional.mse_loss(out["rgb_fine"][..., :3], tgt[..., :3])
+    reg = 1e-5 * (torch.norm(ts.data.reshape(-1), p=2) + torch.norm(tt.data.reshape(-1), p=2))
+    (lc + lf + reg).backward()
+    same(out["rgb_coarse"].detach(), g["rgb_coarse"], 1e-6)
+    same(out["rgb_fine"].detach(), g["rgb_fine"], 1e-6)
+    same(lc.detach(), g["lc"], 1e-7)
+    same(lf.detach(), g["lf"], 1e-7)
+    same(reg, g["reg"], 1e-9)
+    named = {**{f"nerf_coarse.{k}": v for k, v in pc.items()}, **{f"nerf_fine.{k}": v for k, v in pf.items()}}
+    for idx, k in enumerate(sorted(named), start=2):   # make_golden's index counts the two embedding tables
+        p = named[k]
+        ref = g["gnorm_" + k].item()
+        assert abs(p.grad.norm().item() - ref) <= 1e-5 * ref + 1e-9, k
+        r = torch.randn((16,) + tuple(p.shape), generator=torch.Generator().manual_seed(7000 + idx))
+        pr = (r.double() * p.grad.double()[None]).reshape(16, -1).sum(1)
+        assert (pr - g["gproj_" + k].double()).abs().max().item() <= 1e-4 * ref + 1e-9, k
+    for k in ("nerf_coarse.layer_dir1.weight", "nerf_coarse.shape_code_layer1.weight", "nerf_fine.fc_rgb.weight",
+              "nerf_fine.fc_out.bias", "nerf_fine.layer_xyz1.weight"):
+        same(named[k].grad, g["g_" + k], 1e-5 * g["g_" + k].abs().max().item())
+    oid = int(ids[0])
+    assert torch.equal(ids, torch.full_like(ids, oid))
+    for t, k in ((ts, "shape_embedding"), (tt, "texture_embedding")):
+        ref = g[f"grows_embedding.{k}.weight"]
+        same(t.grad[[oid]], ref, 1e-5 * ref.abs().max().item())
+
+
+def test_eval_c5_chairs_gradients():
+    """eval.py:141-168 at srn-chairs-code.yml's shape (4096 rays, 32 + 128 perturbed, near 1.25 far
+    2.75, make_golden.py gen_c5_chairs) through the oracle's autograd equals the reference's own."""
+    g = load("eval_c5_chairs.npz")
+    torch.manual_seed(4244)
+    t_rand, u = torch.rand(4096, 32), torch.rand(4096, 128)
+    same(t_rand[:4], g["t_rand_head"])
+    same(u[:4], g["u_head"])
+    theta, phi, rho = [g[k].clone().requires_grad_(True) for k in ("theta", "phi", "rho")]
+    zs, zt = g["z_s"].clone().requires_grad_(True), g["z_t"].clone().requires_grad_(True)
+    pc, pf = synthetic.codenerf_params(0), synthetic.codenerf_params(1)
+    for p in list(pc.values()) + list(pf.values()):
+        p.requires_grad_(True)
+    c2w = O.pose_spherical(theta, phi, rho)[None]
+    d = O.ray_directions(128, 128, synthetic.srn_intrinsics(128))
+    ro, rd = O.ray_bundle(d, c2w)
+    sel = g["select_inds"].numpy()
+    ro, rd = O.gather_rays(ro, rd, sel)
+    n = ro.shape[0]
+    tp = g["target"][None][..., sel, :].squeeze()
+    zse, zte = zs.expand(n, -1), zt.expand(n, -1)
+    out = O.predict_radiance_and_render(ro, rd, O.Sampling(32, 128, 1.25, 2.75), O.EmbedCfg(), pc, pf, zse, zte,
+                                        t_rand, u)
+    lc = torch.nn.functional.mse_loss(out["rgb_coarse"][..., :3], tp[..., :3])
+    lf = torch.nn.functional.mse_loss(out["rgb_fine"][..., :3], tp[..., :3])
+    loss = lc + lf + 1e-5 * (torch.norm(zse, p=2) + torch.norm(zte, p=2))
+    loss.backward()
+    same(out["rgb_coarse"].detach(), g["rgb_coarse"], 1e-6)
+    same(out["rgb_fine"].detach(), g["rgb_fine"], 1e-6)
+    same(loss.detach(), g["loss"], 1e-7)
+    for t, k in [(theta, "theta"), (phi, "phi"), (rho, "rho"), (zs, "z_s"), (zt, "z_t")]:
+        ref = g["g_" + k]
+        same(t.grad, ref, 1e-5 * max(1e-2, ref.abs().max().item()))
+    same(pf["fc_rgb.weight"].grad, g["g_fine_fc_rgb_w"], 1e-5 * g["g_fine_fc_rgb_w"].abs().max().item())
