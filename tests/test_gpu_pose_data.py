@@ -209,7 +209,10 @@ def test_eval_c5_fused_at_size(dev, precision):
     close(zt.grad, g["g_z_t"], 2e-3, "g_z_t")
 
 
-C5_CHAIRS_RTOL = 2e-3      # as C5's; margins recorded (profiles/r06/parity_margins.json)
+# twice the largest error the first GPU run measured (d z_s 4.83e-5, loss 3.9e-7; gpurun_out/r06a,
+# profiles/r06/parity_margins.json); the eval step is bit-reproducible
+C5_CHAIRS_RTOL = 1e-4
+C5_CHAIRS_LOSS = 1e-6
 
 
 def test_eval_c5_chairs_fused_at_size(dev):
@@ -241,7 +244,7 @@ def test_eval_c5_chairs_fused_at_size(dev):
     for a, b in zip(runs[0][1], runs[1][1]):
         assert torch.equal(a, b)
     tag = "eval_c5_chairs[f32]"
-    margin(tag, "loss", abs(runs[0][0] - g["loss"].item()), 1e-5)
+    margin(tag, "loss", abs(runs[0][0] - g["loss"].item()), C5_CHAIRS_LOSS)
     for name, t in zip(("theta", "phi", "rho", "z_s", "z_t"), runs[0][1]):
         ref = g["g_" + name]
         scale = max(1e-2, ref.abs().max().item()) if name in ("theta", "phi", "rho") else ref.abs().max().item()

@@ -621,10 +621,11 @@ def test_train_c3_chunk_at_size(dev, precision, host_ids):
 
 
 # The reference's runnable training shapes (round 6; make_golden.py gen_train_shape, one object per
-# chunk): bounds as C3's -- set from the first GPU run's margins (profiles/r06/parity_margins.json).
-SHAPE_GRAD_RTOL = {"train_cars_code": 1e-3, "train_3080": 1e-3}
-SHAPE_PROJ_RTOL = {"train_cars_code": 1.2e-3, "train_3080": 1.2e-3}
-SHAPE_STEP_PROJ = {"train_cars_code": 6e-3, "train_3080": 6e-3}
+# chunk): about twice the errors the first GPU run measured (gpurun_out/r06a, profiles/r06/parity_margins.json:
+# full tensors 2.84e-4 / 4.47e-4, projections 9.59e-4 / 7.08e-4; the step is bit-reproducible, so the
+# same kernels give the same errors on every box).
+SHAPE_GRAD_RTOL = {"train_cars_code": 6e-4, "train_3080": 9e-4}
+SHAPE_PROJ_RTOL = {"train_cars_code": 1.9e-3, "train_3080": 1.4e-3}
 
 
 @pytest.mark.parametrize("name", ["train_cars_code", "train_3080"])
@@ -705,14 +706,21 @@ def test_train_shape_chunk_at_size(dev, name):
         r = _proj_directions(idx, p.shape)
         gn = max(g["gnorm_" + k].item(), 1e-12)
         worst["proj"] = max(worst["proj"], ((_proj(r, p.grad) - g["gproj_" + k].cpu()).abs().max().item() / gn, k))
-        dp = (_proj(r, p.detach() - before[k]) - g["pproj_" + k].cpu()).abs().max().item()
-        worst["step_proj"] = max(worst["step_proj"], (dp / (lr * p.numel() ** 0.5), k))
+        # post-step change, projected: AdamW's first step is lr sign(g) (+ decay) per element, so only
+        # elements whose gradient sign is undetermined at the gradient tolerance (|g| <= rtol max|g|) can
+        # move differently, by at most 2 lr each: the bound per direction is 2 lr sum of |r| over them
+        # (+ float slack), the error is stated as a fraction of it
+        dp = (_proj(r, p.detach() - before[k]) - g["pproj_" + k].cpu()).abs()
+        gd = p.grad.detach().double().cpu().reshape(-1)
+        undet = gd.abs() <= rtol * gd.abs().max()
+        cap = 2.05 * lr * (r.double().reshape(r.shape[0], -1).abs() * undet[None]).sum(1) + 1e-3 * lr * p.numel() ** 0.5
+        worst["step_proj"] = max(worst["step_proj"], ((dp / cap).max().item(), k))
     margin(tag, "grad full tensors (worst: %s)" % worst["grad"][1], worst["grad"][0], rtol)
     margin(tag, "grad projections (worst: %s)" % worst["proj"][1], worst["proj"][0], prtol)
     margin(tag, "firm post-step (worst: %s)" % worst["firm_step"][1], worst["firm_step"][0], 1e-6,
            sign_undetermined_elements=flips)
-    margin(tag, "post-step projections (worst: %s)" % worst["step_proj"][1], worst["step_proj"][0],
-           SHAPE_STEP_PROJ[name])
+    margin(tag, "post-step projections / sign-undetermined cap (worst: %s)" % worst["step_proj"][1],
+           worst["step_proj"][0], 1.0)
 
 
 def _post_step(got, ref, g_ref, lr, rtol):
