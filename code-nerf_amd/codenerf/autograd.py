@@ -342,7 +342,8 @@ class _FieldMeta:
     """Non-tensor arguments of the field Functions."""
 
     def __init__(self, n_samples, chunk_rows, fx, fd, code_index=None, precision="f32", train_precision="f32",
-                 sink=None, ray_sink=None):
+                 sink=None, ray_sink=None, pair=None):
+        self.pair = pair       # FieldPair of a train step's render, or None
         self.n_samples, self.chunk_rows = n_samples, chunk_rows
         self.precision = precision
         self.train_precision = train_precision
@@ -372,6 +373,10 @@ def _code_grads(meta, params, z_s, z_t, g_code, pg, want_z, act=None):
     return ops.code_bias_backward(params, z_s, z_t, g_code, pg, want_z=want_z)
 
 
+class _Slots(list):
+    """The optimiser's flat gradient slots handed to a backward (_param_grad_buffers)."""
+
+
 def _param_grad_buffers(params, needs, orig=None):
     """Zeroed gradient buffers the backward kernels accumulate into: the optimizer's flat-buffer
     slices when every parameter still has no .grad this step (optim.AdamW.zero_grad), else fresh
@@ -383,8 +388,62 @@ def _param_grad_buffers(params, needs, orig=None):
         if all(s is not None and p.grad is None for s, p in zip(slots, orig)):
             for p in orig:
                 p._cn_grad_slot = None       # one use per zero_grad
-            return slots
+            # (no other reference to a slot may survive the backward: AccumulateGrad adopts a returned
+            # gradient as .grad only when nothing else holds it -- else it clones, one copy per tensor)
+            return _Slots(slots)
     return [torch.zeros_like(p) for p in params]
+
+
+class FieldPair:
+    """A training step's two fields (predict_radiance_and_render's coarse and fine, nerf/__init__.py:81-89):
+    their backwards are independent (the fine depths are detached, point_sampler.py:115), so the first one
+    autograd reaches waits and the second runs both in ONE cn_field_backward_train_multi call (one dX
+    launch, one batched dW launch, one layer_xyz1 launch and one reduction launch for the two; every
+    gradient bitwise that of the per-field calls).  Armed by train_minibatch only (paired_fields()): the
+    waiting field hands its gradients over in place -- the optimiser's flat slots installed as .grad at
+    once, the code rows' dz through the CodeGradSink -- so it returns none through autograd."""
+
+    __slots__ = ("pending", "fields")
+
+    def __init__(self):
+        self.pending = None
+        self.fields = 0
+
+
+_PAIRING = [False]
+
+
+class paired_fields:
+    """Context in which render_rays pairs its two fields' training backwards (FieldPair)."""
+
+    def __enter__(self):
+        self.prev = _PAIRING[0]
+        _PAIRING[0] = True
+        return self
+
+    def __exit__(self, *exc):
+        _PAIRING[0] = self.prev
+        return False
+
+
+def new_field_pair():
+    """render_rays: a FieldPair for its two fields inside paired_fields(), else None."""
+    return FieldPair() if (_PAIRING[0] and torch.is_grad_enabled()) else None
+
+
+def _pair_flush(pair):
+    """End of the backward pass (queued by the waiting field): a field whose partner never ran its
+    backward runs alone.  Its code gradient must still reach the code rows' sink."""
+    if pair.pending is None:
+        return
+    job, post = pair.pending
+    pair.pending = None
+    r = ops.field_backward_train_multi([job], post[0].precision)[0]
+    meta, params, z_s, z_t, pg, want_z, act = post
+    if want_z and (meta.sink is None or meta.sink.rows() is None):
+        raise RuntimeError("paired field backward: the partner field never ran and the code rows' gradient "
+                           "buffers were already handed out")
+    _code_grads(meta, params, z_s, z_t, r["g_code"], pg, want_z, act)
 
 
 class RadianceField(torch.autograd.Function):
@@ -451,6 +510,8 @@ class RadianceField(torch.autograd.Function):
                            and ops.fused_backward_supported(z_s.shape[0], meta.n_samples, meta.code_index,
                                                             meta.precision))
         ctx.masks = None
+        if meta.pair is not None and ctx.train_fused and meta.precision == "f32":
+            meta.pair.fields += 1
         if ctx.train_fused:
             x3 = meta.precision == "bf16x3"
             raw, saved, ctx.masks = ops.radiance_field_train_w16(
@@ -493,18 +554,41 @@ class RadianceField(torch.autograd.Function):
             ctx.masks = None
             d_ro, d_rd = (None, None) if ray_into is not None else (r["d_ro"], r["d_rd"])
             return (None, d_rd, r["d_pts"], d_ro, None, dz_s, dz_t, *([None] * len(params)))
-        pg = _param_grad_buffers(params, needs[7:], ctx.orig_params)
+        orig = ctx.orig_params
+        pg = _param_grad_buffers(params, needs[7:], orig)
+        slots = isinstance(pg, _Slots)
         ctx.orig_params = None
         want_z = needs[5] or needs[6]
         if ctx.train_fused:
             x3 = meta.precision == "bf16x3"
-            r = ops.field_backward_train(_packed(ctx.owner, params, "bf16x3_t" if x3 else "f32_w16_t"), params, ctx.masks,
-                                         ctx.acts, ctx.x_enc, g_raw.contiguous(), rd.shape[0], meta.n_samples,
-                                         meta.chunk_rows, z_s.shape[0], meta.fx, meta.fd, rd=rd, pts=pts, ro=ro, z=z,
-                                         code_index=meta.code_index, param_grads=pg, want_pts=needs[2],
-                                         want_ro=needs[3], want_rd=needs[1], precision=meta.precision,
-                                         g_code=ctx.g_code)
+            job = dict(packed_t=_packed(ctx.owner, params, "bf16x3_t" if x3 else "f32_w16_t"), params=params,
+                       masks=ctx.masks, saved=ctx.acts, x_enc=ctx.x_enc, d_raw=g_raw.contiguous(), n_rays=rd.shape[0],
+                       n_samples=meta.n_samples, chunk_rows=meta.chunk_rows, n_codes=z_s.shape[0], freqs_xyz=meta.fx,
+                       freqs_dir=meta.fd, rd=rd, pts=pts, ro=ro, z=z, code_index=meta.code_index, param_grads=pg,
+                       want_pts=needs[2], want_ro=needs[3], want_rd=needs[1], g_code=ctx.g_code)
             act, ctx.acts, ctx.x_enc, ctx.masks, ctx.g_code, ctx.code_act = ctx.code_act, None, None, None, None, None
+            post = (meta, params, z_s, z_t, pg, want_z, act)
+            pair = meta.pair
+            if pair is not None and pair.fields == 2 and not x3:
+                if pair.pending is None:
+                    # the first of the pair waits for the other: only when everything it returns goes in place
+                    # (the flat slots as .grad now, the code rows through the sink) and no ray gradient is wanted
+                    if (slots and act is not None and not any(needs[1:4])
+                            and (not want_z or (meta.sink is not None and meta.sink.rows() is not None))):
+                        pair.pending = (job, post)
+                        for p, g in zip(orig, pg):
+                            p.grad = g                  # filled by the shared launch, on the stream
+                        torch.autograd.Variable._execution_engine.queue_callback(lambda: _pair_flush(pair))
+                        return (None,) * len(needs)
+                else:
+                    other_job, other_post = pair.pending
+                    pair.pending = None
+                    r_other, r = ops.field_backward_train_multi([other_job, job], meta.precision)
+                    _code_grads(*other_post[:4], r_other["g_code"], *other_post[4:])
+                    dz_s, dz_t = _code_grads(meta, params, z_s, z_t, r["g_code"], pg, want_z, act)
+                    grads = pg if pg is not None else [None] * len(params)
+                    return (None, r["d_rd"], r["d_pts"], r["d_ro"], None, dz_s, dz_t, *grads)
+            r = ops.field_backward_train(precision=meta.precision, **job)
             dz_s, dz_t = _code_grads(meta, params, z_s, z_t, r["g_code"], pg, want_z, act)
             grads = pg if pg is not None else [None] * len(params)
             return (None, r["d_rd"], r["d_pts"], r["d_ro"], None, dz_s, dz_t, *grads)
@@ -662,19 +746,20 @@ def mlp_forward_autograd(model, z_s, z_t, x):
     return MLPForward.apply(getattr(model, "train_precision", "f32"), x, cs, ct, *model.param_list())
 
 
-def _field_meta(model, cs, ct, n_samples, chunk_rows, fx, fd, code_index, rd=None, ro=None):
+def _field_meta(model, cs, ct, n_samples, chunk_rows, fx, fd, code_index, rd=None, ro=None, pair=None):
     sink = getattr(cs, "_cn_sink", None)
     return _FieldMeta(n_samples, chunk_rows, fx, fd, code_index=code_index,
                       precision=getattr(model, "precision", "f32"),
                       train_precision=getattr(model, "train_precision", "f32"),
                       sink=sink if sink is not None and getattr(ct, "_cn_sink", None) is sink else None,
-                      ray_sink=_ray_sink(rd, ro) if (rd is not None and ro is not None) else None)
+                      ray_sink=_ray_sink(rd, ro) if (rd is not None and ro is not None) else None, pair=pair)
 
 
-def radiance_field_autograd(model, rd, z_s, z_t, chunk_rows, fx, fd, pts=None, ro=None, z=None, code_index=None):
+def radiance_field_autograd(model, rd, z_s, z_t, chunk_rows, fx, fd, pts=None, ro=None, z=None, code_index=None,
+                            pair=None):
     cs, ct = (z_s, z_t) if code_index is not None else _code_rows(z_s, z_t)
     n_samples = pts.shape[1] if pts is not None else z.shape[1]
-    meta = _field_meta(model, cs, ct, n_samples, chunk_rows, fx, fd, code_index, rd, ro)
+    meta = _field_meta(model, cs, ct, n_samples, chunk_rows, fx, fd, code_index, rd, ro, pair)
     return RadianceField.apply(meta, rd, pts, ro, _d(z), cs, ct, *model.param_list())
 
 

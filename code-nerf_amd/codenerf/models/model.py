@@ -112,15 +112,17 @@ class CodeNeRFModel(torch.nn.Module):
         return ops.mlp_forward(self.packed(), cb, x, index, precision=self.kernel_format())
 
 
-def _field_op(m: CodeNeRFModel, cs, ct, rd, chunk_rows, fx, fd, pts=None, ro=None, z=None, code_index=None):
-    """The fused radiance field (encode + MLP) of ``m`` on distinct code rows cs / ct."""
+def _field_op(m: CodeNeRFModel, cs, ct, rd, chunk_rows, fx, fd, pts=None, ro=None, z=None, code_index=None,
+              pair=None):
+    """The fused radiance field (encode + MLP) of ``m`` on distinct code rows cs / ct (``pair``: the render's
+    autograd.FieldPair, or None)."""
     needs_grad = torch.is_grad_enabled() and (
         any(t is not None and t.requires_grad for t in (rd, cs, ct, pts, ro)) or
         any(p.requires_grad for p in m.param_list()))
     if needs_grad:
         from ..autograd import radiance_field_autograd
         return radiance_field_autograd(m, rd, cs, ct, chunk_rows, fx, fd, pts=pts, ro=ro, z=z,
-                                       code_index=code_index)
+                                       code_index=code_index, pair=pair)
     cb = m.code_bias(cs, ct)
     n_samples = pts.shape[1] if pts is not None else z.shape[1]
     return ops.radiance_field(m.packed(), cb, rd, n_samples, chunk_rows, fx, fd, pts=pts, ro=ro, z=z,

@@ -88,7 +88,7 @@ def _expand_base(z: torch.Tensor) -> torch.Tensor:
     return z[:1]
 
 
-def _field(model, embedders, rd, z_s, z_t, chunk_rows, pts=None, ro=None, z=None):
+def _field(model, embedders, rd, z_s, z_t, chunk_rows, pts=None, ro=None, z=None, pair=None):
     """The fused field of ``model`` (a CodeNeRFModel or a DDP wrapper of one): through the module's
     ``forward`` (its ``field`` form), so a DistributedDataParallel wrapper runs its forward
     bookkeeping and its gradient hooks fire in the backward, as in the reference's DDP training."""
@@ -98,7 +98,8 @@ def _field(model, embedders, rd, z_s, z_t, chunk_rows, pts=None, ro=None, z=None
         return model(cs, ct, field=dict(rd=rd, chunk_rows=chunk_rows, fx=fx, fd=fd, pts=pts, ro=ro, z=z,
                                         code_index=code_index))
     from ..models.model import _field_op
-    return _field_op(_unwrap(model), cs, ct, rd, chunk_rows, fx, fd, pts=pts, ro=ro, z=z, code_index=code_index)
+    return _field_op(_unwrap(model), cs, ct, rd, chunk_rows, fx, fd, pts=pts, ro=ro, z=z, code_index=code_index,
+                     pair=pair)
 
 
 def forward_pass(model, embedders, rd: torch.Tensor, pts: torch.Tensor,
@@ -142,17 +143,20 @@ def render_rays(ro: torch.Tensor, rd: torch.Tensor, z_s: torch.Tensor, z_t: torc
         t_rand = torch.rand(n, ps.num_samples_coarse, dtype=torch.float32, device=ro.device)
     _, z_c = ops.sample_uniform(ro.detach(), rd.detach(), ps.z_vals, ps.lower, ps.upper,
                                 t_rand if ps.perturb else None, want_pts=False)
+    pair = None
     if fine_model is not None and not coarse_only:
         # the two differentiable fields' pre-field launches (code terms, packs, zeroed accumulators) as
         # one launch; each field takes its part (no launch when either runs without gradients)
-        from ..autograd import prefetch_render_prepares
+        from ..autograd import new_field_pair, prefetch_render_prepares
+        if not any(isinstance(m, torch.nn.parallel.DistributedDataParallel) for m in (coarse_model, fine_model)):
+            pair = new_field_pair()     # train_minibatch: the two training backwards in shared launches
         fx, fd = _check_embedders(embedders)
         cs, ct, code_index = _codes(z_s, z_t)
         prefetch_render_prepares(_unwrap(coarse_model), _unwrap(fine_model), rd, ro, cs, ct, ps.num_samples_coarse,
                                  ps.num_samples_coarse + ps.num_samples_fine, chunk_rows, fx, fd, code_index)
     # pts = ro + rd z is formed inside the field kernel (z detached, point_sampler.py:115); with
     # gradients on, the field's backward returns d ro / d rd through both the points and the view dirs
-    raw_c = timed_field(coarse_model, embedders, rd, z_s, z_t, chunk_rows, ro=ro, z=z_c)
+    raw_c = timed_field(coarse_model, embedders, rd, z_s, z_t, chunk_rows, ro=ro, z=z_c, pair=pair)
     rgb_c, disp_c, acc_c, w_c, depth_c = volume_render(raw_c, z_c, rd)
     out = {"rgb_coarse": rgb_c, "disp_coarse": disp_c, "acc_coarse": acc_c, "weights_coarse": w_c,
            "depth_coarse": depth_c, "z_coarse": z_c}
@@ -162,7 +166,7 @@ def render_rays(ro: torch.Tensor, rd: torch.Tensor, z_s: torch.Tensor, z_t: torc
         u = torch.rand(n, ps.num_samples_fine, dtype=torch.float32, device=ro.device)
     _, z_f = ops.sample_pdf(ro.detach(), rd.detach(), w_c.detach()[..., 1:-1], z_c, ps.num_samples_fine,
                             u if ps.perturb else ps.u_lin, want_pts=False)
-    raw_f = timed_field(fine_model, embedders, rd, z_s, z_t, chunk_rows, ro=ro, z=z_f)
+    raw_f = timed_field(fine_model, embedders, rd, z_s, z_t, chunk_rows, ro=ro, z=z_f, pair=pair)
     rgb_f, disp_f, acc_f, _, depth_f = volume_render(raw_f, z_f, rd)
     out.update({"rgb_fine": rgb_f, "disp_fine": disp_f, "acc_fine": acc_f, "depth_fine": depth_f, "z_fine": z_f})
     return out

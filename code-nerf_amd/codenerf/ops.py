@@ -563,45 +563,73 @@ def field_backward_train(packed_t: Tensor, params: Sequence[Tensor], masks: Tens
     """Fused training backward (one dX launch + deterministic dW GEMMs) -> dict g_code / d_pts / d_ro / d_rd.
     precision "f32" (packed_t "f32_w16_t") or "bf16x3" (packed_t "bf16x3_t", 3xbf16 dW GEMMs).
     ``g_code``: a zeroed (n_codes, CN_CODE_BIAS_STRIDE) accumulator (field_prepare's), else allocated."""
+    return field_backward_train_multi([dict(
+        packed_t=packed_t, params=params, masks=masks, saved=saved, x_enc=x_enc, d_raw=d_raw, n_rays=n_rays,
+        n_samples=n_samples, chunk_rows=chunk_rows, n_codes=n_codes, freqs_xyz=freqs_xyz, freqs_dir=freqs_dir, rd=rd,
+        pts=pts, ro=ro, z=z, code_index=code_index, param_grads=param_grads, want_pts=want_pts, want_ro=want_ro,
+        want_rd=want_rd, g_code=g_code)], precision)[0]
+
+
+def field_backward_train_multi(fields: Sequence[dict], precision: str = "f32"):
+    """The training backwards of a render's fields (field_backward_train's keyword arguments, one dict
+    per field, 1 or 2) through ONE cn_field_backward_train_multi call: with two fp32 fields on rays +
+    depths, one dX launch, one batched dW launch, one layer_xyz1 launch and one reduction launch for
+    both, every gradient bitwise that of the per-field calls -> one result dict per field."""
+    assert len(fields) in (1, 2)
     fmt_t = _lib.CN_FMT_BF16X3_T if precision == "bf16x3" else _lib.CN_FMT_F32_W16_T
     lib = _lib_ready()
-    m = n_rays * n_samples
-    params = [_cuda(p.detach(), f"param{i}") for i, p in enumerate(params)]
-    d_raw = _aligned16(_cuda(d_raw, "d_raw"))
-    assert d_raw.numel() == 4 * m and saved.shape == (5, m, 256) and (x_enc is None or x_enc.shape == (m, 90))
-    if m and precision != "bf16x3" and x_enc is None:
-        # the fp32 backward reads the forward's encoding plane at saved + 5 M 256 (cn_field_backward_train_fmt):
-        # ``saved`` must be radiance_field_train_w16's view of its whole save buffer, not a copy of the planes
-        need = 4 * int(lib.cn_field_train_saved_floats(_lib.CN_FMT_F32_W16, m))
-        assert saved.is_contiguous() and saved.storage_offset() == 0 and \
-            saved.untyped_storage().nbytes() >= need, \
-            "field_backward_train: saved must be the training forward's own buffer (planes + encoding plane)"
-    dev = d_raw.device
-    rd, pts, ro, z = _opt(rd, "rd"), _opt(pts, "pts"), _opt(ro, "ro"), _opt(z, "z")
-    if code_index is not None:
-        code_index = _cuda(code_index, "code_index", torch.int64)
-    ws = torch.empty(max(0, int(lib.cn_field_backward_train_workspace_floats(m))), device=dev, dtype=torch.float32)
-    if g_code is None:
-        g_code = torch.zeros(n_codes, _lib.CN_CODE_BIAS_STRIDE, device=dev, dtype=torch.float32)
-    else:
-        assert g_code.shape == (n_codes, _lib.CN_CODE_BIAS_STRIDE) and g_code.is_contiguous()
-    d_pts = torch.empty(n_rays, n_samples, 3, device=dev, dtype=torch.float32) if want_pts else None
-    d_ro = torch.zeros(n_rays, 3, device=dev, dtype=torch.float32) if want_ro else None
-    d_rd = torch.zeros(n_rays, 3, device=dev, dtype=torch.float32) if want_rd else None
-    if m == 0:      # no samples: nothing accumulates (the C ABI refuses n_rays == 0)
-        return {"g_code": g_code, "d_pts": d_pts, "d_ro": d_ro, "d_rd": d_rd}
-    arr, keep = _lib.pointer_array(params)
-    garr, gkeep = (None, None)
-    if param_grads is not None:
-        assert len(param_grads) == _lib.CN_NUM_PARAMS and all(g.is_contiguous() for g in param_grads)
-        garr, gkeep = _lib.pointer_array(list(param_grads))
-    check(lib.cn_field_backward_train_fmt(fmt_t, ptr(packed_t), arr, ptr(masks), ptr(saved), ptr(x_enc), ptr(d_raw),
-                                          ptr(pts), ptr(ro), ptr(rd), ptr(z), n_rays, n_samples, chunk_rows,
-                                          ptr(code_index), n_codes, _lib.host_floats(freqs_xyz),
-                                          _lib.host_floats(freqs_dir), ptr(ws), garr, ptr(g_code), ptr(d_pts),
-                                          ptr(d_ro), ptr(d_rd), stream_of(d_raw)), "cn_field_backward_train_fmt")
-    del keep, gkeep
-    return {"g_code": g_code, "d_pts": d_pts, "d_ro": d_ro, "d_rd": d_rd}
+    outs, structs, keep = [], [], []
+    stream = None
+    for f in fields:
+        n_rays, n_samples, n_codes = f["n_rays"], f["n_samples"], f["n_codes"]
+        m = n_rays * n_samples
+        params = [_cuda(p.detach(), f"param{i}") for i, p in enumerate(f["params"])]
+        d_raw = _aligned16(_cuda(f["d_raw"], "d_raw"))
+        saved, x_enc = f["saved"], f.get("x_enc")
+        assert d_raw.numel() == 4 * m and saved.shape == (5, m, 256) and (x_enc is None or x_enc.shape == (m, 90))
+        if m and precision != "bf16x3" and x_enc is None:
+            # the fp32 backward reads the forward's encoding plane at saved + 5 M 256 (cn_field_backward_train_fmt):
+            # ``saved`` must be radiance_field_train_w16's view of its whole save buffer, not a copy of the planes
+            need = 4 * int(lib.cn_field_train_saved_floats(_lib.CN_FMT_F32_W16, m))
+            assert saved.is_contiguous() and saved.storage_offset() == 0 and \
+                saved.untyped_storage().nbytes() >= need, \
+                "field_backward_train: saved must be the training forward's own buffer (planes + encoding plane)"
+        dev = d_raw.device
+        rd, pts, ro, z = _opt(f["rd"], "rd"), _opt(f.get("pts"), "pts"), _opt(f.get("ro"), "ro"), _opt(f.get("z"), "z")
+        code_index = f.get("code_index")
+        if code_index is not None:
+            code_index = _cuda(code_index, "code_index", torch.int64)
+        ws = torch.empty(max(0, int(lib.cn_field_backward_train_workspace_floats(m))), device=dev, dtype=torch.float32)
+        g_code = f.get("g_code")
+        if g_code is None:
+            g_code = torch.zeros(n_codes, _lib.CN_CODE_BIAS_STRIDE, device=dev, dtype=torch.float32)
+        else:
+            assert g_code.shape == (n_codes, _lib.CN_CODE_BIAS_STRIDE) and g_code.is_contiguous()
+        d_pts = torch.empty(n_rays, n_samples, 3, device=dev, dtype=torch.float32) if f.get("want_pts") else None
+        d_ro = torch.zeros(n_rays, 3, device=dev, dtype=torch.float32) if f.get("want_ro") else None
+        d_rd = torch.zeros(n_rays, 3, device=dev, dtype=torch.float32) if f.get("want_rd") else None
+        outs.append({"g_code": g_code, "d_pts": d_pts, "d_ro": d_ro, "d_rd": d_rd})
+        if m == 0:      # no samples: nothing accumulates (the C ABI refuses n_rays == 0)
+            continue
+        arr, k1 = _lib.pointer_array(params)
+        garr, k2 = (None, None)
+        pg = f.get("param_grads")
+        if pg is not None:
+            assert len(pg) == _lib.CN_NUM_PARAMS and all(g.is_contiguous() for g in pg)
+            garr, k2 = _lib.pointer_array(list(pg))
+        fx, fd = _lib.host_floats(f["freqs_xyz"]), _lib.host_floats(f["freqs_dir"])
+        keep += [params, d_raw, ws, arr, k1, garr, k2, fx, fd, rd, pts, ro, z, code_index]
+        structs.append(_lib.FieldTrainBwd(
+            ptr(f["packed_t"]), arr, ptr(f["masks"]), ptr(saved), ptr(x_enc), ptr(d_raw), ptr(pts), ptr(ro), ptr(rd),
+            ptr(z), n_rays, n_samples, f["chunk_rows"], ptr(code_index), n_codes,
+            ctypes.cast(fx, ctypes.POINTER(ctypes.c_float)), ctypes.cast(fd, ctypes.POINTER(ctypes.c_float)), ptr(ws),
+            garr, ptr(g_code), ptr(d_pts), ptr(d_ro), ptr(d_rd)))
+        stream = stream_of(d_raw)
+    if structs:
+        jobs = (_lib.FieldTrainBwd * len(structs))(*structs)
+        check(lib.cn_field_backward_train_multi(fmt_t, jobs, len(structs), stream), "cn_field_backward_train_multi")
+    del keep
+    return outs
 
 
 def mlp_forward_train(packed: Tensor, cb: Tensor, x: Tensor, code_index: Optional[Tensor] = None

@@ -33,7 +33,7 @@ import torch.distributed as dist
 from . import nerf
 from .models import CodeNeRFModel, ShapeTextureEmbedding, get_params_tensor
 from .optim import AdamW
-from .autograd import backward_from, render_loss_autograd
+from .autograd import backward_from, paired_fields, render_loss_autograd
 from .utils import get_minibatches, mse2psnr
 
 
@@ -119,14 +119,16 @@ def train_minibatch(models, optimizer, scheduler, point_sampler, embedders, ro, 
     read back every chunk as train.py:105 does).  ``uniforms``: (t_rand, u), the stratified / fine
     draws of point_sampler.py:64,93 injected (parity tests) instead of drawn on the device."""
     target_object_embedding = models["embedding"](object_ids)
-    if uniforms is None:
-        rgb_coarse, rgb_fine = nerf.predict_radiance_and_render((ro, rd), point_sampler, embedders,
-                                                                models["nerf_coarse"], models["nerf_fine"],
-                                                                target_object_embedding)
-    else:
-        out = nerf.render_rays(ro, rd, *target_object_embedding, point_sampler, embedders, models["nerf_coarse"],
-                               models["nerf_fine"], t_rand=uniforms[0], u=uniforms[1])
-        rgb_coarse, rgb_fine = out["rgb_coarse"], out["rgb_fine"]
+    # both fields' training backwards in shared launches (autograd.FieldPair): the loss below reaches both
+    with paired_fields():
+        if uniforms is None:
+            rgb_coarse, rgb_fine = nerf.predict_radiance_and_render((ro, rd), point_sampler, embedders,
+                                                                    models["nerf_coarse"], models["nerf_fine"],
+                                                                    target_object_embedding)
+        else:
+            out = nerf.render_rays(ro, rd, *target_object_embedding, point_sampler, embedders, models["nerf_coarse"],
+                                   models["nerf_fine"], t_rand=uniforms[0], u=uniforms[1])
+            rgb_coarse, rgb_fine = out["rgb_coarse"], out["rgb_fine"]
     # mse coarse + mse fine + lambda (||shape table|| + ||texture table||) on .data (a constant):
     # one cn_render_loss launch forward, one backward into the two rgb tensors
     shape_params, texture_params = get_params_tensor(models["embedding"], is_distributed)

@@ -260,7 +260,7 @@ struct ReduceJob {
   int N, K;
   float* C2;  // a second target (g_code's entries that are also bias gradients), or null
 };
-constexpr int kMaxReduceJobs = 16;
+constexpr int kMaxReduceJobs = 32;   // a training backward queues <= 15 per field; two fields flush together
 struct ReduceJobs {
   ReduceJob j[kMaxReduceJobs];
   int n;
@@ -674,7 +674,7 @@ struct TnJob {
   int first_block, n_blocks;
   DirFold dir;
 };
-constexpr int kMaxTnJobs = 5;
+constexpr int kMaxTnJobs = 10;   // a field's five, or a render's two fields' (tn_batch_launch2)
 struct TnJobs {
   TnJob j[kMaxTnJobs];
   int n;
@@ -1427,15 +1427,15 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __rest
 // the encodings are exactly the forward's (lazy fast_sincosf or ocml sincosf, per wave).
 // Wave w: output rows 32 w .. + 31, both 32-column blocks (c' 0..63); fp32 32x32x2.
 constexpr int kXRS = 288, kXES = 96;   // LDS row strides (floats): 32 banks between a pair's rows
-__global__ __launch_bounds__(512, 1) void gemm_tn_xenc_kernel(const float* __restrict__ A, const float* __restrict__ X,
-                                                              int64_t M, float* __restrict__ part,
-                                                              float* __restrict__ bias_part, int64_t rows_per_block,
-                                                              mlp::FieldArgs a, DirRole dr) {
-  if (blockIdx.x < dr.n) {
-    dir_enc_dw_block(a, dr.dir, dr.part, dr.bias_part, blockIdx.x);
+__device__ __forceinline__ void xenc_body(const float* __restrict__ A, const float* __restrict__ X, int64_t M,
+                                          float* __restrict__ part, float* __restrict__ bias_part,
+                                          int64_t rows_per_block, const mlp::FieldArgs& a, const DirRole& dr,
+                                          const unsigned bid) {
+  if (bid < dr.n) {
+    dir_enc_dw_block(a, dr.dir, dr.part, dr.bias_part, bid);
     return;
   }
-  const unsigned blk = blockIdx.x - dr.n;
+  const unsigned blk = bid - dr.n;
   __shared__ __attribute__((aligned(16))) float ring[kEncRing][kEncRows * kXRS];
   __shared__ __attribute__((aligned(16))) float xring[kEncRing][kEncRows * kXES];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1505,6 +1505,36 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_xenc_kernel(const float* __res
     const float b = bsum + __shfl_xor(bsum, 32);
     if (h == 0) bias_part[(int64_t)blk * 256 + 32 * wave + i] = b;
   }
+}
+
+__global__ __launch_bounds__(512, 1) void gemm_tn_xenc_kernel(const float* __restrict__ A, const float* __restrict__ X,
+                                                              int64_t M, float* __restrict__ part,
+                                                              float* __restrict__ bias_part, int64_t rows_per_block,
+                                                              mlp::FieldArgs a, DirRole dr) {
+  xenc_body(A, X, M, part, bias_part, rows_per_block, a, dr, blockIdx.x);
+}
+
+// One field's layer_xyz1 dW pass (gemm_tn_xenc_kernel's arguments).
+struct XencJob {
+  const float* A;
+  const float* X;
+  int64_t M;
+  float* part;
+  float* bias_part;
+  int64_t rows_per_block;
+  mlp::FieldArgs a;
+  DirRole dr;
+};
+
+// A render's two fields' layer_xyz1 dW passes in one launch: workgroups 0 .. first1 - 1 are field j0's
+// launch (its DIRS role blocks, then its row blocks), the rest field j1's -- each the same blocks with the
+// same rows as its own launch (bitwise the same partials).  Two instances of the body, each reading its
+// own kernel argument (no runtime select between the structs).
+__global__ __launch_bounds__(512, 1) void gemm_tn_xenc2_kernel(XencJob j0, XencJob j1, unsigned first1) {
+  if (blockIdx.x >= first1)
+    xenc_body(j1.A, j1.X, j1.M, j1.part, j1.bias_part, j1.rows_per_block, j1.a, j1.dr, blockIdx.x - first1);
+  else
+    xenc_body(j0.A, j0.X, j0.M, j0.part, j0.bias_part, j0.rows_per_block, j0.a, j0.dr, blockIdx.x);
 }
 
 __global__ __launch_bounds__(256) void dir_enc_dw_kernel(mlp::FieldArgs a, DirFold dir, float* __restrict__ part,
@@ -2943,6 +2973,16 @@ static bool dir_in_enc_enabled() {
   return on != 0;
 }
 
+// CN_FIELD_PAIR=0: a render's two fields' backward and dW launches one field after the other (A/B;
+// bitwise the same gradients)
+static bool pair_enabled() {
+  static const int on = [] {
+    const char* e = getenv("CN_FIELD_PAIR");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return on != 0;
+}
+
 static bool tn_jobs_enabled() {
   static const int on = [] {
     const char* e = getenv("CN_TN_JOBS");
@@ -2975,14 +3015,14 @@ static bool dirs_foldable(const mlp::FieldArgs& a) {
          a.m >= 64 * 1024;
 }
 
-// dir_out: when set, the DIRS fold's dir_enc_dw work is not launched here but returned as a role
-// for the next gemm_tn_enc launch (its partials' reductions are queued here either way).
-static int tn_batch_launch(TnBatch& b, bool x3, hipStream_t st, Reducer* rd, grad::DirRole* dir_out = nullptr) {
-  if (b.n == 0) return CN_OK;
+// The batched launch's jobs for one TnBatch: the grid split over the jobs in proportion to their rows
+// times their per-row cost (kGrid workgroups), each job's partial tiles taken from the reducer.  -> the
+// workgroups the jobs use.
+static int tn_batch_plan(TnBatch& b, Reducer* rd, grad::TnJobs& jobs) {
   double total = 0.0;
   for (int k = 0; k < b.n; ++k) total += b.p[k].cost * static_cast<double>(b.p[k].M);
   constexpr int kGrid = 256;  // one workgroup per CU (the ring fills the LDS)
-  grad::TnJobs jobs = {};
+  jobs = {};
   jobs.n = b.n;
   int first = 0;
   for (int k = 0; k < b.n; ++k) {
@@ -3024,9 +3064,19 @@ static int tn_batch_launch(TnBatch& b, bool x3, hipStream_t st, Reducer* rd, gra
     j.sig_part = q.kind == 1 ? rd->take((int64_t)j.n_blocks * 256) : nullptr;
     first += j.n_blocks;
   }
-  if (x3) hipLaunchKernelGGL(grad::gemm_tn256_jobs_kernel<true>, dim3(static_cast<unsigned>(first)), dim3(512), 0, st, jobs);
-  else hipLaunchKernelGGL(grad::gemm_tn256_jobs_kernel<false>, dim3(static_cast<unsigned>(first)), dim3(512), 0, st, jobs);
-  CN_TRY(launch_status());
+  return first;
+}
+
+static int tn_jobs_launch(const grad::TnJobs& jobs, int grid, bool x3, hipStream_t st) {
+  if (x3) hipLaunchKernelGGL(grad::gemm_tn256_jobs_kernel<true>, dim3(static_cast<unsigned>(grid)), dim3(512), 0, st, jobs);
+  else hipLaunchKernelGGL(grad::gemm_tn256_jobs_kernel<false>, dim3(static_cast<unsigned>(grid)), dim3(512), 0, st, jobs);
+  return launch_status();
+}
+
+// After the launch: the fixed-order sums of every job's partials queued on the reducer (the DIRS job's
+// dir_enc_dw pass launched here, or -- dir_out set -- returned as a role for the next gemm_tn_enc /
+// gemm_tn_xenc launch; its partials' reductions are queued here either way).
+static int tn_batch_post(TnBatch& b, const grad::TnJobs& jobs, hipStream_t st, Reducer* rd, grad::DirRole* dir_out) {
   for (int k = 0; k < b.n; ++k) {
     const TnBatch::Pending& q = b.p[k];
     const grad::TnJob& j = jobs.j[k];
@@ -3058,6 +3108,53 @@ static int tn_batch_launch(TnBatch& b, bool x3, hipStream_t st, Reducer* rd, gra
   }
   b.n = 0;
   return CN_OK;
+}
+
+static int tn_batch_launch(TnBatch& b, bool x3, hipStream_t st, Reducer* rd, grad::DirRole* dir_out = nullptr) {
+  if (b.n == 0) return CN_OK;
+  grad::TnJobs jobs;
+  const int grid = tn_batch_plan(b, rd, jobs);
+  CN_TRY(tn_jobs_launch(jobs, grid, x3, st));
+  return tn_batch_post(b, jobs, st, rd, dir_out);
+}
+
+// Two fields' batches (a render's coarse and fine backward) as ONE launch: each field's jobs keep the
+// split of their own launch (the same workgroup counts and rows, so the same partial tiles), field 1's
+// workgroups after field 0's -- they start on the CUs field 0's leave, filling its finish spread.
+static int tn_batch_launch2(TnBatch& b0, Reducer* r0, grad::DirRole* d0, TnBatch& b1, Reducer* r1,
+                            grad::DirRole* d1, bool x3, hipStream_t st) {
+  if (b0.n == 0 || b1.n == 0 || b0.n + b1.n > grad::kMaxTnJobs) {
+    CN_TRY(tn_batch_launch(b0, x3, st, r0, d0));
+    return tn_batch_launch(b1, x3, st, r1, d1);
+  }
+  grad::TnJobs j0, j1, both = {};
+  const int g0 = tn_batch_plan(b0, r0, j0);
+  const int g1 = tn_batch_plan(b1, r1, j1);
+  both.n = j0.n + j1.n;
+  for (int k = 0; k < j0.n; ++k) both.j[k] = j0.j[k];
+  for (int k = 0; k < j1.n; ++k) {
+    both.j[j0.n + k] = j1.j[k];
+    both.j[j0.n + k].first_block += g0;
+  }
+  CN_TRY(tn_jobs_launch(both, g0 + g1, x3, st));
+  CN_TRY(tn_batch_post(b0, j0, st, r0, d0));
+  return tn_batch_post(b1, j1, st, r1, d1);
+}
+
+// Two reducers' queued sums in one launch (each sum is computed exactly as in its own flush).
+static int flush2(Reducer& a, Reducer& b) {
+  if (a.jobs.n + b.jobs.n > grad::kMaxReduceJobs) {
+    CN_TRY(a.flush());
+    return b.flush();
+  }
+  for (int k = 0; k < b.jobs.n; ++k) {
+    a.jobs.j[a.jobs.n] = b.jobs.j[k];
+    a.jobs.j[a.jobs.n++].first_block += a.blocks;
+  }
+  a.blocks += b.blocks;
+  b.jobs.n = 0;
+  b.blocks = 0;
+  return a.flush();
 }
 
 // fc_rgb's dW (C += d rgb^T v2, d_raw's columns 0..2) and, in the same pass, the d raw column sums
@@ -3152,6 +3249,247 @@ extern "C" int cn_field_backward_train(const float* packed_t, const float* const
                                      workspace, grads, g_code, d_pts, d_ro, d_rd, stream);
 }
 
+// One field of a training backward: cn_field_backward_train_fmt's arguments and launch state, run in
+// stages so that a render's two fields can share their launches (cn_field_backward_train_multi).
+struct TrainBwd {
+  bool x3 = false, wg = false, fold_code = false, jobs = false, rgb_role = false, dual_code = false, dirs = false;
+  int mode = 0;
+  mlp::FieldArgs a = {};
+  const float* saved = nullptr;
+  const float* x_enc = nullptr;
+  const float* d_raw = nullptr;
+  float* const* grads = nullptr;
+  float* g_code = nullptr;
+  float* workspace = nullptr;
+  const float* P[5] = {};
+  Reducer red = {};
+  TnBatch tb;
+  grad::DirRole dir_role = {};
+};
+
+static int train_bwd_setup(int fmt_t, const cn_field_train_bwd& f, TrainBwd& t) {
+  using namespace mlp;
+  CN_CHECK_ARG(fmt_t == CN_FMT_F32_W16_T || fmt_t == CN_FMT_BF16X3_T);
+  t.x3 = fmt_t == CN_FMT_BF16X3_T;
+  CN_CHECK_ARG(f.packed_t && f.params && f.masks && f.saved && f.d_raw && f.rd && f.g_code && f.workspace);
+  CN_CHECK_ARG(f.freqs_xyz && f.freqs_dir && f.n_rays > 0 && f.n_samples > 0 && f.chunk_rows > 0 && f.n_codes > 0);
+  CN_CHECK_ARG(f.pts || (f.ro && f.z));
+  CN_CHECK_ARG(!f.d_pts || f.pts);
+  CN_CHECK_ARG(!f.d_ro || (f.ro && f.z && !f.pts));
+  CN_CHECK_ARG(f.code_index || f.n_codes == 1 || f.n_codes == f.n_rays);
+  for (int i = 0; i < CN_NUM_PARAMS; ++i) CN_CHECK_ARG(f.params[i]);
+  // one code row per wave (32 samples x3, 16 samples w16)
+  if (!(f.n_codes == 1 || f.n_samples % (t.x3 ? 32 : 16) == 0)) return CN_EUNSUPPORTED;
+  const int64_t M = f.n_rays * f.n_samples;
+  CN_CHECK_ARG(ceil_div(M, 128) <= 0x7fffffff);
+  CN_CHECK_ARG(cn::aligned16(f.d_raw));  // float4 rows (include/codenerf.h)
+  FieldArgs& a = t.a;
+  a = {};
+  a.packed = f.packed_t;
+  a.code_index = f.code_index;
+  a.n_codes = f.n_codes;
+  a.pts = f.pts;
+  a.ro = f.ro;
+  a.rd = f.rd;
+  a.z = f.z;
+  a.n_rays = f.n_rays;
+  a.n_samples = f.n_samples;
+  a.chunk_rows = f.chunk_rows;
+  a.m = M;
+  for (int i = 0; i < 10; ++i) a.fx[i] = f.freqs_xyz[i];
+  for (int i = 0; i < 4; ++i) a.fd[i] = f.freqs_dir[i];
+  a.masks = const_cast<uint32_t*>(f.masks);
+  a.d_raw = f.d_raw;
+  a.g_code = f.g_code;
+  a.d_pts = f.d_pts;
+  a.d_ro = f.d_ro;
+  a.d_rd = f.d_rd;
+  a.dpre = f.workspace;
+  t.mode = f.pts ? kFromPts : kFromRayZ;
+  t.saved = f.saved;
+  t.x_enc = f.x_enc;
+  t.d_raw = f.d_raw;
+  t.grads = f.grads;
+  t.g_code = f.g_code;
+  t.workspace = f.workspace;
+  t.wg = f.grads && f.grads[0];
+  // the bias gradients of layer_dir2 / layer_dir1 / layer_xyz1 are column sums of their dPre planes,
+  // folded into the dW kernels below that stream those planes (deterministic partials), so the
+  // fused backward sums none of them (a.gbias stays null).  With ONE code row (a chunk of one
+  // object: every C3 step) g_code is column sums too -- of d feat (plane 2), of layer_xyz2's dPre
+  // (plane 3) and of d raw -- folded the same way, so the step is deterministic in both precisions
+  // (no float atomics anywhere in it) and the fused kernel skips its code sums (fp32) or leaves its
+  // LDS sums unflushed (3xbf16).
+  t.fold_code = t.wg && f.n_codes == 1;
+  if (t.fold_code) a.g_code = nullptr;
+  for (int k = 0; k < 5; ++k) t.P[k] = f.workspace + k * M * 256;
+  t.red = Reducer{nullptr, f.workspace + 5 * M * 256, {}, 0};
+  t.jobs = tn_jobs_enabled() && M >= 64 * 1024;
+  // fc_rgb (h half): dW += d rgb^T v2 (+ g_code's rgb / sigma entries, folded, in the same pass); as the
+  // batched launch's RGB role where that runs (fp32, folded code)
+  t.rgb_role = t.jobs && t.fold_code && !t.x3;
+  t.dual_code = t.rgb_role;  // the g_code sums also land in the bias gradients (below)
+  t.dirs = t.jobs && !t.x3 && !t.x_enc && dirs_foldable(a);
+  return CN_OK;
+}
+
+// After the dX launch, up to the batched dW launch: the launches before it and the jobs queued (t.tb;
+// without the batched plan, the four 256 x 256 GEMMs run here one by one).
+static int train_bwd_queue(TrainBwd& t, hipStream_t st) {
+  using namespace mlp;
+  t.red.st = st;
+  const int64_t M = t.a.m;
+  float* const* grads = t.grads;
+  auto G = [&](int i) { return grads[i]; };
+  auto B = [&](int i) { return grads[i]; };  // bias folded into this GEMM
+  // biases: layer_dir2 / layer_dir1 / layer_xyz1 summed in the kernel; the others are g_code's
+  // column sums (after the deferred reduction when g_code itself is folded)
+  if (!t.fold_code) {
+    hipLaunchKernelGGL(grad::gcode_bias_kernel, dim3(3), dim3(256), 0, st, t.g_code, t.a.n_codes, G(kBXyz2), G(kBOut),
+                       G(kBRgb));
+    CN_TRY(launch_status());
+  }
+  float* const gc_feat = t.fold_code ? t.g_code + kCbFeat : nullptr;
+  float* const gc_xyz2 = t.fold_code ? t.g_code + kCbXyz2 : nullptr;
+  float* const ws = nullptr;
+  float* const bws = nullptr;
+  Reducer* red = &t.red;
+  const float* const* P = t.P;
+  const float* h1 = t.saved;
+  const float* h2 = t.saved + M * 256;
+  const float* feat = t.saved + 2 * M * 256;
+  const float* v1 = t.saved + 3 * M * 256;
+  const float* v2 = t.saved + 4 * M * 256;
+  const bool x3 = t.x3;
+  if (t.rgb_role) {
+  } else if (t.fold_code) {
+    CN_TRY(rgb_dw_draw_sums(t.d_raw, v2, G(kWRgb), 512, M, t.g_code + kCbRgb, t.g_code + kCbSigma, st, red));
+  } else {
+    CN_TRY(gemm_tn(t.d_raw, 4, v2, 256, G(kWRgb), 512, M, 3, 256, st, x3, ws, nullptr, nullptr, red));
+  }
+  if (t.jobs) {
+    // the four 256 x 256 layers as ONE whole-tile launch (TnBatch): layer_dir2, layer_dir1 [feat]
+    // (+ its view-encoding columns by the DIRS fold where it applies), fc_out (+ sigma row),
+    // layer_xyz2
+    TnBatch& tb = t.tb;
+    tb.n = 0;
+    const float* c = tn_slot_cost();
+    // with one code row the g_code entries summed here ARE the bias gradients of layer_xyz2, fc_out
+    // and fc_rgb (gcode_bias_kernel's column sums over one row): the reductions add each sum to both
+    // (bias2 / sig2), bitwise gcode_bias_kernel's 0 + g then b + that, and that launch is not needed
+    float* const b_xyz2 = t.dual_code ? G(kBXyz2) : nullptr;
+    float* const b_feat = t.dual_code ? G(kBOut) + 1 : nullptr;
+    tb.p[tb.n++] = {P[0], v1, M, 0, G(kWDir2), 256, B(kBDir2), nullptr, nullptr, {}, c[0], nullptr, nullptr};
+    tb.p[tb.n++] = {P[1], feat, M, t.dirs ? 2 : 0, G(kWDir1), 283, B(kBDir1), nullptr, nullptr, t.a, c[1], nullptr,
+                    nullptr};
+    tb.p[tb.n++] = {P[2], h2, M, 1, G(kWOut) + 512, 512, gc_feat, t.d_raw + 3, G(kWOut), {}, c[2], b_feat, nullptr};
+    tb.p[tb.n++] = {P[3], h1, M, 0, G(kWXyz2), 512, gc_xyz2, nullptr, nullptr, {}, c[3], b_xyz2, nullptr};
+    if (t.rgb_role)
+      tb.p[tb.n++] = {t.d_raw, v2, M, 3, G(kWRgb), 512, t.g_code + kCbRgb, t.d_raw, t.g_code + kCbSigma, {}, c[4],
+                      t.dual_code ? G(kBRgb) : nullptr, t.dual_code ? G(kBOut) : nullptr};
+    return CN_OK;
+  }
+  // layer_dir2
+  CN_TRY(gemm_tn(P[0], 256, v1, 256, G(kWDir2), 256, M, 256, 256, st, x3, ws, B(kBDir2), bws, red));
+  // layer_dir1: [feat | dir enc]
+  const int64_t dir1_budget =
+      tn_ws_floats(M, 256, 256) + std::max(tn_ws_floats(M, 256, 27), enc_parts(M) * 256 * 27) + dirs_ws_floats(M);
+  const int folded = x3 || t.x_enc ? CN_EUNSUPPORTED
+                                   : dir1_dw_folded(P[1], feat, G(kWDir1), B(kBDir1), t.a, st, red, dir1_budget);
+  if (folded != CN_OK) {
+    if (folded != CN_EUNSUPPORTED) return folded;
+    CN_TRY(gemm_tn(P[1], 256, feat, 256, G(kWDir1), 283, M, 256, 256, st, x3, ws, B(kBDir1), bws, red));
+    if (t.x_enc)
+      CN_TRY(gemm_tn(P[1], 256, t.x_enc + 63, 90, G(kWDir1) + 256, 283, M, 256, 27, st, x3, ws, nullptr, nullptr, red));
+    else CN_TRY(gemm_tn_enc(1, P[1], t.a, G(kWDir1) + 256, 283, st, x3, ws, nullptr, nullptr, red));
+  }
+  // fc_out (h half): row 0 from d sigma, rows 1.. from d feat
+  CN_TRY(gemm_tn(P[2], 256, h2, 256, G(kWOut) + 512, 512, M, 256, 256, st, x3, ws, gc_feat, bws, red, t.d_raw + 3,
+                 G(kWOut)));
+  // layer_xyz2 (h half)
+  return gemm_tn(P[3], 256, h1, 256, G(kWXyz2), 512, M, 256, 256, st, x3, ws, gc_xyz2, bws, red);
+}
+
+// The DIRS fold's per-direction pass rides in layer_xyz1's encoding dW launch when that is a gemm_tn_enc /
+// gemm_tn_xenc launch: one launch fewer per field and chunk.
+static grad::DirRole* train_bwd_dir_out(TrainBwd& t) {
+  return t.jobs && t.dirs && !t.x_enc && dir_in_enc_enabled() ? &t.dir_role : nullptr;
+}
+
+// After the batched launch: layer_dir1's view columns where the DIRS fold did not take them.
+static int train_bwd_after_jobs(TrainBwd& t, hipStream_t st) {
+  using namespace mlp;
+  if (!t.jobs || t.dirs) return CN_OK;
+  float* C = t.grads[kWDir1] + 256;
+  if (t.x_enc) return gemm_tn(t.P[1], 256, t.x_enc + 63, 90, C, 283, t.a.m, 256, 27, st, t.x3, nullptr, nullptr, nullptr, &t.red);
+  return gemm_tn_enc(1, t.P[1], t.a, C, 283, st, t.x3, nullptr, nullptr, nullptr, &t.red);
+}
+
+// layer_xyz1's dW reads the fp32 forward's own encodings (saved's encoding plane)
+static bool train_bwd_xenc(const TrainBwd& t) { return !t.x_enc && !t.x3 && xenc_plane_enabled(); }
+
+// layer_xyz1 (its own launch: as a role of the batched launch it ran no faster per CU -- it is compute
+// work, not a bandwidth pass that could hide beside the GEMMs; r03m)
+static int train_bwd_xyz1(TrainBwd& t, hipStream_t st) {
+  using namespace mlp;
+  float* C = t.grads[kWXyz1];
+  float* bias = t.grads[kBXyz1];
+  if (t.x_enc)
+    return gemm_tn(t.P[4], 256, t.x_enc, 90, C, 63, t.a.m, 256, 63, st, t.x3, nullptr, bias, nullptr, &t.red);
+  if (train_bwd_xenc(t)) return gemm_tn_xenc(t.P[4], t.saved + 5 * t.a.m * 256, t.a, C, 63, st, bias, &t.red, t.dir_role);
+  return gemm_tn_enc(0, t.P[4], t.a, C, 63, st, t.x3, nullptr, bias, nullptr, &t.red, t.dir_role);
+}
+
+// Two fields' layer_xyz1 dW passes (gemm_tn_xenc each) as one gemm_tn_xenc2_kernel launch.
+static int train_bwd_xyz1_pair(TrainBwd& t0, TrainBwd& t1, hipStream_t st) {
+  using namespace mlp;
+  grad::XencJob j[2];
+  TrainBwd* t[2] = {&t0, &t1};
+  unsigned blocks[2];
+  for (int f = 0; f < 2; ++f) {
+    const int64_t m = t[f]->a.m, rows = enc_rows(m);
+    const unsigned nb = static_cast<unsigned>(ceil_div(m, rows));
+    float* bias = t[f]->grads[kBXyz1];
+    j[f] = grad::XencJob{t[f]->P[4], t[f]->saved + 5 * m * 256, m, t[f]->red.take((int64_t)nb * 256 * 63),
+                         bias ? t[f]->red.take((int64_t)nb * 256) : nullptr, rows, t[f]->a, t[f]->dir_role};
+    blocks[f] = nb + t[f]->dir_role.n;
+  }
+  hipLaunchKernelGGL(grad::gemm_tn_xenc2_kernel, dim3(blocks[0] + blocks[1]), dim3(512), 0, st, j[0], j[1], blocks[0]);
+  CN_TRY(launch_status());
+  for (int f = 0; f < 2; ++f) {
+    const unsigned nb = blocks[f] - t[f]->dir_role.n;
+    CN_TRY(reduce(&t[f]->red, j[f].part, nb, 256, 63, t[f]->grads[kWXyz1], 63, st));
+    if (j[f].bias_part) CN_TRY(reduce(&t[f]->red, j[f].bias_part, nb, 1, 256, t[f]->grads[kBXyz1], 256, st));
+  }
+  return CN_OK;
+}
+
+// After the deferred reduction: the biases formed from a folded g_code where no reduction did it.
+static int train_bwd_tail(TrainBwd& t, hipStream_t st) {
+  using namespace mlp;
+  if (t.fold_code && !t.dual_code) {
+    hipLaunchKernelGGL(grad::gcode_bias_kernel, dim3(3), dim3(256), 0, st, t.g_code, t.a.n_codes, t.grads[kBXyz2],
+                       t.grads[kBOut], t.grads[kBRgb]);
+    CN_TRY(launch_status());
+  }
+  return CN_OK;
+}
+
+static int train_bwd_dx(TrainBwd& t, hipStream_t st) {
+  return t.x3 ? mlp::launch_field_x3_bwd(t.mode, t.a, st) : mlp::launch_field_w16_bwd(t.mode, t.a, st);
+}
+
+static int train_bwd_one(TrainBwd& t, hipStream_t st) {
+  CN_TRY(train_bwd_dx(t, st));
+  if (!t.wg) return CN_OK;
+  CN_TRY(train_bwd_queue(t, st));
+  if (t.jobs) CN_TRY(tn_batch_launch(t.tb, t.x3, st, &t.red, train_bwd_dir_out(t)));
+  CN_TRY(train_bwd_after_jobs(t, st));
+  CN_TRY(train_bwd_xyz1(t, st));
+  CN_TRY(t.red.flush());
+  return train_bwd_tail(t, st);
+}
+
 extern "C" int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, const float* const* params,
                                            const uint32_t* masks, const float* saved, const float* x_enc,
                                            const float* d_raw, const float* pts, const float* ro, const float* rd,
@@ -3160,148 +3498,43 @@ extern "C" int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, con
                                            const float* freqs_dir, float* workspace, float* const* grads,
                                            float* g_code, float* d_pts, float* d_ro, float* d_rd,
                                            cn_stream_t stream) {
-  using namespace mlp;
-  CN_CHECK_ARG(fmt_t == CN_FMT_F32_W16_T || fmt_t == CN_FMT_BF16X3_T);
-  const bool x3 = fmt_t == CN_FMT_BF16X3_T;
-  CN_CHECK_ARG(packed_t && params && masks && saved && d_raw && rd && g_code && workspace);
-  CN_CHECK_ARG(freqs_xyz && freqs_dir && n_rays > 0 && n_samples > 0 && chunk_rows > 0 && n_codes > 0);
-  CN_CHECK_ARG(pts || (ro && z));
-  CN_CHECK_ARG(!d_pts || pts);
-  CN_CHECK_ARG(!d_ro || (ro && z && !pts));
-  CN_CHECK_ARG(code_index || n_codes == 1 || n_codes == n_rays);
-  for (int i = 0; i < CN_NUM_PARAMS; ++i) CN_CHECK_ARG(params[i]);
-  // one code row per wave (32 samples x3, 16 samples w16)
-  if (!(n_codes == 1 || n_samples % (x3 ? 32 : 16) == 0)) return CN_EUNSUPPORTED;
+  const cn_field_train_bwd f{packed_t, params, masks, saved, x_enc, d_raw, pts, ro, rd, z, n_rays, n_samples, chunk_rows,
+                             code_index, n_codes, freqs_xyz, freqs_dir, workspace, grads, g_code, d_pts, d_ro, d_rd};
+  return cn_field_backward_train_multi(fmt_t, &f, 1, stream);
+}
+
+// A render's fields in shared launches: both fields' dX chains in one field_w16_bwd2_kernel launch, their
+// batched dW GEMMs in one gemm_tn256_jobs_kernel launch, their layer_xyz1 passes in one
+// gemm_tn_xenc2_kernel launch and their deferred sums in one reduction launch -- every launch running
+// each field's workgroups exactly as its own launch would, so every gradient is bitwise that of the
+// per-field calls.  Pairs that cannot share (3xbf16, points input, small chunks without the batched dW
+// plan, x_enc given, different kernel forms) run one after the other.
+extern "C" int cn_field_backward_train_multi(int fmt_t, const cn_field_train_bwd* fields, int n_fields,
+                                             cn_stream_t stream) {
+  CN_CHECK_ARG(fields && (n_fields == 1 || n_fields == 2));
   hipStream_t st = as_stream(stream);
-  const int64_t M = n_rays * n_samples;
-  CN_CHECK_ARG(ceil_div(M, 128) <= 0x7fffffff);
-  FieldArgs a = {};
-  a.packed = packed_t;
-  a.code_index = code_index;
-  a.n_codes = n_codes;
-  a.pts = pts;
-  a.ro = ro;
-  a.rd = rd;
-  a.z = z;
-  a.n_rays = n_rays;
-  a.n_samples = n_samples;
-  a.chunk_rows = chunk_rows;
-  a.m = M;
-  for (int i = 0; i < 10; ++i) a.fx[i] = freqs_xyz[i];
-  for (int i = 0; i < 4; ++i) a.fd[i] = freqs_dir[i];
-  a.masks = const_cast<uint32_t*>(masks);
-  a.d_raw = d_raw;
-  CN_CHECK_ARG(cn::aligned16(d_raw));  // float4 rows (include/codenerf.h)
-  a.g_code = g_code;
-  a.d_pts = d_pts;
-  a.d_ro = d_ro;
-  a.d_rd = d_rd;
-  a.dpre = workspace;
-  const bool wg = grads && grads[0];
-  // the bias gradients of layer_dir2 / layer_dir1 / layer_xyz1 are column sums of their dPre planes,
-  // folded into the dW kernels below that stream those planes (deterministic partials), so the
-  // fused backward sums none of them (a.gbias stays null).  With ONE code row (a chunk of one
-  // object: every C3 step) g_code is column sums too -- of d feat (plane 2), of layer_xyz2's dPre
-  // (plane 3) and of d raw -- folded the same way, so the step is deterministic in both precisions
-  // (no float atomics anywhere in it) and the fused kernel skips its code sums (fp32) or leaves its
-  // LDS sums unflushed (3xbf16).
-  const bool fold_code = wg && n_codes == 1;
-  if (fold_code) a.g_code = nullptr;
-  CN_TRY(x3 ? launch_field_x3_bwd(pts ? kFromPts : kFromRayZ, a, st)
-            : launch_field_w16_bwd(pts ? kFromPts : kFromRayZ, a, st));
-  if (!wg) return CN_OK;
-  auto G = [&](int i) { return grads[i]; };
-  // biases: layer_dir2 / layer_dir1 / layer_xyz1 summed in the kernel; the others are g_code's
-  // column sums (after the deferred reduction when g_code itself is folded)
-  if (!fold_code) {
-    hipLaunchKernelGGL(grad::gcode_bias_kernel, dim3(3), dim3(256), 0, st, g_code, n_codes, G(kBXyz2), G(kBOut),
-                       G(kBRgb));
-    CN_TRY(launch_status());
+  TrainBwd t[2];
+  for (int k = 0; k < n_fields; ++k) CN_TRY(train_bwd_setup(fmt_t, fields[k], t[k]));
+  bool pair = n_fields == 2 && !t[0].x3 && pair_enabled();
+  for (int k = 0; pair && k < 2; ++k)
+    pair = t[k].wg && t[k].jobs && t[k].mode == mlp::kFromRayZ && train_bwd_xenc(t[k]);
+  if (pair) {
+    const int rc = mlp::launch_field_w16_bwd2(mlp::kFromRayZ, t[0].a, t[1].a, st);
+    if (rc == CN_EUNSUPPORTED) pair = false;
+    else if (rc != CN_OK) return rc;
   }
-  float* const gc_feat = fold_code ? g_code + kCbFeat : nullptr;
-  float* const gc_xyz2 = fold_code ? g_code + kCbXyz2 : nullptr;
-  const float* P[5];
-  for (int k = 0; k < 5; ++k) P[k] = workspace + k * M * 256;
-  // partial tiles of every dW GEMM in their own slices, summed by ONE deferred launch
-  Reducer red{st, workspace + 5 * M * 256, {}, 0};
-  float* const ws = nullptr;
-  float* const bws = nullptr;
-  auto B = [&](int i) { return grads[i]; };  // bias folded into this GEMM
-  const float* h1 = saved;
-  const float* h2 = saved + M * 256;
-  const float* feat = saved + 2 * M * 256;
-  const float* v1 = saved + 3 * M * 256;
-  const float* v2 = saved + 4 * M * 256;
-  const bool jobs = tn_jobs_enabled() && M >= 64 * 1024;
-  grad::DirRole dir_role = {};
-  // fc_rgb (h half): dW += d rgb^T v2 (+ g_code's rgb / sigma entries, folded, in the same pass); as
-  // the batched launch's RGB role where that runs (fp32, folded code)
-  const bool rgb_role = jobs && fold_code && !x3;
-  const bool dual_code = rgb_role;  // the g_code sums also land in the bias gradients (below)
-  if (rgb_role) {
-  } else if (fold_code) {
-    CN_TRY(rgb_dw_draw_sums(d_raw, v2, G(kWRgb), 512, M, g_code + kCbRgb, g_code + kCbSigma, st, &red));
-  } else {
-    CN_TRY(gemm_tn(d_raw, 4, v2, 256, G(kWRgb), 512, M, 3, 256, st, x3, ws, nullptr, nullptr, &red));
+  if (!pair) {
+    for (int k = 0; k < n_fields; ++k) CN_TRY(train_bwd_one(t[k], st));
+    return CN_OK;
   }
-  if (jobs) {
-    // the four 256 x 256 layers as ONE whole-tile launch (TnBatch): layer_dir2, layer_dir1 [feat]
-    // (+ its view-encoding columns by the DIRS fold where it applies), fc_out (+ sigma row),
-    // layer_xyz2
-    TnBatch tb;
-    const bool dirs = !x3 && !x_enc && dirs_foldable(a);
-    const float* c = tn_slot_cost();
-    // with one code row the g_code entries summed here ARE the bias gradients of layer_xyz2, fc_out
-    // and fc_rgb (gcode_bias_kernel's column sums over one row): the reductions add each sum to both
-    // (bias2 / sig2), bitwise gcode_bias_kernel's 0 + g then b + that, and that launch is not needed
-    float* const b_xyz2 = dual_code ? G(kBXyz2) : nullptr;
-    float* const b_feat = dual_code ? G(kBOut) + 1 : nullptr;
-    tb.p[tb.n++] = {P[0], v1, M, 0, G(kWDir2), 256, B(kBDir2), nullptr, nullptr, {}, c[0], nullptr, nullptr};
-    tb.p[tb.n++] = {P[1], feat, M, dirs ? 2 : 0, G(kWDir1), 283, B(kBDir1), nullptr, nullptr, a, c[1], nullptr,
-                    nullptr};
-    tb.p[tb.n++] = {P[2], h2, M, 1, G(kWOut) + 512, 512, gc_feat, d_raw + 3, G(kWOut), {}, c[2], b_feat, nullptr};
-    tb.p[tb.n++] = {P[3], h1, M, 0, G(kWXyz2), 512, gc_xyz2, nullptr, nullptr, {}, c[3], b_xyz2, nullptr};
-    if (rgb_role)
-      tb.p[tb.n++] = {d_raw, v2, M, 3, G(kWRgb), 512, g_code + kCbRgb, d_raw, g_code + kCbSigma, {}, c[4],
-                      dual_code ? G(kBRgb) : nullptr, dual_code ? G(kBOut) : nullptr};
-    // the DIRS fold's per-direction pass rides in layer_xyz1's encoding dW launch (below) when that
-    // is a gemm_tn_enc launch: one launch fewer per field and chunk
-    CN_TRY(tn_batch_launch(tb, x3, st, &red, dirs && !x_enc && dir_in_enc_enabled() ? &dir_role : nullptr));
-    if (!dirs) {
-      if (x_enc) CN_TRY(gemm_tn(P[1], 256, x_enc + 63, 90, G(kWDir1) + 256, 283, M, 256, 27, st, x3, ws, nullptr, nullptr, &red));
-      else CN_TRY(gemm_tn_enc(1, P[1], a, G(kWDir1) + 256, 283, st, x3, ws, nullptr, nullptr, &red));
-    }
-  } else {
-    // layer_dir2
-    CN_TRY(gemm_tn(P[0], 256, v1, 256, G(kWDir2), 256, M, 256, 256, st, x3, ws, B(kBDir2), bws, &red));
-    // layer_dir1: [feat | dir enc]
-    const int64_t dir1_budget =
-        tn_ws_floats(M, 256, 256) + std::max(tn_ws_floats(M, 256, 27), enc_parts(M) * 256 * 27) + dirs_ws_floats(M);
-    const int folded = x3 || x_enc ? CN_EUNSUPPORTED
-                                   : dir1_dw_folded(P[1], feat, G(kWDir1), B(kBDir1), a, st, &red, dir1_budget);
-    if (folded != CN_OK) {
-      if (folded != CN_EUNSUPPORTED) return folded;
-      CN_TRY(gemm_tn(P[1], 256, feat, 256, G(kWDir1), 283, M, 256, 256, st, x3, ws, B(kBDir1), bws, &red));
-      if (x_enc) CN_TRY(gemm_tn(P[1], 256, x_enc + 63, 90, G(kWDir1) + 256, 283, M, 256, 27, st, x3, ws, nullptr, nullptr, &red));
-      else CN_TRY(gemm_tn_enc(1, P[1], a, G(kWDir1) + 256, 283, st, x3, ws, nullptr, nullptr, &red));
-    }
-    // fc_out (h half): row 0 from d sigma, rows 1.. from d feat
-    CN_TRY(gemm_tn(P[2], 256, h2, 256, G(kWOut) + 512, 512, M, 256, 256, st, x3, ws, gc_feat, bws, &red, d_raw + 3,
-                   G(kWOut)));
-    // layer_xyz2 (h half)
-    CN_TRY(gemm_tn(P[3], 256, h1, 256, G(kWXyz2), 512, M, 256, 256, st, x3, ws, gc_xyz2, bws, &red));
-  }
-  // layer_xyz1 (its own launch: as a role of the batched launch it ran no faster per CU -- it is
-  // compute work, not a bandwidth pass that could hide beside the GEMMs; r03m)
-  if (x_enc) CN_TRY(gemm_tn(P[4], 256, x_enc, 90, G(kWXyz1), 63, M, 256, 63, st, x3, ws, B(kBXyz1), bws, &red));
-  else if (!x3 && xenc_plane_enabled())   // the fp32 forward's own encodings (saved's encoding plane)
-    CN_TRY(gemm_tn_xenc(P[4], saved + 5 * M * 256, a, G(kWXyz1), 63, st, B(kBXyz1), &red, dir_role));
-  else CN_TRY(gemm_tn_enc(0, P[4], a, G(kWXyz1), 63, st, x3, ws, B(kBXyz1), bws, &red, dir_role));
-  CN_TRY(red.flush());
-  if (fold_code && !dual_code) {
-    hipLaunchKernelGGL(grad::gcode_bias_kernel, dim3(3), dim3(256), 0, st, g_code, n_codes, G(kBXyz2), G(kBOut),
-                       G(kBRgb));
-    CN_TRY(launch_status());
-  }
-  return CN_OK;
+  CN_TRY(train_bwd_queue(t[0], st));
+  CN_TRY(train_bwd_queue(t[1], st));
+  CN_TRY(tn_batch_launch2(t[0].tb, &t[0].red, train_bwd_dir_out(t[0]), t[1].tb, &t[1].red, train_bwd_dir_out(t[1]),
+                          false, st));
+  CN_TRY(train_bwd_after_jobs(t[0], st));
+  CN_TRY(train_bwd_after_jobs(t[1], st));
+  CN_TRY(train_bwd_xyz1_pair(t[0], t[1], st));
+  CN_TRY(flush2(t[0].red, t[1].red));
+  CN_TRY(train_bwd_tail(t[0], st));
+  return train_bwd_tail(t[1], st);
 }

@@ -309,6 +309,7 @@ struct PrepareModel {
 int launch_field_prepare_w16(const PrepareModel* models, int n_models, const float* z_s, const float* z_t,
                              int64_t n_codes, hipStream_t st);
 int launch_field_w16_bwd(int mode, FieldArgs& a, hipStream_t st);
+int launch_field_w16_bwd2(int mode, FieldArgs& a0, FieldArgs& a1, hipStream_t st);
 // cn_field_backward_fused's argument checks, into a (mlp.hip).
 int fused_backward_args(int fmt_t, const float* packed_t, const uint32_t* masks, const float* d_raw,
                         const float* pts, const float* ro, const float* rd, const float* z, int64_t n_rays,

@@ -1431,10 +1431,9 @@ __device__ __forceinline__ void bwd_tile(State& s, const FieldArgs& a, float4* l
   }
 }
 
-template <int MODE, bool TRAIN, bool NOGEO = false, bool DET = false>
-__global__ __launch_bounds__(kThreads, 2) void field_w16_bwd_kernel(FieldArgs a) {
-  static_assert(!NOGEO || TRAIN, "the no-geometry schedule is the training backward's");
-  __shared__ __attribute__((aligned(16))) float4 lds[kBwdLdsQuads];
+// One field's share of a backward launch: workgroup blk of nblk walks tiles blk, blk + nblk, ...
+template <int MODE, bool TRAIN, bool NOGEO, bool DET>
+__device__ __forceinline__ void bwd_body(const FieldArgs& a, float4* lds, const unsigned blk, const unsigned nblk) {
   float* blds = reinterpret_cast<float*>(lds + kRing * kChunkQuads);
   State s;
   s.lane = threadIdx.x & 63;
@@ -1459,7 +1458,7 @@ __global__ __launch_bounds__(kThreads, 2) void field_w16_bwd_kernel(FieldArgs a)
   const int64_t n_tiles = (a.m + kTile - 1) / kTile;
   int crun = 0;
   int64_t prev = -1;
-  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+  for (int64_t tile = blk; tile < n_tiles; tile += nblk) {
     bwd_tile<MODE, TRAIN, NOGEO, DET>(s, a, lds, grow, tile, cur_code, crun, prev);
   }
   if constexpr (NOGEO) {
@@ -1470,7 +1469,7 @@ __global__ __launch_bounds__(kThreads, 2) void field_w16_bwd_kernel(FieldArgs a)
     // deterministic form (one code row, host-checked): this wave's g_code row into its gc_part row
     // (every wave writes its row, zeros included)
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS atomics landed
-    float* out = a.gc_part + ((int64_t)blockIdx.x * kWaves + s.wave) * kCbStride;
+    float* out = a.gc_part + ((int64_t)blk * kWaves + s.wave) * kCbStride;
 #pragma unroll
     for (int k = 0; k < (kCbStride + 63) / 64; ++k) {
       const int j = s.lane + 64 * k;
@@ -1479,6 +1478,29 @@ __global__ __launch_bounds__(kThreads, 2) void field_w16_bwd_kernel(FieldArgs a)
   } else if (cur_code >= 0) {
     flush_gcode(s, a, grow, cur_code);
   }
+}
+
+template <int MODE, bool TRAIN, bool NOGEO = false, bool DET = false>
+__global__ __launch_bounds__(kThreads, 2) void field_w16_bwd_kernel(FieldArgs a) {
+  static_assert(!NOGEO || TRAIN, "the no-geometry schedule is the training backward's");
+  __shared__ __attribute__((aligned(16))) float4 lds[kBwdLdsQuads];
+  bwd_body<MODE, TRAIN, NOGEO, DET>(a, lds, blockIdx.x, gridDim.x);
+}
+
+// A render's two fields (coarse, fine) in ONE launch: workgroups 0 .. first1 - 1 run field a0's tiles,
+// the rest field a1's, each exactly as its own launch would (same workgroup count and tile walk, so the
+// same sums in the same order).  One workgroup per CU is resident: field a1's workgroups start on the
+// CUs field a0's leave, so the second field fills the first one's finish spread instead of waiting
+// for its last workgroup and a new launch (point_sampler.py:115: the fine depths are detached, so the
+// two backwards are independent).
+template <int MODE, bool TRAIN, bool NOGEO = false, bool DET = false>
+__global__ __launch_bounds__(kThreads, 2) void field_w16_bwd2_kernel(FieldArgs a0, FieldArgs a1, unsigned first1) {
+  static_assert(!NOGEO || TRAIN, "the no-geometry schedule is the training backward's");
+  __shared__ __attribute__((aligned(16))) float4 lds[kBwdLdsQuads];
+  // two instances of the body, each reading its own kernel argument (a runtime select between the two
+  // structs put the selected one in scratch: ~550 B per lane)
+  if (blockIdx.x >= first1) bwd_body<MODE, TRAIN, NOGEO, DET>(a1, lds, blockIdx.x - first1, gridDim.x - first1);
+  else bwd_body<MODE, TRAIN, NOGEO, DET>(a0, lds, blockIdx.x, first1);
 }
 
 }  // namespace w16
@@ -1564,6 +1586,33 @@ bool nogeo_enabled() {
     return (e && e[0] == '0') ? 0 : 1;
   }();
   return on != 0;
+}
+
+static unsigned bwd_grid_w16(const FieldArgs& a) {
+  return static_cast<unsigned>(
+      std::min<int64_t>(std::min<int64_t>(cn::ceil_div(a.m, w16::kTile), cu_count_w16()), kMaxBwdBlocks));
+}
+
+// Two fields' fused backwards in one launch (field_w16_bwd2_kernel): both must take the same kernel form
+// (the same mode, training / no-geometry / deterministic choice), else CN_EUNSUPPORTED before any launch.
+int launch_field_w16_bwd2(int mode, FieldArgs& a0, FieldArgs& a1, hipStream_t st) {
+  auto form = [](const FieldArgs& a) {
+    if (a.dpre) return (!a.d_pts && !a.d_ro && !a.d_rd && nogeo_enabled()) ? 2 : 1;
+    return a.gc_part ? 3 : 0;
+  };
+  const int f = form(a0);
+  if (form(a1) != f || mode != kFromRayZ) return CN_EUNSUPPORTED;
+  const unsigned g0 = bwd_grid_w16(a0), g1 = bwd_grid_w16(a1);
+  a0.n_blocks = g0;
+  a1.n_blocks = g1;
+  const dim3 grid(g0 + g1), b(w16::kThreads);
+  switch (f) {
+    case 2: hipLaunchKernelGGL((w16::field_w16_bwd2_kernel<kFromRayZ, true, true>), grid, b, 0, st, a0, a1, g0); break;
+    case 1: hipLaunchKernelGGL((w16::field_w16_bwd2_kernel<kFromRayZ, true>), grid, b, 0, st, a0, a1, g0); break;
+    case 3: hipLaunchKernelGGL((w16::field_w16_bwd2_kernel<kFromRayZ, false, false, true>), grid, b, 0, st, a0, a1, g0); break;
+    default: hipLaunchKernelGGL((w16::field_w16_bwd2_kernel<kFromRayZ, false>), grid, b, 0, st, a0, a1, g0); break;
+  }
+  return cn::launch_status();
 }
 
 int launch_field_w16_bwd(int mode, FieldArgs& a, hipStream_t st) {

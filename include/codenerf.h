@@ -410,6 +410,39 @@ int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, const float* c
                                 const float* freqs_xyz, const float* freqs_dir, float* workspace,
                                 float* const* grads, float* g_code, float* d_pts, float* d_ro, float* d_rd,
                                 cn_stream_t stream);
+/* A render's fields' training backwards in shared launches (replaces two cn_field_backward_train_fmt
+ * calls for predict_radiance_and_render's coarse and fine fields, nerf/__init__.py:81-89 under
+ * train.py:112's loss.backward(): the fine depths are detached, point_sampler.py:115, so the two
+ * backwards are independent).  Each field: the arguments of cn_field_backward_train_fmt, with its own
+ * workspace.  With two fp32 fields on rays + depths that both take the batched dW plan and the forward's
+ * encoding plane (every runnable training config): ONE dX launch, ONE batched dW launch, ONE layer_xyz1
+ * launch and ONE reduction launch for both, each running every field's workgroups as its own launch
+ * would -- the gradients are bitwise those of the per-field calls.  Otherwise the fields run one after
+ * the other.  n_fields 1 or 2. */
+typedef struct cn_field_train_bwd {
+  const float* packed_t;
+  const float* const* params;
+  const uint32_t* masks;
+  const float* saved;
+  const float* x_enc;
+  const float* d_raw;
+  const float* pts;
+  const float* ro;
+  const float* rd;
+  const float* z;
+  int64_t n_rays, n_samples, chunk_rows;
+  const int64_t* code_index;
+  int64_t n_codes;
+  const float* freqs_xyz;
+  const float* freqs_dir;
+  float* workspace;
+  float* const* grads;
+  float* g_code;
+  float* d_pts;
+  float* d_ro;
+  float* d_rd;
+} cn_field_train_bwd;
+int cn_field_backward_train_multi(int fmt_t, const cn_field_train_bwd* fields, int n_fields, cn_stream_t stream);
 
 /* Backward of cn_code_bias (the code layers, model.py:174-177, and the code
  * halves of layer_xyz2 / fc_out / fc_rgb) from g_code.  dz_s / dz_t (n_codes, 256)

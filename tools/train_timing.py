@@ -14,6 +14,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--precision", default="f32")
     ap.add_argument("--iters", type=int, default=8)
+    ap.add_argument("--shape", default="c3", help="bench.TRAIN_SHAPES key: c3, cars_code, 3080")
     args = ap.parse_args()
     import torch
     import bench
@@ -21,7 +22,7 @@ def main():
     torch.cuda.set_device(dev)
     from codenerf import synthetic
     k = synthetic.srn_intrinsics(bench.H, bench.FOCAL)
-    r = bench.train_bench(dev, k, args.iters, 1, args.precision)
+    r = bench.train_bench(dev, k, args.iters, 1, args.precision, shape=args.shape)
     print(json.dumps({kk: v for kk, v in r.items() if kk != "note"}))
 
 
