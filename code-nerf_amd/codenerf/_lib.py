@@ -61,6 +61,20 @@ class FieldTrainBwd(ctypes.Structure):
                 ("d_rd", _p)]
 
 
+class FieldFusedBwd(ctypes.Structure):
+    """cn_field_fused_bwd (include/codenerf.h): one field's part of cn_field_backward_fused_multi."""
+    _fields_ = [("packed_t", _p), ("masks", _p), ("d_raw", _p), ("pts", _p), ("ro", _p), ("rd", _p), ("z", _p),
+                ("n_rays", _i64), ("n_samples", _i64), ("chunk_rows", _i64), ("code_index", _p), ("n_codes", _i64),
+                ("freqs_xyz", _fp), ("freqs_dir", _fp), ("g_code", _p), ("d_pts", _p), ("d_ro", _p), ("d_rd", _p),
+                ("workspace", _p)]
+
+
+class CodeActJob(ctypes.Structure):
+    """cn_code_act_job (include/codenerf.h): one field's part of cn_code_bias_backward_act_multi."""
+    _fields_ = [("params", ctypes.POINTER(_p)), ("code_act", _p), ("g_code", _p), ("grads", ctypes.POINTER(_p)),
+                ("workspace", _p)]
+
+
 # name -> (restype, argtypes); mirrors include/codenerf.h one to one.
 SIGNATURES = {
     "cn_version": (ctypes.c_char_p, []),
@@ -115,6 +129,8 @@ SIGNATURES = {
     "cn_field_backward_train_fmt": (_i, [_i, _p, ctypes.POINTER(_p), _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p,
                                      _i64, _fp, _fp, _p, ctypes.POINTER(_p), _p, _p, _p, _p, _p]),
     "cn_field_backward_train_multi": (_i, [_i, ctypes.POINTER(FieldTrainBwd), _i, _p]),
+    "cn_field_backward_fused_multi": (_i, [_i, ctypes.POINTER(FieldFusedBwd), _i, _p, _p]),
+    "cn_code_bias_backward_act_multi": (_i, [ctypes.POINTER(CodeActJob), _i, _p, _p, _i64, _p]),
     "cn_field_backward_x3": (_i, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _p, _i64, _fp, _fp, _p, _p, _p, _p,
                                   _p]),
     "cn_code_bias_backward": (_i, [ctypes.POINTER(_p), _p, _p, _i64, _p, _p, _p, ctypes.POINTER(_p), _p]),

@@ -143,10 +143,11 @@ class RaySink:
     both volume renders and both fused field backwards add, returning no gradient; PoseRays.backward
     reads the sum.  Replaces four (R, 3) autograd adds per eval step (eval.py:145-163)."""
 
-    __slots__ = ("buf",)
+    __slots__ = ("buf", "hold")
 
     def __init__(self):
         self.buf = None
+        self.hold = None     # a FieldPair whose first field waits: ray gradients arriving meanwhile go to it
 
 
 _RAY_SINKS = [False]
@@ -325,6 +326,13 @@ class VolumeRender(torch.autograd.Function):
             return None, None, None
         raw, z, rd = ctx.saved_tensors
         sink, ctx.ray_sink = ctx.ray_sink, None
+        if sink is not None and sink.hold is not None and sink.buf is not None and ctx.needs_input_grad[2]:
+            # a paired field backward is waiting (FieldPair): this d rd is added in its place by the shared launch
+            d_raw, d_rd = ops.volume_render_backward(raw, z, rd, _c(g_rgb), _c(g_disp), _c(g_acc), _c(g_w),
+                                                     _c(g_depth), want_rd=True)
+            pair = sink.hold
+            pair.between = d_rd if pair.between is None else pair.between + d_rd
+            return d_raw, None, None
         into = sink.buf[1] if (sink is not None and sink.buf is not None and ctx.needs_input_grad[2]) else None
         d_raw, d_rd = ops.volume_render_backward(raw, z, rd, _c(g_rgb), _c(g_disp), _c(g_acc), _c(g_w), _c(g_depth),
                                                  want_rd=ctx.needs_input_grad[2], d_rd_into=into)
@@ -403,22 +411,33 @@ class FieldPair:
     waiting field hands its gradients over in place -- the optimiser's flat slots installed as .grad at
     once, the code rows' dz through the CodeGradSink -- so it returns none through autograd."""
 
-    __slots__ = ("pending", "fields")
+    __slots__ = ("pending", "kinds", "between", "sink", "on_grads")
 
-    def __init__(self):
+    def __init__(self, on_grads=None):
+        self.on_grads = on_grads    # training: called once both fields' weight gradients are enqueued
         self.pending = None
-        self.fields = 0
+        self.kinds = []         # per field forward: "train" (fp32 training) or "fused" (fp32 eval); else None
+        self.between = None     # eval: the rays' d rd that arrived while the first field waited
+        self.sink = None        # eval: the RaySink held meanwhile
+
+    def ready(self, kind) -> bool:
+        return len(self.kinds) == 2 and self.kinds[0] == self.kinds[1] == kind
 
 
-_PAIRING = [False]
+_PAIRING = [None]
 
 
 class paired_fields:
-    """Context in which render_rays pairs its two fields' training backwards (FieldPair)."""
+    """Context in which render_rays pairs its two fields' backwards (FieldPair).  ``on_grads``: a callable
+    the training pair calls (once) right after both fields' weight gradients are enqueued -- the data-
+    parallel step starts its first gradient bucket there (optim.AdamW.allreduce_begin)."""
+
+    def __init__(self, on_grads=None):
+        self.on_grads = on_grads
 
     def __enter__(self):
         self.prev = _PAIRING[0]
-        _PAIRING[0] = True
+        _PAIRING[0] = self
         return self
 
     def __exit__(self, *exc):
@@ -428,7 +447,8 @@ class paired_fields:
 
 def new_field_pair():
     """render_rays: a FieldPair for its two fields inside paired_fields(), else None."""
-    return FieldPair() if (_PAIRING[0] and torch.is_grad_enabled()) else None
+    ctx = _PAIRING[0]
+    return FieldPair(ctx.on_grads) if (ctx is not None and torch.is_grad_enabled()) else None
 
 
 def _pair_flush(pair):
@@ -438,12 +458,37 @@ def _pair_flush(pair):
         return
     job, post = pair.pending
     pair.pending = None
-    r = ops.field_backward_train_multi([job], post[0].precision)[0]
     meta, params, z_s, z_t, pg, want_z, act = post
     if want_z and (meta.sink is None or meta.sink.rows() is None):
         raise RuntimeError("paired field backward: the partner field never ran and the code rows' gradient "
                            "buffers were already handed out")
+    if pair.kinds[0] == "fused":
+        sink, pair.sink = pair.sink, None
+        sink.hold = None
+        r = ops.field_backward_x3(**job)
+        if pair.between is not None:
+            r["d_rd"].add_(pair.between)
+            pair.between = None
+    else:
+        r = ops.field_backward_train_multi([job], meta.precision)[0]
     _code_grads(meta, params, z_s, z_t, r["g_code"], pg, want_z, act)
+
+
+def _code_grads_pair(first, second):
+    """_code_grads of a FieldPair's two fields (first: the one that waited) with their first halves in one
+    launch (cn_code_bias_backward_act_multi); their dz queued in that order.  Each item: (meta, params, z_s,
+    z_t, g_code, pg, want_z, act) with act given.  -> (dz_s, dz_t) of the second."""
+    items = (first, second)
+    wss = ops.code_ds_outer_multi([(it[1], it[7], it[4], it[5]) for it in items], first[2], first[3])
+    out = None
+    for (meta, params, z_s, z_t, g_code, pg, want_z, act), ws in zip(items, wss):
+        out = (None, None)
+        if not want_z:
+            continue
+        if meta.sink is not None and meta.sink.defer(params, g_code, ws):
+            continue
+        out = ops.code_dz([(params, g_code, ws)], z_s.shape[0])
+    return out
 
 
 class RadianceField(torch.autograd.Function):
@@ -494,6 +539,8 @@ class RadianceField(torch.autograd.Function):
         else:
             cb = ops.code_bias(params, z_s, z_t)
         if fused:
+            if meta.pair is not None:
+                meta.pair.kinds.append("fused" if meta.precision == "f32" else None)
             pack = "bf16x3" if meta.precision == "bf16x3" else "f32_w16"
             raw, masks = ops.radiance_field_masks(_packed(ctx.owner, params, pack), cb, rd, meta.n_samples,
                                                   meta.chunk_rows, meta.fx, meta.fd, pts=pts, ro=ro, z=z,
@@ -510,8 +557,8 @@ class RadianceField(torch.autograd.Function):
                            and ops.fused_backward_supported(z_s.shape[0], meta.n_samples, meta.code_index,
                                                             meta.precision))
         ctx.masks = None
-        if meta.pair is not None and ctx.train_fused and meta.precision == "f32":
-            meta.pair.fields += 1
+        if meta.pair is not None:
+            meta.pair.kinds.append("train" if (ctx.train_fused and meta.precision == "f32") else None)
         if ctx.train_fused:
             x3 = meta.precision == "bf16x3"
             raw, saved, ctx.masks = ops.radiance_field_train_w16(
@@ -541,17 +588,42 @@ class RadianceField(torch.autograd.Function):
             # the rays' gradients added in place into the pose's RaySink (no autograd sums)
             rs = meta.ray_sink
             ray_into = rs.buf if (rs is not None and rs.buf is not None and needs[1] and needs[3]) else None
-            r = ops.field_backward_x3(_packed(ctx.owner, params, pack_t), ctx.masks, g_raw.contiguous(), rd.shape[0],
-                                      meta.n_samples, meta.chunk_rows, z_s.shape[0], meta.fx, meta.fd, rd=rd,
-                                      pts=pts, ro=ro, z=z, code_index=meta.code_index, want_pts=needs[2],
-                                      want_ro=needs[3], want_rd=needs[1], precision=meta.precision, acc=ctx.acc,
-                                      ray_into=ray_into)
-            ctx.acc = None
+            job = dict(packed_t=_packed(ctx.owner, params, pack_t), masks=ctx.masks, d_raw=g_raw.contiguous(),
+                       n_rays=rd.shape[0], n_samples=meta.n_samples, chunk_rows=meta.chunk_rows, n_codes=z_s.shape[0],
+                       freqs_xyz=meta.fx, freqs_dir=meta.fd, rd=rd, pts=pts, ro=ro, z=z, code_index=meta.code_index,
+                       want_pts=needs[2], want_ro=needs[3], want_rd=needs[1], precision=meta.precision, acc=ctx.acc,
+                       ray_into=ray_into)
+            act = ctx.code_act
+            ctx.acc = ctx.code_act = ctx.masks = None
+            post = (meta, params, z_s, z_t, None, want_z, act)
+            pair = meta.pair
+            if pair is not None and pair.ready("fused"):
+                # a field pairs when everything it returns goes in place -- the rays' gradient into the pose's
+                # RaySink, the codes' through the code rows' sink -- and the shared launch takes its shape
+                pairable = (ray_into is not None and act is not None and not needs[2] and z_s.shape[0] == 1
+                            and meta.n_samples % 16 == 0 and pts is None
+                            and (not want_z or (meta.sink is not None and meta.sink.rows() is not None)))
+                if pair.pending is None:
+                    if pairable:         # the first of the pair waits for the other
+                        pair.pending = (job, post)
+                        pair.sink, rs.hold = rs, pair
+                        torch.autograd.Variable._execution_engine.queue_callback(lambda: _pair_flush(pair))
+                        return (None,) * len(needs)
+                elif not pairable:
+                    _pair_flush(pair)    # the waiting one alone (its sums, then the held d rd), then this one
+                else:
+                    other_job, other_post = pair.pending
+                    pair.pending = None
+                    pair.sink.hold, pair.sink = None, None
+                    between, pair.between = pair.between, None
+                    r_other, r = ops.field_backward_x3_multi([other_job, job], d_rd_between=between)
+                    dz_s, dz_t = _code_grads_pair(other_post[:4] + (r_other["g_code"],) + other_post[4:],
+                                                  post[:4] + (r["g_code"],) + post[4:])
+                    return (None, None, r["d_pts"], None, None, dz_s, dz_t, *([None] * len(params)))
+            r = ops.field_backward_x3(**job)
             dz_s = dz_t = None
             if want_z:
-                dz_s, dz_t = _code_grads(meta, params, z_s, z_t, r["g_code"], None, True, ctx.code_act)
-            ctx.code_act = None
-            ctx.masks = None
+                dz_s, dz_t = _code_grads(meta, params, z_s, z_t, r["g_code"], None, True, act)
             d_ro, d_rd = (None, None) if ray_into is not None else (r["d_ro"], r["d_rd"])
             return (None, d_rd, r["d_pts"], d_ro, None, dz_s, dz_t, *([None] * len(params)))
         orig = ctx.orig_params
@@ -569,7 +641,7 @@ class RadianceField(torch.autograd.Function):
             act, ctx.acts, ctx.x_enc, ctx.masks, ctx.g_code, ctx.code_act = ctx.code_act, None, None, None, None, None
             post = (meta, params, z_s, z_t, pg, want_z, act)
             pair = meta.pair
-            if pair is not None and pair.fields == 2 and not x3:
+            if pair is not None and pair.ready("train") and not x3:
                 if pair.pending is None:
                     # the first of the pair waits for the other: only when everything it returns goes in place
                     # (the flat slots as .grad now, the code rows through the sink) and no ray gradient is wanted
@@ -584,8 +656,18 @@ class RadianceField(torch.autograd.Function):
                     other_job, other_post = pair.pending
                     pair.pending = None
                     r_other, r = ops.field_backward_train_multi([other_job, job], meta.precision)
-                    _code_grads(*other_post[:4], r_other["g_code"], *other_post[4:])
-                    dz_s, dz_t = _code_grads(meta, params, z_s, z_t, r["g_code"], pg, want_z, act)
+                    if act is not None and other_post[6] is not None:
+                        dz_s, dz_t = _code_grads_pair(other_post[:4] + (r_other["g_code"],) + other_post[4:],
+                                                      post[:4] + (r["g_code"],) + post[4:])
+                    else:
+                        _code_grads(*other_post[:4], r_other["g_code"], *other_post[4:])
+                        dz_s, dz_t = _code_grads(meta, params, z_s, z_t, r["g_code"], pg, want_z, act)
+                    if pair.on_grads is not None and slots:
+                        for p, g in zip(orig, pg):
+                            p.grad = g               # (autograd then finds .grad set and adds nothing: None below)
+                        on_grads, pair.on_grads = pair.on_grads, None
+                        on_grads()
+                        return (None, None, None, None, None, dz_s, dz_t, *([None] * len(params)))
                     grads = pg if pg is not None else [None] * len(params)
                     return (None, r["d_rd"], r["d_pts"], r["d_ro"], None, dz_s, dz_t, *grads)
             r = ops.field_backward_train(precision=meta.precision, **job)

@@ -66,9 +66,12 @@ def eval_step_loss(theta, phi, rho, shape_code, texture_code, target_pixels, sam
     z_s, z_t = shape_code.expand(n, -1), texture_code.expand(n, -1)
     if shape_code.dim() == 2 and shape_code.shape[0] == 1:
         z_s._cn_code_rows = z_t._cn_code_rows = CodeRows(shape_code, texture_code, None)
-    # predict_radiance_and_render (nerf/__init__.py:74-91) over the whole ray batch
-    out = nerf.render_rays(ro, rd, z_s, z_t, point_sampler, embedders, models["nerf_coarse"], models["nerf_fine"],
-                           chunk_rows=n, t_rand=t_rand, u=u)
+    # predict_radiance_and_render (nerf/__init__.py:74-91) over the whole ray batch; the two fields' backwards
+    # in shared launches (autograd.FieldPair: the loss below reaches both)
+    from .autograd import paired_fields
+    with paired_fields():
+        out = nerf.render_rays(ro, rd, z_s, z_t, point_sampler, embedders, models["nerf_coarse"],
+                               models["nerf_fine"], chunk_rows=n, t_rand=t_rand, u=u)
     rgb_c, rgb_f = out["rgb_coarse"], out["rgb_fine"]
     # mse(coarse) + mse(fine) + lambda (||z_s|| + ||z_t||), the codes expanded over the n rays
     psnr = torch.empty((), dtype=torch.float64, device=tp.device)   # eval.py:159's psnr, by the loss launch

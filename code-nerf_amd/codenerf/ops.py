@@ -771,6 +771,32 @@ def code_ds_outer(params: Sequence[Tensor], z_s: Tensor, z_t: Tensor, code_act: 
     return ws
 
 
+def code_ds_outer_multi(jobs, z_s: Tensor, z_t: Tensor):
+    """code_ds_outer of a render's 1 or 2 fields on the same codes in ONE launch
+    (cn_code_bias_backward_act_multi); jobs: [(params, code_act, g_code, param_grads | None)] -> the
+    workspaces, one per job (bitwise code_ds_outer's)."""
+    lib = _lib_ready()
+    assert 1 <= len(jobs) <= 2, "one or two jobs"
+    z_s, z_t = _cuda(z_s.detach(), "z_s"), _cuda(z_t.detach(), "z_t")
+    n = z_s.shape[0]
+    structs, keep, outs = [], [], []
+    for params, code_act, g_code, param_grads in jobs:
+        params = [_cuda(p.detach(), f"param{i}") for i, p in enumerate(params)]
+        g_code, code_act = _cuda(g_code, "g_code"), _cuda(code_act, "code_act")
+        assert code_act.numel() == n * 768, "code_act: (n_codes, 768)"
+        ws = torch.empty(lib.cn_code_bias_backward_workspace_floats(n), device=g_code.device, dtype=torch.float32)
+        arr, k1 = _lib.pointer_array(params)
+        garr, k2 = _lib.pointer_array(list(param_grads)) if param_grads is not None else (None, None)
+        keep += [params, g_code, code_act, arr, k1, garr, k2]
+        structs.append(_lib.CodeActJob(arr, ptr(code_act), ptr(g_code), garr, ptr(ws)))
+        outs.append(ws)
+    js = (_lib.CodeActJob * len(structs))(*structs)
+    check(lib.cn_code_bias_backward_act_multi(js, len(structs), ptr(z_s), ptr(z_t), n, stream_of(z_s)),
+          "cn_code_bias_backward_act_multi")
+    del keep
+    return outs
+
+
 def code_dz(jobs: Sequence[Tuple[Sequence[Tensor], Tensor, Tensor]], n_codes: int,
             dz_into: Optional[Tuple[Tensor, Tensor]] = None):
     """cn_code_dz: dz_s, dz_t of one or two fields' code backwards [(params, g_code, code_ds_outer's
@@ -960,6 +986,50 @@ def field_backward_x3(packed_t: Tensor, masks: Tensor, d_raw: Tensor, n_rays: in
                                          ptr(d_pts), ptr(d_ro), ptr(d_rd), ptr(ws), stream_of(d_raw)),
           "cn_field_backward_fused_ws")
     return {"g_code": g_code, "d_pts": d_pts, "d_ro": d_ro, "d_rd": d_rd}
+
+
+def field_backward_x3_multi(fields: Sequence[dict], d_rd_between: Optional[Tensor] = None):
+    """The eval step's two fields' fused backwards (field_backward_x3's keyword arguments, one dict per
+    field, both adding into the same ``ray_into`` d ro / d rd) through ONE cn_field_backward_fused_multi
+    call: fp32, one code row, whole waves per ray -> one dX launch, one ray / g_code-row launch and one
+    g_code reduction for both.  d ro / d rd end bitwise as field 0's call, then d rd += ``d_rd_between``,
+    then field 1's call.  -> one result dict per field."""
+    assert len(fields) == 2
+    lib = _lib_ready()
+    fmt_t = _lib.CN_FMT_F32_W16_T
+    structs, keep, outs = [], [], []
+    stream = None
+    for f in fields:
+        assert f.get("precision", "f32") == "f32" and f.get("ray_into") is not None and f.get("acc") is not None
+        n_rays, n_samples, n_codes = f["n_rays"], f["n_samples"], f["n_codes"]
+        assert n_codes == 1 and n_samples % 16 == 0 and f.get("pts") is None and not f.get("want_pts")
+        m = n_rays * n_samples
+        d_raw = _aligned16(_cuda(f["d_raw"], "d_raw"))
+        assert d_raw.numel() == 4 * m and m > 0
+        dev = d_raw.device
+        rd, ro, z = _opt(f["rd"], "rd"), _opt(f.get("ro"), "ro"), _opt(f.get("z"), "z")
+        acc = f["acc"]
+        assert acc.numel() == field_backward_x3_acc_floats(n_codes, n_rays, True, True) and acc.is_contiguous()
+        g_code = acc[:_lib.CN_CODE_BIAS_STRIDE].view(1, _lib.CN_CODE_BIAS_STRIDE)
+        d_ro, d_rd = f["ray_into"]
+        assert all(t.is_cuda and t.is_contiguous() and t.shape == (n_rays, 3) for t in (d_ro, d_rd))
+        ws = torch.empty(int(lib.cn_field_backward_fused_workspace_floats(fmt_t, n_rays, n_samples)), device=dev,
+                         dtype=torch.float32)
+        fx, fd = _lib.host_floats(f["freqs_xyz"]), _lib.host_floats(f["freqs_dir"])
+        keep += [d_raw, rd, ro, z, ws, fx, fd]
+        structs.append(_lib.FieldFusedBwd(
+            ptr(f["packed_t"]), ptr(f["masks"]), ptr(d_raw), None, ptr(ro), ptr(rd), ptr(z), n_rays, n_samples,
+            f["chunk_rows"], None, 1, ctypes.cast(fx, ctypes.POINTER(ctypes.c_float)),
+            ctypes.cast(fd, ctypes.POINTER(ctypes.c_float)), ptr(g_code), None, ptr(d_ro), ptr(d_rd), ptr(ws)))
+        outs.append({"g_code": g_code, "d_pts": None, "d_ro": d_ro, "d_rd": d_rd})
+        stream = stream_of(d_raw)
+    if d_rd_between is not None:
+        d_rd_between = _cuda(d_rd_between, "d_rd_between").contiguous()
+        assert d_rd_between.shape == outs[0]["d_rd"].shape
+    js = (_lib.FieldFusedBwd * 2)(*structs)
+    check(lib.cn_field_backward_fused_multi(fmt_t, js, 2, ptr(d_rd_between), stream), "cn_field_backward_fused_multi")
+    del keep
+    return outs
 
 
 # ------------------------------------------------------------------ training step: optimiser (SURVEY 8(f) row 1)

@@ -37,6 +37,11 @@ def _round_up(n: int) -> int:
 class AdamW(torch.optim.Optimizer):
     """torch.optim.AdamW (decoupled weight decay; amsgrad / maximize off) on flat buffers."""
 
+    # process-group backends on which allreduce_begin starts its bucket asynchronously: RCCL ("nccl"),
+    # whose collective stream waits for the enqueued work without a host wait (gloo stages device tensors
+    # through the host; the two-rank gloo tests add it to check the bucketed sums)
+    bucket_backends = ("nccl",)
+
     def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 1e-2, amsgrad: bool = False, *, maximize: bool = False,
                  foreach=None, capturable: bool = False, differentiable: bool = False, fused=None):
@@ -270,6 +275,32 @@ class AdamW(torch.optim.Optimizer):
         self._adopt_state()
 
     # ---- data parallel ------------------------------------------------
+    def allreduce_begin(self, n_groups: int, group=None) -> bool:
+        """Start the all-reduce of the first ``n_groups`` parameter groups' gradients now, asynchronously
+        (the first bucket of DDP's overlap, util.py:139-142): called from inside the backward once those
+        gradients are final -- train_minibatch hands it to the render's FieldPair, which calls it right
+        after both fields' weight gradients are enqueued -- so the collective runs while the rest of the
+        backward (the code tables' dz, the pose / ray tail) does; allreduce_grads() then reduces the rest
+        and waits for both.  On RCCL the collective's stream waits for the work enqueued so far and runs
+        beside what follows.  Only when every parameter of those groups holds its gradient (else nothing
+        starts and allreduce_grads() reduces everything at once).  -> whether it started."""
+        if not (dist.is_available() and dist.is_initialized()) or getattr(self, "_pending_bucket", None):
+            return False
+        if dist.get_backend(group) not in self.bucket_backends:
+            return False
+        params = [p for g in self.param_groups[:n_groups] for p in g["params"]]
+        if any(p.grad is None for p in params):
+            return False
+        with torch.no_grad():
+            for p in params:
+                view = self._view("grad", p)
+                if p.grad.data_ptr() != view.data_ptr():
+                    return False
+        split = self._starts[n_groups]
+        work = dist.all_reduce(self._grad_ext[:split], op=dist.ReduceOp.SUM, group=group, async_op=True)
+        self._pending_bucket = (split, work, group)
+        return True
+
     def allreduce_grads(self, group=None, average: bool = True) -> None:
         """Average the gradients over the process group (the reference's DDP, util.py:139-142):
         ONE all-reduce (SUM, then a division by the world size -- the same arithmetic on RCCL and
@@ -300,7 +331,15 @@ class AdamW(torch.optim.Optimizer):
         ext[n:n + len(params)].copy_(flags)
         for p in missing:
             self._view("grad", p).zero_()
-        dist.all_reduce(ext, op=dist.ReduceOp.SUM, group=group)
+        pending, self._pending_bucket = getattr(self, "_pending_bucket", None), None
+        if pending is not None:
+            # the first bucket went out during the backward (allreduce_begin): the rest now, then both done
+            split, work, group0 = pending
+            assert group0 is group, "allreduce_begin / allreduce_grads on different groups"
+            dist.all_reduce(ext[split:], op=dist.ReduceOp.SUM, group=group)
+            work.wait()
+        else:
+            dist.all_reduce(ext, op=dist.ReduceOp.SUM, group=group)
         if average:
             ext.div_(world)
         if missing:

@@ -119,8 +119,14 @@ def train_minibatch(models, optimizer, scheduler, point_sampler, embedders, ro, 
     read back every chunk as train.py:105 does).  ``uniforms``: (t_rand, u), the stratified / fine
     draws of point_sampler.py:64,93 injected (parity tests) instead of drawn on the device."""
     target_object_embedding = models["embedding"](object_ids)
-    # both fields' training backwards in shared launches (autograd.FieldPair): the loss below reaches both
-    with paired_fields():
+    # both fields' training backwards in shared launches (autograd.FieldPair: the loss below reaches both);
+    # data parallel with the flat AdamW, the two MLPs' gradients (param groups 0, 1: util.py:151-156) start
+    # their all-reduce as soon as that shared backward has enqueued them (allreduce_begin), beside the rest
+    # of the backward, as DDP's bucketed reduction overlaps its backward
+    early = None
+    if is_distributed and not _ddp_wrapped(models) and hasattr(optimizer, "allreduce_begin"):
+        early = lambda: optimizer.allreduce_begin(2)  # noqa: E731
+    with paired_fields(on_grads=early):
         if uniforms is None:
             rgb_coarse, rgb_fine = nerf.predict_radiance_and_render((ro, rd), point_sampler, embedders,
                                                                     models["nerf_coarse"], models["nerf_fine"],

@@ -2068,14 +2068,14 @@ __device__ __forceinline__ float sum16_bfly(float x) {
   return x;
 }
 
-__global__ __launch_bounds__(256) void code_ds_outer_kernel(mlp::Params P, const float* __restrict__ z_s,
-                                                            const float* __restrict__ z_t, const float* __restrict__ g,
-                                                            const float* __restrict__ act, float* __restrict__ ws,
-                                                            mlp::Params G) {
+__device__ __forceinline__ void code_ds_outer_body(const mlp::Params& P, const float* __restrict__ z_s,
+                                                   const float* __restrict__ z_t, const float* __restrict__ g,
+                                                   const float* __restrict__ act, float* __restrict__ ws,
+                                                   const mlp::Params& G, const int c, const int y) {
   using namespace mlp;
   static_assert(kCodeRows == 4, "thread map: 8 row groups of 16 lanes = 2 vectors x 4 rows");
   __shared__ float gx2[256], go[257], grgb[3], ds[3][kCodeRows];
-  const int c = blockIdx.x, y = blockIdx.y, tid = threadIdx.x;
+  const int tid = threadIdx.x;
   const int r0 = kCodeRows * y;
   const float* gr = g + (int64_t)c * kCbStride;
   if (!code_row_used(gr, tid)) return;  // code_dz_kernel skips the code too
@@ -2134,6 +2134,31 @@ __global__ __launch_bounds__(256) void code_ds_outer_kernel(mlp::Params P, const
     grad_add(G.p[kWOut], 256 + jb, go[0] * a[256 + jb]);  // fc_out row 0 (sigma)
     for (int r = 0; r < 3; ++r) grad_add(G.p[kWRgb], r * 512 + 256 + jb, grgb[r] * a[512 + jb]);
   }
+}
+
+__global__ __launch_bounds__(256) void code_ds_outer_kernel(mlp::Params P, const float* __restrict__ z_s,
+                                                            const float* __restrict__ z_t, const float* __restrict__ g,
+                                                            const float* __restrict__ act, float* __restrict__ ws,
+                                                            mlp::Params G) {
+  code_ds_outer_body(P, z_s, z_t, g, act, ws, G, blockIdx.x, blockIdx.y);
+}
+
+// One field's part of code_ds_outer2_kernel (cn_code_bias_backward_act's arguments).
+struct CodeDsJob {
+  mlp::Params P, G;
+  const float* g;
+  const float* act;
+  float* ws;
+};
+
+// A render's two fields' code backward first halves in one launch (slices y < kCodeSlices: field j0's);
+// each field writes only its own gradients and workspace, as its own launch would.
+__global__ __launch_bounds__(256) void code_ds_outer2_kernel(CodeDsJob j0, CodeDsJob j1, const float* __restrict__ z_s,
+                                                             const float* __restrict__ z_t) {
+  if (static_cast<int>(blockIdx.y) >= kCodeSlices)
+    code_ds_outer_body(j1.P, z_s, z_t, j1.g, j1.act, j1.ws, j1.G, blockIdx.x, blockIdx.y - kCodeSlices);
+  else
+    code_ds_outer_body(j0.P, z_s, z_t, j0.g, j0.act, j0.ws, j0.G, blockIdx.x, blockIdx.y);
 }
 
 struct DzJob {
@@ -2237,27 +2262,11 @@ __global__ void gcode_bias_kernel(const float* __restrict__ g_code, int64_t n_co
 // d ro[r] += points' d ro and d rd[r] += points' d rd + Q1 d rd.
 // Blocks past the rays' (gc_blocks of them) add each backward workgroup's wave rows of gc_part in wave
 // order into gc_rows (one row per workgroup), which reduce_partials_kernel then sums in block order.
-__global__ __launch_bounds__(256) void ray_grad_reduce_kernel(const float* __restrict__ ray_part,
-                                                              const float* __restrict__ q1_part, int64_t n_rays,
-                                                              int64_t S, int64_t chunk_rows, int wave_samples,
-                                                              float* __restrict__ d_ro, float* __restrict__ d_rd,
-                                                              const float* __restrict__ gc_part, int gc_waves,
-                                                              float* __restrict__ gc_rows) {
-  const int64_t ray_blocks = (n_rays + 3) / 4;
-  if ((int64_t)blockIdx.x >= ray_blocks) {
-    const int64_t b = (int64_t)blockIdx.x - ray_blocks;
-    const float* rows = gc_part + b * gc_waves * mlp::kCbStride;
-    for (int j = threadIdx.x; j < mlp::kCbStride; j += 256) {
-      float v = rows[j];
-      for (int w = 1; w < gc_waves; ++w) v += rows[(int64_t)w * mlp::kCbStride + j];
-      gc_rows[b * mlp::kCbStride + j] = v;
-    }
-    return;
-  }
-  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (r >= n_rays) return;  // wave-uniform
-  float v[9];
+// One ray's sums of one field's deterministic eval backward: v[0..2] its points' d ro, v[3..5] their d rd,
+// v[6..8] its Q1 view-direction d rd (lane-strided over the wave, then a fixed butterfly).
+__device__ __forceinline__ void ray_sums(const float* __restrict__ ray_part, const float* __restrict__ q1_part,
+                                         int64_t n_rays, int64_t S, int64_t chunk_rows, int wave_samples, int64_t r,
+                                         int lane, float (&v)[9]) {
 #pragma unroll
   for (int i = 0; i < 9; ++i) v[i] = 0.0f;
   if (ray_part) {
@@ -2282,6 +2291,35 @@ __global__ __launch_bounds__(256) void ray_grad_reduce_kernel(const float* __res
   for (int off = 32; off >= 1; off >>= 1)
 #pragma unroll
     for (int i = 0; i < 9; ++i) v[i] += __shfl_xor(v[i], off);
+}
+
+// Blocks past the rays': workgroup b's wave rows of gc_part added in wave order into gc_rows[b].
+__device__ __forceinline__ void gc_rows_block(const float* __restrict__ gc_part, int gc_waves, float* __restrict__ gc_rows,
+                                              int64_t b) {
+  const float* rows = gc_part + b * gc_waves * mlp::kCbStride;
+  for (int j = threadIdx.x; j < mlp::kCbStride; j += 256) {
+    float v = rows[j];
+    for (int w = 1; w < gc_waves; ++w) v += rows[(int64_t)w * mlp::kCbStride + j];
+    gc_rows[b * mlp::kCbStride + j] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void ray_grad_reduce_kernel(const float* __restrict__ ray_part,
+                                                              const float* __restrict__ q1_part, int64_t n_rays,
+                                                              int64_t S, int64_t chunk_rows, int wave_samples,
+                                                              float* __restrict__ d_ro, float* __restrict__ d_rd,
+                                                              const float* __restrict__ gc_part, int gc_waves,
+                                                              float* __restrict__ gc_rows) {
+  const int64_t ray_blocks = (n_rays + 3) / 4;
+  if ((int64_t)blockIdx.x >= ray_blocks) {
+    gc_rows_block(gc_part, gc_waves, gc_rows, (int64_t)blockIdx.x - ray_blocks);
+    return;
+  }
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= n_rays) return;  // wave-uniform
+  float v[9];
+  ray_sums(ray_part, q1_part, n_rays, S, chunk_rows, wave_samples, r, lane, v);
   if (lane == 0) {
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -2289,6 +2327,67 @@ __global__ __launch_bounds__(256) void ray_grad_reduce_kernel(const float* __res
       if (d_rd) d_rd[3 * r + i] += v[3 + i] + v[6 + i];
     }
   }
+}
+
+// One field's part of ray_grad_reduce2_kernel.
+struct RayRed {
+  const float* ray_part;
+  const float* q1_part;
+  int64_t S, chunk_rows;
+  const float* gc_part;
+  float* gc_rows;
+  int64_t gc_blocks;
+  int wave_samples, gc_waves;
+};
+
+// ray_grad_reduce_kernel for a render's two fields on the same rays and the same d ro / d rd (the eval
+// step's ray sink): per ray, d ro += field 0's, then += field 1's; d rd += field 0's, += between (the rays'
+// gradient that reached them between the two field backwards -- the coarse volume render's), += field 1's:
+// the additions of the two per-field launches with the volume render's in between, in their order.  Then
+// both fields' g_code row blocks.
+__global__ __launch_bounds__(256) void ray_grad_reduce2_kernel(RayRed f0, RayRed f1, int64_t n_rays,
+                                                               const float* __restrict__ between,
+                                                               float* __restrict__ d_ro, float* __restrict__ d_rd) {
+  const int64_t ray_blocks = (n_rays + 3) / 4;
+  const int64_t b = (int64_t)blockIdx.x - ray_blocks;
+  if (b >= f0.gc_blocks) {
+    gc_rows_block(f1.gc_part, f1.gc_waves, f1.gc_rows, b - f0.gc_blocks);
+    return;
+  }
+  if (b >= 0) {
+    gc_rows_block(f0.gc_part, f0.gc_waves, f0.gc_rows, b);
+    return;
+  }
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= n_rays) return;  // wave-uniform
+  float v0[9], v1[9];
+  ray_sums(f0.ray_part, f0.q1_part, n_rays, f0.S, f0.chunk_rows, f0.wave_samples, r, lane, v0);
+  ray_sums(f1.ray_part, f1.q1_part, n_rays, f1.S, f1.chunk_rows, f1.wave_samples, r, lane, v1);
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      if (d_ro) {
+        float o = d_ro[3 * r + i];
+        o += v0[i];
+        o += v1[i];
+        d_ro[3 * r + i] = o;
+      }
+      if (d_rd) {
+        float d = d_rd[3 * r + i];
+        d += v0[3 + i] + v0[6 + i];
+        if (between) d += between[3 * r + i];
+        d += v1[3 + i] + v1[6 + i];
+        d_rd[3 * r + i] = d;
+      }
+    }
+  }
+}
+
+// dst += src over n floats (the fallback of the paired eval backward's in-between ray gradient).
+__global__ void add_into_kernel(float* __restrict__ dst, const float* __restrict__ src, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] += src[i];
 }
 
 }  // namespace grad
@@ -3231,6 +3330,103 @@ extern "C" int cn_field_backward_fused_ws(int fmt_t, const float* packed_t, cons
                      d_rd, a.gc_part, x3 ? 4 : 8, gc_rows);
   CN_TRY(launch_status());
   return reduce(nullptr, gc_rows, a.n_blocks, 1, mlp::kCbStride, g_code, mlp::kCbStride, st);
+}
+
+// A render's two fields' deterministic eval backwards (the eval step's coarse and fine fields on the same
+// rays, adding into the same d ro / d rd -- the pose's ray sink): one dX launch for both
+// (field_w16_bwd2_kernel), one ray / g_code-row launch (ray_grad_reduce2_kernel) and one g_code
+// reduction launch (two jobs), instead of three per field.  The rays' sums are added in the per-field
+// calls' order with d_rd_between (the gradient that reached d rd between the two backwards) in its place,
+// so d ro / d rd are bitwise those of: field 0's call, d_rd += d_rd_between, field 1's call.  Fields that
+// cannot share run exactly that way.
+extern "C" int cn_field_backward_fused_multi(int fmt_t, const cn_field_fused_bwd* fields, int n_fields,
+                                             const float* d_rd_between, cn_stream_t stream) {
+  CN_CHECK_ARG(fields && (n_fields == 1 || n_fields == 2));
+  hipStream_t st = as_stream(stream);
+  auto one = [&](const cn_field_fused_bwd& f) {
+    return cn_field_backward_fused_ws(fmt_t, f.packed_t, f.masks, f.d_raw, f.pts, f.ro, f.rd, f.z, f.n_rays,
+                                      f.n_samples, f.chunk_rows, f.code_index, f.n_codes, f.freqs_xyz, f.freqs_dir,
+                                      f.g_code, f.d_pts, f.d_ro, f.d_rd, f.workspace, stream);
+  };
+  if (n_fields == 1) {
+    CN_CHECK_ARG(!d_rd_between);
+    return one(fields[0]);
+  }
+  const cn_field_fused_bwd &f0 = fields[0], &f1 = fields[1];
+  CN_CHECK_ARG(!d_rd_between || (f0.d_rd && f0.d_rd == f1.d_rd && f0.n_rays == f1.n_rays));
+  bool pair = fmt_t == CN_FMT_F32_W16_T && pair_enabled() && f0.n_rays == f1.n_rays && f0.d_ro == f1.d_ro &&
+              f0.d_rd == f1.d_rd && !f0.pts && !f1.pts && !f0.d_pts && !f1.d_pts;
+  for (const cn_field_fused_bwd* f : {&f0, &f1})
+    pair = pair && f->workspace && f->n_codes == 1 && f->n_samples % 16 == 0 && f->ro && f->z;
+  mlp::FieldArgs a[2];
+  if (pair) {
+    for (int k = 0; k < 2; ++k) {
+      const cn_field_fused_bwd& f = fields[k];
+      CN_TRY(mlp::fused_backward_args(fmt_t, f.packed_t, f.masks, f.d_raw, f.pts, f.ro, f.rd, f.z, f.n_rays,
+                                      f.n_samples, f.chunk_rows, f.code_index, f.n_codes, f.freqs_xyz, f.freqs_dir,
+                                      f.g_code, f.d_pts, f.d_ro, f.d_rd, a[k]));
+      int64_t ray_off = 0, q1_off = 0, rows_off = 0;
+      fused_ws_layout(fmt_t, a[k].m, &ray_off, &q1_off, &rows_off);
+      a[k].gc_part = f.workspace;
+      a[k].ray_part = (f.d_ro || f.d_rd) ? f.workspace + ray_off : nullptr;
+      a[k].q1_part = f.d_rd ? f.workspace + q1_off : nullptr;
+    }
+    const int rc = mlp::launch_field_w16_bwd2(mlp::kFromRayZ, a[0], a[1], st);
+    if (rc == CN_EUNSUPPORTED) pair = false;
+    else if (rc != CN_OK) return rc;
+  }
+  if (!pair) {
+    CN_TRY(one(f0));
+    if (d_rd_between) {
+      const int64_t n = 3 * f0.n_rays;
+      hipLaunchKernelGGL(grad::add_into_kernel, dim3(static_cast<unsigned>(ceil_div(n, 256))), dim3(256), 0, st,
+                         f0.d_rd, d_rd_between, n);
+      CN_TRY(launch_status());
+    }
+    return one(f1);
+  }
+  grad::RayRed rr[2];
+  for (int k = 0; k < 2; ++k) {
+    int64_t rows_off = 0;
+    fused_ws_layout(fmt_t, a[k].m, nullptr, nullptr, &rows_off);
+    rr[k] = grad::RayRed{a[k].ray_part, a[k].q1_part, fields[k].n_samples, fields[k].chunk_rows, a[k].gc_part,
+                         fields[k].workspace + rows_off, a[k].n_blocks, 16, 8};
+  }
+  const int64_t ray_blocks = (f0.d_ro || f0.d_rd) ? ceil_div(f0.n_rays, 4) : 0;
+  hipLaunchKernelGGL(grad::ray_grad_reduce2_kernel,
+                     dim3(static_cast<unsigned>(ray_blocks + rr[0].gc_blocks + rr[1].gc_blocks)), dim3(256), 0, st, rr[0],
+                     rr[1], ray_blocks ? f0.n_rays : 0, d_rd_between, f0.d_ro, f0.d_rd);
+  CN_TRY(launch_status());
+  Reducer red{st, nullptr, {}, 0};
+  for (int k = 0; k < 2; ++k)
+    CN_TRY(reduce(&red, rr[k].gc_rows, a[k].n_blocks, 1, mlp::kCbStride, fields[k].g_code, mlp::kCbStride, st));
+  return red.flush();
+}
+
+// The code backward's first half (cn_code_bias_backward_act) of a render's fields in one launch.
+extern "C" int cn_code_bias_backward_act_multi(const cn_code_act_job* jobs, int n_jobs, const float* z_s,
+                                               const float* z_t, int64_t n_codes, cn_stream_t stream) {
+  using namespace mlp;
+  CN_CHECK_ARG(jobs && (n_jobs == 1 || n_jobs == 2) && z_s && z_t && n_codes > 0 && n_codes < (1ll << 31));
+  grad::CodeDsJob j[2] = {};
+  for (int k = 0; k < n_jobs; ++k) {
+    CN_CHECK_ARG(jobs[k].params && jobs[k].code_act && jobs[k].g_code && jobs[k].workspace);
+    for (int i = 0; i < CN_NUM_PARAMS; ++i) {
+      CN_CHECK_ARG(jobs[k].params[i]);
+      j[k].P.p[i] = jobs[k].params[i];
+      j[k].G.p[i] = jobs[k].grads ? jobs[k].grads[i] : nullptr;
+    }
+    j[k].g = jobs[k].g_code;
+    j[k].act = jobs[k].code_act;
+    j[k].ws = jobs[k].workspace;
+  }
+  if (n_jobs == 1)
+    hipLaunchKernelGGL(grad::code_ds_outer_kernel, dim3(static_cast<unsigned>(n_codes), grad::kCodeSlices), dim3(256), 0,
+                       as_stream(stream), j[0].P, z_s, z_t, j[0].g, j[0].act, j[0].ws, j[0].G);
+  else
+    hipLaunchKernelGGL(grad::code_ds_outer2_kernel, dim3(static_cast<unsigned>(n_codes), 2 * grad::kCodeSlices),
+                       dim3(256), 0, as_stream(stream), j[0], j[1], z_s, z_t);
+  return launch_status();
 }
 
 extern "C" int64_t cn_field_backward_train_workspace_floats(int64_t m) {

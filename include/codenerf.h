@@ -361,6 +361,35 @@ int cn_field_backward_fused_ws(int fmt_t, const float* packed_t, const uint32_t*
                                int64_t n_samples, int64_t chunk_rows, const int64_t* code_index, int64_t n_codes,
                                const float* freqs_xyz, const float* freqs_dir, float* g_code, float* d_pts,
                                float* d_ro, float* d_rd, float* workspace, cn_stream_t stream);
+/* The eval step's two fields (eval.py:153-167: predict_radiance_and_render's coarse and fine fields on the
+ * same rays; the fine depths are detached, point_sampler.py:115, so the two backwards are independent) in
+ * shared launches: each field the arguments of one cn_field_backward_fused_ws call, both adding into the
+ * same d_ro / d_rd.  fp32, rays + depths, one code row, whole waves per ray: one dX launch, one ray /
+ * g_code-row launch and one g_code reduction launch for both; d_ro / d_rd bitwise those of field 0's call,
+ * then d_rd += d_rd_between (optional, n_rays x 3: the rays' gradient that arrives between the two
+ * backwards -- the coarse volume render's), then field 1's call -- which is how fields that cannot share
+ * run.  n_fields 1 or 2 (d_rd_between: 2 only). */
+typedef struct cn_field_fused_bwd {
+  const float* packed_t;
+  const uint32_t* masks;
+  const float* d_raw;
+  const float* pts;
+  const float* ro;
+  const float* rd;
+  const float* z;
+  int64_t n_rays, n_samples, chunk_rows;
+  const int64_t* code_index;
+  int64_t n_codes;
+  const float* freqs_xyz;
+  const float* freqs_dir;
+  float* g_code;
+  float* d_pts;
+  float* d_ro;
+  float* d_rd;
+  float* workspace;
+} cn_field_fused_bwd;
+int cn_field_backward_fused_multi(int fmt_t, const cn_field_fused_bwd* fields, int n_fields, const float* d_rd_between,
+                                  cn_stream_t stream);
 
 /* --- Fused fp32 training step (train.py:92-114; weights trained) ------------------
  * Forward: cn_radiance_field on a CN_FMT_F32_W16 pack that also writes the ReLU masks
@@ -465,6 +494,17 @@ int64_t cn_code_bias_backward_workspace_floats(int64_t n_codes);
 int cn_code_bias_backward_act(const float* const* params, const float* z_s, const float* z_t, int64_t n_codes,
                               const float* code_act, const float* g_code, float* const* grads, float* workspace,
                               cn_stream_t stream);
+/* cn_code_bias_backward_act of a render's 1 or 2 fields on the same codes in ONE launch (each job: the
+ * arguments of one cn_code_bias_backward_act call; bitwise those calls' results). */
+typedef struct cn_code_act_job {
+  const float* const* params;
+  const float* code_act;
+  const float* g_code;
+  float* const* grads;
+  float* workspace;
+} cn_code_act_job;
+int cn_code_bias_backward_act_multi(const cn_code_act_job* jobs, int n_jobs, const float* z_s, const float* z_t,
+                                    int64_t n_codes, cn_stream_t stream);
 /* One field's part of cn_code_dz: its parameters, g_code and cn_code_bias_backward_act's workspace. */
 typedef struct cn_code_dz_job {
   const float* const* params;

@@ -960,3 +960,54 @@ def test_training_forward_encoding_plane(dev, mode, far):
         else:
             assert not plane[:, cp].any(), "padding slot"
     assert (got - ref).abs().max().item() <= 2e-6
+
+
+@pytest.mark.parametrize("r,sc,sf", [(2048, 64, 128), (4096, 32, 160), (300, 16, 32)])
+def test_fused_backward_pair_bitwise(dev, r, sc, sf):
+    """cn_field_backward_fused_multi (the eval step's two fields on the same rays: one dX launch, one ray /
+    g_code-row launch, one g_code reduction) against the two per-field deterministic calls with the
+    in-between d rd added between them: g_code of both fields, d ro and d rd bit for bit.  Also the
+    paired code backward first halves (cn_code_bias_backward_act_multi) against two single calls."""
+    from codenerf import ops, synthetic
+    fx, fd = [2.0 ** k for k in range(10)], [2.0 ** k for k in range(4)]
+    g = torch.Generator().manual_seed(r + sc)
+    ro = (torch.randn(r, 3, generator=g) * 0.3 + torch.tensor([0.0, 0.0, 1.3])).to(dev)
+    rd = torch.randn(r, 3, generator=g).to(dev)
+    zs, zt = synthetic.latent_codes(5, 1).to(dev), synthetic.latent_codes(6, 1).to(dev)
+    between = torch.randn(r, 3, generator=g).to(dev)
+    start = torch.randn(2, r, 3, generator=g).to(dev)
+    fields, acts = [], []
+    for seed, s in ((1, sf), (0, sc)):                      # fine first, as the eval step's pair runs them
+        m = model(dev, seed)
+        params = [p.detach() for p in m.param_list()]
+        z = torch.sort(0.8 + torch.rand(r, s, generator=g), dim=-1).values.to(dev)
+        (cb, _, _, _, act), = ops.field_prepare_models([(params, False, False, 0)], zs, zt, want_act=True)
+        _, masks = ops.radiance_field_masks(ops.mlp_pack(params, "f32_w16"), cb, rd, s, r, fx, fd, ro=ro, z=z,
+                                            precision="f32")
+        fields.append(dict(packed_t=ops.mlp_pack(params, "f32_w16_t"), masks=masks,
+                           d_raw=torch.randn(r, s, 4, generator=g).to(dev), n_rays=r, n_samples=s, chunk_rows=r,
+                           n_codes=1, freqs_xyz=fx, freqs_dir=fd, rd=rd, ro=ro, z=z, want_ro=True, want_rd=True,
+                           precision="f32"))
+        acts.append((params, act))
+    out = {}
+    for mode in ("single", "pair"):
+        d_ro, d_rd = start[0].clone(), start[1].clone()
+        accs = [torch.zeros(ops.field_backward_x3_acc_floats(1, r, True, True), device=dev) for _ in fields]
+        jobs = [dict(f, acc=a, ray_into=(d_ro, d_rd)) for f, a in zip(fields, accs)]
+        if mode == "single":
+            res = [ops.field_backward_x3(**jobs[0])]
+            d_rd.add_(between)
+            res.append(ops.field_backward_x3(**jobs[1]))
+            wss = [ops.code_ds_outer(p, zs, zt, act, rr["g_code"]) for (p, act), rr in zip(acts, res)]
+        else:
+            res = ops.field_backward_x3_multi(jobs, d_rd_between=between)
+            wss = ops.code_ds_outer_multi([(p, act, rr["g_code"], None) for (p, act), rr in zip(acts, res)], zs, zt)
+        torch.cuda.synchronize()
+        out[mode] = (d_ro, d_rd, [rr["g_code"].clone() for rr in res], wss)
+    a, b = out["pair"], out["single"]
+    assert torch.equal(a[0], b[0]), ("d ro", (a[0] - b[0]).abs().max().item())
+    assert torch.equal(a[1], b[1]), ("d rd", (a[1] - b[1]).abs().max().item())
+    for k in range(2):
+        assert torch.equal(a[2][k], b[2][k]), ("g_code", k)
+        # (the first half writes ds1 / ds2 / dt1 into workspace rows 3..5 of each code; rows 0..2 are cn_code_dz's)
+        assert torch.equal(a[3][k][768:1536], b[3][k][768:1536]), ("code_ds_outer workspace", k)

@@ -106,6 +106,7 @@ def _setup(dev, distributed):
 
 
 def _train_worker(rank, world, port, out_dir):
+    import numpy as np
     import torch.distributed as dist
     from codenerf import train as T
     from test_gpu_train import embedders
@@ -116,10 +117,18 @@ def _train_worker(rank, world, port, out_dir):
             with torch.no_grad():
                 models["nerf_fine"].fc_rgb.weight.add_(1.0)
         opt.broadcast_params(0)
+        # the bucketed reduction (the two MLPs' gradients start during the backward, AdamW.allreduce_begin) on
+        # this gloo group too: the sums must be those of the one all-reduce
+        opt.bucket_backends = ("nccl", "gloo")
+        began = []
+        real_begin = opt.allreduce_begin
+        opt.allreduce_begin = lambda *a, **k: began.append(real_begin(*a, **k)) or began[-1]
         ro, rd, ids, tgt = _chunk(dev, 4096, 10 + rank)
+        ids._cn_host_ids = np.full(ids.shape[0], 1, dtype=np.int64)   # as train_iteration hands them over
         for _ in range(2):
             T.train_minibatch(models, opt, sched, ps, embedders(dev), ro, rd, ids, tgt, 1e-5, is_distributed=True)
         torch.cuda.synchronize()
+        assert began == [True, True], began
         torch.save({f"{k}.{n}": p.detach().cpu() for k, m in models.items() for n, p in m.named_parameters()},
                    os.path.join(out_dir, f"params{rank}.pt"))
     finally:
@@ -181,7 +190,8 @@ def test_train_minibatch_two_ranks_no_host_sync(tmp_path):
 
 
 def test_train_allreduce_two_ranks(tmp_path):
-    """Two data-parallel chunk steps on 2 ranks vs one process averaging both chunks' gradients."""
+    """Two data-parallel chunk steps on 2 ranks vs one process averaging both chunks' gradients; the ranks
+    reduce in two buckets (the MLPs' gradients started during the backward, then the rest)."""
     from codenerf import train as T
     from test_gpu_train import embedders
     _spawn(_train_worker, 2, str(tmp_path))

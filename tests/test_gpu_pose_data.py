@@ -251,6 +251,91 @@ def test_eval_c5_chairs_fused_at_size(dev):
         margin(tag, "d " + name, (t - ref).abs().max().item() / scale, C5_CHAIRS_RTOL)
 
 
+def test_ray_sharded_step_equals_full_batch(dev):
+    """The ray-sharded eval step's weighting (evaluate.sharded_eval_step: each share's loss weighted by
+    share / rays, the regulariser expanded over ALL the iteration's rows, the shares' gradients summed)
+    against the unsharded full-batch step.  The one intended difference -- each share is its own Q1
+    chunk, so the view direction paired with a sample differs -- is taken out by zeroing the view-direction
+    columns of both fields' layer_dir1 (the radiance then does not depend on the view direction at all):
+    the two shares' summed loss terms and code / pose gradients must then equal the full batch's to fp32
+    reassociation.  A weighting error common to the sharded path (the rows_total expand, the n / N scale)
+    would show here."""
+    from codenerf import synthetic
+    from codenerf.evaluate import eval_step_loss, shard_of
+    from codenerf.nerf import PointSampler, RaySampler
+    g = gload("eval_c5.npz", dev)
+    rs = RaySampler(128, 128, synthetic.srn_intrinsics(128), sample_size=2048, device=dev, datatype=torch.float32)
+    ps = PointSampler(64, 64, 0.8, 1.8, "lindepth", True, torch.float32, dev)
+    models = _eval_models(dev)
+    with torch.no_grad():
+        for m in models.values():
+            m.layer_dir1.weight[:, 256:].zero_()        # [feat | 27 view-encoding columns]: no view dependence
+    sel = torch.from_numpy(g["select_inds"].cpu().numpy().reshape(1, -1)).to(dev)
+    n = sel.shape[1]
+    runs = {}
+    for mode in ("full", "sharded"):
+        lv = [g[k].clone().requires_grad_(True) for k in ("theta", "phi", "rho", "z_s", "z_t")]
+        parts = [slice(0, n)] if mode == "full" else [shard_of(n, 2, r) for r in range(2)]
+        total, terms = 0.0, torch.zeros(3, dtype=torch.float64)
+        for sl in parts:
+            kw = {} if mode == "full" else dict(rows_total=n)
+            loss, logs = eval_step_loss(*lv, g["target"], (rs, ps), embedders(dev), models, 1e-5, t_rand=g["t_rand"][sl],
+                                        u=g["u"][sl], sel=sel[:, sl], **kw)
+            loss.backward()
+            w = (sl.stop - sl.start) / n
+            total += loss.item()
+            terms += torch.tensor([float(logs["nerf_loss_coarse"]) * w, float(logs["nerf_loss_fine"]) * w,
+                                   float(logs["embedding_loss"])], dtype=torch.float64)
+        runs[mode] = (total, terms, [t.grad.detach().clone() for t in lv])
+    (lf, tf, gf), (ls, ts, gs) = runs["full"], runs["sharded"]
+    assert abs(ls - lf) <= 1e-6 * abs(lf), (ls, lf)
+    assert abs(ts[0] - tf[0]) <= 1e-6 * tf[0] and abs(ts[1] - tf[1]) <= 1e-6 * tf[1], (ts, tf)
+    assert ts[2] / 2 == tf[2], "the regulariser of each share is the whole iteration's (expanded over all rows)"
+    for name, a, b in zip(("theta", "phi", "rho", "z_s", "z_t"), gs, gf):
+        err = (a - b).abs().max().item() / max(b.abs().max().item(), 1e-6)
+        assert err <= 1e-5, (name, err)
+
+
+def test_eval_step_paired_fields(dev, monkeypatch):
+    """eval_step_loss pairs the two fields' fused backwards (autograd.FieldPair: the fine field's waits, the
+    coarse volume render's d rd is held for it, then ONE cn_field_backward_fused_multi call runs both and one
+    cn_code_bias_backward_act_multi their code halves): every gradient -- codes and pose -- and the loss bit
+    for bit those of the unpaired step, on the C5 fixture."""
+    from codenerf import autograd as A, ops, synthetic
+    from codenerf.evaluate import eval_step_loss
+    from codenerf.nerf import PointSampler, RaySampler
+    from codenerf.optim import AdamW
+    g = gload("eval_c5.npz", dev)
+    rs = RaySampler(128, 128, synthetic.srn_intrinsics(128), sample_size=2048, device=dev, datatype=torch.float32)
+    ps = PointSampler(64, 64, 0.8, 1.8, "lindepth", True, torch.float32, dev)
+    models = _eval_models(dev)
+    calls = []
+    real = ops.field_backward_x3_multi
+
+    def spy(*a, **k):
+        calls.append(1)
+        return real(*a, **k)
+    monkeypatch.setattr(ops, "field_backward_x3_multi", spy)
+    out = []
+    for paired in (True, False):
+        if not paired:
+            monkeypatch.setattr(A, "new_field_pair", lambda: None)
+        calls.clear()
+        lv = [g[k].clone().requires_grad_(True) for k in ("theta", "phi", "rho", "z_s", "z_t")]
+        opt = AdamW([{"params": lv[3:]}, {"params": lv[:2]}, {"params": lv[2:3]}], lr=1e-2)
+        opt.zero_grad()
+        np.random.seed(17)
+        loss, _ = eval_step_loss(*lv, g["target"], (rs, ps), embedders(dev), models, 1e-5, t_rand=g["t_rand"],
+                                 u=g["u"])
+        A.backward_from(loss)
+        torch.cuda.synchronize()
+        out.append((loss.item(), [t.grad.clone() for t in lv], len(calls)))
+    assert out[0][2] == 1 and out[1][2] == 0, (out[0][2], out[1][2])
+    assert out[0][0] == out[1][0]
+    for name, a, b in zip(("theta", "phi", "rho", "z_s", "z_t"), out[0][1], out[1][1]):
+        assert torch.equal(a, b), (name, (a - b).abs().max().item())
+
+
 @pytest.mark.parametrize("precision", ["f32", "bf16x3"])
 def test_eval_step_in_place_gradients(dev, monkeypatch, precision):
     """The eval step's gradient sinks (C5 inputs, the flat AdamW's zeroed slots handed out by zero_grad):

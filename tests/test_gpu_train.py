@@ -707,15 +707,17 @@ def test_train_shape_chunk_at_size(dev, name):
         gn = max(g["gnorm_" + k].item(), 1e-12)
         perr = _proj(r, p.grad) - g["gproj_" + k].cpu()
         worst["proj"] = max(worst["proj"], (perr.abs().max().item() / gn, k))
-        # post-step change, projected: AdamW's first step is lr sign(g) (+ decay) per element, so only
-        # elements whose gradient sign the gradient error can flip move differently, by at most 2 lr each.
-        # The error's norm is estimated from the 16 projections (E[(r . e)^2] = |e|^2); an element with
-        # |g| above twice that estimate keeps its sign.  The bound per direction is 2 lr sum of |r| over the
-        # others (+ float slack); the error is stated as a fraction of it.
+        # post-step change, projected: AdamW's first step moves element i by lr q(g_i), q(x) = x / (|x| + eps)
+        # (+ the same decay), so an element moves differently only as far as the gradient error e_i moves
+        # q: by at most 2 lr where |g_i| <= E (the sign may flip), else by lr eps E / ((|g_i| + eps)
+        # (|g_i| - E + eps)) -- with E twice the error norm estimated from the 16 projections
+        # (E[(r . e)^2] = |e|^2).  The bound per direction sums those caps weighted by |r| (+ float slack);
+        # the error is stated as a fraction of it.
         dp = (_proj(r, p.detach() - before[k]) - g["pproj_" + k].cpu()).abs()
-        gd = p.grad.detach().double().cpu().reshape(-1)
-        undet = gd.abs() <= 2.0 * perr.pow(2).mean().sqrt() + 1e-12
-        cap = 2.05 * lr * (r.double().reshape(r.shape[0], -1).abs() * undet[None]).sum(1) + 1e-3 * lr * p.numel() ** 0.5
+        gd = p.grad.detach().double().cpu().reshape(-1).abs()
+        E, eps = 2.0 * perr.pow(2).mean().sqrt().item() + 1e-12, 1e-8
+        ci = torch.where(gd <= E, torch.full_like(gd, 2.0), eps * E / ((gd + eps) * (gd - E + eps)))
+        cap = 1.05 * lr * (r.double().reshape(r.shape[0], -1).abs() * ci[None]).sum(1) + 1e-3 * lr * p.numel() ** 0.5
         worst["step_proj"] = max(worst["step_proj"], ((dp / cap).max().item(), k))
     margin(tag, "grad full tensors (worst: %s)" % worst["grad"][1], worst["grad"][0], rtol)
     margin(tag, "grad projections (worst: %s)" % worst["proj"][1], worst["proj"][0], prtol)
