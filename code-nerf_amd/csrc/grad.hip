@@ -670,11 +670,12 @@ struct TnJob {
   const float* draw; // SIG, RGB: the (M, 4) d raw rows
   float* sig_part;   // SIG: n_blocks x 256
   int64_t M, rows_per_block;
-  int kind;          // 0 plain, 1 SIG (fc_out's sigma row), 2 DIRS (layer_dir1's view-encoding fold), 3 RGB
+  int kind;          // 0 plain, 1 SIG (fc_out's sigma row), 2 DIRS (layer_dir1's view-encoding fold), 3 RGB,
+                     // 4 XENC (layer_xyz1's dW from the encoding plane, gemm_tn_xenc_kernel's row pass)
   int first_block, n_blocks;
   DirFold dir;
 };
-constexpr int kMaxTnJobs = 10;   // a field's five, or a render's two fields' (tn_batch_launch2)
+constexpr int kMaxTnJobs = 12;   // a field's five (six with the XENC role), or a render's two fields' (tn_batch_launch2)
 struct TnJobs {
   TnJob j[kMaxTnJobs];
   int n;
@@ -771,26 +772,6 @@ __device__ __forceinline__ void rgb_body(float* ring, const float* __restrict__ 
 }
 
 
-template <bool X3>
-__global__ __launch_bounds__(512, 2) void gemm_tn256_jobs_kernel(TnJobs jobs) {
-  __shared__ __attribute__((aligned(16))) float ring[kTwRing * kTwStage];
-  int k = jobs.n - 1;
-  while (k > 0 && static_cast<int>(blockIdx.x) < jobs.j[k].first_block) --k;
-  const TnJob& j = jobs.j[k];
-  const unsigned blk = blockIdx.x - static_cast<unsigned>(j.first_block), nblk = static_cast<unsigned>(j.n_blocks);
-  if (j.kind == 1) {
-    tn256_body<X3, true, false>(ring, j.A, j.B, nullptr, 0, j.part, j.bias_part, j.draw, j.sig_part, j.M,
-                                j.rows_per_block, j.dir, blk, nblk);
-  } else if (!X3 && j.kind == 2) {
-    tn256_body<false, false, true>(ring, j.A, j.B, nullptr, 0, j.part, j.bias_part, nullptr, nullptr, j.M,
-                                   j.rows_per_block, j.dir, blk, nblk);
-  } else if (!X3 && j.kind == 3) {
-    rgb_body(ring, j.draw, j.B, j.part, j.bias_part, j.M, j.rows_per_block, blk, nblk);
-  } else {
-    tn256_body<X3, false, false>(ring, j.A, j.B, nullptr, 0, j.part, j.bias_part, nullptr, nullptr, j.M,
-                                 j.rows_per_block, j.dir, blk, nblk);
-  }
-}
 
 // gemm_tn for a skinny dPre (N = NA <= 4 columns, e.g. d rgb / d sigma of d raw) against a
 // 256-wide X: a streaming pass over X (float4 per lane, 4 rows per 256-thread step) with the
@@ -1427,17 +1408,12 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_enc_kernel(const float* __rest
 // the encodings are exactly the forward's (lazy fast_sincosf or ocml sincosf, per wave).
 // Wave w: output rows 32 w .. + 31, both 32-column blocks (c' 0..63); fp32 32x32x2.
 constexpr int kXRS = 288, kXES = 96;   // LDS row strides (floats): 32 banks between a pair's rows
-__device__ __forceinline__ void xenc_body(const float* __restrict__ A, const float* __restrict__ X, int64_t M,
-                                          float* __restrict__ part, float* __restrict__ bias_part,
-                                          int64_t rows_per_block, const mlp::FieldArgs& a, const DirRole& dr,
-                                          const unsigned bid) {
-  if (bid < dr.n) {
-    dir_enc_dw_block(a, dr.dir, dr.part, dr.bias_part, bid);
-    return;
-  }
-  const unsigned blk = bid - dr.n;
-  __shared__ __attribute__((aligned(16))) float ring[kEncRing][kEncRows * kXRS];
-  __shared__ __attribute__((aligned(16))) float xring[kEncRing][kEncRows * kXES];
+constexpr int kXencLds = kEncRing * kEncRows * (kXRS + kXES);   // floats of LDS the row pass takes
+// Workgroup blk's rows of layer_xyz1's dW from the encoding plane; ring_a / ring_x: its LDS rings
+// (kEncRing slots of kEncRows rows, strides kXRS / kXES floats).
+__device__ __forceinline__ void xenc_rows(float* ring_a, float* ring_x, const float* __restrict__ A,
+                                          const float* __restrict__ X, int64_t M, float* __restrict__ part,
+                                          float* __restrict__ bias_part, int64_t rows_per_block, const unsigned blk) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int i = lane & 31, h = lane >> 5;
@@ -1452,8 +1428,8 @@ __device__ __forceinline__ void xenc_body(const float* __restrict__ A, const flo
       const_cast<float*>(X + mb * 64), 0, static_cast<unsigned>(rows * 64 * 4), 0x00020000);
   // stage st: wave w moves A rows w, w + 8 and X rows w, w + 8 (4 vector-memory ops per wave)
   auto dma = [&](int st) {
-    float* slot = ring[st % kEncRing];
-    float* xslot = xring[st % kEncRing];
+    float* slot = ring_a + (st % kEncRing) * (kEncRows * kXRS);
+    float* xslot = ring_x + (st % kEncRing) * (kEncRows * kXES);
 #pragma unroll
     for (int j = 0; j < kEncRows / 8; ++j) {
       const int r = wave + 8 * j;
@@ -1474,8 +1450,8 @@ __device__ __forceinline__ void xenc_body(const float* __restrict__ A, const flo
     asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     dma(st + 2);  // always (past the slab: zeros), so every wave's vmcnt above stays exact
-    const float* sa = ring[st % kEncRing];
-    const float* sx = xring[st % kEncRing];
+    const float* sa = ring_a + (st % kEncRing) * (kEncRows * kXRS);
+    const float* sx = ring_x + (st % kEncRing) * (kEncRows * kXES);
     float xa[8], xb[2][8];
     ring_read8<2 * kXRS * 4>(sa + h * kXRS + 32 * wave + i, xa);   // rows 2 p + h
 #pragma unroll
@@ -1507,6 +1483,18 @@ __device__ __forceinline__ void xenc_body(const float* __restrict__ A, const flo
   }
 }
 
+__device__ __forceinline__ void xenc_body(const float* __restrict__ A, const float* __restrict__ X, int64_t M,
+                                          float* __restrict__ part, float* __restrict__ bias_part,
+                                          int64_t rows_per_block, const mlp::FieldArgs& a, const DirRole& dr,
+                                          const unsigned bid) {
+  if (bid < dr.n) {
+    dir_enc_dw_block(a, dr.dir, dr.part, dr.bias_part, bid);
+    return;
+  }
+  __shared__ __attribute__((aligned(16))) float lds[kXencLds];
+  xenc_rows(lds, lds + kEncRing * kEncRows * kXRS, A, X, M, part, bias_part, rows_per_block, bid - dr.n);
+}
+
 __global__ __launch_bounds__(512, 1) void gemm_tn_xenc_kernel(const float* __restrict__ A, const float* __restrict__ X,
                                                               int64_t M, float* __restrict__ part,
                                                               float* __restrict__ bias_part, int64_t rows_per_block,
@@ -1535,6 +1523,31 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_xenc2_kernel(XencJob j0, XencJ
     xenc_body(j1.A, j1.X, j1.M, j1.part, j1.bias_part, j1.rows_per_block, j1.a, j1.dr, blockIdx.x - first1);
   else
     xenc_body(j0.A, j0.X, j0.M, j0.part, j0.bias_part, j0.rows_per_block, j0.a, j0.dr, blockIdx.x);
+}
+
+// (the batched dW launch: defined after the roles it runs)
+static_assert(kXencLds <= kTwRing * kTwStage, "the XENC role's rings live in the whole-tile ring's LDS");
+template <bool X3>
+__global__ __launch_bounds__(512, 2) void gemm_tn256_jobs_kernel(TnJobs jobs) {
+  __shared__ __attribute__((aligned(16))) float ring[kTwRing * kTwStage];
+  int k = jobs.n - 1;
+  while (k > 0 && static_cast<int>(blockIdx.x) < jobs.j[k].first_block) --k;
+  const TnJob& j = jobs.j[k];
+  const unsigned blk = blockIdx.x - static_cast<unsigned>(j.first_block), nblk = static_cast<unsigned>(j.n_blocks);
+  if (j.kind == 1) {
+    tn256_body<X3, true, false>(ring, j.A, j.B, nullptr, 0, j.part, j.bias_part, j.draw, j.sig_part, j.M,
+                                j.rows_per_block, j.dir, blk, nblk);
+  } else if (!X3 && j.kind == 2) {
+    tn256_body<false, false, true>(ring, j.A, j.B, nullptr, 0, j.part, j.bias_part, nullptr, nullptr, j.M,
+                                   j.rows_per_block, j.dir, blk, nblk);
+  } else if (!X3 && j.kind == 3) {
+    rgb_body(ring, j.draw, j.B, j.part, j.bias_part, j.M, j.rows_per_block, blk, nblk);
+  } else if (!X3 && j.kind == 4) {
+    xenc_rows(ring, ring + kEncRing * kEncRows * kXRS, j.A, j.B, j.M, j.part, j.bias_part, j.rows_per_block, blk);
+  } else {
+    tn256_body<X3, false, false>(ring, j.A, j.B, nullptr, 0, j.part, j.bias_part, nullptr, nullptr, j.M,
+                                 j.rows_per_block, j.dir, blk, nblk);
+  }
 }
 
 __global__ __launch_bounds__(256) void dir_enc_dw_kernel(mlp::FieldArgs a, DirFold dir, float* __restrict__ part,
@@ -3063,6 +3076,21 @@ static bool xenc_plane_enabled() {
   return on != 0;
 }
 
+// layer_xyz1's dW (the fp32 encoding-plane pass) as a job of the batched dW launch instead of its own
+// launch (the DIRS fold's per-direction pass then runs alone after it, on the launch's direction sums):
+// the batched launch grows by ~220 us per C3 chunk -- the pass is MFMA work (a quarter of a 256 x 256
+// GEMM's per row), not a stream that hides beside the GEMMs -- against ~237 us for its own launch and
+// fewer partial tiles to reduce (r06f: C3 39.14 / 39.19 -> 39.17 / 38.96 ms, 3080 13.77 / 13.80 ->
+// 13.63 / 13.60 ms at slot cost 0.3; 0.25 starves it: 42.7 ms; 0.4 takes CUs from the GEMMs).
+// CN_XENC_ROLE=0: its own launch (A/B).
+static bool xenc_role_enabled() {
+  static const int on = [] {
+    const char* e = getenv("CN_XENC_ROLE");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return on != 0;
+}
+
 // CN_DIR_IN_ENC=0: the DIRS fold's dir_enc_dw pass as its own launch again (A/B; bitwise the same)
 static bool dir_in_enc_enabled() {
   static const int on = [] {
@@ -3097,10 +3125,10 @@ static bool tn_jobs_enabled() {
 // 41.7 ms per C3 iteration), 1 KiB per row, ~0.12 of a whole-tile row.  Kept a little above that:
 // a late RGB workgroup holds up the whole launch, a spare one costs 1/256 of it.
 static const float* tn_slot_cost() {
-  static float w[5] = {1.0f, 1.03f, 1.05f, 1.0f, 0.16f};
+  static float w[6] = {1.0f, 1.03f, 1.05f, 1.0f, 0.16f, 0.3f};
   static const bool init = [] {
     const char* e = getenv("CN_TN_COST");
-    if (e) sscanf(e, "%f,%f,%f,%f,%f", &w[0], &w[1], &w[2], &w[3], &w[4]);
+    if (e) sscanf(e, "%f,%f,%f,%f,%f,%f", &w[0], &w[1], &w[2], &w[3], &w[4], &w[5]);
     return true;
   }();
   (void)init;
@@ -3149,6 +3177,14 @@ static int tn_batch_plan(TnBatch& b, Reducer* rd, grad::TnJobs& jobs) {
       j.n_blocks = static_cast<int>(ceil_div(q.M, rows));
       j.rows_per_block = rows;
     }
+    if (q.kind == 4) {  // XENC: 256 x 63 partials (PositionalEmbedder column order), bias column sums
+      j.part = rd->take((int64_t)j.n_blocks * 256 * 63);
+      j.bias_part = q.bias ? rd->take((int64_t)j.n_blocks * 256) : nullptr;
+      j.draw = nullptr;
+      j.sig_part = nullptr;
+      first += j.n_blocks;
+      continue;
+    }
     if (q.kind == 3) {  // RGB: 3 x 256 partials, 4 d raw column sums per block
       j.part = rd->take((int64_t)j.n_blocks * 3 * 256);
       j.bias_part = rd->take((int64_t)j.n_blocks * 4);
@@ -3193,6 +3229,11 @@ static int tn_batch_post(TnBatch& b, const grad::TnJobs& jobs, hipStream_t st, R
       CN_TRY(reduce(rd, j.part, j.n_blocks, 256, 256, q.C, q.ldc, st));
       CN_TRY(reduce(rd, ep, nd, 256, 27, q.C + 256, q.ldc, st));
       CN_TRY(reduce(rd, bp, nd, 1, 256, q.bias, 256, st));
+      continue;
+    }
+    if (q.kind == 4) {
+      CN_TRY(reduce(rd, j.part, j.n_blocks, 256, 63, q.C, q.ldc, st));
+      if (q.bias) CN_TRY(reduce(rd, j.bias_part, j.n_blocks, 1, 256, q.bias, 256, st));
       continue;
     }
     if (q.kind == 3) {
@@ -3449,6 +3490,7 @@ extern "C" int cn_field_backward_train(const float* packed_t, const float* const
 // stages so that a render's two fields can share their launches (cn_field_backward_train_multi).
 struct TrainBwd {
   bool x3 = false, wg = false, fold_code = false, jobs = false, rgb_role = false, dual_code = false, dirs = false;
+  bool xenc_job = false;   // layer_xyz1's dW rides in the batched launch (CN_XENC_ROLE=1)
   int mode = 0;
   mlp::FieldArgs a = {};
   const float* saved = nullptr;
@@ -3462,6 +3504,9 @@ struct TrainBwd {
   TnBatch tb;
   grad::DirRole dir_role = {};
 };
+
+// layer_xyz1's dW reads the fp32 forward's own encodings (saved's encoding plane)
+static bool train_bwd_xenc(const TrainBwd& t) { return !t.x_enc && !t.x3 && xenc_plane_enabled(); }
 
 static int train_bwd_setup(int fmt_t, const cn_field_train_bwd& f, TrainBwd& t) {
   using namespace mlp;
@@ -3526,6 +3571,7 @@ static int train_bwd_setup(int fmt_t, const cn_field_train_bwd& f, TrainBwd& t) 
   t.rgb_role = t.jobs && t.fold_code && !t.x3;
   t.dual_code = t.rgb_role;  // the g_code sums also land in the bias gradients (below)
   t.dirs = t.jobs && !t.x3 && !t.x_enc && dirs_foldable(a);
+  t.xenc_job = t.jobs && t.wg && train_bwd_xenc(t) && xenc_role_enabled();
   return CN_OK;
 }
 
@@ -3583,6 +3629,9 @@ static int train_bwd_queue(TrainBwd& t, hipStream_t st) {
     if (t.rgb_role)
       tb.p[tb.n++] = {t.d_raw, v2, M, 3, G(kWRgb), 512, t.g_code + kCbRgb, t.d_raw, t.g_code + kCbSigma, {}, c[4],
                       t.dual_code ? G(kBRgb) : nullptr, t.dual_code ? G(kBOut) : nullptr};
+    if (t.xenc_job)   // layer_xyz1 from the forward's encoding plane (saved + 5 M 256)
+      tb.p[tb.n++] = {P[4], t.saved + 5 * M * 256, M, 4, G(kWXyz1), 63, B(kBXyz1), nullptr, nullptr, {}, c[5], nullptr,
+                      nullptr};
     return CN_OK;
   }
   // layer_dir2
@@ -3621,8 +3670,6 @@ static int train_bwd_after_jobs(TrainBwd& t, hipStream_t st) {
   return gemm_tn_enc(1, t.P[1], t.a, C, 283, st, t.x3, nullptr, nullptr, nullptr, &t.red);
 }
 
-// layer_xyz1's dW reads the fp32 forward's own encodings (saved's encoding plane)
-static bool train_bwd_xenc(const TrainBwd& t) { return !t.x_enc && !t.x3 && xenc_plane_enabled(); }
 
 // layer_xyz1 (its own launch: as a role of the batched launch it ran no faster per CU -- it is compute
 // work, not a bandwidth pass that could hide beside the GEMMs; r03m)
@@ -3630,6 +3677,12 @@ static int train_bwd_xyz1(TrainBwd& t, hipStream_t st) {
   using namespace mlp;
   float* C = t.grads[kWXyz1];
   float* bias = t.grads[kBXyz1];
+  if (t.xenc_job) {   // its dW ran in the batched launch: the DIRS fold's per-direction pass alone
+    if (t.dir_role.n == 0) return CN_OK;
+    hipLaunchKernelGGL(grad::gemm_tn_xenc_kernel, dim3(t.dir_role.n), dim3(512), 0, st, nullptr, nullptr, 0, nullptr,
+                       nullptr, 0, t.a, t.dir_role);
+    return launch_status();
+  }
   if (t.x_enc)
     return gemm_tn(t.P[4], 256, t.x_enc, 90, C, 63, t.a.m, 256, 63, st, t.x3, nullptr, bias, nullptr, &t.red);
   if (train_bwd_xenc(t)) return gemm_tn_xenc(t.P[4], t.saved + 5 * t.a.m * 256, t.a, C, 63, st, bias, &t.red, t.dir_role);
@@ -3642,6 +3695,15 @@ static int train_bwd_xyz1_pair(TrainBwd& t0, TrainBwd& t1, hipStream_t st) {
   grad::XencJob j[2];
   TrainBwd* t[2] = {&t0, &t1};
   unsigned blocks[2];
+  if (t0.xenc_job && t1.xenc_job) {   // their dW ran in the batched launch: the DIRS passes alone
+    for (int f = 0; f < 2; ++f) {
+      j[f] = grad::XencJob{nullptr, nullptr, 0, nullptr, nullptr, 0, t[f]->a, t[f]->dir_role};
+      blocks[f] = t[f]->dir_role.n;
+    }
+    if (blocks[0] + blocks[1] == 0) return CN_OK;
+    hipLaunchKernelGGL(grad::gemm_tn_xenc2_kernel, dim3(blocks[0] + blocks[1]), dim3(512), 0, st, j[0], j[1], blocks[0]);
+    return launch_status();
+  }
   for (int f = 0; f < 2; ++f) {
     const int64_t m = t[f]->a.m, rows = enc_rows(m);
     const unsigned nb = static_cast<unsigned>(ceil_div(m, rows));
