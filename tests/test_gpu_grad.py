@@ -606,7 +606,9 @@ def test_field_backward_train_dir1_fold(dev, mode, r, s, chunk):
     sums of its dPre plane taken during the [feat] pass (gemm_tn256_kernel DIRS +
     dir_enc_dw_kernel): the Q1 map makes rows j rcnt + d of a chunk share direction d.  Checked
     against the x_enc-plane GEMMs (the encodings as the forward made them) at GEMM_TOL; every other
-    gradient is the same computation, bit for bit; two runs are bitwise identical."""
+    gradient is the same products, at fp32 rounding: with generated encodings layer_xyz1's dW joins the
+    batched dW launch (grad.hip xenc_role_enabled), whose split of rows over the jobs -- so the other
+    weights' partial-tile grouping -- follows its job list; two runs are bitwise identical."""
     from codenerf import ops, synthetic
     m = model(dev, 0)
     params = [p.detach() for p in m.param_list()]
@@ -636,10 +638,8 @@ def test_field_backward_train_dir1_fold(dev, mode, r, s, chunk):
             close(a, b.double(), GEMM_TOL["f32"], f"param {k} folded vs plane")
         elif k == 13:
             close(a, b.double(), 1e-5, "layer_dir1 bias")
-        elif k in (2, 4, 14, 16):
-            assert torch.equal(a, b), f"param {k}: weight gradient outside the fold changed"
         else:
-            close(a, b.double(), 1e-5, f"bias {k}")
+            close(a, b.double(), 1e-5, f"param {k}")
         assert torch.equal(a, out["folded2"][k]), f"param {k}: not reproducible"
 
 
