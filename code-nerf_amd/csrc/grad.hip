@@ -2317,13 +2317,33 @@ __device__ __forceinline__ void gc_rows_block(const float* __restrict__ gc_part,
   }
 }
 
+// The g_code rows' fixed-order sum (reduce_partials_kernel's reduce_block over the workgroups' rows) as
+// blocks of the ray launch, when the backward already wrote one row per workgroup (fp32: gc_rows).
+struct GcFinal {
+  const float* rows;
+  int64_t n_rows;
+  float* g_code;
+  int64_t blocks;
+};
+
+__device__ __forceinline__ void gc_final_block(const GcFinal& f, int64_t b, float4 (&red)[16][64]) {
+  if (reduce_groups(f.n_rows) == 16) reduce_block<16>(f.rows, f.n_rows, 1, mlp::kCbStride, f.g_code, mlp::kCbStride, b, red);
+  else reduce_block<4>(f.rows, f.n_rows, 1, mlp::kCbStride, f.g_code, mlp::kCbStride, b, red);
+}
+
 __global__ __launch_bounds__(256) void ray_grad_reduce_kernel(const float* __restrict__ ray_part,
                                                               const float* __restrict__ q1_part, int64_t n_rays,
                                                               int64_t S, int64_t chunk_rows, int wave_samples,
                                                               float* __restrict__ d_ro, float* __restrict__ d_rd,
                                                               const float* __restrict__ gc_part, int gc_waves,
-                                                              float* __restrict__ gc_rows) {
+                                                              float* __restrict__ gc_rows, int64_t gc_blocks,
+                                                              GcFinal fin) {
+  __shared__ float4 red[16][64];
   const int64_t ray_blocks = (n_rays + 3) / 4;
+  if ((int64_t)blockIdx.x >= ray_blocks + gc_blocks) {
+    gc_final_block(fin, (int64_t)blockIdx.x - ray_blocks - gc_blocks, red);
+    return;
+  }
   if ((int64_t)blockIdx.x >= ray_blocks) {
     gc_rows_block(gc_part, gc_waves, gc_rows, (int64_t)blockIdx.x - ray_blocks);
     return;
@@ -2347,28 +2367,27 @@ struct RayRed {
   const float* ray_part;
   const float* q1_part;
   int64_t S, chunk_rows;
-  const float* gc_part;
-  float* gc_rows;
-  int64_t gc_blocks;
-  int wave_samples, gc_waves;
+  GcFinal fin;        // the field's g_code: its workgroups' rows (written by the backward) summed here
+  int wave_samples;
 };
 
 // ray_grad_reduce_kernel for a render's two fields on the same rays and the same d ro / d rd (the eval
 // step's ray sink): per ray, d ro += field 0's, then += field 1's; d rd += field 0's, += between (the rays'
 // gradient that reached them between the two field backwards -- the coarse volume render's), += field 1's:
 // the additions of the two per-field launches with the volume render's in between, in their order.  Then
-// both fields' g_code row blocks.
+// both fields' g_code sums (their workgroups' rows, written by the backward).
 __global__ __launch_bounds__(256) void ray_grad_reduce2_kernel(RayRed f0, RayRed f1, int64_t n_rays,
                                                                const float* __restrict__ between,
                                                                float* __restrict__ d_ro, float* __restrict__ d_rd) {
+  __shared__ float4 red[16][64];
   const int64_t ray_blocks = (n_rays + 3) / 4;
   const int64_t b = (int64_t)blockIdx.x - ray_blocks;
-  if (b >= f0.gc_blocks) {
-    gc_rows_block(f1.gc_part, f1.gc_waves, f1.gc_rows, b - f0.gc_blocks);
+  if (b >= f0.fin.blocks) {
+    gc_final_block(f1.fin, b - f0.fin.blocks, red);
     return;
   }
   if (b >= 0) {
-    gc_rows_block(f0.gc_part, f0.gc_waves, f0.gc_rows, b);
+    gc_final_block(f0.fin, b, red);
     return;
   }
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -3319,6 +3338,15 @@ static int rgb_dw_draw_sums(const float* d_raw, const float* v2, float* C, int64
 
 // ---- the fused eval backward without float atomics (one code row, every wave inside one ray)
 
+// The g_code sum of rows (n_rows x kCbStride, one per backward workgroup) as blocks of a ray launch
+// (grad::gc_final_block: reduce()'s blocks for the same sum); rows null -> none.
+static grad::GcFinal gc_final(const float* rows, int64_t n_rows, float* g_code) {
+  if (!rows) return grad::GcFinal{nullptr, 0, nullptr, 0};
+  const int64_t blocks = ceil_div(
+      mlp::kCbStride, grad::reduce_block_elems(grad::reduce_groups(n_rows), grad::reduce_vec4(rows, mlp::kCbStride)));
+  return grad::GcFinal{rows, n_rows, g_code, blocks};
+}
+
 static int64_t fused_ws_layout(int fmt_t, int64_t m, int64_t* ray_off, int64_t* q1_off, int64_t* rows_off) {
   const int64_t ws = fmt_t == CN_FMT_BF16X3_T ? 32 : 16;
   // the launch's grid is at most one workgroup per 128-sample tile and kMaxBwdBlocks
@@ -3359,24 +3387,28 @@ extern "C" int cn_field_backward_fused_ws(int fmt_t, const float* packed_t, cons
     a.gc_part = workspace;
     a.ray_part = mode == mlp::kFromRayZ && (d_ro || d_rd) ? workspace + ray_off : nullptr;
     a.q1_part = d_rd ? workspace + q1_off : nullptr;
+    if (!x3) a.gc_rows = workspace + rows_off;  // the fp32 kernel adds its waves' rows itself
   }
   CN_TRY(x3 ? mlp::launch_field_x3_bwd(mode, a, st) : mlp::launch_field_w16_bwd(mode, a, st));
   if (!det) return CN_OK;
-  // one launch: the rays' sums, and each workgroup's wave rows added in wave order (gc_rows); then
-  // g_code += those rows in block order (the dW GEMMs' fixed-order reduction)
+  // one launch: the rays' sums; each workgroup's wave rows added in wave order (gc_rows: the fp32
+  // kernel's own tail, x3 here); g_code += those rows in block order (the dW GEMMs' fixed-order
+  // reduction: here for fp32, a launch of its own after this one for x3)
   float* gc_rows = workspace + rows_off;
   const int64_t ray_blocks = a.ray_part || a.q1_part ? ceil_div(n_rays, 4) : 0;
-  hipLaunchKernelGGL(grad::ray_grad_reduce_kernel, dim3(static_cast<unsigned>(ray_blocks + a.n_blocks)), dim3(256), 0,
-                     st, a.ray_part, a.q1_part, ray_blocks ? n_rays : 0, n_samples, chunk_rows, wave_samples, d_ro,
-                     d_rd, a.gc_part, x3 ? 4 : 8, gc_rows);
+  const grad::GcFinal fin = gc_final(x3 ? nullptr : gc_rows, a.n_blocks, g_code);
+  const int64_t row_blocks = x3 ? a.n_blocks : 0;
+  hipLaunchKernelGGL(grad::ray_grad_reduce_kernel, dim3(static_cast<unsigned>(ray_blocks + row_blocks + fin.blocks)),
+                     dim3(256), 0, st, a.ray_part, a.q1_part, ray_blocks ? n_rays : 0, n_samples, chunk_rows,
+                     wave_samples, d_ro, d_rd, a.gc_part, 4, gc_rows, row_blocks, fin);
   CN_TRY(launch_status());
-  return reduce(nullptr, gc_rows, a.n_blocks, 1, mlp::kCbStride, g_code, mlp::kCbStride, st);
+  return x3 ? reduce(nullptr, gc_rows, a.n_blocks, 1, mlp::kCbStride, g_code, mlp::kCbStride, st) : CN_OK;
 }
 
 // A render's two fields' deterministic eval backwards (the eval step's coarse and fine fields on the same
 // rays, adding into the same d ro / d rd -- the pose's ray sink): one dX launch for both
-// (field_w16_bwd2_kernel), one ray / g_code-row launch (ray_grad_reduce2_kernel) and one g_code
-// reduction launch (two jobs), instead of three per field.  The rays' sums are added in the per-field
+// (field_w16_bwd2_kernel, whose workgroups also add up their waves' g_code rows) and one ray / g_code
+// launch (ray_grad_reduce2_kernel), instead of two per field.  The rays' sums are added in the per-field
 // calls' order with d_rd_between (the gradient that reached d rd between the two backwards) in its place,
 // so d ro / d rd are bitwise those of: field 0's call, d_rd += d_rd_between, field 1's call.  Fields that
 // cannot share run exactly that way.
@@ -3411,6 +3443,7 @@ extern "C" int cn_field_backward_fused_multi(int fmt_t, const cn_field_fused_bwd
       a[k].gc_part = f.workspace;
       a[k].ray_part = (f.d_ro || f.d_rd) ? f.workspace + ray_off : nullptr;
       a[k].q1_part = f.d_rd ? f.workspace + q1_off : nullptr;
+      a[k].gc_rows = f.workspace + rows_off;
     }
     const int rc = mlp::launch_field_w16_bwd2(mlp::kFromRayZ, a[0], a[1], st);
     if (rc == CN_EUNSUPPORTED) pair = false;
@@ -3427,21 +3460,14 @@ extern "C" int cn_field_backward_fused_multi(int fmt_t, const cn_field_fused_bwd
     return one(f1);
   }
   grad::RayRed rr[2];
-  for (int k = 0; k < 2; ++k) {
-    int64_t rows_off = 0;
-    fused_ws_layout(fmt_t, a[k].m, nullptr, nullptr, &rows_off);
-    rr[k] = grad::RayRed{a[k].ray_part, a[k].q1_part, fields[k].n_samples, fields[k].chunk_rows, a[k].gc_part,
-                         fields[k].workspace + rows_off, a[k].n_blocks, 16, 8};
-  }
+  for (int k = 0; k < 2; ++k)
+    rr[k] = grad::RayRed{a[k].ray_part, a[k].q1_part, fields[k].n_samples, fields[k].chunk_rows,
+                         gc_final(a[k].gc_rows, a[k].n_blocks, fields[k].g_code), 16};
   const int64_t ray_blocks = (f0.d_ro || f0.d_rd) ? ceil_div(f0.n_rays, 4) : 0;
   hipLaunchKernelGGL(grad::ray_grad_reduce2_kernel,
-                     dim3(static_cast<unsigned>(ray_blocks + rr[0].gc_blocks + rr[1].gc_blocks)), dim3(256), 0, st, rr[0],
-                     rr[1], ray_blocks ? f0.n_rays : 0, d_rd_between, f0.d_ro, f0.d_rd);
-  CN_TRY(launch_status());
-  Reducer red{st, nullptr, {}, 0};
-  for (int k = 0; k < 2; ++k)
-    CN_TRY(reduce(&red, rr[k].gc_rows, a[k].n_blocks, 1, mlp::kCbStride, fields[k].g_code, mlp::kCbStride, st));
-  return red.flush();
+                     dim3(static_cast<unsigned>(ray_blocks + rr[0].fin.blocks + rr[1].fin.blocks)), dim3(256), 0, st,
+                     rr[0], rr[1], ray_blocks ? f0.n_rays : 0, d_rd_between, f0.d_ro, f0.d_rd);
+  return launch_status();
 }
 
 // The code backward's first half (cn_code_bias_backward_act) of a render's fields in one launch.

@@ -49,6 +49,7 @@ struct FieldArgs {
   // fused eval backward, deterministic form (cn_field_backward_fused_ws: one code row, every wave inside
   // one ray): no float atomics -- partials a fixed-order reduction adds up afterwards
   float* gc_part;        // (blocks x waves, kCbStride): each wave's g_code row
+  float* gc_rows;        // fp32: set -> each workgroup's wave rows summed in wave order, one row per workgroup
   float* ray_part;       // (m / wave samples, 6): each wave's d ro, d rd of its ray (the points' part)
   float* q1_part;        // (m, 3): each sample's d rd of its Q1 view-direction ray
   int64_t n_blocks;      // set by the backward launchers: the grid they launched

@@ -1469,11 +1469,23 @@ __device__ __forceinline__ void bwd_body(const FieldArgs& a, float4* lds, const 
     // deterministic form (one code row, host-checked): this wave's g_code row into its gc_part row
     // (every wave writes its row, zeros included)
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS atomics landed
-    float* out = a.gc_part + ((int64_t)blk * kWaves + s.wave) * kCbStride;
+    if (a.gc_rows) {
+      // the workgroup's wave rows added in wave order into its one row (what ray_grad_reduce_kernel's row
+      // blocks did from the per-wave rows: the same additions, without the (waves x 2 KiB) round trip)
+      __syncthreads();
+      const float* rows = blds + kBGacc;
+      for (int j = threadIdx.x; j < kCbStride; j += kThreads) {
+        float v = rows[j];
+        for (int w = 1; w < kWaves; ++w) v += rows[w * kCbStride + j];
+        a.gc_rows[(int64_t)blk * kCbStride + j] = v;
+      }
+    } else {
+      float* out = a.gc_part + ((int64_t)blk * kWaves + s.wave) * kCbStride;
 #pragma unroll
-    for (int k = 0; k < (kCbStride + 63) / 64; ++k) {
-      const int j = s.lane + 64 * k;
-      if (j < kCbStride) out[j] = grow[j];
+      for (int k = 0; k < (kCbStride + 63) / 64; ++k) {
+        const int j = s.lane + 64 * k;
+        if (j < kCbStride) out[j] = grow[j];
+      }
     }
   } else if (cur_code >= 0) {
     flush_gcode(s, a, grow, cur_code);
