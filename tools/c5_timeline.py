@@ -32,7 +32,7 @@ def main():
         models.append(m.to(dev).eval())
     iters = int(os.environ.get("C5_ITERS", "40"))
     for prec in os.environ.get("C5_PRECISIONS", "f32 bf16x3").split():
-        for graph in (False, True):
+        for graph in [g == "1" for g in os.environ.get("C5_GRAPH", "0 1").split()]:
             r = bench.eval_bench(dev, rs, emb, models, iters, prec, graph=graph)
             print(json.dumps({"precision": prec, "graph": graph, "ms_per_iter": r["ms_per_iter"],
                               "t_end": time.perf_counter()}), flush=True)
