@@ -16,7 +16,7 @@ stores the activations the layer-wise backward reads.
 from __future__ import annotations
 
 import weakref
-from typing import Optional, Sequence
+from typing import Sequence
 
 import torch
 

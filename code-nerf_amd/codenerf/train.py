@@ -34,7 +34,7 @@ from . import nerf
 from .models import CodeNeRFModel, ShapeTextureEmbedding, get_params_tensor
 from .optim import AdamW
 from .autograd import backward_from, paired_fields, render_loss_autograd
-from .utils import get_minibatches, mse2psnr
+from .utils import get_minibatches
 
 
 def prepare_models(cfg, num_objects: int, device) -> "OrderedDict[str, torch.nn.Module]":
