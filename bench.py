@@ -132,11 +132,14 @@ def run(args):
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
+        # the launcher's env:// rendezvous, or a file:// one (CODENERF_INIT_METHOD: the multi-rank tests)
+        init = os.environ.get("CODENERF_INIT_METHOD") or None
         if args.backend == "nccl":
-            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", init_method=init, rank=rank, world_size=world,
+                                    device_id=torch.device("cuda", local))
             rccl_world = dist.get_world_size()
         else:       # gloo: the multi-rank test harness (ranks sharing one GPU; tests/test_gpu_multirank.py)
-            dist.init_process_group("gloo", rank=rank, world_size=world)
+            dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
     dev = torch.device("cuda", local)
 
     import codenerf

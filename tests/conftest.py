@@ -16,6 +16,13 @@ for p in (ROOT, os.path.join(ROOT, "code-nerf_amd")):
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 
+def rendezvous() -> str:
+    """A ``file://`` init_method for a spawned gloo group (or a bench worker): no TCP port to pick and then
+    lose to another process before the store binds it (EADDRINUSE, seen once on a shared GPU box)."""
+    import tempfile
+    return "file://" + os.path.join(tempfile.mkdtemp(prefix="cn_rdv_"), "store")
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP path through the C ABI)")
 

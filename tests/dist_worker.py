@@ -30,12 +30,12 @@ class _Params(dict):
         return self
 
 
-def run(rank, world, port, nc, nf, out_path):
+def run(rank, world, rdv, nc, nf, out_path):
     import codenerf.nerf as N
     from codenerf import synthetic
     import oracle.codenerf_oracle as O
 
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=rdv, rank=rank, world_size=world)
     try:
         g = np.load(os.path.join(HERE, "golden", "render_small.npz"))
         K, pose = torch.from_numpy(g["intrinsics"]), torch.from_numpy(g["pose"])

@@ -5,26 +5,19 @@ parallel_image_render with 2 / 3 ranks) must come back on rank 0 from the
 package's sharding + all-gather, with each rank holding the Q5 share.
 """
 import os
-import socket
 
 import numpy as np
 import pytest
 import torch
 import torch.multiprocessing as mp
 
-from conftest import GOLDEN
-
-
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+from conftest import GOLDEN, rendezvous
 
 
 def _launch(world, nc, nf, tmp_path):
     import dist_worker
     out = str(tmp_path / f"r{world}.npz")
-    mp.start_processes(dist_worker.run, args=(world, _free_port(), nc, nf, out), nprocs=world, join=True,
+    mp.start_processes(dist_worker.run, args=(world, rendezvous(), nc, nf, out), nprocs=world, join=True,
                        start_method="spawn")
     return np.load(out)
 
@@ -39,11 +32,11 @@ def test_parallel_image_render_gloo(world, nc, nf, tmp_path):
     assert np.abs(res["rgb"] - g[f"nc{nc}_n{world}_rgb"]).max() <= 1e-5
 
 
-def _gather_worker(rank, world, port, out_path, single_tensor):
+def _gather_worker(rank, world, rdv, out_path, single_tensor):
     import torch.distributed as dist
     from codenerf.nerf import gather_rows
     from codenerf.utils import split_sizes
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=rdv, rank=rank, world_size=world)
     try:
         per, _ = split_sizes(1001, world)
         start = sum(per[:rank])
@@ -63,18 +56,18 @@ def test_gather_rows_uneven_shares(world, single_tensor, tmp_path):
     """gather_rows' two branches: all_gather_into_tensor (the default, RCCL's form, run on gloo here) and
     the list all_gather, with uneven Q5 shares."""
     out = str(tmp_path / "g.npy")
-    mp.start_processes(_gather_worker, args=(world, _free_port(), out, single_tensor), nprocs=world, join=True,
+    mp.start_processes(_gather_worker, args=(world, rendezvous(), out, single_tensor), nprocs=world, join=True,
                        start_method="spawn")
     got = np.load(out)
     assert got.shape == (1001, 3)
     assert np.array_equal(got[:, 0], np.arange(1001, dtype=np.float32))
 
 
-def _views_worker(rank, world, port, n_pix, n_views, out_path):
+def _views_worker(rank, world, rdv, n_pix, n_views, out_path):
     import torch.distributed as dist
     from codenerf.nerf import gather_views
     from codenerf.utils import split_sizes
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=rdv, rank=rank, world_size=world)
     try:
         per, _ = split_sizes(n_pix, world)
         start = sum(per[:rank])
@@ -96,7 +89,7 @@ def test_gather_views_layout(world, n_pix, tmp_path):
     """bench.py's multi-view gather (every view split over the ranks as parallel_image_render splits
     one, nerf/__init__.py:179-218, rank 0 re-interleaving the blocks), with uneven Q5 shares."""
     out = str(tmp_path / "v.npy")
-    mp.start_processes(_views_worker, args=(world, _free_port(), n_pix, 5, out), nprocs=world, join=True,
+    mp.start_processes(_views_worker, args=(world, rendezvous(), n_pix, 5, out), nprocs=world, join=True,
                        start_method="spawn")
     got = np.load(out)
     want = (np.arange(5, dtype=np.float32)[:, None] * 1000 + np.arange(n_pix, dtype=np.float32)[None, :])
@@ -104,11 +97,11 @@ def test_gather_views_layout(world, n_pix, tmp_path):
     assert np.array_equal(got[..., 0], want) and np.array_equal(got[..., 2], want)
 
 
-def _shard_sync_worker(rank, world, port, out_path):
+def _shard_sync_worker(rank, world, rdv, out_path):
     import torch.distributed as dist
     from types import SimpleNamespace as NS
     from codenerf.evaluate import shard_of, sync_shard_state
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=rdv, rank=rank, world_size=world)
     try:
         np.random.seed(100 + rank)              # per-rank streams, as eval.py seeds them ((r + 1) + seed)
         torch.manual_seed(200 + rank)
@@ -135,7 +128,7 @@ def test_ray_sharded_eval_state_sync(world, tmp_path):
     parallel_image_render's Q5 split."""
     from codenerf.utils import split_sizes
     out = str(tmp_path / "s")
-    mp.start_processes(_shard_sync_worker, args=(world, _free_port(), out), nprocs=world, join=True,
+    mp.start_processes(_shard_sync_worker, args=(world, rendezvous(), out), nprocs=world, join=True,
                        start_method="spawn")
     got = [torch.load(f"{out}.{r}", weights_only=True) for r in range(world)]
     for g in got[1:]:

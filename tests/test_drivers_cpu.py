@@ -21,7 +21,7 @@ import pytest
 import torch
 import torch.multiprocessing as mp
 
-from conftest import GOLDEN
+from conftest import GOLDEN, rendezvous
 
 sys.path.insert(0, GOLDEN)
 import srn_tree  # noqa: E402
@@ -95,12 +95,12 @@ def test_launch_single_process_when_not_distributed(tree, tmp_path):
     assert seen == [(0, 2)]                                          # train.py:178-179
 
 
-def _ckpt_worker(rank, world, port, path, out_dir, per_rank):
+def _ckpt_worker(rank, world, rdv, path, out_dir, per_rank):
     import torch.distributed as dist
     from codenerf import checkpoint as C
     from codenerf.models import CodeNeRFModel, ShapeTextureEmbedding
     from collections import OrderedDict
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=rdv, rank=rank, world_size=world)
     try:
         np.random.seed(rank + 1 + 55)
         torch.manual_seed(rank + 1 + 55)
@@ -151,7 +151,7 @@ def _ckpt_worker(rank, world, port, path, out_dir, per_rank):
 @pytest.mark.parametrize("per_rank", [True, False])
 def test_checkpoint_rng_is_per_rank(tmp_path, per_rank):
     path = str(tmp_path / "checkpoint    3.ckpt")
-    mp.start_processes(_ckpt_worker, args=(2, _free_port(), path, str(tmp_path), per_rank), nprocs=2, join=True,
+    mp.start_processes(_ckpt_worker, args=(2, rendezvous(), path, str(tmp_path), per_rank), nprocs=2, join=True,
                        start_method="spawn")
     recs = [json.load(open(tmp_path / f"ck{r}.json")) for r in range(2)]
     for r in recs:

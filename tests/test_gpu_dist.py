@@ -2,7 +2,6 @@
 GPU of the test box: a world-size-1 "nccl" (RCCL) process group, so ``all_gather_into_tensor`` runs
 for real; parallel_image_render in distributed mode on top of it.  World sizes 2-4 are covered on
 CPU with gloo (tests/test_distributed_cpu.py); 8-GPU runs are the driver's."""
-import socket
 
 import pytest
 import torch
@@ -13,15 +12,9 @@ from test_gpu_parity import dev, embedders, load, maxdiff  # noqa: F401
 pytestmark = pytest.mark.gpu
 
 
-def _port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
 @pytest.fixture
 def rccl_world1(dev):
-    store = dist.TCPStore("127.0.0.1", _port(), 1, True)
+    store = dist.HashStore()   # one process: an in-memory store, no port to pick
     dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=dev)
     try:
         yield dist.get_world_size()

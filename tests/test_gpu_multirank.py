@@ -15,7 +15,6 @@ profiles/r04/gloo_probe.jsonl), so the product code runs unchanged on the gloo g
 """
 import json
 import os
-import socket
 import sys
 from types import SimpleNamespace as NS
 
@@ -28,35 +27,30 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 
 
-def _port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
 def _spawn(fn, world, *args):
     import torch.multiprocessing as mp
-    mp.start_processes(fn, args=(world, _port()) + args, nprocs=world, join=True, start_method="spawn")
+    from conftest import rendezvous
+    mp.start_processes(fn, args=(world, rendezvous()) + args, nprocs=world, join=True, start_method="spawn")
 
 
-def _init(rank, world, port):
+def _init(rank, world, rdv):
     import torch.distributed as dist
     import codenerf
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=rdv, rank=rank, world_size=world)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     codenerf.load_library()
     return dev
 
 
-def _chairs_worker(rank, world, port, out_path):
+def _chairs_worker(rank, world, rdv, out_path):
     import torch.distributed as dist
     from codenerf import synthetic
     from codenerf.nerf import PointSampler, RaySampler, parallel_image_render
     from test_gpu_configs import model_from
     from test_gpu_parity import load
     from test_gpu_train import embedders
-    dev = _init(rank, world, port)
+    dev = _init(rank, world, rdv)
     try:
         g = load("render_chairs.npz", dev)
         rs = RaySampler(128, 128, g["intrinsics"].cpu(), sample_size=4096, device=dev, datatype=torch.float32)
@@ -105,12 +99,12 @@ def _setup(dev, distributed):
     return models, opt, sched, ps
 
 
-def _train_worker(rank, world, port, out_dir):
+def _train_worker(rank, world, rdv, out_dir):
     import numpy as np
     import torch.distributed as dist
     from codenerf import train as T
     from test_gpu_train import embedders
-    dev = _init(rank, world, port)
+    dev = _init(rank, world, rdv)
     try:
         models, opt, sched, ps = _setup(dev, True)
         if rank == 1:       # a different start on rank 1: prepare_optimizer's broadcast must undo it
@@ -135,7 +129,7 @@ def _train_worker(rank, world, port, out_dir):
         dist.destroy_process_group()
 
 
-def _nosync_worker(rank, world, port, out_dir):
+def _nosync_worker(rank, world, rdv, out_dir):
     """train_minibatch on 2 gloo ranks under torch's sync debug mode "error": the product code between
     the collectives must not synchronise (gloo itself stages device tensors through the host, so the
     mode is lifted for the duration of its all-reduce only)."""
@@ -143,7 +137,7 @@ def _nosync_worker(rank, world, port, out_dir):
     import torch.distributed as dist
     from codenerf import train as T
     from test_gpu_train import embedders
-    dev = _init(rank, world, port)
+    dev = _init(rank, world, rdv)
     try:
         models, opt, sched, ps = _setup(dev, True)
         opt.broadcast_params(0)
@@ -223,9 +217,9 @@ def test_train_allreduce_two_ranks(tmp_path):
 _BENCH_HEADLINE = ["--steps", "2", "--warmup", "1", "--images-per-step", "2", "--no-extras"]
 
 
-def _bench_worker(rank, world, port, out_dir, argv=_BENCH_HEADLINE):
+def _bench_worker(rank, world, rdv, out_dir, argv=_BENCH_HEADLINE):
     os.environ.update(RANK=str(rank), LOCAL_RANK="0", WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
-                      MASTER_PORT=str(port))
+                      CODENERF_INIT_METHOD=rdv)
     sys.path.insert(0, ROOT)
     import bench
     res = bench.run(bench.parse_args(list(argv) + ["--no-cpu-baseline", "--backend", "gloo", "--quiet"]))
@@ -284,11 +278,11 @@ def _eval_cfg(tree, logdir, world):
     return cfg
 
 
-def _eval_worker(rank, world, port, tree, out_dir):
+def _eval_worker(rank, world, rdv, tree, out_dir):
     import numpy as np
     import torch.distributed as dist
     from codenerf.evaluate import validate
-    dev = _init(rank, world, port)
+    dev = _init(rank, world, rdv)
     try:
         cfg = _eval_cfg(tree, os.path.join(out_dir, "e"), world)
         loader, models, samplers, embedders, k = _eval_setup(cfg, dev, rank)
@@ -381,11 +375,11 @@ def test_validate_two_ranks_q6(tmp_path):
     assert abs(got[0]["loss"] - mse) <= 1e-6 * max(1.0, mse)
 
 
-def _shard_worker(rank, world, port, tree, out_dir):
+def _shard_worker(rank, world, rdv, tree, out_dir):
     import numpy as np
     import torch.distributed as dist
     from codenerf.evaluate import _pose_lr, sync_shard_state, test_time_optimize, validate
-    dev = _init(rank, world, port)
+    dev = _init(rank, world, rdv)
     try:
         cfg = _eval_cfg(tree, os.path.join(out_dir, "s"), world)
         cfg.nerf.point_sampler.perturb = True        # the stratified / fine uniforms are sliced too
@@ -501,11 +495,11 @@ def test_eval_ray_sharded_two_ranks(tmp_path):
     assert g0["v_rgb_rows"] == h * w
 
 
-def _train_driver_worker(rank, world, port, tree, out_dir, tag, ckpt):
+def _train_driver_worker(rank, world, rdv, tree, out_dir, tag, ckpt):
     import torch.distributed as dist
     from codenerf.train import train
     from test_gpu_drivers import _cfg
-    dev = _init(rank, world, port)
+    dev = _init(rank, world, rdv)
     try:
         cfg = _cfg(tree, os.path.join(out_dir, tag), iterations=6, save_every=4, validate_every=1000)
         cfg.nerf.train.chunksize = 64                    # 128 rays per image -> 2 chunks per iteration

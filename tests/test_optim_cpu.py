@@ -6,18 +6,13 @@ gradients landing in the flat buffer), zero_grad semantics, the refusal to updat
 without a GPU, and the data-parallel pieces -- the gradient average and the
 start-of-training parameter broadcast -- over gloo with 2 ranks.
 """
-import socket
 
 import numpy as np
 import pytest
 import torch
 import torch.multiprocessing as mp
 
-
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+from conftest import rendezvous
 
 
 SHAPES = [(256, 63), (256,), (3, 512), (3,), (40, 256)]
@@ -107,9 +102,9 @@ def test_state_dict_matches_torch_layout():
     assert set(a["param_groups"][0]) == set(b["param_groups"][0])
 
 
-def _dp_worker(rank, world, port, out):
+def _dp_worker(rank, world, rdv, out):
     import torch.distributed as dist
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=rdv, rank=rank, world_size=world)
     try:
         ps = _params(seed=rank)                  # replicas start apart (train.py:29-31 seeds by rank)
         opt = _opt(ps)
@@ -154,7 +149,7 @@ def test_allreduce_and_broadcast_gloo(world, tmp_path):
     a gradient missing on a rank counts as zero, one missing everywhere stays None; changing patterns
     between steps (the per-pattern flag cache) reduce correctly."""
     out = str(tmp_path / "r{}.npz")
-    mp.start_processes(_dp_worker, args=(world, _free_port(), out), nprocs=world, join=True, start_method="spawn")
+    mp.start_processes(_dp_worker, args=(world, rendezvous(), out), nprocs=world, join=True, start_method="spawn")
     res = [np.load(out.format(r)) for r in range(world)]
     ref = torch.cat([p.detach().reshape(-1) for p in _params(seed=0)]).numpy()
     sizes = [int(np.prod(s)) for s in SHAPES]
