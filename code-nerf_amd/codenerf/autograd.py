@@ -403,13 +403,15 @@ def _param_grad_buffers(params, needs, orig=None):
 
 
 class FieldPair:
-    """A training step's two fields (predict_radiance_and_render's coarse and fine, nerf/__init__.py:81-89):
-    their backwards are independent (the fine depths are detached, point_sampler.py:115), so the first one
-    autograd reaches waits and the second runs both in ONE cn_field_backward_train_multi call (one dX
-    launch, one batched dW launch, one layer_xyz1 launch and one reduction launch for the two; every
-    gradient bitwise that of the per-field calls).  Armed by train_minibatch only (paired_fields()): the
-    waiting field hands its gradients over in place -- the optimiser's flat slots installed as .grad at
-    once, the code rows' dz through the CodeGradSink -- so it returns none through autograd."""
+    """A step's two fields (predict_radiance_and_render's coarse and fine, nerf/__init__.py:81-89): their
+    backwards are independent (the fine depths are detached, point_sampler.py:115), so the first one
+    autograd reaches waits and the second runs both -- training: ONE cn_field_backward_train_multi call
+    (one dX launch, one batched dW launch with layer_xyz1's dW among its jobs, one DIRS-pass launch and
+    one reduction launch for the two); eval: ONE cn_field_backward_fused_multi call (one dX launch, one
+    ray / g_code launch).  Every gradient is bitwise that of the per-field calls.  Armed by train_minibatch
+    and eval_step_loss (paired_fields()): the waiting field hands its gradients over in place -- the
+    optimiser's flat slots installed as .grad at once, the code rows' dz through the CodeGradSink, the
+    rays' gradient into the pose's RaySink -- so it returns none through autograd."""
 
     __slots__ = ("pending", "kinds", "between", "sink", "on_grads")
 

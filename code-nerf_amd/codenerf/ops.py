@@ -573,8 +573,9 @@ def field_backward_train(packed_t: Tensor, params: Sequence[Tensor], masks: Tens
 def field_backward_train_multi(fields: Sequence[dict], precision: str = "f32"):
     """The training backwards of a render's fields (field_backward_train's keyword arguments, one dict
     per field, 1 or 2) through ONE cn_field_backward_train_multi call: with two fp32 fields on rays +
-    depths, one dX launch, one batched dW launch, one layer_xyz1 launch and one reduction launch for
-    both, every gradient bitwise that of the per-field calls -> one result dict per field."""
+    depths, one dX launch, one batched dW launch (layer_xyz1's dW among its jobs), one DIRS-pass launch
+    and one reduction launch for both, every gradient bitwise that of the per-field calls -> one result
+    dict per field."""
     assert len(fields) in (1, 2)
     fmt_t = _lib.CN_FMT_BF16X3_T if precision == "bf16x3" else _lib.CN_FMT_F32_W16_T
     lib = _lib_ready()

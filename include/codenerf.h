@@ -364,8 +364,8 @@ int cn_field_backward_fused_ws(int fmt_t, const float* packed_t, const uint32_t*
 /* The eval step's two fields (eval.py:153-167: predict_radiance_and_render's coarse and fine fields on the
  * same rays; the fine depths are detached, point_sampler.py:115, so the two backwards are independent) in
  * shared launches: each field the arguments of one cn_field_backward_fused_ws call, both adding into the
- * same d_ro / d_rd.  fp32, rays + depths, one code row, whole waves per ray: one dX launch, one ray /
- * g_code-row launch and one g_code reduction launch for both; d_ro / d_rd bitwise those of field 0's call,
+ * same d_ro / d_rd.  fp32, rays + depths, one code row, whole waves per ray: one dX launch and one ray /
+ * g_code launch for both; d_ro / d_rd and g_code bitwise those of field 0's call,
  * then d_rd += d_rd_between (optional, n_rays x 3: the rays' gradient that arrives between the two
  * backwards -- the coarse volume render's), then field 1's call -- which is how fields that cannot share
  * run.  n_fields 1 or 2 (d_rd_between: 2 only). */
@@ -444,9 +444,9 @@ int cn_field_backward_train_fmt(int fmt_t, const float* packed_t, const float* c
  * train.py:112's loss.backward(): the fine depths are detached, point_sampler.py:115, so the two
  * backwards are independent).  Each field: the arguments of cn_field_backward_train_fmt, with its own
  * workspace.  With two fp32 fields on rays + depths that both take the batched dW plan and the forward's
- * encoding plane (every runnable training config): ONE dX launch, ONE batched dW launch, ONE layer_xyz1
- * launch and ONE reduction launch for both, each running every field's workgroups as its own launch
- * would -- the gradients are bitwise those of the per-field calls.  Otherwise the fields run one after
+ * encoding plane (every runnable training config): ONE dX launch, ONE batched dW launch (layer_xyz1's
+ * dW among its jobs), ONE DIRS-pass launch and ONE reduction launch for both, each running every field's
+ * workgroups as its own launch would -- the gradients are bitwise those of the per-field calls.  Otherwise the fields run one after
  * the other.  n_fields 1 or 2. */
 typedef struct cn_field_train_bwd {
   const float* packed_t;
