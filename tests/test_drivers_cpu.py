@@ -12,7 +12,6 @@
 """
 import json
 import os
-import socket
 import sys
 from types import SimpleNamespace as NS
 
@@ -25,12 +24,6 @@ from conftest import GOLDEN, rendezvous
 
 sys.path.insert(0, GOLDEN)
 import srn_tree  # noqa: E402
-
-
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
 
 
 def _cfg(base, out_dir, gpus=2):
@@ -67,7 +60,7 @@ def test_launch_spawns_ranks_with_reference_seeds_and_epochs(tree, tmp_path):
     from codenerf.datasets import SRNDataset
     from codenerf.train import launch
     cfg = _cfg(tree, str(tmp_path))
-    launch(_stub_body, cfg, backend="gloo", port=_free_port())
+    launch(_stub_body, cfg, backend="gloo", init_method=rendezvous())
     recs = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(2)]
     ds = SRNDataset(tree, "train")
     for r, rec in enumerate(recs):
